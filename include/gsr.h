@@ -1,0 +1,128 @@
+/*
+ * gsr.h — C ABI of the MI355X-native differentiable 3D Gaussian Splatting rasterizer.
+ *
+ * This is the drop-in boundary for the hot path of lizhiqi49/threestudio-3dgs.  The
+ * reference never ships a rasterizer: every renderer (e.g. renderer/diff_gaussian_rasterizer.py:8-11,
+ * renderer/diff_gaussian_rasterizer_background.py:119-128, renderer/diff_gaussian_rasterizer_advanced.py:122)
+ * imports the external pybind module `diff_gaussian_rasterization._C` (ashawkey 4-output fork,
+ * README.md:17,28).  Its three entry points are
+ *     _C.rasterize_gaussians(...)          -> (num_rendered, color, depth, alpha, radii, geomBuf, binningBuf, imgBuf)
+ *     _C.rasterize_gaussians_backward(...) -> 8 gradients
+ *     _C.mark_visible(...)                 -> bool mask
+ * (SURVEY.md §8b).  This header restates them as plain C: device pointers, sizes and a HIP stream
+ * handle; no torch types.  The host binding (threestudio-3dgs_amd/diff_gaussian_rasterization/_C.py)
+ * calls these through ctypes with buffers allocated by the PyTorch caching allocator.
+ *
+ * Conventions (unchanged from the reference call sites):
+ *   - all float arrays are fp32, row-major, device-resident;
+ *   - viewmatrix / projmatrix are 4x4 *transposed* (row-vector) matrices read column-major
+ *     (world_view_transform / full_proj_transform, geometry/sugar.py:891-896);
+ *   - shs is (P, M, 3); rotations are (w, x, y, z), used as given (not renormalised);
+ *   - color output is planar (3, H, W); depth and alpha are (1, H, W);
+ *   - radii is int32 (P,); means2D gradient is (P, 3) in pixel units (x W/2, H/2), z = 0.
+ *
+ * Work is split into the phases the reference performs inside one call so that the host can
+ * size the K-dependent buffers between them (the reference does the same D2H read of K,
+ * SURVEY.md §2a "cub::DeviceScan ... host sync"):
+ *   1. gsr_forward_preprocess   — cull/project/EWA/SH, depth sort of visible Gaussians, K
+ *   2. gsr_num_rendered         — read K (and the visible count) back to the host
+ *   3. gsr_forward_render       — duplicate, tile sort, tile ranges, front-to-back blend
+ *   4. gsr_backward             — back-to-front replay + fused per-Gaussian chain rule
+ *
+ * Every function returns GSR_OK (0) or an error code; gsr_last_error() gives the message for
+ * the calling thread.  Kernels are enqueued on `stream` (a hipStream_t; NULL = legacy stream);
+ * only gsr_num_rendered synchronises.
+ */
+#ifndef GSR_H
+#define GSR_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define GSR_OK 0
+#define GSR_EINVAL 1 /* bad argument (shape / size / null pointer)          */
+#define GSR_EHIP 2   /* a HIP runtime call failed                            */
+
+#define GSR_TILE_X 16 /* BLOCK_X of the reference algorithm (16x16 tiles)      */
+#define GSR_TILE_Y 16
+
+/* Library identification ("gsr <version> gfx950"). */
+const char* gsr_version(void);
+/* Message of the last failing call on this thread ("" if none). */
+const char* gsr_last_error(void);
+
+/* ---- workspace sizing (bytes).  Buffers are opaque, 256-byte aligned uint8 regions. ---- */
+/* Per-Gaussian state: replaces the reference's geomBuffer (rasterize_points.cu, [EXT]). */
+size_t gsr_geom_bytes(int P);
+/* Per-instance state for K (Gaussian, tile) pairs: replaces binningBuffer. */
+size_t gsr_binning_bytes(int K, int width, int height);
+/* Per-pixel state (final transmittance, last contributor, tile ranges): replaces imgBuffer. */
+size_t gsr_image_bytes(int width, int height);
+/* Scratch for gsr_backward (per-instance gradient rows). */
+size_t gsr_backward_bytes(int P, int K);
+
+/*
+ * Phase 1 — replaces FORWARD::preprocessCUDA + InclusiveSum of rasterize_points.cu [EXT]
+ * (SURVEY.md §2a rows 1-2, §8a A4-A8).  Exactly one of (shs, colors_precomp) and one of
+ * ((scales, rotations), cov3D_precomp) must be non-NULL (checked; GSR_EINVAL otherwise).
+ * Writes radii (P,) and the geom workspace; the visible count and K stay on the device.
+ *   means3D (P,3)  scales (P,3)  rotations (P,4)  opacities (P,1)  shs (P,M,3)
+ *   colors_precomp (P,3)  cov3D_precomp (P,6)  viewmatrix/projmatrix (16)  campos (3)
+ * `degree` is the active SH degree; the kernel uses min(degree, sqrt(M)-1).
+ */
+int gsr_forward_preprocess(int P, int degree, int M,
+                           const float* means3D, const float* scales, float scale_modifier,
+                           const float* rotations, const float* opacities, const float* shs,
+                           const float* colors_precomp, const float* cov3D_precomp,
+                           const float* viewmatrix, const float* projmatrix, const float* campos,
+                           int width, int height, float tanfovx, float tanfovy, int prefiltered,
+                           int* radii, void* geom, void* stream);
+
+/* Phase 2 — D2H read of K (num_rendered) and of the visible-Gaussian count; synchronises `stream`. */
+int gsr_num_rendered(const void* geom, int P, int* num_rendered, int* num_visible, void* stream);
+
+/*
+ * Phase 3 — replaces duplicateWithKeys + DeviceRadixSort::SortPairs + identifyTileRanges +
+ * FORWARD::renderCUDA [EXT].  K must be the value from gsr_num_rendered.
+ * bg is (3,) on the device.  Writes color (3,H,W), depth (1,H,W), alpha (1,H,W) and the
+ * binning / image workspaces that gsr_backward reads.
+ */
+int gsr_forward_render(int P, int K, int width, int height, const float* bg,
+                       void* geom, void* binning, void* image,
+                       float* out_color, float* out_depth, float* out_alpha, void* stream);
+
+/*
+ * Phase 4 — replaces BACKWARD::renderCUDA + computeCov2DCUDA + preprocessCUDA [EXT]
+ * (SURVEY.md §8a A11-A12).  Reads (never writes) geom/binning/image, so it may be called
+ * repeatedly on the same forward state (retain_graph=True, system/gaussian_splatting.py:129,138).
+ * Gradient outputs are fully overwritten (no pre-zeroing needed):
+ *   dL_dmeans2D (P,3)  dL_dcolors (P,3)  dL_dopacity (P,1)  dL_dmeans3D (P,3)
+ *   dL_dcov3D (P,6) [may be NULL if cov3D_precomp is NULL]  dL_dsh (P,M,3) [NULL if shs NULL]
+ *   dL_dscales (P,3), dL_drotations (P,4) [NULL if scales/rotations NULL]
+ * dL_ddepth / dL_dalpha may be NULL (treated as zero).
+ */
+int gsr_backward(int P, int degree, int M, int K, int width, int height, const float* bg,
+                 const float* means3D, const float* scales, float scale_modifier,
+                 const float* rotations, const float* opacities, const float* shs,
+                 const float* colors_precomp, const float* cov3D_precomp,
+                 const float* viewmatrix, const float* projmatrix, const float* campos,
+                 float tanfovx, float tanfovy, const int* radii,
+                 const void* geom, const void* binning, const void* image,
+                 const float* dL_dcolor, const float* dL_ddepth, const float* dL_dalpha,
+                 float* dL_dmeans2D, float* dL_dcolors, float* dL_dopacity, float* dL_dmeans3D,
+                 float* dL_dcov3D, float* dL_dsh, float* dL_dscales, float* dL_drotations,
+                 void* work, void* stream);
+
+/* Replaces markVisible/checkFrustum (API completeness; unused by the reference).  present (P,) u8. */
+int gsr_mark_visible(int P, const float* means3D, const float* viewmatrix, const float* projmatrix,
+                     uint8_t* present, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* GSR_H */

@@ -1,0 +1,160 @@
+"""HIP rasterizer vs the CPU restatement (oracle, fp32 build) on identical seeded inputs.
+
+Tolerances: RGB / alpha 1e-5 abs, depth 1e-5 abs+rel, gradients 1e-4 of the
+tensor's max |g| (or 1 if larger), with a small allowance for discrete fp32 decision flips.
+"""
+import numpy as np
+import pytest
+
+import oracle
+from gsr_testutil import assert_grad_parity, assert_image_parity, gpu_render, gs, make_camera, oracle_cam
+
+pytestmark = pytest.mark.gpu
+
+GRAD_KEYS_SH = ["means3D", "means2D", "opacity", "sh", "scales", "rotations"]
+
+
+def _run(scene, cam, bg, grads=True, mod=1.0, cov3d=False, keys=GRAD_KEYS_SH, what=""):
+    g = gs.upstream_grads(cam["H"], cam["W"], seed=7) if grads else None
+    gpu = gpu_render(scene, cam, bg, grads=g, mod=mod, cov3d=cov3d)
+    ref = oracle.forward(scene, oracle_cam(cam), np.asarray(bg, np.float32), "f32", mod=mod)
+    nbad = assert_image_parity(gpu, ref, what)
+    rep = None
+    if grads:
+        rb = oracle.backward(scene, oracle_cam(cam), np.asarray(bg, np.float32), *g, prec="f32", mod=mod)
+        rep = assert_grad_parity(gpu, rb, keys, what)
+    return gpu, ref, nbad, rep
+
+
+def test_c1_forward_backward_sh0():
+    """C1: 10k Gaussians, 256^2, SH degree 0, white background."""
+    scene = gs.make_scene(10_000, sh_degree=0, seed=0)
+    cam = make_camera(256, 256)
+    _run(scene, cam, [1.0, 1.0, 1.0], what="C1")
+
+
+def test_c2_small_sh3_black_bg():
+    """C2 shape at reduced N: SH degree 3, 512^2, zero background (background path)."""
+    scene = gs.make_scene(30_000, sh_degree=3, seed=1)
+    cam = make_camera(512, 512, elevation=30.0, azimuth=45.0)
+    _run(scene, cam, [0.0, 0.0, 0.0], what="C2-small")
+
+
+def test_ragged_image_and_aspect():
+    """Image sizes not multiple of 16, fovx != fovy, coloured background."""
+    scene = gs.make_scene(5_000, sh_degree=1, seed=2)
+    cam = make_camera(200, 120, fovy_deg=50.0, fovx_deg=70.0, azimuth=100.0)
+    _run(scene, cam, [0.2, 0.5, 0.9], what="ragged")
+
+
+@pytest.mark.parametrize("deg", [1, 2])
+def test_sh_degrees(deg):
+    scene = gs.make_scene(4_000, sh_degree=deg, seed=3 + deg)
+    cam = make_camera(128, 128, azimuth=30.0 * deg)
+    _run(scene, cam, [1.0, 1.0, 1.0], what=f"deg{deg}")
+
+
+def test_degree_larger_than_coefficients():
+    """Pred-normal quirk: sh_degree > sqrt(M)-1 (renderer/diff_gaussian_rasterizer_shading.py:178-181)."""
+    scene = gs.make_scene(3_000, sh_degree=0, seed=9)
+    scene["sh_degree"] = 3
+    cam = make_camera(128, 128)
+    _run(scene, cam, [0.0, 0.0, 0.0], what="deg-quirk")
+
+
+def test_colors_precomp_path():
+    scene = gs.make_scene(6_000, sh_degree=0, seed=11)
+    rng = np.random.default_rng(5)
+    scene["colors_precomp"] = rng.random((6_000, 3)).astype(np.float32)
+    scene.pop("shs")
+    cam = make_camera(160, 160)
+    _run(scene, cam, [1.0, 1.0, 1.0], keys=["means3D", "means2D", "opacity", "colors", "scales", "rotations"],
+         what="colors_precomp")
+
+
+def test_cov3d_precomp_path():
+    scene = gs.make_scene(6_000, sh_degree=1, seed=12)
+    scene["cov3D_precomp"] = oracle.cov3d(scene["scales"], scene["rotations"]).astype(np.float32)
+    cam = make_camera(160, 160)
+    _run(scene, cam, [1.0, 1.0, 1.0], cov3d=True, keys=["means3D", "means2D", "opacity", "sh", "cov3D"],
+         what="cov3D_precomp")
+
+
+def test_scale_modifier():
+    scene = gs.make_scene(5_000, sh_degree=1, seed=13)
+    cam = make_camera(128, 128)
+    _run(scene, cam, [1.0, 1.0, 1.0], mod=0.7, what="scale_modifier")
+
+
+def test_flat_surface_gaussians():
+    """SuGaR-like: one axis 1e-6 thick (geometry/sugar.py:201,493-496) stresses the +0.3 dilation."""
+    scene = gs.make_scene(6_000, sh_degree=0, seed=14)
+    scene["scales"][:, 0] = 1e-6
+    cam = make_camera(200, 200)
+    _run(scene, cam, [0.0, 0.0, 0.0], what="flat")
+
+
+def test_empty_and_culled():
+    import torch
+
+    from diff_gaussian_rasterization import GaussianRasterizationSettings, GaussianRasterizer
+
+    cam = make_camera(64, 48)
+    # P = 0: zero outputs, no launch (reference behaviour)
+    scene = gs.make_scene(0, sh_degree=0, seed=0)
+    out = gpu_render(scene, cam, [1.0, 1.0, 1.0])
+    assert out["color"].shape == (3, 48, 64) and np.all(out["color"] == 0)
+    # all behind the camera: background everywhere, radii 0, zero grads
+    scene = gs.make_scene(500, sh_degree=0, seed=1)
+    scene["means3D"] = scene["means3D"] * 0.1 + np.array([5.0, 0.0, 1.5], np.float32) * 2.0
+    g = gs.upstream_grads(48, 64)
+    out = gpu_render(scene, cam, [0.25, 0.5, 1.0], grads=g)
+    ref = oracle.forward(scene, oracle_cam(cam), np.array([0.25, 0.5, 1.0], np.float32), "f32")
+    assert_image_parity(out, ref, "culled")
+    assert np.all(out["radii"] == ref["radii"])
+    del torch, GaussianRasterizationSettings, GaussianRasterizer
+
+
+def test_single_gaussian_and_tile_edges():
+    scene = gs.make_scene(1, sh_degree=0, seed=0)
+    scene["means3D"][:] = 0.0
+    scene["scales"][:] = 0.2
+    cam = make_camera(100, 100)
+    _run(scene, cam, [1.0, 1.0, 1.0], what="single")
+
+
+def test_backward_is_repeatable():
+    """retain_graph double backward (system/gaussian_splatting.py:129,138): bitwise-identical grads."""
+    scene = gs.make_scene(8_000, sh_degree=2, seed=21)
+    cam = make_camera(192, 192)
+    g = gs.upstream_grads(192, 192, seed=3)
+    out = gpu_render(scene, cam, [1.0, 1.0, 1.0], grads=g, backward_twice=True)
+    assert np.array_equal(out["g_means3D"], out["g2_means3D"])
+
+
+def test_forward_deterministic():
+    scene = gs.make_scene(20_000, sh_degree=3, seed=22)
+    cam = make_camera(256, 256)
+    a = gpu_render(scene, cam, [0.0, 0.0, 0.0])
+    b = gpu_render(scene, cam, [0.0, 0.0, 0.0])
+    for k in ("color", "depth", "alpha", "radii"):
+        assert np.array_equal(a[k], b[k]), k
+
+
+def test_mark_visible():
+    import torch
+
+    from diff_gaussian_rasterization import GaussianRasterizationSettings, GaussianRasterizer
+
+    scene = gs.make_scene(2_000, sh_degree=0, seed=3)
+    scene["means3D"][:1000] += np.array([3.0, 0.0, 0.5], np.float32)  # some behind the camera
+    cam = make_camera(64, 64)
+    dev = "cuda"
+    s = GaussianRasterizationSettings(64, 64, cam["tanx"], cam["tany"], torch.zeros(3, device=dev), 1.0,
+                                      torch.tensor(cam["view"], device=dev), torch.tensor(cam["proj"], device=dev),
+                                      0, torch.tensor(cam["campos"], device=dev), False, False)
+    vis = GaussianRasterizer(s).markVisible(torch.tensor(scene["means3D"], device=dev)).cpu().numpy()
+    v = cam["view"].reshape(-1)
+    p = scene["means3D"]
+    z = v[2] * p[:, 0] + v[6] * p[:, 1] + v[10] * p[:, 2] + v[14]
+    assert np.array_equal(vis, z > 0.2)

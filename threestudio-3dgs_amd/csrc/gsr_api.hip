@@ -1,0 +1,243 @@
+// gsr_api.hip — extern "C" entry points declared in include/gsr.h.
+//
+// Phase structure mirrors what the reference's _C.rasterize_gaussians does internally
+// (CudaRasterizer::Rasterizer::forward / backward [EXT]); argument checking mirrors its
+// TORCH_CHECKs and Python-side exceptions (SURVEY.md §8b "Errors").
+#include <stdio.h>
+#include <string.h>
+
+#include <cmath>
+
+#include "../../include/gsr.h"
+#include "gsr_kernels.h"
+
+using namespace gsr;
+
+static thread_local char g_err[512] = "";
+
+static int fail(int code, const char* fmt, const char* what) {
+  snprintf(g_err, sizeof(g_err), fmt, what);
+  return code;
+}
+
+#define GSR_HIP_CHECK(expr)                                                        \
+  do {                                                                             \
+    hipError_t e_ = (expr);                                                        \
+    if (e_ != hipSuccess) return fail(GSR_EHIP, "HIP error: %s", hipGetErrorString(e_)); \
+  } while (0)
+
+static int last_launch() {
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return fail(GSR_EHIP, "HIP launch error: %s", hipGetErrorString(e));
+  g_err[0] = 0;
+  return GSR_OK;
+}
+
+static int effective_degree(int degree, int M) {
+  // the reference reads sqrt(M)-1 coefficients at most (pred-normal pass quirk)
+  int dm = (int)std::lround(std::sqrt((double)(M > 0 ? M : 1))) - 1;
+  int d = degree < dm ? degree : dm;
+  if (d < 0) d = 0;
+  if (d > 3) d = 3;
+  return d;
+}
+
+static int tile_key_bits(int W, int H) {
+  const int tiles = div_up(W, GSR_TILE_X) * div_up(H, GSR_TILE_Y);
+  int bits = 0;
+  while ((1 << bits) < tiles) ++bits;
+  return bits < 1 ? 1 : bits;
+}
+
+extern "C" {
+
+const char* gsr_version(void) { return "gsr 0.1.0 gfx950"; }
+const char* gsr_last_error(void) { return g_err; }
+
+size_t gsr_geom_bytes(int P) {
+  size_t b = 0;
+  GeomState::carve(nullptr, P, &b);
+  return b;
+}
+size_t gsr_binning_bytes(int K, int width, int height) {
+  (void)width;
+  (void)height;
+  size_t b = 0;
+  BinningState::carve(nullptr, K, &b);
+  return b;
+}
+size_t gsr_image_bytes(int width, int height) {
+  size_t b = 0;
+  ImageState::carve(nullptr, width, height, &b);
+  return b;
+}
+size_t gsr_backward_bytes(int P, int K) {
+  (void)P;
+  size_t b = 0;
+  BackwardState::carve(nullptr, K, &b);
+  return b;
+}
+
+int gsr_forward_preprocess(int P, int degree, int M, const float* means3D, const float* scales,
+                           float scale_modifier, const float* rotations, const float* opacities,
+                           const float* shs, const float* colors_precomp, const float* cov3D_precomp,
+                           const float* viewmatrix, const float* projmatrix, const float* campos,
+                           int width, int height, float tanfovx, float tanfovy, int prefiltered,
+                           int* radii, void* geom, void* stream) {
+  (void)prefiltered;
+  if (P < 0) return fail(GSR_EINVAL, "%s", "P must be >= 0");
+  if (width <= 0 || height <= 0) return fail(GSR_EINVAL, "%s", "image size must be positive");
+  if ((shs == nullptr) == (colors_precomp == nullptr))
+    return fail(GSR_EINVAL, "%s", "Please provide exactly one of either SHs or precomputed colors!");
+  if (((scales == nullptr || rotations == nullptr) && cov3D_precomp == nullptr) ||
+      ((scales != nullptr || rotations != nullptr) && cov3D_precomp != nullptr))
+    return fail(GSR_EINVAL, "%s",
+                "Please provide exactly one of either scale/rotation pair or precomputed 3D covariance!");
+  if (geom == nullptr || viewmatrix == nullptr || projmatrix == nullptr || campos == nullptr ||
+      (P > 0 && (means3D == nullptr || opacities == nullptr || radii == nullptr)))
+    return fail(GSR_EINVAL, "%s", "null pointer argument");
+  if (shs != nullptr && M <= 0) return fail(GSR_EINVAL, "%s", "M must be >= 1 with SHs");
+  hipStream_t s = (hipStream_t)stream;
+  GeomState g = GeomState::carve(geom, P, nullptr);
+  GSR_HIP_CHECK(hipMemsetAsync(g.counters, 0, 16 * sizeof(uint32_t), s));
+  if (P == 0) return last_launch();
+
+  PreprocessArgs a;
+  a.P = P;
+  a.deg = effective_degree(degree, M);
+  a.M = M;
+  a.means3D = means3D;
+  a.scales = scales;
+  a.rotations = rotations;
+  a.opacities = opacities;
+  a.shs = shs;
+  a.colors_precomp = colors_precomp;
+  a.cov3D_precomp = cov3D_precomp;
+  a.scale_modifier = scale_modifier;
+  a.viewmatrix = viewmatrix;
+  a.projmatrix = projmatrix;
+  a.campos = campos;
+  a.W = width;
+  a.H = height;
+  a.tanfovx = tanfovx;
+  a.tanfovy = tanfovy;
+  a.focal_y = height / (2.0f * tanfovy);
+  a.focal_x = width / (2.0f * tanfovx);
+  a.radii = radii;
+  launch_preprocess(a, g, s);
+  // visible compaction -> depth sort -> instance offsets in depth order
+  scan_exclusive(SCAN_FLAG, g.tiles_touched, nullptr, g.vis_off, nullptr, P, g.scan_blk,
+                 g.counters + 0, s);
+  launch_compact_visible(P, g, s);
+  const int res = radix_sort_pairs(g.dkey, g.dval, false, g.counters + 0, P, 32, g.hist, g.hist_blk, s);
+  if (res != 0) return fail(GSR_EHIP, "%s", "internal: depth sort result buffer");
+  scan_exclusive(SCAN_GATHER, g.tiles_touched, g.dval[0], g.point_offsets, g.counters + 0, P,
+                 g.scan_blk, g.counters + 1, s);
+  return last_launch();
+}
+
+int gsr_num_rendered(const void* geom, int P, int* num_rendered, int* num_visible, void* stream) {
+  if (geom == nullptr || num_rendered == nullptr) return fail(GSR_EINVAL, "%s", "null pointer argument");
+  GeomState g = GeomState::carve((void*)geom, P, nullptr);
+  uint32_t h[2] = {0, 0};
+  hipStream_t s = (hipStream_t)stream;
+  GSR_HIP_CHECK(hipMemcpyAsync(h, g.counters, sizeof(h), hipMemcpyDeviceToHost, s));
+  GSR_HIP_CHECK(hipStreamSynchronize(s));
+  *num_rendered = (int)h[1];
+  if (num_visible) *num_visible = (int)h[0];
+  g_err[0] = 0;
+  return GSR_OK;
+}
+
+int gsr_forward_render(int P, int K, int width, int height, const float* bg, void* geom,
+                       void* binning, void* image, float* out_color, float* out_depth,
+                       float* out_alpha, void* stream) {
+  if (P < 0 || K < 0 || width <= 0 || height <= 0) return fail(GSR_EINVAL, "%s", "bad sizes");
+  if (geom == nullptr || binning == nullptr || image == nullptr || bg == nullptr ||
+      out_color == nullptr || out_depth == nullptr || out_alpha == nullptr)
+    return fail(GSR_EINVAL, "%s", "null pointer argument");
+  hipStream_t s = (hipStream_t)stream;
+  GeomState g = GeomState::carve(geom, P, nullptr);
+  BinningState b = BinningState::carve(binning, K, nullptr);
+  ImageState img = ImageState::carve(image, width, height, nullptr);
+  const int gx = div_up(width, GSR_TILE_X), gy = div_up(height, GSR_TILE_Y);
+  GSR_HIP_CHECK(hipMemsetAsync(img.ranges, 0, sizeof(uint2) * (size_t)gx * gy, s));
+  if (K > 0) {
+    launch_duplicate(P, gx, g.dval[0], g, b, s);
+    const int res = radix_sort_pairs(b.key, b.val, true, nullptr, K, tile_key_bits(width, height),
+                                     b.hist, b.hist_blk, s);
+    launch_finalize_bins(K, b.key[res], b.val[res], b, img.ranges, s);
+  }
+  launch_render_forward(width, height, g, b, img, bg, out_color, out_depth, out_alpha, s);
+  return last_launch();
+}
+
+int gsr_backward(int P, int degree, int M, int K, int width, int height, const float* bg,
+                 const float* means3D, const float* scales, float scale_modifier,
+                 const float* rotations, const float* opacities, const float* shs,
+                 const float* colors_precomp, const float* cov3D_precomp, const float* viewmatrix,
+                 const float* projmatrix, const float* campos, float tanfovx, float tanfovy,
+                 const int* radii, const void* geom, const void* binning, const void* image,
+                 const float* dL_dcolor, const float* dL_ddepth, const float* dL_dalpha,
+                 float* dL_dmeans2D, float* dL_dcolors, float* dL_dopacity, float* dL_dmeans3D,
+                 float* dL_dcov3D, float* dL_dsh, float* dL_dscales, float* dL_drotations,
+                 void* work, void* stream) {
+  (void)opacities;
+  (void)colors_precomp;
+  if (P < 0 || K < 0 || width <= 0 || height <= 0) return fail(GSR_EINVAL, "%s", "bad sizes");
+  if (P == 0) return last_launch();
+  if (geom == nullptr || binning == nullptr || image == nullptr || work == nullptr || bg == nullptr ||
+      dL_dcolor == nullptr || dL_dmeans2D == nullptr || dL_dcolors == nullptr ||
+      dL_dopacity == nullptr || dL_dmeans3D == nullptr || radii == nullptr || means3D == nullptr)
+    return fail(GSR_EINVAL, "%s", "null pointer argument");
+  if (shs != nullptr && dL_dsh == nullptr) return fail(GSR_EINVAL, "%s", "dL_dsh required with SHs");
+  if (cov3D_precomp == nullptr && (scales == nullptr || rotations == nullptr || dL_dscales == nullptr ||
+                                   dL_drotations == nullptr))
+    return fail(GSR_EINVAL, "%s", "scales/rotations and their gradients required");
+  hipStream_t s = (hipStream_t)stream;
+  GeomState g = GeomState::carve((void*)geom, P, nullptr);
+  BinningState b = BinningState::carve((void*)binning, K, nullptr);
+  ImageState img = ImageState::carve((void*)image, width, height, nullptr);
+  BackwardState bw = BackwardState::carve(work, K, nullptr);
+  launch_render_backward(width, height, K, g, b, img, bg, dL_dcolor, dL_ddepth, dL_dalpha, bw, s);
+
+  GaussBackwardArgs a;
+  a.P = P;
+  a.deg = effective_degree(degree, M);
+  a.M = shs ? M : 0;
+  a.means3D = means3D;
+  a.scales = scales;
+  a.rotations = rotations;
+  a.shs = shs;
+  a.cov3D_precomp = cov3D_precomp;
+  a.scale_modifier = scale_modifier;
+  a.viewmatrix = viewmatrix;
+  a.projmatrix = projmatrix;
+  a.campos = campos;
+  a.tanfovx = tanfovx;
+  a.tanfovy = tanfovy;
+  a.focal_y = height / (2.0f * tanfovy);
+  a.focal_x = width / (2.0f * tanfovx);
+  a.radii = radii;
+  a.dL_dmeans2D = dL_dmeans2D;
+  a.dL_dcolors = dL_dcolors;
+  a.dL_dopacity = dL_dopacity;
+  a.dL_dmeans3D = dL_dmeans3D;
+  a.dL_dcov3D = dL_dcov3D;
+  a.dL_dsh = shs ? dL_dsh : nullptr;
+  a.dL_dscales = cov3D_precomp ? nullptr : dL_dscales;
+  a.dL_drotations = cov3D_precomp ? nullptr : dL_drotations;
+  launch_gauss_backward(a, g, b, bw, s);
+  return last_launch();
+}
+
+int gsr_mark_visible(int P, const float* means3D, const float* viewmatrix, const float* projmatrix,
+                     uint8_t* present, void* stream) {
+  if (P < 0) return fail(GSR_EINVAL, "%s", "P must be >= 0");
+  if (P > 0 && (means3D == nullptr || viewmatrix == nullptr || present == nullptr))
+    return fail(GSR_EINVAL, "%s", "null pointer argument");
+  launch_mark_visible(P, means3D, viewmatrix, projmatrix, present, (hipStream_t)stream);
+  return last_launch();
+}
+
+}  // extern "C"

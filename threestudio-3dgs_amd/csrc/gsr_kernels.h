@@ -1,0 +1,69 @@
+// gsr_kernels.h — host-side launchers for the device kernels (internal; the public ABI is
+// include/gsr.h).  All launchers enqueue on `stream` and never synchronise.
+#pragma once
+
+#include "gsr_common.h"
+
+namespace gsr {
+
+enum ScanMode { SCAN_PLAIN = 0, SCAN_FLAG = 1, SCAN_GATHER = 2 };
+
+// Exclusive scan of n u32 values (n = min(*n_dev, n_max) when n_dev != nullptr).
+//   PLAIN: x_i = in[i];  FLAG: x_i = in[i] > 0;  GATHER: x_i = in[idx[i]]
+// out may alias in for PLAIN.  blk needs scan_blocks(n_max) + 1 words.  *total (device) = sum.
+void scan_exclusive(ScanMode mode, const uint32_t* in, const uint32_t* idx, uint32_t* out,
+                    const uint32_t* n_dev, int n_max, uint32_t* blk, uint32_t* total,
+                    hipStream_t stream);
+
+// Stable LSD radix sort of (key, value) pairs on key bits [0, key_bits) using <= 8-bit digits.
+// Ping-pongs between keys[0]/vals[0] and keys[1]/vals[1]; returns the index (0/1) holding
+// the result.  vals_identity: the input values are the input positions (vals[0] not read).  hist needs
+// RADIX * scan_blocks(n_max) words, hist_blk scan_blocks(RADIX * scan_blocks(n_max)) + 1.
+int radix_sort_pairs(uint32_t* keys[2], uint32_t* vals[2], bool vals_identity, const uint32_t* n_dev,
+                     int n_max, int key_bits, uint32_t* hist, uint32_t* hist_blk, hipStream_t stream);
+
+// Forward preprocess (cull, project, EWA, SH) — gsr_preprocess.hip
+struct PreprocessArgs {
+  int P, deg, M;
+  const float *means3D, *scales, *rotations, *opacities, *shs, *colors_precomp, *cov3D_precomp;
+  float scale_modifier;
+  const float *viewmatrix, *projmatrix, *campos;
+  int W, H;
+  float tanfovx, tanfovy, focal_x, focal_y;
+  int* radii;
+};
+void launch_preprocess(const PreprocessArgs& a, const GeomState& g, hipStream_t stream);
+
+// Binning — gsr_binning.hip
+void launch_compact_visible(int P, const GeomState& g, hipStream_t stream);
+void launch_duplicate(int P, int grid_x, const uint32_t* order, const GeomState& g,
+                      const BinningState& b, hipStream_t stream);
+void launch_finalize_bins(int K, const uint32_t* keys, const uint32_t* vals, const BinningState& b,
+                          uint2* ranges, hipStream_t stream);
+void launch_mark_visible(int P, const float* means3D, const float* view, const float* proj,
+                         uint8_t* present, hipStream_t stream);
+
+// Tile blend — gsr_render.hip
+void launch_render_forward(int W, int H, const GeomState& g, const BinningState& b,
+                           const ImageState& img, const float* bg, float* out_color,
+                           float* out_depth, float* out_alpha, hipStream_t stream);
+void launch_render_backward(int W, int H, int K, const GeomState& g, const BinningState& b,
+                            const ImageState& img, const float* bg, const float* dL_dcolor,
+                            const float* dL_ddepth, const float* dL_dalpha,
+                            const BackwardState& bw, hipStream_t stream);
+
+// Fused per-Gaussian backward — gsr_backward.hip
+struct GaussBackwardArgs {
+  int P, deg, M;
+  const float *means3D, *scales, *rotations, *shs, *cov3D_precomp;
+  float scale_modifier;
+  const float *viewmatrix, *projmatrix, *campos;
+  float tanfovx, tanfovy, focal_x, focal_y;
+  const int* radii;
+  float *dL_dmeans2D, *dL_dcolors, *dL_dopacity, *dL_dmeans3D, *dL_dcov3D, *dL_dsh, *dL_dscales,
+      *dL_drotations;
+};
+void launch_gauss_backward(const GaussBackwardArgs& a, const GeomState& g, const BinningState& b,
+                           const BackwardState& bw, hipStream_t stream);
+
+}  // namespace gsr

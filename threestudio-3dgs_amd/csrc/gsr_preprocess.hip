@@ -1,0 +1,85 @@
+// gsr_preprocess.hip — per-Gaussian forward preprocess.
+//
+// Replaces FORWARD::preprocessCUDA of the reference rasterizer [EXT]: frustum cull
+// (view z <= 0.2), projection, 3D covariance, EWA 2D covariance (+0.3 low-pass), conic,
+// 3-sigma radius, 16x16 tile rect, SH -> RGB (clamped at 0, flags kept for backward).
+// One thread per Gaussian; HBM-bound: reads 44 + 12*M bytes, writes the 48-byte render record,
+// an 8-byte tile rect, radius, clamp flags and the instance count.
+#include "gsr_kernels.h"
+#include "gsr_math.h"
+
+namespace gsr {
+
+__global__ __launch_bounds__(256) void k_preprocess(PreprocessArgs a, GeomState g) {
+  const int idx = blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= a.P) return;
+  a.radii[idx] = 0;
+  g.tiles_touched[idx] = 0;
+
+  const float3 p_orig = make_float3(a.means3D[3 * idx], a.means3D[3 * idx + 1], a.means3D[3 * idx + 2]);
+  // near-plane cull on the view-space depth (in_frustum of the reference)
+  const float3 p_view = xform_point4x3(p_orig, a.viewmatrix);
+  if (p_view.z <= GSR_NEAR_CULL) return;
+  const float4 p_hom = xform_point4x4(p_orig, a.projmatrix);
+  const float p_w = 1.0f / (p_hom.w + 0.0000001f);
+  const float3 p_proj = make_float3(p_hom.x * p_w, p_hom.y * p_w, p_hom.z * p_w);
+
+  float cov3D[6];
+  if (a.cov3D_precomp != nullptr) {
+#pragma unroll
+    for (int i = 0; i < 6; ++i) cov3D[i] = a.cov3D_precomp[6 * idx + i];
+  } else {
+    const float3 s = make_float3(a.scales[3 * idx], a.scales[3 * idx + 1], a.scales[3 * idx + 2]);
+    const float4 q = make_float4(a.rotations[4 * idx], a.rotations[4 * idx + 1],
+                                 a.rotations[4 * idx + 2], a.rotations[4 * idx + 3]);
+    cov3d_from_scale_rot(s, a.scale_modifier, q, cov3D);
+  }
+
+  Cov2DState st;
+  const float3 cov = cov2d_ewa(p_orig, a.focal_x, a.focal_y, a.tanfovx, a.tanfovy, cov3D, a.viewmatrix, st);
+  const float det = cov.x * cov.z - cov.y * cov.y;
+  if (det == 0.0f) return;
+  const float det_inv = 1.f / det;
+  const float3 conic = make_float3(cov.z * det_inv, -cov.y * det_inv, cov.x * det_inv);
+
+  const float mid = 0.5f * (cov.x + cov.z);
+  const float lambda1 = mid + sqrtf(fmaxf(0.1f, mid * mid - det));
+  const float lambda2 = mid - sqrtf(fmaxf(0.1f, mid * mid - det));
+  const float my_radius = ceilf(3.f * sqrtf(fmaxf(lambda1, lambda2)));
+  const float2 pimg = make_float2(ndc2pix(p_proj.x, a.W), ndc2pix(p_proj.y, a.H));
+
+  // tile rect [min, max) clamped to the grid (getRect of the reference)
+  const int gx = (a.W + GSR_TILE_X - 1) / GSR_TILE_X;
+  const int gy = (a.H + GSR_TILE_Y - 1) / GSR_TILE_Y;
+  const int r = (int)my_radius;
+  const int xmin = min(gx, max(0, (int)((pimg.x - r) / GSR_TILE_X)));
+  const int ymin = min(gy, max(0, (int)((pimg.y - r) / GSR_TILE_Y)));
+  const int xmax = min(gx, max(0, (int)((pimg.x + r + GSR_TILE_X - 1) / GSR_TILE_X)));
+  const int ymax = min(gy, max(0, (int)((pimg.y + r + GSR_TILE_Y - 1) / GSR_TILE_Y)));
+  const int area = (xmax - xmin) * (ymax - ymin);
+  if (area == 0) return;
+
+  float3 rgb;
+  uint32_t clamp_bits = 0;
+  if (a.colors_precomp != nullptr) {
+    rgb = make_float3(a.colors_precomp[3 * idx], a.colors_precomp[3 * idx + 1], a.colors_precomp[3 * idx + 2]);
+  } else {
+    rgb = sh_to_rgb(a.deg, a.shs + (size_t)idx * a.M * 3, p_orig,
+                    make_float3(a.campos[0], a.campos[1], a.campos[2]), &clamp_bits);
+  }
+
+  g.rec0[idx] = make_float4(pimg.x, pimg.y, conic.x, conic.y);
+  g.rec1[idx] = make_float4(conic.z, a.opacities[idx], p_view.z, 0.0f);
+  g.rec2[idx] = make_float4(rgb.x, rgb.y, rgb.z, 0.0f);
+  g.rect[idx] = make_uint2((uint32_t)xmin | ((uint32_t)ymin << 16), (uint32_t)xmax | ((uint32_t)ymax << 16));
+  g.clamped[idx] = clamp_bits;
+  a.radii[idx] = r;
+  g.tiles_touched[idx] = (uint32_t)area;
+}
+
+void launch_preprocess(const PreprocessArgs& a, const GeomState& g, hipStream_t stream) {
+  if (a.P <= 0) return;
+  hipLaunchKernelGGL(k_preprocess, dim3((a.P + 255) / 256), dim3(256), 0, stream, a, g);
+}
+
+}  // namespace gsr

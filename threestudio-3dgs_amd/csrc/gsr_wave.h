@@ -1,0 +1,88 @@
+// gsr_wave.h — wave64 / workgroup primitives for CDNA4 (gfx950): DPP reductions, ballot-based
+// digit matching, block scans.  Wave width is hard-coded to 64.
+#pragma once
+
+#include "gsr_common.h"
+
+namespace gsr {
+
+__device__ __forceinline__ int lane_id() { return __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0)); }
+
+// popcount of the bits of `mask` below this lane (v_mbcnt).
+__device__ __forceinline__ uint32_t mask_rank(unsigned long long mask) {
+  return __builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0));
+}
+
+template <int CTRL, int ROW_MASK = 0xf>
+__device__ __forceinline__ float dpp_f32(float x) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), CTRL, ROW_MASK, 0xf, true));
+}
+
+// Sum over the 64 lanes of a wave (all lanes must be active).  Row prefix via DPP row_shr
+// 1/2/4/8, then row_bcast:15 / row_bcast:31 fold the four rows into lane 63, read back as a
+// wave-uniform value.  6 DPP adds + 1 readlane.
+__device__ __forceinline__ float wave_sum(float x) {
+  x += dpp_f32<0x111>(x);
+  x += dpp_f32<0x112>(x);
+  x += dpp_f32<0x114>(x);
+  x += dpp_f32<0x118>(x);
+  x += dpp_f32<0x142, 0xa>(x);
+  x += dpp_f32<0x143, 0xc>(x);
+  return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(x), 63));
+}
+
+// Lanes of this wave whose `bits`-bit digit equals ours (restricted to lanes with valid=true).
+__device__ __forceinline__ unsigned long long match_digit(uint32_t d, int bits, bool valid) {
+  unsigned long long peers = __ballot(valid);
+  for (int b = 0; b < bits; ++b) {
+    const bool bit = (d >> b) & 1u;
+    const unsigned long long bal = __ballot(bit);
+    peers &= bit ? bal : ~bal;
+  }
+  return peers;
+}
+
+// Inclusive scan over a wave (u32), Hillis-Steele via shuffles.
+__device__ __forceinline__ uint32_t wave_inclusive_scan(uint32_t x) {
+  const int lane = threadIdx.x & 63;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint32_t y = __shfl_up(x, o, 64);
+    if (lane >= o) x += y;
+  }
+  return x;
+}
+
+// Exclusive scan of one value per thread over a workgroup of NT threads (NT/64 <= 16 waves).
+// s_wave: NT/64 + 1 words of LDS.  Returns the exclusive prefix; *total gets the block sum.
+template <int NT>
+__device__ __forceinline__ uint32_t block_exclusive_scan(uint32_t v, uint32_t* total, uint32_t* s_wave) {
+  constexpr int NW = NT / 64;
+  const int t = threadIdx.x, w = t >> 6, lane = t & 63;
+  const uint32_t inc = wave_inclusive_scan(v);
+  if (lane == 63) s_wave[w] = inc;
+  __syncthreads();
+  if (t == 0) {
+    uint32_t run = 0;
+    for (int i = 0; i < NW; ++i) {
+      const uint32_t c = s_wave[i];
+      s_wave[i] = run;
+      run += c;
+    }
+    s_wave[NW] = run;
+  }
+  __syncthreads();
+  const uint32_t res = s_wave[w] + inc - v;
+  *total = s_wave[NW];
+  __syncthreads();
+  return res;
+}
+
+template <int NT>
+__device__ __forceinline__ uint32_t block_sum_u32(uint32_t v, uint32_t* s_wave) {
+  uint32_t tot;
+  block_exclusive_scan<NT>(v, &tot, s_wave);
+  return tot;
+}
+
+}  // namespace gsr

@@ -1,0 +1,239 @@
+"""ctypes binding of libgsr_hip.so (include/gsr.h) exposing the reference extension's entry points.
+
+The reference imports the pybind module ``diff_gaussian_rasterization._C`` (external, ashawkey
+4-output fork; call sites e.g. renderer/diff_gaussian_rasterizer_background.py:119-128 through the
+Python wrapper).  This module provides the same three functions with the same argument order and
+return tuples, implemented over the C ABI:
+
+    rasterize_gaussians(...)          -> (num_rendered, color, depth, alpha, radii, geomBuf, binningBuf, imgBuf)
+    rasterize_gaussians_backward(...) -> (dL_dmeans2D, dL_dcolors, dL_dopacity, dL_dmeans3D,
+                                          dL_dcov3D, dL_dsh, dL_dscales, dL_drotations)
+    mark_visible(means3D, viewmatrix, projmatrix) -> bool (P,)
+
+All buffers are torch tensors from the caching allocator on ``means3D.device``; kernels run on the
+current HIP stream.  There is no CPU fallback: a missing library or a non-GPU tensor raises.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+import torch
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get("GSR_HIP_LIB", os.path.join(_HERE, "libgsr_hip.so"))
+
+_lib = None
+
+_vp = ctypes.c_void_p
+_i = ctypes.c_int
+_f = ctypes.c_float
+_sz = ctypes.c_size_t
+
+# name -> (restype, argtypes); must match include/gsr.h exactly (checked by tests/test_abi.py)
+SIGNATURES = {
+    "gsr_version": (ctypes.c_char_p, []),
+    "gsr_last_error": (ctypes.c_char_p, []),
+    "gsr_geom_bytes": (_sz, [_i]),
+    "gsr_binning_bytes": (_sz, [_i, _i, _i]),
+    "gsr_image_bytes": (_sz, [_i, _i]),
+    "gsr_backward_bytes": (_sz, [_i, _i]),
+    "gsr_forward_preprocess": (
+        _i,
+        [_i, _i, _i, _vp, _vp, _f, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i, _i, _f, _f, _i, _vp, _vp, _vp],
+    ),
+    "gsr_num_rendered": (_i, [_vp, _i, ctypes.POINTER(_i), ctypes.POINTER(_i), _vp]),
+    "gsr_forward_render": (_i, [_i, _i, _i, _i, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
+    "gsr_backward": (
+        _i,
+        [_i, _i, _i, _i, _i, _i, _vp, _vp, _vp, _f, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _f, _f,
+         _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp],
+    ),
+    "gsr_mark_visible": (_i, [_i, _vp, _vp, _vp, _vp, _vp]),
+}
+
+
+class GSRError(RuntimeError):
+    pass
+
+
+def load_library(path: str | None = None):
+    """Load (once) and type the C-ABI library.  Raises ImportError if it is missing."""
+    global _lib
+    if _lib is not None and path is None:
+        return _lib
+    p = path or LIB_PATH
+    if not os.path.exists(p):
+        raise ImportError(
+            f"diff_gaussian_rasterization: HIP library not found at {p}; "
+            "build it with `make -C threestudio-3dgs_amd/csrc` (or __graft_entry__.build())"
+        )
+    lib = ctypes.CDLL(p)
+    for name, (res, args) in SIGNATURES.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    if path is None:
+        _lib = lib
+    return lib
+
+
+def _check(rc: int):
+    if rc != 0:
+        msg = load_library().gsr_last_error().decode(errors="replace")
+        if rc == 1:
+            raise GSRError(msg)
+        raise GSRError(f"HIP failure: {msg}")
+
+
+def _ptr(t):
+    if t is None or t.numel() == 0:
+        return None
+    return ctypes.c_void_p(t.data_ptr())
+
+
+def _stream(device):
+    return ctypes.c_void_p(torch.cuda.current_stream(device).cuda_stream)
+
+
+def _f32(t, name, device):
+    if t is None or t.numel() == 0:
+        return None
+    if not t.is_cuda:
+        raise GSRError(f"{name} must be a GPU tensor (the rasterizer has no CPU path)")
+    if t.device != device:
+        raise GSRError(f"{name} is on {t.device}, expected {device}")
+    if t.dtype != torch.float32:
+        t = t.float()
+    return t.contiguous()
+
+
+def _require_gpu(device):
+    if device.type != "cuda":
+        raise GSRError("diff_gaussian_rasterization requires tensors on a ROCm GPU (device 'cuda')")
+
+
+def sh_coeff_count(sh) -> int:
+    return 0 if sh is None or sh.numel() == 0 else int(sh.shape[1])
+
+
+def rasterize_gaussians(bg, means3D, colors, opacity, scales, rotations, scale_modifier, cov3D_precomp,
+                        viewmatrix, projmatrix, tan_fovx, tan_fovy, image_height, image_width, sh, degree,
+                        campos, prefiltered, debug):
+    """Forward pass; argument order of the reference's _C.rasterize_gaussians."""
+    if means3D.dim() != 2 or means3D.size(1) != 3:
+        raise GSRError("means3D must have dimensions (num_points, 3)")
+    device = means3D.device
+    _require_gpu(device)
+    lib = load_library()
+    P = int(means3D.size(0))
+    H, W = int(image_height), int(image_width)
+    fopt = dict(dtype=torch.float32, device=device)
+    out_color = torch.zeros((3, H, W), **fopt)
+    out_depth = torch.zeros((1, H, W), **fopt)
+    out_alpha = torch.zeros((1, H, W), **fopt)
+    radii = torch.zeros((P,), dtype=torch.int32, device=device)
+    u8 = dict(dtype=torch.uint8, device=device)
+    if P == 0:
+        return 0, out_color, out_depth, out_alpha, radii, torch.empty(0, **u8), torch.empty(0, **u8), torch.empty(0, **u8)
+
+    means3D = _f32(means3D, "means3D", device)
+    colors = _f32(colors, "colors_precomp", device)
+    opacity = _f32(opacity, "opacities", device)
+    scales = _f32(scales, "scales", device)
+    rotations = _f32(rotations, "rotations", device)
+    cov3D_precomp = _f32(cov3D_precomp, "cov3D_precomp", device)
+    sh = _f32(sh, "sh", device)
+    view = _f32(viewmatrix, "viewmatrix", device)
+    proj = _f32(projmatrix, "projmatrix", device)
+    cam = _f32(campos, "campos", device)
+    bg = _f32(bg, "bg", device)
+    M = sh_coeff_count(sh)
+    for name, t, n in (("opacities", opacity, P), ("scales", scales, 3 * P), ("rotations", rotations, 4 * P),
+                       ("colors_precomp", colors, 3 * P), ("cov3D_precomp", cov3D_precomp, 6 * P),
+                       ("sh", sh, 3 * M * P)):
+        if t is not None and t.numel() != n:
+            raise GSRError(f"{name} has {t.numel()} elements, expected {n}")
+    if view is None or view.numel() != 16 or proj is None or proj.numel() != 16:
+        raise GSRError("viewmatrix and projmatrix must be 4x4")
+    if cam is None or cam.numel() != 3 or bg is None or bg.numel() != 3:
+        raise GSRError("campos and bg must have 3 elements")
+
+    stream = _stream(device)
+    geom = torch.empty(int(lib.gsr_geom_bytes(P)), **u8)
+    _check(lib.gsr_forward_preprocess(
+        P, int(degree), M, _ptr(means3D), _ptr(scales), float(scale_modifier), _ptr(rotations), _ptr(opacity),
+        _ptr(sh), _ptr(colors), _ptr(cov3D_precomp), _ptr(view), _ptr(proj), _ptr(cam), W, H,
+        float(tan_fovx), float(tan_fovy), int(bool(prefiltered)), _ptr(radii), _ptr(geom), stream))
+    K = ctypes.c_int(0)
+    nvis = ctypes.c_int(0)
+    _check(lib.gsr_num_rendered(_ptr(geom), P, ctypes.byref(K), ctypes.byref(nvis), stream))
+    num_rendered = int(K.value)
+    binning = torch.empty(int(lib.gsr_binning_bytes(num_rendered, W, H)), **u8)
+    image = torch.empty(int(lib.gsr_image_bytes(W, H)), **u8)
+    _check(lib.gsr_forward_render(P, num_rendered, W, H, _ptr(bg), _ptr(geom), _ptr(binning), _ptr(image),
+                                  _ptr(out_color), _ptr(out_depth), _ptr(out_alpha), stream))
+    return num_rendered, out_color, out_depth, out_alpha, radii, geom, binning, image
+
+
+def rasterize_gaussians_backward(bg, means3D, radii, colors, scales, rotations, scale_modifier, cov3D_precomp,
+                                 viewmatrix, projmatrix, tan_fovx, tan_fovy, dL_dout_color, dL_dout_depth,
+                                 dL_dout_alpha, sh, degree, campos, geomBuffer, R, binningBuffer, imageBuffer,
+                                 alpha, debug):
+    """Backward pass; argument order and return tuple of the reference's _C.rasterize_gaussians_backward."""
+    device = means3D.device
+    _require_gpu(device)
+    lib = load_library()
+    P = int(means3D.size(0))
+    H, W = int(dL_dout_color.size(1)), int(dL_dout_color.size(2))
+    M = sh_coeff_count(sh)
+    fopt = dict(dtype=torch.float32, device=device)
+    dL_dmeans3D = torch.zeros((P, 3), **fopt) if P == 0 else torch.empty((P, 3), **fopt)
+    dL_dmeans2D = torch.zeros((P, 3), **fopt) if P == 0 else torch.empty((P, 3), **fopt)
+    dL_dcolors = torch.zeros((P, 3), **fopt) if P == 0 else torch.empty((P, 3), **fopt)
+    dL_dopacity = torch.zeros((P, 1), **fopt) if P == 0 else torch.empty((P, 1), **fopt)
+    dL_dcov3D = torch.zeros((P, 6), **fopt) if P == 0 else torch.empty((P, 6), **fopt)
+    dL_dsh = torch.zeros((P, M, 3), **fopt) if (P == 0 or M == 0) else torch.empty((P, M, 3), **fopt)
+    dL_dscales = torch.zeros((P, 3), **fopt)
+    dL_drotations = torch.zeros((P, 4), **fopt)
+    if P == 0:
+        return dL_dmeans2D, dL_dcolors, dL_dopacity, dL_dmeans3D, dL_dcov3D, dL_dsh, dL_dscales, dL_drotations
+
+    means3D = _f32(means3D, "means3D", device)
+    scales = _f32(scales, "scales", device)
+    rotations = _f32(rotations, "rotations", device)
+    cov3D_precomp = _f32(cov3D_precomp, "cov3D_precomp", device)
+    sh = _f32(sh, "sh", device)
+    colors = _f32(colors, "colors_precomp", device)
+    view = _f32(viewmatrix, "viewmatrix", device)
+    proj = _f32(projmatrix, "projmatrix", device)
+    cam = _f32(campos, "campos", device)
+    bg = _f32(bg, "bg", device)
+    gc = _f32(dL_dout_color, "dL_dout_color", device)
+    gd = _f32(dL_dout_depth, "dL_dout_depth", device)
+    ga = _f32(dL_dout_alpha, "dL_dout_alpha", device)
+    if radii.dtype != torch.int32:
+        radii = radii.int()
+    radii = radii.contiguous()
+    K = int(R)
+    stream = _stream(device)
+    work = torch.empty(int(lib.gsr_backward_bytes(P, K)), dtype=torch.uint8, device=device)
+    _check(lib.gsr_backward(
+        P, int(degree), M, K, W, H, _ptr(bg), _ptr(means3D), _ptr(scales), float(scale_modifier), _ptr(rotations),
+        None, _ptr(sh), _ptr(colors), _ptr(cov3D_precomp), _ptr(view), _ptr(proj), _ptr(cam),
+        float(tan_fovx), float(tan_fovy), _ptr(radii), _ptr(geomBuffer), _ptr(binningBuffer), _ptr(imageBuffer),
+        _ptr(gc), _ptr(gd), _ptr(ga), _ptr(dL_dmeans2D), _ptr(dL_dcolors), _ptr(dL_dopacity), _ptr(dL_dmeans3D),
+        _ptr(dL_dcov3D), _ptr(dL_dsh), _ptr(dL_dscales), _ptr(dL_drotations), _ptr(work), stream))
+    return dL_dmeans2D, dL_dcolors, dL_dopacity, dL_dmeans3D, dL_dcov3D, dL_dsh, dL_dscales, dL_drotations
+
+
+def mark_visible(means3D, viewmatrix, projmatrix):
+    device = means3D.device
+    _require_gpu(device)
+    lib = load_library()
+    P = int(means3D.size(0))
+    present = torch.zeros((P,), dtype=torch.uint8, device=device)
+    if P > 0:
+        _check(lib.gsr_mark_visible(P, _ptr(_f32(means3D, "means3D", device)), _ptr(_f32(viewmatrix, "viewmatrix", device)),
+                                    _ptr(_f32(projmatrix, "projmatrix", device)), _ptr(present), _stream(device)))
+    return present.bool()
