@@ -1,0 +1,277 @@
+#!/usr/bin/env python
+"""Benchmark: rendered views/sec, forward+backward, 1M Gaussians, 1024^2, SH degree 3 (BASELINE.json).
+
+A step is one pass of the hot path over one batch of views: every view of the batch is rendered
+through the drop-in GaussianRasterizer API (preprocess, binning, forward blend), composited on a
+constant background exactly like renderer/diff_gaussian_rasterizer_background.py:129-132, the
+rendered images are all-gathered across ranks (RCCL over xGMI; the north_star exchange), then the
+backward of a seeded synthetic loss runs through the rasterizer and the per-Gaussian parameter
+gradients are all-reduced (sum) so every replica holds the full-batch gradient.
+
+Workload (BASELINE.json configs[2] / configs[3]): C3 per view (1M Gaussians, 1024^2,
+SH3, background path: bg = 0 + constant composite) over the C4 64-view MVDream-style orbit batch
+(4 elevations x 16 azimuths), views sharded across ranks (strong scaling: the 64-view batch is fixed).
+
+Single GPU:  python bench.py [--steps K --warmup W]
+N GPUs:      python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 \
+                 --master-port P bench.py --gpus N --steps K --warmup W
+Rank 0 prints one JSON line.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import math
+import os
+import platform
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "threestudio-3dgs_amd"))
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+METRIC = "rendered views/sec fwd+bwd @1M Gaussians, 1024², SH=3; 1/2/4/8 GPU"
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md chip table)
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--gaussians", type=int, default=1_000_000)
+    ap.add_argument("--res", type=int, default=1024)
+    ap.add_argument("--views", type=int, default=64, help="global views per step (sharded over ranks)")
+    ap.add_argument("--sh-degree", type=int, default=3)
+    ap.add_argument("--cpu-views", type=int, default=3, help="views of the same workload timed on the CPU oracle")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-profile", action="store_true")
+    return ap.parse_args()
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+class Replica:
+    """Gaussian parameters (activated values, as the geometry getters return them) on one GPU."""
+
+    def __init__(self, scene, device):
+        def leaf(x):
+            return torch.tensor(x, device=device, requires_grad=True)
+
+        self.means3D = leaf(scene["means3D"])
+        self.scales = leaf(scene["scales"])
+        self.rotations = leaf(scene["rotations"])
+        self.opacities = leaf(scene["opacities"])
+        self.shs = leaf(scene["shs"])
+        self.sh_degree = int(scene["sh_degree"])
+        self.params = [self.means3D, self.scales, self.rotations, self.opacities, self.shs]
+
+    def zero_grad(self):
+        for p in self.params:
+            p.grad = None
+
+
+def build_views(n_views, res, device):
+    from diff_gaussian_rasterization.cameras import get_cam_info_gaussian, orbit_c2w
+
+    n_el = 4
+    per = max(1, n_views // n_el)
+    elev = torch.tensor([[0.0, 10.0, 20.0, 30.0][(i // per) % n_el] for i in range(n_views)])
+    azim = torch.tensor([(i % per) * 360.0 / per for i in range(n_views)])
+    fovy = math.radians(60.0)
+    c2w = orbit_c2w(torch.full((n_views,), 2.5), elev, azim)
+    wv, fp, cc = get_cam_info_gaussian(c2w, fovy, fovy, 0.1, 100.0)
+    tan = math.tan(fovy * 0.5)
+    return [dict(view=wv[i].to(device), proj=fp[i].to(device), campos=cc[i].to(device), tan=tan, H=res, W=res)
+            for i in range(n_views)]
+
+
+def render_view(rep: Replica, cam, bg_zero, bg_const):
+    from diff_gaussian_rasterization import GaussianRasterizationSettings, GaussianRasterizer
+
+    P = rep.means3D.shape[0]
+    screenspace = torch.zeros((P, 3), device=rep.means3D.device, requires_grad=True) + 0
+    s = GaussianRasterizationSettings(image_height=cam["H"], image_width=cam["W"], tanfovx=cam["tan"],
+                                      tanfovy=cam["tan"], bg=bg_zero, scale_modifier=1.0,
+                                      viewmatrix=cam["view"], projmatrix=cam["proj"], sh_degree=rep.sh_degree,
+                                      campos=cam["campos"], prefiltered=False, debug=False)
+    color, radii, depth, alpha = GaussianRasterizer(raster_settings=s)(
+        means3D=rep.means3D, means2D=screenspace, shs=rep.shs, colors_precomp=None, opacities=rep.opacities,
+        scales=rep.scales, rotations=rep.rotations, cov3D_precomp=None)
+    # background path composite (renderer/diff_gaussian_rasterizer_background.py:129-132)
+    comp = color + (1 - alpha) * bg_const[:, None, None]
+    return comp, depth, alpha, radii
+
+
+def cpu_baseline(scene, res, n_views):
+    """The CPU restatement (oracle, fp32, single thread) on `n_views` views of the same workload."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle  # test infrastructure; timed here only as the reported CPU baseline
+
+    import gsr_synthetic as gs
+    from diff_gaussian_rasterization.cameras import get_cam_info_gaussian, orbit_c2w
+
+    oracle.lib()
+    fovy = math.radians(60.0)
+    tan = math.tan(fovy / 2)
+    g = gs.upstream_grads(res, res, seed=1)
+    bg = np.zeros(3, np.float32)
+    t0 = time.perf_counter()
+    for i in range(n_views):
+        c2w = orbit_c2w(2.5, 0.0, i * 360.0 / 16)
+        wv, fp, cc = get_cam_info_gaussian(c2w, fovy, fovy, 0.1, 100.0)
+        cam = (wv.numpy().ravel(), fp.numpy().ravel(), cc.numpy(), tan, tan, res, res)
+        oracle.forward(scene, cam, bg, "f32")
+        oracle.backward(scene, cam, bg, *g, prec="f32")
+    dt = time.perf_counter() - t0
+    return dict(value=n_views / dt, unit="views/s", cores=1, kind="port",
+                sample=f"{n_views} views of the benchmark workload ({scene['means3D'].shape[0]} Gaussians, "
+                       f"{res}x{res}, SH{scene['sh_degree']}), forward + backward, oracle/gsr_oracle.c fp32, "
+                       f"1 thread on {platform.processor() or platform.machine()} "
+                       f"({os.cpu_count()} logical CPUs visible)",
+                seconds=dt)
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    device = torch.device("cuda", local)
+    torch.cuda.set_device(device)
+
+    import gsr_synthetic as gs
+    from diff_gaussian_rasterization import _C
+
+    assert args.views % world == 0, "views must divide evenly over ranks"
+    t_setup = time.perf_counter()
+    scene = gs.make_scene(args.gaussians, sh_degree=args.sh_degree, seed=0)  # identical replica on every rank
+    rep = Replica(scene, device)
+    cams = build_views(args.views, args.res, device)
+    per = args.views // world
+    mine = cams[rank * per:(rank + 1) * per]
+    H = W = args.res
+    gen = torch.Generator(device=device).manual_seed(1234 + rank)
+    upstream = [(torch.randn((3, H, W), generator=gen, device=device),
+                 torch.randn((1, H, W), generator=gen, device=device),
+                 torch.randn((1, H, W), generator=gen, device=device)) for _ in mine]
+    bg_zero = torch.zeros(3, device=device)
+    bg_const = torch.tensor([0.5, 0.5, 0.5], device=device)
+    gathered = torch.empty((args.views, 5, H, W), device=device) if world > 1 else None
+    flat_grad = None
+    log(f"[bench] rank {rank}/{world}: setup {time.perf_counter() - t_setup:.1f}s, {len(mine)} views/rank")
+
+    def step():
+        nonlocal flat_grad
+        outs = [render_view(rep, cam, bg_zero, bg_const) for cam in mine]
+        if world > 1:
+            local_imgs = torch.stack([torch.cat([c, d, a], 0) for c, d, a, _ in outs]).detach()
+            dist.all_gather_into_tensor(gathered, local_imgs)
+        loss = sum((c * g[0]).sum() + (d * g[1]).sum() + (a * g[2]).sum() for (c, d, a, _), g in zip(outs, upstream))
+        loss.backward()
+        if world > 1:
+            grads = [p.grad.reshape(-1) for p in rep.params]
+            flat_grad = torch.cat(grads) if flat_grad is None else torch.cat(grads, out=flat_grad)
+            dist.all_reduce(flat_grad)
+        rep.zero_grad()
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    _C.RECENT_FORWARDS.clear()
+    if not args.no_profile:
+        _C.profile_read(reset=True)
+        _C.profile_enable(True)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    phases = None
+    if not args.no_profile:
+        _C.profile_enable(False)
+        phases = _C.profile_read(reset=True)
+    if world > 1:
+        t = torch.tensor([elapsed], device=device, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+
+    total_views = args.views * args.steps
+    value = total_views / elapsed
+    Ks = [k for k, _, _ in _C.RECENT_FORWARDS]
+    K_mean = float(np.mean(Ks)) if Ks else 0.0
+
+    if rank != 0:
+        if world > 1:
+            dist.destroy_process_group()
+        return
+
+    res = {
+        "metric": METRIC,
+        "value": round(value, 3),
+        "unit": "views/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(1000.0 * elapsed / args.steps, 3),
+        "higher_is_better": True,
+        "scaling": "strong",
+        "vs_baseline": None,
+        "dtype": "fp32",
+        "data": "synthetic (seeded scene per SURVEY.md §8d; no datasets offline)",
+        "config": {
+            "workload": "C3 per view (1M Gaussians, 1024x1024, SH3, background path) over the C4 64-view "
+                        "orbit batch, fwd+bwd + image all-gather + gradient all-reduce",
+            "n_gaussians": args.gaussians, "resolution": [H, W], "sh_degree": args.sh_degree,
+            "global_views_per_step": args.views, "views_per_rank": per,
+            "parallelism": f"views sharded over {world} rank(s) (RCCL all-gather images, all-reduce grads)",
+            "mean_instances_K": round(K_mean),
+        },
+    }
+    if phases is not None:
+        nv = max(1, args.steps * per)
+        kern = {k: {"ms_per_view": round(ms / nv, 4), "launches": n} for k, (ms, n) in phases.items()}
+        res["kernels"] = kern
+        # forward tile blend (north_star roofline kernel): SURVEY.md §8d B_fwd = 44 K + 28 HW + 8 tiles
+        tiles = math.ceil(W / 16) * math.ceil(H / 16)
+        f_ms, f_n = phases["render_fwd"]
+        b_ms, b_n = phases["render_bwd"]
+        bytes_fwd = 44.0 * K_mean + 28.0 * H * W + 8.0 * tiles
+        bytes_bwd = 84.0 * K_mean + 28.0 * H * W + 8.0 * tiles  # 44 K gathered + 40 K grads + per-pixel
+        fwd_gbs = bytes_fwd / (f_ms / max(1, f_n) * 1e-3) / 1e9 if f_n else 0.0
+        bwd_gbs = bytes_bwd / (b_ms / max(1, b_n) * 1e-3) / 1e9 if b_n else 0.0
+        dominant = max(phases.items(), key=lambda kv: kv[1][0])[0]
+        roof_fwd = {"kernel": "k_render_fwd", "bound": "hbm", "achieved": round(fwd_gbs, 1), "peak": HBM_PEAK_GBS,
+                    "unit": "GB/s", "frac": round(fwd_gbs / HBM_PEAK_GBS, 4), "traffic": None,
+                    "avg_launch_us": round(1000 * f_ms / max(1, f_n), 2), "algorithmic_bytes": round(bytes_fwd)}
+        roof_bwd = {"kernel": "k_render_bwd", "bound": "hbm", "achieved": round(bwd_gbs, 1), "peak": HBM_PEAK_GBS,
+                    "unit": "GB/s", "frac": round(bwd_gbs / HBM_PEAK_GBS, 4), "traffic": None,
+                    "avg_launch_us": round(1000 * b_ms / max(1, b_n), 2), "algorithmic_bytes": round(bytes_bwd)}
+        res["roofline"] = roof_bwd if dominant == "render_bwd" else roof_fwd
+        res["roofline_fwd_blend"] = roof_fwd
+        res["dominant_kernel"] = dominant
+    if world == 1 and not args.no_cpu_baseline:
+        cb = cpu_baseline(scene, args.res, args.cpu_views)
+        res["cpu_baseline"] = {k: (round(v, 5) if isinstance(v, float) else v) for k, v in cb.items()}
+    print(json.dumps(res), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

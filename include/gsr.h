@@ -117,6 +117,22 @@ int gsr_backward(int P, int degree, int M, int K, int width, int height, const f
                  float* dL_dcov3D, float* dL_dsh, float* dL_dscales, float* dL_drotations,
                  void* work, void* stream);
 
+/*
+ * Optional phase timing with HIP events recorded on the launch stream around each phase's kernels.
+ * Off by default; while on, every call above records one event pair per phase it runs.
+ * gsr_profile_read synchronises the recorded events and returns, per phase, the accumulated
+ * milliseconds and the number of timed launches since the last reset (arrays of GSR_NUM_PHASES).
+ */
+#define GSR_PHASE_PREPROCESS 0 /* k_preprocess                                              */
+#define GSR_PHASE_DEPTH_SORT 1 /* visible compaction, depth radix sort, instance-offset scan */
+#define GSR_PHASE_BINNING 2    /* duplicate, tile radix sort, tile ranges                   */
+#define GSR_PHASE_RENDER_FWD 3 /* k_render_fwd: forward tile blend                          */
+#define GSR_PHASE_RENDER_BWD 4 /* k_render_bwd: backward tile blend                         */
+#define GSR_PHASE_GAUSS_BWD 5  /* k_gauss_bwd: fused per-Gaussian backward                   */
+#define GSR_NUM_PHASES 6
+int gsr_profile_enable(int enable);
+int gsr_profile_read(double* ms, long long* launches, int reset);
+
 /* Replaces markVisible/checkFrustum (API completeness; unused by the reference).  present (P,) u8. */
 int gsr_mark_visible(int P, const float* means3D, const float* viewmatrix, const float* projmatrix,
                      uint8_t* present, void* stream);

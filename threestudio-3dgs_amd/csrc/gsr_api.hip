@@ -7,6 +7,8 @@
 #include <string.h>
 
 #include <cmath>
+#include <mutex>
+#include <vector>
 
 #include "../../include/gsr.h"
 #include "gsr_kernels.h"
@@ -32,6 +34,57 @@ static int last_launch() {
   g_err[0] = 0;
   return GSR_OK;
 }
+
+// ---- phase profiler: event pairs on the launch stream, resolved lazily in gsr_profile_read ----
+namespace {
+struct PhaseEvents {
+  int phase;
+  hipEvent_t a, b;
+};
+struct Profiler {
+  std::mutex mu;
+  bool on = false;
+  std::vector<hipEvent_t> pool;
+  std::vector<PhaseEvents> pending;
+  double ms[GSR_NUM_PHASES] = {0};
+  long long n[GSR_NUM_PHASES] = {0};
+  hipEvent_t get() {
+    if (!pool.empty()) {
+      hipEvent_t e = pool.back();
+      pool.pop_back();
+      return e;
+    }
+    hipEvent_t e = nullptr;
+    if (hipEventCreate(&e) != hipSuccess) return nullptr;
+    return e;
+  }
+};
+Profiler& prof() {
+  static Profiler p;
+  return p;
+}
+// RAII scope: records a start event at construction and an end event at destruction.
+struct PhaseScope {
+  hipEvent_t a = nullptr, b = nullptr;
+  hipStream_t s;
+  int phase;
+  PhaseScope(int ph, hipStream_t st) : s(st), phase(ph) {
+    Profiler& p = prof();
+    if (!p.on) return;
+    std::lock_guard<std::mutex> g(p.mu);
+    a = p.get();
+    b = p.get();
+    if (a) (void)hipEventRecord(a, s);
+  }
+  ~PhaseScope() {
+    if (a == nullptr || b == nullptr) return;
+    (void)hipEventRecord(b, s);
+    Profiler& p = prof();
+    std::lock_guard<std::mutex> g(p.mu);
+    p.pending.push_back({phase, a, b});
+  }
+};
+}  // namespace
 
 static int effective_degree(int degree, int M) {
   // the reference reads sqrt(M)-1 coefficients at most (pred-normal pass quirk)
@@ -124,15 +177,21 @@ int gsr_forward_preprocess(int P, int degree, int M, const float* means3D, const
   a.focal_y = height / (2.0f * tanfovy);
   a.focal_x = width / (2.0f * tanfovx);
   a.radii = radii;
-  launch_preprocess(a, g, s);
-  // visible compaction -> depth sort -> instance offsets in depth order
-  scan_exclusive(SCAN_FLAG, g.tiles_touched, nullptr, g.vis_off, nullptr, P, g.scan_blk,
-                 g.counters + 0, s);
-  launch_compact_visible(P, g, s);
-  const int res = radix_sort_pairs(g.dkey, g.dval, false, g.counters + 0, P, 32, g.hist, g.hist_blk, s);
-  if (res != 0) return fail(GSR_EHIP, "%s", "internal: depth sort result buffer");
-  scan_exclusive(SCAN_GATHER, g.tiles_touched, g.dval[0], g.point_offsets, g.counters + 0, P,
-                 g.scan_blk, g.counters + 1, s);
+  {
+    PhaseScope ps(GSR_PHASE_PREPROCESS, s);
+    launch_preprocess(a, g, s);
+  }
+  {
+    // visible compaction -> depth sort -> instance offsets in depth order
+    PhaseScope ps(GSR_PHASE_DEPTH_SORT, s);
+    scan_exclusive(SCAN_FLAG, g.tiles_touched, nullptr, g.vis_off, nullptr, P, g.scan_blk,
+                   g.counters + 0, s);
+    launch_compact_visible(P, g, s);
+    const int res = radix_sort_pairs(g.dkey, g.dval, false, g.counters + 0, P, 32, g.hist, g.hist_blk, s);
+    if (res != 0) return fail(GSR_EHIP, "%s", "internal: depth sort result buffer");
+    scan_exclusive(SCAN_GATHER, g.tiles_touched, g.dval[0], g.point_offsets, g.counters + 0, P,
+                   g.scan_blk, g.counters + 1, s);
+  }
   return last_launch();
 }
 
@@ -163,12 +222,16 @@ int gsr_forward_render(int P, int K, int width, int height, const float* bg, voi
   const int gx = div_up(width, GSR_TILE_X), gy = div_up(height, GSR_TILE_Y);
   GSR_HIP_CHECK(hipMemsetAsync(img.ranges, 0, sizeof(uint2) * (size_t)gx * gy, s));
   if (K > 0) {
+    PhaseScope ps(GSR_PHASE_BINNING, s);
     launch_duplicate(P, gx, g.dval[0], g, b, s);
     const int res = radix_sort_pairs(b.key, b.val, true, nullptr, K, tile_key_bits(width, height),
                                      b.hist, b.hist_blk, s);
     launch_finalize_bins(K, b.key[res], b.val[res], b, img.ranges, s);
   }
-  launch_render_forward(width, height, g, b, img, bg, out_color, out_depth, out_alpha, s);
+  {
+    PhaseScope ps(GSR_PHASE_RENDER_FWD, s);
+    launch_render_forward(width, height, g, b, img, bg, out_color, out_depth, out_alpha, s);
+  }
   return last_launch();
 }
 
@@ -199,7 +262,10 @@ int gsr_backward(int P, int degree, int M, int K, int width, int height, const f
   BinningState b = BinningState::carve((void*)binning, K, nullptr);
   ImageState img = ImageState::carve((void*)image, width, height, nullptr);
   BackwardState bw = BackwardState::carve(work, K, nullptr);
-  launch_render_backward(width, height, K, g, b, img, bg, dL_dcolor, dL_ddepth, dL_dalpha, bw, s);
+  {
+    PhaseScope ps(GSR_PHASE_RENDER_BWD, s);
+    launch_render_backward(width, height, K, g, b, img, bg, dL_dcolor, dL_ddepth, dL_dalpha, bw, s);
+  }
 
   GaussBackwardArgs a;
   a.P = P;
@@ -227,8 +293,42 @@ int gsr_backward(int P, int degree, int M, int K, int width, int height, const f
   a.dL_dsh = shs ? dL_dsh : nullptr;
   a.dL_dscales = cov3D_precomp ? nullptr : dL_dscales;
   a.dL_drotations = cov3D_precomp ? nullptr : dL_drotations;
-  launch_gauss_backward(a, g, b, bw, s);
+  {
+    PhaseScope ps(GSR_PHASE_GAUSS_BWD, s);
+    launch_gauss_backward(a, g, b, bw, s);
+  }
   return last_launch();
+}
+
+int gsr_profile_enable(int enable) {
+  Profiler& p = prof();
+  std::lock_guard<std::mutex> g(p.mu);
+  p.on = enable != 0;
+  return GSR_OK;
+}
+
+int gsr_profile_read(double* ms, long long* launches, int reset) {
+  Profiler& p = prof();
+  std::lock_guard<std::mutex> g(p.mu);
+  for (const PhaseEvents& e : p.pending) {
+    float t = 0.f;
+    GSR_HIP_CHECK(hipEventSynchronize(e.b));
+    GSR_HIP_CHECK(hipEventElapsedTime(&t, e.a, e.b));
+    p.ms[e.phase] += t;
+    p.n[e.phase] += 1;
+    p.pool.push_back(e.a);
+    p.pool.push_back(e.b);
+  }
+  p.pending.clear();
+  for (int i = 0; i < GSR_NUM_PHASES; ++i) {
+    if (ms) ms[i] = p.ms[i];
+    if (launches) launches[i] = p.n[i];
+    if (reset) {
+      p.ms[i] = 0;
+      p.n[i] = 0;
+    }
+  }
+  return GSR_OK;
 }
 
 int gsr_mark_visible(int P, const float* means3D, const float* viewmatrix, const float* projmatrix,

@@ -50,7 +50,13 @@ SIGNATURES = {
          _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp],
     ),
     "gsr_mark_visible": (_i, [_i, _vp, _vp, _vp, _vp, _vp]),
+    "gsr_profile_enable": (_i, [_i]),
+    "gsr_profile_read": (_i, [ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_longlong), _i]),
 }
+
+PHASES = ("preprocess", "depth_sort", "binning", "render_fwd", "render_bwd", "gauss_bwd")
+# (num_rendered, H, W) of recent forward calls, for instrumentation (bench.py roofline numbers)
+RECENT_FORWARDS: list = []
 
 
 class GSRError(RuntimeError):
@@ -169,6 +175,8 @@ def rasterize_gaussians(bg, means3D, colors, opacity, scales, rotations, scale_m
     nvis = ctypes.c_int(0)
     _check(lib.gsr_num_rendered(_ptr(geom), P, ctypes.byref(K), ctypes.byref(nvis), stream))
     num_rendered = int(K.value)
+    if len(RECENT_FORWARDS) < 4096:
+        RECENT_FORWARDS.append((num_rendered, H, W))
     binning = torch.empty(int(lib.gsr_binning_bytes(num_rendered, W, H)), **u8)
     image = torch.empty(int(lib.gsr_image_bytes(W, H)), **u8)
     _check(lib.gsr_forward_render(P, num_rendered, W, H, _ptr(bg), _ptr(geom), _ptr(binning), _ptr(image),
@@ -237,3 +245,16 @@ def mark_visible(means3D, viewmatrix, projmatrix):
         _check(lib.gsr_mark_visible(P, _ptr(_f32(means3D, "means3D", device)), _ptr(_f32(viewmatrix, "viewmatrix", device)),
                                     _ptr(_f32(projmatrix, "projmatrix", device)), _ptr(present), _stream(device)))
     return present.bool()
+
+
+def profile_enable(on: bool = True):
+    _check(load_library().gsr_profile_enable(1 if on else 0))
+
+
+def profile_read(reset: bool = True) -> dict:
+    """Accumulated per-phase kernel milliseconds and launch counts (HIP events on the launch stream)."""
+    n = len(PHASES)
+    ms = (ctypes.c_double * n)()
+    cnt = (ctypes.c_longlong * n)()
+    _check(load_library().gsr_profile_read(ms, cnt, 1 if reset else 0))
+    return {PHASES[i]: (float(ms[i]), int(cnt[i])) for i in range(n)}
