@@ -102,6 +102,12 @@ static int tile_key_bits(int W, int H) {
   return bits < 1 ? 1 : bits;
 }
 
+// ping-pong buffer holding the tile sort's result (one radix pass per <= 8 key bits)
+static int tile_sort_result(int W, int H) {
+  const int passes = (tile_key_bits(W, H) + GSR_RADIX_BITS - 1) / GSR_RADIX_BITS;
+  return passes & 1;
+}
+
 extern "C" {
 
 const char* gsr_version(void) { return "gsr 0.1.0 gfx950"; }
@@ -224,13 +230,15 @@ int gsr_forward_render(int P, int K, int width, int height, const float* bg, voi
   if (K > 0) {
     PhaseScope ps(GSR_PHASE_BINNING, s);
     launch_duplicate(P, gx, g.dval[0], g, b, s);
-    const int res = radix_sort_pairs(b.key, b.val, true, nullptr, K, tile_key_bits(width, height),
+    const int res = radix_sort_pairs(b.key, b.val, false, nullptr, K, tile_key_bits(width, height),
                                      b.hist, b.hist_blk, s);
-    launch_finalize_bins(K, b.key[res], b.val[res], b, img.ranges, s);
+    if (res != tile_sort_result(width, height)) return fail(GSR_EHIP, "%s", "internal: tile sort buffer");
+    launch_tile_ranges(K, b.key[res], img.ranges, s);
   }
   {
     PhaseScope ps(GSR_PHASE_RENDER_FWD, s);
-    launch_render_forward(width, height, g, b, img, bg, out_color, out_depth, out_alpha, s);
+    launch_render_forward(width, height, g, b.val[tile_sort_result(width, height)], img, bg, out_color,
+                          out_depth, out_alpha, s);
   }
   return last_launch();
 }
@@ -264,7 +272,8 @@ int gsr_backward(int P, int degree, int M, int K, int width, int height, const f
   BackwardState bw = BackwardState::carve(work, K, nullptr);
   {
     PhaseScope ps(GSR_PHASE_RENDER_BWD, s);
-    launch_render_backward(width, height, K, g, b, img, bg, dL_dcolor, dL_ddepth, dL_dalpha, bw, s);
+    launch_render_backward(width, height, K, g, b.val[tile_sort_result(width, height)], img, bg, dL_dcolor,
+                           dL_ddepth, dL_dalpha, bw, s);
   }
 
   GaussBackwardArgs a;
@@ -295,7 +304,7 @@ int gsr_backward(int P, int degree, int M, int K, int width, int height, const f
   a.dL_drotations = cov3D_precomp ? nullptr : dL_drotations;
   {
     PhaseScope ps(GSR_PHASE_GAUSS_BWD, s);
-    launch_gauss_backward(a, g, b, bw, s);
+    launch_gauss_backward(a, width, height, g, img, bw, s);
   }
   return last_launch();
 }

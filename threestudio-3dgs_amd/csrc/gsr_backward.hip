@@ -1,8 +1,8 @@
 // gsr_backward.hip — fused per-Gaussian backward.
 //
 // One thread per Gaussian:
-//   1. gather-sum of the Gaussian's per-instance gradient rows written by k_render_bwd
-//      (instances visited in pre-sort order -> fixed summation order, bitwise reproducible);
+//   1. gather-sum of the Gaussian's per-instance gradient rows written by k_render_bwd into the
+//      Gaussian's own contiguous slots (fixed summation order -> bitwise reproducible);
 //   2. BACKWARD::computeCov2DCUDA [EXT]: conic -> 2D cov -> 3D cov and camera-space mean;
 //   3. BACKWARD::preprocessCUDA [EXT]: 2D mean -> 3D mean through the projection, view-depth
 //      term (ashawkey depth output), SH -> RGB backward incl. the view-direction term,
@@ -16,8 +16,8 @@
 
 namespace gsr {
 
-__global__ __launch_bounds__(256) void k_gauss_bwd(GaussBackwardArgs a, GeomState g, BinningState b,
-                                                   BackwardState bw) {
+__global__ __launch_bounds__(256) void k_gauss_bwd(GaussBackwardArgs a, int grid_x, GeomState g,
+                                                   const uint4* __restrict__ tile_info, BackwardState bw) {
   const int idx = blockIdx.x * blockDim.x + threadIdx.x;
   if (idx >= a.P) return;
   const int Mc = a.M;
@@ -26,14 +26,23 @@ __global__ __launch_bounds__(256) void k_gauss_bwd(GaussBackwardArgs a, GeomStat
   float dmx = 0.f, dmy = 0.f, dca = 0.f, dcb = 0.f, dcc = 0.f, dop = 0.f;
   float dcr = 0.f, dcg = 0.f, dcbl = 0.f, ddep = 0.f;
   if (visible) {
-    const uint32_t i0 = g.goff[idx], cnt = g.tiles_touched[idx];
-    for (uint32_t i = i0; i < i0 + cnt; ++i) {
-      const size_t p = b.inv[i];
-      const float4 r0 = bw.grow[3 * p], r1 = bw.grow[3 * p + 1], r2 = bw.grow[3 * p + 2];
-      dmx += r0.x; dmy += r0.y; dca += r0.z; dcb += r0.w;
-      dcc += r1.x; dop += r1.y; dcr += r1.z; dcg += r1.w;
-      dcbl += r2.x; ddep += r2.y;
-    }
+    // rows of this Gaussian's instances are contiguous (tile rect, row-major); an instance's row is
+    // valid only if its tile's blend reached it: (depth key, index) < the tile's first unblended one
+    const size_t i0 = g.goff[idx];
+    const uint2 rc = g.rect[idx];
+    const int xmin = rc.x & 0xffff, ymin = rc.x >> 16, xmax = rc.y & 0xffff, ymax = rc.y >> 16;
+    const uint32_t dkey = __float_as_uint(g.rec1[idx].z);
+    size_t i = i0;
+    for (int ty = ymin; ty < ymax; ++ty)
+      for (int tx = xmin; tx < xmax; ++tx, ++i) {
+        const uint4 info = tile_info[ty * grid_x + tx];
+        const bool valid = dkey < info.y || (dkey == info.y && (uint32_t)idx < info.z);
+        if (!valid) continue;
+        const float4 r0 = bw.grow[3 * i], r1 = bw.grow[3 * i + 1], r2 = bw.grow[3 * i + 2];
+        dmx += r0.x; dmy += r0.y; dca += r0.z; dcb += r0.w;
+        dcc += r1.x; dop += r1.y; dcr += r1.z; dcg += r1.w;
+        dcbl += r2.x; ddep += r2.y;
+      }
   }
   a.dL_dmeans2D[3 * idx] = dmx;
   a.dL_dmeans2D[3 * idx + 1] = dmy;
@@ -268,10 +277,12 @@ __global__ __launch_bounds__(256) void k_gauss_bwd(GaussBackwardArgs a, GeomStat
   }
 }
 
-void launch_gauss_backward(const GaussBackwardArgs& a, const GeomState& g, const BinningState& b,
-                           const BackwardState& bw, hipStream_t stream) {
+void launch_gauss_backward(const GaussBackwardArgs& a, int W, int H, const GeomState& g,
+                           const ImageState& img, const BackwardState& bw, hipStream_t stream) {
+  (void)H;
   if (a.P <= 0) return;
-  hipLaunchKernelGGL(k_gauss_bwd, dim3((a.P + 255) / 256), dim3(256), 0, stream, a, g, b, bw);
+  hipLaunchKernelGGL(k_gauss_bwd, dim3((a.P + 255) / 256), dim3(256), 0, stream, a,
+                     div_up(W, GSR_TILE_X), g, (const uint4*)img.tile_info, bw);
 }
 
 }  // namespace gsr

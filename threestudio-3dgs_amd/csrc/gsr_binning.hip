@@ -32,7 +32,7 @@ __global__ __launch_bounds__(256) void k_duplicate(const uint32_t* __restrict__ 
                                                    const uint32_t* __restrict__ point_offsets,
                                                    const uint2* __restrict__ rect, int grid_x,
                                                    uint32_t* __restrict__ keys,
-                                                   uint32_t* __restrict__ inst_gauss,
+                                                   uint32_t* __restrict__ vals,
                                                    uint32_t* __restrict__ goff) {
   const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
   const uint32_t nv = min(*n_dev, (uint32_t)P);
@@ -45,7 +45,7 @@ __global__ __launch_bounds__(256) void k_duplicate(const uint32_t* __restrict__ 
   for (int y = ymin; y < ymax; ++y)
     for (int x = xmin; x < xmax; ++x) {
       keys[off] = (uint32_t)(y * grid_x + x);
-      inst_gauss[off] = gi;
+      vals[off] = gi;
       ++off;
     }
 }
@@ -56,32 +56,22 @@ void launch_duplicate(int P, int grid_x, const uint32_t* order, const GeomState&
   hipLaunchKernelGGL(k_duplicate, dim3((P + 255) / 256), dim3(256), 0, stream,
                      (const uint32_t*)(g.counters + 0), P, order,
                      (const uint32_t*)g.point_offsets, (const uint2*)g.rect, grid_x, b.key[0],
-                     b.inst_gauss, g.goff);
+                     b.val[0], g.goff);
 }
 
-// After the tile sort: resolve instance -> Gaussian, build the inverse permutation (for the
-// backward gather-sum) and the per-tile [start, end) ranges.
-__global__ __launch_bounds__(256) void k_finalize_bins(int K, const uint32_t* __restrict__ keys,
-                                                       const uint32_t* __restrict__ vals,
-                                                       const uint32_t* __restrict__ inst_gauss,
-                                                       uint32_t* __restrict__ sorted_gauss,
-                                                       uint32_t* __restrict__ inv,
-                                                       uint2* __restrict__ ranges) {
+// After the tile sort: per-tile [start, end) ranges of the sorted instance list.
+__global__ __launch_bounds__(256) void k_tile_ranges(int K, const uint32_t* __restrict__ keys,
+                                                     uint2* __restrict__ ranges) {
   const int p = blockIdx.x * blockDim.x + threadIdx.x;
   if (p >= K) return;
-  const uint32_t i = vals[p];
-  sorted_gauss[p] = inst_gauss[i];
-  inv[i] = (uint32_t)p;
   const uint32_t tile = keys[p];
   if (p == 0 || keys[p - 1] != tile) ranges[tile].x = (uint32_t)p;
   if (p == K - 1 || keys[p + 1] != tile) ranges[tile].y = (uint32_t)(p + 1);
 }
 
-void launch_finalize_bins(int K, const uint32_t* keys, const uint32_t* vals, const BinningState& b,
-                          uint2* ranges, hipStream_t stream) {
+void launch_tile_ranges(int K, const uint32_t* keys, uint2* ranges, hipStream_t stream) {
   if (K <= 0) return;
-  hipLaunchKernelGGL(k_finalize_bins, dim3((K + 255) / 256), dim3(256), 0, stream, K, keys, vals,
-                     (const uint32_t*)b.inst_gauss, b.sorted_gauss, b.inv, ranges);
+  hipLaunchKernelGGL(k_tile_ranges, dim3((K + 255) / 256), dim3(256), 0, stream, K, keys, ranges);
 }
 
 // markVisible / checkFrustum of the reference (API completeness).

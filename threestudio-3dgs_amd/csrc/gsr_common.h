@@ -94,10 +94,7 @@ struct GeomState {
 // Per-instance state for the K (Gaussian, tile) pairs ("binning").
 struct BinningState {
   uint32_t* key[2];        // tile id ping-pong
-  uint32_t* val[2];        // pre-sort instance position ping-pong
-  uint32_t* inst_gauss;    // pre-sort position -> Gaussian
-  uint32_t* sorted_gauss;  // sorted position -> Gaussian (what the blend kernels gather by)
-  uint32_t* inv;           // pre-sort position -> sorted position (backward gather-sum)
+  uint32_t* val[2];        // Gaussian index ping-pong; after the sort: sorted position -> Gaussian
   uint32_t* hist;
   uint32_t* hist_blk;
   static BinningState carve(void* base, int K, size_t* bytes) {
@@ -109,9 +106,6 @@ struct BinningState {
     b.key[1] = c.take<uint32_t>(n);
     b.val[0] = c.take<uint32_t>(n);
     b.val[1] = c.take<uint32_t>(n);
-    b.inst_gauss = c.take<uint32_t>(n);
-    b.sorted_gauss = c.take<uint32_t>(n);
-    b.inv = c.take<uint32_t>(n);
     b.hist = c.take<uint32_t>((size_t)GSR_RADIX * nb);
     b.hist_blk = c.take<uint32_t>(scan_blocks((long long)GSR_RADIX * nb) + 64);
     if (bytes) *bytes = align_up(c.off, 256);
@@ -122,6 +116,8 @@ struct BinningState {
 // Per-pixel / per-tile state ("image").
 struct ImageState {
   uint2* ranges;       // [tiles] sorted-instance range of each tile
+  uint4* tile_info;    // [tiles] (instances any pixel blended = max n_contrib, first unblended instance's
+                       //          depth key, its Gaussian index, 0) — written by the forward blend
   float* final_T;      // [H*W]
   uint32_t* n_contrib; // [H*W]
   static ImageState carve(void* base, int W, int H, size_t* bytes) {
@@ -130,6 +126,7 @@ struct ImageState {
     int tiles = div_up(W, GSR_TILE_X) * div_up(H, GSR_TILE_Y);
     size_t pix = (size_t)W * H;
     s.ranges = c.take<uint2>(tiles > 0 ? tiles : 1);
+    s.tile_info = c.take<uint4>(tiles > 0 ? tiles : 1);
     s.final_T = c.take<float>(pix > 0 ? pix : 1);
     s.n_contrib = c.take<uint32_t>(pix > 0 ? pix : 1);
     if (bytes) *bytes = align_up(c.off, 256);
@@ -137,12 +134,14 @@ struct ImageState {
   }
 };
 
-// Backward scratch: one 48-byte gradient row per sorted instance:
+// Backward scratch: one 48-byte gradient row per instance, stored at the instance's pre-sort slot
+// goff[g] + (row-major index of its tile inside the Gaussian's tile rect), so each Gaussian's rows
+// are contiguous for the per-Gaussian gather-sum:
 //   g0 = (dmean2D.x, dmean2D.y, dconic.a, dconic.b)   [pixel units; b in the reference's half convention]
 //   g1 = (dconic.c, dopacity, dcolor.r, dcolor.g)
 //   g2 = (dcolor.b, ddepth, 0, 0)
 struct BackwardState {
-  float4* grow;  // [3*K], row p = grow[3p .. 3p+2]
+  float4* grow;  // [3*K], row i = grow[3i .. 3i+2]
   static BackwardState carve(void* base, int K, size_t* bytes) {
     Carver c(base);
     BackwardState s;
@@ -176,6 +175,8 @@ __device__ __forceinline__ float3 xform_vec4x3_T(const float3 p, const float* m)
 __device__ __forceinline__ float ndc2pix(float v, int S) {
   return (float)((((double)v + 1.0) * (double)S - 1.0) * 0.5);
 }
+
+__device__ __forceinline__ float fast_rcp(float x) { return __builtin_amdgcn_rcpf(x); }
 
 // Screen-space Gaussian exponent for pixel offset (dx, dy) = mean - pixel.  Written with
 // explicit fmaf so the forward and backward kernels (and oracle/) evaluate it bit-identically:

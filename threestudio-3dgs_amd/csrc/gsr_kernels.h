@@ -38,16 +38,16 @@ void launch_preprocess(const PreprocessArgs& a, const GeomState& g, hipStream_t 
 void launch_compact_visible(int P, const GeomState& g, hipStream_t stream);
 void launch_duplicate(int P, int grid_x, const uint32_t* order, const GeomState& g,
                       const BinningState& b, hipStream_t stream);
-void launch_finalize_bins(int K, const uint32_t* keys, const uint32_t* vals, const BinningState& b,
-                          uint2* ranges, hipStream_t stream);
+void launch_tile_ranges(int K, const uint32_t* keys, uint2* ranges, hipStream_t stream);
 void launch_mark_visible(int P, const float* means3D, const float* view, const float* proj,
                          uint8_t* present, hipStream_t stream);
 
 // Tile blend — gsr_render.hip
-void launch_render_forward(int W, int H, const GeomState& g, const BinningState& b,
+// `sorted_gauss` = the tile sort's value buffer holding the result (sorted position -> Gaussian).
+void launch_render_forward(int W, int H, const GeomState& g, const uint32_t* sorted_gauss,
                            const ImageState& img, const float* bg, float* out_color,
                            float* out_depth, float* out_alpha, hipStream_t stream);
-void launch_render_backward(int W, int H, int K, const GeomState& g, const BinningState& b,
+void launch_render_backward(int W, int H, int K, const GeomState& g, const uint32_t* sorted_gauss,
                             const ImageState& img, const float* bg, const float* dL_dcolor,
                             const float* dL_ddepth, const float* dL_dalpha,
                             const BackwardState& bw, hipStream_t stream);
@@ -63,7 +63,7 @@ struct GaussBackwardArgs {
   float *dL_dmeans2D, *dL_dcolors, *dL_dopacity, *dL_dmeans3D, *dL_dcov3D, *dL_dsh, *dL_dscales,
       *dL_drotations;
 };
-void launch_gauss_backward(const GaussBackwardArgs& a, const GeomState& g, const BinningState& b,
-                           const BackwardState& bw, hipStream_t stream);
+void launch_gauss_backward(const GaussBackwardArgs& a, int W, int H, const GeomState& g,
+                           const ImageState& img, const BackwardState& bw, hipStream_t stream);
 
 }  // namespace gsr

@@ -1,16 +1,19 @@
 // gsr_render.hip — per-tile alpha blending, forward and backward.
 //
-// One 256-thread workgroup per 16x16 tile; the four waves each own an 8x8 pixel quadrant
-// (compact wave footprints: a Gaussian that misses a quadrant costs that wave nothing in the
-// backward pass, and whole waves finish early together in the forward pass).
+// One 256-thread workgroup per 16x16 tile; the four waves each own an 8x8 pixel quadrant.
 // Gaussian records (48 B: xy, conic, opacity, depth, rgb) are gathered by sorted instance into
-// LDS in chunks of 256 and read back as broadcast ds_read_b128.
+// LDS in chunks of 256 and read back as broadcast ds_read_b128.  While staging a chunk, each
+// thread also computes a conservative 4-bit quadrant mask for its Gaussian (bounding box of the
+// alpha >= 1/255 ellipse, padded): a wave skips, with one scalar test, every Gaussian that cannot
+// reach any of its 64 pixels.  The skipped pairs are exactly pairs the reference rejects with
+// alpha < 1/255, so results are unchanged.
 //
 // Forward replaces FORWARD::renderCUDA [EXT] (ashawkey 4-output: color, depth = sum z a T,
-// alpha = 1 - T).  Backward replaces BACKWARD::renderCUDA [EXT] but, instead of 9 global float
-// atomics per (pixel, Gaussian) pair, reduces each pair's 10 gradient terms over the wave with
-// DPP, sums the 4 waves in LDS, and writes ONE 48-byte row per sorted instance with coalesced
-// stores; gsr_backward.hip then sums each Gaussian's rows in a fixed order (deterministic).
+// alpha = 1 - T).  Backward replaces BACKWARD::renderCUDA [EXT]: instead of 9 global float atomics
+// per (pixel, Gaussian) pair it reduces each pair's 10 gradient terms over 16-lane rows with DPP,
+// parks the 16 row partials per Gaussian in LDS, and every 32 Gaussians sums them and writes ONE
+// 48-byte row per instance into the Gaussian's own slot (gsr_backward.hip sums a Gaussian's rows in
+// a fixed order -> deterministic, no atomics, no inverse permutation).
 #include "gsr_kernels.h"
 #include "gsr_wave.h"
 
@@ -31,6 +34,32 @@ __device__ __forceinline__ void tile_pixel(int t, int& lx, int& ly) {
   ly = ((w >> 1) << 3) | (l >> 3);
 }
 
+// Bit q set when some pixel centre of quadrant q (8x8, origin (x0 + 8 (q&1), y0 + 8 (q>>1))) can
+// satisfy o * exp(power) >= 1/255, i.e. d^T Q d <= 2 ln(255 o) with Q the conic.  The ellipse's
+// half extents are sqrt(2 tau Q^-1_xx), sqrt(2 tau Q^-1_yy); tau and the extents are padded far
+// beyond fp32 rounding of the exact per-pixel test, so the mask never drops a contributing pair.
+__device__ __forceinline__ uint32_t quadrant_mask(const float4 r0, const float4 r1, float x0, float y0) {
+  const float o = r1.y;
+  if (!(o >= GSR_ALPHA_MIN * 0.9999f)) return 0u;  // alpha <= o < 1/255 everywhere
+  const float a = r0.z, b = r0.w, c = r1.x;
+  const float det = a * c - b * b;
+  if (!(det > 0.0f)) return 0xFu;
+  const float tau = fmaxf(0.0f, __logf(255.0f * o));
+  const float r2 = 2.0f * (tau * 1.001f + 1e-3f);
+  const float inv_det = 1.0f / det;
+  const float hx = sqrtf(r2 * c * inv_det) * 1.001f + 0.02f;
+  const float hy = sqrtf(r2 * a * inv_det) * 1.001f + 0.02f;
+  uint32_t m = 0;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const float qx = x0 + (float)((q & 1) * 8), qy = y0 + (float)((q >> 1) * 8);
+    const bool hitx = (r0.x + hx >= qx) && (r0.x - hx <= qx + 7.0f);
+    const bool hity = (r0.y + hy >= qy) && (r0.y - hy <= qy + 7.0f);
+    m |= (hitx && hity) ? (1u << q) : 0u;
+  }
+  return m;
+}
+
 __global__ __launch_bounds__(256) void k_render_fwd(int W, int H, int grid_x, int n_tiles,
                                                     const uint2* __restrict__ ranges,
                                                     const uint32_t* __restrict__ sorted_gauss,
@@ -42,35 +71,42 @@ __global__ __launch_bounds__(256) void k_render_fwd(int W, int H, int grid_x, in
                                                     float* __restrict__ out_depth,
                                                     float* __restrict__ out_alpha,
                                                     float* __restrict__ final_T,
-                                                    uint32_t* __restrict__ n_contrib) {
+                                                    uint32_t* __restrict__ n_contrib,
+                                                    uint4* __restrict__ tile_info) {
   __shared__ float4 s0[256], s1[256], s2[256];
+  __shared__ uint32_t s_mask[256];
+  __shared__ uint32_t s_red[4];
   const int tile = xcd_tile(blockIdx.x, n_tiles);
-  const int t = threadIdx.x;
+  const int t = threadIdx.x, w = t >> 6, lane = t & 63;
   int lx, ly;
   tile_pixel(t, lx, ly);
-  const int px = (tile % grid_x) * GSR_TILE_X + lx;
-  const int py = (tile / grid_x) * GSR_TILE_Y + ly;
+  const int tx0 = (tile % grid_x) * GSR_TILE_X, ty0 = (tile / grid_x) * GSR_TILE_Y;
+  const int px = tx0 + lx, py = ty0 + ly;
   const bool inside = px < W && py < H;
   const float pxf = (float)px, pyf = (float)py;
   const uint2 range = ranges[tile];
+  const int n = (int)(range.y - range.x);
 
   bool done = !inside;
   float T = 1.0f, Cr = 0.f, Cg = 0.f, Cb = 0.f, D = 0.f;
-  uint32_t contributor = 0, last_contributor = 0;
-  int todo = (int)(range.y - range.x);
-  for (uint32_t start = range.x; start < range.y; start += 256, todo -= 256) {
+  uint32_t last_contributor = 0;
+  for (int base = 0; base < n; base += 256) {
     if (__syncthreads_count(done) == 256) break;
-    const uint32_t p = start + t;
-    if (p < range.y) {
-      const uint32_t gi = sorted_gauss[p];
-      s0[t] = rec0[gi];
-      s1[t] = rec1[gi];
+    const int cnt = min(256, n - base);
+    if (t < cnt) {
+      const uint32_t gi = sorted_gauss[range.x + base + t];
+      const float4 r0 = rec0[gi], r1 = rec1[gi];
+      s0[t] = r0;
+      s1[t] = r1;
       s2[t] = rec2[gi];
+      s_mask[t] = quadrant_mask(r0, r1, (float)tx0, (float)ty0);
     }
     __syncthreads();
-    const int cnt = todo < 256 ? todo : 256;
-    for (int j = 0; !done && j < cnt; ++j) {
-      ++contributor;
+    for (int j = 0; j < cnt; ++j) {
+      if (__all(done)) break;
+      const uint32_t m = __builtin_amdgcn_readfirstlane(s_mask[j]);
+      if (!((m >> w) & 1u)) continue;
+      if (done) continue;
       const float4 a = s0[j];
       const float4 b = s1[j];
       const float dx = a.x - pxf, dy = a.y - pyf;
@@ -89,7 +125,7 @@ __global__ __launch_bounds__(256) void k_render_fwd(int W, int H, int grid_x, in
       Cb += c.z * alpha * T;
       D += b.z * alpha * T;
       T = test_T;
-      last_contributor = contributor;
+      last_contributor = (uint32_t)(base + j + 1);
     }
   }
   if (inside) {
@@ -103,18 +139,35 @@ __global__ __launch_bounds__(256) void k_render_fwd(int W, int H, int grid_x, in
     out_depth[pid] = D;
     out_alpha[pid] = 1.0f - T;
   }
+  // per-tile blend extent for the backward pass: instances [0, maxc) were blended by some pixel;
+  // record the (depth key, Gaussian) of the first instance nobody blended.
+  uint32_t mc = last_contributor;
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) mc = max(mc, (uint32_t)__shfl_xor((int)mc, o, 64));
+  if (lane == 0) s_red[w] = mc;
+  __syncthreads();
+  if (t == 0) {
+    const uint32_t maxc = max(max(s_red[0], s_red[1]), max(s_red[2], s_red[3]));
+    uint4 info = make_uint4(maxc, 0xFFFFFFFFu, 0xFFFFFFFFu, 0u);
+    if ((int)maxc < n) {
+      const uint32_t gi = sorted_gauss[range.x + maxc];
+      info.y = __float_as_uint(rec1[gi].z);
+      info.z = gi;
+    }
+    tile_info[tile] = info;
+  }
 }
 
-void launch_render_forward(int W, int H, const GeomState& g, const BinningState& b,
+void launch_render_forward(int W, int H, const GeomState& g, const uint32_t* sorted_gauss,
                            const ImageState& img, const float* bg, float* out_color,
                            float* out_depth, float* out_alpha, hipStream_t stream) {
   const int gx = div_up(W, GSR_TILE_X), gy = div_up(H, GSR_TILE_Y);
   const int nt = gx * gy;
   if (nt <= 0) return;
   hipLaunchKernelGGL(k_render_fwd, dim3(nt), dim3(256), 0, stream, W, H, gx, nt,
-                     (const uint2*)img.ranges, (const uint32_t*)b.sorted_gauss,
-                     (const float4*)g.rec0, (const float4*)g.rec1, (const float4*)g.rec2, bg,
-                     out_color, out_depth, out_alpha, img.final_T, img.n_contrib);
+                     (const uint2*)img.ranges, sorted_gauss, (const float4*)g.rec0,
+                     (const float4*)g.rec1, (const float4*)g.rec2, bg, out_color, out_depth, out_alpha,
+                     img.final_T, img.n_contrib, img.tile_info);
 }
 
 // ---------------------------------------------------------------------------------------
@@ -122,13 +175,23 @@ void launch_render_forward(int W, int H, const GeomState& g, const BinningState&
 // colour/depth/alpha accumulators, background term.  Per pair the 10 gradient terms are
 //   0,1 dmean2D (x W/2, H/2)  2,3,4 dconic (a, b[half], c)  5 dopacity  6,7,8 dcolor  9 ddepth
 #define NGV 10
+#define BWD_SUB 32  // Gaussians per LDS partial flush
+
+template <int SHIFT>
+__device__ __forceinline__ void row_reduce_step(float (&v)[NGV]) {
+#pragma unroll
+  for (int k = 0; k < NGV; ++k) v[k] += dpp_f32<0x110 | SHIFT>(v[k]);
+}
 
 __global__ __launch_bounds__(256) void k_render_bwd(int W, int H, int grid_x, int n_tiles,
                                                     const uint2* __restrict__ ranges,
+                                                    const uint4* __restrict__ tile_info,
                                                     const uint32_t* __restrict__ sorted_gauss,
                                                     const float4* __restrict__ rec0,
                                                     const float4* __restrict__ rec1,
                                                     const float4* __restrict__ rec2,
+                                                    const uint2* __restrict__ rect,
+                                                    const uint32_t* __restrict__ goff,
                                                     const float* __restrict__ bg,
                                                     const float* __restrict__ final_Ts,
                                                     const uint32_t* __restrict__ n_contrib,
@@ -137,18 +200,19 @@ __global__ __launch_bounds__(256) void k_render_bwd(int W, int H, int grid_x, in
                                                     const float* __restrict__ dL_dalpha,
                                                     float4* __restrict__ grow) {
   __shared__ float4 s0[256], s1[256], s2[256];
-  __shared__ float s_part[4][NGV][256];
-  __shared__ uint32_t s_red[8];
+  __shared__ uint32_t s_mask[256], s_dest[256];
+  __shared__ float4 s_part[BWD_SUB][16][3];
   const int tile = xcd_tile(blockIdx.x, n_tiles);
   const int t = threadIdx.x, w = t >> 6, lane = t & 63;
   int lx, ly;
   tile_pixel(t, lx, ly);
-  const int px = (tile % grid_x) * GSR_TILE_X + lx;
-  const int py = (tile / grid_x) * GSR_TILE_Y + ly;
+  const int txi = tile % grid_x, tyi = tile / grid_x;
+  const int tx0 = txi * GSR_TILE_X, ty0 = tyi * GSR_TILE_Y;
+  const int px = tx0 + lx, py = ty0 + ly;
   const bool inside = px < W && py < H;
   const float pxf = (float)px, pyf = (float)py;
   const uint2 range = ranges[tile];
-  const int n = (int)(range.y - range.x);
+  const int maxc = (int)tile_info[tile].x;
   const size_t pid = (size_t)py * W + px;
   const size_t HW = (size_t)H * W;
 
@@ -165,118 +229,132 @@ __global__ __launch_bounds__(256) void k_render_bwd(int W, int H, int grid_x, in
     if (dL_dalpha) dpix_a = dL_dalpha[pid];
   }
   const float bg_dot = bg[0] * dpix[0] + bg[1] * dpix[1] + bg[2] * dpix[2];
-
-  // the deepest instance any pixel of the tile blended
-  uint32_t mc = last_contributor;
+  // the deepest instance any pixel of this wave blended (wave-uniform)
+  uint32_t wmax = last_contributor;
 #pragma unroll
-  for (int o = 32; o > 0; o >>= 1) mc = max(mc, (uint32_t)__shfl_xor((int)mc, o, 64));
-  if (lane == 0) s_red[w] = mc;
-  __syncthreads();
-  const int maxc = (int)max(max(s_red[0], s_red[1]), max(s_red[2], s_red[3]));
-
-  // instances nobody blended contribute nothing: zero their rows
-  for (int rel = maxc + t; rel < n; rel += 256) {
-    const size_t p = (size_t)range.x + rel;
-    grow[3 * p] = make_float4(0.f, 0.f, 0.f, 0.f);
-    grow[3 * p + 1] = make_float4(0.f, 0.f, 0.f, 0.f);
-    grow[3 * p + 2] = make_float4(0.f, 0.f, 0.f, 0.f);
-  }
+  for (int o = 32; o > 0; o >>= 1) wmax = max(wmax, (uint32_t)__shfl_xor((int)wmax, o, 64));
+  wmax = __builtin_amdgcn_readfirstlane(wmax);
 
   float acc_r = 0.f, acc_g = 0.f, acc_b = 0.f, acc_d = 0.f, acc_a = 0.f;
   float last_alpha = 0.f, last_r = 0.f, last_g = 0.f, last_b = 0.f, last_depth = 0.f;
   const float ddelx_dx = 0.5f * W, ddely_dy = 0.5f * H;
-  uint32_t contributor = (uint32_t)maxc;
+  const int prow = lane >> 4;
 
   for (int hi = maxc; hi > 0; hi -= 256) {
     const int cnt = hi < 256 ? hi : 256;
     if (t < cnt) {
       const uint32_t gi = sorted_gauss[range.x + hi - 1 - t];
-      s0[t] = rec0[gi];
-      s1[t] = rec1[gi];
+      const float4 r0 = rec0[gi], r1 = rec1[gi];
+      s0[t] = r0;
+      s1[t] = r1;
       s2[t] = rec2[gi];
+      s_mask[t] = quadrant_mask(r0, r1, (float)tx0, (float)ty0);
+      const uint2 rc = rect[gi];
+      const int xmin = rc.x & 0xffff, ymin = rc.x >> 16, xmax = rc.y & 0xffff;
+      s_dest[t] = goff[gi] + (uint32_t)((tyi - ymin) * (xmax - xmin) + (txi - xmin));
     }
     __syncthreads();
-    for (int j = 0; j < cnt; ++j) {
-      --contributor;
-      float v[NGV];
+    for (int sub = 0; sub < cnt; sub += BWD_SUB) {
+      const int scnt = min(BWD_SUB, cnt - sub);
+      for (int jj = 0; jj < scnt; ++jj) {
+        const int j = sub + jj;
+        const uint32_t rel = (uint32_t)(hi - 1 - j);
+        const uint32_t m = __builtin_amdgcn_readfirstlane(s_mask[j]);
+        float v[NGV];
 #pragma unroll
-      for (int k = 0; k < NGV; ++k) v[k] = 0.f;
-      bool hit = false;
-      if (contributor < last_contributor) {
-        const float4 a = s0[j];
-        const float4 b = s1[j];
-        const float dx = a.x - pxf, dy = a.y - pyf;
-        const float power = gauss_power(a.z, a.w, b.x, dx, dy);
-        if (power <= 0.0f) {
-          const float G = __expf(power);
-          const float alpha = fminf(GSR_ALPHA_MAX, b.y * G);
-          if (alpha >= GSR_ALPHA_MIN) {
-            hit = true;
-            const float4 c = s2[j];
-            T = T / (1.f - alpha);
-            const float dchannel_dcolor = alpha * T;
-            float dL_dalpha = 0.0f;
-            acc_r = last_alpha * last_r + (1.f - last_alpha) * acc_r;
-            acc_g = last_alpha * last_g + (1.f - last_alpha) * acc_g;
-            acc_b = last_alpha * last_b + (1.f - last_alpha) * acc_b;
-            last_r = c.x;
-            last_g = c.y;
-            last_b = c.z;
-            dL_dalpha += (c.x - acc_r) * dpix[0];
-            dL_dalpha += (c.y - acc_g) * dpix[1];
-            dL_dalpha += (c.z - acc_b) * dpix[2];
-            v[6] = dchannel_dcolor * dpix[0];
-            v[7] = dchannel_dcolor * dpix[1];
-            v[8] = dchannel_dcolor * dpix[2];
-            acc_d = last_alpha * last_depth + (1.f - last_alpha) * acc_d;
-            last_depth = b.z;
-            dL_dalpha += (b.z - acc_d) * dpix_d;
-            v[9] = dchannel_dcolor * dpix_d;
-            acc_a = last_alpha * 1.0f + (1.f - last_alpha) * acc_a;
-            dL_dalpha += (1.f - acc_a) * dpix_a;
-            dL_dalpha *= T;
-            last_alpha = alpha;
-            dL_dalpha += (-T_final / (1.f - alpha)) * bg_dot;
-            const float dL_dG = b.y * dL_dalpha;
-            const float gdx = G * dx, gdy = G * dy;
-            const float dG_ddelx = -gdx * a.z - gdy * a.w;
-            const float dG_ddely = -gdy * b.x - gdx * a.w;
-            v[0] = dL_dG * dG_ddelx * ddelx_dx;
-            v[1] = dL_dG * dG_ddely * ddely_dy;
-            v[2] = -0.5f * gdx * dx * dL_dG;
-            v[3] = -0.5f * gdx * dy * dL_dG;
-            v[4] = -0.5f * gdy * dy * dL_dG;
-            v[5] = G * dL_dalpha;
+        for (int k = 0; k < NGV; ++k) v[k] = 0.f;
+        bool hit = false;
+        if (((m >> w) & 1u) && rel < wmax) {
+          if (rel < last_contributor) {
+            const float4 a = s0[j];
+            const float4 b = s1[j];
+            const float dx = a.x - pxf, dy = a.y - pyf;
+            const float power = gauss_power(a.z, a.w, b.x, dx, dy);
+            if (power <= 0.0f) {
+              const float G = __expf(power);
+              const float alpha = fminf(GSR_ALPHA_MAX, b.y * G);
+              if (alpha >= GSR_ALPHA_MIN) {
+                hit = true;
+                const float4 c = s2[j];
+                const float inv_1ma = fast_rcp(1.f - alpha);
+                T = T * inv_1ma;
+                const float dchannel_dcolor = alpha * T;
+                float dL_dalpha = 0.0f;
+                acc_r = last_alpha * last_r + (1.f - last_alpha) * acc_r;
+                acc_g = last_alpha * last_g + (1.f - last_alpha) * acc_g;
+                acc_b = last_alpha * last_b + (1.f - last_alpha) * acc_b;
+                last_r = c.x;
+                last_g = c.y;
+                last_b = c.z;
+                dL_dalpha += (c.x - acc_r) * dpix[0];
+                dL_dalpha += (c.y - acc_g) * dpix[1];
+                dL_dalpha += (c.z - acc_b) * dpix[2];
+                v[6] = dchannel_dcolor * dpix[0];
+                v[7] = dchannel_dcolor * dpix[1];
+                v[8] = dchannel_dcolor * dpix[2];
+                acc_d = last_alpha * last_depth + (1.f - last_alpha) * acc_d;
+                last_depth = b.z;
+                dL_dalpha += (b.z - acc_d) * dpix_d;
+                v[9] = dchannel_dcolor * dpix_d;
+                acc_a = last_alpha * 1.0f + (1.f - last_alpha) * acc_a;
+                dL_dalpha += (1.f - acc_a) * dpix_a;
+                dL_dalpha *= T;
+                last_alpha = alpha;
+                dL_dalpha += (-T_final * inv_1ma) * bg_dot;
+                const float dL_dG = b.y * dL_dalpha;
+                const float gdx = G * dx, gdy = G * dy;
+                const float dG_ddelx = -gdx * a.z - gdy * a.w;
+                const float dG_ddely = -gdy * b.x - gdx * a.w;
+                v[0] = dL_dG * dG_ddelx * ddelx_dx;
+                v[1] = dL_dG * dG_ddely * ddely_dy;
+                v[2] = -0.5f * gdx * dx * dL_dG;
+                v[3] = -0.5f * gdx * dy * dL_dG;
+                v[4] = -0.5f * gdy * dy * dL_dG;
+                v[5] = G * dL_dalpha;
+              }
+            }
           }
         }
-      }
-      // wave-uniform: reduce only when some pixel of this quadrant used the Gaussian
-      if (__any(hit)) {
-#pragma unroll
-        for (int k = 0; k < NGV; ++k) {
-          const float s = wave_sum(v[k]);
-          if (lane == 0) s_part[w][k][j] = s;
+        float4* part = s_part[jj][w * 4 + prow];
+        if (__any(hit)) {
+          // 16-lane row sums (interleaved over the 10 terms: no DPP hazard stalls); lane 15 of
+          // each row holds its row's total
+          row_reduce_step<1>(v);
+          row_reduce_step<2>(v);
+          row_reduce_step<4>(v);
+          row_reduce_step<8>(v);
+          if ((lane & 15) == 15) {
+            part[0] = make_float4(v[0], v[1], v[2], v[3]);
+            part[1] = make_float4(v[4], v[5], v[6], v[7]);
+            part[2] = make_float4(v[8], v[9], 0.f, 0.f);
+          }
+        } else if ((lane & 15) == 15) {
+          const float4 z = make_float4(0.f, 0.f, 0.f, 0.f);
+          part[0] = z;
+          part[1] = z;
+          part[2] = z;
         }
-      } else if (lane == 0) {
-#pragma unroll
-        for (int k = 0; k < NGV; ++k) s_part[w][k][j] = 0.f;
       }
-    }
-    __syncthreads();
-    if (t < cnt) {
-      float r[NGV];
+      __syncthreads();
+      if (t < scnt * 3) {
+        const int jj = t / 3, grp = t - jj * 3;
+        float4 acc = s_part[jj][0][grp];
 #pragma unroll
-      for (int k = 0; k < NGV; ++k) r[k] = (s_part[0][k][t] + s_part[1][k][t]) + (s_part[2][k][t] + s_part[3][k][t]);
-      const size_t p = (size_t)range.x + hi - 1 - t;
-      grow[3 * p] = make_float4(r[0], r[1], r[2], r[3]);
-      grow[3 * p + 1] = make_float4(r[4], r[5], r[6], r[7]);
-      grow[3 * p + 2] = make_float4(r[8], r[9], 0.f, 0.f);
+        for (int q = 1; q < 16; ++q) {
+          const float4 x = s_part[jj][q][grp];
+          acc.x += x.x;
+          acc.y += x.y;
+          acc.z += x.z;
+          acc.w += x.w;
+        }
+        grow[3 * (size_t)s_dest[sub + jj] + grp] = acc;
+      }
+      __syncthreads();
     }
-    __syncthreads();
   }
 }
 
-void launch_render_backward(int W, int H, int K, const GeomState& g, const BinningState& b,
+void launch_render_backward(int W, int H, int K, const GeomState& g, const uint32_t* sorted_gauss,
                             const ImageState& img, const float* bg, const float* dL_dcolor,
                             const float* dL_ddepth, const float* dL_dalpha,
                             const BackwardState& bw, hipStream_t stream) {
@@ -284,10 +362,10 @@ void launch_render_backward(int W, int H, int K, const GeomState& g, const Binni
   const int nt = gx * gy;
   if (nt <= 0 || K <= 0) return;
   hipLaunchKernelGGL(k_render_bwd, dim3(nt), dim3(256), 0, stream, W, H, gx, nt,
-                     (const uint2*)img.ranges, (const uint32_t*)b.sorted_gauss,
-                     (const float4*)g.rec0, (const float4*)g.rec1, (const float4*)g.rec2, bg,
-                     (const float*)img.final_T, (const uint32_t*)img.n_contrib, dL_dcolor,
-                     dL_ddepth, dL_dalpha, bw.grow);
+                     (const uint2*)img.ranges, (const uint4*)img.tile_info, sorted_gauss,
+                     (const float4*)g.rec0, (const float4*)g.rec1, (const float4*)g.rec2,
+                     (const uint2*)g.rect, (const uint32_t*)g.goff, bg, (const float*)img.final_T,
+                     (const uint32_t*)img.n_contrib, dL_dcolor, dL_ddepth, dL_dalpha, bw.grow);
 }
 
 }  // namespace gsr
