@@ -365,7 +365,13 @@ static int setup(ctx_t* c, int P, int deg, int M, const float* means, const floa
   return 0;
 }
 
+/* pair statistics of the last forward (diagnostics): [0] pairs iterated, [1] pairs blended,
+ * [2] pixels inside the image */
+static long g_stats[4];
+void FN(oracle_last_stats)(long* out) { for (int i = 0; i < 4; ++i) out[i] = g_stats[i]; }
+
 static void forward_core(const ctx_t* c, int* radii, fwd_t* f, real* out_color, real* out_depth, real* out_alpha) {
+  g_stats[0] = g_stats[1] = g_stats[2] = g_stats[3] = 0;
   const int P = c->P, W = c->W, H = c->H, nt = c->gx * c->gy;
   f->gs = (gstate*)calloc((size_t)(P > 0 ? P : 1), sizeof(gstate));
   long K = 0;
@@ -406,8 +412,10 @@ static void forward_core(const ctx_t* c, int* radii, fwd_t* f, real* out_color, 
           if (px >= W || py >= H) continue;
           real T = 1, C[3] = {0, 0, 0}, D = 0;
           uint32_t contributor = 0, last = 0;
+          g_stats[2]++;
           for (uint32_t p = s; p < e; ++p) {
             ++contributor;
+            g_stats[0]++;
             const gstate* g = &f->gs[f->inst[p].g];
             const real dx = g->px - (real)px, dy = g->py - (real)py;
             const real power = gauss_power(g->ca, g->cb, g->cc, dx, dy);
@@ -420,6 +428,7 @@ static void forward_core(const ctx_t* c, int* radii, fwd_t* f, real* out_color, 
             D += g->depth * alpha * T;
             T = test_T;
             last = contributor;
+            g_stats[1]++;
           }
           const size_t pid = (size_t)py * W + px;
           f->final_T[pid] = T;

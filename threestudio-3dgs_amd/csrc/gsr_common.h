@@ -118,6 +118,7 @@ struct ImageState {
   uint2* ranges;       // [tiles] sorted-instance range of each tile
   uint4* tile_info;    // [tiles] (instances any pixel blended = max n_contrib, first unblended instance's
                        //          depth key, its Gaussian index, 0) — written by the forward blend
+  uint32_t* quad_maxc; // [4*tiles] per 8x8 quadrant: instances blended by some pixel
   float* final_T;      // [H*W]
   uint32_t* n_contrib; // [H*W]
   static ImageState carve(void* base, int W, int H, size_t* bytes) {
@@ -127,6 +128,7 @@ struct ImageState {
     size_t pix = (size_t)W * H;
     s.ranges = c.take<uint2>(tiles > 0 ? tiles : 1);
     s.tile_info = c.take<uint4>(tiles > 0 ? tiles : 1);
+    s.quad_maxc = c.take<uint32_t>(4 * (size_t)(tiles > 0 ? tiles : 1));
     s.final_T = c.take<float>(pix > 0 ? pix : 1);
     s.n_contrib = c.take<uint32_t>(pix > 0 ? pix : 1);
     if (bytes) *bytes = align_up(c.off, 256);

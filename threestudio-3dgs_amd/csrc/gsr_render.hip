@@ -60,28 +60,48 @@ __device__ __forceinline__ uint32_t quadrant_mask(const float4 r0, const float4 
   return m;
 }
 
-__global__ __launch_bounds__(256) void k_render_fwd(int W, int H, int grid_x, int n_tiles,
-                                                    const uint2* __restrict__ ranges,
-                                                    const uint32_t* __restrict__ sorted_gauss,
-                                                    const float4* __restrict__ rec0,
-                                                    const float4* __restrict__ rec1,
-                                                    const float4* __restrict__ rec2,
-                                                    const float* __restrict__ bg,
-                                                    float* __restrict__ out_color,
-                                                    float* __restrict__ out_depth,
-                                                    float* __restrict__ out_alpha,
-                                                    float* __restrict__ final_T,
-                                                    uint32_t* __restrict__ n_contrib,
-                                                    uint4* __restrict__ tile_info) {
-  __shared__ float4 s0[256], s1[256], s2[256];
-  __shared__ uint32_t s_mask[256];
-  __shared__ uint32_t s_red[4];
-  const int tile = xcd_tile(blockIdx.x, n_tiles);
-  const int t = threadIdx.x, w = t >> 6, lane = t & 63;
-  int lx, ly;
-  tile_pixel(t, lx, ly);
-  const int tx0 = (tile % grid_x) * GSR_TILE_X, ty0 = (tile / grid_x) * GSR_TILE_Y;
-  const int px = tx0 + lx, py = ty0 + ly;
+// Is some pixel centre of the 8x8 quadrant with origin (qx, qy) inside the padded alpha >= 1/255
+// ellipse of this Gaussian?  (single-quadrant form of quadrant_mask)
+__device__ __forceinline__ bool quadrant_hit(const float4 r0, const float4 r1, float qx, float qy) {
+  const float o = r1.y;
+  if (!(o >= GSR_ALPHA_MIN * 0.9999f)) return false;
+  const float a = r0.z, b = r0.w, c = r1.x;
+  const float det = a * c - b * b;
+  if (!(det > 0.0f)) return true;
+  const float tau = fmaxf(0.0f, __logf(255.0f * o));
+  const float r2 = 2.0f * (tau * 1.001f + 1e-3f);
+  const float inv_det = 1.0f / det;
+  const float hx = sqrtf(r2 * c * inv_det) * 1.001f + 0.02f;
+  const float hy = sqrtf(r2 * a * inv_det) * 1.001f + 0.02f;
+  return (r0.x + hx >= qx) && (r0.x - hx <= qx + 7.0f) && (r0.y + hy >= qy) && (r0.y - hy <= qy + 7.0f);
+}
+
+// Forward: one wave (64 threads) per 8x8 quadrant of a 16x16 tile.  The wave streams the tile's
+// depth-sorted instance list 64 at a time, keeps (ballot compaction, order preserved) only the
+// Gaussians whose alpha >= 1/255 ellipse can reach its quadrant, and blends them with a
+// branch-free predicated body.  No workgroup barriers couple quadrants that terminate at
+// different depths, and 4x more independent waves balance the load across the 256 CUs.
+__global__ __launch_bounds__(64) void k_render_fwd(int W, int H, int grid_x, int n_units,
+                                                   const uint2* __restrict__ ranges,
+                                                   const uint32_t* __restrict__ sorted_gauss,
+                                                   const float4* __restrict__ rec0,
+                                                   const float4* __restrict__ rec1,
+                                                   const float4* __restrict__ rec2,
+                                                   const float* __restrict__ bg,
+                                                   float* __restrict__ out_color,
+                                                   float* __restrict__ out_depth,
+                                                   float* __restrict__ out_alpha,
+                                                   float* __restrict__ final_T,
+                                                   uint32_t* __restrict__ n_contrib,
+                                                   uint32_t* __restrict__ quad_maxc) {
+  __shared__ float4 s0[64], s1[64], s2[64];
+  __shared__ uint32_t s_idx[64];
+  const int unit = xcd_tile(blockIdx.x, n_units);
+  const int tile = unit >> 2, q = unit & 3;
+  const int lane = threadIdx.x;
+  const int qx0 = (tile % grid_x) * GSR_TILE_X + (q & 1) * 8;
+  const int qy0 = (tile / grid_x) * GSR_TILE_Y + (q >> 1) * 8;
+  const int px = qx0 + (lane & 7), py = qy0 + (lane >> 3);
   const bool inside = px < W && py < H;
   const float pxf = (float)px, pyf = (float)py;
   const uint2 range = ranges[tile];
@@ -90,43 +110,49 @@ __global__ __launch_bounds__(256) void k_render_fwd(int W, int H, int grid_x, in
   bool done = !inside;
   float T = 1.0f, Cr = 0.f, Cg = 0.f, Cb = 0.f, D = 0.f;
   uint32_t last_contributor = 0;
-  for (int base = 0; base < n; base += 256) {
-    if (__syncthreads_count(done) == 256) break;
-    const int cnt = min(256, n - base);
-    if (t < cnt) {
-      const uint32_t gi = sorted_gauss[range.x + base + t];
-      const float4 r0 = rec0[gi], r1 = rec1[gi];
-      s0[t] = r0;
-      s1[t] = r1;
-      s2[t] = rec2[gi];
-      s_mask[t] = quadrant_mask(r0, r1, (float)tx0, (float)ty0);
+  for (int base = 0; base < n; base += 64) {
+    if (__all(done)) break;
+    const int i = base + lane;
+    bool keep = false;
+    float4 r0, r1, r2;
+    if (i < n) {
+      const uint32_t gi = sorted_gauss[range.x + i];
+      r0 = rec0[gi];
+      r1 = rec1[gi];
+      r2 = rec2[gi];
+      keep = quadrant_hit(r0, r1, (float)qx0, (float)qy0);
+    }
+    const unsigned long long bal = __ballot(keep);
+    const int cnt = __popcll(bal);
+    if (keep) {
+      const uint32_t pos = mask_rank(bal);
+      s0[pos] = r0;
+      s1[pos] = r1;
+      s2[pos] = r2;
+      s_idx[pos] = (uint32_t)(i + 1);
     }
     __syncthreads();
-    for (int j = 0; j < cnt; ++j) {
-      if (__all(done)) break;
-      const uint32_t m = __builtin_amdgcn_readfirstlane(s_mask[j]);
-      if (!((m >> w) & 1u)) continue;
-      if (done) continue;
-      const float4 a = s0[j];
-      const float4 b = s1[j];
+    for (int k = 0; k < cnt; ++k) {
+      if ((k & 7) == 0 && __all(done)) break;
+      const float4 a = s0[k];
+      const float4 b = s1[k];
+      const float4 c = s2[k];
       const float dx = a.x - pxf, dy = a.y - pyf;
       const float power = gauss_power(a.z, a.w, b.x, dx, dy);
-      if (power > 0.0f) continue;
       const float alpha = fminf(GSR_ALPHA_MAX, b.y * __expf(power));
-      if (alpha < GSR_ALPHA_MIN) continue;
+      const bool ok = !done && power <= 0.0f && alpha >= GSR_ALPHA_MIN;
       const float test_T = T * (1.0f - alpha);
-      if (test_T < GSR_T_EPS) {
-        done = true;
-        continue;
-      }
-      const float4 c = s2[j];
-      Cr += c.x * alpha * T;
-      Cg += c.y * alpha * T;
-      Cb += c.z * alpha * T;
-      D += b.z * alpha * T;
-      T = test_T;
-      last_contributor = (uint32_t)(base + j + 1);
+      const bool term = ok && test_T < GSR_T_EPS;
+      const bool blend = ok && !term;
+      Cr = blend ? Cr + c.x * alpha * T : Cr;
+      Cg = blend ? Cg + c.y * alpha * T : Cg;
+      Cb = blend ? Cb + c.z * alpha * T : Cb;
+      D = blend ? D + b.z * alpha * T : D;
+      T = blend ? test_T : T;
+      last_contributor = blend ? s_idx[k] : last_contributor;
+      done = done || term;
     }
+    __syncthreads();
   }
   if (inside) {
     const size_t pid = (size_t)py * W + px;
@@ -139,23 +165,31 @@ __global__ __launch_bounds__(256) void k_render_fwd(int W, int H, int grid_x, in
     out_depth[pid] = D;
     out_alpha[pid] = 1.0f - T;
   }
-  // per-tile blend extent for the backward pass: instances [0, maxc) were blended by some pixel;
-  // record the (depth key, Gaussian) of the first instance nobody blended.
   uint32_t mc = last_contributor;
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) mc = max(mc, (uint32_t)__shfl_xor((int)mc, o, 64));
-  if (lane == 0) s_red[w] = mc;
-  __syncthreads();
-  if (t == 0) {
-    const uint32_t maxc = max(max(s_red[0], s_red[1]), max(s_red[2], s_red[3]));
-    uint4 info = make_uint4(maxc, 0xFFFFFFFFu, 0xFFFFFFFFu, 0u);
-    if ((int)maxc < n) {
-      const uint32_t gi = sorted_gauss[range.x + maxc];
-      info.y = __float_as_uint(rec1[gi].z);
-      info.z = gi;
-    }
-    tile_info[tile] = info;
+  if (lane == 0) quad_maxc[unit] = mc;
+}
+
+// Per tile: instances [0, maxc) were blended by some pixel (max over the 4 quadrants); record the
+// (depth key, Gaussian) of the first instance nobody blended for the per-Gaussian backward.
+__global__ __launch_bounds__(256) void k_tile_info(int n_tiles, const uint2* __restrict__ ranges,
+                                                   const uint32_t* __restrict__ quad_maxc,
+                                                   const uint32_t* __restrict__ sorted_gauss,
+                                                   const float4* __restrict__ rec1,
+                                                   uint4* __restrict__ tile_info) {
+  const int tile = blockIdx.x * blockDim.x + threadIdx.x;
+  if (tile >= n_tiles) return;
+  const uint4 m = reinterpret_cast<const uint4*>(quad_maxc)[tile];
+  const uint32_t maxc = max(max(m.x, m.y), max(m.z, m.w));
+  const uint2 range = ranges[tile];
+  uint4 info = make_uint4(maxc, 0xFFFFFFFFu, 0xFFFFFFFFu, 0u);
+  if (maxc < range.y - range.x) {
+    const uint32_t gi = sorted_gauss[range.x + maxc];
+    info.y = __float_as_uint(rec1[gi].z);
+    info.z = gi;
   }
+  tile_info[tile] = info;
 }
 
 void launch_render_forward(int W, int H, const GeomState& g, const uint32_t* sorted_gauss,
@@ -164,10 +198,13 @@ void launch_render_forward(int W, int H, const GeomState& g, const uint32_t* sor
   const int gx = div_up(W, GSR_TILE_X), gy = div_up(H, GSR_TILE_Y);
   const int nt = gx * gy;
   if (nt <= 0) return;
-  hipLaunchKernelGGL(k_render_fwd, dim3(nt), dim3(256), 0, stream, W, H, gx, nt,
+  hipLaunchKernelGGL(k_render_fwd, dim3(4 * nt), dim3(64), 0, stream, W, H, gx, 4 * nt,
                      (const uint2*)img.ranges, sorted_gauss, (const float4*)g.rec0,
                      (const float4*)g.rec1, (const float4*)g.rec2, bg, out_color, out_depth, out_alpha,
-                     img.final_T, img.n_contrib, img.tile_info);
+                     img.final_T, img.n_contrib, img.quad_maxc);
+  hipLaunchKernelGGL(k_tile_info, dim3(div_up(nt, 256)), dim3(256), 0, stream, nt,
+                     (const uint2*)img.ranges, (const uint32_t*)img.quad_maxc, sorted_gauss,
+                     (const float4*)g.rec1, img.tile_info);
 }
 
 // ---------------------------------------------------------------------------------------
