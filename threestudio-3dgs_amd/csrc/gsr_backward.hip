@@ -17,7 +17,7 @@
 namespace gsr {
 
 __global__ __launch_bounds__(256) void k_gauss_bwd(GaussBackwardArgs a, int grid_x, GeomState g,
-                                                   const uint4* __restrict__ tile_info, BackwardState bw) {
+                                                   const uint2* __restrict__ quad_cut, BackwardState bw) {
   const int idx = blockIdx.x * blockDim.x + threadIdx.x;
   if (idx >= a.P) return;
   const int Mc = a.M;
@@ -26,8 +26,9 @@ __global__ __launch_bounds__(256) void k_gauss_bwd(GaussBackwardArgs a, int grid
   float dmx = 0.f, dmy = 0.f, dca = 0.f, dcb = 0.f, dcc = 0.f, dop = 0.f;
   float dcr = 0.f, dcg = 0.f, dcbl = 0.f, ddep = 0.f;
   if (visible) {
-    // rows of this Gaussian's instances are contiguous (tile rect, row-major); an instance's row is
-    // valid only if its tile's blend reached it: (depth key, index) < the tile's first unblended one
+    // rows of this Gaussian's instances are contiguous (tile rect, row-major, 4 quadrant rows each);
+    // a quadrant row is valid only if that quadrant's blend reached the instance:
+    // (depth key, index) < the quadrant's first unblended instance
     const size_t i0 = g.goff[idx];
     const uint2 rc = g.rect[idx];
     const int xmin = rc.x & 0xffff, ymin = rc.x >> 16, xmax = rc.y & 0xffff, ymax = rc.y >> 16;
@@ -35,13 +36,18 @@ __global__ __launch_bounds__(256) void k_gauss_bwd(GaussBackwardArgs a, int grid
     size_t i = i0;
     for (int ty = ymin; ty < ymax; ++ty)
       for (int tx = xmin; tx < xmax; ++tx, ++i) {
-        const uint4 info = tile_info[ty * grid_x + tx];
-        const bool valid = dkey < info.y || (dkey == info.y && (uint32_t)idx < info.z);
-        if (!valid) continue;
-        const float4 r0 = bw.grow[3 * i], r1 = bw.grow[3 * i + 1], r2 = bw.grow[3 * i + 2];
-        dmx += r0.x; dmy += r0.y; dca += r0.z; dcb += r0.w;
-        dcc += r1.x; dop += r1.y; dcr += r1.z; dcg += r1.w;
-        dcbl += r2.x; ddep += r2.y;
+        const uint2* cut = quad_cut + 4 * (size_t)(ty * grid_x + tx);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const uint2 c = cut[q];
+          const bool valid = dkey < c.x || (dkey == c.x && (uint32_t)idx < c.y);
+          if (!valid) continue;
+          const size_t r = 4 * i + q;
+          const float4 r0 = bw.grow[3 * r], r1 = bw.grow[3 * r + 1], r2 = bw.grow[3 * r + 2];
+          dmx += r0.x; dmy += r0.y; dca += r0.z; dcb += r0.w;
+          dcc += r1.x; dop += r1.y; dcr += r1.z; dcg += r1.w;
+          dcbl += r2.x; ddep += r2.y;
+        }
       }
   }
   a.dL_dmeans2D[3 * idx] = dmx;
@@ -282,7 +288,7 @@ void launch_gauss_backward(const GaussBackwardArgs& a, int W, int H, const GeomS
   (void)H;
   if (a.P <= 0) return;
   hipLaunchKernelGGL(k_gauss_bwd, dim3((a.P + 255) / 256), dim3(256), 0, stream, a,
-                     div_up(W, GSR_TILE_X), g, (const uint4*)img.tile_info, bw);
+                     div_up(W, GSR_TILE_X), g, (const uint2*)img.quad_cut, bw);
 }
 
 }  // namespace gsr

@@ -116,9 +116,8 @@ struct BinningState {
 // Per-pixel / per-tile state ("image").
 struct ImageState {
   uint2* ranges;       // [tiles] sorted-instance range of each tile
-  uint4* tile_info;    // [tiles] (instances any pixel blended = max n_contrib, first unblended instance's
-                       //          depth key, its Gaussian index, 0) — written by the forward blend
-  uint32_t* quad_maxc; // [4*tiles] per 8x8 quadrant: instances blended by some pixel
+  uint32_t* quad_maxc; // [4*tiles] per 8x8 quadrant: instances [0, maxc) of the tile list were blended
+  uint2* quad_cut;     // [4*tiles] (depth key, Gaussian) of the quadrant's first unblended instance
   float* final_T;      // [H*W]
   uint32_t* n_contrib; // [H*W]
   static ImageState carve(void* base, int W, int H, size_t* bytes) {
@@ -127,8 +126,8 @@ struct ImageState {
     int tiles = div_up(W, GSR_TILE_X) * div_up(H, GSR_TILE_Y);
     size_t pix = (size_t)W * H;
     s.ranges = c.take<uint2>(tiles > 0 ? tiles : 1);
-    s.tile_info = c.take<uint4>(tiles > 0 ? tiles : 1);
     s.quad_maxc = c.take<uint32_t>(4 * (size_t)(tiles > 0 ? tiles : 1));
+    s.quad_cut = c.take<uint2>(4 * (size_t)(tiles > 0 ? tiles : 1));
     s.final_T = c.take<float>(pix > 0 ? pix : 1);
     s.n_contrib = c.take<uint32_t>(pix > 0 ? pix : 1);
     if (bytes) *bytes = align_up(c.off, 256);
@@ -136,18 +135,18 @@ struct ImageState {
   }
 };
 
-// Backward scratch: one 48-byte gradient row per instance, stored at the instance's pre-sort slot
-// goff[g] + (row-major index of its tile inside the Gaussian's tile rect), so each Gaussian's rows
-// are contiguous for the per-Gaussian gather-sum:
+// Backward scratch: one 48-byte gradient row per (instance, 8x8 quadrant), stored at
+// 4 * slot + quadrant, slot = goff[g] + (row-major index of the tile inside the Gaussian's tile
+// rect), so each Gaussian's rows are contiguous for the per-Gaussian gather-sum:
 //   g0 = (dmean2D.x, dmean2D.y, dconic.a, dconic.b)   [pixel units; b in the reference's half convention]
 //   g1 = (dconic.c, dopacity, dcolor.r, dcolor.g)
 //   g2 = (dcolor.b, ddepth, 0, 0)
 struct BackwardState {
-  float4* grow;  // [3*K], row i = grow[3i .. 3i+2]
+  float4* grow;  // [12*K], row r = grow[3r .. 3r+2], r = 4 * slot + quadrant
   static BackwardState carve(void* base, int K, size_t* bytes) {
     Carver c(base);
     BackwardState s;
-    s.grow = c.take<float4>((size_t)3 * (K > 0 ? K : 1));
+    s.grow = c.take<float4>((size_t)12 * (K > 0 ? K : 1));
     if (bytes) *bytes = align_up(c.off, 256);
     return s;
   }

@@ -34,32 +34,6 @@ __device__ __forceinline__ void tile_pixel(int t, int& lx, int& ly) {
   ly = ((w >> 1) << 3) | (l >> 3);
 }
 
-// Bit q set when some pixel centre of quadrant q (8x8, origin (x0 + 8 (q&1), y0 + 8 (q>>1))) can
-// satisfy o * exp(power) >= 1/255, i.e. d^T Q d <= 2 ln(255 o) with Q the conic.  The ellipse's
-// half extents are sqrt(2 tau Q^-1_xx), sqrt(2 tau Q^-1_yy); tau and the extents are padded far
-// beyond fp32 rounding of the exact per-pixel test, so the mask never drops a contributing pair.
-__device__ __forceinline__ uint32_t quadrant_mask(const float4 r0, const float4 r1, float x0, float y0) {
-  const float o = r1.y;
-  if (!(o >= GSR_ALPHA_MIN * 0.9999f)) return 0u;  // alpha <= o < 1/255 everywhere
-  const float a = r0.z, b = r0.w, c = r1.x;
-  const float det = a * c - b * b;
-  if (!(det > 0.0f)) return 0xFu;
-  const float tau = fmaxf(0.0f, __logf(255.0f * o));
-  const float r2 = 2.0f * (tau * 1.001f + 1e-3f);
-  const float inv_det = 1.0f / det;
-  const float hx = sqrtf(r2 * c * inv_det) * 1.001f + 0.02f;
-  const float hy = sqrtf(r2 * a * inv_det) * 1.001f + 0.02f;
-  uint32_t m = 0;
-#pragma unroll
-  for (int q = 0; q < 4; ++q) {
-    const float qx = x0 + (float)((q & 1) * 8), qy = y0 + (float)((q >> 1) * 8);
-    const bool hitx = (r0.x + hx >= qx) && (r0.x - hx <= qx + 7.0f);
-    const bool hity = (r0.y + hy >= qy) && (r0.y - hy <= qy + 7.0f);
-    m |= (hitx && hity) ? (1u << q) : 0u;
-  }
-  return m;
-}
-
 // Is some pixel centre of the 8x8 quadrant with origin (qx, qy) inside the padded alpha >= 1/255
 // ellipse of this Gaussian?  (single-quadrant form of quadrant_mask)
 __device__ __forceinline__ bool quadrant_hit(const float4 r0, const float4 r1, float qx, float qy) {
@@ -171,25 +145,24 @@ __global__ __launch_bounds__(64) void k_render_fwd(int W, int H, int grid_x, int
   if (lane == 0) quad_maxc[unit] = mc;
 }
 
-// Per tile: instances [0, maxc) were blended by some pixel (max over the 4 quadrants); record the
-// (depth key, Gaussian) of the first instance nobody blended for the per-Gaussian backward.
-__global__ __launch_bounds__(256) void k_tile_info(int n_tiles, const uint2* __restrict__ ranges,
+// Per quadrant: instances [0, maxc) of the tile list were blended by some pixel of the quadrant;
+// record the (depth key, Gaussian) of the first instance nobody in the quadrant blended, for the
+// per-Gaussian backward's validity test of the quadrant's gradient rows.
+__global__ __launch_bounds__(256) void k_quad_info(int n_units, const uint2* __restrict__ ranges,
                                                    const uint32_t* __restrict__ quad_maxc,
                                                    const uint32_t* __restrict__ sorted_gauss,
                                                    const float4* __restrict__ rec1,
-                                                   uint4* __restrict__ tile_info) {
-  const int tile = blockIdx.x * blockDim.x + threadIdx.x;
-  if (tile >= n_tiles) return;
-  const uint4 m = reinterpret_cast<const uint4*>(quad_maxc)[tile];
-  const uint32_t maxc = max(max(m.x, m.y), max(m.z, m.w));
-  const uint2 range = ranges[tile];
-  uint4 info = make_uint4(maxc, 0xFFFFFFFFu, 0xFFFFFFFFu, 0u);
+                                                   uint2* __restrict__ quad_cut) {
+  const int u = blockIdx.x * blockDim.x + threadIdx.x;
+  if (u >= n_units) return;
+  const uint32_t maxc = quad_maxc[u];
+  const uint2 range = ranges[u >> 2];
+  uint2 cut = make_uint2(0xFFFFFFFFu, 0xFFFFFFFFu);
   if (maxc < range.y - range.x) {
     const uint32_t gi = sorted_gauss[range.x + maxc];
-    info.y = __float_as_uint(rec1[gi].z);
-    info.z = gi;
+    cut = make_uint2(__float_as_uint(rec1[gi].z), gi);
   }
-  tile_info[tile] = info;
+  quad_cut[u] = cut;
 }
 
 void launch_render_forward(int W, int H, const GeomState& g, const uint32_t* sorted_gauss,
@@ -202,9 +175,9 @@ void launch_render_forward(int W, int H, const GeomState& g, const uint32_t* sor
                      (const uint2*)img.ranges, sorted_gauss, (const float4*)g.rec0,
                      (const float4*)g.rec1, (const float4*)g.rec2, bg, out_color, out_depth, out_alpha,
                      img.final_T, img.n_contrib, img.quad_maxc);
-  hipLaunchKernelGGL(k_tile_info, dim3(div_up(nt, 256)), dim3(256), 0, stream, nt,
+  hipLaunchKernelGGL(k_quad_info, dim3(div_up(4 * nt, 256)), dim3(256), 0, stream, 4 * nt,
                      (const uint2*)img.ranges, (const uint32_t*)img.quad_maxc, sorted_gauss,
-                     (const float4*)g.rec1, img.tile_info);
+                     (const float4*)g.rec1, img.quad_cut);
 }
 
 // ---------------------------------------------------------------------------------------
@@ -220,36 +193,42 @@ __device__ __forceinline__ void row_reduce_step(float (&v)[NGV]) {
   for (int k = 0; k < NGV; ++k) v[k] += dpp_f32<0x110 | SHIFT>(v[k]);
 }
 
-__global__ __launch_bounds__(256) void k_render_bwd(int W, int H, int grid_x, int n_tiles,
-                                                    const uint2* __restrict__ ranges,
-                                                    const uint4* __restrict__ tile_info,
-                                                    const uint32_t* __restrict__ sorted_gauss,
-                                                    const float4* __restrict__ rec0,
-                                                    const float4* __restrict__ rec1,
-                                                    const float4* __restrict__ rec2,
-                                                    const uint2* __restrict__ rect,
-                                                    const uint32_t* __restrict__ goff,
-                                                    const float* __restrict__ bg,
-                                                    const float* __restrict__ final_Ts,
-                                                    const uint32_t* __restrict__ n_contrib,
-                                                    const float* __restrict__ dL_dcolor,
-                                                    const float* __restrict__ dL_ddepth,
-                                                    const float* __restrict__ dL_dalpha,
-                                                    float4* __restrict__ grow) {
-  __shared__ float4 s0[256], s1[256], s2[256];
-  __shared__ uint32_t s_mask[256], s_dest[256];
-  __shared__ float4 s_part[BWD_SUB][16][3];
-  const int tile = xcd_tile(blockIdx.x, n_tiles);
-  const int t = threadIdx.x, w = t >> 6, lane = t & 63;
-  int lx, ly;
-  tile_pixel(t, lx, ly);
+// One wave per 8x8 quadrant (as the forward).  The wave walks its tile's list back to front from
+// the quadrant's deepest blended instance, 64 at a time, keeps (ballot compaction, order kept) the
+// Gaussians whose alpha >= 1/255 ellipse reaches the quadrant, replays them per pixel, reduces each
+// Gaussian's 10 terms over 16-lane rows with DPP, parks the 4 row partials in LDS and every 32
+// Gaussians writes one 48-byte row per (instance, quadrant) at 4 * slot + quadrant, where slot is
+// the instance's place in its Gaussian's contiguous row range.  Culled instances get zero rows.
+__global__ __launch_bounds__(64) void k_render_bwd(int W, int H, int grid_x, int n_units,
+                                                   const uint2* __restrict__ ranges,
+                                                   const uint32_t* __restrict__ quad_maxc,
+                                                   const uint32_t* __restrict__ sorted_gauss,
+                                                   const float4* __restrict__ rec0,
+                                                   const float4* __restrict__ rec1,
+                                                   const float4* __restrict__ rec2,
+                                                   const uint2* __restrict__ rect,
+                                                   const uint32_t* __restrict__ goff,
+                                                   const float* __restrict__ bg,
+                                                   const float* __restrict__ final_Ts,
+                                                   const uint32_t* __restrict__ n_contrib,
+                                                   const float* __restrict__ dL_dcolor,
+                                                   const float* __restrict__ dL_ddepth,
+                                                   const float* __restrict__ dL_dalpha,
+                                                   float4* __restrict__ grow) {
+  __shared__ float4 s0[64], s1[64], s2[64];
+  __shared__ uint32_t s_dest[64], s_rel[64];
+  __shared__ float4 s_part[BWD_SUB][4][3];
+  const int unit = xcd_tile(blockIdx.x, n_units);
+  const int tile = unit >> 2, q = unit & 3;
+  const int lane = threadIdx.x;
   const int txi = tile % grid_x, tyi = tile / grid_x;
-  const int tx0 = txi * GSR_TILE_X, ty0 = tyi * GSR_TILE_Y;
-  const int px = tx0 + lx, py = ty0 + ly;
+  const int qx0 = txi * GSR_TILE_X + (q & 1) * 8;
+  const int qy0 = tyi * GSR_TILE_Y + (q >> 1) * 8;
+  const int px = qx0 + (lane & 7), py = qy0 + (lane >> 3);
   const bool inside = px < W && py < H;
   const float pxf = (float)px, pyf = (float)py;
   const uint2 range = ranges[tile];
-  const int maxc = (int)tile_info[tile].x;
+  const int maxc = (int)quad_maxc[unit];
   const size_t pid = (size_t)py * W + px;
   const size_t HW = (size_t)H * W;
 
@@ -266,96 +245,104 @@ __global__ __launch_bounds__(256) void k_render_bwd(int W, int H, int grid_x, in
     if (dL_dalpha) dpix_a = dL_dalpha[pid];
   }
   const float bg_dot = bg[0] * dpix[0] + bg[1] * dpix[1] + bg[2] * dpix[2];
-  // the deepest instance any pixel of this wave blended (wave-uniform)
-  uint32_t wmax = last_contributor;
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) wmax = max(wmax, (uint32_t)__shfl_xor((int)wmax, o, 64));
-  wmax = __builtin_amdgcn_readfirstlane(wmax);
 
   float acc_r = 0.f, acc_g = 0.f, acc_b = 0.f, acc_d = 0.f, acc_a = 0.f;
   float last_alpha = 0.f, last_r = 0.f, last_g = 0.f, last_b = 0.f, last_depth = 0.f;
   const float ddelx_dx = 0.5f * W, ddely_dy = 0.5f * H;
   const int prow = lane >> 4;
+  const float4 zero4 = make_float4(0.f, 0.f, 0.f, 0.f);
 
-  for (int hi = maxc; hi > 0; hi -= 256) {
-    const int cnt = hi < 256 ? hi : 256;
-    if (t < cnt) {
-      const uint32_t gi = sorted_gauss[range.x + hi - 1 - t];
-      const float4 r0 = rec0[gi], r1 = rec1[gi];
-      s0[t] = r0;
-      s1[t] = r1;
-      s2[t] = rec2[gi];
-      s_mask[t] = quadrant_mask(r0, r1, (float)tx0, (float)ty0);
+  for (int hi = maxc; hi > 0; hi -= 64) {
+    const int rel_l = hi - 1 - lane;
+    bool keep = false;
+    float4 r0, r1, r2;
+    uint32_t dest = 0;
+    if (rel_l >= 0) {
+      const uint32_t gi = sorted_gauss[range.x + rel_l];
+      r0 = rec0[gi];
+      r1 = rec1[gi];
+      r2 = rec2[gi];
       const uint2 rc = rect[gi];
       const int xmin = rc.x & 0xffff, ymin = rc.x >> 16, xmax = rc.y & 0xffff;
-      s_dest[t] = goff[gi] + (uint32_t)((tyi - ymin) * (xmax - xmin) + (txi - xmin));
+      dest = 4u * (goff[gi] + (uint32_t)((tyi - ymin) * (xmax - xmin) + (txi - xmin))) + (uint32_t)q;
+      keep = quadrant_hit(r0, r1, (float)qx0, (float)qy0);
+      if (!keep) {
+        grow[3 * (size_t)dest] = zero4;
+        grow[3 * (size_t)dest + 1] = zero4;
+        grow[3 * (size_t)dest + 2] = zero4;
+      }
+    }
+    const unsigned long long bal = __ballot(keep);
+    const int cnt = __popcll(bal);
+    if (keep) {
+      const uint32_t pos = mask_rank(bal);
+      s0[pos] = r0;
+      s1[pos] = r1;
+      s2[pos] = r2;
+      s_dest[pos] = dest;
+      s_rel[pos] = (uint32_t)rel_l;
     }
     __syncthreads();
     for (int sub = 0; sub < cnt; sub += BWD_SUB) {
       const int scnt = min(BWD_SUB, cnt - sub);
-      for (int jj = 0; jj < scnt; ++jj) {
-        const int j = sub + jj;
-        const uint32_t rel = (uint32_t)(hi - 1 - j);
-        const uint32_t m = __builtin_amdgcn_readfirstlane(s_mask[j]);
+      for (int kk = 0; kk < scnt; ++kk) {
+        const int k = sub + kk;
+        const uint32_t rel = __builtin_amdgcn_readfirstlane(s_rel[k]);
         float v[NGV];
 #pragma unroll
-        for (int k = 0; k < NGV; ++k) v[k] = 0.f;
+        for (int e = 0; e < NGV; ++e) v[e] = 0.f;
         bool hit = false;
-        if (((m >> w) & 1u) && rel < wmax) {
-          if (rel < last_contributor) {
-            const float4 a = s0[j];
-            const float4 b = s1[j];
-            const float dx = a.x - pxf, dy = a.y - pyf;
-            const float power = gauss_power(a.z, a.w, b.x, dx, dy);
-            if (power <= 0.0f) {
-              const float G = __expf(power);
-              const float alpha = fminf(GSR_ALPHA_MAX, b.y * G);
-              if (alpha >= GSR_ALPHA_MIN) {
-                hit = true;
-                const float4 c = s2[j];
-                const float inv_1ma = fast_rcp(1.f - alpha);
-                T = T * inv_1ma;
-                const float dchannel_dcolor = alpha * T;
-                float dL_dalpha = 0.0f;
-                acc_r = last_alpha * last_r + (1.f - last_alpha) * acc_r;
-                acc_g = last_alpha * last_g + (1.f - last_alpha) * acc_g;
-                acc_b = last_alpha * last_b + (1.f - last_alpha) * acc_b;
-                last_r = c.x;
-                last_g = c.y;
-                last_b = c.z;
-                dL_dalpha += (c.x - acc_r) * dpix[0];
-                dL_dalpha += (c.y - acc_g) * dpix[1];
-                dL_dalpha += (c.z - acc_b) * dpix[2];
-                v[6] = dchannel_dcolor * dpix[0];
-                v[7] = dchannel_dcolor * dpix[1];
-                v[8] = dchannel_dcolor * dpix[2];
-                acc_d = last_alpha * last_depth + (1.f - last_alpha) * acc_d;
-                last_depth = b.z;
-                dL_dalpha += (b.z - acc_d) * dpix_d;
-                v[9] = dchannel_dcolor * dpix_d;
-                acc_a = last_alpha * 1.0f + (1.f - last_alpha) * acc_a;
-                dL_dalpha += (1.f - acc_a) * dpix_a;
-                dL_dalpha *= T;
-                last_alpha = alpha;
-                dL_dalpha += (-T_final * inv_1ma) * bg_dot;
-                const float dL_dG = b.y * dL_dalpha;
-                const float gdx = G * dx, gdy = G * dy;
-                const float dG_ddelx = -gdx * a.z - gdy * a.w;
-                const float dG_ddely = -gdy * b.x - gdx * a.w;
-                v[0] = dL_dG * dG_ddelx * ddelx_dx;
-                v[1] = dL_dG * dG_ddely * ddely_dy;
-                v[2] = -0.5f * gdx * dx * dL_dG;
-                v[3] = -0.5f * gdx * dy * dL_dG;
-                v[4] = -0.5f * gdy * dy * dL_dG;
-                v[5] = G * dL_dalpha;
-              }
+        if (rel < last_contributor) {
+          const float4 a = s0[k];
+          const float4 b = s1[k];
+          const float dx = a.x - pxf, dy = a.y - pyf;
+          const float power = gauss_power(a.z, a.w, b.x, dx, dy);
+          if (power <= 0.0f) {
+            const float G = __expf(power);
+            const float alpha = fminf(GSR_ALPHA_MAX, b.y * G);
+            if (alpha >= GSR_ALPHA_MIN) {
+              hit = true;
+              const float4 c = s2[k];
+              const float inv_1ma = fast_rcp(1.f - alpha);
+              T = T * inv_1ma;
+              const float dchannel_dcolor = alpha * T;
+              float dL_dalpha = 0.0f;
+              acc_r = last_alpha * last_r + (1.f - last_alpha) * acc_r;
+              acc_g = last_alpha * last_g + (1.f - last_alpha) * acc_g;
+              acc_b = last_alpha * last_b + (1.f - last_alpha) * acc_b;
+              last_r = c.x;
+              last_g = c.y;
+              last_b = c.z;
+              dL_dalpha += (c.x - acc_r) * dpix[0];
+              dL_dalpha += (c.y - acc_g) * dpix[1];
+              dL_dalpha += (c.z - acc_b) * dpix[2];
+              v[6] = dchannel_dcolor * dpix[0];
+              v[7] = dchannel_dcolor * dpix[1];
+              v[8] = dchannel_dcolor * dpix[2];
+              acc_d = last_alpha * last_depth + (1.f - last_alpha) * acc_d;
+              last_depth = b.z;
+              dL_dalpha += (b.z - acc_d) * dpix_d;
+              v[9] = dchannel_dcolor * dpix_d;
+              acc_a = last_alpha * 1.0f + (1.f - last_alpha) * acc_a;
+              dL_dalpha += (1.f - acc_a) * dpix_a;
+              dL_dalpha *= T;
+              last_alpha = alpha;
+              dL_dalpha += (-T_final * inv_1ma) * bg_dot;
+              const float dL_dG = b.y * dL_dalpha;
+              const float gdx = G * dx, gdy = G * dy;
+              const float dG_ddelx = -gdx * a.z - gdy * a.w;
+              const float dG_ddely = -gdy * b.x - gdx * a.w;
+              v[0] = dL_dG * dG_ddelx * ddelx_dx;
+              v[1] = dL_dG * dG_ddely * ddely_dy;
+              v[2] = -0.5f * gdx * dx * dL_dG;
+              v[3] = -0.5f * gdx * dy * dL_dG;
+              v[4] = -0.5f * gdy * dy * dL_dG;
+              v[5] = G * dL_dalpha;
             }
           }
         }
-        float4* part = s_part[jj][w * 4 + prow];
+        float4* part = s_part[kk][prow];
         if (__any(hit)) {
-          // 16-lane row sums (interleaved over the 10 terms: no DPP hazard stalls); lane 15 of
-          // each row holds its row's total
           row_reduce_step<1>(v);
           row_reduce_step<2>(v);
           row_reduce_step<4>(v);
@@ -366,25 +353,19 @@ __global__ __launch_bounds__(256) void k_render_bwd(int W, int H, int grid_x, in
             part[2] = make_float4(v[8], v[9], 0.f, 0.f);
           }
         } else if ((lane & 15) == 15) {
-          const float4 z = make_float4(0.f, 0.f, 0.f, 0.f);
-          part[0] = z;
-          part[1] = z;
-          part[2] = z;
+          part[0] = zero4;
+          part[1] = zero4;
+          part[2] = zero4;
         }
       }
       __syncthreads();
-      if (t < scnt * 3) {
-        const int jj = t / 3, grp = t - jj * 3;
-        float4 acc = s_part[jj][0][grp];
-#pragma unroll
-        for (int q = 1; q < 16; ++q) {
-          const float4 x = s_part[jj][q][grp];
-          acc.x += x.x;
-          acc.y += x.y;
-          acc.z += x.z;
-          acc.w += x.w;
-        }
-        grow[3 * (size_t)s_dest[sub + jj] + grp] = acc;
+      for (int task = lane; task < scnt * 3; task += 64) {
+        const int kk = task / 3, grp = task - kk * 3;
+        const float4 x0 = s_part[kk][0][grp], x1 = s_part[kk][1][grp];
+        const float4 x2 = s_part[kk][2][grp], x3 = s_part[kk][3][grp];
+        const float4 acc = make_float4((x0.x + x1.x) + (x2.x + x3.x), (x0.y + x1.y) + (x2.y + x3.y),
+                                       (x0.z + x1.z) + (x2.z + x3.z), (x0.w + x1.w) + (x2.w + x3.w));
+        grow[3 * (size_t)s_dest[sub + kk] + grp] = acc;
       }
       __syncthreads();
     }
@@ -398,8 +379,8 @@ void launch_render_backward(int W, int H, int K, const GeomState& g, const uint3
   const int gx = div_up(W, GSR_TILE_X), gy = div_up(H, GSR_TILE_Y);
   const int nt = gx * gy;
   if (nt <= 0 || K <= 0) return;
-  hipLaunchKernelGGL(k_render_bwd, dim3(nt), dim3(256), 0, stream, W, H, gx, nt,
-                     (const uint2*)img.ranges, (const uint4*)img.tile_info, sorted_gauss,
+  hipLaunchKernelGGL(k_render_bwd, dim3(4 * nt), dim3(64), 0, stream, W, H, gx, 4 * nt,
+                     (const uint2*)img.ranges, (const uint32_t*)img.quad_maxc, sorted_gauss,
                      (const float4*)g.rec0, (const float4*)g.rec1, (const float4*)g.rec2,
                      (const uint2*)g.rect, (const uint32_t*)g.goff, bg, (const float*)img.final_T,
                      (const uint32_t*)img.n_contrib, dL_dcolor, dL_ddepth, dL_dalpha, bw.grow);
