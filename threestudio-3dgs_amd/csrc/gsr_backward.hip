@@ -17,7 +17,7 @@
 namespace gsr {
 
 __global__ __launch_bounds__(256) void k_gauss_bwd(GaussBackwardArgs a, int grid_x, GeomState g,
-                                                   const uint2* __restrict__ quad_cut, BackwardState bw) {
+                                                   const uint4* __restrict__ tile_info, BackwardState bw) {
   const int idx = blockIdx.x * blockDim.x + threadIdx.x;
   if (idx >= a.P) return;
   const int Mc = a.M;
@@ -27,8 +27,8 @@ __global__ __launch_bounds__(256) void k_gauss_bwd(GaussBackwardArgs a, int grid
   float dcr = 0.f, dcg = 0.f, dcbl = 0.f, ddep = 0.f;
   if (visible) {
     // rows of this Gaussian's instances are contiguous (tile rect, row-major, 4 quadrant rows each);
-    // a quadrant row is valid only if that quadrant's blend reached the instance:
-    // (depth key, index) < the quadrant's first unblended instance
+    // an instance's rows are valid iff its tile's blend reached it:
+    // (depth key, index) < the tile's first unblended instance
     const size_t i0 = g.goff[idx];
     const uint2 rc = g.rect[idx];
     const int xmin = rc.x & 0xffff, ymin = rc.x >> 16, xmax = rc.y & 0xffff, ymax = rc.y >> 16;
@@ -36,14 +36,13 @@ __global__ __launch_bounds__(256) void k_gauss_bwd(GaussBackwardArgs a, int grid
     size_t i = i0;
     for (int ty = ymin; ty < ymax; ++ty)
       for (int tx = xmin; tx < xmax; ++tx, ++i) {
-        const uint2* cut = quad_cut + 4 * (size_t)(ty * grid_x + tx);
+        const uint4 info = tile_info[ty * grid_x + tx];
+        const bool valid = dkey < info.y || (dkey == info.y && (uint32_t)idx < info.z);
+        if (!valid) continue;
+        const float4* row = bw.grow + 12 * i;
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
-          const uint2 c = cut[q];
-          const bool valid = dkey < c.x || (dkey == c.x && (uint32_t)idx < c.y);
-          if (!valid) continue;
-          const size_t r = 4 * i + q;
-          const float4 r0 = bw.grow[3 * r], r1 = bw.grow[3 * r + 1], r2 = bw.grow[3 * r + 2];
+          const float4 r0 = row[3 * q], r1 = row[3 * q + 1], r2 = row[3 * q + 2];
           dmx += r0.x; dmy += r0.y; dca += r0.z; dcb += r0.w;
           dcc += r1.x; dop += r1.y; dcr += r1.z; dcg += r1.w;
           dcbl += r2.x; ddep += r2.y;
@@ -288,7 +287,7 @@ void launch_gauss_backward(const GaussBackwardArgs& a, int W, int H, const GeomS
   (void)H;
   if (a.P <= 0) return;
   hipLaunchKernelGGL(k_gauss_bwd, dim3((a.P + 255) / 256), dim3(256), 0, stream, a,
-                     div_up(W, GSR_TILE_X), g, (const uint2*)img.quad_cut, bw);
+                     div_up(W, GSR_TILE_X), g, (const uint4*)img.tile_info, bw);
 }
 
 }  // namespace gsr

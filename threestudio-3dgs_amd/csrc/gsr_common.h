@@ -117,7 +117,7 @@ struct BinningState {
 struct ImageState {
   uint2* ranges;       // [tiles] sorted-instance range of each tile
   uint32_t* quad_maxc; // [4*tiles] per 8x8 quadrant: instances [0, maxc) of the tile list were blended
-  uint2* quad_cut;     // [4*tiles] (depth key, Gaussian) of the quadrant's first unblended instance
+  uint4* tile_info;    // [tiles] (tile maxc, depth key and Gaussian of the first unblended instance, 0)
   float* final_T;      // [H*W]
   uint32_t* n_contrib; // [H*W]
   static ImageState carve(void* base, int W, int H, size_t* bytes) {
@@ -127,7 +127,7 @@ struct ImageState {
     size_t pix = (size_t)W * H;
     s.ranges = c.take<uint2>(tiles > 0 ? tiles : 1);
     s.quad_maxc = c.take<uint32_t>(4 * (size_t)(tiles > 0 ? tiles : 1));
-    s.quad_cut = c.take<uint2>(4 * (size_t)(tiles > 0 ? tiles : 1));
+    s.tile_info = c.take<uint4>(tiles > 0 ? tiles : 1);
     s.final_T = c.take<float>(pix > 0 ? pix : 1);
     s.n_contrib = c.take<uint32_t>(pix > 0 ? pix : 1);
     if (bytes) *bytes = align_up(c.off, 256);

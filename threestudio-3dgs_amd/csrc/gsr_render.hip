@@ -145,24 +145,27 @@ __global__ __launch_bounds__(64) void k_render_fwd(int W, int H, int grid_x, int
   if (lane == 0) quad_maxc[unit] = mc;
 }
 
-// Per quadrant: instances [0, maxc) of the tile list were blended by some pixel of the quadrant;
-// record the (depth key, Gaussian) of the first instance nobody in the quadrant blended, for the
-// per-Gaussian backward's validity test of the quadrant's gradient rows.
-__global__ __launch_bounds__(256) void k_quad_info(int n_units, const uint2* __restrict__ ranges,
+// Per tile: instances [0, maxc) were blended by some pixel (max over the 4 quadrants); record the
+// (depth key, Gaussian) of the first instance nobody blended.  The backward writes gradient rows
+// for exactly the instances [0, maxc) of each tile (all 4 quadrants), so the per-Gaussian
+// gather-sum can test validity per instance against this cutoff.
+__global__ __launch_bounds__(256) void k_tile_info(int n_tiles, const uint2* __restrict__ ranges,
                                                    const uint32_t* __restrict__ quad_maxc,
                                                    const uint32_t* __restrict__ sorted_gauss,
                                                    const float4* __restrict__ rec1,
-                                                   uint2* __restrict__ quad_cut) {
-  const int u = blockIdx.x * blockDim.x + threadIdx.x;
-  if (u >= n_units) return;
-  const uint32_t maxc = quad_maxc[u];
-  const uint2 range = ranges[u >> 2];
-  uint2 cut = make_uint2(0xFFFFFFFFu, 0xFFFFFFFFu);
+                                                   uint4* __restrict__ tile_info) {
+  const int tile = blockIdx.x * blockDim.x + threadIdx.x;
+  if (tile >= n_tiles) return;
+  const uint4 m = reinterpret_cast<const uint4*>(quad_maxc)[tile];
+  const uint32_t maxc = max(max(m.x, m.y), max(m.z, m.w));
+  const uint2 range = ranges[tile];
+  uint4 info = make_uint4(maxc, 0xFFFFFFFFu, 0xFFFFFFFFu, 0u);
   if (maxc < range.y - range.x) {
     const uint32_t gi = sorted_gauss[range.x + maxc];
-    cut = make_uint2(__float_as_uint(rec1[gi].z), gi);
+    info.y = __float_as_uint(rec1[gi].z);
+    info.z = gi;
   }
-  quad_cut[u] = cut;
+  tile_info[tile] = info;
 }
 
 void launch_render_forward(int W, int H, const GeomState& g, const uint32_t* sorted_gauss,
@@ -175,9 +178,9 @@ void launch_render_forward(int W, int H, const GeomState& g, const uint32_t* sor
                      (const uint2*)img.ranges, sorted_gauss, (const float4*)g.rec0,
                      (const float4*)g.rec1, (const float4*)g.rec2, bg, out_color, out_depth, out_alpha,
                      img.final_T, img.n_contrib, img.quad_maxc);
-  hipLaunchKernelGGL(k_quad_info, dim3(div_up(4 * nt, 256)), dim3(256), 0, stream, 4 * nt,
+  hipLaunchKernelGGL(k_tile_info, dim3(div_up(nt, 256)), dim3(256), 0, stream, nt,
                      (const uint2*)img.ranges, (const uint32_t*)img.quad_maxc, sorted_gauss,
-                     (const float4*)g.rec1, img.quad_cut);
+                     (const float4*)g.rec1, img.tile_info);
 }
 
 // ---------------------------------------------------------------------------------------
@@ -194,11 +197,13 @@ __device__ __forceinline__ void row_reduce_step(float (&v)[NGV]) {
 }
 
 // One wave per 8x8 quadrant (as the forward).  The wave walks its tile's list back to front from
-// the quadrant's deepest blended instance, 64 at a time, keeps (ballot compaction, order kept) the
-// Gaussians whose alpha >= 1/255 ellipse reaches the quadrant, replays them per pixel, reduces each
-// Gaussian's 10 terms over 16-lane rows with DPP, parks the 4 row partials in LDS and every 32
-// Gaussians writes one 48-byte row per (instance, quadrant) at 4 * slot + quadrant, where slot is
-// the instance's place in its Gaussian's contiguous row range.  Culled instances get zero rows.
+// the tile's deepest blended instance, 64 at a time, keeps (ballot compaction, order kept) the
+// Gaussians that are above the quadrant's own deepest blended instance and whose alpha >= 1/255
+// ellipse reaches the quadrant, replays them per pixel, reduces each Gaussian's 10 terms over
+// 16-lane rows with DPP, parks the 4 row partials in LDS and every 32 Gaussians writes one 48-byte
+// row per (instance, quadrant) at 4 * slot + quadrant, where slot is the instance's place in its
+// Gaussian's contiguous row range.  Instances the quadrant skips get zero rows, so every instance
+// above the tile cutoff has all 4 rows written.
 __global__ __launch_bounds__(64) void k_render_bwd(int W, int H, int grid_x, int n_units,
                                                    const uint2* __restrict__ ranges,
                                                    const uint32_t* __restrict__ quad_maxc,
@@ -228,7 +233,9 @@ __global__ __launch_bounds__(64) void k_render_bwd(int W, int H, int grid_x, int
   const bool inside = px < W && py < H;
   const float pxf = (float)px, pyf = (float)py;
   const uint2 range = ranges[tile];
-  const int maxc = (int)quad_maxc[unit];
+  const int qmaxc = (int)quad_maxc[unit];
+  const uint4 qm = reinterpret_cast<const uint4*>(quad_maxc)[tile];
+  const int maxc = (int)max(max(qm.x, qm.y), max(qm.z, qm.w));
   const size_t pid = (size_t)py * W + px;
   const size_t HW = (size_t)H * W;
 
@@ -265,7 +272,7 @@ __global__ __launch_bounds__(64) void k_render_bwd(int W, int H, int grid_x, int
       const uint2 rc = rect[gi];
       const int xmin = rc.x & 0xffff, ymin = rc.x >> 16, xmax = rc.y & 0xffff;
       dest = 4u * (goff[gi] + (uint32_t)((tyi - ymin) * (xmax - xmin) + (txi - xmin))) + (uint32_t)q;
-      keep = quadrant_hit(r0, r1, (float)qx0, (float)qy0);
+      keep = rel_l < qmaxc && quadrant_hit(r0, r1, (float)qx0, (float)qy0);
       if (!keep) {
         grow[3 * (size_t)dest] = zero4;
         grow[3 * (size_t)dest + 1] = zero4;
