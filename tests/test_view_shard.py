@@ -1,0 +1,117 @@
+"""View sharding across ranks with the gloo backend on CPU, world_size 2 and 3:
+the gathered batch images, the all-reduced Gaussian gradients and the reduced densification statistics
+must equal a single-process render of the whole batch.  The per-view renderer is the differentiable
+torch formulation (tests/torch_reference.py) so the sharding/collective logic runs without a GPU."""
+import math
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+import torch_reference as tr
+from diff_gaussian_rasterization.cameras import get_cam_info_gaussian, orbit_c2w
+from diff_gaussian_rasterization.view_shard import (ViewShardedBatchRenderer, allreduce_grads,
+                                                    reduce_densify_stats, shard_range)
+from gsr_testutil import gs
+
+H = W = 24
+B = 5
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _params():
+    scene = gs.make_scene(40, sh_degree=1, seed=3, radius=0.5)
+    return {k: torch.tensor(scene[k], dtype=torch.float64, requires_grad=True)
+            for k in ("means3D", "scales", "rotations", "opacities", "shs")}
+
+
+def _batch():
+    c2w = orbit_c2w(torch.full((B,), 2.5), torch.linspace(0, 30, B), torch.linspace(0, 288, B))
+    return {"c2w": c2w, "fovy": torch.full((B,), math.radians(60.0)), "height": H, "width": W}
+
+
+def _render_view(params):
+    def fn(batch_idx, batch):
+        fov = float(batch["fovy"][batch_idx])
+        wv, fp, cc = get_cam_info_gaussian(batch["c2w"][batch_idx], fov, fov)
+        P = params["means3D"].shape[0]
+        sp = torch.zeros(P, 3, dtype=torch.float64, requires_grad=True)
+        sp.retain_grad()
+        tan = math.tan(fov / 2)
+        color, radii, depth, alpha = tr.render(params["means3D"], sp, params["opacities"], wv.reshape(-1),
+                                               fp.reshape(-1), cc, tan, tan, W, H, torch.zeros(3), sh=params["shs"],
+                                               deg=1, scales=params["scales"], rotations=params["rotations"])
+        return {"render": color, "depth": depth, "mask": alpha, "viewspace_points": sp,
+                "visibility_filter": radii > 0, "radii": radii}
+    return fn
+
+
+def _loss(out):
+    g = torch.Generator().manual_seed(0)
+    wc = torch.randn(out["comp_rgb"].shape, generator=g, dtype=torch.float64)
+    wd = torch.randn(out["comp_depth"].shape, generator=g, dtype=torch.float64)
+    return (out["comp_rgb"] * wc).sum() + (out["comp_depth"] * wd).sum() + out["comp_mask"].sum()
+
+
+def _single_process():
+    params = _params()
+    r = ViewShardedBatchRenderer(_render_view(params))
+    out = r.batch_forward(_batch())
+    _loss(out).backward()
+    stats = reduce_densify_stats(out["radii"], out["viewspace_points"], out["visibility_filter"], 40)
+    return ({k: out[k].detach().numpy() for k in ("comp_rgb", "comp_depth", "comp_mask")},
+            {k: v.grad.numpy() for k, v in params.items()}, [s.numpy() for s in stats])
+
+
+def _worker(rank, world, port, tmp):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        params = _params()
+        r = ViewShardedBatchRenderer(_render_view(params))
+        out = r.batch_forward(_batch())
+        assert out["view_range"] == shard_range(B, world, rank)
+        _loss(out).backward()
+        allreduce_grads(list(params.values()))
+        stats = reduce_densify_stats(out["radii"], out["viewspace_points"], out["visibility_filter"], 40)
+        np.savez(os.path.join(tmp, f"rank{rank}.npz"),
+                 **{k: out[k].detach().numpy() for k in ("comp_rgb", "comp_depth", "comp_mask")},
+                 **{"grad_" + k: v.grad.numpy() for k, v in params.items()},
+                 **{f"stat{i}": s.numpy() for i, s in enumerate(stats)})
+    finally:
+        dist.destroy_process_group()
+
+
+def test_shard_range_covers_batch():
+    for bs in (1, 5, 8, 64):
+        for world in (1, 2, 3, 8):
+            spans = [shard_range(bs, world, r) for r in range(world)]
+            assert spans[0][0] == 0 and spans[-1][1] == bs
+            assert all(spans[i][1] == spans[i + 1][0] for i in range(world - 1))
+            sizes = [e - s for s, e in spans]
+            assert max(sizes) - min(sizes) <= 1
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_sharded_batch_equals_single_process(world, tmp_path):
+    ref_imgs, ref_grads, ref_stats = _single_process()
+    mp.spawn(_worker, args=(world, _free_port(), str(tmp_path)), nprocs=world, join=True)
+    for rank in range(world):
+        z = np.load(tmp_path / f"rank{rank}.npz")
+        for k, v in ref_imgs.items():
+            np.testing.assert_array_equal(z[k], v, err_msg=f"rank {rank} {k}")
+        for k, v in ref_grads.items():
+            np.testing.assert_allclose(z["grad_" + k], v, rtol=1e-10, atol=1e-12, err_msg=f"rank {rank} grad {k}")
+        for i, v in enumerate(ref_stats):
+            np.testing.assert_allclose(z[f"stat{i}"], v, rtol=1e-6, atol=1e-9, err_msg=f"rank {rank} stat {i}")

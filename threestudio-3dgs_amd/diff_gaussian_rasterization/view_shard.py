@@ -1,0 +1,152 @@
+"""View-sharded batch rendering across the GPUs of one node.
+
+The reference renders a batch with a serial per-view Python loop on one device
+(GaussianBatchRenderer.batch_forward, renderer/gaussian_batch_renderer.py:9-122) and has no
+distributed code.  Views are independent given replicated Gaussians, so here rank r of G renders
+views [r*B/G, (r+1)*B/G) of the batch with a full replica of the Gaussian parameters, and:
+
+  forward   the rendered images are all-gathered (RCCL over xGMI; the north_star exchange) so that
+            every rank holds the full batch for batch-level losses (e.g. MVDream's multi-view SDS).
+            Only the local slice carries autograd history, so each view's gradient is computed on
+            exactly one rank.
+  backward  allreduce_grads() sums the per-Gaussian parameter gradients (one flat bucket), giving every
+            replica the full-batch gradient; reduce_densify_stats() pre-reduces the densification
+            statistics (max radii, sum of |means2D.grad[:, :2]|, visibility counts) that
+            geometry/gaussian_base.py:815-851 would otherwise need per view from every rank.
+
+One process per GPU; `torch.distributed` backend "nccl" is RCCL on ROCm.  Everything here is also
+exercised with the gloo backend on CPU (tests/test_view_shard.py).
+"""
+from __future__ import annotations
+
+from typing import Callable
+
+import torch
+import torch.distributed as dist
+
+# render_pkg keys of the reference wrappers that are per-view images (C, H, W) -> stacked to BHWC
+_IMAGE_KEYS = (("render", "comp_rgb"), ("normal", "comp_normal"), ("normal_from_dist", "comp_normal_from_dist"),
+               ("pred_normal", "comp_pred_normal"), ("depth", "comp_depth"), ("mask", "comp_mask"))
+
+
+def _world():
+    if dist.is_available() and dist.is_initialized():
+        return dist.get_world_size(), dist.get_rank()
+    return 1, 0
+
+
+def shard_range(batch_size: int, world: int, rank: int):
+    """Contiguous view slice of `rank`; views are split as evenly as possible (first ranks take the remainder)."""
+    base, extra = divmod(batch_size, world)
+    start = rank * base + min(rank, extra)
+    return start, start + base + (1 if rank < extra else 0)
+
+
+def all_gather_views(local: torch.Tensor, batch_size: int, group=None) -> torch.Tensor:
+    """Gather per-rank view slices (n_r, ...) into the full (batch_size, ...) tensor on every rank.
+
+    The local slice keeps its autograd history; the other ranks' slices are constants here.
+    """
+    world, rank = _world()
+    if world == 1:
+        return local
+    counts = [shard_range(batch_size, world, r) for r in range(world)]
+    n_max = max(e - s for s, e in counts)
+    pad = local.new_zeros((n_max,) + tuple(local.shape[1:]))
+    pad[: local.shape[0]] = local.detach()
+    if dist.get_backend(group) == "nccl":
+        out = local.new_empty((world * n_max,) + tuple(local.shape[1:]))
+        dist.all_gather_into_tensor(out, pad.contiguous(), group=group)
+        parts = list(out.split(n_max))
+    else:
+        parts = [torch.empty_like(pad) for _ in range(world)]
+        dist.all_gather(parts, pad.contiguous(), group=group)
+    pieces = []
+    for r, (s, e) in enumerate(counts):
+        pieces.append(local if r == rank else parts[r][: e - s])
+    return torch.cat(pieces, 0)
+
+
+def allreduce_grads(params, group=None, average: bool = False):
+    """Sum (or average) the .grad of `params` over ranks in one flat bucket (one RCCL all-reduce)."""
+    world, _ = _world()
+    if world == 1:
+        return
+    grads = [p.grad for p in params if p.grad is not None]
+    if not grads:
+        return
+    flat = torch.cat([g.reshape(-1) for g in grads])
+    dist.all_reduce(flat, group=group)
+    if average:
+        flat /= world
+    off = 0
+    for g in grads:
+        n = g.numel()
+        g.copy_(flat[off:off + n].view_as(g))
+        off += n
+
+
+def reduce_densify_stats(radii, viewspace_points, visibility_filter, num_points: int, group=None):
+    """Per-Gaussian densification statistics over the whole batch (all ranks).
+
+    Returns (max_radii, grad_norm_sum, count) with the semantics of update_states /
+    add_densification_stats (geometry/gaussian_base.py:815-851) applied to every view of the batch:
+      max_radii     = max over views of radii
+      grad_norm_sum = sum over views of |viewspace_points.grad[:, :2]| where visible
+      count         = number of views in which the Gaussian is visible
+    """
+    dev = radii[0].device if radii else torch.device("cpu")
+    max_r = torch.zeros(num_points, device=dev, dtype=torch.float32)
+    gsum = torch.zeros(num_points, device=dev, dtype=torch.float32)
+    cnt = torch.zeros(num_points, device=dev, dtype=torch.float32)
+    for r, vp, vis in zip(radii, viewspace_points, visibility_filter):
+        max_r = torch.maximum(max_r, r.float())
+        if vp.grad is not None:
+            gsum[vis] += torch.norm(vp.grad[vis, :2], dim=-1)
+        cnt[vis] += 1
+    world, _ = _world()
+    if world > 1:
+        dist.all_reduce(max_r, op=dist.ReduceOp.MAX, group=group)
+        both = torch.stack([gsum, cnt])
+        dist.all_reduce(both, group=group)
+        gsum, cnt = both[0], both[1]
+    return max_r, gsum, cnt
+
+
+class ViewShardedBatchRenderer:
+    """batch_forward() with the output contract of GaussianBatchRenderer (renderer/gaussian_batch_renderer.py:78-121),
+    rendering only this rank's views.
+
+    `render_view(batch_idx, batch) -> render_pkg` renders one view (in threestudio: build the Camera from
+    batch["c2w"][batch_idx] with get_cam_info_gaussian and call DiffGaussian.forward, :22-56).
+    Image outputs are gathered to the full batch on every rank; the per-view lists
+    (viewspace_points, visibility_filter, radii) hold the local views, with "view_range" telling
+    which batch indices they are.
+    """
+
+    def __init__(self, render_view: Callable[[int, dict], dict], group=None):
+        self.render_view = render_view
+        self.group = group
+
+    def batch_forward(self, batch: dict) -> dict:
+        bs = int(batch["c2w"].shape[0])
+        world, rank = _world()
+        start, end = shard_range(bs, world, rank)
+        pkgs = []
+        for batch_idx in range(start, end):
+            batch["batch_idx"] = batch_idx
+            pkgs.append(self.render_view(batch_idx, batch))
+        out = {
+            "viewspace_points": [p["viewspace_points"] for p in pkgs],
+            "visibility_filter": [p["visibility_filter"] for p in pkgs],
+            "radii": [p["radii"] for p in pkgs],
+            "view_range": (start, end),
+        }
+        for key, name in _IMAGE_KEYS:
+            if pkgs and key in pkgs[0] and pkgs[0][key] is not None:
+                local = torch.stack([p[key] for p in pkgs], 0)
+                out[name] = all_gather_views(local, bs, self.group).permute(0, 2, 3, 1)
+        if pkgs and "comp_rgb_bg" in pkgs[0]:
+            local = torch.cat([p["comp_rgb_bg"] for p in pkgs], 0)
+            out["comp_rgb_bg"] = all_gather_views(local, bs, self.group).permute(0, 2, 3, 1)
+        return out
