@@ -152,14 +152,15 @@ def main():
 
     import gsr_synthetic as gs
     from diff_gaussian_rasterization import _C
+    from diff_gaussian_rasterization.view_shard import all_gather_views, allreduce_grads, shard_range
 
-    assert args.views % world == 0, "views must divide evenly over ranks"
     t_setup = time.perf_counter()
     scene = gs.make_scene(args.gaussians, sh_degree=args.sh_degree, seed=0)  # identical replica on every rank
     rep = Replica(scene, device)
     cams = build_views(args.views, args.res, device)
-    per = args.views // world
-    mine = cams[rank * per:(rank + 1) * per]
+    v0, v1 = shard_range(args.views, world, rank)
+    per = v1 - v0
+    mine = cams[v0:v1]
     H = W = args.res
     gen = torch.Generator(device=device).manual_seed(1234 + rank)
     upstream = [(torch.randn((3, H, W), generator=gen, device=device),
@@ -167,22 +168,16 @@ def main():
                  torch.randn((1, H, W), generator=gen, device=device)) for _ in mine]
     bg_zero = torch.zeros(3, device=device)
     bg_const = torch.tensor([0.5, 0.5, 0.5], device=device)
-    gathered = torch.empty((args.views, 5, H, W), device=device) if world > 1 else None
-    flat_grad = None
     log(f"[bench] rank {rank}/{world}: setup {time.perf_counter() - t_setup:.1f}s, {len(mine)} views/rank")
 
     def step():
-        nonlocal flat_grad
         outs = [render_view(rep, cam, bg_zero, bg_const) for cam in mine]
         if world > 1:
-            local_imgs = torch.stack([torch.cat([c, d, a], 0) for c, d, a, _ in outs]).detach()
-            dist.all_gather_into_tensor(gathered, local_imgs)
+            # forward exchange: every rank receives the whole batch of rendered images
+            all_gather_views(torch.stack([torch.cat([c, d, a], 0) for c, d, a, _ in outs]), args.views)
         loss = sum((c * g[0]).sum() + (d * g[1]).sum() + (a * g[2]).sum() for (c, d, a, _), g in zip(outs, upstream))
         loss.backward()
-        if world > 1:
-            grads = [p.grad.reshape(-1) for p in rep.params]
-            flat_grad = torch.cat(grads) if flat_grad is None else torch.cat(grads, out=flat_grad)
-            dist.all_reduce(flat_grad)
+        allreduce_grads(rep.params)  # one flat RCCL all-reduce of the Gaussian parameter gradients
         rep.zero_grad()
 
     for _ in range(args.warmup):

@@ -1,0 +1,43 @@
+"""Summarise a rocprofv3 capture (profiles/run_profiles.sh) into committed files:
+  <tag>_kernel_stats.csv   rocprofv3 --kernel-trace --stats summary (as written by rocprofv3)
+  <tag>_pmc.csv            per kernel: dispatches, mean FETCH_SIZE / WRITE_SIZE (KB, raw counter values) and the
+                           corrected HBM bytes per launch = (2 * FETCH_SIZE + WRITE_SIZE) * 1024
+                           (gfx950: FETCH_SIZE reads 1/2 of a wide coalesced read; MI355X_MICROARCH.md §HBM)
+  <tag>_traffic.json       the same per-launch bytes for the blend kernels, read by bench.py for roofline.traffic
+"""
+import collections
+import csv
+import json
+import os
+import shutil
+import sys
+
+tag = sys.argv[1] if len(sys.argv) > 1 else "r01"
+src = os.path.join("gpurun_out", f"prof_{tag}")
+dst = os.path.dirname(os.path.abspath(__file__))
+shutil.copy(os.path.join(src, "trace", "run_kernel_stats.csv"), os.path.join(dst, f"{tag}_kernel_stats.csv"))
+
+
+def agg(path, counter):
+    d = collections.defaultdict(list)
+    for r in csv.DictReader(open(path)):
+        if r["Counter_Name"] == counter:
+            d[r["Kernel_Name"].split("(")[0]].append(float(r["Counter_Value"]))
+    return d
+
+
+f = agg(os.path.join(src, "fetch", "run_counter_collection.csv"), "FETCH_SIZE")
+w = agg(os.path.join(src, "write", "run_counter_collection.csv"), "WRITE_SIZE")
+rows = []
+for k in sorted(f, key=lambda k: -sum(f[k]) / len(f[k])):
+    fk = sum(f[k]) / len(f[k])
+    wk = sum(w.get(k, [0.0])) / max(1, len(w.get(k, [0.0])))
+    rows.append((k, len(f[k]), round(fk, 1), round(wk, 1), int((2 * fk + wk) * 1024)))
+with open(os.path.join(dst, f"{tag}_pmc.csv"), "w", newline="") as fh:
+    wr = csv.writer(fh)
+    wr.writerow(["kernel", "dispatches", "FETCH_SIZE_KB", "WRITE_SIZE_KB", "hbm_bytes_per_launch_corrected"])
+    wr.writerows(rows)
+traffic = {r[0].replace("gsr::", ""): r[4] for r in rows if r[0].startswith("gsr::")}
+json.dump({"source": f"profiles/{tag}_pmc.csv", "per_launch_bytes": traffic},
+          open(os.path.join(dst, f"{tag}_traffic.json"), "w"), indent=1)
+print("\n".join(f"{r[0]:40s} {r[4] / 1e6:10.1f} MB/launch" for r in rows[:12]))
