@@ -19,13 +19,26 @@
 
 namespace gsr {
 
-// blockIdx -> tile index: blocks b and b+8 share an XCD (round-robin dispatch), so give each
-// group of blocks with equal b % 8 one contiguous band of tile rows -> neighbouring tiles, which
-// share most of their Gaussians, hit the same L2.  Bijective for any tile count.
-__device__ __forceinline__ int xcd_tile(int b, int nt) {
-  const int xcd = b & 7, k = b >> 3;
-  const int q = nt >> 3, r = nt & 7;
-  return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + k;
+// blockIdx -> (tile, quadrant).  Blocks b and b+8 share an XCD under round-robin dispatch (speed
+// only, never correctness).  Units are grouped in 2x2-tile super-tiles (16 quadrant waves that share
+// most of their Gaussians -> one L2), and super-tiles are dealt round-robin over the 8 XCD groups so
+// the spatially clustered heavy tiles spread evenly over the chip (contiguous bands per XCD left the
+// scene centre on 2-3 XCDs).  Grid = 128 * ceil(super-tiles / 8); surplus blocks return false.
+__host__ __device__ __forceinline__ int unit_grid(int gx, int gy) {
+  const int S = ((gx + 1) >> 1) * ((gy + 1) >> 1);
+  return 128 * ((S + 7) >> 3);
+}
+__device__ __forceinline__ bool unit_of_block(int b, int gx, int gy, int& tile, int& q) {
+  const int sgx = (gx + 1) >> 1, sgy = (gy + 1) >> 1;
+  const int x = b & 7, k = b >> 3;
+  const int s = ((k >> 4) << 3) + x;
+  const int w = k & 15;
+  if (s >= sgx * sgy) return false;
+  const int tx = (s % sgx) * 2 + ((w >> 2) & 1), ty = (s / sgx) * 2 + (w >> 3);
+  if (tx >= gx || ty >= gy) return false;
+  tile = ty * gx + tx;
+  q = w & 3;
+  return true;
 }
 
 __device__ __forceinline__ void tile_pixel(int t, int& lx, int& ly) {
@@ -55,7 +68,7 @@ __device__ __forceinline__ bool quadrant_hit(const float4 r0, const float4 r1, f
 // Gaussians whose alpha >= 1/255 ellipse can reach its quadrant, and blends them with a
 // branch-free predicated body.  No workgroup barriers couple quadrants that terminate at
 // different depths, and 4x more independent waves balance the load across the 256 CUs.
-__global__ __launch_bounds__(64) void k_render_fwd(int W, int H, int grid_x, int n_units,
+__global__ __launch_bounds__(64) void k_render_fwd(int W, int H, int grid_x, int grid_y,
                                                    const uint2* __restrict__ ranges,
                                                    const uint32_t* __restrict__ sorted_gauss,
                                                    const float4* __restrict__ rec0,
@@ -70,8 +83,9 @@ __global__ __launch_bounds__(64) void k_render_fwd(int W, int H, int grid_x, int
                                                    uint32_t* __restrict__ quad_maxc) {
   __shared__ float4 s0[64], s1[64], s2[64];
   __shared__ uint32_t s_idx[64];
-  const int unit = xcd_tile(blockIdx.x, n_units);
-  const int tile = unit >> 2, q = unit & 3;
+  int tile, q;
+  if (!unit_of_block(blockIdx.x, grid_x, grid_y, tile, q)) return;
+  const int unit = 4 * tile + q;
   const int lane = threadIdx.x;
   const int qx0 = (tile % grid_x) * GSR_TILE_X + (q & 1) * 8;
   const int qy0 = (tile / grid_x) * GSR_TILE_Y + (q >> 1) * 8;
@@ -174,7 +188,7 @@ void launch_render_forward(int W, int H, const GeomState& g, const uint32_t* sor
   const int gx = div_up(W, GSR_TILE_X), gy = div_up(H, GSR_TILE_Y);
   const int nt = gx * gy;
   if (nt <= 0) return;
-  hipLaunchKernelGGL(k_render_fwd, dim3(4 * nt), dim3(64), 0, stream, W, H, gx, 4 * nt,
+  hipLaunchKernelGGL(k_render_fwd, dim3(unit_grid(gx, gy)), dim3(64), 0, stream, W, H, gx, gy,
                      (const uint2*)img.ranges, sorted_gauss, (const float4*)g.rec0,
                      (const float4*)g.rec1, (const float4*)g.rec2, bg, out_color, out_depth, out_alpha,
                      img.final_T, img.n_contrib, img.quad_maxc);
@@ -204,7 +218,7 @@ __device__ __forceinline__ void row_reduce_step(float (&v)[NGV]) {
 // row per (instance, quadrant) at 4 * slot + quadrant, where slot is the instance's place in its
 // Gaussian's contiguous row range.  Instances the quadrant skips get zero rows, so every instance
 // above the tile cutoff has all 4 rows written.
-__global__ __launch_bounds__(64) void k_render_bwd(int W, int H, int grid_x, int n_units,
+__global__ __launch_bounds__(64) void k_render_bwd(int W, int H, int grid_x, int grid_y,
                                                    const uint2* __restrict__ ranges,
                                                    const uint32_t* __restrict__ quad_maxc,
                                                    const uint32_t* __restrict__ sorted_gauss,
@@ -223,8 +237,9 @@ __global__ __launch_bounds__(64) void k_render_bwd(int W, int H, int grid_x, int
   __shared__ float4 s0[64], s1[64], s2[64];
   __shared__ uint32_t s_dest[64], s_rel[64];
   __shared__ float4 s_part[BWD_SUB][4][3];
-  const int unit = xcd_tile(blockIdx.x, n_units);
-  const int tile = unit >> 2, q = unit & 3;
+  int tile, q;
+  if (!unit_of_block(blockIdx.x, grid_x, grid_y, tile, q)) return;
+  const int unit = 4 * tile + q;
   const int lane = threadIdx.x;
   const int txi = tile % grid_x, tyi = tile / grid_x;
   const int qx0 = txi * GSR_TILE_X + (q & 1) * 8;
@@ -386,7 +401,7 @@ void launch_render_backward(int W, int H, int K, const GeomState& g, const uint3
   const int gx = div_up(W, GSR_TILE_X), gy = div_up(H, GSR_TILE_Y);
   const int nt = gx * gy;
   if (nt <= 0 || K <= 0) return;
-  hipLaunchKernelGGL(k_render_bwd, dim3(4 * nt), dim3(64), 0, stream, W, H, gx, 4 * nt,
+  hipLaunchKernelGGL(k_render_bwd, dim3(unit_grid(gx, gy)), dim3(64), 0, stream, W, H, gx, gy,
                      (const uint2*)img.ranges, (const uint32_t*)img.quad_maxc, sorted_gauss,
                      (const float4*)g.rec0, (const float4*)g.rec1, (const float4*)g.rec2,
                      (const uint2*)g.rect, (const uint32_t*)g.goff, bg, (const float*)img.final_T,
