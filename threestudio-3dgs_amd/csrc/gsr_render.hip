@@ -310,59 +310,49 @@ __global__ __launch_bounds__(64) void k_render_bwd(int W, int H, int grid_x, int
       for (int kk = 0; kk < scnt; ++kk) {
         const int k = sub + kk;
         const uint32_t rel = __builtin_amdgcn_readfirstlane(s_rel[k]);
-        float v[NGV];
-#pragma unroll
-        for (int e = 0; e < NGV; ++e) v[e] = 0.f;
-        bool hit = false;
-        if (rel < last_contributor) {
-          const float4 a = s0[k];
-          const float4 b = s1[k];
-          const float dx = a.x - pxf, dy = a.y - pyf;
-          const float power = gauss_power(a.z, a.w, b.x, dx, dy);
-          if (power <= 0.0f) {
-            const float G = __expf(power);
-            const float alpha = fminf(GSR_ALPHA_MAX, b.y * G);
-            if (alpha >= GSR_ALPHA_MIN) {
-              hit = true;
-              const float4 c = s2[k];
-              const float inv_1ma = fast_rcp(1.f - alpha);
-              T = T * inv_1ma;
-              const float dchannel_dcolor = alpha * T;
-              float dL_dalpha = 0.0f;
-              acc_r = last_alpha * last_r + (1.f - last_alpha) * acc_r;
-              acc_g = last_alpha * last_g + (1.f - last_alpha) * acc_g;
-              acc_b = last_alpha * last_b + (1.f - last_alpha) * acc_b;
-              last_r = c.x;
-              last_g = c.y;
-              last_b = c.z;
-              dL_dalpha += (c.x - acc_r) * dpix[0];
-              dL_dalpha += (c.y - acc_g) * dpix[1];
-              dL_dalpha += (c.z - acc_b) * dpix[2];
-              v[6] = dchannel_dcolor * dpix[0];
-              v[7] = dchannel_dcolor * dpix[1];
-              v[8] = dchannel_dcolor * dpix[2];
-              acc_d = last_alpha * last_depth + (1.f - last_alpha) * acc_d;
-              last_depth = b.z;
-              dL_dalpha += (b.z - acc_d) * dpix_d;
-              v[9] = dchannel_dcolor * dpix_d;
-              acc_a = last_alpha * 1.0f + (1.f - last_alpha) * acc_a;
-              dL_dalpha += (1.f - acc_a) * dpix_a;
-              dL_dalpha *= T;
-              last_alpha = alpha;
-              dL_dalpha += (-T_final * inv_1ma) * bg_dot;
-              const float dL_dG = b.y * dL_dalpha;
-              const float gdx = G * dx, gdy = G * dy;
-              const float dG_ddelx = -gdx * a.z - gdy * a.w;
-              const float dG_ddely = -gdy * b.x - gdx * a.w;
-              v[0] = dL_dG * dG_ddelx * ddelx_dx;
-              v[1] = dL_dG * dG_ddely * ddely_dy;
-              v[2] = -0.5f * gdx * dx * dL_dG;
-              v[3] = -0.5f * gdx * dy * dL_dG;
-              v[4] = -0.5f * gdy * dy * dL_dG;
-              v[5] = G * dL_dalpha;
-            }
-          }
-        }
+        // branch-free replay step (reference order of operations); non-contributing lanes keep
+        // their state and contribute zeros
+        const float4 a = s0[k];
+        const float4 b = s1[k];
+        const float4 c = s2[k];
+        const float dx = a.x - pxf, dy = a.y - pyf;
+        const float power = gauss_power(a.z, a.w, b.x, dx, dy);
+        const float G = __expf(power);
+        const float alpha = fminf(GSR_ALPHA_MAX, b.y * G);
+        const bool hit = rel < last_contributor && power <= 0.0f && alpha >= GSR_ALPHA_MIN;
+        const float inv_1ma = fast_rcp(1.f - alpha);
+        T = hit ? T * inv_1ma : T;
+        const float oml = 1.f - last_alpha;
+        const float nr = last_alpha * last_r + oml * acc_r;
+        const float ng = last_alpha * last_g + oml * acc_g;
+        const float nb = last_alpha * last_b + oml * acc_b;
+        const float nd = last_alpha * last_depth + oml * acc_d;
+        const float na = last_alpha * 1.0f + oml * acc_a;
+        float dL_dalpha = 0.0f;
+        dL_dalpha += (c.x - nr) * dpix[0];
+        dL_dalpha += (c.y - ng) * dpix[1];
+        dL_dalpha += (c.z - nb) * dpix[2];
+        dL_dalpha += (b.z - nd) * dpix_d;
+        dL_dalpha += (1.f - na) * dpix_a;
+        dL_dalpha *= T;
+        dL_dalpha += (-T_final * inv_1ma) * bg_dot;
+        const float u = hit ? G * dL_dalpha : 0.0f;  // dL/dG / opacity
+        const float w = hit ? alpha * T : 0.0f;      // dL/dcolor per unit dL/dpixel
+        acc_r = hit ? nr : acc_r;
+        acc_g = hit ? ng : acc_g;
+        acc_b = hit ? nb : acc_b;
+        acc_d = hit ? nd : acc_d;
+        acc_a = hit ? na : acc_a;
+        last_r = hit ? c.x : last_r;
+        last_g = hit ? c.y : last_g;
+        last_b = hit ? c.z : last_b;
+        last_depth = hit ? b.z : last_depth;
+        last_alpha = hit ? alpha : last_alpha;
+        // per pair: moments of u over the pixel offsets (mean2D / conic / opacity gradients are
+        // linear in them) and the colour / depth weights
+        const float udx = u * dx, udy = u * dy;
+        float v[NGV] = {u, udx, udy, udx * dx, udx * dy, udy * dy,
+                        w * dpix[0], w * dpix[1], w * dpix[2], w * dpix_d};
         float4* part = s_part[kk][prow];
         if (__any(hit)) {
           row_reduce_step<1>(v);
@@ -381,13 +371,27 @@ __global__ __launch_bounds__(64) void k_render_bwd(int W, int H, int grid_x, int
         }
       }
       __syncthreads();
-      for (int task = lane; task < scnt * 3; task += 64) {
-        const int kk = task / 3, grp = task - kk * 3;
-        const float4 x0 = s_part[kk][0][grp], x1 = s_part[kk][1][grp];
-        const float4 x2 = s_part[kk][2][grp], x3 = s_part[kk][3][grp];
-        const float4 acc = make_float4((x0.x + x1.x) + (x2.x + x3.x), (x0.y + x1.y) + (x2.y + x3.y),
-                                       (x0.z + x1.z) + (x2.z + x3.z), (x0.w + x1.w) + (x2.w + x3.w));
-        grow[3 * (size_t)s_dest[sub + kk] + grp] = acc;
+      if (lane < scnt) {
+        // one lane per Gaussian: sum the 4 row partials, turn moments into the reference's terms
+        //   dmean2D = -o (W/2, H/2) (a m1 + b m2, c m2 + b m1), dconic = -o/2 (m3, m4, m5), dopacity = m0
+        const int kk = lane;
+        float4 p0 = s_part[kk][0][0], p1 = s_part[kk][0][1], p2 = s_part[kk][0][2];
+#pragma unroll
+        for (int r = 1; r < 4; ++r) {
+          const float4 x0 = s_part[kk][r][0], x1 = s_part[kk][r][1], x2 = s_part[kk][r][2];
+          p0.x += x0.x; p0.y += x0.y; p0.z += x0.z; p0.w += x0.w;
+          p1.x += x1.x; p1.y += x1.y; p1.z += x1.z; p1.w += x1.w;
+          p2.x += x2.x; p2.y += x2.y;
+        }
+        const float4 a = s0[sub + kk];
+        const float4 b = s1[sub + kk];
+        const float o = b.y;
+        const float dmx = -o * ddelx_dx * (a.z * p0.y + a.w * p0.z);
+        const float dmy = -o * ddely_dy * (b.x * p0.z + a.w * p0.y);
+        const size_t d = 3 * (size_t)s_dest[sub + kk];
+        grow[d] = make_float4(dmx, dmy, -0.5f * o * p0.w, -0.5f * o * p1.x);
+        grow[d + 1] = make_float4(-0.5f * o * p1.y, p0.x, p1.z, p1.w);
+        grow[d + 2] = make_float4(p2.x, p2.y, 0.f, 0.f);
       }
       __syncthreads();
     }
