@@ -16,10 +16,11 @@
 
 namespace gsr {
 
-__global__ __launch_bounds__(256) void k_gauss_bwd(GaussBackwardArgs a, int grid_x, GeomState g,
-                                                   const uint4* __restrict__ tile_info, BackwardState bw) {
-  const int idx = blockIdx.x * blockDim.x + threadIdx.x;
-  if (idx >= a.P) return;
+// One Gaussian.  sh_l / dsh_l point at this Gaussian's SH block and dL/dSH block in LDS (the kernel
+// stages them with coalesced global accesses); both may be null without SHs.
+__device__ __forceinline__ void gauss_bwd_one(const GaussBackwardArgs& a, int idx, int grid_x, const GeomState& g,
+                                              const uint4* __restrict__ tile_info, const BackwardState& bw,
+                                              const float* sh_l, float* dsh_l) {
   const int Mc = a.M;
   const bool visible = a.radii[idx] > 0;
 
@@ -64,7 +65,7 @@ __global__ __launch_bounds__(256) void k_gauss_bwd(GaussBackwardArgs a, int grid
     if (a.dL_dcov3D)
       for (int k = 0; k < 6; ++k) a.dL_dcov3D[6 * idx + k] = 0.f;
     if (a.dL_dsh)
-      for (int k = 0; k < 3 * Mc; ++k) a.dL_dsh[(size_t)3 * Mc * idx + k] = 0.f;
+      for (int k = 0; k < 3 * Mc; ++k) dsh_l[k] = 0.f;
     if (a.dL_dscales)
       for (int k = 0; k < 3; ++k) a.dL_dscales[3 * idx + k] = 0.f;
     if (a.dL_drotations)
@@ -153,8 +154,8 @@ __global__ __launch_bounds__(256) void k_gauss_bwd(GaussBackwardArgs a, int grid
 
   // ---- SH backward -------------------------------------------------------------------
   if (a.shs) {
-    const float* sh = a.shs + (size_t)idx * Mc * 3;
-    float* dsh = a.dL_dsh + (size_t)idx * Mc * 3;
+    const float* sh = sh_l;
+    float* dsh = dsh_l;
     const uint32_t cl = g.clamped[idx];
     const float3 dRGB = make_float3((cl & 1u) ? 0.f : dcr, (cl & 2u) ? 0.f : dcg, (cl & 4u) ? 0.f : dcbl);
     const float3 dir_orig = make_float3(mean.x - a.campos[0], mean.y - a.campos[1], mean.z - a.campos[2]);
@@ -203,6 +204,16 @@ __global__ __launch_bounds__(256) void k_gauss_bwd(GaussBackwardArgs a, int grid
     float3 dRGBdx = make_float3(0.f, 0.f, 0.f), dRGBdy = dRGBdx, dRGBdz = dRGBdx;
     const int ncoef = (deg + 1) * (deg + 1);
 #pragma unroll
+    for (int k = 1; k < 16; ++k) {
+      if (k < ncoef) {
+        const float3 s = make_float3(sh[3 * k], sh[3 * k + 1], sh[3 * k + 2]);
+        dRGBdx.x += bdx[k] * s.x; dRGBdx.y += bdx[k] * s.y; dRGBdx.z += bdx[k] * s.z;
+        dRGBdy.x += bdy[k] * s.x; dRGBdy.y += bdy[k] * s.y; dRGBdy.z += bdy[k] * s.z;
+        dRGBdz.x += bdz[k] * s.x; dRGBdz.y += bdz[k] * s.y; dRGBdz.z += bdz[k] * s.z;
+      }
+    }
+    // dL/dSH last: it overwrites the SH row in LDS (same row) that the loop above reads
+#pragma unroll
     for (int k = 0; k < 16; ++k) {
       if (k < Mc) {
         const float bk = k < ncoef ? basis[k] : 0.f;
@@ -212,15 +223,6 @@ __global__ __launch_bounds__(256) void k_gauss_bwd(GaussBackwardArgs a, int grid
       }
     }
     for (int k = 16; k < Mc; ++k) dsh[3 * k] = dsh[3 * k + 1] = dsh[3 * k + 2] = 0.f;
-#pragma unroll
-    for (int k = 1; k < 16; ++k) {
-      if (k < ncoef) {
-        const float3 s = make_float3(sh[3 * k], sh[3 * k + 1], sh[3 * k + 2]);
-        dRGBdx.x += bdx[k] * s.x; dRGBdx.y += bdx[k] * s.y; dRGBdx.z += bdx[k] * s.z;
-        dRGBdy.x += bdy[k] * s.x; dRGBdy.y += bdy[k] * s.y; dRGBdy.z += bdy[k] * s.z;
-        dRGBdz.x += bdz[k] * s.x; dRGBdz.y += bdz[k] * s.y; dRGBdz.z += bdz[k] * s.z;
-      }
-    }
     const float3 ddir = make_float3(dRGBdx.x * dRGB.x + dRGBdx.y * dRGB.y + dRGBdx.z * dRGB.z,
                                     dRGBdy.x * dRGB.x + dRGBdy.y * dRGB.y + dRGBdy.z * dRGB.z,
                                     dRGBdz.x * dRGB.x + dRGBdz.y * dRGB.y + dRGBdz.z * dRGB.z);
@@ -282,11 +284,53 @@ __global__ __launch_bounds__(256) void k_gauss_bwd(GaussBackwardArgs a, int grid
   }
 }
 
+// LDS row stride (floats) of one Gaussian's 3M SH values: 16-byte multiple plus 16 bytes of padding so
+// per-thread ds_read_b128 / ds_write_b128 at this stride are bank-conflict free.
+static inline __host__ __device__ int sh_lds_stride(int M) { return ((3 * M + 3) & ~3) + 4; }
+
+// 256 Gaussians per block.  The block's SH rows (P x M x 3 floats, contiguous) are loaded into LDS with
+// fully coalesced 4-byte loads, each thread computes its Gaussian reading its row from LDS and writes its
+// dL/dSH row back into the same LDS row, and the block stores the rows with coalesced stores.  Direct
+// per-thread 192-byte row accesses (stride 192 B across lanes) left 2/3 of the wave time waiting on memory.
+__global__ __launch_bounds__(256) void k_gauss_bwd(GaussBackwardArgs a, int grid_x, GeomState g,
+                                                   const uint4* __restrict__ tile_info, BackwardState bw) {
+  extern __shared__ __attribute__((aligned(16))) float s_sh[];
+  const int t = threadIdx.x;
+  const int block0 = blockIdx.x * 256;
+  const int idx = block0 + t;
+  const int nblk = min(256, a.P - block0);
+  const int F = 3 * a.M;
+  const int S = sh_lds_stride(a.M);
+  const bool has_sh = a.shs != nullptr && F > 0;
+  const float invF = has_sh ? 1.0f / (float)F : 0.0f;
+  if (has_sh) {
+    const float* src = a.shs + (size_t)block0 * F;
+    const int cnt = nblk * F;
+    for (int e = t; e < cnt; e += 256) {
+      const int te = (int)(((float)e + 0.5f) * invF);
+      s_sh[te * S + (e - te * F)] = src[e];
+    }
+    __syncthreads();
+  }
+  if (idx < a.P) gauss_bwd_one(a, idx, grid_x, g, tile_info, bw, has_sh ? s_sh + t * S : nullptr,
+                               has_sh ? s_sh + t * S : nullptr);
+  if (has_sh) {
+    __syncthreads();
+    float* dst = a.dL_dsh + (size_t)block0 * F;
+    const int cnt = nblk * F;
+    for (int e = t; e < cnt; e += 256) {
+      const int te = (int)(((float)e + 0.5f) * invF);
+      dst[e] = s_sh[te * S + (e - te * F)];
+    }
+  }
+}
+
 void launch_gauss_backward(const GaussBackwardArgs& a, int W, int H, const GeomState& g,
                            const ImageState& img, const BackwardState& bw, hipStream_t stream) {
   (void)H;
   if (a.P <= 0) return;
-  hipLaunchKernelGGL(k_gauss_bwd, dim3((a.P + 255) / 256), dim3(256), 0, stream, a,
+  const size_t lds = (a.shs && a.M > 0) ? (size_t)256 * sh_lds_stride(a.M) * sizeof(float) : 0;
+  hipLaunchKernelGGL(k_gauss_bwd, dim3((a.P + 255) / 256), dim3(256), lds, stream, a,
                      div_up(W, GSR_TILE_X), g, (const uint4*)img.tile_info, bw);
 }
 
