@@ -118,6 +118,33 @@ int gsr_backward(int P, int degree, int M, int K, int width, int height, const f
                  void* work, void* stream);
 
 /*
+ * View-batched path: one set of Gaussians rendered from V cameras.
+ * gsr_forward_preprocess / gsr_forward_render stay per view; these three replace the per-view K
+ * readback (V syncs -> 1) and split the backward so the per-Gaussian chain rule runs once per batch:
+ * shared-parameter gradients (means3D, opacity, SH, scales, rotations, cov3D, colors) are summed over
+ * the V views inside the kernel, the parameters and SH rows are read once per 16 views.
+ * Per-view arguments are HOST arrays of V values / device pointers.
+ */
+int gsr_num_rendered_many(int n_views, const void* const* geoms, int P, int* num_rendered, void* stream);
+/* Backward tile blend of one view: writes that view's per-instance gradient rows into `work`. */
+int gsr_backward_render(int P, int K, int width, int height, const float* bg, const void* geom,
+                        const void* binning, const void* image, const float* dL_dcolor,
+                        const float* dL_ddepth, const float* dL_dalpha, void* work, void* stream);
+/* Per-Gaussian backward over the V views whose rows gsr_backward_render produced.  dL_dmeans2D is
+ * per view ((P,3) each); the other gradients are summed over views, and added to the existing
+ * contents when accumulate != 0.  dL_dcolors / dL_dcov3D may be NULL. */
+int gsr_backward_gaussians_many(int n_views, int P, int degree, int M, const int* widths, const int* heights,
+                                const float* tanfovx, const float* tanfovy, const float* const* viewmatrices,
+                                const float* const* projmatrices, const float* const* campos,
+                                const int* const* radii, const void* const* geoms, const void* const* images,
+                                const void* const* works, const int* Ks, const float* means3D,
+                                const float* scales, float scale_modifier, const float* rotations,
+                                const float* shs, const float* cov3D_precomp, float* const* dL_dmeans2D,
+                                float* dL_dcolors, float* dL_dopacity, float* dL_dmeans3D, float* dL_dcov3D,
+                                float* dL_dsh, float* dL_dscales, float* dL_drotations, int accumulate,
+                                void* stream);
+
+/*
  * Optional phase timing with HIP events recorded on the launch stream around each phase's kernels.
  * Off by default; while on, every call above records one event pair per phase it runs.
  * gsr_profile_read synchronises the recorded events and returns, per phase, the accumulated

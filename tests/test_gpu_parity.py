@@ -158,3 +158,64 @@ def test_mark_visible():
     p = scene["means3D"]
     z = v[2] * p[:, 0] + v[6] * p[:, 1] + v[10] * p[:, 2] + v[14]
     assert np.array_equal(vis, z > 0.2)
+
+
+def _settings(cam, bg, deg, dev="cuda", mod=1.0):
+    import torch
+
+    from diff_gaussian_rasterization import GaussianRasterizationSettings
+
+    return GaussianRasterizationSettings(cam["H"], cam["W"], cam["tanx"], cam["tany"],
+                                         torch.tensor(bg, device=dev, dtype=torch.float32), mod,
+                                         torch.tensor(cam["view"], device=dev), torch.tensor(cam["proj"], device=dev),
+                                         deg, torch.tensor(cam["campos"], device=dev), False, False)
+
+
+@pytest.mark.parametrize("nviews", [1, 5, 19])
+def test_batched_views_match_per_view(nviews):
+    """rasterize_views (one autograd node, fused multi-view per-Gaussian backward) == per-view calls."""
+    import torch
+
+    from diff_gaussian_rasterization import GaussianRasterizer
+    from diff_gaussian_rasterization.batched import rasterize_views
+
+    scene = gs.make_scene(15_000, sh_degree=3, seed=31)
+    cams = [make_camera(160, 128, elevation=10.0 * (i % 3), azimuth=360.0 * i / nviews) for i in range(nviews)]
+    bg = [0.1, 0.2, 0.3]
+    ups = [gs.upstream_grads(128, 160, seed=100 + i) for i in range(nviews)]
+    dev = "cuda"
+    keys = ("means3D", "scales", "rotations", "opacities", "shs")
+
+    def leaves():
+        return {k: torch.tensor(scene[k], device=dev, requires_grad=True) for k in keys}
+
+    # per view
+    t = leaves()
+    per, m2_per = [], []
+    for i, cam in enumerate(cams):
+        m2 = torch.zeros((15_000, 3), device=dev, requires_grad=True)
+        c, r, d, a = GaussianRasterizer(_settings(cam, bg, 3))(means3D=t["means3D"], means2D=m2, opacities=t["opacities"],
+                                                               shs=t["shs"], scales=t["scales"], rotations=t["rotations"])
+        gc, gd, ga = (torch.tensor(x, device=dev) for x in ups[i])
+        ((c * gc).sum() + (d * gd).sum() + (a * ga).sum()).backward()
+        per.append((c.detach(), r, d.detach(), a.detach()))
+        m2_per.append(m2.grad.clone())
+    g_per = {k: v.grad.clone() for k, v in t.items()}
+    # batched
+    t = leaves()
+    m2s = [torch.zeros((15_000, 3), device=dev, requires_grad=True) for _ in cams]
+    c, r, d, a = rasterize_views([_settings(cam, bg, 3) for cam in cams], t["means3D"], m2s, t["opacities"],
+                                 shs=t["shs"], scales=t["scales"], rotations=t["rotations"])
+    gc = torch.stack([torch.tensor(u[0], device=dev) for u in ups])
+    gd = torch.stack([torch.tensor(u[1], device=dev) for u in ups])
+    ga = torch.stack([torch.tensor(u[2], device=dev) for u in ups])
+    ((c * gc).sum() + (d * gd).sum() + (a * ga).sum()).backward()
+    for i in range(nviews):
+        assert torch.equal(c[i], per[i][0]) and torch.equal(r[i], per[i][1])
+        assert torch.equal(d[i], per[i][2]) and torch.equal(a[i], per[i][3])
+        torch.testing.assert_close(m2s[i].grad, m2_per[i], rtol=0, atol=0)
+    for k, v in t.items():
+        ref = g_per[k]
+        scale = max(1.0, float(ref.abs().max()))
+        err = float((v.grad - ref).abs().max())
+        assert err <= 1e-5 * scale, f"{k}: {err} vs scale {scale}"

@@ -108,6 +108,31 @@ static int tile_sort_result(int W, int H) {
   return passes & 1;
 }
 
+static GaussBackwardArgs shared_args(int P, int degree, int M, const float* means3D, const float* scales,
+                                     float scale_modifier, const float* rotations, const float* shs,
+                                     const float* cov3D_precomp, float* dL_dcolors, float* dL_dopacity,
+                                     float* dL_dmeans3D, float* dL_dcov3D, float* dL_dsh, float* dL_dscales,
+                                     float* dL_drotations) {
+  GaussBackwardArgs a;
+  a.P = P;
+  a.deg = effective_degree(degree, M);
+  a.M = shs ? M : 0;
+  a.means3D = means3D;
+  a.scales = scales;
+  a.rotations = rotations;
+  a.shs = shs;
+  a.cov3D_precomp = cov3D_precomp;
+  a.scale_modifier = scale_modifier;
+  a.dL_dcolors = dL_dcolors;
+  a.dL_dopacity = dL_dopacity;
+  a.dL_dmeans3D = dL_dmeans3D;
+  a.dL_dcov3D = dL_dcov3D;
+  a.dL_dsh = shs ? dL_dsh : nullptr;
+  a.dL_dscales = cov3D_precomp ? nullptr : dL_dscales;
+  a.dL_drotations = cov3D_precomp ? nullptr : dL_drotations;
+  return a;
+}
+
 extern "C" {
 
 const char* gsr_version(void) { return "gsr 0.1.0 gfx950"; }
@@ -276,35 +301,108 @@ int gsr_backward(int P, int degree, int M, int K, int width, int height, const f
                            dL_ddepth, dL_dalpha, bw, s);
   }
 
-  GaussBackwardArgs a;
-  a.P = P;
-  a.deg = effective_degree(degree, M);
-  a.M = shs ? M : 0;
-  a.means3D = means3D;
-  a.scales = scales;
-  a.rotations = rotations;
-  a.shs = shs;
-  a.cov3D_precomp = cov3D_precomp;
-  a.scale_modifier = scale_modifier;
-  a.viewmatrix = viewmatrix;
-  a.projmatrix = projmatrix;
-  a.campos = campos;
-  a.tanfovx = tanfovx;
-  a.tanfovy = tanfovy;
-  a.focal_y = height / (2.0f * tanfovy);
-  a.focal_x = width / (2.0f * tanfovx);
-  a.radii = radii;
-  a.dL_dmeans2D = dL_dmeans2D;
-  a.dL_dcolors = dL_dcolors;
-  a.dL_dopacity = dL_dopacity;
-  a.dL_dmeans3D = dL_dmeans3D;
-  a.dL_dcov3D = dL_dcov3D;
-  a.dL_dsh = shs ? dL_dsh : nullptr;
-  a.dL_dscales = cov3D_precomp ? nullptr : dL_dscales;
-  a.dL_drotations = cov3D_precomp ? nullptr : dL_drotations;
+  GaussBackwardArgs a = shared_args(P, degree, M, means3D, scales, scale_modifier, rotations, shs, cov3D_precomp,
+                                     dL_dcolors, dL_dopacity, dL_dmeans3D, dL_dcov3D, dL_dsh, dL_dscales,
+                                     dL_drotations);
+  ViewBatch vb;
+  vb.n = 1;
+  vb.accumulate = 0;
+  vb.v[0] = make_view_desc(viewmatrix, projmatrix, campos, radii, g, img, bw, dL_dmeans2D, width, height,
+                           tanfovx, tanfovy);
   {
     PhaseScope ps(GSR_PHASE_GAUSS_BWD, s);
-    launch_gauss_backward(a, width, height, g, img, bw, s);
+    launch_gauss_backward_views(a, vb, s);
+  }
+  return last_launch();
+}
+
+// ---- view-batched path ---------------------------------------------------------------------
+
+int gsr_num_rendered_many(int n_views, const void* const* geoms, int P, int* num_rendered, void* stream) {
+  if (n_views < 0 || (n_views > 0 && (geoms == nullptr || num_rendered == nullptr)))
+    return fail(GSR_EINVAL, "%s", "null pointer argument");
+  hipStream_t s = (hipStream_t)stream;
+  static thread_local uint32_t* pinned = nullptr;
+  static thread_local int pinned_n = 0;
+  if (pinned_n < n_views) {
+    if (pinned) (void)hipHostFree(pinned);
+    pinned = nullptr;
+    GSR_HIP_CHECK(hipHostMalloc((void**)&pinned, sizeof(uint32_t) * (size_t)n_views, hipHostMallocDefault));
+    pinned_n = n_views;
+  }
+  for (int v = 0; v < n_views; ++v) {
+    if (geoms[v] == nullptr) return fail(GSR_EINVAL, "%s", "null geom buffer");
+    GeomState g = GeomState::carve((void*)geoms[v], P, nullptr);
+    GSR_HIP_CHECK(hipMemcpyAsync(pinned + v, g.counters + 1, sizeof(uint32_t), hipMemcpyDeviceToHost, s));
+  }
+  GSR_HIP_CHECK(hipStreamSynchronize(s));
+  for (int v = 0; v < n_views; ++v) num_rendered[v] = (int)pinned[v];
+  g_err[0] = 0;
+  return GSR_OK;
+}
+
+int gsr_backward_render(int P, int K, int width, int height, const float* bg, const void* geom,
+                        const void* binning, const void* image, const float* dL_dcolor,
+                        const float* dL_ddepth, const float* dL_dalpha, void* work, void* stream) {
+  if (P < 0 || K < 0 || width <= 0 || height <= 0) return fail(GSR_EINVAL, "%s", "bad sizes");
+  if (geom == nullptr || binning == nullptr || image == nullptr || work == nullptr || bg == nullptr ||
+      dL_dcolor == nullptr)
+    return fail(GSR_EINVAL, "%s", "null pointer argument");
+  hipStream_t s = (hipStream_t)stream;
+  GeomState g = GeomState::carve((void*)geom, P, nullptr);
+  BinningState b = BinningState::carve((void*)binning, K, nullptr);
+  ImageState img = ImageState::carve((void*)image, width, height, nullptr);
+  BackwardState bw = BackwardState::carve(work, K, nullptr);
+  {
+    PhaseScope ps(GSR_PHASE_RENDER_BWD, s);
+    launch_render_backward(width, height, K, g, b.val[tile_sort_result(width, height)], img, bg, dL_dcolor,
+                           dL_ddepth, dL_dalpha, bw, s);
+  }
+  return last_launch();
+}
+
+int gsr_backward_gaussians_many(int n_views, int P, int degree, int M, const int* widths, const int* heights,
+                                const float* tanfovx, const float* tanfovy, const float* const* viewmatrices,
+                                const float* const* projmatrices, const float* const* campos,
+                                const int* const* radii, const void* const* geoms, const void* const* images,
+                                const void* const* works, const int* Ks, const float* means3D,
+                                const float* scales, float scale_modifier, const float* rotations,
+                                const float* shs, const float* cov3D_precomp, float* const* dL_dmeans2D,
+                                float* dL_dcolors, float* dL_dopacity, float* dL_dmeans3D, float* dL_dcov3D,
+                                float* dL_dsh, float* dL_dscales, float* dL_drotations, int accumulate,
+                                void* stream) {
+  if (n_views < 0 || P < 0) return fail(GSR_EINVAL, "%s", "bad sizes");
+  if (P == 0 || n_views == 0) return last_launch();
+  if (widths == nullptr || heights == nullptr || tanfovx == nullptr || tanfovy == nullptr ||
+      viewmatrices == nullptr || projmatrices == nullptr || campos == nullptr || radii == nullptr ||
+      geoms == nullptr || images == nullptr || works == nullptr || Ks == nullptr || dL_dmeans2D == nullptr ||
+      means3D == nullptr || dL_dopacity == nullptr || dL_dmeans3D == nullptr)
+    return fail(GSR_EINVAL, "%s", "null pointer argument");
+  if (shs != nullptr && dL_dsh == nullptr) return fail(GSR_EINVAL, "%s", "dL_dsh required with SHs");
+  if (cov3D_precomp == nullptr && (scales == nullptr || rotations == nullptr || dL_dscales == nullptr ||
+                                   dL_drotations == nullptr))
+    return fail(GSR_EINVAL, "%s", "scales/rotations and their gradients required");
+  hipStream_t s = (hipStream_t)stream;
+  GaussBackwardArgs a = shared_args(P, degree, M, means3D, scales, scale_modifier, rotations, shs, cov3D_precomp,
+                                     dL_dcolors, dL_dopacity, dL_dmeans3D, dL_dcov3D, dL_dsh, dL_dscales,
+                                     dL_drotations);
+  for (int v0 = 0; v0 < n_views; v0 += GSR_VIEWS_PER_LAUNCH) {
+    ViewBatch vb;
+    vb.n = n_views - v0 < GSR_VIEWS_PER_LAUNCH ? n_views - v0 : GSR_VIEWS_PER_LAUNCH;
+    vb.accumulate = (accumulate || v0 > 0) ? 1 : 0;
+    for (int j = 0; j < vb.n; ++j) {
+      const int v = v0 + j;
+      if (widths[v] <= 0 || heights[v] <= 0 || Ks[v] < 0) return fail(GSR_EINVAL, "%s", "bad view sizes");
+      if (geoms[v] == nullptr || images[v] == nullptr || works[v] == nullptr || dL_dmeans2D[v] == nullptr)
+        return fail(GSR_EINVAL, "%s", "null per-view buffer");
+      GeomState g = GeomState::carve((void*)geoms[v], P, nullptr);
+      ImageState img = ImageState::carve((void*)images[v], widths[v], heights[v], nullptr);
+      BackwardState bw = BackwardState::carve((void*)works[v], Ks[v], nullptr);
+      vb.v[j] = make_view_desc(viewmatrices[v], projmatrices[v], campos[v], radii[v], g, img, bw, dL_dmeans2D[v],
+                               widths[v], heights[v], tanfovx[v], tanfovy[v]);
+    }
+    PhaseScope ps(GSR_PHASE_GAUSS_BWD, s);
+    launch_gauss_backward_views(a, vb, s);
   }
   return last_launch();
 }

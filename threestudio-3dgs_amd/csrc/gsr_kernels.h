@@ -52,18 +52,33 @@ void launch_render_backward(int W, int H, int K, const GeomState& g, const uint3
                             const float* dL_ddepth, const float* dL_dalpha,
                             const BackwardState& bw, hipStream_t stream);
 
-// Fused per-Gaussian backward — gsr_backward.hip
-struct GaussBackwardArgs {
+// Fused per-Gaussian backward over a batch of views — gsr_backward.hip
+struct GaussBackwardArgs {  // shared Gaussian parameters and the gradients of them (summed over views)
   int P, deg, M;
   const float *means3D, *scales, *rotations, *shs, *cov3D_precomp;
   float scale_modifier;
-  const float *viewmatrix, *projmatrix, *campos;
-  float tanfovx, tanfovy, focal_x, focal_y;
-  const int* radii;
-  float *dL_dmeans2D, *dL_dcolors, *dL_dopacity, *dL_dmeans3D, *dL_dcov3D, *dL_dsh, *dL_dscales,
-      *dL_drotations;
+  float *dL_dcolors, *dL_dopacity, *dL_dmeans3D, *dL_dcov3D, *dL_dsh, *dL_dscales, *dL_drotations;
 };
-void launch_gauss_backward(const GaussBackwardArgs& a, int W, int H, const GeomState& g,
-                           const ImageState& img, const BackwardState& bw, hipStream_t stream);
+struct ViewDesc {  // one view's camera, forward state, gradient rows and its means2D gradient output
+  const float *view, *proj, *campos;
+  const int* radii;
+  const float4* rec1;
+  const uint2* rect;
+  const uint32_t *goff, *clamped;
+  const uint4* tile_info;
+  const float4* grow;
+  float* dmeans2D;
+  float tanx, tany, fx, fy;
+  int grid_x, pad_;
+};
+#define GSR_VIEWS_PER_LAUNCH 16
+struct ViewBatch {  // passed by value as kernel arguments (16 x 112 B)
+  int n, accumulate;
+  ViewDesc v[GSR_VIEWS_PER_LAUNCH];
+};
+ViewDesc make_view_desc(const float* view, const float* proj, const float* campos, const int* radii,
+                        const GeomState& g, const ImageState& img, const BackwardState& bw,
+                        float* dmeans2D, int W, int H, float tanx, float tany);
+void launch_gauss_backward_views(const GaussBackwardArgs& a, const ViewBatch& vb, hipStream_t stream);
 
 }  // namespace gsr

@@ -50,6 +50,14 @@ SIGNATURES = {
          _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp],
     ),
     "gsr_mark_visible": (_i, [_i, _vp, _vp, _vp, _vp, _vp]),
+    "gsr_num_rendered_many": (_i, [_i, ctypes.POINTER(_vp), _i, ctypes.POINTER(_i), _vp]),
+    "gsr_backward_render": (_i, [_i, _i, _i, _i, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
+    "gsr_backward_gaussians_many": (
+        _i,
+        [_i, _i, _i, _i, ctypes.POINTER(_i), ctypes.POINTER(_i), ctypes.POINTER(_f), ctypes.POINTER(_f)]
+        + [ctypes.POINTER(_vp)] * 7 + [ctypes.POINTER(_i), _vp, _vp, _f, _vp, _vp, _vp, ctypes.POINTER(_vp)]
+        + [_vp] * 7 + [_i, _vp],
+    ),
     "gsr_profile_enable": (_i, [_i]),
     "gsr_profile_read": (_i, [ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_longlong), _i]),
 }
