@@ -50,6 +50,12 @@ def parse():
     ap.add_argument("--cpu-views", type=int, default=3, help="views of the same workload timed on the CPU oracle")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-profile", action="store_true")
+    ap.add_argument("--path", choices=["batched", "per-view"], default="batched",
+                    help="batched: rasterize_views (one autograd node per rank's views); per-view: one "
+                         "GaussianRasterizer call per view, exactly as the reference renderer loop does")
+    ap.add_argument("--streams", type=int, default=4, help="HIP streams the batched path deals views over")
+    ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "r01_traffic.json"),
+                    help="PMC summary (profiles/summarize.py) supplying roofline.traffic")
     return ap.parse_args()
 
 
@@ -109,6 +115,39 @@ def render_view(rep: Replica, cam, bg_zero, bg_const):
     return comp, depth, alpha, radii
 
 
+def settings_for(rep: Replica, cam, bg_zero):
+    from diff_gaussian_rasterization import GaussianRasterizationSettings
+
+    return GaussianRasterizationSettings(image_height=cam["H"], image_width=cam["W"], tanfovx=cam["tan"],
+                                         tanfovy=cam["tan"], bg=bg_zero, scale_modifier=1.0,
+                                         viewmatrix=cam["view"], projmatrix=cam["proj"], sh_degree=rep.sh_degree,
+                                         campos=cam["campos"], prefiltered=False, debug=False)
+
+
+def render_views(rep: Replica, settings, bg_const):
+    """The rank's views through rasterize_views; one means2D placeholder per view, as the renderer loop
+    creates (renderer/diff_gaussian_rasterizer.py:73-81)."""
+    from diff_gaussian_rasterization.batched import rasterize_views
+
+    P = rep.means3D.shape[0]
+    m2 = [torch.zeros((P, 3), device=rep.means3D.device, requires_grad=True) for _ in settings]
+    color, radii, depth, alpha = rasterize_views(settings, rep.means3D, m2, rep.opacities, shs=rep.shs,
+                                                 scales=rep.scales, rotations=rep.rotations)
+    comp = color + (1 - alpha) * bg_const[None, :, None, None]
+    return comp, depth, alpha, radii
+
+
+def read_traffic(path, kernel):
+    """HBM bytes per launch of `kernel` from a committed PMC summary (FETCH_SIZE x2 gfx950 correction +
+    WRITE_SIZE, separate --pmc passes; profiles/summarize.py), or None."""
+    try:
+        with open(path) as f:
+            t = json.load(f)
+        return float(t["per_launch_bytes"][kernel])
+    except (OSError, KeyError, ValueError, TypeError):
+        return None
+
+
 def cpu_baseline(scene, res, n_views):
     """The CPU restatement (oracle, fp32, single thread) on `n_views` views of the same workload."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
@@ -152,7 +191,10 @@ def main():
 
     import gsr_synthetic as gs
     from diff_gaussian_rasterization import _C
+    from diff_gaussian_rasterization import batched
     from diff_gaussian_rasterization.view_shard import all_gather_views, allreduce_grads, shard_range
+
+    batched.N_STREAMS = args.streams
 
     t_setup = time.perf_counter()
     scene = gs.make_scene(args.gaussians, sh_degree=args.sh_degree, seed=0)  # identical replica on every rank
@@ -170,12 +212,24 @@ def main():
     bg_const = torch.tensor([0.5, 0.5, 0.5], device=device)
     log(f"[bench] rank {rank}/{world}: setup {time.perf_counter() - t_setup:.1f}s, {len(mine)} views/rank")
 
+    settings = [settings_for(rep, cam, bg_zero) for cam in mine]
+    up_c = torch.stack([u[0] for u in upstream]) if upstream else None
+    up_d = torch.stack([u[1] for u in upstream]) if upstream else None
+    up_a = torch.stack([u[2] for u in upstream]) if upstream else None
+
     def step():
-        outs = [render_view(rep, cam, bg_zero, bg_const) for cam in mine]
-        if world > 1:
-            # forward exchange: every rank receives the whole batch of rendered images
-            all_gather_views(torch.stack([torch.cat([c, d, a], 0) for c, d, a, _ in outs]), args.views)
-        loss = sum((c * g[0]).sum() + (d * g[1]).sum() + (a * g[2]).sum() for (c, d, a, _), g in zip(outs, upstream))
+        if args.path == "batched":
+            c, d, a, _ = render_views(rep, settings, bg_const)
+            if world > 1:
+                # forward exchange: every rank receives the whole batch of rendered images
+                all_gather_views(torch.cat([c, d, a], 1), args.views)
+            loss = (c * up_c).sum() + (d * up_d).sum() + (a * up_a).sum()
+        else:
+            outs = [render_view(rep, cam, bg_zero, bg_const) for cam in mine]
+            if world > 1:
+                all_gather_views(torch.stack([torch.cat([c, d, a], 0) for c, d, a, _ in outs]), args.views)
+            loss = sum((c * g[0]).sum() + (d * g[1]).sum() + (a * g[2]).sum()
+                       for (c, d, a, _), g in zip(outs, upstream))
         loss.backward()
         allreduce_grads(rep.params)  # one flat RCCL all-reduce of the Gaussian parameter gradients
         rep.zero_grad()
@@ -236,6 +290,8 @@ def main():
             "global_views_per_step": args.views, "views_per_rank": per,
             "parallelism": f"views sharded over {world} rank(s) (RCCL all-gather images, all-reduce grads)",
             "mean_instances_K": round(K_mean),
+            "path": args.path,
+            "streams": args.streams if args.path == "batched" else 1,
         },
     }
     if phases is not None:
@@ -252,14 +308,18 @@ def main():
         bwd_gbs = bytes_bwd / (b_ms / max(1, b_n) * 1e-3) / 1e9 if b_n else 0.0
         dominant = max(phases.items(), key=lambda kv: kv[1][0])[0]
         roof_fwd = {"kernel": "k_render_fwd", "bound": "hbm", "achieved": round(fwd_gbs, 1), "peak": HBM_PEAK_GBS,
-                    "unit": "GB/s", "frac": round(fwd_gbs / HBM_PEAK_GBS, 4), "traffic": None,
+                    "unit": "GB/s", "frac": round(fwd_gbs / HBM_PEAK_GBS, 4),
+                    "traffic": read_traffic(args.traffic, "k_render_fwd"),
                     "avg_launch_us": round(1000 * f_ms / max(1, f_n), 2), "algorithmic_bytes": round(bytes_fwd)}
         roof_bwd = {"kernel": "k_render_bwd", "bound": "hbm", "achieved": round(bwd_gbs, 1), "peak": HBM_PEAK_GBS,
-                    "unit": "GB/s", "frac": round(bwd_gbs / HBM_PEAK_GBS, 4), "traffic": None,
+                    "unit": "GB/s", "frac": round(bwd_gbs / HBM_PEAK_GBS, 4),
+                    "traffic": read_traffic(args.traffic, "k_render_bwd"),
                     "avg_launch_us": round(1000 * b_ms / max(1, b_n), 2), "algorithmic_bytes": round(bytes_bwd)}
         res["roofline"] = roof_bwd if dominant == "render_bwd" else roof_fwd
         res["roofline_fwd_blend"] = roof_fwd
         res["dominant_kernel"] = dominant
+        res["traffic_source"] = os.path.relpath(args.traffic, ROOT) + " (HBM bytes/launch, rocprofv3 --pmc " \
+                                "FETCH_SIZE x2 + WRITE_SIZE, 8-view capture of this workload)"
     if world == 1 and not args.no_cpu_baseline:
         cb = cpu_baseline(scene, args.res, args.cpu_views)
         res["cpu_baseline"] = {k: (round(v, 5) if isinstance(v, float) else v) for k, v in cb.items()}

@@ -1,0 +1,86 @@
+"""Per-block timelines of the blend kernels (diagnostic build, `make -C threestudio-3dgs_amd/csrc diag`).
+
+Renders views of the benchmark workload through libgsr_hip_diag.so and summarises, per kernel:
+span, block-duration percentiles, the longest blocks and their work (fwd: last contributor;
+bwd: kept instances), per-XCD finish time, and the occupancy profile over time (how much of the
+span runs with few blocks resident = tail).  Usage (GPU box):  python profiles/diag_timeline.py
+"""
+import ctypes
+import json
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+os.environ["GSR_HIP_LIB"] = os.path.join(ROOT, "threestudio-3dgs_amd", "csrc", "build_diag", "libgsr_hip_diag.so")
+sys.path.insert(0, os.path.join(ROOT, "threestudio-3dgs_amd"))
+sys.path.insert(0, ROOT)
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+import bench  # noqa: E402
+import gsr_synthetic as gs  # noqa: E402
+from diff_gaussian_rasterization import _C  # noqa: E402
+
+
+def summarise(tl, name):
+    tl = tl[tl[:, 1] != 0]
+    t0 = int(tl[:, 0].min())
+    st = (tl[:, 0].astype(np.int64) - t0) * 10  # ns
+    en = (tl[:, 1].astype(np.int64) - t0) * 10
+    dur = en - st
+    xcc = tl[:, 3] >> 24
+    work = tl[:, 3] & 0xFFFFFF
+    span = int(en.max())
+    # occupancy over time in 100 bins
+    bins = np.linspace(0, span, 101)
+    occ = [int(((st <= b) & (en > b)).sum()) for b in bins[:-1]]
+    order = np.argsort(-dur)[:8]
+    busy = dur.sum()
+    return {
+        "kernel": name, "blocks": int(len(tl)), "span_us": span / 1e3,
+        "block_us_p50_p90_p99_max": [float(np.percentile(dur, p)) / 1e3 for p in (50, 90, 99, 100)],
+        "sum_block_us": busy / 1e3, "mean_resident_blocks": busy / max(1, span),
+        "longest": [{"us": int(dur[i]) / 1e3, "work": int(work[i]), "start_us": int(st[i]) / 1e3} for i in order],
+        "work_vs_us_corr": float(np.corrcoef(work, dur)[0, 1]) if len(tl) > 2 else None,
+        "ns_per_work_unit_median": float(np.median(dur[work > 16] / work[work > 16])) if (work > 16).any() else None,
+        "xcd_finish_us": [int(en[xcc == x].max()) / 1e3 if (xcc == x).any() else None for x in range(8)],
+        "xcd_busy_us": [int(dur[xcc == x].sum()) / 1e3 for x in range(8)],
+        "occupancy_profile_10": [int(np.mean(occ[i * 10:(i + 1) * 10])) for i in range(10)],
+        "time_frac_below_512_blocks": float(np.mean(np.array(occ) < 512)),
+    }
+
+
+def main():
+    lib = _C.load_library()
+    lib.gsr_diag_timeline.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_int]
+    dev = torch.device("cuda", 0)
+    scene = gs.make_scene(1_000_000, sh_degree=3, seed=0)
+    rep = bench.Replica(scene, dev)
+    cams = bench.build_views(64, 1024, dev)
+    bg0 = torch.zeros(3, device=dev)
+    bgc = torch.tensor([0.5, 0.5, 0.5], device=dev)
+    gx = gy = 64
+    nb = 128 * ((((gx + 1) // 2) * ((gy + 1) // 2) + 7) // 8)
+    out = []
+    for vi in (0, 40):
+        for rep_i in range(2):  # second pass = warm
+            c, d, a, _ = bench.render_view(rep, cams[vi], bg0, bgc)
+            loss = (c * 0.1).sum() + (d * 0.01).sum() + a.sum()
+            loss.backward()
+            rep.zero_grad()
+        torch.cuda.synchronize()
+        res = {}
+        for which, name in ((0, "k_render_fwd"), (1, "k_render_bwd")):
+            buf = np.zeros((nb, 4), np.uint32)
+            assert lib.gsr_diag_timeline(which, buf.ctypes.data, nb) == 0
+            res[name] = summarise(buf, name)
+        out.append({"view": vi, **res})
+    os.makedirs(os.path.join(ROOT, "gpurun_out"), exist_ok=True)
+    with open(os.path.join(ROOT, "gpurun_out", "timeline.json"), "w") as f:
+        json.dump(out, f, indent=1)
+    print(json.dumps(out, indent=1))
+
+
+if __name__ == "__main__":
+    main()

@@ -95,18 +95,8 @@ static int effective_degree(int degree, int M) {
   return d;
 }
 
-static int tile_key_bits(int W, int H) {
-  const int tiles = div_up(W, GSR_TILE_X) * div_up(H, GSR_TILE_Y);
-  int bits = 0;
-  while ((1 << bits) < tiles) ++bits;
-  return bits < 1 ? 1 : bits;
-}
-
 // ping-pong buffer holding the tile sort's result (one radix pass per <= 8 key bits)
-static int tile_sort_result(int W, int H) {
-  const int passes = (tile_key_bits(W, H) + GSR_RADIX_BITS - 1) / GSR_RADIX_BITS;
-  return passes & 1;
-}
+static int tile_sort_result(int W, int H) { return digit_plan(tile_key_bits(W, H)).passes & 1; }
 
 static GaussBackwardArgs shared_args(int P, int degree, int M, const float* means3D, const float* scales,
                                      float scale_modifier, const float* rotations, const float* shs,
@@ -183,7 +173,8 @@ int gsr_forward_preprocess(int P, int degree, int M, const float* means3D, const
   if (shs != nullptr && M <= 0) return fail(GSR_EINVAL, "%s", "M must be >= 1 with SHs");
   hipStream_t s = (hipStream_t)stream;
   GeomState g = GeomState::carve(geom, P, nullptr);
-  GSR_HIP_CHECK(hipMemsetAsync(g.counters, 0, 16 * sizeof(uint32_t), s));
+  const DigitPlan dplan = digit_plan(32);
+  GSR_HIP_CHECK(hipMemsetAsync(g.sync, 0, g.dsort.used_bytes(g.sync, dplan.passes, dplan.bits, P), s));
   if (P == 0) return last_launch();
 
   PreprocessArgs a;
@@ -213,15 +204,12 @@ int gsr_forward_preprocess(int P, int degree, int M, const float* means3D, const
     launch_preprocess(a, g, s);
   }
   {
-    // visible compaction -> depth sort -> instance offsets in depth order
+    // visible compaction (+ depth digit counts, K) -> depth sort of the visible Gaussians
     PhaseScope ps(GSR_PHASE_DEPTH_SORT, s);
-    scan_exclusive(SCAN_FLAG, g.tiles_touched, nullptr, g.vis_off, nullptr, P, g.scan_blk,
-                   g.counters + 0, s);
     launch_compact_visible(P, g, s);
-    const int res = radix_sort_pairs(g.dkey, g.dval, false, g.counters + 0, P, 32, g.hist, g.hist_blk, s);
+    const int res = onesweep_sort(g.dkey, g.dval, false, g.counters + GSR_CTR_VISIBLE, P, 32, g.dsort,
+                                  g.counters + GSR_CTR_ERR, s);
     if (res != 0) return fail(GSR_EHIP, "%s", "internal: depth sort result buffer");
-    scan_exclusive(SCAN_GATHER, g.tiles_touched, g.dval[0], g.point_offsets, g.counters + 0, P,
-                   g.scan_blk, g.counters + 1, s);
   }
   return last_launch();
 }
@@ -229,11 +217,14 @@ int gsr_forward_preprocess(int P, int degree, int M, const float* means3D, const
 int gsr_num_rendered(const void* geom, int P, int* num_rendered, int* num_visible, void* stream) {
   if (geom == nullptr || num_rendered == nullptr) return fail(GSR_EINVAL, "%s", "null pointer argument");
   GeomState g = GeomState::carve((void*)geom, P, nullptr);
-  uint32_t h[2] = {0, 0};
+  uint32_t h[4] = {0, 0, 0, 0};
   hipStream_t s = (hipStream_t)stream;
-  GSR_HIP_CHECK(hipMemcpyAsync(h, g.counters, sizeof(h), hipMemcpyDeviceToHost, s));
-  GSR_HIP_CHECK(hipStreamSynchronize(s));
-  *num_rendered = (int)h[1];
+  if (P > 0) {
+    GSR_HIP_CHECK(hipMemcpyAsync(h, g.counters, sizeof(h), hipMemcpyDeviceToHost, s));
+    GSR_HIP_CHECK(hipStreamSynchronize(s));
+  }
+  if (h[GSR_CTR_ERR]) return fail(GSR_EHIP, "%s", "internal: look-back timeout in compaction / depth sort");
+  *num_rendered = (int)h[GSR_CTR_K];
   if (num_visible) *num_visible = (int)h[0];
   g_err[0] = 0;
   return GSR_OK;
@@ -251,14 +242,17 @@ int gsr_forward_render(int P, int K, int width, int height, const float* bg, voi
   BinningState b = BinningState::carve(binning, K, nullptr);
   ImageState img = ImageState::carve(image, width, height, nullptr);
   const int gx = div_up(width, GSR_TILE_X), gy = div_up(height, GSR_TILE_Y);
-  GSR_HIP_CHECK(hipMemsetAsync(img.ranges, 0, sizeof(uint2) * (size_t)gx * gy, s));
   if (K > 0) {
     PhaseScope ps(GSR_PHASE_BINNING, s);
-    launch_duplicate(P, gx, g.dval[0], g, b, s);
-    const int res = radix_sort_pairs(b.key, b.val, false, nullptr, K, tile_key_bits(width, height),
-                                     b.hist, b.hist_blk, s);
+    const int kbits = tile_key_bits(width, height);
+    const DigitPlan tplan = digit_plan(kbits);
+    GSR_HIP_CHECK(hipMemsetAsync(b.sync, 0, b.tsort.used_bytes(b.sync, tplan.passes, tplan.bits, K), s));
+    launch_duplicate(P, width, height, g.dval[0], g, b, img.ranges, s);
+    const int res = onesweep_sort(b.key, b.val, false, nullptr, K, kbits, b.tsort, g.counters + GSR_CTR_ERR, s);
     if (res != tile_sort_result(width, height)) return fail(GSR_EHIP, "%s", "internal: tile sort buffer");
     launch_tile_ranges(K, b.key[res], img.ranges, s);
+  } else {
+    GSR_HIP_CHECK(hipMemsetAsync(img.ranges, 0, sizeof(uint2) * (size_t)gx * gy, s));
   }
   {
     PhaseScope ps(GSR_PHASE_RENDER_FWD, s);
@@ -327,16 +321,20 @@ int gsr_num_rendered_many(int n_views, const void* const* geoms, int P, int* num
   if (pinned_n < n_views) {
     if (pinned) (void)hipHostFree(pinned);
     pinned = nullptr;
-    GSR_HIP_CHECK(hipHostMalloc((void**)&pinned, sizeof(uint32_t) * (size_t)n_views, hipHostMallocDefault));
+    GSR_HIP_CHECK(hipHostMalloc((void**)&pinned, 4 * sizeof(uint32_t) * (size_t)n_views, hipHostMallocDefault));
     pinned_n = n_views;
   }
   for (int v = 0; v < n_views; ++v) {
     if (geoms[v] == nullptr) return fail(GSR_EINVAL, "%s", "null geom buffer");
     GeomState g = GeomState::carve((void*)geoms[v], P, nullptr);
-    GSR_HIP_CHECK(hipMemcpyAsync(pinned + v, g.counters + 1, sizeof(uint32_t), hipMemcpyDeviceToHost, s));
+    if (P > 0) GSR_HIP_CHECK(hipMemcpyAsync(pinned + 4 * v, g.counters, 4 * sizeof(uint32_t), hipMemcpyDeviceToHost, s));
+    else pinned[4 * v + GSR_CTR_K] = pinned[4 * v + GSR_CTR_ERR] = 0u;
   }
   GSR_HIP_CHECK(hipStreamSynchronize(s));
-  for (int v = 0; v < n_views; ++v) num_rendered[v] = (int)pinned[v];
+  for (int v = 0; v < n_views; ++v) {
+    if (pinned[4 * v + GSR_CTR_ERR]) return fail(GSR_EHIP, "%s", "internal: look-back timeout in compaction / depth sort");
+    num_rendered[v] = (int)pinned[4 * v + GSR_CTR_K];
+  }
   g_err[0] = 0;
   return GSR_OK;
 }

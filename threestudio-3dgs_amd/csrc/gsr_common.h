@@ -10,12 +10,18 @@
 #define GSR_TILE_Y 16
 #define GSR_TILE_PIX (GSR_TILE_X * GSR_TILE_Y)  // 256 pixels = 4 waves of 64
 
-// Scans and radix passes: 256 threads x 8 items per block.
+// Radix passes: 256 threads x 8 items per block, <= 8-bit digits.
 #define GSR_SCAN_THREADS 256
 #define GSR_SCAN_ITEMS 8
 #define GSR_SCAN_TILE (GSR_SCAN_THREADS * GSR_SCAN_ITEMS)  // 2048
 #define GSR_RADIX_BITS 8
 #define GSR_RADIX (1 << GSR_RADIX_BITS)
+#define GSR_MAX_PASSES 4
+// Visible compaction: 256 threads x 16 Gaussians per block.  Instance emission: 256 x 4.
+#define GSR_COMPACT_ITEMS 16
+#define GSR_COMPACT_TILE (256 * GSR_COMPACT_ITEMS)  // 4096
+#define GSR_DUP_ITEMS 4
+#define GSR_DUP_TILE (256 * GSR_DUP_ITEMS)  // 1024
 
 // Rasterizer constants of the reference algorithm ([EXT] graphdeco
 // cuda_rasterizer/forward.cu + auxiliary.h).
@@ -25,6 +31,35 @@
 #define GSR_T_EPS 0.0001f
 
 namespace gsr {
+
+#ifdef GSR_TIMELINE
+// Diagnostic build only (make diag): per-block phase stamps of the sort/binning kernels.
+// Record = (t0, t1, t2, t3) s_memrealtime ticks (100 MHz), (HW_ID, XCC_ID, ticket id, extra).
+#define GSR_PH_MAX 8192
+enum { GSR_PH_COMPACT = 0, GSR_PH_SORT_DEPTH = 1, GSR_PH_SORT_TILE = 2, GSR_PH_DUP = 3, GSR_PH_KINDS = 4 };
+static __device__ uint4 g_phase_tl[GSR_PH_KINDS][GSR_PH_MAX][2];  // one copy per translation unit
+#define GSR_PH_READER(fname)                                                                           \
+  extern "C" int fname(int kind, void* host, int n) {                                                 \
+    if (kind < 0 || kind >= gsr::GSR_PH_KINDS || n > GSR_PH_MAX) return -1;                           \
+    if (hipDeviceSynchronize() != hipSuccess) return -1;                                              \
+    return hipMemcpyFromSymbol(host, HIP_SYMBOL(gsr::g_phase_tl), sizeof(uint4) * 2 * n,              \
+                               sizeof(uint4) * 2 * GSR_PH_MAX * kind, hipMemcpyDeviceToHost) == hipSuccess \
+               ? 0 : -1;                                                                              \
+  }
+#define GSR_PH_DECL uint32_t ph_t[4] = {(uint32_t)__builtin_amdgcn_s_memrealtime(), 0u, 0u, 0u};
+#define GSR_PH_MARK(i) ph_t[i] = (uint32_t)__builtin_amdgcn_s_memrealtime();
+#define GSR_PH_STORE(kind, vid, extra)                                                                   \
+  if (threadIdx.x == 0 && (vid) < GSR_PH_MAX) {                                                         \
+    ph_t[3] = (uint32_t)__builtin_amdgcn_s_memrealtime();                                               \
+    g_phase_tl[kind][vid][0] = make_uint4(ph_t[0], ph_t[1], ph_t[2], ph_t[3]);                          \
+    g_phase_tl[kind][vid][1] = make_uint4((uint32_t)__builtin_amdgcn_s_getreg((31 << 11) | 4),          \
+                                          (uint32_t)__builtin_amdgcn_s_getreg((15 << 11) | 20), (vid), (extra)); \
+  }
+#else
+#define GSR_PH_DECL
+#define GSR_PH_MARK(i)
+#define GSR_PH_STORE(kind, vid, extra)
+#endif
 
 static inline size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
 
@@ -45,6 +80,63 @@ struct Carver {
 static inline int div_up(long long a, long long b) { return (int)((a + b - 1) / b); }
 static inline int scan_blocks(long long n) { return n <= 0 ? 1 : div_up(n, GSR_SCAN_TILE); }
 
+// Bits of a tile id (row-major over the 16x16 tile grid).
+static inline int tile_key_bits(int W, int H) {
+  const int tiles = div_up(W, GSR_TILE_X) * div_up(H, GSR_TILE_Y);
+  int bits = 0;
+  while ((1 << bits) < tiles) ++bits;
+  return bits < 1 ? 1 : bits;
+}
+
+// LSD digit split of a key_bits-wide key: passes of equal width <= 8 bits.
+struct DigitPlan {
+  int passes, bits;
+  __host__ __device__ int width(int p, int key_bits) const {
+    const int lo = p * bits;
+    return key_bits - lo < bits ? key_bits - lo : bits;
+  }
+};
+static inline DigitPlan digit_plan(int key_bits) {
+  if (key_bits < 1) key_bits = 1;
+  DigitPlan d;
+  d.passes = (key_bits + GSR_RADIX_BITS - 1) / GSR_RADIX_BITS;
+  d.bits = (key_bits + d.passes - 1) / d.passes;
+  return d;
+}
+
+// Zero-before-use words of one onesweep sort: digit counts [pass][256], block tickets [pass],
+// look-back states [pass][block][R] (dense, R = 2^digit bits), the last region of its sync block
+// so only the used prefix is zeroed.
+struct SortSync {
+  uint32_t* digit_count;
+  uint32_t* tickets;
+  uint32_t* states;
+  int blocks;  // look-back blocks per pass (capacity)
+  static size_t words(int blocks) { return GSR_MAX_PASSES * GSR_RADIX + 64 + (size_t)GSR_MAX_PASSES * blocks * GSR_RADIX; }
+  static SortSync carve(uint32_t* w, int blocks) {
+    SortSync s;
+    s.digit_count = w;
+    s.tickets = w + GSR_MAX_PASSES * GSR_RADIX;
+    s.states = s.tickets + 64;
+    s.blocks = blocks;
+    return s;
+  }
+  // bytes from `sync_base` through the states a sort of n items with this plan touches
+  size_t used_bytes(const uint32_t* sync_base, int passes, int bits, long long n) const {
+    const size_t nb = (size_t)(n <= 0 ? 1 : (n + GSR_SCAN_TILE - 1) / GSR_SCAN_TILE);
+    return (size_t)(states - sync_base) * sizeof(uint32_t) + (size_t)passes * nb * ((size_t)1 << bits) * sizeof(uint32_t);
+  }
+};
+
+// The counters word block of a GeomState: [0] visible Gaussians, [1] K instances, [2] error flags
+// (bit 0 look-back timeout), [3] compaction ticket, [4] emission ticket.
+#define GSR_CTR_VISIBLE 0
+#define GSR_CTR_K 1
+#define GSR_CTR_ERR 2
+#define GSR_CTR_TICKET_COMPACT 3
+#define GSR_CTR_TICKET_DUP 4
+#define GSR_NUM_COUNTERS 16
+
 // Per-Gaussian forward state ("geom").  rec0/rec1/rec2 are the 48-byte render record that the
 // blend kernels gather per instance: rec0 = (px, py, conic_a, conic_b),
 // rec1 = (conic_c, opacity, view depth, 0), rec2 = (r, g, b, 0).
@@ -55,37 +147,38 @@ struct GeomState {
   uint2* rect;               // tile rect: x = xmin | ymin << 16, y = xmax | ymax << 16
   uint32_t* clamped;         // SH clamp flags, bit c = channel c clamped to 0
   uint32_t* tiles_touched;   // instances per Gaussian (0 = culled)
-  uint32_t* vis_off;         // exclusive scan of (tiles_touched > 0)
   uint32_t* dkey[2];         // depth-sort ping-pong keys (float bits of view depth)
   uint32_t* dval[2];         // depth-sort ping-pong values (Gaussian index)
-  uint32_t* point_offsets;   // exclusive scan of tiles_touched in depth order
   uint32_t* goff;            // first instance (pre-tile-sort position) of each Gaussian
-  uint32_t* scan_blk;        // block sums for P-sized scans
-  uint32_t* hist;            // radix histogram matrix [RADIX][blocks]
-  uint32_t* hist_blk;        // block sums for scanning hist
-  uint32_t* counters;        // [0] visible count, [1] K
+  // zero-before-use region (one memset per preprocess): counters, compaction look-back, depth sort
+  uint32_t* sync;
+  size_t sync_bytes;
+  uint32_t* counters;        // GSR_CTR_*
+  uint32_t* compact_state;   // [blocks] compaction look-back
+  SortSync dsort;            // depth sort, 4 x 8-bit passes over the visible Gaussians
   static GeomState carve(void* base, int P, size_t* bytes) {
     Carver c(base);
     GeomState g;
     size_t n = (size_t)(P > 0 ? P : 1);
-    int nb = scan_blocks(P);
     g.rec0 = c.take<float4>(n);
     g.rec1 = c.take<float4>(n);
     g.rec2 = c.take<float4>(n);
     g.rect = c.take<uint2>(n);
     g.clamped = c.take<uint32_t>(n);
     g.tiles_touched = c.take<uint32_t>(n);
-    g.vis_off = c.take<uint32_t>(n);
     g.dkey[0] = c.take<uint32_t>(n);
     g.dkey[1] = c.take<uint32_t>(n);
     g.dval[0] = c.take<uint32_t>(n);
     g.dval[1] = c.take<uint32_t>(n);
-    g.point_offsets = c.take<uint32_t>(n);
     g.goff = c.take<uint32_t>(n);
-    g.scan_blk = c.take<uint32_t>(nb + 64);
-    g.hist = c.take<uint32_t>((size_t)GSR_RADIX * nb);
-    g.hist_blk = c.take<uint32_t>(scan_blocks((long long)GSR_RADIX * nb) + 64);
-    g.counters = c.take<uint32_t>(16);
+    const int ncb = div_up((long long)n, GSR_COMPACT_TILE);
+    const int nsb = scan_blocks((long long)n);
+    const size_t words = GSR_NUM_COUNTERS + align_up(ncb, 64) + SortSync::words(nsb);
+    g.sync = c.take<uint32_t>(words);
+    g.sync_bytes = words * sizeof(uint32_t);
+    g.counters = g.sync;
+    g.compact_state = g.sync + GSR_NUM_COUNTERS;
+    g.dsort = SortSync::carve(g.compact_state + align_up(ncb, 64), nsb);
     if (bytes) *bytes = align_up(c.off, 256);
     return g;
   }
@@ -95,19 +188,26 @@ struct GeomState {
 struct BinningState {
   uint32_t* key[2];        // tile id ping-pong
   uint32_t* val[2];        // Gaussian index ping-pong; after the sort: sorted position -> Gaussian
-  uint32_t* hist;
-  uint32_t* hist_blk;
+  // zero-before-use region (one memset per forward render): emission look-back, tile sort
+  uint32_t* sync;
+  size_t sync_bytes;
+  uint32_t* dup_state;     // [blocks] emission look-back (visible Gaussians <= K)
+  SortSync tsort;          // stable tile sort, <= 8-bit passes over K instances
   static BinningState carve(void* base, int K, size_t* bytes) {
     Carver c(base);
     BinningState b;
     size_t n = (size_t)(K > 0 ? K : 1);
-    int nb = scan_blocks(K);
     b.key[0] = c.take<uint32_t>(n);
     b.key[1] = c.take<uint32_t>(n);
     b.val[0] = c.take<uint32_t>(n);
     b.val[1] = c.take<uint32_t>(n);
-    b.hist = c.take<uint32_t>((size_t)GSR_RADIX * nb);
-    b.hist_blk = c.take<uint32_t>(scan_blocks((long long)GSR_RADIX * nb) + 64);
+    const int ndb = div_up((long long)n, GSR_DUP_TILE);
+    const int nsb = scan_blocks((long long)n);
+    const size_t words = align_up(ndb, 64) + SortSync::words(nsb);
+    b.sync = c.take<uint32_t>(words);
+    b.sync_bytes = words * sizeof(uint32_t);
+    b.dup_state = b.sync;
+    b.tsort = SortSync::carve(b.sync + align_up(ndb, 64), nsb);
     if (bytes) *bytes = align_up(c.off, 256);
     return b;
   }

@@ -6,21 +6,13 @@
 
 namespace gsr {
 
-enum ScanMode { SCAN_PLAIN = 0, SCAN_FLAG = 1, SCAN_GATHER = 2 };
-
-// Exclusive scan of n u32 values (n = min(*n_dev, n_max) when n_dev != nullptr).
-//   PLAIN: x_i = in[i];  FLAG: x_i = in[i] > 0;  GATHER: x_i = in[idx[i]]
-// out may alias in for PLAIN.  blk needs scan_blocks(n_max) + 1 words.  *total (device) = sum.
-void scan_exclusive(ScanMode mode, const uint32_t* in, const uint32_t* idx, uint32_t* out,
-                    const uint32_t* n_dev, int n_max, uint32_t* blk, uint32_t* total,
-                    hipStream_t stream);
-
-// Stable LSD radix sort of (key, value) pairs on key bits [0, key_bits) using <= 8-bit digits.
-// Ping-pongs between keys[0]/vals[0] and keys[1]/vals[1]; returns the index (0/1) holding
-// the result.  vals_identity: the input values are the input positions (vals[0] not read).  hist needs
-// RADIX * scan_blocks(n_max) words, hist_blk scan_blocks(RADIX * scan_blocks(n_max)) + 1.
-int radix_sort_pairs(uint32_t* keys[2], uint32_t* vals[2], bool vals_identity, const uint32_t* n_dev,
-                     int n_max, int key_bits, uint32_t* hist, uint32_t* hist_blk, hipStream_t stream);
+// Stable LSD radix sort of n = min(*n_dev, n_max) (key, value) pairs on key bits [0, key_bits),
+// digit_plan(key_bits) passes, one onesweep launch each (gsr_sort.hip).  Ping-pongs between
+// keys[0]/vals[0] and keys[1]/vals[1]; returns the index (0/1) holding the result.  The digit
+// counts of every pass must already be in sync.digit_count (the key producer builds them) and the
+// rest of `sync` zeroed.  vals_identity: the input values are the input positions.
+int onesweep_sort(uint32_t* keys[2], uint32_t* vals[2], bool vals_identity, const uint32_t* n_dev, int n_max,
+                  int key_bits, const SortSync& sync, uint32_t* err, hipStream_t stream);
 
 // Forward preprocess (cull, project, EWA, SH) — gsr_preprocess.hip
 struct PreprocessArgs {
@@ -36,8 +28,8 @@ void launch_preprocess(const PreprocessArgs& a, const GeomState& g, hipStream_t 
 
 // Binning — gsr_binning.hip
 void launch_compact_visible(int P, const GeomState& g, hipStream_t stream);
-void launch_duplicate(int P, int grid_x, const uint32_t* order, const GeomState& g,
-                      const BinningState& b, hipStream_t stream);
+void launch_duplicate(int P, int W, int H, const uint32_t* order, const GeomState& g, const BinningState& b,
+                      uint2* ranges, hipStream_t stream);
 void launch_tile_ranges(int K, const uint32_t* keys, uint2* ranges, hipStream_t stream);
 void launch_mark_visible(int P, const float* means3D, const float* view, const float* proj,
                          uint8_t* present, hipStream_t stream);

@@ -24,6 +24,23 @@ namespace gsr {
 // most of their Gaussians -> one L2), and super-tiles are dealt round-robin over the 8 XCD groups so
 // the spatially clustered heavy tiles spread evenly over the chip (contiguous bands per XCD left the
 // scene centre on 2-3 XCDs).  Grid = 128 * ceil(super-tiles / 8); surplus blocks return false.
+#ifdef GSR_TIMELINE
+// Diagnostic build only (make diag): per-block (start, end) in s_memrealtime ticks (100 MHz), HW_ID,
+// XCC_ID << 24 | work count.  [0] = k_render_fwd, [1] = k_render_bwd.
+#define GSR_TL_MAX 65536
+__device__ uint4 g_timeline[2][GSR_TL_MAX];
+#define GSR_TL_BEGIN const uint32_t tl_t0 = (uint32_t)__builtin_amdgcn_s_memrealtime();
+#define GSR_TL_END(which, work)                                                                  \
+  if (threadIdx.x == 0 && blockIdx.x < GSR_TL_MAX)                                                \
+    g_timeline[which][blockIdx.x] =                                                               \
+        make_uint4(tl_t0, (uint32_t)__builtin_amdgcn_s_memrealtime(),                             \
+                   (uint32_t)__builtin_amdgcn_s_getreg((31 << 11) | 4),                           \
+                   ((uint32_t)__builtin_amdgcn_s_getreg((15 << 11) | 20) << 24) | ((work) & 0xffffffu));
+#else
+#define GSR_TL_BEGIN
+#define GSR_TL_END(which, work)
+#endif
+
 __host__ __device__ __forceinline__ int unit_grid(int gx, int gy) {
   const int S = ((gx + 1) >> 1) * ((gy + 1) >> 1);
   return 128 * ((S + 7) >> 3);
@@ -85,6 +102,7 @@ __global__ __launch_bounds__(64) void k_render_fwd(int W, int H, int grid_x, int
   __shared__ uint32_t s_idx[64];
   int tile, q;
   if (!unit_of_block(blockIdx.x, grid_x, grid_y, tile, q)) return;
+  GSR_TL_BEGIN
   const int unit = 4 * tile + q;
   const int lane = threadIdx.x;
   const int qx0 = (tile % grid_x) * GSR_TILE_X + (q & 1) * 8;
@@ -157,6 +175,7 @@ __global__ __launch_bounds__(64) void k_render_fwd(int W, int H, int grid_x, int
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) mc = max(mc, (uint32_t)__shfl_xor((int)mc, o, 64));
   if (lane == 0) quad_maxc[unit] = mc;
+  GSR_TL_END(0, mc)
 }
 
 // Per tile: instances [0, maxc) were blended by some pixel (max over the 4 quadrants); record the
@@ -239,6 +258,8 @@ __global__ __launch_bounds__(64) void k_render_bwd(int W, int H, int grid_x, int
   __shared__ float4 s_part[BWD_SUB][4][3];
   int tile, q;
   if (!unit_of_block(blockIdx.x, grid_x, grid_y, tile, q)) return;
+  GSR_TL_BEGIN
+  int tl_work = 0;
   const int unit = 4 * tile + q;
   const int lane = threadIdx.x;
   const int txi = tile % grid_x, tyi = tile / grid_x;
@@ -296,6 +317,7 @@ __global__ __launch_bounds__(64) void k_render_bwd(int W, int H, int grid_x, int
     }
     const unsigned long long bal = __ballot(keep);
     const int cnt = __popcll(bal);
+    tl_work += cnt;
     if (keep) {
       const uint32_t pos = mask_rank(bal);
       s0[pos] = r0;
@@ -396,6 +418,8 @@ __global__ __launch_bounds__(64) void k_render_bwd(int W, int H, int grid_x, int
       __syncthreads();
     }
   }
+  GSR_TL_END(1, tl_work)
+  (void)tl_work;
 }
 
 void launch_render_backward(int W, int H, int K, const GeomState& g, const uint32_t* sorted_gauss,
@@ -413,3 +437,14 @@ void launch_render_backward(int W, int H, int K, const GeomState& g, const uint3
 }
 
 }  // namespace gsr
+
+#ifdef GSR_TIMELINE
+extern "C" int gsr_diag_timeline(int which, void* host, int n) {
+  if (which < 0 || which > 1 || n > GSR_TL_MAX) return -1;
+  if (hipDeviceSynchronize() != hipSuccess) return -1;
+  if (hipMemcpyFromSymbol(host, HIP_SYMBOL(gsr::g_timeline), sizeof(uint4) * n,
+                          sizeof(uint4) * GSR_TL_MAX * which, hipMemcpyDeviceToHost) != hipSuccess)
+    return -1;
+  return 0;
+}
+#endif

@@ -21,6 +21,38 @@ from . import _C
 
 # device memory the backward may use at once for per-view gradient rows (views are processed in groups)
 WORK_BUDGET = int(os.environ.get("GSR_BWD_WORK_BYTES", str(24 << 30)))
+# HIP streams the views of a batch are dealt over (views are independent until the per-Gaussian
+# backward): one view's latency-bound sort/scan launches and blend tails overlap another's bulk work
+N_STREAMS = int(os.environ.get("GSR_STREAMS", "4"))
+
+_side: dict = {}
+
+
+class _Fork:
+    """Deal per-view work over side streams that start after everything enqueued so far on the
+    current stream; join() makes the current stream wait for all of them.  Buffers are allocated on
+    the current stream before the fork and released on it after the join, so the caching allocator
+    never hands a side stream memory that is still in use."""
+
+    def __init__(self, dev, n_views):
+        self.main = torch.cuda.current_stream(dev)
+        n = max(1, min(N_STREAMS, n_views))
+        pool = _side.setdefault(dev, [])
+        while len(pool) < n:
+            pool.append(torch.cuda.Stream(dev))
+        self.streams = pool[:n] if n > 1 else [self.main]
+        if n > 1:
+            ev = self.main.record_event()
+            for st in self.streams:
+                st.wait_event(ev)
+
+    def stream(self, v):
+        return ctypes.c_void_p(self.streams[v % len(self.streams)].cuda_stream)
+
+    def join(self):
+        if self.streams[0] is not self.main:
+            for st in self.streams:
+                self.main.wait_event(st.record_event())
 
 
 def _arr(ctype, values):
@@ -57,29 +89,34 @@ class _RasterizeViews(torch.autograd.Function):
         p = _C._ptr
         geoms = []
         if P > 0:
+            geoms = [torch.empty(int(lib.gsr_geom_bytes(P)), dtype=torch.uint8, device=dev) for _ in range(V)]
+            fork = _Fork(dev, V)
             for v, s in enumerate(settings_list):
-                g = torch.empty(int(lib.gsr_geom_bytes(P)), dtype=torch.uint8, device=dev)
                 view, proj, campos, _ = cams[v]
                 _C._check(lib.gsr_forward_preprocess(
                     P, int(s.sh_degree), M, p(m3), p(sc), float(s.scale_modifier), p(rot), p(op), p(shc), p(col),
                     p(c3), p(view), p(proj), p(campos), W, H, float(s.tanfovx), float(s.tanfovy),
-                    int(bool(s.prefiltered)), p(radii[v]), p(g), stream))
-                geoms.append(g)
+                    int(bool(s.prefiltered)), p(radii[v]), p(geoms[v]), fork.stream(v)))
+            fork.join()
             Ks = (ctypes.c_int * V)()
             _C._check(lib.gsr_num_rendered_many(V, _arr(ctypes.c_void_p, [g.data_ptr() for g in geoms]), P, Ks,
                                                 stream))
             Ks = [int(k) for k in Ks]
+            if len(_C.RECENT_FORWARDS) < 4096:
+                _C.RECENT_FORWARDS.extend((k, H, W) for k in Ks)
         else:
             color.zero_(), depth.zero_(), alpha.zero_()
             Ks = [0] * V
         binnings, images = [], []
-        for v in range(V if P > 0 else 0):
-            b = torch.empty(int(lib.gsr_binning_bytes(Ks[v], W, H)), dtype=torch.uint8, device=dev)
-            im = torch.empty(int(lib.gsr_image_bytes(W, H)), dtype=torch.uint8, device=dev)
-            _C._check(lib.gsr_forward_render(P, Ks[v], W, H, p(cams[v][3]), p(geoms[v]), p(b), p(im), p(color[v]),
-                                             p(depth[v]), p(alpha[v]), stream))
-            binnings.append(b)
-            images.append(im)
+        if P > 0:
+            binnings = [torch.empty(int(lib.gsr_binning_bytes(Ks[v], W, H)), dtype=torch.uint8, device=dev)
+                        for v in range(V)]
+            images = [torch.empty(int(lib.gsr_image_bytes(W, H)), dtype=torch.uint8, device=dev) for _ in range(V)]
+            fork = _Fork(dev, V)
+            for v in range(V):
+                _C._check(lib.gsr_forward_render(P, Ks[v], W, H, p(cams[v][3]), p(geoms[v]), p(binnings[v]),
+                                                 p(images[v]), p(color[v]), p(depth[v]), p(alpha[v]), fork.stream(v)))
+            fork.join()
         ctx.settings = settings_list
         ctx.Ks = Ks
         ctx.geoms, ctx.binnings, ctx.images = geoms, binnings, images
@@ -124,14 +161,14 @@ class _RasterizeViews(torch.autograd.Function):
                 cur_b += sizes[v]
             groups.append(cur)
             for gi, grp in enumerate(groups):
-                works = []
-                for v in grp:
-                    w = torch.empty(sizes[v], dtype=torch.uint8, device=dev)
+                works = [torch.empty(sizes[v], dtype=torch.uint8, device=dev) for v in grp]
+                fork = _Fork(dev, len(grp))
+                for j, v in enumerate(grp):
                     _C._check(lib.gsr_backward_render(
                         P, ctx.Ks[v], W, H, p(ctx.cams[v][3]), p(ctx.geoms[v]), p(ctx.binnings[v]), p(ctx.images[v]),
                         p(gc[v]), p(gd[v]) if gd is not None else None, p(ga[v]) if ga is not None else None,
-                        p(w), stream))
-                    works.append(w)
+                        p(works[j]), fork.stream(j)))
+                fork.join()
                 n = len(grp)
                 vp = lambda xs: _arr(ctypes.c_void_p, [x.data_ptr() for x in xs])  # noqa: E731
                 _C._check(lib.gsr_backward_gaussians_many(
