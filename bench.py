@@ -53,7 +53,6 @@ def parse():
     ap.add_argument("--path", choices=["batched", "per-view"], default="batched",
                     help="batched: rasterize_views (one autograd node per rank's views); per-view: one "
                          "GaussianRasterizer call per view, exactly as the reference renderer loop does")
-    ap.add_argument("--streams", type=int, default=4, help="HIP streams the batched path deals views over")
     ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "r01_traffic.json"),
                     help="PMC summary (profiles/summarize.py) supplying roofline.traffic")
     return ap.parse_args()
@@ -191,10 +190,7 @@ def main():
 
     import gsr_synthetic as gs
     from diff_gaussian_rasterization import _C
-    from diff_gaussian_rasterization import batched
     from diff_gaussian_rasterization.view_shard import all_gather_views, allreduce_grads, shard_range
-
-    batched.N_STREAMS = args.streams
 
     t_setup = time.perf_counter()
     scene = gs.make_scene(args.gaussians, sh_degree=args.sh_degree, seed=0)  # identical replica on every rank
@@ -291,19 +287,20 @@ def main():
             "parallelism": f"views sharded over {world} rank(s) (RCCL all-gather images, all-reduce grads)",
             "mean_instances_K": round(K_mean),
             "path": args.path,
-            "streams": args.streams if args.path == "batched" else 1,
         },
     }
     if phases is not None:
         nv = max(1, args.steps * per)
         kern = {k: {"ms_per_view": round(ms / nv, 4), "launches": n} for k, (ms, n) in phases.items()}
         res["kernels"] = kern
-        # forward tile blend (north_star roofline kernel): SURVEY.md §8d B_fwd = 44 K + 28 HW + 8 tiles
+        # forward tile blend (north_star roofline kernel): SURVEY.md §8d B_fwd = 44 K + 28 HW + 8 tiles per
+        # view; a launch blends every view of a view set, so bytes per launch = sum over the timed views / launches
         tiles = math.ceil(W / 16) * math.ceil(H / 16)
         f_ms, f_n = phases["render_fwd"]
         b_ms, b_n = phases["render_bwd"]
-        bytes_fwd = 44.0 * K_mean + 28.0 * H * W + 8.0 * tiles
-        bytes_bwd = 84.0 * K_mean + 28.0 * H * W + 8.0 * tiles  # 44 K gathered + 40 K grads + per-pixel
+        n_fw = max(1, len(Ks))
+        bytes_fwd = (44.0 * sum(Ks) + (28.0 * H * W + 8.0 * tiles) * n_fw) / max(1, f_n)
+        bytes_bwd = (84.0 * sum(Ks) + (28.0 * H * W + 8.0 * tiles) * n_fw) / max(1, b_n)  # 44 K gathered + 40 K grads
         fwd_gbs = bytes_fwd / (f_ms / max(1, f_n) * 1e-3) / 1e9 if f_n else 0.0
         bwd_gbs = bytes_bwd / (b_ms / max(1, b_n) * 1e-3) / 1e9 if b_n else 0.0
         dominant = max(phases.items(), key=lambda kv: kv[1][0])[0]

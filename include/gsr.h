@@ -24,7 +24,7 @@
  * Work is split into the phases the reference performs inside one call so that the host can
  * size the K-dependent buffers between them (the reference does the same D2H read of K,
  * SURVEY.md §2a "cub::DeviceScan ... host sync"):
- *   1. gsr_forward_preprocess   — cull/project/EWA/SH, depth sort of visible Gaussians, K
+ *   1. gsr_forward_preprocess   — cull/project/EWA/SH, depth sort, instance offsets, K
  *   2. gsr_num_rendered         — read K (and the visible count) back to the host
  *   3. gsr_forward_render       — duplicate, tile sort, tile ranges, front-to-back blend
  *   4. gsr_backward             — back-to-front replay + fused per-Gaussian chain rule
@@ -118,31 +118,46 @@ int gsr_backward(int P, int degree, int M, int K, int width, int height, const f
                  void* work, void* stream);
 
 /*
- * View-batched path: one set of Gaussians rendered from V cameras.
- * gsr_forward_preprocess / gsr_forward_render stay per view; these three replace the per-view K
- * readback (V syncs -> 1) and split the backward so the per-Gaussian chain rule runs once per batch:
- * shared-parameter gradients (means3D, opacity, SH, scales, rotations, cov3D, colors) are summed over
- * the V views inside the kernel, the parameters and SH rows are read once per 16 views.
- * Per-view arguments are HOST arrays of V values / device pointers.
+ * View sets: one set of P Gaussians rendered from V <= GSR_SET_MAX cameras
+ * of the same image size by the SAME launches (every stage runs once per set, not once per view;
+ * sorts are segmented by view).  The per-view functions above are sets of one.  The reference
+ * renders a batch with a Python loop over views (renderer/gaussian_batch_renderer.py:9-122), one
+ * rasterizer call each; these replace that loop's V forward and V backward calls.
+ * Per-view arguments are HOST arrays of V values or of V device pointers; images are stacked:
+ * color (V,3,H,W), depth / alpha (V,1,H,W), radii (V,P) int32, dL_dmeans2D (V,P,3).
+ * Shared-parameter gradients (means3D, opacity, SH, scales, rotations, cov3D, colors) are summed
+ * over the V views inside the per-Gaussian kernel.
  */
-int gsr_num_rendered_many(int n_views, const void* const* geoms, int P, int* num_rendered, void* stream);
-/* Backward tile blend of one view: writes that view's per-instance gradient rows into `work`. */
-int gsr_backward_render(int P, int K, int width, int height, const float* bg, const void* geom,
-                        const void* binning, const void* image, const float* dL_dcolor,
-                        const float* dL_ddepth, const float* dL_dalpha, void* work, void* stream);
-/* Per-Gaussian backward over the V views whose rows gsr_backward_render produced.  dL_dmeans2D is
- * per view ((P,3) each); the other gradients are summed over views, and added to the existing
- * contents when accumulate != 0.  dL_dcolors / dL_dcov3D may be NULL. */
-int gsr_backward_gaussians_many(int n_views, int P, int degree, int M, const int* widths, const int* heights,
-                                const float* tanfovx, const float* tanfovy, const float* const* viewmatrices,
-                                const float* const* projmatrices, const float* const* campos,
-                                const int* const* radii, const void* const* geoms, const void* const* images,
-                                const void* const* works, const int* Ks, const float* means3D,
-                                const float* scales, float scale_modifier, const float* rotations,
-                                const float* shs, const float* cov3D_precomp, float* const* dL_dmeans2D,
-                                float* dL_dcolors, float* dL_dopacity, float* dL_dmeans3D, float* dL_dcov3D,
-                                float* dL_dsh, float* dL_dscales, float* dL_drotations, int accumulate,
-                                void* stream);
+#define GSR_SET_MAX 64
+size_t gsr_set_geom_bytes(int V, int P);
+size_t gsr_set_binning_bytes(int V, const int* num_rendered, int width, int height);
+size_t gsr_set_image_bytes(int V, int width, int height);
+/* Scratch holding the gradient rows of all V views; gsr_set_backward also accepts less (>= the
+ * largest single view) and then walks the views in groups that fit. */
+size_t gsr_set_backward_bytes(int V, const int* num_rendered);
+int gsr_set_preprocess(int V, int P, int degree, int M, const float* means3D, const float* scales,
+                       float scale_modifier, const float* rotations, const float* opacities, const float* shs,
+                       const float* colors_precomp, const float* cov3D_precomp,
+                       const float* const* viewmatrices, const float* const* projmatrices,
+                       const float* const* campos, const float* tanfovx, const float* tanfovy,
+                       int width, int height, int prefiltered, int* radii, void* geom, void* stream);
+/* One D2H read of every view's K (and visible count, may be NULL); synchronises `stream`. */
+int gsr_set_num_rendered(int V, const void* geom, int P, int* num_rendered, int* num_visible, void* stream);
+int gsr_set_render(int V, int P, const int* num_rendered, int width, int height, const float* const* bgs,
+                   void* geom, void* binning, void* image, float* out_color, float* out_depth,
+                   float* out_alpha, void* stream);
+/* Gradient outputs are overwritten (accumulate = 0) or added to (accumulate != 0), summed over the
+ * set's views; dL_dmeans2D is per view and always overwritten.  Reads forward state only. */
+int gsr_set_backward(int V, int P, int degree, int M, const int* num_rendered, int width, int height,
+                     const float* const* bgs, const float* means3D, const float* scales, float scale_modifier,
+                     const float* rotations, const float* shs, const float* cov3D_precomp,
+                     const float* const* viewmatrices, const float* const* projmatrices,
+                     const float* const* campos, const float* tanfovx, const float* tanfovy, const int* radii,
+                     const void* geom, const void* binning, const void* image, const float* dL_dcolor,
+                     const float* dL_ddepth, const float* dL_dalpha, float* dL_dmeans2D, float* dL_dcolors,
+                     float* dL_dopacity, float* dL_dmeans3D, float* dL_dcov3D, float* dL_dsh,
+                     float* dL_dscales, float* dL_drotations, int accumulate, void* work, size_t work_bytes,
+                     void* stream);
 
 /*
  * Optional phase timing with HIP events recorded on the launch stream around each phase's kernels.
@@ -151,8 +166,8 @@ int gsr_backward_gaussians_many(int n_views, int P, int degree, int M, const int
  * milliseconds and the number of timed launches since the last reset (arrays of GSR_NUM_PHASES).
  */
 #define GSR_PHASE_PREPROCESS 0 /* k_preprocess                                              */
-#define GSR_PHASE_DEPTH_SORT 1 /* visible compaction, depth radix sort, instance-offset scan */
-#define GSR_PHASE_BINNING 2    /* duplicate, tile radix sort, tile ranges                   */
+#define GSR_PHASE_DEPTH_SORT 1 /* per-view depth radix sort, instance counts and offsets     */
+#define GSR_PHASE_BINNING 2    /* instance emission, tile radix sort, tile ranges           */
 #define GSR_PHASE_RENDER_FWD 3 /* k_render_fwd: forward tile blend                          */
 #define GSR_PHASE_RENDER_BWD 4 /* k_render_bwd: backward tile blend                         */
 #define GSR_PHASE_GAUSS_BWD 5  /* k_gauss_bwd: fused per-Gaussian backward                   */

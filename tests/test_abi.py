@@ -49,7 +49,8 @@ def test_host_only_queries():
     lib = _C.load_library()
     assert lib.gsr_version().decode().startswith("gsr ")
     assert "gfx950" in lib.gsr_version().decode()
-    assert lib.gsr_geom_bytes(1000) >= 1000 * (48 + 8 + 4 * 9)
+    assert lib.gsr_geom_bytes(1000) >= 1000 * (48 + 8 + 4 * 7)  # records, rect, 7 u32 words
+    assert lib.gsr_set_geom_bytes(4, 1000) >= 4 * lib.gsr_geom_bytes(1000) - 4 * 4096
     assert lib.gsr_binning_bytes(5000, 64, 64) >= 5000 * 16
     assert lib.gsr_image_bytes(64, 48) >= 64 * 48 * 8
     assert lib.gsr_backward_bytes(10, 100) >= 100 * 4 * 48

@@ -95,8 +95,9 @@ static int effective_degree(int degree, int M) {
   return d;
 }
 
-// ping-pong buffer holding the tile sort's result (one radix pass per <= 8 key bits)
+// ping-pong buffers holding the sorts' results (one pass per <= 8 key bits)
 static int tile_sort_result(int W, int H) { return digit_plan(tile_key_bits(W, H)).passes & 1; }
+static int depth_sort_result() { return digit_plan(32).passes & 1; }
 
 static GaussBackwardArgs shared_args(int P, int degree, int M, const float* means3D, const float* scales,
                                      float scale_modifier, const float* rotations, const float* shs,
@@ -123,43 +124,88 @@ static GaussBackwardArgs shared_args(int P, int degree, int M, const float* mean
   return a;
 }
 
+// Instance segments of a set from the host copy of K (checked: the set's total < 2^32).
+static int inst_segments(int V, const int* K, SegInfo& seg, long long* total) {
+  seg.V = V;
+  long long run = 0;
+  for (int v = 0; v < V; ++v) {
+    if (K[v] < 0) return fail(GSR_EINVAL, "%s", "negative instance count");
+    seg.n[v] = (uint32_t)K[v];
+    seg.start[v] = (uint32_t)run;
+    run += K[v];
+    if (run >= (1ll << 32)) return fail(GSR_EINVAL, "%s", "instances of a view set exceed 2^32: use smaller sets");
+  }
+  seg_fill_blocks(seg, GSR_SORT_TILE);
+  if (total) *total = run;
+  return GSR_OK;
+}
+
+static int set_cams(int V, const float* const* viewmatrices, const float* const* projmatrices,
+                    const float* const* campos, const float* tanfovx, const float* tanfovy, SetCams& cams) {
+  if (viewmatrices == nullptr || projmatrices == nullptr || campos == nullptr || tanfovx == nullptr ||
+      tanfovy == nullptr)
+    return fail(GSR_EINVAL, "%s", "null camera array");
+  for (int v = 0; v < V; ++v) {
+    if (viewmatrices[v] == nullptr || projmatrices[v] == nullptr || campos[v] == nullptr)
+      return fail(GSR_EINVAL, "%s", "null camera pointer");
+    cams.c[v].view = viewmatrices[v];
+    cams.c[v].proj = projmatrices[v];
+    cams.c[v].campos = campos[v];
+    cams.c[v].tanx = tanfovx[v];
+    cams.c[v].tany = tanfovy[v];
+  }
+  return GSR_OK;
+}
+
+static int check_set(int V, int P) {
+  if (V < 1 || V > GSR_SET_MAX) return fail(GSR_EINVAL, "%s", "a view set holds 1..64 views");
+  if (P < 0) return fail(GSR_EINVAL, "%s", "P must be >= 0");
+  if ((long long)V * (long long)(P > 0 ? P : 1) >= (1ll << 32))
+    return fail(GSR_EINVAL, "%s", "views x Gaussians of a set exceed 2^32: use smaller sets");
+  return GSR_OK;
+}
+
 extern "C" {
 
-const char* gsr_version(void) { return "gsr 0.1.0 gfx950"; }
+const char* gsr_version(void) { return "gsr 0.2.0 gfx950"; }
 const char* gsr_last_error(void) { return g_err; }
 
-size_t gsr_geom_bytes(int P) {
+// ---- view sets ---------------------------------------------------------------------------
+
+size_t gsr_set_geom_bytes(int V, int P) {
   size_t b = 0;
-  GeomState::carve(nullptr, P, &b);
+  GeomState::carve(nullptr, V, P, &b);
   return b;
 }
-size_t gsr_binning_bytes(int K, int width, int height) {
+size_t gsr_set_binning_bytes(int V, const int* K, int width, int height) {
   (void)width;
   (void)height;
+  SegInfo seg;
+  long long total = 0;
+  if (V < 1 || V > GSR_SET_MAX || K == nullptr || inst_segments(V, K, seg, &total) != GSR_OK) return 0;
   size_t b = 0;
-  BinningState::carve(nullptr, K, &b);
+  BinningState::carve(nullptr, V, total, seg.blk[V], &b);
   return b;
 }
-size_t gsr_image_bytes(int width, int height) {
+size_t gsr_set_image_bytes(int V, int width, int height) {
   size_t b = 0;
-  ImageState::carve(nullptr, width, height, &b);
+  ImageState::carve(nullptr, V, width, height, &b);
   return b;
 }
-size_t gsr_backward_bytes(int P, int K) {
-  (void)P;
-  size_t b = 0;
-  BackwardState::carve(nullptr, K, &b);
-  return b;
+size_t gsr_set_backward_bytes(int V, const int* K) {
+  long long total = 0;
+  for (int v = 0; v < V; ++v) total += K[v];
+  return BackwardState::bytes_for(total);
 }
 
-int gsr_forward_preprocess(int P, int degree, int M, const float* means3D, const float* scales,
-                           float scale_modifier, const float* rotations, const float* opacities,
-                           const float* shs, const float* colors_precomp, const float* cov3D_precomp,
-                           const float* viewmatrix, const float* projmatrix, const float* campos,
-                           int width, int height, float tanfovx, float tanfovy, int prefiltered,
-                           int* radii, void* geom, void* stream) {
+int gsr_set_preprocess(int V, int P, int degree, int M, const float* means3D, const float* scales,
+                       float scale_modifier, const float* rotations, const float* opacities, const float* shs,
+                       const float* colors_precomp, const float* cov3D_precomp, const float* const* viewmatrices,
+                       const float* const* projmatrices, const float* const* campos, const float* tanfovx,
+                       const float* tanfovy, int width, int height, int prefiltered, int* radii, void* geom,
+                       void* stream) {
   (void)prefiltered;
-  if (P < 0) return fail(GSR_EINVAL, "%s", "P must be >= 0");
+  if (check_set(V, P) != GSR_OK) return GSR_EINVAL;
   if (width <= 0 || height <= 0) return fail(GSR_EINVAL, "%s", "image size must be positive");
   if ((shs == nullptr) == (colors_precomp == nullptr))
     return fail(GSR_EINVAL, "%s", "Please provide exactly one of either SHs or precomputed colors!");
@@ -167,17 +213,16 @@ int gsr_forward_preprocess(int P, int degree, int M, const float* means3D, const
       ((scales != nullptr || rotations != nullptr) && cov3D_precomp != nullptr))
     return fail(GSR_EINVAL, "%s",
                 "Please provide exactly one of either scale/rotation pair or precomputed 3D covariance!");
-  if (geom == nullptr || viewmatrix == nullptr || projmatrix == nullptr || campos == nullptr ||
-      (P > 0 && (means3D == nullptr || opacities == nullptr || radii == nullptr)))
+  if (geom == nullptr || (P > 0 && (means3D == nullptr || opacities == nullptr || radii == nullptr)))
     return fail(GSR_EINVAL, "%s", "null pointer argument");
   if (shs != nullptr && M <= 0) return fail(GSR_EINVAL, "%s", "M must be >= 1 with SHs");
+  SetCams cams;
+  if (set_cams(V, viewmatrices, projmatrices, campos, tanfovx, tanfovy, cams) != GSR_OK) return GSR_EINVAL;
   hipStream_t s = (hipStream_t)stream;
-  GeomState g = GeomState::carve(geom, P, nullptr);
-  const DigitPlan dplan = digit_plan(32);
-  GSR_HIP_CHECK(hipMemsetAsync(g.sync, 0, g.dsort.used_bytes(g.sync, dplan.passes, dplan.bits, P), s));
-  if (P == 0) return last_launch();
+  GeomState g = GeomState::carve(geom, V, P, nullptr);
 
   PreprocessArgs a;
+  a.V = V;
   a.P = P;
   a.deg = effective_degree(degree, M);
   a.M = M;
@@ -189,77 +234,206 @@ int gsr_forward_preprocess(int P, int degree, int M, const float* means3D, const
   a.colors_precomp = colors_precomp;
   a.cov3D_precomp = cov3D_precomp;
   a.scale_modifier = scale_modifier;
-  a.viewmatrix = viewmatrix;
-  a.projmatrix = projmatrix;
-  a.campos = campos;
   a.W = width;
   a.H = height;
-  a.tanfovx = tanfovx;
-  a.tanfovy = tanfovy;
-  a.focal_y = height / (2.0f * tanfovy);
-  a.focal_x = width / (2.0f * tanfovx);
   a.radii = radii;
   {
     PhaseScope ps(GSR_PHASE_PREPROCESS, s);
-    launch_preprocess(a, g, s);
+    launch_preprocess(a, cams, g, s);
   }
   {
-    // visible compaction (+ depth digit counts, K) -> depth sort of the visible Gaussians
+    // depth sort of every view's Gaussians (culled last) -> instance counts in depth order, K_v
     PhaseScope ps(GSR_PHASE_DEPTH_SORT, s);
-    launch_compact_visible(P, g, s);
-    const int res = onesweep_sort(g.dkey, g.dval, false, g.counters + GSR_CTR_VISIBLE, P, 32, g.dsort,
-                                  g.counters + GSR_CTR_ERR, s);
-    if (res != 0) return fail(GSR_EHIP, "%s", "internal: depth sort result buffer");
+    SegInfo seg;
+    seg.V = V;
+    for (int v = 0; v < V; ++v) {
+      seg.n[v] = (uint32_t)P;
+      seg.start[v] = (uint32_t)((size_t)v * P);
+    }
+    const int res = seg_sort(g.dkey, g.dval, true, seg, 32, g.sort_counts, g.sort_totals, s);
+    if (res != depth_sort_result()) return fail(GSR_EHIP, "%s", "internal: depth sort result buffer");
+    launch_binning_counts(V, P, g, g.dval[res], s);
   }
   return last_launch();
 }
 
-int gsr_num_rendered(const void* geom, int P, int* num_rendered, int* num_visible, void* stream) {
+int gsr_set_num_rendered(int V, const void* geom, int P, int* num_rendered, int* num_visible, void* stream) {
+  if (check_set(V, P) != GSR_OK) return GSR_EINVAL;
   if (geom == nullptr || num_rendered == nullptr) return fail(GSR_EINVAL, "%s", "null pointer argument");
-  GeomState g = GeomState::carve((void*)geom, P, nullptr);
-  uint32_t h[4] = {0, 0, 0, 0};
+  GeomState g = GeomState::carve((void*)geom, V, P, nullptr);
   hipStream_t s = (hipStream_t)stream;
-  if (P > 0) {
-    GSR_HIP_CHECK(hipMemcpyAsync(h, g.counters, sizeof(h), hipMemcpyDeviceToHost, s));
-    GSR_HIP_CHECK(hipStreamSynchronize(s));
+  static thread_local uint32_t* pinned = nullptr;
+  if (pinned == nullptr) GSR_HIP_CHECK(hipHostMalloc((void**)&pinned, 2 * GSR_SET_MAX * sizeof(uint32_t), hipHostMallocDefault));
+  GSR_HIP_CHECK(hipMemcpyAsync(pinned, g.counters, 2 * (size_t)V * sizeof(uint32_t), hipMemcpyDeviceToHost, s));
+  GSR_HIP_CHECK(hipStreamSynchronize(s));
+  for (int v = 0; v < V; ++v) {
+    num_rendered[v] = (int)pinned[v];
+    if (num_visible) num_visible[v] = (int)pinned[V + v];
+    if (pinned[v] > 0x7fffffffu) return fail(GSR_EINVAL, "%s", "instance count of a view exceeds 2^31");
   }
-  if (h[GSR_CTR_ERR]) return fail(GSR_EHIP, "%s", "internal: look-back timeout in compaction / depth sort");
-  *num_rendered = (int)h[GSR_CTR_K];
-  if (num_visible) *num_visible = (int)h[0];
   g_err[0] = 0;
   return GSR_OK;
+}
+
+int gsr_set_render(int V, int P, const int* K, int width, int height, const float* const* bgs, void* geom,
+                   void* binning, void* image, float* out_color, float* out_depth, float* out_alpha, void* stream) {
+  if (check_set(V, P) != GSR_OK) return GSR_EINVAL;
+  if (width <= 0 || height <= 0) return fail(GSR_EINVAL, "%s", "bad sizes");
+  if (K == nullptr || bgs == nullptr || geom == nullptr || binning == nullptr || image == nullptr ||
+      out_color == nullptr || out_depth == nullptr || out_alpha == nullptr)
+    return fail(GSR_EINVAL, "%s", "null pointer argument");
+  SegInfo inst;
+  long long total = 0;
+  if (inst_segments(V, K, inst, &total) != GSR_OK) return GSR_EINVAL;
+  hipStream_t s = (hipStream_t)stream;
+  GeomState g = GeomState::carve(geom, V, P, nullptr);
+  BinningState b = BinningState::carve(binning, V, total, inst.blk[V], nullptr);
+  ImageState img = ImageState::carve(image, V, width, height, nullptr);
+  const int gx = div_up(width, GSR_TILE_X), gy = div_up(height, GSR_TILE_Y);
+  const int tres = tile_sort_result(width, height);
+  {
+    PhaseScope ps(GSR_PHASE_BINNING, s);
+    GSR_HIP_CHECK(hipMemsetAsync(img.ranges, 0, sizeof(uint2) * (size_t)V * gx * gy, s));
+    if (total > 0) {
+      launch_emit(V, P, width, g, g.dval[depth_sort_result()], inst, b.key[0], b.val[0], s);
+      const int res = seg_sort(b.key, b.val, false, inst, tile_key_bits(width, height), b.sort_counts,
+                               b.sort_totals, s);
+      if (res != tres) return fail(GSR_EHIP, "%s", "internal: tile sort buffer");
+      launch_tile_ranges(inst, gx * gy, b.key[res], img.ranges, s);
+    }
+  }
+  {
+    PhaseScope ps(GSR_PHASE_RENDER_FWD, s);
+    RenderSet rs;
+    rs.V = V;
+    rs.v0 = 0;
+    rs.P = P;
+    rs.W = width;
+    rs.H = height;
+    rs.gx = gx;
+    rs.gy = gy;
+    for (int v = 0; v < V; ++v) {
+      if (bgs[v] == nullptr) return fail(GSR_EINVAL, "%s", "null background");
+      rs.inst_start[v] = inst.start[v];
+      rs.row_start[v] = 0;
+      rs.bg[v] = bgs[v];
+    }
+    launch_render_forward(rs, g, b.val[tres], img, out_color, out_depth, out_alpha, s);
+  }
+  return last_launch();
+}
+
+int gsr_set_backward(int V, int P, int degree, int M, const int* K, int width, int height, const float* const* bgs,
+                     const float* means3D, const float* scales, float scale_modifier, const float* rotations,
+                     const float* shs, const float* cov3D_precomp, const float* const* viewmatrices,
+                     const float* const* projmatrices, const float* const* campos, const float* tanfovx,
+                     const float* tanfovy, const int* radii, const void* geom, const void* binning,
+                     const void* image, const float* dL_dcolor, const float* dL_ddepth, const float* dL_dalpha,
+                     float* dL_dmeans2D, float* dL_dcolors, float* dL_dopacity, float* dL_dmeans3D,
+                     float* dL_dcov3D, float* dL_dsh, float* dL_dscales, float* dL_drotations, int accumulate,
+                     void* work, size_t work_bytes, void* stream) {
+  if (check_set(V, P) != GSR_OK) return GSR_EINVAL;
+  if (width <= 0 || height <= 0) return fail(GSR_EINVAL, "%s", "bad sizes");
+  if (P == 0) return last_launch();
+  if (K == nullptr || bgs == nullptr || geom == nullptr || binning == nullptr || image == nullptr ||
+      work == nullptr || dL_dcolor == nullptr || dL_dmeans2D == nullptr || dL_dcolors == nullptr ||
+      dL_dopacity == nullptr || dL_dmeans3D == nullptr || radii == nullptr || means3D == nullptr)
+    return fail(GSR_EINVAL, "%s", "null pointer argument");
+  if (shs != nullptr && dL_dsh == nullptr) return fail(GSR_EINVAL, "%s", "dL_dsh required with SHs");
+  if (cov3D_precomp == nullptr && (scales == nullptr || rotations == nullptr || dL_dscales == nullptr ||
+                                   dL_drotations == nullptr))
+    return fail(GSR_EINVAL, "%s", "scales/rotations and their gradients required");
+  SetCams cams;
+  if (set_cams(V, viewmatrices, projmatrices, campos, tanfovx, tanfovy, cams) != GSR_OK) return GSR_EINVAL;
+  SegInfo inst;
+  long long total = 0;
+  if (inst_segments(V, K, inst, &total) != GSR_OK) return GSR_EINVAL;
+  hipStream_t s = (hipStream_t)stream;
+  GeomState g = GeomState::carve((void*)geom, V, P, nullptr);
+  BinningState b = BinningState::carve((void*)binning, V, total, inst.blk[V], nullptr);
+  ImageState img = ImageState::carve((void*)image, V, width, height, nullptr);
+  const int gx = div_up(width, GSR_TILE_X), gy = div_up(height, GSR_TILE_Y);
+  const size_t HW = (size_t)width * height;
+  const uint32_t* sorted = b.val[tile_sort_result(width, height)];
+  GaussBackwardArgs a = shared_args(P, degree, M, means3D, scales, scale_modifier, rotations, shs, cov3D_precomp,
+                                     dL_dcolors, dL_dopacity, dL_dmeans3D, dL_dcov3D, dL_dsh, dL_dscales,
+                                     dL_drotations);
+  bool first = accumulate == 0;
+  // groups of consecutive views whose gradient rows fit the work buffer
+  for (int g0 = 0; g0 < V;) {
+    int g1 = g0;
+    long long rows = 0;
+    while (g1 < V && (g1 == g0 || BackwardState::bytes_for(rows + K[g1]) <= work_bytes)) rows += K[g1++];
+    if (BackwardState::bytes_for(rows) > work_bytes)
+      return fail(GSR_EINVAL, "%s", "backward work buffer smaller than one view's gradient rows");
+    BackwardState bw = BackwardState::carve(work);
+    RenderSet rs;
+    rs.V = g1 - g0;
+    rs.v0 = g0;
+    rs.P = P;
+    rs.W = width;
+    rs.H = height;
+    rs.gx = gx;
+    rs.gy = gy;
+    for (int v = g0; v < g1; ++v) {
+      if (bgs[v] == nullptr) return fail(GSR_EINVAL, "%s", "null background");
+      rs.inst_start[v - g0] = inst.start[v];
+      rs.row_start[v - g0] = inst.start[v] - inst.start[g0];
+      rs.bg[v - g0] = bgs[v];
+    }
+    {
+      PhaseScope ps(GSR_PHASE_RENDER_BWD, s);
+      launch_render_backward(rs, g, sorted, img, dL_dcolor + (size_t)g0 * 3 * HW,
+                             dL_ddepth ? dL_ddepth + (size_t)g0 * HW : nullptr,
+                             dL_dalpha ? dL_dalpha + (size_t)g0 * HW : nullptr, bw, s);
+    }
+    PhaseScope ps(GSR_PHASE_GAUSS_BWD, s);
+    for (int c0 = g0; c0 < g1; c0 += GSR_VIEWS_PER_LAUNCH) {
+      const int c1 = c0 + GSR_VIEWS_PER_LAUNCH < g1 ? c0 + GSR_VIEWS_PER_LAUNCH : g1;
+      ViewBatch vb;
+      vb.n = c1 - c0;
+      vb.accumulate = first ? 0 : 1;
+      for (int v = c0; v < c1; ++v)
+        vb.v[v - c0] = make_view_desc(cams.c[v], v, P, radii, g, img, bw.grow + (size_t)12 * rs.row_start[v - g0],
+                                      dL_dmeans2D + (size_t)v * P * 3, width, height);
+      launch_gauss_backward_views(a, vb, s);
+      first = false;
+    }
+    g0 = g1;
+  }
+  return last_launch();
+}
+
+// ---- one view (the reference's per-call interface): a set of one --------------------------
+
+size_t gsr_geom_bytes(int P) { return gsr_set_geom_bytes(1, P); }
+size_t gsr_binning_bytes(int K, int width, int height) { return gsr_set_binning_bytes(1, &K, width, height); }
+size_t gsr_image_bytes(int width, int height) { return gsr_set_image_bytes(1, width, height); }
+size_t gsr_backward_bytes(int P, int K) {
+  (void)P;
+  return gsr_set_backward_bytes(1, &K);
+}
+
+int gsr_forward_preprocess(int P, int degree, int M, const float* means3D, const float* scales,
+                           float scale_modifier, const float* rotations, const float* opacities,
+                           const float* shs, const float* colors_precomp, const float* cov3D_precomp,
+                           const float* viewmatrix, const float* projmatrix, const float* campos,
+                           int width, int height, float tanfovx, float tanfovy, int prefiltered,
+                           int* radii, void* geom, void* stream) {
+  return gsr_set_preprocess(1, P, degree, M, means3D, scales, scale_modifier, rotations, opacities, shs,
+                            colors_precomp, cov3D_precomp, &viewmatrix, &projmatrix, &campos, &tanfovx, &tanfovy,
+                            width, height, prefiltered, radii, geom, stream);
+}
+
+int gsr_num_rendered(const void* geom, int P, int* num_rendered, int* num_visible, void* stream) {
+  return gsr_set_num_rendered(1, geom, P, num_rendered, num_visible, stream);
 }
 
 int gsr_forward_render(int P, int K, int width, int height, const float* bg, void* geom,
                        void* binning, void* image, float* out_color, float* out_depth,
                        float* out_alpha, void* stream) {
-  if (P < 0 || K < 0 || width <= 0 || height <= 0) return fail(GSR_EINVAL, "%s", "bad sizes");
-  if (geom == nullptr || binning == nullptr || image == nullptr || bg == nullptr ||
-      out_color == nullptr || out_depth == nullptr || out_alpha == nullptr)
-    return fail(GSR_EINVAL, "%s", "null pointer argument");
-  hipStream_t s = (hipStream_t)stream;
-  GeomState g = GeomState::carve(geom, P, nullptr);
-  BinningState b = BinningState::carve(binning, K, nullptr);
-  ImageState img = ImageState::carve(image, width, height, nullptr);
-  const int gx = div_up(width, GSR_TILE_X), gy = div_up(height, GSR_TILE_Y);
-  if (K > 0) {
-    PhaseScope ps(GSR_PHASE_BINNING, s);
-    const int kbits = tile_key_bits(width, height);
-    const DigitPlan tplan = digit_plan(kbits);
-    GSR_HIP_CHECK(hipMemsetAsync(b.sync, 0, b.tsort.used_bytes(b.sync, tplan.passes, tplan.bits, K), s));
-    launch_duplicate(P, width, height, g.dval[0], g, b, img.ranges, s);
-    const int res = onesweep_sort(b.key, b.val, false, nullptr, K, kbits, b.tsort, g.counters + GSR_CTR_ERR, s);
-    if (res != tile_sort_result(width, height)) return fail(GSR_EHIP, "%s", "internal: tile sort buffer");
-    launch_tile_ranges(K, b.key[res], img.ranges, s);
-  } else {
-    GSR_HIP_CHECK(hipMemsetAsync(img.ranges, 0, sizeof(uint2) * (size_t)gx * gy, s));
-  }
-  {
-    PhaseScope ps(GSR_PHASE_RENDER_FWD, s);
-    launch_render_forward(width, height, g, b.val[tile_sort_result(width, height)], img, bg, out_color,
-                          out_depth, out_alpha, s);
-  }
-  return last_launch();
+  if (K < 0) return fail(GSR_EINVAL, "%s", "bad sizes");
+  return gsr_set_render(1, P, &K, width, height, &bg, geom, binning, image, out_color, out_depth, out_alpha, stream);
 }
 
 int gsr_backward(int P, int degree, int M, int K, int width, int height, const float* bg,
@@ -274,135 +448,11 @@ int gsr_backward(int P, int degree, int M, int K, int width, int height, const f
                  void* work, void* stream) {
   (void)opacities;
   (void)colors_precomp;
-  if (P < 0 || K < 0 || width <= 0 || height <= 0) return fail(GSR_EINVAL, "%s", "bad sizes");
-  if (P == 0) return last_launch();
-  if (geom == nullptr || binning == nullptr || image == nullptr || work == nullptr || bg == nullptr ||
-      dL_dcolor == nullptr || dL_dmeans2D == nullptr || dL_dcolors == nullptr ||
-      dL_dopacity == nullptr || dL_dmeans3D == nullptr || radii == nullptr || means3D == nullptr)
-    return fail(GSR_EINVAL, "%s", "null pointer argument");
-  if (shs != nullptr && dL_dsh == nullptr) return fail(GSR_EINVAL, "%s", "dL_dsh required with SHs");
-  if (cov3D_precomp == nullptr && (scales == nullptr || rotations == nullptr || dL_dscales == nullptr ||
-                                   dL_drotations == nullptr))
-    return fail(GSR_EINVAL, "%s", "scales/rotations and their gradients required");
-  hipStream_t s = (hipStream_t)stream;
-  GeomState g = GeomState::carve((void*)geom, P, nullptr);
-  BinningState b = BinningState::carve((void*)binning, K, nullptr);
-  ImageState img = ImageState::carve((void*)image, width, height, nullptr);
-  BackwardState bw = BackwardState::carve(work, K, nullptr);
-  {
-    PhaseScope ps(GSR_PHASE_RENDER_BWD, s);
-    launch_render_backward(width, height, K, g, b.val[tile_sort_result(width, height)], img, bg, dL_dcolor,
-                           dL_ddepth, dL_dalpha, bw, s);
-  }
-
-  GaussBackwardArgs a = shared_args(P, degree, M, means3D, scales, scale_modifier, rotations, shs, cov3D_precomp,
-                                     dL_dcolors, dL_dopacity, dL_dmeans3D, dL_dcov3D, dL_dsh, dL_dscales,
-                                     dL_drotations);
-  ViewBatch vb;
-  vb.n = 1;
-  vb.accumulate = 0;
-  vb.v[0] = make_view_desc(viewmatrix, projmatrix, campos, radii, g, img, bw, dL_dmeans2D, width, height,
-                           tanfovx, tanfovy);
-  {
-    PhaseScope ps(GSR_PHASE_GAUSS_BWD, s);
-    launch_gauss_backward_views(a, vb, s);
-  }
-  return last_launch();
-}
-
-// ---- view-batched path ---------------------------------------------------------------------
-
-int gsr_num_rendered_many(int n_views, const void* const* geoms, int P, int* num_rendered, void* stream) {
-  if (n_views < 0 || (n_views > 0 && (geoms == nullptr || num_rendered == nullptr)))
-    return fail(GSR_EINVAL, "%s", "null pointer argument");
-  hipStream_t s = (hipStream_t)stream;
-  static thread_local uint32_t* pinned = nullptr;
-  static thread_local int pinned_n = 0;
-  if (pinned_n < n_views) {
-    if (pinned) (void)hipHostFree(pinned);
-    pinned = nullptr;
-    GSR_HIP_CHECK(hipHostMalloc((void**)&pinned, 4 * sizeof(uint32_t) * (size_t)n_views, hipHostMallocDefault));
-    pinned_n = n_views;
-  }
-  for (int v = 0; v < n_views; ++v) {
-    if (geoms[v] == nullptr) return fail(GSR_EINVAL, "%s", "null geom buffer");
-    GeomState g = GeomState::carve((void*)geoms[v], P, nullptr);
-    if (P > 0) GSR_HIP_CHECK(hipMemcpyAsync(pinned + 4 * v, g.counters, 4 * sizeof(uint32_t), hipMemcpyDeviceToHost, s));
-    else pinned[4 * v + GSR_CTR_K] = pinned[4 * v + GSR_CTR_ERR] = 0u;
-  }
-  GSR_HIP_CHECK(hipStreamSynchronize(s));
-  for (int v = 0; v < n_views; ++v) {
-    if (pinned[4 * v + GSR_CTR_ERR]) return fail(GSR_EHIP, "%s", "internal: look-back timeout in compaction / depth sort");
-    num_rendered[v] = (int)pinned[4 * v + GSR_CTR_K];
-  }
-  g_err[0] = 0;
-  return GSR_OK;
-}
-
-int gsr_backward_render(int P, int K, int width, int height, const float* bg, const void* geom,
-                        const void* binning, const void* image, const float* dL_dcolor,
-                        const float* dL_ddepth, const float* dL_dalpha, void* work, void* stream) {
-  if (P < 0 || K < 0 || width <= 0 || height <= 0) return fail(GSR_EINVAL, "%s", "bad sizes");
-  if (geom == nullptr || binning == nullptr || image == nullptr || work == nullptr || bg == nullptr ||
-      dL_dcolor == nullptr)
-    return fail(GSR_EINVAL, "%s", "null pointer argument");
-  hipStream_t s = (hipStream_t)stream;
-  GeomState g = GeomState::carve((void*)geom, P, nullptr);
-  BinningState b = BinningState::carve((void*)binning, K, nullptr);
-  ImageState img = ImageState::carve((void*)image, width, height, nullptr);
-  BackwardState bw = BackwardState::carve(work, K, nullptr);
-  {
-    PhaseScope ps(GSR_PHASE_RENDER_BWD, s);
-    launch_render_backward(width, height, K, g, b.val[tile_sort_result(width, height)], img, bg, dL_dcolor,
-                           dL_ddepth, dL_dalpha, bw, s);
-  }
-  return last_launch();
-}
-
-int gsr_backward_gaussians_many(int n_views, int P, int degree, int M, const int* widths, const int* heights,
-                                const float* tanfovx, const float* tanfovy, const float* const* viewmatrices,
-                                const float* const* projmatrices, const float* const* campos,
-                                const int* const* radii, const void* const* geoms, const void* const* images,
-                                const void* const* works, const int* Ks, const float* means3D,
-                                const float* scales, float scale_modifier, const float* rotations,
-                                const float* shs, const float* cov3D_precomp, float* const* dL_dmeans2D,
-                                float* dL_dcolors, float* dL_dopacity, float* dL_dmeans3D, float* dL_dcov3D,
-                                float* dL_dsh, float* dL_dscales, float* dL_drotations, int accumulate,
-                                void* stream) {
-  if (n_views < 0 || P < 0) return fail(GSR_EINVAL, "%s", "bad sizes");
-  if (P == 0 || n_views == 0) return last_launch();
-  if (widths == nullptr || heights == nullptr || tanfovx == nullptr || tanfovy == nullptr ||
-      viewmatrices == nullptr || projmatrices == nullptr || campos == nullptr || radii == nullptr ||
-      geoms == nullptr || images == nullptr || works == nullptr || Ks == nullptr || dL_dmeans2D == nullptr ||
-      means3D == nullptr || dL_dopacity == nullptr || dL_dmeans3D == nullptr)
-    return fail(GSR_EINVAL, "%s", "null pointer argument");
-  if (shs != nullptr && dL_dsh == nullptr) return fail(GSR_EINVAL, "%s", "dL_dsh required with SHs");
-  if (cov3D_precomp == nullptr && (scales == nullptr || rotations == nullptr || dL_dscales == nullptr ||
-                                   dL_drotations == nullptr))
-    return fail(GSR_EINVAL, "%s", "scales/rotations and their gradients required");
-  hipStream_t s = (hipStream_t)stream;
-  GaussBackwardArgs a = shared_args(P, degree, M, means3D, scales, scale_modifier, rotations, shs, cov3D_precomp,
-                                     dL_dcolors, dL_dopacity, dL_dmeans3D, dL_dcov3D, dL_dsh, dL_dscales,
-                                     dL_drotations);
-  for (int v0 = 0; v0 < n_views; v0 += GSR_VIEWS_PER_LAUNCH) {
-    ViewBatch vb;
-    vb.n = n_views - v0 < GSR_VIEWS_PER_LAUNCH ? n_views - v0 : GSR_VIEWS_PER_LAUNCH;
-    vb.accumulate = (accumulate || v0 > 0) ? 1 : 0;
-    for (int j = 0; j < vb.n; ++j) {
-      const int v = v0 + j;
-      if (widths[v] <= 0 || heights[v] <= 0 || Ks[v] < 0) return fail(GSR_EINVAL, "%s", "bad view sizes");
-      if (geoms[v] == nullptr || images[v] == nullptr || works[v] == nullptr || dL_dmeans2D[v] == nullptr)
-        return fail(GSR_EINVAL, "%s", "null per-view buffer");
-      GeomState g = GeomState::carve((void*)geoms[v], P, nullptr);
-      ImageState img = ImageState::carve((void*)images[v], widths[v], heights[v], nullptr);
-      BackwardState bw = BackwardState::carve((void*)works[v], Ks[v], nullptr);
-      vb.v[j] = make_view_desc(viewmatrices[v], projmatrices[v], campos[v], radii[v], g, img, bw, dL_dmeans2D[v],
-                               widths[v], heights[v], tanfovx[v], tanfovy[v]);
-    }
-    PhaseScope ps(GSR_PHASE_GAUSS_BWD, s);
-    launch_gauss_backward_views(a, vb, s);
-  }
-  return last_launch();
+  if (K < 0) return fail(GSR_EINVAL, "%s", "bad sizes");
+  return gsr_set_backward(1, P, degree, M, &K, width, height, &bg, means3D, scales, scale_modifier, rotations, shs,
+                          cov3D_precomp, &viewmatrix, &projmatrix, &campos, &tanfovx, &tanfovy, radii, geom, binning,
+                          image, dL_dcolor, dL_ddepth, dL_dalpha, dL_dmeans2D, dL_dcolors, dL_dopacity, dL_dmeans3D,
+                          dL_dcov3D, dL_dsh, dL_dscales, dL_drotations, 0, work, gsr_backward_bytes(P, K), stream);
 }
 
 int gsr_profile_enable(int enable) {

@@ -377,26 +377,27 @@ void launch_gauss_backward_views(const GaussBackwardArgs& a, const ViewBatch& vb
     hipLaunchKernelGGL(k_gauss_bwd_views<true>, dim3((a.P + 255) / 256), dim3(256), lds, stream, a, vb);
 }
 
-ViewDesc make_view_desc(const float* view, const float* proj, const float* campos, const int* radii,
-                        const GeomState& g, const ImageState& img, const BackwardState& bw,
-                        float* dmeans2D, int W, int H, float tanx, float tany) {
+ViewDesc make_view_desc(const ViewCam& cam, int vg, int P, const int* radii, const GeomState& g,
+                        const ImageState& img, const float4* grow, float* dmeans2D, int W, int H) {
+  const size_t o = (size_t)vg * P;
+  const int gx = div_up(W, GSR_TILE_X), gy = div_up(H, GSR_TILE_Y);
   ViewDesc d;
-  d.view = view;
-  d.proj = proj;
-  d.campos = campos;
-  d.radii = radii;
-  d.rec1 = g.rec1;
-  d.rect = g.rect;
-  d.goff = g.goff;
-  d.clamped = g.clamped;
-  d.tile_info = img.tile_info;
-  d.grow = bw.grow;
+  d.view = cam.view;
+  d.proj = cam.proj;
+  d.campos = cam.campos;
+  d.radii = radii + o;
+  d.rec1 = g.rec1 + o;
+  d.rect = g.rect + o;
+  d.goff = g.goff + o;
+  d.clamped = g.clamped + o;
+  d.tile_info = img.tile_info + (size_t)vg * gx * gy;
+  d.grow = grow;
   d.dmeans2D = dmeans2D;
-  d.tanx = tanx;
-  d.tany = tany;
-  d.fy = H / (2.0f * tany);
-  d.fx = W / (2.0f * tanx);
-  d.grid_x = div_up(W, GSR_TILE_X);
+  d.tanx = cam.tanx;
+  d.tany = cam.tany;
+  d.fy = H / (2.0f * cam.tany);
+  d.fx = W / (2.0f * cam.tanx);
+  d.grid_x = gx;
   return d;
 }
 

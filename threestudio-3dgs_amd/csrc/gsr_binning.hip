@@ -1,194 +1,121 @@
-// gsr_binning.hip — tile binning (replaces duplicateWithKeys,
-// the 64-bit (tile | depth) radix sort and identifyTileRanges of the reference [EXT]).
+// gsr_binning.hip — tile binning of a view set (replaces the
+// InclusiveSum over tiles_touched, duplicateWithKeys, the 64-bit (tile | depth) radix sort and
+// identifyTileRanges of the reference [EXT]).
 //
 // MI355X design: instead of radix-sorting K 64-bit (tile<<32 | depth) keys (41-45 key bits ->
-// 6 passes over K), the visible Gaussians are depth-sorted once (N keys, 32 bits), the instances
-// are emitted in depth order, and a stable sort on the tile id alone (12 bits at 1024^2 -> 2 passes
-// over K) finishes the job.  Stability makes the result identical to the reference's order:
-// per tile, ascending depth, ties by Gaussian index.  The scans between these steps are fused
-// into the kernels that produce their inputs (decoupled look-back), so a view costs
-// memset + preprocess + compaction + 4 depth passes, then memset + emission + 2 tile passes +
-// ranges + blend.
+// 6 passes over K per view), each view's Gaussians are depth-sorted once (P keys, 32 bits;
+// gsr_sort.hip), the instances are emitted in depth order, and a stable sort on the tile id alone
+// (12 bits at 1024^2 -> 2 passes over K) finishes the job.  Stability makes the result identical
+// to the reference's order: per tile, ascending depth, ties by Gaussian index.  Every step runs
+// once for all views of a set (segments of flat arrays), so a 64-view batch costs the same
+// number of launches as one view.
 #include "gsr_kernels.h"
 #include "gsr_wave.h"
 
 namespace gsr {
 
-__device__ __forceinline__ uint32_t n_of(const uint32_t* n_dev, int n_max) {
-  const uint32_t n = *n_dev;
-  return n < (uint32_t)n_max ? n : (uint32_t)n_max;
-}
-
-// Compact the visible Gaussians (tiles_touched > 0) into (depth bits, index) pairs in index
-// order, fused with everything else that needs one look at them:
-//   * the block's visible count -> decoupled look-back -> its compacted output offset,
-//   * the digit counts of all 4 depth-sort passes (LDS histogram, flushed with global atomics),
-//   * K = sum of tiles_touched and the visible count (integer atomics: order-independent).
-// Thread t owns the 16 consecutive Gaussians [base + 16 t, base + 16 t + 16) (4 x 16-B loads).
-struct CompactLDS {
-  uint32_t hist[4][GSR_RADIX];
-  uint32_t wave[8];
-  uint32_t vid, prefix;
-};
-
-__global__ __launch_bounds__(256) void k_compact_visible(int P, GeomState g) {
-  __shared__ CompactLDS s;
-  GSR_PH_DECL
+// Instances of each 1024-Gaussian block of every view's depth order: counts[v][block].
+__global__ __launch_bounds__(256) void k_inst_count(int P, int nbe, GeomState g, const uint32_t* __restrict__ order) {
+  __shared__ uint32_t s_wave[8];
+  const int v = blockIdx.x / nbe, lb = blockIdx.x % nbe;
   const int t = threadIdx.x;
-  if (t == 0) s.vid = atomicAdd(g.counters + GSR_CTR_TICKET_COMPACT, 1u);
+  const size_t vo = (size_t)v * P;
+  uint32_t sum = 0u, vis = 0u;
 #pragma unroll
-  for (int p = 0; p < 4; ++p) s.hist[p][t] = 0u;
-  __syncthreads();
-  const int vid = (int)s.vid;
-  const int i0 = vid * GSR_COMPACT_TILE + t * GSR_COMPACT_ITEMS;
-  uint32_t tt[GSR_COMPACT_ITEMS];
-  if (i0 + GSR_COMPACT_ITEMS <= P) {
-    const uint4* src = reinterpret_cast<const uint4*>(g.tiles_touched + i0);
-#pragma unroll
-    for (int q = 0; q < GSR_COMPACT_ITEMS / 4; ++q) {
-      const uint4 v = src[q];
-      tt[4 * q] = v.x, tt[4 * q + 1] = v.y, tt[4 * q + 2] = v.z, tt[4 * q + 3] = v.w;
-    }
-  } else {
-#pragma unroll
-    for (int k = 0; k < GSR_COMPACT_ITEMS; ++k) tt[k] = i0 + k < P ? g.tiles_touched[i0 + k] : 0u;
+  for (int k = 0; k < GSR_DUP_ITEMS; ++k) {
+    const int r = lb * GSR_DUP_TILE + k * 256 + t;
+    const uint32_t tt = r < P ? g.tiles_touched[vo + order[vo + r]] : 0u;
+    sum += tt;
+    vis += tt > 0u ? 1u : 0u;
   }
-  uint32_t nvis = 0u, ksum = 0u;
-#pragma unroll
-  for (int k = 0; k < GSR_COMPACT_ITEMS; ++k) {
-    nvis += tt[k] > 0u ? 1u : 0u;
-    ksum += tt[k];
+  const uint32_t tot = block_sum_u32<256>(sum, s_wave);
+  const uint32_t vtot = block_sum_u32<256>(vis, s_wave);
+  if (t == 0) {
+    g.inst_counts[(size_t)v * nbe + lb] = tot;
+    g.vis_counts[(size_t)v * nbe + lb] = vtot;
   }
-  uint32_t btot;
-  const uint32_t local = block_exclusive_scan<256>(nvis, &btot, s.wave);
-  const uint32_t kblock = block_sum_u32<256>(ksum, s.wave);
-  GSR_PH_MARK(1)
-  if (t < 64) {
-    uint32_t* st = g.compact_state + vid;
-    uint32_t prefix = 0u;
-    if (vid == 0) {
-      if (t == 0) lb_publish(st, GSR_LB_INC, btot);
-    } else {
-      if (t == 0) lb_publish(st, GSR_LB_AGG, btot);
-      prefix = lb_prefix_wave(g.compact_state, vid, g.counters + GSR_CTR_ERR);
-      if (t == 0) lb_publish(st, GSR_LB_INC, prefix + btot);
-    }
-    if (t == 0) {
-      s.prefix = prefix;
-      if (btot) atomicAdd(g.counters + GSR_CTR_VISIBLE, btot);
-      if (kblock) atomicAdd(g.counters + GSR_CTR_K, kblock);
-    }
-  }
-  __syncthreads();
-  GSR_PH_MARK(2)
-  uint32_t o = s.prefix + local;
-#pragma unroll
-  for (int k = 0; k < GSR_COMPACT_ITEMS; ++k) {
-    if (tt[k] > 0u) {
-      const int i = i0 + k;
-      const uint32_t key = __float_as_uint(g.rec1[i].z);  // view depth > 0.2: float bits are monotone
-      g.dkey[0][o] = key;
-      g.dval[0][o] = (uint32_t)i;
-      ++o;
-#pragma unroll
-      for (int p = 0; p < 4; ++p) atomicAdd(&s.hist[p][(key >> (8 * p)) & 0xffu], 1u);
-    }
-  }
-  __syncthreads();
-#pragma unroll
-  for (int p = 0; p < 4; ++p) {
-    const uint32_t c = s.hist[p][t];
-    if (c) atomicAdd(g.dsort.digit_count + p * GSR_RADIX + t, c);
-  }
-  GSR_PH_STORE(GSR_PH_COMPACT, (uint32_t)vid, btot)
 }
 
-void launch_compact_visible(int P, const GeomState& g, hipStream_t stream) {
-  if (P <= 0) return;
-  hipLaunchKernelGGL(k_compact_visible, dim3(div_up(P, GSR_COMPACT_TILE)), dim3(256), 0, stream, P, g);
+// One workgroup per view: exclusive scan of its block counts in place; K_v -> counters[v],
+// visible Gaussians -> counters[V + v].
+__global__ __launch_bounds__(256) void k_inst_scan(int nbe, GeomState g) {
+  __shared__ uint32_t s_wave[8];
+  const int v = blockIdx.x, t = threadIdx.x;
+  uint32_t* row = g.inst_counts + (size_t)v * nbe;
+  uint32_t vis = 0u;
+  for (int i = t; i < nbe; i += 256) vis += g.vis_counts[(size_t)v * nbe + i];
+  vis = block_sum_u32<256>(vis, s_wave);
+  uint32_t carry = 0u;
+  for (int c0 = 0; c0 < nbe; c0 += 256 * 4) {
+    uint32_t x[4], run = 0u;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int i = c0 + 4 * t + k;
+      const uint32_t c = i < nbe ? row[i] : 0u;
+      x[k] = run;
+      run += c;
+    }
+    uint32_t tot;
+    const uint32_t off = carry + block_exclusive_scan<256>(run, &tot, s_wave);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int i = c0 + 4 * t + k;
+      if (i < nbe) row[i] = off + x[k];
+    }
+    carry += tot;
+  }
+  if (t == 0) {
+    g.counters[v] = carry;
+    g.counters[gridDim.x + v] = vis;
+  }
 }
 
-// Emit one (tile id, Gaussian) instance per tile of each visible Gaussian, in depth order, fused with
-//   * the exclusive scan of tiles_touched in depth order (block scan + decoupled look-back),
-//   * goff[g] = the Gaussian's first instance,
-//   * the digit counts of every tile-sort pass (LDS histogram, flushed with global atomics),
-//   * zeroing the per-tile ranges.
-// A block owns 1024 consecutive depth-sorted Gaussians (4 per thread); its instances are one
-// contiguous range, written cooperatively: instance j of the block is found by binary search
-// over the block's offsets in LDS, so consecutive lanes write consecutive addresses.
+// Emit one (tile id, Gaussian) instance per tile of each visible Gaussian, in depth order, and
+// goff[g] = the Gaussian's first instance.  A block owns 1024 consecutive depth-sorted Gaussians
+// of one view (4 per thread); its instances are one contiguous range (offset from k_inst_scan),
+// written cooperatively: instance j of the block belongs to the last Gaussian whose local offset
+// is <= j (binary search in LDS), so consecutive lanes write consecutive addresses.
 struct DupLDS {
   uint32_t off[GSR_DUP_TILE + 1];
   uint32_t gi[GSR_DUP_TILE];
   uint2 rect[GSR_DUP_TILE];
-  uint32_t hist[GSR_MAX_PASSES][GSR_RADIX];
   uint32_t wave[8];
-  uint32_t vid, prefix;
 };
 
-__global__ __launch_bounds__(256) void k_duplicate(int P, int grid_x, int n_tiles, int passes, int dbits,
-                                                   const uint32_t* __restrict__ order, GeomState g,
-                                                   uint32_t* __restrict__ keys, uint32_t* __restrict__ vals,
-                                                   uint32_t* dup_state, uint32_t* ticket,
-                                                   uint32_t* __restrict__ digit_count, uint2* __restrict__ ranges) {
+__global__ __launch_bounds__(256) void k_emit(int P, int nbe, int grid_x, GeomState g, const uint32_t* __restrict__ order,
+                                              SegInfo inst, uint32_t* __restrict__ keys, uint32_t* __restrict__ vals) {
   __shared__ DupLDS s;
-  GSR_PH_DECL
+  const int v = blockIdx.x / nbe, lb = blockIdx.x % nbe;
   const int t = threadIdx.x;
-  if (t == 0) s.vid = atomicAdd(ticket, 1u);
-#pragma unroll
-  for (int p = 0; p < GSR_MAX_PASSES; ++p) s.hist[p][t] = 0u;
-  __syncthreads();
-  const int vid = (int)s.vid;
-  const uint32_t n = n_of(g.counters + GSR_CTR_VISIBLE, P);
-  const uint32_t nblocks = (n + GSR_DUP_TILE - 1) / GSR_DUP_TILE;
-  for (uint32_t i = (uint32_t)vid * 256u + t; i < (uint32_t)n_tiles; i += (nblocks > 0 ? nblocks : 1u) * 256u)
-    ranges[i] = make_uint2(0u, 0u);
-  const uint32_t base = (uint32_t)vid * GSR_DUP_TILE;
-  if (base >= n) return;
-
+  const size_t vo = (size_t)v * P;
   uint32_t gi[GSR_DUP_ITEMS], cnt[GSR_DUP_ITEMS];
   uint32_t sum = 0u;
 #pragma unroll
   for (int k = 0; k < GSR_DUP_ITEMS; ++k) {
-    const uint32_t r = base + t * GSR_DUP_ITEMS + k;
-    gi[k] = r < n ? order[r] : 0u;
-    cnt[k] = r < n ? g.tiles_touched[gi[k]] : 0u;
+    const int r = lb * GSR_DUP_TILE + t * GSR_DUP_ITEMS + k;
+    gi[k] = r < P ? order[vo + r] : 0u;
+    cnt[k] = r < P ? g.tiles_touched[vo + gi[k]] : 0u;
     s.gi[t * GSR_DUP_ITEMS + k] = gi[k];
-    s.rect[t * GSR_DUP_ITEMS + k] = r < n ? g.rect[gi[k]] : make_uint2(0u, 0u);
+    s.rect[t * GSR_DUP_ITEMS + k] = cnt[k] ? g.rect[vo + gi[k]] : make_uint2(0u, 0u);
     sum += cnt[k];
   }
   uint32_t btot;
   const uint32_t local = block_exclusive_scan<256>(sum, &btot, s.wave);
-  GSR_PH_MARK(1)
-  if (t < 64) {
-    uint32_t* st = dup_state + vid;
-    uint32_t prefix = 0u;
-    if (vid == 0) {
-      if (t == 0) lb_publish(st, GSR_LB_INC, btot);
-    } else {
-      if (t == 0) lb_publish(st, GSR_LB_AGG, btot);
-      prefix = lb_prefix_wave(dup_state, vid, g.counters + GSR_CTR_ERR);
-      if (t == 0) lb_publish(st, GSR_LB_INC, prefix + btot);
-    }
-    if (t == 0) s.prefix = prefix;
-  }
+  const uint32_t prefix = g.inst_counts[(size_t)v * nbe + lb];
   {
     uint32_t o = local;
 #pragma unroll
     for (int k = 0; k < GSR_DUP_ITEMS; ++k) {
       s.off[t * GSR_DUP_ITEMS + k] = o;
+      if (cnt[k]) g.goff[vo + gi[k]] = prefix + o;
       o += cnt[k];
     }
     if (t == 255) s.off[GSR_DUP_TILE] = btot;
   }
   __syncthreads();
-  GSR_PH_MARK(2)
-  const uint32_t prefix = s.prefix;
-#pragma unroll
-  for (int k = 0; k < GSR_DUP_ITEMS; ++k)
-    if (base + t * GSR_DUP_ITEMS + k < n) g.goff[gi[k]] = prefix + s.off[t * GSR_DUP_ITEMS + k];
-  const uint32_t dmask = (1u << dbits) - 1u;
+  uint32_t* kout = keys + inst.start[v] + prefix;
+  uint32_t* vout = vals + inst.start[v] + prefix;
   for (uint32_t j = t; j < btot; j += 256u) {
-    // owner m: last m with off[m] <= j (empty owners share their successor's offset)
     int lo = 0, hi = GSR_DUP_TILE;  // off[lo] <= j < off[hi]
     while (hi - lo > 1) {
       const int mid = (lo + hi) >> 1;
@@ -199,42 +126,47 @@ __global__ __launch_bounds__(256) void k_duplicate(int P, int grid_x, int n_tile
     const uint32_t xmin = rc.x & 0xffffu, ymin = rc.x >> 16, xmax = rc.y & 0xffffu;
     const uint32_t w = xmax - xmin, l = j - s.off[lo];
     const uint32_t ty = l / w, tx = l - ty * w;
-    const uint32_t tile = (ymin + ty) * (uint32_t)grid_x + xmin + tx;
-    keys[prefix + j] = tile;
-    vals[prefix + j] = s.gi[lo];
-    for (int p = 0; p < passes; ++p) atomicAdd(&s.hist[p][(tile >> (p * dbits)) & dmask], 1u);
+    kout[j] = (ymin + ty) * (uint32_t)grid_x + xmin + tx;
+    vout[j] = s.gi[lo];
   }
-  __syncthreads();
-  for (int p = 0; p < passes; ++p) {
-    const uint32_t c = s.hist[p][t];
-    if (c) atomicAdd(digit_count + p * GSR_RADIX + t, c);
-  }
-  GSR_PH_STORE(GSR_PH_DUP, (uint32_t)vid, btot)
 }
 
-void launch_duplicate(int P, int W, int H, const uint32_t* order, const GeomState& g, const BinningState& b,
-                      uint2* ranges, hipStream_t stream) {
-  const int gx = div_up(W, GSR_TILE_X), gy = div_up(H, GSR_TILE_Y);
-  if (P <= 0) return;
-  const DigitPlan plan = digit_plan(tile_key_bits(W, H));
-  hipLaunchKernelGGL(k_duplicate, dim3(div_up(P, GSR_DUP_TILE)), dim3(256), 0, stream, P, gx, gx * gy,
-                     plan.passes, plan.bits, order, g, b.key[0], b.val[0], b.dup_state,
-                     b.tsort.tickets + 32, b.tsort.digit_count, ranges);
-}
-
-// After the tile sort: per-tile [start, end) ranges of the sorted instance list.
-__global__ __launch_bounds__(256) void k_tile_ranges(int K, const uint32_t* __restrict__ keys,
-                                                     uint2* __restrict__ ranges) {
-  const int p = blockIdx.x * blockDim.x + threadIdx.x;
+// After the tile sort: per-tile [start, end) ranges (view-local positions) of each view's list.
+__global__ __launch_bounds__(GSR_RANGE_TILE) void k_tile_ranges(SegInfo inst, int n_tiles, const uint32_t* __restrict__ keys,
+                                                                uint2* __restrict__ ranges) {
+  uint32_t lb;
+  const int v = seg_of_block(inst, blockIdx.x, lb);
+  const uint32_t p = lb * GSR_RANGE_TILE + threadIdx.x;
+  const uint32_t K = inst.n[v];
   if (p >= K) return;
-  const uint32_t tile = keys[p];
-  if (p == 0 || keys[p - 1] != tile) ranges[tile].x = (uint32_t)p;
-  if (p == K - 1 || keys[p + 1] != tile) ranges[tile].y = (uint32_t)(p + 1);
+  const uint32_t* kv = keys + inst.start[v];
+  uint2* rv = ranges + (size_t)v * n_tiles;
+  const uint32_t tile = kv[p];
+  if (p == 0 || kv[p - 1] != tile) rv[tile].x = p;
+  if (p == K - 1 || kv[p + 1] != tile) rv[tile].y = p + 1;
 }
 
-void launch_tile_ranges(int K, const uint32_t* keys, uint2* ranges, hipStream_t stream) {
-  if (K <= 0) return;
-  hipLaunchKernelGGL(k_tile_ranges, dim3((K + 255) / 256), dim3(256), 0, stream, K, keys, ranges);
+void launch_binning_counts(int V, int P, const GeomState& g, const uint32_t* order, hipStream_t stream) {
+  if (V <= 0) return;
+  const int nbe = GeomState::dup_blocks(P);
+  if (P > 0)
+    hipLaunchKernelGGL(k_inst_count, dim3(V * nbe), dim3(256), 0, stream, P, nbe, g, order);
+  hipLaunchKernelGGL(k_inst_scan, dim3(V), dim3(256), 0, stream, P > 0 ? nbe : 0, g);
+}
+
+void launch_emit(int V, int P, int W, const GeomState& g, const uint32_t* order, const SegInfo& inst,
+                 uint32_t* keys, uint32_t* vals, hipStream_t stream) {
+  if (V <= 0 || P <= 0) return;
+  const int nbe = GeomState::dup_blocks(P);
+  hipLaunchKernelGGL(k_emit, dim3(V * nbe), dim3(256), 0, stream, P, nbe, div_up(W, GSR_TILE_X), g, order, inst,
+                     keys, vals);
+}
+
+void launch_tile_ranges(SegInfo inst, int n_tiles, const uint32_t* keys, uint2* ranges, hipStream_t stream) {
+  seg_fill_blocks(inst, GSR_RANGE_TILE);
+  if (inst.blk[inst.V] == 0) return;
+  hipLaunchKernelGGL(k_tile_ranges, dim3(inst.blk[inst.V]), dim3(GSR_RANGE_TILE), 0, stream, inst, n_tiles, keys,
+                     ranges);
 }
 
 // markVisible / checkFrustum of the reference (API completeness).
@@ -258,7 +190,3 @@ void launch_mark_visible(int P, const float* means3D, const float* view, const f
 }
 
 }  // namespace gsr
-
-#ifdef GSR_TIMELINE
-GSR_PH_READER(gsr_diag_phases_bin)
-#endif

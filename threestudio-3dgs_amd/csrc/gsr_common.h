@@ -10,18 +10,19 @@
 #define GSR_TILE_Y 16
 #define GSR_TILE_PIX (GSR_TILE_X * GSR_TILE_Y)  // 256 pixels = 4 waves of 64
 
-// Radix passes: 256 threads x 8 items per block, <= 8-bit digits.
-#define GSR_SCAN_THREADS 256
-#define GSR_SCAN_ITEMS 8
-#define GSR_SCAN_TILE (GSR_SCAN_THREADS * GSR_SCAN_ITEMS)  // 2048
+// View sets: up to GSR_SET_MAX views of one Gaussian set rendered by the same launches.
+#define GSR_SET_MAX 64
+// Sort passes: 256 threads x 16 items per block, <= 8-bit digits.
+#define GSR_SORT_THREADS 256
+#define GSR_SORT_ITEMS 16
+#define GSR_SORT_TILE (GSR_SORT_THREADS * GSR_SORT_ITEMS)  // 4096
 #define GSR_RADIX_BITS 8
 #define GSR_RADIX (1 << GSR_RADIX_BITS)
-#define GSR_MAX_PASSES 4
-// Visible compaction: 256 threads x 16 Gaussians per block.  Instance emission: 256 x 4.
-#define GSR_COMPACT_ITEMS 16
-#define GSR_COMPACT_TILE (256 * GSR_COMPACT_ITEMS)  // 4096
+// Instance emission: 256 threads x 4 depth-sorted Gaussians per block.
 #define GSR_DUP_ITEMS 4
 #define GSR_DUP_TILE (256 * GSR_DUP_ITEMS)  // 1024
+// Tile ranges: one instance per thread.
+#define GSR_RANGE_TILE 256
 
 // Rasterizer constants of the reference algorithm ([EXT] graphdeco
 // cuda_rasterizer/forward.cu + auxiliary.h).
@@ -32,34 +33,6 @@
 
 namespace gsr {
 
-#ifdef GSR_TIMELINE
-// Diagnostic build only (make diag): per-block phase stamps of the sort/binning kernels.
-// Record = (t0, t1, t2, t3) s_memrealtime ticks (100 MHz), (HW_ID, XCC_ID, ticket id, extra).
-#define GSR_PH_MAX 8192
-enum { GSR_PH_COMPACT = 0, GSR_PH_SORT_DEPTH = 1, GSR_PH_SORT_TILE = 2, GSR_PH_DUP = 3, GSR_PH_KINDS = 4 };
-static __device__ uint4 g_phase_tl[GSR_PH_KINDS][GSR_PH_MAX][2];  // one copy per translation unit
-#define GSR_PH_READER(fname)                                                                           \
-  extern "C" int fname(int kind, void* host, int n) {                                                 \
-    if (kind < 0 || kind >= gsr::GSR_PH_KINDS || n > GSR_PH_MAX) return -1;                           \
-    if (hipDeviceSynchronize() != hipSuccess) return -1;                                              \
-    return hipMemcpyFromSymbol(host, HIP_SYMBOL(gsr::g_phase_tl), sizeof(uint4) * 2 * n,              \
-                               sizeof(uint4) * 2 * GSR_PH_MAX * kind, hipMemcpyDeviceToHost) == hipSuccess \
-               ? 0 : -1;                                                                              \
-  }
-#define GSR_PH_DECL uint32_t ph_t[4] = {(uint32_t)__builtin_amdgcn_s_memrealtime(), 0u, 0u, 0u};
-#define GSR_PH_MARK(i) ph_t[i] = (uint32_t)__builtin_amdgcn_s_memrealtime();
-#define GSR_PH_STORE(kind, vid, extra)                                                                   \
-  if (threadIdx.x == 0 && (vid) < GSR_PH_MAX) {                                                         \
-    ph_t[3] = (uint32_t)__builtin_amdgcn_s_memrealtime();                                               \
-    g_phase_tl[kind][vid][0] = make_uint4(ph_t[0], ph_t[1], ph_t[2], ph_t[3]);                          \
-    g_phase_tl[kind][vid][1] = make_uint4((uint32_t)__builtin_amdgcn_s_getreg((31 << 11) | 4),          \
-                                          (uint32_t)__builtin_amdgcn_s_getreg((15 << 11) | 20), (vid), (extra)); \
-  }
-#else
-#define GSR_PH_DECL
-#define GSR_PH_MARK(i)
-#define GSR_PH_STORE(kind, vid, extra)
-#endif
 
 static inline size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
 
@@ -77,8 +50,7 @@ struct Carver {
   }
 };
 
-static inline int div_up(long long a, long long b) { return (int)((a + b - 1) / b); }
-static inline int scan_blocks(long long n) { return n <= 0 ? 1 : div_up(n, GSR_SCAN_TILE); }
+__host__ __device__ static inline int div_up(long long a, long long b) { return (int)((a + b - 1) / b); }
 
 // Bits of a tile id (row-major over the 16x16 tile grid).
 static inline int tile_key_bits(int W, int H) {
@@ -104,42 +76,44 @@ static inline DigitPlan digit_plan(int key_bits) {
   return d;
 }
 
-// Zero-before-use words of one onesweep sort: digit counts [pass][256], block tickets [pass],
-// look-back states [pass][block][R] (dense, R = 2^digit bits), the last region of its sync block
-// so only the used prefix is zeroed.
-struct SortSync {
-  uint32_t* digit_count;
-  uint32_t* tickets;
-  uint32_t* states;
-  int blocks;  // look-back blocks per pass (capacity)
-  static size_t words(int blocks) { return GSR_MAX_PASSES * GSR_RADIX + 64 + (size_t)GSR_MAX_PASSES * blocks * GSR_RADIX; }
-  static SortSync carve(uint32_t* w, int blocks) {
-    SortSync s;
-    s.digit_count = w;
-    s.tickets = w + GSR_MAX_PASSES * GSR_RADIX;
-    s.states = s.tickets + 64;
-    s.blocks = blocks;
-    return s;
+// Segments of a view set (kernel argument): segment v = items [start[v], start[v] + n[v]) of a
+// flat array, cut into blocks of `tile` items; blocks of segment v are [blk[v], blk[v+1]).
+// Item counts of a set stay below 2^32 (checked on the host).
+struct SegInfo {
+  int V, tile;
+  uint32_t n[GSR_SET_MAX];
+  uint32_t start[GSR_SET_MAX];
+  uint32_t blk[GSR_SET_MAX + 1];
+};
+static inline void seg_fill_blocks(SegInfo& s, int tile) {
+  s.tile = tile;
+  s.blk[0] = 0;
+  for (int v = 0; v < s.V; ++v) s.blk[v + 1] = s.blk[v] + (uint32_t)div_up((long long)s.n[v], tile);
+}
+// block -> (segment, block within segment)
+__device__ __forceinline__ int seg_of_block(const SegInfo& s, uint32_t b, uint32_t& lb) {
+  int lo = 0, hi = s.V;  // blk[lo] <= b < blk[hi]
+  while (hi - lo > 1) {
+    const int mid = (lo + hi) >> 1;
+    if (s.blk[mid] <= b) lo = mid;
+    else hi = mid;
   }
-  // bytes from `sync_base` through the states a sort of n items with this plan touches
-  size_t used_bytes(const uint32_t* sync_base, int passes, int bits, long long n) const {
-    const size_t nb = (size_t)(n <= 0 ? 1 : (n + GSR_SCAN_TILE - 1) / GSR_SCAN_TILE);
-    return (size_t)(states - sync_base) * sizeof(uint32_t) + (size_t)passes * nb * ((size_t)1 << bits) * sizeof(uint32_t);
-  }
+  lb = b - s.blk[lo];
+  return lo;
+}
+
+// One view of a set (kernel argument): camera pointers (device, 16/16/3 floats) and tan(fov/2).
+struct ViewCam {
+  const float *view, *proj, *campos;
+  float tanx, tany;
+};
+struct SetCams {
+  ViewCam c[GSR_SET_MAX];
 };
 
-// The counters word block of a GeomState: [0] visible Gaussians, [1] K instances, [2] error flags
-// (bit 0 look-back timeout), [3] compaction ticket, [4] emission ticket.
-#define GSR_CTR_VISIBLE 0
-#define GSR_CTR_K 1
-#define GSR_CTR_ERR 2
-#define GSR_CTR_TICKET_COMPACT 3
-#define GSR_CTR_TICKET_DUP 4
-#define GSR_NUM_COUNTERS 16
-
-// Per-Gaussian forward state ("geom").  rec0/rec1/rec2 are the 48-byte render record that the
-// blend kernels gather per instance: rec0 = (px, py, conic_a, conic_b),
-// rec1 = (conic_c, opacity, view depth, 0), rec2 = (r, g, b, 0).
+// Per-(view, Gaussian) forward state of a view set ("geom"); element (v, i) at v * P + i.
+// rec0/rec1/rec2 are the 48-byte render record the blend kernels gather per instance:
+// rec0 = (px, py, conic_a, conic_b), rec1 = (conic_c, opacity, view depth, 0), rec2 = (r, g, b, 0).
 struct GeomState {
   float4* rec0;
   float4* rec1;
@@ -147,19 +121,21 @@ struct GeomState {
   uint2* rect;               // tile rect: x = xmin | ymin << 16, y = xmax | ymax << 16
   uint32_t* clamped;         // SH clamp flags, bit c = channel c clamped to 0
   uint32_t* tiles_touched;   // instances per Gaussian (0 = culled)
-  uint32_t* dkey[2];         // depth-sort ping-pong keys (float bits of view depth)
-  uint32_t* dval[2];         // depth-sort ping-pong values (Gaussian index)
-  uint32_t* goff;            // first instance (pre-tile-sort position) of each Gaussian
-  // zero-before-use region (one memset per preprocess): counters, compaction look-back, depth sort
-  uint32_t* sync;
-  size_t sync_bytes;
-  uint32_t* counters;        // GSR_CTR_*
-  uint32_t* compact_state;   // [blocks] compaction look-back
-  SortSync dsort;            // depth sort, 4 x 8-bit passes over the visible Gaussians
-  static GeomState carve(void* base, int P, size_t* bytes) {
+  uint32_t* dkey[2];         // depth sort ping-pong keys (float bits of view depth; culled = ~0)
+  uint32_t* dval[2];         // depth sort ping-pong values (Gaussian index within the view)
+  uint32_t* goff;            // first instance of each Gaussian in its view's (pre-tile-sort) list
+  uint32_t* sort_counts;     // [V][RADIX][sort blocks] per-block digit counts -> scanned offsets
+  uint32_t* sort_totals;     // [V][RADIX] digit totals
+  uint32_t* inst_counts;     // [V][emission blocks] instances per block -> scanned offsets
+  uint32_t* vis_counts;      // [V][emission blocks] visible Gaussians per block
+  uint32_t* counters;        // [0, V) instances K of each view, [V, 2V) visible Gaussians
+  static int sort_blocks(int P) { return div_up(P > 0 ? P : 1, GSR_SORT_TILE); }
+  static int dup_blocks(int P) { return div_up(P > 0 ? P : 1, GSR_DUP_TILE); }
+  static GeomState carve(void* base, int V, int P, size_t* bytes) {
     Carver c(base);
     GeomState g;
-    size_t n = (size_t)(P > 0 ? P : 1);
+    const size_t n = (size_t)(V > 0 ? V : 1) * (size_t)(P > 0 ? P : 1);
+    const size_t nv = (size_t)(V > 0 ? V : 1);
     g.rec0 = c.take<float4>(n);
     g.rec1 = c.take<float4>(n);
     g.rec2 = c.take<float4>(n);
@@ -171,83 +147,74 @@ struct GeomState {
     g.dval[0] = c.take<uint32_t>(n);
     g.dval[1] = c.take<uint32_t>(n);
     g.goff = c.take<uint32_t>(n);
-    const int ncb = div_up((long long)n, GSR_COMPACT_TILE);
-    const int nsb = scan_blocks((long long)n);
-    const size_t words = GSR_NUM_COUNTERS + align_up(ncb, 64) + SortSync::words(nsb);
-    g.sync = c.take<uint32_t>(words);
-    g.sync_bytes = words * sizeof(uint32_t);
-    g.counters = g.sync;
-    g.compact_state = g.sync + GSR_NUM_COUNTERS;
-    g.dsort = SortSync::carve(g.compact_state + align_up(ncb, 64), nsb);
+    g.sort_counts = c.take<uint32_t>(nv * GSR_RADIX * sort_blocks(P));
+    g.sort_totals = c.take<uint32_t>(nv * GSR_RADIX);
+    g.inst_counts = c.take<uint32_t>(nv * dup_blocks(P));
+    g.vis_counts = c.take<uint32_t>(nv * dup_blocks(P));
+    g.counters = c.take<uint32_t>(2 * nv + 64);
     if (bytes) *bytes = align_up(c.off, 256);
     return g;
   }
 };
 
-// Per-instance state for the K (Gaussian, tile) pairs ("binning").
+// Per-instance state of a view set ("binning"): the (tile, Gaussian) pairs of view v are
+// [start_v, start_v + K_v) with start_v = K_0 + ... + K_{v-1}.
 struct BinningState {
   uint32_t* key[2];        // tile id ping-pong
   uint32_t* val[2];        // Gaussian index ping-pong; after the sort: sorted position -> Gaussian
-  // zero-before-use region (one memset per forward render): emission look-back, tile sort
-  uint32_t* sync;
-  size_t sync_bytes;
-  uint32_t* dup_state;     // [blocks] emission look-back (visible Gaussians <= K)
-  SortSync tsort;          // stable tile sort, <= 8-bit passes over K instances
-  static BinningState carve(void* base, int K, size_t* bytes) {
+  uint32_t* sort_counts;   // [RADIX x sort blocks of all views]
+  uint32_t* sort_totals;   // [V][RADIX]
+  static BinningState carve(void* base, int V, long long Ktot, long long sort_blocks, size_t* bytes) {
     Carver c(base);
     BinningState b;
-    size_t n = (size_t)(K > 0 ? K : 1);
+    const size_t n = (size_t)(Ktot > 0 ? Ktot : 1);
     b.key[0] = c.take<uint32_t>(n);
     b.key[1] = c.take<uint32_t>(n);
     b.val[0] = c.take<uint32_t>(n);
     b.val[1] = c.take<uint32_t>(n);
-    const int ndb = div_up((long long)n, GSR_DUP_TILE);
-    const int nsb = scan_blocks((long long)n);
-    const size_t words = align_up(ndb, 64) + SortSync::words(nsb);
-    b.sync = c.take<uint32_t>(words);
-    b.sync_bytes = words * sizeof(uint32_t);
-    b.dup_state = b.sync;
-    b.tsort = SortSync::carve(b.sync + align_up(ndb, 64), nsb);
+    b.sort_counts = c.take<uint32_t>((size_t)GSR_RADIX * (size_t)(sort_blocks > 0 ? sort_blocks : 1));
+    b.sort_totals = c.take<uint32_t>((size_t)GSR_RADIX * (size_t)(V > 0 ? V : 1));
     if (bytes) *bytes = align_up(c.off, 256);
     return b;
   }
 };
 
-// Per-pixel / per-tile state ("image").
+// Per-pixel / per-tile state of a view set ("image"); view v's part at v * (tiles or H*W).
 struct ImageState {
-  uint2* ranges;       // [tiles] sorted-instance range of each tile
-  uint32_t* quad_maxc; // [4*tiles] per 8x8 quadrant: instances [0, maxc) of the tile list were blended
-  uint4* tile_info;    // [tiles] (tile maxc, depth key and Gaussian of the first unblended instance, 0)
-  float* final_T;      // [H*W]
-  uint32_t* n_contrib; // [H*W]
-  static ImageState carve(void* base, int W, int H, size_t* bytes) {
+  uint2* ranges;       // [V][tiles] sorted-instance range of each tile (view-local positions)
+  uint32_t* quad_maxc; // [V][4*tiles] per 8x8 quadrant: instances [0, maxc) of the tile list were blended
+  uint4* tile_info;    // [V][tiles] (tile maxc, depth key and Gaussian of the first unblended instance, 0)
+  float* final_T;      // [V][H*W]
+  uint32_t* n_contrib; // [V][H*W]
+  static ImageState carve(void* base, int V, int W, int H, size_t* bytes) {
     Carver c(base);
     ImageState s;
-    int tiles = div_up(W, GSR_TILE_X) * div_up(H, GSR_TILE_Y);
-    size_t pix = (size_t)W * H;
-    s.ranges = c.take<uint2>(tiles > 0 ? tiles : 1);
-    s.quad_maxc = c.take<uint32_t>(4 * (size_t)(tiles > 0 ? tiles : 1));
-    s.tile_info = c.take<uint4>(tiles > 0 ? tiles : 1);
-    s.final_T = c.take<float>(pix > 0 ? pix : 1);
-    s.n_contrib = c.take<uint32_t>(pix > 0 ? pix : 1);
+    const size_t nv = (size_t)(V > 0 ? V : 1);
+    const size_t tiles = (size_t)div_up(W, GSR_TILE_X) * div_up(H, GSR_TILE_Y);
+    const size_t pix = (size_t)W * H;
+    s.ranges = c.take<uint2>(nv * (tiles > 0 ? tiles : 1));
+    s.quad_maxc = c.take<uint32_t>(nv * 4 * (tiles > 0 ? tiles : 1));
+    s.tile_info = c.take<uint4>(nv * (tiles > 0 ? tiles : 1));
+    s.final_T = c.take<float>(nv * (pix > 0 ? pix : 1));
+    s.n_contrib = c.take<uint32_t>(nv * (pix > 0 ? pix : 1));
     if (bytes) *bytes = align_up(c.off, 256);
     return s;
   }
 };
 
-// Backward scratch: one 48-byte gradient row per (instance, 8x8 quadrant), stored at
-// 4 * slot + quadrant, slot = goff[g] + (row-major index of the tile inside the Gaussian's tile
-// rect), so each Gaussian's rows are contiguous for the per-Gaussian gather-sum:
+// Backward scratch for a group of views: one 48-byte gradient row per (instance, 8x8 quadrant),
+// stored at 4 * slot + quadrant, slot = (view's first instance within the group) + goff[g] +
+// (row-major index of the tile inside the Gaussian's tile rect), so each Gaussian's rows are
+// contiguous for the per-Gaussian gather-sum:
 //   g0 = (dmean2D.x, dmean2D.y, dconic.a, dconic.b)   [pixel units; b in the reference's half convention]
 //   g1 = (dconic.c, dopacity, dcolor.r, dcolor.g)
 //   g2 = (dcolor.b, ddepth, 0, 0)
 struct BackwardState {
-  float4* grow;  // [12*K], row r = grow[3r .. 3r+2], r = 4 * slot + quadrant
-  static BackwardState carve(void* base, int K, size_t* bytes) {
-    Carver c(base);
+  float4* grow;  // [12 * instances of the group]
+  static size_t bytes_for(long long K) { return align_up(sizeof(float4) * 12 * (size_t)(K > 0 ? K : 1), 256); }
+  static BackwardState carve(void* base) {
     BackwardState s;
-    s.grow = c.take<float4>((size_t)12 * (K > 0 ? K : 1));
-    if (bytes) *bytes = align_up(c.off, 256);
+    s.grow = (float4*)base;
     return s;
   }
 };

@@ -3,24 +3,36 @@
 // Replaces FORWARD::preprocessCUDA of the reference rasterizer [EXT]: frustum cull
 // (view z <= 0.2), projection, 3D covariance, EWA 2D covariance (+0.3 low-pass), conic,
 // 3-sigma radius, 16x16 tile rect, SH -> RGB (clamped at 0, flags kept for backward).
-// One thread per Gaussian; HBM-bound: reads 44 + 12*M bytes, writes the 48-byte render record,
-// an 8-byte tile rect, radius, clamp flags and the instance count.
+// One thread per (view, Gaussian) of a view set.  Blocks are dealt view-fastest (block b ->
+// view b % V, Gaussians 256 (b / V) ...), so the V views of one 256-Gaussian slice run together
+// and its parameters (44 + 12*M bytes per Gaussian) are fetched from HBM once per set and served
+// from L2 / MALL for the other views.  Writes per (view, Gaussian) the 48-byte render record,
+// the 8-byte tile rect, radius, clamp flags, instance count and the depth-sort key (culled: ~0,
+// which sorts after every visible depth).
 #include "gsr_kernels.h"
 #include "gsr_math.h"
 
 namespace gsr {
 
-__global__ __launch_bounds__(256) void k_preprocess(PreprocessArgs a, GeomState g) {
-  const int idx = blockIdx.x * blockDim.x + threadIdx.x;
+__global__ __launch_bounds__(256) void k_preprocess(PreprocessArgs a, SetCams cams, GeomState g) {
+  const int v = blockIdx.x % a.V;
+  const int idx = (blockIdx.x / a.V) * blockDim.x + threadIdx.x;
   if (idx >= a.P) return;
-  a.radii[idx] = 0;
-  g.tiles_touched[idx] = 0;
+  const ViewCam cam = cams.c[v];
+  const size_t vi = (size_t)v * a.P + idx;
+  a.radii[vi] = 0;
+  g.tiles_touched[vi] = 0;
+  g.dkey[0][vi] = 0xFFFFFFFFu;
+  const float* viewmatrix = cam.view;
+  const float* projmatrix = cam.proj;
+  const float tanfovx = cam.tanx, tanfovy = cam.tany;
+  const float focal_x = a.W / (2.0f * tanfovx), focal_y = a.H / (2.0f * tanfovy);
 
   const float3 p_orig = make_float3(a.means3D[3 * idx], a.means3D[3 * idx + 1], a.means3D[3 * idx + 2]);
   // near-plane cull on the view-space depth (in_frustum of the reference)
-  const float3 p_view = xform_point4x3(p_orig, a.viewmatrix);
+  const float3 p_view = xform_point4x3(p_orig, viewmatrix);
   if (p_view.z <= GSR_NEAR_CULL) return;
-  const float4 p_hom = xform_point4x4(p_orig, a.projmatrix);
+  const float4 p_hom = xform_point4x4(p_orig, projmatrix);
   const float p_w = 1.0f / (p_hom.w + 0.0000001f);
   const float3 p_proj = make_float3(p_hom.x * p_w, p_hom.y * p_w, p_hom.z * p_w);
 
@@ -36,7 +48,7 @@ __global__ __launch_bounds__(256) void k_preprocess(PreprocessArgs a, GeomState 
   }
 
   Cov2DState st;
-  const float3 cov = cov2d_ewa(p_orig, a.focal_x, a.focal_y, a.tanfovx, a.tanfovy, cov3D, a.viewmatrix, st);
+  const float3 cov = cov2d_ewa(p_orig, focal_x, focal_y, tanfovx, tanfovy, cov3D, viewmatrix, st);
   const float det = cov.x * cov.z - cov.y * cov.y;
   if (det == 0.0f) return;
   const float det_inv = 1.f / det;
@@ -65,21 +77,22 @@ __global__ __launch_bounds__(256) void k_preprocess(PreprocessArgs a, GeomState 
     rgb = make_float3(a.colors_precomp[3 * idx], a.colors_precomp[3 * idx + 1], a.colors_precomp[3 * idx + 2]);
   } else {
     rgb = sh_to_rgb(a.deg, a.shs + (size_t)idx * a.M * 3, p_orig,
-                    make_float3(a.campos[0], a.campos[1], a.campos[2]), &clamp_bits);
+                    make_float3(cam.campos[0], cam.campos[1], cam.campos[2]), &clamp_bits);
   }
 
-  g.rec0[idx] = make_float4(pimg.x, pimg.y, conic.x, conic.y);
-  g.rec1[idx] = make_float4(conic.z, a.opacities[idx], p_view.z, 0.0f);
-  g.rec2[idx] = make_float4(rgb.x, rgb.y, rgb.z, 0.0f);
-  g.rect[idx] = make_uint2((uint32_t)xmin | ((uint32_t)ymin << 16), (uint32_t)xmax | ((uint32_t)ymax << 16));
-  g.clamped[idx] = clamp_bits;
-  a.radii[idx] = r;
-  g.tiles_touched[idx] = (uint32_t)area;
+  g.rec0[vi] = make_float4(pimg.x, pimg.y, conic.x, conic.y);
+  g.rec1[vi] = make_float4(conic.z, a.opacities[idx], p_view.z, 0.0f);
+  g.rec2[vi] = make_float4(rgb.x, rgb.y, rgb.z, 0.0f);
+  g.rect[vi] = make_uint2((uint32_t)xmin | ((uint32_t)ymin << 16), (uint32_t)xmax | ((uint32_t)ymax << 16));
+  g.clamped[vi] = clamp_bits;
+  a.radii[vi] = r;
+  g.tiles_touched[vi] = (uint32_t)area;
+  g.dkey[0][vi] = __float_as_uint(p_view.z);  // > 0.2: float bits are monotone in depth
 }
 
-void launch_preprocess(const PreprocessArgs& a, const GeomState& g, hipStream_t stream) {
-  if (a.P <= 0) return;
-  hipLaunchKernelGGL(k_preprocess, dim3((a.P + 255) / 256), dim3(256), 0, stream, a, g);
+void launch_preprocess(const PreprocessArgs& a, const SetCams& cams, const GeomState& g, hipStream_t stream) {
+  if (a.P <= 0 || a.V <= 0) return;
+  hipLaunchKernelGGL(k_preprocess, dim3(a.V * ((a.P + 255) / 256)), dim3(256), 0, stream, a, cams, g);
 }
 
 }  // namespace gsr

@@ -1,19 +1,19 @@
-// gsr_render.hip — per-tile alpha blending, forward and backward.
+// gsr_render.hip — per-tile alpha blending of a view set, forward and backward.
 //
-// One 256-thread workgroup per 16x16 tile; the four waves each own an 8x8 pixel quadrant.
-// Gaussian records (48 B: xy, conic, opacity, depth, rgb) are gathered by sorted instance into
-// LDS in chunks of 256 and read back as broadcast ds_read_b128.  While staging a chunk, each
-// thread also computes a conservative 4-bit quadrant mask for its Gaussian (bounding box of the
-// alpha >= 1/255 ellipse, padded): a wave skips, with one scalar test, every Gaussian that cannot
-// reach any of its 64 pixels.  The skipped pairs are exactly pairs the reference rejects with
-// alpha < 1/255, so results are unchanged.
+// One 64-thread wave per (view, 16x16 tile, 8x8 quadrant); the views of a set are consecutive
+// ranges of the grid, so one launch blends every view and the heavy tiles of one view overlap the
+// light tiles of the others.  Gaussian records (48 B: xy, conic, opacity, depth, rgb) are gathered
+// by sorted instance in chunks of 64; a conservative quadrant test (bounding box of the
+// alpha >= 1/255 ellipse, padded) drops Gaussians that cannot reach the wave's pixels before they
+// are compacted into LDS (ballot) and read back as broadcast ds_read_b128.  The dropped pairs are
+// exactly pairs the reference rejects with alpha < 1/255, so results are unchanged.
 //
 // Forward replaces FORWARD::renderCUDA [EXT] (ashawkey 4-output: color, depth = sum z a T,
 // alpha = 1 - T).  Backward replaces BACKWARD::renderCUDA [EXT]: instead of 9 global float atomics
-// per (pixel, Gaussian) pair it reduces each pair's 10 gradient terms over 16-lane rows with DPP,
-// parks the 16 row partials per Gaussian in LDS, and every 32 Gaussians sums them and writes ONE
-// 48-byte row per instance into the Gaussian's own slot (gsr_backward.hip sums a Gaussian's rows in
-// a fixed order -> deterministic, no atomics, no inverse permutation).
+// per (pixel, Gaussian) pair it reduces each pair's gradient moments over 16-lane rows with DPP,
+// parks the 4 row partials per Gaussian in LDS, and every 32 Gaussians sums them and writes ONE
+// 48-byte row per (instance, quadrant) into the Gaussian's own slot (gsr_backward.hip sums a
+// Gaussian's rows in a fixed order -> deterministic, no atomics, no inverse permutation).
 #include "gsr_kernels.h"
 #include "gsr_wave.h"
 
@@ -85,13 +85,12 @@ __device__ __forceinline__ bool quadrant_hit(const float4 r0, const float4 r1, f
 // Gaussians whose alpha >= 1/255 ellipse can reach its quadrant, and blends them with a
 // branch-free predicated body.  No workgroup barriers couple quadrants that terminate at
 // different depths, and 4x more independent waves balance the load across the 256 CUs.
-__global__ __launch_bounds__(64) void k_render_fwd(int W, int H, int grid_x, int grid_y,
+__global__ __launch_bounds__(64) void k_render_fwd(RenderSet rs,
                                                    const uint2* __restrict__ ranges,
                                                    const uint32_t* __restrict__ sorted_gauss,
                                                    const float4* __restrict__ rec0,
                                                    const float4* __restrict__ rec1,
                                                    const float4* __restrict__ rec2,
-                                                   const float* __restrict__ bg,
                                                    float* __restrict__ out_color,
                                                    float* __restrict__ out_depth,
                                                    float* __restrict__ out_alpha,
@@ -100,9 +99,27 @@ __global__ __launch_bounds__(64) void k_render_fwd(int W, int H, int grid_x, int
                                                    uint32_t* __restrict__ quad_maxc) {
   __shared__ float4 s0[64], s1[64], s2[64];
   __shared__ uint32_t s_idx[64];
+  const int U = unit_grid(rs.gx, rs.gy);
+  const int v = blockIdx.x / U;
   int tile, q;
-  if (!unit_of_block(blockIdx.x, grid_x, grid_y, tile, q)) return;
+  if (!unit_of_block(blockIdx.x - v * U, rs.gx, rs.gy, tile, q)) return;
   GSR_TL_BEGIN
+  const int W = rs.W, H = rs.H, grid_x = rs.gx;
+  {
+    const size_t vg = (size_t)(rs.v0 + v), tiles = (size_t)rs.gx * rs.gy, HWs = (size_t)W * H;
+    ranges += vg * tiles;
+    quad_maxc += vg * 4 * tiles;
+    sorted_gauss += rs.inst_start[v];
+    rec0 += vg * rs.P;
+    rec1 += vg * rs.P;
+    rec2 += vg * rs.P;
+    out_color += vg * 3 * HWs;
+    out_depth += vg * HWs;
+    out_alpha += vg * HWs;
+    final_T += vg * HWs;
+    n_contrib += vg * HWs;
+  }
+  const float* bg = rs.bg[v];
   const int unit = 4 * tile + q;
   const int lane = threadIdx.x;
   const int qx0 = (tile % grid_x) * GSR_TILE_X + (q & 1) * 8;
@@ -182,13 +199,24 @@ __global__ __launch_bounds__(64) void k_render_fwd(int W, int H, int grid_x, int
 // (depth key, Gaussian) of the first instance nobody blended.  The backward writes gradient rows
 // for exactly the instances [0, maxc) of each tile (all 4 quadrants), so the per-Gaussian
 // gather-sum can test validity per instance against this cutoff.
-__global__ __launch_bounds__(256) void k_tile_info(int n_tiles, const uint2* __restrict__ ranges,
+__global__ __launch_bounds__(256) void k_tile_info(RenderSet rs, const uint2* __restrict__ ranges,
                                                    const uint32_t* __restrict__ quad_maxc,
                                                    const uint32_t* __restrict__ sorted_gauss,
                                                    const float4* __restrict__ rec1,
                                                    uint4* __restrict__ tile_info) {
-  const int tile = blockIdx.x * blockDim.x + threadIdx.x;
+  const int n_tiles = rs.gx * rs.gy;
+  const int nb = div_up(n_tiles, 256);
+  const int v = blockIdx.x / nb;
+  const int tile = (blockIdx.x - v * nb) * blockDim.x + threadIdx.x;
   if (tile >= n_tiles) return;
+  {
+    const size_t vg = (size_t)(rs.v0 + v);
+    ranges += vg * n_tiles;
+    quad_maxc += vg * 4 * n_tiles;
+    tile_info += vg * n_tiles;
+    sorted_gauss += rs.inst_start[v];
+    rec1 += vg * rs.P;
+  }
   const uint4 m = reinterpret_cast<const uint4*>(quad_maxc)[tile];
   const uint32_t maxc = max(max(m.x, m.y), max(m.z, m.w));
   const uint2 range = ranges[tile];
@@ -201,17 +229,16 @@ __global__ __launch_bounds__(256) void k_tile_info(int n_tiles, const uint2* __r
   tile_info[tile] = info;
 }
 
-void launch_render_forward(int W, int H, const GeomState& g, const uint32_t* sorted_gauss,
-                           const ImageState& img, const float* bg, float* out_color,
-                           float* out_depth, float* out_alpha, hipStream_t stream) {
-  const int gx = div_up(W, GSR_TILE_X), gy = div_up(H, GSR_TILE_Y);
-  const int nt = gx * gy;
-  if (nt <= 0) return;
-  hipLaunchKernelGGL(k_render_fwd, dim3(unit_grid(gx, gy)), dim3(64), 0, stream, W, H, gx, gy,
+void launch_render_forward(const RenderSet& rs, const GeomState& g, const uint32_t* sorted_gauss,
+                           const ImageState& img, float* out_color, float* out_depth, float* out_alpha,
+                           hipStream_t stream) {
+  const int nt = rs.gx * rs.gy;
+  if (nt <= 0 || rs.V <= 0) return;
+  hipLaunchKernelGGL(k_render_fwd, dim3(rs.V * unit_grid(rs.gx, rs.gy)), dim3(64), 0, stream, rs,
                      (const uint2*)img.ranges, sorted_gauss, (const float4*)g.rec0,
-                     (const float4*)g.rec1, (const float4*)g.rec2, bg, out_color, out_depth, out_alpha,
+                     (const float4*)g.rec1, (const float4*)g.rec2, out_color, out_depth, out_alpha,
                      img.final_T, img.n_contrib, img.quad_maxc);
-  hipLaunchKernelGGL(k_tile_info, dim3(div_up(nt, 256)), dim3(256), 0, stream, nt,
+  hipLaunchKernelGGL(k_tile_info, dim3(rs.V * div_up(nt, 256)), dim3(256), 0, stream, rs,
                      (const uint2*)img.ranges, (const uint32_t*)img.quad_maxc, sorted_gauss,
                      (const float4*)g.rec1, img.tile_info);
 }
@@ -237,7 +264,7 @@ __device__ __forceinline__ void row_reduce_step(float (&v)[NGV]) {
 // row per (instance, quadrant) at 4 * slot + quadrant, where slot is the instance's place in its
 // Gaussian's contiguous row range.  Instances the quadrant skips get zero rows, so every instance
 // above the tile cutoff has all 4 rows written.
-__global__ __launch_bounds__(64) void k_render_bwd(int W, int H, int grid_x, int grid_y,
+__global__ __launch_bounds__(64) void k_render_bwd(RenderSet rs,
                                                    const uint2* __restrict__ ranges,
                                                    const uint32_t* __restrict__ quad_maxc,
                                                    const uint32_t* __restrict__ sorted_gauss,
@@ -246,7 +273,6 @@ __global__ __launch_bounds__(64) void k_render_bwd(int W, int H, int grid_x, int
                                                    const float4* __restrict__ rec2,
                                                    const uint2* __restrict__ rect,
                                                    const uint32_t* __restrict__ goff,
-                                                   const float* __restrict__ bg,
                                                    const float* __restrict__ final_Ts,
                                                    const uint32_t* __restrict__ n_contrib,
                                                    const float* __restrict__ dL_dcolor,
@@ -256,9 +282,30 @@ __global__ __launch_bounds__(64) void k_render_bwd(int W, int H, int grid_x, int
   __shared__ float4 s0[64], s1[64], s2[64];
   __shared__ uint32_t s_dest[64], s_rel[64];
   __shared__ float4 s_part[BWD_SUB][4][3];
+  const int U = unit_grid(rs.gx, rs.gy);
+  const int v = blockIdx.x / U;
   int tile, q;
-  if (!unit_of_block(blockIdx.x, grid_x, grid_y, tile, q)) return;
+  if (!unit_of_block(blockIdx.x - v * U, rs.gx, rs.gy, tile, q)) return;
   GSR_TL_BEGIN
+  const int W = rs.W, H = rs.H, grid_x = rs.gx;
+  {
+    const size_t vg = (size_t)(rs.v0 + v), tiles = (size_t)rs.gx * rs.gy, HWs = (size_t)W * H;
+    ranges += vg * tiles;
+    quad_maxc += vg * 4 * tiles;
+    sorted_gauss += rs.inst_start[v];
+    rec0 += vg * rs.P;
+    rec1 += vg * rs.P;
+    rec2 += vg * rs.P;
+    rect += vg * rs.P;
+    goff += vg * rs.P;
+    final_Ts += vg * HWs;
+    n_contrib += vg * HWs;
+    dL_dcolor += (size_t)v * 3 * HWs;
+    if (dL_ddepth) dL_ddepth += (size_t)v * HWs;
+    if (dL_dalpha) dL_dalpha += (size_t)v * HWs;
+    grow += (size_t)12 * rs.row_start[v];
+  }
+  const float* bg = rs.bg[v];
   int tl_work = 0;
   const int unit = 4 * tile + q;
   const int lane = threadIdx.x;
@@ -422,17 +469,15 @@ __global__ __launch_bounds__(64) void k_render_bwd(int W, int H, int grid_x, int
   (void)tl_work;
 }
 
-void launch_render_backward(int W, int H, int K, const GeomState& g, const uint32_t* sorted_gauss,
-                            const ImageState& img, const float* bg, const float* dL_dcolor,
-                            const float* dL_ddepth, const float* dL_dalpha,
-                            const BackwardState& bw, hipStream_t stream) {
-  const int gx = div_up(W, GSR_TILE_X), gy = div_up(H, GSR_TILE_Y);
-  const int nt = gx * gy;
-  if (nt <= 0 || K <= 0) return;
-  hipLaunchKernelGGL(k_render_bwd, dim3(unit_grid(gx, gy)), dim3(64), 0, stream, W, H, gx, gy,
+void launch_render_backward(const RenderSet& rs, const GeomState& g, const uint32_t* sorted_gauss,
+                            const ImageState& img, const float* dL_dcolor, const float* dL_ddepth,
+                            const float* dL_dalpha, const BackwardState& bw, hipStream_t stream) {
+  const int nt = rs.gx * rs.gy;
+  if (nt <= 0 || rs.V <= 0) return;
+  hipLaunchKernelGGL(k_render_bwd, dim3(rs.V * unit_grid(rs.gx, rs.gy)), dim3(64), 0, stream, rs,
                      (const uint2*)img.ranges, (const uint32_t*)img.quad_maxc, sorted_gauss,
                      (const float4*)g.rec0, (const float4*)g.rec1, (const float4*)g.rec2,
-                     (const uint2*)g.rect, (const uint32_t*)g.goff, bg, (const float*)img.final_T,
+                     (const uint2*)g.rect, (const uint32_t*)g.goff, (const float*)img.final_T,
                      (const uint32_t*)img.n_contrib, dL_dcolor, dL_ddepth, dL_dalpha, bw.grow);
 }
 

@@ -1,163 +1,203 @@
-// gsr_sort.hip — stable LSD radix sort of (key, value) pairs, one launch per digit pass.
+// gsr_sort.hip — view-segmented stable LSD radix sort of (key, value) pairs.
 //
-// Replaces cub::DeviceRadixSort::SortPairs of the reference rasterizer [EXT].
-// Each pass is a single "onesweep" launch: the digit counts of the whole input come from the
-// producer kernel that wrote the keys (compaction / instance emission build them while the keys
-// are in registers), so a pass only has to
-//   1. load a 2048-item tile (striped: item k of thread t at base + k*256 + t, coalesced),
-//   2. rank it stably inside the block (ballot digit matching per wave + per-wave counts),
-//   3. publish the block's per-digit counts and resolve its per-digit global offsets by
-//      decoupled look-back over the preceding blocks (gsr_wave.h),
-//   4. reorder the tile in LDS by digit and write it out in digit runs.
-// HBM traffic per pass: 8 B read + 8 B written per pair, plus R words of look-back state per
-// 2048 pairs.  The previous design needed a histogram launch and a 3-launch scan per pass.
+// Replaces cub::DeviceRadixSort::SortPairs of the reference rasterizer [EXT],
+// which sorts one view at a time.  Here every view of a set is sorted by the same launches: the
+// flat array holds one segment per view and each pass is reduce-then-scan over all segments:
+//   count   : per 4096-item block, the digit histogram        -> counts[seg][digit][block]
+//   scan    : per (segment, digit) row, exclusive scan over the segment's blocks; row total
+//   scatter : per block, stable in-block ranking, global offset = scan(totals)[digit] +
+//             counts[seg][digit][block] + rank; reorder in LDS; write digit runs.
+// No block ever waits on another (no look-back, no spinning, no memsets): on MI355X a
+// cross-workgroup hand-off is a cross-XCD round trip (≈1-3 µs), which made single-pass
+// look-back chains the critical path (profiles/diag_sort.py).  HBM traffic per pass:
+// 4 B (count) + 8 B read + 8 B written per pair, plus 4 B x 256 per 4096 pairs of counts.
+//
+// In-block ranking is wave-blocked: wave w owns items [1024 w, 1024 w + 1024) of its block and
+// walks them in 16 rounds of 64; a lane's rank among equal digits comes from ballot matching,
+// the wave's running count per digit lives in LDS and is touched only by that wave, so the 16
+// rounds need no workgroup barrier.  Order (wave, round, lane) = index order -> stable.
 #include "gsr_kernels.h"
 #include "gsr_wave.h"
 
 namespace gsr {
 
-__device__ __forceinline__ uint32_t count_of(const uint32_t* n_dev, int n_max) {
-  if (n_dev == nullptr) return (uint32_t)n_max;
-  const uint32_t n = *n_dev;
-  return n < (uint32_t)n_max ? n : (uint32_t)n_max;
-}
-
-struct OnesweepLDS {
-  uint32_t keys[GSR_SCAN_TILE];
-  uint32_t vals[GSR_SCAN_TILE];
-  uint32_t cnt[GSR_SCAN_THREADS / 64][GSR_RADIX];
-  uint32_t run[GSR_RADIX];    // block-local running count per digit
-  uint32_t glob[GSR_RADIX];   // global position of this block's first item of each digit
-  uint32_t local[GSR_RADIX];  // block-local start of each digit
-  uint32_t wave[8];
-  uint32_t vid;
-};
-
-__global__ __launch_bounds__(GSR_SCAN_THREADS) void k_onesweep(
-    const uint32_t* __restrict__ keys_in, const uint32_t* __restrict__ vals_in,
-    uint32_t* __restrict__ keys_out, uint32_t* __restrict__ vals_out, const uint32_t* n_dev, int n_max,
-    int shift, int bits, const uint32_t* __restrict__ digit_count, uint32_t* state, uint32_t* ticket,
-    uint32_t* err) {
-  __shared__ OnesweepLDS s;
-  GSR_PH_DECL
-  const int t = threadIdx.x, w = t >> 6;
-  if (t == 0) s.vid = atomicAdd(ticket, 1u);
-  __syncthreads();
-  const int vid = (int)s.vid;
-  const uint32_t n = count_of(n_dev, n_max);
-  const uint32_t base = (uint32_t)vid * GSR_SCAN_TILE;
-  if (base >= n) return;
+__global__ __launch_bounds__(GSR_SORT_THREADS) void k_seg_count(const uint32_t* __restrict__ keys, SegInfo seg,
+                                                                int shift, int bits,
+                                                                uint32_t* __restrict__ counts) {
+  __shared__ uint32_t s_hist[GSR_RADIX];
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  uint32_t lb;
+  const int v = seg_of_block(seg, blockIdx.x, lb);
+  const uint32_t n = seg.n[v];
+  const uint32_t* src = keys + seg.start[v];
   const uint32_t mask = (1u << bits) - 1u;
   const int R = 1 << bits;
-
-  uint32_t key[GSR_SCAN_ITEMS], val[GSR_SCAN_ITEMS];
+  s_hist[t] = 0u;
+  __syncthreads();
+  const uint32_t b0 = lb * GSR_SORT_TILE + w * (GSR_SORT_TILE / 4);
+  uint32_t key[GSR_SORT_ITEMS];
 #pragma unroll
-  for (int k = 0; k < GSR_SCAN_ITEMS; ++k) {
-    const uint32_t i = base + k * GSR_SCAN_THREADS + t;
-    const bool valid = i < n;
-    key[k] = valid ? keys_in[i] : 0u;
-    val[k] = valid ? (vals_in ? vals_in[i] : i) : 0u;
+  for (int k = 0; k < GSR_SORT_ITEMS; ++k) {
+    const uint32_t i = b0 + k * 64 + lane;
+    key[k] = i < n ? src[i] : 0u;
   }
-  // global start of each digit = exclusive scan of the pass's digit counts
-  uint32_t tot;
-  const uint32_t gstart = block_exclusive_scan<GSR_SCAN_THREADS>(t < R ? digit_count[t] : 0u, &tot, s.wave);
-  s.run[t] = 0u;
-
-  uint32_t pos[GSR_SCAN_ITEMS];
 #pragma unroll
-  for (int k = 0; k < GSR_SCAN_ITEMS; ++k) {
-    const bool valid = base + k * GSR_SCAN_THREADS + t < n;
+  for (int k = 0; k < GSR_SORT_ITEMS; ++k) {
+    const bool valid = b0 + k * 64 + lane < n;
     const uint32_t d = (key[k] >> shift) & mask;
+    const unsigned long long peers = match_digit(d, bits, valid);
+    if (valid && mask_rank(peers) == 0) atomicAdd(&s_hist[d], (uint32_t)__popcll(peers));
+  }
+  __syncthreads();
+  if (t < R) {
+    const uint32_t nb = seg.blk[v + 1] - seg.blk[v];
+    counts[(size_t)R * seg.blk[v] + (size_t)t * nb + lb] = s_hist[t];
+  }
+}
+
+// One workgroup per (segment, digit) row: exclusive scan of the row in place, total -> totals.
+__global__ __launch_bounds__(256) void k_seg_scan(SegInfo seg, int R, uint32_t* __restrict__ counts,
+                                                  uint32_t* __restrict__ totals) {
+  __shared__ uint32_t s_wave[8];
+  const int v = blockIdx.x / R, d = blockIdx.x % R;
+  const int t = threadIdx.x;
+  const uint32_t nb = seg.blk[v + 1] - seg.blk[v];
+  uint32_t* row = counts + (size_t)R * seg.blk[v] + (size_t)d * nb;
+  uint32_t carry = 0u;
+  for (uint32_t c0 = 0; c0 < nb; c0 += 256 * 4) {
+    // thread t owns 4 consecutive entries of this 1024-entry chunk
+    uint32_t x[4], run = 0u;
 #pragma unroll
-    for (int ww = 0; ww < GSR_SCAN_THREADS / 64; ++ww) s.cnt[ww][t] = 0u;
+    for (int k = 0; k < 4; ++k) {
+      const uint32_t i = c0 + 4 * t + k;
+      const uint32_t c = i < nb ? row[i] : 0u;
+      x[k] = run;
+      run += c;
+    }
+    uint32_t tot;
+    const uint32_t off = carry + block_exclusive_scan<256>(run, &tot, s_wave);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const uint32_t i = c0 + 4 * t + k;
+      if (i < nb) row[i] = off + x[k];
+    }
+    carry += tot;
+  }
+  if (t == 0) totals[(size_t)v * GSR_RADIX + d] = carry;
+}
+
+struct ScatterLDS {
+  uint32_t keys[GSR_SORT_TILE];
+  uint32_t vals[GSR_SORT_TILE];
+  uint32_t wcnt[4][GSR_RADIX];  // per-wave running count per digit -> per-wave offset within the digit
+  uint32_t local[GSR_RADIX];    // block-local start of each digit
+  uint32_t glob[GSR_RADIX];     // segment position of this block's first item of each digit
+  uint32_t wave[8];
+};
+
+__global__ __launch_bounds__(GSR_SORT_THREADS) void k_seg_scatter(
+    const uint32_t* __restrict__ keys_in, const uint32_t* __restrict__ vals_in, uint32_t* __restrict__ keys_out,
+    uint32_t* __restrict__ vals_out, SegInfo seg, int shift, int bits, const uint32_t* __restrict__ counts,
+    const uint32_t* __restrict__ totals) {
+  __shared__ ScatterLDS s;
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  uint32_t lb;
+  const int v = seg_of_block(seg, blockIdx.x, lb);
+  const uint32_t n = seg.n[v];
+  const uint32_t start = seg.start[v];
+  const uint32_t mask = (1u << bits) - 1u;
+  const int R = 1 << bits;
+#pragma unroll
+  for (int ww = 0; ww < 4; ++ww) s.wcnt[ww][t] = 0u;
+  const uint32_t b0 = lb * GSR_SORT_TILE + w * (GSR_SORT_TILE / 4);
+  uint32_t key[GSR_SORT_ITEMS], val[GSR_SORT_ITEMS], pos[GSR_SORT_ITEMS];
+#pragma unroll
+  for (int k = 0; k < GSR_SORT_ITEMS; ++k) {
+    const uint32_t i = b0 + k * 64 + lane;
+    key[k] = i < n ? keys_in[start + i] : 0u;
+    val[k] = i < n ? (vals_in ? vals_in[start + i] : i) : 0u;
+  }
+  __syncthreads();
+#pragma unroll
+  for (int k = 0; k < GSR_SORT_ITEMS; ++k) {
+    const bool valid = b0 + k * 64 + lane < n;
+    const uint32_t d = (key[k] >> shift) & mask;
     const unsigned long long peers = match_digit(d, bits, valid);
     const uint32_t rank = mask_rank(peers);
-    __syncthreads();
-    if (valid && rank == 0) s.cnt[w][d] = (uint32_t)__popcll(peers);
-    __syncthreads();
-    if (t < R) {
-      uint32_t run = s.run[t];
-#pragma unroll
-      for (int ww = 0; ww < GSR_SCAN_THREADS / 64; ++ww) {
-        const uint32_t c = s.cnt[ww][t];
-        s.cnt[ww][t] = run;
-        run += c;
-      }
-      s.run[t] = run;
+    uint32_t base = 0u;
+    if (valid && rank == 0) {
+      base = s.wcnt[w][d];
+      s.wcnt[w][d] = base + (uint32_t)__popcll(peers);
     }
-    __syncthreads();
-    pos[k] = s.cnt[w][d] + rank;
-    __syncthreads();
+    const int leader = peers ? (int)__builtin_ctzll(peers) : lane;
+    base = (uint32_t)__shfl((int)base, leader, 64);
+    pos[k] = base + rank;
   }
-
-  // this block's count per digit -> look-back -> global offsets
-  GSR_PH_MARK(1)
-  const uint32_t own = t < R ? s.run[t] : 0u;
-  if (t < R) {
-    uint32_t* st = state + (size_t)vid * R + t;
-    uint32_t prefix = 0u;
-    if (vid == 0) {
-      lb_publish(st, GSR_LB_INC, own);
-    } else {
-      lb_publish(st, GSR_LB_AGG, own);
-      prefix = lb_prefix_serial(state + t, (size_t)R, vid, err);
-      lb_publish(st, GSR_LB_INC, prefix + own);
-    }
-    s.glob[t] = gstart + prefix;
-  }
-  uint32_t btot;
-  const uint32_t lstart = block_exclusive_scan<GSR_SCAN_THREADS>(own, &btot, s.wave);
-  if (t < R) s.local[t] = lstart;
   __syncthreads();
-  GSR_PH_MARK(2)
-  // reorder by digit in LDS, then write digit runs (consecutive lanes -> consecutive addresses)
+  // per digit: wave offsets, block count, block-local start, segment position of the block's run
+  uint32_t bc = 0u;
+  if (t < R) {
 #pragma unroll
-  for (int k = 0; k < GSR_SCAN_ITEMS; ++k) {
-    if (base + k * GSR_SCAN_THREADS + t < n) {
+    for (int ww = 0; ww < 4; ++ww) {
+      const uint32_t c = s.wcnt[ww][t];
+      s.wcnt[ww][t] = bc;
+      bc += c;
+    }
+  }
+  uint32_t tot;
+  const uint32_t lstart = block_exclusive_scan<GSR_SORT_THREADS>(bc, &tot, s.wave);
+  const uint32_t dtot = t < R ? totals[(size_t)v * GSR_RADIX + t] : 0u;
+  const uint32_t dstart = block_exclusive_scan<GSR_SORT_THREADS>(dtot, &tot, s.wave);
+  if (t < R) {
+    const uint32_t nb = seg.blk[v + 1] - seg.blk[v];
+    s.local[t] = lstart;
+    s.glob[t] = dstart + counts[(size_t)R * seg.blk[v] + (size_t)t * nb + lb];
+  }
+  __syncthreads();
+#pragma unroll
+  for (int k = 0; k < GSR_SORT_ITEMS; ++k) {
+    if (b0 + k * 64 + lane < n) {
       const uint32_t d = (key[k] >> shift) & mask;
-      const uint32_t lp = s.local[d] + pos[k];
+      const uint32_t lp = s.local[d] + s.wcnt[w][d] + pos[k];
       s.keys[lp] = key[k];
       s.vals[lp] = val[k];
     }
   }
   __syncthreads();
-  const uint32_t nv = min((uint32_t)GSR_SCAN_TILE, n - base);
+  const uint32_t nv = min((uint32_t)GSR_SORT_TILE, n - lb * GSR_SORT_TILE);
 #pragma unroll
-  for (int k = 0; k < GSR_SCAN_ITEMS; ++k) {
-    const uint32_t j = k * GSR_SCAN_THREADS + t;
+  for (int k = 0; k < GSR_SORT_ITEMS; ++k) {
+    const uint32_t j = k * GSR_SORT_THREADS + t;
     if (j < nv) {
       const uint32_t kk = s.keys[j];
       const uint32_t d = (kk >> shift) & mask;
-      const uint32_t dst = s.glob[d] + (j - s.local[d]);
+      const uint32_t dst = start + s.glob[d] + (j - s.local[d]);
       keys_out[dst] = kk;
       vals_out[dst] = s.vals[j];
     }
   }
-  GSR_PH_STORE(n_dev ? GSR_PH_SORT_DEPTH : GSR_PH_SORT_TILE, (uint32_t)vid, (uint32_t)shift)
 }
 
-
-
-int onesweep_sort(uint32_t* keys[2], uint32_t* vals[2], bool vals_identity, const uint32_t* n_dev, int n_max,
-                  int key_bits, const SortSync& sync, uint32_t* err, hipStream_t stream) {
+int seg_sort(uint32_t* keys[2], uint32_t* vals[2], bool vals_identity, SegInfo seg, int key_bits,
+             uint32_t* counts, uint32_t* totals, hipStream_t stream) {
   const DigitPlan plan = digit_plan(key_bits);
-  const int nb = scan_blocks(n_max);
+  seg_fill_blocks(seg, GSR_SORT_TILE);
+  const uint32_t nb = seg.blk[seg.V];
   int src = 0;
   for (int p = 0; p < plan.passes; ++p) {
     const int bits = plan.width(p, key_bits);
     const int dst = src ^ 1;
-    if (n_max > 0)
-      hipLaunchKernelGGL(k_onesweep, dim3(nb), dim3(GSR_SCAN_THREADS), 0, stream, (const uint32_t*)keys[src],
+    if (nb > 0) {
+      hipLaunchKernelGGL(k_seg_count, dim3(nb), dim3(GSR_SORT_THREADS), 0, stream, (const uint32_t*)keys[src], seg,
+                         p * plan.bits, bits, counts);
+      hipLaunchKernelGGL(k_seg_scan, dim3(seg.V << bits), dim3(256), 0, stream, seg, 1 << bits, counts, totals);
+      hipLaunchKernelGGL(k_seg_scatter, dim3(nb), dim3(GSR_SORT_THREADS), 0, stream, (const uint32_t*)keys[src],
                          (const uint32_t*)((p == 0 && vals_identity) ? nullptr : vals[src]), keys[dst], vals[dst],
-                         n_dev, n_max, p * plan.bits, bits, (const uint32_t*)(sync.digit_count + p * GSR_RADIX),
-                         sync.states + (size_t)p * nb * ((size_t)1 << plan.bits), sync.tickets + p, err);
+                         seg, p * plan.bits, bits, (const uint32_t*)counts, (const uint32_t*)totals);
+    }
     src = dst;
   }
   return src;
 }
 
 }  // namespace gsr
-
-#ifdef GSR_TIMELINE
-GSR_PH_READER(gsr_diag_phases_sort)
-#endif

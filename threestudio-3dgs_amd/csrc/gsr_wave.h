@@ -91,74 +91,4 @@ __device__ __forceinline__ uint32_t wave_sum_u32(uint32_t v) {
   return v;
 }
 
-// ---- decoupled look-back over single-word states -------------------------------------------
-// A state word is flag (bits 31:30; 0 = not yet published, AGG = this block's own count,
-// INC = inclusive prefix through this block) | count (bits 29:0).  Flag and payload share one
-// word, so relaxed agent-scope atomics (global_store/load ... sc1: write-through, L1-bypassing,
-// coherent across the XCDs' L2s) are the whole protocol (MI355X_MICROARCH.md, inter-workgroup
-// visibility).  Block ids come from a ticket (atomicAdd) so every predecessor a block waits on
-// is already resident.  Spins are bounded: on timeout the error word is set and the result is
-// garbage instead of a hung GPU.  States and tickets are zeroed by a memset before each launch.
-#define GSR_LB_AGG 1u
-#define GSR_LB_INC 2u
-#define GSR_LB_MASK 0x3FFFFFFFu
-#define GSR_LB_SPIN_LIMIT (1 << 22)
-
-__device__ __forceinline__ void lb_publish(uint32_t* p, uint32_t flag, uint32_t v) {
-  __hip_atomic_store(p, (flag << 30) | v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ uint32_t lb_poll(const uint32_t* p) {
-  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-
-// One lane: exclusive prefix of block `blk` on one channel (state of block p at st[p * stride]).
-__device__ inline uint32_t lb_prefix_serial(const uint32_t* st, size_t stride, int blk, uint32_t* err) {
-  uint32_t sum = 0;
-  int spins = 0;
-  for (int p = blk - 1; p >= 0;) {
-    const uint32_t w = lb_poll(st + (size_t)p * stride);
-    const uint32_t f = w >> 30;
-    if (f == 0) {
-      if (++spins > GSR_LB_SPIN_LIMIT) {
-        atomicOr(err, 1u);
-        break;
-      }
-      continue;
-    }
-    sum += w & GSR_LB_MASK;
-    if (f == GSR_LB_INC) break;
-    --p;
-  }
-  return sum;
-}
-
-// One whole wave: exclusive prefix of block `blk` (states st[p]); lane l inspects block
-// end-1-l of each 64-block window, so one round trip covers 64 predecessors.
-__device__ inline uint32_t lb_prefix_wave(const uint32_t* st, int blk, uint32_t* err) {
-  const int lane = threadIdx.x & 63;
-  uint32_t sum = 0;
-  int spins = 0;
-  for (int end = blk; end > 0; end -= 64) {
-    const int p = end - 1 - lane;
-    uint32_t w = p >= 0 ? lb_poll(st + p) : (GSR_LB_INC << 30);
-    for (;;) {
-      const unsigned long long inc = __ballot((w >> 30) == GSR_LB_INC);
-      const unsigned long long pending = __ballot((w >> 30) == 0u);
-      const int first = inc ? (int)__builtin_ctzll(inc) : 63;
-      const unsigned long long need = first == 63 ? ~0ull : ((2ull << first) - 1ull);
-      if ((pending & need) == 0ull) {
-        sum += wave_sum_u32(lane <= first ? (w & GSR_LB_MASK) : 0u);
-        if (inc) return sum;
-        break;
-      }
-      if (++spins > GSR_LB_SPIN_LIMIT) {
-        if (lane == 0) atomicOr(err, 1u);
-        return sum;
-      }
-      if ((w >> 30) == 0u) w = lb_poll(st + p);
-    }
-  }
-  return sum;
-}
-
 }  // namespace gsr

@@ -50,13 +50,22 @@ SIGNATURES = {
          _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp],
     ),
     "gsr_mark_visible": (_i, [_i, _vp, _vp, _vp, _vp, _vp]),
-    "gsr_num_rendered_many": (_i, [_i, ctypes.POINTER(_vp), _i, ctypes.POINTER(_i), _vp]),
-    "gsr_backward_render": (_i, [_i, _i, _i, _i, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
-    "gsr_backward_gaussians_many": (
+    "gsr_set_geom_bytes": (_sz, [_i, _i]),
+    "gsr_set_binning_bytes": (_sz, [_i, ctypes.POINTER(_i), _i, _i]),
+    "gsr_set_image_bytes": (_sz, [_i, _i, _i]),
+    "gsr_set_backward_bytes": (_sz, [_i, ctypes.POINTER(_i)]),
+    "gsr_set_preprocess": (
         _i,
-        [_i, _i, _i, _i, ctypes.POINTER(_i), ctypes.POINTER(_i), ctypes.POINTER(_f), ctypes.POINTER(_f)]
-        + [ctypes.POINTER(_vp)] * 7 + [ctypes.POINTER(_i), _vp, _vp, _f, _vp, _vp, _vp, ctypes.POINTER(_vp)]
-        + [_vp] * 7 + [_i, _vp],
+        [_i, _i, _i, _i, _vp, _vp, _f, _vp, _vp, _vp, _vp, _vp] + [ctypes.POINTER(_vp)] * 3
+        + [ctypes.POINTER(_f)] * 2 + [_i, _i, _i, _vp, _vp, _vp],
+    ),
+    "gsr_set_num_rendered": (_i, [_i, _vp, _i, ctypes.POINTER(_i), ctypes.POINTER(_i), _vp]),
+    "gsr_set_render": (_i, [_i, _i, ctypes.POINTER(_i), _i, _i, ctypes.POINTER(_vp)] + [_vp] * 7),
+    "gsr_set_backward": (
+        _i,
+        [_i, _i, _i, _i, ctypes.POINTER(_i), _i, _i, ctypes.POINTER(_vp), _vp, _vp, _f, _vp, _vp, _vp]
+        + [ctypes.POINTER(_vp)] * 3 + [ctypes.POINTER(_f)] * 2 + [_vp] * 4 + [_vp] * 3 + [_vp] * 8
+        + [_i, _vp, _sz, _vp],
     ),
     "gsr_profile_enable": (_i, [_i]),
     "gsr_profile_read": (_i, [ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_longlong), _i]),

@@ -1,14 +1,15 @@
 """View-batched rasterization: one set of Gaussians, V cameras, one autograd node.
 
-Equivalent to calling GaussianRasterizer once per view (same kernels, same per-view outputs), but:
-  * forward: all views' preprocess is enqueued first and the V instance counts are read back with ONE
-    host sync (the per-view API syncs once per view, idling the GPU while the host catches up);
-  * backward: each view's tile blend writes its gradient rows, then one fused per-Gaussian kernel walks
-    up to 16 views per launch and sums the shared-parameter gradients (means3D, opacity, SH, scales,
-    rotations) in registers — the parameters and SH rows are read once and the gradients written once,
-    instead of once per view plus a per-view autograd accumulation of 192 MB SH gradients.
+Equivalent to calling GaussianRasterizer once per view (same per-view outputs and gradients), but the
+views are rendered as view sets of up to 64 (include/gsr.h, gsr_set_*): every stage — preprocess,
+depth sort, instance emission, tile sort, blend, backward blend, per-Gaussian backward — is ONE launch
+per set instead of one per view, sorts are segmented by view, and the instance counts of all views are
+read back with one host sync.  The reference renders a batch with a Python loop over views
+(renderer/gaussian_batch_renderer.py:9-122); this replaces the loop's V rasterizer calls.
+
 Per-view outputs (color, radii, depth, alpha) and per-view means2D gradients (the densification
-statistic of geometry/gaussian_base.py:815-818) are kept.
+statistic of geometry/gaussian_base.py:815-818) are kept; shared-parameter gradients are summed over
+views inside the per-Gaussian kernel.
 """
 from __future__ import annotations
 
@@ -19,44 +20,36 @@ import torch
 
 from . import _C
 
-# device memory the backward may use at once for per-view gradient rows (views are processed in groups)
+SET_MAX = 64
+# device memory the backward may use at once for gradient rows (views are walked in groups that fit)
 WORK_BUDGET = int(os.environ.get("GSR_BWD_WORK_BYTES", str(24 << 30)))
-# HIP streams the views of a batch are dealt over (views are independent until the per-Gaussian
-# backward): one view's latency-bound sort/scan launches and blend tails overlap another's bulk work
-N_STREAMS = int(os.environ.get("GSR_STREAMS", "4"))
-
-_side: dict = {}
-
-
-class _Fork:
-    """Deal per-view work over side streams that start after everything enqueued so far on the
-    current stream; join() makes the current stream wait for all of them.  Buffers are allocated on
-    the current stream before the fork and released on it after the join, so the caching allocator
-    never hands a side stream memory that is still in use."""
-
-    def __init__(self, dev, n_views):
-        self.main = torch.cuda.current_stream(dev)
-        n = max(1, min(N_STREAMS, n_views))
-        pool = _side.setdefault(dev, [])
-        while len(pool) < n:
-            pool.append(torch.cuda.Stream(dev))
-        self.streams = pool[:n] if n > 1 else [self.main]
-        if n > 1:
-            ev = self.main.record_event()
-            for st in self.streams:
-                st.wait_event(ev)
-
-    def stream(self, v):
-        return ctypes.c_void_p(self.streams[v % len(self.streams)].cuda_stream)
-
-    def join(self):
-        if self.streams[0] is not self.main:
-            for st in self.streams:
-                self.main.wait_event(st.record_event())
 
 
 def _arr(ctype, values):
     return (ctype * len(values))(*values)
+
+
+def _ptrs(ts):
+    return _arr(ctypes.c_void_p, [t.data_ptr() for t in ts])
+
+
+class _ViewSet:
+    """Forward state of one set of views."""
+
+    def __init__(self, lo, hi, cams, tanx, tany):
+        self.lo, self.hi = lo, hi
+        self.cams = cams  # [(view, proj, campos, bg)] contiguous fp32 device tensors
+        self.tanx, self.tany = tanx, tany
+        self.K = None
+        self.geom = self.binning = self.image = None
+
+    @property
+    def V(self):
+        return self.hi - self.lo
+
+    def cam_arrays(self):
+        return (_ptrs([c[0] for c in self.cams]), _ptrs([c[1] for c in self.cams]), _ptrs([c[2] for c in self.cams]),
+                _arr(ctypes.c_float, self.tanx), _arr(ctypes.c_float, self.tany))
 
 
 class _RasterizeViews(torch.autograd.Function):
@@ -68,7 +61,8 @@ class _RasterizeViews(torch.autograd.Function):
         dev = means3D.device
         _C._require_gpu(dev)
         P = int(means3D.shape[0])
-        H, W = int(settings_list[0].image_height), int(settings_list[0].image_width)
+        s0 = settings_list[0]
+        H, W = int(s0.image_height), int(s0.image_width)
         if any(int(s.image_height) != H or int(s.image_width) != W for s in settings_list):
             raise _C.GSRError("all views of a batch must have the same image size")
         f = lambda t, n: _C._f32(t, n, dev)  # noqa: E731
@@ -78,49 +72,41 @@ class _RasterizeViews(torch.autograd.Function):
         if (shc is None) == (col is None):
             raise Exception("Please provide excatly one of either SHs or precomputed colors!")
         M = _C.sh_coeff_count(shc)
-        cams = [(f(s.viewmatrix, "viewmatrix"), f(s.projmatrix, "projmatrix"), f(s.campos, "campos"), f(s.bg, "bg"))
-                for s in settings_list]
+        p = _C._ptr
+        stream = _C._stream(dev)
         fopt = dict(dtype=torch.float32, device=dev)
         color = torch.empty((V, 3, H, W), **fopt)
         depth = torch.empty((V, 1, H, W), **fopt)
         alpha = torch.empty((V, 1, H, W), **fopt)
-        radii = torch.zeros((V, P), dtype=torch.int32, device=dev)
-        stream = _C._stream(dev)
-        p = _C._ptr
-        geoms = []
-        if P > 0:
-            geoms = [torch.empty(int(lib.gsr_geom_bytes(P)), dtype=torch.uint8, device=dev) for _ in range(V)]
-            fork = _Fork(dev, V)
-            for v, s in enumerate(settings_list):
-                view, proj, campos, _ = cams[v]
-                _C._check(lib.gsr_forward_preprocess(
-                    P, int(s.sh_degree), M, p(m3), p(sc), float(s.scale_modifier), p(rot), p(op), p(shc), p(col),
-                    p(c3), p(view), p(proj), p(campos), W, H, float(s.tanfovx), float(s.tanfovy),
-                    int(bool(s.prefiltered)), p(radii[v]), p(geoms[v]), fork.stream(v)))
-            fork.join()
-            Ks = (ctypes.c_int * V)()
-            _C._check(lib.gsr_num_rendered_many(V, _arr(ctypes.c_void_p, [g.data_ptr() for g in geoms]), P, Ks,
-                                                stream))
-            Ks = [int(k) for k in Ks]
+        radii = torch.empty((V, P), dtype=torch.int32, device=dev)
+        sets = []
+        for lo in range(0, V, SET_MAX):
+            hi = min(V, lo + SET_MAX)
+            cams = [(f(s.viewmatrix, "viewmatrix"), f(s.projmatrix, "projmatrix"), f(s.campos, "campos"),
+                     f(s.bg, "bg")) for s in settings_list[lo:hi]]
+            vs = _ViewSet(lo, hi, cams, [float(s.tanfovx) for s in settings_list[lo:hi]],
+                          [float(s.tanfovy) for s in settings_list[lo:hi]])
+            vs.geom = torch.empty(int(lib.gsr_set_geom_bytes(vs.V, P)), dtype=torch.uint8, device=dev)
+            views, projs, campos, tx, ty = vs.cam_arrays()
+            _C._check(lib.gsr_set_preprocess(
+                vs.V, P, int(s0.sh_degree), M, p(m3), p(sc), float(s0.scale_modifier), p(rot), p(op), p(shc), p(col),
+                p(c3), views, projs, campos, tx, ty, W, H, int(bool(s0.prefiltered)), p(radii[lo:hi]), p(vs.geom),
+                stream))
+            sets.append(vs)
+        for vs in sets:
+            K = (ctypes.c_int * vs.V)()
+            _C._check(lib.gsr_set_num_rendered(vs.V, p(vs.geom), P, K, None, stream))
+            vs.K = [int(k) for k in K]
             if len(_C.RECENT_FORWARDS) < 4096:
-                _C.RECENT_FORWARDS.extend((k, H, W) for k in Ks)
-        else:
-            color.zero_(), depth.zero_(), alpha.zero_()
-            Ks = [0] * V
-        binnings, images = [], []
-        if P > 0:
-            binnings = [torch.empty(int(lib.gsr_binning_bytes(Ks[v], W, H)), dtype=torch.uint8, device=dev)
-                        for v in range(V)]
-            images = [torch.empty(int(lib.gsr_image_bytes(W, H)), dtype=torch.uint8, device=dev) for _ in range(V)]
-            fork = _Fork(dev, V)
-            for v in range(V):
-                _C._check(lib.gsr_forward_render(P, Ks[v], W, H, p(cams[v][3]), p(geoms[v]), p(binnings[v]),
-                                                 p(images[v]), p(color[v]), p(depth[v]), p(alpha[v]), fork.stream(v)))
-            fork.join()
+                _C.RECENT_FORWARDS.extend((k, H, W) for k in vs.K)
+            Karr = _arr(ctypes.c_int, vs.K)
+            vs.binning = torch.empty(int(lib.gsr_set_binning_bytes(vs.V, Karr, W, H)), dtype=torch.uint8, device=dev)
+            vs.image = torch.empty(int(lib.gsr_set_image_bytes(vs.V, W, H)), dtype=torch.uint8, device=dev)
+            _C._check(lib.gsr_set_render(vs.V, P, Karr, W, H, _ptrs([c[3] for c in vs.cams]), p(vs.geom),
+                                         p(vs.binning), p(vs.image), p(color[vs.lo:vs.hi]), p(depth[vs.lo:vs.hi]),
+                                         p(alpha[vs.lo:vs.hi]), stream))
         ctx.settings = settings_list
-        ctx.Ks = Ks
-        ctx.geoms, ctx.binnings, ctx.images = geoms, binnings, images
-        ctx.cams = cams
+        ctx.sets = sets
         ctx.save_for_backward(m3, shc, col, sc, rot, c3, radii)
         ctx.mark_non_differentiable(radii)
         return color, radii, depth, alpha
@@ -131,55 +117,43 @@ class _RasterizeViews(torch.autograd.Function):
         m3, shc, col, sc, rot, c3, radii = ctx.saved_tensors
         settings = ctx.settings
         V = len(settings)
+        s0 = settings[0]
         dev = m3.device
         P = int(m3.shape[0])
         M = _C.sh_coeff_count(shc)
-        H, W = int(settings[0].image_height), int(settings[0].image_width)
+        H, W = int(s0.image_height), int(s0.image_width)
         fopt = dict(dtype=torch.float32, device=dev)
-        d_m2 = torch.zeros((V, P, 3), **fopt)
-        d_m3 = torch.zeros((P, 3), **fopt)
-        d_op = torch.zeros((P, 1), **fopt)
-        d_col = torch.zeros((P, 3), **fopt) if col is not None else None
-        d_sh = torch.zeros((P, M, 3), **fopt) if shc is not None else None
-        d_c3 = torch.zeros((P, 6), **fopt) if c3 is not None else None
-        d_sc = torch.zeros((P, 3), **fopt) if c3 is None else None
-        d_rot = torch.zeros((P, 4), **fopt) if c3 is None else None
-        if P > 0:
+        d_m2 = torch.empty((V, P, 3), **fopt)
+        d_m3 = torch.empty((P, 3), **fopt)
+        d_op = torch.empty((P, 1), **fopt)
+        d_col = torch.empty((P, 3), **fopt)
+        d_sh = torch.empty((P, M, 3), **fopt) if shc is not None else None
+        d_c3 = torch.empty((P, 6), **fopt) if c3 is not None else None
+        d_sc = torch.empty((P, 3), **fopt) if c3 is None else None
+        d_rot = torch.empty((P, 4), **fopt) if c3 is None else None
+        if P == 0:
+            for t in (d_m2, d_m3, d_op, d_col, d_sh, d_c3, d_sc, d_rot):
+                if t is not None:
+                    t.zero_()
+        else:
             gc = g_color.float().contiguous()
             gd = g_depth.float().contiguous() if g_depth is not None else None
             ga = g_alpha.float().contiguous() if g_alpha is not None else None
             stream = _C._stream(dev)
             p = _C._ptr
-            # group views so the gradient rows of one group fit the work budget
-            sizes = [int(lib.gsr_backward_bytes(P, k)) for k in ctx.Ks]
-            groups, cur, cur_b = [], [], 0
-            for v in range(V):
-                if cur and (cur_b + sizes[v] > WORK_BUDGET or len(cur) == 16):
-                    groups.append(cur)
-                    cur, cur_b = [], 0
-                cur.append(v)
-                cur_b += sizes[v]
-            groups.append(cur)
-            for gi, grp in enumerate(groups):
-                works = [torch.empty(sizes[v], dtype=torch.uint8, device=dev) for v in grp]
-                fork = _Fork(dev, len(grp))
-                for j, v in enumerate(grp):
-                    _C._check(lib.gsr_backward_render(
-                        P, ctx.Ks[v], W, H, p(ctx.cams[v][3]), p(ctx.geoms[v]), p(ctx.binnings[v]), p(ctx.images[v]),
-                        p(gc[v]), p(gd[v]) if gd is not None else None, p(ga[v]) if ga is not None else None,
-                        p(works[j]), fork.stream(j)))
-                fork.join()
-                n = len(grp)
-                vp = lambda xs: _arr(ctypes.c_void_p, [x.data_ptr() for x in xs])  # noqa: E731
-                _C._check(lib.gsr_backward_gaussians_many(
-                    n, P, int(settings[0].sh_degree), M, _arr(ctypes.c_int, [W] * n), _arr(ctypes.c_int, [H] * n),
-                    _arr(ctypes.c_float, [float(settings[v].tanfovx) for v in grp]),
-                    _arr(ctypes.c_float, [float(settings[v].tanfovy) for v in grp]),
-                    vp([ctx.cams[v][0] for v in grp]), vp([ctx.cams[v][1] for v in grp]),
-                    vp([ctx.cams[v][2] for v in grp]), vp([radii[v] for v in grp]), vp([ctx.geoms[v] for v in grp]),
-                    vp([ctx.images[v] for v in grp]), vp(works), _arr(ctypes.c_int, [ctx.Ks[v] for v in grp]),
-                    p(m3), p(sc), float(settings[0].scale_modifier), p(rot), p(shc), p(c3), vp([d_m2[v] for v in grp]),
-                    p(d_col), p(d_op), p(d_m3), p(d_c3), p(d_sh), p(d_sc), p(d_rot), 1 if gi > 0 else 0, stream))
+            for si, vs in enumerate(ctx.sets):
+                Karr = _arr(ctypes.c_int, vs.K)
+                need = int(lib.gsr_set_backward_bytes(vs.V, Karr))
+                largest = max(int(lib.gsr_backward_bytes(P, k)) for k in vs.K)
+                work = torch.empty(max(largest, min(need, WORK_BUDGET)), dtype=torch.uint8, device=dev)
+                views, projs, campos, tx, ty = vs.cam_arrays()
+                sl = slice(vs.lo, vs.hi)
+                _C._check(lib.gsr_set_backward(
+                    vs.V, P, int(s0.sh_degree), M, Karr, W, H, _ptrs([c[3] for c in vs.cams]), p(m3), p(sc),
+                    float(s0.scale_modifier), p(rot), p(shc), p(c3), views, projs, campos, tx, ty, p(radii[sl]),
+                    p(vs.geom), p(vs.binning), p(vs.image), p(gc[sl]), p(gd[sl]) if gd is not None else None,
+                    p(ga[sl]) if ga is not None else None, p(d_m2[sl]), p(d_col), p(d_op), p(d_m3), p(d_c3), p(d_sh),
+                    p(d_sc), p(d_rot), 1 if si > 0 else 0, p(work), work.numel(), stream))
         grads = [None, d_m3, d_sh, d_col, d_op, d_sc, d_rot, d_c3] + [d_m2[v] for v in range(V)]
         for k, need in enumerate(ctx.needs_input_grad):
             if not need:
@@ -190,9 +164,9 @@ class _RasterizeViews(torch.autograd.Function):
 def rasterize_views(settings_list, means3D, means2D_list, opacities, shs=None, colors_precomp=None, scales=None,
                     rotations=None, cov3D_precomp=None):
     """Render V views of one set of Gaussians.  settings_list: V GaussianRasterizationSettings (same image
-    size, same sh_degree and scale_modifier); means2D_list: V screen-space placeholders (P, 3) whose .grad
-    receives each view's viewspace gradient.  Returns (color (V,3,H,W), radii (V,P), depth (V,1,H,W),
-    alpha (V,1,H,W))."""
+    size, same sh_degree, scale_modifier and prefiltered flag); means2D_list: V screen-space placeholders
+    (P, 3) whose .grad receives each view's viewspace gradient.  Returns (color (V,3,H,W), radii (V,P),
+    depth (V,1,H,W), alpha (V,1,H,W))."""
     if (shs is None) == (colors_precomp is None):
         raise Exception("Please provide excatly one of either SHs or precomputed colors!")
     if ((scales is None or rotations is None) and cov3D_precomp is None) or (
@@ -200,9 +174,11 @@ def rasterize_views(settings_list, means3D, means2D_list, opacities, shs=None, c
         raise Exception("Please provide exactly one of either scale/rotation pair or precomputed 3D covariance!")
     if len(means2D_list) != len(settings_list):
         raise ValueError("one means2D placeholder per view")
+    if not settings_list:
+        raise ValueError("at least one view")
     s0 = settings_list[0]
     if any(int(s.sh_degree) != int(s0.sh_degree) or float(s.scale_modifier) != float(s0.scale_modifier)
-           for s in settings_list):
-        raise ValueError("sh_degree and scale_modifier must be shared by the views of a batch")
+           or bool(s.prefiltered) != bool(s0.prefiltered) for s in settings_list):
+        raise ValueError("sh_degree, scale_modifier and prefiltered must be shared by the views of a batch")
     return _RasterizeViews.apply(list(settings_list), means3D, shs, colors_precomp, opacities, scales, rotations,
                                  cov3D_precomp, *means2D_list)
