@@ -132,9 +132,9 @@ int gsr_backward(int P, int degree, int M, int K, int width, int height, const f
 size_t gsr_set_geom_bytes(int V, int P);
 size_t gsr_set_binning_bytes(int V, const int* num_rendered, int width, int height);
 size_t gsr_set_image_bytes(int V, int width, int height);
-/* Scratch holding the gradient rows of all V views; gsr_set_backward also accepts less (>= the
- * largest single view) and then walks the views in groups that fit. */
-size_t gsr_set_backward_bytes(int V, const int* num_rendered);
+/* Scratch holding the gradient rows and per-(view, Gaussian) records of all V views; gsr_set_backward
+ * also accepts less (>= what the largest single view needs) and then walks the views in groups that fit. */
+size_t gsr_set_backward_bytes(int V, int P, const int* num_rendered);
 int gsr_set_preprocess(int V, int P, int degree, int M, const float* means3D, const float* scales,
                        float scale_modifier, const float* rotations, const float* opacities, const float* shs,
                        const float* colors_precomp, const float* cov3D_precomp,

@@ -192,10 +192,10 @@ size_t gsr_set_image_bytes(int V, int width, int height) {
   ImageState::carve(nullptr, V, width, height, &b);
   return b;
 }
-size_t gsr_set_backward_bytes(int V, const int* K) {
+size_t gsr_set_backward_bytes(int V, int P, const int* K) {
   long long total = 0;
   for (int v = 0; v < V; ++v) total += K[v];
-  return BackwardState::bytes_for(total);
+  return BackwardState::bytes_for(total, V, P);
 }
 
 int gsr_set_preprocess(int V, int P, int degree, int M, const float* means3D, const float* scales,
@@ -359,14 +359,15 @@ int gsr_set_backward(int V, int P, int degree, int M, const int* K, int width, i
                                      dL_dcolors, dL_dopacity, dL_dmeans3D, dL_dcov3D, dL_dsh, dL_dscales,
                                      dL_drotations);
   bool first = accumulate == 0;
-  // groups of consecutive views whose gradient rows fit the work buffer
+  // groups of consecutive views whose gradient rows and records fit the work buffer
   for (int g0 = 0; g0 < V;) {
     int g1 = g0;
     long long rows = 0;
-    while (g1 < V && (g1 == g0 || BackwardState::bytes_for(rows + K[g1]) <= work_bytes)) rows += K[g1++];
-    if (BackwardState::bytes_for(rows) > work_bytes)
+    while (g1 < V && (g1 == g0 || BackwardState::bytes_for(rows + K[g1], g1 + 1 - g0, P) <= work_bytes))
+      rows += K[g1++];
+    if (BackwardState::bytes_for(rows, g1 - g0, P) > work_bytes)
       return fail(GSR_EINVAL, "%s", "backward work buffer smaller than one view's gradient rows");
-    BackwardState bw = BackwardState::carve(work);
+    BackwardState bw = BackwardState::carve(work, rows);
     RenderSet rs;
     rs.V = g1 - g0;
     rs.v0 = g0;
@@ -375,11 +376,37 @@ int gsr_set_backward(int V, int P, int degree, int M, const int* K, int width, i
     rs.H = height;
     rs.gx = gx;
     rs.gy = gy;
+    ViewGradArgs va;
+    va.V = g1 - g0;
+    va.v0 = g0;
+    va.W = width;
+    va.H = height;
+    va.gx = gx;
+    va.tiles = gx * gy;
+    va.cut_in_lds = 0;
+    va.pad_ = 0;
+    va.g = g;
+    va.img = img;
+    va.radii = radii;
+    va.grow = bw.grow;
+    va.dmeans2D = dL_dmeans2D;
+    va.vrec = bw.vrec;
+    AccumArgs ab;
+    ab.V = g1 - g0;
+    ab.v0 = g0;
+    ab.accumulate = first ? 0 : 1;
+    ab.pad_ = 0;
+    ab.clamped = g.clamped;
+    ab.radii = radii;
+    ab.vrec = bw.vrec;
     for (int v = g0; v < g1; ++v) {
       if (bgs[v] == nullptr) return fail(GSR_EINVAL, "%s", "null background");
       rs.inst_start[v - g0] = inst.start[v];
       rs.row_start[v - g0] = inst.start[v] - inst.start[g0];
       rs.bg[v - g0] = bgs[v];
+      va.row_start[v - g0] = rs.row_start[v - g0];
+      va.cam[v - g0] = cams.c[v];
+      ab.campos[v - g0] = cams.c[v].campos;
     }
     {
       PhaseScope ps(GSR_PHASE_RENDER_BWD, s);
@@ -387,18 +414,11 @@ int gsr_set_backward(int V, int P, int degree, int M, const int* K, int width, i
                              dL_ddepth ? dL_ddepth + (size_t)g0 * HW : nullptr,
                              dL_dalpha ? dL_dalpha + (size_t)g0 * HW : nullptr, bw, s);
     }
-    PhaseScope ps(GSR_PHASE_GAUSS_BWD, s);
-    for (int c0 = g0; c0 < g1; c0 += GSR_VIEWS_PER_LAUNCH) {
-      const int c1 = c0 + GSR_VIEWS_PER_LAUNCH < g1 ? c0 + GSR_VIEWS_PER_LAUNCH : g1;
-      ViewBatch vb;
-      vb.n = c1 - c0;
-      vb.accumulate = first ? 0 : 1;
-      for (int v = c0; v < c1; ++v)
-        vb.v[v - c0] = make_view_desc(cams.c[v], v, P, radii, g, img, bw.grow + (size_t)12 * rs.row_start[v - g0],
-                                      dL_dmeans2D + (size_t)v * P * 3, width, height);
-      launch_gauss_backward_views(a, vb, s);
-      first = false;
+    {
+      PhaseScope ps(GSR_PHASE_GAUSS_BWD, s);
+      launch_gauss_backward(a, va, ab, s);
     }
+    first = false;
     g0 = g1;
   }
   return last_launch();
@@ -409,10 +429,7 @@ int gsr_set_backward(int V, int P, int degree, int M, const int* K, int width, i
 size_t gsr_geom_bytes(int P) { return gsr_set_geom_bytes(1, P); }
 size_t gsr_binning_bytes(int K, int width, int height) { return gsr_set_binning_bytes(1, &K, width, height); }
 size_t gsr_image_bytes(int width, int height) { return gsr_set_image_bytes(1, width, height); }
-size_t gsr_backward_bytes(int P, int K) {
-  (void)P;
-  return gsr_set_backward_bytes(1, &K);
-}
+size_t gsr_backward_bytes(int P, int K) { return gsr_set_backward_bytes(1, P, &K); }
 
 int gsr_forward_preprocess(int P, int degree, int M, const float* means3D, const float* scales,
                            float scale_modifier, const float* rotations, const float* opacities,

@@ -1,15 +1,17 @@
-// gsr_backward.hip — fused per-Gaussian backward over one or many views.
+// gsr_backward.hip — per-Gaussian backward of a view set.
 //
-// One thread per Gaussian, looping over the views of a batch (1 for the per-view API):
-//   1. gather-sum of the Gaussian's per-instance gradient rows written by k_render_bwd into the
-//      Gaussian's own contiguous slots (fixed summation order -> bitwise reproducible);
-//   2. BACKWARD::computeCov2DCUDA [EXT]: conic -> 2D cov -> 3D cov and camera-space mean;
-//   3. BACKWARD::preprocessCUDA [EXT]: 2D mean -> 3D mean through the projection, view-depth
-//      term (ashawkey depth output), SH -> RGB backward incl. the view-direction term;
-//   4. once per batch: 3D cov -> scale and (unnormalised) quaternion (linear in dL/dcov3D, so the
-//      views' covariance gradients are summed first).
-// The Gaussian parameters and SH rows are read once per batch and the shared-parameter gradients
-// written once, instead of once per view plus a per-view autograd accumulation.
+// Two launches per group of views:
+//   A. k_view_grad, one thread per (view, Gaussian): gather-sum of the Gaussian's per-instance
+//      gradient rows written by k_render_bwd (fixed order -> bitwise reproducible), with the tile
+//      cut-offs of the view staged in LDS so the ~92 % of instances no pixel reached cost one LDS
+//      read each; then BACKWARD::computeCov2DCUDA (conic -> 2D cov -> 3D cov and camera-space mean)
+//      and the projection / view-depth part of BACKWARD::preprocessCUDA [EXT].  Writes the view's
+//      means2D gradient and a 13-float record (dmean3D, dcov3D, raw dcolor, dopacity).
+//   B. k_gauss_accum, one thread per Gaussian: streams its records over the group's views, runs the
+//      SH -> RGB backward (incl. the view-direction term) per view with dL/dSH accumulated in
+//      registers, then 3D cov -> scale and (unnormalised) quaternion once (linear in dL/dcov3D).
+// Splitting at the view boundary keeps A light (≈70 VGPRs, thousands of waves in flight to hide the
+// gather latency) and leaves only B to carry the 48 SH accumulators.
 // Gradient conventions of the reference are kept: the 0.99 alpha clamp is ignored in
 // dL/dG, the frustum clamp zeroes dL/dt_x,y only, denom2inv carries +1e-7, the scale gradient is
 // w.r.t. scale_modifier * scale.
@@ -23,20 +25,18 @@ struct RowSums {
 };
 
 // Sum the 4 quadrant rows of each of the Gaussian's instances that its tile's blend reached:
-// (depth key, index) < the tile's first unblended instance.
-__device__ __forceinline__ RowSums gather_rows(int idx, const ViewDesc& d) {
+// (depth key, index) < the tile's first unblended instance (cut = (key, index) per tile).
+__device__ __forceinline__ RowSums gather_rows(uint32_t idx, uint32_t dkey, uint32_t i0, uint2 rc, int grid_x,
+                                               const uint2* cut, const float4* grow) {
   RowSums r = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-  const size_t i0 = d.goff[idx];
-  const uint2 rc = d.rect[idx];
   const int xmin = rc.x & 0xffff, ymin = rc.x >> 16, xmax = rc.y & 0xffff, ymax = rc.y >> 16;
-  const uint32_t dkey = __float_as_uint(d.rec1[idx].z);
   size_t i = i0;
   for (int ty = ymin; ty < ymax; ++ty)
     for (int tx = xmin; tx < xmax; ++tx, ++i) {
-      const uint4 info = d.tile_info[ty * d.grid_x + tx];
-      const bool valid = dkey < info.y || (dkey == info.y && (uint32_t)idx < info.z);
+      const uint2 c = cut[ty * grid_x + tx];
+      const bool valid = dkey < c.x || (dkey == c.x && idx < c.y);
       if (!valid) continue;
-      const float4* row = d.grow + 12 * i;
+      const float4* row = grow + 12 * i;
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
         const float4 r0 = row[3 * q], r1 = row[3 * q + 1], r2 = row[3 * q + 2];
@@ -48,9 +48,15 @@ __device__ __forceinline__ RowSums gather_rows(int idx, const ViewDesc& d) {
   return r;
 }
 
+// Camera of one view as the chain rule needs it.
+struct ViewGeom {
+  const float *view, *proj;
+  float tanx, tany, fx, fy;
+};
+
 // computeCov2DCUDA: conic gradient -> dL/dcov3D (6, symmetric off-diagonals as scalars) and the
 // camera-space-mean part of dL/dmean.
-__device__ __forceinline__ void cov2d_backward(const float3 mean, const float cov3D[6], const ViewDesc& d,
+__device__ __forceinline__ void cov2d_backward(const float3 mean, const float cov3D[6], const ViewGeom& d,
                                                float dca, float dcb, float dcc, float dcov[6], float3& dmean) {
   Cov2DState st;
   const float3 cov2 = cov2d_ewa(mean, d.fx, d.fy, d.tanx, d.tany, cov3D, d.view, st);
@@ -114,13 +120,10 @@ __device__ __forceinline__ void proj_backward(const float3 mean, const float* pr
   dmean.z += (proj[8] * m_w - proj[11] * mul1) * dmx + (proj[9] * m_w - proj[11] * mul2) * dmy;
 }
 
-// computeColorFromSH backward for one view: accumulates basis x dL/dRGB into dsh (registers, 3 x 16)
-// and adds the view-direction term to dmean.  sh = the Gaussian's (M, 3) row (LDS).
-// MULTI: accumulate basis x dL/dRGB into dsh (registers, summed over views).  Single view: write it
-// into `out` (the Gaussian's LDS row, which aliases `sh`) after every read of sh is done.
-template <bool MULTI>
-__device__ __forceinline__ void sh_backward(int deg, int M, const float* sh, float (&dsh)[48], float* out,
-                                            float3 dRGB, const float3 mean, const float* campos, float3& dmean) {
+// computeColorFromSH backward for one view: accumulates basis x dL/dRGB into dsh (registers, 3 x 16,
+// summed over views) and adds the view-direction term to dmean.  sh = the Gaussian's (M, 3) row (LDS).
+__device__ __forceinline__ void sh_backward(int deg, int M, const float* sh, float (&dsh)[48], float3 dRGB,
+                                            const float3 mean, const float* campos, float3& dmean) {
   const float3 dir_orig = make_float3(mean.x - campos[0], mean.y - campos[1], mean.z - campos[2]);
   const float len = sqrtf(dir_orig.x * dir_orig.x + dir_orig.y * dir_orig.y + dir_orig.z * dir_orig.z);
   const float x = dir_orig.x / len, y = dir_orig.y / len, z = dir_orig.z / len;
@@ -168,11 +171,9 @@ __device__ __forceinline__ void sh_backward(int deg, int M, const float* sh, flo
 #pragma unroll
   for (int k = 0; k < 16; ++k) {
     if (k < ncoef && k < M) {
-      if (MULTI) {
-        dsh[3 * k] += basis[k] * dRGB.x;
-        dsh[3 * k + 1] += basis[k] * dRGB.y;
-        dsh[3 * k + 2] += basis[k] * dRGB.z;
-      }
+      dsh[3 * k] += basis[k] * dRGB.x;
+      dsh[3 * k + 1] += basis[k] * dRGB.y;
+      dsh[3 * k + 2] += basis[k] * dRGB.z;
       if (k > 0) {
         const float3 s = make_float3(sh[3 * k], sh[3 * k + 1], sh[3 * k + 2]);
         dRGBdx.x += bdx[k] * s.x; dRGBdx.y += bdx[k] * s.y; dRGBdx.z += bdx[k] * s.z;
@@ -180,17 +181,6 @@ __device__ __forceinline__ void sh_backward(int deg, int M, const float* sh, flo
         dRGBdz.x += bdz[k] * s.x; dRGBdz.y += bdz[k] * s.y; dRGBdz.z += bdz[k] * s.z;
       }
     }
-  }
-  if (!MULTI) {
-#pragma unroll
-    for (int k = 0; k < 16; ++k)
-      if (k < M) {
-        const float bk = k < ncoef ? basis[k] : 0.f;
-        out[3 * k] = bk * dRGB.x;
-        out[3 * k + 1] = bk * dRGB.y;
-        out[3 * k + 2] = bk * dRGB.z;
-      }
-    for (int k = 16; k < M; ++k) out[3 * k] = out[3 * k + 1] = out[3 * k + 2] = 0.f;
   }
   const float3 ddir = make_float3(dRGBdx.x * dRGB.x + dRGBdx.y * dRGB.y + dRGBdx.z * dRGB.z,
                                   dRGBdy.x * dRGB.x + dRGBdy.y * dRGB.y + dRGBdy.z * dRGB.z,
@@ -245,12 +235,102 @@ __device__ __forceinline__ void put(float* p, float v, bool acc) { *p = acc ? *p
 // per-thread 16-byte LDS accesses at this stride are bank-conflict free.
 static inline __host__ __device__ int sh_lds_stride(int M) { return ((3 * M + 3) & ~3) + 4; }
 
+// ---- A: per (view, Gaussian) ----------------------------------------------------------------
+// Block b -> view b % V, Gaussians [256 (b / V), +256): the views of one Gaussian slice run together,
+// so its parameters come from HBM once per group.  LDS: the view's tile cut-offs (8 B per tile).
+__global__ __launch_bounds__(256) void k_view_grad(GaussBackwardArgs a, ViewGradArgs va) {
+  extern __shared__ uint2 s_cut[];
+  const int t = threadIdx.x;
+  const int vl = blockIdx.x % va.V;
+  const int vg = va.v0 + vl;
+  const uint4* tinfo = va.img.tile_info + (size_t)vg * va.tiles;
+  const uint2* cut = reinterpret_cast<const uint2*>(s_cut);
+  if (va.cut_in_lds) {
+    for (int k = t; k < va.tiles; k += 256) {
+      const uint4 ti = tinfo[k];
+      s_cut[k] = make_uint2(ti.y, ti.z);
+    }
+    __syncthreads();
+  }
+  const int idx = (blockIdx.x / va.V) * 256 + t;
+  if (idx >= a.P) return;
+  const size_t o = (size_t)vg * a.P + idx;
+  float* m2 = va.dmeans2D + 3 * o;
+  float* rec = va.vrec + (size_t)vl * GSR_GRAD_FIELDS * a.P + idx;
+  if (va.radii[o] <= 0) {
+    m2[0] = 0.f;
+    m2[1] = 0.f;
+    m2[2] = 0.f;
+#pragma unroll
+    for (int f = 0; f < GSR_GRAD_FIELDS; ++f) rec[(size_t)f * a.P] = 0.f;
+    return;
+  }
+  RowSums r;
+  if (va.cut_in_lds) {
+    r = gather_rows((uint32_t)idx, __float_as_uint(va.g.rec1[o].z), va.g.goff[o], va.g.rect[o], va.gx, cut,
+                    va.grow + (size_t)12 * va.row_start[vl]);
+  } else {
+    // image too large for LDS: the same cut-offs read from tile_info (L2)
+    r = RowSums{0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    const uint2 rc = va.g.rect[o];
+    const uint32_t dkey = __float_as_uint(va.g.rec1[o].z);
+    const int xmin = rc.x & 0xffff, ymin = rc.x >> 16, xmax = rc.y & 0xffff, ymax = rc.y >> 16;
+    size_t i = (size_t)va.row_start[vl] + va.g.goff[o];
+    for (int ty = ymin; ty < ymax; ++ty)
+      for (int tx = xmin; tx < xmax; ++tx, ++i) {
+        const uint4 c = tinfo[ty * va.gx + tx];
+        if (!(dkey < c.y || (dkey == c.y && (uint32_t)idx < c.z))) continue;
+        const float4* row = va.grow + 12 * i;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const float4 r0 = row[3 * q], r1 = row[3 * q + 1], r2 = row[3 * q + 2];
+          r.dmx += r0.x; r.dmy += r0.y; r.dca += r0.z; r.dcb += r0.w;
+          r.dcc += r1.x; r.dop += r1.y; r.dcr += r1.z; r.dcg += r1.w;
+          r.dcbl += r2.x; r.ddep += r2.y;
+        }
+      }
+  }
+  m2[0] = r.dmx;
+  m2[1] = r.dmy;
+  m2[2] = 0.f;
+  const float3 mean = make_float3(a.means3D[3 * idx], a.means3D[3 * idx + 1], a.means3D[3 * idx + 2]);
+  float cov3D[6];
+  if (a.cov3D_precomp) {
+#pragma unroll
+    for (int k = 0; k < 6; ++k) cov3D[k] = a.cov3D_precomp[6 * idx + k];
+  } else {
+    const float3 scale = make_float3(a.scales[3 * idx], a.scales[3 * idx + 1], a.scales[3 * idx + 2]);
+    const float4 rot = make_float4(a.rotations[4 * idx], a.rotations[4 * idx + 1], a.rotations[4 * idx + 2],
+                                   a.rotations[4 * idx + 3]);
+    cov3d_from_scale_rot(scale, a.scale_modifier, rot, cov3D);
+  }
+  const ViewCam& cam = va.cam[vl];
+  ViewGeom vgm;
+  vgm.view = cam.view;
+  vgm.proj = cam.proj;
+  vgm.tanx = cam.tanx;
+  vgm.tany = cam.tany;
+  vgm.fy = va.H / (2.0f * cam.tany);
+  vgm.fx = va.W / (2.0f * cam.tanx);
+  float dcv[6];
+  float3 dm;
+  cov2d_backward(mean, cov3D, vgm, r.dca, r.dcb, r.dcc, dcv, dm);
+  proj_backward(mean, cam.proj, r.dmx, r.dmy, dm);
+  // view depth = view[2] x + view[6] y + view[10] z + view[14]
+  dm.x += cam.view[2] * r.ddep;
+  dm.y += cam.view[6] * r.ddep;
+  dm.z += cam.view[10] * r.ddep;
+  const float f[GSR_GRAD_FIELDS] = {dm.x, dm.y, dm.z, dcv[0], dcv[1], dcv[2], dcv[3], dcv[4], dcv[5],
+                                    r.dcr, r.dcg, r.dcbl, r.dop};
+#pragma unroll
+  for (int k = 0; k < GSR_GRAD_FIELDS; ++k) rec[(size_t)k * a.P] = f[k];
+}
+
+// ---- B: per Gaussian, over the group's views ---------------------------------------------------
 // 256 Gaussians per block.  The block's SH rows (contiguous in HBM) are loaded into LDS with fully
 // coalesced loads; each thread reads its row from LDS for every view, accumulates dL/dSH in registers,
-// writes it back into its LDS row, and the block stores the rows coalesced (per-thread 192-byte rows
-// at a 192-byte lane stride left 2/3 of the wave time waiting on memory).
-template <bool MULTI>
-__global__ __launch_bounds__(256) void k_gauss_bwd_views(GaussBackwardArgs a, ViewBatch vb) {
+// writes it back into its LDS row, and the block stores the rows coalesced.
+__global__ __launch_bounds__(256) void k_gauss_accum(GaussBackwardArgs a, AccumArgs b) {
   extern __shared__ __attribute__((aligned(16))) float s_sh[];
   const int t = threadIdx.x;
   const int block0 = blockIdx.x * 256;
@@ -259,7 +339,7 @@ __global__ __launch_bounds__(256) void k_gauss_bwd_views(GaussBackwardArgs a, Vi
   const int F = 3 * a.M;
   const int S = sh_lds_stride(a.M);
   const bool has_sh = a.shs != nullptr && F > 0;
-  const bool acc = vb.accumulate != 0;
+  const bool acc = b.accumulate != 0;
   const float invF = has_sh ? 1.0f / (float)F : 0.0f;
   if (has_sh) {
     const float* src = a.shs + (size_t)block0 * F;
@@ -272,63 +352,34 @@ __global__ __launch_bounds__(256) void k_gauss_bwd_views(GaussBackwardArgs a, Vi
   }
   if (idx < a.P) {
     const float3 mean = make_float3(a.means3D[3 * idx], a.means3D[3 * idx + 1], a.means3D[3 * idx + 2]);
-    float cov3D[6];
-    float3 scale = make_float3(0.f, 0.f, 0.f);
-    float4 rot = make_float4(0.f, 0.f, 0.f, 0.f);
-    if (a.cov3D_precomp) {
-#pragma unroll
-      for (int k = 0; k < 6; ++k) cov3D[k] = a.cov3D_precomp[6 * idx + k];
-    } else {
-      scale = make_float3(a.scales[3 * idx], a.scales[3 * idx + 1], a.scales[3 * idx + 2]);
-      rot = make_float4(a.rotations[4 * idx], a.rotations[4 * idx + 1], a.rotations[4 * idx + 2],
-                        a.rotations[4 * idx + 3]);
-      cov3d_from_scale_rot(scale, a.scale_modifier, rot, cov3D);
-    }
     float3 dmean = make_float3(0.f, 0.f, 0.f);
     float dcov[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
     float dop = 0.f, dcr = 0.f, dcg = 0.f, dcb = 0.f;
     float dsh[48];
 #pragma unroll
     for (int k = 0; k < 48; ++k) dsh[k] = 0.f;
-    float* sh_row = has_sh ? s_sh + t * S : nullptr;
-    bool wrote_row = false;
-    const int nv = MULTI ? vb.n : 1;
-    for (int v = 0; v < nv; ++v) {
-      const ViewDesc& d = vb.v[v];
-      float* m2 = d.dmeans2D + 3 * (size_t)idx;
-      if (d.radii[idx] <= 0) {
-        m2[0] = 0.f;
-        m2[1] = 0.f;
-        m2[2] = 0.f;
-        continue;
-      }
-      const RowSums r = gather_rows(idx, d);
-      m2[0] = r.dmx;
-      m2[1] = r.dmy;
-      m2[2] = 0.f;
-      dop += r.dop;
-      dcr += r.dcr;
-      dcg += r.dcg;
-      dcb += r.dcbl;
-      float dcv[6];
-      float3 dm;
-      cov2d_backward(mean, cov3D, d, r.dca, r.dcb, r.dcc, dcv, dm);
+    const float* sh_row = has_sh ? s_sh + t * S : nullptr;
+    for (int vl = 0; vl < b.V; ++vl) {
+      const size_t o = (size_t)(b.v0 + vl) * a.P + idx;
+      if (b.radii[o] <= 0) continue;
+      const float* rec = b.vrec + (size_t)vl * GSR_GRAD_FIELDS * a.P + idx;
+      float f[GSR_GRAD_FIELDS];
 #pragma unroll
-      for (int k = 0; k < 6; ++k) dcov[k] += dcv[k];
-      proj_backward(mean, d.proj, r.dmx, r.dmy, dm);
-      // view depth = view[2] x + view[6] y + view[10] z + view[14]
-      dm.x += d.view[2] * r.ddep;
-      dm.y += d.view[6] * r.ddep;
-      dm.z += d.view[10] * r.ddep;
+      for (int k = 0; k < GSR_GRAD_FIELDS; ++k) f[k] = rec[(size_t)k * a.P];
+      dmean.x += f[0];
+      dmean.y += f[1];
+      dmean.z += f[2];
+#pragma unroll
+      for (int k = 0; k < 6; ++k) dcov[k] += f[3 + k];
+      dcr += f[9];
+      dcg += f[10];
+      dcb += f[11];
+      dop += f[12];
       if (has_sh) {
-        const uint32_t cl = d.clamped[idx];
-        const float3 dRGB = make_float3((cl & 1u) ? 0.f : r.dcr, (cl & 2u) ? 0.f : r.dcg, (cl & 4u) ? 0.f : r.dcbl);
-        sh_backward<MULTI>(a.deg, a.M, sh_row, dsh, sh_row, dRGB, mean, d.campos, dm);
-        wrote_row = !MULTI;
+        const uint32_t cl = b.clamped[o];
+        const float3 dRGB = make_float3((cl & 1u) ? 0.f : f[9], (cl & 2u) ? 0.f : f[10], (cl & 4u) ? 0.f : f[11]);
+        sh_backward(a.deg, a.M, sh_row, dsh, dRGB, mean, b.campos[vl], dmean);
       }
-      dmean.x += dm.x;
-      dmean.y += dm.y;
-      dmean.z += dm.z;
     }
     put(&a.dL_dmeans3D[3 * idx], dmean.x, acc);
     put(&a.dL_dmeans3D[3 * idx + 1], dmean.y, acc);
@@ -342,12 +393,15 @@ __global__ __launch_bounds__(256) void k_gauss_bwd_views(GaussBackwardArgs a, Vi
     if (a.dL_dcov3D)
       for (int k = 0; k < 6; ++k) put(&a.dL_dcov3D[6 * idx + k], dcov[k], acc);
     if (!a.cov3D_precomp && a.dL_dscales) {
+      const float3 scale = make_float3(a.scales[3 * idx], a.scales[3 * idx + 1], a.scales[3 * idx + 2]);
+      const float4 rot = make_float4(a.rotations[4 * idx], a.rotations[4 * idx + 1], a.rotations[4 * idx + 2],
+                                     a.rotations[4 * idx + 3]);
       float ds[3], dq[4];
       scale_rot_backward(scale, rot, a.scale_modifier, dcov, ds, dq);
       for (int k = 0; k < 3; ++k) put(&a.dL_dscales[3 * idx + k], ds[k], acc);
       for (int k = 0; k < 4; ++k) put(&a.dL_drotations[4 * idx + k], dq[k], acc);
     }
-    if (has_sh && !wrote_row) {
+    if (has_sh) {
       // this thread's SH row is no longer read: reuse it for dL/dSH
       float* row = s_sh + t * S;
 #pragma unroll
@@ -368,37 +422,17 @@ __global__ __launch_bounds__(256) void k_gauss_bwd_views(GaussBackwardArgs a, Vi
   }
 }
 
-void launch_gauss_backward_views(const GaussBackwardArgs& a, const ViewBatch& vb, hipStream_t stream) {
-  if (a.P <= 0 || vb.n <= 0) return;
-  const size_t lds = (a.shs && a.M > 0) ? (size_t)256 * sh_lds_stride(a.M) * sizeof(float) : 0;
-  if (vb.n == 1)
-    hipLaunchKernelGGL(k_gauss_bwd_views<false>, dim3((a.P + 255) / 256), dim3(256), lds, stream, a, vb);
-  else
-    hipLaunchKernelGGL(k_gauss_bwd_views<true>, dim3((a.P + 255) / 256), dim3(256), lds, stream, a, vb);
-}
+// LDS budget for the staged tile cut-offs of k_view_grad (larger images read them from L2).
+#define GSR_CUT_LDS_MAX (48 * 1024)
 
-ViewDesc make_view_desc(const ViewCam& cam, int vg, int P, const int* radii, const GeomState& g,
-                        const ImageState& img, const float4* grow, float* dmeans2D, int W, int H) {
-  const size_t o = (size_t)vg * P;
-  const int gx = div_up(W, GSR_TILE_X), gy = div_up(H, GSR_TILE_Y);
-  ViewDesc d;
-  d.view = cam.view;
-  d.proj = cam.proj;
-  d.campos = cam.campos;
-  d.radii = radii + o;
-  d.rec1 = g.rec1 + o;
-  d.rect = g.rect + o;
-  d.goff = g.goff + o;
-  d.clamped = g.clamped + o;
-  d.tile_info = img.tile_info + (size_t)vg * gx * gy;
-  d.grow = grow;
-  d.dmeans2D = dmeans2D;
-  d.tanx = cam.tanx;
-  d.tany = cam.tany;
-  d.fy = H / (2.0f * cam.tany);
-  d.fx = W / (2.0f * cam.tanx);
-  d.grid_x = gx;
-  return d;
+void launch_gauss_backward(const GaussBackwardArgs& a, ViewGradArgs va, const AccumArgs& b, hipStream_t stream) {
+  if (a.P <= 0 || va.V <= 0) return;
+  const size_t cut_bytes = sizeof(uint2) * (size_t)va.tiles;
+  va.cut_in_lds = cut_bytes <= GSR_CUT_LDS_MAX ? 1 : 0;
+  hipLaunchKernelGGL(k_view_grad, dim3(va.V * div_up(a.P, 256)), dim3(256), va.cut_in_lds ? cut_bytes : 0, stream,
+                     a, va);
+  const size_t lds = (a.shs && a.M > 0) ? (size_t)256 * sh_lds_stride(a.M) * sizeof(float) : 0;
+  hipLaunchKernelGGL(k_gauss_accum, dim3(div_up(a.P, 256)), dim3(256), lds, stream, a, b);
 }
 
 }  // namespace gsr

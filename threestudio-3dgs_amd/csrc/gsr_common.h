@@ -209,12 +209,19 @@ struct ImageState {
 //   g0 = (dmean2D.x, dmean2D.y, dconic.a, dconic.b)   [pixel units; b in the reference's half convention]
 //   g1 = (dconic.c, dopacity, dcolor.r, dcolor.g)
 //   g2 = (dcolor.b, ddepth, 0, 0)
+// After the rows: the per-(view, Gaussian) records of gsr_backward.hip's first kernel,
+// [views of the group][13][P] floats.
 struct BackwardState {
   float4* grow;  // [12 * instances of the group]
-  static size_t bytes_for(long long K) { return align_up(sizeof(float4) * 12 * (size_t)(K > 0 ? K : 1), 256); }
-  static BackwardState carve(void* base) {
+  float* vrec;   // [views][13][P]
+  static size_t rows_bytes(long long K) { return align_up(sizeof(float4) * 12 * (size_t)(K > 0 ? K : 1), 256); }
+  static size_t bytes_for(long long K, int views, int P) {
+    return rows_bytes(K) + align_up(sizeof(float) * 13 * (size_t)views * (size_t)(P > 0 ? P : 1), 256);
+  }
+  static BackwardState carve(void* base, long long K) {
     BackwardState s;
     s.grow = (float4*)base;
+    s.vrec = (float*)((char*)base + rows_bytes(K));
     return s;
   }
 };

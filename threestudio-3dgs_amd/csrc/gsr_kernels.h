@@ -56,26 +56,27 @@ struct GaussBackwardArgs {  // shared Gaussian parameters and the gradients of t
   float scale_modifier;
   float *dL_dcolors, *dL_dopacity, *dL_dmeans3D, *dL_dcov3D, *dL_dsh, *dL_dscales, *dL_drotations;
 };
-struct ViewDesc {  // one view's camera, forward state, gradient rows and its means2D gradient output
-  const float *view, *proj, *campos;
-  const int* radii;
-  const float4* rec1;
-  const uint2* rect;
-  const uint32_t *goff, *clamped;
-  const uint4* tile_info;
-  const float4* grow;
-  float* dmeans2D;
-  float tanx, tany, fx, fy;
-  int grid_x, pad_;
+// A: per (view, Gaussian) gather + screen-space chain rule for views v0 .. v0+V-1 of a set.
+#define GSR_GRAD_FIELDS 13  // dmean3D (3), dcov3D (6), raw dcolor (3), dopacity (1)
+struct ViewGradArgs {
+  int V, v0, W, H, gx, tiles, cut_in_lds, pad_;
+  GeomState g;
+  ImageState img;
+  const int* radii;        // the set's (V, P)
+  const float4* grow;      // gradient rows of this group of views
+  float* dmeans2D;         // the set's (V, P, 3)
+  float* vrec;             // [V][GSR_GRAD_FIELDS][P] records of this group
+  uint32_t row_start[GSR_SET_MAX];
+  ViewCam cam[GSR_SET_MAX];
 };
-#define GSR_VIEWS_PER_LAUNCH 16
-struct ViewBatch {  // passed by value as kernel arguments (16 x 112 B)
-  int n, accumulate;
-  ViewDesc v[GSR_VIEWS_PER_LAUNCH];
+// B: per Gaussian, sums the group's records, SH backward per view, scale / rotation once.
+struct AccumArgs {
+  int V, v0, accumulate, pad_;
+  const uint32_t* clamped;  // the set's (V, P)
+  const int* radii;         // the set's (V, P)
+  const float* vrec;
+  const float* campos[GSR_SET_MAX];
 };
-// View vg of a set; radii = the set's (V, P) radii; grow = the view's first gradient row.
-ViewDesc make_view_desc(const ViewCam& cam, int vg, int P, const int* radii, const GeomState& g,
-                        const ImageState& img, const float4* grow, float* dmeans2D, int W, int H);
-void launch_gauss_backward_views(const GaussBackwardArgs& a, const ViewBatch& vb, hipStream_t stream);
+void launch_gauss_backward(const GaussBackwardArgs& a, ViewGradArgs va, const AccumArgs& b, hipStream_t stream);
 
 }  // namespace gsr

@@ -53,7 +53,7 @@ SIGNATURES = {
     "gsr_set_geom_bytes": (_sz, [_i, _i]),
     "gsr_set_binning_bytes": (_sz, [_i, ctypes.POINTER(_i), _i, _i]),
     "gsr_set_image_bytes": (_sz, [_i, _i, _i]),
-    "gsr_set_backward_bytes": (_sz, [_i, ctypes.POINTER(_i)]),
+    "gsr_set_backward_bytes": (_sz, [_i, _i, ctypes.POINTER(_i)]),
     "gsr_set_preprocess": (
         _i,
         [_i, _i, _i, _i, _vp, _vp, _f, _vp, _vp, _vp, _vp, _vp] + [ctypes.POINTER(_vp)] * 3

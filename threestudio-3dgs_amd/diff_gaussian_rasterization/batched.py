@@ -143,7 +143,7 @@ class _RasterizeViews(torch.autograd.Function):
             p = _C._ptr
             for si, vs in enumerate(ctx.sets):
                 Karr = _arr(ctypes.c_int, vs.K)
-                need = int(lib.gsr_set_backward_bytes(vs.V, Karr))
+                need = int(lib.gsr_set_backward_bytes(vs.V, P, Karr))
                 largest = max(int(lib.gsr_backward_bytes(P, k)) for k in vs.K)
                 work = torch.empty(max(largest, min(need, WORK_BUDGET)), dtype=torch.uint8, device=dev)
                 views, projs, campos, tx, ty = vs.cam_arrays()
