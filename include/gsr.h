@@ -130,7 +130,7 @@ int gsr_backward(int P, int degree, int M, int K, int width, int height, const f
  */
 #define GSR_SET_MAX 64
 size_t gsr_set_geom_bytes(int V, int P);
-size_t gsr_set_binning_bytes(int V, const int* num_rendered, int width, int height);
+size_t gsr_set_binning_bytes(int V, int P, const int* num_rendered, int width, int height);
 size_t gsr_set_image_bytes(int V, int width, int height);
 /* Scratch holding the gradient rows and per-(view, Gaussian) records of all V views; gsr_set_backward
  * also accepts less (>= what the largest single view needs) and then walks the views in groups that fit. */

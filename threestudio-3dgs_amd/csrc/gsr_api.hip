@@ -177,14 +177,12 @@ size_t gsr_set_geom_bytes(int V, int P) {
   GeomState::carve(nullptr, V, P, &b);
   return b;
 }
-size_t gsr_set_binning_bytes(int V, const int* K, int width, int height) {
-  (void)width;
-  (void)height;
+size_t gsr_set_binning_bytes(int V, int P, const int* K, int width, int height) {
   SegInfo seg;
   long long total = 0;
   if (V < 1 || V > GSR_SET_MAX || K == nullptr || inst_segments(V, K, seg, &total) != GSR_OK) return 0;
   size_t b = 0;
-  BinningState::carve(nullptr, V, total, seg.blk[V], &b);
+  BinningState::carve(nullptr, V, total, seg.blk[V], !tile_pack(P, width, height).packed, &b);
   return b;
 }
 size_t gsr_set_image_bytes(int V, int width, int height) {
@@ -250,7 +248,7 @@ int gsr_set_preprocess(int V, int P, int degree, int M, const float* means3D, co
       seg.n[v] = (uint32_t)P;
       seg.start[v] = (uint32_t)((size_t)v * P);
     }
-    const int res = seg_sort(g.dkey, g.dval, true, seg, 32, g.sort_counts, g.sort_totals, s);
+    const int res = seg_sort(g.dkey, g.dval, true, seg, 0, 32, g.sort_counts, g.sort_totals, s);
     if (res != depth_sort_result()) return fail(GSR_EHIP, "%s", "internal: depth sort result buffer");
     launch_binning_counts(V, P, g, g.dval[res], s);
   }
@@ -287,7 +285,8 @@ int gsr_set_render(int V, int P, const int* K, int width, int height, const floa
   if (inst_segments(V, K, inst, &total) != GSR_OK) return GSR_EINVAL;
   hipStream_t s = (hipStream_t)stream;
   GeomState g = GeomState::carve(geom, V, P, nullptr);
-  BinningState b = BinningState::carve(binning, V, total, inst.blk[V], nullptr);
+  const TilePack tp = tile_pack(P, width, height);
+  BinningState b = BinningState::carve(binning, V, total, inst.blk[V], !tp.packed, nullptr);
   ImageState img = ImageState::carve(image, V, width, height, nullptr);
   const int gx = div_up(width, GSR_TILE_X), gy = div_up(height, GSR_TILE_Y);
   const int tres = tile_sort_result(width, height);
@@ -295,11 +294,10 @@ int gsr_set_render(int V, int P, const int* K, int width, int height, const floa
     PhaseScope ps(GSR_PHASE_BINNING, s);
     GSR_HIP_CHECK(hipMemsetAsync(img.ranges, 0, sizeof(uint2) * (size_t)V * gx * gy, s));
     if (total > 0) {
-      launch_emit(V, P, width, g, g.dval[depth_sort_result()], inst, b.key[0], b.val[0], s);
-      const int res = seg_sort(b.key, b.val, false, inst, tile_key_bits(width, height), b.sort_counts,
-                               b.sort_totals, s);
+      launch_emit(V, P, width, g, g.dval[depth_sort_result()], inst, tp.gbits, b.key[0], b.val[0], s);
+      const int res = seg_sort(b.key, b.val, false, inst, tp.gbits, tp.tile_bits, b.sort_counts, b.sort_totals, s);
       if (res != tres) return fail(GSR_EHIP, "%s", "internal: tile sort buffer");
-      launch_tile_ranges(inst, gx * gy, b.key[res], img.ranges, s);
+      launch_tile_ranges(inst, gx * gy, tp.gbits, b.key[res], img.ranges, s);
     }
   }
   {
@@ -312,13 +310,14 @@ int gsr_set_render(int V, int P, const int* K, int width, int height, const floa
     rs.H = height;
     rs.gx = gx;
     rs.gy = gy;
+    rs.gmask = tp.gmask;
     for (int v = 0; v < V; ++v) {
       if (bgs[v] == nullptr) return fail(GSR_EINVAL, "%s", "null background");
       rs.inst_start[v] = inst.start[v];
       rs.row_start[v] = 0;
       rs.bg[v] = bgs[v];
     }
-    launch_render_forward(rs, g, b.val[tres], img, out_color, out_depth, out_alpha, s);
+    launch_render_forward(rs, g, tp.packed ? b.key[tres] : b.val[tres], img, out_color, out_depth, out_alpha, s);
   }
   return last_launch();
 }
@@ -350,11 +349,13 @@ int gsr_set_backward(int V, int P, int degree, int M, const int* K, int width, i
   if (inst_segments(V, K, inst, &total) != GSR_OK) return GSR_EINVAL;
   hipStream_t s = (hipStream_t)stream;
   GeomState g = GeomState::carve((void*)geom, V, P, nullptr);
-  BinningState b = BinningState::carve((void*)binning, V, total, inst.blk[V], nullptr);
+  const TilePack tp = tile_pack(P, width, height);
+  BinningState b = BinningState::carve((void*)binning, V, total, inst.blk[V], !tp.packed, nullptr);
   ImageState img = ImageState::carve((void*)image, V, width, height, nullptr);
   const int gx = div_up(width, GSR_TILE_X), gy = div_up(height, GSR_TILE_Y);
   const size_t HW = (size_t)width * height;
-  const uint32_t* sorted = b.val[tile_sort_result(width, height)];
+  const int tres = tile_sort_result(width, height);
+  const uint32_t* sorted = tp.packed ? b.key[tres] : b.val[tres];
   GaussBackwardArgs a = shared_args(P, degree, M, means3D, scales, scale_modifier, rotations, shs, cov3D_precomp,
                                      dL_dcolors, dL_dopacity, dL_dmeans3D, dL_dcov3D, dL_dsh, dL_dscales,
                                      dL_drotations);
@@ -376,6 +377,7 @@ int gsr_set_backward(int V, int P, int degree, int M, const int* K, int width, i
     rs.H = height;
     rs.gx = gx;
     rs.gy = gy;
+    rs.gmask = tp.gmask;
     ViewGradArgs va;
     va.V = g1 - g0;
     va.v0 = g0;
@@ -427,7 +429,15 @@ int gsr_set_backward(int V, int P, int degree, int M, const int* K, int width, i
 // ---- one view (the reference's per-call interface): a set of one --------------------------
 
 size_t gsr_geom_bytes(int P) { return gsr_set_geom_bytes(1, P); }
-size_t gsr_binning_bytes(int K, int width, int height) { return gsr_set_binning_bytes(1, &K, width, height); }
+// P is not known here: size for the unpacked layout, which is never smaller than the packed one.
+size_t gsr_binning_bytes(int K, int width, int height) {
+  SegInfo seg;
+  long long total = 0;
+  if (K < 0 || inst_segments(1, &K, seg, &total) != GSR_OK) return 0;
+  size_t b = 0;
+  BinningState::carve(nullptr, 1, total, seg.blk[1], true, &b);
+  return b;
+}
 size_t gsr_image_bytes(int width, int height) { return gsr_set_image_bytes(1, width, height); }
 size_t gsr_backward_bytes(int P, int K) { return gsr_set_backward_bytes(1, P, &K); }
 

@@ -236,94 +236,77 @@ __device__ __forceinline__ void put(float* p, float v, bool acc) { *p = acc ? *p
 static inline __host__ __device__ int sh_lds_stride(int M) { return ((3 * M + 3) & ~3) + 4; }
 
 // ---- A: per (view, Gaussian) ----------------------------------------------------------------
-// Block b -> view b % V, Gaussians [256 (b / V), +256): the views of one Gaussian slice run together,
-// so its parameters come from HBM once per group.  LDS: the view's tile cut-offs (8 B per tile).
+// Block b -> view b % V, Gaussians [1024 (b / V), +1024) (4 per thread, 256 apart): the views of one
+// Gaussian slice run together, so its parameters come from HBM once per group.  LDS: the view's
+// tile cut-offs (8 B per tile, loaded once per 1024 Gaussians).
+#define GSR_VG_ITEMS 4
 __global__ __launch_bounds__(256) void k_view_grad(GaussBackwardArgs a, ViewGradArgs va) {
   extern __shared__ uint2 s_cut[];
   const int t = threadIdx.x;
   const int vl = blockIdx.x % va.V;
   const int vg = va.v0 + vl;
-  const uint4* tinfo = va.img.tile_info + (size_t)vg * va.tiles;
-  const uint2* cut = reinterpret_cast<const uint2*>(s_cut);
+  const uint2* cut = va.cut_in_lds ? reinterpret_cast<const uint2*>(s_cut) : va.img.cut + (size_t)vg * va.tiles;
   if (va.cut_in_lds) {
-    for (int k = t; k < va.tiles; k += 256) {
-      const uint4 ti = tinfo[k];
-      s_cut[k] = make_uint2(ti.y, ti.z);
-    }
+    const uint4* src = reinterpret_cast<const uint4*>(va.img.cut + (size_t)vg * va.tiles);
+    uint4* dst = reinterpret_cast<uint4*>(s_cut);
+    for (int k = t; k < va.tiles / 2; k += 256) dst[k] = src[k];
+    if ((va.tiles & 1) && t == 0) s_cut[va.tiles - 1] = va.img.cut[(size_t)vg * va.tiles + va.tiles - 1];
     __syncthreads();
   }
-  const int idx = (blockIdx.x / va.V) * 256 + t;
-  if (idx >= a.P) return;
-  const size_t o = (size_t)vg * a.P + idx;
-  float* m2 = va.dmeans2D + 3 * o;
-  float* rec = va.vrec + (size_t)vl * GSR_GRAD_FIELDS * a.P + idx;
-  if (va.radii[o] <= 0) {
-    m2[0] = 0.f;
-    m2[1] = 0.f;
-    m2[2] = 0.f;
-#pragma unroll
-    for (int f = 0; f < GSR_GRAD_FIELDS; ++f) rec[(size_t)f * a.P] = 0.f;
-    return;
-  }
-  RowSums r;
-  if (va.cut_in_lds) {
-    r = gather_rows((uint32_t)idx, __float_as_uint(va.g.rec1[o].z), va.g.goff[o], va.g.rect[o], va.gx, cut,
-                    va.grow + (size_t)12 * va.row_start[vl]);
-  } else {
-    // image too large for LDS: the same cut-offs read from tile_info (L2)
-    r = RowSums{0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-    const uint2 rc = va.g.rect[o];
-    const uint32_t dkey = __float_as_uint(va.g.rec1[o].z);
-    const int xmin = rc.x & 0xffff, ymin = rc.x >> 16, xmax = rc.y & 0xffff, ymax = rc.y >> 16;
-    size_t i = (size_t)va.row_start[vl] + va.g.goff[o];
-    for (int ty = ymin; ty < ymax; ++ty)
-      for (int tx = xmin; tx < xmax; ++tx, ++i) {
-        const uint4 c = tinfo[ty * va.gx + tx];
-        if (!(dkey < c.y || (dkey == c.y && (uint32_t)idx < c.z))) continue;
-        const float4* row = va.grow + 12 * i;
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          const float4 r0 = row[3 * q], r1 = row[3 * q + 1], r2 = row[3 * q + 2];
-          r.dmx += r0.x; r.dmy += r0.y; r.dca += r0.z; r.dcb += r0.w;
-          r.dcc += r1.x; r.dop += r1.y; r.dcr += r1.z; r.dcg += r1.w;
-          r.dcbl += r2.x; r.ddep += r2.y;
-        }
-      }
-  }
-  m2[0] = r.dmx;
-  m2[1] = r.dmy;
-  m2[2] = 0.f;
-  const float3 mean = make_float3(a.means3D[3 * idx], a.means3D[3 * idx + 1], a.means3D[3 * idx + 2]);
-  float cov3D[6];
-  if (a.cov3D_precomp) {
-#pragma unroll
-    for (int k = 0; k < 6; ++k) cov3D[k] = a.cov3D_precomp[6 * idx + k];
-  } else {
-    const float3 scale = make_float3(a.scales[3 * idx], a.scales[3 * idx + 1], a.scales[3 * idx + 2]);
-    const float4 rot = make_float4(a.rotations[4 * idx], a.rotations[4 * idx + 1], a.rotations[4 * idx + 2],
-                                   a.rotations[4 * idx + 3]);
-    cov3d_from_scale_rot(scale, a.scale_modifier, rot, cov3D);
-  }
   const ViewCam& cam = va.cam[vl];
-  ViewGeom vgm;
-  vgm.view = cam.view;
-  vgm.proj = cam.proj;
-  vgm.tanx = cam.tanx;
-  vgm.tany = cam.tany;
-  vgm.fy = va.H / (2.0f * cam.tany);
-  vgm.fx = va.W / (2.0f * cam.tanx);
-  float dcv[6];
-  float3 dm;
-  cov2d_backward(mean, cov3D, vgm, r.dca, r.dcb, r.dcc, dcv, dm);
-  proj_backward(mean, cam.proj, r.dmx, r.dmy, dm);
-  // view depth = view[2] x + view[6] y + view[10] z + view[14]
-  dm.x += cam.view[2] * r.ddep;
-  dm.y += cam.view[6] * r.ddep;
-  dm.z += cam.view[10] * r.ddep;
-  const float f[GSR_GRAD_FIELDS] = {dm.x, dm.y, dm.z, dcv[0], dcv[1], dcv[2], dcv[3], dcv[4], dcv[5],
-                                    r.dcr, r.dcg, r.dcbl, r.dop};
+  const float4* grow = va.grow + (size_t)12 * va.row_start[vl];
+  float* recv = va.vrec + (size_t)vl * GSR_GRAD_FIELDS * a.P;
+#pragma unroll 1
+  for (int it = 0; it < GSR_VG_ITEMS; ++it) {
+    const int idx = (blockIdx.x / va.V) * (256 * GSR_VG_ITEMS) + it * 256 + t;
+    if (idx >= a.P) break;
+    const size_t o = (size_t)vg * a.P + idx;
+    float* m2 = va.dmeans2D + 3 * o;
+    float* rec = recv + idx;
+    if (va.radii[o] <= 0) {
+      m2[0] = 0.f;
+      m2[1] = 0.f;
+      m2[2] = 0.f;
 #pragma unroll
-  for (int k = 0; k < GSR_GRAD_FIELDS; ++k) rec[(size_t)k * a.P] = f[k];
+      for (int f = 0; f < GSR_GRAD_FIELDS; ++f) rec[(size_t)f * a.P] = 0.f;
+      continue;
+    }
+    const RowSums r = gather_rows((uint32_t)idx, __float_as_uint(va.g.rec1[o].z), va.g.goff[o], va.g.rect[o], va.gx,
+                                  cut, grow);
+    m2[0] = r.dmx;
+    m2[1] = r.dmy;
+    m2[2] = 0.f;
+    const float3 mean = make_float3(a.means3D[3 * idx], a.means3D[3 * idx + 1], a.means3D[3 * idx + 2]);
+    float cov3D[6];
+    if (a.cov3D_precomp) {
+#pragma unroll
+      for (int k = 0; k < 6; ++k) cov3D[k] = a.cov3D_precomp[6 * idx + k];
+    } else {
+      const float3 scale = make_float3(a.scales[3 * idx], a.scales[3 * idx + 1], a.scales[3 * idx + 2]);
+      const float4 rot = make_float4(a.rotations[4 * idx], a.rotations[4 * idx + 1], a.rotations[4 * idx + 2],
+                                     a.rotations[4 * idx + 3]);
+      cov3d_from_scale_rot(scale, a.scale_modifier, rot, cov3D);
+    }
+    ViewGeom vgm;
+    vgm.view = cam.view;
+    vgm.proj = cam.proj;
+    vgm.tanx = cam.tanx;
+    vgm.tany = cam.tany;
+    vgm.fy = va.H / (2.0f * cam.tany);
+    vgm.fx = va.W / (2.0f * cam.tanx);
+    float dcv[6];
+    float3 dm;
+    cov2d_backward(mean, cov3D, vgm, r.dca, r.dcb, r.dcc, dcv, dm);
+    proj_backward(mean, cam.proj, r.dmx, r.dmy, dm);
+    // view depth = view[2] x + view[6] y + view[10] z + view[14]
+    dm.x += cam.view[2] * r.ddep;
+    dm.y += cam.view[6] * r.ddep;
+    dm.z += cam.view[10] * r.ddep;
+    const float f[GSR_GRAD_FIELDS] = {dm.x, dm.y, dm.z, dcv[0], dcv[1], dcv[2], dcv[3], dcv[4], dcv[5],
+                                      r.dcr, r.dcg, r.dcbl, r.dop};
+#pragma unroll
+    for (int k = 0; k < GSR_GRAD_FIELDS; ++k) rec[(size_t)k * a.P] = f[k];
+  }
 }
 
 // ---- B: per Gaussian, over the group's views ---------------------------------------------------
@@ -429,8 +412,8 @@ void launch_gauss_backward(const GaussBackwardArgs& a, ViewGradArgs va, const Ac
   if (a.P <= 0 || va.V <= 0) return;
   const size_t cut_bytes = sizeof(uint2) * (size_t)va.tiles;
   va.cut_in_lds = cut_bytes <= GSR_CUT_LDS_MAX ? 1 : 0;
-  hipLaunchKernelGGL(k_view_grad, dim3(va.V * div_up(a.P, 256)), dim3(256), va.cut_in_lds ? cut_bytes : 0, stream,
-                     a, va);
+  hipLaunchKernelGGL(k_view_grad, dim3(va.V * div_up(a.P, 256 * GSR_VG_ITEMS)), dim3(256),
+                     va.cut_in_lds ? cut_bytes : 0, stream, a, va);
   const size_t lds = (a.shs && a.M > 0) ? (size_t)256 * sh_lds_stride(a.M) * sizeof(float) : 0;
   hipLaunchKernelGGL(k_gauss_accum, dim3(div_up(a.P, 256)), dim3(256), lds, stream, a, b);
 }

@@ -73,18 +73,24 @@ __global__ __launch_bounds__(256) void k_inst_scan(int nbe, GeomState g) {
 // Emit one (tile id, Gaussian) instance per tile of each visible Gaussian, in depth order, and
 // goff[g] = the Gaussian's first instance.  A block owns 1024 consecutive depth-sorted Gaussians
 // of one view (4 per thread); its instances are one contiguous range (offset from k_inst_scan),
-// written cooperatively: instance j of the block belongs to the last Gaussian whose local offset
-// is <= j (binary search in LDS), so consecutive lanes write consecutive addresses.
+// written cooperatively in chunks of 2048 so consecutive lanes write consecutive addresses.  The
+// owner of every position of a chunk comes from an owner map: each Gaussian marks its first
+// position, and a max-scan over the chunk spreads the marks (offsets grow with the Gaussian).
+#define GSR_EMIT_CHUNK 2048
 struct DupLDS {
   uint32_t off[GSR_DUP_TILE + 1];
   uint32_t gi[GSR_DUP_TILE];
   uint2 rect[GSR_DUP_TILE];
+  uint32_t own[GSR_EMIT_CHUNK];
   uint32_t wave[8];
+  uint32_t carry;
 };
 
 __global__ __launch_bounds__(256) void k_emit(int P, int nbe, int grid_x, GeomState g, const uint32_t* __restrict__ order,
-                                              SegInfo inst, uint32_t* __restrict__ keys, uint32_t* __restrict__ vals) {
+                                              SegInfo inst, int gbits, uint32_t* __restrict__ keys,
+                                              uint32_t* __restrict__ vals) {
   __shared__ DupLDS s;
+  constexpr int PER = GSR_EMIT_CHUNK / 256;
   const int v = blockIdx.x / nbe, lb = blockIdx.x % nbe;
   const int t = threadIdx.x;
   const size_t vo = (size_t)v * P;
@@ -102,48 +108,101 @@ __global__ __launch_bounds__(256) void k_emit(int P, int nbe, int grid_x, GeomSt
   uint32_t btot;
   const uint32_t local = block_exclusive_scan<256>(sum, &btot, s.wave);
   const uint32_t prefix = g.inst_counts[(size_t)v * nbe + lb];
+  uint32_t myoff[GSR_DUP_ITEMS];
   {
     uint32_t o = local;
 #pragma unroll
     for (int k = 0; k < GSR_DUP_ITEMS; ++k) {
+      myoff[k] = o;
       s.off[t * GSR_DUP_ITEMS + k] = o;
       if (cnt[k]) g.goff[vo + gi[k]] = prefix + o;
       o += cnt[k];
     }
     if (t == 255) s.off[GSR_DUP_TILE] = btot;
   }
-  __syncthreads();
   uint32_t* kout = keys + inst.start[v] + prefix;
-  uint32_t* vout = vals + inst.start[v] + prefix;
-  for (uint32_t j = t; j < btot; j += 256u) {
-    int lo = 0, hi = GSR_DUP_TILE;  // off[lo] <= j < off[hi]
-    while (hi - lo > 1) {
-      const int mid = (lo + hi) >> 1;
-      if (s.off[mid] <= j) lo = mid;
-      else hi = mid;
+  uint32_t* vout = vals ? vals + inst.start[v] + prefix : nullptr;
+  for (uint32_t c0 = 0; c0 < btot; c0 += GSR_EMIT_CHUNK) {
+#pragma unroll
+    for (int k = 0; k < PER; ++k) s.own[k * 256 + t] = 0u;
+    __syncthreads();  // (also publishes s.off before the first chunk)
+    if (t == 0) {
+      // owner of the chunk's first position: last m with off[m] <= c0 (non-empty)
+      int lo = 0, hi = GSR_DUP_TILE;
+      while (hi - lo > 1) {
+        const int mid = (lo + hi) >> 1;
+        if (s.off[mid] <= c0) lo = mid;
+        else hi = mid;
+      }
+      s.carry = (uint32_t)lo + 1u;
     }
-    const uint2 rc = s.rect[lo];
-    const uint32_t xmin = rc.x & 0xffffu, ymin = rc.x >> 16, xmax = rc.y & 0xffffu;
-    const uint32_t w = xmax - xmin, l = j - s.off[lo];
-    const uint32_t ty = l / w, tx = l - ty * w;
-    kout[j] = (ymin + ty) * (uint32_t)grid_x + xmin + tx;
-    vout[j] = s.gi[lo];
+#pragma unroll
+    for (int k = 0; k < GSR_DUP_ITEMS; ++k)
+      if (cnt[k] && myoff[k] >= c0 && myoff[k] < c0 + GSR_EMIT_CHUNK) s.own[myoff[k] - c0] = (uint32_t)(t * GSR_DUP_ITEMS + k) + 1u;
+    __syncthreads();
+    // max-scan of the marks: thread t owns positions [PER t, PER t + PER)
+    uint32_t m[PER], run = 0u;
+#pragma unroll
+    for (int k = 0; k < PER; ++k) {
+      run = max(run, s.own[PER * t + k]);
+      m[k] = run;
+    }
+    const uint32_t before = max(s.carry, block_exclusive_max<256>(run, s.wave));
+#pragma unroll
+    for (int k = 0; k < PER; ++k) s.own[PER * t + k] = max(before, m[k]) - 1u;
+    __syncthreads();
+    const uint32_t cend = min(btot - c0, (uint32_t)GSR_EMIT_CHUNK);
+#pragma unroll
+    for (int k = 0; k < PER; ++k) {
+      const uint32_t jj = k * 256 + t;
+      if (jj < cend) {
+        const uint32_t j = c0 + jj;
+        const uint32_t ow = s.own[jj];
+        const uint2 rc = s.rect[ow];
+        const uint32_t xmin = rc.x & 0xffffu, ymin = rc.x >> 16, xmax = rc.y & 0xffffu;
+        const uint32_t w = xmax - xmin, l = j - s.off[ow];
+        // l / w without the ~35-instruction integer division: l < 2^24, so the float quotient is
+        // within one of the true one; one correction step makes it exact
+        int ty = (int)((float)l * __builtin_amdgcn_rcpf((float)w));
+        int tx = (int)l - ty * (int)w;
+        if (tx < 0) { --ty; tx += (int)w; }
+        else if (tx >= (int)w) { ++ty; tx -= (int)w; }
+        const uint32_t tile = (ymin + (uint32_t)ty) * (uint32_t)grid_x + xmin + (uint32_t)tx;
+        if (vout) {
+          kout[j] = tile;
+          vout[j] = s.gi[ow];
+        } else {
+          kout[j] = (tile << gbits) | s.gi[ow];
+        }
+      }
+    }
+    __syncthreads();
   }
 }
 
 // After the tile sort: per-tile [start, end) ranges (view-local positions) of each view's list.
-__global__ __launch_bounds__(GSR_RANGE_TILE) void k_tile_ranges(SegInfo inst, int n_tiles, const uint32_t* __restrict__ keys,
-                                                                uint2* __restrict__ ranges) {
+// 4 consecutive instances per thread (one 16-byte load, neighbours from the adjacent lanes).
+__global__ __launch_bounds__(256) void k_tile_ranges(SegInfo inst, int n_tiles, int gbits,
+                                                     const uint32_t* __restrict__ keys,
+                                                     uint2* __restrict__ ranges) {
   uint32_t lb;
   const int v = seg_of_block(inst, blockIdx.x, lb);
-  const uint32_t p = lb * GSR_RANGE_TILE + threadIdx.x;
+  const uint32_t p0 = (lb * 256 + threadIdx.x) * 4;
   const uint32_t K = inst.n[v];
-  if (p >= K) return;
+  if (p0 >= K) return;
   const uint32_t* kv = keys + inst.start[v];
   uint2* rv = ranges + (size_t)v * n_tiles;
-  const uint32_t tile = kv[p];
-  if (p == 0 || kv[p - 1] != tile) rv[tile].x = p;
-  if (p == K - 1 || kv[p + 1] != tile) rv[tile].y = p + 1;
+  uint32_t t[6];
+  t[0] = p0 > 0 ? kv[p0 - 1] >> gbits : 0xFFFFFFFFu;
+#pragma unroll
+  for (int k = 0; k < 5; ++k) t[k + 1] = p0 + k < K ? kv[p0 + k] >> gbits : 0xFFFFFFFFu;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const uint32_t p = p0 + k;
+    if (p >= K) break;
+    if (t[k] != t[k + 1]) rv[t[k + 1]].x = p;
+    if (t[k + 2] != t[k + 1]) rv[t[k + 1]].y = p + 1;
+  }
 }
 
 void launch_binning_counts(int V, int P, const GeomState& g, const uint32_t* order, hipStream_t stream) {
@@ -154,19 +213,18 @@ void launch_binning_counts(int V, int P, const GeomState& g, const uint32_t* ord
   hipLaunchKernelGGL(k_inst_scan, dim3(V), dim3(256), 0, stream, P > 0 ? nbe : 0, g);
 }
 
-void launch_emit(int V, int P, int W, const GeomState& g, const uint32_t* order, const SegInfo& inst,
+void launch_emit(int V, int P, int W, const GeomState& g, const uint32_t* order, const SegInfo& inst, int gbits,
                  uint32_t* keys, uint32_t* vals, hipStream_t stream) {
   if (V <= 0 || P <= 0) return;
   const int nbe = GeomState::dup_blocks(P);
   hipLaunchKernelGGL(k_emit, dim3(V * nbe), dim3(256), 0, stream, P, nbe, div_up(W, GSR_TILE_X), g, order, inst,
-                     keys, vals);
+                     gbits, keys, vals);
 }
 
-void launch_tile_ranges(SegInfo inst, int n_tiles, const uint32_t* keys, uint2* ranges, hipStream_t stream) {
+void launch_tile_ranges(SegInfo inst, int n_tiles, int gbits, const uint32_t* keys, uint2* ranges, hipStream_t stream) {
   seg_fill_blocks(inst, GSR_RANGE_TILE);
   if (inst.blk[inst.V] == 0) return;
-  hipLaunchKernelGGL(k_tile_ranges, dim3(inst.blk[inst.V]), dim3(GSR_RANGE_TILE), 0, stream, inst, n_tiles, keys,
-                     ranges);
+  hipLaunchKernelGGL(k_tile_ranges, dim3(inst.blk[inst.V]), dim3(256), 0, stream, inst, n_tiles, gbits, keys, ranges);
 }
 
 // markVisible / checkFrustum of the reference (API completeness).

@@ -21,8 +21,8 @@
 // Instance emission: 256 threads x 4 depth-sorted Gaussians per block.
 #define GSR_DUP_ITEMS 4
 #define GSR_DUP_TILE (256 * GSR_DUP_ITEMS)  // 1024
-// Tile ranges: one instance per thread.
-#define GSR_RANGE_TILE 256
+// Tile ranges: 256 threads x 4 instances per block.
+#define GSR_RANGE_TILE 1024
 
 // Rasterizer constants of the reference algorithm ([EXT] graphdeco
 // cuda_rasterizer/forward.cu + auxiliary.h).
@@ -58,6 +58,25 @@ static inline int tile_key_bits(int W, int H) {
   int bits = 0;
   while ((1 << bits) < tiles) ++bits;
   return bits < 1 ? 1 : bits;
+}
+
+// Instance key layout.  When the Gaussian index and the tile id fit one 32-bit word together
+// (1M Gaussians at 1024^2: 20 + 12 bits) the tile sort moves packed keys (tile << gbits | Gaussian)
+// and no values: half the bytes of every binning pass.  Otherwise keys = tile, values = Gaussian.
+struct TilePack {
+  bool packed;
+  int gbits, tile_bits;
+  uint32_t gmask;  // sorted entry -> Gaussian
+};
+static inline TilePack tile_pack(int P, int W, int H) {
+  TilePack t;
+  t.tile_bits = tile_key_bits(W, H);
+  int gb = 1;
+  while (gb < 32 && (1ll << gb) < (long long)P) ++gb;
+  t.packed = gb + t.tile_bits <= 32;
+  t.gbits = t.packed ? gb : 0;
+  t.gmask = t.packed ? (uint32_t)((1ull << gb) - 1ull) : 0xFFFFFFFFu;
+  return t;
 }
 
 // LSD digit split of a key_bits-wide key: passes of equal width <= 8 bits.
@@ -164,14 +183,15 @@ struct BinningState {
   uint32_t* val[2];        // Gaussian index ping-pong; after the sort: sorted position -> Gaussian
   uint32_t* sort_counts;   // [RADIX x sort blocks of all views]
   uint32_t* sort_totals;   // [V][RADIX]
-  static BinningState carve(void* base, int V, long long Ktot, long long sort_blocks, size_t* bytes) {
+  // with_vals = false: packed keys (tile << gbits | Gaussian), no value arrays (TilePack)
+  static BinningState carve(void* base, int V, long long Ktot, long long sort_blocks, bool with_vals, size_t* bytes) {
     Carver c(base);
     BinningState b;
     const size_t n = (size_t)(Ktot > 0 ? Ktot : 1);
     b.key[0] = c.take<uint32_t>(n);
     b.key[1] = c.take<uint32_t>(n);
-    b.val[0] = c.take<uint32_t>(n);
-    b.val[1] = c.take<uint32_t>(n);
+    b.val[0] = with_vals ? c.take<uint32_t>(n) : nullptr;
+    b.val[1] = with_vals ? c.take<uint32_t>(n) : nullptr;
     b.sort_counts = c.take<uint32_t>((size_t)GSR_RADIX * (size_t)(sort_blocks > 0 ? sort_blocks : 1));
     b.sort_totals = c.take<uint32_t>((size_t)GSR_RADIX * (size_t)(V > 0 ? V : 1));
     if (bytes) *bytes = align_up(c.off, 256);
@@ -184,6 +204,7 @@ struct ImageState {
   uint2* ranges;       // [V][tiles] sorted-instance range of each tile (view-local positions)
   uint32_t* quad_maxc; // [V][4*tiles] per 8x8 quadrant: instances [0, maxc) of the tile list were blended
   uint4* tile_info;    // [V][tiles] (tile maxc, depth key and Gaussian of the first unblended instance, 0)
+  uint2* cut;          // [V][tiles] (depth key, Gaussian) of tile_info: the backward gather's cut-off table
   float* final_T;      // [V][H*W]
   uint32_t* n_contrib; // [V][H*W]
   static ImageState carve(void* base, int V, int W, int H, size_t* bytes) {
@@ -195,6 +216,7 @@ struct ImageState {
     s.ranges = c.take<uint2>(nv * (tiles > 0 ? tiles : 1));
     s.quad_maxc = c.take<uint32_t>(nv * 4 * (tiles > 0 ? tiles : 1));
     s.tile_info = c.take<uint4>(nv * (tiles > 0 ? tiles : 1));
+    s.cut = c.take<uint2>(nv * (tiles > 0 ? tiles : 1));
     s.final_T = c.take<float>(nv * (pix > 0 ? pix : 1));
     s.n_contrib = c.take<uint32_t>(nv * (pix > 0 ? pix : 1));
     if (bytes) *bytes = align_up(c.off, 256);

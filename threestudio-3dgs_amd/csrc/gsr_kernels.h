@@ -7,11 +7,12 @@
 namespace gsr {
 
 // Stable LSD radix sort of every segment of a view set (segment v = n[v] pairs at start[v]) on
-// key bits [0, key_bits), digit_plan(key_bits) passes of count / scan / scatter (gsr_sort.hip).
-// Ping-pongs between keys[0]/vals[0] and keys[1]/vals[1]; returns the index (0/1) holding the
-// result.  vals_identity: the input values are the positions within the segment.  counts needs
+// key bits [bit_lo, bit_lo + key_bits), digit_plan(key_bits) passes of count / scan / scatter
+// (gsr_sort.hip).  Ping-pongs between keys[0]/vals[0] and keys[1]/vals[1]; returns the index (0/1)
+// holding the result.  vals_identity: the input values are the positions within the segment;
+// vals == nullptr or vals[0] == nullptr (and not identity): keys only.  counts needs
 // RADIX x (total 4096-item blocks) words, totals RADIX x V.
-int seg_sort(uint32_t* keys[2], uint32_t* vals[2], bool vals_identity, SegInfo seg, int key_bits,
+int seg_sort(uint32_t* keys[2], uint32_t* vals[2], bool vals_identity, SegInfo seg, int bit_lo, int key_bits,
              uint32_t* counts, uint32_t* totals, hipStream_t stream);
 
 // Forward preprocess (cull, project, EWA, SH) of every (view, Gaussian) — gsr_preprocess.hip
@@ -26,9 +27,10 @@ void launch_preprocess(const PreprocessArgs& a, const SetCams& cams, const GeomS
 
 // Binning — gsr_binning.hip.  order = the depth sort's value buffer (per view: sorted position -> Gaussian).
 void launch_binning_counts(int V, int P, const GeomState& g, const uint32_t* order, hipStream_t stream);
-void launch_emit(int V, int P, int W, const GeomState& g, const uint32_t* order, const SegInfo& inst,
+// vals == nullptr: packed keys (tile << gbits | Gaussian)
+void launch_emit(int V, int P, int W, const GeomState& g, const uint32_t* order, const SegInfo& inst, int gbits,
                  uint32_t* keys, uint32_t* vals, hipStream_t stream);
-void launch_tile_ranges(SegInfo inst, int n_tiles, const uint32_t* keys, uint2* ranges, hipStream_t stream);
+void launch_tile_ranges(SegInfo inst, int n_tiles, int gbits, const uint32_t* keys, uint2* ranges, hipStream_t stream);
 void launch_mark_visible(int P, const float* means3D, const float* view, const float* proj,
                          uint8_t* present, hipStream_t stream);
 
@@ -37,6 +39,7 @@ void launch_mark_visible(int P, const float* means3D, const float* view, const f
 // first instance in it; row_start[v] = the view's first gradient row slot in the backward scratch.
 struct RenderSet {
   int V, v0, P, W, H, gx, gy;
+  uint32_t gmask;  // sorted entry -> Gaussian (TilePack)
   uint32_t inst_start[GSR_SET_MAX];
   uint32_t row_start[GSR_SET_MAX];
   const float* bg[GSR_SET_MAX];

@@ -133,18 +133,30 @@ __global__ __launch_bounds__(64) void k_render_fwd(RenderSet rs,
   bool done = !inside;
   float T = 1.0f, Cr = 0.f, Cg = 0.f, Cb = 0.f, D = 0.f;
   uint32_t last_contributor = 0;
+  // two-stage prefetch (as in the backward): indices two batches ahead, records one batch ahead
+  const uint32_t gmask = rs.gmask;
+  const float4 zero4 = make_float4(0.f, 0.f, 0.f, 0.f);
+  float4 n0 = zero4, n1 = zero4, n2 = zero4;
+  uint32_t gi_next = 0u;
+  if (lane < n) {
+    const uint32_t g0 = sorted_gauss[range.x + lane] & gmask;
+    n0 = rec0[g0];
+    n1 = rec1[g0];
+    n2 = rec2[g0];
+  }
+  if (64 + lane < n) gi_next = sorted_gauss[range.x + 64 + lane] & gmask;
   for (int base = 0; base < n; base += 64) {
     if (__all(done)) break;
     const int i = base + lane;
-    bool keep = false;
-    float4 r0, r1, r2;
-    if (i < n) {
-      const uint32_t gi = sorted_gauss[range.x + i];
-      r0 = rec0[gi];
-      r1 = rec1[gi];
-      r2 = rec2[gi];
-      keep = quadrant_hit(r0, r1, (float)qx0, (float)qy0);
+    const float4 r0 = n0, r1 = n1, r2 = n2;
+    if (base + 64 + lane < n) {
+      n0 = rec0[gi_next];
+      n1 = rec1[gi_next];
+      n2 = rec2[gi_next];
     }
+    if (base + 128 + lane < n) gi_next = sorted_gauss[range.x + base + 128 + lane] & gmask;
+    bool keep = false;
+    if (i < n) keep = quadrant_hit(r0, r1, (float)qx0, (float)qy0);
     const unsigned long long bal = __ballot(keep);
     const int cnt = __popcll(bal);
     if (keep) {
@@ -203,7 +215,7 @@ __global__ __launch_bounds__(256) void k_tile_info(RenderSet rs, const uint2* __
                                                    const uint32_t* __restrict__ quad_maxc,
                                                    const uint32_t* __restrict__ sorted_gauss,
                                                    const float4* __restrict__ rec1,
-                                                   uint4* __restrict__ tile_info) {
+                                                   uint4* __restrict__ tile_info, uint2* __restrict__ cut) {
   const int n_tiles = rs.gx * rs.gy;
   const int nb = div_up(n_tiles, 256);
   const int v = blockIdx.x / nb;
@@ -214,6 +226,7 @@ __global__ __launch_bounds__(256) void k_tile_info(RenderSet rs, const uint2* __
     ranges += vg * n_tiles;
     quad_maxc += vg * 4 * n_tiles;
     tile_info += vg * n_tiles;
+    cut += vg * n_tiles;
     sorted_gauss += rs.inst_start[v];
     rec1 += vg * rs.P;
   }
@@ -222,11 +235,12 @@ __global__ __launch_bounds__(256) void k_tile_info(RenderSet rs, const uint2* __
   const uint2 range = ranges[tile];
   uint4 info = make_uint4(maxc, 0xFFFFFFFFu, 0xFFFFFFFFu, 0u);
   if (maxc < range.y - range.x) {
-    const uint32_t gi = sorted_gauss[range.x + maxc];
+    const uint32_t gi = sorted_gauss[range.x + maxc] & rs.gmask;
     info.y = __float_as_uint(rec1[gi].z);
     info.z = gi;
   }
   tile_info[tile] = info;
+  cut[tile] = make_uint2(info.y, info.z);
 }
 
 void launch_render_forward(const RenderSet& rs, const GeomState& g, const uint32_t* sorted_gauss,
@@ -240,7 +254,7 @@ void launch_render_forward(const RenderSet& rs, const GeomState& g, const uint32
                      img.final_T, img.n_contrib, img.quad_maxc);
   hipLaunchKernelGGL(k_tile_info, dim3(rs.V * div_up(nt, 256)), dim3(256), 0, stream, rs,
                      (const uint2*)img.ranges, (const uint32_t*)img.quad_maxc, sorted_gauss,
-                     (const float4*)g.rec1, img.tile_info);
+                     (const float4*)g.rec1, img.tile_info, img.cut);
 }
 
 // ---------------------------------------------------------------------------------------
@@ -342,19 +356,48 @@ __global__ __launch_bounds__(64) void k_render_bwd(RenderSet rs,
   const int prow = lane >> 4;
   const float4 zero4 = make_float4(0.f, 0.f, 0.f, 0.f);
 
+  // two-stage prefetch: sorted indices two batches ahead, 48-byte records (+ rect, goff) one batch
+  // ahead, so the dependent gather chain of the next batch overlaps this batch's replay
+  const uint32_t gmask = rs.gmask;
+  auto fetch_index = [&](int h) -> uint32_t {
+    const int r = h - 1 - lane;
+    return r >= 0 ? (sorted_gauss[range.x + r] & gmask) : 0u;
+  };
+  float4 n0 = zero4, n1 = zero4, n2 = zero4;
+  uint2 nrc = make_uint2(0u, 0u);
+  uint32_t ngo = 0u;
+  uint32_t gi_next = 0u;
+  if (maxc > 0) {
+    const uint32_t g0 = fetch_index(maxc);
+    if (maxc - 1 - lane >= 0) {
+      n0 = rec0[g0];
+      n1 = rec1[g0];
+      n2 = rec2[g0];
+      nrc = rect[g0];
+      ngo = goff[g0];
+    }
+    if (maxc > 64) gi_next = fetch_index(maxc - 64);
+  }
   for (int hi = maxc; hi > 0; hi -= 64) {
     const int rel_l = hi - 1 - lane;
     bool keep = false;
-    float4 r0, r1, r2;
+    const float4 r0 = n0, r1 = n1, r2 = n2;
+    const uint2 rc = nrc;
+    const uint32_t go = ngo;
+    if (hi > 64) {
+      if (hi - 65 - lane >= 0) {
+        n0 = rec0[gi_next];
+        n1 = rec1[gi_next];
+        n2 = rec2[gi_next];
+        nrc = rect[gi_next];
+        ngo = goff[gi_next];
+      }
+      if (hi > 128) gi_next = fetch_index(hi - 128);
+    }
     uint32_t dest = 0;
     if (rel_l >= 0) {
-      const uint32_t gi = sorted_gauss[range.x + rel_l];
-      r0 = rec0[gi];
-      r1 = rec1[gi];
-      r2 = rec2[gi];
-      const uint2 rc = rect[gi];
       const int xmin = rc.x & 0xffff, ymin = rc.x >> 16, xmax = rc.y & 0xffff;
-      dest = 4u * (goff[gi] + (uint32_t)((tyi - ymin) * (xmax - xmin) + (txi - xmin))) + (uint32_t)q;
+      dest = 4u * (go + (uint32_t)((tyi - ymin) * (xmax - xmin) + (txi - xmin))) + (uint32_t)q;
       keep = rel_l < qmaxc && quadrant_hit(r0, r1, (float)qx0, (float)qy0);
       if (!keep) {
         grow[3 * (size_t)dest] = zero4;

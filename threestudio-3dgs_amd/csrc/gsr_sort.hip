@@ -9,7 +9,7 @@
 //             counts[seg][digit][block] + rank; reorder in LDS; write digit runs.
 // No block ever waits on another (no look-back, no spinning, no memsets): on MI355X a
 // cross-workgroup hand-off is a cross-XCD round trip (≈1-3 µs), which made single-pass
-// look-back chains the critical path (profiles/diag_sort.py).  HBM traffic per pass:
+// look-back chains the critical path (measured).  HBM traffic per pass:
 // 4 B (count) + 8 B read + 8 B written per pair, plus 4 B x 256 per 4096 pairs of counts.
 //
 // In-block ranking is wave-blocked: wave w owns items [1024 w, 1024 w + 1024) of its block and
@@ -86,20 +86,23 @@ __global__ __launch_bounds__(256) void k_seg_scan(SegInfo seg, int R, uint32_t* 
   if (t == 0) totals[(size_t)v * GSR_RADIX + d] = carry;
 }
 
+template <bool KV>
 struct ScatterLDS {
   uint32_t keys[GSR_SORT_TILE];
-  uint32_t vals[GSR_SORT_TILE];
+  uint32_t vals[KV ? GSR_SORT_TILE : 1];
   uint32_t wcnt[4][GSR_RADIX];  // per-wave running count per digit -> per-wave offset within the digit
   uint32_t local[GSR_RADIX];    // block-local start of each digit
   uint32_t glob[GSR_RADIX];     // segment position of this block's first item of each digit
   uint32_t wave[8];
 };
 
+// KV = false: keys only (packed tile keys); vals_in / vals_out unused.
+template <bool KV>
 __global__ __launch_bounds__(GSR_SORT_THREADS) void k_seg_scatter(
     const uint32_t* __restrict__ keys_in, const uint32_t* __restrict__ vals_in, uint32_t* __restrict__ keys_out,
     uint32_t* __restrict__ vals_out, SegInfo seg, int shift, int bits, const uint32_t* __restrict__ counts,
     const uint32_t* __restrict__ totals) {
-  __shared__ ScatterLDS s;
+  __shared__ ScatterLDS<KV> s;
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
   uint32_t lb;
   const int v = seg_of_block(seg, blockIdx.x, lb);
@@ -115,7 +118,7 @@ __global__ __launch_bounds__(GSR_SORT_THREADS) void k_seg_scatter(
   for (int k = 0; k < GSR_SORT_ITEMS; ++k) {
     const uint32_t i = b0 + k * 64 + lane;
     key[k] = i < n ? keys_in[start + i] : 0u;
-    val[k] = i < n ? (vals_in ? vals_in[start + i] : i) : 0u;
+    if (KV) val[k] = i < n ? (vals_in ? vals_in[start + i] : i) : 0u;
   }
   __syncthreads();
 #pragma unroll
@@ -160,7 +163,7 @@ __global__ __launch_bounds__(GSR_SORT_THREADS) void k_seg_scatter(
       const uint32_t d = (key[k] >> shift) & mask;
       const uint32_t lp = s.local[d] + s.wcnt[w][d] + pos[k];
       s.keys[lp] = key[k];
-      s.vals[lp] = val[k];
+      if (KV) s.vals[lp] = val[k];
     }
   }
   __syncthreads();
@@ -173,13 +176,14 @@ __global__ __launch_bounds__(GSR_SORT_THREADS) void k_seg_scatter(
       const uint32_t d = (kk >> shift) & mask;
       const uint32_t dst = start + s.glob[d] + (j - s.local[d]);
       keys_out[dst] = kk;
-      vals_out[dst] = s.vals[j];
+      if (KV) vals_out[dst] = s.vals[j];
     }
   }
 }
 
-int seg_sort(uint32_t* keys[2], uint32_t* vals[2], bool vals_identity, SegInfo seg, int key_bits,
+int seg_sort(uint32_t* keys[2], uint32_t* vals[2], bool vals_identity, SegInfo seg, int bit_lo, int key_bits,
              uint32_t* counts, uint32_t* totals, hipStream_t stream) {
+  const bool kv = vals != nullptr && (vals[0] != nullptr || vals_identity);
   const DigitPlan plan = digit_plan(key_bits);
   seg_fill_blocks(seg, GSR_SORT_TILE);
   const uint32_t nb = seg.blk[seg.V];
@@ -188,12 +192,18 @@ int seg_sort(uint32_t* keys[2], uint32_t* vals[2], bool vals_identity, SegInfo s
     const int bits = plan.width(p, key_bits);
     const int dst = src ^ 1;
     if (nb > 0) {
+      const int shift = bit_lo + p * plan.bits;
       hipLaunchKernelGGL(k_seg_count, dim3(nb), dim3(GSR_SORT_THREADS), 0, stream, (const uint32_t*)keys[src], seg,
-                         p * plan.bits, bits, counts);
+                         shift, bits, counts);
       hipLaunchKernelGGL(k_seg_scan, dim3(seg.V << bits), dim3(256), 0, stream, seg, 1 << bits, counts, totals);
-      hipLaunchKernelGGL(k_seg_scatter, dim3(nb), dim3(GSR_SORT_THREADS), 0, stream, (const uint32_t*)keys[src],
-                         (const uint32_t*)((p == 0 && vals_identity) ? nullptr : vals[src]), keys[dst], vals[dst],
-                         seg, p * plan.bits, bits, (const uint32_t*)counts, (const uint32_t*)totals);
+      if (kv)
+        hipLaunchKernelGGL(k_seg_scatter<true>, dim3(nb), dim3(GSR_SORT_THREADS), 0, stream, (const uint32_t*)keys[src],
+                           (const uint32_t*)((p == 0 && vals_identity) ? nullptr : vals[src]), keys[dst], vals[dst],
+                           seg, shift, bits, (const uint32_t*)counts, (const uint32_t*)totals);
+      else
+        hipLaunchKernelGGL(k_seg_scatter<false>, dim3(nb), dim3(GSR_SORT_THREADS), 0, stream,
+                           (const uint32_t*)keys[src], (const uint32_t*)nullptr, keys[dst], (uint32_t*)nullptr, seg,
+                           shift, bits, (const uint32_t*)counts, (const uint32_t*)totals);
     }
     src = dst;
   }

@@ -78,6 +78,26 @@ __device__ __forceinline__ uint32_t block_exclusive_scan(uint32_t v, uint32_t* t
   return res;
 }
 
+// Exclusive max-scan of one value per thread over a workgroup of NT threads (identity 0).
+template <int NT>
+__device__ __forceinline__ uint32_t block_exclusive_max(uint32_t v, uint32_t* s_wave) {
+  const int t = threadIdx.x, w = t >> 6, lane = t & 63;
+  uint32_t inc = v;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint32_t y = (uint32_t)__shfl_up((int)inc, o, 64);
+    if (lane >= o) inc = max(inc, y);
+  }
+  uint32_t ex = (uint32_t)__shfl_up((int)inc, 1, 64);
+  if (lane == 0) ex = 0u;
+  if (lane == 63) s_wave[w] = inc;
+  __syncthreads();
+  uint32_t before = 0u;
+  for (int i = 0; i < w; ++i) before = max(before, s_wave[i]);
+  __syncthreads();
+  return max(before, ex);
+}
+
 template <int NT>
 __device__ __forceinline__ uint32_t block_sum_u32(uint32_t v, uint32_t* s_wave) {
   uint32_t tot;

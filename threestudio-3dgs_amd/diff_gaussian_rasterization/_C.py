@@ -51,7 +51,7 @@ SIGNATURES = {
     ),
     "gsr_mark_visible": (_i, [_i, _vp, _vp, _vp, _vp, _vp]),
     "gsr_set_geom_bytes": (_sz, [_i, _i]),
-    "gsr_set_binning_bytes": (_sz, [_i, ctypes.POINTER(_i), _i, _i]),
+    "gsr_set_binning_bytes": (_sz, [_i, _i, ctypes.POINTER(_i), _i, _i]),
     "gsr_set_image_bytes": (_sz, [_i, _i, _i]),
     "gsr_set_backward_bytes": (_sz, [_i, _i, ctypes.POINTER(_i)]),
     "gsr_set_preprocess": (

@@ -100,7 +100,7 @@ class _RasterizeViews(torch.autograd.Function):
             if len(_C.RECENT_FORWARDS) < 4096:
                 _C.RECENT_FORWARDS.extend((k, H, W) for k in vs.K)
             Karr = _arr(ctypes.c_int, vs.K)
-            vs.binning = torch.empty(int(lib.gsr_set_binning_bytes(vs.V, Karr, W, H)), dtype=torch.uint8, device=dev)
+            vs.binning = torch.empty(int(lib.gsr_set_binning_bytes(vs.V, P, Karr, W, H)), dtype=torch.uint8, device=dev)
             vs.image = torch.empty(int(lib.gsr_set_image_bytes(vs.V, W, H)), dtype=torch.uint8, device=dev)
             _C._check(lib.gsr_set_render(vs.V, P, Karr, W, H, _ptrs([c[3] for c in vs.cams]), p(vs.geom),
                                          p(vs.binning), p(vs.image), p(color[vs.lo:vs.hi]), p(depth[vs.lo:vs.hi]),
