@@ -64,20 +64,34 @@ __device__ __forceinline__ void tile_pixel(int t, int& lx, int& ly) {
   ly = ((w >> 1) << 3) | (l >> 3);
 }
 
-// Is some pixel centre of the 8x8 quadrant with origin (qx, qy) inside the padded alpha >= 1/255
-// ellipse of this Gaussian?  (single-quadrant form of quadrant_mask)
+// Can some pixel centre of the 8x8 quadrant with origin (qx, qy) reach alpha >= 1/255 for this
+// Gaussian?  alpha = o exp(-q/2), q = a dx^2 + 2 b dx dy + c dy^2 (dx = mean - pixel), so the pair
+// can blend only if q <= 2 ln(255 o).  The test takes the exact minimum of q over the continuous
+// rectangle spanned by the quadrant's pixel centres (<= the minimum over the pixels themselves) and
+// compares it with a padded threshold, so it never drops a pair the reference would blend; for
+// rotated, elongated footprints it is much tighter than the ellipse's bounding box.
+__device__ __forceinline__ float quad_form(float a, float b, float c, float u, float v) {
+  return fmaf(a * u, u, fmaf(2.0f * b * u, v, c * v * v));
+}
 __device__ __forceinline__ bool quadrant_hit(const float4 r0, const float4 r1, float qx, float qy) {
   const float o = r1.y;
   if (!(o >= GSR_ALPHA_MIN * 0.9999f)) return false;
   const float a = r0.z, b = r0.w, c = r1.x;
-  const float det = a * c - b * b;
-  if (!(det > 0.0f)) return true;
+  if (!(a > 0.0f && c > 0.0f && a * c - b * b > 0.0f)) return true;
   const float tau = fmaxf(0.0f, __logf(255.0f * o));
-  const float r2 = 2.0f * (tau * 1.001f + 1e-3f);
-  const float inv_det = 1.0f / det;
-  const float hx = sqrtf(r2 * c * inv_det) * 1.001f + 0.02f;
-  const float hy = sqrtf(r2 * a * inv_det) * 1.001f + 0.02f;
-  return (r0.x + hx >= qx) && (r0.x - hx <= qx + 7.0f) && (r0.y + hy >= qy) && (r0.y - hy <= qy + 7.0f);
+  const float thr = 2.0f * (tau * 1.002f + 2e-3f);
+  // dx ranges over [u0, u1], dy over [v0, v1]
+  const float u1 = r0.x - qx, u0 = u1 - 7.0f;
+  const float v1 = r0.y - qy, v0 = v1 - 7.0f;
+  if (u0 <= 0.0f && u1 >= 0.0f && v0 <= 0.0f && v1 >= 0.0f) return true;
+  const float ia = 1.0f / a, ic = 1.0f / c;
+  // edges u = u0, u1: best v = clamp(-b u / c); edges v = v0, v1: best u = clamp(-b v / a)
+  const float q0 = quad_form(a, b, c, u0, fminf(fmaxf(-b * u0 * ic, v0), v1));
+  const float q1 = quad_form(a, b, c, u1, fminf(fmaxf(-b * u1 * ic, v0), v1));
+  const float q2 = quad_form(a, b, c, fminf(fmaxf(-b * v0 * ia, u0), u1), v0);
+  const float q3 = quad_form(a, b, c, fminf(fmaxf(-b * v1 * ia, u0), u1), v1);
+  const float qmin = fminf(fminf(q0, q1), fminf(q2, q3));
+  return qmin * 0.998f <= thr;
 }
 
 // Forward: one wave (64 threads) per 8x8 quadrant of a 16x16 tile.  The wave streams the tile's
@@ -97,8 +111,8 @@ __global__ __launch_bounds__(64) void k_render_fwd(RenderSet rs,
                                                    float* __restrict__ final_T,
                                                    uint32_t* __restrict__ n_contrib,
                                                    uint32_t* __restrict__ quad_maxc) {
-  __shared__ float4 s0[64], s1[64], s2[64];
-  __shared__ uint32_t s_idx[64];
+  // 65 slots: the loop reads candidate k+1 while blending k (slot 64 is never used)
+  __shared__ float4 s0[65], s1[65], s2[65];
   const int U = unit_grid(rs.gx, rs.gy);
   const int v = blockIdx.x / U;
   int tile, q;
@@ -162,16 +176,14 @@ __global__ __launch_bounds__(64) void k_render_fwd(RenderSet rs,
     if (keep) {
       const uint32_t pos = mask_rank(bal);
       s0[pos] = r0;
-      s1[pos] = r1;
+      s1[pos] = make_float4(r1.x, r1.y, r1.z, __uint_as_float((uint32_t)(i + 1)));  // .w: 1 + list position
       s2[pos] = r2;
-      s_idx[pos] = (uint32_t)(i + 1);
     }
     __syncthreads();
+    float4 a = s0[0], b = s1[0], c = s2[0];
     for (int k = 0; k < cnt; ++k) {
       if ((k & 7) == 0 && __all(done)) break;
-      const float4 a = s0[k];
-      const float4 b = s1[k];
-      const float4 c = s2[k];
+      const float4 an = s0[k + 1], bn = s1[k + 1], cn = s2[k + 1];
       const float dx = a.x - pxf, dy = a.y - pyf;
       const float power = gauss_power(a.z, a.w, b.x, dx, dy);
       const float alpha = fminf(GSR_ALPHA_MAX, b.y * __expf(power));
@@ -184,8 +196,11 @@ __global__ __launch_bounds__(64) void k_render_fwd(RenderSet rs,
       Cb = blend ? Cb + c.z * alpha * T : Cb;
       D = blend ? D + b.z * alpha * T : D;
       T = blend ? test_T : T;
-      last_contributor = blend ? s_idx[k] : last_contributor;
+      last_contributor = blend ? __float_as_uint(b.w) : last_contributor;
       done = done || term;
+      a = an;
+      b = bn;
+      c = cn;
     }
     __syncthreads();
   }
@@ -262,12 +277,41 @@ void launch_render_forward(const RenderSet& rs, const GeomState& g, const uint32
 // colour/depth/alpha accumulators, background term.  Per pair the 10 gradient terms are
 //   0,1 dmean2D (x W/2, H/2)  2,3,4 dconic (a, b[half], c)  5 dopacity  6,7,8 dcolor  9 ddepth
 #define NGV 10
+#ifndef BWD_SUB
 #define BWD_SUB 32  // Gaussians per LDS partial flush
+#endif
 
-template <int SHIFT>
-__device__ __forceinline__ void row_reduce_step(float (&v)[NGV]) {
+#define GSR_SUM_STRIDE 12
+
+__device__ __forceinline__ float swap_add32(float& x, float& y) {
+  // v_permlane32_swap: lanes 32-63 of x <-> lanes 0-31 of y, then add:
+  // result = [x_lo + x_hi | y_lo + y_hi]
+  const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(y), false, false);
+  return __uint_as_float(r[0]) + __uint_as_float(r[1]);
+}
+__device__ __forceinline__ float swap_add16(float x, float y) {
+  // v_permlane16_swap: in each 32-lane half, lanes 16-31 of x <-> lanes 0-15 of y, then add:
+  // rows (16 lanes) of the result = [x_r0 + x_r1, y_r0 + y_r1, x_r2 + x_r3, y_r2 + y_r3]
+  const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(x), __float_as_uint(y), false, false);
+  return __uint_as_float(r[0]) + __uint_as_float(r[1]);
+}
+// Sum two candidates' 10 per-lane values over the 64 lanes.  Transposed reduction: the 32-lane and
+// 16-lane exchanges each halve the register count (one swap + one add per pair), after which register
+// j holds, per 16-lane row, (va[j], va[j+5], vb[j], vb[j+5]) summed over 4 lanes; a 4-step DPP row
+// reduction finishes.  Lane 15 ends with va[0..4], lane 31 va[5..9], lane 47 vb[0..4], lane 63 vb[5..9].
+__device__ __forceinline__ void pair_reduce(float (&va)[NGV], float (&vb)[NGV], float (&out)[5]) {
+  float y[NGV];
 #pragma unroll
-  for (int k = 0; k < NGV; ++k) v[k] += dpp_f32<0x110 | SHIFT>(v[k]);
+  for (int i = 0; i < NGV; ++i) y[i] = swap_add32(va[i], vb[i]);  // [va_i | vb_i], 2 lanes each
+#pragma unroll
+  for (int j = 0; j < 5; ++j) {
+    float z = swap_add16(y[j], y[j + 5]);  // rows: va_j, va_{j+5}, vb_j, vb_{j+5}
+    z += dpp_f32<0x111>(z);
+    z += dpp_f32<0x112>(z);
+    z += dpp_f32<0x114>(z);
+    z += dpp_f32<0x118>(z);
+    out[j] = z;
+  }
 }
 
 // One wave per 8x8 quadrant (as the forward).  The wave walks its tile's list back to front from
@@ -293,9 +337,11 @@ __global__ __launch_bounds__(64) void k_render_bwd(RenderSet rs,
                                                    const float* __restrict__ dL_ddepth,
                                                    const float* __restrict__ dL_dalpha,
                                                    float4* __restrict__ grow) {
-  __shared__ float4 s0[64], s1[64], s2[64];
-  __shared__ uint32_t s_dest[64], s_rel[64];
-  __shared__ float4 s_part[BWD_SUB][4][3];
+  __shared__ float4 s0[65], s1[65], s2[65];
+  __shared__ uint32_t s_dest[64];
+  // per Gaussian of a flush: its 10 summed moments at a 12-float (48 B) stride, at which the
+  // flush's per-lane 16-byte reads hit distinct banks
+  __shared__ __attribute__((aligned(16))) float s_sum[(BWD_SUB + 1) * GSR_SUM_STRIDE];
   const int U = unit_grid(rs.gx, rs.gy);
   const int v = blockIdx.x / U;
   int tile, q;
@@ -353,7 +399,6 @@ __global__ __launch_bounds__(64) void k_render_bwd(RenderSet rs,
   float acc_r = 0.f, acc_g = 0.f, acc_b = 0.f, acc_d = 0.f, acc_a = 0.f;
   float last_alpha = 0.f, last_r = 0.f, last_g = 0.f, last_b = 0.f, last_depth = 0.f;
   const float ddelx_dx = 0.5f * W, ddely_dy = 0.5f * H;
-  const int prow = lane >> 4;
   const float4 zero4 = make_float4(0.f, 0.f, 0.f, 0.f);
 
   // two-stage prefetch: sorted indices two batches ahead, 48-byte records (+ rect, goff) one batch
@@ -411,26 +456,24 @@ __global__ __launch_bounds__(64) void k_render_bwd(RenderSet rs,
     if (keep) {
       const uint32_t pos = mask_rank(bal);
       s0[pos] = r0;
-      s1[pos] = r1;
+      s1[pos] = make_float4(r1.x, r1.y, r1.z, __uint_as_float((uint32_t)rel_l));  // .w: list position
       s2[pos] = r2;
       s_dest[pos] = dest;
-      s_rel[pos] = (uint32_t)rel_l;
     }
     __syncthreads();
     for (int sub = 0; sub < cnt; sub += BWD_SUB) {
       const int scnt = min(BWD_SUB, cnt - sub);
-      for (int kk = 0; kk < scnt; ++kk) {
-        const int k = sub + kk;
-        const uint32_t rel = __builtin_amdgcn_readfirstlane(s_rel[k]);
-        // branch-free replay step (reference order of operations); non-contributing lanes keep
-        // their state and contribute zeros
-        const float4 a = s0[k];
-        const float4 b = s1[k];
-        const float4 c = s2[k];
-        const float dx = a.x - pxf, dy = a.y - pyf;
-        const float power = gauss_power(a.z, a.w, b.x, dx, dy);
+      float4 a = s0[sub], b = s1[sub], c = s2[sub];
+      // branch-free replay step (reference order of operations) for the staged candidate (a, b, c);
+      // non-contributing lanes keep their state and contribute zeros.  Per pair: moments of
+      // u = G dL/dalpha over the pixel offsets (mean2D / conic / opacity gradients are linear in
+      // them) and the colour / depth weights.
+      auto replay = [&](const float4& ga, const float4& gb, const float4& gc, float (&v)[NGV]) -> bool {
+        const uint32_t rel = __float_as_uint(gb.w);
+        const float dx = ga.x - pxf, dy = ga.y - pyf;
+        const float power = gauss_power(ga.z, ga.w, gb.x, dx, dy);
         const float G = __expf(power);
-        const float alpha = fminf(GSR_ALPHA_MAX, b.y * G);
+        const float alpha = fminf(GSR_ALPHA_MAX, gb.y * G);
         const bool hit = rel < last_contributor && power <= 0.0f && alpha >= GSR_ALPHA_MIN;
         const float inv_1ma = fast_rcp(1.f - alpha);
         T = hit ? T * inv_1ma : T;
@@ -441,10 +484,10 @@ __global__ __launch_bounds__(64) void k_render_bwd(RenderSet rs,
         const float nd = last_alpha * last_depth + oml * acc_d;
         const float na = last_alpha * 1.0f + oml * acc_a;
         float dL_dalpha = 0.0f;
-        dL_dalpha += (c.x - nr) * dpix[0];
-        dL_dalpha += (c.y - ng) * dpix[1];
-        dL_dalpha += (c.z - nb) * dpix[2];
-        dL_dalpha += (b.z - nd) * dpix_d;
+        dL_dalpha += (gc.x - nr) * dpix[0];
+        dL_dalpha += (gc.y - ng) * dpix[1];
+        dL_dalpha += (gc.z - nb) * dpix[2];
+        dL_dalpha += (gb.z - nd) * dpix_d;
         dL_dalpha += (1.f - na) * dpix_a;
         dL_dalpha *= T;
         dL_dalpha += (-T_final * inv_1ma) * bg_dot;
@@ -455,52 +498,76 @@ __global__ __launch_bounds__(64) void k_render_bwd(RenderSet rs,
         acc_b = hit ? nb : acc_b;
         acc_d = hit ? nd : acc_d;
         acc_a = hit ? na : acc_a;
-        last_r = hit ? c.x : last_r;
-        last_g = hit ? c.y : last_g;
-        last_b = hit ? c.z : last_b;
-        last_depth = hit ? b.z : last_depth;
+        last_r = hit ? gc.x : last_r;
+        last_g = hit ? gc.y : last_g;
+        last_b = hit ? gc.z : last_b;
+        last_depth = hit ? gb.z : last_depth;
         last_alpha = hit ? alpha : last_alpha;
-        // per pair: moments of u over the pixel offsets (mean2D / conic / opacity gradients are
-        // linear in them) and the colour / depth weights
         const float udx = u * dx, udy = u * dy;
-        float v[NGV] = {u, udx, udy, udx * dx, udx * dy, udy * dy,
-                        w * dpix[0], w * dpix[1], w * dpix[2], w * dpix_d};
-        float4* part = s_part[kk][prow];
+        v[0] = u;
+        v[1] = udx;
+        v[2] = udy;
+        v[3] = udx * dx;
+        v[4] = udx * dy;
+        v[5] = udy * dy;
+        v[6] = w * dpix[0];
+        v[7] = w * dpix[1];
+        v[8] = w * dpix[2];
+        v[9] = w * dpix_d;
+        return hit;
+      };
+      // candidates in pairs: the 2 x 10 per-lane values are summed over the 64 lanes by a
+      // transposed reduction (pair_reduce), ~3x fewer VALU than ten 4-step DPP row reductions
+      // per candidate (DPP row-shift adds issue at ~3x the cost of plain adds on gfx950)
+      for (int kk = 0; kk < scnt; kk += 2) {
+        float va[NGV], vb[NGV];
+        float4 an = s0[sub + kk + 1], bn = s1[sub + kk + 1], cn = s2[sub + kk + 1];
+        bool hit = replay(a, b, c, va);
+        a = an;
+        b = bn;
+        c = cn;
+        if (kk + 1 < scnt) {
+          an = s0[sub + kk + 2];
+          bn = s1[sub + kk + 2];
+          cn = s2[sub + kk + 2];
+          hit = replay(a, b, c, vb) || hit;
+          a = an;
+          b = bn;
+          c = cn;
+        } else {
+#pragma unroll
+          for (int i = 0; i < NGV; ++i) vb[i] = 0.f;
+        }
+        float* sa = s_sum + kk * GSR_SUM_STRIDE;
         if (__any(hit)) {
-          row_reduce_step<1>(v);
-          row_reduce_step<2>(v);
-          row_reduce_step<4>(v);
-          row_reduce_step<8>(v);
+          float r[5];
+          pair_reduce(va, vb, r);
+          // lane 15: candidate kk values 0-4, lane 31: kk values 5-9, lanes 47 / 63: candidate kk+1
           if ((lane & 15) == 15) {
-            part[0] = make_float4(v[0], v[1], v[2], v[3]);
-            part[1] = make_float4(v[4], v[5], v[6], v[7]);
-            part[2] = make_float4(v[8], v[9], 0.f, 0.f);
+            float* dst = sa + (lane >> 5) * GSR_SUM_STRIDE + ((lane >> 4) & 1) * 5;
+#pragma unroll
+            for (int i = 0; i < 5; ++i) dst[i] = r[i];
           }
         } else if ((lane & 15) == 15) {
-          part[0] = zero4;
-          part[1] = zero4;
-          part[2] = zero4;
+          float* dst = sa + (lane >> 5) * GSR_SUM_STRIDE + ((lane >> 4) & 1) * 5;
+#pragma unroll
+          for (int i = 0; i < 5; ++i) dst[i] = 0.f;
         }
       }
       __syncthreads();
       if (lane < scnt) {
-        // one lane per Gaussian: sum the 4 row partials, turn moments into the reference's terms
+        // one lane per Gaussian: turn the summed moments into the reference's terms
         //   dmean2D = -o (W/2, H/2) (a m1 + b m2, c m2 + b m1), dconic = -o/2 (m3, m4, m5), dopacity = m0
-        const int kk = lane;
-        float4 p0 = s_part[kk][0][0], p1 = s_part[kk][0][1], p2 = s_part[kk][0][2];
-#pragma unroll
-        for (int r = 1; r < 4; ++r) {
-          const float4 x0 = s_part[kk][r][0], x1 = s_part[kk][r][1], x2 = s_part[kk][r][2];
-          p0.x += x0.x; p0.y += x0.y; p0.z += x0.z; p0.w += x0.w;
-          p1.x += x1.x; p1.y += x1.y; p1.z += x1.z; p1.w += x1.w;
-          p2.x += x2.x; p2.y += x2.y;
-        }
-        const float4 a = s0[sub + kk];
-        const float4 b = s1[sub + kk];
-        const float o = b.y;
-        const float dmx = -o * ddelx_dx * (a.z * p0.y + a.w * p0.z);
-        const float dmy = -o * ddely_dy * (b.x * p0.z + a.w * p0.y);
-        const size_t d = 3 * (size_t)s_dest[sub + kk];
+        const float* m = s_sum + lane * GSR_SUM_STRIDE;
+        const float4 p0 = *reinterpret_cast<const float4*>(m);
+        const float4 p1 = *reinterpret_cast<const float4*>(m + 4);
+        const float2 p2 = *reinterpret_cast<const float2*>(m + 8);
+        const float4 ga = s0[sub + lane];
+        const float4 gb = s1[sub + lane];
+        const float o = gb.y;
+        const float dmx = -o * ddelx_dx * (ga.z * p0.y + ga.w * p0.z);
+        const float dmy = -o * ddely_dy * (gb.x * p0.z + ga.w * p0.y);
+        const size_t d = 3 * (size_t)s_dest[sub + lane];
         grow[d] = make_float4(dmx, dmy, -0.5f * o * p0.w, -0.5f * o * p1.x);
         grow[d + 1] = make_float4(-0.5f * o * p1.y, p0.x, p1.z, p1.w);
         grow[d + 2] = make_float4(p2.x, p2.y, 0.f, 0.f);
