@@ -53,7 +53,7 @@ def test_host_only_queries():
     assert lib.gsr_set_geom_bytes(4, 1000) >= 4 * lib.gsr_geom_bytes(1000) - 4 * 4096
     assert lib.gsr_binning_bytes(5000, 64, 64) >= 5000 * 16
     assert lib.gsr_image_bytes(64, 48) >= 64 * 48 * 8
-    assert lib.gsr_backward_bytes(10, 100) >= 100 * 4 * 48
+    assert lib.gsr_backward_bytes(10, 100) >= 100 * 48 + 10 * 13 * 4  # one row per instance + per-Gaussian records
     assert lib.gsr_geom_bytes(0) > 0  # sizes stay valid for P = 0
 
 

@@ -24,27 +24,49 @@ struct RowSums {
   float dmx, dmy, dca, dcb, dcc, dop, dcr, dcg, dcbl, ddep;
 };
 
-// Sum the 4 quadrant rows of each of the Gaussian's instances that its tile's blend reached:
-// (depth key, index) < the tile's first unblended instance (cut = (key, index) per tile).
+// Sum the rows of the Gaussian's instances that its tile's blend reached: (depth key, index) < the
+// tile's first unblended instance (cut = (key, index) per tile).  The rect is walked 4 tiles at a
+// time: the 4 cut tests first, then the valid rows' loads together, so a thread has up to 12 loads
+// in flight instead of waiting on each row in turn.
 __device__ __forceinline__ RowSums gather_rows(uint32_t idx, uint32_t dkey, uint32_t i0, uint2 rc, int grid_x,
                                                const uint2* cut, const float4* grow) {
   RowSums r = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
   const int xmin = rc.x & 0xffff, ymin = rc.x >> 16, xmax = rc.y & 0xffff, ymax = rc.y >> 16;
-  size_t i = i0;
-  for (int ty = ymin; ty < ymax; ++ty)
-    for (int tx = xmin; tx < xmax; ++tx, ++i) {
-      const uint2 c = cut[ty * grid_x + tx];
-      const bool valid = dkey < c.x || (dkey == c.x && idx < c.y);
-      if (!valid) continue;
-      const float4* row = grow + 12 * i;
+  const int w = xmax - xmin, n = w * (ymax - ymin);
+  int tx = xmin, ty = ymin;
+  const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
+  for (int l = 0; l < n; l += 4) {
+    bool val[4];
+    int sl[4];
 #pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const float4 r0 = row[3 * q], r1 = row[3 * q + 1], r2 = row[3 * q + 2];
-        r.dmx += r0.x; r.dmy += r0.y; r.dca += r0.z; r.dcb += r0.w;
-        r.dcc += r1.x; r.dop += r1.y; r.dcr += r1.z; r.dcg += r1.w;
-        r.dcbl += r2.x; r.ddep += r2.y;
+    for (int k = 0; k < 4; ++k) {
+      val[k] = false;
+      sl[k] = 0;
+      if (l + k < n) {
+        const uint2 c = cut[ty * grid_x + tx];
+        val[k] = dkey < c.x || (dkey == c.x && idx < c.y);
+        sl[k] = l + k;
+        if (++tx == xmax) {
+          tx = xmin;
+          ++ty;
+        }
       }
     }
+    float4 a[4][3];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const float4* row = grow + 3 * ((size_t)i0 + sl[k]);
+      a[k][0] = val[k] ? row[0] : z4;
+      a[k][1] = val[k] ? row[1] : z4;
+      a[k][2] = val[k] ? row[2] : z4;
+    }
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      r.dmx += a[k][0].x; r.dmy += a[k][0].y; r.dca += a[k][0].z; r.dcb += a[k][0].w;
+      r.dcc += a[k][1].x; r.dop += a[k][1].y; r.dcr += a[k][1].z; r.dcg += a[k][1].w;
+      r.dcbl += a[k][2].x; r.ddep += a[k][2].y;
+    }
+  }
   return r;
 }
 
@@ -254,7 +276,7 @@ __global__ __launch_bounds__(256) void k_view_grad(GaussBackwardArgs a, ViewGrad
     __syncthreads();
   }
   const ViewCam& cam = va.cam[vl];
-  const float4* grow = va.grow + (size_t)12 * va.row_start[vl];
+  const float4* grow = va.grow + (size_t)3 * va.row_start[vl];
   float* recv = va.vrec + (size_t)vl * GSR_GRAD_FIELDS * a.P;
 #pragma unroll 1
   for (int it = 0; it < GSR_VG_ITEMS; ++it) {
@@ -271,8 +293,16 @@ __global__ __launch_bounds__(256) void k_view_grad(GaussBackwardArgs a, ViewGrad
       for (int f = 0; f < GSR_GRAD_FIELDS; ++f) rec[(size_t)f * a.P] = 0.f;
       continue;
     }
+#ifdef GSR_VG_NOGATHER  // timing experiment only (results wrong)
+    const RowSums r = RowSums{0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+#else
     const RowSums r = gather_rows((uint32_t)idx, __float_as_uint(va.g.rec1[o].z), va.g.goff[o], va.g.rect[o], va.gx,
                                   cut, grow);
+#endif
+#ifdef GSR_VG_ONLYGATHER  // timing experiment only (results wrong)
+    m2[0] = r.dmx + r.dmy + r.dca + r.dcb + r.dcc + r.dop + r.dcr + r.dcg + r.dcbl + r.ddep;
+    continue;
+#endif
     m2[0] = r.dmx;
     m2[1] = r.dmy;
     m2[2] = 0.f;

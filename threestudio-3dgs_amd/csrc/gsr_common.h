@@ -224,8 +224,8 @@ struct ImageState {
   }
 };
 
-// Backward scratch for a group of views: one 48-byte gradient row per (instance, 8x8 quadrant),
-// stored at 4 * slot + quadrant, slot = (view's first instance within the group) + goff[g] +
+// Backward scratch for a group of views: one 48-byte gradient row per instance (summed over the
+// tile's 4 quadrants), stored at slot = (view's first instance within the group) + goff[g] +
 // (row-major index of the tile inside the Gaussian's tile rect), so each Gaussian's rows are
 // contiguous for the per-Gaussian gather-sum:
 //   g0 = (dmean2D.x, dmean2D.y, dconic.a, dconic.b)   [pixel units; b in the reference's half convention]
@@ -234,9 +234,9 @@ struct ImageState {
 // After the rows: the per-(view, Gaussian) records of gsr_backward.hip's first kernel,
 // [views of the group][13][P] floats.
 struct BackwardState {
-  float4* grow;  // [12 * instances of the group]
+  float4* grow;  // [3 * instances of the group]
   float* vrec;   // [views][13][P]
-  static size_t rows_bytes(long long K) { return align_up(sizeof(float4) * 12 * (size_t)(K > 0 ? K : 1), 256); }
+  static size_t rows_bytes(long long K) { return align_up(sizeof(float4) * 3 * (size_t)(K > 0 ? K : 1), 256); }
   static size_t bytes_for(long long K, int views, int P) {
     return rows_bytes(K) + align_up(sizeof(float) * 13 * (size_t)views * (size_t)(P > 0 ? P : 1), 256);
   }

@@ -277,11 +277,6 @@ void launch_render_forward(const RenderSet& rs, const GeomState& g, const uint32
 // colour/depth/alpha accumulators, background term.  Per pair the 10 gradient terms are
 //   0,1 dmean2D (x W/2, H/2)  2,3,4 dconic (a, b[half], c)  5 dopacity  6,7,8 dcolor  9 ddepth
 #define NGV 10
-#ifndef BWD_SUB
-#define BWD_SUB 32  // Gaussians per LDS partial flush
-#endif
-
-#define GSR_SUM_STRIDE 12
 
 __device__ __forceinline__ float swap_add32(float& x, float& y) {
   // v_permlane32_swap: lanes 32-63 of x <-> lanes 0-31 of y, then add:
@@ -322,30 +317,58 @@ __device__ __forceinline__ void pair_reduce(float (&va)[NGV], float (&vb)[NGV], 
 // row per (instance, quadrant) at 4 * slot + quadrant, where slot is the instance's place in its
 // Gaussian's contiguous row range.  Instances the quadrant skips get zero rows, so every instance
 // above the tile cutoff has all 4 rows written.
-__global__ __launch_bounds__(64) void k_render_bwd(RenderSet rs,
-                                                   const uint2* __restrict__ ranges,
-                                                   const uint32_t* __restrict__ quad_maxc,
-                                                   const uint32_t* __restrict__ sorted_gauss,
-                                                   const float4* __restrict__ rec0,
-                                                   const float4* __restrict__ rec1,
-                                                   const float4* __restrict__ rec2,
-                                                   const uint2* __restrict__ rect,
-                                                   const uint32_t* __restrict__ goff,
-                                                   const float* __restrict__ final_Ts,
-                                                   const uint32_t* __restrict__ n_contrib,
-                                                   const float* __restrict__ dL_dcolor,
-                                                   const float* __restrict__ dL_ddepth,
-                                                   const float* __restrict__ dL_dalpha,
-                                                   float4* __restrict__ grow) {
-  __shared__ float4 s0[65], s1[65], s2[65];
-  __shared__ uint32_t s_dest[64];
-  // per Gaussian of a flush: its 10 summed moments at a 12-float (48 B) stride, at which the
-  // flush's per-lane 16-byte reads hit distinct banks
-  __shared__ __attribute__((aligned(16))) float s_sum[(BWD_SUB + 1) * GSR_SUM_STRIDE];
-  const int U = unit_grid(rs.gx, rs.gy);
-  const int v = blockIdx.x / U;
-  int tile, q;
-  if (!unit_of_block(blockIdx.x - v * U, rs.gx, rs.gy, tile, q)) return;
+// Backward: one 256-thread workgroup per (view, tile); wave q owns quadrant q.  The four waves walk
+// the tile's list back to front in lockstep batches of 64 candidates: the batch's records are
+// staged in LDS once for all four (one global gather per candidate instead of four), each wave culls
+// the batch for its quadrant and reduces its kept candidates in pairs (pair_reduce) into per-
+// (candidate, quadrant) moment sums in LDS, and one thread per candidate adds the four quadrants
+// and writes ONE 48-byte gradient row per instance (4x fewer row bytes than a row per quadrant,
+// for this kernel's writes and the per-Gaussian gather's reads).
+#define GSR_QSUM_STRIDE 52  // floats per candidate: 4 quadrants x 13 (10 used); 208 B, conflict-free
+struct BwdLDS {
+  float4 s0[65], s1[65], s2[65];
+  uint32_t slot[64];
+  uint32_t list[4][64];
+  float qsum[64 * GSR_QSUM_STRIDE];
+};
+
+__host__ __device__ __forceinline__ int tile_grid(int gx, int gy) {
+  const int S = ((gx + 1) >> 1) * ((gy + 1) >> 1);
+  return 32 * ((S + 7) >> 3);
+}
+// blockIdx -> tile: 2x2-tile super-tiles dealt round-robin over the 8 XCD groups (as unit_of_block)
+__device__ __forceinline__ bool tile_of_block(int b, int gx, int gy, int& tile) {
+  const int sgx = (gx + 1) >> 1, sgy = (gy + 1) >> 1;
+  const int x = b & 7, k = b >> 3;
+  const int s = ((k >> 2) << 3) + x;
+  const int w = k & 3;
+  if (s >= sgx * sgy) return false;
+  const int tx = (s % sgx) * 2 + (w & 1), ty = (s / sgx) * 2 + (w >> 1);
+  if (tx >= gx || ty >= gy) return false;
+  tile = ty * gx + tx;
+  return true;
+}
+
+__global__ __launch_bounds__(256) void k_render_bwd(RenderSet rs,
+                                                    const uint2* __restrict__ ranges,
+                                                    const uint32_t* __restrict__ quad_maxc,
+                                                    const uint32_t* __restrict__ sorted_gauss,
+                                                    const float4* __restrict__ rec0,
+                                                    const float4* __restrict__ rec1,
+                                                    const float4* __restrict__ rec2,
+                                                    const uint2* __restrict__ rect,
+                                                    const uint32_t* __restrict__ goff,
+                                                    const float* __restrict__ final_Ts,
+                                                    const uint32_t* __restrict__ n_contrib,
+                                                    const float* __restrict__ dL_dcolor,
+                                                    const float* __restrict__ dL_ddepth,
+                                                    const float* __restrict__ dL_dalpha,
+                                                    float4* __restrict__ grow) {
+  __shared__ BwdLDS s;
+  const int TG = tile_grid(rs.gx, rs.gy);
+  const int v = blockIdx.x / TG;
+  int tile;
+  if (!tile_of_block(blockIdx.x - v * TG, rs.gx, rs.gy, tile)) return;
   GSR_TL_BEGIN
   const int W = rs.W, H = rs.H, grid_x = rs.gx;
   {
@@ -363,12 +386,11 @@ __global__ __launch_bounds__(64) void k_render_bwd(RenderSet rs,
     dL_dcolor += (size_t)v * 3 * HWs;
     if (dL_ddepth) dL_ddepth += (size_t)v * HWs;
     if (dL_dalpha) dL_dalpha += (size_t)v * HWs;
-    grow += (size_t)12 * rs.row_start[v];
+    grow += (size_t)3 * rs.row_start[v];
   }
   const float* bg = rs.bg[v];
   int tl_work = 0;
-  const int unit = 4 * tile + q;
-  const int lane = threadIdx.x;
+  const int t = threadIdx.x, q = t >> 6, lane = t & 63;
   const int txi = tile % grid_x, tyi = tile / grid_x;
   const int qx0 = txi * GSR_TILE_X + (q & 1) * 8;
   const int qy0 = tyi * GSR_TILE_Y + (q >> 1) * 8;
@@ -376,8 +398,8 @@ __global__ __launch_bounds__(64) void k_render_bwd(RenderSet rs,
   const bool inside = px < W && py < H;
   const float pxf = (float)px, pyf = (float)py;
   const uint2 range = ranges[tile];
-  const int qmaxc = (int)quad_maxc[unit];
   const uint4 qm = reinterpret_cast<const uint4*>(quad_maxc)[tile];
+  const int qmaxc = (int)(q == 0 ? qm.x : q == 1 ? qm.y : q == 2 ? qm.z : qm.w);
   const int maxc = (int)max(max(qm.x, qm.y), max(qm.z, qm.w));
   const size_t pid = (size_t)py * W + px;
   const size_t HW = (size_t)H * W;
@@ -401,8 +423,7 @@ __global__ __launch_bounds__(64) void k_render_bwd(RenderSet rs,
   const float ddelx_dx = 0.5f * W, ddely_dy = 0.5f * H;
   const float4 zero4 = make_float4(0.f, 0.f, 0.f, 0.f);
 
-  // two-stage prefetch: sorted indices two batches ahead, 48-byte records (+ rect, goff) one batch
-  // ahead, so the dependent gather chain of the next batch overlaps this batch's replay
+  // wave 0 stages the batches; two-stage prefetch (indices two batches ahead, records one ahead)
   const uint32_t gmask = rs.gmask;
   auto fetch_index = [&](int h) -> uint32_t {
     const int r = h - 1 - lane;
@@ -410,9 +431,8 @@ __global__ __launch_bounds__(64) void k_render_bwd(RenderSet rs,
   };
   float4 n0 = zero4, n1 = zero4, n2 = zero4;
   uint2 nrc = make_uint2(0u, 0u);
-  uint32_t ngo = 0u;
-  uint32_t gi_next = 0u;
-  if (maxc > 0) {
+  uint32_t ngo = 0u, gi_next = 0u;
+  if (q == 0 && maxc > 0) {
     const uint32_t g0 = fetch_index(maxc);
     if (maxc - 1 - lane >= 0) {
       n0 = rec0[g0];
@@ -423,157 +443,143 @@ __global__ __launch_bounds__(64) void k_render_bwd(RenderSet rs,
     }
     if (maxc > 64) gi_next = fetch_index(maxc - 64);
   }
+
+  // branch-free replay step (reference order of operations); non-contributing lanes keep their
+  // state and contribute zeros.  Per pair: moments of u = G dL/dalpha over the pixel offsets
+  // (mean2D / conic / opacity gradients are linear in them) and the colour / depth weights.
+  auto replay = [&](const float4& ga, const float4& gb, const float4& gc, float (&vv)[NGV]) -> bool {
+    const uint32_t rel = __float_as_uint(gb.w);
+    const float dx = ga.x - pxf, dy = ga.y - pyf;
+    const float power = gauss_power(ga.z, ga.w, gb.x, dx, dy);
+    const float G = __expf(power);
+    const float alpha = fminf(GSR_ALPHA_MAX, gb.y * G);
+    const bool hit = rel < last_contributor && power <= 0.0f && alpha >= GSR_ALPHA_MIN;
+    const float inv_1ma = fast_rcp(1.f - alpha);
+    T = hit ? T * inv_1ma : T;
+    const float oml = 1.f - last_alpha;
+    const float nr = last_alpha * last_r + oml * acc_r;
+    const float ng = last_alpha * last_g + oml * acc_g;
+    const float nb = last_alpha * last_b + oml * acc_b;
+    const float nd = last_alpha * last_depth + oml * acc_d;
+    const float na = last_alpha * 1.0f + oml * acc_a;
+    float dL_dalpha = 0.0f;
+    dL_dalpha += (gc.x - nr) * dpix[0];
+    dL_dalpha += (gc.y - ng) * dpix[1];
+    dL_dalpha += (gc.z - nb) * dpix[2];
+    dL_dalpha += (gb.z - nd) * dpix_d;
+    dL_dalpha += (1.f - na) * dpix_a;
+    dL_dalpha *= T;
+    dL_dalpha += (-T_final * inv_1ma) * bg_dot;
+    const float u = hit ? G * dL_dalpha : 0.0f;  // dL/dG / opacity
+    const float w = hit ? alpha * T : 0.0f;      // dL/dcolor per unit dL/dpixel
+    acc_r = hit ? nr : acc_r;
+    acc_g = hit ? ng : acc_g;
+    acc_b = hit ? nb : acc_b;
+    acc_d = hit ? nd : acc_d;
+    acc_a = hit ? na : acc_a;
+    last_r = hit ? gc.x : last_r;
+    last_g = hit ? gc.y : last_g;
+    last_b = hit ? gc.z : last_b;
+    last_depth = hit ? gb.z : last_depth;
+    last_alpha = hit ? alpha : last_alpha;
+    const float udx = u * dx, udy = u * dy;
+    vv[0] = u;
+    vv[1] = udx;
+    vv[2] = udy;
+    vv[3] = udx * dx;
+    vv[4] = udx * dy;
+    vv[5] = udy * dy;
+    vv[6] = w * dpix[0];
+    vv[7] = w * dpix[1];
+    vv[8] = w * dpix[2];
+    vv[9] = w * dpix_d;
+    return hit;
+  };
+
+  uint32_t* mylist = s.list[q];
+  float* myq = s.qsum + q * 13;
   for (int hi = maxc; hi > 0; hi -= 64) {
+    if (q == 0) {
+      const int rel_l = hi - 1 - lane;
+      if (rel_l >= 0) {
+        const int xmin = nrc.x & 0xffff, ymin = nrc.x >> 16, xmax = nrc.y & 0xffff;
+        s.s0[lane] = n0;
+        s.s1[lane] = make_float4(n1.x, n1.y, n1.z, __uint_as_float((uint32_t)rel_l));  // .w: list position
+        s.s2[lane] = n2;
+        s.slot[lane] = ngo + (uint32_t)((tyi - ymin) * (xmax - xmin) + (txi - xmin));
+      }
+      if (hi > 64) {
+        if (hi - 65 - lane >= 0) {
+          n0 = rec0[gi_next];
+          n1 = rec1[gi_next];
+          n2 = rec2[gi_next];
+          nrc = rect[gi_next];
+          ngo = goff[gi_next];
+        }
+        if (hi > 128) gi_next = fetch_index(hi - 128);
+      }
+    }
+    __syncthreads();
+    // this wave's quadrant: cull the staged batch, list the kept candidates, zero the others' sums
     const int rel_l = hi - 1 - lane;
     bool keep = false;
-    const float4 r0 = n0, r1 = n1, r2 = n2;
-    const uint2 rc = nrc;
-    const uint32_t go = ngo;
-    if (hi > 64) {
-      if (hi - 65 - lane >= 0) {
-        n0 = rec0[gi_next];
-        n1 = rec1[gi_next];
-        n2 = rec2[gi_next];
-        nrc = rect[gi_next];
-        ngo = goff[gi_next];
-      }
-      if (hi > 128) gi_next = fetch_index(hi - 128);
-    }
-    uint32_t dest = 0;
-    if (rel_l >= 0) {
-      const int xmin = rc.x & 0xffff, ymin = rc.x >> 16, xmax = rc.y & 0xffff;
-      dest = 4u * (go + (uint32_t)((tyi - ymin) * (xmax - xmin) + (txi - xmin))) + (uint32_t)q;
-      keep = rel_l < qmaxc && quadrant_hit(r0, r1, (float)qx0, (float)qy0);
-      if (!keep) {
-        grow[3 * (size_t)dest] = zero4;
-        grow[3 * (size_t)dest + 1] = zero4;
-        grow[3 * (size_t)dest + 2] = zero4;
-      }
+    if (rel_l >= 0 && rel_l < qmaxc) keep = quadrant_hit(s.s0[lane], s.s1[lane], (float)qx0, (float)qy0);
+    if (rel_l >= 0 && !keep) {
+      float* z = myq + lane * GSR_QSUM_STRIDE;
+#pragma unroll
+      for (int i = 0; i < NGV; ++i) z[i] = 0.f;
     }
     const unsigned long long bal = __ballot(keep);
     const int cnt = __popcll(bal);
     tl_work += cnt;
-    if (keep) {
-      const uint32_t pos = mask_rank(bal);
-      s0[pos] = r0;
-      s1[pos] = make_float4(r1.x, r1.y, r1.z, __uint_as_float((uint32_t)rel_l));  // .w: list position
-      s2[pos] = r2;
-      s_dest[pos] = dest;
+    if (keep) mylist[mask_rank(bal)] = (uint32_t)lane;
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // this wave's list is read back by its own lanes
+    // kept candidates in pairs: transposed reduction of the 2 x 10 per-lane values (pair_reduce)
+    for (int k = 0; k < cnt; k += 2) {
+      const int j0 = __builtin_amdgcn_readfirstlane(mylist[k]);
+      const int j1 = k + 1 < cnt ? __builtin_amdgcn_readfirstlane(mylist[k + 1]) : -1;
+      float va[NGV], vb[NGV];
+      bool hit = replay(s.s0[j0], s.s1[j0], s.s2[j0], va);
+      if (j1 >= 0) {
+        hit = replay(s.s0[j1], s.s1[j1], s.s2[j1], vb) || hit;
+      } else {
+#pragma unroll
+        for (int i = 0; i < NGV; ++i) vb[i] = 0.f;
+      }
+      // lane 15: candidate j0 values 0-4, lane 31: j0 values 5-9, lanes 47 / 63: candidate j1
+      const int jj = (lane >> 5) ? j1 : j0;
+      float r[5];
+      if (__any(hit)) {
+        pair_reduce(va, vb, r);
+      } else {
+#pragma unroll
+        for (int i = 0; i < 5; ++i) r[i] = 0.f;
+      }
+      if ((lane & 15) == 15 && jj >= 0) {
+        float* dst = myq + jj * GSR_QSUM_STRIDE + ((lane >> 4) & 1) * 5;
+#pragma unroll
+        for (int i = 0; i < 5; ++i) dst[i] = r[i];
+      }
     }
     __syncthreads();
-    for (int sub = 0; sub < cnt; sub += BWD_SUB) {
-      const int scnt = min(BWD_SUB, cnt - sub);
-      float4 a = s0[sub], b = s1[sub], c = s2[sub];
-      // branch-free replay step (reference order of operations) for the staged candidate (a, b, c);
-      // non-contributing lanes keep their state and contribute zeros.  Per pair: moments of
-      // u = G dL/dalpha over the pixel offsets (mean2D / conic / opacity gradients are linear in
-      // them) and the colour / depth weights.
-      auto replay = [&](const float4& ga, const float4& gb, const float4& gc, float (&v)[NGV]) -> bool {
-        const uint32_t rel = __float_as_uint(gb.w);
-        const float dx = ga.x - pxf, dy = ga.y - pyf;
-        const float power = gauss_power(ga.z, ga.w, gb.x, dx, dy);
-        const float G = __expf(power);
-        const float alpha = fminf(GSR_ALPHA_MAX, gb.y * G);
-        const bool hit = rel < last_contributor && power <= 0.0f && alpha >= GSR_ALPHA_MIN;
-        const float inv_1ma = fast_rcp(1.f - alpha);
-        T = hit ? T * inv_1ma : T;
-        const float oml = 1.f - last_alpha;
-        const float nr = last_alpha * last_r + oml * acc_r;
-        const float ng = last_alpha * last_g + oml * acc_g;
-        const float nb = last_alpha * last_b + oml * acc_b;
-        const float nd = last_alpha * last_depth + oml * acc_d;
-        const float na = last_alpha * 1.0f + oml * acc_a;
-        float dL_dalpha = 0.0f;
-        dL_dalpha += (gc.x - nr) * dpix[0];
-        dL_dalpha += (gc.y - ng) * dpix[1];
-        dL_dalpha += (gc.z - nb) * dpix[2];
-        dL_dalpha += (gb.z - nd) * dpix_d;
-        dL_dalpha += (1.f - na) * dpix_a;
-        dL_dalpha *= T;
-        dL_dalpha += (-T_final * inv_1ma) * bg_dot;
-        const float u = hit ? G * dL_dalpha : 0.0f;  // dL/dG / opacity
-        const float w = hit ? alpha * T : 0.0f;      // dL/dcolor per unit dL/dpixel
-        acc_r = hit ? nr : acc_r;
-        acc_g = hit ? ng : acc_g;
-        acc_b = hit ? nb : acc_b;
-        acc_d = hit ? nd : acc_d;
-        acc_a = hit ? na : acc_a;
-        last_r = hit ? gc.x : last_r;
-        last_g = hit ? gc.y : last_g;
-        last_b = hit ? gc.z : last_b;
-        last_depth = hit ? gb.z : last_depth;
-        last_alpha = hit ? alpha : last_alpha;
-        const float udx = u * dx, udy = u * dy;
-        v[0] = u;
-        v[1] = udx;
-        v[2] = udy;
-        v[3] = udx * dx;
-        v[4] = udx * dy;
-        v[5] = udy * dy;
-        v[6] = w * dpix[0];
-        v[7] = w * dpix[1];
-        v[8] = w * dpix[2];
-        v[9] = w * dpix_d;
-        return hit;
-      };
-      // candidates in pairs: the 2 x 10 per-lane values are summed over the 64 lanes by a
-      // transposed reduction (pair_reduce), ~3x fewer VALU than ten 4-step DPP row reductions
-      // per candidate (DPP row-shift adds issue at ~3x the cost of plain adds on gfx950)
-      for (int kk = 0; kk < scnt; kk += 2) {
-        float va[NGV], vb[NGV];
-        float4 an = s0[sub + kk + 1], bn = s1[sub + kk + 1], cn = s2[sub + kk + 1];
-        bool hit = replay(a, b, c, va);
-        a = an;
-        b = bn;
-        c = cn;
-        if (kk + 1 < scnt) {
-          an = s0[sub + kk + 2];
-          bn = s1[sub + kk + 2];
-          cn = s2[sub + kk + 2];
-          hit = replay(a, b, c, vb) || hit;
-          a = an;
-          b = bn;
-          c = cn;
-        } else {
+    if (t < 64 && hi - 1 - t >= 0) {
+      // one thread per candidate: add the 4 quadrants' moments, turn them into the reference's terms
+      //   dmean2D = -o (W/2, H/2) (a m1 + b m2, c m2 + b m1), dconic = -o/2 (m3, m4, m5), dopacity = m0
+      const float* qs = s.qsum + t * GSR_QSUM_STRIDE;
+      float m[NGV];
 #pragma unroll
-          for (int i = 0; i < NGV; ++i) vb[i] = 0.f;
-        }
-        float* sa = s_sum + kk * GSR_SUM_STRIDE;
-        if (__any(hit)) {
-          float r[5];
-          pair_reduce(va, vb, r);
-          // lane 15: candidate kk values 0-4, lane 31: kk values 5-9, lanes 47 / 63: candidate kk+1
-          if ((lane & 15) == 15) {
-            float* dst = sa + (lane >> 5) * GSR_SUM_STRIDE + ((lane >> 4) & 1) * 5;
-#pragma unroll
-            for (int i = 0; i < 5; ++i) dst[i] = r[i];
-          }
-        } else if ((lane & 15) == 15) {
-          float* dst = sa + (lane >> 5) * GSR_SUM_STRIDE + ((lane >> 4) & 1) * 5;
-#pragma unroll
-          for (int i = 0; i < 5; ++i) dst[i] = 0.f;
-        }
-      }
-      __syncthreads();
-      if (lane < scnt) {
-        // one lane per Gaussian: turn the summed moments into the reference's terms
-        //   dmean2D = -o (W/2, H/2) (a m1 + b m2, c m2 + b m1), dconic = -o/2 (m3, m4, m5), dopacity = m0
-        const float* m = s_sum + lane * GSR_SUM_STRIDE;
-        const float4 p0 = *reinterpret_cast<const float4*>(m);
-        const float4 p1 = *reinterpret_cast<const float4*>(m + 4);
-        const float2 p2 = *reinterpret_cast<const float2*>(m + 8);
-        const float4 ga = s0[sub + lane];
-        const float4 gb = s1[sub + lane];
-        const float o = gb.y;
-        const float dmx = -o * ddelx_dx * (ga.z * p0.y + ga.w * p0.z);
-        const float dmy = -o * ddely_dy * (gb.x * p0.z + ga.w * p0.y);
-        const size_t d = 3 * (size_t)s_dest[sub + lane];
-        grow[d] = make_float4(dmx, dmy, -0.5f * o * p0.w, -0.5f * o * p1.x);
-        grow[d + 1] = make_float4(-0.5f * o * p1.y, p0.x, p1.z, p1.w);
-        grow[d + 2] = make_float4(p2.x, p2.y, 0.f, 0.f);
-      }
-      __syncthreads();
+      for (int i = 0; i < NGV; ++i) m[i] = qs[i] + qs[13 + i] + qs[26 + i] + qs[39 + i];
+      const float4 ga = s.s0[t];
+      const float4 gb = s.s1[t];
+      const float o = gb.y;
+      const float dmx = -o * ddelx_dx * (ga.z * m[1] + ga.w * m[2]);
+      const float dmy = -o * ddely_dy * (gb.x * m[2] + ga.w * m[1]);
+      float4* row = grow + 3 * (size_t)s.slot[t];
+      row[0] = make_float4(dmx, dmy, -0.5f * o * m[3], -0.5f * o * m[4]);
+      row[1] = make_float4(-0.5f * o * m[5], m[0], m[6], m[7]);
+      row[2] = make_float4(m[8], m[9], 0.f, 0.f);
     }
+    __syncthreads();
   }
   GSR_TL_END(1, tl_work)
   (void)tl_work;
@@ -584,7 +590,7 @@ void launch_render_backward(const RenderSet& rs, const GeomState& g, const uint3
                             const float* dL_dalpha, const BackwardState& bw, hipStream_t stream) {
   const int nt = rs.gx * rs.gy;
   if (nt <= 0 || rs.V <= 0) return;
-  hipLaunchKernelGGL(k_render_bwd, dim3(rs.V * unit_grid(rs.gx, rs.gy)), dim3(64), 0, stream, rs,
+  hipLaunchKernelGGL(k_render_bwd, dim3(rs.V * tile_grid(rs.gx, rs.gy)), dim3(256), 0, stream, rs,
                      (const uint2*)img.ranges, (const uint32_t*)img.quad_maxc, sorted_gauss,
                      (const float4*)g.rec0, (const float4*)g.rec1, (const float4*)g.rec2,
                      (const uint2*)g.rect, (const uint32_t*)g.goff, (const float*)img.final_T,
