@@ -398,7 +398,7 @@ int gsr_set_backward(int V, int P, int degree, int M, const int* K, int width, i
     ab.v0 = g0;
     ab.accumulate = first ? 0 : 1;
     ab.pad_ = 0;
-    ab.clamped = g.clamped;
+    ab.rec = g.rec;
     ab.radii = radii;
     ab.vrec = bw.vrec;
     for (int v = g0; v < g1; ++v) {

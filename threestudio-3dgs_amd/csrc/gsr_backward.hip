@@ -296,7 +296,9 @@ __global__ __launch_bounds__(256) void k_view_grad(GaussBackwardArgs a, ViewGrad
 #ifdef GSR_VG_NOGATHER  // timing experiment only (results wrong)
     const RowSums r = RowSums{0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
 #else
-    const RowSums r = gather_rows((uint32_t)idx, __float_as_uint(va.g.rec1[o].z), va.g.goff[o], va.g.rect[o], va.gx,
+    const GaussRec& gr = va.g.rec[o];
+    const uint4 gd = gr.d;
+    const RowSums r = gather_rows((uint32_t)idx, __float_as_uint(gr.b.z), gd.z, make_uint2(gd.x, gd.y), va.gx,
                                   cut, grow);
 #endif
 #ifdef GSR_VG_ONLYGATHER  // timing experiment only (results wrong)
@@ -389,7 +391,7 @@ __global__ __launch_bounds__(256) void k_gauss_accum(GaussBackwardArgs a, AccumA
       dcb += f[11];
       dop += f[12];
       if (has_sh) {
-        const uint32_t cl = b.clamped[o];
+        const uint32_t cl = b.rec[o].d.w;
         const float3 dRGB = make_float3((cl & 1u) ? 0.f : f[9], (cl & 2u) ? 0.f : f[10], (cl & 4u) ? 0.f : f[11]);
         sh_backward(a.deg, a.M, sh_row, dsh, dRGB, mean, b.campos[vl], dmean);
       }

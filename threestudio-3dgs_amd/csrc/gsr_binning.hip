@@ -102,7 +102,12 @@ __global__ __launch_bounds__(256) void k_emit(int P, int nbe, int grid_x, GeomSt
     gi[k] = r < P ? order[vo + r] : 0u;
     cnt[k] = r < P ? g.tiles_touched[vo + gi[k]] : 0u;
     s.gi[t * GSR_DUP_ITEMS + k] = gi[k];
-    s.rect[t * GSR_DUP_ITEMS + k] = cnt[k] ? g.rect[vo + gi[k]] : make_uint2(0u, 0u);
+    if (cnt[k]) {
+      const uint4 d = g.rec[vo + gi[k]].d;
+      s.rect[t * GSR_DUP_ITEMS + k] = make_uint2(d.x, d.y);
+    } else {
+      s.rect[t * GSR_DUP_ITEMS + k] = make_uint2(0u, 0u);
+    }
     sum += cnt[k];
   }
   uint32_t btot;
@@ -115,7 +120,7 @@ __global__ __launch_bounds__(256) void k_emit(int P, int nbe, int grid_x, GeomSt
     for (int k = 0; k < GSR_DUP_ITEMS; ++k) {
       myoff[k] = o;
       s.off[t * GSR_DUP_ITEMS + k] = o;
-      if (cnt[k]) g.goff[vo + gi[k]] = prefix + o;
+      if (cnt[k]) g.rec[vo + gi[k]].d.z = prefix + o;
       o += cnt[k];
     }
     if (t == 255) s.off[GSR_DUP_TILE] = btot;

@@ -130,19 +130,20 @@ struct SetCams {
   ViewCam c[GSR_SET_MAX];
 };
 
+// The per-(view, Gaussian) record every per-instance gather reads: one 64-byte line.
+//   a = (px, py, conic_a, conic_b), b = (conic_c, opacity, view depth, 0), c = (r, g, b, 0),
+//   d = (tile rect xmin | ymin << 16, xmax | ymax << 16, goff = first instance, SH clamp flags)
+struct __attribute__((aligned(64))) GaussRec {
+  float4 a, b, c;
+  uint4 d;
+};
+
 // Per-(view, Gaussian) forward state of a view set ("geom"); element (v, i) at v * P + i.
-// rec0/rec1/rec2 are the 48-byte render record the blend kernels gather per instance:
-// rec0 = (px, py, conic_a, conic_b), rec1 = (conic_c, opacity, view depth, 0), rec2 = (r, g, b, 0).
 struct GeomState {
-  float4* rec0;
-  float4* rec1;
-  float4* rec2;
-  uint2* rect;               // tile rect: x = xmin | ymin << 16, y = xmax | ymax << 16
-  uint32_t* clamped;         // SH clamp flags, bit c = channel c clamped to 0
+  GaussRec* rec;
   uint32_t* tiles_touched;   // instances per Gaussian (0 = culled)
   uint32_t* dkey[2];         // depth sort ping-pong keys (float bits of view depth; culled = ~0)
   uint32_t* dval[2];         // depth sort ping-pong values (Gaussian index within the view)
-  uint32_t* goff;            // first instance of each Gaussian in its view's (pre-tile-sort) list
   uint32_t* sort_counts;     // [V][RADIX][sort blocks] per-block digit counts -> scanned offsets
   uint32_t* sort_totals;     // [V][RADIX] digit totals
   uint32_t* inst_counts;     // [V][emission blocks] instances per block -> scanned offsets
@@ -155,17 +156,12 @@ struct GeomState {
     GeomState g;
     const size_t n = (size_t)(V > 0 ? V : 1) * (size_t)(P > 0 ? P : 1);
     const size_t nv = (size_t)(V > 0 ? V : 1);
-    g.rec0 = c.take<float4>(n);
-    g.rec1 = c.take<float4>(n);
-    g.rec2 = c.take<float4>(n);
-    g.rect = c.take<uint2>(n);
-    g.clamped = c.take<uint32_t>(n);
+    g.rec = c.take<GaussRec>(n);
     g.tiles_touched = c.take<uint32_t>(n);
     g.dkey[0] = c.take<uint32_t>(n);
     g.dkey[1] = c.take<uint32_t>(n);
     g.dval[0] = c.take<uint32_t>(n);
     g.dval[1] = c.take<uint32_t>(n);
-    g.goff = c.take<uint32_t>(n);
     g.sort_counts = c.take<uint32_t>(nv * GSR_RADIX * sort_blocks(P));
     g.sort_totals = c.take<uint32_t>(nv * GSR_RADIX);
     g.inst_counts = c.take<uint32_t>(nv * dup_blocks(P));

@@ -75,7 +75,7 @@ struct ViewGradArgs {
 // B: per Gaussian, sums the group's records, SH backward per view, scale / rotation once.
 struct AccumArgs {
   int V, v0, accumulate, pad_;
-  const uint32_t* clamped;  // the set's (V, P)
+  const GaussRec* rec;      // the set's (V, P) records (SH clamp flags in d.w)
   const int* radii;         // the set's (V, P)
   const float* vrec;
   const float* campos[GSR_SET_MAX];

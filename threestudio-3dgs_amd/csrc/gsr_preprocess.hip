@@ -80,11 +80,12 @@ __global__ __launch_bounds__(256) void k_preprocess(PreprocessArgs a, SetCams ca
                     make_float3(cam.campos[0], cam.campos[1], cam.campos[2]), &clamp_bits);
   }
 
-  g.rec0[vi] = make_float4(pimg.x, pimg.y, conic.x, conic.y);
-  g.rec1[vi] = make_float4(conic.z, a.opacities[idx], p_view.z, 0.0f);
-  g.rec2[vi] = make_float4(rgb.x, rgb.y, rgb.z, 0.0f);
-  g.rect[vi] = make_uint2((uint32_t)xmin | ((uint32_t)ymin << 16), (uint32_t)xmax | ((uint32_t)ymax << 16));
-  g.clamped[vi] = clamp_bits;
+  GaussRec rec;
+  rec.a = make_float4(pimg.x, pimg.y, conic.x, conic.y);
+  rec.b = make_float4(conic.z, a.opacities[idx], p_view.z, 0.0f);
+  rec.c = make_float4(rgb.x, rgb.y, rgb.z, 0.0f);
+  rec.d = make_uint4((uint32_t)xmin | ((uint32_t)ymin << 16), (uint32_t)xmax | ((uint32_t)ymax << 16), 0u, clamp_bits);
+  g.rec[vi] = rec;
   a.radii[vi] = r;
   g.tiles_touched[vi] = (uint32_t)area;
   g.dkey[0][vi] = __float_as_uint(p_view.z);  // > 0.2: float bits are monotone in depth

@@ -102,9 +102,7 @@ __device__ __forceinline__ bool quadrant_hit(const float4 r0, const float4 r1, f
 __global__ __launch_bounds__(64) void k_render_fwd(RenderSet rs,
                                                    const uint2* __restrict__ ranges,
                                                    const uint32_t* __restrict__ sorted_gauss,
-                                                   const float4* __restrict__ rec0,
-                                                   const float4* __restrict__ rec1,
-                                                   const float4* __restrict__ rec2,
+                                                   const GaussRec* __restrict__ rec,
                                                    float* __restrict__ out_color,
                                                    float* __restrict__ out_depth,
                                                    float* __restrict__ out_alpha,
@@ -124,9 +122,7 @@ __global__ __launch_bounds__(64) void k_render_fwd(RenderSet rs,
     ranges += vg * tiles;
     quad_maxc += vg * 4 * tiles;
     sorted_gauss += rs.inst_start[v];
-    rec0 += vg * rs.P;
-    rec1 += vg * rs.P;
-    rec2 += vg * rs.P;
+    rec += vg * rs.P;
     out_color += vg * 3 * HWs;
     out_depth += vg * HWs;
     out_alpha += vg * HWs;
@@ -154,9 +150,9 @@ __global__ __launch_bounds__(64) void k_render_fwd(RenderSet rs,
   uint32_t gi_next = 0u;
   if (lane < n) {
     const uint32_t g0 = sorted_gauss[range.x + lane] & gmask;
-    n0 = rec0[g0];
-    n1 = rec1[g0];
-    n2 = rec2[g0];
+    n0 = rec[g0].a;
+    n1 = rec[g0].b;
+    n2 = rec[g0].c;
   }
   if (64 + lane < n) gi_next = sorted_gauss[range.x + 64 + lane] & gmask;
   for (int base = 0; base < n; base += 64) {
@@ -164,9 +160,9 @@ __global__ __launch_bounds__(64) void k_render_fwd(RenderSet rs,
     const int i = base + lane;
     const float4 r0 = n0, r1 = n1, r2 = n2;
     if (base + 64 + lane < n) {
-      n0 = rec0[gi_next];
-      n1 = rec1[gi_next];
-      n2 = rec2[gi_next];
+      n0 = rec[gi_next].a;
+      n1 = rec[gi_next].b;
+      n2 = rec[gi_next].c;
     }
     if (base + 128 + lane < n) gi_next = sorted_gauss[range.x + base + 128 + lane] & gmask;
     bool keep = false;
@@ -229,7 +225,7 @@ __global__ __launch_bounds__(64) void k_render_fwd(RenderSet rs,
 __global__ __launch_bounds__(256) void k_tile_info(RenderSet rs, const uint2* __restrict__ ranges,
                                                    const uint32_t* __restrict__ quad_maxc,
                                                    const uint32_t* __restrict__ sorted_gauss,
-                                                   const float4* __restrict__ rec1,
+                                                   const GaussRec* __restrict__ rec,
                                                    uint4* __restrict__ tile_info, uint2* __restrict__ cut) {
   const int n_tiles = rs.gx * rs.gy;
   const int nb = div_up(n_tiles, 256);
@@ -243,7 +239,7 @@ __global__ __launch_bounds__(256) void k_tile_info(RenderSet rs, const uint2* __
     tile_info += vg * n_tiles;
     cut += vg * n_tiles;
     sorted_gauss += rs.inst_start[v];
-    rec1 += vg * rs.P;
+    rec += vg * rs.P;
   }
   const uint4 m = reinterpret_cast<const uint4*>(quad_maxc)[tile];
   const uint32_t maxc = max(max(m.x, m.y), max(m.z, m.w));
@@ -251,7 +247,7 @@ __global__ __launch_bounds__(256) void k_tile_info(RenderSet rs, const uint2* __
   uint4 info = make_uint4(maxc, 0xFFFFFFFFu, 0xFFFFFFFFu, 0u);
   if (maxc < range.y - range.x) {
     const uint32_t gi = sorted_gauss[range.x + maxc] & rs.gmask;
-    info.y = __float_as_uint(rec1[gi].z);
+    info.y = __float_as_uint(rec[gi].b.z);
     info.z = gi;
   }
   tile_info[tile] = info;
@@ -264,12 +260,11 @@ void launch_render_forward(const RenderSet& rs, const GeomState& g, const uint32
   const int nt = rs.gx * rs.gy;
   if (nt <= 0 || rs.V <= 0) return;
   hipLaunchKernelGGL(k_render_fwd, dim3(rs.V * unit_grid(rs.gx, rs.gy)), dim3(64), 0, stream, rs,
-                     (const uint2*)img.ranges, sorted_gauss, (const float4*)g.rec0,
-                     (const float4*)g.rec1, (const float4*)g.rec2, out_color, out_depth, out_alpha,
+                     (const uint2*)img.ranges, sorted_gauss, (const GaussRec*)g.rec, out_color, out_depth, out_alpha,
                      img.final_T, img.n_contrib, img.quad_maxc);
   hipLaunchKernelGGL(k_tile_info, dim3(rs.V * div_up(nt, 256)), dim3(256), 0, stream, rs,
                      (const uint2*)img.ranges, (const uint32_t*)img.quad_maxc, sorted_gauss,
-                     (const float4*)g.rec1, img.tile_info, img.cut);
+                     (const GaussRec*)g.rec, img.tile_info, img.cut);
 }
 
 // ---------------------------------------------------------------------------------------
@@ -353,11 +348,7 @@ __global__ __launch_bounds__(256) void k_render_bwd(RenderSet rs,
                                                     const uint2* __restrict__ ranges,
                                                     const uint32_t* __restrict__ quad_maxc,
                                                     const uint32_t* __restrict__ sorted_gauss,
-                                                    const float4* __restrict__ rec0,
-                                                    const float4* __restrict__ rec1,
-                                                    const float4* __restrict__ rec2,
-                                                    const uint2* __restrict__ rect,
-                                                    const uint32_t* __restrict__ goff,
+                                                    const GaussRec* __restrict__ rec,
                                                     const float* __restrict__ final_Ts,
                                                     const uint32_t* __restrict__ n_contrib,
                                                     const float* __restrict__ dL_dcolor,
@@ -376,11 +367,7 @@ __global__ __launch_bounds__(256) void k_render_bwd(RenderSet rs,
     ranges += vg * tiles;
     quad_maxc += vg * 4 * tiles;
     sorted_gauss += rs.inst_start[v];
-    rec0 += vg * rs.P;
-    rec1 += vg * rs.P;
-    rec2 += vg * rs.P;
-    rect += vg * rs.P;
-    goff += vg * rs.P;
+    rec += vg * rs.P;
     final_Ts += vg * HWs;
     n_contrib += vg * HWs;
     dL_dcolor += (size_t)v * 3 * HWs;
@@ -430,16 +417,15 @@ __global__ __launch_bounds__(256) void k_render_bwd(RenderSet rs,
     return r >= 0 ? (sorted_gauss[range.x + r] & gmask) : 0u;
   };
   float4 n0 = zero4, n1 = zero4, n2 = zero4;
-  uint2 nrc = make_uint2(0u, 0u);
-  uint32_t ngo = 0u, gi_next = 0u;
+  uint4 nd = make_uint4(0u, 0u, 0u, 0u);
+  uint32_t gi_next = 0u;
   if (q == 0 && maxc > 0) {
     const uint32_t g0 = fetch_index(maxc);
     if (maxc - 1 - lane >= 0) {
-      n0 = rec0[g0];
-      n1 = rec1[g0];
-      n2 = rec2[g0];
-      nrc = rect[g0];
-      ngo = goff[g0];
+      n0 = rec[g0].a;
+      n1 = rec[g0].b;
+      n2 = rec[g0].c;
+      nd = rec[g0].d;
     }
     if (maxc > 64) gi_next = fetch_index(maxc - 64);
   }
@@ -502,19 +488,18 @@ __global__ __launch_bounds__(256) void k_render_bwd(RenderSet rs,
     if (q == 0) {
       const int rel_l = hi - 1 - lane;
       if (rel_l >= 0) {
-        const int xmin = nrc.x & 0xffff, ymin = nrc.x >> 16, xmax = nrc.y & 0xffff;
+        const int xmin = nd.x & 0xffff, ymin = nd.x >> 16, xmax = nd.y & 0xffff;
         s.s0[lane] = n0;
         s.s1[lane] = make_float4(n1.x, n1.y, n1.z, __uint_as_float((uint32_t)rel_l));  // .w: list position
         s.s2[lane] = n2;
-        s.slot[lane] = ngo + (uint32_t)((tyi - ymin) * (xmax - xmin) + (txi - xmin));
+        s.slot[lane] = nd.z + (uint32_t)((tyi - ymin) * (xmax - xmin) + (txi - xmin));
       }
       if (hi > 64) {
         if (hi - 65 - lane >= 0) {
-          n0 = rec0[gi_next];
-          n1 = rec1[gi_next];
-          n2 = rec2[gi_next];
-          nrc = rect[gi_next];
-          ngo = goff[gi_next];
+          n0 = rec[gi_next].a;
+          n1 = rec[gi_next].b;
+          n2 = rec[gi_next].c;
+          nd = rec[gi_next].d;
         }
         if (hi > 128) gi_next = fetch_index(hi - 128);
       }
@@ -592,8 +577,7 @@ void launch_render_backward(const RenderSet& rs, const GeomState& g, const uint3
   if (nt <= 0 || rs.V <= 0) return;
   hipLaunchKernelGGL(k_render_bwd, dim3(rs.V * tile_grid(rs.gx, rs.gy)), dim3(256), 0, stream, rs,
                      (const uint2*)img.ranges, (const uint32_t*)img.quad_maxc, sorted_gauss,
-                     (const float4*)g.rec0, (const float4*)g.rec1, (const float4*)g.rec2,
-                     (const uint2*)g.rect, (const uint32_t*)g.goff, (const float*)img.final_T,
+                     (const GaussRec*)g.rec, (const float*)img.final_T,
                      (const uint32_t*)img.n_contrib, dL_dcolor, dL_ddepth, dL_dalpha, bw.grow);
 }
 
