@@ -53,7 +53,7 @@ def parse():
     ap.add_argument("--path", choices=["batched", "per-view"], default="batched",
                     help="batched: rasterize_views (one autograd node per rank's views); per-view: one "
                          "GaussianRasterizer call per view, exactly as the reference renderer loop does")
-    ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "r01_traffic.json"),
+    ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "r02_traffic.json"),
                     help="PMC summary (profiles/summarize.py) supplying roofline.traffic")
     return ap.parse_args()
 
@@ -293,14 +293,15 @@ def main():
         nv = max(1, args.steps * per)
         kern = {k: {"ms_per_view": round(ms / nv, 4), "launches": n} for k, (ms, n) in phases.items()}
         res["kernels"] = kern
-        # forward tile blend (north_star roofline kernel): SURVEY.md §8d B_fwd = 44 K + 28 HW + 8 tiles per
-        # view; a launch blends every view of a view set, so bytes per launch = sum over the timed views / launches
+        # algorithmic bytes per view, SURVEY.md §8d: forward tile blend B_fwd = 44 K + 28 HW + 8 tiles;
+        # backward blend 44 K + 32 HW read + 2 x 40 K (the reference's atomic read-modify-write).  A launch
+        # covers every view of a view set, so bytes per launch = sum over the timed views / launches.
         tiles = math.ceil(W / 16) * math.ceil(H / 16)
         f_ms, f_n = phases["render_fwd"]
         b_ms, b_n = phases["render_bwd"]
         n_fw = max(1, len(Ks))
         bytes_fwd = (44.0 * sum(Ks) + (28.0 * H * W + 8.0 * tiles) * n_fw) / max(1, f_n)
-        bytes_bwd = (84.0 * sum(Ks) + (28.0 * H * W + 8.0 * tiles) * n_fw) / max(1, b_n)  # 44 K gathered + 40 K grads
+        bytes_bwd = (124.0 * sum(Ks) + 32.0 * H * W * n_fw) / max(1, b_n)
         fwd_gbs = bytes_fwd / (f_ms / max(1, f_n) * 1e-3) / 1e9 if f_n else 0.0
         bwd_gbs = bytes_bwd / (b_ms / max(1, b_n) * 1e-3) / 1e9 if b_n else 0.0
         dominant = max(phases.items(), key=lambda kv: kv[1][0])[0]
@@ -316,7 +317,9 @@ def main():
         res["roofline_fwd_blend"] = roof_fwd
         res["dominant_kernel"] = dominant
         res["traffic_source"] = os.path.relpath(args.traffic, ROOT) + " (HBM bytes/launch, rocprofv3 --pmc " \
-                                "FETCH_SIZE x2 + WRITE_SIZE, 8-view capture of this workload)"
+                                "FETCH_SIZE x2 + WRITE_SIZE, capture of this workload: one 64-view launch)"
+        res["roofline_note"] = ("bytes are SURVEY.md §8d algorithmic bytes; both blends are fp32-VALU-bound "
+                                "(early termination: the forward reads ~1/3 of them, traffic field), see DESIGN.md §6")
     if world == 1 and not args.no_cpu_baseline:
         cb = cpu_baseline(scene, args.res, args.cpu_views)
         res["cpu_baseline"] = {k: (round(v, 5) if isinstance(v, float) else v) for k, v in cb.items()}
