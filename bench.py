@@ -53,7 +53,7 @@ def parse():
     ap.add_argument("--path", choices=["batched", "per-view"], default="batched",
                     help="batched: rasterize_views (one autograd node per rank's views); per-view: one "
                          "GaussianRasterizer call per view, exactly as the reference renderer loop does")
-    ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "r02_traffic.json"),
+    ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "r01_traffic.json"),
                     help="PMC summary (profiles/summarize.py) supplying roofline.traffic")
     return ap.parse_args()
 
