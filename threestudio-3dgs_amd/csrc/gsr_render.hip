@@ -268,63 +268,40 @@ void launch_render_forward(const RenderSet& rs, const GeomState& g, const uint32
 }
 
 // ---------------------------------------------------------------------------------------
-// Backward.  Per pixel the reference's back-to-front replay: T recovered by division, suffix
-// colour/depth/alpha accumulators, background term.  Per pair the 10 gradient terms are
-//   0,1 dmean2D (x W/2, H/2)  2,3,4 dconic (a, b[half], c)  5 dopacity  6,7,8 dcolor  9 ddepth
+// Backward.  Per pixel the reference's back-to-front replay: T recovered by division, the colour
+// accumulated behind each contributor, background term.  Per candidate the 10 gradient sums are
+//   0 sum u  1,2 sum u dx, u dy  3,4,5 sum u dx^2, u dx dy, u dy^2  6,7,8,9 sum w dL/d(r,g,b,depth)
+// with u = G dL/dalpha, w = alpha T (the reference's dmean2D / dconic / dopacity / dcolor / ddepth
+// are these sums times per-candidate factors).
 #define NGV 10
 
-__device__ __forceinline__ float swap_add32(float& x, float& y) {
-  // v_permlane32_swap: lanes 32-63 of x <-> lanes 0-31 of y, then add:
-  // result = [x_lo + x_hi | y_lo + y_hi]
-  const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(y), false, false);
-  return __uint_as_float(r[0]) + __uint_as_float(r[1]);
-}
-__device__ __forceinline__ float swap_add16(float x, float y) {
-  // v_permlane16_swap: in each 32-lane half, lanes 16-31 of x <-> lanes 0-15 of y, then add:
-  // rows (16 lanes) of the result = [x_r0 + x_r1, y_r0 + y_r1, x_r2 + x_r3, y_r2 + y_r3]
-  const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(x), __float_as_uint(y), false, false);
-  return __uint_as_float(r[0]) + __uint_as_float(r[1]);
-}
-// Sum two candidates' 10 per-lane values over the 64 lanes.  Transposed reduction: the 32-lane and
-// 16-lane exchanges each halve the register count (one swap + one add per pair), after which register
-// j holds, per 16-lane row, (va[j], va[j+5], vb[j], vb[j+5]) summed over 4 lanes; a 4-step DPP row
-// reduction finishes.  Lane 15 ends with va[0..4], lane 31 va[5..9], lane 47 vb[0..4], lane 63 vb[5..9].
-__device__ __forceinline__ void pair_reduce(float (&va)[NGV], float (&vb)[NGV], float (&out)[5]) {
-  float y[NGV];
-#pragma unroll
-  for (int i = 0; i < NGV; ++i) y[i] = swap_add32(va[i], vb[i]);  // [va_i | vb_i], 2 lanes each
-#pragma unroll
-  for (int j = 0; j < 5; ++j) {
-    float z = swap_add16(y[j], y[j + 5]);  // rows: va_j, va_{j+5}, vb_j, vb_{j+5}
-    z += dpp_f32<0x111>(z);
-    z += dpp_f32<0x112>(z);
-    z += dpp_f32<0x114>(z);
-    z += dpp_f32<0x118>(z);
-    out[j] = z;
-  }
-}
-
-// One wave per 8x8 quadrant (as the forward).  The wave walks its tile's list back to front from
-// the tile's deepest blended instance, 64 at a time, keeps (ballot compaction, order kept) the
-// Gaussians that are above the quadrant's own deepest blended instance and whose alpha >= 1/255
-// ellipse reaches the quadrant, replays them per pixel, reduces each Gaussian's 10 terms over
-// 16-lane rows with DPP, parks the 4 row partials in LDS and every 32 Gaussians writes one 48-byte
-// row per (instance, quadrant) at 4 * slot + quadrant, where slot is the instance's place in its
-// Gaussian's contiguous row range.  Instances the quadrant skips get zero rows, so every instance
-// above the tile cutoff has all 4 rows written.
 // Backward: one 256-thread workgroup per (view, tile); wave q owns quadrant q.  The four waves walk
 // the tile's list back to front in lockstep batches of 64 candidates: the batch's records are
 // staged in LDS once for all four (one global gather per candidate instead of four), each wave culls
-// the batch for its quadrant and reduces its kept candidates in pairs (pair_reduce) into per-
-// (candidate, quadrant) moment sums in LDS, and one thread per candidate adds the four quadrants
-// and writes ONE 48-byte gradient row per instance (4x fewer row bytes than a row per quadrant,
-// for this kernel's writes and the per-Gaussian gather's reads).
-#define GSR_QSUM_STRIDE 52  // floats per candidate: 4 quadrants x 13 (10 used); 208 B, conflict-free
+// the batch for its quadrant, replays its kept candidates per pixel and sums them over its 64 pixels
+// on the matrix cores, 8 candidates per 16x16 product, into per-(candidate, quadrant) sums in LDS;
+// one thread per candidate then adds the four quadrants and writes ONE 48-byte gradient row per
+// instance.
+// per-lane select by a wave mask: one v_cndmask_b32 (keeps the replay's state updates branch-free;
+// left to itself the compiler turns a run of selects on one condition into an exec-masked branch)
+__device__ __forceinline__ float vsel(unsigned long long m, float if_set, float if_clear) {
+  float r;
+  asm("v_cndmask_b32_e64 %0, %1, %2, %3" : "=v"(r) : "v"(if_clear), "v"(if_set), "s"(m));
+  return r;
+}
+
+#define GSR_QSUM_STRIDE 41  // floats per candidate: 4 quadrants x 10 raw sums, +1 pad
 struct BwdLDS {
   float4 s0[65], s1[65], s2[65];
   uint32_t slot[64];
   uint32_t list[4][64];
   float qsum[64 * GSR_QSUM_STRIDE];
+  // per wave: the group's A operand, u = G dL/dalpha (slots 0-7) and w = alpha T (slots 8-15) of
+  // its 8 candidates, stored so that MFMA lane l's 16 values are 4 chunks of 16 B (swizzled:
+  // conflict-free 16-B reads, 2-way 4-B writes)
+  float uw[4][64 * 16];
+  // per wave: the B operand's dL/d(r, g, b, depth) rows, [4][68] (padded) + a row of zeros
+  float dp[4][4 * 68 + 16];
 };
 
 __host__ __device__ __forceinline__ int tile_grid(int gx, int gy) {
@@ -344,7 +321,7 @@ __device__ __forceinline__ bool tile_of_block(int b, int gx, int gy, int& tile) 
   return true;
 }
 
-__global__ __launch_bounds__(256) void k_render_bwd(RenderSet rs,
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 8))) void k_render_bwd(RenderSet rs,
                                                     const uint2* __restrict__ ranges,
                                                     const uint32_t* __restrict__ quad_maxc,
                                                     const uint32_t* __restrict__ sorted_gauss,
@@ -405,8 +382,15 @@ __global__ __launch_bounds__(256) void k_render_bwd(RenderSet rs,
   }
   const float bg_dot = bg[0] * dpix[0] + bg[1] * dpix[1] + bg[2] * dpix[2];
 
-  float acc_r = 0.f, acc_g = 0.f, acc_b = 0.f, acc_d = 0.f, acc_a = 0.f;
-  float last_alpha = 0.f, last_r = 0.f, last_g = 0.f, last_b = 0.f, last_depth = 0.f;
+  // The reference keeps per channel the colour accumulated behind the current Gaussian
+  // (accum_rec = last_alpha last_c + (1 - last_alpha) accum_rec, deferred by one contributor) and
+  // forms dL/dalpha = T sum_ch (c_ch - accum_ch) dL/dpix_ch - T_final / (1 - alpha) bg . dL/dpix.
+  // Only the dot product with dL/dpix enters, and the update is linear, so one scalar carries all
+  // five channels (r, g, b, depth, alpha with c_alpha = 1):
+  //   S = sum_ch accum_ch dL/dpix_ch,  cd = sum_ch c_ch dL/dpix_ch,  S <- alpha cd + (1 - alpha) S
+  // applied eagerly after each contributor's own dL/dalpha (non-contributors: alpha = 0, identity).
+  float S = 0.f;
+  const float nbg = -T_final * bg_dot;
   const float ddelx_dx = 0.5f * W, ddely_dy = 0.5f * H;
   const float4 zero4 = make_float4(0.f, 0.f, 0.f, 0.f);
 
@@ -430,60 +414,73 @@ __global__ __launch_bounds__(256) void k_render_bwd(RenderSet rs,
     if (maxc > 64) gi_next = fetch_index(maxc - 64);
   }
 
-  // branch-free replay step (reference order of operations); non-contributing lanes keep their
-  // state and contribute zeros.  Per pair: moments of u = G dL/dalpha over the pixel offsets
-  // (mean2D / conic / opacity gradients are linear in them) and the colour / depth weights.
-  auto replay = [&](const float4& ga, const float4& gb, const float4& gc, float (&vv)[NGV]) -> bool {
+  // branch-free replay step; non-contributing lanes run it with alpha = 0 (state unchanged) and
+  // contribute zeros.  Returns per pixel u = G dL/dalpha (the mean2D / conic / opacity
+  // gradients are linear in u's moments over the pixel offsets) and w = alpha T (the colour / depth
+  // weights); the sums over the quadrant's 64 pixels are formed by the matrix cores (below).
+  auto replay = [&](const float4& ga, const float4& gb, const float4& gc, float& u, float& w) {
     const uint32_t rel = __float_as_uint(gb.w);
     const float dx = ga.x - pxf, dy = ga.y - pyf;
     const float power = gauss_power(ga.z, ga.w, gb.x, dx, dy);
     const float G = __expf(power);
     const float alpha = fminf(GSR_ALPHA_MAX, gb.y * G);
     const bool hit = rel < last_contributor && power <= 0.0f && alpha >= GSR_ALPHA_MIN;
-    const float inv_1ma = fast_rcp(1.f - alpha);
-    T = hit ? T * inv_1ma : T;
-    const float oml = 1.f - last_alpha;
-    const float nr = last_alpha * last_r + oml * acc_r;
-    const float ng = last_alpha * last_g + oml * acc_g;
-    const float nb = last_alpha * last_b + oml * acc_b;
-    const float nd = last_alpha * last_depth + oml * acc_d;
-    const float na = last_alpha * 1.0f + oml * acc_a;
-    float dL_dalpha = 0.0f;
-    dL_dalpha += (gc.x - nr) * dpix[0];
-    dL_dalpha += (gc.y - ng) * dpix[1];
-    dL_dalpha += (gc.z - nb) * dpix[2];
-    dL_dalpha += (gb.z - nd) * dpix_d;
-    dL_dalpha += (1.f - na) * dpix_a;
-    dL_dalpha *= T;
-    dL_dalpha += (-T_final * inv_1ma) * bg_dot;
-    const float u = hit ? G * dL_dalpha : 0.0f;  // dL/dG / opacity
-    const float w = hit ? alpha * T : 0.0f;      // dL/dcolor per unit dL/dpixel
-    acc_r = hit ? nr : acc_r;
-    acc_g = hit ? ng : acc_g;
-    acc_b = hit ? nb : acc_b;
-    acc_d = hit ? nd : acc_d;
-    acc_a = hit ? na : acc_a;
-    last_r = hit ? gc.x : last_r;
-    last_g = hit ? gc.y : last_g;
-    last_b = hit ? gc.z : last_b;
-    last_depth = hit ? gb.z : last_depth;
-    last_alpha = hit ? alpha : last_alpha;
-    const float udx = u * dx, udy = u * dy;
-    vv[0] = u;
-    vv[1] = udx;
-    vv[2] = udy;
-    vv[3] = udx * dx;
-    vv[4] = udx * dy;
-    vv[5] = udy * dy;
-    vv[6] = w * dpix[0];
-    vv[7] = w * dpix[1];
-    vv[8] = w * dpix[2];
-    vv[9] = w * dpix_d;
-    return hit;
+    const unsigned long long hm = __ballot(hit);
+    const float a_eff = vsel(hm, alpha, 0.0f);
+    const float g_eff = vsel(hm, G, 0.0f);
+    const float oma = 1.f - a_eff;
+    const float inv_1ma = fast_rcp(oma);  // 1 for non-contributors
+    T = T * inv_1ma;
+    const float cd = fmaf(gc.x, dpix[0], fmaf(gc.y, dpix[1], fmaf(gc.z, dpix[2], fmaf(gb.z, dpix_d, dpix_a))));
+    const float dL_dalpha = fmaf(T, cd - S, inv_1ma * nbg);
+    u = g_eff * dL_dalpha;
+    w = a_eff * T;
+    S = fmaf(a_eff, cd, oma * S);
   };
 
+
+  // Matrix-core reduction.  For a group of 8 candidates c, one 16x16 product over the quadrant's
+  // 64 pixels p: A rows 0-7 = u of the candidates, rows 8-15 = their w; B columns 0-5 =
+  // F(p) = (1, x, y, x^2, x y, y^2) of the pixel's quadrant-local coordinates, columns 6-9 = the
+  // pixel's dL/d(r, g, b, depth).  Rows 0-7 x columns 0-5 are the u moments, rows 8-15 x columns
+  // 6-9 the colour / depth sums; the other quarters are not used.  16 v_mfma_f32_16x16x4_f32
+  // (exact fp32 fma chains, 2 interleaved accumulators for the 40-cycle dependency).
+  // Operand maps (16x16x4): lane l holds A[l & 15][k = l >> 4], B[k = l >> 4][l & 15];
+  // result lane l: column l & 15, rows 4 (l >> 4) + r.
+  // k-step i, k = l >> 4 covers pixel p = 16 k + i: x = p & 7 = i & 7 (uniform), y = p >> 3 =
+  // 2 k + (i >> 3), so F = fa[i >> 3] + x (fbb[i >> 3] + x fc).
+  const int ncol = lane & 15;
+  const bool dcol = ncol >= 6 && ncol <= 9;
+  float fa[2], fbb[2], fc;
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    const float y = (float)(2 * (lane >> 4) + h);
+    fa[h] = ncol == 0 ? 1.f : ncol == 2 ? y : ncol == 5 ? y * y : 0.f;
+    fbb[h] = ncol == 1 ? 1.f : ncol == 4 ? y : 0.f;
+  }
+  fc = ncol == 3 ? 1.f : 0.f;
+  float* sdp = s.dp[q];
+  sdp[0 * 68 + lane] = dpix[0];
+  sdp[1 * 68 + lane] = dpix[1];
+  sdp[2 * 68 + lane] = dpix[2];
+  sdp[3 * 68 + lane] = dpix_d;
+  if (lane < 16) sdp[4 * 68 + lane] = 0.f;
+  const float4* dsrc = reinterpret_cast<const float4*>(sdp + (dcol ? (ncol - 6) * 68 + 16 * (lane >> 4) : 4 * 68));
+  float* uw = s.uw[q];
+  // writer side: (slot r, pixel p = lane) -> 16 r + 256 (p >> 4) + 4 (((p >> 2) & 3) ^ ((r >> 2) & 3)) + (p & 3)
+  int wa[4];
+#pragma unroll
+  for (int sgrp = 0; sgrp < 4; ++sgrp) wa[sgrp] = 256 * (lane >> 4) + 4 * (((lane >> 2) & 3) ^ sgrp) + (lane & 3);
+  // reader side: chunk k of lane l at 16 l + 4 (k ^ ((l >> 2) & 3))
+  const float4* asrc = reinterpret_cast<const float4*>(uw + 16 * lane);
+  const int aswz = (lane >> 2) & 3;
+  // result side: lane l holds rows 4 (l >> 4) + r -> candidate mb + r of the group, u (rows 0-7,
+  // columns 0-5 used) or w (rows 8-15, columns 6-9 used)
+  const int mb = 4 * ((lane >> 4) & 1);
+  const bool useful = (lane < 32) ? (ncol < 6) : dcol;
+
   uint32_t* mylist = s.list[q];
-  float* myq = s.qsum + q * 13;
+  float* myq = s.qsum + q * NGV;
   for (int hi = maxc; hi > 0; hi -= 64) {
     if (q == 0) {
       const int rel_l = hi - 1 - lane;
@@ -519,43 +516,96 @@ __global__ __launch_bounds__(256) void k_render_bwd(RenderSet rs,
     tl_work += cnt;
     if (keep) mylist[mask_rank(bal)] = (uint32_t)lane;
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // this wave's list is read back by its own lanes
-    // kept candidates in pairs: transposed reduction of the 2 x 10 per-lane values (pair_reduce)
-    for (int k = 0; k < cnt; k += 2) {
-      const int j0 = __builtin_amdgcn_readfirstlane(mylist[k]);
-      const int j1 = k + 1 < cnt ? __builtin_amdgcn_readfirstlane(mylist[k + 1]) : -1;
-      float va[NGV], vb[NGV];
-      bool hit = replay(s.s0[j0], s.s1[j0], s.s2[j0], va);
-      if (j1 >= 0) {
-        hit = replay(s.s0[j1], s.s1[j1], s.s2[j1], vb) || hit;
-      } else {
+    // kept candidates in groups of 8: replay -> (u, w) rows in LDS -> matrix-core sums.
+    // The kept set is the uniform ballot mask: walk it with scalar bit scans, prefetching the next
+    // candidate's staged record while the current one is replayed.
+    unsigned long long rest = bal;
+    for (int g0 = 0; g0 < cnt; g0 += 8) {
+      const int gn = min(8, cnt - g0);
+      int j = (int)__builtin_ctzll(rest);
+      float4 ca = s.s0[j], cb = s.s1[j], cc = s.s2[j];
 #pragma unroll
-        for (int i = 0; i < NGV; ++i) vb[i] = 0.f;
+      for (int c = 0; c < 8; ++c) {
+        if (c < gn) {
+          rest &= rest - 1ull;
+          const int jn = (c + 1 < gn) ? (int)__builtin_ctzll(rest) : j;
+          const float4 na = s.s0[jn], nb = s.s1[jn], nc = s.s2[jn];
+          float u, w;
+#ifdef GSR_EXP_NOREPLAY
+          u = ca.x * pxf;
+          w = cb.x * pyf;
+#else
+          replay(ca, cb, cc, u, w);
+#endif
+          uw[16 * c + wa[c >> 2]] = u;
+          uw[16 * (c + 8) + wa[2 + (c >> 2)]] = w;
+          ca = na;
+          cb = nb;
+          cc = nc;
+          j = jn;
+        }
       }
-      // lane 15: candidate j0 values 0-4, lane 31: j0 values 5-9, lanes 47 / 63: candidate j1
-      const int jj = (lane >> 5) ? j1 : j0;
-      float r[5];
-      if (__any(hit)) {
-        pair_reduce(va, vb, r);
-      } else {
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the wave reads its own lanes' rows
+#ifdef GSR_EXP_NOMFMA
+      continue;
+#endif
+      float av[16], dv[16];
 #pragma unroll
-        for (int i = 0; i < 5; ++i) r[i] = 0.f;
+      for (int k = 0; k < 4; ++k) {
+        const float4 a4 = asrc[k ^ aswz];
+        const float4 d4 = dsrc[k];
+        av[4 * k] = a4.x, av[4 * k + 1] = a4.y, av[4 * k + 2] = a4.z, av[4 * k + 3] = a4.w;
+        dv[4 * k] = d4.x, dv[4 * k + 1] = d4.y, dv[4 * k + 2] = d4.z, dv[4 * k + 3] = d4.w;
       }
-      if ((lane & 15) == 15 && jj >= 0) {
-        float* dst = myq + jj * GSR_QSUM_STRIDE + ((lane >> 4) & 1) * 5;
+      // the candidates of this lane's 4 result rows (m = mb + r)
+      const uint4 jl = *reinterpret_cast<const uint4*>(mylist + g0 + mb);
+      typedef float f4 __attribute__((ext_vector_type(4)));
+      f4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-        for (int i = 0; i < 5; ++i) dst[i] = r[i];
+      for (int i = 0; i < 16; ++i) {
+        const float x = (float)(i & 7);
+        // one of the two terms is zero: D for columns 6-9 (zeros row otherwise), F for 0-5
+        const float bv = dv[i] + (fa[i >> 3] + x * (fbb[i >> 3] + x * fc));
+        if (i & 1)
+          acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(av[i], bv, acc1, 0, 0, 0);
+        else
+          acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(av[i], bv, acc0, 0, 0, 0);
       }
+      // lane l: column ncol, rows 4 (l >> 4) + r; u rows 0-7 (columns 0-5), w rows 8-15 (6-9)
+      if (useful) {
+        const uint32_t jr[4] = {jl.x, jl.y, jl.z, jl.w};
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          if (mb + r < gn) myq[jr[r] * (uint32_t)GSR_QSUM_STRIDE + (uint32_t)ncol] = acc0[r] + acc1[r];
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // rows are rewritten by the next group
     }
     __syncthreads();
     if (t < 64 && hi - 1 - t >= 0) {
-      // one thread per candidate: add the 4 quadrants' moments, turn them into the reference's terms
+      // one thread per candidate: per quadrant, turn the sums over quadrant-local pixel coordinates
+      // into the moments of u over dx = mean - pixel (dx = mx' - x with mx' = mean - quadrant origin),
+      // add the 4 quadrants, and form the reference's terms
       //   dmean2D = -o (W/2, H/2) (a m1 + b m2, c m2 + b m1), dconic = -o/2 (m3, m4, m5), dopacity = m0
       const float* qs = s.qsum + t * GSR_QSUM_STRIDE;
-      float m[NGV];
-#pragma unroll
-      for (int i = 0; i < NGV; ++i) m[i] = qs[i] + qs[13 + i] + qs[26 + i] + qs[39 + i];
       const float4 ga = s.s0[t];
       const float4 gb = s.s1[t];
+      float m[NGV] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int qq = 0; qq < 4; ++qq) {
+        const float* C = qs + NGV * qq;
+        const float mx = ga.x - (float)(txi * GSR_TILE_X + (qq & 1) * 8);
+        const float my = ga.y - (float)(tyi * GSR_TILE_Y + (qq >> 1) * 8);
+        m[0] += C[0];
+        m[1] += mx * C[0] - C[1];
+        m[2] += my * C[0] - C[2];
+        m[3] += mx * (mx * C[0] - 2.f * C[1]) + C[3];
+        m[4] += mx * (my * C[0] - C[2]) - my * C[1] + C[4];
+        m[5] += my * (my * C[0] - 2.f * C[2]) + C[5];
+        m[6] += C[6];
+        m[7] += C[7];
+        m[8] += C[8];
+        m[9] += C[9];
+      }
       const float o = gb.y;
       const float dmx = -o * ddelx_dx * (ga.z * m[1] + ga.w * m[2]);
       const float dmy = -o * ddely_dy * (gb.x * m[2] + ga.w * m[1]);
