@@ -48,6 +48,9 @@ def summarise(tl, name):
         "xcd_busy_us": [int(dur[xcc == x].sum()) / 1e3 for x in range(8)],
         "occupancy_profile_10": [int(np.mean(occ[i * 10:(i + 1) * 10])) for i in range(10)],
         "time_frac_below_512_blocks": float(np.mean(np.array(occ) < 512)),
+        # bwd only: z = sum over batches of 4 x the busiest quadrant's kept count -> lockstep slots per kept pair
+        "bwd_lockstep_slots_per_pair": (float(tl[:, 2].astype(np.float64).sum() / max(1, work.sum()))
+                                        if name == "k_render_bwd" else None),
     }
 
 

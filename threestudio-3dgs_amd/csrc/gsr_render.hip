@@ -302,6 +302,9 @@ struct BwdLDS {
   float uw[4][64 * 16];
   // per wave: the B operand's dL/d(r, g, b, depth) rows, [4][68] (padded) + a row of zeros
   float dp[4][4 * 68 + 16];
+#ifdef GSR_TIMELINE
+  int tl_cnt[4];
+#endif
 };
 
 __host__ __device__ __forceinline__ int tile_grid(int gx, int gy) {
@@ -353,7 +356,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 8))) voi
     grow += (size_t)3 * rs.row_start[v];
   }
   const float* bg = rs.bg[v];
-  int tl_work = 0;
+  int tl_work = 0, tl_max = 0;
   const int t = threadIdx.x, q = t >> 6, lane = t & 63;
   const int txi = tile % grid_x, tyi = tile / grid_x;
   const int qx0 = txi * GSR_TILE_X + (q & 1) * 8;
@@ -513,7 +516,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 8))) voi
     }
     const unsigned long long bal = __ballot(keep);
     const int cnt = __popcll(bal);
-    tl_work += cnt;
+#ifdef GSR_TIMELINE
+    if (lane == 0) s.tl_cnt[q] = cnt;
+#endif
     if (keep) mylist[mask_rank(bal)] = (uint32_t)lane;
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // this wave's list is read back by its own lanes
     // kept candidates in groups of 8: replay -> (u, w) rows in LDS -> matrix-core sums.
@@ -581,6 +586,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 8))) voi
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // rows are rewritten by the next group
     }
     __syncthreads();
+#ifdef GSR_TIMELINE
+    if (t == 0) {
+      const int c0 = s.tl_cnt[0], c1 = s.tl_cnt[1], c2 = s.tl_cnt[2], c3 = s.tl_cnt[3];
+      tl_work += c0 + c1 + c2 + c3;                                  // kept (candidate, quadrant) pairs
+      tl_max += 4 * max(max(c0, c1), max(c2, c3));                  // lockstep cost in pair slots
+    }
+#endif
     if (t < 64 && hi - 1 - t >= 0) {
       // one thread per candidate: per quadrant, turn the sums over quadrant-local pixel coordinates
       // into the moments of u over dx = mean - pixel (dx = mx' - x with mx' = mean - quadrant origin),
@@ -616,8 +628,15 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 8))) voi
     }
     __syncthreads();
   }
-  GSR_TL_END(1, tl_work)
+#ifdef GSR_TIMELINE
+  // bwd record: z = sum over batches of 4 x the busiest quadrant's kept count (not HW_ID)
+  if (threadIdx.x == 0 && blockIdx.x < GSR_TL_MAX)
+    g_timeline[1][blockIdx.x] = make_uint4(tl_t0, (uint32_t)__builtin_amdgcn_s_memrealtime(), (uint32_t)tl_max,
+                                           ((uint32_t)__builtin_amdgcn_s_getreg((15 << 11) | 20) << 24) |
+                                               ((uint32_t)tl_work & 0xffffffu));
+#endif
   (void)tl_work;
+  (void)tl_max;
 }
 
 void launch_render_backward(const RenderSet& rs, const GeomState& g, const uint32_t* sorted_gauss,
