@@ -290,6 +290,7 @@ int gsr_set_render(int V, int P, const int* K, int width, int height, const floa
   ImageState img = ImageState::carve(image, V, width, height, nullptr);
   const int gx = div_up(width, GSR_TILE_X), gy = div_up(height, GSR_TILE_Y);
   const int tres = tile_sort_result(width, height);
+  inst.ndev = g.counters + 2 * V;  // kept instances per view (<= K, the list capacity)
   {
     PhaseScope ps(GSR_PHASE_BINNING, s);
     GSR_HIP_CHECK(hipMemsetAsync(img.ranges, 0, sizeof(uint2) * (size_t)V * gx * gy, s));

@@ -24,47 +24,51 @@ struct RowSums {
   float dmx, dmy, dca, dcb, dcc, dop, dcr, dcg, dcbl, ddep;
 };
 
-// Sum the rows of the Gaussian's instances that its tile's blend reached: (depth key, index) < the
-// tile's first unblended instance (cut = (key, index) per tile).  The rect is walked 4 tiles at a
-// time: the 4 cut tests first, then the valid rows' loads together, so a thread has up to 12 loads
-// in flight instead of waiting on each row in turn.
-__device__ __forceinline__ RowSums gather_rows(uint32_t idx, uint32_t dkey, uint32_t i0, uint2 rc, int grid_x,
-                                               const uint2* cut, const float4* grow) {
+// Sum the rows of the Gaussian's instances that its tile's blend reached: the kept tiles of its
+// rectangle (span_row, as emitted) whose (depth key, index) < the tile's first unblended
+// instance (cut = (key, index) per tile).  Rows sit at rectangle positions.  Tiles are walked 4 at
+// a time: the 4 cut tests first, then the valid rows' loads together, so a thread has up to 12
+// loads in flight instead of waiting on each row in turn.
+__device__ __forceinline__ RowSums gather_rows(uint32_t idx, const GaussRec& gr, int grid_x, const uint2* cut,
+                                               const float4* grow) {
   RowSums r = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-  const int xmin = rc.x & 0xffff, ymin = rc.x >> 16, xmax = rc.y & 0xffff, ymax = rc.y >> 16;
-  const int w = xmax - xmin, n = w * (ymax - ymin);
-  int tx = xmin, ty = ymin;
+  const uint4 gd = gr.d;
+  const float4 ga = gr.a, gb = gr.b;
+  const uint32_t dkey = __float_as_uint(gb.z), i0 = gd.z;
+  const int xmin = gd.x & 0xffff, ymin = gd.x >> 16, xmax = gd.y & 0xffff, ymax = gd.y >> 16;
+  const int w = xmax - xmin;
+  const SpanPrep sp = span_prep(ga.x, ga.y, ga.z, ga.w, gb.x, gb.y);
   const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
-  for (int l = 0; l < n; l += 4) {
-    bool val[4];
-    int sl[4];
+  for (int ty = ymin; ty < ymax; ++ty) {
+    int t0, t1;
+    span_row(sp, ty, xmin, xmax, t0, t1);  // the kept tiles of this row, as emitted
+    for (int tx = t0; tx < t1; tx += 4) {
+      bool val[4];
+      int sl[4];
 #pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      val[k] = false;
-      sl[k] = 0;
-      if (l + k < n) {
-        const uint2 c = cut[ty * grid_x + tx];
-        val[k] = dkey < c.x || (dkey == c.x && idx < c.y);
-        sl[k] = l + k;
-        if (++tx == xmax) {
-          tx = xmin;
-          ++ty;
+      for (int k = 0; k < 4; ++k) {
+        val[k] = false;
+        sl[k] = 0;
+        if (tx + k < t1) {
+          const uint2 c = cut[ty * grid_x + tx + k];
+          val[k] = dkey < c.x || (dkey == c.x && idx < c.y);
+          sl[k] = (ty - ymin) * w + (tx + k - xmin);
         }
       }
-    }
-    float4 a[4][3];
+      float4 a[4][3];
 #pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      const float4* row = grow + 3 * ((size_t)i0 + sl[k]);
-      a[k][0] = val[k] ? row[0] : z4;
-      a[k][1] = val[k] ? row[1] : z4;
-      a[k][2] = val[k] ? row[2] : z4;
-    }
+      for (int k = 0; k < 4; ++k) {
+        const float4* row = grow + 3 * ((size_t)i0 + sl[k]);
+        a[k][0] = val[k] ? row[0] : z4;
+        a[k][1] = val[k] ? row[1] : z4;
+        a[k][2] = val[k] ? row[2] : z4;
+      }
 #pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      r.dmx += a[k][0].x; r.dmy += a[k][0].y; r.dca += a[k][0].z; r.dcb += a[k][0].w;
-      r.dcc += a[k][1].x; r.dop += a[k][1].y; r.dcr += a[k][1].z; r.dcg += a[k][1].w;
-      r.dcbl += a[k][2].x; r.ddep += a[k][2].y;
+      for (int k = 0; k < 4; ++k) {
+        r.dmx += a[k][0].x; r.dmy += a[k][0].y; r.dca += a[k][0].z; r.dcb += a[k][0].w;
+        r.dcc += a[k][1].x; r.dop += a[k][1].y; r.dcr += a[k][1].z; r.dcg += a[k][1].w;
+        r.dcbl += a[k][2].x; r.ddep += a[k][2].y;
+      }
     }
   }
   return r;
@@ -293,18 +297,7 @@ __global__ __launch_bounds__(256) void k_view_grad(GaussBackwardArgs a, ViewGrad
       for (int f = 0; f < GSR_GRAD_FIELDS; ++f) rec[(size_t)f * a.P] = 0.f;
       continue;
     }
-#ifdef GSR_VG_NOGATHER  // timing experiment only (results wrong)
-    const RowSums r = RowSums{0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-#else
-    const GaussRec& gr = va.g.rec[o];
-    const uint4 gd = gr.d;
-    const RowSums r = gather_rows((uint32_t)idx, __float_as_uint(gr.b.z), gd.z, make_uint2(gd.x, gd.y), va.gx,
-                                  cut, grow);
-#endif
-#ifdef GSR_VG_ONLYGATHER  // timing experiment only (results wrong)
-    m2[0] = r.dmx + r.dmy + r.dca + r.dcb + r.dcc + r.dop + r.dcr + r.dcg + r.dcbl + r.ddep;
-    continue;
-#endif
+    const RowSums r = gather_rows((uint32_t)idx, va.g.rec[o], va.gx, cut, grow);
     m2[0] = r.dmx;
     m2[1] = r.dmy;
     m2[2] = 0.f;

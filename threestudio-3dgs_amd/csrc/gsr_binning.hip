@@ -14,44 +14,41 @@
 
 namespace gsr {
 
-// Instances of each 1024-Gaussian block of every view's depth order: counts[v][block].
+// Instances of each GSR_DUP_TILE-Gaussian block of every view's depth order: counts[v][block].
 __global__ __launch_bounds__(256) void k_inst_count(int P, int nbe, GeomState g, const uint32_t* __restrict__ order) {
   __shared__ uint32_t s_wave[8];
   const int v = blockIdx.x / nbe, lb = blockIdx.x % nbe;
   const int t = threadIdx.x;
   const size_t vo = (size_t)v * P;
-  uint32_t sum = 0u, vis = 0u;
+  uint32_t sum = 0u, vis = 0u, kept = 0u;
 #pragma unroll
   for (int k = 0; k < GSR_DUP_ITEMS; ++k) {
     const int r = lb * GSR_DUP_TILE + k * 256 + t;
-    const uint32_t tt = r < P ? g.tiles_touched[vo + order[vo + r]] : 0u;
-    sum += tt;
-    vis += tt > 0u ? 1u : 0u;
+    const uint2 tt = r < P ? g.tiles[vo + order[vo + r]] : make_uint2(0u, 0u);
+    sum += tt.x;
+    vis += tt.x > 0u ? 1u : 0u;
+    kept += tt.y;
   }
   const uint32_t tot = block_sum_u32<256>(sum, s_wave);
   const uint32_t vtot = block_sum_u32<256>(vis, s_wave);
+  const uint32_t ktot = block_sum_u32<256>(kept, s_wave);
   if (t == 0) {
     g.inst_counts[(size_t)v * nbe + lb] = tot;
     g.vis_counts[(size_t)v * nbe + lb] = vtot;
+    g.kept_counts[(size_t)v * nbe + lb] = ktot;
   }
 }
 
-// One workgroup per view: exclusive scan of its block counts in place; K_v -> counters[v],
-// visible Gaussians -> counters[V + v].
-__global__ __launch_bounds__(256) void k_inst_scan(int nbe, GeomState g) {
-  __shared__ uint32_t s_wave[8];
-  const int v = blockIdx.x, t = threadIdx.x;
-  uint32_t* row = g.inst_counts + (size_t)v * nbe;
-  uint32_t vis = 0u;
-  for (int i = t; i < nbe; i += 256) vis += g.vis_counts[(size_t)v * nbe + i];
-  vis = block_sum_u32<256>(vis, s_wave);
+// Exclusive scan of one row of n counts in place (one workgroup); returns the total.
+__device__ uint32_t scan_row(uint32_t* row, int n, uint32_t* s_wave) {
+  const int t = threadIdx.x;
   uint32_t carry = 0u;
-  for (int c0 = 0; c0 < nbe; c0 += 256 * 4) {
+  for (int c0 = 0; c0 < n; c0 += 256 * 4) {
     uint32_t x[4], run = 0u;
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
       const int i = c0 + 4 * t + k;
-      const uint32_t c = i < nbe ? row[i] : 0u;
+      const uint32_t c = i < n ? row[i] : 0u;
       x[k] = run;
       run += c;
     }
@@ -60,28 +57,46 @@ __global__ __launch_bounds__(256) void k_inst_scan(int nbe, GeomState g) {
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
       const int i = c0 + 4 * t + k;
-      if (i < nbe) row[i] = off + x[k];
+      if (i < n) row[i] = off + x[k];
     }
     carry += tot;
   }
+  return carry;
+}
+
+// One workgroup per view: exclusive scans of its block counts in place; rectangle tiles K_v ->
+// counters[v], visible Gaussians -> counters[V + v], kept instances -> counters[2V + v].
+__global__ __launch_bounds__(256) void k_inst_scan(int nbe, GeomState g) {
+  __shared__ uint32_t s_wave[8];
+  const int v = blockIdx.x, t = threadIdx.x;
+  uint32_t vis = 0u;
+  for (int i = t; i < nbe; i += 256) vis += g.vis_counts[(size_t)v * nbe + i];
+  vis = block_sum_u32<256>(vis, s_wave);
+  const uint32_t rect = scan_row(g.inst_counts + (size_t)v * nbe, nbe, s_wave);
+  const uint32_t kept = scan_row(g.kept_counts + (size_t)v * nbe, nbe, s_wave);
   if (t == 0) {
-    g.counters[v] = carry;
+    g.counters[v] = rect;
     g.counters[gridDim.x + v] = vis;
+    g.counters[2 * gridDim.x + v] = kept;
   }
 }
 
-// Emit one (tile id, Gaussian) instance per tile of each visible Gaussian, in depth order, and
-// goff[g] = the Gaussian's first instance.  A block owns 1024 consecutive depth-sorted Gaussians
-// of one view (4 per thread); its instances are one contiguous range (offset from k_inst_scan),
-// written cooperatively in chunks of 2048 so consecutive lanes write consecutive addresses.  The
-// owner of every position of a chunk comes from an owner map: each Gaussian marks its first
-// position, and a max-scan over the chunk spreads the marks (offsets grow with the Gaussian).
+// Emit one (tile id, Gaussian) instance per kept tile (span_row) of each visible Gaussian, in
+// depth order, and goff[g] = the Gaussian's first rectangle slot (gradient rows are indexed by
+// rectangle position, the lists hold the kept tiles only).  A block owns GSR_DUP_TILE (512)
+// consecutive depth-sorted Gaussians of one view; their rectangle positions are walked in chunks
+// of 2048 (each wave 512 consecutive positions, 64 per round), the owner of every position comes
+// from an owner map (each Gaussian marks its first position, a max-scan spreads the marks), and
+// the kept positions are compacted in order (ballots within a wave, one exchange of the 4 wave
+// totals) into the block's contiguous output range (offset from k_inst_scan).
 #define GSR_EMIT_CHUNK 2048
 struct DupLDS {
   uint32_t off[GSR_DUP_TILE + 1];
   uint32_t gi[GSR_DUP_TILE];
   uint2 rect[GSR_DUP_TILE];
+  SpanPrep sp[GSR_DUP_TILE];  // tile culling of each Gaussian (span_row)
   uint32_t own[GSR_EMIT_CHUNK];
+  uint32_t kc[4];  // kept positions per wave of the chunk
   uint32_t wave[8];
   uint32_t carry;
 };
@@ -92,7 +107,7 @@ __global__ __launch_bounds__(256) void k_emit(int P, int nbe, int grid_x, GeomSt
   __shared__ DupLDS s;
   constexpr int PER = GSR_EMIT_CHUNK / 256;
   const int v = blockIdx.x / nbe, lb = blockIdx.x % nbe;
-  const int t = threadIdx.x;
+  const int t = threadIdx.x, w = t >> 6, lane = t & 63;
   const size_t vo = (size_t)v * P;
   uint32_t gi[GSR_DUP_ITEMS], cnt[GSR_DUP_ITEMS];
   uint32_t sum = 0u;
@@ -100,18 +115,24 @@ __global__ __launch_bounds__(256) void k_emit(int P, int nbe, int grid_x, GeomSt
   for (int k = 0; k < GSR_DUP_ITEMS; ++k) {
     const int r = lb * GSR_DUP_TILE + t * GSR_DUP_ITEMS + k;
     gi[k] = r < P ? order[vo + r] : 0u;
-    cnt[k] = r < P ? g.tiles_touched[vo + gi[k]] : 0u;
-    s.gi[t * GSR_DUP_ITEMS + k] = gi[k];
+    const uint2 tt = r < P ? g.tiles[vo + gi[k]] : make_uint2(0u, 0u);
+    cnt[k] = tt.y ? tt.x : 0u;  // no kept tile: nothing to emit, no rows used
+    const int m = t * GSR_DUP_ITEMS + k;
+    s.gi[m] = gi[k];
     if (cnt[k]) {
-      const uint4 d = g.rec[vo + gi[k]].d;
-      s.rect[t * GSR_DUP_ITEMS + k] = make_uint2(d.x, d.y);
+      const GaussRec& rc = g.rec[vo + gi[k]];
+      const uint4 d = rc.d;
+      const float4 ra = rc.a, rb = rc.b;
+      s.rect[m] = make_uint2(d.x, d.y);
+      s.sp[m] = span_prep(ra.x, ra.y, ra.z, ra.w, rb.x, rb.y);
     } else {
-      s.rect[t * GSR_DUP_ITEMS + k] = make_uint2(0u, 0u);
+      s.rect[m] = make_uint2(0u, 0u);
     }
     sum += cnt[k];
   }
   uint32_t btot;
   const uint32_t local = block_exclusive_scan<256>(sum, &btot, s.wave);
+  // gradient-row slots: rectangle offsets (all of a visible Gaussian's rectangle, kept or not)
   const uint32_t prefix = g.inst_counts[(size_t)v * nbe + lb];
   uint32_t myoff[GSR_DUP_ITEMS];
   {
@@ -125,8 +146,9 @@ __global__ __launch_bounds__(256) void k_emit(int P, int nbe, int grid_x, GeomSt
     }
     if (t == 255) s.off[GSR_DUP_TILE] = btot;
   }
-  uint32_t* kout = keys + inst.start[v] + prefix;
-  uint32_t* vout = vals ? vals + inst.start[v] + prefix : nullptr;
+  uint32_t kbase = g.kept_counts[(size_t)v * nbe + lb];
+  uint32_t* kout = keys + inst.start[v];
+  uint32_t* vout = vals ? vals + inst.start[v] : nullptr;
   for (uint32_t c0 = 0; c0 < btot; c0 += GSR_EMIT_CHUNK) {
 #pragma unroll
     for (int k = 0; k < PER; ++k) s.own[k * 256 + t] = 0u;
@@ -157,31 +179,59 @@ __global__ __launch_bounds__(256) void k_emit(int P, int nbe, int grid_x, GeomSt
     for (int k = 0; k < PER; ++k) s.own[PER * t + k] = max(before, m[k]) - 1u;
     __syncthreads();
     const uint32_t cend = min(btot - c0, (uint32_t)GSR_EMIT_CHUNK);
+    // wave w emits chunk positions [512 w, 512 w + 512), 64 per round; its kept ones are compacted
+    // in order with ballots, the waves' totals are exchanged once
+    uint32_t key[PER], gv[PER], wo[PER], wrun = 0u;
+    bool kp[PER];
 #pragma unroll
     for (int k = 0; k < PER; ++k) {
-      const uint32_t jj = k * 256 + t;
+      const uint32_t jj = (uint32_t)(w * (GSR_EMIT_CHUNK / 4) + k * 64 + lane);
+      kp[k] = false;
+      key[k] = 0u;
+      gv[k] = 0u;
       if (jj < cend) {
         const uint32_t j = c0 + jj;
         const uint32_t ow = s.own[jj];
         const uint2 rc = s.rect[ow];
         const uint32_t xmin = rc.x & 0xffffu, ymin = rc.x >> 16, xmax = rc.y & 0xffffu;
-        const uint32_t w = xmax - xmin, l = j - s.off[ow];
-        // l / w without the ~35-instruction integer division: l < 2^24, so the float quotient is
+        const uint32_t wd = xmax - xmin, l = j - s.off[ow];
+        // l / wd without the ~35-instruction integer division: l < 2^24, so the float quotient is
         // within one of the true one; one correction step makes it exact
-        int ty = (int)((float)l * __builtin_amdgcn_rcpf((float)w));
-        int tx = (int)l - ty * (int)w;
-        if (tx < 0) { --ty; tx += (int)w; }
-        else if (tx >= (int)w) { ++ty; tx -= (int)w; }
-        const uint32_t tile = (ymin + (uint32_t)ty) * (uint32_t)grid_x + xmin + (uint32_t)tx;
-        if (vout) {
-          kout[j] = tile;
-          vout[j] = s.gi[ow];
-        } else {
-          kout[j] = (tile << gbits) | s.gi[ow];
-        }
+        int ty = (int)((float)l * __builtin_amdgcn_rcpf((float)wd));
+        int tx = (int)l - ty * (int)wd;
+        if (tx < 0) { --ty; tx += (int)wd; }
+        else if (tx >= (int)wd) { ++ty; tx -= (int)wd; }
+        const int row = (int)ymin + ty, col = (int)xmin + tx;
+        const SpanPrep sp = s.sp[ow];
+        int t0, t1;
+        span_row(sp, row, (int)xmin, (int)xmax, t0, t1);
+        kp[k] = col >= t0 && col < t1;
+        const uint32_t tile = (uint32_t)row * (uint32_t)grid_x + (uint32_t)col;
+        key[k] = vout ? tile : ((tile << gbits) | s.gi[ow]);
+        gv[k] = s.gi[ow];
+      }
+      const unsigned long long bal = __ballot(kp[k]);
+      wo[k] = wrun + mask_rank(bal);
+      wrun += (uint32_t)__popcll(bal);
+    }
+    if (lane == 0) s.kc[w] = wrun;
+    __syncthreads();
+    uint32_t wbase = 0u, ctot = 0u;
+#pragma unroll
+    for (int ww = 0; ww < 4; ++ww) {
+      const uint32_t c = s.kc[ww];
+      wbase += ww < w ? c : 0u;
+      ctot += c;
+    }
+#pragma unroll
+    for (int k = 0; k < PER; ++k) {
+      if (kp[k]) {
+        const uint32_t o = kbase + wbase + wo[k];
+        kout[o] = key[k];
+        if (vout) vout[o] = gv[k];
       }
     }
-    __syncthreads();
+    kbase += ctot;
   }
 }
 
@@ -193,7 +243,7 @@ __global__ __launch_bounds__(256) void k_tile_ranges(SegInfo inst, int n_tiles, 
   uint32_t lb;
   const int v = seg_of_block(inst, blockIdx.x, lb);
   const uint32_t p0 = (lb * 256 + threadIdx.x) * 4;
-  const uint32_t K = inst.n[v];
+  const uint32_t K = seg_live(inst, v);
   if (p0 >= K) return;
   const uint32_t* kv = keys + inst.start[v];
   uint2* rv = ranges + (size_t)v * n_tiles;

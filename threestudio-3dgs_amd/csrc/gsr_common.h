@@ -19,8 +19,8 @@
 #define GSR_RADIX_BITS 8
 #define GSR_RADIX (1 << GSR_RADIX_BITS)
 // Instance emission: 256 threads x 4 depth-sorted Gaussians per block.
-#define GSR_DUP_ITEMS 4
-#define GSR_DUP_TILE (256 * GSR_DUP_ITEMS)  // 1024
+#define GSR_DUP_ITEMS 2
+#define GSR_DUP_TILE (256 * GSR_DUP_ITEMS)  // 512
 // Tile ranges: 256 threads x 4 instances per block.
 #define GSR_RANGE_TILE 1024
 
@@ -98,13 +98,20 @@ static inline DigitPlan digit_plan(int key_bits) {
 // Segments of a view set (kernel argument): segment v = items [start[v], start[v] + n[v]) of a
 // flat array, cut into blocks of `tile` items; blocks of segment v are [blk[v], blk[v+1]).
 // Item counts of a set stay below 2^32 (checked on the host).
+// n[] is each segment's capacity (it sizes the grid); when ndev is set, the live item count of
+// segment v is ndev[v] (<= n[v], produced on the device: no host round trip).
 struct SegInfo {
   int V, tile;
   uint32_t n[GSR_SET_MAX];
   uint32_t start[GSR_SET_MAX];
   uint32_t blk[GSR_SET_MAX + 1];
+  const uint32_t* ndev = nullptr;
 };
+__device__ __forceinline__ uint32_t seg_live(const SegInfo& s, int v) {
+  return s.ndev ? min(s.ndev[v], s.n[v]) : s.n[v];
+}
 static inline void seg_fill_blocks(SegInfo& s, int tile) {
+  // (ndev is left as set by the caller; SegInfo is otherwise plain data)
   s.tile = tile;
   s.blk[0] = 0;
   for (int v = 0; v < s.V; ++v) s.blk[v + 1] = s.blk[v] + (uint32_t)div_up((long long)s.n[v], tile);
@@ -141,14 +148,18 @@ struct __attribute__((aligned(64))) GaussRec {
 // Per-(view, Gaussian) forward state of a view set ("geom"); element (v, i) at v * P + i.
 struct GeomState {
   GaussRec* rec;
-  uint32_t* tiles_touched;   // instances per Gaussian (0 = culled)
+  uint2* tiles;              // x: tiles of the Gaussian's 3-sigma rectangle (0 = culled): its gradient
+                             // rows; y: of those, tiles its alpha >= 1/255 ellipse reaches (span_row):
+                             // its list instances
   uint32_t* dkey[2];         // depth sort ping-pong keys (float bits of view depth; culled = ~0)
   uint32_t* dval[2];         // depth sort ping-pong values (Gaussian index within the view)
   uint32_t* sort_counts;     // [V][RADIX][sort blocks] per-block digit counts -> scanned offsets
   uint32_t* sort_totals;     // [V][RADIX] digit totals
-  uint32_t* inst_counts;     // [V][emission blocks] instances per block -> scanned offsets
+  uint32_t* inst_counts;     // [V][emission blocks] rectangle tiles per block -> scanned offsets
+  uint32_t* kept_counts;     // [V][emission blocks] kept instances per block -> scanned offsets
   uint32_t* vis_counts;      // [V][emission blocks] visible Gaussians per block
-  uint32_t* counters;        // [0, V) instances K of each view, [V, 2V) visible Gaussians
+  uint32_t* counters;        // [0, V) rectangle tiles K of each view (the reference's num_rendered),
+                             // [V, 2V) visible Gaussians, [2V, 3V) kept list instances
   static int sort_blocks(int P) { return div_up(P > 0 ? P : 1, GSR_SORT_TILE); }
   static int dup_blocks(int P) { return div_up(P > 0 ? P : 1, GSR_DUP_TILE); }
   static GeomState carve(void* base, int V, int P, size_t* bytes) {
@@ -157,7 +168,7 @@ struct GeomState {
     const size_t n = (size_t)(V > 0 ? V : 1) * (size_t)(P > 0 ? P : 1);
     const size_t nv = (size_t)(V > 0 ? V : 1);
     g.rec = c.take<GaussRec>(n);
-    g.tiles_touched = c.take<uint32_t>(n);
+    g.tiles = c.take<uint2>(n);
     g.dkey[0] = c.take<uint32_t>(n);
     g.dkey[1] = c.take<uint32_t>(n);
     g.dval[0] = c.take<uint32_t>(n);
@@ -166,7 +177,8 @@ struct GeomState {
     g.sort_totals = c.take<uint32_t>(nv * GSR_RADIX);
     g.inst_counts = c.take<uint32_t>(nv * dup_blocks(P));
     g.vis_counts = c.take<uint32_t>(nv * dup_blocks(P));
-    g.counters = c.take<uint32_t>(2 * nv + 64);
+    g.kept_counts = c.take<uint32_t>(nv * dup_blocks(P));
+    g.counters = c.take<uint32_t>(3 * nv + 64);
     if (bytes) *bytes = align_up(c.off, 256);
     return g;
   }
@@ -277,6 +289,66 @@ __device__ __forceinline__ float fast_rcp(float x) { return __builtin_amdgcn_rcp
 __device__ __forceinline__ float gauss_power(float a, float b, float c, float dx, float dy) {
   float q = fmaf(c * dy, dy, (a * dx) * dx);
   return fmaf(-0.5f, q, -((b * dx) * dy));
+}
+
+// Tile-level culling of a Gaussian's 3-sigma rectangle (the reference bins every rectangle tile).
+// Tiles of row ty (pixel rows 16 ty .. 16 ty + 15) that contain a pixel with alpha >= 1/255:
+// [tx0, tx1) within [xmin, xmax).  A pixel contributes only if o exp(-Q/2) >= 1/255 with
+// Q = d^T conic d, d = mean - pixel, i.e. Q <= thr = 2 ln(255 o): the u = mean_x - x extent of
+// that ellipse within the row band v = mean_y - y in [v1 - 15, v1] is [umin, umax] (the ellipse's
+// own x-extreme (+-ue, -+ve) when it lies in the band, else where it crosses a band edge v_e:
+// u = (-b v_e +- sqrt(thr a - D v_e^2)) / a, D = ac - b^2).  The bound is widened (threshold and
+// extent margins) so rounding never drops a contributing tile; dropped tiles hold only pixels
+// every blend step skips, so images and gradients are unchanged.  Every kernel that enumerates
+// instances runs this same code (contraction off): the preprocess count, the emission and the
+// gradient gather agree exactly.
+struct SpanPrep {
+  float px, py, b, D, ia, thra, ue, ve;
+  int mode;  // 0: no tile, 1: every rectangle tile (degenerate conic), 2: ellipse
+};
+__device__ __forceinline__ SpanPrep span_prep(float px, float py, float a, float b, float c, float o) {
+#pragma clang fp contract(off)
+  SpanPrep p;
+  p.px = px;
+  p.py = py;
+  p.b = b;
+  p.D = a * c - b * b;
+  p.mode = !(o >= GSR_ALPHA_MIN * 0.9999f) ? 0 : !(a > 0.0f && c > 0.0f && p.D > 0.0f) ? 1 : 2;
+  const float tau = fmaxf(0.0f, __logf(255.0f * o));
+  const float thr = 2.0f * (tau * 1.002f + 2e-3f);
+  p.ia = __builtin_amdgcn_rcpf(a);
+  p.thra = thr * a;
+  p.ue = __builtin_amdgcn_sqrtf(thr * c * __builtin_amdgcn_rcpf(p.D));
+  p.ve = b * p.ue * __builtin_amdgcn_rcpf(c);
+  return p;
+}
+__device__ __forceinline__ void span_row(const SpanPrep& p, int ty, int xmin, int xmax, int& tx0, int& tx1) {
+#pragma clang fp contract(off)
+  tx0 = xmin;
+  tx1 = p.mode == 1 ? xmax : xmin;
+  if (p.mode != 2) return;
+  const float v1 = p.py - (float)(ty * GSR_TILE_Y), v0 = v1 - (float)(GSR_TILE_Y - 1);
+  float umax = -3.0e38f, umin = 3.0e38f;
+  if (-p.ve >= v0 && -p.ve <= v1) umax = p.ue;
+  if (p.ve >= v0 && p.ve <= v1) umin = -p.ue;
+  const float e0 = p.thra - p.D * (v0 * v0), e1 = p.thra - p.D * (v1 * v1);
+  if (e0 >= 0.0f) {
+    const float r = __builtin_amdgcn_sqrtf(e0), m = -p.b * v0;
+    umax = fmaxf(umax, (m + r) * p.ia);
+    umin = fminf(umin, (m - r) * p.ia);
+  }
+  if (e1 >= 0.0f) {
+    const float r = __builtin_amdgcn_sqrtf(e1), m = -p.b * v1;
+    umax = fmaxf(umax, (m + r) * p.ia);
+    umin = fminf(umin, (m - r) * p.ia);
+  }
+  if (!(umax >= umin)) return;  // the ellipse misses the band
+  // pixel x in [16 tx, 16 tx + 15] has u in [px - 16 tx - 15, px - 16 tx]
+  const float lo = fminf(fmaxf((p.px - (float)(GSR_TILE_X - 1) - umax - 0.05f) * (1.0f / GSR_TILE_X), -1.0e6f), 1.0e6f);
+  const float hi = fminf(fmaxf((p.px - umin + 0.05f) * (1.0f / GSR_TILE_X), -1.0e6f), 1.0e6f);
+  const int a0 = (int)ceilf(lo), a1 = (int)floorf(hi) + 1;
+  tx0 = max(xmin, min(a0, xmax));
+  tx1 = max(tx0, min(a1, xmax));
 }
 
 }  // namespace gsr

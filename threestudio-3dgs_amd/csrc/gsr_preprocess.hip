@@ -21,7 +21,7 @@ __global__ __launch_bounds__(256) void k_preprocess(PreprocessArgs a, SetCams ca
   const ViewCam cam = cams.c[v];
   const size_t vi = (size_t)v * a.P + idx;
   a.radii[vi] = 0;
-  g.tiles_touched[vi] = 0;
+  g.tiles[vi] = make_uint2(0u, 0u);
   g.dkey[0][vi] = 0xFFFFFFFFu;
   const float* viewmatrix = cam.view;
   const float* projmatrix = cam.proj;
@@ -87,7 +87,14 @@ __global__ __launch_bounds__(256) void k_preprocess(PreprocessArgs a, SetCams ca
   rec.d = make_uint4((uint32_t)xmin | ((uint32_t)ymin << 16), (uint32_t)xmax | ((uint32_t)ymax << 16), 0u, clamp_bits);
   g.rec[vi] = rec;
   a.radii[vi] = r;
-  g.tiles_touched[vi] = (uint32_t)area;
+  uint32_t kept = 0;
+  const SpanPrep sp = span_prep(rec.a.x, rec.a.y, rec.a.z, rec.a.w, rec.b.x, rec.b.y);
+  for (int ty = ymin; ty < ymax; ++ty) {
+    int t0, t1;
+    span_row(sp, ty, xmin, xmax, t0, t1);
+    kept += (uint32_t)(t1 - t0);
+  }
+  g.tiles[vi] = make_uint2((uint32_t)area, kept);
   g.dkey[0][vi] = __float_as_uint(p_view.z);  // > 0.2: float bits are monotone in depth
 }
 

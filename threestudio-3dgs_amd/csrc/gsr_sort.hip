@@ -28,7 +28,7 @@ __global__ __launch_bounds__(GSR_SORT_THREADS) void k_seg_count(const uint32_t* 
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
   uint32_t lb;
   const int v = seg_of_block(seg, blockIdx.x, lb);
-  const uint32_t n = seg.n[v];
+  const uint32_t n = seg_live(seg, v);
   const uint32_t* src = keys + seg.start[v];
   const uint32_t mask = (1u << bits) - 1u;
   const int R = 1 << bits;
@@ -106,7 +106,7 @@ __global__ __launch_bounds__(GSR_SORT_THREADS) void k_seg_scatter(
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
   uint32_t lb;
   const int v = seg_of_block(seg, blockIdx.x, lb);
-  const uint32_t n = seg.n[v];
+  const uint32_t n = seg_live(seg, v);
   const uint32_t start = seg.start[v];
   const uint32_t mask = (1u << bits) - 1u;
   const int R = 1 << bits;
@@ -167,7 +167,7 @@ __global__ __launch_bounds__(GSR_SORT_THREADS) void k_seg_scatter(
     }
   }
   __syncthreads();
-  const uint32_t nv = min((uint32_t)GSR_SORT_TILE, n - lb * GSR_SORT_TILE);
+  const uint32_t nv = lb * GSR_SORT_TILE < n ? min((uint32_t)GSR_SORT_TILE, n - lb * GSR_SORT_TILE) : 0u;
 #pragma unroll
   for (int k = 0; k < GSR_SORT_ITEMS; ++k) {
     const uint32_t j = k * GSR_SORT_THREADS + t;
