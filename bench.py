@@ -5,8 +5,9 @@ A step is one pass of the hot path over one batch of views: every view of the ba
 through the drop-in GaussianRasterizer API (preprocess, binning, forward blend), composited on a
 constant background exactly like renderer/diff_gaussian_rasterizer_background.py:129-132, the
 rendered images are all-gathered across ranks (RCCL over xGMI; the north_star exchange), then the
-backward of a seeded synthetic loss runs through the rasterizer and the per-Gaussian parameter
-gradients are all-reduced (sum) so every replica holds the full-batch gradient.
+backward runs from fixed seeded upstream gradients dL/d(image, depth, alpha) (a loss's gradient,
+injected with torch.autograd.backward) through the composite and the rasterizer, and the
+per-Gaussian parameter gradients are all-reduced (sum) so every replica holds the full-batch gradient.
 
 Workload (BASELINE.json configs[2] / configs[3]): C3 per view (1M Gaussians, 1024^2,
 SH3, background path: bg = 0 + constant composite) over the C4 64-view MVDream-style orbit batch
@@ -219,14 +220,13 @@ def main():
             if world > 1:
                 # forward exchange: every rank receives the whole batch of rendered images
                 all_gather_views(torch.cat([c, d, a], 1), args.views)
-            loss = (c * up_c).sum() + (d * up_d).sum() + (a * up_a).sum()
+            # the loss's gradient w.r.t. the rendered images is injected as fixed upstream gradients
+            torch.autograd.backward((c, d, a), (up_c, up_d, up_a))
         else:
             outs = [render_view(rep, cam, bg_zero, bg_const) for cam in mine]
             if world > 1:
                 all_gather_views(torch.stack([torch.cat([c, d, a], 0) for c, d, a, _ in outs]), args.views)
-            loss = sum((c * g[0]).sum() + (d * g[1]).sum() + (a * g[2]).sum()
-                       for (c, d, a, _), g in zip(outs, upstream))
-        loss.backward()
+            torch.autograd.backward([t for c, d, a, _ in outs for t in (c, d, a)], [t for g in upstream for t in g])
         allreduce_grads(rep.params)  # one flat RCCL all-reduce of the Gaussian parameter gradients
         rep.zero_grad()
 
@@ -281,7 +281,8 @@ def main():
         "data": "synthetic (seeded scene per SURVEY.md §8d; no datasets offline)",
         "config": {
             "workload": "C3 per view (1M Gaussians, 1024x1024, SH3, background path) over the C4 64-view "
-                        "orbit batch, fwd+bwd + image all-gather + gradient all-reduce",
+                        "orbit batch, fwd+bwd (fixed random upstream image gradients) + image all-gather + "
+                        "gradient all-reduce",
             "n_gaussians": args.gaussians, "resolution": [H, W], "sh_degree": args.sh_degree,
             "global_views_per_step": args.views, "views_per_rank": per,
             "parallelism": f"views sharded over {world} rank(s) (RCCL all-gather images, all-reduce grads)",
