@@ -49,6 +49,7 @@ def summarise(tl, name):
         "occupancy_profile_10": [int(np.mean(occ[i * 10:(i + 1) * 10])) for i in range(10)],
         "time_frac_below_512_blocks": float(np.mean(np.array(occ) < 512)),
         # bwd only: z = sum over batches of 4 x the busiest quadrant's kept count -> lockstep slots per kept pair
+        "work_sum": int(work.astype(np.int64).sum()),
         "bwd_lockstep_slots_per_pair": (float(tl[:, 2].astype(np.float64).sum() / max(1, work.sum()))
                                         if name == "k_render_bwd" else None),
     }

@@ -95,7 +95,7 @@ struct DupLDS {
   uint32_t gi[GSR_DUP_TILE];
   uint2 rect[GSR_DUP_TILE];
   SpanPrep sp[GSR_DUP_TILE];  // tile culling of each Gaussian (span_row)
-  uint32_t own[GSR_EMIT_CHUNK];
+  alignas(16) uint32_t own[GSR_EMIT_CHUNK];
   uint32_t kc[4];  // kept positions per wave of the chunk
   uint32_t wave[8];
   uint32_t carry;
@@ -167,16 +167,22 @@ __global__ __launch_bounds__(256) void k_emit(int P, int nbe, int grid_x, GeomSt
     for (int k = 0; k < GSR_DUP_ITEMS; ++k)
       if (cnt[k] && myoff[k] >= c0 && myoff[k] < c0 + GSR_EMIT_CHUNK) s.own[myoff[k] - c0] = (uint32_t)(t * GSR_DUP_ITEMS + k) + 1u;
     __syncthreads();
-    // max-scan of the marks: thread t owns positions [PER t, PER t + PER)
-    uint32_t m[PER], run = 0u;
+    // max-scan of the marks: thread t owns positions [PER t, PER t + PER) (16-byte LDS accesses)
+    static_assert(PER == 8, "two uint4 per thread");
+    uint4* own4 = reinterpret_cast<uint4*>(s.own) + 2 * t;
+    const uint4 o0 = own4[0], o1 = own4[1];
+    uint32_t m[PER] = {o0.x, o0.y, o0.z, o0.w, o1.x, o1.y, o1.z, o1.w};
+    uint32_t run = 0u;
 #pragma unroll
     for (int k = 0; k < PER; ++k) {
-      run = max(run, s.own[PER * t + k]);
+      run = max(run, m[k]);
       m[k] = run;
     }
     const uint32_t before = max(s.carry, block_exclusive_max<256>(run, s.wave));
 #pragma unroll
-    for (int k = 0; k < PER; ++k) s.own[PER * t + k] = max(before, m[k]) - 1u;
+    for (int k = 0; k < PER; ++k) m[k] = max(before, m[k]) - 1u;
+    own4[0] = make_uint4(m[0], m[1], m[2], m[3]);
+    own4[1] = make_uint4(m[4], m[5], m[6], m[7]);
     __syncthreads();
     const uint32_t cend = min(btot - c0, (uint32_t)GSR_EMIT_CHUNK);
     // wave w emits chunk positions [512 w, 512 w + 512), 64 per round; its kept ones are compacted

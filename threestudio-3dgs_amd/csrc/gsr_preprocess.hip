@@ -3,39 +3,51 @@
 // Replaces FORWARD::preprocessCUDA of the reference rasterizer [EXT]: frustum cull
 // (view z <= 0.2), projection, 3D covariance, EWA 2D covariance (+0.3 low-pass), conic,
 // 3-sigma radius, 16x16 tile rect, SH -> RGB (clamped at 0, flags kept for backward).
-// One thread per (view, Gaussian) of a view set.  Blocks are dealt view-fastest (block b ->
-// view b % V, Gaussians 256 (b / V) ...), so the V views of one 256-Gaussian slice run together
-// and its parameters (44 + 12*M bytes per Gaussian) are fetched from HBM once per set and served
-// from L2 / MALL for the other views.  Writes per (view, Gaussian) the 48-byte render record,
-// the 8-byte tile rect, radius, clamp flags, instance count and the depth-sort key (culled: ~0,
-// which sorts after every visible depth).
+// A block owns 256 Gaussians (one per thread) for up to GSR_PRE_VIEWS views of the set: the
+// Gaussians' parameters are read once per block (SH staged through LDS with coalesced 16-byte loads
+// instead of 3M strided dword loads per thread), the 3D covariance is built once, and the views
+// are walked in turn.  Writes per (view, Gaussian) the 64-byte render record (incl. tile rect and
+// clamp flags), radius, rectangle / kept tile counts and the depth-sort key (culled: ~0, which
+// sorts after every visible depth).
 #include "gsr_kernels.h"
 #include "gsr_math.h"
 
 namespace gsr {
 
+// Views handled by one block (the Gaussians' view-independent work and SH staging are shared).
+#define GSR_PRE_VIEWS 8
+#define GSR_PRE_LDS_FLOATS (16 * 1024)  // SH staging up to 64 KB (M <= 21); larger M reads SH from HBM
+
 __global__ __launch_bounds__(256) void k_preprocess(PreprocessArgs a, SetCams cams, GeomState g) {
-  const int v = blockIdx.x % a.V;
-  const int idx = (blockIdx.x / a.V) * blockDim.x + threadIdx.x;
+  extern __shared__ float s_sh[];  // [256][3M + 1] this block's SH coefficients (odd stride)
+  const int nvc = (a.V + GSR_PRE_VIEWS - 1) / GSR_PRE_VIEWS;
+  const int vc = blockIdx.x % nvc;
+  const int idx0 = (blockIdx.x / nvc) * 256;
+  const int t = threadIdx.x;
+  const int idx = idx0 + t;
+  const int v0 = vc * GSR_PRE_VIEWS, v1 = min(a.V, v0 + GSR_PRE_VIEWS);
+  const int nsh = a.colors_precomp == nullptr ? 3 * a.M : 0;
+  const int sstride = nsh + 1;
+  const bool staged = nsh > 0 && 256 * sstride <= GSR_PRE_LDS_FLOATS;
+  if (staged) {
+    // coalesced 16-byte loads of the block's contiguous SH slice (256 * 3M floats, 16-B aligned)
+    const int n = min(256, a.P - idx0) * nsh;
+    const float4* src = reinterpret_cast<const float4*>(a.shs + (size_t)idx0 * nsh);
+    for (int e4 = t; e4 * 4 < n; e4 += 256) {
+      const float4 q = src[e4];
+      const float qv[4] = {q.x, q.y, q.z, q.w};
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const int e = 4 * e4 + k;
+        if (e < n) s_sh[(e / nsh) * sstride + e % nsh] = qv[k];
+      }
+    }
+    __syncthreads();
+  }
   if (idx >= a.P) return;
-  const ViewCam cam = cams.c[v];
-  const size_t vi = (size_t)v * a.P + idx;
-  a.radii[vi] = 0;
-  g.tiles[vi] = make_uint2(0u, 0u);
-  g.dkey[0][vi] = 0xFFFFFFFFu;
-  const float* viewmatrix = cam.view;
-  const float* projmatrix = cam.proj;
-  const float tanfovx = cam.tanx, tanfovy = cam.tany;
-  const float focal_x = a.W / (2.0f * tanfovx), focal_y = a.H / (2.0f * tanfovy);
 
+  // view-independent: position, 3D covariance, opacity, precomputed colour
   const float3 p_orig = make_float3(a.means3D[3 * idx], a.means3D[3 * idx + 1], a.means3D[3 * idx + 2]);
-  // near-plane cull on the view-space depth (in_frustum of the reference)
-  const float3 p_view = xform_point4x3(p_orig, viewmatrix);
-  if (p_view.z <= GSR_NEAR_CULL) return;
-  const float4 p_hom = xform_point4x4(p_orig, projmatrix);
-  const float p_w = 1.0f / (p_hom.w + 0.0000001f);
-  const float3 p_proj = make_float3(p_hom.x * p_w, p_hom.y * p_w, p_hom.z * p_w);
-
   float cov3D[6];
   if (a.cov3D_precomp != nullptr) {
 #pragma unroll
@@ -46,61 +58,87 @@ __global__ __launch_bounds__(256) void k_preprocess(PreprocessArgs a, SetCams ca
                                  a.rotations[4 * idx + 2], a.rotations[4 * idx + 3]);
     cov3d_from_scale_rot(s, a.scale_modifier, q, cov3D);
   }
-
-  Cov2DState st;
-  const float3 cov = cov2d_ewa(p_orig, focal_x, focal_y, tanfovx, tanfovy, cov3D, viewmatrix, st);
-  const float det = cov.x * cov.z - cov.y * cov.y;
-  if (det == 0.0f) return;
-  const float det_inv = 1.f / det;
-  const float3 conic = make_float3(cov.z * det_inv, -cov.y * det_inv, cov.x * det_inv);
-
-  const float mid = 0.5f * (cov.x + cov.z);
-  const float lambda1 = mid + sqrtf(fmaxf(0.1f, mid * mid - det));
-  const float lambda2 = mid - sqrtf(fmaxf(0.1f, mid * mid - det));
-  const float my_radius = ceilf(3.f * sqrtf(fmaxf(lambda1, lambda2)));
-  const float2 pimg = make_float2(ndc2pix(p_proj.x, a.W), ndc2pix(p_proj.y, a.H));
-
-  // tile rect [min, max) clamped to the grid (getRect of the reference)
+  const float opacity = a.opacities[idx];
+  float3 rgb_pre = make_float3(0.f, 0.f, 0.f);
+  if (a.colors_precomp != nullptr)
+    rgb_pre = make_float3(a.colors_precomp[3 * idx], a.colors_precomp[3 * idx + 1], a.colors_precomp[3 * idx + 2]);
+  const float* my_sh = staged ? s_sh + t * sstride : a.shs + (size_t)idx * nsh;
   const int gx = (a.W + GSR_TILE_X - 1) / GSR_TILE_X;
   const int gy = (a.H + GSR_TILE_Y - 1) / GSR_TILE_Y;
-  const int r = (int)my_radius;
-  const int xmin = min(gx, max(0, (int)((pimg.x - r) / GSR_TILE_X)));
-  const int ymin = min(gy, max(0, (int)((pimg.y - r) / GSR_TILE_Y)));
-  const int xmax = min(gx, max(0, (int)((pimg.x + r + GSR_TILE_X - 1) / GSR_TILE_X)));
-  const int ymax = min(gy, max(0, (int)((pimg.y + r + GSR_TILE_Y - 1) / GSR_TILE_Y)));
-  const int area = (xmax - xmin) * (ymax - ymin);
-  if (area == 0) return;
 
-  float3 rgb;
-  uint32_t clamp_bits = 0;
-  if (a.colors_precomp != nullptr) {
-    rgb = make_float3(a.colors_precomp[3 * idx], a.colors_precomp[3 * idx + 1], a.colors_precomp[3 * idx + 2]);
-  } else {
-    rgb = sh_to_rgb(a.deg, a.shs + (size_t)idx * a.M * 3, p_orig,
-                    make_float3(cam.campos[0], cam.campos[1], cam.campos[2]), &clamp_bits);
+#pragma unroll 1
+  for (int v = v0; v < v1; ++v) {
+    const ViewCam cam = cams.c[v];
+    const size_t vi = (size_t)v * a.P + idx;
+    const float* viewmatrix = cam.view;
+    const float* projmatrix = cam.proj;
+    const float tanfovx = cam.tanx, tanfovy = cam.tany;
+    const float focal_x = a.W / (2.0f * tanfovx), focal_y = a.H / (2.0f * tanfovy);
+    int radius = 0;
+    uint2 tiles = make_uint2(0u, 0u);
+    uint32_t dkey = 0xFFFFFFFFu;  // culled: sorts after every visible depth
+    // near-plane cull on the view-space depth (in_frustum of the reference)
+    const float3 p_view = xform_point4x3(p_orig, viewmatrix);
+    if (p_view.z > GSR_NEAR_CULL) {
+      const float4 p_hom = xform_point4x4(p_orig, projmatrix);
+      const float p_w = 1.0f / (p_hom.w + 0.0000001f);
+      const float3 p_proj = make_float3(p_hom.x * p_w, p_hom.y * p_w, p_hom.z * p_w);
+      Cov2DState st;
+      const float3 cov = cov2d_ewa(p_orig, focal_x, focal_y, tanfovx, tanfovy, cov3D, viewmatrix, st);
+      const float det = cov.x * cov.z - cov.y * cov.y;
+      if (det != 0.0f) {
+        const float det_inv = 1.f / det;
+        const float3 conic = make_float3(cov.z * det_inv, -cov.y * det_inv, cov.x * det_inv);
+        const float mid = 0.5f * (cov.x + cov.z);
+        const float lambda1 = mid + sqrtf(fmaxf(0.1f, mid * mid - det));
+        const float lambda2 = mid - sqrtf(fmaxf(0.1f, mid * mid - det));
+        const float my_radius = ceilf(3.f * sqrtf(fmaxf(lambda1, lambda2)));
+        const float2 pimg = make_float2(ndc2pix(p_proj.x, a.W), ndc2pix(p_proj.y, a.H));
+        // tile rect [min, max) clamped to the grid (getRect of the reference)
+        const int r = (int)my_radius;
+        const int xmin = min(gx, max(0, (int)((pimg.x - r) / GSR_TILE_X)));
+        const int ymin = min(gy, max(0, (int)((pimg.y - r) / GSR_TILE_Y)));
+        const int xmax = min(gx, max(0, (int)((pimg.x + r + GSR_TILE_X - 1) / GSR_TILE_X)));
+        const int ymax = min(gy, max(0, (int)((pimg.y + r + GSR_TILE_Y - 1) / GSR_TILE_Y)));
+        const int area = (xmax - xmin) * (ymax - ymin);
+        if (area != 0) {
+          float3 rgb = rgb_pre;
+          uint32_t clamp_bits = 0;
+          if (a.colors_precomp == nullptr)
+            rgb = sh_to_rgb(a.deg, my_sh, p_orig, make_float3(cam.campos[0], cam.campos[1], cam.campos[2]),
+                            &clamp_bits);
+          GaussRec rec;
+          rec.a = make_float4(pimg.x, pimg.y, conic.x, conic.y);
+          rec.b = make_float4(conic.z, opacity, p_view.z, 0.0f);
+          rec.c = make_float4(rgb.x, rgb.y, rgb.z, 0.0f);
+          rec.d = make_uint4((uint32_t)xmin | ((uint32_t)ymin << 16), (uint32_t)xmax | ((uint32_t)ymax << 16), 0u,
+                             clamp_bits);
+          g.rec[vi] = rec;
+          radius = r;
+          uint32_t kept = 0;
+          const SpanPrep sp = span_prep(rec.a.x, rec.a.y, rec.a.z, rec.a.w, rec.b.x, rec.b.y);
+          for (int ty = ymin; ty < ymax; ++ty) {
+            int t0, t1;
+            span_row(sp, ty, xmin, xmax, t0, t1);
+            kept += (uint32_t)(t1 - t0);
+          }
+          tiles = make_uint2((uint32_t)area, kept);
+          dkey = __float_as_uint(p_view.z);  // > 0.2: float bits are monotone in depth
+        }
+      }
+    }
+    a.radii[vi] = radius;
+    g.tiles[vi] = tiles;
+    g.dkey[0][vi] = dkey;
   }
-
-  GaussRec rec;
-  rec.a = make_float4(pimg.x, pimg.y, conic.x, conic.y);
-  rec.b = make_float4(conic.z, a.opacities[idx], p_view.z, 0.0f);
-  rec.c = make_float4(rgb.x, rgb.y, rgb.z, 0.0f);
-  rec.d = make_uint4((uint32_t)xmin | ((uint32_t)ymin << 16), (uint32_t)xmax | ((uint32_t)ymax << 16), 0u, clamp_bits);
-  g.rec[vi] = rec;
-  a.radii[vi] = r;
-  uint32_t kept = 0;
-  const SpanPrep sp = span_prep(rec.a.x, rec.a.y, rec.a.z, rec.a.w, rec.b.x, rec.b.y);
-  for (int ty = ymin; ty < ymax; ++ty) {
-    int t0, t1;
-    span_row(sp, ty, xmin, xmax, t0, t1);
-    kept += (uint32_t)(t1 - t0);
-  }
-  g.tiles[vi] = make_uint2((uint32_t)area, kept);
-  g.dkey[0][vi] = __float_as_uint(p_view.z);  // > 0.2: float bits are monotone in depth
 }
 
 void launch_preprocess(const PreprocessArgs& a, const SetCams& cams, const GeomState& g, hipStream_t stream) {
   if (a.P <= 0 || a.V <= 0) return;
-  hipLaunchKernelGGL(k_preprocess, dim3(a.V * ((a.P + 255) / 256)), dim3(256), 0, stream, a, cams, g);
+  const int nvc = (a.V + GSR_PRE_VIEWS - 1) / GSR_PRE_VIEWS;
+  const size_t want = a.colors_precomp == nullptr ? (size_t)256 * (3 * a.M + 1) : 0;
+  const size_t lds = want <= GSR_PRE_LDS_FLOATS ? sizeof(float) * want : 0;
+  hipLaunchKernelGGL(k_preprocess, dim3(nvc * ((a.P + 255) / 256)), dim3(256), lds, stream, a, cams, g);
 }
 
 }  // namespace gsr

@@ -302,6 +302,7 @@ struct BwdLDS {
   float uw[4][64 * 16];
   // per wave: the B operand's dL/d(r, g, b, depth) rows, [4][68] (padded) + a row of zeros
   float dp[4][4 * 68 + 16];
+  unsigned long long kmask[4];  // per quadrant: kept candidates of the batch
 #ifdef GSR_TIMELINE
   int tl_cnt[4];
 #endif
@@ -397,23 +398,20 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 8))) voi
   const float ddelx_dx = 0.5f * W, ddely_dy = 0.5f * H;
   const float4 zero4 = make_float4(0.f, 0.f, 0.f, 0.f);
 
-  // wave 0 stages the batches; two-stage prefetch (indices two batches ahead, records one ahead)
+  // All 256 threads stage the batches: thread t moves 16-byte piece (t & 3) of candidate t >> 2's
+  // 64-byte record (4 lanes read one line: coalesced).  Two-stage prefetch: indices two batches
+  // ahead, record pieces one ahead.
   const uint32_t gmask = rs.gmask;
+  const int cs = t >> 2, piece = t & 3;
   auto fetch_index = [&](int h) -> uint32_t {
-    const int r = h - 1 - lane;
+    const int r = h - 1 - cs;
     return r >= 0 ? (sorted_gauss[range.x + r] & gmask) : 0u;
   };
-  float4 n0 = zero4, n1 = zero4, n2 = zero4;
-  uint4 nd = make_uint4(0u, 0u, 0u, 0u);
+  float4 npc = zero4;  // the next batch's piece
   uint32_t gi_next = 0u;
-  if (q == 0 && maxc > 0) {
+  if (maxc > 0) {
     const uint32_t g0 = fetch_index(maxc);
-    if (maxc - 1 - lane >= 0) {
-      n0 = rec[g0].a;
-      n1 = rec[g0].b;
-      n2 = rec[g0].c;
-      nd = rec[g0].d;
-    }
+    if (maxc - 1 - cs >= 0) npc = reinterpret_cast<const float4*>(rec + g0)[piece];
     if (maxc > 64) gi_next = fetch_index(maxc - 64);
   }
 
@@ -485,22 +483,23 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 8))) voi
   uint32_t* mylist = s.list[q];
   float* myq = s.qsum + q * NGV;
   for (int hi = maxc; hi > 0; hi -= 64) {
-    if (q == 0) {
-      const int rel_l = hi - 1 - lane;
-      if (rel_l >= 0) {
-        const int xmin = nd.x & 0xffff, ymin = nd.x >> 16, xmax = nd.y & 0xffff;
-        s.s0[lane] = n0;
-        s.s1[lane] = make_float4(n1.x, n1.y, n1.z, __uint_as_float((uint32_t)rel_l));  // .w: list position
-        s.s2[lane] = n2;
-        s.slot[lane] = nd.z + (uint32_t)((tyi - ymin) * (xmax - xmin) + (txi - xmin));
+    {
+      const int rel_c = hi - 1 - cs;
+      if (rel_c >= 0) {
+        if (piece == 0) {
+          s.s0[cs] = npc;
+        } else if (piece == 1) {
+          s.s1[cs] = make_float4(npc.x, npc.y, npc.z, __uint_as_float((uint32_t)rel_c));  // .w: list position
+        } else if (piece == 2) {
+          s.s2[cs] = npc;
+        } else {
+          const uint32_t dx_ = __float_as_uint(npc.x), dy_ = __float_as_uint(npc.y), dz_ = __float_as_uint(npc.z);
+          const int xmin = dx_ & 0xffff, ymin = dx_ >> 16, xmax = dy_ & 0xffff;
+          s.slot[cs] = dz_ + (uint32_t)((tyi - ymin) * (xmax - xmin) + (txi - xmin));
+        }
       }
       if (hi > 64) {
-        if (hi - 65 - lane >= 0) {
-          n0 = rec[gi_next].a;
-          n1 = rec[gi_next].b;
-          n2 = rec[gi_next].c;
-          nd = rec[gi_next].d;
-        }
+        if (hi - 65 - cs >= 0) npc = reinterpret_cast<const float4*>(rec + gi_next)[piece];
         if (hi > 128) gi_next = fetch_index(hi - 128);
       }
     }
@@ -508,14 +507,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 8))) voi
     // this wave's quadrant: cull the staged batch, list the kept candidates, zero the others' sums
     const int rel_l = hi - 1 - lane;
     bool keep = false;
+#ifdef GSR_EXP_NOCULL
+    if (rel_l >= 0 && rel_l < qmaxc) keep = s.s0[lane].x > -1e30f;
+#else
     if (rel_l >= 0 && rel_l < qmaxc) keep = quadrant_hit(s.s0[lane], s.s1[lane], (float)qx0, (float)qy0);
-    if (rel_l >= 0 && !keep) {
-      float* z = myq + lane * GSR_QSUM_STRIDE;
-#pragma unroll
-      for (int i = 0; i < NGV; ++i) z[i] = 0.f;
-    }
+#endif
     const unsigned long long bal = __ballot(keep);
     const int cnt = __popcll(bal);
+    if (lane == 0) s.kmask[q] = bal;  // the flush reads this quadrant's sums of kept candidates only
 #ifdef GSR_TIMELINE
     if (lane == 0) s.tl_cnt[q] = cnt;
 #endif
@@ -525,6 +524,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 8))) voi
     // The kept set is the uniform ballot mask: walk it with scalar bit scans, prefetching the next
     // candidate's staged record while the current one is replayed.
     unsigned long long rest = bal;
+#ifdef GSR_EXP_NOGROUP
+    if (cnt < 0)
+#endif
     for (int g0 = 0; g0 < cnt; g0 += 8) {
       const int gn = min(8, cnt - g0);
       int j = (int)__builtin_ctzll(rest);
@@ -593,38 +595,47 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 8))) voi
       tl_max += 4 * max(max(c0, c1), max(c2, c3));                  // lockstep cost in pair slots
     }
 #endif
-    if (t < 64 && hi - 1 - t >= 0) {
-      // one thread per candidate: per quadrant, turn the sums over quadrant-local pixel coordinates
-      // into the moments of u over dx = mean - pixel (dx = mx' - x with mx' = mean - quadrant origin),
-      // add the 4 quadrants, and form the reference's terms
+    if (hi - 1 - cs >= 0) {
+      // four threads per candidate (t = 4 c + quadrant): per quadrant, turn the sums over quadrant-
+      // local pixel coordinates into the moments of u over dx = mean - pixel (dx = mx' - x with
+      // mx' = mean - quadrant origin); add the 4 quadrants (quad DPP); form the reference's terms
       //   dmean2D = -o (W/2, H/2) (a m1 + b m2, c m2 + b m1), dconic = -o/2 (m3, m4, m5), dopacity = m0
-      const float* qs = s.qsum + t * GSR_QSUM_STRIDE;
-      const float4 ga = s.s0[t];
-      const float4 gb = s.s1[t];
+      // and write the 48-byte row, one 16-byte piece per thread.
+      const int qq = piece;
+      const float4 ga = s.s0[cs];
+      const float4 gb = s.s1[cs];
       float m[NGV] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-      for (int qq = 0; qq < 4; ++qq) {
-        const float* C = qs + NGV * qq;
+      if ((s.kmask[qq] >> cs) & 1ull) {
+        const float* C = s.qsum + cs * GSR_QSUM_STRIDE + NGV * qq;
         const float mx = ga.x - (float)(txi * GSR_TILE_X + (qq & 1) * 8);
         const float my = ga.y - (float)(tyi * GSR_TILE_Y + (qq >> 1) * 8);
-        m[0] += C[0];
-        m[1] += mx * C[0] - C[1];
-        m[2] += my * C[0] - C[2];
-        m[3] += mx * (mx * C[0] - 2.f * C[1]) + C[3];
-        m[4] += mx * (my * C[0] - C[2]) - my * C[1] + C[4];
-        m[5] += my * (my * C[0] - 2.f * C[2]) + C[5];
-        m[6] += C[6];
-        m[7] += C[7];
-        m[8] += C[8];
-        m[9] += C[9];
+        m[0] = C[0];
+        m[1] = mx * C[0] - C[1];
+        m[2] = my * C[0] - C[2];
+        m[3] = mx * (mx * C[0] - 2.f * C[1]) + C[3];
+        m[4] = mx * (my * C[0] - C[2]) - my * C[1] + C[4];
+        m[5] = my * (my * C[0] - 2.f * C[2]) + C[5];
+        m[6] = C[6];
+        m[7] = C[7];
+        m[8] = C[8];
+        m[9] = C[9];
+      }
+#pragma unroll
+      for (int i = 0; i < NGV; ++i) {
+        m[i] += dpp_f32<0xB1>(m[i]);  // quad_perm [1,0,3,2]
+        m[i] += dpp_f32<0x4E>(m[i]);  // quad_perm [2,3,0,1]
       }
       const float o = gb.y;
-      const float dmx = -o * ddelx_dx * (ga.z * m[1] + ga.w * m[2]);
-      const float dmy = -o * ddely_dy * (gb.x * m[2] + ga.w * m[1]);
-      float4* row = grow + 3 * (size_t)s.slot[t];
-      row[0] = make_float4(dmx, dmy, -0.5f * o * m[3], -0.5f * o * m[4]);
-      row[1] = make_float4(-0.5f * o * m[5], m[0], m[6], m[7]);
-      row[2] = make_float4(m[8], m[9], 0.f, 0.f);
+      float4* row = grow + 3 * (size_t)s.slot[cs];
+      if (qq == 0) {
+        const float dmx = -o * ddelx_dx * (ga.z * m[1] + ga.w * m[2]);
+        const float dmy = -o * ddely_dy * (gb.x * m[2] + ga.w * m[1]);
+        row[0] = make_float4(dmx, dmy, -0.5f * o * m[3], -0.5f * o * m[4]);
+      } else if (qq == 1) {
+        row[1] = make_float4(-0.5f * o * m[5], m[0], m[6], m[7]);
+      } else if (qq == 2) {
+        row[2] = make_float4(m[8], m[9], 0.f, 0.f);
+      }
     }
     __syncthreads();
   }
