@@ -234,6 +234,7 @@ def main():
         step()
     torch.cuda.synchronize()
     _C.RECENT_FORWARDS.clear()
+    _C.RECENT_LISTED.clear()
     if not args.no_profile:
         _C.profile_read(reset=True)
         _C.profile_enable(True)
@@ -260,6 +261,9 @@ def main():
     value = total_views / elapsed
     Ks = [k for k, _, _ in _C.RECENT_FORWARDS]
     K_mean = float(np.mean(Ks)) if Ks else 0.0
+    # instances the kernels actually walk: the tile lists after the exact ellipse-vs-tile culling
+    Ls = list(_C.RECENT_LISTED) if args.path == "batched" else list(Ks)
+    L_mean = float(np.mean(Ls)) if Ls else 0.0
 
     if rank != 0:
         if world > 1:
@@ -287,6 +291,7 @@ def main():
             "global_views_per_step": args.views, "views_per_rank": per,
             "parallelism": f"views sharded over {world} rank(s) (RCCL all-gather images, all-reduce grads)",
             "mean_instances_K": round(K_mean),
+            "mean_listed_instances": round(L_mean),
             "path": args.path,
         },
     }
@@ -295,14 +300,15 @@ def main():
         kern = {k: {"ms_per_view": round(ms / nv, 4), "launches": n} for k, (ms, n) in phases.items()}
         res["kernels"] = kern
         # algorithmic bytes per view, SURVEY.md §8d: forward tile blend B_fwd = 44 K + 28 HW + 8 tiles;
-        # backward blend 44 K + 32 HW read + 2 x 40 K (the reference's atomic read-modify-write).  A launch
+        # backward blend 44 K + 32 HW read + 2 x 40 K (the reference's atomic read-modify-write), with K =
+        # the instances the lists hold (after the exact tile culling, <= the reference's K).  A launch
         # covers every view of a view set, so bytes per launch = sum over the timed views / launches.
         tiles = math.ceil(W / 16) * math.ceil(H / 16)
         f_ms, f_n = phases["render_fwd"]
         b_ms, b_n = phases["render_bwd"]
         n_fw = max(1, len(Ks))
-        bytes_fwd = (44.0 * sum(Ks) + (28.0 * H * W + 8.0 * tiles) * n_fw) / max(1, f_n)
-        bytes_bwd = (124.0 * sum(Ks) + 32.0 * H * W * n_fw) / max(1, b_n)
+        bytes_fwd = (44.0 * sum(Ls) + (28.0 * H * W + 8.0 * tiles) * n_fw) / max(1, f_n)
+        bytes_bwd = (124.0 * sum(Ls) + 32.0 * H * W * n_fw) / max(1, b_n)
         fwd_gbs = bytes_fwd / (f_ms / max(1, f_n) * 1e-3) / 1e9 if f_n else 0.0
         bwd_gbs = bytes_bwd / (b_ms / max(1, b_n) * 1e-3) / 1e9 if b_n else 0.0
         dominant = max(phases.items(), key=lambda kv: kv[1][0])[0]

@@ -141,8 +141,14 @@ int gsr_set_preprocess(int V, int P, int degree, int M, const float* means3D, co
                        const float* const* viewmatrices, const float* const* projmatrices,
                        const float* const* campos, const float* tanfovx, const float* tanfovy,
                        int width, int height, int prefiltered, int* radii, void* geom, void* stream);
-/* One D2H read of every view's K (and visible count, may be NULL); synchronises `stream`. */
+/* One D2H read of every view's K (and visible count, may be NULL); synchronises `stream`.
+ * K = the reference's num_rendered (tiles of every visible Gaussian's 3-sigma rectangle): the
+ * capacity the binning and backward scratch are sized by. */
 int gsr_set_num_rendered(int V, const void* geom, int P, int* num_rendered, int* num_visible, void* stream);
+/* As gsr_set_num_rendered, plus num_listed[v] (may be NULL): the instances the tile lists actually
+ * hold after the exact ellipse-vs-tile culling (<= K).  Diagnostic / roofline use. */
+int gsr_set_num_rendered_ex(int V, const void* geom, int P, int* num_rendered, int* num_visible, int* num_listed,
+                            void* stream);
 int gsr_set_render(int V, int P, const int* num_rendered, int width, int height, const float* const* bgs,
                    void* geom, void* binning, void* image, float* out_color, float* out_depth,
                    float* out_alpha, void* stream);

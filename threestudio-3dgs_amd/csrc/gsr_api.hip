@@ -255,22 +255,28 @@ int gsr_set_preprocess(int V, int P, int degree, int M, const float* means3D, co
   return last_launch();
 }
 
-int gsr_set_num_rendered(int V, const void* geom, int P, int* num_rendered, int* num_visible, void* stream) {
+int gsr_set_num_rendered_ex(int V, const void* geom, int P, int* num_rendered, int* num_visible, int* num_listed,
+                            void* stream) {
   if (check_set(V, P) != GSR_OK) return GSR_EINVAL;
   if (geom == nullptr || num_rendered == nullptr) return fail(GSR_EINVAL, "%s", "null pointer argument");
   GeomState g = GeomState::carve((void*)geom, V, P, nullptr);
   hipStream_t s = (hipStream_t)stream;
   static thread_local uint32_t* pinned = nullptr;
-  if (pinned == nullptr) GSR_HIP_CHECK(hipHostMalloc((void**)&pinned, 2 * GSR_SET_MAX * sizeof(uint32_t), hipHostMallocDefault));
-  GSR_HIP_CHECK(hipMemcpyAsync(pinned, g.counters, 2 * (size_t)V * sizeof(uint32_t), hipMemcpyDeviceToHost, s));
+  if (pinned == nullptr) GSR_HIP_CHECK(hipHostMalloc((void**)&pinned, 3 * GSR_SET_MAX * sizeof(uint32_t), hipHostMallocDefault));
+  GSR_HIP_CHECK(hipMemcpyAsync(pinned, g.counters, 3 * (size_t)V * sizeof(uint32_t), hipMemcpyDeviceToHost, s));
   GSR_HIP_CHECK(hipStreamSynchronize(s));
   for (int v = 0; v < V; ++v) {
     num_rendered[v] = (int)pinned[v];
     if (num_visible) num_visible[v] = (int)pinned[V + v];
+    if (num_listed) num_listed[v] = (int)pinned[2 * V + v];
     if (pinned[v] > 0x7fffffffu) return fail(GSR_EINVAL, "%s", "instance count of a view exceeds 2^31");
   }
   g_err[0] = 0;
   return GSR_OK;
+}
+
+int gsr_set_num_rendered(int V, const void* geom, int P, int* num_rendered, int* num_visible, void* stream) {
+  return gsr_set_num_rendered_ex(V, geom, P, num_rendered, num_visible, nullptr, stream);
 }
 
 int gsr_set_render(int V, int P, const int* K, int width, int height, const float* const* bgs, void* geom,

@@ -60,6 +60,7 @@ SIGNATURES = {
         + [ctypes.POINTER(_f)] * 2 + [_i, _i, _i, _vp, _vp, _vp],
     ),
     "gsr_set_num_rendered": (_i, [_i, _vp, _i, ctypes.POINTER(_i), ctypes.POINTER(_i), _vp]),
+    "gsr_set_num_rendered_ex": (_i, [_i, _vp, _i, ctypes.POINTER(_i), ctypes.POINTER(_i), ctypes.POINTER(_i), _vp]),
     "gsr_set_render": (_i, [_i, _i, ctypes.POINTER(_i), _i, _i, ctypes.POINTER(_vp)] + [_vp] * 7),
     "gsr_set_backward": (
         _i,
@@ -74,6 +75,8 @@ SIGNATURES = {
 PHASES = ("preprocess", "depth_sort", "binning", "render_fwd", "render_bwd", "gauss_bwd")
 # (num_rendered, H, W) of recent forward calls, for instrumentation (bench.py roofline numbers)
 RECENT_FORWARDS: list = []
+# instances the tile lists held (after the exact tile culling) for recent batched forwards
+RECENT_LISTED: list = []
 
 
 class GSRError(RuntimeError):

@@ -95,8 +95,11 @@ class _RasterizeViews(torch.autograd.Function):
             sets.append(vs)
         for vs in sets:
             K = (ctypes.c_int * vs.V)()
-            _C._check(lib.gsr_set_num_rendered(vs.V, p(vs.geom), P, K, None, stream))
+            L = (ctypes.c_int * vs.V)()
+            _C._check(lib.gsr_set_num_rendered_ex(vs.V, p(vs.geom), P, K, None, L, stream))
             vs.K = [int(k) for k in K]
+            if len(_C.RECENT_LISTED) < 4096:
+                _C.RECENT_LISTED.extend(int(x) for x in L)
             if len(_C.RECENT_FORWARDS) < 4096:
                 _C.RECENT_FORWARDS.extend((k, H, W) for k in vs.K)
             Karr = _arr(ctypes.c_int, vs.K)
