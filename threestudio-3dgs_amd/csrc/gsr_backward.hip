@@ -297,7 +297,9 @@ __global__ __launch_bounds__(256) void k_view_grad(GaussBackwardArgs a, ViewGrad
       for (int f = 0; f < GSR_GRAD_FIELDS; ++f) rec[(size_t)f * a.P] = 0.f;
       continue;
     }
-    const RowSums r = gather_rows((uint32_t)idx, va.g.rec[o], va.gx, cut, grow);
+    const GaussRec& gr = va.g.rec[o];
+    const uint32_t clamp_bits = gr.d.w;
+    const RowSums r = gather_rows((uint32_t)idx, gr, va.gx, cut, grow);
     m2[0] = r.dmx;
     m2[1] = r.dmy;
     m2[2] = 0.f;
@@ -328,7 +330,7 @@ __global__ __launch_bounds__(256) void k_view_grad(GaussBackwardArgs a, ViewGrad
     dm.y += cam.view[6] * r.ddep;
     dm.z += cam.view[10] * r.ddep;
     const float f[GSR_GRAD_FIELDS] = {dm.x, dm.y, dm.z, dcv[0], dcv[1], dcv[2], dcv[3], dcv[4], dcv[5],
-                                      r.dcr, r.dcg, r.dcbl, r.dop};
+                                      r.dcr, r.dcg, r.dcbl, r.dop, __uint_as_float(clamp_bits)};
 #pragma unroll
     for (int k = 0; k < GSR_GRAD_FIELDS; ++k) rec[(size_t)k * a.P] = f[k];
   }
@@ -384,9 +386,17 @@ __global__ __launch_bounds__(256) void k_gauss_accum(GaussBackwardArgs a, AccumA
       dcb += f[11];
       dop += f[12];
       if (has_sh) {
-        const uint32_t cl = b.rec[o].d.w;
+        const uint32_t cl = __float_as_uint(f[13]);
         const float3 dRGB = make_float3((cl & 1u) ? 0.f : f[9], (cl & 2u) ? 0.f : f[10], (cl & 4u) ? 0.f : f[11]);
-        sh_backward(a.deg, a.M, sh_row, dsh, dRGB, mean, b.campos[vl], dmean);
+        // the SH row as 16-byte LDS reads (stride sh_lds_stride: conflict-free); entries past 3M unused
+        float shv[48];
+        const float4* row4 = reinterpret_cast<const float4*>(sh_row);
+#pragma unroll
+        for (int c = 0; c < 12; ++c) {
+          const float4 q = 4 * c < F ? row4[c] : make_float4(0.f, 0.f, 0.f, 0.f);
+          shv[4 * c] = q.x, shv[4 * c + 1] = q.y, shv[4 * c + 2] = q.z, shv[4 * c + 3] = q.w;
+        }
+        sh_backward(a.deg, a.M, shv, dsh, dRGB, mean, b.campos[vl], dmean);
       }
     }
     put(&a.dL_dmeans3D[3 * idx], dmean.x, acc);
@@ -412,9 +422,10 @@ __global__ __launch_bounds__(256) void k_gauss_accum(GaussBackwardArgs a, AccumA
     if (has_sh) {
       // this thread's SH row is no longer read: reuse it for dL/dSH
       float* row = s_sh + t * S;
+      float4* row4w = reinterpret_cast<float4*>(row);
 #pragma unroll
-      for (int k = 0; k < 48; ++k)
-        if (k < F) row[k] = dsh[k];
+      for (int c = 0; c < 12; ++c)  // 16-byte writes; the padding past 3M is never copied out
+        if (4 * c < F) row4w[c] = make_float4(dsh[4 * c], dsh[4 * c + 1], dsh[4 * c + 2], dsh[4 * c + 3]);
       for (int k = 48; k < F; ++k) row[k] = 0.f;
     }
   }

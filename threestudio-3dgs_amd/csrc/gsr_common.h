@@ -240,13 +240,16 @@ struct ImageState {
 //   g1 = (dconic.c, dopacity, dcolor.r, dcolor.g)
 //   g2 = (dcolor.b, ddepth, 0, 0)
 // After the rows: the per-(view, Gaussian) records of gsr_backward.hip's first kernel,
-// [views of the group][13][P] floats.
+// Per-(view, Gaussian) record of the backward's second stage: dmean3D (3), dcov3D (6), raw dcolor (3),
+// dopacity (1), SH clamp flags (uint bits, 1).
+#define GSR_GRAD_FIELDS 14
+// [views of the group][GSR_GRAD_FIELDS][P] floats.
 struct BackwardState {
   float4* grow;  // [3 * instances of the group]
-  float* vrec;   // [views][13][P]
+  float* vrec;   // [views][GSR_GRAD_FIELDS][P]
   static size_t rows_bytes(long long K) { return align_up(sizeof(float4) * 3 * (size_t)(K > 0 ? K : 1), 256); }
   static size_t bytes_for(long long K, int views, int P) {
-    return rows_bytes(K) + align_up(sizeof(float) * 13 * (size_t)views * (size_t)(P > 0 ? P : 1), 256);
+    return rows_bytes(K) + align_up(sizeof(float) * GSR_GRAD_FIELDS * (size_t)views * (size_t)(P > 0 ? P : 1), 256);
   }
   static BackwardState carve(void* base, long long K) {
     BackwardState s;

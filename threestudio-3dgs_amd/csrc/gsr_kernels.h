@@ -60,7 +60,6 @@ struct GaussBackwardArgs {  // shared Gaussian parameters and the gradients of t
   float *dL_dcolors, *dL_dopacity, *dL_dmeans3D, *dL_dcov3D, *dL_dsh, *dL_dscales, *dL_drotations;
 };
 // A: per (view, Gaussian) gather + screen-space chain rule for views v0 .. v0+V-1 of a set.
-#define GSR_GRAD_FIELDS 13  // dmean3D (3), dcov3D (6), raw dcolor (3), dopacity (1)
 struct ViewGradArgs {
   int V, v0, W, H, gx, tiles, cut_in_lds, pad_;
   GeomState g;
