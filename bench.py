@@ -3,14 +3,16 @@
 
 A step is one pass of the hot path over one batch of views: every view of the batch is rendered
 through the drop-in GaussianRasterizer API (preprocess, binning, forward blend), composited on a
-constant background exactly like renderer/diff_gaussian_rasterizer_background.py:129-132, the
+per-view background image and clamped exactly like renderer/diff_gaussian_rasterizer_background.py:
+129-132,139 (batched path: the fused HIP epilogue, diff_gaussian_rasterization/composite.py), the
 rendered images are all-gathered across ranks (RCCL over xGMI; the north_star exchange), then the
 backward runs from fixed seeded upstream gradients dL/d(image, depth, alpha) (a loss's gradient,
 injected with torch.autograd.backward) through the composite and the rasterizer, and the
 per-Gaussian parameter gradients are all-reduced (sum) so every replica holds the full-batch gradient.
 
 Workload (BASELINE.json configs[2] / configs[3]): C3 per view (1M Gaussians, 1024^2,
-SH3, background path: bg = 0 + constant composite) over the C4 64-view MVDream-style orbit batch
+SH3, background path: bg = 0, then composite with a (H, W, 3) background image + clamp) over the C4
+64-view MVDream-style orbit batch
 (4 elevations x 16 azimuths), views sharded across ranks (strong scaling: the 64-view batch is fixed).
 
 Single GPU:  python bench.py [--steps K --warmup W]
@@ -98,7 +100,7 @@ def build_views(n_views, res, device):
             for i in range(n_views)]
 
 
-def render_view(rep: Replica, cam, bg_zero, bg_const):
+def render_view(rep: Replica, cam, bg_zero, bg_img):
     from diff_gaussian_rasterization import GaussianRasterizationSettings, GaussianRasterizer
 
     P = rep.means3D.shape[0]
@@ -110,8 +112,10 @@ def render_view(rep: Replica, cam, bg_zero, bg_const):
     color, radii, depth, alpha = GaussianRasterizer(raster_settings=s)(
         means3D=rep.means3D, means2D=screenspace, shs=rep.shs, colors_precomp=None, opacities=rep.opacities,
         scales=rep.scales, rotations=rep.rotations, cov3D_precomp=None)
-    # background path composite (renderer/diff_gaussian_rasterizer_background.py:129-132)
-    comp = color + (1 - alpha) * bg_const[:, None, None]
+    # background path composite + clamp, the reference's torch lines
+    # (renderer/diff_gaussian_rasterizer_background.py:129-132, 139)
+    H, W = cam["H"], cam["W"]
+    comp = (color + (1 - alpha) * bg_img.reshape(H, W, 3).permute(2, 0, 1)).clamp(0, 1)
     return comp, depth, alpha, radii
 
 
@@ -124,16 +128,18 @@ def settings_for(rep: Replica, cam, bg_zero):
                                          campos=cam["campos"], prefiltered=False, debug=False)
 
 
-def render_views(rep: Replica, settings, bg_const):
+def render_views(rep: Replica, settings, bg_img):
     """The rank's views through rasterize_views; one means2D placeholder per view, as the renderer loop
-    creates (renderer/diff_gaussian_rasterizer.py:73-81)."""
+    creates (renderer/diff_gaussian_rasterizer.py:73-81); the background composite + clamp of
+    renderer/diff_gaussian_rasterizer_background.py:129-132,139 through the fused epilogue."""
     from diff_gaussian_rasterization.batched import rasterize_views
+    from diff_gaussian_rasterization.composite import composite_background
 
     P = rep.means3D.shape[0]
     m2 = [torch.zeros((P, 3), device=rep.means3D.device, requires_grad=True) for _ in settings]
     color, radii, depth, alpha = rasterize_views(settings, rep.means3D, m2, rep.opacities, shs=rep.shs,
                                                  scales=rep.scales, rotations=rep.rotations)
-    comp = color + (1 - alpha) * bg_const[None, :, None, None]
+    comp = composite_background(color, alpha, bg_img)
     return comp, depth, alpha, radii
 
 
@@ -206,7 +212,9 @@ def main():
                  torch.randn((1, H, W), generator=gen, device=device),
                  torch.randn((1, H, W), generator=gen, device=device)) for _ in mine]
     bg_zero = torch.zeros(3, device=device)
-    bg_const = torch.tensor([0.5, 0.5, 0.5], device=device)
+    # the background network's output per view, (H, W, 3) as the reference's background MLP returns it
+    # (renderer/diff_gaussian_rasterizer_background.py:116); a trainable leaf so its gradient is formed
+    bg_img = torch.rand((len(mine), H, W, 3), generator=gen, device=device).requires_grad_(True)
     log(f"[bench] rank {rank}/{world}: setup {time.perf_counter() - t_setup:.1f}s, {len(mine)} views/rank")
 
     settings = [settings_for(rep, cam, bg_zero) for cam in mine]
@@ -216,19 +224,20 @@ def main():
 
     def step():
         if args.path == "batched":
-            c, d, a, _ = render_views(rep, settings, bg_const)
+            c, d, a, _ = render_views(rep, settings, bg_img)
             if world > 1:
                 # forward exchange: every rank receives the whole batch of rendered images
                 all_gather_views(torch.cat([c, d, a], 1), args.views)
             # the loss's gradient w.r.t. the rendered images is injected as fixed upstream gradients
             torch.autograd.backward((c, d, a), (up_c, up_d, up_a))
         else:
-            outs = [render_view(rep, cam, bg_zero, bg_const) for cam in mine]
+            outs = [render_view(rep, cam, bg_zero, bg_img[i]) for i, cam in enumerate(mine)]
             if world > 1:
                 all_gather_views(torch.stack([torch.cat([c, d, a], 0) for c, d, a, _ in outs]), args.views)
             torch.autograd.backward([t for c, d, a, _ in outs for t in (c, d, a)], [t for g in upstream for t in g])
         allreduce_grads(rep.params)  # one flat RCCL all-reduce of the Gaussian parameter gradients
         rep.zero_grad()
+        bg_img.grad = None
 
     for _ in range(args.warmup):
         step()

@@ -181,6 +181,25 @@ int gsr_set_backward(int V, int P, int degree, int M, const int* num_rendered, i
 int gsr_profile_enable(int enable);
 int gsr_profile_read(double* ms, long long* launches, int reset);
 
+/*
+ * Fused background composite of the background renderer (replaces the torch epilogue of
+ * renderer/diff_gaussian_rasterizer_background.py:129-132,139):
+ *     out = clamp(color + (1 - alpha) * bg, 0, 1)       color, out (V, 3, H, W); alpha (V, 1, H, W)
+ * bg_layout: GSR_BG_CONSTANT (V, 3), GSR_BG_HWC (V, H, W, 3) -- the background network's output --,
+ * GSR_BG_CHW (V, 3, H, W).  Backward (pre-clamp value recomputed; clamp's inclusive-bounds gradient):
+ * dL_dcolor = g, dL_dalpha = -sum_c g_c bg_c, dL_dbg = g (1 - alpha) (NULL: not computed; image
+ * layouts only), with g = dL_dout where 0 <= pre <= 1, else 0.  Bit-identical to the torch expression
+ * in the forward.
+ */
+#define GSR_BG_CONSTANT 0
+#define GSR_BG_HWC 1
+#define GSR_BG_CHW 2
+int gsr_composite_forward(int V, int height, int width, const float* color, const float* alpha, const float* bg,
+                          int bg_layout, float* out, void* stream);
+int gsr_composite_backward(int V, int height, int width, const float* dL_dout, const float* color,
+                           const float* alpha, const float* bg, int bg_layout, float* dL_dcolor, float* dL_dalpha,
+                           float* dL_dbg, void* stream);
+
 /* Replaces markVisible/checkFrustum (API completeness; unused by the reference).  present (P,) u8. */
 int gsr_mark_visible(int P, const float* means3D, const float* viewmatrix, const float* projmatrix,
                      uint8_t* present, void* stream);

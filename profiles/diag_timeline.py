@@ -63,7 +63,7 @@ def main():
     rep = bench.Replica(scene, dev)
     cams = bench.build_views(64, 1024, dev)
     bg0 = torch.zeros(3, device=dev)
-    bgc = torch.tensor([0.5, 0.5, 0.5], device=dev)
+    bgc = torch.full((1024, 1024, 3), 0.5, device=dev)
     gx = gy = 64
     nb = 128 * ((((gx + 1) // 2) * ((gy + 1) // 2) + 7) // 8)
     out = []

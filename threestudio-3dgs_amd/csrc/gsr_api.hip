@@ -255,6 +255,31 @@ int gsr_set_preprocess(int V, int P, int degree, int M, const float* means3D, co
   return last_launch();
 }
 
+int gsr_composite_forward(int V, int height, int width, const float* color, const float* alpha, const float* bg,
+                          int bg_layout, float* out, void* stream) {
+  if (V < 0 || height < 0 || width < 0 || bg_layout < 0 || bg_layout > 2) return fail(GSR_EINVAL, "%s", "bad sizes");
+  if (V == 0 || height == 0 || width == 0) return last_launch();
+  if (color == nullptr || alpha == nullptr || bg == nullptr || out == nullptr)
+    return fail(GSR_EINVAL, "%s", "null pointer argument");
+  launch_composite_fwd(V, (size_t)height * width, color, alpha, bg, bg_layout, out, (hipStream_t)stream);
+  return last_launch();
+}
+
+int gsr_composite_backward(int V, int height, int width, const float* dL_dout, const float* color,
+                           const float* alpha, const float* bg, int bg_layout, float* dL_dcolor, float* dL_dalpha,
+                           float* dL_dbg, void* stream) {
+  if (V < 0 || height < 0 || width < 0 || bg_layout < 0 || bg_layout > 2) return fail(GSR_EINVAL, "%s", "bad sizes");
+  if (V == 0 || height == 0 || width == 0) return last_launch();
+  if (dL_dout == nullptr || color == nullptr || alpha == nullptr || bg == nullptr || dL_dcolor == nullptr ||
+      dL_dalpha == nullptr)
+    return fail(GSR_EINVAL, "%s", "null pointer argument");
+  if (dL_dbg != nullptr && bg_layout == GSR_BG_CONSTANT)
+    return fail(GSR_EINVAL, "%s", "dL_dbg is computed for image backgrounds only");
+  launch_composite_bwd(V, (size_t)height * width, dL_dout, color, alpha, bg, bg_layout, dL_dcolor, dL_dalpha,
+                       dL_dbg, (hipStream_t)stream);
+  return last_launch();
+}
+
 int gsr_set_num_rendered_ex(int V, const void* geom, int P, int* num_rendered, int* num_visible, int* num_listed,
                             void* stream) {
   if (check_set(V, P) != GSR_OK) return GSR_EINVAL;

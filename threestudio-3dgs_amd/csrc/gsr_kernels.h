@@ -79,6 +79,12 @@ struct AccumArgs {
   const float* vrec;
   const float* campos[GSR_SET_MAX];
 };
+// Background composite epilogue — gsr_epilogue.hip.
+void launch_composite_fwd(int V, size_t HW, const float* color, const float* alpha, const float* bg, int layout,
+                          float* out, hipStream_t stream);
+void launch_composite_bwd(int V, size_t HW, const float* dout, const float* color, const float* alpha,
+                          const float* bg, int layout, float* dcolor, float* dalpha, float* dbg,
+                          hipStream_t stream);
 void launch_gauss_backward(const GaussBackwardArgs& a, ViewGradArgs va, const AccumArgs& b, hipStream_t stream);
 
 }  // namespace gsr
