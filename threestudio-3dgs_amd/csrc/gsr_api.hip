@@ -326,7 +326,8 @@ int gsr_set_render(int V, int P, const int* K, int width, int height, const floa
     PhaseScope ps(GSR_PHASE_BINNING, s);
     GSR_HIP_CHECK(hipMemsetAsync(img.ranges, 0, sizeof(uint2) * (size_t)V * gx * gy, s));
     if (total > 0) {
-      launch_emit(V, P, width, g, g.dval[depth_sort_result()], inst, tp.gbits, b.key[0], b.val[0], s);
+      launch_emit(V, P, width, g, g.dval[depth_sort_result()], g.dkey[depth_sort_result()], inst, tp.gbits,
+                  b.key[0], b.val[0], s);
       const int res = seg_sort(b.key, b.val, false, inst, tp.gbits, tp.tile_bits, b.sort_counts, b.sort_totals, s);
       if (res != tres) return fail(GSR_EHIP, "%s", "internal: tile sort buffer");
       launch_tile_ranges(inst, gx * gy, tp.gbits, b.key[res], img.ranges, s);

@@ -102,7 +102,8 @@ struct DupLDS {
 };
 
 __global__ __launch_bounds__(256) void k_emit(int P, int nbe, int grid_x, GeomState g, const uint32_t* __restrict__ order,
-                                              SegInfo inst, int gbits, uint32_t* __restrict__ keys,
+                                              const uint32_t* __restrict__ dkeys, SegInfo inst, int gbits,
+                                              uint32_t* __restrict__ keys,
                                               uint32_t* __restrict__ vals) {
   __shared__ DupLDS s;
   constexpr int PER = GSR_EMIT_CHUNK / 256;
@@ -115,18 +116,19 @@ __global__ __launch_bounds__(256) void k_emit(int P, int nbe, int grid_x, GeomSt
   for (int k = 0; k < GSR_DUP_ITEMS; ++k) {
     const int r = lb * GSR_DUP_TILE + t * GSR_DUP_ITEMS + k;
     gi[k] = r < P ? order[vo + r] : 0u;
-    const uint2 tt = r < P ? g.tiles[vo + gi[k]] : make_uint2(0u, 0u);
-    cnt[k] = tt.y ? tt.x : 0u;  // no kept tile: nothing to emit, no rows used
+    // visible (sorted depth key != ~0): its record is valid and its rectangle non-empty
+    const bool vis = r < P && dkeys[vo + r] != 0xFFFFFFFFu;
+    cnt[k] = 0u;
     const int m = t * GSR_DUP_ITEMS + k;
     s.gi[m] = gi[k];
-    if (cnt[k]) {
+    s.rect[m] = make_uint2(0u, 0u);
+    if (vis) {
       const GaussRec& rc = g.rec[vo + gi[k]];
       const uint4 d = rc.d;
       const float4 ra = rc.a, rb = rc.b;
+      cnt[k] = ((d.y & 0xffffu) - (d.x & 0xffffu)) * ((d.y >> 16) - (d.x >> 16));  // rectangle tiles
       s.rect[m] = make_uint2(d.x, d.y);
       s.sp[m] = span_prep(ra.x, ra.y, ra.z, ra.w, rb.x, rb.y);
-    } else {
-      s.rect[m] = make_uint2(0u, 0u);
     }
     sum += cnt[k];
   }
@@ -274,11 +276,12 @@ void launch_binning_counts(int V, int P, const GeomState& g, const uint32_t* ord
   hipLaunchKernelGGL(k_inst_scan, dim3(V), dim3(256), 0, stream, P > 0 ? nbe : 0, g);
 }
 
-void launch_emit(int V, int P, int W, const GeomState& g, const uint32_t* order, const SegInfo& inst, int gbits,
+void launch_emit(int V, int P, int W, const GeomState& g, const uint32_t* order, const uint32_t* dkeys,
+                 const SegInfo& inst, int gbits,
                  uint32_t* keys, uint32_t* vals, hipStream_t stream) {
   if (V <= 0 || P <= 0) return;
   const int nbe = GeomState::dup_blocks(P);
-  hipLaunchKernelGGL(k_emit, dim3(V * nbe), dim3(256), 0, stream, P, nbe, div_up(W, GSR_TILE_X), g, order, inst,
+  hipLaunchKernelGGL(k_emit, dim3(V * nbe), dim3(256), 0, stream, P, nbe, div_up(W, GSR_TILE_X), g, order, dkeys, inst,
                      gbits, keys, vals);
 }
 
