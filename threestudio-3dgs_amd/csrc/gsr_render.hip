@@ -70,6 +70,14 @@ __device__ __forceinline__ void tile_pixel(int t, int& lx, int& ly) {
 // rectangle spanned by the quadrant's pixel centres (<= the minimum over the pixels themselves) and
 // compares it with a padded threshold, so it never drops a pair the reference would blend; for
 // rotated, elongated footprints it is much tighter than the ellipse's bounding box.
+// per-lane select by a wave mask: one v_cndmask_b32 (keeps the replay's state updates branch-free;
+// left to itself the compiler turns a run of selects on one condition into an exec-masked branch)
+__device__ __forceinline__ float vsel(unsigned long long m, float if_set, float if_clear) {
+  float r;
+  asm("v_cndmask_b32_e64 %0, %1, %2, %3" : "=v"(r) : "v"(if_clear), "v"(if_set), "s"(m));
+  return r;
+}
+
 __device__ __forceinline__ float quad_form(float a, float b, float c, float u, float v) {
   return fmaf(a * u, u, fmaf(2.0f * b * u, v, c * v * v));
 }
@@ -187,11 +195,15 @@ __global__ __launch_bounds__(64) void k_render_fwd(RenderSet rs,
       const float test_T = T * (1.0f - alpha);
       const bool term = ok && test_T < GSR_T_EPS;
       const bool blend = ok && !term;
-      Cr = blend ? Cr + c.x * alpha * T : Cr;
-      Cg = blend ? Cg + c.y * alpha * T : Cg;
-      Cb = blend ? Cb + c.z * alpha * T : Cb;
-      D = blend ? D + b.z * alpha * T : D;
-      T = blend ? test_T : T;
+      // non-blending lanes run the same arithmetic with alpha = 0 (no change), no selects of state
+      const unsigned long long bm = __ballot(blend);
+      const float a_eff = vsel(bm, alpha, 0.0f);
+      const float aT = a_eff * T;
+      Cr = fmaf(c.x, aT, Cr);
+      Cg = fmaf(c.y, aT, Cg);
+      Cb = fmaf(c.z, aT, Cb);
+      D = fmaf(b.z, aT, D);
+      T = T * (1.0f - a_eff);
       last_contributor = blend ? __float_as_uint(b.w) : last_contributor;
       done = done || term;
       a = an;
@@ -282,13 +294,6 @@ void launch_render_forward(const RenderSet& rs, const GeomState& g, const uint32
 // on the matrix cores, 8 candidates per 16x16 product, into per-(candidate, quadrant) sums in LDS;
 // one thread per candidate then adds the four quadrants and writes ONE 48-byte gradient row per
 // instance.
-// per-lane select by a wave mask: one v_cndmask_b32 (keeps the replay's state updates branch-free;
-// left to itself the compiler turns a run of selects on one condition into an exec-masked branch)
-__device__ __forceinline__ float vsel(unsigned long long m, float if_set, float if_clear) {
-  float r;
-  asm("v_cndmask_b32_e64 %0, %1, %2, %3" : "=v"(r) : "v"(if_clear), "v"(if_set), "s"(m));
-  return r;
-}
 
 #define GSR_QSUM_STRIDE 41  // floats per candidate: 4 quadrants x 10 raw sums, +1 pad
 struct BwdLDS {
