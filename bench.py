@@ -226,14 +226,15 @@ def main():
         if args.path == "batched":
             c, d, a, _ = render_views(rep, settings, bg_img)
             if world > 1:
-                # forward exchange: every rank receives the whole batch of rendered images
-                all_gather_views(torch.cat([c, d, a], 1), args.views)
+                # forward exchange: every rank receives the whole batch of rendered images (the
+                # composited RGB a batch-level loss consumes; depth / alpha terms are per view)
+                all_gather_views(c, args.views)
             # the loss's gradient w.r.t. the rendered images is injected as fixed upstream gradients
             torch.autograd.backward((c, d, a), (up_c, up_d, up_a))
         else:
             outs = [render_view(rep, cam, bg_zero, bg_img[i]) for i, cam in enumerate(mine)]
             if world > 1:
-                all_gather_views(torch.stack([torch.cat([c, d, a], 0) for c, d, a, _ in outs]), args.views)
+                all_gather_views(torch.stack([c for c, d, a, _ in outs]), args.views)
             torch.autograd.backward([t for c, d, a, _ in outs for t in (c, d, a)], [t for g in upstream for t in g])
         allreduce_grads(rep.params)  # one flat RCCL all-reduce of the Gaussian parameter gradients
         rep.zero_grad()

@@ -42,29 +42,50 @@ def shard_range(batch_size: int, world: int, rank: int):
     return start, start + base + (1 if rank < extra else 0)
 
 
+class _GatherViews(torch.autograd.Function):
+    """All-gather of per-rank view slices; the gradient of the gathered batch flows back to the local
+    slice only (each view's gradient is computed on exactly one rank)."""
+
+    @staticmethod
+    def forward(ctx, local, batch_size, group):
+        world, rank = _world()
+        counts = [shard_range(batch_size, world, r) for r in range(world)]
+        s, e = counts[rank]
+        ctx.slice = (s, e)
+        n_max = max(b - a for a, b in counts)
+        even = all(b - a == n_max for a, b in counts)
+        if dist.get_backend(group) == "nccl" and even:
+            # equal slices: RCCL writes every rank's slice straight into the batch tensor (no staging copies)
+            out = local.new_empty((batch_size,) + tuple(local.shape[1:]))
+            dist.all_gather_into_tensor(out, local.detach().contiguous(), group=group)
+            return out
+        pad = local.new_zeros((n_max,) + tuple(local.shape[1:]))
+        pad[: local.shape[0]] = local.detach()
+        if dist.get_backend(group) == "nccl":
+            buf = local.new_empty((world * n_max,) + tuple(local.shape[1:]))
+            dist.all_gather_into_tensor(buf, pad.contiguous(), group=group)
+            parts = list(buf.split(n_max))
+        else:
+            parts = [torch.empty_like(pad) for _ in range(world)]
+            dist.all_gather(parts, pad.contiguous(), group=group)
+        return torch.cat([parts[r][: b - a] for r, (a, b) in enumerate(counts)], 0)
+
+    @staticmethod
+    def backward(ctx, grad):
+        s, e = ctx.slice
+        return grad[s:e], None, None
+
+
 def all_gather_views(local: torch.Tensor, batch_size: int, group=None) -> torch.Tensor:
     """Gather per-rank view slices (n_r, ...) into the full (batch_size, ...) tensor on every rank.
 
-    The local slice keeps its autograd history; the other ranks' slices are constants here.
+    Autograd: the gathered tensor's gradient reaches the local slice only; the other ranks' slices are
+    constants here (their views' gradients are computed on their own ranks).
     """
-    world, rank = _world()
+    world, _ = _world()
     if world == 1:
         return local
-    counts = [shard_range(batch_size, world, r) for r in range(world)]
-    n_max = max(e - s for s, e in counts)
-    pad = local.new_zeros((n_max,) + tuple(local.shape[1:]))
-    pad[: local.shape[0]] = local.detach()
-    if dist.get_backend(group) == "nccl":
-        out = local.new_empty((world * n_max,) + tuple(local.shape[1:]))
-        dist.all_gather_into_tensor(out, pad.contiguous(), group=group)
-        parts = list(out.split(n_max))
-    else:
-        parts = [torch.empty_like(pad) for _ in range(world)]
-        dist.all_gather(parts, pad.contiguous(), group=group)
-    pieces = []
-    for r, (s, e) in enumerate(counts):
-        pieces.append(local if r == rank else parts[r][: e - s])
-    return torch.cat(pieces, 0)
+    return _GatherViews.apply(local, batch_size, group)
 
 
 def allreduce_grads(params, group=None, average: bool = False):
