@@ -190,8 +190,17 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        # GSR_BENCH_BACKEND=gloo / GSR_BENCH_SHARE_GPU=1: rehearse the multi-rank path on a one-GPU box
+        if os.environ.get("GSR_BENCH_SHARE_GPU") == "1":
+            local = 0
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        backend = os.environ.get("GSR_BENCH_BACKEND", "nccl")
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(backend)
+    elif os.environ.get("GSR_BENCH_SHARE_GPU") == "1":
+        local = 0
     device = torch.device("cuda", local)
     torch.cuda.set_device(device)
 
