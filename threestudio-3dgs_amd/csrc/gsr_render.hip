@@ -600,7 +600,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 8))) voi
       tl_max += 4 * max(max(c0, c1), max(c2, c3));                  // lockstep cost in pair slots
     }
 #endif
-    if (hi - 1 - cs >= 0) {
+#ifdef GSR_EXP_NOFLUSH
+    if (hi < 0)
+#else
+    if (hi - 1 - cs >= 0)
+#endif
+    {
       // four threads per candidate (t = 4 c + quadrant): per quadrant, turn the sums over quadrant-
       // local pixel coordinates into the moments of u over dx = mean - pixel (dx = mx' - x with
       // mx' = mean - quadrant origin); add the 4 quadrants (quad DPP); form the reference's terms
