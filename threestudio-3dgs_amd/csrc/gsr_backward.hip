@@ -285,14 +285,29 @@ __global__ __launch_bounds__(256) void k_view_grad(GaussBackwardArgs a, ViewGrad
   const ViewCam& cam = va.cam[vl];
   const float4* grow = va.grow + (size_t)3 * va.row_start[vl];
   float* recv = va.vrec + (size_t)vl * GSR_GRAD_FIELDS * a.P;
+  // the next item's radius and record are loaded while the current one is processed
+  const int idx_base = (blockIdx.x / va.V) * (256 * GSR_VG_ITEMS) + t;
+  int nrad = 0;
+  GaussRec nrec;
+  if (idx_base < a.P) {
+    const size_t o0 = (size_t)vg * a.P + idx_base;
+    nrad = va.radii[o0];
+    if (nrad > 0) nrec = va.g.rec[o0];
+  }
 #pragma unroll 1
   for (int it = 0; it < GSR_VG_ITEMS; ++it) {
-    const int idx = (blockIdx.x / va.V) * (256 * GSR_VG_ITEMS) + it * 256 + t;
+    const int idx = idx_base + it * 256;
     if (idx >= a.P) break;
     const size_t o = (size_t)vg * a.P + idx;
+    const int rad = nrad;
+    const GaussRec gr = nrec;
+    if (it + 1 < GSR_VG_ITEMS && idx + 256 < a.P) {
+      nrad = va.radii[o + 256];
+      if (nrad > 0) nrec = va.g.rec[o + 256];
+    }
     float* m2 = va.dmeans2D + 3 * o;
     float* rec = recv + idx;
-    if (va.radii[o] <= 0) {
+    if (rad <= 0) {
       m2[0] = 0.f;
       m2[1] = 0.f;
       m2[2] = 0.f;
@@ -300,7 +315,6 @@ __global__ __launch_bounds__(256) void k_view_grad(GaussBackwardArgs a, ViewGrad
       for (int f = 0; f < GSR_GRAD_FIELDS; ++f) rec[(size_t)f * a.P] = 0.f;
       continue;
     }
-    const GaussRec& gr = va.g.rec[o];
     const uint32_t clamp_bits = gr.d.w;
     const RowSums r = gather_rows((uint32_t)idx, gr, va.gx, cut, grow);
     m2[0] = r.dmx;
