@@ -386,13 +386,28 @@ __global__ __launch_bounds__(256) void k_gauss_accum(GaussBackwardArgs a, AccumA
 #pragma unroll
     for (int k = 0; k < 48; ++k) dsh[k] = 0.f;
     const float* sh_row = has_sh ? s_sh + t * S : nullptr;
+    // the next view's radius and record (written for every (view, Gaussian), zeros when culled)
+    // are loaded while the current view's SH backward runs
+    int nrad = 0;
+    float nf[GSR_GRAD_FIELDS];
+    if (b.V > 0) {
+      nrad = b.radii[(size_t)b.v0 * a.P + idx];
+#pragma unroll
+      for (int k = 0; k < GSR_GRAD_FIELDS; ++k) nf[k] = b.vrec[(size_t)k * a.P + idx];
+    }
     for (int vl = 0; vl < b.V; ++vl) {
       const size_t o = (size_t)(b.v0 + vl) * a.P + idx;
-      if (b.radii[o] <= 0) continue;
-      const float* rec = b.vrec + (size_t)vl * GSR_GRAD_FIELDS * a.P + idx;
+      const int rad = nrad;
       float f[GSR_GRAD_FIELDS];
 #pragma unroll
-      for (int k = 0; k < GSR_GRAD_FIELDS; ++k) f[k] = rec[(size_t)k * a.P];
+      for (int k = 0; k < GSR_GRAD_FIELDS; ++k) f[k] = nf[k];
+      if (vl + 1 < b.V) {
+        nrad = b.radii[o + a.P];
+        const float* nrec = b.vrec + (size_t)(vl + 1) * GSR_GRAD_FIELDS * a.P + idx;
+#pragma unroll
+        for (int k = 0; k < GSR_GRAD_FIELDS; ++k) nf[k] = nrec[(size_t)k * a.P];
+      }
+      if (rad <= 0) continue;
       dmean.x += f[0];
       dmean.y += f[1];
       dmean.z += f[2];
