@@ -14,25 +14,21 @@
 
 namespace gsr {
 
-// Instances of each GSR_DUP_TILE-Gaussian block of every view's depth order: counts[v][block].
+// Rectangle tiles, visible Gaussians and kept tiles of each 64-Gaussian group of every view's depth
+// order (one wave per group, 4 groups per block): counts[v][group].
 __global__ __launch_bounds__(256) void k_inst_count(int P, int nbe, GeomState g, const uint32_t* __restrict__ order) {
-  __shared__ uint32_t s_wave[8];
-  const int v = blockIdx.x / nbe, lb = blockIdx.x % nbe;
-  const int t = threadIdx.x;
+  const int nb4 = (nbe + 3) / 4;
+  const int v = blockIdx.x / nb4;
+  const int lb = (blockIdx.x - v * nb4) * 4 + (threadIdx.x >> 6);
+  if (lb >= nbe) return;
+  const int lane = threadIdx.x & 63;
   const size_t vo = (size_t)v * P;
-  uint32_t sum = 0u, vis = 0u, kept = 0u;
-#pragma unroll
-  for (int k = 0; k < GSR_DUP_ITEMS; ++k) {
-    const int r = lb * GSR_DUP_TILE + k * 256 + t;
-    const uint2 tt = r < P ? g.tiles[vo + order[vo + r]] : make_uint2(0u, 0u);
-    sum += tt.x;
-    vis += tt.x > 0u ? 1u : 0u;
-    kept += tt.y;
-  }
-  const uint32_t tot = block_sum_u32<256>(sum, s_wave);
-  const uint32_t vtot = block_sum_u32<256>(vis, s_wave);
-  const uint32_t ktot = block_sum_u32<256>(kept, s_wave);
-  if (t == 0) {
+  const int r = lb * GSR_DUP_TILE + lane;
+  const uint2 tt = r < P ? g.tiles[vo + order[vo + r]] : make_uint2(0u, 0u);
+  const uint32_t tot = __builtin_amdgcn_readlane((int)wave_incl_sum_dpp(tt.x), 63);
+  const uint32_t vtot = __builtin_amdgcn_readlane((int)wave_incl_sum_dpp(tt.x > 0u ? 1u : 0u), 63);
+  const uint32_t ktot = __builtin_amdgcn_readlane((int)wave_incl_sum_dpp(tt.y), 63);
+  if (lane == 0) {
     g.inst_counts[(size_t)v * nbe + lb] = tot;
     g.vis_counts[(size_t)v * nbe + lb] = vtot;
     g.kept_counts[(size_t)v * nbe + lb] = ktot;
@@ -83,163 +79,89 @@ __global__ __launch_bounds__(256) void k_inst_scan(int nbe, GeomState g) {
 
 // Emit one (tile id, Gaussian) instance per kept tile (span_row) of each visible Gaussian, in
 // depth order, and goff[g] = the Gaussian's first rectangle slot (gradient rows are indexed by
-// rectangle position, the lists hold the kept tiles only).  A block owns GSR_DUP_TILE (512)
-// consecutive depth-sorted Gaussians of one view; their rectangle positions are walked in chunks
-// of 2048 (each wave 512 consecutive positions, 64 per round), the owner of every position comes
-// from an owner map (each Gaussian marks its first position, a max-scan spreads the marks), and
-// the kept positions are compacted in order (ballots within a wave, one exchange of the 4 wave
-// totals) into the block's contiguous output range (offset from k_inst_scan).
-#define GSR_EMIT_CHUNK 2048
-struct DupLDS {
-  uint32_t off[GSR_DUP_TILE + 1];
+// rectangle position, the lists hold the kept tiles only).  One wave per 64 consecutive depth-sorted
+// Gaussians, no workgroup barriers: the group's rectangle positions are walked 64 at a time, the
+// owner of every position comes from an owner map in the wave's LDS (each Gaussian marks its first
+// position, a DPP max-scan spreads the marks), and the kept positions are compacted in order with
+// ballots into the group's contiguous output range (offset from k_inst_scan).
+struct EmitLDS {
+  uint32_t off[GSR_DUP_TILE];
   uint32_t gi[GSR_DUP_TILE];
   uint2 rect[GSR_DUP_TILE];
-  SpanPrep sp[GSR_DUP_TILE];  // tile culling of each Gaussian (span_row)
-  alignas(16) uint32_t own[GSR_EMIT_CHUNK];
-  uint32_t kc[4];  // kept positions per wave of the chunk
-  uint32_t wave[8];
-  uint32_t carry;
+  SpanPrep sp[GSR_DUP_TILE];
+  uint32_t own[64];
 };
 
-__global__ __launch_bounds__(256) void k_emit(int P, int nbe, int grid_x, GeomState g, const uint32_t* __restrict__ order,
-                                              const uint32_t* __restrict__ dkeys, SegInfo inst, int gbits,
-                                              uint32_t* __restrict__ keys,
-                                              uint32_t* __restrict__ vals) {
-  __shared__ DupLDS s;
-  constexpr int PER = GSR_EMIT_CHUNK / 256;
+__global__ __launch_bounds__(64) void k_emit(int P, int nbe, int grid_x, GeomState g, const uint32_t* __restrict__ order,
+                                             const uint32_t* __restrict__ dkeys, SegInfo inst, int gbits,
+                                             uint32_t* __restrict__ keys, uint32_t* __restrict__ vals) {
+  __shared__ EmitLDS s;
   const int v = blockIdx.x / nbe, lb = blockIdx.x % nbe;
-  const int t = threadIdx.x, w = t >> 6, lane = t & 63;
+  const int lane = threadIdx.x;
   const size_t vo = (size_t)v * P;
-  uint32_t gi[GSR_DUP_ITEMS], cnt[GSR_DUP_ITEMS];
-  uint32_t sum = 0u;
-#pragma unroll
-  for (int k = 0; k < GSR_DUP_ITEMS; ++k) {
-    const int r = lb * GSR_DUP_TILE + t * GSR_DUP_ITEMS + k;
-    gi[k] = r < P ? order[vo + r] : 0u;
-    // visible (sorted depth key != ~0): its record is valid and its rectangle non-empty
-    const bool vis = r < P && dkeys[vo + r] != 0xFFFFFFFFu;
-    cnt[k] = 0u;
-    const int m = t * GSR_DUP_ITEMS + k;
-    s.gi[m] = gi[k];
-    s.rect[m] = make_uint2(0u, 0u);
-    if (vis) {
-      const GaussRec& rc = g.rec[vo + gi[k]];
-      const uint4 d = rc.d;
-      const float4 ra = rc.a, rb = rc.b;
-      cnt[k] = ((d.y & 0xffffu) - (d.x & 0xffffu)) * ((d.y >> 16) - (d.x >> 16));  // rectangle tiles
-      s.rect[m] = make_uint2(d.x, d.y);
-      s.sp[m] = span_prep(ra.x, ra.y, ra.z, ra.w, rb.x, rb.y);
-    }
-    sum += cnt[k];
+  const int r = lb * GSR_DUP_TILE + lane;
+  const uint32_t gi = r < P ? order[vo + r] : 0u;
+  // visible (sorted depth key != ~0): its record is valid and its rectangle non-empty
+  const bool vis = r < P && dkeys[vo + r] != 0xFFFFFFFFu;
+  uint32_t cnt = 0u;
+  s.gi[lane] = gi;
+  s.rect[lane] = make_uint2(0u, 0u);
+  if (vis) {
+    const GaussRec& rc = g.rec[vo + gi];
+    const uint4 d = rc.d;
+    const float4 ra = rc.a, rb = rc.b;
+    cnt = ((d.y & 0xffffu) - (d.x & 0xffffu)) * ((d.y >> 16) - (d.x >> 16));  // rectangle tiles
+    s.rect[lane] = make_uint2(d.x, d.y);
+    s.sp[lane] = span_prep(ra.x, ra.y, ra.z, ra.w, rb.x, rb.y);
   }
-  uint32_t btot;
-  const uint32_t local = block_exclusive_scan<256>(sum, &btot, s.wave);
+  const uint32_t incl = wave_incl_sum_dpp(cnt);
+  const uint32_t myoff = incl - cnt;
+  const uint32_t btot = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
+  s.off[lane] = myoff;
   // gradient-row slots: rectangle offsets (all of a visible Gaussian's rectangle, kept or not)
-  const uint32_t prefix = g.inst_counts[(size_t)v * nbe + lb];
-  uint32_t myoff[GSR_DUP_ITEMS];
-  {
-    uint32_t o = local;
-#pragma unroll
-    for (int k = 0; k < GSR_DUP_ITEMS; ++k) {
-      myoff[k] = o;
-      s.off[t * GSR_DUP_ITEMS + k] = o;
-      if (cnt[k]) g.rec[vo + gi[k]].d.z = prefix + o;
-      o += cnt[k];
-    }
-    if (t == 255) s.off[GSR_DUP_TILE] = btot;
-  }
+  if (cnt) g.rec[vo + gi].d.z = g.inst_counts[(size_t)v * nbe + lb] + myoff;
   uint32_t kbase = g.kept_counts[(size_t)v * nbe + lb];
   uint32_t* kout = keys + inst.start[v];
   uint32_t* vout = vals ? vals + inst.start[v] : nullptr;
-  for (uint32_t c0 = 0; c0 < btot; c0 += GSR_EMIT_CHUNK) {
-#pragma unroll
-    for (int k = 0; k < PER; ++k) s.own[k * 256 + t] = 0u;
-    __syncthreads();  // (also publishes s.off before the first chunk)
-    if (t == 0) {
-      // owner of the chunk's first position: last m with off[m] <= c0 (non-empty)
-      int lo = 0, hi = GSR_DUP_TILE;
-      while (hi - lo > 1) {
-        const int mid = (lo + hi) >> 1;
-        if (s.off[mid] <= c0) lo = mid;
-        else hi = mid;
-      }
-      s.carry = (uint32_t)lo + 1u;
+  uint32_t carry = 0u;  // 1 + owner of the previous chunk's last position
+  for (uint32_t c0 = 0; c0 < btot; c0 += 64) {
+    s.own[lane] = 0u;
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    if (cnt && myoff >= c0 && myoff < c0 + 64) s.own[myoff - c0] = (uint32_t)lane + 1u;
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    const uint32_t ow1 = max(carry, wave_incl_max_dpp(s.own[lane]));
+    carry = (uint32_t)__builtin_amdgcn_readlane((int)ow1, 63);
+    const uint32_t j = c0 + (uint32_t)lane;
+    bool kp = false;
+    uint32_t key = 0u, gv = 0u;
+    if (j < btot) {
+      const uint32_t ow = ow1 - 1u;
+      const uint2 rc = s.rect[ow];
+      const uint32_t xmin = rc.x & 0xffffu, ymin = rc.x >> 16, xmax = rc.y & 0xffffu;
+      const uint32_t wd = xmax - xmin, l = j - s.off[ow];
+      // l / wd without the ~35-instruction integer division: l < 2^24, so the float quotient is
+      // within one of the true one; one correction step makes it exact
+      int ty = (int)((float)l * __builtin_amdgcn_rcpf((float)wd));
+      int tx = (int)l - ty * (int)wd;
+      if (tx < 0) { --ty; tx += (int)wd; }
+      else if (tx >= (int)wd) { ++ty; tx -= (int)wd; }
+      const int row = (int)ymin + ty, col = (int)xmin + tx;
+      const SpanPrep sp = s.sp[ow];
+      int t0, t1;
+      span_row(sp, row, (int)xmin, (int)xmax, t0, t1);
+      kp = col >= t0 && col < t1;
+      const uint32_t tile = (uint32_t)row * (uint32_t)grid_x + (uint32_t)col;
+      gv = s.gi[ow];
+      key = vout ? tile : ((tile << gbits) | gv);
     }
-#pragma unroll
-    for (int k = 0; k < GSR_DUP_ITEMS; ++k)
-      if (cnt[k] && myoff[k] >= c0 && myoff[k] < c0 + GSR_EMIT_CHUNK) s.own[myoff[k] - c0] = (uint32_t)(t * GSR_DUP_ITEMS + k) + 1u;
-    __syncthreads();
-    // max-scan of the marks: thread t owns positions [PER t, PER t + PER) (16-byte LDS accesses)
-    static_assert(PER == 8, "two uint4 per thread");
-    uint4* own4 = reinterpret_cast<uint4*>(s.own) + 2 * t;
-    const uint4 o0 = own4[0], o1 = own4[1];
-    uint32_t m[PER] = {o0.x, o0.y, o0.z, o0.w, o1.x, o1.y, o1.z, o1.w};
-    uint32_t run = 0u;
-#pragma unroll
-    for (int k = 0; k < PER; ++k) {
-      run = max(run, m[k]);
-      m[k] = run;
+    const unsigned long long bal = __ballot(kp);
+    if (kp) {
+      const uint32_t o = kbase + mask_rank(bal);
+      kout[o] = key;
+      if (vout) vout[o] = gv;
     }
-    const uint32_t before = max(s.carry, block_exclusive_max<256>(run, s.wave));
-#pragma unroll
-    for (int k = 0; k < PER; ++k) m[k] = max(before, m[k]) - 1u;
-    own4[0] = make_uint4(m[0], m[1], m[2], m[3]);
-    own4[1] = make_uint4(m[4], m[5], m[6], m[7]);
-    __syncthreads();
-    const uint32_t cend = min(btot - c0, (uint32_t)GSR_EMIT_CHUNK);
-    // wave w emits chunk positions [512 w, 512 w + 512), 64 per round; its kept ones are compacted
-    // in order with ballots, the waves' totals are exchanged once
-    uint32_t key[PER], gv[PER], wo[PER], wrun = 0u;
-    bool kp[PER];
-#pragma unroll
-    for (int k = 0; k < PER; ++k) {
-      const uint32_t jj = (uint32_t)(w * (GSR_EMIT_CHUNK / 4) + k * 64 + lane);
-      kp[k] = false;
-      key[k] = 0u;
-      gv[k] = 0u;
-      if (jj < cend) {
-        const uint32_t j = c0 + jj;
-        const uint32_t ow = s.own[jj];
-        const uint2 rc = s.rect[ow];
-        const uint32_t xmin = rc.x & 0xffffu, ymin = rc.x >> 16, xmax = rc.y & 0xffffu;
-        const uint32_t wd = xmax - xmin, l = j - s.off[ow];
-        // l / wd without the ~35-instruction integer division: l < 2^24, so the float quotient is
-        // within one of the true one; one correction step makes it exact
-        int ty = (int)((float)l * __builtin_amdgcn_rcpf((float)wd));
-        int tx = (int)l - ty * (int)wd;
-        if (tx < 0) { --ty; tx += (int)wd; }
-        else if (tx >= (int)wd) { ++ty; tx -= (int)wd; }
-        const int row = (int)ymin + ty, col = (int)xmin + tx;
-        const SpanPrep sp = s.sp[ow];
-        int t0, t1;
-        span_row(sp, row, (int)xmin, (int)xmax, t0, t1);
-        kp[k] = col >= t0 && col < t1;
-        const uint32_t tile = (uint32_t)row * (uint32_t)grid_x + (uint32_t)col;
-        key[k] = vout ? tile : ((tile << gbits) | s.gi[ow]);
-        gv[k] = s.gi[ow];
-      }
-      const unsigned long long bal = __ballot(kp[k]);
-      wo[k] = wrun + mask_rank(bal);
-      wrun += (uint32_t)__popcll(bal);
-    }
-    if (lane == 0) s.kc[w] = wrun;
-    __syncthreads();
-    uint32_t wbase = 0u, ctot = 0u;
-#pragma unroll
-    for (int ww = 0; ww < 4; ++ww) {
-      const uint32_t c = s.kc[ww];
-      wbase += ww < w ? c : 0u;
-      ctot += c;
-    }
-#pragma unroll
-    for (int k = 0; k < PER; ++k) {
-      if (kp[k]) {
-        const uint32_t o = kbase + wbase + wo[k];
-        kout[o] = key[k];
-        if (vout) vout[o] = gv[k];
-      }
-    }
-    kbase += ctot;
+    kbase += (uint32_t)__popcll(bal);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // own[] is rewritten by the next chunk
   }
 }
 
@@ -272,17 +194,16 @@ void launch_binning_counts(int V, int P, const GeomState& g, const uint32_t* ord
   if (V <= 0) return;
   const int nbe = GeomState::dup_blocks(P);
   if (P > 0)
-    hipLaunchKernelGGL(k_inst_count, dim3(V * nbe), dim3(256), 0, stream, P, nbe, g, order);
+    hipLaunchKernelGGL(k_inst_count, dim3(V * ((nbe + 3) / 4)), dim3(256), 0, stream, P, nbe, g, order);
   hipLaunchKernelGGL(k_inst_scan, dim3(V), dim3(256), 0, stream, P > 0 ? nbe : 0, g);
 }
 
 void launch_emit(int V, int P, int W, const GeomState& g, const uint32_t* order, const uint32_t* dkeys,
-                 const SegInfo& inst, int gbits,
-                 uint32_t* keys, uint32_t* vals, hipStream_t stream) {
+                 const SegInfo& inst, int gbits, uint32_t* keys, uint32_t* vals, hipStream_t stream) {
   if (V <= 0 || P <= 0) return;
   const int nbe = GeomState::dup_blocks(P);
-  hipLaunchKernelGGL(k_emit, dim3(V * nbe), dim3(256), 0, stream, P, nbe, div_up(W, GSR_TILE_X), g, order, dkeys, inst,
-                     gbits, keys, vals);
+  hipLaunchKernelGGL(k_emit, dim3(V * nbe), dim3(64), 0, stream, P, nbe, div_up(W, GSR_TILE_X), g, order, dkeys,
+                     inst, gbits, keys, vals);
 }
 
 void launch_tile_ranges(SegInfo inst, int n_tiles, int gbits, const uint32_t* keys, uint2* ranges, hipStream_t stream) {

@@ -19,8 +19,7 @@
 #define GSR_RADIX_BITS 8
 #define GSR_RADIX (1 << GSR_RADIX_BITS)
 // Instance emission: 256 threads x 4 depth-sorted Gaussians per block.
-#define GSR_DUP_ITEMS 2
-#define GSR_DUP_TILE (256 * GSR_DUP_ITEMS)  // 512
+#define GSR_DUP_TILE 64  // depth-sorted Gaussians per emission group (one wave)
 // Tile ranges: 256 threads x 4 instances per block.
 #define GSR_RANGE_TILE 1024
 

@@ -42,6 +42,31 @@ __device__ __forceinline__ unsigned long long match_digit(uint32_t d, int bits, 
   return peers;
 }
 
+template <int CTRL, int ROW_MASK = 0xf>
+__device__ __forceinline__ uint32_t dpp_u32(uint32_t x) {
+  return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, CTRL, ROW_MASK, 0xf, true);
+}
+// Inclusive sum / max scans over the 64 lanes with DPP (row_shr 1/2/4/8, then row_bcast 15 / 31);
+// lanes outside a shift read 0 (bound_ctrl), the identity of both.
+__device__ __forceinline__ uint32_t wave_incl_sum_dpp(uint32_t x) {
+  x += dpp_u32<0x111>(x);
+  x += dpp_u32<0x112>(x);
+  x += dpp_u32<0x114>(x);
+  x += dpp_u32<0x118>(x);
+  x += dpp_u32<0x142, 0xa>(x);
+  x += dpp_u32<0x143, 0xc>(x);
+  return x;
+}
+__device__ __forceinline__ uint32_t wave_incl_max_dpp(uint32_t x) {
+  x = max(x, dpp_u32<0x111>(x));
+  x = max(x, dpp_u32<0x112>(x));
+  x = max(x, dpp_u32<0x114>(x));
+  x = max(x, dpp_u32<0x118>(x));
+  x = max(x, dpp_u32<0x142, 0xa>(x));
+  x = max(x, dpp_u32<0x143, 0xc>(x));
+  return x;
+}
+
 // Inclusive scan over a wave (u32), Hillis-Steele via shuffles.
 __device__ __forceinline__ uint32_t wave_inclusive_scan(uint32_t x) {
   const int lane = threadIdx.x & 63;
