@@ -305,8 +305,6 @@ struct BwdLDS {
   // its 8 candidates, stored so that MFMA lane l's 16 values are 4 chunks of 16 B (swizzled:
   // conflict-free 16-B reads, 2-way 4-B writes)
   float uw[4][64 * 16];
-  // per wave: the B operand's dL/d(r, g, b, depth) rows, [4][68] (padded) + a row of zeros
-  float dp[4][4 * 68 + 16];
   unsigned long long kmask[4];  // per quadrant: kept candidates of the batch
 #ifdef GSR_TIMELINE
   int tl_cnt[4];
@@ -330,7 +328,7 @@ __device__ __forceinline__ bool tile_of_block(int b, int gx, int gy, int& tile) 
   return true;
 }
 
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 8))) void k_render_bwd(RenderSet rs,
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5, 8))) void k_render_bwd(RenderSet rs,
                                                     const uint2* __restrict__ ranges,
                                                     const uint32_t* __restrict__ quad_maxc,
                                                     const uint32_t* __restrict__ sorted_gauss,
@@ -465,13 +463,32 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 8))) voi
     fbb[h] = ncol == 1 ? 1.f : ncol == 4 ? y : 0.f;
   }
   fc = ncol == 3 ? 1.f : 0.f;
-  float* sdp = s.dp[q];
-  sdp[0 * 68 + lane] = dpix[0];
-  sdp[1 * 68 + lane] = dpix[1];
-  sdp[2 * 68 + lane] = dpix[2];
-  sdp[3 * 68 + lane] = dpix_d;
-  if (lane < 16) sdp[4 * 68 + lane] = 0.f;
-  const float4* dsrc = reinterpret_cast<const float4*>(sdp + (dcol ? (ncol - 6) * 68 + 16 * (lane >> 4) : 4 * 68));
+  // The B operand is the same for every group: bv[i] = D + F for k-step i, kept in registers.  D
+  // (other lanes' pixels) goes through LDS once, in the qsum area (first written after the first
+  // staging barrier, by which time every wave has read its bv).
+  float bv[16];
+  {
+    float* sdp = s.qsum + q * (4 * 68 + 16);
+    sdp[0 * 68 + lane] = dpix[0];
+    sdp[1 * 68 + lane] = dpix[1];
+    sdp[2 * 68 + lane] = dpix[2];
+    sdp[3 * 68 + lane] = dpix_d;
+    if (lane < 16) sdp[4 * 68 + lane] = 0.f;
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    const float4* dsrc = reinterpret_cast<const float4*>(sdp + (dcol ? (ncol - 6) * 68 + 16 * (lane >> 4) : 4 * 68));
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const float4 d4 = dsrc[k];
+      const float dk[4] = {d4.x, d4.y, d4.z, d4.w};
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int i = 4 * k + e;
+        const float x = (float)(i & 7);
+        // one of the two terms is zero: D for columns 6-9 (zeros row otherwise), F for 0-5
+        bv[i] = dk[e] + (fa[i >> 3] + x * (fbb[i >> 3] + x * fc));
+      }
+    }
+  }
   float* uw = s.uw[q];
   // writer side: (slot r, pixel p = lane) -> 16 r + 256 (p >> 4) + 4 (((p >> 2) & 3) ^ ((r >> 2) & 3)) + (p & 3)
   int wa[4];
@@ -561,13 +578,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 8))) voi
 #ifdef GSR_EXP_NOMFMA
       continue;
 #endif
-      float av[16], dv[16];
+      float av[16];
 #pragma unroll
       for (int k = 0; k < 4; ++k) {
         const float4 a4 = asrc[k ^ aswz];
-        const float4 d4 = dsrc[k];
         av[4 * k] = a4.x, av[4 * k + 1] = a4.y, av[4 * k + 2] = a4.z, av[4 * k + 3] = a4.w;
-        dv[4 * k] = d4.x, dv[4 * k + 1] = d4.y, dv[4 * k + 2] = d4.z, dv[4 * k + 3] = d4.w;
       }
       // the candidates of this lane's 4 result rows (m = mb + r)
       const uint4 jl = *reinterpret_cast<const uint4*>(mylist + g0 + mb);
@@ -575,13 +590,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 8))) voi
       f4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
       for (int i = 0; i < 16; ++i) {
-        const float x = (float)(i & 7);
-        // one of the two terms is zero: D for columns 6-9 (zeros row otherwise), F for 0-5
-        const float bv = dv[i] + (fa[i >> 3] + x * (fbb[i >> 3] + x * fc));
         if (i & 1)
-          acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(av[i], bv, acc1, 0, 0, 0);
+          acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(av[i], bv[i], acc1, 0, 0, 0);
         else
-          acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(av[i], bv, acc0, 0, 0, 0);
+          acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(av[i], bv[i], acc0, 0, 0, 0);
       }
       // lane l: column ncol, rows 4 (l >> 4) + r; u rows 0-7 (columns 0-5), w rows 8-15 (6-9)
       if (useful) {
