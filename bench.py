@@ -53,6 +53,9 @@ def parse():
     ap.add_argument("--cpu-views", type=int, default=3, help="views of the same workload timed on the CPU oracle")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-profile", action="store_true")
+    ap.add_argument("--epilogue", choices=["background", "shading"], default="background",
+                    help="post-raster epilogue: the background renderer's composite (C3) or the MVDream shading "
+                         "renderer's depth-normal + point-light material + composite")
     ap.add_argument("--path", choices=["batched", "per-view"], default="batched",
                     help="batched: rasterize_views (one autograd node per rank's views); per-view: one "
                          "GaussianRasterizer call per view, exactly as the reference renderer loop does")
@@ -96,11 +99,21 @@ def build_views(n_views, res, device):
     c2w = orbit_c2w(torch.full((n_views,), 2.5), elev, azim)
     wv, fp, cc = get_cam_info_gaussian(c2w, fovy, fovy, 0.1, 100.0)
     tan = math.tan(fovy * 0.5)
-    return [dict(view=wv[i].to(device), proj=fp[i].to(device), campos=cc[i].to(device), tan=tan, H=res, W=res)
-            for i in range(n_views)]
+    return [dict(view=wv[i].to(device), proj=fp[i].to(device), campos=cc[i].to(device), tan=tan, H=res, W=res,
+                 c2w=c2w[i], fovy=fovy) for i in range(n_views)]
 
 
-def render_view(rep: Replica, cam, bg_zero, bg_img):
+def shading_inputs(cams, device):
+    """Rays and light positions of the views (the MVDream data module's batch, data/uncond.py:316-344)."""
+    from diff_gaussian_rasterization.cameras import light_positions_dreamfusion, ray_bundle
+
+    c2w = torch.stack([c["c2w"] for c in cams])
+    rays_o, rays_d = ray_bundle(c2w, cams[0]["fovy"], cams[0]["H"], cams[0]["W"])
+    light = light_positions_dreamfusion(c2w, 2.0)
+    return rays_o.to(device), rays_d.contiguous().to(device), light.to(device)
+
+
+def render_view(rep: Replica, cam, bg_zero, bg_img, shade=None):
     from diff_gaussian_rasterization import GaussianRasterizationSettings, GaussianRasterizer
 
     P = rep.means3D.shape[0]
@@ -112,9 +125,17 @@ def render_view(rep: Replica, cam, bg_zero, bg_img):
     color, radii, depth, alpha = GaussianRasterizer(raster_settings=s)(
         means3D=rep.means3D, means2D=screenspace, shs=rep.shs, colors_precomp=None, opacities=rep.opacities,
         scales=rep.scales, rotations=rep.rotations, cov3D_precomp=None)
+    H, W = cam["H"], cam["W"]
+    if shade is not None:
+        # the shading renderer's torch epilogue (renderer/diff_gaussian_rasterizer_shading.py:169-208)
+        import torch_reference as tr
+
+        rays_o, rays_d, light = shade
+        ka, kd = (torch.tensor(k, device=color.device) for k in (SHADE_KA, SHADE_KD))
+        render, normal, depth_m = tr.shading_epilogue(color, depth, alpha, rays_o, rays_d, bg_img, light, ka, kd)
+        return render, depth_m, alpha, radii, normal
     # background path composite + clamp, the reference's torch lines
     # (renderer/diff_gaussian_rasterizer_background.py:129-132, 139)
-    H, W = cam["H"], cam["W"]
     comp = (color + (1 - alpha) * bg_img.reshape(H, W, 3).permute(2, 0, 1)).clamp(0, 1)
     return comp, depth, alpha, radii
 
@@ -128,7 +149,10 @@ def settings_for(rep: Replica, cam, bg_zero):
                                          campos=cam["campos"], prefiltered=False, debug=False)
 
 
-def render_views(rep: Replica, settings, bg_img):
+SHADE_KA, SHADE_KD = (0.1, 0.1, 0.1), (0.9, 0.9, 0.9)  # the material's default ambient / diffuse colours
+
+
+def render_views(rep: Replica, settings, bg_img, shade=None):
     """The rank's views through rasterize_views; one means2D placeholder per view, as the renderer loop
     creates (renderer/diff_gaussian_rasterizer.py:73-81); the background composite + clamp of
     renderer/diff_gaussian_rasterizer_background.py:129-132,139 through the fused epilogue."""
@@ -139,6 +163,13 @@ def render_views(rep: Replica, settings, bg_img):
     m2 = [torch.zeros((P, 3), device=rep.means3D.device, requires_grad=True) for _ in settings]
     color, radii, depth, alpha = rasterize_views(settings, rep.means3D, m2, rep.opacities, shs=rep.shs,
                                                  scales=rep.scales, rotations=rep.rotations)
+    if shade is not None:
+        from diff_gaussian_rasterization.shading import shade_views
+
+        rays_o, rays_d, light = shade
+        render, normal, depth_m = shade_views(color, depth, alpha, rays_o, rays_d, bg_img, light,
+                                              SHADE_KA, SHADE_KD, "diffuse")
+        return render, depth_m, alpha, radii, normal
     comp = composite_background(color, alpha, bg_img)
     return comp, depth, alpha, radii
 
@@ -231,20 +262,38 @@ def main():
     up_d = torch.stack([u[1] for u in upstream]) if upstream else None
     up_a = torch.stack([u[2] for u in upstream]) if upstream else None
 
+    shade = None
+    up_n = None
+    if args.epilogue == "shading":
+        sys.path.insert(0, os.path.join(ROOT, "tests"))  # per-view path: the reference's torch epilogue
+        shade = shading_inputs(mine, device)
+        up_n = torch.randn((len(mine), 3, H, W), generator=gen, device=device)
+
     def step():
         if args.path == "batched":
-            c, d, a, _ = render_views(rep, settings, bg_img)
+            outs = render_views(rep, settings, bg_img, shade)
+            c, d, a = outs[:3]
             if world > 1:
                 # forward exchange: every rank receives the whole batch of rendered images (the
                 # composited RGB a batch-level loss consumes; depth / alpha terms are per view)
                 all_gather_views(c, args.views)
             # the loss's gradient w.r.t. the rendered images is injected as fixed upstream gradients
-            torch.autograd.backward((c, d, a), (up_c, up_d, up_a))
+            if shade is None:
+                torch.autograd.backward((c, d, a), (up_c, up_d, up_a))
+            else:
+                torch.autograd.backward((c, d, a, outs[4]), (up_c, up_d, up_a, up_n))
         else:
-            outs = [render_view(rep, cam, bg_zero, bg_img[i]) for i, cam in enumerate(mine)]
+            outs = [render_view(rep, cam, bg_zero, bg_img[i],
+                                None if shade is None else tuple(t[i] for t in shade))
+                    for i, cam in enumerate(mine)]
             if world > 1:
-                all_gather_views(torch.stack([c for c, d, a, _ in outs]), args.views)
-            torch.autograd.backward([t for c, d, a, _ in outs for t in (c, d, a)], [t for g in upstream for t in g])
+                all_gather_views(torch.stack([o[0] for o in outs]), args.views)
+            ts = [t for o in outs for t in o[:3]]
+            gs_ = [t for g in upstream for t in g]
+            if shade is not None:
+                ts += [o[4] for o in outs]
+                gs_ += list(up_n)
+            torch.autograd.backward(ts, gs_)
         allreduce_grads(rep.params)  # one flat RCCL all-reduce of the Gaussian parameter gradients
         rep.zero_grad()
         bg_img.grad = None
@@ -303,8 +352,9 @@ def main():
         "dtype": "fp32",
         "data": "synthetic (seeded scene per SURVEY.md §8d; no datasets offline)",
         "config": {
-            "workload": "C3 per view (1M Gaussians, 1024x1024, SH3, background path) over the C4 64-view "
-                        "orbit batch, fwd+bwd (fixed random upstream image gradients) + image all-gather + "
+            "workload": ("C3 per view (1M Gaussians, 1024x1024, SH3, background path)" if args.epilogue ==
+                         "background" else "1M Gaussians, 1024x1024, SH3, MVDream shading path (depth-normal, "
+                         "point-light material, composite)") + " over the C4 64-view orbit batch, fwd+bwd (fixed random upstream image gradients) + image all-gather + "
                         "gradient all-reduce",
             "n_gaussians": args.gaussians, "resolution": [H, W], "sh_degree": args.sh_degree,
             "global_views_per_step": args.views, "views_per_rank": per,
@@ -312,6 +362,7 @@ def main():
             "mean_instances_K": round(K_mean),
             "mean_listed_instances": round(L_mean),
             "path": args.path,
+            "epilogue": args.epilogue,
         },
     }
     if phases is not None:

@@ -200,6 +200,40 @@ int gsr_composite_backward(int V, int height, int width, const float* dL_dout, c
                            const float* alpha, const float* bg, int bg_layout, float* dL_dcolor, float* dL_dalpha,
                            float* dL_dbg, void* stream);
 
+/*
+ * Fused shading / depth-normal epilogue of the MVDream shading renderer and the SuGaR normal renderer
+ * (replaces the torch ops of renderer/diff_gaussian_rasterizer_shading.py:169-208 with Depth2Normal
+ * :22-51 and material/gaussian_material.py:41-104; renderer/diff_sugar_rasterizer_normal.py:170-197).
+ * Per pixel of V views (planes (V, 3|1, H, W); rays (V, H, W, 3); light (V, 3)):
+ *     X = rays_o + depth rays_d;  u = normalize(-(dX/dx x dX/dy)), central differences, X zero-padded;
+ *     unit_normal = u;  normal_map = u 0.5 alpha + 0.5;  depth_out = depth
+ * and with GSR_SHADE_MATERIAL the point-light material and background composite:
+ *     s = u (or normalize(2 pred_normal - 1) when pred_normal != NULL, detached);
+ *     t = max(s . normalize(light - X), 0) kd + ka;  albedo = color / (alpha + 1e-6);
+ *     fg = clamp(albedo, 0, 1) t | albedo | t   (mode GSR_SHADING_DIFFUSE | _ALBEDO | _TEXTURELESS);
+ *     render = clamp(fg alpha + (1 - alpha) bg, 0, 1),  bg GSR_BG_CONSTANT (V, 3) or GSR_BG_HWC.
+ * ambient / diffuse: host arrays of 3 floats (ka, kd; ignored without the material flag).
+ * Outputs may be NULL (not written) except render with the material flag.  Backward: gradients of
+ * render / normal_map / unit_normal / depth_out (any may be NULL = zero); the normal-map, unit-normal
+ * and depth_out gradients are kept only where alpha > 0.99 (the reference's in-place detach of the
+ * other pixels).  Outputs dL_ddepth, dL_dalpha (required), dL_dcolor (material), dL_dbg (NULL = not
+ * formed; GSR_BG_HWC only).
+ */
+#define GSR_SHADE_MATERIAL 1
+#define GSR_SHADING_DIFFUSE 0
+#define GSR_SHADING_ALBEDO 1
+#define GSR_SHADING_TEXTURELESS 2
+int gsr_shade_forward(int V, int height, int width, int flags, int mode, const float* color, const float* depth,
+                      const float* alpha, const float* rays_o, const float* rays_d, const float* bg, int bg_layout,
+                      const float* light, const float* pred_normal, const float* ambient, const float* diffuse,
+                      float* render, float* normal_map, float* unit_normal, float* depth_out, void* stream);
+int gsr_shade_backward(int V, int height, int width, int flags, int mode, const float* color, const float* depth,
+                       const float* alpha, const float* rays_o, const float* rays_d, const float* bg, int bg_layout,
+                       const float* light, const float* pred_normal, const float* ambient, const float* diffuse,
+                       const float* dL_drender, const float* dL_dnormal_map, const float* dL_dunit_normal,
+                       const float* dL_ddepth_out, float* dL_dcolor, float* dL_ddepth, float* dL_dalpha,
+                       float* dL_dbg, void* stream);
+
 /* Replaces markVisible/checkFrustum (API completeness; unused by the reference).  present (P,) u8. */
 int gsr_mark_visible(int P, const float* means3D, const float* viewmatrix, const float* projmatrix,
                      uint8_t* present, void* stream);

@@ -1,0 +1,178 @@
+"""Fused shading / depth-normal epilogue (include/gsr.h gsr_shade_*) against a torch restatement of the
+reference's ops (tests/torch_reference.py: renderer/diff_gaussian_rasterizer_shading.py:22-51,169-208,
+material/gaussian_material.py:86-104, renderer/diff_sugar_rasterizer_normal.py:170-197).
+
+Floating-point kernel: the yardstick is torch fp64 on the CPU.  Bars: outputs within 1e-5 absolute
+(render and normal maps live in [0, 1]); gradients within 1e-4 x max(1, max |g_ref|) per tensor, or 4x the
+torch fp32 formulation's own error where that is larger (the normal is a normalised cross product of
+central differences, so its conditioning depends on the surface)."""
+import math
+
+import numpy as np
+import pytest
+
+torch = pytest.importorskip("torch")
+
+import torch_reference as tr  # noqa: E402
+
+
+def _scene(V, H, W, seed):
+    g = torch.Generator().manual_seed(seed)
+    ys, xs = torch.meshgrid(torch.arange(H, dtype=torch.float64), torch.arange(W, dtype=torch.float64),
+                            indexing="ij")
+    out = []
+    for v in range(V):
+        ph = 0.7 * v
+        depth = (2.0 + 0.3 * torch.sin(xs / 7.0 + ph) * torch.cos(ys / 5.0) + 0.002 * torch.rand((H, W), generator=g))
+        # pinhole rays as threestudio builds them (x right, y up, -z forward; not normalised)
+        f = 0.5 * H / math.tan(math.radians(30))
+        d = torch.stack([(xs + 0.5 - W / 2) / f, -(ys + 0.5 - H / 2) / f, -torch.ones_like(xs)], -1)
+        rot = torch.linalg.qr(torch.randn(3, 3, generator=g, dtype=torch.float64))[0]
+        rays_d = d @ rot.T
+        rays_o = torch.randn(3, generator=g, dtype=torch.float64).expand(H, W, 3).clone()
+        alpha = torch.rand((1, H, W), generator=g, dtype=torch.float64)
+        alpha[:, : H // 2, : W // 2] = 1.0                     # opaque block: normal / depth gradients kept
+        alpha[:, H // 2:, : W // 3] = 0.995
+        alpha[:, 0, :] = torch.where(torch.arange(W) % 2 == 0, 0.99, 0.9900001)  # the 0.99 boundary
+        color = torch.rand((3, H, W), generator=g, dtype=torch.float64) * alpha * 1.2 - 0.05  # albedo clamp hits
+        bg = torch.rand((H, W, 3), generator=g, dtype=torch.float64)
+        light = torch.randn(3, generator=g, dtype=torch.float64) * 3
+        pred = torch.rand((3, H, W), generator=g, dtype=torch.float64)
+        ups = [torch.randn((3, H, W), generator=g, dtype=torch.float64),
+               torch.randn((3, H, W), generator=g, dtype=torch.float64),
+               torch.randn((1, H, W), generator=g, dtype=torch.float64)]
+        out.append(dict(color=color, depth=depth[None], alpha=alpha, rays_o=rays_o, rays_d=rays_d, bg=bg,
+                        light=light, pred=pred, ups=ups))
+    return out
+
+
+def _check(name, got, ref64, ref32, tol):
+    got, ref64, ref32 = (x.detach().double().cpu().numpy() for x in (got, ref64, ref32))
+    err = np.abs(got - ref64).max(initial=0.0)
+    yard = np.abs(ref32 - ref64).max(initial=0.0)
+    scale = max(1.0, float(np.abs(ref64).max(initial=0.0)))
+    bar = max(tol * scale, 4.0 * yard)
+    assert err <= bar, f"{name}: max err {err:.3g} > {bar:.3g} (torch fp32 yardstick {yard:.3g})"
+
+
+def _reference(sc, dtype, shading, use_pred, ka, kd):
+    leaves = {k: sc[k].to(dtype).clone().requires_grad_(True) for k in ("color", "depth", "alpha", "bg")}
+    outs = tr.shading_epilogue(leaves["color"], leaves["depth"], leaves["alpha"], sc["rays_o"].to(dtype),
+                               sc["rays_d"].to(dtype), leaves["bg"], sc["light"].to(dtype),
+                               torch.tensor(ka, dtype=dtype), torch.tensor(kd, dtype=dtype), shading,
+                               sc["pred"].to(dtype) if use_pred else None)
+    torch.autograd.backward(outs, [u.to(dtype) for u in sc["ups"]])
+    return outs, {k: v.grad for k, v in leaves.items()}
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("shading,use_pred,V,H,W", [
+    ("diffuse", False, 2, 40, 70),
+    ("diffuse", True, 1, 33, 31),
+    ("albedo", False, 1, 24, 64),
+    ("textureless", False, 3, 17, 45),
+])
+def test_shade_views_match_torch(shading, use_pred, V, H, W):
+    from diff_gaussian_rasterization.shading import shade_views
+
+    ka, kd = (0.1, 0.2, 0.15), (0.9, 0.7, 0.8)
+    scenes = _scene(V, H, W, seed=V * 100 + H)
+    dev = "cuda"
+    st = lambda k, dt=torch.float32: torch.stack([s[k] for s in scenes]).to(dev, dt)  # noqa: E731
+    leaves = {k: st(k).requires_grad_(True) for k in ("color", "depth", "alpha", "bg")}
+    render, nmap, depth = shade_views(leaves["color"], leaves["depth"], leaves["alpha"], st("rays_o"), st("rays_d"),
+                                      leaves["bg"], st("light"), ka, kd, shading,
+                                      st("pred") if use_pred else None)
+    ups = [torch.stack([s["ups"][i] for s in scenes]).to(dev, torch.float32) for i in range(3)]
+    torch.autograd.backward((render, nmap, depth), ups)
+    for v, sc in enumerate(scenes):
+        o64, g64 = _reference(sc, torch.float64, shading, use_pred, ka, kd)
+        o32, g32 = _reference(sc, torch.float32, shading, use_pred, ka, kd)
+        for name, got, r64, r32 in zip(("render", "normal", "depth"), (render[v], nmap[v], depth[v]), o64, o32):
+            _check(f"view {v} {name}", got, r64, r32, 1e-5)
+        for k in ("color", "depth", "alpha", "bg"):
+            _check(f"view {v} d{k}", leaves[k].grad[v], g64[k], g32[k], 1e-4)
+
+
+@pytest.mark.gpu
+def test_shade_views_single_view_constant_background():
+    from diff_gaussian_rasterization.shading import shade_views
+
+    sc = _scene(1, 20, 36, seed=5)[0]
+    ka, kd = (0.1, 0.1, 0.1), (0.9, 0.9, 0.9)
+    bgc = torch.tensor([0.2, 0.5, 0.9], dtype=torch.float64)
+    leaves = {k: sc[k].to("cuda", torch.float32).requires_grad_(True) for k in ("color", "depth", "alpha")}
+    bg = bgc.to("cuda", torch.float32).requires_grad_(True)
+    outs = shade_views(leaves["color"], leaves["depth"], leaves["alpha"], sc["rays_o"].float().cuda(),
+                       sc["rays_d"].float().cuda(), bg, sc["light"].float().cuda(), ka, kd)
+    torch.autograd.backward(outs, [u.float().cuda() for u in sc["ups"]])
+    ref = {k: sc[k].clone().requires_grad_(True) for k in ("color", "depth", "alpha")}
+    bref = bgc.clone().requires_grad_(True)
+    H, W = 20, 36
+    routs = tr.shading_epilogue(ref["color"], ref["depth"], ref["alpha"], sc["rays_o"], sc["rays_d"],
+                                bref.expand(H, W, 3), sc["light"], torch.tensor(ka, dtype=torch.float64),
+                                torch.tensor(kd, dtype=torch.float64))
+    torch.autograd.backward(routs, sc["ups"])
+    for a, b in zip(outs, routs):
+        np.testing.assert_allclose(a.detach().cpu().double().numpy(), b.detach().numpy(), atol=1e-5)
+    for k in ("color", "depth", "alpha"):
+        g = ref[k].grad.numpy()
+        np.testing.assert_allclose(leaves[k].grad.cpu().double().numpy(), g, atol=1e-4 * max(1, np.abs(g).max()))
+    np.testing.assert_allclose(bg.grad.cpu().double().numpy(), bref.grad.numpy(), rtol=1e-4, atol=1e-3)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("V,H,W", [(1, 32, 32), (2, 27, 50)])
+def test_depth_normal_views_match_torch(V, H, W):
+    from diff_gaussian_rasterization.shading import depth_normal_views
+
+    scenes = _scene(V, H, W, seed=7 + W)
+    dev = "cuda"
+    st = lambda k: torch.stack([s[k] for s in scenes]).to(dev, torch.float32)  # noqa: E731
+    depth = st("depth").requires_grad_(True)
+    alpha = st("alpha").requires_grad_(True)
+    unit, nmap = depth_normal_views(depth, alpha, st("rays_o"), st("rays_d"))
+    ups = [torch.stack([s["ups"][i] for s in scenes]).to(dev, torch.float32) for i in (0, 1)]
+    torch.autograd.backward((unit, nmap), ups)
+    for v, sc in enumerate(scenes):
+        res = {}
+        for dt in (torch.float64, torch.float32):
+            d = sc["depth"].to(dt).clone().requires_grad_(True)
+            a = sc["alpha"].to(dt).clone().requires_grad_(True)
+            outs = tr.sugar_normal_from_dist(d, a, sc["rays_o"].to(dt), sc["rays_d"].to(dt))
+            torch.autograd.backward(outs, [sc["ups"][i].to(dt) for i in (0, 1)])
+            res[dt] = (outs, d.grad, a.grad)
+        (o64, d64, a64), (o32, d32, a32) = res[torch.float64], res[torch.float32]
+        _check("unit", unit[v], o64[0], o32[0], 1e-5)
+        _check("nmap", nmap[v], o64[1], o32[1], 1e-5)
+        _check("ddepth", depth.grad[v], d64, d32, 1e-4)
+        _check("dalpha", alpha.grad[v], a64, a32, 1e-4)
+
+
+def test_shading_has_no_cpu_path():
+    from diff_gaussian_rasterization import _C
+    from diff_gaussian_rasterization.shading import depth_normal_views
+
+    sc = _scene(1, 8, 8, seed=1)[0]
+    with pytest.raises(_C.GSRError):
+        depth_normal_views(sc["depth"].float(), sc["alpha"].float(), sc["rays_o"].float(), sc["rays_d"].float())
+
+
+def test_torch_restatement_gradients_finite_difference():
+    """The torch restatement itself: the depth gradient through the normal stencil (incl. the zero-padded
+    border) matches central finite differences in fp64."""
+    sc = _scene(1, 9, 11, seed=2)[0]
+    d = sc["depth"].clone().requires_grad_(True)
+    up = sc["ups"][1]
+
+    def f(dd):
+        xyz = sc["rays_o"] + dd.permute(1, 2, 0) * sc["rays_d"]
+        n = torch.nn.functional.normalize(tr.depth_to_normal(xyz.permute(2, 0, 1).unsqueeze(0))[0], dim=0)
+        return (n * up).sum()
+
+    (g,) = torch.autograd.grad(f(d), d)
+    for (y, x) in [(0, 0), (0, 5), (4, 10), (8, 3), (2, 2)]:
+        e = torch.zeros_like(d)
+        e[0, y, x] = 1e-6
+        fd = (f(sc["depth"] + e) - f(sc["depth"] - e)) / 2e-6
+        assert abs(float(fd) - float(g[0, y, x])) < 1e-6 * max(1.0, abs(float(fd))) + 1e-7

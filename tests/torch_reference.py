@@ -179,3 +179,62 @@ def camera_tensors(cam, dtype=torch.float64):
 
 
 __all__ = ["render", "camera_tensors", "sh_color", "rot_matrix", "math"]
+
+
+# ---- post-raster epilogues of the shading / SuGaR renderers (torch restatement, for tests/test_shading.py) ----
+
+def depth_to_normal(xyz_chw):
+    """``Depth2Normal.forward`` (renderer/diff_gaussian_rasterizer_shading.py:22-51): central differences
+    of the (1, 3, H, W) xyz map by two 3x3 convolutions with zero padding, normal = -(d/dx x d/dy)."""
+    B, C, H, W = xyz_chw.shape
+    kx = torch.zeros(1, 1, 3, 3, dtype=xyz_chw.dtype)
+    kx[0, 0, 1, 0], kx[0, 0, 1, 2] = -1.0, 1.0
+    ky = torch.zeros(1, 1, 3, 3, dtype=xyz_chw.dtype)
+    ky[0, 0, 0, 1], ky[0, 0, 2, 1] = -1.0, 1.0
+    flat = xyz_chw.reshape(B * C, 1, H, W)
+    dx = torch.nn.functional.conv2d(flat, kx, padding=1).reshape(B, C, H, W)
+    dy = torch.nn.functional.conv2d(flat, ky, padding=1).reshape(B, C, H, W)
+    return -torch.cross(dx, dy, dim=1)
+
+
+def shading_epilogue(color, depth, alpha, rays_o, rays_d, bg_hwc, light, ambient, diffuse, shading="diffuse",
+                     pred_normal=None):
+    """One view of renderer/diff_gaussian_rasterizer_shading.py:169-208 with the point-light material
+    (material/gaussian_material.py:86-104): returns (render, normal, depth) as the renderer does."""
+    F = torch.nn.functional
+    H, W = depth.shape[-2:]
+    xyz = rays_o + depth.permute(1, 2, 0) * rays_d
+    normal_map = F.normalize(depth_to_normal(xyz.permute(2, 0, 1).unsqueeze(0))[0], dim=0)
+    if pred_normal is not None:
+        sn = F.normalize(pred_normal.permute(1, 2, 0).detach() * 2 - 1, dim=2)
+    else:
+        sn = normal_map.permute(1, 2, 0)
+    lpos = light[None, None, :].expand(H, W, -1)
+    ldir = F.normalize(lpos - xyz, dim=-1)
+    dl = torch.sum(sn * ldir, -1, keepdim=True).clamp(min=0.0) * diffuse
+    tl = dl + ambient
+    albedo = (color / (alpha + 1e-6)).permute(1, 2, 0)
+    if shading == "albedo":
+        fg = albedo + tl * 0
+    elif shading == "textureless":
+        fg = albedo * 0 + tl
+    else:
+        fg = albedo.clamp(0.0, 1.0) * tl
+    fg = fg.permute(2, 0, 1)
+    img = fg * alpha + (1 - alpha) * bg_hwc.reshape(H, W, 3).permute(2, 0, 1)
+    nmap = normal_map * 0.5 * alpha + 0.5
+    mask = alpha.float() > 0.99  # the reference's fp32 comparison, also when this runs in fp64
+    nmask = mask.repeat(3, 1, 1)
+    nmap = torch.where(nmask, nmap, nmap.detach())
+    depth = torch.where(mask, depth, depth.detach())
+    return img.clamp(0, 1), nmap, depth
+
+
+def sugar_normal_from_dist(depth, alpha, rays_o, rays_d):
+    """renderer/diff_sugar_rasterizer_normal.py:170-177,196-197: (normal_from_dist, normal_map_from_dist)."""
+    F = torch.nn.functional
+    xyz = rays_o + depth.permute(1, 2, 0) * rays_d
+    n = F.normalize(depth_to_normal(xyz.permute(2, 0, 1).unsqueeze(0))[0], dim=0)
+    nmap = n * 0.5 * alpha + 0.5
+    nmask = (alpha.float() > 0.99).repeat(3, 1, 1)
+    return torch.where(nmask, n, n.detach()), torch.where(nmask, nmap, nmap.detach())

@@ -280,6 +280,65 @@ int gsr_composite_backward(int V, int height, int width, const float* dL_dout, c
   return last_launch();
 }
 
+static int shade_args(int V, int H, int W, int flags, int mode, const float* color, const float* depth,
+                      const float* alpha, const float* rays_o, const float* rays_d, const float* bg, int bg_layout,
+                      const float* light, const float* pred_normal, const float* ambient, const float* diffuse,
+                      ShadeArgs& A) {
+  if (V < 0 || H < 0 || W < 0 || V > 65535 || mode < 0 || mode > 2 || (flags & ~GSR_SHADE_MATERIAL) != 0)
+    return fail(GSR_EINVAL, "%s", "bad sizes / mode / flags");
+  if (depth == nullptr || alpha == nullptr || rays_o == nullptr || rays_d == nullptr)
+    return fail(GSR_EINVAL, "%s", "null pointer argument (depth / alpha / rays)");
+  A = ShadeArgs{};
+  A.V = V, A.H = H, A.W = W, A.flags = flags, A.mode = mode, A.bg_layout = bg_layout;
+  A.color = color, A.depth = depth, A.alpha = alpha, A.rays_o = rays_o, A.rays_d = rays_d;
+  A.bg = bg, A.light = light, A.pred_normal = pred_normal;
+  if (flags & GSR_SHADE_MATERIAL) {
+    if (color == nullptr || bg == nullptr || light == nullptr || ambient == nullptr || diffuse == nullptr)
+      return fail(GSR_EINVAL, "%s", "material: color, bg, light, ambient and diffuse are required");
+    if (bg_layout != GSR_BG_CONSTANT && bg_layout != GSR_BG_HWC)
+      return fail(GSR_EINVAL, "%s", "material: bg_layout must be GSR_BG_CONSTANT or GSR_BG_HWC");
+    for (int k = 0; k < 3; ++k) A.ka[k] = ambient[k], A.kd[k] = diffuse[k];
+  }
+  return GSR_OK;
+}
+
+int gsr_shade_forward(int V, int height, int width, int flags, int mode, const float* color, const float* depth,
+                      const float* alpha, const float* rays_o, const float* rays_d, const float* bg, int bg_layout,
+                      const float* light, const float* pred_normal, const float* ambient, const float* diffuse,
+                      float* render, float* normal_map, float* unit_normal, float* depth_out, void* stream) {
+  ShadeArgs A;
+  if (shade_args(V, height, width, flags, mode, color, depth, alpha, rays_o, rays_d, bg, bg_layout, light,
+                 pred_normal, ambient, diffuse, A) != GSR_OK)
+    return GSR_EINVAL;
+  if ((flags & GSR_SHADE_MATERIAL) && render == nullptr)
+    return fail(GSR_EINVAL, "%s", "material: render output is required");
+  if (V == 0 || height == 0 || width == 0) return last_launch();
+  A.render = render, A.nmap = normal_map, A.unit = unit_normal, A.depth_out = depth_out;
+  launch_shade_fwd(A, (hipStream_t)stream);
+  return last_launch();
+}
+
+int gsr_shade_backward(int V, int height, int width, int flags, int mode, const float* color, const float* depth,
+                       const float* alpha, const float* rays_o, const float* rays_d, const float* bg, int bg_layout,
+                       const float* light, const float* pred_normal, const float* ambient, const float* diffuse,
+                       const float* dL_drender, const float* dL_dnormal_map, const float* dL_dunit_normal,
+                       const float* dL_ddepth_out, float* dL_dcolor, float* dL_ddepth, float* dL_dalpha,
+                       float* dL_dbg, void* stream) {
+  ShadeArgs A;
+  if (shade_args(V, height, width, flags, mode, color, depth, alpha, rays_o, rays_d, bg, bg_layout, light,
+                 pred_normal, ambient, diffuse, A) != GSR_OK)
+    return GSR_EINVAL;
+  if (dL_ddepth == nullptr || dL_dalpha == nullptr) return fail(GSR_EINVAL, "%s", "dL_ddepth / dL_dalpha required");
+  if ((flags & GSR_SHADE_MATERIAL) && dL_dcolor == nullptr)
+    return fail(GSR_EINVAL, "%s", "material: dL_dcolor is required");
+  if (dL_dbg != nullptr && !((flags & GSR_SHADE_MATERIAL) && bg_layout == GSR_BG_HWC))
+    return fail(GSR_EINVAL, "%s", "dL_dbg is formed for GSR_BG_HWC material shading only");
+  if (V == 0 || height == 0 || width == 0) return last_launch();
+  ShadeGrads G{dL_drender, dL_dnormal_map, dL_dunit_normal, dL_ddepth_out, dL_dcolor, dL_ddepth, dL_dalpha, dL_dbg};
+  launch_shade_bwd(A, G, (hipStream_t)stream);
+  return last_launch();
+}
+
 int gsr_set_num_rendered_ex(int V, const void* geom, int P, int* num_rendered, int* num_visible, int* num_listed,
                             void* stream) {
   if (check_set(V, P) != GSR_OK) return GSR_EINVAL;

@@ -87,6 +87,35 @@ void launch_composite_fwd(int V, size_t HW, const float* color, const float* alp
 void launch_composite_bwd(int V, size_t HW, const float* dout, const float* color, const float* alpha,
                           const float* bg, int layout, float* dcolor, float* dalpha, float* dbg,
                           hipStream_t stream);
+// Shading / depth-normal epilogue — gsr_shading.hip (include/gsr.h gsr_shade_*).
+struct ShadeArgs {
+  int V, H, W, flags, mode, bg_layout;  // bg_layout: GSR_BG_CONSTANT (V, 3) or GSR_BG_HWC (V, H, W, 3)
+  const float* color;        // (V, 3, H, W)   material only
+  const float* depth;        // (V, 1, H, W)
+  const float* alpha;        // (V, 1, H, W)
+  const float* rays_o;       // (V, H, W, 3)
+  const float* rays_d;       // (V, H, W, 3)
+  const float* bg;           // material only
+  const float* light;        // (V, 3)         material only
+  const float* pred_normal;  // (V, 3, H, W) or null
+  float ka[3], kd[3];        // ambient / diffuse light colours
+  float* render;             // (V, 3, H, W)   material only
+  float* nmap;               // (V, 3, H, W) or null
+  float* unit;               // (V, 3, H, W) or null
+  float* depth_out;          // (V, 1, H, W) or null
+};
+struct ShadeGrads {
+  const float* d_render;     // upstream gradients, any may be null
+  const float* d_nmap;
+  const float* d_unit;
+  const float* d_depth_out;
+  float* d_color;            // outputs (d_color, d_bg: material only; d_bg null = not formed)
+  float* d_depth;
+  float* d_alpha;
+  float* d_bg;
+};
+void launch_shade_fwd(const ShadeArgs& A, hipStream_t stream);
+void launch_shade_bwd(const ShadeArgs& A, const ShadeGrads& G, hipStream_t stream);
 void launch_gauss_backward(const GaussBackwardArgs& a, ViewGradArgs va, const AccumArgs& b, hipStream_t stream);
 
 }  // namespace gsr

@@ -78,3 +78,33 @@ def orbit_c2w(distance, elevation_deg, azimuth_deg) -> torch.Tensor:
 
 def tan_half_fov(fov) -> float:
     return math.tan(float(fov) * 0.5)
+
+
+def ray_bundle(c2w, fovy, height: int, width: int, normalize: bool = False):
+    """Per-pixel rays of the batch (data/uncond.py:316-329 with threestudio's get_ray_directions /
+    get_rays): unit-focal pixel-centre directions (x right, y up, -z), x/y divided by the focal length
+    0.5 H / tan(fovy / 2), rotated by c2w; rays_o is the camera position.  ``rays_d_normalize`` is false
+    in the MVDream config (configs/gaussian_splatting_mvdream.yaml:23), so rays are not normalised by
+    default.  c2w (B, 4, 4) -> rays_o, rays_d (B, H, W, 3)."""
+    c2w = torch.as_tensor(c2w, dtype=torch.float32)
+    if c2w.dim() == 2:
+        c2w = c2w[None]
+    fovy = torch.as_tensor(fovy, dtype=torch.float32).reshape(-1).expand(c2w.shape[0])
+    i, j = torch.meshgrid(torch.arange(width, dtype=torch.float32) + 0.5,
+                          torch.arange(height, dtype=torch.float32) + 0.5, indexing="xy")
+    unit = torch.stack([i - width / 2, -(j - height / 2), -torch.ones_like(i)], -1)
+    focal = 0.5 * height / torch.tan(0.5 * fovy)
+    dirs = unit[None].repeat(c2w.shape[0], 1, 1, 1)
+    dirs[..., :2] = dirs[..., :2] / focal[:, None, None, None]
+    rays_d = (dirs[:, :, :, None, :] * c2w[:, None, None, :3, :3]).sum(-1)
+    if normalize:
+        rays_d = torch.nn.functional.normalize(rays_d, dim=-1)
+    rays_o = c2w[:, None, None, :3, 3].expand(rays_d.shape)
+    return rays_o.contiguous(), rays_d
+
+
+def light_positions_dreamfusion(c2w, distance: float = 2.0):
+    """Light positions of the "dreamfusion" strategy without its random perturbation (data/uncond.py:258-267):
+    the camera direction scaled to the light distance.  c2w (B, 4, 4) -> (B, 3)."""
+    c2w = torch.as_tensor(c2w, dtype=torch.float32)
+    return torch.nn.functional.normalize(c2w[..., :3, 3], dim=-1) * distance

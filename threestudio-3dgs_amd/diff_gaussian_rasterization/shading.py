@@ -1,0 +1,156 @@
+"""Fused shading / depth-normal epilogue (include/gsr.h gsr_shade_*, csrc/gsr_shading.hip).
+
+The MVDream shading renderer follows each rasterizer call with the depth-to-normal, point-light material
+and background composite in ~25 torch ops (renderer/diff_gaussian_rasterizer_shading.py:169-208 with
+``Depth2Normal`` :22-51 and ``GaussianDiffuseWithPointLightMaterial.forward``
+material/gaussian_material.py:41-104); the SuGaR normal renderer uses the depth-to-normal part
+(renderer/diff_sugar_rasterizer_normal.py:170-197).  Here each is one HIP pass forward and one backward
+over a set of views, with the same results and gradients (including the in-place ``detach`` of the
+normal map and depth where ``alpha <= 0.99``):
+
+    shade_views(color, depth, alpha, rays_o, rays_d, bg, light_positions, ...) -> (render, normal, depth)
+        render = the shading renderer's ``render`` (clamped), normal = its ``normal`` map,
+        depth = ``depth`` (gradient masked)
+    depth_normal_views(depth, alpha, rays_o, rays_d) -> (normal_from_dist, normal_map_from_dist)
+        SuGaR's ``raw_normal_from_dist`` and ``normal_from_dist`` outputs (both gradient masked)
+
+Shapes: one view ``color (3, H, W)``, ``depth / alpha (1, H, W)``, ``rays_o / rays_d (H, W, 3)``,
+``bg (H, W, 3)`` (the background network's output) or ``(3,)``, ``light_positions (3,)``; or the same
+with a leading view dimension V.  Ambient / diffuse light colours and the shading mode are the
+material's (its ``ambient_ratio`` / soft-shading choice is made by the caller, as in the reference).
+"""
+from __future__ import annotations
+
+import ctypes
+
+import torch
+
+from . import _C
+
+MATERIAL = 1
+_MODES = {"diffuse": 0, "albedo": 1, "textureless": 2}
+
+
+def _floats3(x):
+    if isinstance(x, torch.Tensor):
+        x = x.detach().cpu().reshape(-1).tolist()
+    x = [float(t) for t in x]
+    if len(x) != 3:
+        raise ValueError("light colours need 3 components")
+    return (ctypes.c_float * 3)(*x)
+
+
+class _Shade(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, color, depth, alpha, rays_o, rays_d, bg, light, pred_normal, flags, mode, bg_layout, ka, kd):
+        lib = _C.load_library()
+        dev = depth.device
+        _C._require_gpu(dev)
+        V, _, H, W = depth.shape
+        t = {}
+        for name, x in (("color", color), ("depth", depth), ("alpha", alpha), ("rays_o", rays_o), ("rays_d", rays_d),
+                        ("bg", bg), ("light", light), ("pred_normal", pred_normal)):
+            t[name] = _C._f32(x, name, dev) if x is not None else None
+        material = bool(flags & MATERIAL)
+        new = lambda c: torch.empty((V, c, H, W), dtype=torch.float32, device=dev)  # noqa: E731
+        render = new(3) if material else None
+        nmap, depth_out = new(3), new(1)
+        unit = None if material else new(3)
+        ka_c, kd_c = _floats3(ka), _floats3(kd)
+        _C._check(lib.gsr_shade_forward(
+            V, H, W, flags, mode, _C._ptr(t["color"]), _C._ptr(t["depth"]), _C._ptr(t["alpha"]), _C._ptr(t["rays_o"]),
+            _C._ptr(t["rays_d"]), _C._ptr(t["bg"]), bg_layout, _C._ptr(t["light"]), _C._ptr(t["pred_normal"]),
+            ka_c, kd_c, _C._ptr(render), _C._ptr(nmap), _C._ptr(unit), _C._ptr(depth_out), _C._stream(dev)))
+        ctx.meta = (flags, mode, bg_layout, ka, kd)
+        ctx.save_for_backward(t["color"], t["depth"], t["alpha"], t["rays_o"], t["rays_d"], t["bg"], t["light"],
+                              t["pred_normal"])
+        if material:
+            return render, nmap, depth_out
+        return unit, nmap, depth_out
+
+    @staticmethod
+    def backward(ctx, g0, g_nmap, g_depth):
+        lib = _C.load_library()
+        color, depth, alpha, rays_o, rays_d, bg, light, pred_normal = ctx.saved_tensors
+        flags, mode, bg_layout, ka, kd = ctx.meta
+        material = bool(flags & MATERIAL)
+        dev = depth.device
+        V, _, H, W = depth.shape
+        g = lambda x: None if x is None else x.float().contiguous()  # noqa: E731
+        g_render, g_unit = (g(g0), None) if material else (None, g(g0))
+        g_nmap, g_depth = g(g_nmap), g(g_depth)
+        d_depth, d_alpha = torch.empty_like(depth), torch.empty_like(alpha)
+        d_color = torch.empty_like(color) if material else None
+        want_bg = material and ctx.needs_input_grad[5] and bg_layout == 1
+        d_bg = torch.empty_like(bg) if want_bg else None
+        _C._check(lib.gsr_shade_backward(
+            V, H, W, flags, mode, _C._ptr(color), _C._ptr(depth), _C._ptr(alpha), _C._ptr(rays_o), _C._ptr(rays_d),
+            _C._ptr(bg), bg_layout, _C._ptr(light), _C._ptr(pred_normal), _floats3(ka), _floats3(kd),
+            _C._ptr(g_render), _C._ptr(g_nmap), _C._ptr(g_unit), _C._ptr(g_depth), _C._ptr(d_color),
+            _C._ptr(d_depth), _C._ptr(d_alpha), _C._ptr(d_bg), _C._stream(dev)))
+        if material and ctx.needs_input_grad[5] and bg_layout == 0:
+            # constant background colour per view: sum over pixels of g (1 - alpha), masked by the clamp
+            d_bg = _constant_bg_grad(ctx, g_render, color, depth, alpha, rays_o, rays_d, bg, light, pred_normal)
+        return d_color, d_depth, d_alpha, None, None, d_bg, None, None, None, None, None, None, None
+
+
+def _constant_bg_grad(ctx, g_render, color, depth, alpha, rays_o, rays_d, bg, light, pred_normal):
+    """dL/dbg for a constant background colour: sum_p g (1 - alpha) [0 <= img <= 1].  The HIP backward
+    forms the per-pixel image gradient for an HWC background; a broadcast one is formed as an expanded
+    HWC image and summed (a rare path: the reference passes the background network's image)."""
+    lib = _C.load_library()
+    flags, mode, _, ka, kd = ctx.meta
+    V, _, H, W = depth.shape
+    dev = depth.device
+    bg_img = bg.view(V, 1, 1, 3).expand(V, H, W, 3).contiguous()
+    d_bg = torch.empty_like(bg_img)
+    scratch = [torch.empty_like(depth), torch.empty_like(alpha), torch.empty_like(color)]
+    _C._check(lib.gsr_shade_backward(
+        V, H, W, flags, mode, _C._ptr(color), _C._ptr(depth), _C._ptr(alpha), _C._ptr(rays_o), _C._ptr(rays_d),
+        _C._ptr(bg_img), 1, _C._ptr(light), _C._ptr(pred_normal), _floats3(ka), _floats3(kd), _C._ptr(g_render),
+        None, None, None, _C._ptr(scratch[2]), _C._ptr(scratch[0]), _C._ptr(scratch[1]), _C._ptr(d_bg),
+        _C._stream(dev)))
+    return d_bg.sum(dim=(1, 2))
+
+
+def _views(x, dims):
+    """Add the view dimension to a single-view tensor."""
+    return x.unsqueeze(0) if x is not None and x.dim() == dims else x
+
+
+def shade_views(color, depth, alpha, rays_o, rays_d, bg, light_positions, ambient=(0.1, 0.1, 0.1),
+                diffuse=(0.9, 0.9, 0.9), shading: str = "diffuse", pred_normal=None):
+    """The shading renderer's post-raster epilogue (renderer/diff_gaussian_rasterizer_shading.py:169-208)
+    for one view or V views.  Returns ``(render, normal, depth)`` = the renderer's ``render``
+    (``clamp(0, 1)`` applied), ``normal`` map and ``depth`` outputs.  ``pred_normal`` is the rasterized
+    predicted-normal image when ``pc.cfg.pred_normal`` (used detached, as in the reference)."""
+    single = depth.dim() == 3
+    color, depth, alpha = _views(color, 3), _views(depth, 3), _views(alpha, 3)
+    rays_o, rays_d = _views(rays_o, 3), _views(rays_d, 3)
+    pred_normal = _views(pred_normal.detach(), 3) if pred_normal is not None else None
+    V, _, H, W = depth.shape
+    if bg.dim() <= 2 and bg.shape[-1] == 3 and bg.numel() in (3, 3 * V):
+        bg_layout, bg = 0, bg.reshape(-1, 3).expand(V, 3)
+    else:
+        bg_layout, bg = 1, bg.reshape(-1, H, W, 3).expand(V, H, W, 3)
+    light = light_positions.reshape(-1, 3).expand(V, 3)
+    rays_o, rays_d = rays_o.expand(V, H, W, 3), rays_d.expand(V, H, W, 3)
+    if shading not in _MODES:
+        raise ValueError(f"Unknown shading type {shading}")
+    out = _Shade.apply(color, depth, alpha, rays_o, rays_d, bg, light, pred_normal, MATERIAL, _MODES[shading],
+                       bg_layout, tuple(ambient) if not isinstance(ambient, torch.Tensor) else ambient,
+                       tuple(diffuse) if not isinstance(diffuse, torch.Tensor) else diffuse)
+    return tuple(o[0] for o in out) if single else out
+
+
+def depth_normal_views(depth, alpha, rays_o, rays_d):
+    """SuGaR's normal-from-distance maps (renderer/diff_sugar_rasterizer_normal.py:170-177,196-197) for
+    one view or V views: ``(normal_from_dist, normal_map_from_dist)`` with the gradient of both kept
+    only where ``alpha > 0.99``."""
+    single = depth.dim() == 3
+    depth, alpha = _views(depth, 3), _views(alpha, 3)
+    V, _, H, W = depth.shape
+    rays_o, rays_d = _views(rays_o, 3).expand(V, H, W, 3), _views(rays_d, 3).expand(V, H, W, 3)
+    unit, nmap, _ = _Shade.apply(None, depth, alpha, rays_o, rays_d, None, None, None, 0, 0, 0, (0, 0, 0),
+                                 (0, 0, 0))
+    return (unit[0], nmap[0]) if single else (unit, nmap)
