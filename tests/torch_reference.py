@@ -187,9 +187,9 @@ def depth_to_normal(xyz_chw):
     """``Depth2Normal.forward`` (renderer/diff_gaussian_rasterizer_shading.py:22-51): central differences
     of the (1, 3, H, W) xyz map by two 3x3 convolutions with zero padding, normal = -(d/dx x d/dy)."""
     B, C, H, W = xyz_chw.shape
-    kx = torch.zeros(1, 1, 3, 3, dtype=xyz_chw.dtype)
+    kx = torch.zeros(1, 1, 3, 3, dtype=xyz_chw.dtype, device=xyz_chw.device)
     kx[0, 0, 1, 0], kx[0, 0, 1, 2] = -1.0, 1.0
-    ky = torch.zeros(1, 1, 3, 3, dtype=xyz_chw.dtype)
+    ky = torch.zeros(1, 1, 3, 3, dtype=xyz_chw.dtype, device=xyz_chw.device)
     ky[0, 0, 0, 1], ky[0, 0, 2, 1] = -1.0, 1.0
     flat = xyz_chw.reshape(B * C, 1, H, W)
     dx = torch.nn.functional.conv2d(flat, kx, padding=1).reshape(B, C, H, W)
