@@ -234,6 +234,18 @@ int gsr_shade_backward(int V, int height, int width, int flags, int mode, const 
                        const float* dL_ddepth_out, float* dL_dcolor, float* dL_ddepth, float* dL_dalpha,
                        float* dL_dbg, void* stream);
 
+/*
+ * Mean squared distance to the 3 nearest other points, for each of P points (P, 3) -> (P,): replaces
+ * simple_knn._C.distCUDA2 (called at geometry/gaussian_base.py:434-437 to initialise scales; also imported by
+ * geometry/sugar.py:18, geometry/gaussian_io.py:25, geometry/spacetime_gaussian.py:15,430,
+ * geometry/dynamic_sugar.py:17, geometry/gaussian_dynamic.py:25).  Exact search; per-pair fp32 distance
+ * fma(dz, dz, fma(dy, dy, dx * dx)); result (b0 + b1 + b2) / 3 over the sorted 3 best (FLT_MAX entries
+ * kept when P < 4).  workspace: gsr_knn_workspace_bytes(P) bytes of device memory (256-B aligned).
+ */
+size_t gsr_knn_workspace_bytes(int P);
+int gsr_knn_mean_dist(int P, const float* points, float* mean_dist, void* workspace, size_t workspace_bytes,
+                      void* stream);
+
 /* Replaces markVisible/checkFrustum (API completeness; unused by the reference).  present (P,) u8. */
 int gsr_mark_visible(int P, const float* means3D, const float* viewmatrix, const float* projmatrix,
                      uint8_t* present, void* stream);

@@ -667,3 +667,33 @@ void FN(oracle_backward)(int P, int deg, int M, const float* means, const float*
   free(radii);
   free_fwd(&f);
 }
+
+/*
+ * simple_knn.distCUDA2 restated (external package graphdeco-inria/simple-knn, unpinned, not in the
+ * reference tree; called at geometry/gaussian_base.py:434-437): for every point the mean of the squared
+ * distances to its 3 nearest other points.  Brute force over all pairs (test sizes only), the published
+ * updateKBest swap-insertion into best[3] initialised to FLT_MAX, mean (best0 + best1 + best2) / 3.
+ * Per-pair distance fma(dz, dz, fma(dy, dy, dx * dx)) with d = other - point.  qidx (nq entries) selects
+ * the query points (NULL: all P, nq = P).
+ */
+#include <float.h>
+void FN(oracle_knn_mean_dist)(int P, const float* pts, int nq, const int* qidx, double* out) {
+  for (int qi = 0; qi < nq; ++qi) {
+    const int i = qidx ? qidx[qi] : qi;
+    real best[3] = {RL(FLT_MAX), RL(FLT_MAX), RL(FLT_MAX)};
+    const real qx = (real)pts[3 * i], qy = (real)pts[3 * i + 1], qz = (real)pts[3 * i + 2];
+    for (int j = 0; j < P; ++j) {
+      if (j == i) continue;
+      const real dx = (real)pts[3 * j] - qx, dy = (real)pts[3 * j + 1] - qy, dz = (real)pts[3 * j + 2] - qz;
+      real d = FMAR(dz, dz, FMAR(dy, dy, dx * dx));
+      for (int k = 0; k < 3; ++k) {
+        if (best[k] > d) {
+          const real t = best[k];
+          best[k] = d;
+          d = t;
+        }
+      }
+    }
+    out[qi] = (double)((best[0] + best[1] + best[2]) / RL(3.0));
+  }
+}

@@ -118,3 +118,15 @@ def cov3d(scales: np.ndarray, rots: np.ndarray, mod: float = 1.0, prec: str = "f
     out = np.zeros((n, 6), np.float64)
     getattr(lib(), f"oracle_cov3d_{prec}")(ctypes.c_int(n), _p(scales), ctypes.c_double(mod), _p(rots), _p(out))
     return out
+
+
+def knn_mean_dist(points: np.ndarray, prec: str = "f32", queries=None) -> np.ndarray:
+    """simple_knn.distCUDA2 restated (oracle/gsr_oracle.c oracle_knn_mean_dist_*): mean squared distance to
+    the 3 nearest other points, brute force; ``queries`` (indices) limits the points evaluated."""
+    pts = np.ascontiguousarray(points, dtype=np.float32).reshape(-1, 3)
+    q = None if queries is None else np.ascontiguousarray(queries, dtype=np.int32)
+    nq = pts.shape[0] if q is None else q.shape[0]
+    out = np.zeros(nq, np.float64)
+    fn = getattr(lib(), f"oracle_knn_mean_dist_{prec}")
+    fn(ctypes.c_int(pts.shape[0]), _p(pts), ctypes.c_int(nq), None if q is None else _p(q), _p(out))
+    return out.astype(np.float32) if prec == "f32" else out

@@ -339,6 +339,19 @@ int gsr_shade_backward(int V, int height, int width, int flags, int mode, const 
   return last_launch();
 }
 
+size_t gsr_knn_workspace_bytes(int P) { return knn_workspace_bytes(P < 0 ? 0 : P); }
+
+int gsr_knn_mean_dist(int P, const float* points, float* mean_dist, void* workspace, size_t workspace_bytes,
+                      void* stream) {
+  if (P < 0) return fail(GSR_EINVAL, "%s", "negative point count");
+  if (P == 0) return last_launch();
+  if (points == nullptr || mean_dist == nullptr || workspace == nullptr)
+    return fail(GSR_EINVAL, "%s", "null pointer argument");
+  if (workspace_bytes < knn_workspace_bytes(P)) return fail(GSR_EINVAL, "%s", "workspace too small");
+  launch_knn_mean_dist(P, points, mean_dist, workspace, (hipStream_t)stream);
+  return last_launch();
+}
+
 int gsr_set_num_rendered_ex(int V, const void* geom, int P, int* num_rendered, int* num_visible, int* num_listed,
                             void* stream) {
   if (check_set(V, P) != GSR_OK) return GSR_EINVAL;

@@ -116,6 +116,9 @@ struct ShadeGrads {
 };
 void launch_shade_fwd(const ShadeArgs& A, hipStream_t stream);
 void launch_shade_bwd(const ShadeArgs& A, const ShadeGrads& G, hipStream_t stream);
+// 3-NN mean squared distance (simple_knn.distCUDA2) — gsr_knn.hip.
+size_t knn_workspace_bytes(int P);
+int launch_knn_mean_dist(int P, const float* points, float* out, void* workspace, hipStream_t stream);
 void launch_gauss_backward(const GaussBackwardArgs& a, ViewGradArgs va, const AccumArgs& b, hipStream_t stream);
 
 }  // namespace gsr

@@ -54,6 +54,8 @@ SIGNATURES = {
     "gsr_composite_backward": (_i, [_i, _i, _i, _vp, _vp, _vp, _vp, _i, _vp, _vp, _vp, _vp]),
     "gsr_shade_forward": (_i, [_i, _i, _i, _i, _i] + [_vp] * 6 + [_i] + [_vp] * 8 + [_vp]),
     "gsr_shade_backward": (_i, [_i, _i, _i, _i, _i] + [_vp] * 6 + [_i] + [_vp] * 12 + [_vp]),
+    "gsr_knn_workspace_bytes": (_sz, [_i]),
+    "gsr_knn_mean_dist": (_i, [_i, _vp, _vp, _vp, _sz, _vp]),
     "gsr_set_geom_bytes": (_sz, [_i, _i]),
     "gsr_set_binning_bytes": (_sz, [_i, _i, ctypes.POINTER(_i), _i, _i]),
     "gsr_set_image_bytes": (_sz, [_i, _i, _i]),
