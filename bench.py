@@ -53,6 +53,7 @@ def parse():
     ap.add_argument("--cpu-views", type=int, default=3, help="views of the same workload timed on the CPU oracle")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-profile", action="store_true")
+    ap.add_argument("--no-knn", action="store_true", help="skip the distCUDA2 timing line")
     ap.add_argument("--epilogue", choices=["background", "shading"], default="background",
                     help="post-raster epilogue: the background renderer's composite (C3) or the MVDream shading "
                          "renderer's depth-normal + point-light material + composite")
@@ -183,6 +184,23 @@ def read_traffic(path, kernel):
         return float(t["per_launch_bytes"][kernel])
     except (OSError, KeyError, ValueError, TypeError):
         return None
+
+
+def time_knn(points, reps=10):
+    """distCUDA2 (simple_knn drop-in, the scale initialisation of geometry/gaussian_base.py:434-438) on the
+    scene's points, HIP events on the launch (current) stream; not part of the step."""
+    from simple_knn._C import distCUDA2
+
+    for _ in range(2):
+        distCUDA2(points)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(reps):
+        distCUDA2(points)
+    e1.record()
+    torch.cuda.synchronize()
+    return {"op": "distCUDA2 (3-NN mean squared distance)", "points": int(points.shape[0]),
+            "ms": round(e0.elapsed_time(e1) / reps, 4)}
 
 
 def cpu_baseline(scene, res, n_views):
@@ -397,6 +415,8 @@ def main():
                                 "FETCH_SIZE x2 + WRITE_SIZE, capture of this workload: one 64-view launch)"
         res["roofline_note"] = ("bytes are SURVEY.md §8d algorithmic bytes; both blends are fp32-VALU-bound "
                                 "(early termination: the forward reads ~1/3 of them, traffic field), see DESIGN.md §6")
+    if not args.no_knn:
+        res["init_knn"] = time_knn(rep.means3D.detach())
     if world == 1 and not args.no_cpu_baseline:
         cb = cpu_baseline(scene, args.res, args.cpu_views)
         res["cpu_baseline"] = {k: (round(v, 5) if isinstance(v, float) else v) for k, v in cb.items()}

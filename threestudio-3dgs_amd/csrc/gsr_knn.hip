@@ -14,16 +14,16 @@
 // contraction of dx*dx + dy*dy + dz*dz).
 //
 // MI355X design (not simple_knn's 1024-point boxes scanned lane by lane):
-//   1. bbox: wave min/max reductions + 6 atomics on order-preserving integer encodings;
+//   1. bbox: per-block min/max partials (256 blocks), folded by every block of the Morton pass;
 //   2. 30-bit Morton codes (10 bits per axis over the bbox), sorted by the segmented LSD radix sort
 //      (gsr_sort.hip, one segment, identity values) — sorted points are spatially coherent;
 //   3. a 3-level AABB hierarchy over the sorted points: boxes of 32, superboxes of 32 boxes (1024
 //      points), hyperboxes of 32 superboxes (32768 points);
 //   4. query: one wave per 64 consecutive sorted points.  The wave walks the hierarchy starting from its
 //      own box / superbox / hyperbox (tight bounds early) and descends into a node only if some lane's
-//      squared distance to the node's AABB is <= that lane's current 3rd-best (ballot); a box is scanned
-//      by having lanes 0..31 load its points once and broadcasting them with v_readlane (SGPR operands),
-//      each lane updating its sorted top-3 with min/max.  Pruning is exact: the fma-chain is monotone
+//      squared distance to the node's AABB is <= that lane's current 3rd-best (ballot); node AABBs and
+//      a scanned box's 32 points are read with scalar loads (wave-uniform addresses -> SGPR operands, a
+//      broadcast without VGPR / LDS traffic), each lane updating its sorted top-3 with min/max.  Pruning is exact: the fma-chain is monotone
 //      in |dx|, |dy|, |dz|, so no box holding a closer point is skipped.
 //   5. results are written back to the input order.
 // HBM traffic is small (≈ 12 B read + 4 B written per point plus the sort); the query is VALU-bound.
@@ -37,14 +37,8 @@ namespace gsr {
 namespace {
 constexpr int KNN_FAN = 32;  // children per node at every level
 constexpr int KNN_BOX = 32, KNN_SUPER = KNN_BOX * KNN_FAN, KNN_HYPER = KNN_SUPER * KNN_FAN;
+constexpr int KNN_BBOX_BLOCKS = 256;  // bbox partials
 
-__device__ __forceinline__ uint32_t f2o(float f) {  // order-preserving float -> uint
-  const uint32_t u = __float_as_uint(f);
-  return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
-}
-__device__ __forceinline__ float o2f(uint32_t o) {
-  return __uint_as_float((o & 0x80000000u) ? (o & 0x7fffffffu) : ~o);
-}
 __device__ __forceinline__ uint32_t spread10(uint32_t x) {  // 10 bits -> every third bit
   x &= 0x3ffu;
   x = (x | (x << 16)) & 0x030000ffu;
@@ -67,8 +61,8 @@ struct KnnWork {
   uint32_t* vals[2];
   uint32_t* counts;
   uint32_t* totals;
-  uint32_t* bbox;  // 6 encoded words: min xyz, max xyz
-  float4* spts;    // Morton-sorted points
+  float* bbox;     // per-block partials: [block][min xyz, max xyz]
+  float* bpts;     // Morton-sorted points, per box of 32 SoA: [box][x | y | z][32], +inf padding
   float4* lo[3];   // AABBs per level (box, super, hyper)
   float4* hi[3];
   int n[3];
@@ -79,8 +73,8 @@ struct KnnWork {
     for (int k = 0; k < 2; ++k) w.keys[k] = c.take<uint32_t>(n), w.vals[k] = c.take<uint32_t>(n);
     w.counts = c.take<uint32_t>((size_t)GSR_RADIX * div_up((long long)n, GSR_SORT_TILE));
     w.totals = c.take<uint32_t>(GSR_RADIX);
-    w.bbox = c.take<uint32_t>(8);
-    w.spts = c.take<float4>(n);
+    w.bbox = c.take<float>(6 * KNN_BBOX_BLOCKS);
+    w.bpts = c.take<float>((size_t)div_up((long long)n, KNN_BOX) * 3 * KNN_BOX);
     int cnt = (int)n;
     const int fan[3] = {KNN_BOX, KNN_FAN, KNN_FAN};
     for (int l = 0; l < 3; ++l) {
@@ -94,12 +88,10 @@ struct KnnWork {
   }
 };
 
-__global__ void k_knn_bbox_init(uint32_t* bbox) {
-  if (threadIdx.x < 3) bbox[threadIdx.x] = 0xffffffffu;
-  else if (threadIdx.x < 6) bbox[threadIdx.x] = 0u;
-}
 
-__global__ __launch_bounds__(256) void k_knn_bbox(int P, const float* __restrict__ pts, uint32_t* bbox) {
+// per-block bbox partials (no same-address atomics: those serialise at the memory side)
+__global__ __launch_bounds__(256) void k_knn_bbox(int P, const float* __restrict__ pts, float* __restrict__ part) {
+  __shared__ float s[4][6];
   float mn[3] = {INFINITY, INFINITY, INFINITY}, mx[3] = {-INFINITY, -INFINITY, -INFINITY};
   for (int i = blockIdx.x * 256 + threadIdx.x; i < P; i += gridDim.x * 256) {
 #pragma unroll
@@ -116,23 +108,49 @@ __global__ __launch_bounds__(256) void k_knn_bbox(int P, const float* __restrict
       mx[k] = fmaxf(mx[k], __shfl_xor(mx[k], off));
     }
   }
+  const int w = threadIdx.x >> 6;
   if ((threadIdx.x & 63) == 0) {
 #pragma unroll
-    for (int k = 0; k < 3; ++k) {
-      atomicMin(&bbox[k], f2o(mn[k]));
-      atomicMax(&bbox[3 + k], f2o(mx[k]));
-    }
+    for (int k = 0; k < 3; ++k) s[w][k] = mn[k], s[w][3 + k] = mx[k];
+  }
+  __syncthreads();
+  if (threadIdx.x < 6) {
+    const int k = threadIdx.x;
+    float r = s[0][k];
+    for (int j = 1; j < 4; ++j) r = k < 3 ? fminf(r, s[j][k]) : fmaxf(r, s[j][k]);
+    part[blockIdx.x * 6 + k] = r;
   }
 }
 
-__global__ __launch_bounds__(256) void k_knn_morton(int P, const float* __restrict__ pts, const uint32_t* bbox,
-                                                    uint32_t* __restrict__ keys) {
+// Morton code per point; every block first folds the bbox partials (6 KB, L2-resident)
+__global__ __launch_bounds__(256) void k_knn_morton(int P, const float* __restrict__ pts, int nparts,
+                                                    const float* __restrict__ part, uint32_t* __restrict__ keys) {
+  __shared__ float s_box[4][6];
+  {
+    float m[6] = {INFINITY, INFINITY, INFINITY, -INFINITY, -INFINITY, -INFINITY};
+    for (int j = threadIdx.x; j < nparts; j += 256) {
+#pragma unroll
+      for (int k = 0; k < 6; ++k) m[k] = k < 3 ? fminf(m[k], part[6 * j + k]) : fmaxf(m[k], part[6 * j + k]);
+    }
+#pragma unroll
+    for (int k = 0; k < 6; ++k)
+      for (int off = 32; off > 0; off >>= 1) {
+        const float o = __shfl_xor(m[k], off);
+        m[k] = k < 3 ? fminf(m[k], o) : fmaxf(m[k], o);
+      }
+    if ((threadIdx.x & 63) == 0) {
+#pragma unroll
+      for (int k = 0; k < 6; ++k) s_box[threadIdx.x >> 6][k] = m[k];
+    }
+  }
+  __syncthreads();
   const int i = blockIdx.x * 256 + threadIdx.x;
   if (i >= P) return;
   uint32_t code = 0;
 #pragma unroll
   for (int k = 0; k < 3; ++k) {
-    const float lo = o2f(bbox[k]), hi = o2f(bbox[3 + k]);
+    const float lo = fminf(fminf(s_box[0][k], s_box[1][k]), fminf(s_box[2][k], s_box[3][k]));
+    const float hi = fmaxf(fmaxf(s_box[0][3 + k], s_box[1][3 + k]), fmaxf(s_box[2][3 + k], s_box[3][3 + k]));
     const float ext = hi - lo;
     const float t = ext > 0.0f ? (pts[3 * (size_t)i + k] - lo) / ext : 0.0f;
     const uint32_t q = (uint32_t)fminf(fmaxf(t * 1024.0f, 0.0f), 1023.0f);
@@ -141,12 +159,34 @@ __global__ __launch_bounds__(256) void k_knn_morton(int P, const float* __restri
   keys[i] = code;
 }
 
-__global__ __launch_bounds__(256) void k_knn_gather(int P, const float* __restrict__ pts,
-                                                    const uint32_t* __restrict__ order, float4* __restrict__ spts) {
+__global__ __launch_bounds__(256) void k_knn_gather(int P, int n_slots, const float* __restrict__ pts,
+                                                    const uint32_t* __restrict__ order, float* __restrict__ bpts) {
   const int i = blockIdx.x * 256 + threadIdx.x;
-  if (i >= P) return;
-  const size_t j = order[i];
-  spts[i] = make_float4(pts[3 * j], pts[3 * j + 1], pts[3 * j + 2], 0.0f);
+  if (i >= n_slots) return;
+  float x = INFINITY, y = INFINITY, z = INFINITY;  // padding of the last box: never a neighbour
+  if (i < P) {
+    const size_t j = order[i];
+    x = pts[3 * j], y = pts[3 * j + 1], z = pts[3 * j + 2];
+  }
+  float* box = bpts + (size_t)(i / KNN_BOX) * 3 * KNN_BOX + (i % KNN_BOX);
+  box[0] = x, box[KNN_BOX] = y, box[2 * KNN_BOX] = z;
+}
+
+// AABB of each box of 32 sorted points (SoA, padding excluded)
+__global__ __launch_bounds__(256) void k_knn_box_aabb(int P, int n_box, const float* __restrict__ bpts,
+                                                      float4* __restrict__ lo, float4* __restrict__ hi) {
+  const int b = blockIdx.x * 256 + threadIdx.x;
+  if (b >= n_box) return;
+  const float* box = bpts + (size_t)b * 3 * KNN_BOX;
+  const int cnt = min(KNN_BOX, P - b * KNN_BOX);
+  float4 a = make_float4(INFINITY, INFINITY, INFINITY, 0.f), c = make_float4(-INFINITY, -INFINITY, -INFINITY, 0.f);
+  for (int j = 0; j < cnt; ++j) {
+    const float x = box[j], y = box[KNN_BOX + j], z = box[2 * KNN_BOX + j];
+    a.x = fminf(a.x, x), a.y = fminf(a.y, y), a.z = fminf(a.z, z);
+    c.x = fmaxf(c.x, x), c.y = fmaxf(c.y, y), c.z = fmaxf(c.z, z);
+  }
+  lo[b] = a;
+  hi[b] = c;
 }
 
 // AABB of each group of `fan` consecutive children (children given as lo / hi float4 arrays)
@@ -168,7 +208,7 @@ __global__ __launch_bounds__(256) void k_knn_aabb(int n_children, int fan, const
 
 struct KnnQuery {
   int P;
-  const float4* spts;
+  const float* bpts;
   const float4* lo[3];
   const float4* hi[3];
   int n[3];
@@ -176,47 +216,119 @@ struct KnnQuery {
   float* out;
 };
 
-__device__ __forceinline__ float rl(float x, int j) { return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(x), j)); }
+// Loads whose index is wave-uniform, through the constant address space: the compiler emits s_load
+// (scalar cache, SGPR results used directly as VALU operands — a broadcast with no VGPR or LDS traffic).
+typedef __attribute__((address_space(4))) const float* cfptr;
+
+__device__ __forceinline__ void knn_insert(float d, float& b0, float& b1, float& b2) {
+  // the "if (best[k] > d) swap" insertion, branch-free
+  const float n0 = fminf(b0, d), c1 = fmaxf(b0, d);
+  const float n1 = fminf(b1, c1), c2 = fmaxf(b1, c1);
+  b0 = n0, b1 = n1, b2 = fminf(b2, c2);
+}
 
 __global__ __launch_bounds__(256) void k_knn_query(KnnQuery Q) {
 #pragma clang fp contract(off)
   const int lane = threadIdx.x & 63;
-  const int wave = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int wave = __builtin_amdgcn_readfirstlane(blockIdx.x * 4 + (threadIdx.x >> 6));
   const int base = wave * 64;
   if (base >= Q.P) return;  // uniform per wave
   const int i = base + lane;
   const bool valid = i < Q.P;
-  const float4 q = Q.spts[valid ? i : base];
+  const int qi = valid ? i : base;
+  const float* qb = Q.bpts + (size_t)(qi / KNN_BOX) * 3 * KNN_BOX + (qi % KNN_BOX);
+  const float4 q = make_float4(qb[0], qb[KNN_BOX], qb[2 * KNN_BOX], 0.0f);
   float b0 = FLT_MAX, b1 = FLT_MAX, b2 = FLT_MAX;
   const float lim_invalid = -1.0f;  // invalid lanes never ask for a node
   auto need = [&](float d) { return valid ? d <= b2 : d <= lim_invalid; };
+  // AABB of the wave's queries and the wave's loosest current bound: a node whose AABB is farther from the
+  // query AABB than sqrt(max b2) holds no lane's neighbour (conservative: exactness kept)
+  float ql[3] = {valid ? q.x : INFINITY, valid ? q.y : INFINITY, valid ? q.z : INFINITY};
+  float qh[3] = {valid ? q.x : -INFINITY, valid ? q.y : -INFINITY, valid ? q.z : -INFINITY};
+#pragma unroll
+  for (int k = 0; k < 3; ++k) {
+    for (int off = 32; off > 0; off >>= 1) {
+      ql[k] = fminf(ql[k], __shfl_xor(ql[k], off));
+      qh[k] = fmaxf(qh[k], __shfl_xor(qh[k], off));
+    }
+  }
+  auto bound = [&]() {
+    float m = valid ? b2 : 0.0f;
+    for (int off = 32; off > 0; off >>= 1) m = fmaxf(m, __shfl_xor(m, off));
+    return m;
+  };
+  // children [c0, c0 + cnt) of level l (cnt <= 64) tested in parallel, one per lane -> candidate mask
+  auto children = [&](int l, int c0, int cnt) -> unsigned long long {
+    const float bd = bound();
+    bool t = false;
+    if (lane < cnt) {
+      const float4 lo = Q.lo[l][c0 + lane], hi = Q.hi[l][c0 + lane];
+      const float dx = fmaxf(0.0f, fmaxf(lo.x - qh[0], ql[0] - hi.x));
+      const float dy = fmaxf(0.0f, fmaxf(lo.y - qh[1], ql[1] - hi.y));
+      const float dz = fmaxf(0.0f, fmaxf(lo.z - qh[2], ql[2] - hi.z));
+      t = dist2(dx, dy, dz) <= bd;
+    }
+    return __ballot(t);
+  };
+  // visit the set bits of `mask` starting at bit `first` (own node first: tight bounds early), wrapping
+  auto order_bits = [](unsigned long long mask, int first, unsigned long long& lo_part) {
+    const unsigned long long at = first > 0 && first < 64 ? (~0ull << first) : (first <= 0 ? ~0ull : 0ull);
+    lo_part = mask & ~at;
+    return mask & at;
+  };
+  // exact per-lane test of one node (scalar loads of its AABB), ballot
+  auto refine = [&](int l, int k) {
+    const cfptr lo = (cfptr)Q.lo[l] + 4 * (size_t)k, hi = (cfptr)Q.hi[l] + 4 * (size_t)k;
+    const float bd = box_dist2(q, make_float4(lo[0], lo[1], lo[2], 0.f), make_float4(hi[0], hi[1], hi[2], 0.f));
+    return __ballot(need(bd)) != 0ull;
+  };
+  auto scan_box = [&](int b) {
+    if (!refine(0, b)) return;
+    const int self = i - b * KNN_BOX;  // position of the lane's own point in this box (or outside 0..31)
+    const cfptr box = (cfptr)Q.bpts + (size_t)b * 3 * KNN_BOX;
+#pragma unroll
+    for (int c = 0; c < KNN_BOX; c += 16) {  // 16 points = 48 SGPRs per batch of s_load_dwordx16
+      float xs[16], ys[16], zs[16];
+#pragma unroll
+      for (int j = 0; j < 16; ++j) xs[j] = box[c + j], ys[j] = box[KNN_BOX + c + j], zs[j] = box[2 * KNN_BOX + c + j];
+#pragma unroll
+      for (int j = 0; j < 16; ++j) {
+        const float d = dist2(xs[j] - q.x, ys[j] - q.y, zs[j] - q.z);
+        knn_insert(c + j == self ? FLT_MAX : d, b0, b1, b2);
+      }
+    }
+  };
 
   const int own[3] = {base / KNN_BOX, base / KNN_SUPER, base / KNN_HYPER};
   const int nh = Q.n[2];
-  for (int hh = 0; hh < nh; ++hh) {
-    const int h = own[2] + hh < nh ? own[2] + hh : own[2] + hh - nh;
-    if (__ballot(need(box_dist2(q, Q.lo[2][h], Q.hi[2][h]))) == 0ull) continue;
-    const int s_lo = h * KNN_FAN, s_n = min(KNN_FAN, Q.n[1] - s_lo);
-    const int s_first = (h == own[2]) ? own[1] - s_lo : 0;
-    for (int ss = 0; ss < s_n; ++ss) {
-      const int s = s_lo + (s_first + ss < s_n ? s_first + ss : s_first + ss - s_n);
-      if (__ballot(need(box_dist2(q, Q.lo[1][s], Q.hi[1][s]))) == 0ull) continue;
-      const int x_lo = s * KNN_FAN, x_n = min(KNN_FAN, Q.n[0] - x_lo);
-      const int x_first = (s == own[1]) ? own[0] - x_lo : 0;
-      for (int xx = 0; xx < x_n; ++xx) {
-        const int b = x_lo + (x_first + xx < x_n ? x_first + xx : x_first + xx - x_n);
-        if (__ballot(need(box_dist2(q, Q.lo[0][b], Q.hi[0][b]))) == 0ull) continue;
-        const int p0 = b * KNN_BOX;
-        const int cnt = min(KNN_BOX, Q.P - p0);
-        const float4 mine = Q.spts[p0 + (lane < cnt ? lane : 0)];
-        for (int j = 0; j < cnt; ++j) {
-          const float px = rl(mine.x, j), py = rl(mine.y, j), pz = rl(mine.z, j);
-          float d = dist2(px - q.x, py - q.y, pz - q.z);
-          d = (p0 + j == i) ? FLT_MAX : d;
-          // "if (best[k] > d) swap" insertion, branch-free
-          const float n0 = fminf(b0, d), c1 = fmaxf(b0, d);
-          const float n1 = fminf(b1, c1), c2 = fmaxf(b1, c1);
-          b0 = n0, b1 = n1, b2 = fminf(b2, c2);
+  for (int h0 = (own[2] / 64) * 64, hv = 0; hv < nh; hv += 64, h0 = (h0 + 64 < nh ? h0 + 64 : 0)) {
+    unsigned long long hrest;
+    unsigned long long hm = order_bits(children(2, h0, min(64, nh - h0)), own[2] - h0, hrest);
+    for (int pass_h = 0; pass_h < 2; ++pass_h, hm = hrest) {
+      while (hm) {
+        const int h = h0 + __builtin_ctzll(hm);
+        hm &= hm - 1;
+        if (!refine(2, h)) continue;
+        const int s_lo = h * KNN_FAN;
+        unsigned long long srest;
+        unsigned long long sm = order_bits(children(1, s_lo, min(KNN_FAN, Q.n[1] - s_lo)), own[1] - s_lo, srest);
+        for (int pass_s = 0; pass_s < 2; ++pass_s, sm = srest) {
+          while (sm) {
+            const int sidx = s_lo + __builtin_ctzll(sm);
+            sm &= sm - 1;
+            if (!refine(1, sidx)) continue;
+            const int x_lo = sidx * KNN_FAN;
+            unsigned long long xrest;
+            unsigned long long xm =
+                order_bits(children(0, x_lo, min(KNN_FAN, Q.n[0] - x_lo)), own[0] - x_lo, xrest);
+            for (int pass_x = 0; pass_x < 2; ++pass_x, xm = xrest) {
+              while (xm) {
+                const int bx = x_lo + __builtin_ctzll(xm);
+                xm &= xm - 1;
+                scan_box(bx);
+              }
+            }
+          }
         }
       }
     }
@@ -232,23 +344,26 @@ size_t knn_workspace_bytes(int P) {
 
 int launch_knn_mean_dist(int P, const float* points, float* out, void* ws, hipStream_t stream) {
   KnnWork w = KnnWork::carve(ws, P, nullptr);
-  hipLaunchKernelGGL(k_knn_bbox_init, dim3(1), dim3(64), 0, stream, w.bbox);
   const int blocks = div_up(P, 256);
-  hipLaunchKernelGGL(k_knn_bbox, dim3((unsigned)min(blocks, 2048)), dim3(256), 0, stream, P, points, w.bbox);
-  hipLaunchKernelGGL(k_knn_morton, dim3((unsigned)blocks), dim3(256), 0, stream, P, points, (const uint32_t*)w.bbox,
-                     w.keys[0]);
+  const int nparts = min(blocks, KNN_BBOX_BLOCKS);
+  hipLaunchKernelGGL(k_knn_bbox, dim3((unsigned)nparts), dim3(256), 0, stream, P, points, w.bbox);
+  hipLaunchKernelGGL(k_knn_morton, dim3((unsigned)blocks), dim3(256), 0, stream, P, points, nparts,
+                     (const float*)w.bbox, w.keys[0]);
   SegInfo seg{};
   seg.V = 1;
   seg.n[0] = (uint32_t)P;
   seg.start[0] = 0;
   const int r = seg_sort(w.keys, w.vals, true, seg, 0, 30, w.counts, w.totals, stream);
-  hipLaunchKernelGGL(k_knn_gather, dim3((unsigned)blocks), dim3(256), 0, stream, P, points,
-                     (const uint32_t*)w.vals[r], w.spts);
+  const int n_slots = w.n[0] * KNN_BOX;
+  hipLaunchKernelGGL(k_knn_gather, dim3((unsigned)div_up(n_slots, 256)), dim3(256), 0, stream, P, n_slots, points,
+                     (const uint32_t*)w.vals[r], w.bpts);
+  hipLaunchKernelGGL(k_knn_box_aabb, dim3((unsigned)div_up(w.n[0], 256)), dim3(256), 0, stream, P, w.n[0],
+                     (const float*)w.bpts, w.lo[0], w.hi[0]);
   const int fan[3] = {KNN_BOX, KNN_FAN, KNN_FAN};
-  int nchild = P;
-  const float4* clo = w.spts;
-  const float4* chi = w.spts;
-  for (int l = 0; l < 3; ++l) {
+  int nchild = w.n[0];
+  const float4* clo = w.lo[0];
+  const float4* chi = w.hi[0];
+  for (int l = 1; l < 3; ++l) {
     hipLaunchKernelGGL(k_knn_aabb, dim3((unsigned)div_up(w.n[l], 256)), dim3(256), 0, stream, nchild, fan[l], clo, chi,
                        w.n[l], w.lo[l], w.hi[l]);
     nchild = w.n[l];
@@ -257,7 +372,7 @@ int launch_knn_mean_dist(int P, const float* points, float* out, void* ws, hipSt
   }
   KnnQuery Q{};
   Q.P = P;
-  Q.spts = w.spts;
+  Q.bpts = w.bpts;
   for (int l = 0; l < 3; ++l) Q.lo[l] = w.lo[l], Q.hi[l] = w.hi[l], Q.n[l] = w.n[l];
   Q.order = w.vals[r];
   Q.out = out;
