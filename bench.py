@@ -54,6 +54,10 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-profile", action="store_true")
     ap.add_argument("--no-knn", action="store_true", help="skip the distCUDA2 timing line")
+    ap.add_argument("--workload", choices=["c3", "sugar"], default="c3",
+                    help="c3: the metric's scene (1M ball Gaussians, SH3); sugar: C5, ~2M surface-aligned SuGaR "
+                         "Gaussians (icosphere, 6 per face), 800x800, the SuGaR normal renderer's two passes "
+                         "(shs image + depth, then face normals as colors_precomp) with normal-from-depth")
     ap.add_argument("--epilogue", choices=["background", "shading"], default="background",
                     help="post-raster epilogue: the background renderer's composite (C3) or the MVDream shading "
                          "renderer's depth-normal + point-light material + composite")
@@ -83,6 +87,9 @@ class Replica:
         self.shs = leaf(scene["shs"])
         self.sh_degree = int(scene["sh_degree"])
         self.params = [self.means3D, self.scales, self.rotations, self.opacities, self.shs]
+        if "normals" in scene:  # SuGaR: per-Gaussian face normals, rasterized as colors_precomp
+            self.normals = leaf(scene["normals"])
+            self.params.append(self.normals)
 
     def zero_grad(self):
         for p in self.params:
@@ -175,6 +182,33 @@ def render_views(rep: Replica, settings, bg_img, shade=None):
     return comp, depth, alpha, radii
 
 
+def render_views_sugar(rep: Replica, settings, shade):
+    """C5: the SuGaR normal renderer (renderer/diff_sugar_rasterizer_normal.py:157-213) over a view set:
+    pass 1 (SH colours) -> render, depth, alpha; normal-from-depth maps (fused HIP epilogue); pass 2 with
+    the face normals as colors_precomp and a fresh zero means2D (no viewspace gradient, :179-189); then
+    normalize, flip x/y, normal map and the alpha > 0.99 gradient masks in torch (:190-197)."""
+    from diff_gaussian_rasterization.batched import rasterize_views
+    from diff_gaussian_rasterization.shading import depth_normal_views
+
+    P = rep.means3D.shape[0]
+    dev = rep.means3D.device
+    m2 = [torch.zeros((P, 3), device=dev, requires_grad=True) for _ in settings]
+    color, radii, depth, alpha = rasterize_views(settings, rep.means3D, m2, rep.opacities, shs=rep.shs,
+                                                 scales=rep.scales, rotations=rep.rotations)
+    rays_o, rays_d, _ = shade
+    _, nmap_dist = depth_normal_views(depth, alpha, rays_o, rays_d)
+    zeros = [torch.zeros((P, 3), device=dev) for _ in settings]
+    normal, _, _, _ = rasterize_views(settings, rep.means3D, zeros, rep.opacities, colors_precomp=rep.normals,
+                                      scales=rep.scales, rotations=rep.rotations)
+    normal = torch.nn.functional.normalize(normal, dim=1)
+    normal = torch.cat([-normal[:, :2], normal[:, 2:]], 1)
+    nmap = normal * 0.5 * alpha + 0.5
+    mask = (alpha > 0.99).expand_as(nmap)
+    nmap = torch.where(mask, nmap, nmap.detach())
+    depth = torch.where(alpha > 0.99, depth, depth.detach())
+    return color.clamp(0, 1), depth, alpha, nmap, nmap_dist
+
+
 def read_traffic(path, kernel):
     """HBM bytes per launch of `kernel` from a committed PMC summary (FETCH_SIZE x2 gfx950 correction +
     WRITE_SIZE, separate --pmc passes; profiles/summarize.py), or None."""
@@ -258,7 +292,13 @@ def main():
     from diff_gaussian_rasterization.view_shard import all_gather_views, allreduce_grads, shard_range
 
     t_setup = time.perf_counter()
-    scene = gs.make_scene(args.gaussians, sh_degree=args.sh_degree, seed=0)  # identical replica on every rank
+    if args.workload == "sugar":
+        if args.res == 1024:
+            args.res = 800
+        scene = gs.make_sugar_scene(7, sh_degree=args.sh_degree, seed=0)
+        args.gaussians = scene["means3D"].shape[0]
+    else:
+        scene = gs.make_scene(args.gaussians, sh_degree=args.sh_degree, seed=0)  # identical replica on every rank
     rep = Replica(scene, device)
     cams = build_views(args.views, args.res, device)
     v0, v1 = shard_range(args.views, world, rank)
@@ -282,13 +322,18 @@ def main():
 
     shade = None
     up_n = None
-    if args.epilogue == "shading":
+    if args.epilogue == "shading" or args.workload == "sugar":
         sys.path.insert(0, os.path.join(ROOT, "tests"))  # per-view path: the reference's torch epilogue
         shade = shading_inputs(mine, device)
         up_n = torch.randn((len(mine), 3, H, W), generator=gen, device=device)
 
     def step():
-        if args.path == "batched":
+        if args.workload == "sugar":
+            outs = render_views_sugar(rep, settings, shade)
+            if world > 1:
+                all_gather_views(outs[0], args.views)
+            torch.autograd.backward(outs, (up_c, up_d, up_a, up_n, up_n))
+        elif args.path == "batched":
             outs = render_views(rep, settings, bg_img, shade)
             c, d, a = outs[:3]
             if world > 1:
@@ -370,7 +415,9 @@ def main():
         "dtype": "fp32",
         "data": "synthetic (seeded scene per SURVEY.md §8d; no datasets offline)",
         "config": {
-            "workload": ("C3 per view (1M Gaussians, 1024x1024, SH3, background path)" if args.epilogue ==
+            "workload": "C5: ~2M surface-aligned SuGaR Gaussians (icosphere, 6 per face), 800x800, SH3, SuGaR "
+                        "normal renderer (2 passes + normal-from-depth) over a 64-view orbit batch, fwd+bwd" if args.workload == "sugar" else
+                        ("C3 per view (1M Gaussians, 1024x1024, SH3, background path)" if args.epilogue ==
                          "background" else "1M Gaussians, 1024x1024, SH3, MVDream shading path (depth-normal, "
                          "point-light material, composite)") + " over the C4 64-view orbit batch, fwd+bwd (fixed random upstream image gradients) + image all-gather + "
                         "gradient all-reduce",
