@@ -157,6 +157,14 @@ def settings_for(rep: Replica, cam, bg_zero):
                                          campos=cam["campos"], prefiltered=False, debug=False)
 
 
+def placeholders(rep: Replica, V: int):
+    """The views' screen-space placeholders (renderer/diff_gaussian_rasterizer.py:73-81 creates one zero
+    (P, 3) tensor per view): V leaves that are views of one zeroed (V, P, 3) buffer — one fill kernel for
+    the batch instead of V."""
+    buf = torch.zeros((V, rep.means3D.shape[0], 3), device=rep.means3D.device)
+    return [buf[v].requires_grad_(True) for v in range(V)]
+
+
 SHADE_KA, SHADE_KD = (0.1, 0.1, 0.1), (0.9, 0.9, 0.9)  # the material's default ambient / diffuse colours
 
 
@@ -167,8 +175,7 @@ def render_views(rep: Replica, settings, bg_img, shade=None):
     from diff_gaussian_rasterization.batched import rasterize_views
     from diff_gaussian_rasterization.composite import composite_background
 
-    P = rep.means3D.shape[0]
-    m2 = [torch.zeros((P, 3), device=rep.means3D.device, requires_grad=True) for _ in settings]
+    m2 = placeholders(rep, len(settings))
     color, radii, depth, alpha = rasterize_views(settings, rep.means3D, m2, rep.opacities, shs=rep.shs,
                                                  scales=rep.scales, rotations=rep.rotations)
     if shade is not None:
@@ -192,7 +199,7 @@ def render_views_sugar(rep: Replica, settings, shade):
 
     P = rep.means3D.shape[0]
     dev = rep.means3D.device
-    m2 = [torch.zeros((P, 3), device=dev, requires_grad=True) for _ in settings]
+    m2 = placeholders(rep, len(settings))
     color, radii, depth, alpha = rasterize_views(settings, rep.means3D, m2, rep.opacities, shs=rep.shs,
                                                  scales=rep.scales, rotations=rep.rotations)
     rays_o, rays_d, _ = shade

@@ -3,7 +3,7 @@
 // Replaces FORWARD::preprocessCUDA of the reference rasterizer [EXT]: frustum cull
 // (view z <= 0.2), projection, 3D covariance, EWA 2D covariance (+0.3 low-pass), conic,
 // 3-sigma radius, 16x16 tile rect, SH -> RGB (clamped at 0, flags kept for backward).
-// A block owns 256 Gaussians (one per thread) for up to GSR_PRE_VIEWS views of the set: the
+// A block owns 128 Gaussians (two threads each) for up to GSR_PRE_VIEWS views of the set: the
 // Gaussians' parameters are read once per block (SH staged through LDS with coalesced 16-byte loads
 // instead of 3M strided dword loads per thread), the 3D covariance is built once, and the views
 // are walked in turn.  Writes per (view, Gaussian) the 64-byte render record (incl. tile rect and
@@ -14,24 +14,30 @@
 
 namespace gsr {
 
-// Views handled by one block (the Gaussians' view-independent work and SH staging are shared).
+// Views handled by one block (the Gaussians' view-independent work and SH staging are shared): the
+// block's 256 threads are 128 Gaussians x 2 halves of the views, so the SH staging (128 x (3M + 1)
+// floats, 24.6 KB at SH3) allows 6 blocks = 6 waves per SIMD instead of 3 with 256 Gaussians.
 #define GSR_PRE_VIEWS 8
-#define GSR_PRE_LDS_FLOATS (16 * 1024)  // SH staging up to 64 KB (M <= 21); larger M reads SH from HBM
+#define GSR_PRE_GAUSS 128
+#define GSR_PRE_LDS_FLOATS (8 * 1024)  // SH staging up to 32 KB (M <= 21); larger M reads SH from HBM
 
 __global__ __launch_bounds__(256) void k_preprocess(PreprocessArgs a, SetCams cams, GeomState g) {
-  extern __shared__ float s_sh[];  // [256][3M + 1] this block's SH coefficients (odd stride)
+  extern __shared__ float s_sh[];  // [128][3M + 1] this block's SH coefficients (odd stride)
   const int nvc = (a.V + GSR_PRE_VIEWS - 1) / GSR_PRE_VIEWS;
   const int vc = blockIdx.x % nvc;
-  const int idx0 = (blockIdx.x / nvc) * 256;
+  const int idx0 = (blockIdx.x / nvc) * GSR_PRE_GAUSS;
   const int t = threadIdx.x;
-  const int idx = idx0 + t;
-  const int v0 = vc * GSR_PRE_VIEWS, v1 = min(a.V, v0 + GSR_PRE_VIEWS);
+  const int gl = t % GSR_PRE_GAUSS, half = t / GSR_PRE_GAUSS;
+  const int idx = idx0 + gl;
+  const int vb = vc * GSR_PRE_VIEWS, ve = min(a.V, vb + GSR_PRE_VIEWS);
+  const int vh = (ve - vb + 1) / 2;
+  const int v0 = vb + half * vh, v1 = half == 0 ? min(ve, vb + vh) : ve;
   const int nsh = a.colors_precomp == nullptr ? 3 * a.M : 0;
   const int sstride = nsh + 1;
-  const bool staged = nsh > 0 && 256 * sstride <= GSR_PRE_LDS_FLOATS;
+  const bool staged = nsh > 0 && GSR_PRE_GAUSS * sstride <= GSR_PRE_LDS_FLOATS;
   if (staged) {
     // coalesced 16-byte loads of the block's contiguous SH slice (256 * 3M floats, 16-B aligned)
-    const int n = min(256, a.P - idx0) * nsh;
+    const int n = min(GSR_PRE_GAUSS, a.P - idx0) * nsh;
     const float4* src = reinterpret_cast<const float4*>(a.shs + (size_t)idx0 * nsh);
     for (int e4 = t; e4 * 4 < n; e4 += 256) {
       const float4 q = src[e4];
@@ -62,7 +68,7 @@ __global__ __launch_bounds__(256) void k_preprocess(PreprocessArgs a, SetCams ca
   float3 rgb_pre = make_float3(0.f, 0.f, 0.f);
   if (a.colors_precomp != nullptr)
     rgb_pre = make_float3(a.colors_precomp[3 * idx], a.colors_precomp[3 * idx + 1], a.colors_precomp[3 * idx + 2]);
-  const float* my_sh = staged ? s_sh + t * sstride : a.shs + (size_t)idx * nsh;
+  const float* my_sh = staged ? s_sh + gl * sstride : a.shs + (size_t)idx * nsh;
   const int gx = (a.W + GSR_TILE_X - 1) / GSR_TILE_X;
   const int gy = (a.H + GSR_TILE_Y - 1) / GSR_TILE_Y;
 
@@ -136,9 +142,10 @@ __global__ __launch_bounds__(256) void k_preprocess(PreprocessArgs a, SetCams ca
 void launch_preprocess(const PreprocessArgs& a, const SetCams& cams, const GeomState& g, hipStream_t stream) {
   if (a.P <= 0 || a.V <= 0) return;
   const int nvc = (a.V + GSR_PRE_VIEWS - 1) / GSR_PRE_VIEWS;
-  const size_t want = a.colors_precomp == nullptr ? (size_t)256 * (3 * a.M + 1) : 0;
+  const size_t want = a.colors_precomp == nullptr ? (size_t)GSR_PRE_GAUSS * (3 * a.M + 1) : 0;
   const size_t lds = want <= GSR_PRE_LDS_FLOATS ? sizeof(float) * want : 0;
-  hipLaunchKernelGGL(k_preprocess, dim3(nvc * ((a.P + 255) / 256)), dim3(256), lds, stream, a, cams, g);
+  hipLaunchKernelGGL(k_preprocess, dim3(nvc * ((a.P + GSR_PRE_GAUSS - 1) / GSR_PRE_GAUSS)), dim3(256), lds, stream, a,
+                     cams, g);
 }
 
 }  // namespace gsr
