@@ -165,6 +165,7 @@ def placeholders(rep: Replica, V: int):
     return [buf[v].requires_grad_(True) for v in range(V)]
 
 
+COMPOSITE = os.environ.get("GSR_BENCH_COMPOSITE", "fused")  # "separate": gsr_composite_* as its own pass
 SHADE_KA, SHADE_KD = (0.1, 0.1, 0.1), (0.9, 0.9, 0.9)  # the material's default ambient / diffuse colours
 
 
@@ -176,16 +177,22 @@ def render_views(rep: Replica, settings, bg_img, shade=None):
     from diff_gaussian_rasterization.composite import composite_background
 
     m2 = placeholders(rep, len(settings))
-    color, radii, depth, alpha = rasterize_views(settings, rep.means3D, m2, rep.opacities, shs=rep.shs,
-                                                 scales=rep.scales, rotations=rep.rotations)
     if shade is not None:
         from diff_gaussian_rasterization.shading import shade_views
 
+        color, radii, depth, alpha = rasterize_views(settings, rep.means3D, m2, rep.opacities, shs=rep.shs,
+                                                     scales=rep.scales, rotations=rep.rotations)
         rays_o, rays_d, light = shade
         render, normal, depth_m = shade_views(color, depth, alpha, rays_o, rays_d, bg_img, light,
                                               SHADE_KA, SHADE_KD, "diffuse")
         return render, depth_m, alpha, radii, normal
-    comp = composite_background(color, alpha, bg_img)
+    if COMPOSITE == "separate":
+        color, radii, depth, alpha = rasterize_views(settings, rep.means3D, m2, rep.opacities, shs=rep.shs,
+                                                     scales=rep.scales, rotations=rep.rotations)
+        return composite_background(color, alpha, bg_img), depth, alpha, radii
+    # the composite + clamp fused into the forward / backward blends (bit-identical to the separate pass)
+    comp, radii, depth, alpha = rasterize_views(settings, rep.means3D, m2, rep.opacities, shs=rep.shs,
+                                                scales=rep.scales, rotations=rep.rotations, background=bg_img)
     return comp, depth, alpha, radii
 
 

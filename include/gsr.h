@@ -164,6 +164,29 @@ int gsr_set_backward(int V, int P, int degree, int M, const int* num_rendered, i
                      float* dL_dopacity, float* dL_dmeans3D, float* dL_dcov3D, float* dL_dsh,
                      float* dL_dscales, float* dL_drotations, int accumulate, void* work, size_t work_bytes,
                      void* stream);
+/*
+ * The background renderer's composite fused into the blends (replaces gsr_set_render + gsr_composite_forward
+ * and gsr_composite_backward + gsr_set_backward for renderer/diff_gaussian_rasterizer_background.py:129-132,139):
+ * bg_images (V, H, W, 3) are the background network's outputs; out_render (V, 3, H, W) =
+ * clamp(color + (1 - alpha) bg, 0, 1), bit-identical to the torch expression on the stored outputs; the
+ * colour / depth / alpha outputs are written as by gsr_set_render.  The backward takes dL/drender in
+ * place of dL/dcolor, the forward's colour output, and forms dL/dbg (NULL: not formed) in the blend's
+ * per-pixel prologue (clamp mask, dL/dalpha += -sum_c g_c bg_c, dL/dbg = g (1 - alpha)).
+ */
+int gsr_set_render_composite(int V, int P, const int* num_rendered, int width, int height, const float* const* bgs,
+                             void* geom, void* binning, void* image, float* out_color, float* out_depth,
+                             float* out_alpha, const float* bg_images, float* out_render, void* stream);
+int gsr_set_backward_composite(int V, int P, int degree, int M, const int* num_rendered, int width, int height,
+                               const float* const* bgs, const float* means3D, const float* scales,
+                               float scale_modifier, const float* rotations, const float* shs,
+                               const float* cov3D_precomp, const float* const* viewmatrices,
+                               const float* const* projmatrices, const float* const* campos, const float* tanfovx,
+                               const float* tanfovy, const int* radii, const void* geom, const void* binning,
+                               const void* image, const float* bg_images, const float* color,
+                               const float* dL_drender, const float* dL_ddepth, const float* dL_dalpha,
+                               float* dL_dbg, float* dL_dmeans2D, float* dL_dcolors, float* dL_dopacity,
+                               float* dL_dmeans3D, float* dL_dcov3D, float* dL_dsh, float* dL_dscales,
+                               float* dL_drotations, int accumulate, void* work, size_t work_bytes, void* stream);
 
 /*
  * Optional phase timing with HIP events recorded on the launch stream around each phase's kernels.

@@ -61,3 +61,51 @@ def test_composite_symbols_exported():
 
     lib = _C.load_library()
     assert hasattr(lib, "gsr_composite_forward") and hasattr(lib, "gsr_composite_backward")
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("V,H,W", [(3, 64, 48), (2, 40, 37)])
+def test_fused_composite_matches_unfused(V, H, W):
+    """rasterize_views(..., background=bg) == composite_background(rasterize_views(...)): forward bit-identical,
+    gradients of every Gaussian parameter and of the background image identical."""
+    import gsr_synthetic as gs
+    from gsr_testutil import make_camera
+    from diff_gaussian_rasterization import GaussianRasterizationSettings
+    from diff_gaussian_rasterization.batched import rasterize_views
+    from diff_gaussian_rasterization.composite import composite_background
+
+    scene = gs.make_scene(3000, sh_degree=3, seed=V)
+    dev = "cuda"
+    settings = []
+    for v in range(V):
+        cam = make_camera(W, H, azimuth=40.0 * v)
+        settings.append(GaussianRasterizationSettings(
+            image_height=H, image_width=W, tanfovx=cam["tanx"], tanfovy=cam["tany"],
+            bg=torch.zeros(3, device=dev), scale_modifier=1.0, viewmatrix=torch.tensor(cam["view"], device=dev),
+            projmatrix=torch.tensor(cam["proj"], device=dev), sh_degree=3,
+            campos=torch.tensor(cam["campos"], device=dev), prefiltered=False, debug=False))
+    g = torch.Generator(device=dev).manual_seed(7)
+    bg = torch.rand((V, H, W, 3), generator=g, device=dev) * 1.2 - 0.1  # clamp bounds reached
+    ups = [torch.randn((V, 3, H, W), generator=g, device=dev), torch.randn((V, 1, H, W), generator=g, device=dev),
+           torch.randn((V, 1, H, W), generator=g, device=dev)]
+    res = []
+    for fused in (False, True):
+        t = {k: torch.tensor(scene[k], device=dev, requires_grad=True)
+             for k in ("means3D", "scales", "rotations", "opacities", "shs")}
+        b = bg.clone().requires_grad_(True)
+        m2 = [torch.zeros((3000, 3), device=dev, requires_grad=True) for _ in range(V)]
+        kw = dict(shs=t["shs"], scales=t["scales"], rotations=t["rotations"])
+        if fused:
+            out, _, depth, alpha = rasterize_views(settings, t["means3D"], m2, t["opacities"], background=b, **kw)
+        else:
+            color, _, depth, alpha = rasterize_views(settings, t["means3D"], m2, t["opacities"], **kw)
+            out = composite_background(color, alpha, b)
+        torch.autograd.backward((out, depth, alpha), ups)
+        res.append((out.detach(), {k: v.grad for k, v in t.items()}, b.grad, [m.grad for m in m2]))
+    (o0, g0, b0, m0), (o1, g1, b1, m1) = res
+    assert torch.equal(o0, o1)
+    assert torch.equal(b0, b1)
+    for k in g0:
+        assert torch.equal(g0[k], g1[k]), k
+    for a, c in zip(m0, m1):
+        assert torch.equal(a, c)

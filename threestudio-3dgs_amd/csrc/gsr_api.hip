@@ -376,8 +376,9 @@ int gsr_set_num_rendered(int V, const void* geom, int P, int* num_rendered, int*
   return gsr_set_num_rendered_ex(V, geom, P, num_rendered, num_visible, nullptr, stream);
 }
 
-int gsr_set_render(int V, int P, const int* K, int width, int height, const float* const* bgs, void* geom,
-                   void* binning, void* image, float* out_color, float* out_depth, float* out_alpha, void* stream) {
+static int set_render(int V, int P, const int* K, int width, int height, const float* const* bgs, void* geom,
+                      void* binning, void* image, float* out_color, float* out_depth, float* out_alpha,
+                      const float* comp_bg, float* out_render, void* stream) {
   if (check_set(V, P) != GSR_OK) return GSR_EINVAL;
   if (width <= 0 || height <= 0) return fail(GSR_EINVAL, "%s", "bad sizes");
   if (K == nullptr || bgs == nullptr || geom == nullptr || binning == nullptr || image == nullptr ||
@@ -408,6 +409,10 @@ int gsr_set_render(int V, int P, const int* K, int width, int height, const floa
   {
     PhaseScope ps(GSR_PHASE_RENDER_FWD, s);
     RenderSet rs;
+    rs.cbg = comp_bg;
+    rs.comp = out_render;
+    rs.ccolor = nullptr;
+    rs.dcbg = nullptr;
     rs.V = V;
     rs.v0 = 0;
     rs.P = P;
@@ -427,15 +432,30 @@ int gsr_set_render(int V, int P, const int* K, int width, int height, const floa
   return last_launch();
 }
 
-int gsr_set_backward(int V, int P, int degree, int M, const int* K, int width, int height, const float* const* bgs,
-                     const float* means3D, const float* scales, float scale_modifier, const float* rotations,
-                     const float* shs, const float* cov3D_precomp, const float* const* viewmatrices,
-                     const float* const* projmatrices, const float* const* campos, const float* tanfovx,
-                     const float* tanfovy, const int* radii, const void* geom, const void* binning,
-                     const void* image, const float* dL_dcolor, const float* dL_ddepth, const float* dL_dalpha,
-                     float* dL_dmeans2D, float* dL_dcolors, float* dL_dopacity, float* dL_dmeans3D,
-                     float* dL_dcov3D, float* dL_dsh, float* dL_dscales, float* dL_drotations, int accumulate,
-                     void* work, size_t work_bytes, void* stream) {
+int gsr_set_render(int V, int P, const int* K, int width, int height, const float* const* bgs, void* geom,
+                   void* binning, void* image, float* out_color, float* out_depth, float* out_alpha, void* stream) {
+  return set_render(V, P, K, width, height, bgs, geom, binning, image, out_color, out_depth, out_alpha, nullptr,
+                    nullptr, stream);
+}
+
+int gsr_set_render_composite(int V, int P, const int* K, int width, int height, const float* const* bgs, void* geom,
+                             void* binning, void* image, float* out_color, float* out_depth, float* out_alpha,
+                             const float* bg_images, float* out_render, void* stream) {
+  if (bg_images == nullptr || out_render == nullptr) return fail(GSR_EINVAL, "%s", "null composite argument");
+  return set_render(V, P, K, width, height, bgs, geom, binning, image, out_color, out_depth, out_alpha, bg_images,
+                    out_render, stream);
+}
+
+static int set_backward(int V, int P, int degree, int M, const int* K, int width, int height, const float* const* bgs,
+                        const float* means3D, const float* scales, float scale_modifier, const float* rotations,
+                        const float* shs, const float* cov3D_precomp, const float* const* viewmatrices,
+                        const float* const* projmatrices, const float* const* campos, const float* tanfovx,
+                        const float* tanfovy, const int* radii, const void* geom, const void* binning,
+                        const void* image, const float* dL_dcolor, const float* dL_ddepth, const float* dL_dalpha,
+                        float* dL_dmeans2D, float* dL_dcolors, float* dL_dopacity, float* dL_dmeans3D,
+                        float* dL_dcov3D, float* dL_dsh, float* dL_dscales, float* dL_drotations, int accumulate,
+                        void* work, size_t work_bytes, const float* comp_bg, const float* color, float* dL_dbg,
+                        void* stream) {
   if (check_set(V, P) != GSR_OK) return GSR_EINVAL;
   if (width <= 0 || height <= 0) return fail(GSR_EINVAL, "%s", "bad sizes");
   if (P == 0) return last_launch();
@@ -475,6 +495,10 @@ int gsr_set_backward(int V, int P, int degree, int M, const int* K, int width, i
       return fail(GSR_EINVAL, "%s", "backward work buffer smaller than one view's gradient rows");
     BackwardState bw = BackwardState::carve(work, rows);
     RenderSet rs;
+    rs.cbg = comp_bg ? comp_bg + (size_t)g0 * HW * 3 : nullptr;
+    rs.comp = nullptr;
+    rs.ccolor = color ? color + (size_t)g0 * 3 * HW : nullptr;
+    rs.dcbg = dL_dbg ? dL_dbg + (size_t)g0 * HW * 3 : nullptr;
     rs.V = g1 - g0;
     rs.v0 = g0;
     rs.P = P;
@@ -529,6 +553,41 @@ int gsr_set_backward(int V, int P, int degree, int M, const int* K, int width, i
     g0 = g1;
   }
   return last_launch();
+}
+
+int gsr_set_backward(int V, int P, int degree, int M, const int* K, int width, int height, const float* const* bgs,
+                     const float* means3D, const float* scales, float scale_modifier, const float* rotations,
+                     const float* shs, const float* cov3D_precomp, const float* const* viewmatrices,
+                     const float* const* projmatrices, const float* const* campos, const float* tanfovx,
+                     const float* tanfovy, const int* radii, const void* geom, const void* binning,
+                     const void* image, const float* dL_dcolor, const float* dL_ddepth, const float* dL_dalpha,
+                     float* dL_dmeans2D, float* dL_dcolors, float* dL_dopacity, float* dL_dmeans3D,
+                     float* dL_dcov3D, float* dL_dsh, float* dL_dscales, float* dL_drotations, int accumulate,
+                     void* work, size_t work_bytes, void* stream) {
+  return set_backward(V, P, degree, M, K, width, height, bgs, means3D, scales, scale_modifier, rotations, shs,
+                      cov3D_precomp, viewmatrices, projmatrices, campos, tanfovx, tanfovy, radii, geom, binning, image,
+                      dL_dcolor, dL_ddepth, dL_dalpha, dL_dmeans2D, dL_dcolors, dL_dopacity, dL_dmeans3D, dL_dcov3D,
+                      dL_dsh, dL_dscales, dL_drotations, accumulate, work, work_bytes, nullptr, nullptr, nullptr,
+                      stream);
+}
+
+int gsr_set_backward_composite(int V, int P, int degree, int M, const int* K, int width, int height,
+                               const float* const* bgs, const float* means3D, const float* scales,
+                               float scale_modifier, const float* rotations, const float* shs,
+                               const float* cov3D_precomp, const float* const* viewmatrices,
+                               const float* const* projmatrices, const float* const* campos, const float* tanfovx,
+                               const float* tanfovy, const int* radii, const void* geom, const void* binning,
+                               const void* image, const float* bg_images, const float* color,
+                               const float* dL_drender, const float* dL_ddepth, const float* dL_dalpha,
+                               float* dL_dbg, float* dL_dmeans2D, float* dL_dcolors, float* dL_dopacity,
+                               float* dL_dmeans3D, float* dL_dcov3D, float* dL_dsh, float* dL_dscales,
+                               float* dL_drotations, int accumulate, void* work, size_t work_bytes, void* stream) {
+  if (bg_images == nullptr || color == nullptr) return fail(GSR_EINVAL, "%s", "null composite argument");
+  return set_backward(V, P, degree, M, K, width, height, bgs, means3D, scales, scale_modifier, rotations, shs,
+                      cov3D_precomp, viewmatrices, projmatrices, campos, tanfovx, tanfovy, radii, geom, binning, image,
+                      dL_drender, dL_ddepth, dL_dalpha, dL_dmeans2D, dL_dcolors, dL_dopacity, dL_dmeans3D, dL_dcov3D,
+                      dL_dsh, dL_dscales, dL_drotations, accumulate, work, work_bytes, bg_images, color, dL_dbg,
+                      stream);
 }
 
 // ---- one view (the reference's per-call interface): a set of one --------------------------

@@ -45,6 +45,12 @@ struct RenderSet {
   uint32_t inst_start[GSR_SET_MAX];
   uint32_t row_start[GSR_SET_MAX];
   const float* bg[GSR_SET_MAX];
+  // fused background composite (renderer/diff_gaussian_rasterizer_background.py:129-132,139), null = off.
+  // Pointers at the launch's first view; per view (H, W, 3) background images / (3, H, W) planes.
+  const float* cbg;  // background network images (V, H, W, 3)
+  float* comp;       // forward: clamp(color + (1 - alpha) bg, 0, 1) (V, 3, H, W)
+  const float* ccolor;  // backward: the forward's colour (V, 3, H, W); dL_dcolor then holds dL/dcomp
+  float* dcbg;       // backward: dL/dbg (V, H, W, 3) or null
 };
 void launch_render_forward(const RenderSet& rs, const GeomState& g, const uint32_t* sorted_gauss,
                            const ImageState& img, float* out_color, float* out_depth, float* out_alpha,

@@ -222,6 +222,16 @@ __global__ __launch_bounds__(64) void k_render_fwd(RenderSet rs,
     out_color[2 * HW + pid] = Cb + T * bg[2];
     out_depth[pid] = D;
     out_alpha[pid] = 1.0f - T;
+    if (rs.cbg != nullptr) {
+      // fused composite, the same operations as the torch epilogue on the stored outputs (bit-identical)
+#pragma clang fp contract(off)
+      const float am = 1.0f - (1.0f - T);
+      const float* bgi = rs.cbg + ((size_t)v * HW + pid) * 3;
+      float* cp = rs.comp + (size_t)v * 3 * HW + pid;
+      cp[0] = fminf(fmaxf((Cr + T * bg[0]) + am * bgi[0], 0.0f), 1.0f);
+      cp[HW] = fminf(fmaxf((Cg + T * bg[1]) + am * bgi[1], 0.0f), 1.0f);
+      cp[2 * HW] = fminf(fmaxf((Cb + T * bg[2]) + am * bgi[2], 0.0f), 1.0f);
+    }
   }
   uint32_t mc = last_contributor;
 #pragma unroll
@@ -386,6 +396,24 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5, 8))) voi
     dpix[2] = dL_dcolor[2 * HW + pid];
     if (dL_ddepth) dpix_d = dL_ddepth[pid];
     if (dL_dalpha) dpix_a = dL_dalpha[pid];
+    if (rs.cbg != nullptr) {
+      // fused composite backward: dL/dcomp masked by the clamp -> dL/dcolor, dL/dalpha, dL/dbg
+#pragma clang fp contract(off)
+      const float am = 1.0f - (1.0f - T_final);
+      const float* bgi = rs.cbg + ((size_t)v * HW + pid) * 3;
+      const float* col = rs.ccolor + (size_t)v * 3 * HW + pid;
+      float da = 0.0f;
+#pragma unroll
+      for (int ch = 0; ch < 3; ++ch) {
+        const float b = bgi[ch];
+        const float pre = col[(size_t)ch * HW] + am * b;
+        const float gch = (pre >= 0.0f && pre <= 1.0f) ? dpix[ch] : 0.0f;
+        dpix[ch] = gch;
+        da -= gch * b;
+        if (rs.dcbg != nullptr) rs.dcbg[((size_t)v * HW + pid) * 3 + ch] = gch * am;
+      }
+      dpix_a = da + dpix_a;
+    }
   }
   const float bg_dot = bg[0] * dpix[0] + bg[1] * dpix[1] + bg[2] * dpix[2];
 

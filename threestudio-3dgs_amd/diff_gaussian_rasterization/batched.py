@@ -55,7 +55,7 @@ class _ViewSet:
 class _RasterizeViews(torch.autograd.Function):
     @staticmethod
     def forward(ctx, settings_list, means3D, sh, colors_precomp, opacities, scales, rotations, cov3D_precomp,
-                *means2D):
+                composite_bg, *means2D):
         lib = _C.load_library()
         V = len(settings_list)
         dev = means3D.device
@@ -76,6 +76,10 @@ class _RasterizeViews(torch.autograd.Function):
         stream = _C._stream(dev)
         fopt = dict(dtype=torch.float32, device=dev)
         color = torch.empty((V, 3, H, W), **fopt)
+        cbg = None
+        if composite_bg is not None:
+            cbg = _C._f32(composite_bg, "background", dev).reshape(V, H, W, 3)
+            render = torch.empty((V, 3, H, W), **fopt)
         depth = torch.empty((V, 1, H, W), **fopt)
         alpha = torch.empty((V, 1, H, W), **fopt)
         radii = torch.empty((V, P), dtype=torch.int32, device=dev)
@@ -105,19 +109,26 @@ class _RasterizeViews(torch.autograd.Function):
             Karr = _arr(ctypes.c_int, vs.K)
             vs.binning = torch.empty(int(lib.gsr_set_binning_bytes(vs.V, P, Karr, W, H)), dtype=torch.uint8, device=dev)
             vs.image = torch.empty(int(lib.gsr_set_image_bytes(vs.V, W, H)), dtype=torch.uint8, device=dev)
-            _C._check(lib.gsr_set_render(vs.V, P, Karr, W, H, _ptrs([c[3] for c in vs.cams]), p(vs.geom),
-                                         p(vs.binning), p(vs.image), p(color[vs.lo:vs.hi]), p(depth[vs.lo:vs.hi]),
-                                         p(alpha[vs.lo:vs.hi]), stream))
+            sl = slice(vs.lo, vs.hi)
+            if cbg is None:
+                _C._check(lib.gsr_set_render(vs.V, P, Karr, W, H, _ptrs([c[3] for c in vs.cams]), p(vs.geom),
+                                             p(vs.binning), p(vs.image), p(color[sl]), p(depth[sl]), p(alpha[sl]),
+                                             stream))
+            else:
+                _C._check(lib.gsr_set_render_composite(
+                    vs.V, P, Karr, W, H, _ptrs([c[3] for c in vs.cams]), p(vs.geom), p(vs.binning), p(vs.image),
+                    p(color[sl]), p(depth[sl]), p(alpha[sl]), p(cbg[sl]), p(render[sl]), stream))
         ctx.settings = settings_list
         ctx.sets = sets
-        ctx.save_for_backward(m3, shc, col, sc, rot, c3, radii)
+        ctx.bg_shape = tuple(composite_bg.shape) if composite_bg is not None else None
+        ctx.save_for_backward(m3, shc, col, sc, rot, c3, radii, cbg, color if cbg is not None else None)
         ctx.mark_non_differentiable(radii)
-        return color, radii, depth, alpha
+        return (color if cbg is None else render), radii, depth, alpha
 
     @staticmethod
     def backward(ctx, g_color, _g_radii, g_depth, g_alpha):
         lib = _C.load_library()
-        m3, shc, col, sc, rot, c3, radii = ctx.saved_tensors
+        m3, shc, col, sc, rot, c3, radii, cbg, color = ctx.saved_tensors
         settings = ctx.settings
         V = len(settings)
         s0 = settings[0]
@@ -134,7 +145,10 @@ class _RasterizeViews(torch.autograd.Function):
         d_c3 = torch.empty((P, 6), **fopt) if c3 is not None else None
         d_sc = torch.empty((P, 3), **fopt) if c3 is None else None
         d_rot = torch.empty((P, 4), **fopt) if c3 is None else None
+        d_bg = torch.empty_like(cbg) if cbg is not None and ctx.needs_input_grad[8] else None
         if P == 0:
+            if d_bg is not None:
+                d_bg.zero_()
             for t in (d_m2, d_m3, d_op, d_col, d_sh, d_c3, d_sc, d_rot):
                 if t is not None:
                     t.zero_()
@@ -151,13 +165,25 @@ class _RasterizeViews(torch.autograd.Function):
                 work = torch.empty(max(largest, min(need, WORK_BUDGET)), dtype=torch.uint8, device=dev)
                 views, projs, campos, tx, ty = vs.cam_arrays()
                 sl = slice(vs.lo, vs.hi)
-                _C._check(lib.gsr_set_backward(
-                    vs.V, P, int(s0.sh_degree), M, Karr, W, H, _ptrs([c[3] for c in vs.cams]), p(m3), p(sc),
-                    float(s0.scale_modifier), p(rot), p(shc), p(c3), views, projs, campos, tx, ty, p(radii[sl]),
-                    p(vs.geom), p(vs.binning), p(vs.image), p(gc[sl]), p(gd[sl]) if gd is not None else None,
-                    p(ga[sl]) if ga is not None else None, p(d_m2[sl]), p(d_col), p(d_op), p(d_m3), p(d_c3), p(d_sh),
-                    p(d_sc), p(d_rot), 1 if si > 0 else 0, p(work), work.numel(), stream))
-        grads = [None, d_m3, d_sh, d_col, d_op, d_sc, d_rot, d_c3] + [d_m2[v] for v in range(V)]
+                gdp = p(gd[sl]) if gd is not None else None
+                gap = p(ga[sl]) if ga is not None else None
+                if cbg is None:
+                    _C._check(lib.gsr_set_backward(
+                        vs.V, P, int(s0.sh_degree), M, Karr, W, H, _ptrs([c[3] for c in vs.cams]), p(m3), p(sc),
+                        float(s0.scale_modifier), p(rot), p(shc), p(c3), views, projs, campos, tx, ty, p(radii[sl]),
+                        p(vs.geom), p(vs.binning), p(vs.image), p(gc[sl]), gdp, gap, p(d_m2[sl]), p(d_col), p(d_op),
+                        p(d_m3), p(d_c3), p(d_sh), p(d_sc), p(d_rot), 1 if si > 0 else 0, p(work), work.numel(),
+                        stream))
+                else:
+                    _C._check(lib.gsr_set_backward_composite(
+                        vs.V, P, int(s0.sh_degree), M, Karr, W, H, _ptrs([c[3] for c in vs.cams]), p(m3), p(sc),
+                        float(s0.scale_modifier), p(rot), p(shc), p(c3), views, projs, campos, tx, ty, p(radii[sl]),
+                        p(vs.geom), p(vs.binning), p(vs.image), p(cbg[sl]), p(color[sl]), p(gc[sl]), gdp, gap,
+                        p(d_bg[sl]) if d_bg is not None else None, p(d_m2[sl]), p(d_col), p(d_op), p(d_m3), p(d_c3),
+                        p(d_sh), p(d_sc), p(d_rot), 1 if si > 0 else 0, p(work), work.numel(), stream))
+        if d_bg is not None:
+            d_bg = d_bg.reshape(ctx.bg_shape)
+        grads = [None, d_m3, d_sh, d_col, d_op, d_sc, d_rot, d_c3, d_bg] + [d_m2[v] for v in range(V)]
         for k, need in enumerate(ctx.needs_input_grad):
             if not need:
                 grads[k] = None
@@ -165,11 +191,16 @@ class _RasterizeViews(torch.autograd.Function):
 
 
 def rasterize_views(settings_list, means3D, means2D_list, opacities, shs=None, colors_precomp=None, scales=None,
-                    rotations=None, cov3D_precomp=None):
+                    rotations=None, cov3D_precomp=None, background=None):
     """Render V views of one set of Gaussians.  settings_list: V GaussianRasterizationSettings (same image
     size, same sh_degree, scale_modifier and prefiltered flag); means2D_list: V screen-space placeholders
     (P, 3) whose .grad receives each view's viewspace gradient.  Returns (color (V,3,H,W), radii (V,P),
-    depth (V,1,H,W), alpha (V,1,H,W))."""
+    depth (V,1,H,W), alpha (V,1,H,W)).
+
+    background: the background renderer's composite fused into the blends — the background network's
+    images (V, H, W, 3) (renderer/diff_gaussian_rasterizer_background.py:116,129-132,139); the first
+    output is then render = clamp(color + (1 - alpha) * background, 0, 1) (bit-identical to the torch
+    expression, same gradients incl. the background's) instead of color."""
     if (shs is None) == (colors_precomp is None):
         raise Exception("Please provide excatly one of either SHs or precomputed colors!")
     if ((scales is None or rotations is None) and cov3D_precomp is None) or (
@@ -183,5 +214,9 @@ def rasterize_views(settings_list, means3D, means2D_list, opacities, shs=None, c
     if any(int(s.sh_degree) != int(s0.sh_degree) or float(s.scale_modifier) != float(s0.scale_modifier)
            or bool(s.prefiltered) != bool(s0.prefiltered) for s in settings_list):
         raise ValueError("sh_degree, scale_modifier and prefiltered must be shared by the views of a batch")
+    if background is not None:
+        H, W = int(s0.image_height), int(s0.image_width)
+        if background.numel() != len(settings_list) * H * W * 3:
+            raise ValueError("background must hold (V, H, W, 3) values")
     return _RasterizeViews.apply(list(settings_list), means3D, shs, colors_precomp, opacities, scales, rotations,
-                                 cov3D_precomp, *means2D_list)
+                                 cov3D_precomp, background, *means2D_list)
