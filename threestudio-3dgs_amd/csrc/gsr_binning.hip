@@ -92,76 +92,100 @@ struct EmitLDS {
   uint32_t own[64];
 };
 
+#define GSR_EMIT_GROUPS 2  // consecutive 64-Gaussian groups per wave (the next group's gathers prefetched)
+
 __global__ __launch_bounds__(64) void k_emit(int P, int nbe, int grid_x, GeomState g, const uint32_t* __restrict__ order,
                                              const uint32_t* __restrict__ dkeys, SegInfo inst, int gbits,
                                              uint32_t* __restrict__ keys, uint32_t* __restrict__ vals) {
   __shared__ EmitLDS s;
-  const int v = blockIdx.x / nbe, lb = blockIdx.x % nbe;
+  const int nw = div_up(nbe, GSR_EMIT_GROUPS);
+  const int v = blockIdx.x / nw;
+  const int lb0 = (blockIdx.x % nw) * GSR_EMIT_GROUPS, lb1 = min(nbe, lb0 + GSR_EMIT_GROUPS);
   const int lane = threadIdx.x;
   const size_t vo = (size_t)v * P;
-  const int r = lb * GSR_DUP_TILE + lane;
-  const uint32_t gi = r < P ? order[vo + r] : 0u;
-  // visible (sorted depth key != ~0): its record is valid and its rectangle non-empty
-  const bool vis = r < P && dkeys[vo + r] != 0xFFFFFFFFu;
-  uint32_t cnt = 0u;
-  s.gi[lane] = gi;
-  s.rect[lane] = make_uint2(0u, 0u);
-  if (vis) {
-    const GaussRec& rc = g.rec[vo + gi];
-    const uint4 d = rc.d;
-    const float4 ra = rc.a, rb = rc.b;
-    cnt = ((d.y & 0xffffu) - (d.x & 0xffffu)) * ((d.y >> 16) - (d.x >> 16));  // rectangle tiles
-    s.rect[lane] = make_uint2(d.x, d.y);
-    s.sp[lane] = span_prep(ra.x, ra.y, ra.z, ra.w, rb.x, rb.y);
-  }
-  const uint32_t incl = wave_incl_sum_dpp(cnt);
-  const uint32_t myoff = incl - cnt;
-  const uint32_t btot = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
-  s.off[lane] = myoff;
-  // gradient-row slots: rectangle offsets (all of a visible Gaussian's rectangle, kept or not)
-  if (cnt) g.rec[vo + gi].d.z = g.inst_counts[(size_t)v * nbe + lb] + myoff;
-  uint32_t kbase = g.kept_counts[(size_t)v * nbe + lb];
   uint32_t* kout = keys + inst.start[v];
   uint32_t* vout = vals ? vals + inst.start[v] : nullptr;
-  uint32_t carry = 0u;  // 1 + owner of the previous chunk's last position
-  for (uint32_t c0 = 0; c0 < btot; c0 += 64) {
-    s.own[lane] = 0u;
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    if (cnt && myoff >= c0 && myoff < c0 + 64) s.own[myoff - c0] = (uint32_t)lane + 1u;
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    const uint32_t ow1 = max(carry, wave_incl_max_dpp(s.own[lane]));
-    carry = (uint32_t)__builtin_amdgcn_readlane((int)ow1, 63);
-    const uint32_t j = c0 + (uint32_t)lane;
-    bool kp = false;
-    uint32_t key = 0u, gv = 0u;
-    if (j < btot) {
-      const uint32_t ow = ow1 - 1u;
-      const uint2 rc = s.rect[ow];
-      const uint32_t xmin = rc.x & 0xffffu, ymin = rc.x >> 16, xmax = rc.y & 0xffffu;
-      const uint32_t wd = xmax - xmin, l = j - s.off[ow];
-      // l / wd without the ~35-instruction integer division: l < 2^24, so the float quotient is
-      // within one of the true one; one correction step makes it exact
-      int ty = (int)((float)l * __builtin_amdgcn_rcpf((float)wd));
-      int tx = (int)l - ty * (int)wd;
-      if (tx < 0) { --ty; tx += (int)wd; }
-      else if (tx >= (int)wd) { ++ty; tx -= (int)wd; }
-      const int row = (int)ymin + ty, col = (int)xmin + tx;
-      const SpanPrep sp = s.sp[ow];
-      int t0, t1;
-      span_row(sp, row, (int)xmin, (int)xmax, t0, t1);
-      kp = col >= t0 && col < t1;
-      const uint32_t tile = (uint32_t)row * (uint32_t)grid_x + (uint32_t)col;
-      gv = s.gi[ow];
-      key = vout ? tile : ((tile << gbits) | gv);
+  // group prefetch: order, visibility and the record pieces of group lb + 1 load while lb emits
+  uint32_t n_gi = 0u, n_ioff = 0u, n_koff = 0u;
+  bool n_vis = false;
+  float4 n_ra = make_float4(0.f, 0.f, 0.f, 0.f), n_rb = n_ra;
+  uint2 n_d = make_uint2(0u, 0u);
+  auto fetch = [&](int lb) {
+    const int r = lb * GSR_DUP_TILE + lane;
+    n_gi = r < P ? order[vo + r] : 0u;
+    n_vis = r < P && dkeys[vo + r] != 0xFFFFFFFFu;
+    n_ioff = g.inst_counts[(size_t)v * nbe + lb];
+    n_koff = g.kept_counts[(size_t)v * nbe + lb];
+    if (n_vis) {
+      const GaussRec& rc = g.rec[vo + n_gi];
+      const uint4 d = rc.d;
+      n_d = make_uint2(d.x, d.y);
+      n_ra = rc.a;
+      n_rb = rc.b;
     }
-    const unsigned long long bal = __ballot(kp);
-    if (kp) {
-      const uint32_t o = kbase + mask_rank(bal);
-      kout[o] = key;
-      if (vout) vout[o] = gv;
+  };
+  if (lb0 < lb1) fetch(lb0);
+  for (int lb = lb0; lb < lb1; ++lb) {
+    const uint32_t gi = n_gi, ioff = n_ioff;
+    const bool vis = n_vis;
+    const float4 ra = n_ra, rb = n_rb;
+    const uint2 d = n_d;
+    uint32_t kbase = n_koff;
+    if (lb + 1 < lb1) fetch(lb + 1);
+    uint32_t cnt = 0u;
+    s.gi[lane] = gi;
+    s.rect[lane] = make_uint2(0u, 0u);
+    if (vis) {
+      cnt = ((d.y & 0xffffu) - (d.x & 0xffffu)) * ((d.y >> 16) - (d.x >> 16));  // rectangle tiles
+      s.rect[lane] = d;
+      s.sp[lane] = span_prep(ra.x, ra.y, ra.z, ra.w, rb.x, rb.y);
     }
-    kbase += (uint32_t)__popcll(bal);
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // own[] is rewritten by the next chunk
+    const uint32_t incl = wave_incl_sum_dpp(cnt);
+    const uint32_t myoff = incl - cnt;
+    const uint32_t btot = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
+    s.off[lane] = myoff;
+    // gradient-row slots: rectangle offsets (all of a visible Gaussian's rectangle, kept or not)
+    if (cnt) g.rec[vo + gi].d.z = ioff + myoff;
+    uint32_t carry = 0u;  // 1 + owner of the previous chunk's last position
+    for (uint32_t c0 = 0; c0 < btot; c0 += 64) {
+      s.own[lane] = 0u;
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      if (cnt && myoff >= c0 && myoff < c0 + 64) s.own[myoff - c0] = (uint32_t)lane + 1u;
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      const uint32_t ow1 = max(carry, wave_incl_max_dpp(s.own[lane]));
+      carry = (uint32_t)__builtin_amdgcn_readlane((int)ow1, 63);
+      const uint32_t j = c0 + (uint32_t)lane;
+      bool kp = false;
+      uint32_t key = 0u, gv = 0u;
+      if (j < btot) {
+        const uint32_t ow = ow1 - 1u;
+        const uint2 rc = s.rect[ow];
+        const uint32_t xmin = rc.x & 0xffffu, ymin = rc.x >> 16, xmax = rc.y & 0xffffu;
+        const uint32_t wd = xmax - xmin, l = j - s.off[ow];
+        // l / wd without the ~35-instruction integer division: l < 2^24, so the float quotient is
+        // within one of the true one; one correction step makes it exact
+        int ty = (int)((float)l * __builtin_amdgcn_rcpf((float)wd));
+        int tx = (int)l - ty * (int)wd;
+        if (tx < 0) { --ty; tx += (int)wd; }
+        else if (tx >= (int)wd) { ++ty; tx -= (int)wd; }
+        const int row = (int)ymin + ty, col = (int)xmin + tx;
+        const SpanPrep sp = s.sp[ow];
+        int t0, t1;
+        span_row(sp, row, (int)xmin, (int)xmax, t0, t1);
+        kp = col >= t0 && col < t1;
+        const uint32_t tile = (uint32_t)row * (uint32_t)grid_x + (uint32_t)col;
+        gv = s.gi[ow];
+        key = vout ? tile : ((tile << gbits) | gv);
+      }
+      const unsigned long long bal = __ballot(kp);
+      if (kp) {
+        const uint32_t o = kbase + mask_rank(bal);
+        kout[o] = key;
+        if (vout) vout[o] = gv;
+      }
+      kbase += (uint32_t)__popcll(bal);
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // own[] is rewritten by the next chunk
+    }
   }
 }
 
@@ -202,8 +226,8 @@ void launch_emit(int V, int P, int W, const GeomState& g, const uint32_t* order,
                  const SegInfo& inst, int gbits, uint32_t* keys, uint32_t* vals, hipStream_t stream) {
   if (V <= 0 || P <= 0) return;
   const int nbe = GeomState::dup_blocks(P);
-  hipLaunchKernelGGL(k_emit, dim3(V * nbe), dim3(64), 0, stream, P, nbe, div_up(W, GSR_TILE_X), g, order, dkeys,
-                     inst, gbits, keys, vals);
+  hipLaunchKernelGGL(k_emit, dim3(V * div_up(nbe, GSR_EMIT_GROUPS)), dim3(64), 0, stream, P, nbe,
+                     div_up(W, GSR_TILE_X), g, order, dkeys, inst, gbits, keys, vals);
 }
 
 void launch_tile_ranges(SegInfo inst, int n_tiles, int gbits, const uint32_t* keys, uint2* ranges, hipStream_t stream) {
