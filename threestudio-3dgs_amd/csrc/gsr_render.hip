@@ -196,8 +196,7 @@ __global__ __launch_bounds__(64) void k_render_fwd(RenderSet rs,
       const bool term = ok && test_T < GSR_T_EPS;
       const bool blend = ok && !term;
       // non-blending lanes run the same arithmetic with alpha = 0 (no change), no selects of state
-      const unsigned long long bm = __ballot(blend);
-      const float a_eff = vsel(bm, alpha, 0.0f);
+      const float a_eff = blend ? alpha : 0.0f;
       const float aT = a_eff * T;
       Cr = fmaf(c.x, aT, Cr);
       Cg = fmaf(c.y, aT, Cg);
@@ -457,9 +456,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5, 8))) voi
     const float G = __expf(power);
     const float alpha = fminf(GSR_ALPHA_MAX, gb.y * G);
     const bool hit = rel < last_contributor && power <= 0.0f && alpha >= GSR_ALPHA_MIN;
-    const unsigned long long hm = __ballot(hit);
-    const float a_eff = vsel(hm, alpha, 0.0f);
-    const float g_eff = vsel(hm, G, 0.0f);
+    const float a_eff = hit ? alpha : 0.0f;
+    const float g_eff = hit ? G : 0.0f;
     const float oma = 1.f - a_eff;
     const float inv_1ma = fast_rcp(oma);  // 1 for non-contributors
     T = T * inv_1ma;
