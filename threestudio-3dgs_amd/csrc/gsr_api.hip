@@ -216,6 +216,10 @@ int gsr_set_preprocess(int V, int P, int degree, int M, const float* means3D, co
   if (shs != nullptr && M <= 0) return fail(GSR_EINVAL, "%s", "M must be >= 1 with SHs");
   SetCams cams;
   if (set_cams(V, viewmatrices, projmatrices, campos, tanfovx, tanfovy, cams) != GSR_OK) return GSR_EINVAL;
+  for (int v = 0; v < V; ++v) {  // IEEE float division on the host = the device's correctly rounded one
+    cams.c[v].fx = (float)width / (2.0f * cams.c[v].tanx);
+    cams.c[v].fy = (float)height / (2.0f * cams.c[v].tany);
+  }
   hipStream_t s = (hipStream_t)stream;
   GeomState g = GeomState::carve(geom, V, P, nullptr);
 

@@ -131,6 +131,7 @@ __device__ __forceinline__ int seg_of_block(const SegInfo& s, uint32_t b, uint32
 struct ViewCam {
   const float *view, *proj, *campos;
   float tanx, tany;
+  float fx, fy;  // focal lengths W / (2 tanx), H / (2 tany) (set by the host for the preprocess)
 };
 struct SetCams {
   ViewCam c[GSR_SET_MAX];

@@ -27,7 +27,8 @@ __global__ __launch_bounds__(256) void k_preprocess(PreprocessArgs a, SetCams ca
   const int vc = blockIdx.x % nvc;
   const int idx0 = (blockIdx.x / nvc) * GSR_PRE_GAUSS;
   const int t = threadIdx.x;
-  const int gl = t % GSR_PRE_GAUSS, half = t / GSR_PRE_GAUSS;
+  const int gl = t % GSR_PRE_GAUSS;
+  const int half = __builtin_amdgcn_readfirstlane(t / GSR_PRE_GAUSS);  // wave-uniform: scalar camera loads
   const int idx = idx0 + gl;
   const int vb = vc * GSR_PRE_VIEWS, ve = min(a.V, vb + GSR_PRE_VIEWS);
   const int vh = (ve - vb + 1) / 2;
@@ -76,10 +77,15 @@ __global__ __launch_bounds__(256) void k_preprocess(PreprocessArgs a, SetCams ca
   for (int v = v0; v < v1; ++v) {
     const ViewCam cam = cams.c[v];
     const size_t vi = (size_t)v * a.P + idx;
-    const float* viewmatrix = cam.view;
-    const float* projmatrix = cam.proj;
+    // the view's matrices through the constant address space: wave-uniform addresses -> s_load
+    typedef __attribute__((address_space(4))) const float* cfptr;
+    float viewmatrix[16], projmatrix[16], cpos[3];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) viewmatrix[i] = ((cfptr)cam.view)[i], projmatrix[i] = ((cfptr)cam.proj)[i];
+#pragma unroll
+    for (int i = 0; i < 3; ++i) cpos[i] = ((cfptr)cam.campos)[i];
     const float tanfovx = cam.tanx, tanfovy = cam.tany;
-    const float focal_x = a.W / (2.0f * tanfovx), focal_y = a.H / (2.0f * tanfovy);
+    const float focal_x = cam.fx, focal_y = cam.fy;
     int radius = 0;
     uint2 tiles = make_uint2(0u, 0u);
     uint32_t dkey = 0xFFFFFFFFu;  // culled: sorts after every visible depth
@@ -111,7 +117,7 @@ __global__ __launch_bounds__(256) void k_preprocess(PreprocessArgs a, SetCams ca
           float3 rgb = rgb_pre;
           uint32_t clamp_bits = 0;
           if (a.colors_precomp == nullptr)
-            rgb = sh_to_rgb(a.deg, my_sh, p_orig, make_float3(cam.campos[0], cam.campos[1], cam.campos[2]),
+            rgb = sh_to_rgb(a.deg, my_sh, p_orig, make_float3(cpos[0], cpos[1], cpos[2]),
                             &clamp_bits);
           GaussRec rec;
           rec.a = make_float4(pimg.x, pimg.y, conic.x, conic.y);
