@@ -283,6 +283,19 @@ __global__ __launch_bounds__(256) void k_view_grad(GaussBackwardArgs a, ViewGrad
     __syncthreads();
   }
   const ViewCam& cam = va.cam[vl];
+  // the view's matrices through the constant address space (block-uniform view: s_load, no VGPRs);
+  // focal lengths once per thread instead of once per item
+  typedef __attribute__((address_space(4))) const float* cfptr;
+  float viewm[16], projm[16];
+#pragma unroll
+  for (int i = 0; i < 16; ++i) viewm[i] = ((cfptr)cam.view)[i], projm[i] = ((cfptr)cam.proj)[i];
+  ViewGeom vgm;
+  vgm.view = viewm;
+  vgm.proj = projm;
+  vgm.tanx = cam.tanx;
+  vgm.tany = cam.tany;
+  vgm.fy = va.H / (2.0f * cam.tany);
+  vgm.fx = va.W / (2.0f * cam.tanx);
   const float4* grow = va.grow + (size_t)3 * va.row_start[vl];
   float* recv = va.vrec + (size_t)vl * GSR_GRAD_FIELDS * a.P;
   // the next item's radius and record are loaded while the current one is processed
@@ -331,21 +344,14 @@ __global__ __launch_bounds__(256) void k_view_grad(GaussBackwardArgs a, ViewGrad
                                      a.rotations[4 * idx + 3]);
       cov3d_from_scale_rot(scale, a.scale_modifier, rot, cov3D);
     }
-    ViewGeom vgm;
-    vgm.view = cam.view;
-    vgm.proj = cam.proj;
-    vgm.tanx = cam.tanx;
-    vgm.tany = cam.tany;
-    vgm.fy = va.H / (2.0f * cam.tany);
-    vgm.fx = va.W / (2.0f * cam.tanx);
     float dcv[6];
     float3 dm;
     cov2d_backward(mean, cov3D, vgm, r.dca, r.dcb, r.dcc, dcv, dm);
-    proj_backward(mean, cam.proj, r.dmx, r.dmy, dm);
+    proj_backward(mean, projm, r.dmx, r.dmy, dm);
     // view depth = view[2] x + view[6] y + view[10] z + view[14]
-    dm.x += cam.view[2] * r.ddep;
-    dm.y += cam.view[6] * r.ddep;
-    dm.z += cam.view[10] * r.ddep;
+    dm.x += viewm[2] * r.ddep;
+    dm.y += viewm[6] * r.ddep;
+    dm.z += viewm[10] * r.ddep;
     const float f[GSR_GRAD_FIELDS] = {dm.x, dm.y, dm.z, dcv[0], dcv[1], dcv[2], dcv[3], dcv[4], dcv[5],
                                       r.dcr, r.dcg, r.dcbl, r.dop, __uint_as_float(clamp_bits)};
 #pragma unroll
