@@ -190,27 +190,44 @@ __global__ __launch_bounds__(64) void k_emit(int P, int nbe, int grid_x, GeomSta
 }
 
 // After the tile sort: per-tile [start, end) ranges (view-local positions) of each view's list.
-// 4 consecutive instances per thread (one 16-byte load, neighbours from the adjacent lanes).
+// One wave streams GSR_RANGE_ROUNDS x 64 consecutive instances, lane-interleaved (coalesced): all
+// rounds' keys are loaded first, neighbours come from the adjacent lanes (shuffles) and, at round
+// edges, from the neighbouring round (readlane).
+#define GSR_RANGE_ROUNDS 16
 __global__ __launch_bounds__(256) void k_tile_ranges(SegInfo inst, int n_tiles, int gbits,
                                                      const uint32_t* __restrict__ keys,
                                                      uint2* __restrict__ ranges) {
   uint32_t lb;
   const int v = seg_of_block(inst, blockIdx.x, lb);
-  const uint32_t p0 = (lb * 256 + threadIdx.x) * 4;
+  const int lane = threadIdx.x & 63;
+  const uint32_t base = (lb * 4 + (threadIdx.x >> 6)) * (64u * GSR_RANGE_ROUNDS);
   const uint32_t K = seg_live(inst, v);
-  if (p0 >= K) return;
+  if (base >= K) return;  // wave-uniform
   const uint32_t* kv = keys + inst.start[v];
   uint2* rv = ranges + (size_t)v * n_tiles;
-  uint32_t t[6];
-  t[0] = p0 > 0 ? kv[p0 - 1] >> gbits : 0xFFFFFFFFu;
+  uint32_t t[GSR_RANGE_ROUNDS];
 #pragma unroll
-  for (int k = 0; k < 5; ++k) t[k + 1] = p0 + k < K ? kv[p0 + k] >> gbits : 0xFFFFFFFFu;
+  for (int r = 0; r < GSR_RANGE_ROUNDS; ++r) {
+    const uint32_t i = base + 64u * r + lane;
+    t[r] = i < K ? kv[i] >> gbits : 0xFFFFFFFFu;
+  }
+  const uint32_t before = base > 0 ? kv[base - 1] >> gbits : 0xFFFFFFFFu;
+  const uint32_t e = base + 64u * GSR_RANGE_ROUNDS;
+  const uint32_t after = e < K ? kv[e] >> gbits : 0xFFFFFFFFu;
 #pragma unroll
-  for (int k = 0; k < 4; ++k) {
-    const uint32_t p = p0 + k;
-    if (p >= K) break;
-    if (t[k] != t[k + 1]) rv[t[k + 1]].x = p;
-    if (t[k + 2] != t[k + 1]) rv[t[k + 1]].y = p + 1;
+  for (int r = 0; r < GSR_RANGE_ROUNDS; ++r) {
+    const uint32_t p = base + 64u * r + lane;
+    if (base + 64u * r >= K) break;  // wave-uniform
+    uint32_t prev = (uint32_t)__shfl_up((int)t[r], 1, 64);
+    uint32_t next = (uint32_t)__shfl_down((int)t[r], 1, 64);
+    if (lane == 0) prev = r == 0 ? before : (uint32_t)__builtin_amdgcn_readlane((int)t[r > 0 ? r - 1 : 0], 63);
+    if (lane == 63)
+      next = r == GSR_RANGE_ROUNDS - 1 ? after
+                                       : (uint32_t)__builtin_amdgcn_readlane((int)t[r + 1 < GSR_RANGE_ROUNDS ? r + 1 : r], 0);
+    if (p < K) {
+      if (prev != t[r]) rv[t[r]].x = p;
+      if (next != t[r]) rv[t[r]].y = p + 1;
+    }
   }
 }
 

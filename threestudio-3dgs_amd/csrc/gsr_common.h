@@ -20,8 +20,8 @@
 #define GSR_RADIX (1 << GSR_RADIX_BITS)
 // Instance emission: 256 threads x 4 depth-sorted Gaussians per block.
 #define GSR_DUP_TILE 64  // depth-sorted Gaussians per emission group (one wave)
-// Tile ranges: 256 threads x 4 instances per block.
-#define GSR_RANGE_TILE 1024
+// Tile ranges: 4 waves x 16 rounds x 64 instances per block.
+#define GSR_RANGE_TILE 4096
 
 // Rasterizer constants of the reference algorithm ([EXT] graphdeco
 // cuda_rasterizer/forward.cu + auxiliary.h).
