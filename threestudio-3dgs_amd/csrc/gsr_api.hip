@@ -252,9 +252,10 @@ int gsr_set_preprocess(int V, int P, int degree, int M, const float* means3D, co
       seg.n[v] = (uint32_t)P;
       seg.start[v] = (uint32_t)((size_t)v * P);
     }
+    seg.rebase = g.drange + 128;  // keys ranked relative to the set's smallest visible key (preprocess)
     const int res = seg_sort(g.dkey, g.dval, true, seg, 0, 32, g.sort_counts, g.sort_totals, s);
     if (res != depth_sort_result()) return fail(GSR_EHIP, "%s", "internal: depth sort result buffer");
-    launch_binning_counts(V, P, g, g.dval[res], s);
+    launch_binning_counts(V, P, g, s);  // reads the sorted buffer the device flag names (3 or 4 passes)
   }
   return last_launch();
 }
@@ -403,8 +404,7 @@ static int set_render(int V, int P, const int* K, int width, int height, const f
     PhaseScope ps(GSR_PHASE_BINNING, s);
     GSR_HIP_CHECK(hipMemsetAsync(img.ranges, 0, sizeof(uint2) * (size_t)V * gx * gy, s));
     if (total > 0) {
-      launch_emit(V, P, width, g, g.dval[depth_sort_result()], g.dkey[depth_sort_result()], inst, tp.gbits,
-                  b.key[0], b.val[0], s);
+      launch_emit(V, P, width, g, inst, tp.gbits, b.key[0], b.val[0], s);
       const int res = seg_sort(b.key, b.val, false, inst, tp.gbits, tp.tile_bits, b.sort_counts, b.sort_totals, s);
       if (res != tres) return fail(GSR_EHIP, "%s", "internal: tile sort buffer");
       launch_tile_ranges(inst, gx * gy, tp.gbits, b.key[res], img.ranges, s);

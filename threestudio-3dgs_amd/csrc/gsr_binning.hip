@@ -16,7 +16,8 @@ namespace gsr {
 
 // Rectangle tiles, visible Gaussians and kept tiles of each 64-Gaussian group of every view's depth
 // order (one wave per group, 4 groups per block): counts[v][group].
-__global__ __launch_bounds__(256) void k_inst_count(int P, int nbe, GeomState g, const uint32_t* __restrict__ order) {
+__global__ __launch_bounds__(256) void k_inst_count(int P, int nbe, GeomState g) {
+  const uint32_t* __restrict__ order = g.sorted_dval();
   const int nb4 = (nbe + 3) / 4;
   const int v = blockIdx.x / nb4;
   const int lb = (blockIdx.x - v * nb4) * 4 + (threadIdx.x >> 6);
@@ -94,9 +95,10 @@ struct EmitLDS {
 
 #define GSR_EMIT_GROUPS 2  // consecutive 64-Gaussian groups per wave (the next group's gathers prefetched)
 
-__global__ __launch_bounds__(64) void k_emit(int P, int nbe, int grid_x, GeomState g, const uint32_t* __restrict__ order,
-                                             const uint32_t* __restrict__ dkeys, SegInfo inst, int gbits,
+__global__ __launch_bounds__(64) void k_emit(int P, int nbe, int grid_x, GeomState g, SegInfo inst, int gbits,
                                              uint32_t* __restrict__ keys, uint32_t* __restrict__ vals) {
+  const uint32_t* __restrict__ order = g.sorted_dval();
+  const uint32_t* __restrict__ dkeys = g.sorted_dkey();
   __shared__ EmitLDS s;
   const int nw = div_up(nbe, GSR_EMIT_GROUPS);
   const int v = blockIdx.x / nw;
@@ -231,20 +233,20 @@ __global__ __launch_bounds__(256) void k_tile_ranges(SegInfo inst, int n_tiles, 
   }
 }
 
-void launch_binning_counts(int V, int P, const GeomState& g, const uint32_t* order, hipStream_t stream) {
+void launch_binning_counts(int V, int P, const GeomState& g, hipStream_t stream) {
   if (V <= 0) return;
   const int nbe = GeomState::dup_blocks(P);
   if (P > 0)
-    hipLaunchKernelGGL(k_inst_count, dim3(V * ((nbe + 3) / 4)), dim3(256), 0, stream, P, nbe, g, order);
+    hipLaunchKernelGGL(k_inst_count, dim3(V * ((nbe + 3) / 4)), dim3(256), 0, stream, P, nbe, g);
   hipLaunchKernelGGL(k_inst_scan, dim3(V), dim3(256), 0, stream, P > 0 ? nbe : 0, g);
 }
 
-void launch_emit(int V, int P, int W, const GeomState& g, const uint32_t* order, const uint32_t* dkeys,
-                 const SegInfo& inst, int gbits, uint32_t* keys, uint32_t* vals, hipStream_t stream) {
+void launch_emit(int V, int P, int W, const GeomState& g, const SegInfo& inst, int gbits, uint32_t* keys,
+                 uint32_t* vals, hipStream_t stream) {
   if (V <= 0 || P <= 0) return;
   const int nbe = GeomState::dup_blocks(P);
   hipLaunchKernelGGL(k_emit, dim3(V * div_up(nbe, GSR_EMIT_GROUPS)), dim3(64), 0, stream, P, nbe,
-                     div_up(W, GSR_TILE_X), g, order, dkeys, inst, gbits, keys, vals);
+                     div_up(W, GSR_TILE_X), g, inst, gbits, keys, vals);
 }
 
 void launch_tile_ranges(SegInfo inst, int n_tiles, int gbits, const uint32_t* keys, uint2* ranges, hipStream_t stream) {

@@ -105,9 +105,21 @@ struct SegInfo {
   uint32_t start[GSR_SET_MAX];
   uint32_t blk[GSR_SET_MAX + 1];
   const uint32_t* ndev = nullptr;
+  // depth sort only: [0] = smallest visible key of the set (keys are ranked as key - [0], culled ~0
+  // stays ~0), [1] != 0 when every rebased visible key is < 2^24 - 1: the last (4th) pass is then a
+  // no-op and its kernels return at once (the result stays in the 3rd pass's buffer)
+  const uint32_t* rebase = nullptr;
 };
 __device__ __forceinline__ uint32_t seg_live(const SegInfo& s, int v) {
   return s.ndev ? min(s.ndev[v], s.n[v]) : s.n[v];
+}
+// the sort key of a raw key given the segment info's base (load it once per kernel: seg_key_base)
+__device__ __forceinline__ uint32_t seg_key_base(const SegInfo& s) { return s.rebase ? s.rebase[0] : 0u; }
+__device__ __forceinline__ uint32_t seg_key(uint32_t kb, uint32_t key) {
+  return key == 0xFFFFFFFFu ? key : key - kb;
+}
+__device__ __forceinline__ bool seg_skip_last(const SegInfo& s, int last) {
+  return last && s.rebase != nullptr && s.rebase[1] != 0u;
 }
 static inline void seg_fill_blocks(SegInfo& s, int tile) {
   // (ndev is left as set by the caller; SegInfo is otherwise plain data)
@@ -158,6 +170,11 @@ struct GeomState {
   uint32_t* inst_counts;     // [V][emission blocks] rectangle tiles per block -> scanned offsets
   uint32_t* kept_counts;     // [V][emission blocks] kept instances per block -> scanned offsets
   uint32_t* vis_counts;      // [V][emission blocks] visible Gaussians per block
+  uint32_t* drange;          // depth key range of the set: [0, 64) min slots, [64, 128) max slots,
+                             // [128] = min visible key, [129] = 1 if 3 depth-sort passes suffice
+  // the depth-sorted (keys, Gaussians) of every view: the 4th pass's output, or the 3rd's when it was skipped
+  __device__ const uint32_t* sorted_dval() const { return drange[129] ? dval[1] : dval[0]; }
+  __device__ const uint32_t* sorted_dkey() const { return drange[129] ? dkey[1] : dkey[0]; }
   uint32_t* counters;        // [0, V) rectangle tiles K of each view (the reference's num_rendered),
                              // [V, 2V) visible Gaussians, [2V, 3V) kept list instances
   static int sort_blocks(int P) { return div_up(P > 0 ? P : 1, GSR_SORT_TILE); }
@@ -179,6 +196,7 @@ struct GeomState {
     g.vis_counts = c.take<uint32_t>(nv * dup_blocks(P));
     g.kept_counts = c.take<uint32_t>(nv * dup_blocks(P));
     g.counters = c.take<uint32_t>(3 * nv + 64);
+    g.drange = c.take<uint32_t>(132);
     if (bytes) *bytes = align_up(c.off, 256);
     return g;
   }

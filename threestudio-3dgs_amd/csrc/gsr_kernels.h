@@ -26,12 +26,11 @@ struct PreprocessArgs {
 void launch_preprocess(const PreprocessArgs& a, const SetCams& cams, const GeomState& g, hipStream_t stream);
 
 // Binning — gsr_binning.hip.  order = the depth sort's value buffer (per view: sorted position -> Gaussian).
-void launch_binning_counts(int V, int P, const GeomState& g, const uint32_t* order, hipStream_t stream);
+void launch_binning_counts(int V, int P, const GeomState& g, hipStream_t stream);
 // vals == nullptr: packed keys (tile << gbits | Gaussian)
 // dkeys = the depth sort's key buffer (sorted depth keys; culled = ~0)
-void launch_emit(int V, int P, int W, const GeomState& g, const uint32_t* order, const uint32_t* dkeys,
-                 const SegInfo& inst, int gbits,
-                 uint32_t* keys, uint32_t* vals, hipStream_t stream);
+void launch_emit(int V, int P, int W, const GeomState& g, const SegInfo& inst, int gbits, uint32_t* keys,
+                 uint32_t* vals, hipStream_t stream);
 void launch_tile_ranges(SegInfo inst, int n_tiles, int gbits, const uint32_t* keys, uint2* ranges, hipStream_t stream);
 void launch_mark_visible(int P, const float* means3D, const float* view, const float* proj,
                          uint8_t* present, hipStream_t stream);

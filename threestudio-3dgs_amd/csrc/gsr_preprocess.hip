@@ -14,6 +14,8 @@
 
 namespace gsr {
 
+void launch_preprocess_kernel(const PreprocessArgs& a, const SetCams& cams, const GeomState& g, hipStream_t stream);
+
 // Views handled by one block (the Gaussians' view-independent work and SH staging are shared): the
 // block's 256 threads are 128 Gaussians x 2 halves of the views, so the SH staging (128 x (3M + 1)
 // floats, 24.6 KB at SH3) allows 6 blocks = 6 waves per SIMD instead of 3 with 256 Gaussians.
@@ -51,25 +53,29 @@ __global__ __launch_bounds__(256) void k_preprocess(PreprocessArgs a, SetCams ca
     }
     __syncthreads();
   }
-  if (idx >= a.P) return;
+  // threads past P run on the block's first Gaussian without writing (every wave stays whole for the
+  // depth-range reduction at the end)
+  const bool valid = idx < a.P;
+  const int ix = valid ? idx : idx0;
+  uint32_t kmn = 0xFFFFFFFFu, kmx = 0u;  // this thread's visible depth keys
 
   // view-independent: position, 3D covariance, opacity, precomputed colour
-  const float3 p_orig = make_float3(a.means3D[3 * idx], a.means3D[3 * idx + 1], a.means3D[3 * idx + 2]);
+  const float3 p_orig = make_float3(a.means3D[3 * ix], a.means3D[3 * ix + 1], a.means3D[3 * ix + 2]);
   float cov3D[6];
   if (a.cov3D_precomp != nullptr) {
 #pragma unroll
-    for (int i = 0; i < 6; ++i) cov3D[i] = a.cov3D_precomp[6 * idx + i];
+    for (int i = 0; i < 6; ++i) cov3D[i] = a.cov3D_precomp[6 * ix + i];
   } else {
-    const float3 s = make_float3(a.scales[3 * idx], a.scales[3 * idx + 1], a.scales[3 * idx + 2]);
-    const float4 q = make_float4(a.rotations[4 * idx], a.rotations[4 * idx + 1],
-                                 a.rotations[4 * idx + 2], a.rotations[4 * idx + 3]);
+    const float3 s = make_float3(a.scales[3 * ix], a.scales[3 * ix + 1], a.scales[3 * ix + 2]);
+    const float4 q = make_float4(a.rotations[4 * ix], a.rotations[4 * ix + 1],
+                                 a.rotations[4 * ix + 2], a.rotations[4 * ix + 3]);
     cov3d_from_scale_rot(s, a.scale_modifier, q, cov3D);
   }
-  const float opacity = a.opacities[idx];
+  const float opacity = a.opacities[ix];
   float3 rgb_pre = make_float3(0.f, 0.f, 0.f);
   if (a.colors_precomp != nullptr)
-    rgb_pre = make_float3(a.colors_precomp[3 * idx], a.colors_precomp[3 * idx + 1], a.colors_precomp[3 * idx + 2]);
-  const float* my_sh = staged ? s_sh + gl * sstride : a.shs + (size_t)idx * nsh;
+    rgb_pre = make_float3(a.colors_precomp[3 * ix], a.colors_precomp[3 * ix + 1], a.colors_precomp[3 * ix + 2]);
+  const float* my_sh = staged ? s_sh + gl * sstride : a.shs + (size_t)ix * nsh;
   const int gx = (a.W + GSR_TILE_X - 1) / GSR_TILE_X;
   const int gy = (a.H + GSR_TILE_Y - 1) / GSR_TILE_Y;
 
@@ -125,7 +131,7 @@ __global__ __launch_bounds__(256) void k_preprocess(PreprocessArgs a, SetCams ca
           rec.c = make_float4(rgb.x, rgb.y, rgb.z, 0.0f);
           rec.d = make_uint4((uint32_t)xmin | ((uint32_t)ymin << 16), (uint32_t)xmax | ((uint32_t)ymax << 16), 0u,
                              clamp_bits);
-          g.rec[vi] = rec;
+          if (valid) g.rec[vi] = rec;
           radius = r;
           uint32_t kept = 0;
           const SpanPrep sp = span_prep(rec.a.x, rec.a.y, rec.a.z, rec.a.w, rec.b.x, rec.b.y);
@@ -139,14 +145,62 @@ __global__ __launch_bounds__(256) void k_preprocess(PreprocessArgs a, SetCams ca
         }
       }
     }
-    a.radii[vi] = radius;
-    g.tiles[vi] = tiles;
-    g.dkey[0][vi] = dkey;
+    if (valid) {
+      a.radii[vi] = radius;
+      g.tiles[vi] = tiles;
+      g.dkey[0][vi] = dkey;
+      if (dkey != 0xFFFFFFFFu) kmn = min(kmn, dkey), kmx = max(kmx, dkey);
+    }
+  }
+  // the set's visible depth-key range (rebases the depth sort: 3 passes when it spans < 24 bits):
+  // wave -> block reduction, then one atomic pair per block into one of 64 slots
+  __shared__ uint32_t s_rng[2][4];
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    kmn = min(kmn, (uint32_t)__shfl_xor((int)kmn, o, 64));
+    kmx = max(kmx, (uint32_t)__shfl_xor((int)kmx, o, 64));
+  }
+  if ((t & 63) == 0) s_rng[0][t >> 6] = kmn, s_rng[1][t >> 6] = kmx;
+  __syncthreads();
+  if (t == 0) {
+    kmn = min(min(s_rng[0][0], s_rng[0][1]), min(s_rng[0][2], s_rng[0][3]));
+    kmx = max(max(s_rng[1][0], s_rng[1][1]), max(s_rng[1][2], s_rng[1][3]));
+    if (kmn != 0xFFFFFFFFu) {
+      atomicMin(&g.drange[blockIdx.x & 63], kmn);
+      atomicMax(&g.drange[64 + (blockIdx.x & 63)], kmx);
+    }
+  }
+}
+
+__global__ void k_depth_range_init(uint32_t* drange) {
+  drange[threadIdx.x] = 0xFFFFFFFFu;
+  drange[64 + threadIdx.x] = 0u;
+}
+
+// Fold the 64 slots: [128] = smallest visible key, [129] = 1 when every rebased visible key is below
+// 2^24 - 1 (the culled marker ~0 then still ranks last after 3 passes).
+__global__ void k_depth_range(uint32_t* drange) {
+  const int t = threadIdx.x;  // 64 threads
+  uint32_t mn = drange[t], mx = drange[64 + t];
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    mn = min(mn, (uint32_t)__shfl_xor((int)mn, o, 64));
+    mx = max(mx, (uint32_t)__shfl_xor((int)mx, o, 64));
+  }
+  if (t == 0) {
+    const bool any = mn != 0xFFFFFFFFu;
+    drange[128] = any ? mn : 0u;
+    drange[129] = (!any || mx - mn < 0x00FFFFFFu) ? 1u : 0u;
   }
 }
 
 void launch_preprocess(const PreprocessArgs& a, const SetCams& cams, const GeomState& g, hipStream_t stream) {
-  if (a.P <= 0 || a.V <= 0) return;
+  hipLaunchKernelGGL(k_depth_range_init, dim3(1), dim3(64), 0, stream, g.drange);
+  if (a.P > 0 && a.V > 0) launch_preprocess_kernel(a, cams, g, stream);
+  hipLaunchKernelGGL(k_depth_range, dim3(1), dim3(64), 0, stream, g.drange);
+}
+
+void launch_preprocess_kernel(const PreprocessArgs& a, const SetCams& cams, const GeomState& g, hipStream_t stream) {
   const int nvc = (a.V + GSR_PRE_VIEWS - 1) / GSR_PRE_VIEWS;
   const size_t want = a.colors_precomp == nullptr ? (size_t)GSR_PRE_GAUSS * (3 * a.M + 1) : 0;
   const size_t lds = want <= GSR_PRE_LDS_FLOATS ? sizeof(float) * want : 0;

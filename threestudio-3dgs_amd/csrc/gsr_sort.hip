@@ -22,8 +22,10 @@
 namespace gsr {
 
 __global__ __launch_bounds__(GSR_SORT_THREADS) void k_seg_count(const uint32_t* __restrict__ keys, SegInfo seg,
-                                                                int shift, int bits,
+                                                                int shift, int bits, int last,
                                                                 uint32_t* __restrict__ counts) {
+  if (seg_skip_last(seg, last)) return;
+  const uint32_t kb = seg_key_base(seg);
   __shared__ uint32_t s_hist[GSR_RADIX];
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
   uint32_t lb;
@@ -44,7 +46,7 @@ __global__ __launch_bounds__(GSR_SORT_THREADS) void k_seg_count(const uint32_t* 
 #pragma unroll
   for (int k = 0; k < GSR_SORT_ITEMS; ++k) {
     const bool valid = b0 + k * 64 + lane < n;
-    const uint32_t d = (key[k] >> shift) & mask;
+    const uint32_t d = (seg_key(kb, key[k]) >> shift) & mask;
     const unsigned long long peers = match_digit(d, bits, valid);
     if (valid && mask_rank(peers) == 0) atomicAdd(&s_hist[d], (uint32_t)__popcll(peers));
   }
@@ -56,8 +58,9 @@ __global__ __launch_bounds__(GSR_SORT_THREADS) void k_seg_count(const uint32_t* 
 }
 
 // One workgroup per (segment, digit) row: exclusive scan of the row in place, total -> totals.
-__global__ __launch_bounds__(256) void k_seg_scan(SegInfo seg, int R, uint32_t* __restrict__ counts,
+__global__ __launch_bounds__(256) void k_seg_scan(SegInfo seg, int R, int last, uint32_t* __restrict__ counts,
                                                   uint32_t* __restrict__ totals) {
+  if (seg_skip_last(seg, last)) return;
   __shared__ uint32_t s_wave[8];
   const int v = blockIdx.x / R, d = blockIdx.x % R;
   const int t = threadIdx.x;
@@ -100,8 +103,10 @@ struct ScatterLDS {
 template <bool KV>
 __global__ __launch_bounds__(GSR_SORT_THREADS) void k_seg_scatter(
     const uint32_t* __restrict__ keys_in, const uint32_t* __restrict__ vals_in, uint32_t* __restrict__ keys_out,
-    uint32_t* __restrict__ vals_out, SegInfo seg, int shift, int bits, const uint32_t* __restrict__ counts,
+    uint32_t* __restrict__ vals_out, SegInfo seg, int shift, int bits, int last, const uint32_t* __restrict__ counts,
     const uint32_t* __restrict__ totals) {
+  if (seg_skip_last(seg, last)) return;
+  const uint32_t kb = seg_key_base(seg);
   __shared__ ScatterLDS<KV> s;
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
   uint32_t lb;
@@ -124,7 +129,7 @@ __global__ __launch_bounds__(GSR_SORT_THREADS) void k_seg_scatter(
 #pragma unroll
   for (int k = 0; k < GSR_SORT_ITEMS; ++k) {
     const bool valid = b0 + k * 64 + lane < n;
-    const uint32_t d = (key[k] >> shift) & mask;
+    const uint32_t d = (seg_key(kb, key[k]) >> shift) & mask;
     const unsigned long long peers = match_digit(d, bits, valid);
     const uint32_t rank = mask_rank(peers);
     uint32_t base = 0u;
@@ -160,7 +165,7 @@ __global__ __launch_bounds__(GSR_SORT_THREADS) void k_seg_scatter(
 #pragma unroll
   for (int k = 0; k < GSR_SORT_ITEMS; ++k) {
     if (b0 + k * 64 + lane < n) {
-      const uint32_t d = (key[k] >> shift) & mask;
+      const uint32_t d = (seg_key(kb, key[k]) >> shift) & mask;
       const uint32_t lp = s.local[d] + s.wcnt[w][d] + pos[k];
       s.keys[lp] = key[k];
       if (KV) s.vals[lp] = val[k];
@@ -173,7 +178,7 @@ __global__ __launch_bounds__(GSR_SORT_THREADS) void k_seg_scatter(
     const uint32_t j = k * GSR_SORT_THREADS + t;
     if (j < nv) {
       const uint32_t kk = s.keys[j];
-      const uint32_t d = (kk >> shift) & mask;
+      const uint32_t d = (seg_key(kb, kk) >> shift) & mask;
       const uint32_t dst = start + s.glob[d] + (j - s.local[d]);
       keys_out[dst] = kk;
       if (KV) vals_out[dst] = s.vals[j];
@@ -193,17 +198,18 @@ int seg_sort(uint32_t* keys[2], uint32_t* vals[2], bool vals_identity, SegInfo s
     const int dst = src ^ 1;
     if (nb > 0) {
       const int shift = bit_lo + p * plan.bits;
+      const int last = p == plan.passes - 1 ? 1 : 0;
       hipLaunchKernelGGL(k_seg_count, dim3(nb), dim3(GSR_SORT_THREADS), 0, stream, (const uint32_t*)keys[src], seg,
-                         shift, bits, counts);
-      hipLaunchKernelGGL(k_seg_scan, dim3(seg.V << bits), dim3(256), 0, stream, seg, 1 << bits, counts, totals);
+                         shift, bits, last, counts);
+      hipLaunchKernelGGL(k_seg_scan, dim3(seg.V << bits), dim3(256), 0, stream, seg, 1 << bits, last, counts, totals);
       if (kv)
         hipLaunchKernelGGL(k_seg_scatter<true>, dim3(nb), dim3(GSR_SORT_THREADS), 0, stream, (const uint32_t*)keys[src],
                            (const uint32_t*)((p == 0 && vals_identity) ? nullptr : vals[src]), keys[dst], vals[dst],
-                           seg, shift, bits, (const uint32_t*)counts, (const uint32_t*)totals);
+                           seg, shift, bits, last, (const uint32_t*)counts, (const uint32_t*)totals);
       else
         hipLaunchKernelGGL(k_seg_scatter<false>, dim3(nb), dim3(GSR_SORT_THREADS), 0, stream,
                            (const uint32_t*)keys[src], (const uint32_t*)nullptr, keys[dst], (uint32_t*)nullptr, seg,
-                           shift, bits, (const uint32_t*)counts, (const uint32_t*)totals);
+                           shift, bits, last, (const uint32_t*)counts, (const uint32_t*)totals);
     }
     src = dst;
   }
