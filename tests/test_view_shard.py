@@ -115,3 +115,65 @@ def test_sharded_batch_equals_single_process(world, tmp_path):
             np.testing.assert_allclose(z["grad_" + k], v, rtol=1e-10, atol=1e-12, err_msg=f"rank {rank} grad {k}")
         for i, v in enumerate(ref_stats):
             np.testing.assert_allclose(z[f"stat{i}"], v, rtol=1e-6, atol=1e-9, err_msg=f"rank {rank} stat {i}")
+
+
+class _CarvedGrads(torch.autograd.Function):
+    """Backward returns its inputs' gradients as views of one buffer, as batched.py's backward does."""
+
+    @staticmethod
+    def forward(ctx, scale, *xs):
+        ctx.scale = scale
+        ctx.shapes = [x.shape for x in xs]
+        return sum(x.sum() for x in xs) * 0.0
+
+    @staticmethod
+    def backward(ctx, g):
+        n = [math.prod(s) for s in ctx.shapes]
+        flat = torch.empty(sum(n), dtype=torch.float64)
+        out, off = [], 0
+        for s, k in zip(ctx.shapes, n):
+            out.append(flat[off:off + k].view(s))
+            off += k
+        flat.copy_(torch.arange(flat.numel(), dtype=torch.float64) * ctx.scale)
+        return (None, *out)
+
+
+def _span_worker(rank, world, port, tmp):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        params = [torch.zeros(s, dtype=torch.float64, requires_grad=True) for s in ((7, 3), (7, 1), (7, 16, 3))]
+        _CarvedGrads.apply(float(rank + 1), *params).backward()
+        base = params[0].grad.untyped_storage().data_ptr()
+        shared = all(p.grad.untyped_storage().data_ptr() == base for p in params)
+        ptrs = [p.grad.data_ptr() for p in params]
+        allreduce_grads(params)
+        same = [p.grad.data_ptr() for p in params] == ptrs
+        np.savez(os.path.join(tmp, f"span{rank}.npz"), shared=shared, same=same,
+                 **{f"g{i}": p.grad.numpy() for i, p in enumerate(params)})
+    finally:
+        dist.destroy_process_group()
+
+
+def test_allreduce_carved_grads_in_place(tmp_path):
+    """Gradients carved from one buffer reach the leaves without a copy and are summed in place."""
+    world = 2
+    mp.spawn(_span_worker, args=(world, _free_port(), str(tmp_path)), nprocs=world, join=True)
+    total = sum(r + 1 for r in range(world))
+    for rank in range(world):
+        z = np.load(tmp_path / f"span{rank}.npz")
+        assert bool(z["shared"]) and bool(z["same"])
+        flat = np.concatenate([z[f"g{i}"].reshape(-1) for i in range(3)])
+        np.testing.assert_array_equal(flat, np.arange(flat.size, dtype=np.float64) * total)
+
+
+def test_contiguous_span_detection():
+    from diff_gaussian_rasterization.view_shard import _contiguous_span
+    buf = torch.arange(20.0)
+    a, b, c = buf[0:6].view(2, 3), buf[6:10], buf[10:20].view(5, 2)
+    span = _contiguous_span([c, a, b])
+    assert span is not None and span.data_ptr() == buf.data_ptr() and span.numel() == 20
+    assert _contiguous_span([a, c]) is None            # gap
+    assert _contiguous_span([buf[0:6], buf[4:10]]) is None  # overlap
+    assert _contiguous_span([a, torch.zeros(4)]) is None    # another buffer
+    assert _contiguous_span([buf[0:10:2]]) is None          # strided

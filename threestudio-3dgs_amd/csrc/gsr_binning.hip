@@ -36,45 +36,70 @@ __global__ __launch_bounds__(256) void k_inst_count(int P, int nbe, GeomState g)
   }
 }
 
-// Exclusive scan of one row of n counts in place (one workgroup); returns the total.
-__device__ uint32_t scan_row(uint32_t* row, int n, uint32_t* s_wave) {
-  const int t = threadIdx.x;
-  uint32_t carry = 0u;
-  for (int c0 = 0; c0 < n; c0 += 256 * 4) {
-    uint32_t x[4], run = 0u;
+// One 1024-thread workgroup per view: exclusive scans of its block counts in place, in one pass per
+// 16K blocks (16 consecutive entries per thread; rectangle and kept counts packed as rect << 32 | kept
+// into one 64-bit scan: a view's kept total is < 2^32).  Rectangle tiles K_v -> counters[v], visible
+// Gaussians -> counters[V + v], kept instances -> counters[2V + v].
+#define GSR_ISCAN_PER 16
+__global__ __launch_bounds__(1024) void k_inst_scan(int nbe, GeomState g) {
+  __shared__ unsigned long long s_w[16];
+  __shared__ uint32_t s_v[16];
+  const int v = blockIdx.x, t = threadIdx.x, w = t >> 6, lane = t & 63;
+  uint32_t* rect = g.inst_counts + (size_t)v * nbe;
+  uint32_t* kept = g.kept_counts + (size_t)v * nbe;
+  const uint32_t* vis = g.vis_counts + (size_t)v * nbe;
+  unsigned long long carry = 0ull;
+  uint32_t vis_total = 0u;
+  for (int c0 = 0; c0 < nbe; c0 += 1024 * GSR_ISCAN_PER) {
+    const int i0 = c0 + t * GSR_ISCAN_PER;
+    unsigned long long x[GSR_ISCAN_PER], run = 0ull;
+    uint32_t vs = 0u;
 #pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      const int i = c0 + 4 * t + k;
-      const uint32_t c = i < n ? row[i] : 0u;
+    for (int k = 0; k < GSR_ISCAN_PER; ++k) {
+      const int i = i0 + k;
+      const bool in = i < nbe;
       x[k] = run;
-      run += c;
+      run += in ? ((unsigned long long)rect[i] << 32 | kept[i]) : 0ull;
+      vs += in ? vis[i] : 0u;
     }
-    uint32_t tot;
-    const uint32_t off = carry + block_exclusive_scan<256>(run, &tot, s_wave);
+    unsigned long long inc = run;
 #pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      const int i = c0 + 4 * t + k;
-      if (i < n) row[i] = off + x[k];
+    for (int o = 1; o < 64; o <<= 1) {
+      const unsigned long long y = __shfl_up(inc, o, 64);
+      if (lane >= o) inc += y;
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) vs += (uint32_t)__shfl_xor((int)vs, o, 64);
+    if (lane == 63) s_w[w] = inc;
+    if (lane == 0) s_v[w] = vs;
+    __syncthreads();
+    unsigned long long before = 0ull, tot = 0ull;
+    uint32_t vt = 0u;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      const unsigned long long sw = s_w[i];
+      before += i < w ? sw : 0ull;
+      tot += sw;
+      vt += s_v[i];
+    }
+    __syncthreads();
+    const unsigned long long off = carry + before + (inc - run);
+#pragma unroll
+    for (int k = 0; k < GSR_ISCAN_PER; ++k) {
+      const int i = i0 + k;
+      if (i < nbe) {
+        const unsigned long long r = off + x[k];
+        rect[i] = (uint32_t)(r >> 32);
+        kept[i] = (uint32_t)r;
+      }
     }
     carry += tot;
+    vis_total += vt;
   }
-  return carry;
-}
-
-// One workgroup per view: exclusive scans of its block counts in place; rectangle tiles K_v ->
-// counters[v], visible Gaussians -> counters[V + v], kept instances -> counters[2V + v].
-__global__ __launch_bounds__(256) void k_inst_scan(int nbe, GeomState g) {
-  __shared__ uint32_t s_wave[8];
-  const int v = blockIdx.x, t = threadIdx.x;
-  uint32_t vis = 0u;
-  for (int i = t; i < nbe; i += 256) vis += g.vis_counts[(size_t)v * nbe + i];
-  vis = block_sum_u32<256>(vis, s_wave);
-  const uint32_t rect = scan_row(g.inst_counts + (size_t)v * nbe, nbe, s_wave);
-  const uint32_t kept = scan_row(g.kept_counts + (size_t)v * nbe, nbe, s_wave);
   if (t == 0) {
-    g.counters[v] = rect;
-    g.counters[gridDim.x + v] = vis;
-    g.counters[2 * gridDim.x + v] = kept;
+    g.counters[v] = (uint32_t)(carry >> 32);
+    g.counters[gridDim.x + v] = vis_total;
+    g.counters[2 * gridDim.x + v] = (uint32_t)carry;
   }
 }
 
@@ -238,7 +263,7 @@ void launch_binning_counts(int V, int P, const GeomState& g, hipStream_t stream)
   const int nbe = GeomState::dup_blocks(P);
   if (P > 0)
     hipLaunchKernelGGL(k_inst_count, dim3(V * ((nbe + 3) / 4)), dim3(256), 0, stream, P, nbe, g);
-  hipLaunchKernelGGL(k_inst_scan, dim3(V), dim3(256), 0, stream, P > 0 ? nbe : 0, g);
+  hipLaunchKernelGGL(k_inst_scan, dim3(V), dim3(1024), 0, stream, P > 0 ? nbe : 0, g);
 }
 
 void launch_emit(int V, int P, int W, const GeomState& g, const SegInfo& inst, int gbits, uint32_t* keys,

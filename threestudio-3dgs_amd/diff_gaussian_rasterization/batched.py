@@ -14,6 +14,7 @@ views inside the per-Gaussian kernel.
 from __future__ import annotations
 
 import ctypes
+import math
 import os
 
 import torch
@@ -138,13 +139,22 @@ class _RasterizeViews(torch.autograd.Function):
         H, W = int(s0.image_height), int(s0.image_width)
         fopt = dict(dtype=torch.float32, device=dev)
         d_m2 = torch.empty((V, P, 3), **fopt)
-        d_m3 = torch.empty((P, 3), **fopt)
-        d_op = torch.empty((P, 1), **fopt)
-        d_col = torch.empty((P, 3), **fopt)
-        d_sh = torch.empty((P, M, 3), **fopt) if shc is not None else None
-        d_c3 = torch.empty((P, 6), **fopt) if c3 is not None else None
-        d_sc = torch.empty((P, 3), **fopt) if c3 is None else None
-        d_rot = torch.empty((P, 4), **fopt) if c3 is None else None
+        # the per-Gaussian gradients are carved from one buffer (means3D, scales, rotations, opacities,
+        # SH, cov3D, colours): autograd hands these views to the leaves as their .grad, and
+        # view_shard.allreduce_grads then sums them over ranks in place as one span, without copies
+        widths = [("m3", (3,)), ("sc", (3,) if c3 is None else None), ("rot", (4,) if c3 is None else None),
+                  ("op", (1,)), ("sh", (M, 3) if shc is not None else None), ("c3", (6,) if c3 is not None else None),
+                  ("col", (3,))]
+        flat = torch.empty(P * sum(math.prod(w) for _, w in widths if w is not None), **fopt)
+        carved, off = {}, 0
+        for name, w in widths:
+            carved[name] = None
+            if w is not None:
+                n = P * math.prod(w)
+                carved[name] = flat[off:off + n].view((P,) + w)
+                off += n
+        d_m3, d_sc, d_rot, d_op = carved["m3"], carved["sc"], carved["rot"], carved["op"]
+        d_sh, d_c3, d_col = carved["sh"], carved["c3"], carved["col"]
         d_bg = torch.empty_like(cbg) if cbg is not None and ctx.needs_input_grad[8] else None
         if P == 0:
             if d_bg is not None:

@@ -88,6 +88,23 @@ def all_gather_views(local: torch.Tensor, batch_size: int, group=None) -> torch.
     return _GatherViews.apply(local, batch_size, group)
 
 
+def _contiguous_span(grads):
+    """The tensors as one 1-D view when they tile a gap-free range of a single storage (in any order,
+    same dtype and device, each contiguous, no overlaps), else None."""
+    g0 = grads[0]
+    base = g0.untyped_storage().data_ptr()
+    if any(g.dtype != g0.dtype or g.device != g0.device or not g.is_contiguous()
+           or g.untyped_storage().data_ptr() != base for g in grads):
+        return None
+    order = sorted(grads, key=lambda g: g.storage_offset())
+    start = end = order[0].storage_offset()
+    for g in order:
+        if g.storage_offset() != end:
+            return None
+        end += g.numel()
+    return g0.as_strided((end - start,), (1,), start)
+
+
 def allreduce_grads(params, group=None, average: bool = False):
     """Sum (or average) the .grad of `params` over ranks in one flat bucket (one RCCL all-reduce)."""
     world, _ = _world()
@@ -95,6 +112,12 @@ def allreduce_grads(params, group=None, average: bool = False):
         return
     grads = [p.grad for p in params if p.grad is not None]
     if not grads:
+        return
+    span = _contiguous_span(grads)
+    if span is not None:  # the batched rasterizer's gradients: one buffer, reduced in place
+        dist.all_reduce(span, group=group)
+        if average:
+            span /= world
         return
     flat = torch.cat([g.reshape(-1) for g in grads])
     dist.all_reduce(flat, group=group)
