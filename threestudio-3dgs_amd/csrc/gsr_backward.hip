@@ -392,28 +392,25 @@ __global__ __launch_bounds__(256) void k_gauss_accum(GaussBackwardArgs a, AccumA
 #pragma unroll
     for (int k = 0; k < 48; ++k) dsh[k] = 0.f;
     const float* sh_row = has_sh ? s_sh + t * S : nullptr;
-    // the next view's radius and record (written for every (view, Gaussian), zeros when culled)
-    // are loaded while the current view's SH backward runs
-    int nrad = 0;
-    float nf[GSR_GRAD_FIELDS];
-    if (b.V > 0) {
-      nrad = b.radii[(size_t)b.v0 * a.P + idx];
+    // the views' records (written for every (view, Gaussian), zeros when culled) stream through three
+    // register buffers: while one view's SH backward runs, the next two views' loads are in flight
+    // (the accumulators hold this kernel to 2 waves per SIMD, so the loads in flight come from depth)
+    // buffer loads: one per-lane byte offset for every field and view, the view's base and the field
+    // offset in scalars (no per-load address registers to recycle while loads are in flight)
+    const int lane_off = idx * 4;
+    const int field_bytes = a.P * 4;
+    auto load = [&](float* f, int& rad, int vl) {
+      const auto rr = __builtin_amdgcn_make_buffer_rsrc((void*)(b.radii + (size_t)(b.v0 + vl) * a.P), 0,
+                                                        field_bytes, 0x00020000);
+      rad = (int)__builtin_amdgcn_raw_buffer_load_b32(rr, lane_off, 0, 0);
+      const auto rv = __builtin_amdgcn_make_buffer_rsrc((void*)(b.vrec + (size_t)vl * GSR_GRAD_FIELDS * a.P), 0,
+                                                        GSR_GRAD_FIELDS * field_bytes, 0x00020000);
 #pragma unroll
-      for (int k = 0; k < GSR_GRAD_FIELDS; ++k) nf[k] = b.vrec[(size_t)k * a.P + idx];
-    }
-    for (int vl = 0; vl < b.V; ++vl) {
-      const size_t o = (size_t)(b.v0 + vl) * a.P + idx;
-      const int rad = nrad;
-      float f[GSR_GRAD_FIELDS];
-#pragma unroll
-      for (int k = 0; k < GSR_GRAD_FIELDS; ++k) f[k] = nf[k];
-      if (vl + 1 < b.V) {
-        nrad = b.radii[o + a.P];
-        const float* nrec = b.vrec + (size_t)(vl + 1) * GSR_GRAD_FIELDS * a.P + idx;
-#pragma unroll
-        for (int k = 0; k < GSR_GRAD_FIELDS; ++k) nf[k] = nrec[(size_t)k * a.P];
-      }
-      if (rad <= 0) continue;
+      for (int k = 0; k < GSR_GRAD_FIELDS; ++k)
+        f[k] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rv, lane_off, k * field_bytes, 0));
+    };
+    auto process = [&](const float* f, int rad, int vl) {
+      if (rad <= 0) return;
       dmean.x += f[0];
       dmean.y += f[1];
       dmean.z += f[2];
@@ -434,9 +431,34 @@ __global__ __launch_bounds__(256) void k_gauss_accum(GaussBackwardArgs a, AccumA
           const float4 q = 4 * c < F ? row4[c] : make_float4(0.f, 0.f, 0.f, 0.f);
           shv[4 * c] = q.x, shv[4 * c + 1] = q.y, shv[4 * c + 2] = q.z, shv[4 * c + 3] = q.w;
         }
-        sh_backward(a.deg, a.M, shv, dsh, dRGB, mean, b.campos[vl], dmean);
+        // the camera position through scalar loads (uniform view): a vector load here would be the
+        // newest in flight and its wait would drain the record prefetch
+        typedef __attribute__((address_space(4))) const float* cfptr;
+        const float cpos[3] = {((cfptr)b.campos[vl])[0], ((cfptr)b.campos[vl])[1], ((cfptr)b.campos[vl])[2]};
+        sh_backward(a.deg, a.M, shv, dsh, dRGB, mean, cpos, dmean);
       }
+    };
+    float fa[GSR_GRAD_FIELDS], fb[GSR_GRAD_FIELDS], fc[GSR_GRAD_FIELDS];
+    int ra = 0, rb = 0, rc = 0;
+    // the parameter loads above complete here (vmcnt(0)), so the loop's waits count record loads only
+    __builtin_amdgcn_s_waitcnt(0x0F70);
+    if (b.V > 0) load(fa, ra, 0);
+    if (b.V > 1) load(fb, rb, 1);
+    if (b.V > 2) load(fc, rc, 2);
+    int vl = 0;
+    // (the refills are unconditional, clamped to the last view, so every path has the same loads in
+    // flight and each process waits for its own buffer only)
+    const int vlast = b.V - 1;
+    for (; vl + 2 < b.V; vl += 3) {
+      process(fa, ra, vl);
+      load(fa, ra, min(vl + 3, vlast));
+      process(fb, rb, vl + 1);
+      load(fb, rb, min(vl + 4, vlast));
+      process(fc, rc, vl + 2);
+      load(fc, rc, min(vl + 5, vlast));
     }
+    if (vl < b.V) process(fa, ra, vl);
+    if (vl + 1 < b.V) process(fb, rb, vl + 1);
     put(&a.dL_dmeans3D[3 * idx], dmean.x, acc);
     put(&a.dL_dmeans3D[3 * idx + 1], dmean.y, acc);
     put(&a.dL_dmeans3D[3 * idx + 2], dmean.z, acc);
