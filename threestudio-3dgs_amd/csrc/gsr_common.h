@@ -312,6 +312,17 @@ __device__ __forceinline__ float gauss_power(float a, float b, float c, float dx
   return fmaf(-0.5f, q, -((b * dx) * dy));
 }
 
+// The blends' form of the same exponent: the conic staged pre-multiplied (A = -0.5 log2e a,
+// B = -log2e b, C = -0.5 log2e c) so that log2e * power = dx (A dx + B dy) + C dy^2 takes 5 fp32
+// operations and alpha = o exp2(.) needs no log2e multiply (8 VALU per (pixel, Gaussian) instead of
+// 11 with the subtractions).  Equal to gauss_power * log2e up to a few ulp (the reference's own
+// rounding of this expression is no closer to exact).
+#define GSR_CONIC_K_AC (-0.72134752044448170f)  // -0.5 log2(e)
+#define GSR_CONIC_K_B (-1.4426950408889634f)    // -log2(e)
+__device__ __forceinline__ float gauss_power2(float A, float B, float C, float dx, float dy) {
+  return fmaf(dx, fmaf(A, dx, B * dy), (C * dy) * dy);
+}
+
 // Tile-level culling of a Gaussian's 3-sigma rectangle (the reference bins every rectangle tile).
 // Tiles of row ty (pixel rows 16 ty .. 16 ty + 15) that contain a pixel with alpha >= 1/255:
 // [tx0, tx1) within [xmin, xmax).  A pixel contributes only if o exp(-Q/2) >= 1/255 with

@@ -178,9 +178,10 @@ __global__ __launch_bounds__(64) void k_render_fwd(RenderSet rs,
     const unsigned long long bal = __ballot(keep);
     const int cnt = __popcll(bal);
     if (keep) {
+      // the conic pre-multiplied for gauss_power2 (.w of s1: 1 + list position)
       const uint32_t pos = mask_rank(bal);
-      s0[pos] = r0;
-      s1[pos] = make_float4(r1.x, r1.y, r1.z, __uint_as_float((uint32_t)(i + 1)));  // .w: 1 + list position
+      s0[pos] = make_float4(r0.x, r0.y, GSR_CONIC_K_AC * r0.z, GSR_CONIC_K_B * r0.w);
+      s1[pos] = make_float4(GSR_CONIC_K_AC * r1.x, r1.y, r1.z, __uint_as_float((uint32_t)(i + 1)));
       s2[pos] = r2;
     }
     __syncthreads();
@@ -189,9 +190,9 @@ __global__ __launch_bounds__(64) void k_render_fwd(RenderSet rs,
       if ((k & 7) == 0 && __all(done)) break;
       const float4 an = s0[k + 1], bn = s1[k + 1], cn = s2[k + 1];
       const float dx = a.x - pxf, dy = a.y - pyf;
-      const float power = gauss_power(a.z, a.w, b.x, dx, dy);
-      const float alpha = fminf(GSR_ALPHA_MAX, b.y * __expf(power));
-      const bool ok = !done && power <= 0.0f && alpha >= GSR_ALPHA_MIN;
+      const float power2 = gauss_power2(a.z, a.w, b.x, dx, dy);  // log2(e) * power
+      const float alpha = fminf(GSR_ALPHA_MAX, b.y * __builtin_amdgcn_exp2f(power2));
+      const bool ok = !done && power2 <= 0.0f && alpha >= GSR_ALPHA_MIN;
       const float test_T = T * (1.0f - alpha);
       const bool term = ok && test_T < GSR_T_EPS;
       const bool blend = ok && !term;
@@ -202,7 +203,7 @@ __global__ __launch_bounds__(64) void k_render_fwd(RenderSet rs,
       Cg = fmaf(c.y, aT, Cg);
       Cb = fmaf(c.z, aT, Cb);
       D = fmaf(b.z, aT, D);
-      T = T * (1.0f - a_eff);
+      T = blend ? test_T : T;  // = T (1 - a_eff)
       last_contributor = blend ? __float_as_uint(b.w) : last_contributor;
       done = done || term;
       a = an;
@@ -452,10 +453,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5, 8))) voi
   auto replay = [&](const float4& ga, const float4& gb, const float4& gc, float& u, float& w) {
     const uint32_t rel = __float_as_uint(gb.w);
     const float dx = ga.x - pxf, dy = ga.y - pyf;
-    const float power = gauss_power(ga.z, ga.w, gb.x, dx, dy);
-    const float G = __expf(power);
+    const float power2 = gauss_power2(ga.z, ga.w, gb.x, dx, dy);  // log2(e) * power
+    const float G = __builtin_amdgcn_exp2f(power2);
     const float alpha = fminf(GSR_ALPHA_MAX, gb.y * G);
-    const bool hit = rel < last_contributor && power <= 0.0f && alpha >= GSR_ALPHA_MIN;
+    const bool hit = rel < last_contributor && power2 <= 0.0f && alpha >= GSR_ALPHA_MIN;
     const float a_eff = hit ? alpha : 0.0f;
     const float g_eff = hit ? G : 0.0f;
     const float oma = 1.f - a_eff;
@@ -534,10 +535,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5, 8))) voi
     {
       const int rel_c = hi - 1 - cs;
       if (rel_c >= 0) {
+        // the conic pre-multiplied for gauss_power2 (.w of s1: list position)
         if (piece == 0) {
-          s.s0[cs] = npc;
+          s.s0[cs] = make_float4(npc.x, npc.y, GSR_CONIC_K_AC * npc.z, GSR_CONIC_K_B * npc.w);
         } else if (piece == 1) {
-          s.s1[cs] = make_float4(npc.x, npc.y, npc.z, __uint_as_float((uint32_t)rel_c));  // .w: list position
+          s.s1[cs] = make_float4(GSR_CONIC_K_AC * npc.x, npc.y, npc.z, __uint_as_float((uint32_t)rel_c));
         } else if (piece == 2) {
           s.s2[cs] = npc;
         } else {
@@ -558,7 +560,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5, 8))) voi
 #ifdef GSR_EXP_NOCULL
     if (rel_l >= 0 && rel_l < qmaxc) keep = s.s0[lane].x > -1e30f;
 #else
-    if (rel_l >= 0 && rel_l < qmaxc) keep = quadrant_hit(s.s0[lane], s.s1[lane], (float)qx0, (float)qy0);
+    if (rel_l >= 0 && rel_l < qmaxc) {
+      // the staged conic back to (a, b, c) for the (padded, conservative) cull
+      const float4 c0 = s.s0[lane], c1 = s.s1[lane];
+      keep = quadrant_hit(make_float4(c0.x, c0.y, c0.z * (1.0f / GSR_CONIC_K_AC), c0.w * (1.0f / GSR_CONIC_K_B)),
+                          make_float4(c1.x * (1.0f / GSR_CONIC_K_AC), c1.y, c1.z, c1.w), (float)qx0, (float)qy0);
+    }
 #endif
     const unsigned long long bal = __ballot(keep);
     const int cnt = __popcll(bal);
@@ -676,8 +683,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5, 8))) voi
       const float o = gb.y;
       float4* row = grow + 3 * (size_t)s.slot[cs];
       if (qq == 0) {
-        const float dmx = -o * ddelx_dx * (ga.z * m[1] + ga.w * m[2]);
-        const float dmy = -o * ddely_dy * (gb.x * m[2] + ga.w * m[1]);
+        // -o (W/2) (a m1 + b m2) etc. with the staged A = -log2e a / 2, B = -log2e b, C = -log2e c / 2
+        const float k = o * (1.0f / 1.4426950408889634f);
+        const float dmx = k * ddelx_dx * (2.0f * ga.z * m[1] + ga.w * m[2]);
+        const float dmy = k * ddely_dy * (2.0f * gb.x * m[2] + ga.w * m[1]);
         row[0] = make_float4(dmx, dmy, -0.5f * o * m[3], -0.5f * o * m[4]);
       } else if (qq == 1) {
         row[1] = make_float4(-0.5f * o * m[5], m[0], m[6], m[7]);
