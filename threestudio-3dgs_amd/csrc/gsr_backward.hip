@@ -29,12 +29,12 @@ struct RowSums {
 // instance (cut = (key, index) per tile).  Rows sit at rectangle positions.  Tiles are walked 4 at
 // a time: the 4 cut tests first, then the valid rows' loads together, so a thread has up to 12
 // loads in flight instead of waiting on each row in turn.
-__device__ __forceinline__ RowSums gather_rows(uint32_t idx, const GaussRec& gr, int grid_x, const uint2* cut,
-                                               const float4* grow) {
+__device__ __forceinline__ RowSums gather_rows(uint32_t idx, const GaussRec& gr, uint32_t i0, int grid_x,
+                                               const uint2* cut, const float4* grow) {
   RowSums r = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
   const uint4 gd = gr.d;
   const float4 ga = gr.a, gb = gr.b;
-  const uint32_t dkey = __float_as_uint(gb.z), i0 = gd.z;
+  const uint32_t dkey = __float_as_uint(gb.z);
   const int xmin = gd.x & 0xffff, ymin = gd.x >> 16, xmax = gd.y & 0xffff, ymax = gd.y >> 16;
   const int w = xmax - xmin;
   const SpanPrep sp = span_prep(ga.x, ga.y, ga.z, ga.w, gb.x, gb.y);
@@ -302,10 +302,11 @@ __global__ __launch_bounds__(256) void k_view_grad(GaussBackwardArgs a, ViewGrad
   const int idx_base = (blockIdx.x / va.V) * (256 * GSR_VG_ITEMS) + t;
   int nrad = 0;
   GaussRec nrec;
+  uint32_t ngo = 0u;
   if (idx_base < a.P) {
     const size_t o0 = (size_t)vg * a.P + idx_base;
     nrad = va.radii[o0];
-    if (nrad > 0) nrec = va.g.rec[o0];
+    if (nrad > 0) nrec = va.g.rec[o0], ngo = va.g.goff[o0];
   }
 #pragma unroll 1
   for (int it = 0; it < GSR_VG_ITEMS; ++it) {
@@ -314,9 +315,10 @@ __global__ __launch_bounds__(256) void k_view_grad(GaussBackwardArgs a, ViewGrad
     const size_t o = (size_t)vg * a.P + idx;
     const int rad = nrad;
     const GaussRec gr = nrec;
+    const uint32_t go = ngo;
     if (it + 1 < GSR_VG_ITEMS && idx + 256 < a.P) {
       nrad = va.radii[o + 256];
-      if (nrad > 0) nrec = va.g.rec[o + 256];
+      if (nrad > 0) nrec = va.g.rec[o + 256], ngo = va.g.goff[o + 256];
     }
     float* m2 = va.dmeans2D + 3 * o;
     float* rec = recv + idx;
@@ -329,7 +331,7 @@ __global__ __launch_bounds__(256) void k_view_grad(GaussBackwardArgs a, ViewGrad
       continue;
     }
     const uint32_t clamp_bits = gr.d.w;
-    const RowSums r = gather_rows((uint32_t)idx, gr, va.gx, cut, grow);
+    const RowSums r = gather_rows((uint32_t)idx, gr, go, va.gx, cut, grow);
     m2[0] = r.dmx;
     m2[1] = r.dmy;
     m2[2] = 0.f;

@@ -103,19 +103,116 @@ __global__ __launch_bounds__(1024) void k_inst_scan(int nbe, GeomState g) {
   }
 }
 
+// Gradient-row slots: goff[v][i] = sum of tiles[v][j].x over j < i (each visible Gaussian owns
+// tiles.x consecutive rows, one per rectangle tile), in three coalesced passes: block sums, one
+// scan per view, block scans + offsets.
+__global__ __launch_bounds__(256) void k_goff_count(int P, int nbg, GeomState g) {
+  __shared__ uint32_t s_wave[8];
+  const int v = blockIdx.x / nbg, b = blockIdx.x - v * nbg, t = threadIdx.x;
+  const uint2* tl = g.tiles + (size_t)v * P;
+  uint32_t sum = 0u;
+#pragma unroll
+  for (int k = 0; k < GSR_GOFF_TILE / 256; ++k) {
+    const int i = b * GSR_GOFF_TILE + k * 256 + t;
+    sum += i < P ? tl[i].x : 0u;
+  }
+  sum = block_sum_u32<256>(sum, s_wave);
+  if (t == 0) g.goff_part[(size_t)v * nbg + b] = sum;
+}
+
+__global__ __launch_bounds__(1024) void k_goff_scan(int nbg, GeomState g) {
+  __shared__ uint32_t s_w[16];
+  const int v = blockIdx.x, t = threadIdx.x, w = t >> 6, lane = t & 63;
+  uint32_t* row = g.goff_part + (size_t)v * nbg;
+  uint32_t carry = 0u;
+  for (int c0 = 0; c0 < nbg; c0 += 1024 * 4) {
+    const int i0 = c0 + 4 * t;
+    uint32_t x[4], run = 0u;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      x[k] = run;
+      run += i0 + k < nbg ? row[i0 + k] : 0u;
+    }
+    uint32_t inc = run;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const uint32_t y = (uint32_t)__shfl_up((int)inc, o, 64);
+      if (lane >= o) inc += y;
+    }
+    if (lane == 63) s_w[w] = inc;
+    __syncthreads();
+    uint32_t before = 0u, tot = 0u;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      const uint32_t sw = s_w[i];
+      before += i < w ? sw : 0u;
+      tot += sw;
+    }
+    __syncthreads();
+    const uint32_t off = carry + before + (inc - run);
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+      if (i0 + k < nbg) row[i0 + k] = off + x[k];
+    carry += tot;
+  }
+}
+
+// (coalesced loads and stores; each thread scans 16 consecutive entries through LDS, one pad word
+// per 16 so the per-thread runs are bank-conflict free)
+__global__ __launch_bounds__(256) void k_goff_write(int P, int nbg, GeomState g) {
+  __shared__ uint32_t s_x[GSR_GOFF_TILE + GSR_GOFF_TILE / 16];
+  __shared__ uint32_t s_wave[8];
+  const int v = blockIdx.x / nbg, b = blockIdx.x - v * nbg, t = threadIdx.x;
+  const uint2* tl = g.tiles + (size_t)v * P + (size_t)b * GSR_GOFF_TILE;
+  uint32_t* go = g.goff + (size_t)v * P + (size_t)b * GSR_GOFF_TILE;
+  const int n = min(GSR_GOFF_TILE, P - b * GSR_GOFF_TILE);
+  constexpr int PER = GSR_GOFF_TILE / 256;
+  auto pad = [](int i) { return i + (i >> 4); };
+#pragma unroll
+  for (int k = 0; k < PER; ++k) {
+    const int i = k * 256 + t;
+    s_x[pad(i)] = i < n ? tl[i].x : 0u;
+  }
+  __syncthreads();
+  uint32_t x[PER], run = 0u;
+#pragma unroll
+  for (int k = 0; k < PER; ++k) {
+    const uint32_t c = s_x[pad(t * PER + k)];
+    x[k] = run;
+    run += c;
+  }
+  uint32_t tot;
+  const uint32_t off = g.goff_part[(size_t)v * nbg + b] + block_exclusive_scan<256>(run, &tot, s_wave);
+#pragma unroll
+  for (int k = 0; k < PER; ++k) s_x[pad(t * PER + k)] = off + x[k];
+  __syncthreads();
+#pragma unroll
+  for (int k = 0; k < PER; ++k) {
+    const int i = k * 256 + t;
+    if (i < n) go[i] = s_x[pad(i)];
+  }
+}
+
 // Emit one (tile id, Gaussian) instance per kept tile (span_row) of each visible Gaussian, in
-// depth order, and goff[g] = the Gaussian's first rectangle slot (gradient rows are indexed by
-// rectangle position, the lists hold the kept tiles only).  One wave per 64 consecutive depth-sorted
-// Gaussians, no workgroup barriers: the group's rectangle positions are walked 64 at a time, the
-// owner of every position comes from an owner map in the wave's LDS (each Gaussian marks its first
-// position, a DPP max-scan spreads the marks), and the kept positions are compacted in order with
-// ballots into the group's contiguous output range (offset from k_inst_scan).
+// depth order (gradient-row slots come from k_goff_*, in Gaussian order: a scattered 4-byte goff
+// store per Gaussian here cost ~20 us/view, DRAM-transaction bound).  One wave per 64 consecutive depth-sorted
+// Gaussians, no workgroup barriers.  Two levels of owner maps (each Gaussian / row marks its first
+// position in the wave's LDS, a DPP max-scan spreads the marks):
+//   rows:  the group's rectangle rows, 64 at a time; one span_row per (Gaussian, row) gives the row's
+//          kept tiles [t0, t1) and, by a DPP prefix sum, their place in the group's output range;
+//   kept:  the kept positions of those rows, 64 at a time; lane j's row owner gives its tile directly
+//          (row tile t0 + offset), so every instance is written with a coalesced store, in order,
+//          without per-position span tests, divisions or ballots.
 struct EmitLDS {
-  uint32_t off[GSR_DUP_TILE];
   uint32_t gi[GSR_DUP_TILE];
+  uint32_t roff[GSR_DUP_TILE];  // per Gaussian: its first row in the group's row list
   uint2 rect[GSR_DUP_TILE];
   SpanPrep sp[GSR_DUP_TILE];
-  uint32_t own[64];
+  uint32_t own[64];             // row -> 1 + owning Gaussian (marks)
+  uint32_t rk[64];              // per row of the chunk: its first kept position (chunk-relative)
+  uint32_t rtile[64];           // per row of the chunk: tile id of its first kept tile
+  uint32_t rgi[64];             // per row of the chunk: the Gaussian
+  uint32_t kown[64];            // kept position -> 1 + owning row (marks)
 };
 
 #define GSR_EMIT_GROUPS 2  // consecutive 64-Gaussian groups per wave (the next group's gathers prefetched)
@@ -133,7 +230,7 @@ __global__ __launch_bounds__(64) void k_emit(int P, int nbe, int grid_x, GeomSta
   uint32_t* kout = keys + inst.start[v];
   uint32_t* vout = vals ? vals + inst.start[v] : nullptr;
   // group prefetch: order, visibility and the record pieces of group lb + 1 load while lb emits
-  uint32_t n_gi = 0u, n_ioff = 0u, n_koff = 0u;
+  uint32_t n_gi = 0u, n_koff = 0u;
   bool n_vis = false;
   float4 n_ra = make_float4(0.f, 0.f, 0.f, 0.f), n_rb = n_ra;
   uint2 n_d = make_uint2(0u, 0u);
@@ -141,7 +238,6 @@ __global__ __launch_bounds__(64) void k_emit(int P, int nbe, int grid_x, GeomSta
     const int r = lb * GSR_DUP_TILE + lane;
     n_gi = r < P ? order[vo + r] : 0u;
     n_vis = r < P && dkeys[vo + r] != 0xFFFFFFFFu;
-    n_ioff = g.inst_counts[(size_t)v * nbe + lb];
     n_koff = g.kept_counts[(size_t)v * nbe + lb];
     if (n_vis) {
       const GaussRec& rc = g.rec[vo + n_gi];
@@ -153,65 +249,73 @@ __global__ __launch_bounds__(64) void k_emit(int P, int nbe, int grid_x, GeomSta
   };
   if (lb0 < lb1) fetch(lb0);
   for (int lb = lb0; lb < lb1; ++lb) {
-    const uint32_t gi = n_gi, ioff = n_ioff;
+    const uint32_t gi = n_gi;
     const bool vis = n_vis;
     const float4 ra = n_ra, rb = n_rb;
     const uint2 d = n_d;
     uint32_t kbase = n_koff;
     if (lb + 1 < lb1) fetch(lb + 1);
-    uint32_t cnt = 0u;
-    s.gi[lane] = gi;
-    s.rect[lane] = make_uint2(0u, 0u);
+    uint32_t cnt = 0u, h = 0u;
     if (vis) {
-      cnt = ((d.y & 0xffffu) - (d.x & 0xffffu)) * ((d.y >> 16) - (d.x >> 16));  // rectangle tiles
-      s.rect[lane] = d;
-      s.sp[lane] = span_prep(ra.x, ra.y, ra.z, ra.w, rb.x, rb.y);
+      const uint32_t wd = (d.y & 0xffffu) - (d.x & 0xffffu);
+      h = (d.y >> 16) - (d.x >> 16);
+      cnt = wd * h;  // rectangle tiles
+      if (cnt == 0u) h = 0u;
     }
-    const uint32_t incl = wave_incl_sum_dpp(cnt);
-    const uint32_t myoff = incl - cnt;
-    const uint32_t btot = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
-    s.off[lane] = myoff;
-    // gradient-row slots: rectangle offsets (all of a visible Gaussian's rectangle, kept or not)
-    if (cnt) g.rec[vo + gi].d.z = ioff + myoff;
-    uint32_t carry = 0u;  // 1 + owner of the previous chunk's last position
-    for (uint32_t c0 = 0; c0 < btot; c0 += 64) {
+    const uint32_t rincl = wave_incl_sum_dpp(h);
+    const uint32_t roff = rincl - h;
+    const uint32_t R = (uint32_t)__builtin_amdgcn_readlane((int)rincl, 63);
+    s.gi[lane] = gi;
+    s.roff[lane] = roff;
+    s.rect[lane] = d;
+    if (h) s.sp[lane] = span_prep(ra.x, ra.y, ra.z, ra.w, rb.x, rb.y);
+    uint32_t carry = 0u;  // 1 + owner of the previous chunk's last row
+    for (uint32_t r0 = 0; r0 < R; r0 += 64) {
       s.own[lane] = 0u;
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      if (cnt && myoff >= c0 && myoff < c0 + 64) s.own[myoff - c0] = (uint32_t)lane + 1u;
+      if (h && roff >= r0 && roff < r0 + 64) s.own[roff - r0] = (uint32_t)lane + 1u;
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       const uint32_t ow1 = max(carry, wave_incl_max_dpp(s.own[lane]));
       carry = (uint32_t)__builtin_amdgcn_readlane((int)ow1, 63);
-      const uint32_t j = c0 + (uint32_t)lane;
-      bool kp = false;
-      uint32_t key = 0u, gv = 0u;
-      if (j < btot) {
+      const uint32_t r = r0 + (uint32_t)lane;
+      uint32_t kc = 0u, tile0 = 0u, rg = 0u;
+      if (r < R) {
         const uint32_t ow = ow1 - 1u;
         const uint2 rc = s.rect[ow];
-        const uint32_t xmin = rc.x & 0xffffu, ymin = rc.x >> 16, xmax = rc.y & 0xffffu;
-        const uint32_t wd = xmax - xmin, l = j - s.off[ow];
-        // l / wd without the ~35-instruction integer division: l < 2^24, so the float quotient is
-        // within one of the true one; one correction step makes it exact
-        int ty = (int)((float)l * __builtin_amdgcn_rcpf((float)wd));
-        int tx = (int)l - ty * (int)wd;
-        if (tx < 0) { --ty; tx += (int)wd; }
-        else if (tx >= (int)wd) { ++ty; tx -= (int)wd; }
-        const int row = (int)ymin + ty, col = (int)xmin + tx;
-        const SpanPrep sp = s.sp[ow];
+        const int xmin = (int)(rc.x & 0xffffu), xmax = (int)(rc.y & 0xffffu);
+        const int row = (int)(rc.x >> 16) + (int)(r - s.roff[ow]);
         int t0, t1;
-        span_row(sp, row, (int)xmin, (int)xmax, t0, t1);
-        kp = col >= t0 && col < t1;
-        const uint32_t tile = (uint32_t)row * (uint32_t)grid_x + (uint32_t)col;
-        gv = s.gi[ow];
-        key = vout ? tile : ((tile << gbits) | gv);
+        span_row(s.sp[ow], row, xmin, xmax, t0, t1);
+        kc = (uint32_t)(t1 - t0);
+        tile0 = (uint32_t)row * (uint32_t)grid_x + (uint32_t)t0;
+        rg = s.gi[ow];
       }
-      const unsigned long long bal = __ballot(kp);
-      if (kp) {
-        const uint32_t o = kbase + mask_rank(bal);
-        kout[o] = key;
-        if (vout) vout[o] = gv;
+      const uint32_t kincl = wave_incl_sum_dpp(kc);
+      const uint32_t kstart = kincl - kc;
+      const uint32_t KC = (uint32_t)__builtin_amdgcn_readlane((int)kincl, 63);
+      s.rk[lane] = kstart;
+      s.rtile[lane] = tile0;
+      s.rgi[lane] = rg;
+      uint32_t kcarry = 0u;  // 1 + owning row of the previous chunk's last kept position
+      for (uint32_t k0 = 0; k0 < KC; k0 += 64) {
+        s.kown[lane] = 0u;
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        if (kc && kstart >= k0 && kstart < k0 + 64) s.kown[kstart - k0] = (uint32_t)lane + 1u;
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        const uint32_t kw1 = max(kcarry, wave_incl_max_dpp(s.kown[lane]));
+        kcarry = (uint32_t)__builtin_amdgcn_readlane((int)kw1, 63);
+        const uint32_t j = k0 + (uint32_t)lane;
+        if (j < KC) {
+          const uint32_t rr = kw1 - 1u;
+          const uint32_t tile = s.rtile[rr] + (j - s.rk[rr]);
+          const uint32_t gv = s.rgi[rr];
+          kout[kbase + j] = vout ? tile : ((tile << gbits) | gv);
+          if (vout) vout[kbase + j] = gv;
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // kown[] is rewritten by the next chunk
       }
-      kbase += (uint32_t)__popcll(bal);
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // own[] is rewritten by the next chunk
+      kbase += KC;
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the row table is rewritten by the next chunk
     }
   }
 }
@@ -261,6 +365,12 @@ __global__ __launch_bounds__(256) void k_tile_ranges(SegInfo inst, int n_tiles, 
 void launch_binning_counts(int V, int P, const GeomState& g, hipStream_t stream) {
   if (V <= 0) return;
   const int nbe = GeomState::dup_blocks(P);
+  if (P > 0) {
+    const int nbg = GeomState::goff_blocks(P);
+    hipLaunchKernelGGL(k_goff_count, dim3(V * nbg), dim3(256), 0, stream, P, nbg, g);
+    hipLaunchKernelGGL(k_goff_scan, dim3(V), dim3(1024), 0, stream, nbg, g);
+    hipLaunchKernelGGL(k_goff_write, dim3(V * nbg), dim3(256), 0, stream, P, nbg, g);
+  }
   if (P > 0)
     hipLaunchKernelGGL(k_inst_count, dim3(V * ((nbe + 3) / 4)), dim3(256), 0, stream, P, nbe, g);
   hipLaunchKernelGGL(k_inst_scan, dim3(V), dim3(1024), 0, stream, P > 0 ? nbe : 0, g);

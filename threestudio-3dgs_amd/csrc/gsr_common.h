@@ -19,6 +19,7 @@
 #define GSR_RADIX_BITS 8
 #define GSR_RADIX (1 << GSR_RADIX_BITS)
 // Instance emission: 256 threads x 4 depth-sorted Gaussians per block.
+#define GSR_GOFF_TILE 4096  // Gaussians per block of the gradient-row offset scan (256 threads x 16)
 #define GSR_DUP_TILE 64  // depth-sorted Gaussians per emission group (one wave)
 // Tile ranges: 4 waves x 16 rounds x 64 instances per block.
 #define GSR_RANGE_TILE 4096
@@ -151,7 +152,7 @@ struct SetCams {
 
 // The per-(view, Gaussian) record every per-instance gather reads: one 64-byte line.
 //   a = (px, py, conic_a, conic_b), b = (conic_c, opacity, view depth, 0), c = (r, g, b, 0),
-//   d = (tile rect xmin | ymin << 16, xmax | ymax << 16, goff = first instance, SH clamp flags)
+//   d = (tile rect xmin | ymin << 16, xmax | ymax << 16, 0, SH clamp flags)
 struct __attribute__((aligned(64))) GaussRec {
   float4 a, b, c;
   uint4 d;
@@ -170,6 +171,10 @@ struct GeomState {
   uint32_t* inst_counts;     // [V][emission blocks] rectangle tiles per block -> scanned offsets
   uint32_t* kept_counts;     // [V][emission blocks] kept instances per block -> scanned offsets
   uint32_t* vis_counts;      // [V][emission blocks] visible Gaussians per block
+  uint32_t* goff;            // [V][P] first gradient-row slot of each visible Gaussian: exclusive scan
+                             // of tiles.x in Gaussian order (any disjoint assignment works; this one is
+                             // written with coalesced stores)
+  uint32_t* goff_part;       // [V][goff blocks] per-4096-Gaussian sums of tiles.x -> scanned offsets
   uint32_t* drange;          // depth key range of the set: [0, 64) min slots, [64, 128) max slots,
                              // [128] = min visible key, [129] = 1 if 3 depth-sort passes suffice
   // the depth-sorted (keys, Gaussians) of every view: the 4th pass's output, or the 3rd's when it was skipped
@@ -179,6 +184,7 @@ struct GeomState {
                              // [V, 2V) visible Gaussians, [2V, 3V) kept list instances
   static int sort_blocks(int P) { return div_up(P > 0 ? P : 1, GSR_SORT_TILE); }
   static int dup_blocks(int P) { return div_up(P > 0 ? P : 1, GSR_DUP_TILE); }
+  static int goff_blocks(int P) { return div_up(P > 0 ? P : 1, GSR_GOFF_TILE); }
   static GeomState carve(void* base, int V, int P, size_t* bytes) {
     Carver c(base);
     GeomState g;
@@ -196,6 +202,8 @@ struct GeomState {
     g.vis_counts = c.take<uint32_t>(nv * dup_blocks(P));
     g.kept_counts = c.take<uint32_t>(nv * dup_blocks(P));
     g.counters = c.take<uint32_t>(3 * nv + 64);
+    g.goff = c.take<uint32_t>(n);
+    g.goff_part = c.take<uint32_t>(nv * goff_blocks(P));
     g.drange = c.take<uint32_t>(132);
     if (bytes) *bytes = align_up(c.off, 256);
     return g;

@@ -343,6 +343,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5, 8))) voi
                                                     const uint32_t* __restrict__ quad_maxc,
                                                     const uint32_t* __restrict__ sorted_gauss,
                                                     const GaussRec* __restrict__ rec,
+                                                    const uint32_t* __restrict__ goff,
                                                     const float* __restrict__ final_Ts,
                                                     const uint32_t* __restrict__ n_contrib,
                                                     const float* __restrict__ dL_dcolor,
@@ -362,6 +363,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5, 8))) voi
     quad_maxc += vg * 4 * tiles;
     sorted_gauss += rs.inst_start[v];
     rec += vg * rs.P;
+    goff += vg * rs.P;
     final_Ts += vg * HWs;
     n_contrib += vg * HWs;
     dL_dcolor += (size_t)v * 3 * HWs;
@@ -438,11 +440,15 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5, 8))) voi
     const int r = h - 1 - cs;
     return r >= 0 ? (sorted_gauss[range.x + r] & gmask) : 0u;
   };
-  float4 npc = zero4;  // the next batch's piece
+  float4 npc = zero4;  // the next batch's piece (piece 3 also carries the Gaussian's first row slot)
+  uint32_t ngo = 0u;
   uint32_t gi_next = 0u;
   if (maxc > 0) {
     const uint32_t g0 = fetch_index(maxc);
-    if (maxc - 1 - cs >= 0) npc = reinterpret_cast<const float4*>(rec + g0)[piece];
+    if (maxc - 1 - cs >= 0) {
+      npc = reinterpret_cast<const float4*>(rec + g0)[piece];
+      if (piece == 3) ngo = goff[g0];
+    }
     if (maxc > 64) gi_next = fetch_index(maxc - 64);
   }
 
@@ -543,13 +549,16 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5, 8))) voi
         } else if (piece == 2) {
           s.s2[cs] = npc;
         } else {
-          const uint32_t dx_ = __float_as_uint(npc.x), dy_ = __float_as_uint(npc.y), dz_ = __float_as_uint(npc.z);
+          const uint32_t dx_ = __float_as_uint(npc.x), dy_ = __float_as_uint(npc.y);
           const int xmin = dx_ & 0xffff, ymin = dx_ >> 16, xmax = dy_ & 0xffff;
-          s.slot[cs] = dz_ + (uint32_t)((tyi - ymin) * (xmax - xmin) + (txi - xmin));
+          s.slot[cs] = ngo + (uint32_t)((tyi - ymin) * (xmax - xmin) + (txi - xmin));
         }
       }
       if (hi > 64) {
-        if (hi - 65 - cs >= 0) npc = reinterpret_cast<const float4*>(rec + gi_next)[piece];
+        if (hi - 65 - cs >= 0) {
+          npc = reinterpret_cast<const float4*>(rec + gi_next)[piece];
+          if (piece == 3) ngo = goff[gi_next];
+        }
         if (hi > 128) gi_next = fetch_index(hi - 128);
       }
     }
@@ -714,7 +723,7 @@ void launch_render_backward(const RenderSet& rs, const GeomState& g, const uint3
   if (nt <= 0 || rs.V <= 0) return;
   hipLaunchKernelGGL(k_render_bwd, dim3(rs.V * tile_grid(rs.gx, rs.gy)), dim3(256), 0, stream, rs,
                      (const uint2*)img.ranges, (const uint32_t*)img.quad_maxc, sorted_gauss,
-                     (const GaussRec*)g.rec, (const float*)img.final_T,
+                     (const GaussRec*)g.rec, (const uint32_t*)g.goff, (const float*)img.final_T,
                      (const uint32_t*)img.n_contrib, dL_dcolor, dL_ddepth, dL_dalpha, bw.grow);
 }
 
