@@ -690,7 +690,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5, 8))) voi
         m[i] += dpp_f32<0x4E>(m[i]);  // quad_perm [2,3,0,1]
       }
       const float o = gb.y;
+#ifdef GSR_EXP_COALROWS
+      float4* row = grow + 3 * ((size_t)blockIdx.x * 64 + cs);  // timing only: coalesced, wrong slots
+#else
       float4* row = grow + 3 * (size_t)s.slot[cs];
+#endif
       if (qq == 0) {
         // -o (W/2) (a m1 + b m2) etc. with the staged A = -log2e a / 2, B = -log2e b, C = -log2e c / 2
         const float k = o * (1.0f / 1.4426950408889634f);
