@@ -253,7 +253,7 @@ int gsr_set_preprocess(int V, int P, int degree, int M, const float* means3D, co
       seg.start[v] = (uint32_t)((size_t)v * P);
     }
     seg.rebase = g.drange + 128;  // keys ranked relative to the set's smallest visible key (preprocess)
-    const int res = seg_sort(g.dkey, g.dval, true, seg, 0, 32, g.sort_counts, g.sort_totals, s);
+    const int res = seg_sort(g.dkey, g.dval, false, seg, 0, 32, g.sort_counts, g.sort_totals, s);
     if (res != depth_sort_result()) return fail(GSR_EHIP, "%s", "internal: depth sort result buffer");
     launch_binning_counts(V, P, g, s);  // reads the sorted buffer the device flag names (3 or 4 passes)
   }

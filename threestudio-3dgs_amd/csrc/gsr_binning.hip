@@ -14,8 +14,9 @@
 
 namespace gsr {
 
-// Rectangle tiles, visible Gaussians and kept tiles of each 64-Gaussian group of every view's depth
-// order (one wave per group, 4 groups per block): counts[v][group].
+// Kept tiles of each 64-Gaussian group of every view's depth order (one wave per group, 4 groups per
+// block): kept_counts[v][group].  The counts ride in the depth-sorted values (streamed); a count that
+// did not fit its field is read from tiles.y.
 __global__ __launch_bounds__(256) void k_inst_count(int P, int nbe, GeomState g) {
   const uint32_t* __restrict__ order = g.sorted_dval();
   const int nb4 = (nbe + 3) / 4;
@@ -25,82 +26,57 @@ __global__ __launch_bounds__(256) void k_inst_count(int P, int nbe, GeomState g)
   const int lane = threadIdx.x & 63;
   const size_t vo = (size_t)v * P;
   const int r = lb * GSR_DUP_TILE + lane;
-  const uint2 tt = r < P ? g.tiles[vo + order[vo + r]] : make_uint2(0u, 0u);
-  const uint32_t tot = __builtin_amdgcn_readlane((int)wave_incl_sum_dpp(tt.x), 63);
-  const uint32_t vtot = __builtin_amdgcn_readlane((int)wave_incl_sum_dpp(tt.x > 0u ? 1u : 0u), 63);
-  const uint32_t ktot = __builtin_amdgcn_readlane((int)wave_incl_sum_dpp(tt.y), 63);
-  if (lane == 0) {
-    g.inst_counts[(size_t)v * nbe + lb] = tot;
-    g.vis_counts[(size_t)v * nbe + lb] = vtot;
-    g.kept_counts[(size_t)v * nbe + lb] = ktot;
+  uint32_t kept = 0u;
+  if (r < P) {
+    const uint32_t val = order[vo + r];
+    const uint32_t ks = g.vsent();
+    kept = g.vbits <= 26 ? val >> g.vbits : ks;
+    if (kept == ks) kept = g.tiles[vo + (val & g.vmask())].y;
   }
+  const uint32_t ktot = __builtin_amdgcn_readlane((int)wave_incl_sum_dpp(kept), 63);
+  if (lane == 0) g.kept_counts[(size_t)v * nbe + lb] = ktot;
 }
 
-// One 1024-thread workgroup per view: exclusive scans of its block counts in place, in one pass per
-// 16K blocks (16 consecutive entries per thread; rectangle and kept counts packed as rect << 32 | kept
-// into one 64-bit scan: a view's kept total is < 2^32).  Rectangle tiles K_v -> counters[v], visible
-// Gaussians -> counters[V + v], kept instances -> counters[2V + v].
+// One 1024-thread workgroup per view: exclusive scan of its kept counts in place, in one pass per 16K
+// blocks (16 consecutive entries per thread); kept instances -> counters[2V + v].
 #define GSR_ISCAN_PER 16
 __global__ __launch_bounds__(1024) void k_inst_scan(int nbe, GeomState g) {
-  __shared__ unsigned long long s_w[16];
-  __shared__ uint32_t s_v[16];
+  __shared__ uint32_t s_w[16];
   const int v = blockIdx.x, t = threadIdx.x, w = t >> 6, lane = t & 63;
-  uint32_t* rect = g.inst_counts + (size_t)v * nbe;
   uint32_t* kept = g.kept_counts + (size_t)v * nbe;
-  const uint32_t* vis = g.vis_counts + (size_t)v * nbe;
-  unsigned long long carry = 0ull;
-  uint32_t vis_total = 0u;
+  uint32_t carry = 0u;
   for (int c0 = 0; c0 < nbe; c0 += 1024 * GSR_ISCAN_PER) {
     const int i0 = c0 + t * GSR_ISCAN_PER;
-    unsigned long long x[GSR_ISCAN_PER], run = 0ull;
-    uint32_t vs = 0u;
+    uint32_t x[GSR_ISCAN_PER], run = 0u;
 #pragma unroll
     for (int k = 0; k < GSR_ISCAN_PER; ++k) {
       const int i = i0 + k;
-      const bool in = i < nbe;
       x[k] = run;
-      run += in ? ((unsigned long long)rect[i] << 32 | kept[i]) : 0ull;
-      vs += in ? vis[i] : 0u;
+      run += i < nbe ? kept[i] : 0u;
     }
-    unsigned long long inc = run;
+    uint32_t inc = run;
 #pragma unroll
     for (int o = 1; o < 64; o <<= 1) {
-      const unsigned long long y = __shfl_up(inc, o, 64);
+      const uint32_t y = (uint32_t)__shfl_up((int)inc, o, 64);
       if (lane >= o) inc += y;
     }
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) vs += (uint32_t)__shfl_xor((int)vs, o, 64);
     if (lane == 63) s_w[w] = inc;
-    if (lane == 0) s_v[w] = vs;
     __syncthreads();
-    unsigned long long before = 0ull, tot = 0ull;
-    uint32_t vt = 0u;
+    uint32_t before = 0u, tot = 0u;
 #pragma unroll
     for (int i = 0; i < 16; ++i) {
-      const unsigned long long sw = s_w[i];
-      before += i < w ? sw : 0ull;
+      const uint32_t sw = s_w[i];
+      before += i < w ? sw : 0u;
       tot += sw;
-      vt += s_v[i];
     }
     __syncthreads();
-    const unsigned long long off = carry + before + (inc - run);
+    const uint32_t off = carry + before + (inc - run);
 #pragma unroll
-    for (int k = 0; k < GSR_ISCAN_PER; ++k) {
-      const int i = i0 + k;
-      if (i < nbe) {
-        const unsigned long long r = off + x[k];
-        rect[i] = (uint32_t)(r >> 32);
-        kept[i] = (uint32_t)r;
-      }
-    }
+    for (int k = 0; k < GSR_ISCAN_PER; ++k)
+      if (i0 + k < nbe) kept[i0 + k] = off + x[k];
     carry += tot;
-    vis_total += vt;
   }
-  if (t == 0) {
-    g.counters[v] = (uint32_t)(carry >> 32);
-    g.counters[gridDim.x + v] = vis_total;
-    g.counters[2 * gridDim.x + v] = (uint32_t)carry;
-  }
+  if (t == 0) g.counters[2 * gridDim.x + v] = carry;
 }
 
 // Gradient-row slots: goff[v][i] = sum of tiles[v][j].x over j < i (each visible Gaussian owns
@@ -110,21 +86,25 @@ __global__ __launch_bounds__(256) void k_goff_count(int P, int nbg, GeomState g)
   __shared__ uint32_t s_wave[8];
   const int v = blockIdx.x / nbg, b = blockIdx.x - v * nbg, t = threadIdx.x;
   const uint2* tl = g.tiles + (size_t)v * P;
-  uint32_t sum = 0u;
+  uint32_t sum = 0u, vis = 0u;
 #pragma unroll
   for (int k = 0; k < GSR_GOFF_TILE / 256; ++k) {
     const int i = b * GSR_GOFF_TILE + k * 256 + t;
-    sum += i < P ? tl[i].x : 0u;
+    const uint32_t x = i < P ? tl[i].x : 0u;
+    sum += x;
+    vis += x > 0u ? 1u : 0u;
   }
   sum = block_sum_u32<256>(sum, s_wave);
-  if (t == 0) g.goff_part[(size_t)v * nbg + b] = sum;
+  vis = block_sum_u32<256>(vis, s_wave);
+  if (t == 0) g.goff_part[(size_t)v * nbg + b] = sum, g.vis_part[(size_t)v * nbg + b] = vis;
 }
 
 __global__ __launch_bounds__(1024) void k_goff_scan(int nbg, GeomState g) {
   __shared__ uint32_t s_w[16];
   const int v = blockIdx.x, t = threadIdx.x, w = t >> 6, lane = t & 63;
   uint32_t* row = g.goff_part + (size_t)v * nbg;
-  uint32_t carry = 0u;
+  uint32_t carry = 0u, vis = 0u;
+  for (int i = t; i < nbg; i += 1024) vis += g.vis_part[(size_t)v * nbg + i];
   for (int c0 = 0; c0 < nbg; c0 += 1024 * 4) {
     const int i0 = c0 + 4 * t;
     uint32_t x[4], run = 0u;
@@ -154,6 +134,18 @@ __global__ __launch_bounds__(1024) void k_goff_scan(int nbg, GeomState g) {
     for (int k = 0; k < 4; ++k)
       if (i0 + k < nbg) row[i0 + k] = off + x[k];
     carry += tot;
+  }
+  // rectangle tiles K_v (the reference's num_rendered) -> counters[v], visible Gaussians -> counters[V + v]
+  __syncthreads();
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) vis += (uint32_t)__shfl_xor((int)vis, o, 64);
+  if (lane == 0) s_w[w] = vis;
+  __syncthreads();
+  if (t == 0) {
+    uint32_t vt = 0u;
+    for (int i = 0; i < 16; ++i) vt += s_w[i];
+    g.counters[v] = carry;
+    g.counters[gridDim.x + v] = vt;
   }
 }
 
@@ -236,7 +228,7 @@ __global__ __launch_bounds__(64) void k_emit(int P, int nbe, int grid_x, GeomSta
   uint2 n_d = make_uint2(0u, 0u);
   auto fetch = [&](int lb) {
     const int r = lb * GSR_DUP_TILE + lane;
-    n_gi = r < P ? order[vo + r] : 0u;
+    n_gi = r < P ? (order[vo + r] & g.vmask()) : 0u;
     n_vis = r < P && dkeys[vo + r] != 0xFFFFFFFFu;
     n_koff = g.kept_counts[(size_t)v * nbe + lb];
     if (n_vis) {
@@ -365,12 +357,10 @@ __global__ __launch_bounds__(256) void k_tile_ranges(SegInfo inst, int n_tiles, 
 void launch_binning_counts(int V, int P, const GeomState& g, hipStream_t stream) {
   if (V <= 0) return;
   const int nbe = GeomState::dup_blocks(P);
-  if (P > 0) {
-    const int nbg = GeomState::goff_blocks(P);
-    hipLaunchKernelGGL(k_goff_count, dim3(V * nbg), dim3(256), 0, stream, P, nbg, g);
-    hipLaunchKernelGGL(k_goff_scan, dim3(V), dim3(1024), 0, stream, nbg, g);
-    hipLaunchKernelGGL(k_goff_write, dim3(V * nbg), dim3(256), 0, stream, P, nbg, g);
-  }
+  const int nbg = GeomState::goff_blocks(P);
+  if (P > 0) hipLaunchKernelGGL(k_goff_count, dim3(V * nbg), dim3(256), 0, stream, P, nbg, g);
+  hipLaunchKernelGGL(k_goff_scan, dim3(V), dim3(1024), 0, stream, P > 0 ? nbg : 0, g);  // K_v, visible
+  if (P > 0) hipLaunchKernelGGL(k_goff_write, dim3(V * nbg), dim3(256), 0, stream, P, nbg, g);
   if (P > 0)
     hipLaunchKernelGGL(k_inst_count, dim3(V * ((nbe + 3) / 4)), dim3(256), 0, stream, P, nbe, g);
   hipLaunchKernelGGL(k_inst_scan, dim3(V), dim3(1024), 0, stream, P > 0 ? nbe : 0, g);

@@ -165,16 +165,21 @@ struct GeomState {
                              // rows; y: of those, tiles its alpha >= 1/255 ellipse reaches (span_row):
                              // its list instances
   uint32_t* dkey[2];         // depth sort ping-pong keys (float bits of view depth; culled = ~0)
-  uint32_t* dval[2];         // depth sort ping-pong values (Gaussian index within the view)
+  uint32_t* dval[2];         // depth sort ping-pong values: Gaussian index | min(kept tiles, vsent) << vbits
+                             // (the kept count rides along so the instance counts stream; vsent = the
+                             // count did not fit: read tiles.y)
   uint32_t* sort_counts;     // [V][RADIX][sort blocks] per-block digit counts -> scanned offsets
   uint32_t* sort_totals;     // [V][RADIX] digit totals
-  uint32_t* inst_counts;     // [V][emission blocks] rectangle tiles per block -> scanned offsets
   uint32_t* kept_counts;     // [V][emission blocks] kept instances per block -> scanned offsets
-  uint32_t* vis_counts;      // [V][emission blocks] visible Gaussians per block
   uint32_t* goff;            // [V][P] first gradient-row slot of each visible Gaussian: exclusive scan
                              // of tiles.x in Gaussian order (any disjoint assignment works; this one is
                              // written with coalesced stores)
   uint32_t* goff_part;       // [V][goff blocks] per-4096-Gaussian sums of tiles.x -> scanned offsets
+  uint32_t* vis_part;        // [V][goff blocks] visible Gaussians per 4096-Gaussian block
+  int vbits;                 // bits of the Gaussian index in the depth-sort values (from P)
+  __host__ __device__ uint32_t vmask() const { return vbits >= 32 ? 0xFFFFFFFFu : (1u << vbits) - 1u; }
+  // kept-count field of a depth-sort value: all ones = did not fit (or no room: P > 2^26)
+  __host__ __device__ uint32_t vsent() const { return vbits > 26 ? 0u : (1u << (32 - vbits)) - 1u; }
   uint32_t* drange;          // depth key range of the set: [0, 64) min slots, [64, 128) max slots,
                              // [128] = min visible key, [129] = 1 if 3 depth-sort passes suffice
   // the depth-sorted (keys, Gaussians) of every view: the 4th pass's output, or the 3rd's when it was skipped
@@ -198,12 +203,13 @@ struct GeomState {
     g.dval[1] = c.take<uint32_t>(n);
     g.sort_counts = c.take<uint32_t>(nv * GSR_RADIX * sort_blocks(P));
     g.sort_totals = c.take<uint32_t>(nv * GSR_RADIX);
-    g.inst_counts = c.take<uint32_t>(nv * dup_blocks(P));
-    g.vis_counts = c.take<uint32_t>(nv * dup_blocks(P));
     g.kept_counts = c.take<uint32_t>(nv * dup_blocks(P));
     g.counters = c.take<uint32_t>(3 * nv + 64);
     g.goff = c.take<uint32_t>(n);
     g.goff_part = c.take<uint32_t>(nv * goff_blocks(P));
+    g.vis_part = c.take<uint32_t>(nv * goff_blocks(P));
+    g.vbits = 1;
+    while (g.vbits < 32 && (1ull << g.vbits) < (unsigned long long)(P > 1 ? P : 2)) ++g.vbits;
     g.drange = c.take<uint32_t>(132);
     if (bytes) *bytes = align_up(c.off, 256);
     return g;

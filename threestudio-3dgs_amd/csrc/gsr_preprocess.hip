@@ -149,6 +149,9 @@ __global__ __launch_bounds__(256) void k_preprocess(PreprocessArgs a, SetCams ca
       a.radii[vi] = radius;
       g.tiles[vi] = tiles;
       g.dkey[0][vi] = dkey;
+      // the depth sort's value: index | kept tiles (k_inst_count reads them in depth order, streaming)
+      const uint32_t ks = g.vsent();
+      g.dval[0][vi] = (uint32_t)idx | (g.vbits <= 26 ? min(tiles.y, ks) << g.vbits : 0u);
       if (dkey != 0xFFFFFFFFu) kmn = min(kmn, dkey), kmx = max(kmx, dkey);
     }
   }
