@@ -292,6 +292,7 @@ def main():
             local = 0
         torch.cuda.set_device(local)
         backend = os.environ.get("GSR_BENCH_BACKEND", "nccl")
+        comm = "RCCL" if backend == "nccl" else backend
         if backend == "nccl":
             dist.init_process_group("nccl", device_id=torch.device("cuda", local))
         else:
@@ -437,7 +438,8 @@ def main():
                         "gradient all-reduce",
             "n_gaussians": args.gaussians, "resolution": [H, W], "sh_degree": args.sh_degree,
             "global_views_per_step": args.views, "views_per_rank": per,
-            "parallelism": f"views sharded over {world} rank(s) (RCCL all-gather images, all-reduce grads)",
+            "parallelism": (f"views sharded over {world} rank(s) ({comm} all-gather of the images, in-place "
+                            "all-reduce of the Gaussian gradients)" if world > 1 else "1 rank, no collectives"),
             "mean_instances_K": round(K_mean),
             "mean_listed_instances": round(L_mean),
             "path": args.path,
