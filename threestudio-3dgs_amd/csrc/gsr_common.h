@@ -14,7 +14,9 @@
 #define GSR_SET_MAX 64
 // Sort passes: 256 threads x 16 items per block, <= 8-bit digits.
 #define GSR_SORT_THREADS 256
+#ifndef GSR_SORT_ITEMS
 #define GSR_SORT_ITEMS 16
+#endif
 #define GSR_SORT_TILE (GSR_SORT_THREADS * GSR_SORT_ITEMS)  // 4096
 #define GSR_RADIX_BITS 8
 #define GSR_RADIX (1 << GSR_RADIX_BITS)
