@@ -54,8 +54,9 @@ __device__ __forceinline__ P3 normalize_bwd(P3 x, float len, P3 g) {
   const float inv = 1.0f / den;
   P3 dx = p3(g.x * inv, g.y * inv, g.z * inv);
   if (len >= kEps && len > 0.0f) {
+    // here den == len: dden / len = dden * inv (one reciprocal per normalisation)
     const float dden = -dot3(g, x) * inv * inv;
-    const float k = dden / len;
+    const float k = dden * inv;
     dx.x += k * x.x;
     dx.y += k * x.y;
     dx.z += k * x.z;
@@ -163,8 +164,10 @@ __device__ __forceinline__ void shade_bwd_pixel(const ShadeArgs& A, const ShadeG
   const P3 c = cross3(a, b);
   const P3 n = p3(-c.x, -c.y, -c.z);
   const float len = sqrtf(dot3(n, n));
-  const float den = fmaxf(len, kEps);
-  const P3 u = p3(n.x / den, n.y / den, n.z / den);
+  // the backward's recomputed forward values use one reciprocal per normalisation (gradients are
+  // compared with a tolerance; the forward kernel keeps the reference's IEEE divides)
+  const float rden = 1.0f / fmaxf(len, kEps);
+  const P3 u = p3(n.x * rden, n.y * rden, n.z * rden);
   const float al = A.alpha[(size_t)v * HW + p];
   const bool m = al > 0.99f;
   P3 gu = p3(0.f, 0.f, 0.f);
@@ -185,11 +188,11 @@ __device__ __forceinline__ void shade_bwd_pixel(const ShadeArgs& A, const ShadeG
     const P3 s = own_normal ? u : pred_normal(A, v, HW, p);
     const P3 L = sub3(p3(A.light[3 * v], A.light[3 * v + 1], A.light[3 * v + 2]), X);
     const float llen = sqrtf(dot3(L, L));
-    const float lden = fmaxf(llen, kEps);
-    const P3 l = p3(L.x / lden, L.y / lden, L.z / lden);
+    const float rlden = 1.0f / fmaxf(llen, kEps);
+    const P3 l = p3(L.x * rlden, L.y * rlden, L.z * rlden);
     const float dt = dot3(s, l);
     const float dl = fmaxf(dt, 0.0f);
-    const float ad = al + 1e-6f;
+    const float rad = 1.0f / (al + 1e-6f);
     float ddl = 0.0f;
     float dad = 0.0f;
     float gcol[3], gbg[3];
@@ -197,7 +200,7 @@ __device__ __forceinline__ void shade_bwd_pixel(const ShadeArgs& A, const ShadeG
     for (int k = 0; k < 3; ++k) {
       const float tl = dl * A.kd[k] + A.ka[k];
       const float col = A.color[plane + k * HW];
-      const float alb = col / ad;
+      const float alb = col * rad;
       const float albc = fminf(fmaxf(alb, 0.0f), 1.0f);
       const float fg = A.mode == GSR_SHADING_DIFFUSE ? albc * tl : (A.mode == GSR_SHADING_ALBEDO ? alb : tl);
       const float bgk = bg_at(A, v, HW, p, k);
@@ -216,8 +219,8 @@ __device__ __forceinline__ void shade_bwd_pixel(const ShadeArgs& A, const ShadeG
         dtl = dfg;
       }
       ddl += dtl * A.kd[k];
-      gcol[k] = dalb / ad;
-      dad -= dalb * col / (ad * ad);
+      gcol[k] = dalb * rad;
+      dad -= dalb * alb * rad;  // col / ad^2 = alb / ad
     }
     dal += dad;
     if (own) {
