@@ -149,11 +149,22 @@ int gsr_set_num_rendered(int V, const void* geom, int P, int* num_rendered, int*
  * hold after the exact ellipse-vs-tile culling (<= K).  Diagnostic / roofline use. */
 int gsr_set_num_rendered_ex(int V, const void* geom, int P, int* num_rendered, int* num_visible, int* num_listed,
                             void* stream);
+/* Diagnostic copy (device to device, on `stream`) of the preprocess state of every (view, Gaussian):
+ * out_rec (V, P, 16) 32-bit words = (pixel x, pixel y, conic a, conic b | conic c, opacity, view depth, 0 |
+ * r, g, b, 0 | tile rect xmin | ymin << 16, xmax | ymax << 16, 0, SH clamp flags), written only for
+ * visible Gaussians; out_tiles (V, P, 2) u32 = (3-sigma rectangle tiles, 0 = culled; tiles the
+ * alpha >= 1/255 ellipse reaches).  Either may be NULL.  Parity tests compare these with the oracle's
+ * per-Gaussian preprocess values (the reference's geomBuffer has no public layout). */
+int gsr_set_gauss_state(int V, const void* geom, int P, void* out_rec, void* out_tiles, void* stream);
 int gsr_set_render(int V, int P, const int* num_rendered, int width, int height, const float* const* bgs,
                    void* geom, void* binning, void* image, float* out_color, float* out_depth,
                    float* out_alpha, void* stream);
-/* Gradient outputs are overwritten (accumulate = 0) or added to (accumulate != 0), summed over the
- * set's views; dL_dmeans2D is per view and always overwritten.  Reads forward state only. */
+/* Gradient outputs are overwritten (accumulate = 0) or continued (accumulate != 0: every per-Gaussian
+ * sum resumes from the stored value in view order), summed over the set's views; dL_dmeans2D is per view
+ * and always overwritten.  The views are processed in groups that fit work_bytes
+ * (gsr_set_backward_bytes = all in one group); any grouping gives bitwise the same gradients.  With
+ * accumulate in the scale / rotation path, dL_dcov3D is required: it carries the running dL/dcov3D
+ * that the scale and rotation gradients are recomputed from.  Reads forward state only. */
 int gsr_set_backward(int V, int P, int degree, int M, const int* num_rendered, int width, int height,
                      const float* const* bgs, const float* means3D, const float* scales, float scale_modifier,
                      const float* rotations, const float* shs, const float* cov3D_precomp,

@@ -70,14 +70,20 @@ static int imax(int a, int b) { return a > b ? a : b; }
 /* ------------------------------------------------------------------------------------------ */
 /* pieces (exported for golden-vector checks)                                                  */
 
+/* transformPoint4x3 / 4x4: m[0] p.x + m[4] p.y + m[8] p.z + m[12] evaluated as the left-to-right fma
+ * chain a contracting compiler emits (the kernels use the same chain, csrc/gsr_common.h xform_row), so
+ * the fp32 view depths — which decide the order of nearly coincident Gaussians — agree bit for bit. */
+static real xrow(real m0, real m1, real m2, real m3, const real* p) {
+  return FMAR(m2, p[2], FMAR(m1, p[1], m0 * p[0])) + m3;
+}
 static void xform4x3(const real* p, const real* m, real* o) {
-  o[0] = m[0] * p[0] + m[4] * p[1] + m[8] * p[2] + m[12];
-  o[1] = m[1] * p[0] + m[5] * p[1] + m[9] * p[2] + m[13];
-  o[2] = m[2] * p[0] + m[6] * p[1] + m[10] * p[2] + m[14];
+  o[0] = xrow(m[0], m[4], m[8], m[12], p);
+  o[1] = xrow(m[1], m[5], m[9], m[13], p);
+  o[2] = xrow(m[2], m[6], m[10], m[14], p);
 }
 static void xform4x4(const real* p, const real* m, real* o) {
   xform4x3(p, m, o);
-  o[3] = m[3] * p[0] + m[7] * p[1] + m[11] * p[2] + m[15];
+  o[3] = xrow(m[3], m[7], m[11], m[15], p);
 }
 
 /* R[c][r] exactly as the kernels build it (glm column-major of the reference) */
@@ -259,6 +265,7 @@ typedef struct {
 typedef struct {
   int radius, tiles, xmin, ymin, xmax, ymax;
   real px, py, ca, cb, cc, op, depth, rgb[3];
+  real rad3; /* 3 sqrt(max eigenvalue) before the ceil (radius adjudication), -1 if culled earlier */
   uint32_t clamp;
 } gstate;
 
@@ -291,6 +298,7 @@ static void get_cov3(const ctx_t* c, int i, real* cov) {
 
 static void preprocess(const ctx_t* c, int i, gstate* g, int* radii) {
   memset(g, 0, sizeof(*g));
+  g->rad3 = -1;
   radii[i] = 0;
   real p[3];
   load_vec(c->means + 3 * i, p, 3);
@@ -312,6 +320,8 @@ static void preprocess(const ctx_t* c, int i, gstate* g, int* radii) {
   const real l2 = mid - SQRTR(rmax(RL(0.1), mid * mid - det));
   const real rad = CEILR(RL(3) * SQRTR(rmax(l1, l2)));
   const real px = ndc2pix(pp[0], c->W), py = ndc2pix(pp[1], c->H);
+  g->rad3 = RL(3) * SQRTR(rmax(l1, l2));
+  g->px = px; g->py = py;
   const int r = (int)rad;
   const int xmin = imin(c->gx, imax(0, (int)((px - r) / TILE)));
   const int ymin = imin(c->gy, imax(0, (int)((py - r) / TILE)));
@@ -459,6 +469,32 @@ long FN(oracle_forward)(int P, int deg, int M, const float* means, const float* 
   const long K = f.K;
   free_fwd(&f);
   return K;
+}
+
+/* Per-Gaussian preprocess values for the parity tests (no blending): aux (P, 16) doubles = (pixel x,
+ * pixel y, 3 sqrt(max eigenvalue) before the ceil, rectangle tiles, conic a, b, c, opacity, view depth,
+ * r, g, b, tile rect xmin, ymin, xmax, ymax); rad3 = -1 for Gaussians culled before the radius (near
+ * plane, singular cov2D); fields after px, py stay 0 for culled Gaussians.  With the fp64 build, a GPU radius that differs
+ * from the fp32 oracle's is a legitimate fp32 rounding flip only when rad3 lies within a few ulp of an
+ * integer; the rectangle tile count of any radius follows from (px, py) with the getRect formula. */
+void FN(oracle_gauss_aux)(int P, int deg, int M, const float* means, const float* scales, float mod,
+                          const float* rots, const float* opac, const float* shs, const float* colors,
+                          const float* cov3p, const float* view, const float* proj, const float* campos,
+                          int W, int H, float tanx, float tany, double* aux) {
+  ctx_t c;
+  const float bg0[3] = {0, 0, 0};
+  setup(&c, P, deg, M, means, scales, mod, rots, opac, shs, colors, cov3p, view, proj, campos, W, H, tanx, tany, bg0);
+  int* radii = (int*)calloc((size_t)(P > 0 ? P : 1), sizeof(int));
+  for (int i = 0; i < P; ++i) {
+    gstate g;
+    preprocess(&c, i, &g, radii);
+    double* o = aux + 16 * (size_t)i;
+    o[0] = (double)g.px; o[1] = (double)g.py; o[2] = (double)g.rad3; o[3] = (double)g.tiles;
+    o[4] = (double)g.ca; o[5] = (double)g.cb; o[6] = (double)g.cc; o[7] = (double)g.op; o[8] = (double)g.depth;
+    o[9] = (double)g.rgb[0]; o[10] = (double)g.rgb[1]; o[11] = (double)g.rgb[2];
+    o[12] = g.xmin; o[13] = g.ymin; o[14] = g.xmax; o[15] = g.ymax;
+  }
+  free(radii);
 }
 
 /* Backward (re-runs the forward).  Gradient outputs (REAL): dmeans2D (P,3), dcolors (P,3),

@@ -99,6 +99,22 @@ def backward(scene: dict, cam, bg, dL_dcolor, dL_ddepth=None, dL_dalpha=None, pr
     return res
 
 
+def gauss_aux(scene: dict, cam, prec: str = "f64", mod: float = 1.0):
+    """Per-Gaussian preprocess values (oracle_gauss_aux): dict(px, py, rad3 = 3 sqrt(max eigenvalue) before
+    the ceil (-1 when culled before it), tiles = rectangle tiles of the oracle's radius, conic (P, 3),
+    opacity, depth, rgb (P, 3), rect (P, 4) = tile xmin, ymin, xmax, ymax)."""
+    P, M, k, (W, H, tanx, tany) = _args(scene, cam, np.zeros(3, np.float32))
+    aux = np.zeros((max(P, 1), 16), np.float64)
+    fn = getattr(lib(), f"oracle_gauss_aux_{prec}")
+    fn.restype = None
+    fn(ctypes.c_int(P), ctypes.c_int(int(scene.get("sh_degree", 0))), ctypes.c_int(M), _p(k[0]), _p(k[1]),
+       ctypes.c_float(mod), _p(k[2]), _p(k[3]), _p(k[4]), _p(k[5]), _p(k[6]), _p(k[7]), _p(k[8]), _p(k[9]),
+       ctypes.c_int(W), ctypes.c_int(H), ctypes.c_float(tanx), ctypes.c_float(tany), _p(aux))
+    aux = aux[:P]
+    return dict(px=aux[:, 0], py=aux[:, 1], rad3=aux[:, 2], tiles=aux[:, 3].astype(np.int64), conic=aux[:, 4:7],
+                opacity=aux[:, 7], depth=aux[:, 8], rgb=aux[:, 9:12], rect=aux[:, 12:16].astype(np.int64))
+
+
 def eval_sh(deg: int, sh: np.ndarray, pos: np.ndarray, campos: np.ndarray, prec: str = "f64") -> np.ndarray:
     """eval_sh of the reference (without +0.5/clamp) at normalize(pos - campos).  sh (n, M, 3)."""
     sh = np.ascontiguousarray(sh, np.float64)

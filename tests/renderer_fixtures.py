@@ -1,0 +1,180 @@
+"""Stand-ins for the reference's renderer objects, for the batch-renderer tests (test infrastructure).
+
+``make_renderer(mode, scene, device)`` builds an object with what the reference's renderers use —
+``geometry`` (getters of geometry/gaussian_base.py:371-411 / geometry/sugar.py:547-556 as leaves),
+``background`` (a per-ray function standing in for the background network), ``material`` (the point
+light material's fields, material/gaussian_material.py:17-41), ``background_tensor``, ``cfg`` and
+``training`` — whose per-view ``forward`` restates the reference's DiffGaussian.forward for that mode:
+
+    plain         renderer/diff_gaussian_rasterizer.py:45-145
+    background    renderer/diff_gaussian_rasterizer_background.py:44-145
+    shading       renderer/diff_gaussian_rasterizer_shading.py:79-231 (Depth2Normal + material: the
+                  tests/torch_reference.shading_epilogue restatement)
+    sugar_normal  renderer/diff_sugar_rasterizer_normal.py:80-223
+
+The per-view rasterizer call goes through ``RASTERIZE`` (GaussianRasterizer on the GPU); the CPU tests
+swap it for the torch formulation (tests/torch_reference.render) together with the batch renderer's
+``_rasterize_views`` so the batching / sharding logic runs without a GPU.
+"""
+from __future__ import annotations
+
+import math
+from types import SimpleNamespace
+
+import torch
+
+import torch_reference as tr
+from diff_gaussian_rasterization import GaussianRasterizationSettings
+from diff_gaussian_rasterization.batch_renderer import GaussianBatchRenderer, material_params
+
+
+def gpu_rasterize(settings, **kw):
+    from diff_gaussian_rasterization import GaussianRasterizer
+
+    return GaussianRasterizer(raster_settings=settings)(**kw)
+
+
+def torch_rasterize(settings, means3D, means2D, opacities, shs=None, colors_precomp=None, scales=None,
+                    rotations=None, cov3D_precomp=None):
+    """GaussianRasterizer's call restated with the dense torch formulation (CPU / any device)."""
+    s = settings
+    dt = means3D.dtype
+    return tr.render(means3D, means2D, opacities, s.viewmatrix.reshape(-1).to(dt), s.projmatrix.reshape(-1).to(dt),
+                     s.campos.to(dt), s.tanfovx, s.tanfovy, s.image_width, s.image_height, s.bg.to(dt), sh=shs,
+                     deg=s.sh_degree, colors=colors_precomp, scales=scales, rotations=rotations, cov3D=cov3D_precomp,
+                     mod=s.scale_modifier)
+
+
+RASTERIZE = gpu_rasterize
+
+
+def torch_rasterize_views(settings_list, means3D, means2D_list, opacities, shs=None, colors_precomp=None,
+                          scales=None, rotations=None, cov3D_precomp=None, background=None):
+    """batched.rasterize_views restated as a loop over torch_rasterize (for the CPU tests)."""
+    outs = [torch_rasterize(s, means3D, m2, opacities, shs=shs, colors_precomp=colors_precomp, scales=scales,
+                            rotations=rotations, cov3D_precomp=cov3D_precomp)
+            for s, m2 in zip(settings_list, means2D_list)]
+    color, radii, depth, alpha = (torch.stack([o[i] for o in outs]) for i in range(4))
+    if background is not None:
+        color = (color + (1 - alpha) * background.permute(0, 3, 1, 2)).clamp(0, 1)
+    return color, radii, depth, alpha
+
+
+class FakeGeometry:
+    def __init__(self, scene, device, dtype=torch.float32):
+        leaf = lambda x: torch.tensor(x, device=device, dtype=dtype, requires_grad=True)  # noqa: E731
+        self.params = {k: leaf(scene[k]) for k in ("means3D", "shs", "opacities", "scales", "rotations")}
+        if "normals" in scene:
+            self.params["normals"] = leaf(scene["normals"])
+        self.active_sh_degree = int(scene.get("sh_degree", 0))
+        self.cfg = SimpleNamespace(pred_normal=False)
+
+    get_xyz = property(lambda self: self.params["means3D"])
+    get_features = property(lambda self: self.params["shs"])
+    get_opacity = property(lambda self: self.params["opacities"])
+    get_scaling = property(lambda self: self.params["scales"])
+    get_rotation = property(lambda self: self.params["rotations"])
+    get_gs_normals = property(lambda self: self.params["normals"])
+
+
+def _background_net(dirs):
+    """Per-ray background colours (stands in for the background MLP: (n, H, W, 3) -> (n, H, W, 3))."""
+    return torch.sigmoid(2.0 * dirs)
+
+
+class FakeRenderer(GaussianBatchRenderer):
+    def __init__(self, mode, scene, device, dtype=torch.float32):
+        self.batch_render_mode = mode
+        self.geometry = FakeGeometry(scene, device, dtype)
+        self.background_tensor = torch.tensor([1.0, 1.0, 1.0], device=device, dtype=dtype)
+        self.background = lambda dirs: _background_net(dirs)
+        self.material = SimpleNamespace(cfg=SimpleNamespace(soft_shading=False, diffuse_prob=0.75,
+                                                            textureless_prob=0.5),
+                                        ambient_light_color=torch.tensor([0.1, 0.1, 0.1]),
+                                        diffuse_light_color=torch.tensor([0.9, 0.9, 0.9]), ambient_only=False)
+        self.cfg = SimpleNamespace(invert_bg_prob=0.5, debug=False)
+        self.training = False
+        self.mode = mode
+
+    # the reference's per-view DiffGaussian.forward of each mode
+    def forward(self, cam, bg_color, scaling_modifier=1.0, override_color=None, **kwargs):
+        pc = self.geometry
+        if self.mode in ("background", "shading"):
+            bg_color = bg_color * 0
+        else:
+            invert = True  # eval: renderer/diff_gaussian_rasterizer.py:59-64
+            bg_color = 1.0 - bg_color if invert else bg_color
+        sp = torch.zeros_like(pc.get_xyz, requires_grad=True) + 0
+        sp.retain_grad()
+        settings = GaussianRasterizationSettings(
+            image_height=int(cam.image_height), image_width=int(cam.image_width),
+            tanfovx=math.tan(cam.FoVx * 0.5), tanfovy=math.tan(cam.FoVy * 0.5), bg=bg_color,
+            scale_modifier=scaling_modifier, viewmatrix=cam.world_view_transform,
+            projmatrix=cam.full_proj_transform, sh_degree=pc.active_sh_degree, campos=cam.camera_center,
+            prefiltered=False, debug=False)
+        shs = pc.get_features if override_color is None else None
+        kw = dict(means3D=pc.get_xyz, means2D=sp, shs=shs, colors_precomp=override_color, opacities=pc.get_opacity,
+                  scales=pc.get_scaling, rotations=pc.get_rotation, cov3D_precomp=None)
+        img, radii, depth, alpha = RASTERIZE(settings, **kw)
+        _, H, W = img.shape
+        b = kwargs["batch_idx"]
+        pkg = {"viewspace_points": sp, "visibility_filter": radii > 0, "radii": radii}
+        if self.mode == "plain":
+            pkg["render"] = img.clamp(0, 1)
+        elif self.mode == "background":
+            comp_rgb_bg = self.background(dirs=kwargs["rays_d"][b].unsqueeze(0))
+            img = img + (1 - alpha) * comp_rgb_bg.reshape(H, W, 3).permute(2, 0, 1)
+            pkg["render"] = img.clamp(0, 1)
+        elif self.mode == "shading":
+            comp_rgb_bg = self.background(dirs=kwargs["rays_d"][b].unsqueeze(0))
+            ka, kd, smode = material_params(self.material, self.training)
+            dt = img.dtype
+            render, nmap, depth_m = tr.shading_epilogue(
+                img, depth, alpha, kwargs["rays_o"][b], kwargs["rays_d"][b], comp_rgb_bg, kwargs["light_positions"][b],
+                torch.tensor(ka, device=img.device, dtype=dt), torch.tensor(kd, device=img.device, dtype=dt), smode)
+            pkg.update(render=render, normal=nmap, pred_normal=None, mask=alpha, depth=depth_m, comp_rgb_bg=comp_rgb_bg)
+        elif self.mode == "sugar_normal":
+            nfd, nmap_dist = tr.sugar_normal_from_dist(depth, alpha, kwargs["rays_o"][b], kwargs["rays_d"][b])
+            kw2 = dict(kw, means2D=torch.zeros_like(sp), shs=None, colors_precomp=pc.get_gs_normals)
+            normal, _, _, _ = RASTERIZE(settings, **kw2)
+            normal = torch.nn.functional.normalize(normal, dim=0)
+            normal = torch.cat([-normal[:2], normal[2:]], 0)
+            nmap = normal * 0.5 * alpha + 0.5
+            mask = alpha > 0.99
+            nmap = torch.where(mask.expand_as(nmap), nmap, nmap.detach())
+            depth = torch.where(mask, depth, depth.detach())
+            pkg.update(render=img.clamp(0, 1), normal=nmap, normal_from_dist=nmap_dist, mask=alpha, depth=depth)
+        return pkg
+
+
+class PerViewRenderer(FakeRenderer):
+    """The same renderer with the reference's per-view batch loop (batch_render_mode = "per_view")."""
+
+    def __init__(self, mode, scene, device, dtype=torch.float32):
+        super().__init__(mode, scene, device, dtype)
+        self.batch_render_mode = "per_view"
+
+
+def make_batch(B, H, W, device, dtype=torch.float32, seed=0):
+    """The data module's batch dict (data/uncond.py:338-352): orbit cameras, rays, light positions."""
+    from diff_gaussian_rasterization.cameras import light_positions_dreamfusion, orbit_c2w, ray_bundle
+
+    g = torch.Generator().manual_seed(seed)
+    elev = torch.rand(B, generator=g) * 30.0
+    azim = torch.rand(B, generator=g) * 360.0
+    c2w = orbit_c2w(torch.full((B,), 2.5), elev, azim)
+    fovy = torch.full((B,), math.radians(60.0))
+    rays_o, rays_d = ray_bundle(c2w, fovy, H, W)
+    return {"c2w": c2w.to(device), "fovy": fovy.to(device), "height": H, "width": W,
+            "rays_o": rays_o.to(device, dtype), "rays_d": rays_d.to(device, dtype),
+            "light_positions": light_positions_dreamfusion(c2w, 2.0).to(device, dtype)}
+
+
+def loss_of(out, seed=1):
+    g = torch.Generator().manual_seed(seed)
+    total = 0
+    for k in ("comp_rgb", "comp_depth", "comp_mask", "comp_normal", "comp_normal_from_dist"):
+        if k in out:
+            w = torch.randn(out[k].shape, generator=g, dtype=torch.float64).to(out[k].device, out[k].dtype)
+            total = total + (out[k] * w).sum()
+    return total

@@ -1,0 +1,372 @@
+"""Parity at the BASELINE.json configurations and of the view-set path, against the oracle.
+
+- C2 at full size (100k Gaussians, 512^2, SH3) through the per-view GaussianRasterizer;
+- C3 (1M Gaussians, 1024^2, SH3, background path: bg = 0, then the composite with the background
+  network's image + clamp of renderer/diff_gaussian_rasterizer_background.py:58,116-139) through
+  rasterize_views with the composite fused into the blends, two views of the bench's orbit;
+- rasterize_views compared directly with the oracle, view by view, on a 4-view set;
+- equal-depth Gaussians keep the reference's (depth, index) order (stable sorts);
+- the backward split into view groups (GSR_BWD_WORK_BYTES) and into view sets is bitwise invariant;
+- C5: the SuGaR normal renderer (renderer/diff_sugar_rasterizer_normal.py:157-213) on ~2M
+  surface-aligned Gaussians at 800^2: pass 1 with colors_precomp = get_points_rgb()
+  (system/sugar_static.py:117-121, geometry/sugar.py:650-660: SH2RGB of the DC coefficients), the
+  normal-from-distance maps, pass 2 with the face normals as colors_precomp and a zero means2D, the
+  normal map and the alpha > 0.99 gradient masks; gradients of a loss over every output.
+
+Bars as tests/gsr_testutil.py (fp64-oracle adjudication of fp32 decision flips).
+"""
+import math
+
+import numpy as np
+import pytest
+
+import oracle
+from gsr_testutil import (adjudicate, check_forward, check_grads, check_radii, gs, make_camera, oracle_cam,
+                          print_report, run_oracle)
+
+pytestmark = pytest.mark.gpu
+
+GRAD_KEYS = ["means3D", "opacity", "sh", "scales", "rotations"]
+TORCH_NAMES = dict(means3D="means3D", scales="scales", rotations="rotations", opacities="opacity", shs="sh",
+                   colors_precomp="colors")
+
+
+@pytest.fixture(autouse=True)
+def _parity_report():
+    yield
+    print_report()
+
+
+def _settings(cam, bg, deg, mod=1.0):
+    import torch
+
+    from diff_gaussian_rasterization import GaussianRasterizationSettings
+
+    dev = "cuda"
+    return GaussianRasterizationSettings(cam["H"], cam["W"], cam["tanx"], cam["tany"],
+                                         torch.tensor(bg, device=dev, dtype=torch.float32), mod,
+                                         torch.tensor(cam["view"], device=dev), torch.tensor(cam["proj"], device=dev),
+                                         deg, torch.tensor(cam["campos"], device=dev), False, False)
+
+
+def _gpu_views(scene, cams, bgs, ups=None, background=None):
+    """rasterize_views over `cams`; returns per-view numpy outputs, K, means2D grads and summed grads."""
+    import torch
+
+    from diff_gaussian_rasterization import _C
+    from diff_gaussian_rasterization.batched import rasterize_views
+
+    dev = "cuda"
+    keys = [k for k in ("means3D", "scales", "rotations", "opacities", "shs", "colors_precomp") if scene.get(k) is not None]
+    t = {k: torch.tensor(scene[k], device=dev, requires_grad=True) for k in keys}
+    P = scene["means3D"].shape[0]
+    V = len(cams)
+    m2s = [torch.zeros((P, 3), device=dev, requires_grad=True) for _ in cams]
+    bg_t = None if background is None else torch.tensor(background, device=dev, requires_grad=True)
+    settings = [_settings(c, b, int(scene.get("sh_degree", 0))) for c, b in zip(cams, bgs)]
+    c, r, d, a = rasterize_views(settings, t["means3D"], m2s, t["opacities"], shs=t.get("shs"),
+                                 colors_precomp=t.get("colors_precomp"), scales=t["scales"],
+                                 rotations=t["rotations"], background=bg_t)
+    Ks = [k for k, _, _ in list(_C.RECENT_FORWARDS)[-V:]]
+    out = dict(color=c.detach().cpu().numpy(), depth=d.detach().cpu().numpy(), alpha=a.detach().cpu().numpy(),
+               radii=r.cpu().numpy(), K=Ks)
+    if ups is not None:
+        gc = torch.stack([torch.tensor(u[0], device=dev) for u in ups])
+        gd = torch.stack([torch.tensor(u[1], device=dev) for u in ups])
+        ga = torch.stack([torch.tensor(u[2], device=dev) for u in ups])
+        ((c * gc).sum() + (d * gd).sum() + (a * ga).sum()).backward()
+        for k, v in t.items():
+            out["g_" + TORCH_NAMES[k]] = v.grad.cpu().numpy()
+        out["g_means2D"] = [m.grad.cpu().numpy() for m in m2s]
+        if bg_t is not None:
+            out["g_background"] = bg_t.grad.cpu().numpy()
+    return out
+
+
+def _view(out, v):
+    return dict(color=out["color"][v], depth=out["depth"][v], alpha=out["alpha"][v], radii=out["radii"][v])
+
+
+def _sum_grads(refs, prec, keys):
+    return {k: sum(np.asarray(r[prec][k], np.float64) for r in refs) for k in keys}
+
+
+def _composite(color, alpha, bg_hwc):
+    """renderer/diff_gaussian_rasterizer_background.py:129-132,139 in the arrays' precision, torch's op
+    order: color + (1 - alpha) * bg, then clamp(0, 1).  Returns (render, pre-clamp value)."""
+    one = color.dtype.type(1)
+    pre = color + (one - alpha) * bg_hwc.transpose(2, 0, 1).astype(color.dtype)
+    return np.clip(pre, 0, 1), pre
+
+
+def _composite_upstream(g_render, g_alpha, pre, bg_hwc):
+    """Gradients of the composite + clamp: dL/dcolor = g [0 <= pre <= 1], dL/dalpha += -sum_ch dL/dcolor bg,
+    dL/dbg = dL/dcolor (1 - alpha) (torch's clamp passes the gradient on the closed interval)."""
+    m = (pre >= 0) & (pre <= 1)
+    gcol = np.where(m, g_render.astype(pre.dtype), 0)
+    ga = g_alpha.astype(pre.dtype) - (gcol * bg_hwc.transpose(2, 0, 1).astype(pre.dtype)).sum(0, keepdims=True)
+    return gcol, ga
+
+
+# ------------------------------------------------------------------------------------------------
+
+@pytest.mark.slow
+def test_c2_full_100k_512_sh3():
+    """C2 (BASELINE.json configs[1]): 100k Gaussians, 512^2, SH degree 3, fwd + bwd, white background."""
+    from gsr_testutil import gpu_render
+
+    scene = gs.make_scene(100_000, sh_degree=3, seed=0)
+    cam = make_camera(512, 512)
+    g = gs.upstream_grads(512, 512, seed=5)
+    gpu = gpu_render(scene, cam, [1.0, 1.0, 1.0], grads=g)
+    ref = run_oracle(scene, cam, [1.0, 1.0, 1.0], grads=g)
+    check_forward(gpu, ref, "C2", K_gpu=gpu["K"])
+    check_grads(gpu, ref, ["means3D", "means2D", "opacity", "sh", "scales", "rotations"], "C2")
+
+
+@pytest.mark.slow
+def test_c3_views_fused_background_composite():
+    """C3 (configs[2]): 1M Gaussians, 1024^2, SH3, the background path with the composite fused into the
+    blends, two views of the bench's 64-view orbit, forward + backward through rasterize_views."""
+    scene = gs.make_scene(1_000_000, sh_degree=3, seed=0)
+    cams = [make_camera(1024, 1024, elevation=0.0, azimuth=0.0), make_camera(1024, 1024, elevation=20.0, azimuth=202.5)]
+    rng = np.random.default_rng(11)
+    bg_img = rng.random((len(cams), 1024, 1024, 3)).astype(np.float32)
+    ups = [gs.upstream_grads(1024, 1024, seed=40 + v) for v in range(len(cams))]
+    zero = [0.0, 0.0, 0.0]
+    gpu = _gpu_views(scene, cams, [zero] * len(cams), ups, background=bg_img)
+    refs = []
+    for v, cam in enumerate(cams):
+        ref = run_oracle(scene, cam, zero)
+        g_r, g_d, g_a = ups[v]
+        b = {}
+        for prec, dt in (("f32", np.float32), ("f64", np.float64)):
+            f = ref[prec]
+            render, pre = _composite(f["color"].astype(dt), f["alpha"].astype(dt), bg_img[v].astype(dt))
+            f["color"] = render
+            gcol, ga = _composite_upstream(g_r, g_a, pre, bg_img[v])
+            b[prec] = oracle.backward(scene, oracle_cam(cam), np.zeros(3, np.float32), gcol, g_d, ga,
+                                      prec=prec)
+            b["bg_" + prec] = (gcol * (dt(1) - f["alpha"].astype(dt))).transpose(1, 2, 0)
+        check_forward(_view(gpu, v), ref, f"C3 view {v}", K_gpu=gpu["K"][v])
+        adjudicate(gpu["g_means2D"][v], b["f32"]["means2D"], b["f64"]["means2D"],
+                   1e-4 * np.maximum(1.0, np.abs(b["f64"]["means2D"])), f"C3 view {v}", "grad means2D")
+        adjudicate(gpu["g_background"][v].reshape(-1, 3), b["bg_f32"].reshape(-1, 3), b["bg_f64"].reshape(-1, 3),
+                   1e-4 * np.maximum(1.0, np.abs(b["bg_f64"].reshape(-1, 3))), f"C3 view {v}", "grad background")
+        refs.append(b)
+    tot = dict(b32=_sum_grads(refs, "f32", GRAD_KEYS), b64=_sum_grads(refs, "f64", GRAD_KEYS))
+    check_grads(gpu, tot, GRAD_KEYS, "C3 summed")
+
+
+def test_view_set_vs_oracle():
+    """rasterize_views (one launch per stage for the set) vs the oracle per view: images, radii, K,
+    per-view means2D gradients, and the parameter gradients summed over the views."""
+    scene = gs.make_scene(30_000, sh_degree=3, seed=17)
+    cams = [make_camera(320, 256, elevation=10.0 * i, azimuth=90.0 * i + 15.0) for i in range(4)]
+    bgs = [[1.0, 1.0, 1.0], [0.0, 0.0, 0.0], [0.2, 0.5, 0.9], [0.7, 0.1, 0.3]]
+    ups = [gs.upstream_grads(256, 320, seed=60 + v) for v in range(4)]
+    gpu = _gpu_views(scene, cams, bgs, ups)
+    refs = []
+    for v, cam in enumerate(cams):
+        ref = run_oracle(scene, cam, bgs[v], grads=ups[v])
+        check_forward(_view(gpu, v), ref, f"set view {v}", K_gpu=gpu["K"][v])
+        adjudicate(gpu["g_means2D"][v], ref["b32"]["means2D"], ref["b64"]["means2D"],
+                   1e-4 * np.maximum(1.0, np.abs(ref["b64"]["means2D"])), f"set view {v}", "grad means2D")
+        refs.append(ref)
+    tot = dict(b32=_sum_grads(refs, "b32", GRAD_KEYS), b64=_sum_grads(refs, "b64", GRAD_KEYS))
+    check_grads(gpu, tot, GRAD_KEYS, "set summed")
+
+
+@pytest.mark.parametrize("layout", ["duplicates", "plane"])
+def test_equal_depth_tie_order(layout):
+    """Gaussians at exactly equal view depth blend in index order (the reference's stable radix sort of
+    (tile | depth) keys over index-ordered instances).  duplicates: 3 copies of 300 means with different
+    colours / opacities / footprints at indices i, i + 300, i + 600; plane: a camera looking straight
+    along -x (elevation 0, azimuth 0: an exact axis-aligned view matrix) at Gaussians on three x = const
+    planes (view depth depends on x only)."""
+    from gsr_testutil import gpu_render
+
+    rng = np.random.default_rng(3)
+    if layout == "duplicates":
+        base = gs.make_scene(300, sh_degree=0, seed=23)
+        scene = {k: np.concatenate([base[k]] * 3, 0) for k in ("means3D", "scales", "rotations", "opacities")}
+        scene["scales"] = scene["scales"] * rng.uniform(0.6, 1.6, size=(900, 1)).astype(np.float32)
+        scene["opacities"] = rng.uniform(0.3, 0.95, size=(900, 1)).astype(np.float32)
+        cam = make_camera(160, 144, azimuth=35.0)
+    else:
+        n = 900
+        yz = rng.uniform(-0.5, 0.5, size=(n, 2)).astype(np.float32)
+        x = np.float32(0.25) * rng.integers(0, 3, size=(n, 1)).astype(np.float32)
+        scene = dict(means3D=np.concatenate([x, yz], 1), scales=np.full((n, 3), 0.04, np.float32),
+                     rotations=np.tile(np.array([[1, 0, 0, 0]], np.float32), (n, 1)),
+                     opacities=rng.uniform(0.3, 0.95, size=(n, 1)).astype(np.float32))
+        cam = make_camera(160, 144, elevation=0.0, azimuth=0.0)  # exact axis-aligned view: depth = f(x)
+        v = cam["view"].reshape(-1)
+        depth = v[2] * scene["means3D"][:, 0] + v[6] * scene["means3D"][:, 1] + v[10] * scene["means3D"][:, 2] + v[14]
+        assert len(np.unique(depth)) < n // 10, "plane layout should produce equal depths"
+    P = scene["means3D"].shape[0]
+    scene["colors_precomp"] = rng.random((P, 3)).astype(np.float32)
+    scene["sh_degree"] = 0
+    g = gs.upstream_grads(cam["H"], cam["W"], seed=9)
+    gpu = gpu_render(scene, cam, [0.1, 0.1, 0.1], grads=g)
+    ref = run_oracle(scene, cam, [0.1, 0.1, 0.1], grads=g)
+    check_forward(gpu, ref, f"ties {layout}", K_gpu=gpu["K"])
+    # a swapped pair of equal-depth Gaussians changes the colour by O(0.1): far beyond any flip allowance
+    assert np.abs(gpu["color"] - ref["f32"]["color"]).max() < 1e-3
+    check_grads(gpu, ref, ["means3D", "means2D", "opacity", "colors", "scales", "rotations"], f"ties {layout}")
+
+
+def _batched_grads(scene, cams, ups, monkeypatch=None, budget=None, set_max=None):
+    import torch
+
+    from diff_gaussian_rasterization import batched
+
+    if monkeypatch is not None:
+        if budget is not None:
+            monkeypatch.setattr(batched, "WORK_BUDGET", budget)
+        if set_max is not None:
+            monkeypatch.setattr(batched, "SET_MAX", set_max)
+    out = _gpu_views(scene, cams, [[0.3, 0.3, 0.3]] * len(cams), ups)
+    torch.cuda.synchronize()
+    return out
+
+
+def test_backward_view_groups_bitwise(monkeypatch):
+    """gsr_set_backward walks the views in groups that fit the work buffer (GSR_BWD_WORK_BYTES);
+    the per-Gaussian sums continue across groups in view order, so one view per group gives bitwise
+    the gradients of one group for all views (include/gsr.h gsr_set_backward)."""
+    from diff_gaussian_rasterization import _C
+
+    scene = gs.make_scene(20_000, sh_degree=3, seed=29)
+    cams = [make_camera(192, 160, elevation=5.0 * i, azimuth=60.0 * i) for i in range(6)]
+    ups = [gs.upstream_grads(160, 192, seed=80 + v) for v in range(6)]
+    one = _batched_grads(scene, cams, ups)
+    lib = _C.load_library()
+    import ctypes
+
+    Ks = (ctypes.c_int * 6)(*one["K"])
+    need = int(lib.gsr_set_backward_bytes(6, 20_000, Ks))
+    largest = max(int(lib.gsr_backward_bytes(20_000, k)) for k in one["K"])
+    assert largest * 3 <= need, "the split must produce at least 3 groups"
+    split = _batched_grads(scene, cams, ups, monkeypatch, budget=1)  # work = one view's bytes: 6 groups
+    for k in ("g_means3D", "g_opacity", "g_sh", "g_scales", "g_rotations"):
+        assert np.array_equal(one[k], split[k]), k
+    for v in range(6):
+        assert np.array_equal(one["g_means2D"][v], split["g_means2D"][v])
+
+
+def test_view_sets_bitwise(monkeypatch):
+    """20 views as one set vs four sets of 5 (later sets continue the sums: include/gsr.h accumulate with
+    the running dL/dcov3D): identical images and bitwise identical gradients."""
+    scene = gs.make_scene(12_000, sh_degree=2, seed=31)
+    cams = [make_camera(128, 112, elevation=(i % 3) * 12.0, azimuth=18.0 * i) for i in range(20)]
+    ups = [gs.upstream_grads(112, 128, seed=120 + v) for v in range(20)]
+    one = _batched_grads(scene, cams, ups)
+    sets = _batched_grads(scene, cams, ups, monkeypatch, set_max=5)
+    for k in ("color", "depth", "alpha", "radii"):
+        assert np.array_equal(one[k], sets[k]), k
+    for k in ("g_means3D", "g_opacity", "g_sh", "g_scales", "g_rotations"):
+        assert np.array_equal(one[k], sets[k]), k
+
+
+# ------------------------------------------------------------------------------------------------
+# C5: the SuGaR normal renderer
+
+def _sugar_epilogue(torch, color, depth, alpha, normal, rays_o, rays_d, depth_normal):
+    """renderer/diff_sugar_rasterizer_normal.py:169-213 after the two rasterizer calls, one view (C,H,W).
+    depth_normal(depth, alpha) -> (normal_from_dist, normal_map_from_dist) (both gradient masked)."""
+    F = torch.nn.functional
+    nfd, nmap_dist = depth_normal(depth, alpha)
+    n = F.normalize(normal, dim=0)
+    n = torch.cat([-n[:2], n[2:]], 0)
+    nmap = n * 0.5 * alpha + 0.5
+    mask = alpha > 0.99
+    nmap = torch.where(mask.expand_as(nmap), nmap, nmap.detach())
+    depth_m = torch.where(mask, depth, depth.detach())
+    return dict(render=color.clamp(0, 1), normal=nmap, normal_from_dist=nmap_dist, mask=alpha, depth=depth_m,
+                raw_normal_from_dist=nfd)
+
+
+SUGAR_OUT = ("render", "normal", "normal_from_dist", "mask", "depth")
+
+
+@pytest.mark.slow
+def test_c5_sugar_normal_renderer():
+    import torch
+
+    import torch_reference as tr
+    from diff_gaussian_rasterization.batched import rasterize_views
+    from diff_gaussian_rasterization.cameras import orbit_c2w, ray_bundle
+    from diff_gaussian_rasterization.shading import depth_normal_views
+
+    S = 800
+    scene = gs.make_sugar_scene(7, sh_degree=0, seed=0)
+    P = scene["means3D"].shape[0]
+    assert P > 1_900_000
+    colors = (scene["shs"][:, 0, :] * np.float32(gs.C0) + np.float32(0.5)).astype(np.float32)  # SH2RGB(dc)
+    normals = scene["normals"]
+    cam = make_camera(S, S, elevation=15.0, azimuth=40.0)
+    rays_o, rays_d = ray_bundle(orbit_c2w(2.5, 15.0, 40.0)[None], math.radians(60.0), S, S)
+    rays_o, rays_d = rays_o[0].float(), rays_d[0].float()
+    rng = np.random.default_rng(77)
+    ups = {k: rng.standard_normal((1 if k in ("mask", "depth") else 3, S, S)).astype(np.float32) for k in SUGAR_OUT}
+
+    def loss_of(out, tt):
+        return sum((out[k] * tt(ups[k])).sum() for k in SUGAR_OUT)
+
+    # ---- GPU: the two rasterize_views passes + the fused normal-from-depth epilogue ----
+    dev = "cuda"
+    leaf = lambda x: torch.tensor(x, device=dev, requires_grad=True)  # noqa: E731
+    t = dict(means3D=leaf(scene["means3D"]), scales=leaf(scene["scales"]), rotations=leaf(scene["rotations"]),
+             opacities=leaf(scene["opacities"]), colors=leaf(colors), normals=leaf(normals))
+    s = _settings(cam, [0.0, 0.0, 0.0], 0)
+    m2 = torch.zeros((P, 3), device=dev, requires_grad=True)
+    c, r, d, a = rasterize_views([s], t["means3D"], [m2], t["opacities"], colors_precomp=t["colors"],
+                                 scales=t["scales"], rotations=t["rotations"])
+    nrm, _, _, _ = rasterize_views([s], t["means3D"], [torch.zeros((P, 3), device=dev)], t["opacities"],
+                                   colors_precomp=t["normals"], scales=t["scales"], rotations=t["rotations"])
+    ro, rd = rays_o.to(dev), rays_d.to(dev)
+    out = _sugar_epilogue(torch, c[0], d[0], a[0], nrm[0], ro, rd, lambda dd, aa: depth_normal_views(dd, aa, ro, rd))
+    loss_of(out, lambda x: torch.tensor(x, device=dev)).backward()
+    gpu_out = {k: out[k].detach().cpu().numpy() for k in SUGAR_OUT}
+    gpu_grads = dict(g_means3D=t["means3D"].grad.cpu().numpy(), g_scales=t["scales"].grad.cpu().numpy(),
+                     g_rotations=t["rotations"].grad.cpu().numpy(), g_opacity=t["opacities"].grad.cpu().numpy(),
+                     g_colors=t["colors"].grad.cpu().numpy(), g_normals=t["normals"].grad.cpu().numpy(),
+                     g_means2D=m2.grad.cpu().numpy())
+    gpu_pass1 = dict(color=c[0].detach().cpu().numpy(), depth=d[0].detach().cpu().numpy(),
+                     alpha=a[0].detach().cpu().numpy(), radii=r[0].cpu().numpy())
+    del t, c, d, a, nrm, out
+    torch.cuda.empty_cache()
+
+    # ---- oracle: both passes in fp32 and fp64, the torch epilogue on CPU in the same precision ----
+    sc1 = dict(scene, colors_precomp=colors)
+    sc1.pop("shs")
+    sc2 = dict(sc1, colors_precomp=normals)
+    ref1 = run_oracle(sc1, cam, [0.0, 0.0, 0.0])
+    ref2 = run_oracle(sc2, cam, [0.0, 0.0, 0.0])
+    check_forward(gpu_pass1, ref1, "C5 pass 1")
+    epi, grads = {}, {}
+    for prec, dt in (("f32", torch.float32), ("f64", torch.float64)):
+        f1, f2 = ref1[prec], ref2[prec]
+        lc, ld, la, ln = (torch.tensor(x, dtype=dt, requires_grad=True)
+                          for x in (f1["color"], f1["depth"], f1["alpha"], f2["color"]))
+        o = _sugar_epilogue(torch, lc, ld, la, ln, rays_o.to(dt), rays_d.to(dt),
+                            lambda dd, aa: tr.sugar_normal_from_dist(dd, aa, rays_o.to(dt), rays_d.to(dt)))
+        loss_of(o, lambda x: torch.tensor(x, dtype=dt)).backward()
+        epi[prec] = {k: o[k].detach().numpy() for k in SUGAR_OUT}
+        as32 = lambda x: x.grad.numpy().astype(np.float32)  # noqa: E731  (the C ABI takes fp32 gradients)
+        b1 = oracle.backward(sc1, oracle_cam(cam), np.zeros(3, np.float32), as32(lc), as32(ld), as32(la), prec=prec)
+        b2 = oracle.backward(sc2, oracle_cam(cam), np.zeros(3, np.float32), as32(ln), None, None, prec=prec)
+        grads[prec] = {k: np.asarray(b1[k], np.float64) + np.asarray(b2[k], np.float64)
+                       for k in ("means3D", "scales", "rotations", "opacity")}
+        grads[prec]["colors"] = b1["colors"]
+        grads[prec]["normals"] = b2["colors"]
+        grads[prec]["means2D"] = b1["means2D"]
+    for k in SUGAR_OUT:
+        a64 = epi["f64"][k]
+        rows = lambda x: np.asarray(x).reshape(x.shape[0], -1).T  # noqa: E731
+        adjudicate(rows(gpu_out[k]), rows(epi["f32"][k]), rows(a64), 1e-5 + 1e-5 * np.abs(rows(a64)), "C5", k,
+                   cap=0.05 * max(1.0, float(np.abs(a64).max())))
+    check_grads(gpu_grads, dict(b32=grads["f32"], b64=grads["f64"]),
+                ["means3D", "means2D", "opacity", "colors", "normals", "scales", "rotations"], "C5")
+    check_radii(gpu_pass1["radii"], ref1, "C5 pass 1")

@@ -190,10 +190,13 @@ size_t gsr_set_image_bytes(int V, int width, int height) {
   ImageState::carve(nullptr, V, width, height, &b);
   return b;
 }
+// the running dL/dcov3D (P x 6) kept at the end of the work buffer across view groups
+static size_t carry_bytes(int P) { return align_up(sizeof(float) * 6 * (size_t)(P > 0 ? P : 1), 256); }
+
 size_t gsr_set_backward_bytes(int V, int P, const int* K) {
   long long total = 0;
   for (int v = 0; v < V; ++v) total += K[v];
-  return BackwardState::bytes_for(total, V, P);
+  return BackwardState::bytes_for(total, V, P) + carry_bytes(P);
 }
 
 int gsr_set_preprocess(int V, int P, int degree, int M, const float* means3D, const float* scales,
@@ -377,6 +380,18 @@ int gsr_set_num_rendered_ex(int V, const void* geom, int P, int* num_rendered, i
   return GSR_OK;
 }
 
+int gsr_set_gauss_state(int V, const void* geom, int P, void* out_rec, void* out_tiles, void* stream) {
+  if (check_set(V, P) != GSR_OK) return GSR_EINVAL;
+  if (geom == nullptr) return fail(GSR_EINVAL, "%s", "null pointer argument");
+  if (P == 0) return GSR_OK;
+  GeomState g = GeomState::carve((void*)geom, V, P, nullptr);
+  hipStream_t s = (hipStream_t)stream;
+  const size_t n = (size_t)V * (size_t)P;
+  if (out_rec) GSR_HIP_CHECK(hipMemcpyAsync(out_rec, g.rec, n * sizeof(GaussRec), hipMemcpyDeviceToDevice, s));
+  if (out_tiles) GSR_HIP_CHECK(hipMemcpyAsync(out_tiles, g.tiles, n * sizeof(uint2), hipMemcpyDeviceToDevice, s));
+  return last_launch();
+}
+
 int gsr_set_num_rendered(int V, const void* geom, int P, int* num_rendered, int* num_visible, void* stream) {
   return gsr_set_num_rendered_ex(V, geom, P, num_rendered, num_visible, nullptr, stream);
 }
@@ -488,14 +503,20 @@ static int set_backward(int V, int P, int degree, int M, const int* K, int width
   GaussBackwardArgs a = shared_args(P, degree, M, means3D, scales, scale_modifier, rotations, shs, cov3D_precomp,
                                      dL_dcolors, dL_dopacity, dL_dmeans3D, dL_dcov3D, dL_dsh, dL_dscales,
                                      dL_drotations);
+  if (accumulate != 0 && cov3D_precomp == nullptr && dL_dcov3D == nullptr)
+    return fail(GSR_EINVAL, "%s", "accumulate needs dL_dcov3D: it carries the running dL/dcov3D between calls");
+  if (work_bytes < carry_bytes(P)) return fail(GSR_EINVAL, "%s", "backward work buffer too small");
+  // the running dL/dcov3D: the caller's output when given, else the end of the work buffer
+  const size_t avail = work_bytes - carry_bytes(P);
+  float* carry = dL_dcov3D ? dL_dcov3D : (float*)((char*)work + avail);
   bool first = accumulate == 0;
   // groups of consecutive views whose gradient rows and records fit the work buffer
   for (int g0 = 0; g0 < V;) {
     int g1 = g0;
     long long rows = 0;
-    while (g1 < V && (g1 == g0 || BackwardState::bytes_for(rows + K[g1], g1 + 1 - g0, P) <= work_bytes))
+    while (g1 < V && (g1 == g0 || BackwardState::bytes_for(rows + K[g1], g1 + 1 - g0, P) <= avail))
       rows += K[g1++];
-    if (BackwardState::bytes_for(rows, g1 - g0, P) > work_bytes)
+    if (BackwardState::bytes_for(rows, g1 - g0, P) > avail)
       return fail(GSR_EINVAL, "%s", "backward work buffer smaller than one view's gradient rows");
     BackwardState bw = BackwardState::carve(work, rows);
     RenderSet rs;
@@ -534,6 +555,7 @@ static int set_backward(int V, int P, int degree, int M, const int* K, int width
     ab.rec = g.rec;
     ab.radii = radii;
     ab.vrec = bw.vrec;
+    ab.dcov_carry = carry;
     for (int v = g0; v < g1; ++v) {
       if (bgs[v] == nullptr) return fail(GSR_EINVAL, "%s", "null background");
       rs.inst_start[v - g0] = inst.start[v];

@@ -255,7 +255,6 @@ __device__ __forceinline__ void scale_rot_backward(const float3 scale, const flo
           4.f * z * dR[1][1] + 2.f * y * dR[1][2] + 2.f * x * dR[2][0] + 2.f * y * dR[2][1];
 }
 
-__device__ __forceinline__ void put(float* p, float v, bool acc) { *p = acc ? *p + v : v; }
 
 // LDS row stride (floats) of one Gaussian's 3M SH values: 16-byte multiple plus 16 bytes of padding so
 // per-thread 16-byte LDS accesses at this stride are bank-conflict free.
@@ -393,6 +392,21 @@ __global__ __launch_bounds__(256) void k_gauss_accum(GaussBackwardArgs a, AccumA
     float dsh[48];
 #pragma unroll
     for (int k = 0; k < 48; ++k) dsh[k] = 0.f;
+    if (acc) {
+      // continue the earlier groups' sums in place (same summation order as one group)
+      dmean = make_float3(a.dL_dmeans3D[3 * idx], a.dL_dmeans3D[3 * idx + 1], a.dL_dmeans3D[3 * idx + 2]);
+      dop = a.dL_dopacity[idx];
+      if (a.dL_dcolors) dcr = a.dL_dcolors[3 * idx], dcg = a.dL_dcolors[3 * idx + 1], dcb = a.dL_dcolors[3 * idx + 2];
+      if (b.dcov_carry)
+#pragma unroll
+        for (int k = 0; k < 6; ++k) dcov[k] = b.dcov_carry[6 * idx + k];
+      if (has_sh) {
+        const float* prev = a.dL_dsh + (size_t)idx * F;
+#pragma unroll
+        for (int k = 0; k < 48; ++k)
+          if (k < F) dsh[k] = prev[k];
+      }
+    }
     const float* sh_row = has_sh ? s_sh + t * S : nullptr;
     // the views' records (written for every (view, Gaussian), zeros when culled) stream through three
     // register buffers: while one view's SH backward runs, the next two views' loads are in flight
@@ -461,25 +475,30 @@ __global__ __launch_bounds__(256) void k_gauss_accum(GaussBackwardArgs a, AccumA
     }
     if (vl < b.V) process(fa, ra, vl);
     if (vl + 1 < b.V) process(fb, rb, vl + 1);
-    put(&a.dL_dmeans3D[3 * idx], dmean.x, acc);
-    put(&a.dL_dmeans3D[3 * idx + 1], dmean.y, acc);
-    put(&a.dL_dmeans3D[3 * idx + 2], dmean.z, acc);
-    put(&a.dL_dopacity[idx], dop, acc);
+    // (the sums already include the earlier groups: plain stores)
+    a.dL_dmeans3D[3 * idx] = dmean.x;
+    a.dL_dmeans3D[3 * idx + 1] = dmean.y;
+    a.dL_dmeans3D[3 * idx + 2] = dmean.z;
+    a.dL_dopacity[idx] = dop;
     if (a.dL_dcolors) {
-      put(&a.dL_dcolors[3 * idx], dcr, acc);
-      put(&a.dL_dcolors[3 * idx + 1], dcg, acc);
-      put(&a.dL_dcolors[3 * idx + 2], dcb, acc);
+      a.dL_dcolors[3 * idx] = dcr;
+      a.dL_dcolors[3 * idx + 1] = dcg;
+      a.dL_dcolors[3 * idx + 2] = dcb;
     }
-    if (a.dL_dcov3D)
-      for (int k = 0; k < 6; ++k) put(&a.dL_dcov3D[6 * idx + k], dcov[k], acc);
+    if (b.dcov_carry)
+      for (int k = 0; k < 6; ++k) b.dcov_carry[6 * idx + k] = dcov[k];
+    if (a.dL_dcov3D && a.dL_dcov3D != b.dcov_carry)
+      for (int k = 0; k < 6; ++k) a.dL_dcov3D[6 * idx + k] = dcov[k];
     if (!a.cov3D_precomp && a.dL_dscales) {
+      // from the running dL/dcov3D total (linear, but recomputed rather than summed per group so the
+      // result does not depend on the grouping)
       const float3 scale = make_float3(a.scales[3 * idx], a.scales[3 * idx + 1], a.scales[3 * idx + 2]);
       const float4 rot = make_float4(a.rotations[4 * idx], a.rotations[4 * idx + 1], a.rotations[4 * idx + 2],
                                      a.rotations[4 * idx + 3]);
       float ds[3], dq[4];
       scale_rot_backward(scale, rot, a.scale_modifier, dcov, ds, dq);
-      for (int k = 0; k < 3; ++k) put(&a.dL_dscales[3 * idx + k], ds[k], acc);
-      for (int k = 0; k < 4; ++k) put(&a.dL_drotations[4 * idx + k], dq[k], acc);
+      for (int k = 0; k < 3; ++k) a.dL_dscales[3 * idx + k] = ds[k];
+      for (int k = 0; k < 4; ++k) a.dL_drotations[4 * idx + k] = dq[k];
     }
     if (has_sh) {
       // this thread's SH row is no longer read: reuse it for dL/dSH
@@ -498,7 +517,7 @@ __global__ __launch_bounds__(256) void k_gauss_accum(GaussBackwardArgs a, AccumA
     for (int e = t; e < cnt; e += 256) {
       const int te = (int)(((float)e + 0.5f) * invF);
       const float x = s_sh[te * S + (e - te * F)];
-      dst[e] = acc ? dst[e] + x : x;
+      dst[e] = x;
     }
   }
 }

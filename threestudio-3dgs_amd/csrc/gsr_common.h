@@ -297,16 +297,20 @@ struct BackwardState {
 // Device math shared by the forward and backward kernels.  The operation order mirrors the
 // published reference algorithm so fp32 results agree with the CPU restatement in oracle/.
 
+// Point transforms with an explicit operation order (left-to-right fma chains, as a contracting
+// compiler evaluates the reference's m[0] * p.x + m[4] * p.y + m[8] * p.z + m[12]); the oracle
+// (oracle/gsr_oracle.c xform4x3 / xform4x4) uses the same chain, so view depths — and with them the
+// depth order of nearly coincident Gaussians — agree bit for bit.
+__device__ __forceinline__ float xform_row(float m0, float m1, float m2, float m3, const float3 p) {
+  return fmaf(m2, p.z, fmaf(m1, p.y, m0 * p.x)) + m3;
+}
 __device__ __forceinline__ float3 xform_point4x3(const float3 p, const float* m) {
-  return make_float3(m[0] * p.x + m[4] * p.y + m[8] * p.z + m[12],
-                     m[1] * p.x + m[5] * p.y + m[9] * p.z + m[13],
-                     m[2] * p.x + m[6] * p.y + m[10] * p.z + m[14]);
+  return make_float3(xform_row(m[0], m[4], m[8], m[12], p), xform_row(m[1], m[5], m[9], m[13], p),
+                     xform_row(m[2], m[6], m[10], m[14], p));
 }
 __device__ __forceinline__ float4 xform_point4x4(const float3 p, const float* m) {
-  return make_float4(m[0] * p.x + m[4] * p.y + m[8] * p.z + m[12],
-                     m[1] * p.x + m[5] * p.y + m[9] * p.z + m[13],
-                     m[2] * p.x + m[6] * p.y + m[10] * p.z + m[14],
-                     m[3] * p.x + m[7] * p.y + m[11] * p.z + m[15]);
+  return make_float4(xform_row(m[0], m[4], m[8], m[12], p), xform_row(m[1], m[5], m[9], m[13], p),
+                     xform_row(m[2], m[6], m[10], m[14], p), xform_row(m[3], m[7], m[11], m[15], p));
 }
 __device__ __forceinline__ float3 xform_vec4x3_T(const float3 p, const float* m) {
   return make_float3(m[0] * p.x + m[1] * p.y + m[2] * p.z,

@@ -84,6 +84,11 @@ struct AccumArgs {
   const GaussRec* rec;      // the set's (V, P) records (SH clamp flags in d.w)
   const int* radii;         // the set's (V, P)
   const float* vrec;
+  // running dL/dcov3D over the groups / sets already summed (P x 6; the dL_dcov3D output itself when the
+  // caller wants it): with accumulate, every sum continues from the stored value in view order, so a
+  // backward split into view groups is bitwise equal to one group, and the scale / rotation gradients
+  // are recomputed from the running total instead of being added per group
+  float* dcov_carry;
   const float* campos[GSR_SET_MAX];
 };
 // Background composite epilogue — gsr_epilogue.hip.

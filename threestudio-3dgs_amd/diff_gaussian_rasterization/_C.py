@@ -15,6 +15,7 @@ current HIP stream.  There is no CPU fallback: a missing library or a non-GPU te
 """
 from __future__ import annotations
 
+import collections
 import ctypes
 import os
 
@@ -67,6 +68,7 @@ SIGNATURES = {
     ),
     "gsr_set_num_rendered": (_i, [_i, _vp, _i, ctypes.POINTER(_i), ctypes.POINTER(_i), _vp]),
     "gsr_set_num_rendered_ex": (_i, [_i, _vp, _i, ctypes.POINTER(_i), ctypes.POINTER(_i), ctypes.POINTER(_i), _vp]),
+    "gsr_set_gauss_state": (_i, [_i, _vp, _i, _vp, _vp, _vp]),
     "gsr_set_render": (_i, [_i, _i, ctypes.POINTER(_i), _i, _i, ctypes.POINTER(_vp)] + [_vp] * 7),
     "gsr_set_backward": (
         _i,
@@ -86,10 +88,13 @@ SIGNATURES = {
 }
 
 PHASES = ("preprocess", "depth_sort", "binning", "render_fwd", "render_bwd", "gauss_bwd")
-# (num_rendered, H, W) of recent forward calls, for instrumentation (bench.py roofline numbers)
-RECENT_FORWARDS: list = []
+# (num_rendered, H, W) of the most recent forward calls, for instrumentation (bench.py roofline numbers)
+RECENT_FORWARDS: collections.deque = collections.deque(maxlen=4096)
+# tests set KEEP_GEOM to keep the last per-view forward's geometry buffer in LAST_GEOM (gauss_state)
+KEEP_GEOM = False
+LAST_GEOM = None
 # instances the tile lists held (after the exact tile culling) for recent batched forwards
-RECENT_LISTED: list = []
+RECENT_LISTED: collections.deque = collections.deque(maxlen=4096)
 
 
 class GSRError(RuntimeError):
@@ -208,8 +213,10 @@ def rasterize_gaussians(bg, means3D, colors, opacity, scales, rotations, scale_m
     nvis = ctypes.c_int(0)
     _check(lib.gsr_num_rendered(_ptr(geom), P, ctypes.byref(K), ctypes.byref(nvis), stream))
     num_rendered = int(K.value)
-    if len(RECENT_FORWARDS) < 4096:
-        RECENT_FORWARDS.append((num_rendered, H, W))
+    RECENT_FORWARDS.append((num_rendered, H, W))
+    if KEEP_GEOM:
+        global LAST_GEOM
+        LAST_GEOM = geom
     binning = torch.empty(int(lib.gsr_binning_bytes(num_rendered, W, H)), **u8)
     image = torch.empty(int(lib.gsr_image_bytes(W, H)), **u8)
     _check(lib.gsr_forward_render(P, num_rendered, W, H, _ptr(bg), _ptr(geom), _ptr(binning), _ptr(image),
@@ -278,6 +285,17 @@ def mark_visible(means3D, viewmatrix, projmatrix):
         _check(lib.gsr_mark_visible(P, _ptr(_f32(means3D, "means3D", device)), _ptr(_f32(viewmatrix, "viewmatrix", device)),
                                     _ptr(_f32(projmatrix, "projmatrix", device)), _ptr(present), _stream(device)))
     return present.bool()
+
+
+def gauss_state(geom, V: int, P: int):
+    """Preprocess state of a view set's geometry buffer (include/gsr.h gsr_set_gauss_state): returns
+    (rec (V, P, 16) float32 — integer words viewed as float bits —, tiles (V, P, 2) int32) on the device."""
+    lib = load_library()
+    dev = geom.device
+    rec = torch.zeros((V, P, 16), dtype=torch.float32, device=dev)
+    tiles = torch.zeros((V, P, 2), dtype=torch.int32, device=dev)
+    _check(lib.gsr_set_gauss_state(V, _ptr(geom), P, _ptr(rec), _ptr(tiles), _stream(dev)))
+    return rec, tiles
 
 
 def profile_enable(on: bool = True):

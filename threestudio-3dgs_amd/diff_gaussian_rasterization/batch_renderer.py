@@ -1,0 +1,327 @@
+"""Drop-in ``GaussianBatchRenderer`` on the view-set path.
+
+The reference renders a batch with a serial Python loop (renderer/gaussian_batch_renderer.py:9-76): per
+view it builds the camera (``get_cam_info_gaussian`` + ``Camera``, :22-49), calls the renderer's
+``forward`` (one rasterizer call, one host sync and ~30 launches per view), then stacks the per-view
+outputs into the batch dict (:78-121).  This mixin keeps that contract — same input batch dict
+(``c2w``, ``fovy``, ``height``, ``width``, ``rays_o``, ``rays_d``, ``light_positions``,
+``override_color``), same output keys (``comp_rgb``, ``comp_depth``, ``comp_mask``, ``comp_normal``,
+``comp_normal_from_dist``, ``comp_pred_normal``, ``comp_rgb_bg`` as (B, H, W, C), and the per-view
+lists ``viewspace_points``, ``visibility_filter``, ``radii``) — but renders the whole batch with one
+``rasterize_views`` call (every kernel stage is one launch per set of up to 64 views) followed by the
+renderer's epilogue fused on the GPU:
+
+    "plain"         renderer/diff_gaussian_rasterizer.py:45-145          bg (randomly inverted), clamp
+    "background"    renderer/diff_gaussian_rasterizer_background.py:44-145  bg = 0, background network
+                                                                         composite + clamp fused into the blends
+    "shading"       renderer/diff_gaussian_rasterizer_shading.py:79-231  Depth2Normal + point-light
+                                                                         material + composite (gsr_shade_*)
+    "sugar_normal"  renderer/diff_sugar_rasterizer_normal.py:80-223      two passes (colours, face normals)
+                                                                         + normal-from-distance (gsr_shade_*)
+
+The mode comes from the renderer's ``batch_render_mode`` attribute or, when unset, from the module the
+renderer class is defined in (the reference's file names above).  Any other renderer (advanced, normal,
+st, temporal, sugar shading) keeps the reference's per-view loop, still on the HIP rasterizer.
+
+With ``torch.distributed`` initialised, every rank renders its contiguous slice of the batch
+(view_shard.shard_range) and the image outputs are all-gathered (RCCL over xGMI); the per-view lists
+hold the rank's own views and ``view_range`` says which.  Ranks with no view (batch < world) still take
+part in every gather with empty slices, so the collectives always match.
+
+Randomness follows the reference per view (background inversion); the material's random ambient ratio
+and shading mode (material/gaussian_material.py:52-96) are drawn once per batch — the fused shading
+epilogue takes one set of light colours per launch (the material's own comment: "adopt the same type of
+augmentation for the whole batch").
+"""
+from __future__ import annotations
+
+import math
+import random
+from typing import NamedTuple
+
+import numpy as np
+import torch
+
+from .cameras import get_cam_info_gaussian
+from .view_shard import _world, all_gather_views, shard_range
+
+MODES = ("plain", "background", "shading", "sugar_normal")
+_MODULE_MODES = {
+    "diff_gaussian_rasterizer": "plain",
+    "diff_gaussian_rasterizer_background": "background",
+    "diff_gaussian_rasterizer_shading": "shading",
+    "diff_sugar_rasterizer_normal": "sugar_normal",
+}
+# batch dict image keys of the reference (renderer/gaussian_batch_renderer.py:78-121) -> channels
+_OUT_KEYS = (("comp_rgb", 3), ("comp_normal", 3), ("comp_normal_from_dist", 3), ("comp_pred_normal", 3),
+             ("comp_depth", 1), ("comp_mask", 1))
+
+
+class Camera(NamedTuple):
+    """geometry/gaussian_base.py:175-184 (A15), for the per-view fallback loop."""
+    FoVx: torch.Tensor
+    FoVy: torch.Tensor
+    camera_center: torch.Tensor
+    image_width: int
+    image_height: int
+    world_view_transform: torch.Tensor
+    full_proj_transform: torch.Tensor
+    timestamp: torch.Tensor = None
+    frame_idx: torch.Tensor = None
+
+
+def batch_mode(renderer):
+    """The fused path for `renderer` (one of MODES), or None for the reference's per-view loop."""
+    mode = getattr(renderer, "batch_render_mode", None)
+    if mode is not None:
+        if mode not in MODES and mode != "per_view":
+            raise ValueError(f"unknown batch_render_mode {mode!r}")
+        return None if mode == "per_view" else mode
+    return _MODULE_MODES.get(type(renderer).__module__.rsplit(".", 1)[-1])
+
+
+def _rasterize_views(*args, **kwargs):
+    from .batched import rasterize_views
+
+    return rasterize_views(*args, **kwargs)
+
+
+def _shade_views(*args, **kwargs):
+    from .shading import shade_views
+
+    return shade_views(*args, **kwargs)
+
+
+def _depth_normal_views(*args, **kwargs):
+    from .shading import depth_normal_views
+
+    return depth_normal_views(*args, **kwargs)
+
+
+def material_params(material, training: bool):
+    """The point-light material's light colours and shading mode (material/gaussian_material.py:52-96
+    with ambient_ratio = shading = None, as the shading renderer calls it), drawn once for the batch."""
+    cfg = material.cfg
+    if training and cfg.soft_shading:
+        kd = random.random()
+        ka, kd = (1.0 - kd,) * 3, (kd,) * 3
+    else:
+        ka = tuple(float(x) for x in material.ambient_light_color.reshape(-1))
+        kd = tuple(float(x) for x in material.diffuse_light_color.reshape(-1))
+    if training:
+        if material.ambient_only or random.random() > cfg.diffuse_prob:
+            mode = "albedo"
+        elif random.random() < cfg.textureless_prob:
+            mode = "textureless"
+        else:
+            mode = "diffuse"
+    else:
+        mode = "albedo" if material.ambient_only else "diffuse"
+    return ka, kd, mode
+
+
+def _settings(pc, cams, bgs, H, W, scaling_modifier):
+    from . import GaussianRasterizationSettings
+
+    w2c, proj, campos, fovs = cams
+    return [GaussianRasterizationSettings(image_height=H, image_width=W, tanfovx=math.tan(f * 0.5),
+                                          tanfovy=math.tan(f * 0.5), bg=bgs[v], scale_modifier=scaling_modifier,
+                                          viewmatrix=w2c[v], projmatrix=proj[v], sh_degree=pc.active_sh_degree,
+                                          campos=campos[v], prefiltered=False, debug=False)
+            for v, f in enumerate(fovs)]
+
+
+def _inverted_bgs(renderer, n):
+    """Per-view background colour of the plain / SuGaR renderers: inverted unless a draw keeps it
+    (renderer/diff_gaussian_rasterizer.py:59-64, renderer/diff_sugar_rasterizer_normal.py:94-99)."""
+    bg = renderer.background_tensor
+    out = []
+    for _ in range(n):
+        invert = (np.random.rand() > renderer.cfg.invert_bg_prob) if renderer.training else True
+        out.append(1.0 - bg if invert else bg)
+    return out
+
+
+def _placeholders(P, n, dev, dtype):
+    """One screen-space placeholder per view (renderer/diff_gaussian_rasterizer.py:67-77): leaves whose
+    .grad is the view's viewspace gradient, carved from one zeroed buffer (one fill for the batch)."""
+    buf = torch.zeros((n, P, 3), device=dev, dtype=dtype)
+    return [buf[v].requires_grad_(True) for v in range(n)]
+
+
+def render_views_local(renderer, batch: dict, mode: str, lo: int, hi: int) -> dict:
+    """Render views [lo, hi) of the batch with the fused path of `mode`.  Returns per-view stacked images
+    (n, C, H, W) under the batch dict's keys, plus the per-view lists."""
+    pc = renderer.geometry
+    H, W = int(batch["height"]), int(batch["width"])
+    means3D = pc.get_xyz
+    dev, P = means3D.device, int(means3D.shape[0])
+    n = hi - lo
+    out = {"viewspace_points": [], "visibility_filter": [], "radii": []}
+    if n <= 0:
+        return out
+    fovy = torch.as_tensor(batch["fovy"])[lo:hi].reshape(-1)
+    w2c, proj, campos = get_cam_info_gaussian(batch["c2w"][lo:hi], fovy, fovy, znear=0.1, zfar=100)
+    cams = (w2c.to(dev), proj.to(dev), campos.to(dev), [float(f) for f in fovy])
+    scaling_modifier = float(batch.get("scaling_modifier", 1.0))
+    override = batch.get("override_color")
+    shs = pc.get_features if override is None else None
+    m2 = _placeholders(P, n, dev, means3D.dtype)
+    common = dict(opacities=pc.get_opacity, scales=pc.get_scaling, rotations=pc.get_rotation)
+    with torch.autocast(device_type=dev.type, enabled=False):
+        if mode == "plain":
+            settings = _settings(pc, cams, _inverted_bgs(renderer, n), H, W, scaling_modifier)
+            color, radii, _, _ = _rasterize_views(settings, means3D, m2, shs=shs, colors_precomp=override, **common)
+            out["comp_rgb"] = color.clamp(0, 1)
+        elif mode == "background":
+            zero = [renderer.background_tensor * 0] * n
+            settings = _settings(pc, cams, zero, H, W, scaling_modifier)
+            bg_img = renderer.background(dirs=batch["rays_d"][lo:hi])
+            render, radii, _, _ = _rasterize_views(settings, means3D, m2, shs=shs, colors_precomp=override,
+                                                   background=bg_img.reshape(n, H, W, 3), **common)
+            out["comp_rgb"] = render
+        elif mode == "shading":
+            zero = [renderer.background_tensor * 0] * n
+            settings = _settings(pc, cams, zero, H, W, scaling_modifier)
+            color, radii, depth, alpha = _rasterize_views(settings, means3D, m2, shs=shs, colors_precomp=override,
+                                                          **common)
+            rays_o, rays_d = batch["rays_o"][lo:hi], batch["rays_d"][lo:hi]
+            if batch.get("override_bg_color") is not None:
+                bg_img = batch["override_bg_color"].reshape(1, 1, 1, 3).expand(n, H, W, 3)
+            else:
+                bg_img = renderer.background(dirs=rays_d)
+            pred = None
+            if getattr(pc.cfg, "pred_normal", False):
+                zeros = [torch.zeros_like(m) for m in m2]
+                pred, _, _, _ = _rasterize_views(settings, means3D, zeros, shs=pc.get_normal.unsqueeze(1),
+                                                 colors_precomp=None, **common)
+                out["comp_pred_normal"] = pred
+            ka, kd, smode = material_params(renderer.material, renderer.training)
+            render, nmap, depth_m = _shade_views(color, depth, alpha, rays_o, rays_d, bg_img.reshape(n, H, W, 3),
+                                                 batch["light_positions"][lo:hi], ka, kd, smode, pred_normal=pred)
+            out.update(comp_rgb=render, comp_normal=nmap, comp_depth=depth_m, comp_mask=alpha,
+                       comp_rgb_bg=bg_img.reshape(n, H, W, 3))
+        elif mode == "sugar_normal":
+            settings = _settings(pc, cams, _inverted_bgs(renderer, n), H, W, scaling_modifier)
+            color, radii, depth, alpha = _rasterize_views(settings, means3D, m2, shs=shs, colors_precomp=override,
+                                                          **common)
+            if batch.get("compute_normal_from_dist", True):
+                _, nmap_dist = _depth_normal_views(depth, alpha, batch["rays_o"][lo:hi], batch["rays_d"][lo:hi])
+                out["comp_normal_from_dist"] = nmap_dist
+            zeros = [torch.zeros_like(m) for m in m2]
+            normal, _, _, _ = _rasterize_views(settings, means3D, zeros, shs=None, colors_precomp=pc.get_gs_normals,
+                                               **common)
+            normal = torch.nn.functional.normalize(normal, dim=1)
+            normal = torch.cat([-normal[:, :2], normal[:, 2:]], 1)  # p3d -> threestudio axes (:193)
+            nmap = normal * 0.5 * alpha + 0.5
+            mask = alpha > 0.99
+            out.update(comp_rgb=color.clamp(0, 1), comp_normal=torch.where(mask.expand_as(nmap), nmap, nmap.detach()),
+                       comp_depth=torch.where(mask, depth, depth.detach()), comp_mask=alpha)
+        else:
+            raise ValueError(f"unknown mode {mode!r}")
+    out["viewspace_points"] = m2
+    out["radii"] = [radii[v] for v in range(n)]
+    out["visibility_filter"] = [radii[v] > 0 for v in range(n)]
+    return out
+
+
+def _mode_keys(renderer, mode):
+    keys = {"plain": ["comp_rgb"], "background": ["comp_rgb"],
+            "shading": ["comp_rgb", "comp_normal", "comp_depth", "comp_mask"],
+            "sugar_normal": ["comp_rgb", "comp_normal", "comp_depth", "comp_mask"]}[mode]
+    if mode == "shading" and getattr(renderer.geometry.cfg, "pred_normal", False):
+        keys.append("comp_pred_normal")
+    return keys
+
+
+def render_batch(renderer, batch: dict, mode: str, group=None, shard: bool = True) -> dict:
+    """batch_forward of the fused path: this rank's slice of views, images gathered over ranks."""
+    bs = int(batch["c2w"].shape[0])
+    world, rank = _world() if shard else (1, 0)
+    lo, hi = shard_range(bs, world, rank)
+    local = render_views_local(renderer, batch, mode, lo, hi)
+    H, W = int(batch["height"]), int(batch["width"])
+    dev, dtype = renderer.geometry.get_xyz.device, renderer.geometry.get_xyz.dtype
+    keys = _mode_keys(renderer, mode)
+    if mode == "sugar_normal" and batch.get("compute_normal_from_dist", True):
+        keys.append("comp_normal_from_dist")
+    outputs = {"viewspace_points": local["viewspace_points"], "visibility_filter": local["visibility_filter"],
+               "radii": local["radii"]}
+    if world > 1:
+        outputs["view_range"] = (lo, hi)
+    channels = dict(_OUT_KEYS)
+    for key in keys:
+        img = local.get(key)
+        if img is None:  # a rank without views: an empty slice of the agreed shape (a leaf, so that the
+            # rank's loss still has a graph and its backward runs; its parameter gradients stay None and
+            # view_shard.allreduce_grads contributes zeros for them)
+            img = torch.empty((0, channels[key], H, W), device=dev, dtype=dtype, requires_grad=True)
+        full = all_gather_views(img, bs, group) if world > 1 else img
+        outputs[key] = full.permute(0, 2, 3, 1)
+    if mode == "shading":
+        bgl = local.get("comp_rgb_bg")
+        if bgl is None:
+            bgl = torch.empty((0, H, W, 3), device=dev, dtype=dtype)
+        full = all_gather_views(bgl, bs, group) if world > 1 else bgl
+        # torch.cat of the views' (1, H, W, 3) backgrounds, then the reference's permute(0, 2, 3, 1)
+        # (renderer/gaussian_batch_renderer.py:116-120: a (B, W, 3, H) tensor, kept as the reference has it)
+        outputs["comp_rgb_bg"] = full.permute(0, 2, 3, 1)
+    return outputs
+
+
+def reference_batch_forward(renderer, batch: dict) -> dict:
+    """The reference's per-view loop (renderer/gaussian_batch_renderer.py:9-122), for renderers without a
+    fused path; each view still runs on the HIP rasterizer through the renderer's own forward."""
+    bs = batch["c2w"].shape[0]
+    lists = {k: [] for k in ("render", "viewspace_points", "visibility_filter", "radii", "normal",
+                             "normal_from_dist", "pred_normal", "depth", "mask", "comp_rgb_bg")}
+    for batch_idx in range(bs):
+        batch["batch_idx"] = batch_idx
+        fovy = batch["fovy"][batch_idx]
+        w2c, proj, cam_p = get_cam_info_gaussian(c2w=batch["c2w"][batch_idx], fovx=fovy, fovy=fovy, znear=0.1,
+                                                 zfar=100)
+        dev = batch["c2w"].device
+        cam = Camera(FoVx=fovy, FoVy=fovy, image_width=batch["width"], image_height=batch["height"],
+                     world_view_transform=w2c.to(dev), full_proj_transform=proj.to(dev), camera_center=cam_p.to(dev),
+                     timestamp=batch["timestamp"][batch_idx] if "timestamp" in batch else None,
+                     frame_idx=batch["frame_indices"][batch_idx] if "frame_indices" in batch else None)
+        with torch.autocast(device_type=dev.type, enabled=False):
+            pkg = renderer.forward(cam, renderer.background_tensor, **batch)
+        for k in ("render", "viewspace_points", "visibility_filter", "radii"):
+            lists[k].append(pkg[k])
+        for k in ("normal", "depth", "mask", "comp_rgb_bg"):
+            if k in pkg:
+                lists[k].append(pkg[k])
+        for k in ("normal_from_dist", "pred_normal"):
+            if pkg.get(k) is not None:
+                lists[k].append(pkg[k])
+    out = {"comp_rgb": torch.stack(lists["render"], 0).permute(0, 2, 3, 1),
+           "viewspace_points": lists["viewspace_points"], "visibility_filter": lists["visibility_filter"],
+           "radii": lists["radii"]}
+    for k, name in (("normal", "comp_normal"), ("normal_from_dist", "comp_normal_from_dist"),
+                    ("pred_normal", "comp_pred_normal"), ("depth", "comp_depth"), ("mask", "comp_mask")):
+        if lists[k]:
+            out[name] = torch.stack(lists[k], 0).permute(0, 2, 3, 1)
+    if lists["comp_rgb_bg"]:
+        out["comp_rgb_bg"] = torch.cat(lists["comp_rgb_bg"], 0).permute(0, 2, 3, 1)
+    return out
+
+
+class GaussianBatchRenderer:
+    """Mixin replacing renderer/gaussian_batch_renderer.py:GaussianBatchRenderer (same ``batch_forward``
+    contract).  Set ``batch_render_mode`` to force a mode ("per_view" = the reference loop); set
+    ``shard_views = False`` to render every view on every rank."""
+
+    batch_render_mode = None
+    shard_views = True
+    shard_group = None
+
+    def batch_forward(self, batch):
+        mode = batch_mode(self)
+        if mode is None:
+            return reference_batch_forward(self, batch)
+        return render_batch(self, batch, mode, group=self.shard_group, shard=self.shard_views)
+
+
+__all__ = ["GaussianBatchRenderer", "Camera", "MODES", "batch_mode", "material_params", "render_batch",
+           "render_views_local", "reference_batch_forward"]

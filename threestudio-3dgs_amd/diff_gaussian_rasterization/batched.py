@@ -103,10 +103,8 @@ class _RasterizeViews(torch.autograd.Function):
             L = (ctypes.c_int * vs.V)()
             _C._check(lib.gsr_set_num_rendered_ex(vs.V, p(vs.geom), P, K, None, L, stream))
             vs.K = [int(k) for k in K]
-            if len(_C.RECENT_LISTED) < 4096:
-                _C.RECENT_LISTED.extend(int(x) for x in L)
-            if len(_C.RECENT_FORWARDS) < 4096:
-                _C.RECENT_FORWARDS.extend((k, H, W) for k in vs.K)
+            _C.RECENT_LISTED.extend(int(x) for x in L)
+            _C.RECENT_FORWARDS.extend((k, H, W) for k in vs.K)
             Karr = _arr(ctypes.c_int, vs.K)
             vs.binning = torch.empty(int(lib.gsr_set_binning_bytes(vs.V, P, Karr, W, H)), dtype=torch.uint8, device=dev)
             vs.image = torch.empty(int(lib.gsr_set_image_bytes(vs.V, W, H)), dtype=torch.uint8, device=dev)
@@ -156,6 +154,11 @@ class _RasterizeViews(torch.autograd.Function):
         d_m3, d_sc, d_rot, d_op = carved["m3"], carved["sc"], carved["rot"], carved["op"]
         d_sh, d_c3, d_col = carved["sh"], carved["c3"], carved["col"]
         d_bg = torch.empty_like(cbg) if cbg is not None and ctx.needs_input_grad[8] else None
+        # more than one view set in the scale / rotation path: the running dL/dcov3D the later sets
+        # continue from (include/gsr.h gsr_set_backward, accumulate)
+        if d_c3 is None and len(ctx.sets) > 1:
+            d_c3 = torch.empty((P, 6), **fopt)
+            ctx.needs_c3_scratch = True
         if P == 0:
             if d_bg is not None:
                 d_bg.zero_()
@@ -193,6 +196,8 @@ class _RasterizeViews(torch.autograd.Function):
                         p(d_sh), p(d_sc), p(d_rot), 1 if si > 0 else 0, p(work), work.numel(), stream))
         if d_bg is not None:
             d_bg = d_bg.reshape(ctx.bg_shape)
+        if getattr(ctx, "needs_c3_scratch", False):
+            d_c3 = None
         grads = [None, d_m3, d_sh, d_col, d_op, d_sc, d_rot, d_c3, d_bg] + [d_m2[v] for v in range(V)]
         for k, need in enumerate(ctx.needs_input_grad):
             if not need:

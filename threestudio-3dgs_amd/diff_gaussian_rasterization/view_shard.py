@@ -105,15 +105,31 @@ def _contiguous_span(grads):
     return g0.as_strided((end - start,), (1,), start)
 
 
-def allreduce_grads(params, group=None, average: bool = False):
-    """Sum (or average) the .grad of `params` over ranks in one flat bucket (one RCCL all-reduce)."""
-    world, _ = _world()
-    if world == 1:
-        return
-    grads = [p.grad for p in params if p.grad is not None]
-    if not grads:
-        return
+def _span_in_order(grads):
+    """The one-buffer span of `grads` when they tile it in exactly the given order, else None."""
     span = _contiguous_span(grads)
+    if span is None:
+        return None
+    offs = [g.storage_offset() for g in grads]
+    return span if all(a < b for a, b in zip(offs, offs[1:])) else None
+
+
+def allreduce_grads(params, group=None, average: bool = False):
+    """Sum (or average) the .grad of `params` over ranks in one flat bucket (one RCCL all-reduce).
+
+    Every rank reduces the same elements in the same order — the order of `params` — so a rank whose
+    gradients are missing (a rank that rendered no view: .grad is None) takes part with zeros.  When the
+    gradients tile one buffer in that order (the batched rasterizer's carved gradients, batched.py:
+    means3D, scales, rotations, opacities, SH, ... — pass the parameters in that order) the buffer is
+    reduced in place, without a copy."""
+    world, _ = _world()
+    if world == 1 or not params:
+        return
+    for p in params:
+        if p.grad is None:
+            p.grad = torch.zeros_like(p)
+    grads = [p.grad for p in params]
+    span = _span_in_order(grads)
     if span is not None:  # the batched rasterizer's gradients: one buffer, reduced in place
         dist.all_reduce(span, group=group)
         if average:
@@ -130,7 +146,7 @@ def allreduce_grads(params, group=None, average: bool = False):
         off += n
 
 
-def reduce_densify_stats(radii, viewspace_points, visibility_filter, num_points: int, group=None):
+def reduce_densify_stats(radii, viewspace_points, visibility_filter, num_points: int, group=None, device=None):
     """Per-Gaussian densification statistics over the whole batch (all ranks).
 
     Returns (max_radii, grad_norm_sum, count) with the semantics of update_states /
@@ -138,8 +154,9 @@ def reduce_densify_stats(radii, viewspace_points, visibility_filter, num_points:
       max_radii     = max over views of radii
       grad_norm_sum = sum over views of |viewspace_points.grad[:, :2]| where visible
       count         = number of views in which the Gaussian is visible
+    A rank without views passes empty lists (and `device`); it still joins the reductions.
     """
-    dev = radii[0].device if radii else torch.device("cpu")
+    dev = device if device is not None else (radii[0].device if radii else torch.device("cpu"))
     max_r = torch.zeros(num_points, device=dev, dtype=torch.float32)
     gsum = torch.zeros(num_points, device=dev, dtype=torch.float32)
     cnt = torch.zeros(num_points, device=dev, dtype=torch.float32)
@@ -161,36 +178,77 @@ class ViewShardedBatchRenderer:
     """batch_forward() with the output contract of GaussianBatchRenderer (renderer/gaussian_batch_renderer.py:78-121),
     rendering only this rank's views.
 
-    `render_view(batch_idx, batch) -> render_pkg` renders one view (in threestudio: build the Camera from
-    batch["c2w"][batch_idx] with get_cam_info_gaussian and call DiffGaussian.forward, :22-56).
-    Image outputs are gathered to the full batch on every rank; the per-view lists
-    (viewspace_points, visibility_filter, radii) hold the local views, with "view_range" telling
-    which batch indices they are.
+    Built either from a renderer object (a DiffGaussian of the reference): its fused view-set path
+    (batch_renderer.render_batch: one rasterize_views call for the rank's views + the fused epilogue)
+    when it has one, else its per-view ``forward``; or from a callback ``render_view(batch_idx, batch) ->
+    render_pkg`` rendering one view.  Image outputs are gathered to the full batch on every rank; the
+    per-view lists (viewspace_points, visibility_filter, radii) hold the local views, with "view_range"
+    telling which batch indices they are.  Every rank issues the same gathers, also a rank that gets no
+    view (batch smaller than the world): it contributes empty slices of the shapes the other ranks report.
     """
 
-    def __init__(self, render_view: Callable[[int, dict], dict], group=None):
-        self.render_view = render_view
+    def __init__(self, render_view_or_renderer, group=None):
         self.group = group
+        if hasattr(render_view_or_renderer, "geometry"):
+            self.renderer, self.render_view = render_view_or_renderer, None
+        else:
+            self.renderer, self.render_view = None, render_view_or_renderer
 
     def batch_forward(self, batch: dict) -> dict:
+        if self.renderer is not None:
+            from .batch_renderer import batch_mode, render_batch
+
+            mode = batch_mode(self.renderer)
+            if mode is not None:
+                return render_batch(self.renderer, batch, mode, group=self.group, shard=True)
+        return self._per_view(batch)
+
+    def _render_one(self, batch_idx, batch):
+        if self.render_view is not None:
+            return self.render_view(batch_idx, batch)
+        from .batch_renderer import Camera
+        from .cameras import get_cam_info_gaussian
+
+        fovy = batch["fovy"][batch_idx]
+        w2c, proj, cam_p = get_cam_info_gaussian(batch["c2w"][batch_idx], fovy, fovy, 0.1, 100)
+        dev = batch["c2w"].device
+        cam = Camera(FoVx=fovy, FoVy=fovy, camera_center=cam_p.to(dev), image_width=batch["width"],
+                     image_height=batch["height"], world_view_transform=w2c.to(dev), full_proj_transform=proj.to(dev))
+        return self.renderer.forward(cam, self.renderer.background_tensor, **batch)
+
+    def _per_view(self, batch: dict) -> dict:
         bs = int(batch["c2w"].shape[0])
         world, rank = _world()
         start, end = shard_range(bs, world, rank)
         pkgs = []
         for batch_idx in range(start, end):
             batch["batch_idx"] = batch_idx
-            pkgs.append(self.render_view(batch_idx, batch))
+            pkgs.append(self._render_one(batch_idx, batch))
         out = {
             "viewspace_points": [p["viewspace_points"] for p in pkgs],
             "visibility_filter": [p["visibility_filter"] for p in pkgs],
             "radii": [p["radii"] for p in pkgs],
             "view_range": (start, end),
         }
+        # agree on the gathered keys and per-view shapes (a rank without views knows neither)
+        local = {}
         for key, name in _IMAGE_KEYS:
             if pkgs and key in pkgs[0] and pkgs[0][key] is not None:
-                local = torch.stack([p[key] for p in pkgs], 0)
-                out[name] = all_gather_views(local, bs, self.group).permute(0, 2, 3, 1)
+                local[name] = torch.stack([p[key] for p in pkgs], 0)
         if pkgs and "comp_rgb_bg" in pkgs[0]:
-            local = torch.cat([p["comp_rgb_bg"] for p in pkgs], 0)
-            out["comp_rgb_bg"] = all_gather_views(local, bs, self.group).permute(0, 2, 3, 1)
+            local["comp_rgb_bg_raw"] = torch.cat([p["comp_rgb_bg"] for p in pkgs], 0)
+        meta = {k: (tuple(v.shape[1:]), str(v.dtype).replace("torch.", "")) for k, v in local.items()} if pkgs else None
+        metas = [meta]
+        if world > 1:
+            metas = [None] * world
+            dist.all_gather_object(metas, meta, group=self.group)
+        agreed = next((m for m in metas if m is not None), {})
+        dev = batch["c2w"].device if not pkgs else next(iter(local.values())).device
+        for name in sorted(agreed):
+            shape, dtype = agreed[name]
+            t = local.get(name)
+            if t is None:
+                t = torch.empty((0,) + tuple(shape), device=dev, dtype=getattr(torch, dtype), requires_grad=True)
+            full = all_gather_views(t, bs, self.group).permute(0, 2, 3, 1)
+            out["comp_rgb_bg" if name == "comp_rgb_bg_raw" else name] = full
         return out
