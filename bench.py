@@ -39,6 +39,11 @@ import torch.distributed as dist  # noqa: E402
 
 METRIC = "rendered views/sec fwd+bwd @1M Gaussians, 1024², SH=3; 1/2/4/8 GPU"
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md chip table)
+# VALU issue peak: 256 CUs x 4 SIMDs x 2.4 GHz, one wave64 instruction per SIMD every 2 cycles
+# (MI355X_MICROARCH.md: "issues each VALU instruction over 2 cycles") = 157.3 TFLOP/s fp32 as FMAs
+VALU_PEAK_INSTS = 256 * 4 * 2.4e9 / 2
+FP32_PEAK_TFLOPS = 157.3
+SH_C0 = 0.28209479177387814
 
 
 def parse():
@@ -64,8 +69,13 @@ def parse():
     ap.add_argument("--path", choices=["batched", "per-view"], default="batched",
                     help="batched: rasterize_views (one autograd node per rank's views); per-view: one "
                          "GaussianRasterizer call per view, exactly as the reference renderer loop does")
-    ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "r01_traffic.json"),
-                    help="PMC summary (profiles/summarize.py) supplying roofline.traffic")
+    ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "r02_traffic.json"),
+                    help="PMC summary (profiles/summarize.py) supplying roofline.traffic and the VALU counts")
+    ap.add_argument("--pairs", default=os.path.join(ROOT, "profiles", "r02_pairs.json"),
+                    help="device-counted blend pairs (profiles/diag_pairs.py) for the VALU roofline")
+    ap.add_argument("--per-view-views", type=int, default=16,
+                    help="views of the drop-in per-view path (one GaussianRasterizer call per view, the "
+                         "reference's loop) timed after the headline, reported beside it (0 = skip)")
     return ap.parse_args()
 
 
@@ -198,7 +208,7 @@ def render_views(rep: Replica, settings, bg_img, shade=None):
 
 def render_views_sugar(rep: Replica, settings, shade):
     """C5: the SuGaR normal renderer (renderer/diff_sugar_rasterizer_normal.py:157-213) over a view set:
-    pass 1 (SH colours) -> render, depth, alpha; normal-from-depth maps (fused HIP epilogue); pass 2 with
+    pass 1 (colors_precomp = SH2RGB(dc), the SuGaR refinement's override_color) -> render, depth, alpha; normal-from-depth maps (fused HIP epilogue); pass 2 with
     the face normals as colors_precomp and a fresh zero means2D (no viewspace gradient, :179-189); then
     normalize, flip x/y, normal map and the alpha > 0.99 gradient masks in torch (:190-197)."""
     from diff_gaussian_rasterization.batched import rasterize_views
@@ -207,7 +217,10 @@ def render_views_sugar(rep: Replica, settings, shade):
     P = rep.means3D.shape[0]
     dev = rep.means3D.device
     m2 = placeholders(rep, len(settings))
-    color, radii, depth, alpha = rasterize_views(settings, rep.means3D, m2, rep.opacities, shs=rep.shs,
+    # pass 1 colours: SuGaRModel.get_points_rgb() = SH2RGB of the DC coefficients, passed as override_color
+    # (system/sugar_static.py:117-121, geometry/sugar.py:650-660)
+    colors = rep.shs[:, 0, :] * SH_C0 + 0.5
+    color, radii, depth, alpha = rasterize_views(settings, rep.means3D, m2, rep.opacities, colors_precomp=colors,
                                                  scales=rep.scales, rotations=rep.rotations)
     rays_o, rays_d, _ = shade
     _, nmap_dist = depth_normal_views(depth, alpha, rays_o, rays_d)
@@ -223,14 +236,22 @@ def render_views_sugar(rep: Replica, settings, shade):
     return color.clamp(0, 1), depth, alpha, nmap, nmap_dist
 
 
-def read_traffic(path, kernel):
-    """HBM bytes per launch of `kernel` from a committed PMC summary (FETCH_SIZE x2 gfx950 correction +
-    WRITE_SIZE, separate --pmc passes; profiles/summarize.py), or None."""
+def read_traffic(path, kernel, field="per_launch_bytes"):
+    """Per-launch value of `kernel` from a committed PMC summary (profiles/summarize.py): HBM bytes
+    (FETCH_SIZE x2 gfx950 correction + WRITE_SIZE, separate --pmc passes) or SQ_INSTS_VALU; None if absent."""
     try:
         with open(path) as f:
             t = json.load(f)
-        return float(t["per_launch_bytes"][kernel])
+        return float(t[field][kernel])
     except (OSError, KeyError, ValueError, TypeError):
+        return None
+
+
+def read_json(path):
+    try:
+        with open(path) as f:
+            return json.load(f)
+    except (OSError, ValueError):
         return None
 
 
@@ -251,33 +272,179 @@ def time_knn(points, reps=10):
             "ms": round(e0.elapsed_time(e1) / reps, 4)}
 
 
-def cpu_baseline(scene, res, n_views):
-    """The CPU restatement (oracle, fp32, single thread) on `n_views` views of the same workload."""
+def _cpu_threads():
+    """Threads for the CPU baseline: the job's CPU share (OMP_NUM_THREADS on the GPU box = 16), else the
+    CPUs this process may run on."""
+    env = os.environ.get("OMP_NUM_THREADS")
+    if env and env.isdigit() and int(env) > 0:
+        return int(env)
+    try:
+        return len(os.sched_getaffinity(0))
+    except AttributeError:
+        return os.cpu_count() or 1
+
+
+def _cpu_model():
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return platform.processor() or platform.machine()
+
+
+def cpu_baseline(c3_scene, c3_res, c3_views):
+    """The CPU restatement of the reference algorithm (oracle/gsr_oracle.c, fp32, OpenMP over tiles with
+    per-thread gradient partials) timed on this host's cores: BASELINE.md's C1 (10k Gaussians, 256^2,
+    SH0, 1 view: forward, and forward + backward) as the reported value, plus a bounded sample of the
+    benchmark workload itself (C3 views, forward + backward)."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle  # test infrastructure; timed here only as the reported CPU baseline
 
     import gsr_synthetic as gs
     from diff_gaussian_rasterization.cameras import get_cam_info_gaussian, orbit_c2w
 
-    oracle.lib()
+    threads = _cpu_threads()
+    oracle.lib().oracle_set_threads(threads)
     fovy = math.radians(60.0)
     tan = math.tan(fovy / 2)
-    g = gs.upstream_grads(res, res, seed=1)
-    bg = np.zeros(3, np.float32)
+
+    def cam(res, el, az):
+        wv, fp, cc = get_cam_info_gaussian(orbit_c2w(2.5, el, az), fovy, fovy, 0.1, 100.0)
+        return (wv.numpy().ravel(), fp.numpy().ravel(), cc.numpy(), tan, tan, res, res)
+
+    # C1: 10k Gaussians, 256^2, SH0, white background (BASELINE.md); repeated until ~3 s per mode
+    c1 = gs.make_scene(10_000, sh_degree=0, seed=0)
+    c1_cam = cam(256, 15.0, 0.0)
+    g1 = gs.upstream_grads(256, 256, seed=1)
+    bg1 = np.ones(3, np.float32)
+    oracle.forward(c1, c1_cam, bg1, "f32")  # warm (thread pool)
+
+    def rate(fn, budget=3.0):
+        n, t0 = 0, time.perf_counter()
+        while True:
+            fn()
+            n += 1
+            dt = time.perf_counter() - t0
+            if dt >= budget or n >= 2000:
+                return n / dt, n, dt
+
+    fwd, n_f, t_f = rate(lambda: oracle.forward(c1, c1_cam, bg1, "f32"))
+    # oracle.backward re-runs the forward first (as the reference's backward reads the forward's state,
+    # the restatement recomputes it): one call = forward + backward
+    fb, n_fb, t_fb = rate(lambda: oracle.backward(c1, c1_cam, bg1, *g1, prec="f32"))
+    # C3 sample: views of the benchmark workload, forward + backward
+    g3 = gs.upstream_grads(c3_res, c3_res, seed=1)
+    bg3 = np.zeros(3, np.float32)
     t0 = time.perf_counter()
-    for i in range(n_views):
-        c2w = orbit_c2w(2.5, 0.0, i * 360.0 / 16)
-        wv, fp, cc = get_cam_info_gaussian(c2w, fovy, fovy, 0.1, 100.0)
-        cam = (wv.numpy().ravel(), fp.numpy().ravel(), cc.numpy(), tan, tan, res, res)
-        oracle.forward(scene, cam, bg, "f32")
-        oracle.backward(scene, cam, bg, *g, prec="f32")
+    for i in range(c3_views):
+        oracle.backward(c3_scene, cam(c3_res, 0.0, i * 360.0 / 16), bg3, *g3, prec="f32")
+    t3 = time.perf_counter() - t0
+    oracle.lib().oracle_set_threads(1)
+    host = f"{_cpu_model()}, {os.cpu_count()} logical CPUs on the host, {threads} threads used"
+    return dict(
+        value=fb, unit="views/s", cores=threads, kind="port",
+        sample=f"C1 (10k Gaussians, 256x256, SH0, 1 view): forward + backward, oracle/gsr_oracle.c fp32 restatement "
+               f"of the reference algorithm, OpenMP over tiles, {n_fb} repetitions in {t_fb:.2f} s on {host}",
+        c1={"fwd_views_per_s": fwd, "fwd_bwd_views_per_s": fb, "fwd_reps": n_f, "fwd_bwd_reps": n_fb},
+        c3_sample={"views_per_s": c3_views / t3, "views": c3_views, "seconds": t3,
+                   "workload": f"{c3_scene['means3D'].shape[0]} Gaussians, {c3_res}x{c3_res}, "
+                               f"SH{c3_scene['sh_degree']}, forward + backward"},
+        host_logical_cpus=os.cpu_count(), cpu_model=_cpu_model())
+
+
+def time_per_view_path(rep, cams, bg_zero, bg_img, upstream, n_views):
+    """The drop-in per-view path — one GaussianRasterizer call per view, exactly the reference's loop
+    (renderer/gaussian_batch_renderer.py:21-76) with the background composite in torch — timed on
+    n_views views of the same workload (views/s; 1 GPU)."""
+    n = min(n_views, len(cams))
+
+    def run():
+        outs = [render_view(rep, cams[i], bg_zero, bg_img[i]) for i in range(n)]
+        ts = [t for o in outs for t in o[:3]]
+        torch.autograd.backward(ts, [g for u in upstream[:n] for g in u])
+        rep.zero_grad()
+        bg_img.grad = None
+
+    run()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    run()
+    torch.cuda.synchronize()
     dt = time.perf_counter() - t0
-    return dict(value=n_views / dt, unit="views/s", cores=1, kind="port",
-                sample=f"{n_views} views of the benchmark workload ({scene['means3D'].shape[0]} Gaussians, "
-                       f"{res}x{res}, SH{scene['sh_degree']}), forward + backward, oracle/gsr_oracle.c fp32, "
-                       f"1 thread on {platform.processor() or platform.machine()} "
-                       f"({os.cpu_count()} logical CPUs visible)",
-                seconds=dt)
+    return {"views_per_s": round(n / dt, 2), "views": n,
+            "path": "GaussianRasterizer per view + torch composite (the reference's unchanged renderer loop)"}
+
+
+def roofline_fields(args, phases, Ks, Ls, H, W):
+    """roofline (the dominant kernel) and roofline_fwd_blend, per launch, from the live HIP-event phase
+    timings of this run.
+
+    achieved = SURVEY.md §8d algorithmic bytes per launch / the launch's average duration, with K = the
+    instances the tile lists hold (after the exact tile culling):
+      forward blend   44 K + 28 H W + 8 tiles
+      backward blend  44 K + 32 H W   (§8d's further 2 x 40 K of atomic read-modify-write is what the
+                                       reference's atomic backward moves; this design writes one row per
+                                       instance with plain stores and never performs it — reported as
+                                       reference_rmw_bytes, not counted)
+    counter_frac = PMC HBM bytes per launch (profiles/<tag>_traffic.json) / duration / 8 TB/s;
+    valu = SQ_INSTS_VALU per launch (profiles/<tag>_traffic.json) against the VALU issue peak (one wave64
+    instruction per SIMD per 2 cycles, 157.3 TF fp32 as FMAs) and the device-counted pairs
+    (profiles/<tag>_pairs.json, diagnostic build): the blends are issue / latency bound, not HBM bound."""
+    tiles = math.ceil(W / 16) * math.ceil(H / 16)
+    pairs = read_json(args.pairs)
+    out = {}
+    n_fw = max(1, len(Ks))
+    rows = {}
+    for phase, kernel in (("render_fwd", "k_render_fwd"), ("render_bwd", "k_render_bwd")):
+        ms, n = phases[phase]
+        n = max(1, n)
+        if phase == "render_fwd":
+            alg = (44.0 * sum(Ls) + (28.0 * H * W + 8.0 * tiles) * n_fw) / n
+        else:
+            alg = (44.0 * sum(Ls) + 32.0 * H * W * n_fw) / n
+        sec = ms / n * 1e-3
+        gbs = alg / sec / 1e9 if sec > 0 else 0.0
+        traffic = read_traffic(args.traffic, kernel)
+        valu = read_traffic(args.traffic, kernel, "valu_insts_per_launch")
+        views_per_launch = n_fw / n
+        r = {"kernel": kernel, "bound": "hbm", "achieved": round(gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+             "frac": round(gbs / HBM_PEAK_GBS, 4), "traffic": traffic, "avg_launch_us": round(1e6 * sec, 2),
+             "algorithmic_bytes": round(alg), "views_per_launch": round(views_per_launch, 2)}
+        if traffic is not None and sec > 0:
+            r["counter_frac"] = round(traffic / sec / (HBM_PEAK_GBS * 1e9), 4)
+        if phase == "render_bwd":
+            r["reference_rmw_bytes"] = round(80.0 * sum(Ls) / n)
+        v = {}
+        if valu is not None and sec > 0:
+            v["insts_per_launch"] = valu
+            v["valu_frac"] = round(valu / sec / VALU_PEAK_INSTS, 4)
+        if pairs:
+            key = "fwd_pairs_evaluated_per_view" if phase == "render_fwd" else "bwd_pairs_replayed_per_view"
+            pl = pairs[key] * views_per_launch
+            v["pairs_per_launch"] = round(pl)
+            v["pairs_per_s"] = round(pl / sec) if sec > 0 else None
+            if valu is not None:
+                v["valu_insts_per_64_pairs"] = round(valu / (pl / 64.0), 2)
+            if phase == "render_bwd":
+                v["lockstep_slots_per_kept_pair"] = round(pairs["bwd_lockstep_slots_per_kept_pair"], 3)
+        if v:
+            v["peak_insts_per_s"] = VALU_PEAK_INSTS
+            v["source"] = ("SQ_INSTS_VALU: " + os.path.relpath(args.traffic, ROOT) +
+                           ("; pairs: " + os.path.relpath(args.pairs, ROOT) if pairs else ""))
+            r["valu"] = v
+        r["limiter"] = "VALU issue / LDS latency per (pixel, Gaussian) pair, not HBM (see counter_frac, valu)"
+        rows[phase] = r
+    dominant = max(phases.items(), key=lambda kv: kv[1][0])[0]
+    out["roofline"] = rows["render_bwd"] if dominant == "render_bwd" else rows["render_fwd"]
+    out["roofline_fwd_blend"] = rows["render_fwd"]
+    out["dominant_kernel"] = dominant
+    out["roofline_note"] = ("frac = SURVEY.md §8d algorithmic bytes / HIP-event duration (backward without the "
+                            "reference's 80 B/instance atomic RMW, never performed here); counter_frac = PMC HBM "
+                            "bytes / duration; valu_frac = SQ_INSTS_VALU / (duration x VALU issue peak). Both "
+                            "blends are issue/latency bound; DESIGN.md §6")
+    return out
 
 
 def main():
@@ -443,46 +610,24 @@ def main():
             "mean_instances_K": round(K_mean),
             "mean_listed_instances": round(L_mean),
             "path": args.path,
-            "epilogue": args.epilogue,
+            "epilogue": "sugar_normal (normal-from-depth, 2 passes)" if args.workload == "sugar" else args.epilogue,
         },
     }
     if phases is not None:
         nv = max(1, args.steps * per)
         kern = {k: {"ms_per_view": round(ms / nv, 4), "launches": n} for k, (ms, n) in phases.items()}
         res["kernels"] = kern
-        # algorithmic bytes per view, SURVEY.md §8d: forward tile blend B_fwd = 44 K + 28 HW + 8 tiles;
-        # backward blend 44 K + 32 HW read + 2 x 40 K (the reference's atomic read-modify-write), with K =
-        # the instances the lists hold (after the exact tile culling, <= the reference's K).  A launch
-        # covers every view of a view set, so bytes per launch = sum over the timed views / launches.
-        tiles = math.ceil(W / 16) * math.ceil(H / 16)
-        f_ms, f_n = phases["render_fwd"]
-        b_ms, b_n = phases["render_bwd"]
-        n_fw = max(1, len(Ks))
-        bytes_fwd = (44.0 * sum(Ls) + (28.0 * H * W + 8.0 * tiles) * n_fw) / max(1, f_n)
-        bytes_bwd = (124.0 * sum(Ls) + 32.0 * H * W * n_fw) / max(1, b_n)
-        fwd_gbs = bytes_fwd / (f_ms / max(1, f_n) * 1e-3) / 1e9 if f_n else 0.0
-        bwd_gbs = bytes_bwd / (b_ms / max(1, b_n) * 1e-3) / 1e9 if b_n else 0.0
-        dominant = max(phases.items(), key=lambda kv: kv[1][0])[0]
-        roof_fwd = {"kernel": "k_render_fwd", "bound": "hbm", "achieved": round(fwd_gbs, 1), "peak": HBM_PEAK_GBS,
-                    "unit": "GB/s", "frac": round(fwd_gbs / HBM_PEAK_GBS, 4),
-                    "traffic": read_traffic(args.traffic, "k_render_fwd"),
-                    "avg_launch_us": round(1000 * f_ms / max(1, f_n), 2), "algorithmic_bytes": round(bytes_fwd)}
-        roof_bwd = {"kernel": "k_render_bwd", "bound": "hbm", "achieved": round(bwd_gbs, 1), "peak": HBM_PEAK_GBS,
-                    "unit": "GB/s", "frac": round(bwd_gbs / HBM_PEAK_GBS, 4),
-                    "traffic": read_traffic(args.traffic, "k_render_bwd"),
-                    "avg_launch_us": round(1000 * b_ms / max(1, b_n), 2), "algorithmic_bytes": round(bytes_bwd)}
-        res["roofline"] = roof_bwd if dominant == "render_bwd" else roof_fwd
-        res["roofline_fwd_blend"] = roof_fwd
-        res["dominant_kernel"] = dominant
-        res["traffic_source"] = os.path.relpath(args.traffic, ROOT) + " (HBM bytes/launch, rocprofv3 --pmc " \
-                                "FETCH_SIZE x2 + WRITE_SIZE, capture of this workload: one 64-view launch)"
-        res["roofline_note"] = ("bytes are SURVEY.md §8d algorithmic bytes; both blends are fp32-VALU-bound "
-                                "(early termination: the forward reads ~1/3 of them, traffic field), see DESIGN.md §6")
+        res.update(roofline_fields(args, phases, Ks, Ls, H, W))
     if not args.no_knn:
         res["init_knn"] = time_knn(rep.means3D.detach())
+    if world == 1 and args.per_view_views > 0 and args.workload == "c3" and args.epilogue == "background" \
+            and args.path == "batched":
+        res["per_view_path"] = time_per_view_path(rep, mine, bg_zero, bg_img, upstream, args.per_view_views)
     if world == 1 and not args.no_cpu_baseline:
         cb = cpu_baseline(scene, args.res, args.cpu_views)
-        res["cpu_baseline"] = {k: (round(v, 5) if isinstance(v, float) else v) for k, v in cb.items()}
+        rnd = lambda v: round(v, 5) if isinstance(v, float) else v  # noqa: E731
+        res["cpu_baseline"] = {k: ({kk: rnd(vv) for kk, vv in v.items()} if isinstance(v, dict) else rnd(v))
+                               for k, v in cb.items()}
     print(json.dumps(res), flush=True)
     if world > 1:
         dist.destroy_process_group()

@@ -378,6 +378,21 @@ static int setup(ctx_t* c, int P, int deg, int M, const float* means, const floa
 /* pair statistics of the last forward (diagnostics): [0] pairs iterated, [1] pairs blended,
  * [2] pixels inside the image */
 static long g_stats[4];
+
+/* Worker threads of the forward / backward loops (OpenMP).  1 (the default, what the parity tests use)
+ * runs the serial loops in the order written; n > 1 is for the CPU baseline timing (bench.py): the
+ * tiles are blended in parallel and the backward sums per-thread partial gradients, so the gradients
+ * differ from the serial build in the last bits (summation order).  Shared by the fp32 / fp64 builds. */
+#ifdef _OPENMP
+#include <omp.h>
+#endif
+#ifndef ORACLE_F64
+int g_oracle_threads = 1;
+void oracle_set_threads(int n) { g_oracle_threads = n > 0 ? n : 1; }
+int oracle_get_threads(void) { return g_oracle_threads; }
+#else
+extern int g_oracle_threads;
+#endif
 void FN(oracle_last_stats)(long* out) { for (int i = 0; i < 4; ++i) out[i] = g_stats[i]; }
 
 static void forward_core(const ctx_t* c, int* radii, fwd_t* f, real* out_color, real* out_depth, real* out_alpha) {
@@ -385,6 +400,8 @@ static void forward_core(const ctx_t* c, int* radii, fwd_t* f, real* out_color, 
   const int P = c->P, W = c->W, H = c->H, nt = c->gx * c->gy;
   f->gs = (gstate*)calloc((size_t)(P > 0 ? P : 1), sizeof(gstate));
   long K = 0;
+  const int nth = g_oracle_threads;
+#pragma omp parallel for num_threads(nth) schedule(static) reduction(+ : K) if (nth > 1)
   for (int i = 0; i < P; ++i) {
     preprocess(c, i, &f->gs[i], radii);
     K += f->gs[i].tiles;
@@ -412,9 +429,11 @@ static void forward_core(const ctx_t* c, int* radii, fwd_t* f, real* out_color, 
   f->final_T = (real*)calloc((size_t)W * H, sizeof(real));
   f->n_contrib = (uint32_t*)calloc((size_t)W * H, sizeof(uint32_t));
   const size_t HW = (size_t)W * H;
-  for (int ty = 0; ty < c->gy; ++ty)
-    for (int tx = 0; tx < c->gx; ++tx) {
-      const uint32_t t = (uint32_t)(ty * c->gx + tx);
+  long st0 = 0, st1 = 0, st2 = 0;
+#pragma omp parallel for num_threads(nth) schedule(dynamic, 1) reduction(+ : st0, st1, st2) if (nth > 1)
+  for (int tt = 0; tt < nt; ++tt) {
+      const int ty = tt / c->gx, tx = tt - ty * c->gx;
+      const uint32_t t = (uint32_t)tt;
       const uint32_t s = f->range[2 * t], e = f->range[2 * t + 1];
       for (int ly = 0; ly < TILE; ++ly)
         for (int lx = 0; lx < TILE; ++lx) {
@@ -422,10 +441,10 @@ static void forward_core(const ctx_t* c, int* radii, fwd_t* f, real* out_color, 
           if (px >= W || py >= H) continue;
           real T = 1, C[3] = {0, 0, 0}, D = 0;
           uint32_t contributor = 0, last = 0;
-          g_stats[2]++;
+          st2++;
           for (uint32_t p = s; p < e; ++p) {
             ++contributor;
-            g_stats[0]++;
+            st0++;
             const gstate* g = &f->gs[f->inst[p].g];
             const real dx = g->px - (real)px, dy = g->py - (real)py;
             const real power = gauss_power(g->ca, g->cb, g->cc, dx, dy);
@@ -438,7 +457,7 @@ static void forward_core(const ctx_t* c, int* radii, fwd_t* f, real* out_color, 
             D += g->depth * alpha * T;
             T = test_T;
             last = contributor;
-            g_stats[1]++;
+            st1++;
           }
           const size_t pid = (size_t)py * W + px;
           f->final_T[pid] = T;
@@ -448,7 +467,8 @@ static void forward_core(const ctx_t* c, int* radii, fwd_t* f, real* out_color, 
           if (out_depth) out_depth[pid] = D;
           if (out_alpha) out_alpha[pid] = RL(1) - T;
         }
-    }
+  }
+  g_stats[0] = st0; g_stats[1] = st1; g_stats[2] = st2;
 }
 
 static void free_fwd(fwd_t* f) {
@@ -513,12 +533,22 @@ void FN(oracle_backward)(int P, int deg, int M, const float* means, const float*
   fwd_t f;
   forward_core(&c, radii, &f, NULL, NULL, NULL);
   const size_t HW = (size_t)W * H;
-  /* per-Gaussian accumulators: m2x, m2y, ca, cb, cc, op, r, g, b, depth */
-  real* acc = (real*)calloc((size_t)10 * (P > 0 ? P : 1), sizeof(real));
+  /* per-Gaussian accumulators: m2x, m2y, ca, cb, cc, op, r, g, b, depth (one set per worker thread) */
+  const int nth = g_oracle_threads;
+  const size_t nacc = (size_t)10 * (P > 0 ? P : 1);
+  real* acc_all = (real*)calloc(nacc * (size_t)nth, sizeof(real));
+  real* acc = acc_all;
   const real ddelx_dx = RL(0.5) * W, ddely_dy = RL(0.5) * H;
-  for (int ty = 0; ty < c.gy; ++ty)
-    for (int tx = 0; tx < c.gx; ++tx) {
-      const uint32_t t = (uint32_t)(ty * c.gx + tx);
+  const int ntiles = c.gx * c.gy;
+#pragma omp parallel for num_threads(nth) schedule(dynamic, 1) if (nth > 1)
+  for (int tt = 0; tt < ntiles; ++tt) {
+      const int ty = tt / c.gx, tx = tt - ty * c.gx;
+      int me = 0;
+#ifdef _OPENMP
+      if (nth > 1) me = omp_get_thread_num();
+#endif
+      real* tacc = acc_all + nacc * (size_t)me;
+      const uint32_t t = (uint32_t)tt;
       const uint32_t s = f.range[2 * t];
       for (int ly = 0; ly < TILE; ++ly)
         for (int lx = 0; lx < TILE; ++lx) {
@@ -545,7 +575,7 @@ void FN(oracle_backward)(int P, int deg, int M, const float* means, const float*
             T = T / (RL(1) - alpha);
             const real dcd = alpha * T;
             real dL_dalpha = 0;
-            real* a = acc + (size_t)10 * gi;
+            real* a = tacc + (size_t)10 * gi;
             for (int ch = 0; ch < 3; ++ch) {
               accr[ch] = last_alpha * last_c[ch] + (RL(1) - last_alpha) * accr[ch];
               last_c[ch] = g->rgb[ch];
@@ -573,8 +603,11 @@ void FN(oracle_backward)(int P, int deg, int M, const float* means, const float*
             a[5] += G * dL_dalpha;
           }
         }
-    }
+  }
+  for (int th = 1; th < nth; ++th)
+    for (size_t k = 0; k < nacc; ++k) acc[k] += acc_all[nacc * (size_t)th + k];
 
+#pragma omp parallel for num_threads(nth) schedule(static) if (nth > 1)
   for (int i = 0; i < P; ++i) {
     const real* a = acc + (size_t)10 * i;
     dmeans2D[3 * i] = a[0]; dmeans2D[3 * i + 1] = a[1]; dmeans2D[3 * i + 2] = 0;
@@ -699,7 +732,7 @@ void FN(oracle_backward)(int P, int deg, int M, const float* means, const float*
       drots[4 * i + 3] = -4 * z * dR[0][0] - 2 * r * dR[0][1] + 2 * x * dR[0][2] + 2 * r * dR[1][0] - 4 * z * dR[1][1] + 2 * y * dR[1][2] + 2 * x * dR[2][0] + 2 * y * dR[2][1];
     }
   }
-  free(acc);
+  free(acc_all);
   free(radii);
   free_fwd(&f);
 }

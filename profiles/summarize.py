@@ -3,7 +3,8 @@
   <tag>_pmc.csv            per kernel: dispatches, mean FETCH_SIZE / WRITE_SIZE (KB, raw counter values) and the
                            corrected HBM bytes per launch = (2 * FETCH_SIZE + WRITE_SIZE) * 1024
                            (gfx950: FETCH_SIZE reads 1/2 of a wide coalesced read; MI355X_MICROARCH.md §HBM)
-  <tag>_traffic.json       the same per-launch bytes for the blend kernels, read by bench.py for roofline.traffic
+  <tag>_traffic.json       the same per-launch bytes for the blend kernels, read by bench.py for roofline.traffic,
+                           and SQ_INSTS_VALU per launch (the VALU roofline), when the valu pass exists
 """
 import collections
 import csv
@@ -38,6 +39,19 @@ with open(os.path.join(dst, f"{tag}_pmc.csv"), "w", newline="") as fh:
     wr.writerow(["kernel", "dispatches", "FETCH_SIZE_KB", "WRITE_SIZE_KB", "hbm_bytes_per_launch_corrected"])
     wr.writerows(rows)
 traffic = {r[0].replace("gsr::", ""): r[4] for r in rows if r[0].startswith("gsr::")}
-json.dump({"source": f"profiles/{tag}_pmc.csv", "per_launch_bytes": traffic},
-          open(os.path.join(dst, f"{tag}_traffic.json"), "w"), indent=1)
+summary = {"source": f"profiles/{tag}_pmc.csv", "per_launch_bytes": traffic}
+vpath = os.path.join(src, "valu", "run_counter_collection.csv")
+if os.path.exists(vpath):
+    v = agg(vpath, "SQ_INSTS_VALU")
+    wv = agg(vpath, "SQ_WAVES")
+    summary["valu_insts_per_launch"] = {k.replace("gsr::", ""): round(sum(x) / len(x)) for k, x in v.items()
+                                        if k.startswith("gsr::")}
+    summary["waves_per_launch"] = {k.replace("gsr::", ""): round(sum(x) / len(x)) for k, x in wv.items()
+                                   if k.startswith("gsr::")}
+    with open(os.path.join(dst, f"{tag}_valu.csv"), "w", newline="") as fh:
+        wr = csv.writer(fh)
+        wr.writerow(["kernel", "dispatches", "SQ_INSTS_VALU_per_launch", "SQ_WAVES_per_launch"])
+        for k in sorted(v, key=lambda k: -sum(v[k]) / len(v[k])):
+            wr.writerow([k, len(v[k]), round(sum(v[k]) / len(v[k])), round(sum(wv.get(k, [0])) / max(1, len(wv.get(k, [0]))))])
+json.dump(summary, open(os.path.join(dst, f"{tag}_traffic.json"), "w"), indent=1)
 print("\n".join(f"{r[0]:40s} {r[4] / 1e6:10.1f} MB/launch" for r in rows[:12]))

@@ -121,7 +121,7 @@ def run_oracle(scene, cam, bg, grads=None, mod=1.0):
     return ref
 
 
-def adjudicate(gpu, r32, r64, bar, what, name, cap=None):
+def adjudicate(gpu, r32, r64, bar, what, name, cap=None, excuse=None):
     """Rows (first axis) whose GPU value misses the fp64 value by more than `bar` (elementwise) may be at
     most FLIP_RATIO x the fp32 oracle's such rows + FLIP_SLACK; with `cap`, no GPU miss exceeds
     max(cap, 4 x the fp32 oracle's largest miss).  Returns the stats."""
@@ -134,10 +134,15 @@ def adjudicate(gpu, r32, r64, bar, what, name, cap=None):
     bad_g = (e_g > bar).reshape(n, -1).any(1) if n else np.zeros(0, bool)
     bad_3 = (e_3 > bar).reshape(n, -1).any(1) if n else np.zeros(0, bool)
     ok_rows = ~bad_g
+    n_excused = 0
+    if excuse is not None and n:  # rows that depend on a pixel the GPU flipped where the fp32 oracle did not
+        n_excused = int((bad_g & excuse).sum())
+        bad_g = bad_g & ~excuse
+        bad_3 = bad_3 & ~excuse
     st = dict(rows=int(n), gpu_miss=int(bad_g.sum()), f32_miss=int(bad_3.sum()),
               max_err_gpu=float(e_g.max()) if e_g.size else 0.0, max_err_f32=float(e_3.max()) if e_3.size else 0.0,
               max_err_gpu_in_bar=float(e_g.reshape(n, -1)[ok_rows].max()) if ok_rows.any() and e_g.size else 0.0,
-              max_diff_gpu_f32=float(np.abs(gpu - r32).max()) if e_g.size else 0.0)
+              max_diff_gpu_f32=float(np.abs(gpu - r32).max()) if e_g.size else 0.0, excused=n_excused)
     REPORT.append((what, name, st))
     allowed = FLIP_RATIO * st["f32_miss"] + FLIP_SLACK
     assert st["gpu_miss"] <= allowed, f"{what}: {name}: {st['gpu_miss']} rows miss the fp64 bar (allowed {allowed}): {st}"
@@ -208,25 +213,52 @@ def check_forward(gpu, ref, what="", K_gpu=None, color_key="color"):
     radii and K as check_radii."""
     f32, f64 = ref["f32"], ref["f64"]
     scale_c = max(1.0, float(np.abs(f64["color"]).max()))
-    adjudicate(_pixels(gpu[color_key]), _pixels(f32["color"]), _pixels(f64["color"]), RGB_ATOL, what, "color",
-               cap=0.02 * scale_c)
-    adjudicate(_pixels(gpu["alpha"]), _pixels(f32["alpha"]), _pixels(f64["alpha"]), RGB_ATOL, what, "alpha", cap=0.02)
     d64 = _pixels(f64["depth"])
     scale_d = max(1.0, float(np.abs(d64).max()))
-    adjudicate(_pixels(gpu["depth"]), _pixels(f32["depth"]), d64, RGB_ATOL + DEPTH_RTOL * np.abs(d64), what, "depth",
-               cap=0.02 * scale_d)
+    gpu_only = np.zeros(d64.shape[0], bool)
+    for key, bar, cap in ((color_key, RGB_ATOL, 0.02 * scale_c), ("alpha", RGB_ATOL, 0.02),
+                          ("depth", RGB_ATOL + DEPTH_RTOL * np.abs(d64), 0.02 * scale_d)):
+        rk = "color" if key == color_key else key
+        g, o3, o6 = _pixels(gpu[key]).astype(np.float64), _pixels(f32[rk]).astype(np.float64), _pixels(f64[rk])
+        adjudicate(g, o3, o6, bar, what, rk, cap=cap)
+        gpu_only |= (np.abs(g - o6) > bar).any(1) & ~(np.abs(o3 - o6) > bar).any(1)
+    # pixels where the GPU took a different discrete decision than both oracles (allowed above, as often
+    # as the fp32 oracle does so): every Gaussian blended at such a pixel has a legitimately different
+    # gradient; check_grads excuses those rows
+    ref["gpu_only_px"] = np.nonzero(gpu_only)[0]
     if "radii" in gpu:
         check_radii(gpu["radii"], ref, what, K_gpu)
 
 
+def flip_dependents(ref, pixels):
+    """Gaussians that reach alpha >= 1/255 (fp64 preprocess values, 1 % margin) at any of `pixels`."""
+    a = ref["aux64"]
+    P = a["px"].shape[0]
+    dep = np.zeros(P, bool)
+    if len(pixels) == 0 or P == 0:
+        return dep
+    vis = a["tiles"] > 0
+    W = ref["W"]
+    for pid in pixels:
+        y, x = divmod(int(pid), W)
+        dx, dy = a["px"] - x, a["py"] - y
+        power = -0.5 * (a["conic"][:, 0] * dx * dx + a["conic"][:, 2] * dy * dy) - a["conic"][:, 1] * dx * dy
+        alpha = np.minimum(0.99, a["opacity"] * np.exp(np.minimum(power, 0.0)))
+        dep |= vis & (power <= 0) & (alpha >= 0.99 / 255.0)
+    return dep
+
+
 def check_grads(gpu, ref, keys, what=""):
-    """Elementwise |g - g64| <= 1e-4 max(1, |g64|) with fp32-oracle adjudication of flip-affected rows."""
+    """Elementwise |g - g64| <= 1e-4 max(1, |g64|) with fp32-oracle adjudication of flip-affected rows;
+    rows of Gaussians blended at a pixel the GPU flipped on its own (check_forward) are excused."""
     b32, b64 = ref["b32"], ref["b64"]
+    excuse = flip_dependents(ref, ref.get("gpu_only_px", ())) if "aux64" in ref else None
     out = {}
     for k in keys:
         r64 = b64[k]
         bar = GRAD_TOL * np.maximum(1.0, np.abs(r64))
-        out[k] = adjudicate(gpu["g_" + k], b32[k], r64, bar, what, "grad " + k)
+        ex = excuse if excuse is not None and excuse.shape[0] == r64.shape[0] else None
+        out[k] = adjudicate(gpu["g_" + k], b32[k], r64, bar, what, "grad " + k, excuse=ex)
     return out
 
 

@@ -176,3 +176,40 @@ def test_torch_restatement_gradients_finite_difference():
         e[0, y, x] = 1e-6
         fd = (f(sc["depth"] + e) - f(sc["depth"] - e)) / 2e-6
         assert abs(float(fd) - float(g[0, y, x])) < 1e-6 * max(1.0, abs(float(fd))) + 1e-7
+
+
+@pytest.mark.gpu
+def test_shade_saturated_masks_match_torch():
+    """Pixels whose albedo col / (alpha + 1e-6) sits exactly on (or one ulp beside) the [0, 1] clamp edges
+    and whose composited image saturates: the HIP backward must take every clamp-mask decision as the
+    forward (and torch autograd in fp32 on the same inputs) does — a differing decision changes the
+    gradient by O(1), far above the bar."""
+    from diff_gaussian_rasterization.shading import shade_views
+
+    H, W = 32, 48
+    sc = _scene(1, H, W, seed=7)[0]
+    dev = "cuda"
+    al = sc["alpha"].float()
+    ad = al + 1e-6
+    g = torch.Generator().manual_seed(3)
+    pick = torch.randint(0, 5, (3, H, W), generator=g)
+    one = torch.ones_like(ad.expand(3, H, W))
+    factor = torch.stack([one, torch.nextafter(one, 2 * one), torch.nextafter(one, 0 * one),
+                          torch.full_like(one, 1.5), torch.zeros_like(one)])
+    color = (ad * factor.gather(0, pick[None])[0]).float()  # alb exactly 1, 1 + ulp, 1 - ulp, 1.5, 0
+    bg = torch.where(torch.rand((H, W, 3), generator=g) < 0.5, torch.ones(H, W, 3), torch.rand((H, W, 3), generator=g))
+    ka, kd = (0.3, 0.3, 0.3), (0.9, 0.9, 0.9)  # tl up to 1.2: the image clamp at 1 saturates
+    leaves = dict(color=color.to(dev), depth=sc["depth"].float().to(dev), alpha=al.to(dev), bg=bg.float().to(dev))
+    ups = [u.float().to(dev) for u in sc["ups"]]
+    ro, rd, light = sc["rays_o"].float().to(dev), sc["rays_d"].float().to(dev), sc["light"].float().to(dev)
+    t = {k: v.clone().requires_grad_(True) for k, v in leaves.items()}
+    outs = shade_views(t["color"], t["depth"], t["alpha"], ro, rd, t["bg"], light, ka, kd, "diffuse")
+    torch.autograd.backward(outs, ups)
+    r = {k: v.clone().requires_grad_(True) for k, v in leaves.items()}
+    ref = tr.shading_epilogue(r["color"], r["depth"], r["alpha"], ro, rd, r["bg"], light,
+                              torch.tensor(ka, device=dev), torch.tensor(kd, device=dev), "diffuse")
+    torch.autograd.backward(ref, ups)
+    for k in ("color", "bg", "alpha"):
+        a, b = t[k].grad.double(), r[k].grad.double()
+        err = ((a - b).abs() / b.abs().clamp(min=1.0)).max()
+        assert float(err) <= 1e-4, f"grad {k}: {float(err)}"

@@ -177,3 +177,69 @@ def test_contiguous_span_detection():
     assert _contiguous_span([buf[0:6], buf[4:10]]) is None  # overlap
     assert _contiguous_span([a, torch.zeros(4)]) is None    # another buffer
     assert _contiguous_span([buf[0:10:2]]) is None          # strided
+
+
+def _densify_views(P, B, lo, hi):
+    """Per-view densification inputs of views [lo, hi) (as the renderer returns them), deterministic per
+    view so that the union over ranks is the single-process batch."""
+    radii, vps, vis = [], [], []
+    for v in range(lo, hi):
+        g = torch.Generator().manual_seed(1000 + v)
+        r = torch.randint(0, 6, (P,), generator=g, dtype=torch.int32)
+        vp = torch.zeros(P, 3, requires_grad=True)
+        vp.grad = torch.randn(P, 3, generator=g) * 0.02
+        radii.append(r)
+        vps.append(vp)
+        vis.append(r > 0)
+    return {"radii": radii, "viewspace_points": vps, "visibility_filter": vis}
+
+
+def _densify_worker(rank, world, port, tmp, synced):
+    import densify_reference as dr
+    from diff_gaussian_rasterization.view_shard import replica_checksum, update_states_sharded
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        torch.manual_seed(100 + rank)  # the usual per-rank seeding
+        scene = gs.make_scene(200, sh_degree=1, seed=8, radius=0.5)
+        model = dr.DensifyModel(scene, "cpu", densify_grad_threshold=0.005)
+        B = 6
+        lo, hi = shard_range(B, world, rank)
+        outs = _densify_views(200, B, lo, hi)
+        if synced:
+            update_states_sharded(model, 5, outs)
+        else:  # the reduced statistics, but the densification draws left to each rank's RNG
+            max_r, gsum, cnt = reduce_densify_stats(outs["radii"], outs["viewspace_points"], outs["visibility_filter"], 200)
+            model.max_radii2D = torch.max(model.max_radii2D, max_r)
+            model.xyz_gradient_accum += gsum[:, None]
+            model.denom += cnt[:, None]
+            model.update_states(5, [], [], [])
+        tensors = model.parameters() + [model.xyz_gradient_accum, model.max_radii2D]
+        same = replica_checksum(tensors)
+        np.savez(os.path.join(tmp, f"dens{int(synced)}_{rank}.npz"), same=same, P=model.get_xyz.shape[0],
+                 xyz=model.get_xyz.detach().numpy())
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("synced", [True, False])
+def test_densify_keeps_replicas_identical(synced, tmp_path):
+    """update_states_sharded: reduced statistics + replica_rng -> every rank densifies and prunes the same
+    Gaussians with the same random split samples (bitwise-identical replicas); without the shared RNG the
+    split samples differ between ranks (the test is sensitive to it)."""
+    import densify_reference as dr
+
+    world = 2
+    mp.spawn(_densify_worker, args=(world, _free_port(), str(tmp_path), synced), nprocs=world, join=True)
+    z = [np.load(tmp_path / f"dens{int(synced)}_{r}.npz") for r in range(world)]
+    # single process over the whole batch: same Gaussian count (the decisions do not depend on the samples)
+    model = dr.DensifyModel(gs.make_scene(200, sh_degree=1, seed=8, radius=0.5), "cpu", densify_grad_threshold=0.005)
+    outs = _densify_views(200, 6, 0, 6)
+    model.update_states(5, outs["visibility_filter"], outs["radii"], outs["viewspace_points"])
+    assert int(z[0]["P"]) == int(z[1]["P"]) == model.get_xyz.shape[0] > 200
+    if synced:
+        assert bool(z[0]["same"]) and bool(z[1]["same"])
+        np.testing.assert_array_equal(z[0]["xyz"], z[1]["xyz"])
+    else:
+        assert not bool(z[0]["same"])

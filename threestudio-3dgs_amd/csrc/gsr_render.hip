@@ -29,6 +29,11 @@ namespace gsr {
 // XCC_ID << 24 | work count.  [0] = k_render_fwd, [1] = k_render_bwd.
 #define GSR_TL_MAX 65536
 __device__ uint4 g_timeline[2][GSR_TL_MAX];
+// pair counters (vector global atomics, diagnostic build only): [0] forward (pixel, Gaussian) pairs
+// evaluated (lanes not yet terminated), [1] forward pair slots issued (64 lanes x candidates walked),
+// [2] backward kept (candidate, quadrant) pairs replayed x 64 pixels, [3] backward pair slots of the
+// lockstep batches (4 x the busiest quadrant's kept count x 64)
+__device__ unsigned long long g_pairs[4];
 #define GSR_TL_BEGIN const uint32_t tl_t0 = (uint32_t)__builtin_amdgcn_s_memrealtime();
 #define GSR_TL_END(which, work)                                                                  \
   if (threadIdx.x == 0 && blockIdx.x < GSR_TL_MAX)                                                \
@@ -151,6 +156,9 @@ __global__ __launch_bounds__(64) void k_render_fwd(RenderSet rs,
   bool done = !inside;
   float T = 1.0f, Cr = 0.f, Cg = 0.f, Cb = 0.f, D = 0.f;
   uint32_t last_contributor = 0;
+#ifdef GSR_TIMELINE
+  unsigned long long pc_eval = 0, pc_slot = 0;
+#endif
   // two-stage prefetch (as in the backward): indices two batches ahead, records one batch ahead
   const uint32_t gmask = rs.gmask;
   const float4 zero4 = make_float4(0.f, 0.f, 0.f, 0.f);
@@ -192,6 +200,10 @@ __global__ __launch_bounds__(64) void k_render_fwd(RenderSet rs,
       const float dx = a.x - pxf, dy = a.y - pyf;
       const float power2 = gauss_power2(a.z, a.w, b.x, dx, dy);  // log2(e) * power
       const float alpha = fminf(GSR_ALPHA_MAX, b.y * __builtin_amdgcn_exp2f(power2));
+#ifdef GSR_TIMELINE
+      pc_eval += done ? 0ull : 1ull;
+      pc_slot += 1ull;
+#endif
       const bool ok = !done && power2 <= 0.0f && alpha >= GSR_ALPHA_MIN;
       const float test_T = T * (1.0f - alpha);
       const bool term = ok && test_T < GSR_T_EPS;
@@ -237,6 +249,10 @@ __global__ __launch_bounds__(64) void k_render_fwd(RenderSet rs,
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) mc = max(mc, (uint32_t)__shfl_xor((int)mc, o, 64));
   if (lane == 0) quad_maxc[unit] = mc;
+#ifdef GSR_TIMELINE
+  atomicAdd(&g_pairs[0], pc_eval);  // per-lane values; the backend's atomic optimizer combines the wave
+  atomicAdd(&g_pairs[1], pc_slot);
+#endif
   GSR_TL_END(0, mc)
 }
 
@@ -711,6 +727,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5, 8))) voi
   }
 #ifdef GSR_TIMELINE
   // bwd record: z = sum over batches of 4 x the busiest quadrant's kept count (not HW_ID)
+  if (threadIdx.x == 0) {
+    atomicAdd(&g_pairs[2], 64ull * (unsigned long long)tl_work);
+    atomicAdd(&g_pairs[3], 64ull * (unsigned long long)tl_max);
+  }
   if (threadIdx.x == 0 && blockIdx.x < GSR_TL_MAX)
     g_timeline[1][blockIdx.x] = make_uint4(tl_t0, (uint32_t)__builtin_amdgcn_s_memrealtime(), (uint32_t)tl_max,
                                            ((uint32_t)__builtin_amdgcn_s_getreg((15 << 11) | 20) << 24) |
@@ -734,6 +754,18 @@ void launch_render_backward(const RenderSet& rs, const GeomState& g, const uint3
 }  // namespace gsr
 
 #ifdef GSR_TIMELINE
+// diagnostic build only: read (and optionally reset) the pair counters (4 x u64, see g_pairs)
+extern "C" int gsr_diag_pairs(void* host, int reset) {
+  if (hipDeviceSynchronize() != hipSuccess) return -1;
+  if (hipMemcpyFromSymbol(host, HIP_SYMBOL(gsr::g_pairs), 4 * sizeof(unsigned long long), 0,
+                          hipMemcpyDeviceToHost) != hipSuccess)
+    return -1;
+  if (reset) {
+    const unsigned long long z[4] = {0, 0, 0, 0};
+    if (hipMemcpyToSymbol(HIP_SYMBOL(gsr::g_pairs), z, sizeof(z), 0, hipMemcpyHostToDevice) != hipSuccess) return -1;
+  }
+  return 0;
+}
 extern "C" int gsr_diag_timeline(int which, void* host, int n) {
   if (which < 0 || which > 1 || n > GSR_TL_MAX) return -1;
   if (hipDeviceSynchronize() != hipSuccess) return -1;

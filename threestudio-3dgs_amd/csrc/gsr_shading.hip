@@ -164,10 +164,12 @@ __device__ __forceinline__ void shade_bwd_pixel(const ShadeArgs& A, const ShadeG
   const P3 c = cross3(a, b);
   const P3 n = p3(-c.x, -c.y, -c.z);
   const float len = sqrtf(dot3(n, n));
-  // the backward's recomputed forward values use one reciprocal per normalisation (gradients are
-  // compared with a tolerance; the forward kernel keeps the reference's IEEE divides)
-  const float rden = 1.0f / fmaxf(len, kEps);
-  const P3 u = p3(n.x * rden, n.y * rden, n.z * rden);
+  // the recomputed forward values that decide a clamp mask (the unit normal and light direction feed
+  // dot >= 0 and the image clamp, the albedo its own clamp) use the forward kernel's IEEE divides, so
+  // every mask matches the forward's — and torch autograd's — decision bit for bit; the gradient
+  // arithmetic below uses one reciprocal per normalisation
+  const float den = fmaxf(len, kEps);
+  const P3 u = p3(n.x / den, n.y / den, n.z / den);
   const float al = A.alpha[(size_t)v * HW + p];
   const bool m = al > 0.99f;
   P3 gu = p3(0.f, 0.f, 0.f);
@@ -188,8 +190,8 @@ __device__ __forceinline__ void shade_bwd_pixel(const ShadeArgs& A, const ShadeG
     const P3 s = own_normal ? u : pred_normal(A, v, HW, p);
     const P3 L = sub3(p3(A.light[3 * v], A.light[3 * v + 1], A.light[3 * v + 2]), X);
     const float llen = sqrtf(dot3(L, L));
-    const float rlden = 1.0f / fmaxf(llen, kEps);
-    const P3 l = p3(L.x * rlden, L.y * rlden, L.z * rlden);
+    const float lden = fmaxf(llen, kEps);
+    const P3 l = p3(L.x / lden, L.y / lden, L.z / lden);
     const float dt = dot3(s, l);
     const float dl = fmaxf(dt, 0.0f);
     const float rad = 1.0f / (al + 1e-6f);
@@ -200,7 +202,7 @@ __device__ __forceinline__ void shade_bwd_pixel(const ShadeArgs& A, const ShadeG
     for (int k = 0; k < 3; ++k) {
       const float tl = dl * A.kd[k] + A.ka[k];
       const float col = A.color[plane + k * HW];
-      const float alb = col * rad;
+      const float alb = col / (al + 1e-6f);
       const float albc = fminf(fmaxf(alb, 0.0f), 1.0f);
       const float fg = A.mode == GSR_SHADING_DIFFUSE ? albc * tl : (A.mode == GSR_SHADING_ALBEDO ? alb : tl);
       const float bgk = bg_at(A, v, HW, p, k);

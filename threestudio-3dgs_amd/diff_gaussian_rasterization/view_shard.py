@@ -19,6 +19,7 @@ exercised with the gloo backend on CPU (tests/test_view_shard.py).
 """
 from __future__ import annotations
 
+import contextlib
 from typing import Callable
 
 import torch
@@ -252,3 +253,83 @@ class ViewShardedBatchRenderer:
             full = all_gather_views(t, bs, self.group).permute(0, 2, 3, 1)
             out["comp_rgb_bg" if name == "comp_rgb_bg_raw" else name] = full
         return out
+
+
+# ---- keeping the replicas identical through densification -------------------------------------------
+
+def _coll_device(group=None):
+    """Device for small control tensors of the collective backend (RCCL needs device memory)."""
+    return torch.device("cuda", torch.cuda.current_device()) if dist.get_backend(group) == "nccl" else torch.device("cpu")
+
+
+@contextlib.contextmanager
+def replica_rng(group=None):
+    """Run the body with the torch RNG (CPU and every GPU) seeded identically on all ranks.
+
+    The reference's densification draws random numbers — ``torch.normal`` samples for split Gaussians
+    (geometry/gaussian_base.py:733) and a ``torch.randperm`` prune above max_num (:838).  With the usual
+    per-rank seeding those draws differ between ranks and the replicas stop being identical, after which
+    the gradient all-reduce would sum gradients of different models.  Inside this context the draws are
+    the same everywhere (rank 0 picks the seed; the outer RNG state is restored afterwards)."""
+    world, rank = _world()
+    if world == 1:
+        yield
+        return
+    seed = torch.randint(0, 2 ** 62, (1,), dtype=torch.int64) if rank == 0 else torch.zeros(1, dtype=torch.int64)
+    seed = seed.to(_coll_device(group))
+    dist.broadcast(seed, src=dist.get_global_rank(group, 0) if group is not None else 0, group=group)
+    devices = list(range(torch.cuda.device_count())) if torch.cuda.is_available() else []
+    with torch.random.fork_rng(devices=devices):
+        torch.manual_seed(int(seed.item()))
+        yield
+
+
+def update_states_sharded(geometry, iteration, outputs: dict, group=None):
+    """``geometry.update_states`` (geometry/gaussian_base.py:821-869) for a view-sharded batch.
+
+    The reference loops over the batch's per-view lists, taking the max of the radii and adding
+    |viewspace grad[:, :2]| and a visibility count per view (:845-851).  Each rank holds only its own
+    views, so the statistics are reduced over the ranks first (reduce_densify_stats: MAX / SUM), applied
+    exactly where the reference applies them (not when it returns early for the SuGaR prune or the max_num
+    prune, :827-841), and the rest of update_states — prune and densify — runs with no views under
+    replica_rng, so every rank takes the same decisions and draws the same samples."""
+    P = int(geometry.get_xyz.shape[0])
+    max_r, gsum, cnt = reduce_densify_stats(outputs["radii"], outputs["viewspace_points"],
+                                            outputs["visibility_filter"], P, group, device=geometry.get_xyz.device)
+    cfg = geometry.cfg
+    early = (getattr(cfg, "sugar_prune_at", None) is not None and iteration == cfg.sugar_prune_at) or \
+        P >= cfg.max_num + 100
+    with torch.no_grad():
+        if not early:
+            geometry.max_radii2D = torch.max(geometry.max_radii2D, max_r)
+            geometry.xyz_gradient_accum += gsum[:, None]
+            geometry.denom += cnt[:, None]
+        with replica_rng(group):
+            geometry.update_states(iteration, [], [], [])
+
+
+def replica_checksum(tensors, group=None) -> bool:
+    """True when every rank holds bitwise-identical `tensors` (one small all-gather of checksums)."""
+    world, _ = _world()
+    if world == 1:
+        return True
+    dev = _coll_device(group)
+    sums = []
+    for t in tensors:
+        b = t.detach().contiguous().view(-1).view(torch.uint8) if t.numel() else torch.zeros(1, dtype=torch.uint8)
+        w = torch.arange(1, b.numel() + 1, device=b.device, dtype=torch.int64) % 65521
+        sums += [float(b.numel()), float((b.to(torch.int64) * w).sum().item())]
+    mine = torch.tensor(sums, dtype=torch.float64, device=dev)
+    allv = [torch.empty_like(mine) for _ in range(world)]
+    dist.all_gather(allv, mine, group=group)
+    return all(torch.equal(a, allv[0]) for a in allv)
+
+
+def broadcast_replica(tensors, group=None, src: int = 0):
+    """Overwrite `tensors` on every rank with rank `src`'s values (e.g. parameters and optimizer moments
+    after a checkpoint load); shapes must already agree."""
+    world, _ = _world()
+    if world == 1:
+        return
+    for t in tensors:
+        dist.broadcast(t.data, src=src, group=group)
