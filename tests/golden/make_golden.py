@@ -11,6 +11,10 @@ Two kinds of fixtures:
      getProjectionMatrix, getWorld2View2
                                      utils/sugar_utils.py:796-829
      camera construction             geometry/sugar.py:891-896 (world_view, full_proj, camera_center)
+     Depth2Normal                    renderer/diff_gaussian_rasterizer_shading.py:22-51
+     GaussianDiffuseWithPointLightMaterial.forward
+                                     material/gaussian_material.py:41-104 (method body; threestudio's dot
+                                     supplied), composed as the shading renderer does (:169-208)
    They pin the CPU restatement's SH, covariance and projection pieces (tests/test_golden.py).
    Only inputs and outputs are written; no reference source is stored.
 
@@ -116,6 +120,95 @@ def make_reference(ref: str):
                         **{f"{k}_{i}": np.asarray(v) for i, c in enumerate(cams) for k, v in c.items()})
 
 
+def lift_method(path: str, cls: str, method: str, extra_globals: dict):
+    """One method of a reference class as a plain function (annotations stripped: the class itself needs
+    threestudio; the method body needs only torch)."""
+    tree = ast.parse(open(path).read())
+    node = next(n for n in tree.body if isinstance(n, ast.ClassDef) and n.name == cls)
+    fn = next(n for n in node.body if isinstance(n, ast.FunctionDef) and n.name == method)
+    fn.decorator_list = []
+    fn.returns = None
+    for a in fn.args.args + fn.args.kwonlyargs:
+        a.annotation = None
+    code = ast.unparse(ast.Module(body=[fn], type_ignores=[]))
+    ns = dict(extra_globals)
+    exec(compile(code, path, "exec"), ns)  # noqa: S102 — reference pure method body, CPU only
+    return ns[method]
+
+
+def make_shading_reference(ref: str):
+    """The shading renderer's post-raster epilogue from the reference's own code: Depth2Normal
+    (renderer/diff_gaussian_rasterizer_shading.py:22-51) and GaussianDiffuseWithPointLightMaterial.forward
+    (material/gaussian_material.py:41-104), composed as the renderer does (:169-208); threestudio's
+    dot(x, y) = sum(x * y, -1, keepdim=True) is supplied.  fp64, CPU; outputs and gradients for seeded
+    upstream gradients."""
+    from types import SimpleNamespace
+
+    import random
+
+    F = torch.nn.functional
+    g = {"torch": torch, "F": F, "random": random, "dot": lambda x, y: torch.sum(x * y, -1, keepdim=True)}
+    d2n = lift(os.path.join(ref, "renderer/diff_gaussian_rasterizer_shading.py"), ["Depth2Normal"], g)["Depth2Normal"]()
+    # its stencil weights (0, +-1) as fp64 so the fixture is computed in fp64 (the values are exact)
+    d2n.delzdelxkernel = d2n.delzdelxkernel.double()
+    d2n.delzdelykernel = d2n.delzdelykernel.double()
+    material_forward = lift_method(os.path.join(ref, "material/gaussian_material.py"),
+                                   "GaussianDiffuseWithPointLightMaterial", "forward", g)
+    rng = np.random.default_rng(77)
+    out = {}
+    H, W = 20, 28
+    ys, xs = np.meshgrid(np.arange(H, dtype=np.float64), np.arange(W, dtype=np.float64), indexing="ij")
+    depth = (2.0 + 0.3 * np.sin(xs / 5.0) * np.cos(ys / 4.0) + 0.01 * rng.random((H, W)))[None]
+    f = 0.5 * H / math.tan(math.radians(30))
+    rays_d = np.stack([(xs + 0.5 - W / 2) / f, -(ys + 0.5 - H / 2) / f, -np.ones_like(xs)], -1)
+    Qm, _ = np.linalg.qr(rng.normal(size=(3, 3)))
+    rays_d = rays_d @ Qm.T
+    rays_o = np.broadcast_to(rng.normal(size=3), (H, W, 3)).copy()
+    alpha = rng.random((1, H, W))
+    alpha[:, : H // 2, : W // 2] = 1.0
+    color = rng.random((3, H, W)) * alpha * 1.2 - 0.05
+    bg = rng.random((H, W, 3))
+    light = rng.normal(size=3) * 3
+    ups = [rng.normal(size=(3, H, W)), rng.normal(size=(3, H, W)), rng.normal(size=(1, H, W))]
+    out.update(color=color, depth=depth, alpha=alpha, rays_o=rays_o, rays_d=rays_d, bg=bg, light=light,
+               up_render=ups[0], up_normal=ups[1], up_depth=ups[2])
+    for shading in ("diffuse", "albedo", "textureless"):
+        t = {k: torch.tensor(v, requires_grad=True) for k, v in (("color", color), ("depth", depth), ("alpha", alpha),
+                                                                 ("bg", bg))}
+        ro, rd = torch.tensor(rays_o), torch.tensor(rays_d)
+        mat = SimpleNamespace(training=False, ambient_only=False,
+                              cfg=SimpleNamespace(soft_shading=False, diffuse_prob=0.75, textureless_prob=0.5),
+                              diffuse_light_color=torch.tensor([0.9, 0.8, 0.7], dtype=torch.float64),
+                              ambient_light_color=torch.tensor([0.1, 0.2, 0.15], dtype=torch.float64))
+        # renderer/diff_gaussian_rasterizer_shading.py:172-208 (pred_normal off, comp_rgb_bg = bg)
+        rendered_depth = t["depth"].clone()
+        xyz_map = ro + rendered_depth.permute(1, 2, 0) * rd
+        normal_map = d2n(xyz_map.permute(2, 0, 1).unsqueeze(0))[0]
+        normal_map = F.normalize(normal_map, dim=0)
+        light_positions = torch.tensor(light)[None, None, :].expand(H, W, -1)
+        shading_normal = normal_map.permute(1, 2, 0)
+        rgb_fg = material_forward(mat, positions=xyz_map, shading_normal=shading_normal,
+                                  albedo=(t["color"] / (t["alpha"] + 1e-6)).permute(1, 2, 0),
+                                  light_positions=light_positions, shading=shading).permute(2, 0, 1)
+        rendered_image = rgb_fg * t["alpha"] + (1 - t["alpha"]) * t["bg"].reshape(H, W, 3).permute(2, 0, 1)
+        normal_map = normal_map * 0.5 * t["alpha"] + 0.5
+        mask = t["alpha"] > 0.99
+        normal_mask = mask.repeat(3, 1, 1)
+        normal_map = torch.where(normal_mask, normal_map, normal_map.detach())
+        rendered_depth = torch.where(mask, rendered_depth, rendered_depth.detach())
+        render = rendered_image.clamp(0, 1)
+        torch.autograd.backward([render, normal_map, rendered_depth],
+                                [torch.tensor(ups[0]), torch.tensor(ups[1]), torch.tensor(ups[2])])
+        out[f"{shading}_render"] = render.detach().numpy()
+        out[f"{shading}_normal"] = normal_map.detach().numpy()
+        out[f"{shading}_depth"] = rendered_depth.detach().numpy()
+        for k, v in t.items():
+            out[f"{shading}_grad_{k}"] = v.grad.numpy()
+    out["ambient"] = np.array([0.1, 0.2, 0.15])
+    out["diffuse"] = np.array([0.9, 0.8, 0.7])
+    np.savez_compressed(os.path.join(HERE, "reference_shading.npz"), **out)
+
+
 def make_oracle_scene():
     sys.path.insert(0, os.path.join(ROOT, "threestudio-3dgs_amd"))
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
@@ -146,5 +239,6 @@ if __name__ == "__main__":
     a = ap.parse_args()
     if not a.skip_reference:
         make_reference(a.reference)
+        make_shading_reference(a.reference)
     make_oracle_scene()
     print("golden vectors written to", HERE)
