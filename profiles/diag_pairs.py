@@ -26,8 +26,10 @@ def main():
     lib = _C.load_library()
     lib.gsr_diag_pairs.argtypes = [ctypes.c_void_p, ctypes.c_int]
     dev = torch.device("cuda", 0)
-    V, R = 64, 1024
-    scene = gs.make_scene(1_000_000, sh_degree=3, seed=0)
+    workload = sys.argv[2] if len(sys.argv) > 2 else "c3"
+    V, R = 64, (800 if workload == "sugar" else 1024)
+    scene = gs.make_sugar_scene(7, sh_degree=3, seed=0) if workload == "sugar" else \
+        gs.make_scene(1_000_000, sh_degree=3, seed=0)
     rep = bench.Replica(scene, dev)
     cams = bench.build_views(V, R, dev)
     bg0 = torch.zeros(3, device=dev)
@@ -40,14 +42,21 @@ def main():
     for it in range(2):  # the second pass is the counted one
         assert lib.gsr_diag_pairs(buf.ctypes.data, 1) == 0
         _C.RECENT_LISTED.clear()
-        c, d, a, _ = bench.render_views(rep, settings, bg_img)
-        torch.autograd.backward((c, d, a), ups)
+        if workload == "sugar":
+            shade = bench.shading_inputs(cams, dev)
+            outs = bench.render_views_sugar(rep, settings, shade)
+            torch.autograd.backward(outs, (ups[0], ups[1], ups[2], ups[0], ups[0]))
+        else:
+            c, d, a, _ = bench.render_views(rep, settings, bg_img)
+            torch.autograd.backward((c, d, a), ups)
         rep.zero_grad()
         torch.cuda.synchronize()
     assert lib.gsr_diag_pairs(buf.ctypes.data, 1) == 0
     listed = float(np.mean(list(_C.RECENT_LISTED)))
     out = {
-        "workload": f"bench.py default: 1M Gaussians, {R}x{R}, SH3, {V}-view set, fused background composite",
+        "workload": (f"bench.py --workload sugar: {scene['means3D'].shape[0]} SuGaR Gaussians, {R}x{R}, two passes "
+                     f"(colours, normals), {V}-view set" if workload == "sugar" else
+                     f"bench.py default: 1M Gaussians, {R}x{R}, SH3, {V}-view set, fused background composite"),
         "views": V,
         "fwd_pairs_evaluated_per_view": float(buf[0]) / V,
         "fwd_pair_slots_per_view": float(buf[1]) / V,
@@ -59,7 +68,7 @@ def main():
                 "terminated lanes; bwd pairs = kept (candidate, 8x8 quadrant) pairs x 64 pixels",
     }
     os.makedirs(os.path.join(ROOT, "gpurun_out"), exist_ok=True)
-    with open(os.path.join(ROOT, "gpurun_out", f"pairs_{tag}.json"), "w") as f:
+    with open(os.path.join(ROOT, "gpurun_out", f"pairs_{tag}{'_sugar' if workload == 'sugar' else ''}.json"), "w") as f:
         json.dump(out, f, indent=1)
     print(json.dumps(out, indent=1))
 
