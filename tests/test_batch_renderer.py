@@ -86,8 +86,9 @@ def _free_port():
 
 
 def _worker(rank, world, port, tmp, B, kind):
-    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
-    dist.init_process_group("gloo", rank=rank, world_size=world)
+    # file rendezvous (no TCP port to race for); `port` only makes the file name unique
+    dist.init_process_group("gloo", init_method="file://" + os.path.join(tmp, f"rendezvous_{port}"), rank=rank,
+                            world_size=world)
     try:
         _cpu()
         batch = rf.make_batch(B, H, W, "cpu", torch.float64)

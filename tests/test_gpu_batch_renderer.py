@@ -110,9 +110,10 @@ def _step(rank_world, B, tmp, tag):
 def _worker(rank, world, port, tmp, B):
     import torch.distributed as dist
 
-    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     torch.cuda.set_device(0)
-    dist.init_process_group("gloo", rank=rank, world_size=world)
+    # file rendezvous (no TCP port to race for); `port` only makes the file name unique
+    dist.init_process_group("gloo", init_method="file://" + os.path.join(tmp, f"rendezvous_{port}"), rank=rank,
+                            world_size=world)
     try:
         torch.manual_seed(100 + rank)
         _step((rank, world), B, tmp, "shard")

@@ -75,8 +75,9 @@ def _single_process():
 
 
 def _worker(rank, world, port, tmp):
-    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
-    dist.init_process_group("gloo", rank=rank, world_size=world)
+    # file rendezvous (no TCP port to race for); `port` only makes the file name unique
+    dist.init_process_group("gloo", init_method="file://" + os.path.join(tmp, f"rendezvous_{port}"), rank=rank,
+                            world_size=world)
     try:
         params = _params()
         r = ViewShardedBatchRenderer(_render_view(params))
@@ -139,8 +140,9 @@ class _CarvedGrads(torch.autograd.Function):
 
 
 def _span_worker(rank, world, port, tmp):
-    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
-    dist.init_process_group("gloo", rank=rank, world_size=world)
+    # file rendezvous (no TCP port to race for); `port` only makes the file name unique
+    dist.init_process_group("gloo", init_method="file://" + os.path.join(tmp, f"rendezvous_{port}"), rank=rank,
+                            world_size=world)
     try:
         params = [torch.zeros(s, dtype=torch.float64, requires_grad=True) for s in ((7, 3), (7, 1), (7, 16, 3))]
         _CarvedGrads.apply(float(rank + 1), *params).backward()
@@ -198,8 +200,9 @@ def _densify_worker(rank, world, port, tmp, synced):
     import densify_reference as dr
     from diff_gaussian_rasterization.view_shard import replica_checksum, update_states_sharded
 
-    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
-    dist.init_process_group("gloo", rank=rank, world_size=world)
+    # file rendezvous (no TCP port to race for); `port` only makes the file name unique
+    dist.init_process_group("gloo", init_method="file://" + os.path.join(tmp, f"rendezvous_{port}"), rank=rank,
+                            world_size=world)
     try:
         torch.manual_seed(100 + rank)  # the usual per-rank seeding
         scene = gs.make_scene(200, sh_degree=1, seed=8, radius=0.5)
