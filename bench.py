@@ -176,6 +176,7 @@ def placeholders(rep: Replica, V: int):
 
 
 COMPOSITE = os.environ.get("GSR_BENCH_COMPOSITE", "fused")  # "separate": gsr_composite_* as its own pass
+SUGAR_SEPARATE = os.environ.get("GSR_BENCH_SUGAR_SEPARATE") == "1"  # C5: two separate rasterizer passes
 SHADE_KA, SHADE_KD = (0.1, 0.1, 0.1), (0.9, 0.9, 0.9)  # the material's default ambient / diffuse colours
 
 
@@ -220,13 +221,19 @@ def render_views_sugar(rep: Replica, settings, shade):
     # pass 1 colours: SuGaRModel.get_points_rgb() = SH2RGB of the DC coefficients, passed as override_color
     # (system/sugar_static.py:117-121, geometry/sugar.py:650-660)
     colors = rep.shs[:, 0, :] * SH_C0 + 0.5
-    color, radii, depth, alpha = rasterize_views(settings, rep.means3D, m2, rep.opacities, colors_precomp=colors,
-                                                 scales=rep.scales, rotations=rep.rotations)
+    if SUGAR_SEPARATE:  # the two rasterizer calls as two view-set renders (A/B of the shared-geometry path)
+        color, radii, depth, alpha = rasterize_views(settings, rep.means3D, m2, rep.opacities, colors_precomp=colors,
+                                                     scales=rep.scales, rotations=rep.rotations)
+        zeros = [torch.zeros((P, 3), device=dev) for _ in settings]
+        normal, _, _, _ = rasterize_views(settings, rep.means3D, zeros, rep.opacities, colors_precomp=rep.normals,
+                                          scales=rep.scales, rotations=rep.rotations)
+    else:
+        # pass 2 (face normals, zero means2D) shares pass 1's geometry, sorts and blend (colors2)
+        color, radii, depth, alpha, normal = rasterize_views(settings, rep.means3D, m2, rep.opacities,
+                                                             colors_precomp=colors, scales=rep.scales,
+                                                             rotations=rep.rotations, colors2=rep.normals)
     rays_o, rays_d, _ = shade
     _, nmap_dist = depth_normal_views(depth, alpha, rays_o, rays_d)
-    zeros = [torch.zeros((P, 3), device=dev) for _ in settings]
-    normal, _, _, _ = rasterize_views(settings, rep.means3D, zeros, rep.opacities, colors_precomp=rep.normals,
-                                      scales=rep.scales, rotations=rep.rotations)
     normal = torch.nn.functional.normalize(normal, dim=1)
     normal = torch.cat([-normal[:, :2], normal[:, 2:]], 1)
     nmap = normal * 0.5 * alpha + 0.5

@@ -176,6 +176,36 @@ int gsr_set_backward(int V, int P, int degree, int M, const int* num_rendered, i
                      float* dL_dscales, float* dL_drotations, int accumulate, void* work, size_t work_bytes,
                      void* stream);
 /*
+ * Two rasterizer calls that differ only in their colours, sharing one geometry (the SuGaR normal renderer,
+ * renderer/diff_sugar_rasterizer_normal.py:157-191: the same Gaussians, camera and settings rendered with
+ * the SH / override colours, then with colors_precomp = the face normals and a zero means2D).  The second
+ * call's preprocess, sorts and binning are the first's; its blend weights too, so the forward blends both
+ * colour sets in one pass:
+ *   gsr_set_render_two_colors  as gsr_set_render (bg_images / out_render: the fused composite, both NULL
+ *                              for none) plus out_color2 (V, 3, H, W) = the blend of colors2 (P, 3) with
+ *                              the same weights and background: the second call's colour output (its
+ *                              radii / depth / alpha equal the first call's).
+ *   gsr_set_backward_colors    the second call's backward on the shared forward state: colours = colors2,
+ *                              dL_dcolor = dL/d(out_color2), no depth / alpha gradient, no SH; dL_dmeans2D
+ *                              receives the second call's screen-space gradient (the reference discards it:
+ *                              pass scratch), dL_dcolors the gradient of colors2.  With accumulate the
+ *                              parameter gradients continue the first call's (gsr_set_backward with
+ *                              dL_dcov3D as the running dL/dcov3D carry).
+ */
+int gsr_set_render_two_colors(int V, int P, const int* num_rendered, int width, int height, const float* const* bgs,
+                              void* geom, void* binning, void* image, float* out_color, float* out_depth,
+                              float* out_alpha, const float* bg_images, float* out_render, const float* colors2,
+                              float* out_color2, void* stream);
+int gsr_set_backward_colors(int V, int P, const int* num_rendered, int width, int height, const float* const* bgs,
+                            const float* means3D, const float* scales, float scale_modifier, const float* rotations,
+                            const float* cov3D_precomp, const float* const* viewmatrices,
+                            const float* const* projmatrices, const float* const* campos, const float* tanfovx,
+                            const float* tanfovy, const int* radii, const void* geom, const void* binning,
+                            const void* image, const float* colors, const float* dL_dcolor, float* dL_dmeans2D,
+                            float* dL_dcolors, float* dL_dopacity, float* dL_dmeans3D, float* dL_dcov3D,
+                            float* dL_dscales, float* dL_drotations, int accumulate, void* work, size_t work_bytes,
+                            void* stream);
+/*
  * The background renderer's composite fused into the blends (replaces gsr_set_render + gsr_composite_forward
  * and gsr_composite_backward + gsr_set_backward for renderer/diff_gaussian_rasterizer_background.py:129-132,139):
  * bg_images (V, H, W, 3) are the background network's outputs; out_render (V, 3, H, W) =

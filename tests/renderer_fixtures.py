@@ -49,7 +49,7 @@ RASTERIZE = gpu_rasterize
 
 
 def torch_rasterize_views(settings_list, means3D, means2D_list, opacities, shs=None, colors_precomp=None,
-                          scales=None, rotations=None, cov3D_precomp=None, background=None):
+                          scales=None, rotations=None, cov3D_precomp=None, background=None, colors2=None):
     """batched.rasterize_views restated as a loop over torch_rasterize (for the CPU tests)."""
     outs = [torch_rasterize(s, means3D, m2, opacities, shs=shs, colors_precomp=colors_precomp, scales=scales,
                             rotations=rotations, cov3D_precomp=cov3D_precomp)
@@ -57,7 +57,12 @@ def torch_rasterize_views(settings_list, means3D, means2D_list, opacities, shs=N
     color, radii, depth, alpha = (torch.stack([o[i] for o in outs]) for i in range(4))
     if background is not None:
         color = (color + (1 - alpha) * background.permute(0, 3, 1, 2)).clamp(0, 1)
-    return color, radii, depth, alpha
+    if colors2 is None:
+        return color, radii, depth, alpha
+    second = [torch_rasterize(s, means3D, torch.zeros_like(m2), opacities, colors_precomp=colors2, scales=scales,
+                              rotations=rotations, cov3D_precomp=cov3D_precomp)[0]
+              for s, m2 in zip(settings_list, means2D_list)]
+    return color, radii, depth, alpha, torch.stack(second)
 
 
 class FakeGeometry:

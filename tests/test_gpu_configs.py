@@ -321,10 +321,9 @@ def test_c5_sugar_normal_renderer():
              opacities=leaf(scene["opacities"]), colors=leaf(colors), normals=leaf(normals))
     s = _settings(cam, [0.0, 0.0, 0.0], 0)
     m2 = torch.zeros((P, 3), device=dev, requires_grad=True)
-    c, r, d, a = rasterize_views([s], t["means3D"], [m2], t["opacities"], colors_precomp=t["colors"],
-                                 scales=t["scales"], rotations=t["rotations"])
-    nrm, _, _, _ = rasterize_views([s], t["means3D"], [torch.zeros((P, 3), device=dev)], t["opacities"],
-                                   colors_precomp=t["normals"], scales=t["scales"], rotations=t["rotations"])
+    # both rasterizer calls from one geometry / sort / blend (colors2 = the second call's colours)
+    c, r, d, a, nrm = rasterize_views([s], t["means3D"], [m2], t["opacities"], colors_precomp=t["colors"],
+                                      scales=t["scales"], rotations=t["rotations"], colors2=t["normals"])
     ro, rd = rays_o.to(dev), rays_d.to(dev)
     out = _sugar_epilogue(torch, c[0], d[0], a[0], nrm[0], ro, rd, lambda dd, aa: depth_normal_views(dd, aa, ro, rd))
     loss_of(out, lambda x: torch.tensor(x, device=dev)).backward()
@@ -370,3 +369,48 @@ def test_c5_sugar_normal_renderer():
     check_grads(gpu_grads, dict(b32=grads["f32"], b64=grads["f64"]),
                 ["means3D", "means2D", "opacity", "colors", "normals", "scales", "rotations"], "C5")
     check_radii(gpu_pass1["radii"], ref1, "C5 pass 1")
+
+
+def test_second_colors_match_separate_call():
+    """rasterize_views(colors2=...) — the SuGaR normal renderer's second rasterizer call from the first's
+    geometry, sorts and blend — against the two separate calls (renderer/diff_sugar_rasterizer_normal.py:
+    157-191): the second colour image bitwise equal, the first call's outputs and means2D gradient bitwise
+    equal, parameter gradients (summed over both calls) within 1e-5 relative, colors2's gradient equal."""
+    import torch
+
+    from diff_gaussian_rasterization.batched import rasterize_views
+
+    scene = gs.make_scene(15_000, sh_degree=1, seed=44)
+    rng = np.random.default_rng(4)
+    n = rng.normal(size=(15_000, 3)).astype(np.float32)
+    normals = n / np.linalg.norm(n, axis=1, keepdims=True)
+    cams = [make_camera(144, 112, elevation=10.0 * i, azimuth=70.0 * i) for i in range(3)]
+    ups = [torch.tensor(rng.standard_normal((3, 3, 112, 144)).astype(np.float32), device="cuda") for _ in range(3)]
+    dev = "cuda"
+
+    def run(fused):
+        t = {k: torch.tensor(scene[k], device=dev, requires_grad=True)
+             for k in ("means3D", "scales", "rotations", "opacities", "shs")}
+        t["normals"] = torch.tensor(normals, device=dev, requires_grad=True)
+        st = [_settings(c, [0.2, 0.4, 0.6], 1) for c in cams]
+        m2 = [torch.zeros((15_000, 3), device=dev, requires_grad=True) for _ in cams]
+        common = dict(opacities=t["opacities"], scales=t["scales"], rotations=t["rotations"])
+        if fused:
+            c, r, d, a, c2 = rasterize_views(st, t["means3D"], m2, shs=t["shs"], colors2=t["normals"], **common)
+        else:
+            c, r, d, a = rasterize_views(st, t["means3D"], m2, shs=t["shs"], **common)
+            z = [torch.zeros((15_000, 3), device=dev) for _ in cams]
+            c2, _, _, _ = rasterize_views(st, t["means3D"], z, colors_precomp=t["normals"], **common)
+        ((c * ups[0]).sum() + (d * ups[1][:, :1]).sum() + (a * ups[1][:, 1:2]).sum() + (c2 * ups[2]).sum()).backward()
+        return dict(c=c.detach(), c2=c2.detach(), d=d.detach(), a=a.detach(), r=r,
+                    m2=[m.grad.clone() for m in m2], g={k: v.grad.clone() for k, v in t.items()})
+
+    f, s_ = run(True), run(False)
+    for k in ("c", "c2", "d", "a", "r"):
+        assert torch.equal(f[k], s_[k]), k
+    for v in range(3):
+        assert torch.equal(f["m2"][v], s_["m2"][v])
+    for k in f["g"]:
+        ref = s_["g"][k].double()
+        err = float(((f["g"][k].double() - ref).abs() / ref.abs().clamp(min=1.0)).max())
+        assert err <= 1e-5, f"grad {k}: {err}"

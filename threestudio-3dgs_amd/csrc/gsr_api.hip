@@ -398,7 +398,8 @@ int gsr_set_num_rendered(int V, const void* geom, int P, int* num_rendered, int*
 
 static int set_render(int V, int P, const int* K, int width, int height, const float* const* bgs, void* geom,
                       void* binning, void* image, float* out_color, float* out_depth, float* out_alpha,
-                      const float* comp_bg, float* out_render, void* stream) {
+                      const float* comp_bg, float* out_render, void* stream, const float* colors2 = nullptr,
+                      float* out_color2 = nullptr) {
   if (check_set(V, P) != GSR_OK) return GSR_EINVAL;
   if (width <= 0 || height <= 0) return fail(GSR_EINVAL, "%s", "bad sizes");
   if (K == nullptr || bgs == nullptr || geom == nullptr || binning == nullptr || image == nullptr ||
@@ -432,6 +433,8 @@ static int set_render(int V, int P, const int* K, int width, int height, const f
     rs.comp = out_render;
     rs.ccolor = nullptr;
     rs.dcbg = nullptr;
+    rs.col2 = colors2;
+    rs.out_col2 = out_color2;
     rs.V = V;
     rs.v0 = 0;
     rs.P = P;
@@ -465,6 +468,16 @@ int gsr_set_render_composite(int V, int P, const int* K, int width, int height, 
                     out_render, stream);
 }
 
+int gsr_set_render_two_colors(int V, int P, const int* K, int width, int height, const float* const* bgs,
+                              void* geom, void* binning, void* image, float* out_color, float* out_depth,
+                              float* out_alpha, const float* bg_images, float* out_render, const float* colors2,
+                              float* out_color2, void* stream) {
+  if (colors2 == nullptr || out_color2 == nullptr) return fail(GSR_EINVAL, "%s", "null second colour argument");
+  if ((bg_images == nullptr) != (out_render == nullptr)) return fail(GSR_EINVAL, "%s", "composite needs both images");
+  return set_render(V, P, K, width, height, bgs, geom, binning, image, out_color, out_depth, out_alpha, bg_images,
+                    out_render, stream, colors2, out_color2);
+}
+
 static int set_backward(int V, int P, int degree, int M, const int* K, int width, int height, const float* const* bgs,
                         const float* means3D, const float* scales, float scale_modifier, const float* rotations,
                         const float* shs, const float* cov3D_precomp, const float* const* viewmatrices,
@@ -474,7 +487,7 @@ static int set_backward(int V, int P, int degree, int M, const int* K, int width
                         float* dL_dmeans2D, float* dL_dcolors, float* dL_dopacity, float* dL_dmeans3D,
                         float* dL_dcov3D, float* dL_dsh, float* dL_dscales, float* dL_drotations, int accumulate,
                         void* work, size_t work_bytes, const float* comp_bg, const float* color, float* dL_dbg,
-                        void* stream) {
+                        void* stream, const float* colors_override = nullptr) {
   if (check_set(V, P) != GSR_OK) return GSR_EINVAL;
   if (width <= 0 || height <= 0) return fail(GSR_EINVAL, "%s", "bad sizes");
   if (P == 0) return last_launch();
@@ -524,6 +537,8 @@ static int set_backward(int V, int P, int degree, int M, const int* K, int width
     rs.comp = nullptr;
     rs.ccolor = color ? color + (size_t)g0 * 3 * HW : nullptr;
     rs.dcbg = dL_dbg ? dL_dbg + (size_t)g0 * HW * 3 : nullptr;
+    rs.col2 = colors_override;
+    rs.out_col2 = nullptr;
     rs.V = g1 - g0;
     rs.v0 = g0;
     rs.P = P;
@@ -629,6 +644,22 @@ size_t gsr_binning_bytes(int K, int width, int height) {
   return b;
 }
 size_t gsr_image_bytes(int width, int height) { return gsr_set_image_bytes(1, width, height); }
+int gsr_set_backward_colors(int V, int P, const int* K, int width, int height, const float* const* bgs,
+                            const float* means3D, const float* scales, float scale_modifier, const float* rotations,
+                            const float* cov3D_precomp, const float* const* viewmatrices,
+                            const float* const* projmatrices, const float* const* campos, const float* tanfovx,
+                            const float* tanfovy, const int* radii, const void* geom, const void* binning,
+                            const void* image, const float* colors, const float* dL_dcolor, float* dL_dmeans2D,
+                            float* dL_dcolors, float* dL_dopacity, float* dL_dmeans3D, float* dL_dcov3D,
+                            float* dL_dscales, float* dL_drotations, int accumulate, void* work, size_t work_bytes,
+                            void* stream) {
+  if (colors == nullptr) return fail(GSR_EINVAL, "%s", "null colours");
+  return set_backward(V, P, 0, 0, K, width, height, bgs, means3D, scales, scale_modifier, rotations, nullptr,
+                      cov3D_precomp, viewmatrices, projmatrices, campos, tanfovx, tanfovy, radii, geom, binning, image,
+                      dL_dcolor, nullptr, nullptr, dL_dmeans2D, dL_dcolors, dL_dopacity, dL_dmeans3D, dL_dcov3D, nullptr,
+                      dL_dscales, dL_drotations, accumulate, work, work_bytes, nullptr, nullptr, nullptr, stream, colors);
+}
+
 size_t gsr_backward_bytes(int P, int K) { return gsr_set_backward_bytes(1, P, &K); }
 
 int gsr_forward_preprocess(int P, int degree, int M, const float* means3D, const float* scales,

@@ -50,6 +50,12 @@ struct RenderSet {
   float* comp;       // forward: clamp(color + (1 - alpha) bg, 0, 1) (V, 3, H, W)
   const float* ccolor;  // backward: the forward's colour (V, 3, H, W); dL_dcolor then holds dL/dcomp
   float* dcbg;       // backward: dL/dbg (V, H, W, 3) or null
+  // a second colour per Gaussian blended with the same weights (the SuGaR normal renderer's second
+  // rasterizer call, renderer/diff_sugar_rasterizer_normal.py:182-191: same geometry, colors_precomp =
+  // the face normals), (P, 3); null = off.  Forward: blended into out_col2 (V, 3, H, W) beside the
+  // first colour.  Backward: replaces the records' colour (the second call's backward).
+  const float* col2;
+  float* out_col2;
 };
 void launch_render_forward(const RenderSet& rs, const GeomState& g, const uint32_t* sorted_gauss,
                            const ImageState& img, float* out_color, float* out_depth, float* out_alpha,

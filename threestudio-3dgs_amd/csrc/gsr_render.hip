@@ -112,6 +112,7 @@ __device__ __forceinline__ bool quadrant_hit(const float4 r0, const float4 r1, f
 // Gaussians whose alpha >= 1/255 ellipse can reach its quadrant, and blends them with a
 // branch-free predicated body.  No workgroup barriers couple quadrants that terminate at
 // different depths, and 4x more independent waves balance the load across the 256 CUs.
+template <bool C2>
 __global__ __launch_bounds__(64) void k_render_fwd(RenderSet rs,
                                                    const uint2* __restrict__ ranges,
                                                    const uint32_t* __restrict__ sorted_gauss,
@@ -124,6 +125,7 @@ __global__ __launch_bounds__(64) void k_render_fwd(RenderSet rs,
                                                    uint32_t* __restrict__ quad_maxc) {
   // 65 slots: the loop reads candidate k+1 while blending k (slot 64 is never used)
   __shared__ float4 s0[65], s1[65], s2[65];
+  __shared__ float4 s3[C2 ? 65 : 1];  // the second colour (C2)
   const int U = unit_grid(rs.gx, rs.gy);
   const int v = blockIdx.x / U;
   int tile, q;
@@ -155,6 +157,7 @@ __global__ __launch_bounds__(64) void k_render_fwd(RenderSet rs,
 
   bool done = !inside;
   float T = 1.0f, Cr = 0.f, Cg = 0.f, Cb = 0.f, D = 0.f;
+  float Er = 0.f, Eg = 0.f, Eb = 0.f;  // second colour (C2)
   uint32_t last_contributor = 0;
 #ifdef GSR_TIMELINE
   unsigned long long pc_eval = 0, pc_slot = 0;
@@ -162,23 +165,26 @@ __global__ __launch_bounds__(64) void k_render_fwd(RenderSet rs,
   // two-stage prefetch (as in the backward): indices two batches ahead, records one batch ahead
   const uint32_t gmask = rs.gmask;
   const float4 zero4 = make_float4(0.f, 0.f, 0.f, 0.f);
-  float4 n0 = zero4, n1 = zero4, n2 = zero4;
+  float4 n0 = zero4, n1 = zero4, n2 = zero4, n3 = zero4;
   uint32_t gi_next = 0u;
+  const float* col2 = rs.col2;
   if (lane < n) {
     const uint32_t g0 = sorted_gauss[range.x + lane] & gmask;
     n0 = rec[g0].a;
     n1 = rec[g0].b;
     n2 = rec[g0].c;
+    if (C2) n3 = make_float4(col2[3 * g0], col2[3 * g0 + 1], col2[3 * g0 + 2], 0.f);
   }
   if (64 + lane < n) gi_next = sorted_gauss[range.x + 64 + lane] & gmask;
   for (int base = 0; base < n; base += 64) {
     if (__all(done)) break;
     const int i = base + lane;
-    const float4 r0 = n0, r1 = n1, r2 = n2;
+    const float4 r0 = n0, r1 = n1, r2 = n2, r3 = n3;
     if (base + 64 + lane < n) {
       n0 = rec[gi_next].a;
       n1 = rec[gi_next].b;
       n2 = rec[gi_next].c;
+      if (C2) n3 = make_float4(col2[3 * gi_next], col2[3 * gi_next + 1], col2[3 * gi_next + 2], 0.f);
     }
     if (base + 128 + lane < n) gi_next = sorted_gauss[range.x + base + 128 + lane] & gmask;
     bool keep = false;
@@ -191,12 +197,14 @@ __global__ __launch_bounds__(64) void k_render_fwd(RenderSet rs,
       s0[pos] = make_float4(r0.x, r0.y, GSR_CONIC_K_AC * r0.z, GSR_CONIC_K_B * r0.w);
       s1[pos] = make_float4(GSR_CONIC_K_AC * r1.x, r1.y, r1.z, __uint_as_float((uint32_t)(i + 1)));
       s2[pos] = r2;
+      if (C2) s3[pos] = r3;
     }
     __syncthreads();
-    float4 a = s0[0], b = s1[0], c = s2[0];
+    float4 a = s0[0], b = s1[0], c = s2[0], e = C2 ? s3[0] : zero4;
     for (int k = 0; k < cnt; ++k) {
       if ((k & 7) == 0 && __all(done)) break;
       const float4 an = s0[k + 1], bn = s1[k + 1], cn = s2[k + 1];
+      const float4 en = C2 ? s3[k + 1] : zero4;
       const float dx = a.x - pxf, dy = a.y - pyf;
       const float power2 = gauss_power2(a.z, a.w, b.x, dx, dy);  // log2(e) * power
       const float alpha = fminf(GSR_ALPHA_MAX, b.y * __builtin_amdgcn_exp2f(power2));
@@ -215,12 +223,18 @@ __global__ __launch_bounds__(64) void k_render_fwd(RenderSet rs,
       Cg = fmaf(c.y, aT, Cg);
       Cb = fmaf(c.z, aT, Cb);
       D = fmaf(b.z, aT, D);
+      if (C2) {
+        Er = fmaf(e.x, aT, Er);
+        Eg = fmaf(e.y, aT, Eg);
+        Eb = fmaf(e.z, aT, Eb);
+      }
       T = blend ? test_T : T;  // = T (1 - a_eff)
       last_contributor = blend ? __float_as_uint(b.w) : last_contributor;
       done = done || term;
       a = an;
       b = bn;
       c = cn;
+      e = en;
     }
     __syncthreads();
   }
@@ -234,6 +248,12 @@ __global__ __launch_bounds__(64) void k_render_fwd(RenderSet rs,
     out_color[2 * HW + pid] = Cb + T * bg[2];
     out_depth[pid] = D;
     out_alpha[pid] = 1.0f - T;
+    if (C2) {
+      float* o2 = rs.out_col2 + (size_t)(rs.v0 + v) * 3 * HW + pid;
+      o2[0] = Er + T * bg[0];
+      o2[HW] = Eg + T * bg[1];
+      o2[2 * HW] = Eb + T * bg[2];
+    }
     if (rs.cbg != nullptr) {
       // fused composite, the same operations as the torch epilogue on the stored outputs (bit-identical)
 #pragma clang fp contract(off)
@@ -297,9 +317,14 @@ void launch_render_forward(const RenderSet& rs, const GeomState& g, const uint32
                            hipStream_t stream) {
   const int nt = rs.gx * rs.gy;
   if (nt <= 0 || rs.V <= 0) return;
-  hipLaunchKernelGGL(k_render_fwd, dim3(rs.V * unit_grid(rs.gx, rs.gy)), dim3(64), 0, stream, rs,
-                     (const uint2*)img.ranges, sorted_gauss, (const GaussRec*)g.rec, out_color, out_depth, out_alpha,
-                     img.final_T, img.n_contrib, img.quad_maxc);
+  if (rs.col2 != nullptr)
+    hipLaunchKernelGGL(k_render_fwd<true>, dim3(rs.V * unit_grid(rs.gx, rs.gy)), dim3(64), 0, stream, rs,
+                       (const uint2*)img.ranges, sorted_gauss, (const GaussRec*)g.rec, out_color, out_depth,
+                       out_alpha, img.final_T, img.n_contrib, img.quad_maxc);
+  else
+    hipLaunchKernelGGL(k_render_fwd<false>, dim3(rs.V * unit_grid(rs.gx, rs.gy)), dim3(64), 0, stream, rs,
+                       (const uint2*)img.ranges, sorted_gauss, (const GaussRec*)g.rec, out_color, out_depth,
+                       out_alpha, img.final_T, img.n_contrib, img.quad_maxc);
   hipLaunchKernelGGL(k_tile_info, dim3(rs.V * div_up(nt, 256)), dim3(256), 0, stream, rs,
                      (const uint2*)img.ranges, (const uint32_t*)img.quad_maxc, sorted_gauss,
                      (const GaussRec*)g.rec, img.tile_info, img.cut);
@@ -463,6 +488,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5, 8))) voi
     const uint32_t g0 = fetch_index(maxc);
     if (maxc - 1 - cs >= 0) {
       npc = reinterpret_cast<const float4*>(rec + g0)[piece];
+      if (piece == 2 && rs.col2 != nullptr)  // the second rasterizer call's colours
+        npc = make_float4(rs.col2[3 * g0], rs.col2[3 * g0 + 1], rs.col2[3 * g0 + 2], 0.f);
       if (piece == 3) ngo = goff[g0];
     }
     if (maxc > 64) gi_next = fetch_index(maxc - 64);
@@ -573,6 +600,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5, 8))) voi
       if (hi > 64) {
         if (hi - 65 - cs >= 0) {
           npc = reinterpret_cast<const float4*>(rec + gi_next)[piece];
+          if (piece == 2 && rs.col2 != nullptr)
+            npc = make_float4(rs.col2[3 * gi_next], rs.col2[3 * gi_next + 1], rs.col2[3 * gi_next + 2], 0.f);
           if (piece == 3) ngo = goff[gi_next];
         }
         if (hi > 128) gi_next = fetch_index(hi - 128);

@@ -83,6 +83,13 @@ SIGNATURES = {
         + [ctypes.POINTER(_vp)] * 3 + [ctypes.POINTER(_f)] * 2 + [_vp] * 4 + [_vp] * 6 + [_vp] * 8
         + [_i, _vp, _sz, _vp],
     ),
+    "gsr_set_render_two_colors": (_i, [_i, _i, ctypes.POINTER(_i), _i, _i, ctypes.POINTER(_vp)] + [_vp] * 11),
+    "gsr_set_backward_colors": (
+        _i,
+        [_i, _i, ctypes.POINTER(_i), _i, _i, ctypes.POINTER(_vp), _vp, _vp, _f, _vp, _vp]
+        + [ctypes.POINTER(_vp)] * 3 + [ctypes.POINTER(_f)] * 2 + [_vp] * 4 + [_vp] * 2 + [_vp] * 7
+        + [_i, _vp, _sz, _vp],
+    ),
     "gsr_profile_enable": (_i, [_i]),
     "gsr_profile_read": (_i, [ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_longlong), _i]),
 }

@@ -203,14 +203,14 @@ def render_views_local(renderer, batch: dict, mode: str, lo: int, hi: int) -> di
                        comp_rgb_bg=bg_img.reshape(n, H, W, 3))
         elif mode == "sugar_normal":
             settings = _settings(pc, cams, _inverted_bgs(renderer, n), H, W, scaling_modifier)
-            color, radii, depth, alpha = _rasterize_views(settings, means3D, m2, shs=shs, colors_precomp=override,
-                                                          **common)
+            # both rasterizer calls of the renderer (:157-166 colours, :182-191 face normals with a zero
+            # means2D) from one geometry, sort and blend: the normals are the second colour set
+            color, radii, depth, alpha, normal = _rasterize_views(settings, means3D, m2, shs=shs,
+                                                                  colors_precomp=override,
+                                                                  colors2=pc.get_gs_normals, **common)
             if batch.get("compute_normal_from_dist", True):
                 _, nmap_dist = _depth_normal_views(depth, alpha, batch["rays_o"][lo:hi], batch["rays_d"][lo:hi])
                 out["comp_normal_from_dist"] = nmap_dist
-            zeros = [torch.zeros_like(m) for m in m2]
-            normal, _, _, _ = _rasterize_views(settings, means3D, zeros, shs=None, colors_precomp=pc.get_gs_normals,
-                                               **common)
             normal = torch.nn.functional.normalize(normal, dim=1)
             normal = torch.cat([-normal[:, :2], normal[:, 2:]], 1)  # p3d -> threestudio axes (:193)
             nmap = normal * 0.5 * alpha + 0.5

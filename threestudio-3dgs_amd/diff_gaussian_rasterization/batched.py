@@ -56,7 +56,7 @@ class _ViewSet:
 class _RasterizeViews(torch.autograd.Function):
     @staticmethod
     def forward(ctx, settings_list, means3D, sh, colors_precomp, opacities, scales, rotations, cov3D_precomp,
-                composite_bg, *means2D):
+                composite_bg, colors2, *means2D):
         lib = _C.load_library()
         V = len(settings_list)
         dev = means3D.device
@@ -83,6 +83,12 @@ class _RasterizeViews(torch.autograd.Function):
             render = torch.empty((V, 3, H, W), **fopt)
         depth = torch.empty((V, 1, H, W), **fopt)
         alpha = torch.empty((V, 1, H, W), **fopt)
+        c2 = None
+        if colors2 is not None:
+            c2 = _C._f32(colors2, "colors2", dev)
+            if c2.numel() != 3 * P:
+                raise _C.GSRError(f"colors2 has {c2.numel()} elements, expected {3 * P}")
+            color2 = torch.empty((V, 3, H, W), **fopt)
         radii = torch.empty((V, P), dtype=torch.int32, device=dev)
         sets = []
         for lo in range(0, V, SET_MAX):
@@ -109,7 +115,12 @@ class _RasterizeViews(torch.autograd.Function):
             vs.binning = torch.empty(int(lib.gsr_set_binning_bytes(vs.V, P, Karr, W, H)), dtype=torch.uint8, device=dev)
             vs.image = torch.empty(int(lib.gsr_set_image_bytes(vs.V, W, H)), dtype=torch.uint8, device=dev)
             sl = slice(vs.lo, vs.hi)
-            if cbg is None:
+            if c2 is not None:
+                _C._check(lib.gsr_set_render_two_colors(
+                    vs.V, P, Karr, W, H, _ptrs([c[3] for c in vs.cams]), p(vs.geom), p(vs.binning), p(vs.image),
+                    p(color[sl]), p(depth[sl]), p(alpha[sl]), p(cbg[sl]) if cbg is not None else None,
+                    p(render[sl]) if cbg is not None else None, p(c2), p(color2[sl]), stream))
+            elif cbg is None:
                 _C._check(lib.gsr_set_render(vs.V, P, Karr, W, H, _ptrs([c[3] for c in vs.cams]), p(vs.geom),
                                              p(vs.binning), p(vs.image), p(color[sl]), p(depth[sl]), p(alpha[sl]),
                                              stream))
@@ -120,14 +131,17 @@ class _RasterizeViews(torch.autograd.Function):
         ctx.settings = settings_list
         ctx.sets = sets
         ctx.bg_shape = tuple(composite_bg.shape) if composite_bg is not None else None
-        ctx.save_for_backward(m3, shc, col, sc, rot, c3, radii, cbg, color if cbg is not None else None)
+        ctx.save_for_backward(m3, shc, col, sc, rot, c3, radii, cbg, color if cbg is not None else None, c2)
         ctx.mark_non_differentiable(radii)
+        if c2 is not None:
+            return (color if cbg is None else render), radii, depth, alpha, color2
         return (color if cbg is None else render), radii, depth, alpha
 
     @staticmethod
-    def backward(ctx, g_color, _g_radii, g_depth, g_alpha):
+    def backward(ctx, g_color, _g_radii, g_depth, g_alpha, g_color2=None):
         lib = _C.load_library()
-        m3, shc, col, sc, rot, c3, radii, cbg, color = ctx.saved_tensors
+        m3, shc, col, sc, rot, c3, radii, cbg, color, c2 = ctx.saved_tensors
+        second = c2 is not None and g_color2 is not None
         settings = ctx.settings
         V = len(settings)
         s0 = settings[0]
@@ -156,13 +170,14 @@ class _RasterizeViews(torch.autograd.Function):
         d_bg = torch.empty_like(cbg) if cbg is not None and ctx.needs_input_grad[8] else None
         # more than one view set in the scale / rotation path: the running dL/dcov3D the later sets
         # continue from (include/gsr.h gsr_set_backward, accumulate)
-        if d_c3 is None and len(ctx.sets) > 1:
+        d_c2 = torch.zeros((P, 3), **fopt) if second else None
+        if d_c3 is None and (len(ctx.sets) > 1 or second):
             d_c3 = torch.empty((P, 6), **fopt)
             ctx.needs_c3_scratch = True
         if P == 0:
             if d_bg is not None:
                 d_bg.zero_()
-            for t in (d_m2, d_m3, d_op, d_col, d_sh, d_c3, d_sc, d_rot):
+            for t in (d_m2, d_m3, d_op, d_col, d_sh, d_c3, d_sc, d_rot, d_c2):
                 if t is not None:
                     t.zero_()
         else:
@@ -194,11 +209,21 @@ class _RasterizeViews(torch.autograd.Function):
                         p(vs.geom), p(vs.binning), p(vs.image), p(cbg[sl]), p(color[sl]), p(gc[sl]), gdp, gap,
                         p(d_bg[sl]) if d_bg is not None else None, p(d_m2[sl]), p(d_col), p(d_op), p(d_m3), p(d_c3),
                         p(d_sh), p(d_sc), p(d_rot), 1 if si > 0 else 0, p(work), work.numel(), stream))
+                if second:
+                    # the second call's backward on the shared forward state (its screen-space gradient
+                    # is discarded, as the reference's fresh zero means2D of that call is)
+                    g2 = g_color2.float().contiguous()
+                    m2_scratch = torch.empty((vs.V, P, 3), **fopt)
+                    _C._check(lib.gsr_set_backward_colors(
+                        vs.V, P, Karr, W, H, _ptrs([c[3] for c in vs.cams]), p(m3), p(sc), float(s0.scale_modifier),
+                        p(rot), p(c3), views, projs, campos, tx, ty, p(radii[sl]), p(vs.geom), p(vs.binning),
+                        p(vs.image), p(c2), p(g2[sl]), p(m2_scratch), p(d_c2), p(d_op), p(d_m3), p(d_c3), p(d_sc),
+                        p(d_rot), 1, p(work), work.numel(), stream))
         if d_bg is not None:
             d_bg = d_bg.reshape(ctx.bg_shape)
         if getattr(ctx, "needs_c3_scratch", False):
             d_c3 = None
-        grads = [None, d_m3, d_sh, d_col, d_op, d_sc, d_rot, d_c3, d_bg] + [d_m2[v] for v in range(V)]
+        grads = [None, d_m3, d_sh, d_col, d_op, d_sc, d_rot, d_c3, d_bg, d_c2] + [d_m2[v] for v in range(V)]
         for k, need in enumerate(ctx.needs_input_grad):
             if not need:
                 grads[k] = None
@@ -206,7 +231,7 @@ class _RasterizeViews(torch.autograd.Function):
 
 
 def rasterize_views(settings_list, means3D, means2D_list, opacities, shs=None, colors_precomp=None, scales=None,
-                    rotations=None, cov3D_precomp=None, background=None):
+                    rotations=None, cov3D_precomp=None, background=None, colors2=None):
     """Render V views of one set of Gaussians.  settings_list: V GaussianRasterizationSettings (same image
     size, same sh_degree, scale_modifier and prefiltered flag); means2D_list: V screen-space placeholders
     (P, 3) whose .grad receives each view's viewspace gradient.  Returns (color (V,3,H,W), radii (V,P),
@@ -215,7 +240,14 @@ def rasterize_views(settings_list, means3D, means2D_list, opacities, shs=None, c
     background: the background renderer's composite fused into the blends — the background network's
     images (V, H, W, 3) (renderer/diff_gaussian_rasterizer_background.py:116,129-132,139); the first
     output is then render = clamp(color + (1 - alpha) * background, 0, 1) (bit-identical to the torch
-    expression, same gradients incl. the background's) instead of color."""
+    expression, same gradients incl. the background's) instead of color.
+
+    colors2 (P, 3): a second rasterizer call that differs only in its colours — the SuGaR normal renderer's
+    ``rasterizer(..., means2D=zeros_like(means2D), shs=None, colors_precomp=pc.get_gs_normals, ...)``
+    (renderer/diff_sugar_rasterizer_normal.py:182-191) — rendered from the same geometry, sorts and blend
+    weights (include/gsr.h gsr_set_render_two_colors); a fifth output holds its colour image (V, 3, H, W).
+    Its backward adds that call's parameter gradients (colors2 receives its colour gradient); its
+    screen-space gradient is not added to means2D, as in the reference."""
     if (shs is None) == (colors_precomp is None):
         raise Exception("Please provide excatly one of either SHs or precomputed colors!")
     if ((scales is None or rotations is None) and cov3D_precomp is None) or (
@@ -234,4 +266,4 @@ def rasterize_views(settings_list, means3D, means2D_list, opacities, shs=None, c
         if background.numel() != len(settings_list) * H * W * 3:
             raise ValueError("background must hold (V, H, W, 3) values")
     return _RasterizeViews.apply(list(settings_list), means3D, shs, colors_precomp, opacities, scales, rotations,
-                                 cov3D_precomp, background, *means2D_list)
+                                 cov3D_precomp, background, colors2, *means2D_list)
