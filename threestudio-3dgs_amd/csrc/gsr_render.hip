@@ -243,18 +243,22 @@ __global__ __launch_bounds__(64) void k_render_fwd(RenderSet rs,
     const size_t HW = (size_t)H * W;
     final_T[pid] = T;
     n_contrib[pid] = last_contributor;
-    // C + T bg as a rounded product then a rounded sum (the oracle's order, and the same value the fused
-    // composite below starts from), whatever the surrounding code lets the compiler contract
-    out_color[pid] = __fadd_rn(Cr, __fmul_rn(T, bg[0]));
-    out_color[HW + pid] = __fadd_rn(Cg, __fmul_rn(T, bg[1]));
-    out_color[2 * HW + pid] = __fadd_rn(Cb, __fmul_rn(T, bg[2]));
+    {
+      // C + T bg as a rounded product then a rounded sum (the oracle's order, and the same value the fused
+      // composite below starts from), never contracted: every instantiation stores the same bits
+#pragma clang fp contract(off)
+      out_color[pid] = Cr + T * bg[0];
+      out_color[HW + pid] = Cg + T * bg[1];
+      out_color[2 * HW + pid] = Cb + T * bg[2];
+    }
     out_depth[pid] = D;
     out_alpha[pid] = 1.0f - T;
     if (C2) {
+#pragma clang fp contract(off)
       float* o2 = rs.out_col2 + (size_t)(rs.v0 + v) * 3 * HW + pid;
-      o2[0] = __fadd_rn(Er, __fmul_rn(T, bg[0]));
-      o2[HW] = __fadd_rn(Eg, __fmul_rn(T, bg[1]));
-      o2[2 * HW] = __fadd_rn(Eb, __fmul_rn(T, bg[2]));
+      o2[0] = Er + T * bg[0];
+      o2[HW] = Eg + T * bg[1];
+      o2[2 * HW] = Eb + T * bg[2];
     }
     if (rs.cbg != nullptr) {
       // fused composite, the same operations as the torch epilogue on the stored outputs (bit-identical)
