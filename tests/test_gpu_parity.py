@@ -251,3 +251,53 @@ def test_batched_views_match_per_view(nviews):
         scale = max(1.0, float(ref.abs().max()))
         err = float((v.grad - ref).abs().max())
         assert err <= 1e-5 * scale, f"{k}: {err} vs scale {scale}"
+
+
+@pytest.mark.parametrize("kind", ["ball_composite", "sugar_two_colors"])
+def test_forward_kernels_bitwise(kind, monkeypatch):
+    """The one-wave-per-tile forward (default) and the quadrant-wave forward (GSR_FWD_KERNEL=quadrant)
+    blend exactly the same candidates per pixel in the same order: every output — colour, depth, alpha,
+    the composite, the second colour set, radii — and every gradient (the backward reads the forward's
+    per-pixel state) must be bitwise equal."""
+    import torch
+
+    from diff_gaussian_rasterization.batched import rasterize_views
+
+    dev = "cuda"
+    if kind == "ball_composite":
+        scene = gs.make_scene(40_000, sh_degree=3, seed=51)
+        W_, H_ = 200, 168  # ragged: partial tiles and quadrants at the edges
+    else:
+        scene = gs.make_sugar_scene(5, sh_degree=0, seed=3)
+        W_, H_ = 256, 256
+    rng = np.random.default_rng(8)
+    cams = [make_camera(W_, H_, elevation=12.0 * i, azimuth=55.0 * i + 5.0) for i in range(3)]
+    ups = [torch.tensor(rng.standard_normal((3, 3, H_, W_)).astype(np.float32), device=dev) for _ in range(3)]
+    bgimg = torch.tensor(rng.random((3, H_, W_, 3)).astype(np.float32), device=dev)
+
+    def run(kernel):
+        monkeypatch.setenv("GSR_FWD_KERNEL", kernel)
+        from test_gpu_configs import _settings
+
+        P = scene["means3D"].shape[0]
+        t = {k: torch.tensor(scene[k], device=dev, requires_grad=True)
+             for k in ("means3D", "scales", "rotations", "opacities", "shs")}
+        m2 = [torch.zeros((P, 3), device=dev, requires_grad=True) for _ in cams]
+        st = [_settings(c, [0.1, 0.2, 0.3], int(scene["sh_degree"])) for c in cams]
+        common = dict(opacities=t["opacities"], scales=t["scales"], rotations=t["rotations"])
+        if kind == "ball_composite":
+            outs = rasterize_views(st, t["means3D"], m2, shs=t["shs"], background=bgimg, **common)
+        else:
+            t["normals"] = torch.tensor(scene["normals"], device=dev, requires_grad=True)
+            outs = rasterize_views(st, t["means3D"], m2, shs=t["shs"], colors2=t["normals"], **common)
+        c, r, d, a = outs[:4]
+        loss = (c * ups[0]).sum() + (d * ups[1][:, :1]).sum() + (a * ups[1][:, 1:2]).sum()
+        if len(outs) > 4:
+            loss = loss + (outs[4] * ups[2]).sum()
+        loss.backward()
+        res = [x.detach().clone() for x in outs] + [m.grad.clone() for m in m2]
+        return res + [v.grad.clone() for v in t.values()]
+
+    tile, quad = run("tile"), run("quadrant")
+    for i, (x, y) in enumerate(zip(tile, quad)):
+        assert torch.equal(x, y), f"output {i} differs: {float((x.double() - y.double()).abs().max())}"

@@ -449,7 +449,8 @@ static int set_render(int V, int P, const int* K, int width, int height, const f
       rs.row_start[v] = 0;
       rs.bg[v] = bgs[v];
     }
-    launch_render_forward(rs, g, tp.packed ? b.key[tres] : b.val[tres], img, out_color, out_depth, out_alpha, s);
+    launch_render_forward(rs, g, tp.packed ? b.key[tres] : b.val[tres], img, out_color, out_depth, out_alpha, total,
+                          s);
   }
   return last_launch();
 }

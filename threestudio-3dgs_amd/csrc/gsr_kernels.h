@@ -57,9 +57,10 @@ struct RenderSet {
   const float* col2;
   float* out_col2;
 };
+// instances: the set's rectangle tiles (sum of K) — picks the forward kernel (gsr_render.hip)
 void launch_render_forward(const RenderSet& rs, const GeomState& g, const uint32_t* sorted_gauss,
                            const ImageState& img, float* out_color, float* out_depth, float* out_alpha,
-                           hipStream_t stream);
+                           long long instances, hipStream_t stream);
 // dL_d* point at view v0's planes.
 void launch_render_backward(const RenderSet& rs, const GeomState& g, const uint32_t* sorted_gauss,
                             const ImageState& img, const float* dL_dcolor, const float* dL_ddepth,

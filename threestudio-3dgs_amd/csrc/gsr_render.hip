@@ -14,6 +14,9 @@
 // parks the 4 row partials per Gaussian in LDS, and every 32 Gaussians sums them and writes ONE
 // 48-byte row per (instance, quadrant) into the Gaussian's own slot (gsr_backward.hip sums a
 // Gaussian's rows in a fixed order -> deterministic, no atomics, no inverse permutation).
+#include <cstdlib>
+#include <cstring>
+
 #include "gsr_kernels.h"
 #include "gsr_wave.h"
 
@@ -318,24 +321,6 @@ __global__ __launch_bounds__(256) void k_tile_info(RenderSet rs, const uint2* __
   cut[tile] = make_uint2(info.y, info.z);
 }
 
-void launch_render_forward(const RenderSet& rs, const GeomState& g, const uint32_t* sorted_gauss,
-                           const ImageState& img, float* out_color, float* out_depth, float* out_alpha,
-                           hipStream_t stream) {
-  const int nt = rs.gx * rs.gy;
-  if (nt <= 0 || rs.V <= 0) return;
-  if (rs.col2 != nullptr)
-    hipLaunchKernelGGL(k_render_fwd<true>, dim3(rs.V * unit_grid(rs.gx, rs.gy)), dim3(64), 0, stream, rs,
-                       (const uint2*)img.ranges, sorted_gauss, (const GaussRec*)g.rec, out_color, out_depth,
-                       out_alpha, img.final_T, img.n_contrib, img.quad_maxc);
-  else
-    hipLaunchKernelGGL(k_render_fwd<false>, dim3(rs.V * unit_grid(rs.gx, rs.gy)), dim3(64), 0, stream, rs,
-                       (const uint2*)img.ranges, sorted_gauss, (const GaussRec*)g.rec, out_color, out_depth,
-                       out_alpha, img.final_T, img.n_contrib, img.quad_maxc);
-  hipLaunchKernelGGL(k_tile_info, dim3(rs.V * div_up(nt, 256)), dim3(256), 0, stream, rs,
-                     (const uint2*)img.ranges, (const uint32_t*)img.quad_maxc, sorted_gauss,
-                     (const GaussRec*)g.rec, img.tile_info, img.cut);
-}
-
 // ---------------------------------------------------------------------------------------
 // Backward.  Per pixel the reference's back-to-front replay: T recovered by division, the colour
 // accumulated behind each contributor, background term.  Per candidate the 10 gradient sums are
@@ -383,6 +368,226 @@ __device__ __forceinline__ bool tile_of_block(int b, int gx, int gy, int& tile) 
   if (tx >= gx || ty >= gy) return false;
   tile = ty * gx + tx;
   return true;
+}
+
+// Forward, one 64-thread wave per 16x16 tile (4 pixels per lane: the same pixel of each 8x8 quadrant).
+// The wave gathers each tile candidate once (the quadrant-wave kernel above gathers it in each of the
+// four waves), tests it against the four quadrants (quadrant_hit, the same conservative test) and keeps
+// the 4-bit mask with the staged record; the blend walks the staged candidates and evaluates a quadrant's
+// pixel only for candidates whose mask has that quadrant — per pixel exactly the candidates, in the same
+// order, with the same operations as the quadrant-wave kernel, so the outputs are bitwise identical.
+// Finished quadrants leave the mask (uniform), and the wave stops when all four are done.
+template <bool C2>
+__global__ __launch_bounds__(64) void k_render_fwd_tile(RenderSet rs, const uint2* __restrict__ ranges,
+                                                        const uint32_t* __restrict__ sorted_gauss,
+                                                        const GaussRec* __restrict__ rec, float* __restrict__ out_color,
+                                                        float* __restrict__ out_depth, float* __restrict__ out_alpha,
+                                                        float* __restrict__ final_T, uint32_t* __restrict__ n_contrib,
+                                                        uint32_t* __restrict__ quad_maxc) {
+  __shared__ float4 s0[64], s1[64], s2[64];
+  __shared__ float4 s3[C2 ? 64 : 1];
+  __shared__ uint32_t smask[64];
+  const int TG = tile_grid(rs.gx, rs.gy);
+  const int v = blockIdx.x / TG;
+  int tile;
+  if (!tile_of_block(blockIdx.x - v * TG, rs.gx, rs.gy, tile)) return;
+  const int W = rs.W, H = rs.H, grid_x = rs.gx;
+  const size_t HWs = (size_t)W * H;
+  {
+    const size_t vg = (size_t)(rs.v0 + v), tiles = (size_t)rs.gx * rs.gy;
+    ranges += vg * tiles;
+    quad_maxc += vg * 4 * tiles;
+    sorted_gauss += rs.inst_start[v];
+    rec += vg * rs.P;
+    out_color += vg * 3 * HWs;
+    out_depth += vg * HWs;
+    out_alpha += vg * HWs;
+    final_T += vg * HWs;
+    n_contrib += vg * HWs;
+  }
+  const float* bg = rs.bg[v];
+  const int lane = threadIdx.x;
+  const int tx0 = (tile % grid_x) * GSR_TILE_X, ty0 = (tile / grid_x) * GSR_TILE_Y;
+  float pxf[4], pyf[4], T[4], Cr[4], Cg[4], Cb[4], D[4], Er[4], Eg[4], Eb[4];
+  uint32_t last[4];
+  bool done[4], inside[4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const int px = tx0 + (q & 1) * 8 + (lane & 7), py = ty0 + (q >> 1) * 8 + (lane >> 3);
+    inside[q] = px < W && py < H;
+    done[q] = !inside[q];
+    pxf[q] = (float)px;
+    pyf[q] = (float)py;
+    T[q] = 1.0f;
+    Cr[q] = Cg[q] = Cb[q] = D[q] = 0.f;
+    Er[q] = Eg[q] = Eb[q] = 0.f;
+    last[q] = 0u;
+  }
+  const uint2 range = ranges[tile];
+  const int n = (int)(range.y - range.x);
+  const uint32_t gmask = rs.gmask;
+  const float4 zero4 = make_float4(0.f, 0.f, 0.f, 0.f);
+  const float* col2 = rs.col2;
+  float4 n0 = zero4, n1 = zero4, n2 = zero4, n3 = zero4;
+  uint32_t gi_next = 0u;
+  if (lane < n) {
+    const uint32_t g0 = sorted_gauss[range.x + lane] & gmask;
+    n0 = rec[g0].a;
+    n1 = rec[g0].b;
+    n2 = rec[g0].c;
+    if (C2) n3 = make_float4(col2[3 * g0], col2[3 * g0 + 1], col2[3 * g0 + 2], 0.f);
+  }
+  if (64 + lane < n) gi_next = sorted_gauss[range.x + 64 + lane] & gmask;
+  // quadrants with a pixel still blending (uniform)
+  auto active_mask = [&]() -> uint32_t {
+    uint32_t m = 0u;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) m |= __all(done[q]) ? 0u : (1u << q);
+    return m;
+  };
+  uint32_t qactive = active_mask();
+  for (int base = 0; base < n && qactive != 0u; base += 64) {
+    const int i = base + lane;
+    const float4 r0 = n0, r1 = n1, r2 = n2, r3 = n3;
+    if (base + 64 + lane < n) {
+      n0 = rec[gi_next].a;
+      n1 = rec[gi_next].b;
+      n2 = rec[gi_next].c;
+      if (C2) n3 = make_float4(col2[3 * gi_next], col2[3 * gi_next + 1], col2[3 * gi_next + 2], 0.f);
+    }
+    if (base + 128 + lane < n) gi_next = sorted_gauss[range.x + base + 128 + lane] & gmask;
+    uint32_t m = 0u;
+    if (i < n) {
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+        m |= quadrant_hit(r0, r1, (float)(tx0 + (q & 1) * 8), (float)(ty0 + (q >> 1) * 8)) ? (1u << q) : 0u;
+    }
+    // the conic pre-multiplied for gauss_power2 (.w of s1: 1 + list position)
+    s0[lane] = make_float4(r0.x, r0.y, GSR_CONIC_K_AC * r0.z, GSR_CONIC_K_B * r0.w);
+    s1[lane] = make_float4(GSR_CONIC_K_AC * r1.x, r1.y, r1.z, __uint_as_float((uint32_t)(i + 1)));
+    s2[lane] = r2;
+    if (C2) s3[lane] = r3;
+    smask[lane] = m;
+    __syncthreads();
+    const int cnt = min(64, n - base);
+    for (int k = 0; k < cnt; ++k) {
+      if ((k & 7) == 0) {
+        qactive = active_mask();
+        if (qactive == 0u) break;
+      }
+      const uint32_t mk = __builtin_amdgcn_readfirstlane(smask[k]) & qactive;
+      if (mk == 0u) continue;
+      const float4 a = s0[k], b = s1[k], c = s2[k];
+      const float4 e = C2 ? s3[k] : zero4;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        if (mk & (1u << q)) {
+          const float dx = a.x - pxf[q], dy = a.y - pyf[q];
+          const float power2 = gauss_power2(a.z, a.w, b.x, dx, dy);  // log2(e) * power
+          const float alpha = fminf(GSR_ALPHA_MAX, b.y * __builtin_amdgcn_exp2f(power2));
+          const bool ok = !done[q] && power2 <= 0.0f && alpha >= GSR_ALPHA_MIN;
+          const float test_T = T[q] * (1.0f - alpha);
+          const bool term = ok && test_T < GSR_T_EPS;
+          const bool blend = ok && !term;
+          const float a_eff = blend ? alpha : 0.0f;
+          const float aT = a_eff * T[q];
+          Cr[q] = fmaf(c.x, aT, Cr[q]);
+          Cg[q] = fmaf(c.y, aT, Cg[q]);
+          Cb[q] = fmaf(c.z, aT, Cb[q]);
+          D[q] = fmaf(b.z, aT, D[q]);
+          if (C2) {
+            Er[q] = fmaf(e.x, aT, Er[q]);
+            Eg[q] = fmaf(e.y, aT, Eg[q]);
+            Eb[q] = fmaf(e.z, aT, Eb[q]);
+          }
+          T[q] = blend ? test_T : T[q];
+          last[q] = blend ? __float_as_uint(b.w) : last[q];
+          done[q] = done[q] || term;
+        }
+      }
+    }
+    __syncthreads();
+    qactive = active_mask();
+  }
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const int px = tx0 + (q & 1) * 8 + (lane & 7), py = ty0 + (q >> 1) * 8 + (lane >> 3);
+    if (inside[q]) {
+      const size_t pid = (size_t)py * W + px;
+      const float Tq = T[q];
+      final_T[pid] = Tq;
+      n_contrib[pid] = last[q];
+      {
+#pragma clang fp contract(off)
+        out_color[pid] = Cr[q] + Tq * bg[0];
+        out_color[HWs + pid] = Cg[q] + Tq * bg[1];
+        out_color[2 * HWs + pid] = Cb[q] + Tq * bg[2];
+      }
+      out_depth[pid] = D[q];
+      out_alpha[pid] = 1.0f - Tq;
+      if (C2) {
+#pragma clang fp contract(off)
+        float* o2 = rs.out_col2 + (size_t)(rs.v0 + v) * 3 * HWs + pid;
+        o2[0] = Er[q] + Tq * bg[0];
+        o2[HWs] = Eg[q] + Tq * bg[1];
+        o2[2 * HWs] = Eb[q] + Tq * bg[2];
+      }
+      if (rs.cbg != nullptr) {
+#pragma clang fp contract(off)
+        const float am = 1.0f - (1.0f - Tq);
+        const float* bgi = rs.cbg + ((size_t)v * HWs + pid) * 3;
+        float* cp = rs.comp + (size_t)v * 3 * HWs + pid;
+        cp[0] = fminf(fmaxf((Cr[q] + Tq * bg[0]) + am * bgi[0], 0.0f), 1.0f);
+        cp[HWs] = fminf(fmaxf((Cg[q] + Tq * bg[1]) + am * bgi[1], 0.0f), 1.0f);
+        cp[2 * HWs] = fminf(fmaxf((Cb[q] + Tq * bg[2]) + am * bgi[2], 0.0f), 1.0f);
+      }
+    }
+    uint32_t mc = last[q];
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) mc = max(mc, (uint32_t)__shfl_xor((int)mc, o, 64));
+    if (lane == 0) quad_maxc[4 * tile + q] = mc;
+  }
+}
+
+// Which forward: the tile-wave kernel gathers each candidate once but walks a quadrant's candidates one
+// branch at a time and the whole tile list to the tile's deepest termination; it wins when Gaussians span
+// several tiles (C3: 6.7 rectangle tiles per Gaussian, render_fwd -3 %), the quadrant-wave kernel when
+// they are small (C5 SuGaR, 1.7 tiles per Gaussian: the tile kernel is 1.6x slower).  Both give identical
+// outputs.  GSR_FWD_KERNEL=tile|quadrant forces one (A/B and tests).
+static bool fwd_tile_kernel(long long instances, long long gaussians) {
+  const char* e = getenv("GSR_FWD_KERNEL");
+  if (e != nullptr && strcmp(e, "quadrant") == 0) return false;
+  if (e != nullptr && strcmp(e, "tile") == 0) return true;
+  return gaussians > 0 && instances >= 3 * gaussians;
+}
+
+void launch_render_forward(const RenderSet& rs, const GeomState& g, const uint32_t* sorted_gauss,
+                           const ImageState& img, float* out_color, float* out_depth, float* out_alpha,
+                           long long instances, hipStream_t stream) {
+  const int nt = rs.gx * rs.gy;
+  if (nt <= 0 || rs.V <= 0) return;
+  if (fwd_tile_kernel(instances, (long long)rs.V * rs.P)) {
+    const dim3 grid(rs.V * tile_grid(rs.gx, rs.gy));
+    if (rs.col2 != nullptr)
+      hipLaunchKernelGGL(k_render_fwd_tile<true>, grid, dim3(64), 0, stream, rs, (const uint2*)img.ranges,
+                         sorted_gauss, (const GaussRec*)g.rec, out_color, out_depth, out_alpha, img.final_T,
+                         img.n_contrib, img.quad_maxc);
+    else
+      hipLaunchKernelGGL(k_render_fwd_tile<false>, grid, dim3(64), 0, stream, rs, (const uint2*)img.ranges,
+                         sorted_gauss, (const GaussRec*)g.rec, out_color, out_depth, out_alpha, img.final_T,
+                         img.n_contrib, img.quad_maxc);
+  } else if (rs.col2 != nullptr) {
+    hipLaunchKernelGGL(k_render_fwd<true>, dim3(rs.V * unit_grid(rs.gx, rs.gy)), dim3(64), 0, stream, rs,
+                       (const uint2*)img.ranges, sorted_gauss, (const GaussRec*)g.rec, out_color, out_depth,
+                       out_alpha, img.final_T, img.n_contrib, img.quad_maxc);
+  } else {
+    hipLaunchKernelGGL(k_render_fwd<false>, dim3(rs.V * unit_grid(rs.gx, rs.gy)), dim3(64), 0, stream, rs,
+                       (const uint2*)img.ranges, sorted_gauss, (const GaussRec*)g.rec, out_color, out_depth,
+                       out_alpha, img.final_T, img.n_contrib, img.quad_maxc);
+  }
+  hipLaunchKernelGGL(k_tile_info, dim3(rs.V * div_up(nt, 256)), dim3(256), 0, stream, rs,
+                     (const uint2*)img.ranges, (const uint32_t*)img.quad_maxc, sorted_gauss,
+                     (const GaussRec*)g.rec, img.tile_info, img.cut);
 }
 
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5, 8))) void k_render_bwd(RenderSet rs,
