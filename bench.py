@@ -244,14 +244,18 @@ def render_views_sugar(rep: Replica, settings, shade):
 
 
 def read_traffic(path, kernel, field="per_launch_bytes"):
-    """Per-launch value of `kernel` from a committed PMC summary (profiles/summarize.py): HBM bytes
-    (FETCH_SIZE x2 gfx950 correction + WRITE_SIZE, separate --pmc passes) or SQ_INSTS_VALU; None if absent."""
+    """Per-launch value of `kernel` (a name or a list of names, first found wins) from a committed PMC
+    summary (profiles/summarize.py): HBM bytes (FETCH_SIZE x2 gfx950 correction + WRITE_SIZE, separate
+    --pmc passes) or SQ_INSTS_VALU; None if absent."""
     try:
         with open(path) as f:
-            t = json.load(f)
-        return float(t[field][kernel])
+            t = json.load(f)[field]
     except (OSError, KeyError, ValueError, TypeError):
         return None
+    for k in ([kernel] if isinstance(kernel, str) else kernel):
+        if k in t:
+            return float(t[k])
+    return None
 
 
 def read_json(path):
@@ -404,7 +408,9 @@ def roofline_fields(args, phases, Ks, Ls, H, W):
     out = {}
     n_fw = max(1, len(Ks))
     rows = {}
-    for phase, kernel in (("render_fwd", "k_render_fwd"), ("render_bwd", "k_render_bwd")):
+    # the forward of this workload: the tile-wave kernel when Gaussians span >= 3 tiles (gsr_render.hip)
+    fwd_names = ["k_render_fwd_tile<false>", "k_render_fwd<false>", "k_render_fwd"]
+    for phase, kernel in (("render_fwd", fwd_names), ("render_bwd", "k_render_bwd")):
         ms, n = phases[phase]
         n = max(1, n)
         if phase == "render_fwd":
@@ -416,7 +422,8 @@ def roofline_fields(args, phases, Ks, Ls, H, W):
         traffic = read_traffic(args.traffic, kernel)
         valu = read_traffic(args.traffic, kernel, "valu_insts_per_launch")
         views_per_launch = n_fw / n
-        r = {"kernel": kernel, "bound": "hbm", "achieved": round(gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+        r = {"kernel": kernel if isinstance(kernel, str) else "k_render_fwd (tile / quadrant waves)", "bound": "hbm",
+             "achieved": round(gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
              "frac": round(gbs / HBM_PEAK_GBS, 4), "traffic": traffic, "avg_launch_us": round(1e6 * sec, 2),
              "algorithmic_bytes": round(alg), "views_per_launch": round(views_per_launch, 2)}
         if traffic is not None and sec > 0:

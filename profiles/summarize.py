@@ -20,10 +20,15 @@ shutil.copy(os.path.join(src, "trace", "run_kernel_stats.csv"), os.path.join(dst
 
 
 def agg(path, counter):
+    """Mean per launch by kernel, keyed by the kernel name without parameters, 'void ' and 'gsr::'
+    (templates keep their arguments: 'k_render_fwd_tile<false>')."""
     d = collections.defaultdict(list)
     for r in csv.DictReader(open(path)):
         if r["Counter_Name"] == counter:
-            d[r["Kernel_Name"].split("(")[0]].append(float(r["Counter_Value"]))
+            name = r["Kernel_Name"].split("(")[0].strip()
+            if name.startswith("void "):
+                name = name[5:]
+            d[name].append(float(r["Counter_Value"]))
     return d
 
 
@@ -38,7 +43,7 @@ with open(os.path.join(dst, f"{tag}_pmc.csv"), "w", newline="") as fh:
     wr = csv.writer(fh)
     wr.writerow(["kernel", "dispatches", "FETCH_SIZE_KB", "WRITE_SIZE_KB", "hbm_bytes_per_launch_corrected"])
     wr.writerows(rows)
-traffic = {r[0].replace("gsr::", ""): r[4] for r in rows if r[0].startswith("gsr::")}
+traffic = {r[0].replace("gsr::", ""): r[4] for r in rows if r[0].startswith("gsr::")}  # ours only
 summary = {"source": f"profiles/{tag}_pmc.csv", "per_launch_bytes": traffic}
 vpath = os.path.join(src, "valu", "run_counter_collection.csv")
 if os.path.exists(vpath):

@@ -446,6 +446,9 @@ __global__ __launch_bounds__(64) void k_render_fwd_tile(RenderSet rs, const uint
     return m;
   };
   uint32_t qactive = active_mask();
+#ifdef GSR_TIMELINE
+  unsigned long long pc_eval = 0, pc_slot = 0;
+#endif
   for (int base = 0; base < n && qactive != 0u; base += 64) {
     const int i = base + lane;
     const float4 r0 = n0, r1 = n1, r2 = n2, r3 = n3;
@@ -482,6 +485,10 @@ __global__ __launch_bounds__(64) void k_render_fwd_tile(RenderSet rs, const uint
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
         if (mk & (1u << q)) {
+#ifdef GSR_TIMELINE
+          pc_eval += done[q] ? 0ull : 1ull;
+          pc_slot += 1ull;
+#endif
           const float dx = a.x - pxf[q], dy = a.y - pyf[q];
           const float power2 = gauss_power2(a.z, a.w, b.x, dx, dy);  // log2(e) * power
           const float alpha = fminf(GSR_ALPHA_MAX, b.y * __builtin_amdgcn_exp2f(power2));
@@ -547,6 +554,10 @@ __global__ __launch_bounds__(64) void k_render_fwd_tile(RenderSet rs, const uint
     for (int o = 32; o > 0; o >>= 1) mc = max(mc, (uint32_t)__shfl_xor((int)mc, o, 64));
     if (lane == 0) quad_maxc[4 * tile + q] = mc;
   }
+#ifdef GSR_TIMELINE
+  atomicAdd(&g_pairs[0], pc_eval);  // per-lane values (vector atomics)
+  atomicAdd(&g_pairs[1], pc_slot);
+#endif
 }
 
 // Which forward: the tile-wave kernel gathers each candidate once but walks a quadrant's candidates one
