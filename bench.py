@@ -434,8 +434,8 @@ def roofline_fields(args, phases, Ks, Ls, H, W):
         if valu is not None and sec > 0:
             v["insts_per_launch"] = valu
             v["valu_frac"] = round(valu / sec / VALU_PEAK_INSTS, 4)
-        if pairs:
-            key = "fwd_pairs_evaluated_per_view" if phase == "render_fwd" else "bwd_pairs_replayed_per_view"
+        key = "fwd_pairs_evaluated_per_view" if phase == "render_fwd" else "bwd_pairs_replayed_per_view"
+        if pairs and pairs.get(key, 0) > 0:
             pl = pairs[key] * views_per_launch
             v["pairs_per_launch"] = round(pl)
             v["pairs_per_s"] = round(pl / sec) if sec > 0 else None
