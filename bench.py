@@ -627,6 +627,12 @@ def main():
             "epilogue": "sugar_normal (normal-from-depth, 2 passes)" if args.workload == "sugar" else args.epilogue,
         },
     }
+    if args.workload == "sugar":
+        # how the two rasterizer calls run: one forward blending both colour sets + one backward pass for
+        # both (gsr_set_backward_two_colors), or A/B variants
+        res["config"]["two_calls"] = ("separate renders" if SUGAR_SEPARATE else "shared forward, " + (
+            "separate backward passes" if os.environ.get("GSR_TWO_COLOR_BWD") == "separate"
+            else "one two-colour backward pass"))
     if phases is not None:
         nv = max(1, args.steps * per)
         kern = {k: {"ms_per_view": round(ms / nv, 4), "launches": n} for k, (ms, n) in phases.items()}

@@ -191,6 +191,15 @@ int gsr_set_backward(int V, int P, int degree, int M, const int* num_rendered, i
  *                              pass scratch), dL_dcolors the gradient of colors2.  With accumulate the
  *                              parameter gradients continue the first call's (gsr_set_backward with
  *                              dL_dcov3D as the running dL/dcov3D carry).
+ *   gsr_set_backward_two_colors  both calls' backward in one pass (replaces gsr_set_backward[_composite]
+ *                              followed by gsr_set_backward_colors): the blend is replayed once, forming
+ *                              both calls' dL/dalpha; arguments as gsr_set_backward_composite (bg_images
+ *                              and color both NULL: no composite) plus colors2, dL_dcolor2 = dL/d(out_color2)
+ *                              and dL_dcolors2 (P, 3) = the gradient of colors2.  dL_dmeans2D receives the
+ *                              first call's screen-space gradient only (the second call's means2D is the
+ *                              reference's fresh zero tensor); the parameter gradients hold both calls'
+ *                              (equal to the two-call sequence up to fp32 summation order).  Scratch:
+ *                              gsr_set_backward_two_colors_bytes (64-byte gradient rows).
  */
 int gsr_set_render_two_colors(int V, int P, const int* num_rendered, int width, int height, const float* const* bgs,
                               void* geom, void* binning, void* image, float* out_color, float* out_depth,
@@ -205,6 +214,19 @@ int gsr_set_backward_colors(int V, int P, const int* num_rendered, int width, in
                             float* dL_dcolors, float* dL_dopacity, float* dL_dmeans3D, float* dL_dcov3D,
                             float* dL_dscales, float* dL_drotations, int accumulate, void* work, size_t work_bytes,
                             void* stream);
+size_t gsr_set_backward_two_colors_bytes(int V, int P, const int* num_rendered);
+int gsr_set_backward_two_colors(int V, int P, int degree, int M, const int* num_rendered, int width, int height,
+                                const float* const* bgs, const float* means3D, const float* scales,
+                                float scale_modifier, const float* rotations, const float* shs,
+                                const float* cov3D_precomp, const float* const* viewmatrices,
+                                const float* const* projmatrices, const float* const* campos, const float* tanfovx,
+                                const float* tanfovy, const int* radii, const void* geom, const void* binning,
+                                const void* image, const float* bg_images, const float* color,
+                                const float* dL_dcolor, const float* dL_ddepth, const float* dL_dalpha,
+                                float* dL_dbg, const float* colors2, const float* dL_dcolor2, float* dL_dmeans2D,
+                                float* dL_dcolors, float* dL_dcolors2, float* dL_dopacity, float* dL_dmeans3D,
+                                float* dL_dcov3D, float* dL_dsh, float* dL_dscales, float* dL_drotations,
+                                int accumulate, void* work, size_t work_bytes, void* stream);
 /*
  * The background renderer's composite fused into the blends (replaces gsr_set_render + gsr_composite_forward
  * and gsr_composite_backward + gsr_set_backward for renderer/diff_gaussian_rasterizer_background.py:129-132,139):

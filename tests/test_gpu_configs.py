@@ -371,12 +371,19 @@ def test_c5_sugar_normal_renderer():
     check_radii(gpu_pass1["radii"], ref1, "C5 pass 1")
 
 
-def test_second_colors_match_separate_call():
+@pytest.mark.parametrize("bwd", ["fused", "separate"])
+def test_second_colors_match_separate_call(bwd, monkeypatch):
     """rasterize_views(colors2=...) — the SuGaR normal renderer's second rasterizer call from the first's
     geometry, sorts and blend — against the two separate calls (renderer/diff_sugar_rasterizer_normal.py:
     157-191): the second colour image bitwise equal, the first call's outputs and means2D gradient bitwise
-    equal, parameter gradients (summed over both calls) within 1e-5 relative, colors2's gradient equal."""
+    equal; parameter gradients (summed over both calls) within 1e-5 relative when the backward runs the two
+    calls one after the other (GSR_TWO_COLOR_BWD=separate), within the gradient bar 1e-4 max(1, |g|) for the
+    one-pass two-colour backward (gsr_set_backward_two_colors: both calls' dL/dalpha are added per pixel
+    before the moments and the chain rule, an fp32 reassociation of the two-call sum; measured 4.8e-5;
+    test_c5_sugar_normal_renderer holds it to the fp64 oracle)."""
     import torch
+
+    monkeypatch.setenv("GSR_TWO_COLOR_BWD", bwd)
 
     from diff_gaussian_rasterization.batched import rasterize_views
 
@@ -413,4 +420,4 @@ def test_second_colors_match_separate_call():
     for k in f["g"]:
         ref = s_["g"][k].double()
         err = float(((f["g"][k].double() - ref).abs() / ref.abs().clamp(min=1.0)).max())
-        assert err <= 1e-5, f"grad {k}: {err}"
+        assert err <= (1e-4 if bwd == "fused" else 1e-5), f"grad {k}: {err}"

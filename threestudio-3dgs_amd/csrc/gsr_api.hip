@@ -435,6 +435,7 @@ static int set_render(int V, int P, const int* K, int width, int height, const f
     rs.dcbg = nullptr;
     rs.col2 = colors2;
     rs.out_col2 = out_color2;
+    rs.dpix2 = nullptr;
     rs.V = V;
     rs.v0 = 0;
     rs.P = P;
@@ -488,8 +489,13 @@ static int set_backward(int V, int P, int degree, int M, const int* K, int width
                         float* dL_dmeans2D, float* dL_dcolors, float* dL_dopacity, float* dL_dmeans3D,
                         float* dL_dcov3D, float* dL_dsh, float* dL_dscales, float* dL_drotations, int accumulate,
                         void* work, size_t work_bytes, const float* comp_bg, const float* color, float* dL_dbg,
-                        void* stream, const float* colors_override = nullptr) {
+                        void* stream, const float* colors_override = nullptr, const float* colors2 = nullptr,
+                        const float* dL_dcolor2 = nullptr, float* dL_dcolors2 = nullptr) {
   if (check_set(V, P) != GSR_OK) return GSR_EINVAL;
+  // both rasterizer calls of the SuGaR normal renderer in one pass (64-byte rows, 17-field records)
+  const bool two = dL_dcolor2 != nullptr;
+  if (two && (colors2 == nullptr || dL_dcolors2 == nullptr || colors_override != nullptr))
+    return fail(GSR_EINVAL, "%s", "two-colour backward needs colors2, dL_dcolor2 and dL_dcolors2");
   if (width <= 0 || height <= 0) return fail(GSR_EINVAL, "%s", "bad sizes");
   if (P == 0) return last_launch();
   if (K == nullptr || bgs == nullptr || geom == nullptr || binning == nullptr || image == nullptr ||
@@ -528,18 +534,19 @@ static int set_backward(int V, int P, int degree, int M, const int* K, int width
   for (int g0 = 0; g0 < V;) {
     int g1 = g0;
     long long rows = 0;
-    while (g1 < V && (g1 == g0 || BackwardState::bytes_for(rows + K[g1], g1 + 1 - g0, P) <= avail))
+    while (g1 < V && (g1 == g0 || BackwardState::bytes_for(rows + K[g1], g1 + 1 - g0, P, two) <= avail))
       rows += K[g1++];
-    if (BackwardState::bytes_for(rows, g1 - g0, P) > avail)
+    if (BackwardState::bytes_for(rows, g1 - g0, P, two) > avail)
       return fail(GSR_EINVAL, "%s", "backward work buffer smaller than one view's gradient rows");
-    BackwardState bw = BackwardState::carve(work, rows);
+    BackwardState bw = BackwardState::carve(work, rows, two);
     RenderSet rs;
     rs.cbg = comp_bg ? comp_bg + (size_t)g0 * HW * 3 : nullptr;
     rs.comp = nullptr;
     rs.ccolor = color ? color + (size_t)g0 * 3 * HW : nullptr;
     rs.dcbg = dL_dbg ? dL_dbg + (size_t)g0 * HW * 3 : nullptr;
-    rs.col2 = colors_override;
+    rs.col2 = two ? colors2 : colors_override;
     rs.out_col2 = nullptr;
+    rs.dpix2 = two ? dL_dcolor2 + (size_t)g0 * 3 * HW : nullptr;
     rs.V = g1 - g0;
     rs.v0 = g0;
     rs.P = P;
@@ -572,6 +579,7 @@ static int set_backward(int V, int P, int degree, int M, const int* K, int width
     ab.radii = radii;
     ab.vrec = bw.vrec;
     ab.dcov_carry = carry;
+    ab.dcolors2 = two ? dL_dcolors2 : nullptr;
     for (int v = g0; v < g1; ++v) {
       if (bgs[v] == nullptr) return fail(GSR_EINVAL, "%s", "null background");
       rs.inst_start[v - g0] = inst.start[v];
@@ -662,6 +670,34 @@ int gsr_set_backward_colors(int V, int P, const int* K, int width, int height, c
 }
 
 size_t gsr_backward_bytes(int P, int K) { return gsr_set_backward_bytes(1, P, &K); }
+
+size_t gsr_set_backward_two_colors_bytes(int V, int P, const int* K) {
+  long long total = 0;
+  for (int v = 0; v < V; ++v) total += K[v];
+  return BackwardState::bytes_for(total, V, P, true) + carry_bytes(P);
+}
+
+int gsr_set_backward_two_colors(int V, int P, int degree, int M, const int* K, int width, int height,
+                                const float* const* bgs, const float* means3D, const float* scales,
+                                float scale_modifier, const float* rotations, const float* shs,
+                                const float* cov3D_precomp, const float* const* viewmatrices,
+                                const float* const* projmatrices, const float* const* campos, const float* tanfovx,
+                                const float* tanfovy, const int* radii, const void* geom, const void* binning,
+                                const void* image, const float* bg_images, const float* color,
+                                const float* dL_dcolor, const float* dL_ddepth, const float* dL_dalpha,
+                                float* dL_dbg, const float* colors2, const float* dL_dcolor2, float* dL_dmeans2D,
+                                float* dL_dcolors, float* dL_dcolors2, float* dL_dopacity, float* dL_dmeans3D,
+                                float* dL_dcov3D, float* dL_dsh, float* dL_dscales, float* dL_drotations,
+                                int accumulate, void* work, size_t work_bytes, void* stream) {
+  if (colors2 == nullptr || dL_dcolor2 == nullptr || dL_dcolors2 == nullptr)
+    return fail(GSR_EINVAL, "%s", "null second colour argument");
+  if ((bg_images == nullptr) != (color == nullptr)) return fail(GSR_EINVAL, "%s", "composite needs both images");
+  return set_backward(V, P, degree, M, K, width, height, bgs, means3D, scales, scale_modifier, rotations, shs,
+                      cov3D_precomp, viewmatrices, projmatrices, campos, tanfovx, tanfovy, radii, geom, binning, image,
+                      dL_dcolor, dL_ddepth, dL_dalpha, dL_dmeans2D, dL_dcolors, dL_dopacity, dL_dmeans3D, dL_dcov3D,
+                      dL_dsh, dL_dscales, dL_drotations, accumulate, work, work_bytes, bg_images, color, dL_dbg,
+                      stream, nullptr, colors2, dL_dcolor2, dL_dcolors2);
+}
 
 int gsr_forward_preprocess(int P, int degree, int M, const float* means3D, const float* scales,
                            float scale_modifier, const float* rotations, const float* opacities,

@@ -22,6 +22,7 @@ namespace gsr {
 
 struct RowSums {
   float dmx, dmy, dca, dcb, dcc, dop, dcr, dcg, dcbl, ddep;
+  float dmx1, dmy1, dr2, dg2, db2;  // two-colour rows (gsr_common.h BackwardState)
 };
 
 // Sum the rows of the Gaussian's instances that its tile's blend reached: the kept tiles of its
@@ -29,9 +30,11 @@ struct RowSums {
 // instance (cut = (key, index) per tile).  Rows sit at rectangle positions.  Tiles are walked 4 at
 // a time: the 4 cut tests first, then the valid rows' loads together, so a thread has up to 12
 // loads in flight instead of waiting on each row in turn.
+template <bool TWO>
 __device__ __forceinline__ RowSums gather_rows(uint32_t idx, const GaussRec& gr, uint32_t i0, int grid_x,
                                                const uint2* cut, const float4* grow) {
-  RowSums r = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  RowSums r = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  constexpr int RW = TWO ? 4 : 3;
   const uint4 gd = gr.d;
   const float4 ga = gr.a, gb = gr.b;
   const uint32_t dkey = __float_as_uint(gb.z);
@@ -55,19 +58,22 @@ __device__ __forceinline__ RowSums gather_rows(uint32_t idx, const GaussRec& gr,
           sl[k] = (ty - ymin) * w + (tx + k - xmin);
         }
       }
-      float4 a[4][3];
+      float4 a[4][RW];
 #pragma unroll
       for (int k = 0; k < 4; ++k) {
-        const float4* row = grow + 3 * ((size_t)i0 + sl[k]);
-        a[k][0] = val[k] ? row[0] : z4;
-        a[k][1] = val[k] ? row[1] : z4;
-        a[k][2] = val[k] ? row[2] : z4;
+        const float4* row = grow + RW * ((size_t)i0 + sl[k]);
+#pragma unroll
+        for (int e = 0; e < RW; ++e) a[k][e] = val[k] ? row[e] : z4;
       }
 #pragma unroll
       for (int k = 0; k < 4; ++k) {
         r.dmx += a[k][0].x; r.dmy += a[k][0].y; r.dca += a[k][0].z; r.dcb += a[k][0].w;
         r.dcc += a[k][1].x; r.dop += a[k][1].y; r.dcr += a[k][1].z; r.dcg += a[k][1].w;
         r.dcbl += a[k][2].x; r.ddep += a[k][2].y;
+        if (TWO) {
+          r.dr2 += a[k][2].z; r.dg2 += a[k][2].w;
+          r.db2 += a[k][RW - 1].x; r.dmx1 += a[k][RW - 1].y; r.dmy1 += a[k][RW - 1].z;
+        }
       }
     }
   }
@@ -268,7 +274,9 @@ static inline __host__ __device__ int sh_lds_stride(int M) { return ((3 * M + 3)
 #ifndef GSR_VG_ITEMS
 #define GSR_VG_ITEMS 16
 #endif
+template <bool TWO>
 __global__ __launch_bounds__(256) void k_view_grad(GaussBackwardArgs a, ViewGradArgs va) {
+  constexpr int NF = TWO ? GSR_GRAD_FIELDS2 : GSR_GRAD_FIELDS;
   extern __shared__ uint2 s_cut[];
   const int t = threadIdx.x;
   const int vl = blockIdx.x % va.V;
@@ -295,8 +303,8 @@ __global__ __launch_bounds__(256) void k_view_grad(GaussBackwardArgs a, ViewGrad
   vgm.tany = cam.tany;
   vgm.fy = va.H / (2.0f * cam.tany);
   vgm.fx = va.W / (2.0f * cam.tanx);
-  const float4* grow = va.grow + (size_t)3 * va.row_start[vl];
-  float* recv = va.vrec + (size_t)vl * GSR_GRAD_FIELDS * a.P;
+  const float4* grow = va.grow + (size_t)(TWO ? 4 : 3) * va.row_start[vl];
+  float* recv = va.vrec + (size_t)vl * NF * a.P;
   // the next item's radius and record are loaded while the current one is processed
   const int idx_base = (blockIdx.x / va.V) * (256 * GSR_VG_ITEMS) + t;
   int nrad = 0;
@@ -326,13 +334,14 @@ __global__ __launch_bounds__(256) void k_view_grad(GaussBackwardArgs a, ViewGrad
       m2[1] = 0.f;
       m2[2] = 0.f;
 #pragma unroll
-      for (int f = 0; f < GSR_GRAD_FIELDS; ++f) rec[(size_t)f * a.P] = 0.f;
+      for (int f = 0; f < NF; ++f) rec[(size_t)f * a.P] = 0.f;
       continue;
     }
     const uint32_t clamp_bits = gr.d.w;
-    const RowSums r = gather_rows((uint32_t)idx, gr, go, va.gx, cut, grow);
-    m2[0] = r.dmx;
-    m2[1] = r.dmy;
+    const RowSums r = gather_rows<TWO>((uint32_t)idx, gr, go, va.gx, cut, grow);
+    // (two colours: the first call's own screen-space gradient; the chain below takes both calls')
+    m2[0] = TWO ? r.dmx1 : r.dmx;
+    m2[1] = TWO ? r.dmy1 : r.dmy;
     m2[2] = 0.f;
     const float3 mean = make_float3(a.means3D[3 * idx], a.means3D[3 * idx + 1], a.means3D[3 * idx + 2]);
     float cov3D[6];
@@ -353,10 +362,10 @@ __global__ __launch_bounds__(256) void k_view_grad(GaussBackwardArgs a, ViewGrad
     dm.x += viewm[2] * r.ddep;
     dm.y += viewm[6] * r.ddep;
     dm.z += viewm[10] * r.ddep;
-    const float f[GSR_GRAD_FIELDS] = {dm.x, dm.y, dm.z, dcv[0], dcv[1], dcv[2], dcv[3], dcv[4], dcv[5],
-                                      r.dcr, r.dcg, r.dcbl, r.dop, __uint_as_float(clamp_bits)};
+    const float f[GSR_GRAD_FIELDS2] = {dm.x,  dm.y,  dm.z,  dcv[0], dcv[1], dcv[2], dcv[3], dcv[4], dcv[5],
+                                       r.dcr, r.dcg, r.dcbl, r.dop, __uint_as_float(clamp_bits), r.dr2, r.dg2, r.db2};
 #pragma unroll
-    for (int k = 0; k < GSR_GRAD_FIELDS; ++k) rec[(size_t)k * a.P] = f[k];
+    for (int k = 0; k < NF; ++k) rec[(size_t)k * a.P] = f[k];
   }
 }
 
@@ -415,11 +424,12 @@ __global__ __launch_bounds__(256) void k_gauss_accum(GaussBackwardArgs a, AccumA
     // offset in scalars (no per-load address registers to recycle while loads are in flight)
     const int lane_off = idx * 4;
     const int field_bytes = a.P * 4;
+    const int nf = b.dcolors2 ? GSR_GRAD_FIELDS2 : GSR_GRAD_FIELDS;  // record stride (fields) per view
     auto load = [&](float* f, int& rad, int vl) {
       const auto rr = __builtin_amdgcn_make_buffer_rsrc((void*)(b.radii + (size_t)(b.v0 + vl) * a.P), 0,
                                                         field_bytes, 0x00020000);
       rad = (int)__builtin_amdgcn_raw_buffer_load_b32(rr, lane_off, 0, 0);
-      const auto rv = __builtin_amdgcn_make_buffer_rsrc((void*)(b.vrec + (size_t)vl * GSR_GRAD_FIELDS * a.P), 0,
+      const auto rv = __builtin_amdgcn_make_buffer_rsrc((void*)(b.vrec + (size_t)vl * nf * a.P), 0,
                                                         GSR_GRAD_FIELDS * field_bytes, 0x00020000);
 #pragma unroll
       for (int k = 0; k < GSR_GRAD_FIELDS; ++k)
@@ -485,6 +495,17 @@ __global__ __launch_bounds__(256) void k_gauss_accum(GaussBackwardArgs a, AccumA
       a.dL_dcolors[3 * idx + 1] = dcg;
       a.dL_dcolors[3 * idx + 2] = dcb;
     }
+    if (b.dcolors2) {
+      // two colours: the second colour's sums (zero records for culled views add nothing)
+      float d2[3] = {0.f, 0.f, 0.f};
+      if (acc)
+        for (int k = 0; k < 3; ++k) d2[k] = b.dcolors2[3 * idx + k];
+      for (int w = 0; w < b.V; ++w) {
+        const float* r2 = b.vrec + ((size_t)w * GSR_GRAD_FIELDS2 + GSR_GRAD_FIELDS) * a.P + idx;
+        for (int k = 0; k < 3; ++k) d2[k] += r2[(size_t)k * a.P];
+      }
+      for (int k = 0; k < 3; ++k) b.dcolors2[3 * idx + k] = d2[k];
+    }
     if (b.dcov_carry)
       for (int k = 0; k < 6; ++k) b.dcov_carry[6 * idx + k] = dcov[k];
     if (a.dL_dcov3D && a.dL_dcov3D != b.dcov_carry)
@@ -529,8 +550,12 @@ void launch_gauss_backward(const GaussBackwardArgs& a, ViewGradArgs va, const Ac
   if (a.P <= 0 || va.V <= 0) return;
   const size_t cut_bytes = sizeof(uint2) * (size_t)va.tiles;
   va.cut_in_lds = cut_bytes <= GSR_CUT_LDS_MAX ? 1 : 0;
-  hipLaunchKernelGGL(k_view_grad, dim3(va.V * div_up(a.P, 256 * GSR_VG_ITEMS)), dim3(256),
-                     va.cut_in_lds ? cut_bytes : 0, stream, a, va);
+  if (b.dcolors2)
+    hipLaunchKernelGGL(k_view_grad<true>, dim3(va.V * div_up(a.P, 256 * GSR_VG_ITEMS)), dim3(256),
+                       va.cut_in_lds ? cut_bytes : 0, stream, a, va);
+  else
+    hipLaunchKernelGGL(k_view_grad<false>, dim3(va.V * div_up(a.P, 256 * GSR_VG_ITEMS)), dim3(256),
+                       va.cut_in_lds ? cut_bytes : 0, stream, a, va);
   const size_t lds = (a.shs && a.M > 0) ? (size_t)256 * sh_lds_stride(a.M) * sizeof(float) : 0;
   hipLaunchKernelGGL(k_gauss_accum, dim3(div_up(a.P, 256)), dim3(256), lds, stream, a, b);
 }

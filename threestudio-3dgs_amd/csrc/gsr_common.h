@@ -273,22 +273,32 @@ struct ImageState {
 //   g0 = (dmean2D.x, dmean2D.y, dconic.a, dconic.b)   [pixel units; b in the reference's half convention]
 //   g1 = (dconic.c, dopacity, dcolor.r, dcolor.g)
 //   g2 = (dcolor.b, ddepth, 0, 0)
+// The two-colour backward (one pass for both of the SuGaR normal renderer's rasterizer calls) writes
+// 64-byte rows: g0, g1 as above with the conic / opacity / mean2D terms of both calls' summed
+// dL/dalpha,
+//   g2 = (dcolor.b, ddepth, dcolor2.r, dcolor2.g)
+//   g3 = (dcolor2.b, dmean2D_1.x, dmean2D_1.y, 0)   [the first call's own screen-space gradient]
 // After the rows: the per-(view, Gaussian) records of gsr_backward.hip's first kernel,
 // Per-(view, Gaussian) record of the backward's second stage: dmean3D (3), dcov3D (6), raw dcolor (3),
-// dopacity (1), SH clamp flags (uint bits, 1).
+// dopacity (1), SH clamp flags (uint bits, 1); two-colour: + raw dcolor2 (3).
 #define GSR_GRAD_FIELDS 14
-// [views of the group][GSR_GRAD_FIELDS][P] floats.
+#define GSR_GRAD_FIELDS2 17
+// [views of the group][fields][P] floats.
 struct BackwardState {
-  float4* grow;  // [3 * instances of the group]
-  float* vrec;   // [views][GSR_GRAD_FIELDS][P]
-  static size_t rows_bytes(long long K) { return align_up(sizeof(float4) * 3 * (size_t)(K > 0 ? K : 1), 256); }
-  static size_t bytes_for(long long K, int views, int P) {
-    return rows_bytes(K) + align_up(sizeof(float) * GSR_GRAD_FIELDS * (size_t)views * (size_t)(P > 0 ? P : 1), 256);
+  float4* grow;  // [3 (two colours: 4) * instances of the group]
+  float* vrec;   // [views][GSR_GRAD_FIELDS (two colours: GSR_GRAD_FIELDS2)][P]
+  static size_t rows_bytes(long long K, bool two = false) {
+    return align_up(sizeof(float4) * (two ? 4 : 3) * (size_t)(K > 0 ? K : 1), 256);
   }
-  static BackwardState carve(void* base, long long K) {
+  static size_t bytes_for(long long K, int views, int P, bool two = false) {
+    return rows_bytes(K, two) + align_up(sizeof(float) * (two ? GSR_GRAD_FIELDS2 : GSR_GRAD_FIELDS) * (size_t)views *
+                                             (size_t)(P > 0 ? P : 1),
+                                         256);
+  }
+  static BackwardState carve(void* base, long long K, bool two = false) {
     BackwardState s;
     s.grow = (float4*)base;
-    s.vrec = (float*)((char*)base + rows_bytes(K));
+    s.vrec = (float*)((char*)base + rows_bytes(K, two));
     return s;
   }
 };

@@ -56,6 +56,9 @@ struct RenderSet {
   // first colour.  Backward: replaces the records' colour (the second call's backward).
   const float* col2;
   float* out_col2;
+  // backward of both calls in one pass: dL/d(second colour image) (V, 3, H, W) at the launch's first
+  // view; col2 then holds the second colours and the records keep the first (null = off)
+  const float* dpix2;
 };
 // instances: the set's rectangle tiles (sum of K) — picks the forward kernel (gsr_render.hip)
 void launch_render_forward(const RenderSet& rs, const GeomState& g, const uint32_t* sorted_gauss,
@@ -96,6 +99,9 @@ struct AccumArgs {
   // backward split into view groups is bitwise equal to one group, and the scale / rotation gradients
   // are recomputed from the running total instead of being added per group
   float* dcov_carry;
+  // two-colour backward: dL/dcolors2 (P x 3; with accumulate continued from the stored value); its
+  // records have GSR_GRAD_FIELDS2 fields and rows 4 float4 (null = the one-colour layout)
+  float* dcolors2;
   const float* campos[GSR_SET_MAX];
 };
 // Background composite epilogue — gsr_epilogue.hip.

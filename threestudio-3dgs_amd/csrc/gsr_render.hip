@@ -337,12 +337,22 @@ __global__ __launch_bounds__(256) void k_tile_info(RenderSet rs, const uint2* __
 // one thread per candidate then adds the four quadrants and writes ONE 48-byte gradient row per
 // instance.
 
-#define GSR_QSUM_STRIDE 41  // floats per candidate: 4 quadrants x 10 raw sums, +1 pad
+//
+// Two-colour variant (TWO, the SuGaR normal renderer's two rasterizer calls on shared geometry in one
+// pass): the replay forms both calls' dL/dalpha (the second with its own dL/dpixel and accumulated
+// colour, no depth / alpha terms), u_1 = G dL/dalpha_1 and u = u_1 + u_2; 16 sums per candidate:
+//   0-5 the u moments, 6-9 sum w dL/d(r,g,b,depth), 10-12 sum u_1 (1, x, y), 13-15 sum w dL/d(r2,g2,b2)
+// from 4 candidates per product (A rows 0-3 u, 4-7 u_1, 8-11 w; B columns 6-12 the 7 pixel planes).
+#define NGV2 16
+#define GSR_QSUM_STRIDE 41   // floats per candidate: 4 quadrants x 10 raw sums, +1 pad
+#define GSR_QSUM_STRIDE2 65  // two colours: 4 x 16, +1
+template <bool TWO>
 struct BwdLDS {
   float4 s0[65], s1[65], s2[65];
+  float4 s3[TWO ? 65 : 1];  // two colours: the second colour
   uint32_t slot[64];
   uint32_t list[4][64];
-  float qsum[64 * GSR_QSUM_STRIDE];
+  float qsum[64 * (TWO ? GSR_QSUM_STRIDE2 : GSR_QSUM_STRIDE)];
   // per wave: the group's A operand, u = G dL/dalpha (slots 0-7) and w = alpha T (slots 8-15) of
   // its 8 candidates, stored so that MFMA lane l's 16 values are 4 chunks of 16 B (swizzled:
   // conflict-free 16-B reads, 2-way 4-B writes)
@@ -601,7 +611,8 @@ void launch_render_forward(const RenderSet& rs, const GeomState& g, const uint32
                      (const GaussRec*)g.rec, img.tile_info, img.cut);
 }
 
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5, 8))) void k_render_bwd(RenderSet rs,
+template <bool TWO>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(TWO ? 4 : 5, 8))) void k_render_bwd(RenderSet rs,
                                                     const uint2* __restrict__ ranges,
                                                     const uint32_t* __restrict__ quad_maxc,
                                                     const uint32_t* __restrict__ sorted_gauss,
@@ -613,7 +624,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5, 8))) voi
                                                     const float* __restrict__ dL_ddepth,
                                                     const float* __restrict__ dL_dalpha,
                                                     float4* __restrict__ grow) {
-  __shared__ BwdLDS s;
+  __shared__ BwdLDS<TWO> s;
+  constexpr int NG = TWO ? NGV2 : NGV;                           // raw sums per (candidate, quadrant)
+  constexpr int QS = TWO ? GSR_QSUM_STRIDE2 : GSR_QSUM_STRIDE;  // per candidate
+  constexpr int GS = TWO ? 4 : 8;                                // candidates per 16x16 product
+  constexpr int NPL = TWO ? 7 : 4;                               // dL/dpixel planes in the B operand
+  constexpr int RW = TWO ? 4 : 3;                                // float4 per gradient row
   const int TG = tile_grid(rs.gx, rs.gy);
   const int v = blockIdx.x / TG;
   int tile;
@@ -632,7 +648,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5, 8))) voi
     dL_dcolor += (size_t)v * 3 * HWs;
     if (dL_ddepth) dL_ddepth += (size_t)v * HWs;
     if (dL_dalpha) dL_dalpha += (size_t)v * HWs;
-    grow += (size_t)3 * rs.row_start[v];
+    grow += (size_t)RW * rs.row_start[v];
   }
   const float* bg = rs.bg[v];
   int tl_work = 0, tl_max = 0;
@@ -681,6 +697,16 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5, 8))) voi
     }
   }
   const float bg_dot = bg[0] * dpix[0] + bg[1] * dpix[1] + bg[2] * dpix[2];
+  // two colours: the second call's dL/dpixel (same background, no depth / alpha outputs)
+  float dpix2[3] = {0.f, 0.f, 0.f};
+  if (TWO && inside) {
+    const float* d2 = rs.dpix2 + (size_t)v * 3 * HW;
+    dpix2[0] = d2[pid];
+    dpix2[1] = d2[HW + pid];
+    dpix2[2] = d2[2 * HW + pid];
+  }
+  const float nbg2 = TWO ? -T_final * (bg[0] * dpix2[0] + bg[1] * dpix2[1] + bg[2] * dpix2[2]) : 0.f;
+  float S2 = 0.f;
 
   // The reference keeps per channel the colour accumulated behind the current Gaussian
   // (accum_rec = last_alpha last_c + (1 - last_alpha) accum_rec, deferred by one contributor) and
@@ -704,14 +730,19 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5, 8))) voi
     return r >= 0 ? (sorted_gauss[range.x + r] & gmask) : 0u;
   };
   float4 npc = zero4;  // the next batch's piece (piece 3 also carries the Gaussian's first row slot)
+  float4 npc2 = zero4;  // two colours: piece 2's thread also moves the second colour
   uint32_t ngo = 0u;
   uint32_t gi_next = 0u;
   if (maxc > 0) {
     const uint32_t g0 = fetch_index(maxc);
     if (maxc - 1 - cs >= 0) {
       npc = reinterpret_cast<const float4*>(rec + g0)[piece];
-      if (piece == 2 && rs.col2 != nullptr)  // the second rasterizer call's colours
-        npc = make_float4(rs.col2[3 * g0], rs.col2[3 * g0 + 1], rs.col2[3 * g0 + 2], 0.f);
+      if (piece == 2 && rs.col2 != nullptr) {
+        if (TWO)
+          npc2 = make_float4(rs.col2[3 * g0], rs.col2[3 * g0 + 1], rs.col2[3 * g0 + 2], 0.f);
+        else  // the second rasterizer call's colours replace the first's
+          npc = make_float4(rs.col2[3 * g0], rs.col2[3 * g0 + 1], rs.col2[3 * g0 + 2], 0.f);
+      }
       if (piece == 3) ngo = goff[g0];
     }
     if (maxc > 64) gi_next = fetch_index(maxc - 64);
@@ -739,6 +770,28 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5, 8))) voi
     w = a_eff * T;
     S = fmaf(a_eff, cd, oma * S);
   };
+  // two colours: gd = the second colour; uT = u_1 + u_2, u1 = u_1
+  auto replay2 = [&](const float4& ga, const float4& gb, const float4& gc, const float4& gd, float& uT, float& u1,
+                     float& w) {
+    const uint32_t rel = __float_as_uint(gb.w);
+    const float dx = ga.x - pxf, dy = ga.y - pyf;
+    const float power2 = gauss_power2(ga.z, ga.w, gb.x, dx, dy);
+    const float G = __builtin_amdgcn_exp2f(power2);
+    const float alpha = fminf(GSR_ALPHA_MAX, gb.y * G);
+    const bool hit = rel < last_contributor && power2 <= 0.0f && alpha >= GSR_ALPHA_MIN;
+    const float a_eff = hit ? alpha : 0.0f;
+    const float g_eff = hit ? G : 0.0f;
+    const float oma = 1.f - a_eff;
+    const float inv_1ma = fast_rcp(oma);
+    T = T * inv_1ma;
+    const float cd = fmaf(gc.x, dpix[0], fmaf(gc.y, dpix[1], fmaf(gc.z, dpix[2], fmaf(gb.z, dpix_d, dpix_a))));
+    const float cd2 = fmaf(gd.x, dpix2[0], fmaf(gd.y, dpix2[1], gd.z * dpix2[2]));
+    u1 = g_eff * fmaf(T, cd - S, inv_1ma * nbg);
+    uT = fmaf(g_eff, fmaf(T, cd2 - S2, inv_1ma * nbg2), u1);
+    w = a_eff * T;
+    S = fmaf(a_eff, cd, oma * S);
+    S2 = fmaf(a_eff, cd2, oma * S2);
+  };
 
 
   // Matrix-core reduction.  For a group of 8 candidates c, one 16x16 product over the quadrant's
@@ -752,7 +805,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5, 8))) voi
   // k-step i, k = l >> 4 covers pixel p = 16 k + i: x = p & 7 = i & 7 (uniform), y = p >> 3 =
   // 2 k + (i >> 3), so F = fa[i >> 3] + x (fbb[i >> 3] + x fc).
   const int ncol = lane & 15;
-  const bool dcol = ncol >= 6 && ncol <= 9;
+  const bool dcol = ncol >= 6 && ncol < 6 + NPL;
   float fa[2], fbb[2], fc;
 #pragma unroll
   for (int h = 0; h < 2; ++h) {
@@ -766,14 +819,20 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5, 8))) voi
   // staging barrier, by which time every wave has read its bv).
   float bv[16];
   {
-    float* sdp = s.qsum + q * (4 * 68 + 16);
+    float* sdp = s.qsum + q * (NPL * 68 + 16);
     sdp[0 * 68 + lane] = dpix[0];
     sdp[1 * 68 + lane] = dpix[1];
     sdp[2 * 68 + lane] = dpix[2];
     sdp[3 * 68 + lane] = dpix_d;
-    if (lane < 16) sdp[4 * 68 + lane] = 0.f;
+    if (TWO) {
+      sdp[4 * 68 + lane] = dpix2[0];
+      sdp[5 * 68 + lane] = dpix2[1];
+      sdp[6 * 68 + lane] = dpix2[2];
+    }
+    if (lane < 16) sdp[NPL * 68 + lane] = 0.f;
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    const float4* dsrc = reinterpret_cast<const float4*>(sdp + (dcol ? (ncol - 6) * 68 + 16 * (lane >> 4) : 4 * 68));
+    const float4* dsrc =
+        reinterpret_cast<const float4*>(sdp + (dcol ? (ncol - 6) * 68 + 16 * (lane >> 4) : NPL * 68));
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
       const float4 d4 = dsrc[k];
@@ -797,11 +856,26 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5, 8))) voi
   const int aswz = (lane >> 2) & 3;
   // result side: lane l holds rows 4 (l >> 4) + r -> candidate mb + r of the group, u (rows 0-7,
   // columns 0-5 used) or w (rows 8-15, columns 6-9 used)
-  const int mb = 4 * ((lane >> 4) & 1);
-  const bool useful = (lane < 32) ? (ncol < 6) : dcol;
+  // two colours: rows 4 (l >> 4) + r are candidate r's u (lanes 0-15, columns 0-5), u_1 (16-31,
+  // columns 0-2 -> sums 10-12) or w (32-47, columns 6-12 -> sums 6-9, 13-15); lanes 48-63 unused
+  const int mb = TWO ? 0 : 4 * ((lane >> 4) & 1);
+  bool useful;
+  int field = ncol;
+  if (TWO) {
+    const int rg = lane >> 4;
+    useful = rg == 0 ? ncol < 6 : rg == 1 ? ncol < 3 : rg == 2 ? dcol : false;
+    field = rg == 1 ? 10 + ncol : (rg == 2 && ncol >= 10) ? ncol + 3 : ncol;
+  } else {
+    useful = (lane < 32) ? (ncol < 6) : dcol;
+  }
+  if (TWO) {
+    // A rows 12-15 are never written: zero them once (their products are not read either)
+#pragma unroll
+    for (int r = 12; r < 16; ++r) s.uw[q][16 * r + wa[3]] = 0.f;
+  }
 
   uint32_t* mylist = s.list[q];
-  float* myq = s.qsum + q * NGV;
+  float* myq = s.qsum + q * NG;
   for (int hi = maxc; hi > 0; hi -= 64) {
     {
       const int rel_c = hi - 1 - cs;
@@ -813,6 +887,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5, 8))) voi
           s.s1[cs] = make_float4(GSR_CONIC_K_AC * npc.x, npc.y, npc.z, __uint_as_float((uint32_t)rel_c));
         } else if (piece == 2) {
           s.s2[cs] = npc;
+          if (TWO) s.s3[cs] = npc2;
         } else {
           const uint32_t dx_ = __float_as_uint(npc.x), dy_ = __float_as_uint(npc.y);
           const int xmin = dx_ & 0xffff, ymin = dx_ >> 16, xmax = dy_ & 0xffff;
@@ -822,8 +897,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5, 8))) voi
       if (hi > 64) {
         if (hi - 65 - cs >= 0) {
           npc = reinterpret_cast<const float4*>(rec + gi_next)[piece];
-          if (piece == 2 && rs.col2 != nullptr)
-            npc = make_float4(rs.col2[3 * gi_next], rs.col2[3 * gi_next + 1], rs.col2[3 * gi_next + 2], 0.f);
+          if (piece == 2 && rs.col2 != nullptr) {
+            const float4 c2 =
+                make_float4(rs.col2[3 * gi_next], rs.col2[3 * gi_next + 1], rs.col2[3 * gi_next + 2], 0.f);
+            if (TWO)
+              npc2 = c2;
+            else
+              npc = c2;
+          }
           if (piece == 3) ngo = goff[gi_next];
         }
         if (hi > 128) gi_next = fetch_index(hi - 128);
@@ -858,28 +939,39 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5, 8))) voi
 #ifdef GSR_EXP_NOGROUP
     if (cnt < 0)
 #endif
-    for (int g0 = 0; g0 < cnt; g0 += 8) {
-      const int gn = min(8, cnt - g0);
+    for (int g0 = 0; g0 < cnt; g0 += GS) {
+      const int gn = min(GS, cnt - g0);
       int j = (int)__builtin_ctzll(rest);
       float4 ca = s.s0[j], cb = s.s1[j], cc = s.s2[j];
+      float4 cd2 = TWO ? s.s3[j] : zero4;
 #pragma unroll
-      for (int c = 0; c < 8; ++c) {
+      for (int c = 0; c < GS; ++c) {
         if (c < gn) {
           rest &= rest - 1ull;
           const int jn = (c + 1 < gn) ? (int)__builtin_ctzll(rest) : j;
           const float4 na = s.s0[jn], nb = s.s1[jn], nc = s.s2[jn];
-          float u, w;
+          const float4 nd = TWO ? s.s3[jn] : zero4;
+          if (TWO) {
+            float uT, u1, w;
+            replay2(ca, cb, cc, cd2, uT, u1, w);
+            uw[16 * c + wa[0]] = uT;
+            uw[16 * (c + 4) + wa[1]] = u1;
+            uw[16 * (c + 8) + wa[2]] = w;
+          } else {
+            float u, w;
 #ifdef GSR_EXP_NOREPLAY
-          u = ca.x * pxf;
-          w = cb.x * pyf;
+            u = ca.x * pxf;
+            w = cb.x * pyf;
 #else
-          replay(ca, cb, cc, u, w);
+            replay(ca, cb, cc, u, w);
 #endif
-          uw[16 * c + wa[c >> 2]] = u;
-          uw[16 * (c + 8) + wa[2 + (c >> 2)]] = w;
+            uw[16 * c + wa[c >> 2]] = u;
+            uw[16 * (c + 8) + wa[2 + (c >> 2)]] = w;
+          }
           ca = na;
           cb = nb;
           cc = nc;
+          cd2 = nd;
           j = jn;
         }
       }
@@ -909,7 +1001,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5, 8))) voi
         const uint32_t jr[4] = {jl.x, jl.y, jl.z, jl.w};
 #pragma unroll
         for (int r = 0; r < 4; ++r)
-          if (mb + r < gn) myq[jr[r] * (uint32_t)GSR_QSUM_STRIDE + (uint32_t)ncol] = acc0[r] + acc1[r];
+          if (mb + r < gn) myq[jr[r] * (uint32_t)QS + (uint32_t)field] = acc0[r] + acc1[r];
       }
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // rows are rewritten by the next group
     }
@@ -935,9 +1027,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5, 8))) voi
       const int qq = piece;
       const float4 ga = s.s0[cs];
       const float4 gb = s.s1[cs];
-      float m[NGV] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+      // two colours: m[10], m[11] the u_1 first moments, m[12-14] the second colour sums
+      constexpr int NM = TWO ? 15 : NGV;
+      float m[NM];
+#pragma unroll
+      for (int i = 0; i < NM; ++i) m[i] = 0.f;
       if ((s.kmask[qq] >> cs) & 1ull) {
-        const float* C = s.qsum + cs * GSR_QSUM_STRIDE + NGV * qq;
+        const float* C = s.qsum + cs * QS + NG * qq;
         const float mx = ga.x - (float)(txi * GSR_TILE_X + (qq & 1) * 8);
         const float my = ga.y - (float)(tyi * GSR_TILE_Y + (qq >> 1) * 8);
         m[0] = C[0];
@@ -950,28 +1046,39 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5, 8))) voi
         m[7] = C[7];
         m[8] = C[8];
         m[9] = C[9];
+        if (TWO) {
+          m[10 % NM] = mx * C[10] - C[11];
+          m[11 % NM] = my * C[10] - C[12];
+          m[12 % NM] = C[13];
+          m[13 % NM] = C[14];
+          m[14 % NM] = C[15];
+        }
       }
 #pragma unroll
-      for (int i = 0; i < NGV; ++i) {
+      for (int i = 0; i < NM; ++i) {
         m[i] += dpp_f32<0xB1>(m[i]);  // quad_perm [1,0,3,2]
         m[i] += dpp_f32<0x4E>(m[i]);  // quad_perm [2,3,0,1]
       }
       const float o = gb.y;
 #ifdef GSR_EXP_COALROWS
-      float4* row = grow + 3 * ((size_t)blockIdx.x * 64 + cs);  // timing only: coalesced, wrong slots
+      float4* row = grow + RW * ((size_t)blockIdx.x * 64 + cs);  // timing only: coalesced, wrong slots
 #else
-      float4* row = grow + 3 * (size_t)s.slot[cs];
+      float4* row = grow + RW * (size_t)s.slot[cs];
 #endif
+      // -o (W/2) (a m1 + b m2) etc. with the staged A = -log2e a / 2, B = -log2e b, C = -log2e c / 2
+      const float k = o * (1.0f / 1.4426950408889634f);
       if (qq == 0) {
-        // -o (W/2) (a m1 + b m2) etc. with the staged A = -log2e a / 2, B = -log2e b, C = -log2e c / 2
-        const float k = o * (1.0f / 1.4426950408889634f);
         const float dmx = k * ddelx_dx * (2.0f * ga.z * m[1] + ga.w * m[2]);
         const float dmy = k * ddely_dy * (2.0f * gb.x * m[2] + ga.w * m[1]);
         row[0] = make_float4(dmx, dmy, -0.5f * o * m[3], -0.5f * o * m[4]);
       } else if (qq == 1) {
         row[1] = make_float4(-0.5f * o * m[5], m[0], m[6], m[7]);
       } else if (qq == 2) {
-        row[2] = make_float4(m[8], m[9], 0.f, 0.f);
+        row[2] = TWO ? make_float4(m[8], m[9], m[12 % NM], m[13 % NM]) : make_float4(m[8], m[9], 0.f, 0.f);
+      } else if (TWO) {
+        const float dmx1 = k * ddelx_dx * (2.0f * ga.z * m[10 % NM] + ga.w * m[11 % NM]);
+        const float dmy1 = k * ddely_dy * (2.0f * gb.x * m[11 % NM] + ga.w * m[10 % NM]);
+        row[3] = make_float4(m[14 % NM], dmx1, dmy1, 0.f);
       }
     }
     __syncthreads();
@@ -996,10 +1103,17 @@ void launch_render_backward(const RenderSet& rs, const GeomState& g, const uint3
                             const float* dL_dalpha, const BackwardState& bw, hipStream_t stream) {
   const int nt = rs.gx * rs.gy;
   if (nt <= 0 || rs.V <= 0) return;
-  hipLaunchKernelGGL(k_render_bwd, dim3(rs.V * tile_grid(rs.gx, rs.gy)), dim3(256), 0, stream, rs,
-                     (const uint2*)img.ranges, (const uint32_t*)img.quad_maxc, sorted_gauss,
-                     (const GaussRec*)g.rec, (const uint32_t*)g.goff, (const float*)img.final_T,
-                     (const uint32_t*)img.n_contrib, dL_dcolor, dL_ddepth, dL_dalpha, bw.grow);
+  const dim3 grid(rs.V * tile_grid(rs.gx, rs.gy));
+  if (rs.dpix2 != nullptr)
+    hipLaunchKernelGGL(k_render_bwd<true>, grid, dim3(256), 0, stream, rs, (const uint2*)img.ranges,
+                       (const uint32_t*)img.quad_maxc, sorted_gauss, (const GaussRec*)g.rec,
+                       (const uint32_t*)g.goff, (const float*)img.final_T, (const uint32_t*)img.n_contrib,
+                       dL_dcolor, dL_ddepth, dL_dalpha, bw.grow);
+  else
+    hipLaunchKernelGGL(k_render_bwd<false>, grid, dim3(256), 0, stream, rs, (const uint2*)img.ranges,
+                       (const uint32_t*)img.quad_maxc, sorted_gauss, (const GaussRec*)g.rec,
+                       (const uint32_t*)g.goff, (const float*)img.final_T, (const uint32_t*)img.n_contrib,
+                       dL_dcolor, dL_ddepth, dL_dalpha, bw.grow);
 }
 
 }  // namespace gsr

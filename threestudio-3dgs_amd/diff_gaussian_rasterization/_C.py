@@ -84,6 +84,13 @@ SIGNATURES = {
         + [_i, _vp, _sz, _vp],
     ),
     "gsr_set_render_two_colors": (_i, [_i, _i, ctypes.POINTER(_i), _i, _i, ctypes.POINTER(_vp)] + [_vp] * 11),
+    "gsr_set_backward_two_colors_bytes": (_sz, [_i, _i, ctypes.POINTER(_i)]),
+    "gsr_set_backward_two_colors": (
+        _i,
+        [_i, _i, _i, _i, ctypes.POINTER(_i), _i, _i, ctypes.POINTER(_vp), _vp, _vp, _f, _vp, _vp, _vp]
+        + [ctypes.POINTER(_vp)] * 3 + [ctypes.POINTER(_f)] * 2 + [_vp] * 4 + [_vp] * 8 + [_vp] * 9
+        + [_i, _vp, _sz, _vp],
+    ),
     "gsr_set_backward_colors": (
         _i,
         [_i, _i, ctypes.POINTER(_i), _i, _i, ctypes.POINTER(_vp), _vp, _vp, _f, _vp, _vp]

@@ -186,15 +186,35 @@ class _RasterizeViews(torch.autograd.Function):
             ga = g_alpha.float().contiguous() if g_alpha is not None else None
             stream = _C._stream(dev)
             p = _C._ptr
+            # both calls of a two-colour forward in one backward pass (gsr_set_backward_two_colors);
+            # GSR_TWO_COLOR_BWD=separate runs the second call's backward after the first's instead
+            fused2 = second and os.environ.get("GSR_TWO_COLOR_BWD", "fused") != "separate"
+            if fused2:
+                g2 = g_color2.float().contiguous()
             for si, vs in enumerate(ctx.sets):
                 Karr = _arr(ctypes.c_int, vs.K)
-                need = int(lib.gsr_set_backward_bytes(vs.V, P, Karr))
-                largest = max(int(lib.gsr_backward_bytes(P, k)) for k in vs.K)
+                if fused2:
+                    need = int(lib.gsr_set_backward_two_colors_bytes(vs.V, P, Karr))
+                    largest = max(int(lib.gsr_set_backward_two_colors_bytes(1, P, _arr(ctypes.c_int, [k])))
+                                  for k in vs.K)
+                else:
+                    need = int(lib.gsr_set_backward_bytes(vs.V, P, Karr))
+                    largest = max(int(lib.gsr_backward_bytes(P, k)) for k in vs.K)
                 work = torch.empty(max(largest, min(need, WORK_BUDGET)), dtype=torch.uint8, device=dev)
                 views, projs, campos, tx, ty = vs.cam_arrays()
                 sl = slice(vs.lo, vs.hi)
                 gdp = p(gd[sl]) if gd is not None else None
                 gap = p(ga[sl]) if ga is not None else None
+                if fused2:
+                    _C._check(lib.gsr_set_backward_two_colors(
+                        vs.V, P, int(s0.sh_degree), M, Karr, W, H, _ptrs([c[3] for c in vs.cams]), p(m3), p(sc),
+                        float(s0.scale_modifier), p(rot), p(shc), p(c3), views, projs, campos, tx, ty, p(radii[sl]),
+                        p(vs.geom), p(vs.binning), p(vs.image), p(cbg[sl]) if cbg is not None else None,
+                        p(color[sl]) if cbg is not None else None, p(gc[sl]), gdp, gap,
+                        p(d_bg[sl]) if d_bg is not None else None, p(c2), p(g2[sl]), p(d_m2[sl]), p(d_col), p(d_c2),
+                        p(d_op), p(d_m3), p(d_c3), p(d_sh), p(d_sc), p(d_rot), 1 if si > 0 else 0, p(work),
+                        work.numel(), stream))
+                    continue
                 if cbg is None:
                     _C._check(lib.gsr_set_backward(
                         vs.V, P, int(s0.sh_degree), M, Karr, W, H, _ptrs([c[3] for c in vs.cams]), p(m3), p(sc),
