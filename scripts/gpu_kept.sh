@@ -1,0 +1,8 @@
+# Full GPU parity suite, then the C3 and C5 bench lines (after a backward change).
+set -o pipefail
+mkdir -p gpurun_out
+TAG=${TAG:-kept}
+timeout -k 10 900 python -u -m pytest tests -m gpu -v -s -rf --timeout 600 --timeout-method thread > gpurun_out/${TAG}_parity.log 2>&1
+echo "pytest exit $?" >> gpurun_out/${TAG}_parity.log
+timeout -k 10 300 python -u bench.py --no-cpu-baseline --no-knn --per-view-views 0 > gpurun_out/${TAG}_bench.json 2> gpurun_out/${TAG}_bench.log || exit 1
+timeout -k 10 300 python -u bench.py --workload sugar --no-cpu-baseline --no-knn > gpurun_out/${TAG}_bench_sugar.json 2> gpurun_out/${TAG}_bench_sugar.log

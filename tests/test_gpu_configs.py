@@ -377,10 +377,11 @@ def test_second_colors_match_separate_call(bwd, monkeypatch):
     geometry, sorts and blend — against the two separate calls (renderer/diff_sugar_rasterizer_normal.py:
     157-191): the second colour image bitwise equal, the first call's outputs and means2D gradient bitwise
     equal; parameter gradients (summed over both calls) within 1e-5 relative when the backward runs the two
-    calls one after the other (GSR_TWO_COLOR_BWD=separate), within the gradient bar 1e-4 max(1, |g|) for the
-    one-pass two-colour backward (gsr_set_backward_two_colors: both calls' dL/dalpha are added per pixel
-    before the moments and the chain rule, an fp32 reassociation of the two-call sum; measured 4.8e-5;
-    test_c5_sugar_normal_renderer holds it to the fp64 oracle)."""
+    calls one after the other (GSR_TWO_COLOR_BWD=separate).  The one-pass two-colour backward
+    (gsr_set_backward_two_colors) adds both calls' dL/dalpha per pixel before the moments and the chain
+    rule, an fp32 reassociation of the two-call sum (measured up to 1.6e-4 max(1, |g|) apart from the
+    two-call sequence where the calls' gradients cancel): it is held to the fp64 oracle's two summed
+    backward passes with the gradient bar of every parity test (check_grads)."""
     import torch
 
     monkeypatch.setenv("GSR_TWO_COLOR_BWD", bwd)
@@ -395,7 +396,7 @@ def test_second_colors_match_separate_call(bwd, monkeypatch):
     ups = [torch.tensor(rng.standard_normal((3, 3, 112, 144)).astype(np.float32), device="cuda") for _ in range(3)]
     dev = "cuda"
 
-    def run(fused):
+    def run(fused, part=None):
         t = {k: torch.tensor(scene[k], device=dev, requires_grad=True)
              for k in ("means3D", "scales", "rotations", "opacities", "shs")}
         t["normals"] = torch.tensor(normals, device=dev, requires_grad=True)
@@ -408,16 +409,42 @@ def test_second_colors_match_separate_call(bwd, monkeypatch):
             c, r, d, a = rasterize_views(st, t["means3D"], m2, shs=t["shs"], **common)
             z = [torch.zeros((15_000, 3), device=dev) for _ in cams]
             c2, _, _, _ = rasterize_views(st, t["means3D"], z, colors_precomp=t["normals"], **common)
-        ((c * ups[0]).sum() + (d * ups[1][:, :1]).sum() + (a * ups[1][:, 1:2]).sum() + (c2 * ups[2]).sum()).backward()
+        l1 = (c * ups[0]).sum() + (d * ups[1][:, :1]).sum() + (a * ups[1][:, 1:2]).sum()
+        l2 = (c2 * ups[2]).sum()
+        (l1 + l2 if part is None else l1 if part == 1 else l2).backward()
+        grad = lambda v: v.grad.clone() if v.grad is not None else torch.zeros_like(v)  # noqa: E731
         return dict(c=c.detach(), c2=c2.detach(), d=d.detach(), a=a.detach(), r=r,
-                    m2=[m.grad.clone() for m in m2], g={k: v.grad.clone() for k, v in t.items()})
+                    m2=[grad(m) for m in m2], g={k: grad(v) for k, v in t.items()})
 
     f, s_ = run(True), run(False)
     for k in ("c", "c2", "d", "a", "r"):
         assert torch.equal(f[k], s_[k]), k
     for v in range(3):
         assert torch.equal(f["m2"][v], s_["m2"][v])
-    for k in f["g"]:
-        ref = s_["g"][k].double()
-        err = float(((f["g"][k].double() - ref).abs() / ref.abs().clamp(min=1.0)).max())
-        assert err <= (1e-4 if bwd == "fused" else 1e-5), f"grad {k}: {err}"
+    if bwd == "separate":
+        for k in f["g"]:
+            ref = s_["g"][k].double()
+            err = float(((f["g"][k].double() - ref).abs() / ref.abs().clamp(min=1.0)).max())
+            assert err <= 1e-5, f"grad {k}: {err}"
+        return
+    # the one-pass backward against the oracle's two backward passes, summed over the views (fp32 / fp64)
+    bg = np.array([0.2, 0.4, 0.6], np.float32)
+    sc2 = dict(scene, colors_precomp=normals)
+    sc2.pop("shs")
+    ref = {}
+    for prec in ("f32", "f64"):
+        acc = {}
+        for v, cam in enumerate(cams):
+            u0, u1, u2 = (ups[i][v].cpu().numpy() for i in range(3))
+            b1 = oracle.backward(scene, oracle_cam(cam), bg, u0, u1[:1], u1[1:2], prec=prec)
+            b2 = oracle.backward(sc2, oracle_cam(cam), bg, u2, None, None, prec=prec)
+            terms = {k: np.asarray(b1[k], np.float64) + np.asarray(b2[k], np.float64)
+                     for k in ("means3D", "scales", "rotations", "opacity")}
+            terms["sh"], terms["normals"] = np.asarray(b1["sh"], np.float64), np.asarray(b2["colors"], np.float64)
+            for k, x in terms.items():
+                acc[k] = acc.get(k, 0.0) + x
+        ref["b32" if prec == "f32" else "b64"] = acc
+    gpu = {"g_" + k: f["g"][src].cpu().numpy() for k, src in (("means3D", "means3D"), ("scales", "scales"),
+           ("rotations", "rotations"), ("opacity", "opacities"), ("sh", "shs"), ("normals", "normals"))}
+    check_grads(gpu, ref, ["means3D", "scales", "rotations", "opacity", "sh", "normals"], "two-colour backward")
+    print_report()
