@@ -38,7 +38,7 @@ def main():
     bg_img = torch.rand((V, R, R, 3), generator=gen, device=dev)
     ups = [torch.randn((V, 3, R, R), generator=gen, device=dev), torch.randn((V, 1, R, R), generator=gen, device=dev),
            torch.randn((V, 1, R, R), generator=gen, device=dev)]
-    buf = np.zeros(4, np.uint64)
+    buf = np.zeros(5, np.uint64)
     for it in range(2):  # the second pass is the counted one
         assert lib.gsr_diag_pairs(buf.ctypes.data, 1) == 0
         _C.RECENT_LISTED.clear()
@@ -63,6 +63,8 @@ def main():
         "bwd_pairs_replayed_per_view": float(buf[2]) / V,
         "bwd_lockstep_pair_slots_per_view": float(buf[3]) / V,
         "bwd_lockstep_slots_per_kept_pair": float(buf[3]) / max(1.0, float(buf[2])),
+        # lower bound of any batch-level rebalancing (ring, larger batches): the tile's busiest quadrant
+        "bwd_tile_bound_slots_per_kept_pair": float(buf[4]) / max(1.0, float(buf[2])),
         "mean_listed_instances": listed,
         "note": "fwd evaluated = (pixel, candidate) iterations of lanes not yet terminated; slots include "
                 "terminated lanes; bwd pairs = kept (candidate, 8x8 quadrant) pairs x 64 pixels",

@@ -36,7 +36,7 @@ __device__ uint4 g_timeline[2][GSR_TL_MAX];
 // evaluated (lanes not yet terminated), [1] forward pair slots issued (64 lanes x candidates walked),
 // [2] backward kept (candidate, quadrant) pairs replayed x 64 pixels, [3] backward pair slots of the
 // lockstep batches (4 x the busiest quadrant's kept count x 64)
-__device__ unsigned long long g_pairs[4];
+__device__ unsigned long long g_pairs[8];
 #define GSR_TL_BEGIN const uint32_t tl_t0 = (uint32_t)__builtin_amdgcn_s_memrealtime();
 #define GSR_TL_END(which, work)                                                                  \
   if (threadIdx.x == 0 && blockIdx.x < GSR_TL_MAX)                                                \
@@ -361,6 +361,9 @@ struct BwdLDS {
 #ifdef GSR_TIMELINE
   int tl_cnt[4];
 #endif
+#ifdef GSR_EXP_LDSPAD
+  char pad[GSR_EXP_LDSPAD];  // timing only: occupancy sensitivity (fewer workgroups per CU)
+#endif
 };
 
 __host__ __device__ __forceinline__ int tile_grid(int gx, int gy) {
@@ -652,6 +655,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(TWO ? 4 : 5
   }
   const float* bg = rs.bg[v];
   int tl_work = 0, tl_max = 0;
+  int tl_q[4] = {0, 0, 0, 0};  // per-quadrant kept totals of the tile (the per-tile imbalance bound)
   const int t = threadIdx.x, q = t >> 6, lane = t & 63;
   const int txi = tile % grid_x, tyi = tile / grid_x;
   const int qx0 = txi * GSR_TILE_X + (q & 1) * 8;
@@ -1011,6 +1015,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(TWO ? 4 : 5
       const int c0 = s.tl_cnt[0], c1 = s.tl_cnt[1], c2 = s.tl_cnt[2], c3 = s.tl_cnt[3];
       tl_work += c0 + c1 + c2 + c3;                                  // kept (candidate, quadrant) pairs
       tl_max += 4 * max(max(c0, c1), max(c2, c3));                  // lockstep cost in pair slots
+      tl_q[0] += c0, tl_q[1] += c1, tl_q[2] += c2, tl_q[3] += c3;
     }
 #endif
 #ifdef GSR_EXP_NOFLUSH
@@ -1088,6 +1093,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(TWO ? 4 : 5
   if (threadIdx.x == 0) {
     atomicAdd(&g_pairs[2], 64ull * (unsigned long long)tl_work);
     atomicAdd(&g_pairs[3], 64ull * (unsigned long long)tl_max);
+    // any batch-level scheme still waits for the tile's busiest quadrant: 4 x its total
+    atomicAdd(&g_pairs[4], 256ull * (unsigned long long)max(max(tl_q[0], tl_q[1]), max(tl_q[2], tl_q[3])));
   }
   if (threadIdx.x == 0 && blockIdx.x < GSR_TL_MAX)
     g_timeline[1][blockIdx.x] = make_uint4(tl_t0, (uint32_t)__builtin_amdgcn_s_memrealtime(), (uint32_t)tl_max,
@@ -1096,6 +1103,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(TWO ? 4 : 5
 #endif
   (void)tl_work;
   (void)tl_max;
+  (void)tl_q;
 }
 
 void launch_render_backward(const RenderSet& rs, const GeomState& g, const uint32_t* sorted_gauss,
@@ -1119,14 +1127,14 @@ void launch_render_backward(const RenderSet& rs, const GeomState& g, const uint3
 }  // namespace gsr
 
 #ifdef GSR_TIMELINE
-// diagnostic build only: read (and optionally reset) the pair counters (4 x u64, see g_pairs)
+// diagnostic build only: read (and optionally reset) the pair counters (5 x u64, see g_pairs)
 extern "C" int gsr_diag_pairs(void* host, int reset) {
   if (hipDeviceSynchronize() != hipSuccess) return -1;
-  if (hipMemcpyFromSymbol(host, HIP_SYMBOL(gsr::g_pairs), 4 * sizeof(unsigned long long), 0,
+  if (hipMemcpyFromSymbol(host, HIP_SYMBOL(gsr::g_pairs), 5 * sizeof(unsigned long long), 0,
                           hipMemcpyDeviceToHost) != hipSuccess)
     return -1;
   if (reset) {
-    const unsigned long long z[4] = {0, 0, 0, 0};
+    const unsigned long long z[5] = {0, 0, 0, 0, 0};
     if (hipMemcpyToSymbol(HIP_SYMBOL(gsr::g_pairs), z, sizeof(z), 0, hipMemcpyHostToDevice) != hipSuccess) return -1;
   }
   return 0;
