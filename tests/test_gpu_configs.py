@@ -448,3 +448,44 @@ def test_second_colors_match_separate_call(bwd, monkeypatch):
            ("rotations", "rotations"), ("opacity", "opacities"), ("sh", "shs"), ("normals", "normals"))}
     check_grads(gpu, ref, ["means3D", "scales", "rotations", "opacity", "sh", "normals"], "two-colour backward")
     print_report()
+
+
+def test_two_color_backward_groups_and_sets_bitwise(monkeypatch):
+    """The one-pass two-colour backward (gsr_set_backward_two_colors) walked in view groups that fit a small
+    work buffer, and over several view sets (accumulate: dL/dcolors2 and the running dL/dcov3D continue in
+    view order): bitwise the gradients of one group / one set."""
+    import torch
+
+    from diff_gaussian_rasterization import batched
+
+    scene = gs.make_scene(12_000, sh_degree=1, seed=61)
+    rng = np.random.default_rng(6)
+    n = rng.normal(size=(12_000, 3)).astype(np.float32)
+    normals = n / np.linalg.norm(n, axis=1, keepdims=True)
+    cams = [make_camera(128, 96, elevation=8.0 * i, azimuth=50.0 * i) for i in range(6)]
+    ups = [torch.tensor(rng.standard_normal((6, 3, 96, 128)).astype(np.float32), device="cuda") for _ in range(3)]
+
+    def run():
+        t = {k: torch.tensor(scene[k], device="cuda", requires_grad=True)
+             for k in ("means3D", "scales", "rotations", "opacities", "shs")}
+        t["normals"] = torch.tensor(normals, device="cuda", requires_grad=True)
+        st = [_settings(c, [0.1, 0.2, 0.3], 1) for c in cams]
+        m2 = [torch.zeros((12_000, 3), device="cuda", requires_grad=True) for _ in cams]
+        c, _, d, a, c2 = batched.rasterize_views(st, t["means3D"], m2, t["opacities"], shs=t["shs"],
+                                                 scales=t["scales"], rotations=t["rotations"], colors2=t["normals"])
+        ((c * ups[0]).sum() + (d * ups[1][:, :1]).sum() + (a * ups[1][:, 1:2]).sum() + (c2 * ups[2]).sum()).backward()
+        torch.cuda.synchronize()
+        return [m.grad.clone() for m in m2], {k: v.grad.clone() for k, v in t.items()}
+
+    m2_one, g_one = run()
+    with monkeypatch.context() as mp:
+        mp.setattr(batched, "WORK_BUDGET", 1)  # one view per group
+        m2_grp, g_grp = run()
+    with monkeypatch.context() as mp:
+        mp.setattr(batched, "SET_MAX", 2)  # three sets of two views
+        m2_set, g_set = run()
+    for other, what in ((g_grp, "groups"), (g_set, "sets")):
+        for k in g_one:
+            assert torch.equal(g_one[k], other[k]), f"{what}: grad {k}"
+    for v in range(6):
+        assert torch.equal(m2_one[v], m2_grp[v]) and torch.equal(m2_one[v], m2_set[v]), f"means2D {v}"
