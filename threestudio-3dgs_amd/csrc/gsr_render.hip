@@ -656,7 +656,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(TWO ? 4 : 5
   const float* bg = rs.bg[v];
   int tl_work = 0, tl_max = 0;
   int tl_q[4] = {0, 0, 0, 0};  // per-quadrant kept totals of the tile (the per-tile imbalance bound)
-  const int t = threadIdx.x, q = t >> 6, lane = t & 63;
+  // (the wave's quadrant is wave-uniform: readfirstlane keeps it and what derives from it in scalars)
+  const int t = threadIdx.x, q = __builtin_amdgcn_readfirstlane(t >> 6), lane = t & 63;
   const int txi = tile % grid_x, tyi = tile / grid_x;
   const int qx0 = txi * GSR_TILE_X + (q & 1) * 8;
   const int qy0 = tyi * GSR_TILE_Y + (q >> 1) * 8;
