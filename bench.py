@@ -243,6 +243,9 @@ def render_views_sugar(rep: Replica, settings, shade):
     return color.clamp(0, 1), depth, alpha, nmap, nmap_dist
 
 
+PROFILE_VIEWS_PER_LAUNCH = 64  # profiles/run_profiles.sh: bench.py defaults, one 64-view set per launch
+
+
 def read_traffic(path, kernel, field="per_launch_bytes"):
     """Per-launch value of `kernel` (a name or a list of names, first found wins) from a committed PMC
     summary (profiles/summarize.py): HBM bytes (FETCH_SIZE x2 gfx950 correction + WRITE_SIZE, separate
@@ -404,13 +407,19 @@ def roofline_fields(args, phases, Ks, Ls, H, W):
     instruction per SIMD per 2 cycles, 157.3 TF fp32 as FMAs) and the device-counted pairs
     (profiles/<tag>_pairs.json, diagnostic build): the blends are issue / latency bound, not HBM bound."""
     tiles = math.ceil(W / 16) * math.ceil(H / 16)
-    pairs = read_json(args.pairs)
+    # the committed counters (profiles/run_profiles.sh) are of bench.py's default workload at N = 1: one
+    # 64-view launch per blend.  Other workloads get no counter fields; a rank of an N > 1 run launches
+    # fewer views: the per-launch counts scale with the views (per-view work is the same)
+    profiled = (args.workload == "c3" and args.epilogue == "background" and args.res == 1024
+                and args.gaussians == 1_000_000 and args.sh_degree == 3 and args.path == "batched")
+    pairs = read_json(args.pairs) if profiled else None
     out = {}
     n_fw = max(1, len(Ks))
     rows = {}
     # the forward of this workload: the tile-wave kernel when Gaussians span >= 3 tiles (gsr_render.hip)
     fwd_names = ["k_render_fwd_tile<false>", "k_render_fwd<false>", "k_render_fwd"]
-    for phase, kernel in (("render_fwd", fwd_names), ("render_bwd", "k_render_bwd")):
+    bwd_names = ["k_render_bwd<false>", "k_render_bwd"]
+    for phase, kernel in (("render_fwd", fwd_names), ("render_bwd", bwd_names)):
         ms, n = phases[phase]
         n = max(1, n)
         if phase == "render_fwd":
@@ -419,10 +428,14 @@ def roofline_fields(args, phases, Ks, Ls, H, W):
             alg = (44.0 * sum(Ls) + 32.0 * H * W * n_fw) / n
         sec = ms / n * 1e-3
         gbs = alg / sec / 1e9 if sec > 0 else 0.0
-        traffic = read_traffic(args.traffic, kernel)
-        valu = read_traffic(args.traffic, kernel, "valu_insts_per_launch")
         views_per_launch = n_fw / n
-        r = {"kernel": kernel if isinstance(kernel, str) else "k_render_fwd (tile / quadrant waves)", "bound": "hbm",
+        scale = views_per_launch / PROFILE_VIEWS_PER_LAUNCH
+        traffic = read_traffic(args.traffic, kernel) if profiled else None
+        valu = read_traffic(args.traffic, kernel, "valu_insts_per_launch") if profiled else None
+        traffic = round(traffic * scale) if traffic is not None else None
+        valu = round(valu * scale) if valu is not None else None
+        r = {"kernel": "k_render_bwd" if phase == "render_bwd" else "k_render_fwd (tile / quadrant waves)",
+             "bound": "hbm",
              "achieved": round(gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
              "frac": round(gbs / HBM_PEAK_GBS, 4), "traffic": traffic, "avg_launch_us": round(1e6 * sec, 2),
              "algorithmic_bytes": round(alg), "views_per_launch": round(views_per_launch, 2)}
@@ -451,9 +464,13 @@ def roofline_fields(args, phases, Ks, Ls, H, W):
         r["limiter"] = "VALU issue / LDS latency per (pixel, Gaussian) pair, not HBM (see counter_frac, valu)"
         rows[phase] = r
     dominant = max(phases.items(), key=lambda kv: kv[1][0])[0]
-    out["roofline"] = rows["render_bwd"] if dominant == "render_bwd" else rows["render_fwd"]
+    blend = "render_bwd" if phases["render_bwd"][0] >= phases["render_fwd"][0] else "render_fwd"
+    out["roofline"] = rows[blend]
     out["roofline_fwd_blend"] = rows["render_fwd"]
     out["dominant_kernel"] = dominant
+    if not profiled:
+        out["counters_note"] = ("no counter fields: profiles/ holds PMC counters of the default workload "
+                                "(C3 background path, 1M, 1024^2) only")
     out["roofline_note"] = ("frac = SURVEY.md §8d algorithmic bytes / HIP-event duration (backward without the "
                             "reference's 80 B/instance atomic RMW, never performed here); counter_frac = PMC HBM "
                             "bytes / duration; valu_frac = SQ_INSTS_VALU / (duration x VALU issue peak). Both "
