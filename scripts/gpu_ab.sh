@@ -1,5 +1,6 @@
 # A/B of an experiment build against the product on one workload (alternated; timing only).
-# usage: EXP=<build_exp_ suffix> WL=<c3|sugar> bash scripts/gpu_ab.sh
+# usage: EXP=<build_exp_ suffix> WL=<c3|sugar> bash scripts/gpu_ab.sh, after (CPU side)
+#   make -C threestudio-3dgs_amd/csrc OBJDIR=build_exp_<X> OUT=build_exp_<X>/libgsr_hip.so EXTRA=-DGSR_EXP_<X>
 set -o pipefail
 mkdir -p gpurun_out
 OUTF=gpurun_out/ab_${EXP}_${WL}.txt

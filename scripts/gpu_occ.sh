@@ -1,5 +1,7 @@
 # Occupancy sensitivity of the backward blend (LDS padding: 5 -> 4 -> 3 workgroups per CU; timing only)
-# and the per-tile quadrant-imbalance bound (diagnostic build).
+# and the per-tile quadrant-imbalance bound (diagnostic build).  Build first (CPU side):
+#   for p in 8192 22000; do make -C threestudio-3dgs_amd/csrc OBJDIR=build_exp_PAD$p OUT=build_exp_PAD$p/libgsr_hip.so \
+#     EXTRA=-DGSR_EXP_LDSPAD=$p; done; make -C threestudio-3dgs_amd/csrc diag
 set -o pipefail
 mkdir -p gpurun_out
 OUTF=gpurun_out/occ.txt
