@@ -489,3 +489,65 @@ def test_two_color_backward_groups_and_sets_bitwise(monkeypatch):
             assert torch.equal(g_one[k], other[k]), f"{what}: grad {k}"
     for v in range(6):
         assert torch.equal(m2_one[v], m2_grp[v]) and torch.equal(m2_one[v], m2_set[v]), f"means2D {v}"
+
+
+def test_two_color_backward_with_fused_composite():
+    """rasterize_views(background=..., colors2=...): the background renderer's fused composite on the first
+    colour set and a second colour set in the same forward and the same one-pass backward
+    (gsr_set_render_two_colors / gsr_set_backward_two_colors with bg_images): the parameter, background and
+    colors2 gradients against the fp64 oracle's two backward passes with the composite's upstream gradients
+    (renderer/diff_gaussian_rasterizer_background.py:129-132,139 restated in _composite_upstream)."""
+    import torch
+
+    from diff_gaussian_rasterization.batched import rasterize_views
+
+    P = 15_000
+    scene = gs.make_scene(P, sh_degree=1, seed=71)
+    rng = np.random.default_rng(8)
+    n = rng.normal(size=(P, 3)).astype(np.float32)
+    normals = n / np.linalg.norm(n, axis=1, keepdims=True)
+    cams = [make_camera(144, 112, elevation=12.0 * i, azimuth=80.0 * i) for i in range(2)]
+    bg_img = rng.random((2, 112, 144, 3)).astype(np.float32)
+    ups = [rng.standard_normal((2, 3, 112, 144)).astype(np.float32) for _ in range(3)]
+    dev = "cuda"
+    t = {k: torch.tensor(scene[k], device=dev, requires_grad=True)
+         for k in ("means3D", "scales", "rotations", "opacities", "shs")}
+    t["normals"] = torch.tensor(normals, device=dev, requires_grad=True)
+    bg_t = torch.tensor(bg_img, device=dev, requires_grad=True)
+    st = [_settings(c, [0.0, 0.0, 0.0], 1) for c in cams]
+    m2 = [torch.zeros((P, 3), device=dev, requires_grad=True) for _ in cams]
+    render, _, d, a, c2 = rasterize_views(st, t["means3D"], m2, t["opacities"], shs=t["shs"], scales=t["scales"],
+                                          rotations=t["rotations"], background=bg_t, colors2=t["normals"])
+    u = [torch.tensor(x, device=dev) for x in ups]
+    ((render * u[0]).sum() + (d * u[1][:, :1]).sum() + (a * u[1][:, 1:2]).sum() + (c2 * u[2]).sum()).backward()
+
+    sc2 = dict(scene, colors_precomp=normals)
+    sc2.pop("shs")
+    zero = np.zeros(3, np.float32)
+    ref = {"b32": {}, "b64": {}}
+    for v, cam in enumerate(cams):
+        fw = run_oracle(scene, cam, [0.0, 0.0, 0.0])
+        g_r, g_d, g_a = ups[0][v], ups[1][v][:1], ups[1][v][1:2]
+        bgs = {}
+        for prec, dt in (("f32", np.float32), ("f64", np.float64)):
+            f = fw[prec]
+            _, pre = _composite(f["color"].astype(dt), f["alpha"].astype(dt), bg_img[v].astype(dt))
+            gcol, ga = _composite_upstream(g_r, g_a, pre, bg_img[v])
+            b1 = oracle.backward(scene, oracle_cam(cam), zero, gcol, g_d, ga, prec=prec)
+            b2 = oracle.backward(sc2, oracle_cam(cam), zero, ups[2][v], None, None, prec=prec)
+            acc = ref["b32" if prec == "f32" else "b64"]
+            terms = {k: np.asarray(b1[k], np.float64) + np.asarray(b2[k], np.float64)
+                     for k in ("means3D", "scales", "rotations", "opacity")}
+            terms["sh"], terms["normals"] = np.asarray(b1["sh"], np.float64), np.asarray(b2["colors"], np.float64)
+            for k, x in terms.items():
+                acc[k] = acc.get(k, 0.0) + x
+            bgs[prec] = (gcol * (dt(1) - f["alpha"].astype(dt))).transpose(1, 2, 0).reshape(-1, 3)
+            bgs["m2_" + prec] = b1["means2D"]
+        adjudicate(bg_t.grad[v].detach().cpu().numpy().reshape(-1, 3), bgs["f32"], bgs["f64"],
+                   1e-4 * np.maximum(1.0, np.abs(bgs["f64"])), f"two colours + composite view {v}", "grad background")
+        adjudicate(m2[v].grad.cpu().numpy(), bgs["m2_f32"], bgs["m2_f64"],
+                   1e-4 * np.maximum(1.0, np.abs(bgs["m2_f64"])), f"two colours + composite view {v}", "grad means2D")
+    gpu = {"g_" + k: t[src].grad.cpu().numpy() for k, src in (("means3D", "means3D"), ("scales", "scales"),
+           ("rotations", "rotations"), ("opacity", "opacities"), ("sh", "shs"), ("normals", "normals"))}
+    check_grads(gpu, ref, ["means3D", "scales", "rotations", "opacity", "sh", "normals"], "two colours + composite")
+    print_report()
