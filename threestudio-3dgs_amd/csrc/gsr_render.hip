@@ -576,13 +576,17 @@ __global__ __launch_bounds__(64) void k_render_fwd_tile(RenderSet rs, const uint
 // Which forward: the tile-wave kernel gathers each candidate once but walks a quadrant's candidates one
 // branch at a time and the whole tile list to the tile's deepest termination; it wins when Gaussians span
 // several tiles (C3: 6.7 rectangle tiles per Gaussian, render_fwd -3 %), the quadrant-wave kernel when
-// they are small (C5 SuGaR, 1.7 tiles per Gaussian: the tile kernel is 1.6x slower).  Both give identical
-// outputs.  GSR_FWD_KERNEL=tile|quadrant forces one (A/B and tests).
-static bool fwd_tile_kernel(long long instances, long long gaussians) {
+// they are small (C5 SuGaR, 1.7 tiles per Gaussian: the tile kernel is 1.6x slower).  A launch's duration
+// is also bounded by its slowest wave — a heavy tile's whole list for the tile kernel, only a quadrant's
+// for the other — which many views hide: at C3 the tile kernel needs >= 48 views per launch (ms / view,
+// tile vs quadrant: 1 view 0.298 vs 0.124, 8 views 0.076 vs 0.060, 32 views 0.054 vs 0.052, 64 views 0.050
+// vs 0.052; profiles/r02_fwd_kernel_ab.txt).  Both give identical outputs.  GSR_FWD_KERNEL=tile|quadrant
+// forces one (A/B and tests).
+static bool fwd_tile_kernel(long long instances, long long gaussians, int views) {
   const char* e = getenv("GSR_FWD_KERNEL");
   if (e != nullptr && strcmp(e, "quadrant") == 0) return false;
   if (e != nullptr && strcmp(e, "tile") == 0) return true;
-  return gaussians > 0 && instances >= 3 * gaussians;
+  return views >= 48 && gaussians > 0 && instances >= 3 * gaussians;
 }
 
 void launch_render_forward(const RenderSet& rs, const GeomState& g, const uint32_t* sorted_gauss,
@@ -590,7 +594,7 @@ void launch_render_forward(const RenderSet& rs, const GeomState& g, const uint32
                            long long instances, hipStream_t stream) {
   const int nt = rs.gx * rs.gy;
   if (nt <= 0 || rs.V <= 0) return;
-  if (fwd_tile_kernel(instances, (long long)rs.V * rs.P)) {
+  if (fwd_tile_kernel(instances, (long long)rs.V * rs.P, rs.V)) {
     const dim3 grid(rs.V * tile_grid(rs.gx, rs.gy));
     if (rs.col2 != nullptr)
       hipLaunchKernelGGL(k_render_fwd_tile<true>, grid, dim3(64), 0, stream, rs, (const uint2*)img.ranges,
