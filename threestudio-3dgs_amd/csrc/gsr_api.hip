@@ -425,6 +425,7 @@ static int set_render(int V, int P, const int* K, int width, int height, const f
       if (res != tres) return fail(GSR_EHIP, "%s", "internal: tile sort buffer");
       launch_tile_ranges(inst, gx * gy, tp.gbits, b.key[res], img.ranges, s);
     }
+    launch_tile_order(V, gx, gy, img.ranges, img.order, s);  // always written: the backward may use it
   }
   {
     PhaseScope ps(GSR_PHASE_RENDER_FWD, s);
@@ -436,6 +437,7 @@ static int set_render(int V, int P, const int* K, int width, int height, const f
     rs.col2 = colors2;
     rs.out_col2 = out_color2;
     rs.dpix2 = nullptr;
+    rs.order = tile_order_on() ? img.order : nullptr;
     rs.V = V;
     rs.v0 = 0;
     rs.P = P;
@@ -547,6 +549,7 @@ static int set_backward(int V, int P, int degree, int M, const int* K, int width
     rs.col2 = two ? colors2 : colors_override;
     rs.out_col2 = nullptr;
     rs.dpix2 = two ? dL_dcolor2 + (size_t)g0 * 3 * HW : nullptr;
+    rs.order = tile_order_on() ? img.order : nullptr;
     rs.V = g1 - g0;
     rs.v0 = g0;
     rs.P = P;

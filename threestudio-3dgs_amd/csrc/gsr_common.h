@@ -249,6 +249,8 @@ struct ImageState {
   uint2* cut;          // [V][tiles] (depth key, Gaussian) of tile_info: the backward gather's cut-off table
   float* final_T;      // [V][H*W]
   uint32_t* n_contrib; // [V][H*W]
+  uint32_t* order;     // [V][super-tiles] each view's 2x2-tile super-tiles, most listed instances first
+                       // (written after binning; the blends' dispatch order, gsr_render.hip block_map)
   static ImageState carve(void* base, int V, int W, int H, size_t* bytes) {
     Carver c(base);
     ImageState s;
@@ -261,6 +263,8 @@ struct ImageState {
     s.cut = c.take<uint2>(nv * (tiles > 0 ? tiles : 1));
     s.final_T = c.take<float>(nv * (pix > 0 ? pix : 1));
     s.n_contrib = c.take<uint32_t>(nv * (pix > 0 ? pix : 1));
+    const size_t st = (size_t)((div_up(W, GSR_TILE_X) + 1) >> 1) * ((div_up(H, GSR_TILE_Y) + 1) >> 1);
+    s.order = c.take<uint32_t>(nv * (st > 0 ? st : 1));
     if (bytes) *bytes = align_up(c.off, 256);
     return s;
   }

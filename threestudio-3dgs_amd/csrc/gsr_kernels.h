@@ -59,7 +59,13 @@ struct RenderSet {
   // backward of both calls in one pass: dL/d(second colour image) (V, 3, H, W) at the launch's first
   // view; col2 then holds the second colours and the records keep the first (null = off)
   const float* dpix2;
+  // dispatch order (ImageState::order of the set, indexed by v0 + v): null = views in turn, raster order
+  const uint32_t* order;
 };
+// Each view's super-tiles by listed instances, heaviest first (after binning) — gsr_render.hip
+void launch_tile_order(int V, int gx, int gy, const uint2* ranges, uint32_t* order, hipStream_t stream);
+// GSR_TILE_ORDER=raster: the blends dispatch views in turn in raster order (A/B); the order is still written
+bool tile_order_on();
 // instances: the set's rectangle tiles (sum of K) — picks the forward kernel (gsr_render.hip)
 void launch_render_forward(const RenderSet& rs, const GeomState& g, const uint32_t* sorted_gauss,
                            const ImageState& img, float* out_color, float* out_depth, float* out_alpha,

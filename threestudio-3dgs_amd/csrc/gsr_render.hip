@@ -49,22 +49,44 @@ __device__ unsigned long long g_pairs[8];
 #define GSR_TL_END(which, work)
 #endif
 
-__host__ __device__ __forceinline__ int unit_grid(int gx, int gy) {
-  const int S = ((gx + 1) >> 1) * ((gy + 1) >> 1);
-  return 128 * ((S + 7) >> 3);
-}
-__device__ __forceinline__ bool unit_of_block(int b, int gx, int gy, int& tile, int& q) {
-  const int sgx = (gx + 1) >> 1, sgy = (gy + 1) >> 1;
-  const int x = b & 7, k = b >> 3;
-  const int s = ((k >> 4) << 3) + x;
-  const int w = k & 15;
-  if (s >= sgx * sgy) return false;
-  const int tx = (s % sgx) * 2 + ((w >> 2) & 1), ty = (s / sgx) * 2 + (w >> 3);
-  if (tx >= gx || ty >= gy) return false;
-  tile = ty * gx + tx;
+// blockIdx -> (view of the launch, tile, quadrant) for PER blocks per 2x2-tile super-tile (4: a workgroup
+// per tile; 16: a wave per 8x8 quadrant).  Groups of 8 consecutive super-tiles are dealt one to each XCD
+// (x = b & 7) with all blocks of a super-tile on the same XCD (its tiles share Gaussians in L2).  With an
+// order (rs.order): dispatch position m interleaves the launch's views (m % V) and walks each view's
+// super-tiles heaviest first (m / V) — a launch lasts at least its slowest workgroup, so the long tiles
+// start first and the short ones fill the tail.  Without: the views in turn, super-tiles in raster order.
+template <int PER>
+__device__ __forceinline__ bool block_map(int b, const RenderSet& rs, int& v, int& tile, int& q) {
+  const int sgx = (rs.gx + 1) >> 1, sgy = (rs.gy + 1) >> 1, S = sgx * sgy;
+  int s, w;
+  if (rs.order != nullptr) {
+    const int x = b & 7, k = b >> 3;
+    w = k & (PER - 1);
+    const int m = ((k / PER) << 3) + x;
+    if (m >= rs.V * S) return false;
+    v = m % rs.V;
+    s = (int)rs.order[(size_t)(rs.v0 + v) * S + m / rs.V];
+  } else {
+    const int G = PER * 8 * ((S + 7) >> 3);
+    v = b / G;
+    const int bl = b - v * G, x = bl & 7, k = bl >> 3;
+    w = k & (PER - 1);
+    s = ((k / PER) << 3) + x;
+    if (s >= S) return false;
+  }
+  const int tx = (s % sgx) * 2 + (PER == 16 ? (w >> 2) & 1 : w & 1);
+  const int ty = (s / sgx) * 2 + (PER == 16 ? w >> 3 : w >> 1);
+  if (tx >= rs.gx || ty >= rs.gy) return false;
+  tile = ty * rs.gx + tx;
   q = w & 3;
   return true;
 }
+// launch sizes for block_map
+static int block_grid(const RenderSet& rs, int per) {
+  const int S = ((rs.gx + 1) >> 1) * ((rs.gy + 1) >> 1);
+  return rs.order != nullptr ? per * 8 * div_up((long long)rs.V * S, 8) : rs.V * per * 8 * ((S + 7) >> 3);
+}
+
 
 __device__ __forceinline__ void tile_pixel(int t, int& lx, int& ly) {
   const int w = t >> 6, l = t & 63;
@@ -129,10 +151,8 @@ __global__ __launch_bounds__(64) void k_render_fwd(RenderSet rs,
   // 65 slots: the loop reads candidate k+1 while blending k (slot 64 is never used)
   __shared__ float4 s0[65], s1[65], s2[65];
   __shared__ float4 s3[C2 ? 65 : 1];  // the second colour (C2)
-  const int U = unit_grid(rs.gx, rs.gy);
-  const int v = blockIdx.x / U;
-  int tile, q;
-  if (!unit_of_block(blockIdx.x - v * U, rs.gx, rs.gy, tile, q)) return;
+  int v, tile, q;
+  if (!block_map<16>(blockIdx.x, rs, v, tile, q)) return;
   GSR_TL_BEGIN
   const int W = rs.W, H = rs.H, grid_x = rs.gx;
   {
@@ -366,22 +386,6 @@ struct BwdLDS {
 #endif
 };
 
-__host__ __device__ __forceinline__ int tile_grid(int gx, int gy) {
-  const int S = ((gx + 1) >> 1) * ((gy + 1) >> 1);
-  return 32 * ((S + 7) >> 3);
-}
-// blockIdx -> tile: 2x2-tile super-tiles dealt round-robin over the 8 XCD groups (as unit_of_block)
-__device__ __forceinline__ bool tile_of_block(int b, int gx, int gy, int& tile) {
-  const int sgx = (gx + 1) >> 1, sgy = (gy + 1) >> 1;
-  const int x = b & 7, k = b >> 3;
-  const int s = ((k >> 2) << 3) + x;
-  const int w = k & 3;
-  if (s >= sgx * sgy) return false;
-  const int tx = (s % sgx) * 2 + (w & 1), ty = (s / sgx) * 2 + (w >> 1);
-  if (tx >= gx || ty >= gy) return false;
-  tile = ty * gx + tx;
-  return true;
-}
 
 // Forward, one 64-thread wave per 16x16 tile (4 pixels per lane: the same pixel of each 8x8 quadrant).
 // The wave gathers each tile candidate once (the quadrant-wave kernel above gathers it in each of the
@@ -400,10 +404,8 @@ __global__ __launch_bounds__(64) void k_render_fwd_tile(RenderSet rs, const uint
   __shared__ float4 s0[64], s1[64], s2[64];
   __shared__ float4 s3[C2 ? 64 : 1];
   __shared__ uint32_t smask[64];
-  const int TG = tile_grid(rs.gx, rs.gy);
-  const int v = blockIdx.x / TG;
-  int tile;
-  if (!tile_of_block(blockIdx.x - v * TG, rs.gx, rs.gy, tile)) return;
+  int v, tile, q_unused;
+  if (!block_map<4>(blockIdx.x, rs, v, tile, q_unused)) return;
   const int W = rs.W, H = rs.H, grid_x = rs.gx;
   const size_t HWs = (size_t)W * H;
   {
@@ -573,6 +575,53 @@ __global__ __launch_bounds__(64) void k_render_fwd_tile(RenderSet rs, const uint
 #endif
 }
 
+// One block per view: bucket its super-tiles by the bit length of their listed instances (sum over the
+// 2x2 tiles), heaviest bucket first (LDS counts, exclusive scan, LDS-atomic placement: the order inside a
+// bucket may vary between runs — it only changes which workgroup starts first, never a result).
+__global__ __launch_bounds__(256) void k_tile_order(int gx, int gy, const uint2* __restrict__ ranges,
+                                                    uint32_t* __restrict__ order) {
+  __shared__ uint32_t cnt[33], cur[33];
+  const int t = threadIdx.x, v = blockIdx.x;
+  const int sgx = (gx + 1) >> 1, sgy = (gy + 1) >> 1, S = sgx * sgy;
+  ranges += (size_t)v * gx * gy;
+  order += (size_t)v * S;
+  if (t < 33) cnt[t] = 0u;
+  __syncthreads();
+  auto bucket = [&](int s) -> int {
+    const int x0 = (s % sgx) * 2, y0 = (s / sgx) * 2;
+    uint32_t w = 0u;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int x = x0 + (k & 1), y = y0 + (k >> 1);
+      if (x < gx && y < gy) {
+        const uint2 r = ranges[y * gx + x];
+        w += r.y - r.x;
+      }
+    }
+    return 32 - (w ? 32 - __clz((int)w) : 0);  // 0 = the most instances (bit length 32) ... 32 = none
+  };
+  for (int s = t; s < S; s += 256) atomicAdd(&cnt[bucket(s)], 1u);
+  __syncthreads();
+  if (t == 0) {
+    uint32_t run = 0u;
+    for (int b = 0; b < 33; ++b) {
+      cur[b] = run;
+      run += cnt[b];
+    }
+  }
+  __syncthreads();
+  for (int s = t; s < S; s += 256) order[atomicAdd(&cur[bucket(s)], 1u)] = (uint32_t)s;
+}
+
+void launch_tile_order(int V, int gx, int gy, const uint2* ranges, uint32_t* order, hipStream_t stream) {
+  if (V > 0 && gx > 0 && gy > 0) hipLaunchKernelGGL(k_tile_order, dim3(V), dim3(256), 0, stream, gx, gy, ranges, order);
+}
+
+bool tile_order_on() {
+  const char* e = getenv("GSR_TILE_ORDER");
+  return !(e != nullptr && strcmp(e, "raster") == 0);
+}
+
 // Which forward: the tile-wave kernel gathers each candidate once but walks a quadrant's candidates one
 // branch at a time and the whole tile list to the tile's deepest termination; it wins when Gaussians span
 // several tiles (C3: 6.7 rectangle tiles per Gaussian, render_fwd -3 %), the quadrant-wave kernel when
@@ -595,21 +644,25 @@ void launch_render_forward(const RenderSet& rs, const GeomState& g, const uint32
   const int nt = rs.gx * rs.gy;
   if (nt <= 0 || rs.V <= 0) return;
   if (fwd_tile_kernel(instances, (long long)rs.V * rs.P, rs.V)) {
-    const dim3 grid(rs.V * tile_grid(rs.gx, rs.gy));
+    // (>= 48 views per launch: the tail is hidden, and raster order keeps neighbouring super-tiles of a
+    // view close in time for L2; work order measured 0.0495 -> 0.0535 ms/view here, profiles/r02_tile_order_ab.txt)
+    RenderSet rsr = rs;
+    rsr.order = nullptr;
+    const dim3 grid(block_grid(rsr, 4));
     if (rs.col2 != nullptr)
-      hipLaunchKernelGGL(k_render_fwd_tile<true>, grid, dim3(64), 0, stream, rs, (const uint2*)img.ranges,
+      hipLaunchKernelGGL(k_render_fwd_tile<true>, grid, dim3(64), 0, stream, rsr, (const uint2*)img.ranges,
                          sorted_gauss, (const GaussRec*)g.rec, out_color, out_depth, out_alpha, img.final_T,
                          img.n_contrib, img.quad_maxc);
     else
-      hipLaunchKernelGGL(k_render_fwd_tile<false>, grid, dim3(64), 0, stream, rs, (const uint2*)img.ranges,
+      hipLaunchKernelGGL(k_render_fwd_tile<false>, grid, dim3(64), 0, stream, rsr, (const uint2*)img.ranges,
                          sorted_gauss, (const GaussRec*)g.rec, out_color, out_depth, out_alpha, img.final_T,
                          img.n_contrib, img.quad_maxc);
   } else if (rs.col2 != nullptr) {
-    hipLaunchKernelGGL(k_render_fwd<true>, dim3(rs.V * unit_grid(rs.gx, rs.gy)), dim3(64), 0, stream, rs,
+    hipLaunchKernelGGL(k_render_fwd<true>, dim3(block_grid(rs, 16)), dim3(64), 0, stream, rs,
                        (const uint2*)img.ranges, sorted_gauss, (const GaussRec*)g.rec, out_color, out_depth,
                        out_alpha, img.final_T, img.n_contrib, img.quad_maxc);
   } else {
-    hipLaunchKernelGGL(k_render_fwd<false>, dim3(rs.V * unit_grid(rs.gx, rs.gy)), dim3(64), 0, stream, rs,
+    hipLaunchKernelGGL(k_render_fwd<false>, dim3(block_grid(rs, 16)), dim3(64), 0, stream, rs,
                        (const uint2*)img.ranges, sorted_gauss, (const GaussRec*)g.rec, out_color, out_depth,
                        out_alpha, img.final_T, img.n_contrib, img.quad_maxc);
   }
@@ -637,10 +690,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(TWO ? 4 : 5
   constexpr int GS = TWO ? 4 : 8;                                // candidates per 16x16 product
   constexpr int NPL = TWO ? 7 : 4;                               // dL/dpixel planes in the B operand
   constexpr int RW = TWO ? 4 : 3;                                // float4 per gradient row
-  const int TG = tile_grid(rs.gx, rs.gy);
-  const int v = blockIdx.x / TG;
-  int tile;
-  if (!tile_of_block(blockIdx.x - v * TG, rs.gx, rs.gy, tile)) return;
+  int v, tile, q_unused;
+  if (!block_map<4>(blockIdx.x, rs, v, tile, q_unused)) return;
   GSR_TL_BEGIN
   const int W = rs.W, H = rs.H, grid_x = rs.gx;
   {
@@ -1116,7 +1167,7 @@ void launch_render_backward(const RenderSet& rs, const GeomState& g, const uint3
                             const float* dL_dalpha, const BackwardState& bw, hipStream_t stream) {
   const int nt = rs.gx * rs.gy;
   if (nt <= 0 || rs.V <= 0) return;
-  const dim3 grid(rs.V * tile_grid(rs.gx, rs.gy));
+  const dim3 grid(block_grid(rs, 4));
   if (rs.dpix2 != nullptr)
     hipLaunchKernelGGL(k_render_bwd<true>, grid, dim3(256), 0, stream, rs, (const uint2*)img.ranges,
                        (const uint32_t*)img.quad_maxc, sorted_gauss, (const GaussRec*)g.rec,
