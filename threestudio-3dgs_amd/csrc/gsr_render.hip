@@ -52,9 +52,14 @@ __device__ unsigned long long g_pairs[8];
 // blockIdx -> (view of the launch, tile, quadrant) for PER blocks per 2x2-tile super-tile (4: a workgroup
 // per tile; 16: a wave per 8x8 quadrant).  Groups of 8 consecutive super-tiles are dealt one to each XCD
 // (x = b & 7) with all blocks of a super-tile on the same XCD (its tiles share Gaussians in L2).  With an
-// order (rs.order): dispatch position m interleaves the launch's views (m % V) and walks each view's
-// super-tiles heaviest first (m / V) — a launch lasts at least its slowest workgroup, so the long tiles
-// start first and the short ones fill the tail.  Without: the views in turn, super-tiles in raster order.
+// order (rs.order): chunks of GSR_ORDER_CHUNK views in turn, inside a chunk all its views' super-tiles
+// heaviest first — a launch lasts at least its slowest workgroup, so the long tiles start first and the
+// short ones fill the tail; chunks bound how many views' records compete in L2 at once (chunk 1 / 4 / 8 /
+// 16 / all 64: C3 backward 0.0976 / 0.0955 / 0.0955 / 0.098 / 0.100 ms/view, 8-view launches best fully
+// interleaved; profiles/r02_tile_order_ab.txt).  Without: the views in turn, super-tiles in raster order.
+#ifndef GSR_ORDER_CHUNK
+#define GSR_ORDER_CHUNK 8
+#endif
 template <int PER>
 __device__ __forceinline__ bool block_map(int b, const RenderSet& rs, int& v, int& tile, int& q) {
   const int sgx = (rs.gx + 1) >> 1, sgy = (rs.gy + 1) >> 1, S = sgx * sgy;
@@ -64,8 +69,12 @@ __device__ __forceinline__ bool block_map(int b, const RenderSet& rs, int& v, in
     w = k & (PER - 1);
     const int m = ((k / PER) << 3) + x;
     if (m >= rs.V * S) return false;
-    v = m % rs.V;
-    s = (int)rs.order[(size_t)(rs.v0 + v) * S + m / rs.V];
+    // chunks of GSR_ORDER_CHUNK views, interleaved inside a chunk (all its views' heaviest super-tiles
+    // first), the chunks in turn
+    const int c = m / (GSR_ORDER_CHUNK * S), local = m - c * GSR_ORDER_CHUNK * S;
+    const int vc = min(GSR_ORDER_CHUNK, rs.V - c * GSR_ORDER_CHUNK);
+    v = c * GSR_ORDER_CHUNK + local % vc;
+    s = (int)rs.order[(size_t)(rs.v0 + v) * S + local / vc];
   } else {
     const int G = PER * 8 * ((S + 7) >> 3);
     v = b / G;
