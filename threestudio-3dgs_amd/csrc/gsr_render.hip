@@ -656,7 +656,9 @@ void launch_render_forward(const RenderSet& rs, const GeomState& g, const uint32
     // (>= 48 views per launch: the tail is hidden, and raster order keeps neighbouring super-tiles of a
     // view close in time for L2; work order measured 0.0495 -> 0.0535 ms/view here, profiles/r02_tile_order_ab.txt)
     RenderSet rsr = rs;
+#ifndef GSR_EXP_FWDORDER
     rsr.order = nullptr;
+#endif
     const dim3 grid(block_grid(rsr, 4));
     if (rs.col2 != nullptr)
       hipLaunchKernelGGL(k_render_fwd_tile<true>, grid, dim3(64), 0, stream, rsr, (const uint2*)img.ranges,
