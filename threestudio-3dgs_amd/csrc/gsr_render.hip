@@ -653,19 +653,13 @@ void launch_render_forward(const RenderSet& rs, const GeomState& g, const uint32
   const int nt = rs.gx * rs.gy;
   if (nt <= 0 || rs.V <= 0) return;
   if (fwd_tile_kernel(instances, (long long)rs.V * rs.P, rs.V)) {
-    // (>= 48 views per launch: the tail is hidden, and raster order keeps neighbouring super-tiles of a
-    // view close in time for L2; work order measured 0.0495 -> 0.0535 ms/view here, profiles/r02_tile_order_ab.txt)
-    RenderSet rsr = rs;
-#ifndef GSR_EXP_FWDORDER
-    rsr.order = nullptr;
-#endif
-    const dim3 grid(block_grid(rsr, 4));
+    const dim3 grid(block_grid(rs, 4));
     if (rs.col2 != nullptr)
-      hipLaunchKernelGGL(k_render_fwd_tile<true>, grid, dim3(64), 0, stream, rsr, (const uint2*)img.ranges,
+      hipLaunchKernelGGL(k_render_fwd_tile<true>, grid, dim3(64), 0, stream, rs, (const uint2*)img.ranges,
                          sorted_gauss, (const GaussRec*)g.rec, out_color, out_depth, out_alpha, img.final_T,
                          img.n_contrib, img.quad_maxc);
     else
-      hipLaunchKernelGGL(k_render_fwd_tile<false>, grid, dim3(64), 0, stream, rsr, (const uint2*)img.ranges,
+      hipLaunchKernelGGL(k_render_fwd_tile<false>, grid, dim3(64), 0, stream, rs, (const uint2*)img.ranges,
                          sorted_gauss, (const GaussRec*)g.rec, out_color, out_depth, out_alpha, img.final_T,
                          img.n_contrib, img.quad_maxc);
   } else if (rs.col2 != nullptr) {
