@@ -253,12 +253,14 @@ def test_batched_views_match_per_view(nviews):
         assert err <= 1e-5 * scale, f"{k}: {err} vs scale {scale}"
 
 
+@pytest.mark.parametrize("switch", ["fwd_kernel", "dispatch_order"])
 @pytest.mark.parametrize("kind", ["ball_composite", "sugar_two_colors"])
-def test_forward_kernels_bitwise(kind, monkeypatch):
-    """The one-wave-per-tile forward (default) and the quadrant-wave forward (GSR_FWD_KERNEL=quadrant)
-    blend exactly the same candidates per pixel in the same order: every output — colour, depth, alpha,
-    the composite, the second colour set, radii — and every gradient (the backward reads the forward's
-    per-pixel state) must be bitwise equal."""
+def test_forward_kernels_bitwise(kind, switch, monkeypatch):
+    """fwd_kernel: the one-wave-per-tile forward and the quadrant-wave forward (GSR_FWD_KERNEL) blend
+    exactly the same candidates per pixel in the same order; dispatch_order: the blends' work-ordered
+    dispatch and raster order (GSR_TILE_ORDER=raster) only change which workgroup starts first.  Every
+    output — colour, depth, alpha, the composite, the second colour set, radii — and every gradient (the
+    backward reads the forward's per-pixel state) must be bitwise equal."""
     import torch
 
     from diff_gaussian_rasterization.batched import rasterize_views
@@ -276,7 +278,12 @@ def test_forward_kernels_bitwise(kind, monkeypatch):
     bgimg = torch.tensor(rng.random((3, H_, W_, 3)).astype(np.float32), device=dev)
 
     def run(kernel):
-        monkeypatch.setenv("GSR_FWD_KERNEL", kernel)
+        if switch == "fwd_kernel":
+            monkeypatch.setenv("GSR_FWD_KERNEL", kernel)
+        elif kernel == "tile":
+            monkeypatch.delenv("GSR_TILE_ORDER", raising=False)
+        else:
+            monkeypatch.setenv("GSR_TILE_ORDER", "raster")
         from test_gpu_configs import _settings
 
         P = scene["means3D"].shape[0]
