@@ -27,6 +27,8 @@ void launch_preprocess_kernel(const PreprocessArgs& a, const SetCams& cams, cons
 #define GSR_PRE_GAUSS 128
 #define GSR_PRE_LDS_FLOATS (8 * 1024)  // SH staging up to 32 KB (M <= 21); larger M reads SH from HBM
 
+// (6 waves per SIMD: 86 -> 79 VGPRs without spills; the LDS allows 6 blocks — 1 % faster)
+__attribute__((amdgpu_waves_per_eu(6, 8)))
 __global__ __launch_bounds__(256) void k_preprocess(PreprocessArgs a, SetCams cams, GeomState g) {
   extern __shared__ float s_sh[];  // [128][3M + 1] this block's SH coefficients (odd stride)
   const int nvc = (a.V + GSR_PRE_VIEWS - 1) / GSR_PRE_VIEWS;

@@ -404,6 +404,10 @@ struct BwdLDS {
 // order, with the same operations as the quadrant-wave kernel, so the outputs are bitwise identical.
 // Finished quadrants leave the mask (uniform), and the wave stops when all four are done.
 template <bool C2>
+// 6 waves per SIMD for the one-colour variant (89 -> 80 VGPRs, 3 spilled outside the candidate loop:
+// render_fwd 0.049 -> 0.047 ms/view at C3, profiles/r02_fwd_occupancy_ab.txt); the two-colour one would
+// spill 32 VGPRs and keeps the compiler's choice
+__attribute__((amdgpu_waves_per_eu(C2 ? 1 : 6, 8)))
 __global__ __launch_bounds__(64) void k_render_fwd_tile(RenderSet rs, const uint2* __restrict__ ranges,
                                                         const uint32_t* __restrict__ sorted_gauss,
                                                         const GaussRec* __restrict__ rec, float* __restrict__ out_color,
