@@ -52,6 +52,15 @@ extern "C" {
 
 /* Library identification ("gsr <version> gfx950"). */
 const char* gsr_version(void);
+/*
+ * ABI revision of this header (GSR_ABI_VERSION), for callers binding the library at run time.
+ *   2  gsr_set_backward* `accumulate` CONTINUES every per-Gaussian sum from the stored value in view order
+ *      (round 1's revision 1 added the new sums to the stored values); with accumulate in the scale / rotation
+ *      path dL_dcov3D is required (the running dL/dcov3D carry), otherwise GSR_EINVAL.
+ *   3  gsr_shade_views_forward / gsr_shade_views_backward (per-view light colours and shading modes).
+ */
+#define GSR_ABI_VERSION 3
+int gsr_abi_version(void);
 /* Message of the last failing call on this thread ("" if none). */
 const char* gsr_last_error(void);
 
@@ -319,6 +328,25 @@ int gsr_shade_backward(int V, int height, int width, int flags, int mode, const 
                        const float* dL_drender, const float* dL_dnormal_map, const float* dL_dunit_normal,
                        const float* dL_ddepth_out, float* dL_dcolor, float* dL_ddepth, float* dL_dalpha,
                        float* dL_dbg, void* stream);
+/*
+ * As gsr_shade_forward / gsr_shade_backward with the light colours and shading mode given PER VIEW:
+ * modes (V,) host ints, ambient / diffuse (V, 3) host floats.  The reference's material draws its soft-shading
+ * ambient ratio and its shading mode once per view (material/gaussian_material.py:59-64,80-88, called once per
+ * view by renderer/diff_gaussian_rasterizer_shading.py:200-205 inside the per-view loop of
+ * renderer/gaussian_batch_renderer.py:21-54), so a fused batch needs one (ka, kd, mode) per view.
+ * modes / ambient / diffuse may be NULL without GSR_SHADE_MATERIAL.
+ */
+int gsr_shade_views_forward(int V, int height, int width, int flags, const int* modes, const float* color,
+                            const float* depth, const float* alpha, const float* rays_o, const float* rays_d,
+                            const float* bg, int bg_layout, const float* light, const float* pred_normal,
+                            const float* ambient, const float* diffuse, float* render, float* normal_map,
+                            float* unit_normal, float* depth_out, void* stream);
+int gsr_shade_views_backward(int V, int height, int width, int flags, const int* modes, const float* color,
+                             const float* depth, const float* alpha, const float* rays_o, const float* rays_d,
+                             const float* bg, int bg_layout, const float* light, const float* pred_normal,
+                             const float* ambient, const float* diffuse, const float* dL_drender,
+                             const float* dL_dnormal_map, const float* dL_dunit_normal, const float* dL_ddepth_out,
+                             float* dL_dcolor, float* dL_ddepth, float* dL_dalpha, float* dL_dbg, void* stream);
 
 /*
  * Mean squared distance to the 3 nearest other points, for each of P points (P, 3) -> (P,): replaces

@@ -21,6 +21,7 @@ from __future__ import annotations
 import math
 from types import SimpleNamespace
 
+import numpy as np
 import torch
 
 import torch_reference as tr
@@ -39,9 +40,12 @@ def torch_rasterize(settings, means3D, means2D, opacities, shs=None, colors_prec
     """GaussianRasterizer's call restated with the dense torch formulation (CPU / any device)."""
     s = settings
     dt = means3D.dtype
+    deg = s.sh_degree
+    if shs is not None:  # the rasterizer reads sqrt(M) - 1 degrees at most (the pred-normal pass: M = 1)
+        deg = min(deg, int(round(math.sqrt(shs.shape[1]))) - 1)
     return tr.render(means3D, means2D, opacities, s.viewmatrix.reshape(-1).to(dt), s.projmatrix.reshape(-1).to(dt),
                      s.campos.to(dt), s.tanfovx, s.tanfovy, s.image_width, s.image_height, s.bg.to(dt), sh=shs,
-                     deg=s.sh_degree, colors=colors_precomp, scales=scales, rotations=rotations, cov3D=cov3D_precomp,
+                     deg=deg, colors=colors_precomp, scales=scales, rotations=rotations, cov3D=cov3D_precomp,
                      mod=s.scale_modifier)
 
 
@@ -65,14 +69,51 @@ def torch_rasterize_views(settings_list, means3D, means2D_list, opacities, shs=N
     return color, radii, depth, alpha, torch.stack(second)
 
 
+def torch_shade_views(color, depth, alpha, rays_o, rays_d, bg, light_positions, ambient, diffuse, shading,
+                      pred_normal=None):
+    """shading.shade_views restated per view with tests/torch_reference.shading_epilogue (for the CPU tests);
+    ambient / diffuse / shading per view."""
+    outs = []
+    for v in range(depth.shape[0]):
+        dt = depth.dtype
+        ka = torch.tensor(ambient[v], dtype=dt, device=depth.device)
+        kd = torch.tensor(diffuse[v], dtype=dt, device=depth.device)
+        outs.append(tr.shading_epilogue(color[v], depth[v], alpha[v], rays_o[v], rays_d[v], bg[v], light_positions[v],
+                                        ka, kd, shading[v], pred_normal[v] if pred_normal is not None else None))
+    return tuple(torch.stack([o[i] for o in outs]) for i in range(3))
+
+
+def _normal_maps_one(depth, alpha, rays_o, rays_d):
+    """The normal renderer's epilogue (renderer/diff_gaussian_rasterizer_normal.py:172-193) for one view."""
+    xyz = rays_o + depth.permute(1, 2, 0) * rays_d
+    n = torch.nn.functional.normalize(tr.depth_to_normal(xyz.permute(2, 0, 1).unsqueeze(0))[0], dim=0)
+    nmap = n * 0.5 * alpha + 0.5
+    mask = alpha.float() > 0.99
+    return (torch.where(mask.repeat(3, 1, 1), nmap, nmap.detach()), torch.where(mask, depth, depth.detach()))
+
+
+def torch_depth_normal_maps(depth, alpha, rays_o, rays_d):
+    outs = [_normal_maps_one(depth[v], alpha[v], rays_o[v], rays_d[v]) for v in range(depth.shape[0])]
+    return torch.stack([o[0] for o in outs]), torch.stack([o[1] for o in outs])
+
+
+def torch_depth_normal_views(depth, alpha, rays_o, rays_d):
+    outs = [tr.sugar_normal_from_dist(depth[v], alpha[v], rays_o[v], rays_d[v]) for v in range(depth.shape[0])]
+    return torch.stack([o[0] for o in outs]), torch.stack([o[1] for o in outs])
+
+
 class FakeGeometry:
-    def __init__(self, scene, device, dtype=torch.float32):
+    def __init__(self, scene, device, dtype=torch.float32, pred_normal=False):
         leaf = lambda x: torch.tensor(x, device=device, dtype=dtype, requires_grad=True)  # noqa: E731
         self.params = {k: leaf(scene[k]) for k in ("means3D", "shs", "opacities", "scales", "rotations")}
         if "normals" in scene:
             self.params["normals"] = leaf(scene["normals"])
+        elif pred_normal:  # the geometry's per-Gaussian normal (pc.get_normal) for the predicted-normal pass
+            g = torch.Generator().manual_seed(17)
+            n = torch.randn(len(scene["means3D"]), 3, generator=g, dtype=torch.float64)
+            self.params["normals"] = leaf((n / n.norm(dim=-1, keepdim=True)).numpy())
         self.active_sh_degree = int(scene.get("sh_degree", 0))
-        self.cfg = SimpleNamespace(pred_normal=False)
+        self.cfg = SimpleNamespace(pred_normal=pred_normal)
 
     get_xyz = property(lambda self: self.params["means3D"])
     get_features = property(lambda self: self.params["shs"])
@@ -80,6 +121,7 @@ class FakeGeometry:
     get_scaling = property(lambda self: self.params["scales"])
     get_rotation = property(lambda self: self.params["rotations"])
     get_gs_normals = property(lambda self: self.params["normals"])
+    get_normal = property(lambda self: self.params["normals"])
 
 
 def _background_net(dirs):
@@ -88,17 +130,19 @@ def _background_net(dirs):
 
 
 class FakeRenderer(GaussianBatchRenderer):
-    def __init__(self, mode, scene, device, dtype=torch.float32):
+    def __init__(self, mode, scene, device, dtype=torch.float32, training=False, soft_shading=False,
+                 pred_normal=False):
         self.batch_render_mode = mode
-        self.geometry = FakeGeometry(scene, device, dtype)
+        self.geometry = FakeGeometry(scene, device, dtype, pred_normal=pred_normal)
         self.background_tensor = torch.tensor([1.0, 1.0, 1.0], device=device, dtype=dtype)
         self.background = lambda dirs: _background_net(dirs)
-        self.material = SimpleNamespace(cfg=SimpleNamespace(soft_shading=False, diffuse_prob=0.75,
+        # the MVDream config's material (configs/gaussian_splatting_mvdream.yaml:62-67: soft_shading true)
+        self.material = SimpleNamespace(cfg=SimpleNamespace(soft_shading=soft_shading, diffuse_prob=0.75,
                                                             textureless_prob=0.5),
                                         ambient_light_color=torch.tensor([0.1, 0.1, 0.1]),
                                         diffuse_light_color=torch.tensor([0.9, 0.9, 0.9]), ambient_only=False)
         self.cfg = SimpleNamespace(invert_bg_prob=0.5, debug=False)
-        self.training = False
+        self.training = training
         self.mode = mode
 
     # the reference's per-view DiffGaussian.forward of each mode
@@ -106,8 +150,8 @@ class FakeRenderer(GaussianBatchRenderer):
         pc = self.geometry
         if self.mode in ("background", "shading"):
             bg_color = bg_color * 0
-        else:
-            invert = True  # eval: renderer/diff_gaussian_rasterizer.py:59-64
+        else:  # renderer/diff_gaussian_rasterizer.py:59-64
+            invert = (np.random.rand() > self.cfg.invert_bg_prob) if self.training else True
             bg_color = 1.0 - bg_color if invert else bg_color
         sp = torch.zeros_like(pc.get_xyz, requires_grad=True) + 0
         sp.retain_grad()
@@ -124,8 +168,18 @@ class FakeRenderer(GaussianBatchRenderer):
         _, H, W = img.shape
         b = kwargs["batch_idx"]
         pkg = {"viewspace_points": sp, "visibility_filter": radii > 0, "radii": radii}
+        pred = None
+        if self.mode in ("shading", "normal") and pc.cfg.pred_normal:
+            # renderer/diff_gaussian_rasterizer_shading.py:177-187 (normal.py:175-185)
+            kwp = dict(kw, means2D=torch.zeros_like(sp), shs=pc.get_normal.unsqueeze(1), colors_precomp=None)
+            pred, _, _, _ = RASTERIZE(settings, **kwp)
         if self.mode == "plain":
             pkg["render"] = img.clamp(0, 1)
+        elif self.mode == "advanced":
+            pkg.update(render=img.clamp(0, 1), depth=depth, mask=alpha)
+        elif self.mode == "normal":
+            nmap, depth_m = _normal_maps_one(depth, alpha, kwargs["rays_o"][b], kwargs["rays_d"][b])
+            pkg.update(render=img.clamp(0, 1), normal=nmap, pred_normal=pred, mask=alpha, depth=depth_m)
         elif self.mode == "background":
             comp_rgb_bg = self.background(dirs=kwargs["rays_d"][b].unsqueeze(0))
             img = img + (1 - alpha) * comp_rgb_bg.reshape(H, W, 3).permute(2, 0, 1)
@@ -136,8 +190,9 @@ class FakeRenderer(GaussianBatchRenderer):
             dt = img.dtype
             render, nmap, depth_m = tr.shading_epilogue(
                 img, depth, alpha, kwargs["rays_o"][b], kwargs["rays_d"][b], comp_rgb_bg, kwargs["light_positions"][b],
-                torch.tensor(ka, device=img.device, dtype=dt), torch.tensor(kd, device=img.device, dtype=dt), smode)
-            pkg.update(render=render, normal=nmap, pred_normal=None, mask=alpha, depth=depth_m, comp_rgb_bg=comp_rgb_bg)
+                torch.tensor(ka, device=img.device, dtype=dt), torch.tensor(kd, device=img.device, dtype=dt), smode,
+                pred)
+            pkg.update(render=render, normal=nmap, pred_normal=pred, mask=alpha, depth=depth_m, comp_rgb_bg=comp_rgb_bg)
         elif self.mode == "sugar_normal":
             nfd, nmap_dist = tr.sugar_normal_from_dist(depth, alpha, kwargs["rays_o"][b], kwargs["rays_d"][b])
             kw2 = dict(kw, means2D=torch.zeros_like(sp), shs=None, colors_precomp=pc.get_gs_normals)
@@ -155,8 +210,8 @@ class FakeRenderer(GaussianBatchRenderer):
 class PerViewRenderer(FakeRenderer):
     """The same renderer with the reference's per-view batch loop (batch_render_mode = "per_view")."""
 
-    def __init__(self, mode, scene, device, dtype=torch.float32):
-        super().__init__(mode, scene, device, dtype)
+    def __init__(self, mode, scene, device, dtype=torch.float32, **kw):
+        super().__init__(mode, scene, device, dtype, **kw)
         self.batch_render_mode = "per_view"
 
 
@@ -178,7 +233,7 @@ def make_batch(B, H, W, device, dtype=torch.float32, seed=0):
 def loss_of(out, seed=1):
     g = torch.Generator().manual_seed(seed)
     total = 0
-    for k in ("comp_rgb", "comp_depth", "comp_mask", "comp_normal", "comp_normal_from_dist"):
+    for k in ("comp_rgb", "comp_depth", "comp_mask", "comp_normal", "comp_normal_from_dist", "comp_pred_normal"):
         if k in out:
             w = torch.randn(out[k].shape, generator=g, dtype=torch.float64).to(out[k].device, out[k].dtype)
             total = total + (out[k] * w).sum()

@@ -47,6 +47,7 @@ def test_binding_signatures_match_header():
 
 def test_host_only_queries():
     lib = _C.load_library()
+    assert lib.gsr_abi_version() == _C.ABI_VERSION
     assert lib.gsr_version().decode().startswith("gsr ")
     assert "gfx950" in lib.gsr_version().decode()
     assert lib.gsr_geom_bytes(1000) >= 1000 * (48 + 8 + 4 * 7)  # records, rect, 7 u32 words

@@ -25,13 +25,19 @@ def _scene():
     return gs.make_scene(30, sh_degree=1, seed=5, radius=0.5)
 
 
+_SWAPS = (("_rasterize_views", rf.torch_rasterize_views), ("_shade_views", rf.torch_shade_views),
+          ("_depth_normal_maps", rf.torch_depth_normal_maps), ("_depth_normal_views", rf.torch_depth_normal_views))
+
+
 def _cpu(monkeypatch=None):
     if monkeypatch is not None:
         monkeypatch.setattr(rf, "RASTERIZE", rf.torch_rasterize)
-        monkeypatch.setattr(br, "_rasterize_views", rf.torch_rasterize_views)
+        for name, fn in _SWAPS:
+            monkeypatch.setattr(br, name, fn)
     else:
         rf.RASTERIZE = rf.torch_rasterize
-        br._rasterize_views = rf.torch_rasterize_views
+        for name, fn in _SWAPS:
+            setattr(br, name, fn)
 
 
 def _run(renderer, batch):
@@ -41,18 +47,46 @@ def _run(renderer, batch):
     return out, grads
 
 
-@pytest.mark.parametrize("mode", ["plain", "background"])
-def test_fused_equals_per_view_loop(mode, monkeypatch):
+def _mode_scene(mode):
+    if mode == "sugar_normal":
+        sc = gs.make_sugar_scene(1, sh_degree=0, seed=2)
+        sc["shs"] = sc["shs"][:, :1]
+        return sc
+    return _scene()
+
+
+@pytest.mark.parametrize("mode,training,pred_normal", [
+    ("plain", False, False), ("background", False, False), ("advanced", False, False), ("shading", False, False),
+    ("normal", False, False), ("sugar_normal", False, False),
+    # training: the per-view random draws (background inversion; soft-shading ambient ratio and shading mode)
+    ("plain", True, False), ("advanced", True, False), ("normal", True, False), ("shading", True, False),
+    ("sugar_normal", True, False),
+    # the predicted-normal second pass (renderer/diff_gaussian_rasterizer_shading.py:177-197, _normal.py:175-185)
+    ("shading", True, True), ("normal", False, True),
+])
+def test_fused_equals_per_view_loop(mode, training, pred_normal, monkeypatch):
+    """Each fused mode against the reference's per-view loop over the same renderer: same outputs, gradients
+    and — with the RNGs seeded alike — the same per-view random draws (B = 7 views, so that a per-batch draw
+    would differ from the per-view ones)."""
+    import random
+
     _cpu(monkeypatch)
-    batch = rf.make_batch(3, H, W, "cpu", torch.float64)
-    fused, g_fused = _run(rf.FakeRenderer(mode, _scene(), "cpu", torch.float64), dict(batch))
-    ref, g_ref = _run(rf.PerViewRenderer(mode, _scene(), "cpu", torch.float64), dict(batch))
+    batch = rf.make_batch(7, H, W, "cpu", torch.float64)
+    kw = dict(training=training, soft_shading=training, pred_normal=pred_normal)
+    random.seed(11), np.random.seed(11)
+    fused, g_fused = _run(rf.FakeRenderer(mode, _mode_scene(mode), "cpu", torch.float64, **kw), dict(batch))
+    draws_fused = (random.random(), np.random.rand())
+    random.seed(11), np.random.seed(11)
+    ref, g_ref = _run(rf.PerViewRenderer(mode, _mode_scene(mode), "cpu", torch.float64, **kw), dict(batch))
+    assert draws_fused == (random.random(), np.random.rand()), "the fused path consumed other draws than the loop"
     assert set(k for k in ref if k.startswith("comp_")) == set(k for k in fused if k.startswith("comp_"))
     for k in ref:
         if k.startswith("comp_"):
             assert fused[k].shape == ref[k].shape, k
             torch.testing.assert_close(fused[k], ref[k], rtol=1e-12, atol=1e-12)
-    for i in range(3):
+    if pred_normal:
+        assert "comp_pred_normal" in fused and "normals" in g_ref
+    for i in range(7):
         assert torch.equal(fused["radii"][i], ref["radii"][i])
         assert torch.equal(fused["visibility_filter"][i], ref["visibility_filter"][i])
         torch.testing.assert_close(fused["viewspace_points"][i].grad, ref["viewspace_points"][i].grad,
@@ -68,6 +102,10 @@ def test_mode_detection():
     Plain.__module__ = "threestudio_3dgs.renderer.diff_gaussian_rasterizer_background"
     assert br.batch_mode(Plain()) == "background"
     Plain.__module__ = "threestudio_3dgs.renderer.diff_gaussian_rasterizer_advanced"
+    assert br.batch_mode(Plain()) == "advanced"
+    Plain.__module__ = "threestudio_3dgs.renderer.diff_gaussian_rasterizer_normal"
+    assert br.batch_mode(Plain()) == "normal"
+    Plain.__module__ = "threestudio_3dgs.renderer.diff_sugar_rasterizer_temporal"
     assert br.batch_mode(Plain()) is None  # keeps the per-view loop
     p = Plain()
     p.batch_render_mode = "shading"
@@ -95,6 +133,12 @@ def _worker(rank, world, port, tmp, B, kind):
         if kind == "fused":
             r = rf.FakeRenderer("background", _scene(), "cpu", torch.float64)
             out, _ = _run(r, batch)
+        elif kind == "fused_shading_train":  # per-view random lights: the rank's views get the loop's draws
+            import random
+
+            random.seed(5)
+            r = rf.FakeRenderer("shading", _scene(), "cpu", torch.float64, training=True, soft_shading=True)
+            out, _ = _run(r, batch)
         else:  # the callback form of ViewShardedBatchRenderer (per-view forward)
             r = rf.PerViewRenderer("background", _scene(), "cpu", torch.float64)
             out = ViewShardedBatchRenderer(r).batch_forward(batch)
@@ -109,11 +153,17 @@ def _worker(rank, world, port, tmp, B, kind):
 
 
 @pytest.mark.parametrize("world,B", [(2, 5), (3, 2)])
-@pytest.mark.parametrize("kind", ["fused", "callback"])
+@pytest.mark.parametrize("kind", ["fused", "callback", "fused_shading_train"])
 def test_sharded_equals_single_process(world, B, kind, tmp_path, monkeypatch):
+    import random
+
     _cpu(monkeypatch)
     batch = rf.make_batch(B, H, W, "cpu", torch.float64)
-    r = rf.FakeRenderer("background", _scene(), "cpu", torch.float64)
+    if kind == "fused_shading_train":
+        random.seed(5)
+        r = rf.FakeRenderer("shading", _scene(), "cpu", torch.float64, training=True, soft_shading=True)
+    else:
+        r = rf.FakeRenderer("background", _scene(), "cpu", torch.float64)
     out, grads = _run(r, batch)
     mp.spawn(_worker, args=(world, _free_port(), str(tmp_path), B, kind), nprocs=world, join=True)
     for rank in range(world):

@@ -150,9 +150,10 @@ def test_c3_views_fused_background_composite():
             b["bg_" + prec] = (gcol * (dt(1) - f["alpha"].astype(dt))).transpose(1, 2, 0)
         check_forward(_view(gpu, v), ref, f"C3 view {v}", K_gpu=gpu["K"][v])
         adjudicate(gpu["g_means2D"][v], b["f32"]["means2D"], b["f64"]["means2D"],
-                   1e-4 * np.maximum(1.0, np.abs(b["f64"]["means2D"])), f"C3 view {v}", "grad means2D")
+                   1e-4 * np.maximum(1.0, np.abs(b["f64"]["means2D"])), f"C3 view {v}", "grad means2D", rowwise=True)
         adjudicate(gpu["g_background"][v].reshape(-1, 3), b["bg_f32"].reshape(-1, 3), b["bg_f64"].reshape(-1, 3),
-                   1e-4 * np.maximum(1.0, np.abs(b["bg_f64"].reshape(-1, 3))), f"C3 view {v}", "grad background")
+                   1e-4 * np.maximum(1.0, np.abs(b["bg_f64"].reshape(-1, 3))), f"C3 view {v}", "grad background",
+                   rowwise=True)
         refs.append(b)
     tot = dict(b32=_sum_grads(refs, "f32", GRAD_KEYS), b64=_sum_grads(refs, "f64", GRAD_KEYS))
     check_grads(gpu, tot, GRAD_KEYS, "C3 summed")
@@ -171,7 +172,8 @@ def test_view_set_vs_oracle():
         ref = run_oracle(scene, cam, bgs[v], grads=ups[v])
         check_forward(_view(gpu, v), ref, f"set view {v}", K_gpu=gpu["K"][v])
         adjudicate(gpu["g_means2D"][v], ref["b32"]["means2D"], ref["b64"]["means2D"],
-                   1e-4 * np.maximum(1.0, np.abs(ref["b64"]["means2D"])), f"set view {v}", "grad means2D")
+                   1e-4 * np.maximum(1.0, np.abs(ref["b64"]["means2D"])), f"set view {v}", "grad means2D",
+                   rowwise=True)
         refs.append(ref)
     tot = dict(b32=_sum_grads(refs, "b32", GRAD_KEYS), b64=_sum_grads(refs, "b64", GRAD_KEYS))
     check_grads(gpu, tot, GRAD_KEYS, "set summed")
@@ -544,9 +546,11 @@ def test_two_color_backward_with_fused_composite():
             bgs[prec] = (gcol * (dt(1) - f["alpha"].astype(dt))).transpose(1, 2, 0).reshape(-1, 3)
             bgs["m2_" + prec] = b1["means2D"]
         adjudicate(bg_t.grad[v].detach().cpu().numpy().reshape(-1, 3), bgs["f32"], bgs["f64"],
-                   1e-4 * np.maximum(1.0, np.abs(bgs["f64"])), f"two colours + composite view {v}", "grad background")
+                   1e-4 * np.maximum(1.0, np.abs(bgs["f64"])), f"two colours + composite view {v}", "grad background",
+                   rowwise=True)
         adjudicate(m2[v].grad.cpu().numpy(), bgs["m2_f32"], bgs["m2_f64"],
-                   1e-4 * np.maximum(1.0, np.abs(bgs["m2_f64"])), f"two colours + composite view {v}", "grad means2D")
+                   1e-4 * np.maximum(1.0, np.abs(bgs["m2_f64"])), f"two colours + composite view {v}", "grad means2D",
+                   rowwise=True)
     gpu = {"g_" + k: t[src].grad.cpu().numpy() for k, src in (("means3D", "means3D"), ("scales", "scales"),
            ("rotations", "rotations"), ("opacity", "opacities"), ("sh", "shs"), ("normals", "normals"))}
     check_grads(gpu, ref, ["means3D", "scales", "rotations", "opacity", "sh", "normals"], "two colours + composite")

@@ -95,6 +95,48 @@ def test_shade_views_match_torch(shading, use_pred, V, H, W):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("V,H,W", [(3, 24, 40), (67, 9, 13)])
+def test_shade_views_per_view_lights_and_modes(V, H, W):
+    """Per-view (ka, kd, mode), as the material draws them once per view in training
+    (material/gaussian_material.py:59-64,80-88); 67 views cross the 64-view launch chunk."""
+    from diff_gaussian_rasterization.shading import shade_views
+
+    modes = [("albedo", "textureless", "diffuse")[(7 * v + 1) % 3] for v in range(V)]
+    kd = [(0.25 + 0.7 * ((v * 0.37) % 1.0),) * 3 for v in range(V)]  # soft shading: kd ~ U(0, 1), ka = 1 - kd
+    ka = [(1.0 - d[0],) * 3 for d in kd]
+    scenes = _scene(V, H, W, seed=11 + V)
+    dev = "cuda"
+    st = lambda k, dt=torch.float32: torch.stack([s[k] for s in scenes]).to(dev, dt)  # noqa: E731
+    leaves = {k: st(k).requires_grad_(True) for k in ("color", "depth", "alpha", "bg")}
+    render, nmap, depth = shade_views(leaves["color"], leaves["depth"], leaves["alpha"], st("rays_o"), st("rays_d"),
+                                      leaves["bg"], st("light"), ka, kd, modes)
+    ups = [torch.stack([s["ups"][i] for s in scenes]).to(dev, torch.float32) for i in range(3)]
+    torch.autograd.backward((render, nmap, depth), ups)
+    for v, sc in enumerate(scenes):
+        o64, g64 = _reference(sc, torch.float64, modes[v], False, ka[v], kd[v])
+        o32, g32 = _reference(sc, torch.float32, modes[v], False, ka[v], kd[v])
+        for name, got, r64, r32 in zip(("render", "normal", "depth"), (render[v], nmap[v], depth[v]), o64, o32):
+            _check(f"view {v} {name}", got, r64, r32, 1e-5)
+        for k in ("color", "depth", "alpha", "bg"):
+            _check(f"view {v} d{k}", leaves[k].grad[v], g64[k], g32[k], 1e-4)
+
+
+def test_shade_tables_host_checks():
+    from diff_gaussian_rasterization.shading import _light_table, _mode_table
+
+    assert _light_table((0.1, 0.2, 0.3), 2) == (0.1, 0.2, 0.3, 0.1, 0.2, 0.3)
+    assert _light_table([(0.1,) * 3, (0.5,) * 3], 2) == (0.1,) * 3 + (0.5,) * 3
+    assert _mode_table("albedo", 2) == (1, 1)
+    assert _mode_table(["diffuse", "textureless"], 2) == (0, 2)
+    with pytest.raises(ValueError):
+        _mode_table(["diffuse"], 2)
+    with pytest.raises(ValueError):
+        _mode_table("glossy", 1)
+    with pytest.raises(ValueError):
+        _light_table((0.1, 0.2), 1)
+
+
+@pytest.mark.gpu
 def test_shade_views_single_view_constant_background():
     from diff_gaussian_rasterization.shading import shade_views
 

@@ -64,17 +64,27 @@ def _loss(out):
     return (out["comp_rgb"] * wc).sum() + (out["comp_depth"] * wd).sum() + out["comp_mask"].sum()
 
 
-def _single_process():
+def _regularisers(params):
+    """Parameter-direct loss terms as the systems add them (lambda_position / lambda_opacity / lambda_scales,
+    system/gaussian_splatting.py:89-106): computed on every rank from the replicated parameters."""
+    return (0.3 * (params["means3D"] ** 2).sum() + 0.2 * params["opacities"].sum()
+            + 0.1 * params["scales"].norm(dim=-1).mean())
+
+
+def _single_process(reg=False):
     params = _params()
     r = ViewShardedBatchRenderer(_render_view(params))
     out = r.batch_forward(_batch())
-    _loss(out).backward()
+    loss = _loss(out) + (_regularisers(params) if reg else 0)
+    loss.backward()
     stats = reduce_densify_stats(out["radii"], out["viewspace_points"], out["visibility_filter"], 40)
     return ({k: out[k].detach().numpy() for k in ("comp_rgb", "comp_depth", "comp_mask")},
             {k: v.grad.numpy() for k, v in params.items()}, [s.numpy() for s in stats])
 
 
-def _worker(rank, world, port, tmp):
+def _worker(rank, world, port, tmp, reg=False):
+    from diff_gaussian_rasterization.view_shard import replicated_loss
+
     # file rendezvous (no TCP port to race for); `port` only makes the file name unique
     dist.init_process_group("gloo", init_method="file://" + os.path.join(tmp, f"rendezvous_{port}"), rank=rank,
                             world_size=world)
@@ -83,7 +93,8 @@ def _worker(rank, world, port, tmp):
         r = ViewShardedBatchRenderer(_render_view(params))
         out = r.batch_forward(_batch())
         assert out["view_range"] == shard_range(B, world, rank)
-        _loss(out).backward()
+        loss = _loss(out) + (replicated_loss(_regularisers(params)) if reg else 0)
+        loss.backward()
         allreduce_grads(list(params.values()))
         stats = reduce_densify_stats(out["radii"], out["viewspace_points"], out["visibility_filter"], 40)
         np.savez(os.path.join(tmp, f"rank{rank}.npz"),
@@ -104,10 +115,12 @@ def test_shard_range_covers_batch():
             assert max(sizes) - min(sizes) <= 1
 
 
-@pytest.mark.parametrize("world", [2, 3])
-def test_sharded_batch_equals_single_process(world, tmp_path):
-    ref_imgs, ref_grads, ref_stats = _single_process()
-    mp.spawn(_worker, args=(world, _free_port(), str(tmp_path)), nprocs=world, join=True)
+@pytest.mark.parametrize("world,reg", [(2, False), (3, False), (2, True)])
+def test_sharded_batch_equals_single_process(world, reg, tmp_path):
+    """reg: the loss also holds parameter-direct regularisers, added through replicated_loss on every rank
+    (without the 1/world scaling the summed all-reduce would count them `world` times)."""
+    ref_imgs, ref_grads, ref_stats = _single_process(reg)
+    mp.spawn(_worker, args=(world, _free_port(), str(tmp_path), reg), nprocs=world, join=True)
     for rank in range(world):
         z = np.load(tmp_path / f"rank{rank}.npz")
         for k, v in ref_imgs.items():
@@ -246,3 +259,65 @@ def test_densify_keeps_replicas_identical(synced, tmp_path):
         np.testing.assert_array_equal(z[0]["xyz"], z[1]["xyz"])
     else:
         assert not bool(z[0]["same"])
+
+
+def _grad_flag_worker(rank, world, port, tmp):
+    dist.init_process_group("gloo", init_method="file://" + os.path.join(tmp, f"rendezvous_{port}"), rank=rank,
+                            world_size=world)
+    try:
+        used = torch.zeros(4, dtype=torch.float64, requires_grad=True)      # every rank
+        only0 = torch.zeros(3, dtype=torch.float64, requires_grad=True)     # rank 0 only (a rank without views)
+        unused = torch.zeros(2, dtype=torch.float64, requires_grad=True)    # no rank
+        loss = (used * (rank + 1)).sum() + ((only0 * 2.0).sum() if rank == 0 else 0)
+        loss.backward()
+        allreduce_grads([used, only0, unused])
+        np.savez(os.path.join(tmp, f"flags{rank}.npz"), used=used.grad.numpy(), only0=only0.grad.numpy(),
+                 unused_none=unused.grad is None)
+    finally:
+        dist.destroy_process_group()
+
+
+def test_allreduce_keeps_untouched_grads_none(tmp_path):
+    """A parameter no rank has a gradient for keeps .grad = None (the single-process reference's state, which
+    optimizers skip); one only some ranks touched is summed with zeros from the others."""
+    world = 2
+    mp.spawn(_grad_flag_worker, args=(world, _free_port(), str(tmp_path)), nprocs=world, join=True)
+    for rank in range(world):
+        z = np.load(tmp_path / f"flags{rank}.npz")
+        np.testing.assert_array_equal(z["used"], np.full(4, 3.0))
+        np.testing.assert_array_equal(z["only0"], np.full(3, 2.0))
+        assert bool(z["unused_none"])
+
+
+class _TemporalRenderer:
+    """A per-view renderer that reads the camera's timestamp / frame index, as the temporal and spacetime
+    renderers do (renderer/diff_sugar_rasterizer_temporal.py:150,181, renderer/diff_gaussian_rasterizer_st.py:135),
+    and records the autocast state its forward runs under."""
+
+    def __init__(self, params):
+        self.geometry = object()
+        self.background_tensor = torch.zeros(3)
+        self.params = params
+        self.seen = []
+
+    def forward(self, cam, bg, **batch):
+        self.seen.append((float(cam.timestamp), int(cam.frame_idx), torch.is_autocast_enabled("cpu")))
+        t = self.params["means3D"].sum() * float(cam.timestamp)
+        P = 3
+        sp = torch.zeros(P, 3, requires_grad=True)
+        img = torch.ones(3, 4, 4, dtype=torch.float64) * t
+        return {"render": img, "viewspace_points": sp, "visibility_filter": torch.ones(P, dtype=torch.bool),
+                "radii": torch.ones(P, dtype=torch.int32)}
+
+
+def test_per_view_fallback_passes_timestamp_and_disables_autocast():
+    params = _params()
+    r = _TemporalRenderer(params)
+    batch = _batch()
+    batch.update(timestamp=torch.linspace(0.1, 0.5, B), frame_indices=torch.arange(B) + 7, height=4, width=4)
+    with torch.autocast(device_type="cpu", dtype=torch.bfloat16):
+        out = ViewShardedBatchRenderer(r).batch_forward(batch)
+    assert [s[1] for s in r.seen] == list(range(7, 7 + B))
+    np.testing.assert_allclose([s[0] for s in r.seen], np.linspace(0.1, 0.5, B), rtol=1e-6)
+    assert not any(s[2] for s in r.seen)
+    assert out["comp_rgb"].shape == (B, 4, 4, 3)

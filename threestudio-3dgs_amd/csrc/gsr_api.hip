@@ -167,7 +167,8 @@ static int check_set(int V, int P) {
 
 extern "C" {
 
-const char* gsr_version(void) { return "gsr 0.2.0 gfx950"; }
+const char* gsr_version(void) { return "gsr 0.3.0 gfx950"; }
+int gsr_abi_version(void) { return GSR_ABI_VERSION; }
 const char* gsr_last_error(void) { return g_err; }
 
 // ---- view sets ---------------------------------------------------------------------------
@@ -288,52 +289,77 @@ int gsr_composite_backward(int V, int height, int width, const float* dL_dout, c
   return last_launch();
 }
 
-static int shade_args(int V, int H, int W, int flags, int mode, const float* color, const float* depth,
+static int shade_args(int V, int H, int W, int flags, const int* modes, const float* color, const float* depth,
                       const float* alpha, const float* rays_o, const float* rays_d, const float* bg, int bg_layout,
                       const float* light, const float* pred_normal, const float* ambient, const float* diffuse,
                       ShadeArgs& A) {
-  if (V < 0 || H < 0 || W < 0 || V > 65535 || mode < 0 || mode > 2 || (flags & ~GSR_SHADE_MATERIAL) != 0)
-    return fail(GSR_EINVAL, "%s", "bad sizes / mode / flags");
+  if (V < 0 || H < 0 || W < 0 || (flags & ~GSR_SHADE_MATERIAL) != 0)
+    return fail(GSR_EINVAL, "%s", "bad sizes / flags");
   if (depth == nullptr || alpha == nullptr || rays_o == nullptr || rays_d == nullptr)
     return fail(GSR_EINVAL, "%s", "null pointer argument (depth / alpha / rays)");
   A = ShadeArgs{};
-  A.V = V, A.H = H, A.W = W, A.flags = flags, A.mode = mode, A.bg_layout = bg_layout;
+  A.V = V, A.H = H, A.W = W, A.flags = flags, A.bg_layout = bg_layout;
   A.color = color, A.depth = depth, A.alpha = alpha, A.rays_o = rays_o, A.rays_d = rays_d;
   A.bg = bg, A.light = light, A.pred_normal = pred_normal;
   if (flags & GSR_SHADE_MATERIAL) {
-    if (color == nullptr || bg == nullptr || light == nullptr || ambient == nullptr || diffuse == nullptr)
-      return fail(GSR_EINVAL, "%s", "material: color, bg, light, ambient and diffuse are required");
+    if (color == nullptr || bg == nullptr || light == nullptr || ambient == nullptr || diffuse == nullptr ||
+        modes == nullptr)
+      return fail(GSR_EINVAL, "%s", "material: color, bg, light, ambient, diffuse and modes are required");
     if (bg_layout != GSR_BG_CONSTANT && bg_layout != GSR_BG_HWC)
       return fail(GSR_EINVAL, "%s", "material: bg_layout must be GSR_BG_CONSTANT or GSR_BG_HWC");
-    for (int k = 0; k < 3; ++k) A.ka[k] = ambient[k], A.kd[k] = diffuse[k];
+    for (int v = 0; v < V; ++v)
+      if (modes[v] < GSR_SHADING_DIFFUSE || modes[v] > GSR_SHADING_TEXTURELESS)
+        return fail(GSR_EINVAL, "%s", "bad shading mode");
   }
   return GSR_OK;
 }
 
-int gsr_shade_forward(int V, int height, int width, int flags, int mode, const float* color, const float* depth,
-                      const float* alpha, const float* rays_o, const float* rays_d, const float* bg, int bg_layout,
-                      const float* light, const float* pred_normal, const float* ambient, const float* diffuse,
-                      float* render, float* normal_map, float* unit_normal, float* depth_out, void* stream) {
+// Launches in chunks of GSR_SET_MAX views, each with its views' light colours and modes in the arguments.
+static void shade_launch(ShadeArgs A, const ShadeGrads* G, const int* modes, const float* ambient,
+                         const float* diffuse, hipStream_t s) {
+  const int V = A.V;
+  for (int v0 = 0; v0 < V; v0 += GSR_SET_MAX) {
+    const int n = V - v0 < GSR_SET_MAX ? V - v0 : GSR_SET_MAX;
+    A.v0 = v0, A.V = n;
+    for (int i = 0; i < n; ++i) {
+      A.mode[i] = (A.flags & GSR_SHADE_MATERIAL) ? modes[v0 + i] : 0;
+      for (int k = 0; k < 3; ++k) {
+        A.ka[i][k] = (A.flags & GSR_SHADE_MATERIAL) ? ambient[3 * (v0 + i) + k] : 0.0f;
+        A.kd[i][k] = (A.flags & GSR_SHADE_MATERIAL) ? diffuse[3 * (v0 + i) + k] : 0.0f;
+      }
+    }
+    if (G == nullptr)
+      launch_shade_fwd(A, s);
+    else
+      launch_shade_bwd(A, *G, s);
+  }
+}
+
+int gsr_shade_views_forward(int V, int height, int width, int flags, const int* modes, const float* color,
+                            const float* depth, const float* alpha, const float* rays_o, const float* rays_d,
+                            const float* bg, int bg_layout, const float* light, const float* pred_normal,
+                            const float* ambient, const float* diffuse, float* render, float* normal_map,
+                            float* unit_normal, float* depth_out, void* stream) {
   ShadeArgs A;
-  if (shade_args(V, height, width, flags, mode, color, depth, alpha, rays_o, rays_d, bg, bg_layout, light,
+  if (shade_args(V, height, width, flags, modes, color, depth, alpha, rays_o, rays_d, bg, bg_layout, light,
                  pred_normal, ambient, diffuse, A) != GSR_OK)
     return GSR_EINVAL;
   if ((flags & GSR_SHADE_MATERIAL) && render == nullptr)
     return fail(GSR_EINVAL, "%s", "material: render output is required");
   if (V == 0 || height == 0 || width == 0) return last_launch();
   A.render = render, A.nmap = normal_map, A.unit = unit_normal, A.depth_out = depth_out;
-  launch_shade_fwd(A, (hipStream_t)stream);
+  shade_launch(A, nullptr, modes, ambient, diffuse, (hipStream_t)stream);
   return last_launch();
 }
 
-int gsr_shade_backward(int V, int height, int width, int flags, int mode, const float* color, const float* depth,
-                       const float* alpha, const float* rays_o, const float* rays_d, const float* bg, int bg_layout,
-                       const float* light, const float* pred_normal, const float* ambient, const float* diffuse,
-                       const float* dL_drender, const float* dL_dnormal_map, const float* dL_dunit_normal,
-                       const float* dL_ddepth_out, float* dL_dcolor, float* dL_ddepth, float* dL_dalpha,
-                       float* dL_dbg, void* stream) {
+int gsr_shade_views_backward(int V, int height, int width, int flags, const int* modes, const float* color,
+                             const float* depth, const float* alpha, const float* rays_o, const float* rays_d,
+                             const float* bg, int bg_layout, const float* light, const float* pred_normal,
+                             const float* ambient, const float* diffuse, const float* dL_drender,
+                             const float* dL_dnormal_map, const float* dL_dunit_normal, const float* dL_ddepth_out,
+                             float* dL_dcolor, float* dL_ddepth, float* dL_dalpha, float* dL_dbg, void* stream) {
   ShadeArgs A;
-  if (shade_args(V, height, width, flags, mode, color, depth, alpha, rays_o, rays_d, bg, bg_layout, light,
+  if (shade_args(V, height, width, flags, modes, color, depth, alpha, rays_o, rays_d, bg, bg_layout, light,
                  pred_normal, ambient, diffuse, A) != GSR_OK)
     return GSR_EINVAL;
   if (dL_ddepth == nullptr || dL_dalpha == nullptr) return fail(GSR_EINVAL, "%s", "dL_ddepth / dL_dalpha required");
@@ -343,8 +369,51 @@ int gsr_shade_backward(int V, int height, int width, int flags, int mode, const 
     return fail(GSR_EINVAL, "%s", "dL_dbg is formed for GSR_BG_HWC material shading only");
   if (V == 0 || height == 0 || width == 0) return last_launch();
   ShadeGrads G{dL_drender, dL_dnormal_map, dL_dunit_normal, dL_ddepth_out, dL_dcolor, dL_ddepth, dL_dalpha, dL_dbg};
-  launch_shade_bwd(A, G, (hipStream_t)stream);
+  shade_launch(A, &G, modes, ambient, diffuse, (hipStream_t)stream);
   return last_launch();
+}
+
+// one (ambient, diffuse, mode) for every view: the per-view tables filled with copies
+struct SharedLight {
+  std::vector<int> modes;
+  std::vector<float> ka, kd;
+  SharedLight(int V, int mode, const float* ambient, const float* diffuse)
+      : modes(V > 0 ? V : 0, mode), ka(3 * (size_t)(V > 0 ? V : 0)), kd(3 * (size_t)(V > 0 ? V : 0)) {
+    for (int v = 0; v < V; ++v)
+      for (int k = 0; k < 3; ++k) {
+        ka[3 * v + k] = ambient ? ambient[k] : 0.0f;
+        kd[3 * v + k] = diffuse ? diffuse[k] : 0.0f;
+      }
+  }
+};
+
+int gsr_shade_forward(int V, int height, int width, int flags, int mode, const float* color, const float* depth,
+                      const float* alpha, const float* rays_o, const float* rays_d, const float* bg, int bg_layout,
+                      const float* light, const float* pred_normal, const float* ambient, const float* diffuse,
+                      float* render, float* normal_map, float* unit_normal, float* depth_out, void* stream) {
+  if (V < 0 || V > 65535 || mode < 0 || mode > 2) return fail(GSR_EINVAL, "%s", "bad sizes / mode / flags");
+  if ((flags & GSR_SHADE_MATERIAL) && (ambient == nullptr || diffuse == nullptr))
+    return fail(GSR_EINVAL, "%s", "material: color, bg, light, ambient, diffuse and modes are required");
+  SharedLight L(V, mode, ambient, diffuse);
+  return gsr_shade_views_forward(V, height, width, flags, L.modes.data(), color, depth, alpha, rays_o, rays_d, bg,
+                                 bg_layout, light, pred_normal, L.ka.data(), L.kd.data(), render, normal_map,
+                                 unit_normal, depth_out, stream);
+}
+
+int gsr_shade_backward(int V, int height, int width, int flags, int mode, const float* color, const float* depth,
+                       const float* alpha, const float* rays_o, const float* rays_d, const float* bg, int bg_layout,
+                       const float* light, const float* pred_normal, const float* ambient, const float* diffuse,
+                       const float* dL_drender, const float* dL_dnormal_map, const float* dL_dunit_normal,
+                       const float* dL_ddepth_out, float* dL_dcolor, float* dL_ddepth, float* dL_dalpha,
+                       float* dL_dbg, void* stream) {
+  if (V < 0 || V > 65535 || mode < 0 || mode > 2) return fail(GSR_EINVAL, "%s", "bad sizes / mode / flags");
+  if ((flags & GSR_SHADE_MATERIAL) && (ambient == nullptr || diffuse == nullptr))
+    return fail(GSR_EINVAL, "%s", "material: color, bg, light, ambient, diffuse and modes are required");
+  SharedLight L(V, mode, ambient, diffuse);
+  return gsr_shade_views_backward(V, height, width, flags, L.modes.data(), color, depth, alpha, rays_o, rays_d, bg,
+                                  bg_layout, light, pred_normal, L.ka.data(), L.kd.data(), dL_drender,
+                                  dL_dnormal_map, dL_dunit_normal, dL_ddepth_out, dL_dcolor, dL_ddepth, dL_dalpha,
+                                  dL_dbg, stream);
 }
 
 size_t gsr_knn_workspace_bytes(int P) { return knn_workspace_bytes(P < 0 ? 0 : P); }

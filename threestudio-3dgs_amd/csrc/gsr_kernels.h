@@ -118,7 +118,8 @@ void launch_composite_bwd(int V, size_t HW, const float* dout, const float* colo
                           hipStream_t stream);
 // Shading / depth-normal epilogue — gsr_shading.hip (include/gsr.h gsr_shade_*).
 struct ShadeArgs {
-  int V, H, W, flags, mode, bg_layout;  // bg_layout: GSR_BG_CONSTANT (V, 3) or GSR_BG_HWC (V, H, W, 3)
+  // a launch covers views v0 .. v0+V-1 (V <= GSR_SET_MAX); the view planes below are the whole call's
+  int V, v0, H, W, flags, bg_layout;  // bg_layout: GSR_BG_CONSTANT (V, 3) or GSR_BG_HWC (V, H, W, 3)
   const float* color;        // (V, 3, H, W)   material only
   const float* depth;        // (V, 1, H, W)
   const float* alpha;        // (V, 1, H, W)
@@ -127,7 +128,10 @@ struct ShadeArgs {
   const float* bg;           // material only
   const float* light;        // (V, 3)         material only
   const float* pred_normal;  // (V, 3, H, W) or null
-  float ka[3], kd[3];        // ambient / diffuse light colours
+  // per view of the launch (index v - v0): ambient / diffuse light colours and shading mode — the material
+  // draws them per view (material/gaussian_material.py:59-64,80-88, called once per view)
+  float ka[GSR_SET_MAX][3], kd[GSR_SET_MAX][3];
+  int mode[GSR_SET_MAX];
   float* render;             // (V, 3, H, W)   material only
   float* nmap;               // (V, 3, H, W) or null
   float* unit;               // (V, 3, H, W) or null

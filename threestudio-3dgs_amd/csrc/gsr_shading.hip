@@ -91,7 +91,7 @@ __device__ __forceinline__ P3 pred_normal(const ShadeArgs& A, int v, size_t HW, 
 __global__ __launch_bounds__(256) void k_shade_fwd(ShadeArgs A) {
 #pragma clang fp contract(off)
   __shared__ float sX[3][STY + 2][STX + 2];
-  const int v = blockIdx.z;
+  const int lv = blockIdx.z, v = A.v0 + lv;
   const int x0 = blockIdx.x * STX, y0 = blockIdx.y * STY;
   const int t = threadIdx.x;
   for (int i = t; i < (STX + 2) * (STY + 2); i += 256) {
@@ -139,10 +139,10 @@ __global__ __launch_bounds__(256) void k_shade_fwd(ShadeArgs A) {
   const float ad = al + 1e-6f;
 #pragma unroll
   for (int k = 0; k < 3; ++k) {
-    const float tl = dl * A.kd[k] + A.ka[k];
+    const float tl = dl * A.kd[lv][k] + A.ka[lv][k];
     const float alb = A.color[plane + k * HW] / ad;
-    const float fg = A.mode == GSR_SHADING_DIFFUSE ? fminf(fmaxf(alb, 0.0f), 1.0f) * tl
-                                                   : (A.mode == GSR_SHADING_ALBEDO ? alb : tl);
+    const float fg = A.mode[lv] == GSR_SHADING_DIFFUSE ? fminf(fmaxf(alb, 0.0f), 1.0f) * tl
+                                                       : (A.mode[lv] == GSR_SHADING_ALBEDO ? alb : tl);
     const float img = fg * al + (1.0f - al) * bg_at(A, v, HW, p, k);
     A.render[plane + k * HW] = fminf(fmaxf(img, 0.0f), 1.0f);
   }
@@ -157,6 +157,8 @@ __device__ __forceinline__ void shade_bwd_pixel(const ShadeArgs& A, const ShadeG
 #pragma clang fp contract(off)
   const size_t HW = (size_t)A.H * A.W, p = (size_t)y * A.W + x;
   const size_t plane = (size_t)v * 3 * HW + p;
+  const int lv = v - A.v0;
+  const int mode = A.mode[lv];
   const P3 a = p3(sX[0][cy][cx + 1] - sX[0][cy][cx - 1], sX[1][cy][cx + 1] - sX[1][cy][cx - 1],
                   sX[2][cy][cx + 1] - sX[2][cy][cx - 1]);
   const P3 b = p3(sX[0][cy + 1][cx] - sX[0][cy - 1][cx], sX[1][cy + 1][cx] - sX[1][cy - 1][cx],
@@ -200,11 +202,11 @@ __device__ __forceinline__ void shade_bwd_pixel(const ShadeArgs& A, const ShadeG
     float gcol[3], gbg[3];
 #pragma unroll
     for (int k = 0; k < 3; ++k) {
-      const float tl = dl * A.kd[k] + A.ka[k];
+      const float tl = dl * A.kd[lv][k] + A.ka[lv][k];
       const float col = A.color[plane + k * HW];
       const float alb = col / (al + 1e-6f);
       const float albc = fminf(fmaxf(alb, 0.0f), 1.0f);
-      const float fg = A.mode == GSR_SHADING_DIFFUSE ? albc * tl : (A.mode == GSR_SHADING_ALBEDO ? alb : tl);
+      const float fg = mode == GSR_SHADING_DIFFUSE ? albc * tl : (mode == GSR_SHADING_ALBEDO ? alb : tl);
       const float bgk = bg_at(A, v, HW, p, k);
       const float img = fg * al + (1.0f - al) * bgk;
       const float gi = (img >= 0.0f && img <= 1.0f) ? G.d_render[plane + k * HW] : 0.0f;
@@ -212,15 +214,15 @@ __device__ __forceinline__ void shade_bwd_pixel(const ShadeArgs& A, const ShadeG
       dal += gi * (fg - bgk);
       gbg[k] = gi * (1.0f - al);
       float dalb = 0.0f, dtl = 0.0f;
-      if (A.mode == GSR_SHADING_DIFFUSE) {
+      if (mode == GSR_SHADING_DIFFUSE) {
         dalb = (alb >= 0.0f && alb <= 1.0f) ? dfg * tl : 0.0f;
         dtl = dfg * albc;
-      } else if (A.mode == GSR_SHADING_ALBEDO) {
+      } else if (mode == GSR_SHADING_ALBEDO) {
         dalb = dfg;
       } else {
         dtl = dfg;
       }
-      ddl += dtl * A.kd[k];
+      ddl += dtl * A.kd[lv][k];
       gcol[k] = dalb * rad;
       dad -= dalb * alb * rad;  // col / ad^2 = alb / ad
     }
@@ -259,7 +261,7 @@ __global__ __launch_bounds__(256) void k_shade_bwd(ShadeArgs A, ShadeGrads G) {
 #pragma clang fp contract(off)
   __shared__ float sX[3][STY + 4][STX + 4];
   __shared__ float sG[6][STY + 2][STX + 2];
-  const int v = blockIdx.z;
+  const int v = A.v0 + (int)blockIdx.z;
   const int x0 = blockIdx.x * STX, y0 = blockIdx.y * STY;
   const int t = threadIdx.x;
   for (int i = t; i < (STX + 4) * (STY + 4); i += 256) {

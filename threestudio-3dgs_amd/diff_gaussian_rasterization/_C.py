@@ -34,6 +34,7 @@ _sz = ctypes.c_size_t
 # name -> (restype, argtypes); must match include/gsr.h exactly (checked by tests/test_abi.py)
 SIGNATURES = {
     "gsr_version": (ctypes.c_char_p, []),
+    "gsr_abi_version": (_i, []),
     "gsr_last_error": (ctypes.c_char_p, []),
     "gsr_geom_bytes": (_sz, [_i]),
     "gsr_binning_bytes": (_sz, [_i, _i, _i]),
@@ -55,6 +56,10 @@ SIGNATURES = {
     "gsr_composite_backward": (_i, [_i, _i, _i, _vp, _vp, _vp, _vp, _i, _vp, _vp, _vp, _vp]),
     "gsr_shade_forward": (_i, [_i, _i, _i, _i, _i] + [_vp] * 6 + [_i] + [_vp] * 8 + [_vp]),
     "gsr_shade_backward": (_i, [_i, _i, _i, _i, _i] + [_vp] * 6 + [_i] + [_vp] * 12 + [_vp]),
+    "gsr_shade_views_forward": (_i, [_i, _i, _i, _i, ctypes.POINTER(_i)] + [_vp] * 6 + [_i] + [_vp] * 2
+                                + [ctypes.POINTER(_f)] * 2 + [_vp] * 4 + [_vp]),
+    "gsr_shade_views_backward": (_i, [_i, _i, _i, _i, ctypes.POINTER(_i)] + [_vp] * 6 + [_i] + [_vp] * 2
+                                 + [ctypes.POINTER(_f)] * 2 + [_vp] * 8 + [_vp]),
     "gsr_knn_workspace_bytes": (_sz, [_i]),
     "gsr_knn_mean_dist": (_i, [_i, _vp, _vp, _vp, _sz, _vp]),
     "gsr_set_geom_bytes": (_sz, [_i, _i]),
@@ -115,8 +120,11 @@ class GSRError(RuntimeError):
     pass
 
 
+ABI_VERSION = 3  # include/gsr.h GSR_ABI_VERSION this binding is written against
+
+
 def load_library(path: str | None = None):
-    """Load (once) and type the C-ABI library.  Raises ImportError if it is missing."""
+    """Load (once) and type the C-ABI library.  Raises ImportError if it is missing or of another ABI."""
     global _lib
     if _lib is not None and path is None:
         return _lib
@@ -127,6 +135,11 @@ def load_library(path: str | None = None):
             "build it with `make -C threestudio-3dgs_amd/csrc` (or __graft_entry__.build())"
         )
     lib = ctypes.CDLL(p)
+    abi = getattr(lib, "gsr_abi_version", None)
+    got = abi() if abi is not None else 1
+    if got != ABI_VERSION:
+        raise ImportError(f"diff_gaussian_rasterization: {p} has C-ABI revision {got}, this binding needs "
+                          f"{ABI_VERSION}; rebuild it with `make -C threestudio-3dgs_amd/csrc`")
     for name, (res, args) in SIGNATURES.items():
         fn = getattr(lib, name)
         fn.restype = res

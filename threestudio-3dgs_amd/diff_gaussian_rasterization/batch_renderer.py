@@ -14,24 +14,31 @@ renderer's epilogue fused on the GPU:
     "plain"         renderer/diff_gaussian_rasterizer.py:45-145          bg (randomly inverted), clamp
     "background"    renderer/diff_gaussian_rasterizer_background.py:44-145  bg = 0, background network
                                                                          composite + clamp fused into the blends
+    "advanced"      renderer/diff_gaussian_rasterizer_advanced.py:45-146 bg (randomly inverted), clamp,
+                                                                         depth and alpha outputs
     "shading"       renderer/diff_gaussian_rasterizer_shading.py:79-231  Depth2Normal + point-light
                                                                          material + composite (gsr_shade_*)
+    "normal"        renderer/diff_gaussian_rasterizer_normal.py:79-210   bg (randomly inverted), clamp,
+                                                                         Depth2Normal map + masked depth
     "sugar_normal"  renderer/diff_sugar_rasterizer_normal.py:80-223      two passes (colours, face normals)
                                                                          + normal-from-distance (gsr_shade_*)
 
 The mode comes from the renderer's ``batch_render_mode`` attribute or, when unset, from the module the
-renderer class is defined in (the reference's file names above).  Any other renderer (advanced, normal,
-st, temporal, sugar shading) keeps the reference's per-view loop, still on the HIP rasterizer.
+renderer class is defined in (the reference's file names above).  Any other renderer (st, temporal, sugar
+shading) keeps the reference's per-view loop, still on the HIP rasterizer.
 
 With ``torch.distributed`` initialised, every rank renders its contiguous slice of the batch
 (view_shard.shard_range) and the image outputs are all-gathered (RCCL over xGMI); the per-view lists
 hold the rank's own views and ``view_range`` says which.  Ranks with no view (batch < world) still take
 part in every gather with empty slices, so the collectives always match.
 
-Randomness follows the reference per view (background inversion); the material's random ambient ratio
-and shading mode (material/gaussian_material.py:52-96) are drawn once per batch — the fused shading
-epilogue takes one set of light colours per launch (the material's own comment: "adopt the same type of
-augmentation for the whole batch").
+Randomness follows the reference's per-view loop draw for draw: the background inversion
+(``np.random.rand()`` per view, renderer/diff_gaussian_rasterizer.py:59-64) and the material's soft-shading
+ambient ratio and shading mode (``random.random()`` per view, material/gaussian_material.py:59-64,80-88,
+called once per view by renderer/diff_gaussian_rasterizer_shading.py:200-205) are drawn for every view of
+the batch in view order — also on a rank that renders only some of them, so the draws consumed and the
+values each view gets are those of the single-process reference whatever the world size — and the fused
+shading epilogue takes one (ambient, diffuse, mode) per view.
 """
 from __future__ import annotations
 
@@ -45,13 +52,17 @@ import torch
 from .cameras import get_cam_info_gaussian
 from .view_shard import _world, all_gather_views, shard_range
 
-MODES = ("plain", "background", "shading", "sugar_normal")
+MODES = ("plain", "background", "advanced", "shading", "normal", "sugar_normal")
 _MODULE_MODES = {
     "diff_gaussian_rasterizer": "plain",
     "diff_gaussian_rasterizer_background": "background",
+    "diff_gaussian_rasterizer_advanced": "advanced",
     "diff_gaussian_rasterizer_shading": "shading",
+    "diff_gaussian_rasterizer_normal": "normal",
     "diff_sugar_rasterizer_normal": "sugar_normal",
 }
+# modes whose renderer draws a background inversion per view / calls the material per view
+_INVERT_BG = ("plain", "advanced", "normal", "sugar_normal")
 # batch dict image keys of the reference (renderer/gaussian_batch_renderer.py:78-121) -> channels
 _OUT_KEYS = (("comp_rgb", 3), ("comp_normal", 3), ("comp_normal_from_dist", 3), ("comp_pred_normal", 3),
              ("comp_depth", 1), ("comp_mask", 1))
@@ -98,9 +109,16 @@ def _depth_normal_views(*args, **kwargs):
     return depth_normal_views(*args, **kwargs)
 
 
+def _depth_normal_maps(*args, **kwargs):
+    from .shading import depth_normal_maps
+
+    return depth_normal_maps(*args, **kwargs)
+
+
 def material_params(material, training: bool):
-    """The point-light material's light colours and shading mode (material/gaussian_material.py:52-96
-    with ambient_ratio = shading = None, as the shading renderer calls it), drawn once for the batch."""
+    """The point-light material's light colours and shading mode for one view
+    (material/gaussian_material.py:52-96 with ambient_ratio = shading = None, as the shading renderer calls
+    it once per view): the same random draws, in the same order."""
     cfg = material.cfg
     if training and cfg.soft_shading:
         kd = random.random()
@@ -132,14 +150,47 @@ def _settings(pc, cams, bgs, H, W, scaling_modifier):
 
 
 def _inverted_bgs(renderer, n):
-    """Per-view background colour of the plain / SuGaR renderers: inverted unless a draw keeps it
-    (renderer/diff_gaussian_rasterizer.py:59-64, renderer/diff_sugar_rasterizer_normal.py:94-99)."""
+    """Per-view background colour of the plain / advanced / normal / SuGaR renderers: inverted unless a draw
+    keeps it (renderer/diff_gaussian_rasterizer.py:59-64, renderer/diff_sugar_rasterizer_normal.py:94-99)."""
     bg = renderer.background_tensor
     out = []
     for _ in range(n):
         invert = (np.random.rand() > renderer.cfg.invert_bg_prob) if renderer.training else True
         out.append(1.0 - bg if invert else bg)
     return out
+
+
+def batch_draws(renderer, mode: str, bs: int) -> dict:
+    """The random draws the reference's per-view loop makes for a batch of `bs` views, in view order:
+    "bgs" (per-view background colour) for the modes that invert it, "lights" (per-view (ka, kd, shading))
+    for the shading mode.  Every rank makes all of them and keeps its slice."""
+    out = {}
+    if mode in _INVERT_BG:
+        out["bgs"] = _inverted_bgs(renderer, bs)
+    if mode == "shading":
+        out["lights"] = [material_params(renderer.material, renderer.training) for _ in range(bs)]
+    return out
+
+
+def view_camera(batch: dict, batch_idx: int):
+    """The per-view camera of the reference's loop (renderer/gaussian_batch_renderer.py:22-49), including the
+    optional timestamp / frame index the temporal and spacetime renderers read."""
+    fovy = batch["fovy"][batch_idx]
+    w2c, proj, cam_p = get_cam_info_gaussian(c2w=batch["c2w"][batch_idx], fovx=fovy, fovy=fovy, znear=0.1, zfar=100)
+    dev = batch["c2w"].device
+    return Camera(FoVx=fovy, FoVy=fovy, image_width=batch["width"], image_height=batch["height"],
+                  world_view_transform=w2c.to(dev), full_proj_transform=proj.to(dev), camera_center=cam_p.to(dev),
+                  timestamp=batch["timestamp"][batch_idx] if "timestamp" in batch else None,
+                  frame_idx=batch["frame_indices"][batch_idx] if "frame_indices" in batch else None)
+
+
+def render_view_reference(renderer, batch: dict, batch_idx: int) -> dict:
+    """One iteration of the reference's loop: camera, then the renderer's forward in fp32 (autocast off,
+    renderer/gaussian_batch_renderer.py:51-54)."""
+    batch["batch_idx"] = batch_idx
+    cam = view_camera(batch, batch_idx)
+    with torch.autocast(device_type=batch["c2w"].device.type, enabled=False):
+        return renderer.forward(cam, renderer.background_tensor, **batch)
 
 
 def _placeholders(P, n, dev, dtype):
@@ -149,9 +200,10 @@ def _placeholders(P, n, dev, dtype):
     return [buf[v].requires_grad_(True) for v in range(n)]
 
 
-def render_views_local(renderer, batch: dict, mode: str, lo: int, hi: int) -> dict:
+def render_views_local(renderer, batch: dict, mode: str, lo: int, hi: int, draws: dict | None = None) -> dict:
     """Render views [lo, hi) of the batch with the fused path of `mode`.  Returns per-view stacked images
-    (n, C, H, W) under the batch dict's keys, plus the per-view lists."""
+    (n, C, H, W) under the batch dict's keys, plus the per-view lists.  `draws`: batch_draws of the whole
+    batch (made here for [lo, hi) only when not given)."""
     pc = renderer.geometry
     H, W = int(batch["height"]), int(batch["width"])
     means3D = pc.get_xyz
@@ -166,13 +218,37 @@ def render_views_local(renderer, batch: dict, mode: str, lo: int, hi: int) -> di
     scaling_modifier = float(batch.get("scaling_modifier", 1.0))
     override = batch.get("override_color")
     shs = pc.get_features if override is None else None
+    if draws is None:
+        draws = {k: [None] * lo + v for k, v in batch_draws(renderer, mode, n).items()}
+    draws = {k: v[lo:hi] for k, v in draws.items()}
     m2 = _placeholders(P, n, dev, means3D.dtype)
     common = dict(opacities=pc.get_opacity, scales=pc.get_scaling, rotations=pc.get_rotation)
+
+    def pred_normal_pass(settings):
+        # the predicted-normal call (renderer/diff_gaussian_rasterizer_shading.py:177-187,
+        # renderer/diff_gaussian_rasterizer_normal.py:175-185): same settings, SH = the geometry's normals
+        # (degree 0 through M = 1), a fresh zero means2D per view
+        zeros = [torch.zeros_like(m) for m in m2]
+        pred, _, _, _ = _rasterize_views(settings, means3D, zeros, shs=pc.get_normal.unsqueeze(1),
+                                         colors_precomp=None, **common)
+        return pred
+
     with torch.autocast(device_type=dev.type, enabled=False):
-        if mode == "plain":
-            settings = _settings(pc, cams, _inverted_bgs(renderer, n), H, W, scaling_modifier)
-            color, radii, _, _ = _rasterize_views(settings, means3D, m2, shs=shs, colors_precomp=override, **common)
+        if mode in ("plain", "advanced"):
+            settings = _settings(pc, cams, draws["bgs"], H, W, scaling_modifier)
+            color, radii, depth, alpha = _rasterize_views(settings, means3D, m2, shs=shs, colors_precomp=override,
+                                                          **common)
             out["comp_rgb"] = color.clamp(0, 1)
+            if mode == "advanced":
+                out.update(comp_depth=depth, comp_mask=alpha)
+        elif mode == "normal":
+            settings = _settings(pc, cams, draws["bgs"], H, W, scaling_modifier)
+            color, radii, depth, alpha = _rasterize_views(settings, means3D, m2, shs=shs, colors_precomp=override,
+                                                          **common)
+            nmap, depth_m = _depth_normal_maps(depth, alpha, batch["rays_o"][lo:hi], batch["rays_d"][lo:hi])
+            if getattr(pc.cfg, "pred_normal", False):
+                out["comp_pred_normal"] = pred_normal_pass(settings)
+            out.update(comp_rgb=color.clamp(0, 1), comp_normal=nmap, comp_depth=depth_m, comp_mask=alpha)
         elif mode == "background":
             zero = [renderer.background_tensor * 0] * n
             settings = _settings(pc, cams, zero, H, W, scaling_modifier)
@@ -192,17 +268,16 @@ def render_views_local(renderer, batch: dict, mode: str, lo: int, hi: int) -> di
                 bg_img = renderer.background(dirs=rays_d)
             pred = None
             if getattr(pc.cfg, "pred_normal", False):
-                zeros = [torch.zeros_like(m) for m in m2]
-                pred, _, _, _ = _rasterize_views(settings, means3D, zeros, shs=pc.get_normal.unsqueeze(1),
-                                                 colors_precomp=None, **common)
+                pred = pred_normal_pass(settings)
                 out["comp_pred_normal"] = pred
-            ka, kd, smode = material_params(renderer.material, renderer.training)
+            lights = draws["lights"]
             render, nmap, depth_m = _shade_views(color, depth, alpha, rays_o, rays_d, bg_img.reshape(n, H, W, 3),
-                                                 batch["light_positions"][lo:hi], ka, kd, smode, pred_normal=pred)
+                                                 batch["light_positions"][lo:hi], [x[0] for x in lights],
+                                                 [x[1] for x in lights], [x[2] for x in lights], pred_normal=pred)
             out.update(comp_rgb=render, comp_normal=nmap, comp_depth=depth_m, comp_mask=alpha,
                        comp_rgb_bg=bg_img.reshape(n, H, W, 3))
         elif mode == "sugar_normal":
-            settings = _settings(pc, cams, _inverted_bgs(renderer, n), H, W, scaling_modifier)
+            settings = _settings(pc, cams, draws["bgs"], H, W, scaling_modifier)
             # both rasterizer calls of the renderer (:157-166 colours, :182-191 face normals with a zero
             # means2D) from one geometry, sort and blend: the normals are the second colour set
             color, radii, depth, alpha, normal = _rasterize_views(settings, means3D, m2, shs=shs,
@@ -226,10 +301,11 @@ def render_views_local(renderer, batch: dict, mode: str, lo: int, hi: int) -> di
 
 
 def _mode_keys(renderer, mode):
-    keys = {"plain": ["comp_rgb"], "background": ["comp_rgb"],
+    keys = {"plain": ["comp_rgb"], "background": ["comp_rgb"], "advanced": ["comp_rgb", "comp_depth", "comp_mask"],
             "shading": ["comp_rgb", "comp_normal", "comp_depth", "comp_mask"],
+            "normal": ["comp_rgb", "comp_normal", "comp_depth", "comp_mask"],
             "sugar_normal": ["comp_rgb", "comp_normal", "comp_depth", "comp_mask"]}[mode]
-    if mode == "shading" and getattr(renderer.geometry.cfg, "pred_normal", False):
+    if mode in ("shading", "normal") and getattr(renderer.geometry.cfg, "pred_normal", False):
         keys.append("comp_pred_normal")
     return keys
 
@@ -239,7 +315,7 @@ def render_batch(renderer, batch: dict, mode: str, group=None, shard: bool = Tru
     bs = int(batch["c2w"].shape[0])
     world, rank = _world() if shard else (1, 0)
     lo, hi = shard_range(bs, world, rank)
-    local = render_views_local(renderer, batch, mode, lo, hi)
+    local = render_views_local(renderer, batch, mode, lo, hi, draws=batch_draws(renderer, mode, bs))
     H, W = int(batch["height"]), int(batch["width"])
     dev, dtype = renderer.geometry.get_xyz.device, renderer.geometry.get_xyz.dtype
     keys = _mode_keys(renderer, mode)
@@ -276,17 +352,7 @@ def reference_batch_forward(renderer, batch: dict) -> dict:
     lists = {k: [] for k in ("render", "viewspace_points", "visibility_filter", "radii", "normal",
                              "normal_from_dist", "pred_normal", "depth", "mask", "comp_rgb_bg")}
     for batch_idx in range(bs):
-        batch["batch_idx"] = batch_idx
-        fovy = batch["fovy"][batch_idx]
-        w2c, proj, cam_p = get_cam_info_gaussian(c2w=batch["c2w"][batch_idx], fovx=fovy, fovy=fovy, znear=0.1,
-                                                 zfar=100)
-        dev = batch["c2w"].device
-        cam = Camera(FoVx=fovy, FoVy=fovy, image_width=batch["width"], image_height=batch["height"],
-                     world_view_transform=w2c.to(dev), full_proj_transform=proj.to(dev), camera_center=cam_p.to(dev),
-                     timestamp=batch["timestamp"][batch_idx] if "timestamp" in batch else None,
-                     frame_idx=batch["frame_indices"][batch_idx] if "frame_indices" in batch else None)
-        with torch.autocast(device_type=dev.type, enabled=False):
-            pkg = renderer.forward(cam, renderer.background_tensor, **batch)
+        pkg = render_view_reference(renderer, batch, batch_idx)
         for k in ("render", "viewspace_points", "visibility_filter", "radii"):
             lists[k].append(pkg[k])
         for k in ("normal", "depth", "mask", "comp_rgb_bg"):
@@ -323,5 +389,5 @@ class GaussianBatchRenderer:
         return render_batch(self, batch, mode, group=self.shard_group, shard=self.shard_views)
 
 
-__all__ = ["GaussianBatchRenderer", "Camera", "MODES", "batch_mode", "material_params", "render_batch",
-           "render_views_local", "reference_batch_forward"]
+__all__ = ["GaussianBatchRenderer", "Camera", "MODES", "batch_mode", "batch_draws", "material_params", "render_batch",
+           "render_views_local", "render_view_reference", "reference_batch_forward", "view_camera"]

@@ -31,18 +31,36 @@ MATERIAL = 1
 _MODES = {"diffuse": 0, "albedo": 1, "textureless": 2}
 
 
-def _floats3(x):
+def _light_table(x, V):
+    """Light colours as V x 3 floats: one (3,) colour for every view, or (V, 3) per view."""
     if isinstance(x, torch.Tensor):
         x = x.detach().cpu().reshape(-1).tolist()
-    x = [float(t) for t in x]
-    if len(x) != 3:
-        raise ValueError("light colours need 3 components")
-    return (ctypes.c_float * 3)(*x)
+    else:
+        x = [float(t) for row in x for t in (row if isinstance(row, (list, tuple)) else [row])]
+    if len(x) == 3:
+        x = x * V
+    if len(x) != 3 * V:
+        raise ValueError(f"light colours need 3 or 3 x {V} components, got {len(x)}")
+    return tuple(float(t) for t in x)
+
+
+def _mode_table(shading, V):
+    modes = [shading] * V if isinstance(shading, str) else list(shading)
+    if len(modes) != V:
+        raise ValueError(f"{len(modes)} shading modes for {V} views")
+    for m in modes:
+        if m not in _MODES:
+            raise ValueError(f"Unknown shading type {m}")
+    return tuple(_MODES[m] for m in modes)
+
+
+def _c(ctype, values):
+    return (ctype * max(1, len(values)))(*values)
 
 
 class _Shade(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, color, depth, alpha, rays_o, rays_d, bg, light, pred_normal, flags, mode, bg_layout, ka, kd):
+    def forward(ctx, color, depth, alpha, rays_o, rays_d, bg, light, pred_normal, flags, modes, bg_layout, ka, kd):
         lib = _C.load_library()
         dev = depth.device
         _C._require_gpu(dev)
@@ -56,12 +74,12 @@ class _Shade(torch.autograd.Function):
         render = new(3) if material else None
         nmap, depth_out = new(3), new(1)
         unit = None if material else new(3)
-        ka_c, kd_c = _floats3(ka), _floats3(kd)
-        _C._check(lib.gsr_shade_forward(
-            V, H, W, flags, mode, _C._ptr(t["color"]), _C._ptr(t["depth"]), _C._ptr(t["alpha"]), _C._ptr(t["rays_o"]),
+        _C._check(lib.gsr_shade_views_forward(
+            V, H, W, flags, _c(ctypes.c_int, modes), _C._ptr(t["color"]), _C._ptr(t["depth"]), _C._ptr(t["alpha"]), _C._ptr(t["rays_o"]),
             _C._ptr(t["rays_d"]), _C._ptr(t["bg"]), bg_layout, _C._ptr(t["light"]), _C._ptr(t["pred_normal"]),
-            ka_c, kd_c, _C._ptr(render), _C._ptr(nmap), _C._ptr(unit), _C._ptr(depth_out), _C._stream(dev)))
-        ctx.meta = (flags, mode, bg_layout, ka, kd)
+            _c(ctypes.c_float, ka), _c(ctypes.c_float, kd), _C._ptr(render), _C._ptr(nmap), _C._ptr(unit),
+            _C._ptr(depth_out), _C._stream(dev)))
+        ctx.meta = (flags, modes, bg_layout, ka, kd)
         ctx.save_for_backward(t["color"], t["depth"], t["alpha"], t["rays_o"], t["rays_d"], t["bg"], t["light"],
                               t["pred_normal"])
         if material:
@@ -72,7 +90,7 @@ class _Shade(torch.autograd.Function):
     def backward(ctx, g0, g_nmap, g_depth):
         lib = _C.load_library()
         color, depth, alpha, rays_o, rays_d, bg, light, pred_normal = ctx.saved_tensors
-        flags, mode, bg_layout, ka, kd = ctx.meta
+        flags, modes, bg_layout, ka, kd = ctx.meta
         material = bool(flags & MATERIAL)
         dev = depth.device
         V, _, H, W = depth.shape
@@ -83,10 +101,10 @@ class _Shade(torch.autograd.Function):
         d_color = torch.empty_like(color) if material else None
         want_bg = material and ctx.needs_input_grad[5] and bg_layout == 1
         d_bg = torch.empty_like(bg) if want_bg else None
-        _C._check(lib.gsr_shade_backward(
-            V, H, W, flags, mode, _C._ptr(color), _C._ptr(depth), _C._ptr(alpha), _C._ptr(rays_o), _C._ptr(rays_d),
-            _C._ptr(bg), bg_layout, _C._ptr(light), _C._ptr(pred_normal), _floats3(ka), _floats3(kd),
-            _C._ptr(g_render), _C._ptr(g_nmap), _C._ptr(g_unit), _C._ptr(g_depth), _C._ptr(d_color),
+        _C._check(lib.gsr_shade_views_backward(
+            V, H, W, flags, _c(ctypes.c_int, modes), _C._ptr(color), _C._ptr(depth), _C._ptr(alpha), _C._ptr(rays_o),
+            _C._ptr(rays_d), _C._ptr(bg), bg_layout, _C._ptr(light), _C._ptr(pred_normal), _c(ctypes.c_float, ka),
+            _c(ctypes.c_float, kd), _C._ptr(g_render), _C._ptr(g_nmap), _C._ptr(g_unit), _C._ptr(g_depth), _C._ptr(d_color),
             _C._ptr(d_depth), _C._ptr(d_alpha), _C._ptr(d_bg), _C._stream(dev)))
         if material and ctx.needs_input_grad[5] and bg_layout == 0:
             # constant background colour per view: sum over pixels of g (1 - alpha), masked by the clamp
@@ -99,15 +117,16 @@ def _constant_bg_grad(ctx, g_render, color, depth, alpha, rays_o, rays_d, bg, li
     forms the per-pixel image gradient for an HWC background; a broadcast one is formed as an expanded
     HWC image and summed (a rare path: the reference passes the background network's image)."""
     lib = _C.load_library()
-    flags, mode, _, ka, kd = ctx.meta
+    flags, modes, _, ka, kd = ctx.meta
     V, _, H, W = depth.shape
     dev = depth.device
     bg_img = bg.view(V, 1, 1, 3).expand(V, H, W, 3).contiguous()
     d_bg = torch.empty_like(bg_img)
     scratch = [torch.empty_like(depth), torch.empty_like(alpha), torch.empty_like(color)]
-    _C._check(lib.gsr_shade_backward(
-        V, H, W, flags, mode, _C._ptr(color), _C._ptr(depth), _C._ptr(alpha), _C._ptr(rays_o), _C._ptr(rays_d),
-        _C._ptr(bg_img), 1, _C._ptr(light), _C._ptr(pred_normal), _floats3(ka), _floats3(kd), _C._ptr(g_render),
+    _C._check(lib.gsr_shade_views_backward(
+        V, H, W, flags, _c(ctypes.c_int, modes), _C._ptr(color), _C._ptr(depth), _C._ptr(alpha), _C._ptr(rays_o),
+        _C._ptr(rays_d), _C._ptr(bg_img), 1, _C._ptr(light), _C._ptr(pred_normal), _c(ctypes.c_float, ka),
+        _c(ctypes.c_float, kd), _C._ptr(g_render),
         None, None, None, _C._ptr(scratch[2]), _C._ptr(scratch[0]), _C._ptr(scratch[1]), _C._ptr(d_bg),
         _C._stream(dev)))
     return d_bg.sum(dim=(1, 2))
@@ -119,11 +138,13 @@ def _views(x, dims):
 
 
 def shade_views(color, depth, alpha, rays_o, rays_d, bg, light_positions, ambient=(0.1, 0.1, 0.1),
-                diffuse=(0.9, 0.9, 0.9), shading: str = "diffuse", pred_normal=None):
+                diffuse=(0.9, 0.9, 0.9), shading="diffuse", pred_normal=None):
     """The shading renderer's post-raster epilogue (renderer/diff_gaussian_rasterizer_shading.py:169-208)
     for one view or V views.  Returns ``(render, normal, depth)`` = the renderer's ``render``
     (``clamp(0, 1)`` applied), ``normal`` map and ``depth`` outputs.  ``pred_normal`` is the rasterized
-    predicted-normal image when ``pc.cfg.pred_normal`` (used detached, as in the reference)."""
+    predicted-normal image when ``pc.cfg.pred_normal`` (used detached, as in the reference).
+    ``ambient`` / ``diffuse`` are one (3,) light colour or (V, 3) per view, ``shading`` one mode or a
+    sequence of V modes: the material draws them per view (material/gaussian_material.py:59-64,80-88)."""
     single = depth.dim() == 3
     color, depth, alpha = _views(color, 3), _views(depth, 3), _views(alpha, 3)
     rays_o, rays_d = _views(rays_o, 3), _views(rays_d, 3)
@@ -135,11 +156,8 @@ def shade_views(color, depth, alpha, rays_o, rays_d, bg, light_positions, ambien
         bg_layout, bg = 1, bg.reshape(-1, H, W, 3).expand(V, H, W, 3)
     light = light_positions.reshape(-1, 3).expand(V, 3)
     rays_o, rays_d = rays_o.expand(V, H, W, 3), rays_d.expand(V, H, W, 3)
-    if shading not in _MODES:
-        raise ValueError(f"Unknown shading type {shading}")
-    out = _Shade.apply(color, depth, alpha, rays_o, rays_d, bg, light, pred_normal, MATERIAL, _MODES[shading],
-                       bg_layout, tuple(ambient) if not isinstance(ambient, torch.Tensor) else ambient,
-                       tuple(diffuse) if not isinstance(diffuse, torch.Tensor) else diffuse)
+    out = _Shade.apply(color, depth, alpha, rays_o, rays_d, bg, light, pred_normal, MATERIAL, _mode_table(shading, V),
+                       bg_layout, _light_table(ambient, V), _light_table(diffuse, V))
     return tuple(o[0] for o in out) if single else out
 
 
@@ -151,6 +169,17 @@ def depth_normal_views(depth, alpha, rays_o, rays_d):
     depth, alpha = _views(depth, 3), _views(alpha, 3)
     V, _, H, W = depth.shape
     rays_o, rays_d = _views(rays_o, 3).expand(V, H, W, 3), _views(rays_d, 3).expand(V, H, W, 3)
-    unit, nmap, _ = _Shade.apply(None, depth, alpha, rays_o, rays_d, None, None, None, 0, 0, 0, (0, 0, 0),
-                                 (0, 0, 0))
+    unit, nmap, _ = _Shade.apply(None, depth, alpha, rays_o, rays_d, None, None, None, 0, (), 0, (), ())
     return (unit[0], nmap[0]) if single else (unit, nmap)
+
+
+def depth_normal_maps(depth, alpha, rays_o, rays_d):
+    """The normal renderer's depth-to-normal epilogue (renderer/diff_gaussian_rasterizer_normal.py:172-193)
+    for V views: ``(normal, depth)`` = its ``normal`` output (``u * 0.5 * alpha + 0.5`` of the unit
+    Depth2Normal normal) and its ``depth`` output, both with the gradient kept only where ``alpha > 0.99``."""
+    single = depth.dim() == 3
+    depth, alpha = _views(depth, 3), _views(alpha, 3)
+    V, _, H, W = depth.shape
+    rays_o, rays_d = _views(rays_o, 3).expand(V, H, W, 3), _views(rays_d, 3).expand(V, H, W, 3)
+    _, nmap, depth_out = _Shade.apply(None, depth, alpha, rays_o, rays_d, None, None, None, 0, (), 0, (), ())
+    return (nmap[0], depth_out[0]) if single else (nmap, depth_out)

@@ -115,16 +115,39 @@ def _span_in_order(grads):
     return span if all(a < b for a, b in zip(offs, offs[1:])) else None
 
 
+def replicated_loss(term: torch.Tensor, group=None) -> torch.Tensor:
+    """A loss term every rank computes identically from the replicated parameters (the systems'
+    lambda_position / lambda_opacity / lambda_scales regularisers, system/gaussian_splatting.py:89-106),
+    scaled by 1/world: allreduce_grads SUMS the ranks' gradients, so the unscaled term would count `world`
+    times.  Image terms on the gathered batch need no scaling (their gradient reaches each view's own rank
+    only, view_shard.all_gather_views)."""
+    world = dist.get_world_size(group) if dist.is_available() and dist.is_initialized() else 1
+    return term if world == 1 else term / world
+
+
+def _has_grad_flags(params, group):
+    """Per parameter: does any rank hold a gradient for it (one small MAX all-reduce)?"""
+    mine = torch.tensor([p.grad is not None for p in params], dtype=torch.int32, device=_coll_device(group))
+    dist.all_reduce(mine, op=dist.ReduceOp.MAX, group=group)
+    return [bool(x) for x in mine.cpu().tolist()]
+
+
 def allreduce_grads(params, group=None, average: bool = False):
     """Sum (or average) the .grad of `params` over ranks in one flat bucket (one RCCL all-reduce).
 
     Every rank reduces the same elements in the same order — the order of `params` — so a rank whose
-    gradients are missing (a rank that rendered no view: .grad is None) takes part with zeros.  When the
-    gradients tile one buffer in that order (the batched rasterizer's carved gradients, batched.py:
+    gradients are missing (a rank that rendered no view: .grad is None) takes part with zeros.  A parameter
+    no rank has a gradient for keeps .grad = None, as in the single-process reference (optimizers skip it).
+    When the gradients tile one buffer in that order (the batched rasterizer's carved gradients, batched.py:
     means3D, scales, rotations, opacities, SH, ... — pass the parameters in that order) the buffer is
-    reduced in place, without a copy."""
+    reduced in place, without a copy.  Loss terms computed on every rank from the parameters directly go
+    through replicated_loss first."""
     world, _ = _world()
     if world == 1 or not params:
+        return
+    flags = _has_grad_flags(params, group)  # collective on every rank (which ranks lack a grad is rank-local)
+    params = [p for p, f in zip(params, flags) if f]
+    if not params:
         return
     for p in params:
         if p.grad is None:
@@ -207,15 +230,11 @@ class ViewShardedBatchRenderer:
     def _render_one(self, batch_idx, batch):
         if self.render_view is not None:
             return self.render_view(batch_idx, batch)
-        from .batch_renderer import Camera
-        from .cameras import get_cam_info_gaussian
+        from .batch_renderer import render_view_reference
 
-        fovy = batch["fovy"][batch_idx]
-        w2c, proj, cam_p = get_cam_info_gaussian(batch["c2w"][batch_idx], fovy, fovy, 0.1, 100)
-        dev = batch["c2w"].device
-        cam = Camera(FoVx=fovy, FoVy=fovy, camera_center=cam_p.to(dev), image_width=batch["width"],
-                     image_height=batch["height"], world_view_transform=w2c.to(dev), full_proj_transform=proj.to(dev))
-        return self.renderer.forward(cam, self.renderer.background_tensor, **batch)
+        # the reference loop's camera (with timestamp / frame index for the temporal and spacetime renderers)
+        # and its fp32 forward (autocast off), renderer/gaussian_batch_renderer.py:22-54
+        return render_view_reference(self.renderer, batch, batch_idx)
 
     def _per_view(self, batch: dict) -> dict:
         bs = int(batch["c2w"].shape[0])
