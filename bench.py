@@ -73,6 +73,11 @@ def parse():
                     help="PMC summary (profiles/summarize.py) supplying roofline.traffic and the VALU counts")
     ap.add_argument("--pairs", default=os.path.join(ROOT, "profiles", "r02_pairs.json"),
                     help="device-counted blend pairs (profiles/diag_pairs.py) for the VALU roofline")
+    ap.add_argument("--overlap-reduce", choices=["on", "off"], default="on",
+                    help="N > 1: sum the Gaussian gradients over ranks inside the backward, range by range as the "
+                         "per-Gaussian backward forms them (view_shard.ChunkedGradReduce, overlapped on a side "
+                         "stream) instead of one flat all-reduce after it")
+    ap.add_argument("--grad-chunks", type=int, default=4, help="Gaussian ranges of the overlapped reduction")
     ap.add_argument("--per-view-views", type=int, default=16,
                     help="views of the drop-in per-view path (one GaussianRasterizer call per view, the "
                          "reference's loop) timed after the headline, reported beside it (0 = skip)")
@@ -180,6 +185,9 @@ SUGAR_SEPARATE = os.environ.get("GSR_BENCH_SUGAR_SEPARATE") == "1"  # C5: two se
 SHADE_KA, SHADE_KD = (0.1, 0.1, 0.1), (0.9, 0.9, 0.9)  # the material's default ambient / diffuse colours
 
 
+GRAD_REDUCE = None  # view_shard.ChunkedGradReduce when the reduction is overlapped with the backward (N > 1)
+
+
 def render_views(rep: Replica, settings, bg_img, shade=None):
     """The rank's views through rasterize_views; one means2D placeholder per view, as the renderer loop
     creates (renderer/diff_gaussian_rasterizer.py:73-81); the background composite + clamp of
@@ -192,18 +200,21 @@ def render_views(rep: Replica, settings, bg_img, shade=None):
         from diff_gaussian_rasterization.shading import shade_views
 
         color, radii, depth, alpha = rasterize_views(settings, rep.means3D, m2, rep.opacities, shs=rep.shs,
-                                                     scales=rep.scales, rotations=rep.rotations)
+                                                     scales=rep.scales, rotations=rep.rotations,
+                                                     grad_reduce=GRAD_REDUCE)
         rays_o, rays_d, light = shade
         render, normal, depth_m = shade_views(color, depth, alpha, rays_o, rays_d, bg_img, light,
                                               SHADE_KA, SHADE_KD, "diffuse")
         return render, depth_m, alpha, radii, normal
     if COMPOSITE == "separate":
         color, radii, depth, alpha = rasterize_views(settings, rep.means3D, m2, rep.opacities, shs=rep.shs,
-                                                     scales=rep.scales, rotations=rep.rotations)
+                                                     scales=rep.scales, rotations=rep.rotations,
+                                                     grad_reduce=GRAD_REDUCE)
         return composite_background(color, alpha, bg_img), depth, alpha, radii
     # the composite + clamp fused into the forward / backward blends (bit-identical to the separate pass)
     comp, radii, depth, alpha = rasterize_views(settings, rep.means3D, m2, rep.opacities, shs=rep.shs,
-                                                scales=rep.scales, rotations=rep.rotations, background=bg_img)
+                                                scales=rep.scales, rotations=rep.rotations, background=bg_img,
+                                                grad_reduce=GRAD_REDUCE)
     return comp, depth, alpha, radii
 
 
@@ -231,7 +242,8 @@ def render_views_sugar(rep: Replica, settings, shade):
         # pass 2 (face normals, zero means2D) shares pass 1's geometry, sorts and blend (colors2)
         color, radii, depth, alpha, normal = rasterize_views(settings, rep.means3D, m2, rep.opacities,
                                                              colors_precomp=colors, scales=rep.scales,
-                                                             rotations=rep.rotations, colors2=rep.normals)
+                                                             rotations=rep.rotations, colors2=rep.normals,
+                                                             grad_reduce=GRAD_REDUCE)
     rays_o, rays_d, _ = shade
     _, nmap_dist = depth_normal_views(depth, alpha, rays_o, rays_d)
     normal = torch.nn.functional.normalize(normal, dim=1)
@@ -502,7 +514,12 @@ def main():
 
     import gsr_synthetic as gs
     from diff_gaussian_rasterization import _C
-    from diff_gaussian_rasterization.view_shard import all_gather_views, allreduce_grads, shard_range
+    from diff_gaussian_rasterization.view_shard import ChunkedGradReduce, all_gather_views, allreduce_grads, shard_range
+
+    global GRAD_REDUCE
+    overlap = world > 1 and args.overlap_reduce == "on" and args.path == "batched" and args.views >= world \
+        and not SUGAR_SEPARATE
+    GRAD_REDUCE = ChunkedGradReduce(n_chunks=args.grad_chunks) if overlap else None
 
     t_setup = time.perf_counter()
     if args.workload == "sugar":
@@ -570,7 +587,9 @@ def main():
                 ts += [o[4] for o in outs]
                 gs_ += list(up_n)
             torch.autograd.backward(ts, gs_)
-        allreduce_grads(rep.params)  # one flat RCCL all-reduce of the Gaussian parameter gradients
+        if GRAD_REDUCE is None:
+            allreduce_grads(rep.params)  # one flat RCCL all-reduce of the Gaussian parameter gradients
+        # (else the rasterizer's backward summed them over ranks range by range, overlapped with it)
         rep.zero_grad()
         bg_img.grad = None
 
@@ -636,8 +655,10 @@ def main():
                         "gradient all-reduce",
             "n_gaussians": args.gaussians, "resolution": [H, W], "sh_degree": args.sh_degree,
             "global_views_per_step": args.views, "views_per_rank": per,
-            "parallelism": (f"views sharded over {world} rank(s) ({comm} all-gather of the images, in-place "
-                            "all-reduce of the Gaussian gradients)" if world > 1 else "1 rank, no collectives"),
+            "parallelism": (f"views sharded over {world} rank(s) ({comm} all-gather of the images, " + (
+                f"all-reduce of the Gaussian gradients in {args.grad_chunks} ranges overlapped with the "
+                "per-Gaussian backward)" if GRAD_REDUCE is not None else "in-place all-reduce of the Gaussian "
+                "gradients)") if world > 1 else "1 rank, no collectives"),
             "mean_instances_K": round(K_mean),
             "mean_listed_instances": round(L_mean),
             "path": args.path,

@@ -57,7 +57,8 @@ const char* gsr_version(void);
  *   2  gsr_set_backward* `accumulate` CONTINUES every per-Gaussian sum from the stored value in view order
  *      (round 1's revision 1 added the new sums to the stored values); with accumulate in the scale / rotation
  *      path dL_dcov3D is required (the running dL/dcov3D carry), otherwise GSR_EINVAL.
- *   3  gsr_shade_views_forward / gsr_shade_views_backward (per-view light colours and shading modes).
+ *   3  gsr_shade_views_forward / gsr_shade_views_backward (per-view light colours and shading modes);
+ *      gsr_set_backward_chunks / gsr_grad_chunk_range (per-Gaussian sums in ranges, events for overlap).
  */
 #define GSR_ABI_VERSION 3
 int gsr_abi_version(void);
@@ -184,6 +185,21 @@ int gsr_set_backward(int V, int P, int degree, int M, const int* num_rendered, i
                      float* dL_dopacity, float* dL_dmeans3D, float* dL_dcov3D, float* dL_dsh,
                      float* dL_dscales, float* dL_drotations, int accumulate, void* work, size_t work_bytes,
                      void* stream);
+/*
+ * Overlap of the per-Gaussian sums with their reduction across ranks.  A backward's final
+ * per-Gaussian gradients are formed in one pass after the backward blend; gsr_set_backward_chunks asks the
+ * NEXT gsr_set_backward* call made on this thread to form them in n_chunks Gaussian ranges instead, recording
+ * events[c] (hipEvent_t, may be NULL) on the stream after range c, so that the caller can start reducing range
+ * c (e.g. an RCCL all-reduce on another stream waiting on the event) while the later ranges are computed.
+ * Range c = [c S, min(P, (c + 1) S)) with S = GSR_GRAD_CHUNK_ALIGN x ceil(ceil(P / n_chunks) / ALIGN)
+ * (gsr_grad_chunk_range); ranges may be empty.  Results are bitwise those of the unchunked call.  The request
+ * applies to one call only (n_chunks = 0 cancels it).
+ */
+#define GSR_GRAD_CHUNKS_MAX 16
+#define GSR_GRAD_CHUNK_ALIGN 4096
+int gsr_set_backward_chunks(int n_chunks, void* const* events);
+int gsr_grad_chunk_range(int P, int n_chunks, int chunk, int* g0, int* g1);
+
 /*
  * Two rasterizer calls that differ only in their colours, sharing one geometry (the SuGaR normal renderer,
  * renderer/diff_sugar_rasterizer_normal.py:157-191: the same Gaussians, camera and settings rendered with

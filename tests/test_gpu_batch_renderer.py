@@ -96,23 +96,31 @@ def _free_port():
     return p
 
 
-def _step(rank_world, B, tmp, tag):
-    """One training step of the background renderer on this process's views; saves the results."""
+def _step(rank_world, B, tmp, tag, overlap=False):
+    """One training step of the background renderer on this process's views; saves the results.  overlap:
+    the rasterizer's per-Gaussian gradients are summed over ranks inside its backward (ChunkedGradReduce)
+    instead of by allreduce_grads afterwards."""
     import torch.distributed as dist
 
     import densify_reference as dr
-    from diff_gaussian_rasterization.view_shard import allreduce_grads, replica_checksum, update_states_sharded
+    from diff_gaussian_rasterization.view_shard import (ChunkedGradReduce, allreduce_grads, replica_checksum,
+                                                        update_states_sharded)
 
     rank, world = rank_world
     scene = _scene("background")
     r = rf.FakeRenderer("background", scene, "cuda")
     model = dr.DensifyModel(scene, "cuda", densify_grad_threshold=2e-4)
     r.geometry = model
+    if overlap:
+        r.grad_reduce = ChunkedGradReduce(n_chunks=3)
     batch = rf.make_batch(B, H, W, "cuda", seed=5)
     out = r.batch_forward(batch)
     rf.loss_of(out).backward()
     params = model.parameters()
-    allreduce_grads(params)
+    if not overlap:
+        allreduce_grads(params)
+    else:
+        assert r.grad_reduce.launched == (1 if world > 1 else 0)
     grads = [p.grad.detach().cpu().numpy().copy() for p in params]
     update_states_sharded(model, 5, out)
     same = replica_checksum(model.parameters() + [model.max_radii2D]) if world > 1 else True
@@ -122,7 +130,7 @@ def _step(rank_world, B, tmp, tag):
         dist.barrier()
 
 
-def _worker(rank, world, port, tmp, B):
+def _worker(rank, world, port, tmp, B, overlap=False):
     import torch.distributed as dist
 
     torch.cuda.set_device(0)
@@ -131,18 +139,20 @@ def _worker(rank, world, port, tmp, B):
                             world_size=world)
     try:
         torch.manual_seed(100 + rank)
-        _step((rank, world), B, tmp, "shard")
+        _step((rank, world), B, tmp, "shard", overlap=overlap)
     finally:
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("B", [5, 4])
-def test_sharded_hip_path_world2(B, tmp_path):
+@pytest.mark.parametrize("B,overlap", [(5, False), (4, False), (5, True)])
+def test_sharded_hip_path_world2(B, overlap, tmp_path):
+    """overlap: ChunkedGradReduce — the per-Gaussian backward in Gaussian ranges with an event after each,
+    each range's rows all-reduced on a side stream while the next is formed (gsr_set_backward_chunks)."""
     import torch.multiprocessing as mp
 
     _step((0, 1), B, str(tmp_path), "single")
     single = np.load(tmp_path / "single0.npz")
-    mp.spawn(_worker, args=(2, _free_port(), str(tmp_path), B), nprocs=2, join=True)
+    mp.spawn(_worker, args=(2, _free_port(), str(tmp_path), B, overlap), nprocs=2, join=True)
     for rank in range(2):
         z = np.load(tmp_path / f"shard{rank}.npz")
         np.testing.assert_array_equal(z["comp_rgb"], single["comp_rgb"], err_msg=f"rank {rank} images")
@@ -152,6 +162,70 @@ def test_sharded_hip_path_world2(B, tmp_path):
             assert err.max() <= 1e-5, f"rank {rank} grad {i}: {err.max()}"
         assert bool(z["same"]), f"rank {rank}: replicas differ after densification"
         assert int(z["P"]) == int(single["P"]) > 20_000
+
+
+class _ForceChunks:
+    """A grad_reduce stand-in that makes a one-process backward run chunked (the ranges and events of
+    ChunkedGradReduce) without reducing anything."""
+
+    def __init__(self, n):
+        from diff_gaussian_rasterization.view_shard import ChunkedGradReduce
+
+        self._r = ChunkedGradReduce(n_chunks=n)
+        self.n_chunks = n
+        self.ranges_seen = 0
+
+    def active(self):
+        return True
+
+    def chunk_events(self, device):
+        return self._r.chunk_events(device)
+
+    def launch(self, grads, P, events=None):
+        for e in events:
+            e.synchronize()  # every range's event was recorded by the library
+        self.ranges_seen = len(events)
+
+
+@pytest.mark.parametrize("n_chunks,P", [(4, 20_000), (3, 4096 * 5 + 17), (16, 9000)])
+def test_chunked_gauss_backward_bitwise(n_chunks, P):
+    """gsr_set_backward_chunks: the per-Gaussian backward in Gaussian ranges (with events) gives bitwise the
+    gradients of the one-pass backward, also with the background composite and several view sets."""
+    from diff_gaussian_rasterization import GaussianRasterizationSettings
+    from diff_gaussian_rasterization.batched import rasterize_views
+
+    scene = gs.make_scene(P, sh_degree=2, seed=6)
+    batch = rf.make_batch(3, H, W, "cuda", seed=9)
+    from diff_gaussian_rasterization.cameras import get_cam_info_gaussian
+
+    fovy = batch["fovy"]
+    w2c, proj, campos = get_cam_info_gaussian(batch["c2w"], fovy, fovy, znear=0.1, zfar=100)
+    tan = math.tan(float(fovy[0]) * 0.5)
+    settings = [GaussianRasterizationSettings(image_height=H, image_width=W, tanfovx=tan, tanfovy=tan,
+                                              bg=torch.zeros(3, device="cuda"), scale_modifier=1.0,
+                                              viewmatrix=w2c[v], projmatrix=proj[v], sh_degree=2, campos=campos[v],
+                                              prefiltered=False, debug=False) for v in range(3)]
+    bg_img = torch.rand((3, H, W, 3), device="cuda", generator=torch.Generator("cuda").manual_seed(2))
+    up = torch.randn((3, 3, H, W), device="cuda", generator=torch.Generator("cuda").manual_seed(3))
+
+    def run(reduce):
+        t = {k: torch.tensor(scene[k], device="cuda", requires_grad=True)
+             for k in ("means3D", "shs", "opacities", "scales", "rotations")}
+        m2 = [torch.zeros((P, 3), device="cuda", requires_grad=True) for _ in range(3)]
+        out, _, _, _ = rasterize_views(settings, t["means3D"], m2, t["opacities"], shs=t["shs"], scales=t["scales"],
+                                       rotations=t["rotations"], background=bg_img, grad_reduce=reduce)
+        (out * up).sum().backward()
+        torch.cuda.synchronize()
+        return {k: v.grad.cpu() for k, v in t.items()}, [m.grad.cpu() for m in m2]
+
+    ref, ref_m2 = run(None)
+    force = _ForceChunks(n_chunks)
+    got, got_m2 = run(force)
+    assert force.ranges_seen == n_chunks
+    for k in ref:
+        assert torch.equal(ref[k], got[k]), k
+    for a, b in zip(ref_m2, got_m2):
+        assert torch.equal(a, b)
 
 
 # ---- C4: the 64-view MVDream-style batch at 1M Gaussians, single process vs two ranks ----------------------

@@ -321,3 +321,56 @@ def test_per_view_fallback_passes_timestamp_and_disables_autocast():
     np.testing.assert_allclose([s[0] for s in r.seen], np.linspace(0.1, 0.5, B), rtol=1e-6)
     assert not any(s[2] for s in r.seen)
     assert out["comp_rgb"].shape == (B, 4, 4, 3)
+
+
+def test_grad_chunk_range_matches_library():
+    from diff_gaussian_rasterization import _C
+    from diff_gaussian_rasterization.view_shard import grad_chunk_range
+
+    lib = _C.load_library()
+    import ctypes
+
+    for P in (0, 1, 4095, 4096, 4097, 100_000, 1_000_000, 1_966_080):
+        for n in (1, 2, 3, 4, 7, 16):
+            covered = 0
+            for c in range(n):
+                a, b = ctypes.c_int(), ctypes.c_int()
+                assert lib.gsr_grad_chunk_range(P, n, c, ctypes.byref(a), ctypes.byref(b)) == 0
+                assert (a.value, b.value) == grad_chunk_range(P, n, c)
+                assert a.value == min(covered, P) and b.value >= a.value
+                assert a.value % 4096 == 0 or a.value == P
+                covered = b.value
+            assert covered == P
+
+
+def _chunk_worker(rank, world, port, tmp):
+    from diff_gaussian_rasterization.view_shard import ChunkedGradReduce
+
+    dist.init_process_group("gloo", init_method="file://" + os.path.join(tmp, f"rendezvous_{port}"), rank=rank,
+                            world_size=world)
+    try:
+        P = 10_000
+        g = torch.Generator().manual_seed(rank)
+        shapes = [(P, 3), (P, 1), (P, 16, 3), (P, 4)]
+        a = [torch.randn(s, generator=g) for s in shapes]
+        b = [t.clone() for t in a]
+        params = [torch.zeros(s, requires_grad=True) for s in shapes]
+        for p, t in zip(params, a):
+            p.grad = t
+        allreduce_grads(params)
+        ChunkedGradReduce(n_chunks=3).launch(b, P)
+        np.savez(os.path.join(tmp, f"chunk{rank}.npz"), **{f"a{i}": p.grad.numpy() for i, p in enumerate(params)},
+                 **{f"b{i}": t.numpy() for i, t in enumerate(b)})
+    finally:
+        dist.destroy_process_group()
+
+
+def test_chunked_reduce_equals_flat(tmp_path):
+    """ChunkedGradReduce (range-by-range grouped all-reduces, overlapped with the backward on the GPU) gives
+    bitwise the flat all-reduce's sums."""
+    world = 2
+    mp.spawn(_chunk_worker, args=(world, _free_port(), str(tmp_path)), nprocs=world, join=True)
+    for rank in range(world):
+        z = np.load(tmp_path / f"chunk{rank}.npz")
+        for i in range(4):
+            np.testing.assert_array_equal(z[f"a{i}"], z[f"b{i}"])

@@ -106,6 +106,8 @@ static GaussBackwardArgs shared_args(int P, int degree, int M, const float* mean
                                      float* dL_drotations) {
   GaussBackwardArgs a;
   a.P = P;
+  a.g0 = 0;
+  a.g1 = P;
   a.deg = effective_degree(degree, M);
   a.M = shs ? M : 0;
   a.means3D = means3D;
@@ -551,6 +553,18 @@ int gsr_set_render_two_colors(int V, int P, const int* K, int width, int height,
                     out_render, stream, colors2, out_color2);
 }
 
+// One-shot per-thread request (gsr_set_backward_chunks) for the next backward call on this thread.
+struct GradChunks {
+  int n = 0;
+  void* events[GSR_GRAD_CHUNKS_MAX] = {};
+};
+static thread_local GradChunks g_next_chunks;
+
+static int grad_chunk_size(int P, int n) {
+  const int q = (P + n - 1) / n;
+  return (q + GSR_GRAD_CHUNK_ALIGN - 1) / GSR_GRAD_CHUNK_ALIGN * GSR_GRAD_CHUNK_ALIGN;
+}
+
 static int set_backward(int V, int P, int degree, int M, const int* K, int width, int height, const float* const* bgs,
                         const float* means3D, const float* scales, float scale_modifier, const float* rotations,
                         const float* shs, const float* cov3D_precomp, const float* const* viewmatrices,
@@ -562,6 +576,8 @@ static int set_backward(int V, int P, int degree, int M, const int* K, int width
                         void* work, size_t work_bytes, const float* comp_bg, const float* color, float* dL_dbg,
                         void* stream, const float* colors_override = nullptr, const float* colors2 = nullptr,
                         const float* dL_dcolor2 = nullptr, float* dL_dcolors2 = nullptr) {
+  const GradChunks chunks = g_next_chunks;  // consumed by this call, whatever its outcome
+  g_next_chunks = GradChunks{};
   if (check_set(V, P) != GSR_OK) return GSR_EINVAL;
   // both rasterizer calls of the SuGaR normal renderer in one pass (64-byte rows, 17-field records)
   const bool two = dL_dcolor2 != nullptr;
@@ -669,12 +685,45 @@ static int set_backward(int V, int P, int degree, int M, const int* K, int width
     }
     {
       PhaseScope ps(GSR_PHASE_GAUSS_BWD, s);
-      launch_gauss_backward(a, va, ab, s);
+      const bool last = g1 == V;
+      if (last && chunks.n > 0) {
+        // the final sums in Gaussian ranges, an event after each (the caller's reduction of a range starts
+        // while the next range is computed)
+        const int cs = grad_chunk_size(P, chunks.n);
+        for (int c = 0; c < chunks.n; ++c) {
+          GaussBackwardArgs ac = a;
+          ac.g0 = c * cs < P ? c * cs : P;
+          ac.g1 = (c + 1) * cs < P ? (c + 1) * cs : P;
+          launch_gauss_backward(ac, va, ab, s);
+          if (chunks.events[c] != nullptr) GSR_HIP_CHECK(hipEventRecord((hipEvent_t)chunks.events[c], s));
+        }
+      } else {
+        launch_gauss_backward(a, va, ab, s);
+      }
     }
     first = false;
     g0 = g1;
   }
   return last_launch();
+}
+
+int gsr_set_backward_chunks(int n_chunks, void* const* events) {
+  if (n_chunks < 0 || n_chunks > GSR_GRAD_CHUNKS_MAX || (n_chunks > 0 && events == nullptr))
+    return fail(GSR_EINVAL, "%s", "bad gradient chunk request");
+  g_next_chunks = GradChunks{};
+  g_next_chunks.n = n_chunks;
+  for (int c = 0; c < n_chunks; ++c) g_next_chunks.events[c] = events[c];
+  return GSR_OK;
+}
+
+int gsr_grad_chunk_range(int P, int n_chunks, int chunk, int* g0, int* g1) {
+  if (P < 0 || n_chunks < 1 || n_chunks > GSR_GRAD_CHUNKS_MAX || chunk < 0 || chunk >= n_chunks || g0 == nullptr ||
+      g1 == nullptr)
+    return fail(GSR_EINVAL, "%s", "bad gradient chunk query");
+  const int cs = grad_chunk_size(P, n_chunks);
+  *g0 = chunk * cs < P ? chunk * cs : P;
+  *g1 = (chunk + 1) * cs < P ? (chunk + 1) * cs : P;
+  return GSR_OK;
 }
 
 int gsr_set_backward(int V, int P, int degree, int M, const int* K, int width, int height, const float* const* bgs,

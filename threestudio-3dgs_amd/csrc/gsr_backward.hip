@@ -309,11 +309,11 @@ __global__ __launch_bounds__(256) void k_view_grad(GaussBackwardArgs a, ViewGrad
   const float4* grow = va.grow + (size_t)(TWO ? 4 : 3) * va.row_start[vl];
   float* recv = va.vrec + (size_t)vl * NF * a.P;
   // the next item's radius and record are loaded while the current one is processed
-  const int idx_base = (blockIdx.x / va.V) * (256 * GSR_VG_ITEMS) + t;
+  const int idx_base = a.g0 + (blockIdx.x / va.V) * (256 * GSR_VG_ITEMS) + t;
   int nrad = 0;
   GaussRec nrec;
   uint32_t ngo = 0u;
-  if (idx_base < a.P) {
+  if (idx_base < a.g1) {
     const size_t o0 = (size_t)vg * a.P + idx_base;
     nrad = va.radii[o0];
     if (nrad > 0) nrec = va.g.rec[o0], ngo = va.g.goff[o0];
@@ -321,12 +321,12 @@ __global__ __launch_bounds__(256) void k_view_grad(GaussBackwardArgs a, ViewGrad
 #pragma unroll 1
   for (int it = 0; it < GSR_VG_ITEMS; ++it) {
     const int idx = idx_base + it * 256;
-    if (idx >= a.P) break;
+    if (idx >= a.g1) break;
     const size_t o = (size_t)vg * a.P + idx;
     const int rad = nrad;
     const GaussRec gr = nrec;
     const uint32_t go = ngo;
-    if (it + 1 < GSR_VG_ITEMS && idx + 256 < a.P) {
+    if (it + 1 < GSR_VG_ITEMS && idx + 256 < a.g1) {
       nrad = va.radii[o + 256];
       if (nrad > 0) nrec = va.g.rec[o + 256], ngo = va.g.goff[o + 256];
     }
@@ -379,9 +379,9 @@ __global__ __launch_bounds__(256) void k_view_grad(GaussBackwardArgs a, ViewGrad
 __global__ __launch_bounds__(256) void k_gauss_accum(GaussBackwardArgs a, AccumArgs b) {
   extern __shared__ __attribute__((aligned(16))) float s_sh[];
   const int t = threadIdx.x;
-  const int block0 = blockIdx.x * 256;
+  const int block0 = a.g0 + blockIdx.x * 256;
   const int idx = block0 + t;
-  const int nblk = min(256, a.P - block0);
+  const int nblk = min(256, a.g1 - block0);
   const int F = 3 * a.M;
   const int S = sh_lds_stride(a.M);
   const bool has_sh = a.shs != nullptr && F > 0;
@@ -396,7 +396,7 @@ __global__ __launch_bounds__(256) void k_gauss_accum(GaussBackwardArgs a, AccumA
     }
     __syncthreads();
   }
-  if (idx < a.P) {
+  if (idx < a.g1) {
     const float3 mean = make_float3(a.means3D[3 * idx], a.means3D[3 * idx + 1], a.means3D[3 * idx + 2]);
     float3 dmean = make_float3(0.f, 0.f, 0.f);
     float dcov[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
@@ -550,17 +550,18 @@ __global__ __launch_bounds__(256) void k_gauss_accum(GaussBackwardArgs a, AccumA
 #define GSR_CUT_LDS_MAX (48 * 1024)
 
 void launch_gauss_backward(const GaussBackwardArgs& a, ViewGradArgs va, const AccumArgs& b, hipStream_t stream) {
-  if (a.P <= 0 || va.V <= 0) return;
+  const int n = a.g1 - a.g0;
+  if (n <= 0 || va.V <= 0) return;
   const size_t cut_bytes = sizeof(uint2) * (size_t)va.tiles;
   va.cut_in_lds = cut_bytes <= GSR_CUT_LDS_MAX ? 1 : 0;
   if (b.dcolors2)
-    hipLaunchKernelGGL(k_view_grad<true>, dim3(va.V * div_up(a.P, 256 * GSR_VG_ITEMS)), dim3(256),
+    hipLaunchKernelGGL(k_view_grad<true>, dim3(va.V * div_up(n, 256 * GSR_VG_ITEMS)), dim3(256),
                        va.cut_in_lds ? cut_bytes : 0, stream, a, va);
   else
-    hipLaunchKernelGGL(k_view_grad<false>, dim3(va.V * div_up(a.P, 256 * GSR_VG_ITEMS)), dim3(256),
+    hipLaunchKernelGGL(k_view_grad<false>, dim3(va.V * div_up(n, 256 * GSR_VG_ITEMS)), dim3(256),
                        va.cut_in_lds ? cut_bytes : 0, stream, a, va);
   const size_t lds = (a.shs && a.M > 0) ? (size_t)256 * sh_lds_stride(a.M) * sizeof(float) : 0;
-  hipLaunchKernelGGL(k_gauss_accum, dim3(div_up(a.P, 256)), dim3(256), lds, stream, a, b);
+  hipLaunchKernelGGL(k_gauss_accum, dim3(div_up(n, 256)), dim3(256), lds, stream, a, b);
 }
 
 }  // namespace gsr

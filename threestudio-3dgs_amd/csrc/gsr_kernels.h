@@ -78,6 +78,7 @@ void launch_render_backward(const RenderSet& rs, const GeomState& g, const uint3
 // Fused per-Gaussian backward over a batch of views — gsr_backward.hip
 struct GaussBackwardArgs {  // shared Gaussian parameters and the gradients of them (summed over views)
   int P, deg, M;
+  int g0, g1;  // the Gaussians [g0, g1) this launch covers (all: 0, P)
   const float *means3D, *scales, *rotations, *shs, *cov3D_precomp;
   float scale_modifier;
   float *dL_dcolors, *dL_dopacity, *dL_dmeans3D, *dL_dcov3D, *dL_dsh, *dL_dscales, *dL_drotations;

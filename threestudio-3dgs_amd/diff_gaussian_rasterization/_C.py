@@ -102,6 +102,8 @@ SIGNATURES = {
         + [ctypes.POINTER(_vp)] * 3 + [ctypes.POINTER(_f)] * 2 + [_vp] * 4 + [_vp] * 2 + [_vp] * 7
         + [_i, _vp, _sz, _vp],
     ),
+    "gsr_set_backward_chunks": (_i, [_i, ctypes.POINTER(_vp)]),
+    "gsr_grad_chunk_range": (_i, [_i, _i, _i, ctypes.POINTER(_i), ctypes.POINTER(_i)]),
     "gsr_profile_enable": (_i, [_i]),
     "gsr_profile_read": (_i, [ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_longlong), _i]),
 }

@@ -223,6 +223,13 @@ def render_views_local(renderer, batch: dict, mode: str, lo: int, hi: int, draws
     draws = {k: v[lo:hi] for k, v in draws.items()}
     m2 = _placeholders(P, n, dev, means3D.dtype)
     common = dict(opacities=pc.get_opacity, scales=pc.get_scaling, rotations=pc.get_rotation)
+    reduce = getattr(renderer, "grad_reduce", None)
+    if reduce is not None:  # the main call's per-Gaussian gradients summed over ranks inside its backward
+        if mode in ("shading", "normal") and getattr(pc.cfg, "pred_normal", False):
+            raise ValueError("grad_reduce covers one rasterizer call: not with the predicted-normal pass")
+        common_main = dict(common, grad_reduce=reduce)
+    else:
+        common_main = common
 
     def pred_normal_pass(settings):
         # the predicted-normal call (renderer/diff_gaussian_rasterizer_shading.py:177-187,
@@ -237,14 +244,14 @@ def render_views_local(renderer, batch: dict, mode: str, lo: int, hi: int, draws
         if mode in ("plain", "advanced"):
             settings = _settings(pc, cams, draws["bgs"], H, W, scaling_modifier)
             color, radii, depth, alpha = _rasterize_views(settings, means3D, m2, shs=shs, colors_precomp=override,
-                                                          **common)
+                                                          **common_main)
             out["comp_rgb"] = color.clamp(0, 1)
             if mode == "advanced":
                 out.update(comp_depth=depth, comp_mask=alpha)
         elif mode == "normal":
             settings = _settings(pc, cams, draws["bgs"], H, W, scaling_modifier)
             color, radii, depth, alpha = _rasterize_views(settings, means3D, m2, shs=shs, colors_precomp=override,
-                                                          **common)
+                                                          **common_main)
             nmap, depth_m = _depth_normal_maps(depth, alpha, batch["rays_o"][lo:hi], batch["rays_d"][lo:hi])
             if getattr(pc.cfg, "pred_normal", False):
                 out["comp_pred_normal"] = pred_normal_pass(settings)
@@ -254,13 +261,13 @@ def render_views_local(renderer, batch: dict, mode: str, lo: int, hi: int, draws
             settings = _settings(pc, cams, zero, H, W, scaling_modifier)
             bg_img = renderer.background(dirs=batch["rays_d"][lo:hi])
             render, radii, _, _ = _rasterize_views(settings, means3D, m2, shs=shs, colors_precomp=override,
-                                                   background=bg_img.reshape(n, H, W, 3), **common)
+                                                   background=bg_img.reshape(n, H, W, 3), **common_main)
             out["comp_rgb"] = render
         elif mode == "shading":
             zero = [renderer.background_tensor * 0] * n
             settings = _settings(pc, cams, zero, H, W, scaling_modifier)
             color, radii, depth, alpha = _rasterize_views(settings, means3D, m2, shs=shs, colors_precomp=override,
-                                                          **common)
+                                                          **common_main)
             rays_o, rays_d = batch["rays_o"][lo:hi], batch["rays_d"][lo:hi]
             if batch.get("override_bg_color") is not None:
                 bg_img = batch["override_bg_color"].reshape(1, 1, 1, 3).expand(n, H, W, 3)
@@ -282,7 +289,7 @@ def render_views_local(renderer, batch: dict, mode: str, lo: int, hi: int, draws
             # means2D) from one geometry, sort and blend: the normals are the second colour set
             color, radii, depth, alpha, normal = _rasterize_views(settings, means3D, m2, shs=shs,
                                                                   colors_precomp=override,
-                                                                  colors2=pc.get_gs_normals, **common)
+                                                                  colors2=pc.get_gs_normals, **common_main)
             if batch.get("compute_normal_from_dist", True):
                 _, nmap_dist = _depth_normal_views(depth, alpha, batch["rays_o"][lo:hi], batch["rays_d"][lo:hi])
                 out["comp_normal_from_dist"] = nmap_dist
@@ -381,6 +388,10 @@ class GaussianBatchRenderer:
     batch_render_mode = None
     shard_views = True
     shard_group = None
+    # view_shard.ChunkedGradReduce: the fused path's main rasterizer call sums its per-Gaussian gradients over
+    # ranks inside the backward (overlapped); needs a view on every rank (batch >= world).  The predicted-
+    # normal pass and any parameter-direct loss terms are not covered: reduce those with allreduce_grads.
+    grad_reduce = None
 
     def batch_forward(self, batch):
         mode = batch_mode(self)

@@ -55,8 +55,8 @@ class _ViewSet:
 
 class _RasterizeViews(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, settings_list, means3D, sh, colors_precomp, opacities, scales, rotations, cov3D_precomp,
-                composite_bg, colors2, *means2D):
+    def forward(ctx, settings_list, grad_reduce, means3D, sh, colors_precomp, opacities, scales, rotations,
+                cov3D_precomp, composite_bg, colors2, *means2D):
         lib = _C.load_library()
         V = len(settings_list)
         dev = means3D.device
@@ -129,6 +129,7 @@ class _RasterizeViews(torch.autograd.Function):
                     vs.V, P, Karr, W, H, _ptrs([c[3] for c in vs.cams]), p(vs.geom), p(vs.binning), p(vs.image),
                     p(color[sl]), p(depth[sl]), p(alpha[sl]), p(cbg[sl]), p(render[sl]), stream))
         ctx.settings = settings_list
+        ctx.grad_reduce = grad_reduce
         ctx.sets = sets
         ctx.bg_shape = tuple(composite_bg.shape) if composite_bg is not None else None
         ctx.save_for_backward(m3, shc, col, sc, rot, c3, radii, cbg, color if cbg is not None else None, c2)
@@ -167,7 +168,7 @@ class _RasterizeViews(torch.autograd.Function):
                 off += n
         d_m3, d_sc, d_rot, d_op = carved["m3"], carved["sc"], carved["rot"], carved["op"]
         d_sh, d_c3, d_col = carved["sh"], carved["c3"], carved["col"]
-        d_bg = torch.empty_like(cbg) if cbg is not None and ctx.needs_input_grad[8] else None
+        d_bg = torch.empty_like(cbg) if cbg is not None and ctx.needs_input_grad[9] else None
         # more than one view set in the scale / rotation path: the running dL/dcov3D the later sets
         # continue from (include/gsr.h gsr_set_backward, accumulate)
         d_c2 = torch.zeros((P, 3), **fopt) if second else None
@@ -191,7 +192,13 @@ class _RasterizeViews(torch.autograd.Function):
             fused2 = second and os.environ.get("GSR_TWO_COLOR_BWD", "fused") != "separate"
             if fused2:
                 g2 = g_color2.float().contiguous()
+            reducer = ctx.grad_reduce if ctx.grad_reduce is not None and ctx.grad_reduce.active() else None
+            events = reducer.chunk_events(dev) if reducer is not None else None
             for si, vs in enumerate(ctx.sets):
+                if events is not None and si == len(ctx.sets) - 1:
+                    # the last set's call forms the final per-Gaussian sums: in ranges, an event after each
+                    _C._check(lib.gsr_set_backward_chunks(
+                        len(events), _arr(ctypes.c_void_p, [e.cuda_event for e in events])))
                 Karr = _arr(ctypes.c_int, vs.K)
                 if fused2:
                     need = int(lib.gsr_set_backward_two_colors_bytes(vs.V, P, Karr))
@@ -243,15 +250,19 @@ class _RasterizeViews(torch.autograd.Function):
             d_bg = d_bg.reshape(ctx.bg_shape)
         if getattr(ctx, "needs_c3_scratch", False):
             d_c3 = None
-        grads = [None, d_m3, d_sh, d_col, d_op, d_sc, d_rot, d_c3, d_bg, d_c2] + [d_m2[v] for v in range(V)]
+        grads = [None, None, d_m3, d_sh, d_col, d_op, d_sc, d_rot, d_c3, d_bg, d_c2] + [d_m2[v] for v in range(V)]
         for k, need in enumerate(ctx.needs_input_grad):
             if not need:
                 grads[k] = None
+        if ctx.grad_reduce is not None and P > 0:
+            # the per-Gaussian gradients' sums over ranks, range by range as the backward finishes them
+            shared = [grads[k] for k in (2, 3, 4, 5, 6, 7, 8, 10)]
+            ctx.grad_reduce.launch(shared, P, events if P > 0 and ctx.grad_reduce.active() else None)
         return tuple(grads)
 
 
 def rasterize_views(settings_list, means3D, means2D_list, opacities, shs=None, colors_precomp=None, scales=None,
-                    rotations=None, cov3D_precomp=None, background=None, colors2=None):
+                    rotations=None, cov3D_precomp=None, background=None, colors2=None, grad_reduce=None):
     """Render V views of one set of Gaussians.  settings_list: V GaussianRasterizationSettings (same image
     size, same sh_degree, scale_modifier and prefiltered flag); means2D_list: V screen-space placeholders
     (P, 3) whose .grad receives each view's viewspace gradient.  Returns (color (V,3,H,W), radii (V,P),
@@ -267,7 +278,11 @@ def rasterize_views(settings_list, means3D, means2D_list, opacities, shs=None, c
     (renderer/diff_sugar_rasterizer_normal.py:182-191) — rendered from the same geometry, sorts and blend
     weights (include/gsr.h gsr_set_render_two_colors); a fifth output holds its colour image (V, 3, H, W).
     Its backward adds that call's parameter gradients (colors2 receives its colour gradient); its
-    screen-space gradient is not added to means2D, as in the reference."""
+    screen-space gradient is not added to means2D, as in the reference.
+
+    grad_reduce (view_shard.ChunkedGradReduce): with torch.distributed initialised, the per-Gaussian
+    parameter gradients are summed over ranks inside the backward, range by range as they are formed
+    (overlapping the per-Gaussian backward); the screen-space and background gradients stay per rank."""
     if (shs is None) == (colors_precomp is None):
         raise Exception("Please provide excatly one of either SHs or precomputed colors!")
     if ((scales is None or rotations is None) and cov3D_precomp is None) or (
@@ -285,5 +300,5 @@ def rasterize_views(settings_list, means3D, means2D_list, opacities, shs=None, c
         H, W = int(s0.image_height), int(s0.image_width)
         if background.numel() != len(settings_list) * H * W * 3:
             raise ValueError("background must hold (V, H, W, 3) values")
-    return _RasterizeViews.apply(list(settings_list), means3D, shs, colors_precomp, opacities, scales, rotations,
-                                 cov3D_precomp, background, colors2, *means2D_list)
+    return _RasterizeViews.apply(list(settings_list), grad_reduce, means3D, shs, colors_precomp, opacities, scales,
+                                 rotations, cov3D_precomp, background, colors2, *means2D_list)

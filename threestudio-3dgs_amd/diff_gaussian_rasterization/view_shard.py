@@ -170,6 +170,106 @@ def allreduce_grads(params, group=None, average: bool = False):
         off += n
 
 
+GRAD_CHUNKS_MAX = 16      # include/gsr.h GSR_GRAD_CHUNKS_MAX
+GRAD_CHUNK_ALIGN = 4096   # include/gsr.h GSR_GRAD_CHUNK_ALIGN
+
+
+def grad_chunk_range(P: int, n_chunks: int, chunk: int):
+    """Gaussian range [g0, g1) of gradient chunk `chunk` (include/gsr.h gsr_grad_chunk_range)."""
+    q = -(-P // n_chunks)
+    size = -(-q // GRAD_CHUNK_ALIGN) * GRAD_CHUNK_ALIGN
+    return min(chunk * size, P), min((chunk + 1) * size, P)
+
+
+def _coalesced_all_reduce(tensors, group):
+    """One grouped collective for a list of tensors (RCCL group call), or one call each."""
+    try:
+        from torch.distributed.distributed_c10d import _coalescing_manager
+    except ImportError:  # pragma: no cover
+        _coalescing_manager = None
+    if _coalescing_manager is not None and len(tensors) > 1 and dist.get_backend(group) == "nccl":
+        with _coalescing_manager(group=group, device=tensors[0].device):
+            for t in tensors:
+                dist.all_reduce(t, group=group)
+        return
+    for t in tensors:
+        dist.all_reduce(t, group=group)
+
+
+class ChunkedGradReduce:
+    """Sum over ranks of the rasterizer's per-Gaussian parameter gradients, overlapped with the backward that
+    forms them.
+
+    Passed to ``batched.rasterize_views(..., grad_reduce=...)``.  The backward then forms its final
+    per-Gaussian sums in `n_chunks` Gaussian ranges (include/gsr.h gsr_set_backward_chunks) with an event after
+    each; a communication stream waits on range c's event and all-reduces that range's rows of every
+    parameter gradient (one grouped RCCL call per range) while the later ranges are computed; the launch stream
+    then waits for the communication stream (GPU-side, no host block) before autograd hands the gradients to
+    the leaves.  Bitwise the same sums as allreduce_grads over the finished gradients.  Every rank must render
+    at least one view (the ranges' collectives are issued from the backward); the rasterizer's gradients are
+    then already reduced — do not pass those parameters to allreduce_grads again.  Parameter-direct loss terms
+    are not reduced here and need no replicated_loss scaling."""
+
+    def __init__(self, n_chunks: int = 4, group=None, average: bool = False):
+        if not 1 <= n_chunks <= GRAD_CHUNKS_MAX:
+            raise ValueError(f"n_chunks must be 1..{GRAD_CHUNKS_MAX}")
+        self.n_chunks, self.group, self.average = n_chunks, group, average
+        self._comm = None
+        self.launched = 0
+
+    def active(self) -> bool:
+        return _world()[0] > 1
+
+    def chunk_events(self, device):
+        """Events the backward records after each range (created now: torch creates them on first record)."""
+        if device.type != "cuda":
+            return None
+        evs = [torch.cuda.Event() for _ in range(self.n_chunks)]
+        for e in evs:
+            e.record()
+        return evs
+
+    def _stream(self, device):
+        if self._comm is None:
+            self._comm = torch.cuda.Stream(device=device)
+        return self._comm
+
+    def launch(self, grads, P: int, events=None):
+        """Reduce `grads` ((P, ...) tensors, rows = Gaussians) range by range; with `events` each range waits
+        for its event on the communication stream."""
+        grads = [g for g in grads if g is not None]
+        if not grads or not self.active():
+            return
+        world = _world()[0]
+        dev = grads[0].device
+        comm = self._stream(dev) if dev.type == "cuda" else None
+        for c in range(self.n_chunks):
+            g0, g1 = grad_chunk_range(P, self.n_chunks, c)
+            if g1 <= g0:
+                continue
+            parts = [g[g0:g1] for g in grads]
+            if comm is None:
+                _coalesced_all_reduce(parts, self.group)
+            else:
+                if events is not None:
+                    comm.wait_event(events[c])
+                else:
+                    comm.wait_stream(torch.cuda.current_stream(dev))
+                with torch.cuda.stream(comm):
+                    _coalesced_all_reduce(parts, self.group)
+                    if self.average:
+                        for t in parts:
+                            t.div_(world)
+            if comm is None and self.average:
+                for t in parts:
+                    t.div_(world)
+        if comm is not None:
+            for g in grads:
+                g.record_stream(comm)
+            torch.cuda.current_stream(dev).wait_stream(comm)
+        self.launched += 1
+
+
 def reduce_densify_stats(radii, viewspace_points, visibility_filter, num_points: int, group=None, device=None):
     """Per-Gaussian densification statistics over the whole batch (all ranks).
 
