@@ -38,7 +38,7 @@ def main():
     bg_img = torch.rand((V, R, R, 3), generator=gen, device=dev)
     ups = [torch.randn((V, 3, R, R), generator=gen, device=dev), torch.randn((V, 1, R, R), generator=gen, device=dev),
            torch.randn((V, 1, R, R), generator=gen, device=dev)]
-    buf = np.zeros(5, np.uint64)
+    buf = np.zeros(7, np.uint64)
     for it in range(2):  # the second pass is the counted one
         assert lib.gsr_diag_pairs(buf.ctypes.data, 1) == 0
         _C.RECENT_LISTED.clear()
@@ -66,6 +66,10 @@ def main():
         # lower bound of any batch-level rebalancing (ring, larger batches): the tile's busiest quadrant
         "bwd_tile_bound_slots_per_kept_pair": float(buf[4]) / max(1.0, float(buf[2])),
         "mean_listed_instances": listed,
+        # backward blend: candidates staged (every listed instance before the tile's deepest blended one) and
+        # those at least one quadrant keeps (the rest are gathered, culled and given a zero row)
+        "bwd_staged_candidates_per_view": float(buf[5]) / V,
+        "bwd_kept_candidates_per_view": float(buf[6]) / V,
         "note": "fwd evaluated = (pixel, candidate) iterations of lanes not yet terminated; slots include "
                 "terminated lanes; bwd pairs = kept (candidate, 8x8 quadrant) pairs x 64 pixels",
     }

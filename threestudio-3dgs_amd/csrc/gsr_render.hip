@@ -720,6 +720,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(TWO ? 4 : 5
   const float* bg = rs.bg[v];
   int tl_work = 0, tl_max = 0;
   int tl_q[4] = {0, 0, 0, 0};  // per-quadrant kept totals of the tile (the per-tile imbalance bound)
+  int tl_staged = 0, tl_any = 0;  // staged candidates / candidates kept by at least one quadrant
   // (the wave's quadrant is wave-uniform: readfirstlane keeps it and what derives from it in scalars)
   const int t = threadIdx.x, q = __builtin_amdgcn_readfirstlane(t >> 6), lane = t & 63;
   const int txi = tile % grid_x, tyi = tile / grid_x;
@@ -1081,6 +1082,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(TWO ? 4 : 5
       tl_work += c0 + c1 + c2 + c3;                                  // kept (candidate, quadrant) pairs
       tl_max += 4 * max(max(c0, c1), max(c2, c3));                  // lockstep cost in pair slots
       tl_q[0] += c0, tl_q[1] += c1, tl_q[2] += c2, tl_q[3] += c3;
+      tl_staged += min(hi, 64);
+      tl_any += __popcll(s.kmask[0] | s.kmask[1] | s.kmask[2] | s.kmask[3]);
     }
 #endif
 #ifdef GSR_EXP_NOFLUSH
@@ -1160,6 +1163,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(TWO ? 4 : 5
     atomicAdd(&g_pairs[3], 64ull * (unsigned long long)tl_max);
     // any batch-level scheme still waits for the tile's busiest quadrant: 4 x its total
     atomicAdd(&g_pairs[4], 256ull * (unsigned long long)max(max(tl_q[0], tl_q[1]), max(tl_q[2], tl_q[3])));
+    atomicAdd(&g_pairs[5], (unsigned long long)tl_staged);
+    atomicAdd(&g_pairs[6], (unsigned long long)tl_any);
   }
   if (threadIdx.x == 0 && blockIdx.x < GSR_TL_MAX)
     g_timeline[1][blockIdx.x] = make_uint4(tl_t0, (uint32_t)__builtin_amdgcn_s_memrealtime(), (uint32_t)tl_max,
@@ -1169,6 +1174,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(TWO ? 4 : 5
   (void)tl_work;
   (void)tl_max;
   (void)tl_q;
+  (void)tl_staged;
+  (void)tl_any;
 }
 
 void launch_render_backward(const RenderSet& rs, const GeomState& g, const uint32_t* sorted_gauss,
@@ -1192,14 +1199,14 @@ void launch_render_backward(const RenderSet& rs, const GeomState& g, const uint3
 }  // namespace gsr
 
 #ifdef GSR_TIMELINE
-// diagnostic build only: read (and optionally reset) the pair counters (5 x u64, see g_pairs)
+// diagnostic build only: read (and optionally reset) the pair counters (7 x u64, see g_pairs)
 extern "C" int gsr_diag_pairs(void* host, int reset) {
   if (hipDeviceSynchronize() != hipSuccess) return -1;
-  if (hipMemcpyFromSymbol(host, HIP_SYMBOL(gsr::g_pairs), 5 * sizeof(unsigned long long), 0,
+  if (hipMemcpyFromSymbol(host, HIP_SYMBOL(gsr::g_pairs), 7 * sizeof(unsigned long long), 0,
                           hipMemcpyDeviceToHost) != hipSuccess)
     return -1;
   if (reset) {
-    const unsigned long long z[5] = {0, 0, 0, 0, 0};
+    const unsigned long long z[7] = {0, 0, 0, 0, 0, 0, 0};
     if (hipMemcpyToSymbol(HIP_SYMBOL(gsr::g_pairs), z, sizeof(z), 0, hipMemcpyHostToDevice) != hipSuccess) return -1;
   }
   return 0;
