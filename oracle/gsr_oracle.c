@@ -390,8 +390,16 @@ static long g_stats[4];
 int g_oracle_threads = 1;
 void oracle_set_threads(int n) { g_oracle_threads = n > 0 ? n : 1; }
 int oracle_get_threads(void) { return g_oracle_threads; }
+/* Order in which the backward visits the pixels, i.e. in which every per-Gaussian gradient sum adds its
+ * per-pixel terms: 0 = tiles and pixels in raster order; 1 = both reversed.  The reference accumulates these
+ * sums with float atomicAdd from concurrently running pixel threads (BACKWARD::renderCUDA [EXT]), so its
+ * summation order is unspecified and changes from run to run: order 1 is another equally faithful run of it
+ * (tests/gsr_testutil.py uses the pair to measure how far the reference is from itself, row by row). */
+int g_oracle_order = 0;
+void oracle_set_order(int order) { g_oracle_order = order; }
 #else
 extern int g_oracle_threads;
+extern int g_oracle_order;
 #endif
 void FN(oracle_last_stats)(long* out) { for (int i = 0; i < 4; ++i) out[i] = g_stats[i]; }
 
@@ -541,7 +549,9 @@ void FN(oracle_backward)(int P, int deg, int M, const float* means, const float*
   const real ddelx_dx = RL(0.5) * W, ddely_dy = RL(0.5) * H;
   const int ntiles = c.gx * c.gy;
 #pragma omp parallel for num_threads(nth) schedule(dynamic, 1) if (nth > 1)
-  for (int tt = 0; tt < ntiles; ++tt) {
+  for (int tt0 = 0; tt0 < ntiles; ++tt0) {
+      const int rev = g_oracle_order == 1;
+      const int tt = rev ? ntiles - 1 - tt0 : tt0;
       const int ty = tt / c.gx, tx = tt - ty * c.gx;
       int me = 0;
 #ifdef _OPENMP
@@ -550,8 +560,9 @@ void FN(oracle_backward)(int P, int deg, int M, const float* means, const float*
       real* tacc = acc_all + nacc * (size_t)me;
       const uint32_t t = (uint32_t)tt;
       const uint32_t s = f.range[2 * t];
-      for (int ly = 0; ly < TILE; ++ly)
-        for (int lx = 0; lx < TILE; ++lx) {
+      for (int ly0 = 0; ly0 < TILE; ++ly0)
+        for (int lx0 = 0; lx0 < TILE; ++lx0) {
+          const int ly = rev ? TILE - 1 - ly0 : ly0, lx = rev ? TILE - 1 - lx0 : lx0;
           const int px = tx * TILE + lx, py = ty * TILE + ly;
           if (px >= W || py >= H) continue;
           const size_t pid = (size_t)py * W + px;

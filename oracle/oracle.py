@@ -78,8 +78,12 @@ def forward(scene: dict, cam, bg, prec: str = "f32", mod: float = 1.0):
     return dict(color=color, depth=depth, alpha=alpha, radii=radii[:P], K=int(K))
 
 
-def backward(scene: dict, cam, bg, dL_dcolor, dL_ddepth=None, dL_dalpha=None, prec: str = "f32", mod: float = 1.0):
+def backward(scene: dict, cam, bg, dL_dcolor, dL_ddepth=None, dL_dalpha=None, prec: str = "f32", mod: float = 1.0,
+             order: int = 0):
+    """order 1: the per-Gaussian sums add their per-pixel terms in the reverse pixel order (another run of the
+    reference's atomic accumulation, whose order is unspecified); 0 = raster order."""
     P, M, k, (W, H, tanx, tany) = _args(scene, cam, bg)
+    lib().oracle_set_order(ctypes.c_int(order))
     dt = _dtype(prec)
     n = max(P, 1)
     out = dict(means2D=np.zeros((n, 3), dt), colors=np.zeros((n, 3), dt), opacity=np.zeros((n, 1), dt),
@@ -93,6 +97,7 @@ def backward(scene: dict, cam, bg, dL_dcolor, dL_ddepth=None, dL_dalpha=None, pr
        ctypes.c_int(W), ctypes.c_int(H), ctypes.c_float(tanx), ctypes.c_float(tany), _p(k[10]),
        _p(gc), _p(gd), _p(ga), _p(out["means2D"]), _p(out["colors"]), _p(out["opacity"]), _p(out["means3D"]),
        _p(out["cov3D"]), _p(out["sh"]) if M > 0 else None, _p(out["scales"]), _p(out["rotations"]))
+    lib().oracle_set_order(ctypes.c_int(0))
     res = {key: v[:P] for key, v in out.items()}
     if M == 0:
         res["sh"] = np.zeros((P, 0, 3), dt)

@@ -30,6 +30,10 @@ FLIP_SLACK = 3
 # more); at most ROW_SLACK rows (besides the excused flip dependents) may break that.
 ROW_RATIO = 4.0
 ROW_SLACK = 3
+# The reference accumulates the per-Gaussian gradient sums with float atomics, so its own summation order is
+# unspecified: a second fp32 oracle run with the pixels visited in reverse order (oracle.backward order=1) is
+# another faithful run of it.  Where that run breaks the row rule against the first on `null` rows, the GPU
+# may break it on ROW_SLACK + 2 null rows ("as far from the reference as the reference is from itself").
 RAD_TIE = 1e-5
 RECT_TIE = 2e-5  # in tiles
 REPORT = []  # (what, name, stats) of every adjudication, printed by the tests with -s
@@ -123,11 +127,12 @@ def run_oracle(scene, cam, bg, grads=None, mod=1.0):
                W=cam["W"], H=cam["H"])
     if grads is not None:
         ref["b32"] = oracle.backward(scene, oc, bg, *grads, prec="f32", mod=mod)
+        ref["b32r"] = oracle.backward(scene, oc, bg, *grads, prec="f32", mod=mod, order=1)
         ref["b64"] = oracle.backward(scene, oc, bg, *grads, prec="f64", mod=mod)
     return ref
 
 
-def adjudicate(gpu, r32, r64, bar, what, name, cap=None, excuse=None, rowwise=False):
+def adjudicate(gpu, r32, r64, bar, what, name, cap=None, excuse=None, rowwise=False, r32b=None):
     """Rows (first axis) whose GPU value misses the fp64 value by more than `bar` (elementwise) may be at
     most FLIP_RATIO x the fp32 oracle's such rows + FLIP_SLACK; with `cap`, no GPU miss exceeds
     max(cap, 4 x the fp32 oracle's largest miss).  With `rowwise` (gradients) every element must also satisfy
@@ -156,8 +161,16 @@ def adjudicate(gpu, r32, r64, bar, what, name, cap=None, excuse=None, rowwise=Fa
     worst = ratio.reshape(n, -1).max(1) if n and ratio.size else np.zeros(0)
     worst_row = int(np.argmax(np.where(excuse, 0, worst))) if excuse is not None and n and worst.size else (
         int(np.argmax(worst)) if worst.size else -1)
+    null = 0
+    if r32b is not None and n:  # the reference against itself (another summation order)
+        e_b = np.abs(np.asarray(r32b, np.float64).reshape(r64.shape) - r64)
+        nb = (e_b > lim).reshape(n, -1).any(1) | (e_3 > np.maximum(bar, ROW_RATIO * e_b)).reshape(n, -1).any(1)
+        if excuse is not None:
+            nb = nb & ~excuse
+        null = int(nb.sum())
     st = dict(rows=int(n), gpu_miss=int(bad_g.sum()), f32_miss=int(bad_3.sum()),
               gpu_only_miss=int((bad_g & ~bad_3).sum()), beyond_ratio=int(beyond.sum()),
+              null_beyond=null if r32b is not None else None,
               worst_ratio=float(worst[worst_row]) if worst_row >= 0 else 0.0, worst_row=worst_row,
               max_err_gpu=float(e_g.max()) if e_g.size else 0.0, max_err_f32=float(e_3.max()) if e_3.size else 0.0,
               max_err_gpu_in_bar=float(e_g.reshape(n, -1)[ok_rows].max()) if ok_rows.any() and e_g.size else 0.0,
@@ -169,9 +182,10 @@ def adjudicate(gpu, r32, r64, bar, what, name, cap=None, excuse=None, rowwise=Fa
         lim = max(cap, 4.0 * st["max_err_f32"])
         assert st["max_err_gpu"] <= lim, f"{what}: {name}: miss {st['max_err_gpu']} beyond flip size {lim}: {st}"
     if rowwise:
-        assert st["beyond_ratio"] <= ROW_SLACK, (
+        allowed_rows = ROW_SLACK + 2 * null
+        assert st["beyond_ratio"] <= allowed_rows, (
             f"{what}: {name}: {st['beyond_ratio']} rows miss the fp64 value by more than max(bar, {ROW_RATIO} x the "
-            f"fp32 oracle's miss) (allowed {ROW_SLACK}): {st}")
+            f"fp32 oracle's miss) (allowed {allowed_rows}): {st}")
     return st
 
 
@@ -274,14 +288,15 @@ def flip_dependents(ref, pixels):
 def check_grads(gpu, ref, keys, what=""):
     """Elementwise |g - g64| <= 1e-4 max(1, |g64|) with fp32-oracle adjudication of flip-affected rows;
     rows of Gaussians blended at a pixel the GPU flipped on its own (check_forward) are excused."""
-    b32, b64 = ref["b32"], ref["b64"]
+    b32, b64, b32r = ref["b32"], ref["b64"], ref.get("b32r")
     excuse = flip_dependents(ref, ref.get("gpu_only_px", ())) if "aux64" in ref else None
     out = {}
     for k in keys:
         r64 = b64[k]
         bar = GRAD_TOL * np.maximum(1.0, np.abs(r64))
         ex = excuse if excuse is not None and excuse.shape[0] == r64.shape[0] else None
-        out[k] = adjudicate(gpu["g_" + k], b32[k], r64, bar, what, "grad " + k, excuse=ex, rowwise=True)
+        out[k] = adjudicate(gpu["g_" + k], b32[k], r64, bar, what, "grad " + k, excuse=ex, rowwise=True,
+                            r32b=b32r[k] if b32r is not None else None)
     return out
 
 

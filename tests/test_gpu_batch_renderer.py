@@ -273,8 +273,9 @@ def _c4_step(rank_world, B, S, tmp, tag, check_views=()):
     w = _c4_upstream(B, S).to("cuda")
     (out["comp_rgb"] * w).sum().backward()
     params = model.parameters()
+    grads = {f"pre{i}": p.grad.detach().cpu().numpy().copy() for i, p in enumerate(params)}  # this rank's sums
     allreduce_grads(params)
-    grads = {f"g{i}": p.grad.detach().cpu().numpy().copy() for i, p in enumerate(params)}
+    grads.update({f"g{i}": p.grad.detach().cpu().numpy().copy() for i, p in enumerate(params)})
     lo = out.get("view_range", (0, B))[0]
     extra = {}
     if check_views:  # the cameras exactly as render_views_local builds them (batched, on the device)
@@ -327,12 +328,16 @@ def test_c4_batch_single_vs_two_ranks(B, S, tmp_path):
     single = np.load(tmp_path / "single0.npz")
     torch.cuda.empty_cache()
     mp.spawn(_c4_worker, args=(2, _free_port(), str(tmp_path), B, S), nprocs=2, join=True)
-    for rank in range(2):
-        z = np.load(tmp_path / f"shard{rank}.npz")
+    zs = [np.load(tmp_path / f"shard{rank}.npz") for rank in range(2)]
+    for rank, z in enumerate(zs):
         np.testing.assert_array_equal(z["comp_rgb"], single["comp_rgb"], err_msg=f"rank {rank} images")
         for i in range(6):
+            # one process sums the 64 views' terms in view order, two ranks each sum their half and the
+            # all-reduce adds the halves: an fp32 reassociation whose rounding scales with the halves'
+            # magnitudes (they may cancel), so the bar is relative to max(1, |g|, |half_0| + |half_1|)
             g, ref = z[f"g{i}"].astype(np.float64), single[f"g{i}"].astype(np.float64)
-            err = np.abs(g - ref) / np.maximum(np.abs(ref), 1.0)
+            halves = np.abs(zs[0][f"pre{i}"].astype(np.float64)) + np.abs(zs[1][f"pre{i}"].astype(np.float64))
+            err = np.abs(g - ref) / np.maximum(np.maximum(np.abs(ref), halves), 1.0)
             assert err.max() <= 1e-5, f"rank {rank} grad {i}: {err.max()}"
         assert bool(z["same"]), f"rank {rank}: replicas differ after densification"
         assert int(z["P"]) == int(single["P"]) > C4_P
@@ -361,6 +366,9 @@ def _c4_oracle_views(single, B, S, views):
             gcol, ga = _composite_upstream(g_r, np.zeros((1, S, S), np.float32), pre, bg_img[v])
             b[prec] = oracle.backward(scene, oracle_cam(cam), np.zeros(3, np.float32), gcol.astype(np.float32),
                                       np.zeros((1, S, S), np.float32), ga.astype(np.float32), prec=prec)
+            if prec == "f32":
+                b["f32r"] = oracle.backward(scene, oracle_cam(cam), np.zeros(3, np.float32), gcol.astype(np.float32),
+                                            np.zeros((1, S, S), np.float32), ga.astype(np.float32), prec=prec, order=1)
         px = lambda a: np.asarray(a).reshape(3, -1).T  # noqa: E731
         gpu_img = single["comp_rgb"][v].transpose(2, 0, 1)
         adjudicate(px(gpu_img), px(b["render_f32"]), px(b["render_f64"]), 1e-5, f"C4 {S}^2 view {v}", "comp_rgb",
@@ -368,4 +376,4 @@ def _c4_oracle_views(single, B, S, views):
         check_radii(single[f"radii_{v}"], ref, f"C4 {S}^2 view {v}")
         m64 = b["f64"]["means2D"]
         adjudicate(single[f"m2_{v}"], b["f32"]["means2D"], m64, 1e-4 * np.maximum(1.0, np.abs(m64)),
-                   f"C4 {S}^2 view {v}", "grad means2D", rowwise=True)
+                   f"C4 {S}^2 view {v}", "grad means2D", rowwise=True, r32b=b["f32r"]["means2D"])

@@ -147,15 +147,20 @@ def test_c3_views_fused_background_composite():
             gcol, ga = _composite_upstream(g_r, g_a, pre, bg_img[v])
             b[prec] = oracle.backward(scene, oracle_cam(cam), np.zeros(3, np.float32), gcol, g_d, ga,
                                       prec=prec)
+            if prec == "f32":  # another run of the reference's (unordered, atomic) accumulation
+                b["f32r"] = oracle.backward(scene, oracle_cam(cam), np.zeros(3, np.float32), gcol, g_d, ga,
+                                            prec=prec, order=1)
             b["bg_" + prec] = (gcol * (dt(1) - f["alpha"].astype(dt))).transpose(1, 2, 0)
         check_forward(_view(gpu, v), ref, f"C3 view {v}", K_gpu=gpu["K"][v])
         adjudicate(gpu["g_means2D"][v], b["f32"]["means2D"], b["f64"]["means2D"],
-                   1e-4 * np.maximum(1.0, np.abs(b["f64"]["means2D"])), f"C3 view {v}", "grad means2D", rowwise=True)
+                   1e-4 * np.maximum(1.0, np.abs(b["f64"]["means2D"])), f"C3 view {v}", "grad means2D", rowwise=True,
+                   r32b=b["f32r"]["means2D"])
         adjudicate(gpu["g_background"][v].reshape(-1, 3), b["bg_f32"].reshape(-1, 3), b["bg_f64"].reshape(-1, 3),
                    1e-4 * np.maximum(1.0, np.abs(b["bg_f64"].reshape(-1, 3))), f"C3 view {v}", "grad background",
                    rowwise=True)
         refs.append(b)
-    tot = dict(b32=_sum_grads(refs, "f32", GRAD_KEYS), b64=_sum_grads(refs, "f64", GRAD_KEYS))
+    tot = dict(b32=_sum_grads(refs, "f32", GRAD_KEYS), b64=_sum_grads(refs, "f64", GRAD_KEYS),
+               b32r=_sum_grads(refs, "f32r", GRAD_KEYS))
     check_grads(gpu, tot, GRAD_KEYS, "C3 summed")
 
 
@@ -173,9 +178,10 @@ def test_view_set_vs_oracle():
         check_forward(_view(gpu, v), ref, f"set view {v}", K_gpu=gpu["K"][v])
         adjudicate(gpu["g_means2D"][v], ref["b32"]["means2D"], ref["b64"]["means2D"],
                    1e-4 * np.maximum(1.0, np.abs(ref["b64"]["means2D"])), f"set view {v}", "grad means2D",
-                   rowwise=True)
+                   rowwise=True, r32b=ref["b32r"]["means2D"])
         refs.append(ref)
-    tot = dict(b32=_sum_grads(refs, "b32", GRAD_KEYS), b64=_sum_grads(refs, "b64", GRAD_KEYS))
+    tot = dict(b32=_sum_grads(refs, "b32", GRAD_KEYS), b64=_sum_grads(refs, "b64", GRAD_KEYS),
+               b32r=_sum_grads(refs, "b32r", GRAD_KEYS))
     check_grads(gpu, tot, GRAD_KEYS, "set summed")
 
 
@@ -347,28 +353,34 @@ def test_c5_sugar_normal_renderer():
     ref2 = run_oracle(sc2, cam, [0.0, 0.0, 0.0])
     check_forward(gpu_pass1, ref1, "C5 pass 1")
     epi, grads = {}, {}
-    for prec, dt in (("f32", torch.float32), ("f64", torch.float64)):
+    # f32r: the fp32 oracle again with the per-Gaussian sums in reverse pixel order (another run of the
+    # reference's unordered atomic accumulation): the rows it moves measure the reference against itself
+    for prec, dt in (("f32", torch.float32), ("f64", torch.float64), ("f32r", torch.float32)):
+        order = 1 if prec == "f32r" else 0
+        prec, key = ("f32", "f32r") if prec == "f32r" else (prec, prec)
         f1, f2 = ref1[prec], ref2[prec]
         lc, ld, la, ln = (torch.tensor(x, dtype=dt, requires_grad=True)
                           for x in (f1["color"], f1["depth"], f1["alpha"], f2["color"]))
         o = _sugar_epilogue(torch, lc, ld, la, ln, rays_o.to(dt), rays_d.to(dt),
                             lambda dd, aa: tr.sugar_normal_from_dist(dd, aa, rays_o.to(dt), rays_d.to(dt)))
         loss_of(o, lambda x: torch.tensor(x, dtype=dt)).backward()
-        epi[prec] = {k: o[k].detach().numpy() for k in SUGAR_OUT}
+        epi[key] = {k: o[k].detach().numpy() for k in SUGAR_OUT}
         as32 = lambda x: x.grad.numpy().astype(np.float32)  # noqa: E731  (the C ABI takes fp32 gradients)
-        b1 = oracle.backward(sc1, oracle_cam(cam), np.zeros(3, np.float32), as32(lc), as32(ld), as32(la), prec=prec)
-        b2 = oracle.backward(sc2, oracle_cam(cam), np.zeros(3, np.float32), as32(ln), None, None, prec=prec)
-        grads[prec] = {k: np.asarray(b1[k], np.float64) + np.asarray(b2[k], np.float64)
-                       for k in ("means3D", "scales", "rotations", "opacity")}
-        grads[prec]["colors"] = b1["colors"]
-        grads[prec]["normals"] = b2["colors"]
-        grads[prec]["means2D"] = b1["means2D"]
+        b1 = oracle.backward(sc1, oracle_cam(cam), np.zeros(3, np.float32), as32(lc), as32(ld), as32(la), prec=prec,
+                             order=order)
+        b2 = oracle.backward(sc2, oracle_cam(cam), np.zeros(3, np.float32), as32(ln), None, None, prec=prec,
+                             order=order)
+        grads[key] = {k: np.asarray(b1[k], np.float64) + np.asarray(b2[k], np.float64)
+                      for k in ("means3D", "scales", "rotations", "opacity")}
+        grads[key]["colors"] = b1["colors"]
+        grads[key]["normals"] = b2["colors"]
+        grads[key]["means2D"] = b1["means2D"]
     for k in SUGAR_OUT:
         a64 = epi["f64"][k]
         rows = lambda x: np.asarray(x).reshape(x.shape[0], -1).T  # noqa: E731
         adjudicate(rows(gpu_out[k]), rows(epi["f32"][k]), rows(a64), 1e-5 + 1e-5 * np.abs(rows(a64)), "C5", k,
                    cap=0.05 * max(1.0, float(np.abs(a64).max())))
-    check_grads(gpu_grads, dict(b32=grads["f32"], b64=grads["f64"]),
+    check_grads(gpu_grads, dict(b32=grads["f32"], b64=grads["f64"], b32r=grads["f32r"]),
                 ["means3D", "means2D", "opacity", "colors", "normals", "scales", "rotations"], "C5")
     check_radii(gpu_pass1["radii"], ref1, "C5 pass 1")
 
@@ -434,18 +446,18 @@ def test_second_colors_match_separate_call(bwd, monkeypatch):
     sc2 = dict(scene, colors_precomp=normals)
     sc2.pop("shs")
     ref = {}
-    for prec in ("f32", "f64"):
+    for prec, order, key in (("f32", 0, "b32"), ("f64", 0, "b64"), ("f32", 1, "b32r")):
         acc = {}
         for v, cam in enumerate(cams):
             u0, u1, u2 = (ups[i][v].cpu().numpy() for i in range(3))
-            b1 = oracle.backward(scene, oracle_cam(cam), bg, u0, u1[:1], u1[1:2], prec=prec)
-            b2 = oracle.backward(sc2, oracle_cam(cam), bg, u2, None, None, prec=prec)
+            b1 = oracle.backward(scene, oracle_cam(cam), bg, u0, u1[:1], u1[1:2], prec=prec, order=order)
+            b2 = oracle.backward(sc2, oracle_cam(cam), bg, u2, None, None, prec=prec, order=order)
             terms = {k: np.asarray(b1[k], np.float64) + np.asarray(b2[k], np.float64)
                      for k in ("means3D", "scales", "rotations", "opacity")}
             terms["sh"], terms["normals"] = np.asarray(b1["sh"], np.float64), np.asarray(b2["colors"], np.float64)
             for k, x in terms.items():
                 acc[k] = acc.get(k, 0.0) + x
-        ref["b32" if prec == "f32" else "b64"] = acc
+        ref[key] = acc
     gpu = {"g_" + k: f["g"][src].cpu().numpy() for k, src in (("means3D", "means3D"), ("scales", "scales"),
            ("rotations", "rotations"), ("opacity", "opacities"), ("sh", "shs"), ("normals", "normals"))}
     check_grads(gpu, ref, ["means3D", "scales", "rotations", "opacity", "sh", "normals"], "two-colour backward")
@@ -526,31 +538,35 @@ def test_two_color_backward_with_fused_composite():
     sc2 = dict(scene, colors_precomp=normals)
     sc2.pop("shs")
     zero = np.zeros(3, np.float32)
-    ref = {"b32": {}, "b64": {}}
+    ref = {"b32": {}, "b64": {}, "b32r": {}}
     for v, cam in enumerate(cams):
         fw = run_oracle(scene, cam, [0.0, 0.0, 0.0])
         g_r, g_d, g_a = ups[0][v], ups[1][v][:1], ups[1][v][1:2]
         bgs = {}
-        for prec, dt in (("f32", np.float32), ("f64", np.float64)):
+        for prec, dt, order, key in (("f32", np.float32, 0, "b32"), ("f64", np.float64, 0, "b64"),
+                                     ("f32", np.float32, 1, "b32r")):
             f = fw[prec]
             _, pre = _composite(f["color"].astype(dt), f["alpha"].astype(dt), bg_img[v].astype(dt))
             gcol, ga = _composite_upstream(g_r, g_a, pre, bg_img[v])
-            b1 = oracle.backward(scene, oracle_cam(cam), zero, gcol, g_d, ga, prec=prec)
-            b2 = oracle.backward(sc2, oracle_cam(cam), zero, ups[2][v], None, None, prec=prec)
-            acc = ref["b32" if prec == "f32" else "b64"]
+            b1 = oracle.backward(scene, oracle_cam(cam), zero, gcol, g_d, ga, prec=prec, order=order)
+            b2 = oracle.backward(sc2, oracle_cam(cam), zero, ups[2][v], None, None, prec=prec, order=order)
+            acc = ref[key]
             terms = {k: np.asarray(b1[k], np.float64) + np.asarray(b2[k], np.float64)
                      for k in ("means3D", "scales", "rotations", "opacity")}
             terms["sh"], terms["normals"] = np.asarray(b1["sh"], np.float64), np.asarray(b2["colors"], np.float64)
             for k, x in terms.items():
                 acc[k] = acc.get(k, 0.0) + x
-            bgs[prec] = (gcol * (dt(1) - f["alpha"].astype(dt))).transpose(1, 2, 0).reshape(-1, 3)
-            bgs["m2_" + prec] = b1["means2D"]
+            if order == 0:
+                bgs[prec] = (gcol * (dt(1) - f["alpha"].astype(dt))).transpose(1, 2, 0).reshape(-1, 3)
+                bgs["m2_" + prec] = b1["means2D"]
+            else:
+                bgs["m2_f32r"] = b1["means2D"]
         adjudicate(bg_t.grad[v].detach().cpu().numpy().reshape(-1, 3), bgs["f32"], bgs["f64"],
                    1e-4 * np.maximum(1.0, np.abs(bgs["f64"])), f"two colours + composite view {v}", "grad background",
                    rowwise=True)
         adjudicate(m2[v].grad.cpu().numpy(), bgs["m2_f32"], bgs["m2_f64"],
                    1e-4 * np.maximum(1.0, np.abs(bgs["m2_f64"])), f"two colours + composite view {v}", "grad means2D",
-                   rowwise=True)
+                   rowwise=True, r32b=bgs["m2_f32r"])
     gpu = {"g_" + k: t[src].grad.cpu().numpy() for k, src in (("means3D", "means3D"), ("scales", "scales"),
            ("rotations", "rotations"), ("opacity", "opacities"), ("sh", "shs"), ("normals", "normals"))}
     check_grads(gpu, ref, ["means3D", "scales", "rotations", "opacity", "sh", "normals"], "two colours + composite")

@@ -866,20 +866,23 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(TWO ? 4 : 5
 
   // Matrix-core reduction.  For a group of 8 candidates c, one 16x16 product over the quadrant's
   // 64 pixels p: A rows 0-7 = u of the candidates, rows 8-15 = their w; B columns 0-5 =
-  // F(p) = (1, x, y, x^2, x y, y^2) of the pixel's quadrant-local coordinates, columns 6-9 = the
+  // F(p) = (1, x, y, x^2, x y, y^2) of the pixel's coordinates relative to the quadrant's centre
+  // (x, y in -3.5 .. 3.5, exact in fp32: the flush's conversion to moments about the mean cancels
+  // 4x less than with the quadrant's corner as origin — the sums' rounding is what the cancellation
+  // amplifies for small Gaussians), columns 6-9 = the
   // pixel's dL/d(r, g, b, depth).  Rows 0-7 x columns 0-5 are the u moments, rows 8-15 x columns
   // 6-9 the colour / depth sums; the other quarters are not used.  16 v_mfma_f32_16x16x4_f32
   // (exact fp32 fma chains, 2 interleaved accumulators for the 40-cycle dependency).
   // Operand maps (16x16x4): lane l holds A[l & 15][k = l >> 4], B[k = l >> 4][l & 15];
   // result lane l: column l & 15, rows 4 (l >> 4) + r.
-  // k-step i, k = l >> 4 covers pixel p = 16 k + i: x = p & 7 = i & 7 (uniform), y = p >> 3 =
-  // 2 k + (i >> 3), so F = fa[i >> 3] + x (fbb[i >> 3] + x fc).
+  // k-step i, k = l >> 4 covers pixel p = 16 k + i: x = (p & 7) - 3.5 = (i & 7) - 3.5 (uniform),
+  // y = (p >> 3) - 3.5 = 2 k + (i >> 3) - 3.5, so F = fa[i >> 3] + x (fbb[i >> 3] + x fc).
   const int ncol = lane & 15;
   const bool dcol = ncol >= 6 && ncol < 6 + NPL;
   float fa[2], fbb[2], fc;
 #pragma unroll
   for (int h = 0; h < 2; ++h) {
-    const float y = (float)(2 * (lane >> 4) + h);
+    const float y = (float)(2 * (lane >> 4) + h) - 3.5f;
     fa[h] = ncol == 0 ? 1.f : ncol == 2 ? y : ncol == 5 ? y * y : 0.f;
     fbb[h] = ncol == 1 ? 1.f : ncol == 4 ? y : 0.f;
   }
@@ -910,7 +913,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(TWO ? 4 : 5
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
         const int i = 4 * k + e;
-        const float x = (float)(i & 7);
+        const float x = (float)(i & 7) - 3.5f;
         // one of the two terms is zero: D for columns 6-9 (zeros row otherwise), F for 0-5
         bv[i] = dk[e] + (fa[i >> 3] + x * (fbb[i >> 3] + x * fc));
       }
@@ -1092,9 +1095,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(TWO ? 4 : 5
     if (hi - 1 - cs >= 0)
 #endif
     {
-      // four threads per candidate (t = 4 c + quadrant): per quadrant, turn the sums over quadrant-
-      // local pixel coordinates into the moments of u over dx = mean - pixel (dx = mx' - x with
-      // mx' = mean - quadrant origin); add the 4 quadrants (quad DPP); form the reference's terms
+      // four threads per candidate (t = 4 c + quadrant): per quadrant, turn the sums over pixel
+      // coordinates relative to the quadrant centre into the moments of u over dx = mean - pixel
+      // (dx = mx' - x with mx' = mean - quadrant centre); add the 4 quadrants (quad DPP); form the reference's terms
       //   dmean2D = -o (W/2, H/2) (a m1 + b m2, c m2 + b m1), dconic = -o/2 (m3, m4, m5), dopacity = m0
       // and write the 48-byte row, one 16-byte piece per thread.
       const int qq = piece;
@@ -1107,8 +1110,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(TWO ? 4 : 5
       for (int i = 0; i < NM; ++i) m[i] = 0.f;
       if ((s.kmask[qq] >> cs) & 1ull) {
         const float* C = s.qsum + cs * QS + NG * qq;
-        const float mx = ga.x - (float)(txi * GSR_TILE_X + (qq & 1) * 8);
-        const float my = ga.y - (float)(tyi * GSR_TILE_Y + (qq >> 1) * 8);
+        const float mx = ga.x - ((float)(txi * GSR_TILE_X + (qq & 1) * 8) + 3.5f);
+        const float my = ga.y - ((float)(tyi * GSR_TILE_Y + (qq >> 1) * 8) + 3.5f);
         m[0] = C[0];
         m[1] = mx * C[0] - C[1];
         m[2] = my * C[0] - C[2];
