@@ -373,13 +373,8 @@ __global__ __launch_bounds__(256) void k_tile_info(RenderSet rs, const uint2* __
 //   0-5 the u moments, 6-9 sum w dL/d(r,g,b,depth), 10-12 sum u_1 (1, x, y), 13-15 sum w dL/d(r2,g2,b2)
 // from 4 candidates per product (A rows 0-3 u, 4-7 u_1, 8-11 w; B columns 6-12 the 7 pixel planes).
 #define NGV2 16
-// The per-(candidate, quadrant) sums in LDS: the u moments (sums 0-5, two colours also 10-12) as doubles
-// (two 32-bit words each: the flush's conversion to moments about the mean cancels, so they are formed and
-// kept in fp64), the colour / depth sums as floats.  Words per quadrant, then per candidate (+1 pad).
-#define GSR_QSUM_QW 16   // 6 doubles + 4 floats
-#define GSR_QSUM_QW2 25  // two colours: 9 doubles + 7 floats
-#define GSR_QSUM_STRIDE (4 * GSR_QSUM_QW + 1)
-#define GSR_QSUM_STRIDE2 (4 * GSR_QSUM_QW2 + 1)
+#define GSR_QSUM_STRIDE 41   // floats per candidate: 4 quadrants x 10 raw sums, +1 pad
+#define GSR_QSUM_STRIDE2 65  // two colours: 4 x 16, +1
 template <bool TWO>
 struct BwdLDS {
   float4 s0[65], s1[65], s2[65];
@@ -686,7 +681,7 @@ void launch_render_forward(const RenderSet& rs, const GeomState& g, const uint32
 }
 
 template <bool TWO>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(TWO ? 3 : 4, 8))) void k_render_bwd(RenderSet rs,
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(TWO ? 4 : 5, 8))) void k_render_bwd(RenderSet rs,
                                                     const uint2* __restrict__ ranges,
                                                     const uint32_t* __restrict__ quad_maxc,
                                                     const uint32_t* __restrict__ sorted_gauss,
@@ -699,7 +694,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(TWO ? 3 : 4
                                                     const float* __restrict__ dL_dalpha,
                                                     float4* __restrict__ grow) {
   __shared__ BwdLDS<TWO> s;
-  constexpr int QW = TWO ? GSR_QSUM_QW2 : GSR_QSUM_QW;            // LDS words per (candidate, quadrant)
+  constexpr int NG = TWO ? NGV2 : NGV;                           // raw sums per (candidate, quadrant)
   constexpr int QS = TWO ? GSR_QSUM_STRIDE2 : GSR_QSUM_STRIDE;  // per candidate
   constexpr int GS = TWO ? 4 : 8;                                // candidates per 16x16 product
   constexpr int NPL = TWO ? 7 : 4;                               // dL/dpixel planes in the B operand
@@ -872,17 +867,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(TWO ? 3 : 4
   // Matrix-core reduction.  For a group of 8 candidates c, one 16x16 product over the quadrant's
   // 64 pixels p: A rows 0-7 = u of the candidates, rows 8-15 = their w; B columns 0-5 =
   // F(p) = (1, x, y, x^2, x y, y^2) of the pixel's coordinates relative to the quadrant's centre
-  // (x, y in -3.5 .. 3.5, exact), columns 6-9 = the
+  // (x, y in -3.5 .. 3.5, exact in fp32: the flush's conversion to moments about the mean cancels
+  // 4x less than with the quadrant's corner as origin — the sums' rounding is what the cancellation
+  // amplifies for small Gaussians), columns 6-9 = the
   // pixel's dL/d(r, g, b, depth).  Rows 0-7 x columns 0-5 are the u moments, rows 8-15 x columns
-  // 6-9 the colour / depth sums; the other quarters are not used.  16 v_mfma_f64_16x16x4_f64: the
-  // products u F and w D are exact in fp64 and so are the sums to ~2^-53, so the flush's conversion
-  // to moments about the Gaussian's mean (mx^2 C0 - 2 mx C1 + C3 ..., which cancels by up to
-  // (distance of the mean from the centre / footprint)^2 for small Gaussians) leaves only its final
-  // rounding: the gradients are as accurate as the reference's per-pixel fp32 accumulation, also for
-  // SuGaR's sub-pixel-thick Gaussians (fp32 sums here lost up to ~10 bits there).  2 interleaved
-  // accumulators for the dependency.
-  // Operand maps (16x16x4, f64 as f32): lane l holds A[l & 15][k = l >> 4], B[k = l >> 4][l & 15];
-  // f64 result lane l: column l & 15, rows (l >> 4) + 4 r.
+  // 6-9 the colour / depth sums; the other quarters are not used.  16 v_mfma_f32_16x16x4_f32
+  // (exact fp32 fma chains, 2 interleaved accumulators for the 40-cycle dependency).
+  // Operand maps (16x16x4): lane l holds A[l & 15][k = l >> 4], B[k = l >> 4][l & 15];
+  // result lane l: column l & 15, rows 4 (l >> 4) + r.
   // k-step i, k = l >> 4 covers pixel p = 16 k + i: x = (p & 7) - 3.5 = (i & 7) - 3.5 (uniform),
   // y = (p >> 3) - 3.5 = 2 k + (i >> 3) - 3.5, so F = fa[i >> 3] + x (fbb[i >> 3] + x fc).
   const int ncol = lane & 15;
@@ -898,7 +890,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(TWO ? 3 : 4
   // The B operand is the same for every group: bv[i] = D + F for k-step i, kept in registers.  D
   // (other lanes' pixels) goes through LDS once, in the qsum area (first written after the first
   // staging barrier, by which time every wave has read its bv).
-  double bv[16];
+  float bv[16];
   {
     float* sdp = s.qsum + q * (NPL * 68 + 16);
     sdp[0 * 68 + lane] = dpix[0];
@@ -923,7 +915,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(TWO ? 3 : 4
         const int i = 4 * k + e;
         const float x = (float)(i & 7) - 3.5f;
         // one of the two terms is zero: D for columns 6-9 (zeros row otherwise), F for 0-5
-        bv[i] = (double)(dk[e] + (fa[i >> 3] + x * (fbb[i >> 3] + x * fc)));
+        bv[i] = dk[e] + (fa[i >> 3] + x * (fbb[i >> 3] + x * fc));
       }
     }
   }
@@ -935,27 +927,19 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(TWO ? 3 : 4
   // reader side: chunk k of lane l at 16 l + 4 (k ^ ((l >> 2) & 3))
   const float4* asrc = reinterpret_cast<const float4*>(uw + 16 * lane);
   const int aswz = (lane >> 2) & 3;
-  // result side: lane l (g = l >> 4) holds rows g + 4 r: u of candidates g (r = 0) and g + 4 (r = 1),
-  // columns 0-5 used; w of candidates g (r = 2) and g + 4 (r = 3), columns 6-9 used.
-  // two colours: rows 0-3 u, 4-7 u_1, 8-11 w of candidates 0-3: lane l holds candidate g's u (r = 0,
-  // columns 0-5), u_1 (r = 1, columns 0-2 -> sums 10-12) and w (r = 2, columns 6-12 -> sums 6-9, 13-15)
-  const int rg = lane >> 4;
-  // LDS word of this lane's result r within a (candidate, quadrant) block, -1 = not used; doubles for the
-  // u moments (two words), floats for the w sums
-  int wofs[4];
-  bool wdbl[4];
-#pragma unroll
-  for (int r = 0; r < 4; ++r) {
-    if (TWO) {
-      wofs[r] = r == 0 ? (ncol < 6 ? 2 * ncol : -1)
-              : r == 1 ? (ncol < 3 ? 12 + 2 * ncol : -1)
-              : r == 2 ? (ncol >= 6 && ncol < 10 ? 18 + ncol - 6 : ncol >= 10 && ncol < 13 ? 22 + ncol - 10 : -1)
-                       : -1;
-      wdbl[r] = r < 2;
-    } else {
-      wofs[r] = r < 2 ? (ncol < 6 ? 2 * ncol : -1) : (dcol ? 12 + ncol - 6 : -1);
-      wdbl[r] = r < 2;
-    }
+  // result side: lane l holds rows 4 (l >> 4) + r -> candidate mb + r of the group, u (rows 0-7,
+  // columns 0-5 used) or w (rows 8-15, columns 6-9 used)
+  // two colours: rows 4 (l >> 4) + r are candidate r's u (lanes 0-15, columns 0-5), u_1 (16-31,
+  // columns 0-2 -> sums 10-12) or w (32-47, columns 6-12 -> sums 6-9, 13-15); lanes 48-63 unused
+  const int mb = TWO ? 0 : 4 * ((lane >> 4) & 1);
+  bool useful;
+  int field = ncol;
+  if (TWO) {
+    const int rg = lane >> 4;
+    useful = rg == 0 ? ncol < 6 : rg == 1 ? ncol < 3 : rg == 2 ? dcol : false;
+    field = rg == 1 ? 10 + ncol : (rg == 2 && ncol >= 10) ? ncol + 3 : ncol;
+  } else {
+    useful = (lane < 32) ? (ncol < 6) : dcol;
   }
   if (TWO) {
     // A rows 12-15 are never written: zero them once (their products are not read either)
@@ -964,7 +948,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(TWO ? 3 : 4
   }
 
   uint32_t* mylist = s.list[q];
-  float* myq = s.qsum + q * QW;
+  float* myq = s.qsum + q * NG;
   for (int hi = maxc; hi > 0; hi -= 64) {
     {
       const int rel_c = hi - 1 - cs;
@@ -1074,27 +1058,23 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(TWO ? 3 : 4
         const float4 a4 = asrc[k ^ aswz];
         av[4 * k] = a4.x, av[4 * k + 1] = a4.y, av[4 * k + 2] = a4.z, av[4 * k + 3] = a4.w;
       }
-      // the candidates of this lane's result rows: g, g + 4 (two colours: g)
-      const uint32_t ja = mylist[g0 + rg], jb = TWO ? ja : mylist[g0 + rg + 4];
-      typedef double d4 __attribute__((ext_vector_type(4)));
-      // one accumulator: the other waves of the SIMD fill the chain's dependency stalls (a second one
-      // would take the kernel past 128 registers, 4 -> 3 waves per SIMD)
-      d4 acc = {0.0, 0.0, 0.0, 0.0};
+      // the candidates of this lane's 4 result rows (m = mb + r)
+      const uint4 jl = *reinterpret_cast<const uint4*>(mylist + g0 + mb);
+      typedef float f4 __attribute__((ext_vector_type(4)));
+      f4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-      for (int i = 0; i < 16; ++i) acc = __builtin_amdgcn_mfma_f64_16x16x4f64((double)av[i], bv[i], acc, 0, 0, 0);
+      for (int i = 0; i < 16; ++i) {
+        if (i & 1)
+          acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(av[i], bv[i], acc1, 0, 0, 0);
+        else
+          acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(av[i], bv[i], acc0, 0, 0, 0);
+      }
+      // lane l: column ncol, rows 4 (l >> 4) + r; u rows 0-7 (columns 0-5), w rows 8-15 (6-9)
+      if (useful) {
+        const uint32_t jr[4] = {jl.x, jl.y, jl.z, jl.w};
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int cand = TWO ? rg : rg + 4 * (r & 1);
-        if (wofs[r] >= 0 && cand < gn) {
-          float* dst = myq + ((r & 1) && !TWO ? jb : ja) * (uint32_t)QS + (uint32_t)wofs[r];
-          const double x = acc[r];
-          if (wdbl[r]) {
-            dst[0] = __int_as_float(__double2loint(x));
-            dst[1] = __int_as_float(__double2hiint(x));
-          } else {
-            dst[0] = (float)x;
-          }
-        }
+        for (int r = 0; r < 4; ++r)
+          if (mb + r < gn) myq[jr[r] * (uint32_t)QS + (uint32_t)field] = acc0[r] + acc1[r];
       }
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // rows are rewritten by the next group
     }
@@ -1129,30 +1109,25 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(TWO ? 3 : 4
 #pragma unroll
       for (int i = 0; i < NM; ++i) m[i] = 0.f;
       if ((s.kmask[qq] >> cs) & 1ull) {
-        const float* Cw = s.qsum + cs * QS + QW * qq;
-        auto D = [&](int w) { return __hiloint2double(__float_as_int(Cw[w + 1]), __float_as_int(Cw[w])); };
-        const double C0 = D(0), C1 = D(2), C2 = D(4), C3 = D(6), C4 = D(8), C5 = D(10);
-        // (the mean's offset from the quadrant centre: exact in fp32 for on-screen means)
-        const double mx = (double)(ga.x - ((float)(txi * GSR_TILE_X + (qq & 1) * 8) + 3.5f));
-        const double my = (double)(ga.y - ((float)(tyi * GSR_TILE_Y + (qq >> 1) * 8) + 3.5f));
-        m[0] = (float)C0;
-        m[1] = (float)(mx * C0 - C1);
-        m[2] = (float)(my * C0 - C2);
-        m[3] = (float)(mx * (mx * C0 - 2.0 * C1) + C3);
-        m[4] = (float)(mx * (my * C0 - C2) - my * C1 + C4);
-        m[5] = (float)(my * (my * C0 - 2.0 * C2) + C5);
-        constexpr int WF = TWO ? 18 : 12;  // first float word
-        m[6] = Cw[WF];
-        m[7] = Cw[WF + 1];
-        m[8] = Cw[WF + 2];
-        m[9] = Cw[WF + 3];
+        const float* C = s.qsum + cs * QS + NG * qq;
+        const float mx = ga.x - ((float)(txi * GSR_TILE_X + (qq & 1) * 8) + 3.5f);
+        const float my = ga.y - ((float)(tyi * GSR_TILE_Y + (qq >> 1) * 8) + 3.5f);
+        m[0] = C[0];
+        m[1] = mx * C[0] - C[1];
+        m[2] = my * C[0] - C[2];
+        m[3] = mx * (mx * C[0] - 2.f * C[1]) + C[3];
+        m[4] = mx * (my * C[0] - C[2]) - my * C[1] + C[4];
+        m[5] = my * (my * C[0] - 2.f * C[2]) + C[5];
+        m[6] = C[6];
+        m[7] = C[7];
+        m[8] = C[8];
+        m[9] = C[9];
         if (TWO) {
-          const double U0 = D(12), U1 = D(14), U2 = D(16);
-          m[10 % NM] = (float)(mx * U0 - U1);
-          m[11 % NM] = (float)(my * U0 - U2);
-          m[12 % NM] = Cw[22];
-          m[13 % NM] = Cw[23];
-          m[14 % NM] = Cw[24];
+          m[10 % NM] = mx * C[10] - C[11];
+          m[11 % NM] = my * C[10] - C[12];
+          m[12 % NM] = C[13];
+          m[13 % NM] = C[14];
+          m[14 % NM] = C[15];
         }
       }
 #pragma unroll
