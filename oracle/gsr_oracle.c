@@ -397,10 +397,33 @@ int oracle_get_threads(void) { return g_oracle_threads; }
  * (tests/gsr_testutil.py uses the pair to measure how far the reference is from itself, row by row). */
 int g_oracle_order = 0;
 void oracle_set_order(int order) { g_oracle_order = order; }
+/* DIAGNOSTIC ONLY (scripts/parity_sources.py; never set by a parity test): evaluate pieces of the per-pixel
+ * arithmetic the way the HIP blends do, to attribute their differences from this restatement.
+ *   1  exponent: conic pre-multiplied by -log2(e)/2, -log2(e) (rounded), exp2 (csrc/gsr_common.h gauss_power2)
+ *   2  transmittance recovery T * (1 / (1 - alpha)) instead of T / (1 - alpha)
+ *   4  dL/dalpha from one scalar S = sum_ch accum_ch dL/dpix_ch (csrc/gsr_render.hip k_render_bwd replay)
+ *   8  dL/dmean2D from the first moments of u = G dL/dalpha and the pre-multiplied conic, as the blend's
+ *      flush forms it: (o / log2 e) (W/2) (2 A m1 + B m2), A = -log2(e)/2 a, B = -log2(e) b (rounded) */
+int g_oracle_variant = 0;
+void oracle_set_variant(int v) { g_oracle_variant = v; }
 #else
 extern int g_oracle_threads;
 extern int g_oracle_order;
+extern int g_oracle_variant;
 #endif
+/* the exponent (and G) under the diagnostic variant bit 1: returns the exponent's sign test value, G in *G */
+static real blend_G(const gstate* g, real dx, real dy, real* G) {
+  if (g_oracle_variant & 1) {
+    const float A = -0.72134752044448170f * (float)g->ca, B = -1.4426950408889634f * (float)g->cb,
+                C = -0.72134752044448170f * (float)g->cc;
+    const float p2 = fmaf((float)dx, fmaf(A, (float)dx, B * (float)dy), (C * (float)dy) * (float)dy);
+    *G = (real)exp2f(p2);
+    return (real)p2;
+  }
+  const real power = gauss_power(g->ca, g->cb, g->cc, dx, dy);
+  *G = EXPR(power);
+  return power;
+}
 void FN(oracle_last_stats)(long* out) { for (int i = 0; i < 4; ++i) out[i] = g_stats[i]; }
 
 static void forward_core(const ctx_t* c, int* radii, fwd_t* f, real* out_color, real* out_depth, real* out_alpha) {
@@ -455,9 +478,10 @@ static void forward_core(const ctx_t* c, int* radii, fwd_t* f, real* out_color, 
             st0++;
             const gstate* g = &f->gs[f->inst[p].g];
             const real dx = g->px - (real)px, dy = g->py - (real)py;
-            const real power = gauss_power(g->ca, g->cb, g->cc, dx, dy);
+            real Gv;
+            const real power = blend_G(g, dx, dy, &Gv);
             if (power > 0) continue;
-            const real alpha = rmin(RL(0.99), g->op * EXPR(power));
+            const real alpha = rmin(RL(0.99), g->op * Gv);
             if (alpha < RL(1.0) / RL(255.0)) continue;
             const real test_T = T * (RL(1) - alpha);
             if (test_T < RL(0.0001)) break;
@@ -574,19 +598,31 @@ void FN(oracle_backward)(int P, int deg, int M, const float* means, const float*
           const real dpa = dL_dalpha ? (real)dL_dalpha[pid] : 0;
           const real bg_dot = c.bg[0] * dpix[0] + c.bg[1] * dpix[1] + c.bg[2] * dpix[2];
           real accr[3] = {0, 0, 0}, accd = 0, acca = 0, last_alpha = 0, last_c[3] = {0, 0, 0}, last_d = 0;
+          real S = 0;  /* diagnostic variant 4 */
           for (long rel = (long)last - 1; rel >= 0; --rel) {
             const uint32_t gi = f.inst[s + rel].g;
             const gstate* g = &f.gs[gi];
             const real dx = g->px - (real)px, dy = g->py - (real)py;
-            const real power = gauss_power(g->ca, g->cb, g->cc, dx, dy);
+            real G;
+            const real power = blend_G(g, dx, dy, &G);
             if (power > 0) continue;
-            const real G = EXPR(power);
             const real alpha = rmin(RL(0.99), g->op * G);
             if (alpha < RL(1.0) / RL(255.0)) continue;
-            T = T / (RL(1) - alpha);
+            if (g_oracle_variant & 2)
+              T = T * (RL(1) / (RL(1) - alpha));
+            else
+              T = T / (RL(1) - alpha);
             const real dcd = alpha * T;
             real dL_dalpha = 0;
             real* a = tacc + (size_t)10 * gi;
+            if (g_oracle_variant & 4) {
+              const real cd = FMAR(g->rgb[0], dpix[0], FMAR(g->rgb[1], dpix[1], FMAR(g->rgb[2], dpix[2],
+                                   FMAR(g->depth, dpd, dpa))));
+              dL_dalpha = FMAR(T, cd - S, (RL(1) / (RL(1) - alpha)) * (-T_final * bg_dot));
+              S = FMAR(alpha, cd, (RL(1) - alpha) * S);
+              for (int ch = 0; ch < 3; ++ch) a[6 + ch] += dcd * dpix[ch];
+              a[9] += dcd * dpd;
+            } else {
             for (int ch = 0; ch < 3; ++ch) {
               accr[ch] = last_alpha * last_c[ch] + (RL(1) - last_alpha) * accr[ch];
               last_c[ch] = g->rgb[ch];
@@ -602,12 +638,18 @@ void FN(oracle_backward)(int P, int deg, int M, const float* means, const float*
             dL_dalpha *= T;
             last_alpha = alpha;
             dL_dalpha += (-T_final / (RL(1) - alpha)) * bg_dot;
+            }
             const real dL_dG = g->op * dL_dalpha;
             const real gdx = G * dx, gdy = G * dy;
             const real dG_ddelx = -gdx * g->ca - gdy * g->cb;
             const real dG_ddely = -gdy * g->cc - gdx * g->cb;
+            if (g_oracle_variant & 8) {  /* first moments of u (finished after the loop) */
+              a[0] += G * dL_dalpha * dx;
+              a[1] += G * dL_dalpha * dy;
+            } else {
             a[0] += dL_dG * dG_ddelx * ddelx_dx;
             a[1] += dL_dG * dG_ddely * ddely_dy;
+            }
             a[2] += RL(-0.5) * gdx * dx * dL_dG;
             a[3] += RL(-0.5) * gdx * dy * dL_dG;
             a[4] += RL(-0.5) * gdy * dy * dL_dG;
@@ -617,6 +659,17 @@ void FN(oracle_backward)(int P, int deg, int M, const float* means, const float*
   }
   for (int th = 1; th < nth; ++th)
     for (size_t k = 0; k < nacc; ++k) acc[k] += acc_all[nacc * (size_t)th + k];
+  if (g_oracle_variant & 8)
+    for (int i = 0; i < P; ++i) {
+      real* a = acc + (size_t)10 * i;
+      const gstate* g = &f.gs[i];
+      const float A = -0.72134752044448170f * (float)g->ca, B = -1.4426950408889634f * (float)g->cb,
+                  C = -0.72134752044448170f * (float)g->cc;
+      const float k = (float)g->op * (1.0f / 1.4426950408889634f);
+      const float m1 = (float)a[0], m2 = (float)a[1];
+      a[0] = (real)(k * (0.5f * W) * (2.0f * A * m1 + B * m2));
+      a[1] = (real)(k * (0.5f * H) * (2.0f * C * m2 + B * m1));
+    }
 
 #pragma omp parallel for num_threads(nth) schedule(static) if (nth > 1)
   for (int i = 0; i < P; ++i) {

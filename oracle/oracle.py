@@ -104,6 +104,12 @@ def backward(scene: dict, cam, bg, dL_dcolor, dL_ddepth=None, dL_dalpha=None, pr
     return res
 
 
+def set_variant(v: int):
+    """DIAGNOSTIC ONLY (gsr_oracle.c g_oracle_variant): evaluate pieces of the per-pixel arithmetic the way the
+    HIP blends do.  Never used by a parity test."""
+    lib().oracle_set_variant(ctypes.c_int(v))
+
+
 def gauss_aux(scene: dict, cam, prec: str = "f64", mod: float = 1.0):
     """Per-Gaussian preprocess values (oracle_gauss_aux): dict(px, py, rad3 = 3 sqrt(max eigenvalue) before
     the ceil (-1 when culled before it), tiles = rectangle tiles of the oracle's radius, conic (P, 3),

@@ -285,11 +285,25 @@ def flip_dependents(ref, pixels):
     return dep
 
 
-def check_grads(gpu, ref, keys, what=""):
+def flip_excuse(refs):
+    """Union over views (run_oracle dicts that went through check_forward) of the Gaussians blended at a pixel
+    the GPU flipped on its own: their gradient rows legitimately differ (see check_forward)."""
+    out = None
+    for r in refs:
+        if "aux64" not in r:
+            continue
+        d = flip_dependents(r, r.get("gpu_only_px", ()))
+        out = d if out is None else (out | d)
+    return out
+
+
+def check_grads(gpu, ref, keys, what="", excuse=None):
     """Elementwise |g - g64| <= 1e-4 max(1, |g64|) with fp32-oracle adjudication of flip-affected rows;
-    rows of Gaussians blended at a pixel the GPU flipped on its own (check_forward) are excused."""
+    rows of Gaussians blended at a pixel the GPU flipped on its own (check_forward) are excused (`excuse`:
+    the rows to excuse when `ref` is not a run_oracle dict, e.g. gradients summed over views: flip_excuse)."""
     b32, b64, b32r = ref["b32"], ref["b64"], ref.get("b32r")
-    excuse = flip_dependents(ref, ref.get("gpu_only_px", ())) if "aux64" in ref else None
+    if excuse is None:
+        excuse = flip_dependents(ref, ref.get("gpu_only_px", ())) if "aux64" in ref else None
     out = {}
     for k in keys:
         r64 = b64[k]
@@ -327,4 +341,4 @@ def scene_subset(scene, **over):
 
 
 __all__ = ["gs", "make_camera", "oracle_cam", "gpu_render", "run_oracle", "check_forward", "check_grads",
-           "check_radii", "adjudicate", "print_report", "last_num_rendered"]
+           "check_radii", "adjudicate", "print_report", "last_num_rendered", "flip_excuse", "flip_dependents"]

@@ -346,7 +346,7 @@ def test_c4_batch_single_vs_two_ranks(B, S, tmp_path):
 
 def _c4_oracle_views(single, B, S, views):
     import oracle
-    from gsr_testutil import adjudicate, check_radii, oracle_cam, run_oracle
+    from gsr_testutil import adjudicate, check_radii, flip_excuse, oracle_cam, run_oracle
     from test_gpu_configs import _composite, _composite_upstream
 
     scene = gs.make_scene(C4_P, sh_degree=3, seed=0)
@@ -374,6 +374,12 @@ def _c4_oracle_views(single, B, S, views):
         adjudicate(px(gpu_img), px(b["render_f32"]), px(b["render_f64"]), 1e-5, f"C4 {S}^2 view {v}", "comp_rgb",
                    cap=0.02)
         check_radii(single[f"radii_{v}"], ref, f"C4 {S}^2 view {v}")
+        # pixels where the GPU's composited image missed the fp64 value and the fp32 oracle's did not: a discrete
+        # decision (alpha >= 1/255, T < 1e-4) taken differently; the Gaussians blended there are excused
+        e_g = np.abs(px(gpu_img) - px(b["render_f64"])).max(1)
+        e_3 = np.abs(px(b["render_f32"]) - px(b["render_f64"])).max(1)
+        ref["gpu_only_px"] = np.nonzero((e_g > 1e-5) & ~(e_3 > 1e-5))[0]
         m64 = b["f64"]["means2D"]
         adjudicate(single[f"m2_{v}"], b["f32"]["means2D"], m64, 1e-4 * np.maximum(1.0, np.abs(m64)),
-                   f"C4 {S}^2 view {v}", "grad means2D", rowwise=True, r32b=b["f32r"]["means2D"])
+                   f"C4 {S}^2 view {v}", "grad means2D", rowwise=True, r32b=b["f32r"]["means2D"],
+                   excuse=flip_excuse([ref]))

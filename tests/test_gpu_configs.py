@@ -21,7 +21,7 @@ import numpy as np
 import pytest
 
 import oracle
-from gsr_testutil import (adjudicate, check_forward, check_grads, check_radii, gs, make_camera, oracle_cam,
+from gsr_testutil import (adjudicate, check_forward, check_grads, check_radii, flip_excuse, gs, make_camera, oracle_cam,
                           print_report, run_oracle)
 
 pytestmark = pytest.mark.gpu
@@ -154,14 +154,15 @@ def test_c3_views_fused_background_composite():
         check_forward(_view(gpu, v), ref, f"C3 view {v}", K_gpu=gpu["K"][v])
         adjudicate(gpu["g_means2D"][v], b["f32"]["means2D"], b["f64"]["means2D"],
                    1e-4 * np.maximum(1.0, np.abs(b["f64"]["means2D"])), f"C3 view {v}", "grad means2D", rowwise=True,
-                   r32b=b["f32r"]["means2D"])
+                   r32b=b["f32r"]["means2D"], excuse=flip_excuse([ref]))
+        b["oracle_fwd"] = ref
         adjudicate(gpu["g_background"][v].reshape(-1, 3), b["bg_f32"].reshape(-1, 3), b["bg_f64"].reshape(-1, 3),
                    1e-4 * np.maximum(1.0, np.abs(b["bg_f64"].reshape(-1, 3))), f"C3 view {v}", "grad background",
                    rowwise=True)
         refs.append(b)
     tot = dict(b32=_sum_grads(refs, "f32", GRAD_KEYS), b64=_sum_grads(refs, "f64", GRAD_KEYS),
                b32r=_sum_grads(refs, "f32r", GRAD_KEYS))
-    check_grads(gpu, tot, GRAD_KEYS, "C3 summed")
+    check_grads(gpu, tot, GRAD_KEYS, "C3 summed", excuse=flip_excuse([b["oracle_fwd"] for b in refs]))
 
 
 def test_view_set_vs_oracle():
@@ -178,11 +179,11 @@ def test_view_set_vs_oracle():
         check_forward(_view(gpu, v), ref, f"set view {v}", K_gpu=gpu["K"][v])
         adjudicate(gpu["g_means2D"][v], ref["b32"]["means2D"], ref["b64"]["means2D"],
                    1e-4 * np.maximum(1.0, np.abs(ref["b64"]["means2D"])), f"set view {v}", "grad means2D",
-                   rowwise=True, r32b=ref["b32r"]["means2D"])
+                   rowwise=True, r32b=ref["b32r"]["means2D"], excuse=flip_excuse([ref]))
         refs.append(ref)
     tot = dict(b32=_sum_grads(refs, "b32", GRAD_KEYS), b64=_sum_grads(refs, "b64", GRAD_KEYS),
                b32r=_sum_grads(refs, "b32r", GRAD_KEYS))
-    check_grads(gpu, tot, GRAD_KEYS, "set summed")
+    check_grads(gpu, tot, GRAD_KEYS, "set summed", excuse=flip_excuse(refs))
 
 
 @pytest.mark.parametrize("layout", ["duplicates", "plane"])
@@ -381,7 +382,8 @@ def test_c5_sugar_normal_renderer():
         adjudicate(rows(gpu_out[k]), rows(epi["f32"][k]), rows(a64), 1e-5 + 1e-5 * np.abs(rows(a64)), "C5", k,
                    cap=0.05 * max(1.0, float(np.abs(a64).max())))
     check_grads(gpu_grads, dict(b32=grads["f32"], b64=grads["f64"], b32r=grads["f32r"]),
-                ["means3D", "means2D", "opacity", "colors", "normals", "scales", "rotations"], "C5")
+                ["means3D", "means2D", "opacity", "colors", "normals", "scales", "rotations"], "C5",
+                excuse=flip_excuse([ref1]))
     check_radii(gpu_pass1["radii"], ref1, "C5 pass 1")
 
 
