@@ -42,6 +42,16 @@ typedef double real;
 #define SQRTR sqrt
 #define FMAR fma
 #define CEILR ceil
+#elif defined(ORACLE_F32C)
+/* fp32 with the compiler's multiply-add contraction (built -ffp-contract=fast -mfma): another faithful fp32
+ * evaluation, as nvcc's default --fmad=true compiles the reference's CUDA; tests/gsr_testutil.py uses it to
+ * measure how far faithful fp32 evaluations of the reference algorithm are from each other, row by row */
+typedef float real;
+#define FN(name) name##_f32c
+#define EXPR expf
+#define SQRTR sqrtf
+#define FMAR fmaf
+#define CEILR ceilf
 #else
 typedef float real;
 #define FN(name) name##_f32
@@ -386,7 +396,7 @@ static long g_stats[4];
 #ifdef _OPENMP
 #include <omp.h>
 #endif
-#ifndef ORACLE_F64
+#if !defined(ORACLE_F64) && !defined(ORACLE_F32C)
 int g_oracle_threads = 1;
 void oracle_set_threads(int n) { g_oracle_threads = n > 0 ? n : 1; }
 int oracle_get_threads(void) { return g_oracle_threads; }

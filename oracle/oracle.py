@@ -42,7 +42,7 @@ def _f32(a):
 
 
 def _dtype(prec):
-    return np.float32 if prec == "f32" else np.float64
+    return np.float32 if prec in ("f32", "f32c") else np.float64
 
 
 def _args(scene, cam, bg):

@@ -353,37 +353,65 @@ def test_c5_sugar_normal_renderer():
     ref1 = run_oracle(sc1, cam, [0.0, 0.0, 0.0])
     ref2 = run_oracle(sc2, cam, [0.0, 0.0, 0.0])
     check_forward(gpu_pass1, ref1, "C5 pass 1")
-    epi, grads = {}, {}
-    # f32r: the fp32 oracle again with the per-Gaussian sums in reverse pixel order (another run of the
-    # reference's unordered atomic accumulation): the rows it moves measure the reference against itself
-    for prec, dt in (("f32", torch.float32), ("f64", torch.float64), ("f32r", torch.float32)):
-        order = 1 if prec == "f32r" else 0
-        prec, key = ("f32", "f32r") if prec == "f32r" else (prec, prec)
+    # The epilogue's upstream gradients into the rasterizer, from the torch restatement on the oracle's fp32 /
+    # fp64 outputs (the normal-from-distance stencil is ill-conditioned: its fp32 and fp64 gradients differ
+    # far more than the rasterizer's do, and the GPU's fused HIP epilogue — held to torch in
+    # tests/test_shading.py — sees the GPU's depth)
+    epi, ups_r = {}, {}
+    for prec, dt in (("f32", torch.float32), ("f64", torch.float64)):
         f1, f2 = ref1[prec], ref2[prec]
         lc, ld, la, ln = (torch.tensor(x, dtype=dt, requires_grad=True)
                           for x in (f1["color"], f1["depth"], f1["alpha"], f2["color"]))
         o = _sugar_epilogue(torch, lc, ld, la, ln, rays_o.to(dt), rays_d.to(dt),
                             lambda dd, aa: tr.sugar_normal_from_dist(dd, aa, rays_o.to(dt), rays_d.to(dt)))
         loss_of(o, lambda x: torch.tensor(x, dtype=dt)).backward()
-        epi[key] = {k: o[k].detach().numpy() for k in SUGAR_OUT}
-        as32 = lambda x: x.grad.numpy().astype(np.float32)  # noqa: E731  (the C ABI takes fp32 gradients)
-        b1 = oracle.backward(sc1, oracle_cam(cam), np.zeros(3, np.float32), as32(lc), as32(ld), as32(la), prec=prec,
+        epi[prec] = {k: o[k].detach().numpy() for k in SUGAR_OUT}
+        # (the C ABI takes fp32 gradients)
+        ups_r[prec] = [x.grad.numpy().astype(np.float32) for x in (lc, ld, la, ln)]
+
+    def oracle_grads(prec, up, order=0):
+        b1 = oracle.backward(sc1, oracle_cam(cam), np.zeros(3, np.float32), up[0], up[1], up[2], prec=prec,
                              order=order)
-        b2 = oracle.backward(sc2, oracle_cam(cam), np.zeros(3, np.float32), as32(ln), None, None, prec=prec,
+        b2 = oracle.backward(sc2, oracle_cam(cam), np.zeros(3, np.float32), up[3], None, None, prec=prec,
                              order=order)
-        grads[key] = {k: np.asarray(b1[k], np.float64) + np.asarray(b2[k], np.float64)
-                      for k in ("means3D", "scales", "rotations", "opacity")}
-        grads[key]["colors"] = b1["colors"]
-        grads[key]["normals"] = b2["colors"]
-        grads[key]["means2D"] = b1["means2D"]
+        g = {k: np.asarray(b1[k], np.float64) + np.asarray(b2[k], np.float64)
+             for k in ("means3D", "scales", "rotations", "opacity")}
+        g.update(colors=b1["colors"], normals=b2["colors"], means2D=b1["means2D"])
+        return g
+
     for k in SUGAR_OUT:
         a64 = epi["f64"][k]
         rows = lambda x: np.asarray(x).reshape(x.shape[0], -1).T  # noqa: E731
         adjudicate(rows(gpu_out[k]), rows(epi["f32"][k]), rows(a64), 1e-5 + 1e-5 * np.abs(rows(a64)), "C5", k,
                    cap=0.05 * max(1.0, float(np.abs(a64).max())))
-    check_grads(gpu_grads, dict(b32=grads["f32"], b64=grads["f64"], b32r=grads["f32r"]),
-                ["means3D", "means2D", "opacity", "colors", "normals", "scales", "rotations"], "C5",
+    keys = ["means3D", "means2D", "opacity", "colors", "normals", "scales", "rotations"]
+    # (1) the rasterizer (both calls' backward in one pass): the GPU backward with the fp32 epilogue's upstream
+    # gradients, against the oracle's two backward passes with the same upstream gradients in fp32 / fp64 and
+    # the fp32 one in reverse pixel order (another run of the reference's unordered atomic accumulation):
+    # every row under the row rule
+    up32 = ups_r["f32"]
+    t = dict(means3D=leaf(scene["means3D"]), scales=leaf(scene["scales"]), rotations=leaf(scene["rotations"]),
+             opacities=leaf(scene["opacities"]), colors=leaf(colors), normals=leaf(normals))
+    m2 = torch.zeros((P, 3), device=dev, requires_grad=True)
+    c, r, d, a, nrm = rasterize_views([s], t["means3D"], [m2], t["opacities"], colors_precomp=t["colors"],
+                                      scales=t["scales"], rotations=t["rotations"], colors2=t["normals"])
+    torch.autograd.backward((c[0], d[0], a[0], nrm[0]), [torch.tensor(x, device=dev) for x in up32])
+    gpu_rast = dict(g_means3D=t["means3D"].grad.cpu().numpy(), g_scales=t["scales"].grad.cpu().numpy(),
+                    g_rotations=t["rotations"].grad.cpu().numpy(), g_opacity=t["opacities"].grad.cpu().numpy(),
+                    g_colors=t["colors"].grad.cpu().numpy(), g_normals=t["normals"].grad.cpu().numpy(),
+                    g_means2D=m2.grad.cpu().numpy())
+    del t, c, d, a, nrm
+    torch.cuda.empty_cache()
+    check_grads(gpu_rast, dict(b32=oracle_grads("f32", up32), b64=oracle_grads("f64", up32),
+                               b32r=oracle_grads("f32", up32, order=1)), keys, "C5 rasterizer",
                 excuse=flip_excuse([ref1]))
+    # (2) the renderer end to end (fused HIP epilogue + rasterizer) against the oracle's pipeline in fp32 / fp64:
+    # the count rule (the epilogue's conditioning moves rows that no rasterizer difference explains)
+    pipe32, pipe64 = oracle_grads("f32", up32), oracle_grads("f64", ups_r["f64"])
+    for k in keys:
+        r64 = np.asarray(pipe64[k], np.float64)
+        adjudicate(gpu_grads["g_" + k], pipe32[k], r64, 1e-4 * np.maximum(1.0, np.abs(r64)), "C5 end to end",
+                   "grad " + k, excuse=flip_excuse([ref1]))
     check_radii(gpu_pass1["radii"], ref1, "C5 pass 1")
 
 
