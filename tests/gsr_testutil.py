@@ -305,13 +305,17 @@ def check_grads(gpu, ref, keys, what="", excuse=None):
     b32, b64, b32r = ref["b32"], ref["b64"], ref.get("b32r")
     if excuse is None:
         excuse = flip_dependents(ref, ref.get("gpu_only_px", ())) if "aux64" in ref else None
-    out = {}
-    for k in keys:
+    out, failed = {}, []
+    for k in keys:  # every tensor is adjudicated (and reported) before the first failure is raised
         r64 = b64[k]
         bar = GRAD_TOL * np.maximum(1.0, np.abs(r64))
         ex = excuse if excuse is not None and excuse.shape[0] == r64.shape[0] else None
-        out[k] = adjudicate(gpu["g_" + k], b32[k], r64, bar, what, "grad " + k, excuse=ex, rowwise=True,
-                            r32b=b32r[k] if b32r is not None else None)
+        try:
+            out[k] = adjudicate(gpu["g_" + k], b32[k], r64, bar, what, "grad " + k, excuse=ex, rowwise=True,
+                                r32b=b32r[k] if b32r is not None else None)
+        except AssertionError as e:
+            failed.append(str(e))
+    assert not failed, "\n".join(failed)
     return out
 
 
