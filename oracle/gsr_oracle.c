@@ -411,7 +411,8 @@ void oracle_set_order(int order) { g_oracle_order = order; }
  * arithmetic the way the HIP blends do, to attribute their differences from this restatement.
  *   1  exponent: conic pre-multiplied by -log2(e)/2, -log2(e) (rounded), exp2 (csrc/gsr_common.h gauss_power2)
  *   2  transmittance recovery T * (1 / (1 - alpha)) instead of T / (1 - alpha)
- *   4  dL/dalpha from one scalar S = sum_ch accum_ch dL/dpix_ch (csrc/gsr_render.hip k_render_bwd replay)
+ *   4  dL/dalpha from one scalar S = sum_ch accum_ch dL/dpix_ch over colour and alpha, the depth channel as
+ *      (depth - accumulated depth) dL/ddepth (csrc/gsr_render.hip k_render_bwd replay)
  *   8  dL/dmean2D from the first moments of u = G dL/dalpha and the pre-multiplied conic, as the blend's
  *      flush forms it: (o / log2 e) (W/2) (2 A m1 + B m2), A = -log2(e)/2 a, B = -log2(e) b (rounded) */
 int g_oracle_variant = 0;
@@ -608,7 +609,7 @@ void FN(oracle_backward)(int P, int deg, int M, const float* means, const float*
           const real dpa = dL_dalpha ? (real)dL_dalpha[pid] : 0;
           const real bg_dot = c.bg[0] * dpix[0] + c.bg[1] * dpix[1] + c.bg[2] * dpix[2];
           real accr[3] = {0, 0, 0}, accd = 0, acca = 0, last_alpha = 0, last_c[3] = {0, 0, 0}, last_d = 0;
-          real S = 0;  /* diagnostic variant 4 */
+          real S = 0, Sd = 0;  /* diagnostic variant 4 */
           for (long rel = (long)last - 1; rel >= 0; --rel) {
             const uint32_t gi = f.inst[s + rel].g;
             const gstate* g = &f.gs[gi];
@@ -626,10 +627,10 @@ void FN(oracle_backward)(int P, int deg, int M, const float* means, const float*
             real dL_dalpha = 0;
             real* a = tacc + (size_t)10 * gi;
             if (g_oracle_variant & 4) {
-              const real cd = FMAR(g->rgb[0], dpix[0], FMAR(g->rgb[1], dpix[1], FMAR(g->rgb[2], dpix[2],
-                                   FMAR(g->depth, dpd, dpa))));
-              dL_dalpha = FMAR(T, cd - S, (RL(1) / (RL(1) - alpha)) * (-T_final * bg_dot));
+              const real cd = FMAR(g->rgb[0], dpix[0], FMAR(g->rgb[1], dpix[1], FMAR(g->rgb[2], dpix[2], dpa)));
+              dL_dalpha = FMAR(T, FMAR(g->depth - Sd, dpd, cd - S), (RL(1) / (RL(1) - alpha)) * (-T_final * bg_dot));
               S = FMAR(alpha, cd, (RL(1) - alpha) * S);
+              Sd = FMAR(alpha, g->depth, (RL(1) - alpha) * Sd);
               for (int ch = 0; ch < 3; ++ch) a[6 + ch] += dcd * dpix[ch];
               a[9] += dcd * dpd;
             } else {

@@ -368,7 +368,7 @@ def _c4_oracle_views(single, B, S, views):
                                       np.zeros((1, S, S), np.float32), ga.astype(np.float32), prec=prec)
             if prec == "f32":
                 b["f32r"] = oracle.backward(scene, oracle_cam(cam), np.zeros(3, np.float32), gcol.astype(np.float32),
-                                            np.zeros((1, S, S), np.float32), ga.astype(np.float32), prec=prec, order=1)
+                                            np.zeros((1, S, S), np.float32), ga.astype(np.float32), prec="f32c", order=1)
         px = lambda a: np.asarray(a).reshape(3, -1).T  # noqa: E731
         gpu_img = single["comp_rgb"][v].transpose(2, 0, 1)
         adjudicate(px(gpu_img), px(b["render_f32"]), px(b["render_f64"]), 1e-5, f"C4 {S}^2 view {v}", "comp_rgb",

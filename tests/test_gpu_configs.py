@@ -149,7 +149,7 @@ def test_c3_views_fused_background_composite():
                                       prec=prec)
             if prec == "f32":  # another run of the reference's (unordered, atomic) accumulation
                 b["f32r"] = oracle.backward(scene, oracle_cam(cam), np.zeros(3, np.float32), gcol, g_d, ga,
-                                            prec=prec, order=1)
+                                            prec="f32c", order=1)
             b["bg_" + prec] = (gcol * (dt(1) - f["alpha"].astype(dt))).transpose(1, 2, 0)
         check_forward(_view(gpu, v), ref, f"C3 view {v}", K_gpu=gpu["K"][v])
         adjudicate(gpu["g_means2D"][v], b["f32"]["means2D"], b["f64"]["means2D"],
@@ -403,7 +403,7 @@ def test_c5_sugar_normal_renderer():
     del t, c, d, a, nrm
     torch.cuda.empty_cache()
     check_grads(gpu_rast, dict(b32=oracle_grads("f32", up32), b64=oracle_grads("f64", up32),
-                               b32r=oracle_grads("f32", up32, order=1)), keys, "C5 rasterizer",
+                               b32r=oracle_grads("f32c", up32, order=1)), keys, "C5 rasterizer",
                 excuse=flip_excuse([ref1]))
     # (2) the renderer end to end (fused HIP epilogue + rasterizer) against the oracle's pipeline in fp32 / fp64:
     # the count rule (the epilogue's conditioning moves rows that no rasterizer difference explains)
@@ -476,7 +476,7 @@ def test_second_colors_match_separate_call(bwd, monkeypatch):
     sc2 = dict(scene, colors_precomp=normals)
     sc2.pop("shs")
     ref = {}
-    for prec, order, key in (("f32", 0, "b32"), ("f64", 0, "b64"), ("f32", 1, "b32r")):
+    for prec, order, key in (("f32", 0, "b32"), ("f64", 0, "b64"), ("f32c", 1, "b32r")):
         acc = {}
         for v, cam in enumerate(cams):
             u0, u1, u2 = (ups[i][v].cpu().numpy() for i in range(3))
@@ -574,8 +574,8 @@ def test_two_color_backward_with_fused_composite():
         g_r, g_d, g_a = ups[0][v], ups[1][v][:1], ups[1][v][1:2]
         bgs = {}
         for prec, dt, order, key in (("f32", np.float32, 0, "b32"), ("f64", np.float64, 0, "b64"),
-                                     ("f32", np.float32, 1, "b32r")):
-            f = fw[prec]
+                                     ("f32c", np.float32, 1, "b32r")):
+            f = fw["f32" if prec == "f32c" else prec]
             _, pre = _composite(f["color"].astype(dt), f["alpha"].astype(dt), bg_img[v].astype(dt))
             gcol, ga = _composite_upstream(g_r, g_a, pre, bg_img[v])
             b1 = oracle.backward(scene, oracle_cam(cam), zero, gcol, g_d, ga, prec=prec, order=order)
@@ -586,7 +586,7 @@ def test_two_color_backward_with_fused_composite():
             terms["sh"], terms["normals"] = np.asarray(b1["sh"], np.float64), np.asarray(b2["colors"], np.float64)
             for k, x in terms.items():
                 acc[k] = acc.get(k, 0.0) + x
-            if order == 0:
+            if prec != "f32c":
                 bgs[prec] = (gcol * (dt(1) - f["alpha"].astype(dt))).transpose(1, 2, 0).reshape(-1, 3)
                 bgs["m2_" + prec] = b1["means2D"]
             else:

@@ -781,11 +781,15 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(TWO ? 4 : 5
   // The reference keeps per channel the colour accumulated behind the current Gaussian
   // (accum_rec = last_alpha last_c + (1 - last_alpha) accum_rec, deferred by one contributor) and
   // forms dL/dalpha = T sum_ch (c_ch - accum_ch) dL/dpix_ch - T_final / (1 - alpha) bg . dL/dpix.
-  // Only the dot product with dL/dpix enters, and the update is linear, so one scalar carries all
-  // five channels (r, g, b, depth, alpha with c_alpha = 1):
+  // Only the dot product with dL/dpix enters, and the update is linear, so one scalar carries the
+  // colour and alpha channels (r, g, b, alpha with c_alpha = 1):
   //   S = sum_ch accum_ch dL/dpix_ch,  cd = sum_ch c_ch dL/dpix_ch,  S <- alpha cd + (1 - alpha) S
   // applied eagerly after each contributor's own dL/dalpha (non-contributors: alpha = 0, identity).
-  float S = 0.f;
+  // The depth channel keeps its own accumulated depth Sd and enters as (depth - Sd) dL/ddepth, the
+  // reference's order: the depths of a surface's Gaussians nearly coincide, so folded into S the
+  // difference would be taken after the multiplication by dL/ddepth (which reaches ~1e3 through a
+  // normal-from-depth loss) and lose its significant bits.
+  float S = 0.f, Sd = 0.f;
   const float nbg = -T_final * bg_dot;
   const float ddelx_dx = 0.5f * W, ddely_dy = 0.5f * H;
   const float4 zero4 = make_float4(0.f, 0.f, 0.f, 0.f);
@@ -834,11 +838,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(TWO ? 4 : 5
     const float oma = 1.f - a_eff;
     const float inv_1ma = fast_rcp(oma);  // 1 for non-contributors
     T = T * inv_1ma;
-    const float cd = fmaf(gc.x, dpix[0], fmaf(gc.y, dpix[1], fmaf(gc.z, dpix[2], fmaf(gb.z, dpix_d, dpix_a))));
-    const float dL_dalpha = fmaf(T, cd - S, inv_1ma * nbg);
+    const float cd = fmaf(gc.x, dpix[0], fmaf(gc.y, dpix[1], fmaf(gc.z, dpix[2], dpix_a)));
+    const float dL_dalpha = fmaf(T, fmaf(gb.z - Sd, dpix_d, cd - S), inv_1ma * nbg);
     u = g_eff * dL_dalpha;
     w = a_eff * T;
     S = fmaf(a_eff, cd, oma * S);
+    Sd = fmaf(a_eff, gb.z, oma * Sd);
   };
   // two colours: gd = the second colour; uT = u_1 + u_2, u1 = u_1
   auto replay2 = [&](const float4& ga, const float4& gb, const float4& gc, const float4& gd, float& uT, float& u1,
@@ -854,12 +859,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(TWO ? 4 : 5
     const float oma = 1.f - a_eff;
     const float inv_1ma = fast_rcp(oma);
     T = T * inv_1ma;
-    const float cd = fmaf(gc.x, dpix[0], fmaf(gc.y, dpix[1], fmaf(gc.z, dpix[2], fmaf(gb.z, dpix_d, dpix_a))));
+    const float cd = fmaf(gc.x, dpix[0], fmaf(gc.y, dpix[1], fmaf(gc.z, dpix[2], dpix_a)));
     const float cd2 = fmaf(gd.x, dpix2[0], fmaf(gd.y, dpix2[1], gd.z * dpix2[2]));
-    u1 = g_eff * fmaf(T, cd - S, inv_1ma * nbg);
+    u1 = g_eff * fmaf(T, fmaf(gb.z - Sd, dpix_d, cd - S), inv_1ma * nbg);
     uT = fmaf(g_eff, fmaf(T, cd2 - S2, inv_1ma * nbg2), u1);
     w = a_eff * T;
     S = fmaf(a_eff, cd, oma * S);
+    Sd = fmaf(a_eff, gb.z, oma * Sd);
     S2 = fmaf(a_eff, cd2, oma * S2);
   };
 
