@@ -598,6 +598,7 @@ def main():
     torch.cuda.synchronize()
     _C.RECENT_FORWARDS.clear()
     _C.RECENT_LISTED.clear()
+    _C.host_trace_read(reset=True)
     if not args.no_profile:
         _C.profile_read(reset=True)
         _C.profile_enable(True)
@@ -671,10 +672,16 @@ def main():
         res["config"]["two_calls"] = ("separate renders" if SUGAR_SEPARATE else "shared forward, " + (
             "separate backward passes" if os.environ.get("GSR_TWO_COLOR_BWD") == "separate"
             else "one two-colour backward pass"))
+    if _C.HOST_TRACE:  # GSR_HOST_TRACE=1: host (Python + ctypes) time per step of the rasterizer's phases
+        res["host_ms_per_step"] = {k: round(1000.0 * v / args.steps, 3) for k, v in _C.host_trace_read().items()}
     if phases is not None:
         nv = max(1, args.steps * per)
         kern = {k: {"ms_per_view": round(ms / nv, 4), "launches": n} for k, (ms, n) in phases.items()}
         res["kernels"] = kern
+        # wall time per step not covered by the rasterizer's kernels (the composite / collectives / torch ops
+        # and the GPU idling while the host prepares launches)
+        res["gap_ms_per_step"] = round(1000.0 * elapsed / args.steps - sum(ms for ms, _ in phases.values()) /
+                                       args.steps, 3)
         res.update(roofline_fields(args, phases, Ks, Ls, H, W))
     if not args.no_knn:
         res["init_knn"] = time_knn(rep.means3D.detach())

@@ -342,6 +342,19 @@ __global__ __launch_bounds__(256) void k_view_grad(GaussBackwardArgs a, ViewGrad
     }
     const uint32_t clamp_bits = gr.d.w;
     const RowSums r = gather_rows<TWO>((uint32_t)idx, gr, go, va.gx, cut, grow);
+    // A Gaussian no blended pixel reached in this view (occluded, or only in tiles past their cut) has
+    // all-zero sums: its record is zeros without the chain rule (most Gaussians of a view at 1M)
+    bool reached = (r.dmx != 0.f) | (r.dmy != 0.f) | (r.dca != 0.f) | (r.dcb != 0.f) | (r.dcc != 0.f) |
+                   (r.dop != 0.f) | (r.dcr != 0.f) | (r.dcg != 0.f) | (r.dcbl != 0.f) | (r.ddep != 0.f);
+    if (TWO) reached = reached | (r.dr2 != 0.f) | (r.dg2 != 0.f) | (r.db2 != 0.f);
+    if (!reached) {
+      m2[0] = 0.f;
+      m2[1] = 0.f;
+      m2[2] = 0.f;
+#pragma unroll
+      for (int f = 0; f < NF; ++f) rec[(size_t)f * a.P] = f == 13 ? __uint_as_float(clamp_bits) : 0.f;
+      continue;
+    }
     // (two colours: the first call's own screen-space gradient; the chain below takes both calls')
     m2[0] = TWO ? r.dmx1 : r.dmx;
     m2[1] = TWO ? r.dmy1 : r.dmy;
@@ -449,7 +462,9 @@ __global__ __launch_bounds__(256) void k_gauss_accum(GaussBackwardArgs a, AccumA
       dcg += f[10];
       dcb += f[11];
       dop += f[12];
-      if (has_sh) {
+      // (a view whose colour gradient is zero adds nothing to dL/dSH nor, through the view direction,
+      // to dL/dmean: skipped)
+      if (has_sh && ((f[9] != 0.f) | (f[10] != 0.f) | (f[11] != 0.f))) {
         const uint32_t cl = __float_as_uint(f[13]);
         const float3 dRGB = make_float3((cl & 1u) ? 0.f : f[9], (cl & 2u) ? 0.f : f[10], (cl & 4u) ? 0.f : f[11]);
         // the SH row as 16-byte LDS reads (stride sh_lds_stride: conflict-free); entries past 3M unused

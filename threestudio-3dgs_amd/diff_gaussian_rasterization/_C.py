@@ -122,6 +122,29 @@ class GSRError(RuntimeError):
     pass
 
 
+# Host-side time of the rasterizer's Python phases (GSR_HOST_TRACE=1; bench.py reports it): seconds per
+# phase name, accumulated until host_trace_read(reset=True).  Off: one attribute test per phase.
+HOST_TRACE = os.environ.get("GSR_HOST_TRACE") == "1"
+_HOST = collections.defaultdict(float)
+
+
+def host_mark(name: str, t0: float) -> float:
+    """Add the time since t0 to phase `name`; returns now (the next phase's t0)."""
+    import time
+
+    now = time.perf_counter()
+    if HOST_TRACE:
+        _HOST[name] += now - t0
+    return now
+
+
+def host_trace_read(reset: bool = True) -> dict:
+    out = dict(_HOST)
+    if reset:
+        _HOST.clear()
+    return out
+
+
 ABI_VERSION = 3  # include/gsr.h GSR_ABI_VERSION this binding is written against
 
 

@@ -16,6 +16,7 @@ from __future__ import annotations
 import ctypes
 import math
 import os
+import time
 
 import torch
 
@@ -43,20 +44,25 @@ class _ViewSet:
         self.tanx, self.tany = tanx, tany
         self.K = None
         self.geom = self.binning = self.image = None
+        # the host arrays the C ABI takes, built once for the forward and the backward
+        self.arrays = (_ptrs([c[0] for c in cams]), _ptrs([c[1] for c in cams]), _ptrs([c[2] for c in cams]),
+                       _arr(ctypes.c_float, tanx), _arr(ctypes.c_float, tany))
+        self.bgs = _ptrs([c[3] for c in cams])
+        self.Karr = None
 
     @property
     def V(self):
         return self.hi - self.lo
 
     def cam_arrays(self):
-        return (_ptrs([c[0] for c in self.cams]), _ptrs([c[1] for c in self.cams]), _ptrs([c[2] for c in self.cams]),
-                _arr(ctypes.c_float, self.tanx), _arr(ctypes.c_float, self.tany))
+        return self.arrays
 
 
 class _RasterizeViews(torch.autograd.Function):
     @staticmethod
     def forward(ctx, settings_list, grad_reduce, means3D, sh, colors_precomp, opacities, scales, rotations,
                 cov3D_precomp, composite_bg, colors2, *means2D):
+        t0 = time.perf_counter()
         lib = _C.load_library()
         V = len(settings_list)
         dev = means3D.device
@@ -99,35 +105,40 @@ class _RasterizeViews(torch.autograd.Function):
                           [float(s.tanfovy) for s in settings_list[lo:hi]])
             vs.geom = torch.empty(int(lib.gsr_set_geom_bytes(vs.V, P)), dtype=torch.uint8, device=dev)
             views, projs, campos, tx, ty = vs.cam_arrays()
+            t0 = _C.host_mark("fwd_setup", t0)
             _C._check(lib.gsr_set_preprocess(
                 vs.V, P, int(s0.sh_degree), M, p(m3), p(sc), float(s0.scale_modifier), p(rot), p(op), p(shc), p(col),
                 p(c3), views, projs, campos, tx, ty, W, H, int(bool(s0.prefiltered)), p(radii[lo:hi]), p(vs.geom),
                 stream))
             sets.append(vs)
+            t0 = _C.host_mark("fwd_preprocess_launch", t0)
         for vs in sets:
             K = (ctypes.c_int * vs.V)()
             L = (ctypes.c_int * vs.V)()
+            # the reference's one host sync: the instance counts size the binning buffers
             _C._check(lib.gsr_set_num_rendered_ex(vs.V, p(vs.geom), P, K, None, L, stream))
-            vs.K = [int(k) for k in K]
-            _C.RECENT_LISTED.extend(int(x) for x in L)
+            t0 = _C.host_mark("fwd_sync_wait", t0)
+            vs.K = list(K)
+            _C.RECENT_LISTED.extend(L)
             _C.RECENT_FORWARDS.extend((k, H, W) for k in vs.K)
-            Karr = _arr(ctypes.c_int, vs.K)
+            Karr = vs.Karr = _arr(ctypes.c_int, vs.K)
             vs.binning = torch.empty(int(lib.gsr_set_binning_bytes(vs.V, P, Karr, W, H)), dtype=torch.uint8, device=dev)
             vs.image = torch.empty(int(lib.gsr_set_image_bytes(vs.V, W, H)), dtype=torch.uint8, device=dev)
             sl = slice(vs.lo, vs.hi)
             if c2 is not None:
                 _C._check(lib.gsr_set_render_two_colors(
-                    vs.V, P, Karr, W, H, _ptrs([c[3] for c in vs.cams]), p(vs.geom), p(vs.binning), p(vs.image),
+                    vs.V, P, Karr, W, H, vs.bgs, p(vs.geom), p(vs.binning), p(vs.image),
                     p(color[sl]), p(depth[sl]), p(alpha[sl]), p(cbg[sl]) if cbg is not None else None,
                     p(render[sl]) if cbg is not None else None, p(c2), p(color2[sl]), stream))
             elif cbg is None:
-                _C._check(lib.gsr_set_render(vs.V, P, Karr, W, H, _ptrs([c[3] for c in vs.cams]), p(vs.geom),
+                _C._check(lib.gsr_set_render(vs.V, P, Karr, W, H, vs.bgs, p(vs.geom),
                                              p(vs.binning), p(vs.image), p(color[sl]), p(depth[sl]), p(alpha[sl]),
                                              stream))
             else:
                 _C._check(lib.gsr_set_render_composite(
-                    vs.V, P, Karr, W, H, _ptrs([c[3] for c in vs.cams]), p(vs.geom), p(vs.binning), p(vs.image),
+                    vs.V, P, Karr, W, H, vs.bgs, p(vs.geom), p(vs.binning), p(vs.image),
                     p(color[sl]), p(depth[sl]), p(alpha[sl]), p(cbg[sl]), p(render[sl]), stream))
+            t0 = _C.host_mark("fwd_render_launch", t0)
         ctx.settings = settings_list
         ctx.grad_reduce = grad_reduce
         ctx.sets = sets
@@ -140,6 +151,7 @@ class _RasterizeViews(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, g_color, _g_radii, g_depth, g_alpha, g_color2=None):
+        t0 = time.perf_counter()
         lib = _C.load_library()
         m3, shc, col, sc, rot, c3, radii, cbg, color, c2 = ctx.saved_tensors
         second = c2 is not None and g_color2 is not None
@@ -199,14 +211,15 @@ class _RasterizeViews(torch.autograd.Function):
                     # the last set's call forms the final per-Gaussian sums: in ranges, an event after each
                     _C._check(lib.gsr_set_backward_chunks(
                         len(events), _arr(ctypes.c_void_p, [e.cuda_event for e in events])))
-                Karr = _arr(ctypes.c_int, vs.K)
+                Karr = vs.Karr
+                # (the scratch grows with K: the largest single view bounds what a view group needs)
+                kmax = _arr(ctypes.c_int, [max(vs.K)])
                 if fused2:
                     need = int(lib.gsr_set_backward_two_colors_bytes(vs.V, P, Karr))
-                    largest = max(int(lib.gsr_set_backward_two_colors_bytes(1, P, _arr(ctypes.c_int, [k])))
-                                  for k in vs.K)
+                    largest = int(lib.gsr_set_backward_two_colors_bytes(1, P, kmax))
                 else:
                     need = int(lib.gsr_set_backward_bytes(vs.V, P, Karr))
-                    largest = max(int(lib.gsr_backward_bytes(P, k)) for k in vs.K)
+                    largest = int(lib.gsr_set_backward_bytes(1, P, kmax))
                 work = torch.empty(max(largest, min(need, WORK_BUDGET)), dtype=torch.uint8, device=dev)
                 views, projs, campos, tx, ty = vs.cam_arrays()
                 sl = slice(vs.lo, vs.hi)
@@ -214,7 +227,7 @@ class _RasterizeViews(torch.autograd.Function):
                 gap = p(ga[sl]) if ga is not None else None
                 if fused2:
                     _C._check(lib.gsr_set_backward_two_colors(
-                        vs.V, P, int(s0.sh_degree), M, Karr, W, H, _ptrs([c[3] for c in vs.cams]), p(m3), p(sc),
+                        vs.V, P, int(s0.sh_degree), M, Karr, W, H, vs.bgs, p(m3), p(sc),
                         float(s0.scale_modifier), p(rot), p(shc), p(c3), views, projs, campos, tx, ty, p(radii[sl]),
                         p(vs.geom), p(vs.binning), p(vs.image), p(cbg[sl]) if cbg is not None else None,
                         p(color[sl]) if cbg is not None else None, p(gc[sl]), gdp, gap,
@@ -224,14 +237,14 @@ class _RasterizeViews(torch.autograd.Function):
                     continue
                 if cbg is None:
                     _C._check(lib.gsr_set_backward(
-                        vs.V, P, int(s0.sh_degree), M, Karr, W, H, _ptrs([c[3] for c in vs.cams]), p(m3), p(sc),
+                        vs.V, P, int(s0.sh_degree), M, Karr, W, H, vs.bgs, p(m3), p(sc),
                         float(s0.scale_modifier), p(rot), p(shc), p(c3), views, projs, campos, tx, ty, p(radii[sl]),
                         p(vs.geom), p(vs.binning), p(vs.image), p(gc[sl]), gdp, gap, p(d_m2[sl]), p(d_col), p(d_op),
                         p(d_m3), p(d_c3), p(d_sh), p(d_sc), p(d_rot), 1 if si > 0 else 0, p(work), work.numel(),
                         stream))
                 else:
                     _C._check(lib.gsr_set_backward_composite(
-                        vs.V, P, int(s0.sh_degree), M, Karr, W, H, _ptrs([c[3] for c in vs.cams]), p(m3), p(sc),
+                        vs.V, P, int(s0.sh_degree), M, Karr, W, H, vs.bgs, p(m3), p(sc),
                         float(s0.scale_modifier), p(rot), p(shc), p(c3), views, projs, campos, tx, ty, p(radii[sl]),
                         p(vs.geom), p(vs.binning), p(vs.image), p(cbg[sl]), p(color[sl]), p(gc[sl]), gdp, gap,
                         p(d_bg[sl]) if d_bg is not None else None, p(d_m2[sl]), p(d_col), p(d_op), p(d_m3), p(d_c3),
@@ -242,7 +255,7 @@ class _RasterizeViews(torch.autograd.Function):
                     g2 = g_color2.float().contiguous()
                     m2_scratch = torch.empty((vs.V, P, 3), **fopt)
                     _C._check(lib.gsr_set_backward_colors(
-                        vs.V, P, Karr, W, H, _ptrs([c[3] for c in vs.cams]), p(m3), p(sc), float(s0.scale_modifier),
+                        vs.V, P, Karr, W, H, vs.bgs, p(m3), p(sc), float(s0.scale_modifier),
                         p(rot), p(c3), views, projs, campos, tx, ty, p(radii[sl]), p(vs.geom), p(vs.binning),
                         p(vs.image), p(c2), p(g2[sl]), p(m2_scratch), p(d_c2), p(d_op), p(d_m3), p(d_c3), p(d_sc),
                         p(d_rot), 1, p(work), work.numel(), stream))
@@ -258,6 +271,7 @@ class _RasterizeViews(torch.autograd.Function):
             # the per-Gaussian gradients' sums over ranks, range by range as the backward finishes them
             shared = [grads[k] for k in (2, 3, 4, 5, 6, 7, 8, 10)]
             ctx.grad_reduce.launch(shared, P, events if P > 0 and ctx.grad_reduce.active() else None)
+        _C.host_mark("bwd_host", t0)
         return tuple(grads)
 
 
