@@ -52,6 +52,12 @@ def summarise(tl, name):
         "work_sum": int(work.astype(np.int64).sum()),
         "bwd_lockstep_slots_per_pair": (float(tl[:, 2].astype(np.float64).sum() / max(1, work.sum()))
                                         if name == "k_render_bwd" else None),
+        # bwd: block duration = fixed + per-slot cost (least squares over the recorded blocks): the fixed part is
+        # what a workgroup spends outside its candidate groups (prologue loads, staging latency, barriers)
+        "bwd_fit_fixed_us_per_slot_ns": ([float(x) for x in np.polyfit(tl[:, 2].astype(np.float64), dur, 1)[::-1] /
+                                          np.array([1e3, 1.0])] if name == "k_render_bwd" and len(tl) > 2 else None),
+        "bwd_us_blocks_without_kept_p50": (float(np.median(dur[tl[:, 2] == 0])) / 1e3
+                                           if name == "k_render_bwd" and (tl[:, 2] == 0).any() else None),
     }
 
 
@@ -67,6 +73,25 @@ def main():
     gx = gy = 64
     nb = 128 * ((((gx + 1) // 2) * ((gy + 1) // 2) + 7) // 8)
     out = []
+    if len(sys.argv) > 1 and sys.argv[1] == "set":  # one 64-view set (the bench's launch); the first 64k blocks
+        gen = torch.Generator(device=dev).manual_seed(7)
+        settings = [bench.settings_for(rep, cm, bg0) for cm in cams]
+        bg_img = torch.rand((64, 1024, 1024, 3), generator=gen, device=dev)
+        ups = [torch.randn((64, 3, 1024, 1024), generator=gen, device=dev),
+               torch.randn((64, 1, 1024, 1024), generator=gen, device=dev),
+               torch.randn((64, 1, 1024, 1024), generator=gen, device=dev)]
+        for _ in range(2):
+            c, d, a, _ = bench.render_views(rep, settings, bg_img)
+            torch.autograd.backward((c, d, a), ups)
+            rep.zero_grad()
+        torch.cuda.synchronize()
+        res = {}
+        nbs = 65536
+        for which, name in ((0, "k_render_fwd"), (1, "k_render_bwd")):
+            buf = np.zeros((nbs, 4), np.uint32)
+            assert lib.gsr_diag_timeline(which, buf.ctypes.data, nbs) == 0
+            res[name] = summarise(buf, name)
+        out.append({"view": "set of 64 (first 65536 blocks)", **res})
     for vi in (0, 40):
         for rep_i in range(2):  # second pass = warm
             c, d, a, _ = bench.render_view(rep, cams[vi], bg0, bgc)
