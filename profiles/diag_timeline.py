@@ -25,6 +25,8 @@ from diff_gaussian_rasterization import _C  # noqa: E402
 
 def summarise(tl, name):
     tl = tl[tl[:, 1] != 0]
+    if len(tl) == 0:
+        return {"kernel": name, "blocks": 0}
     t0 = int(tl[:, 0].min())
     st = (tl[:, 0].astype(np.int64) - t0) * 10  # ns
     en = (tl[:, 1].astype(np.int64) - t0) * 10

@@ -613,8 +613,9 @@ static int set_backward(int V, int P, int degree, int M, const int* K, int width
   if (accumulate != 0 && cov3D_precomp == nullptr && dL_dcov3D == nullptr)
     return fail(GSR_EINVAL, "%s", "accumulate needs dL_dcov3D: it carries the running dL/dcov3D between calls");
   if (work_bytes < carry_bytes(P)) return fail(GSR_EINVAL, "%s", "backward work buffer too small");
-  // the running dL/dcov3D: the caller's output when given, else the end of the work buffer
-  const size_t avail = work_bytes - carry_bytes(P);
+  // the running dL/dcov3D: the caller's output when given, else the end of the work buffer (at a 256-byte
+  // boundary whatever work_bytes is)
+  const size_t avail = (work_bytes - carry_bytes(P)) & ~(size_t)255;
   float* carry = dL_dcov3D ? dL_dcov3D : (float*)((char*)work + avail);
   bool first = accumulate == 0;
   // groups of consecutive views whose gradient rows and records fit the work buffer

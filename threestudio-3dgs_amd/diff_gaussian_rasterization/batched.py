@@ -24,7 +24,7 @@ from . import _C
 
 SET_MAX = 64
 # device memory the backward may use at once for gradient rows (views are walked in groups that fit)
-WORK_BUDGET = int(os.environ.get("GSR_BWD_WORK_BYTES", str(24 << 30)))
+WORK_BUDGET = int(os.environ.get("GSR_BWD_WORK_BYTES", str(24 << 30))) & ~255  # (256-byte granularity)
 
 
 def _arr(ctype, values):
