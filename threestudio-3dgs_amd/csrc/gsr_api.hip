@@ -626,7 +626,7 @@ static int set_backward(int V, int P, int degree, int M, const int* K, int width
       rows += K[g1++];
     if (BackwardState::bytes_for(rows, g1 - g0, P, two) > avail)
       return fail(GSR_EINVAL, "%s", "backward work buffer smaller than one view's gradient rows");
-    BackwardState bw = BackwardState::carve(work, rows, two);
+    BackwardState bw = BackwardState::carve(work, rows, P, two);
     RenderSet rs;
     rs.cbg = comp_bg ? comp_bg + (size_t)g0 * HW * 3 : nullptr;
     rs.comp = nullptr;
@@ -655,7 +655,7 @@ static int set_backward(int V, int P, int degree, int M, const int* K, int width
     va.pad_ = 0;
     va.g = g;
     va.img = img;
-    va.radii = radii;
+    va.reach = bw.reach;
     va.grow = bw.grow;
     va.dmeans2D = dL_dmeans2D;
     va.vrec = bw.vrec;
@@ -664,8 +664,7 @@ static int set_backward(int V, int P, int degree, int M, const int* K, int width
     ab.v0 = g0;
     ab.accumulate = first ? 0 : 1;
     ab.pad_ = 0;
-    ab.rec = g.rec;
-    ab.radii = radii;
+    ab.reach = bw.reach;
     ab.vrec = bw.vrec;
     ab.dcov_carry = carry;
     ab.dcolors2 = two ? dL_dcolors2 : nullptr;
@@ -680,6 +679,8 @@ static int set_backward(int V, int P, int degree, int M, const int* K, int width
     }
     {
       PhaseScope ps(GSR_PHASE_RENDER_BWD, s);
+      // the group's reach bits (set by k_render_bwd, read by the per-Gaussian backward)
+      GSR_HIP_CHECK(hipMemsetAsync(bw.reach, 0, sizeof(unsigned long long) * (size_t)P, s));
       launch_render_backward(rs, g, sorted, img, dL_dcolor + (size_t)g0 * 3 * HW,
                              dL_ddepth ? dL_ddepth + (size_t)g0 * HW : nullptr,
                              dL_dalpha ? dL_dalpha + (size_t)g0 * HW : nullptr, bw, s);

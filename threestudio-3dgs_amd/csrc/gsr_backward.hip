@@ -279,7 +279,6 @@ static inline __host__ __device__ int sh_lds_stride(int M) { return ((3 * M + 3)
 template <bool TWO>
 __attribute__((amdgpu_waves_per_eu(4, 8)))
 __global__ __launch_bounds__(256) void k_view_grad(GaussBackwardArgs a, ViewGradArgs va) {
-  constexpr int NF = TWO ? GSR_GRAD_FIELDS2 : GSR_GRAD_FIELDS;
   extern __shared__ uint2 s_cut[];
   const int t = threadIdx.x;
   const int vl = blockIdx.x % va.V;
@@ -307,43 +306,48 @@ __global__ __launch_bounds__(256) void k_view_grad(GaussBackwardArgs a, ViewGrad
   vgm.fy = va.H / (2.0f * cam.tany);
   vgm.fx = va.W / (2.0f * cam.tanx);
   const float4* grow = va.grow + (size_t)(TWO ? 4 : 3) * va.row_start[vl];
-  float* recv = va.vrec + (size_t)vl * NF * a.P;
-  // the next item's radius and record are loaded while the current one is processed
+  constexpr int RS = TWO ? GSR_REC_STRIDE2 : GSR_REC_STRIDE;
+  float4* recv = reinterpret_cast<float4*>(va.vrec + (size_t)vl * RS * a.P);
+  const unsigned long long vbit = 1ull << vl;
+  // Only the Gaussians this view's blend gave a gradient row (reach bit, set by k_render_bwd; ~15 % of a
+  // view at 1M) are loaded and get a record; the others write their zero means2D gradient only
+  // (k_gauss_accum reads the reached records only).  The next item's reach bit and record are loaded
+  // while the current one is processed.
   const int idx_base = a.g0 + (blockIdx.x / va.V) * (256 * GSR_VG_ITEMS) + t;
-  int nrad = 0;
+  bool nreach = false;
   GaussRec nrec;
   uint32_t ngo = 0u;
   if (idx_base < a.g1) {
-    const size_t o0 = (size_t)vg * a.P + idx_base;
-    nrad = va.radii[o0];
-    if (nrad > 0) nrec = va.g.rec[o0], ngo = va.g.goff[o0];
+    nreach = (va.reach[idx_base] & vbit) != 0ull;
+    if (nreach) {
+      const size_t o0 = (size_t)vg * a.P + idx_base;
+      nrec = va.g.rec[o0], ngo = va.g.goff[o0];
+    }
   }
 #pragma unroll 1
   for (int it = 0; it < GSR_VG_ITEMS; ++it) {
     const int idx = idx_base + it * 256;
     if (idx >= a.g1) break;
     const size_t o = (size_t)vg * a.P + idx;
-    const int rad = nrad;
+    const bool has_rows = nreach;
     const GaussRec gr = nrec;
     const uint32_t go = ngo;
     if (it + 1 < GSR_VG_ITEMS && idx + 256 < a.g1) {
-      nrad = va.radii[o + 256];
-      if (nrad > 0) nrec = va.g.rec[o + 256], ngo = va.g.goff[o + 256];
+      nreach = (va.reach[idx + 256] & vbit) != 0ull;
+      if (nreach) nrec = va.g.rec[o + 256], ngo = va.g.goff[o + 256];
     }
     float* m2 = va.dmeans2D + 3 * o;
-    float* rec = recv + idx;
-    if (rad <= 0) {
+    float4* rec = recv + (size_t)idx * (RS / 4);
+    if (!has_rows) {
       m2[0] = 0.f;
       m2[1] = 0.f;
       m2[2] = 0.f;
-#pragma unroll
-      for (int f = 0; f < NF; ++f) rec[(size_t)f * a.P] = 0.f;
       continue;
     }
     const uint32_t clamp_bits = gr.d.w;
     const RowSums r = gather_rows<TWO>((uint32_t)idx, gr, go, va.gx, cut, grow);
-    // A Gaussian no blended pixel reached in this view (occluded, or only in tiles past their cut) has
-    // all-zero sums: its record is zeros without the chain rule (most Gaussians of a view at 1M)
+    // rows that sum to zero (no pixel of the staged tiles kept the Gaussian): a zero record without the
+    // chain rule
     bool reached = (r.dmx != 0.f) | (r.dmy != 0.f) | (r.dca != 0.f) | (r.dcb != 0.f) | (r.dcc != 0.f) |
                    (r.dop != 0.f) | (r.dcr != 0.f) | (r.dcg != 0.f) | (r.dcbl != 0.f) | (r.ddep != 0.f);
     if (TWO) reached = reached | (r.dr2 != 0.f) | (r.dg2 != 0.f) | (r.db2 != 0.f);
@@ -352,7 +356,8 @@ __global__ __launch_bounds__(256) void k_view_grad(GaussBackwardArgs a, ViewGrad
       m2[1] = 0.f;
       m2[2] = 0.f;
 #pragma unroll
-      for (int f = 0; f < NF; ++f) rec[(size_t)f * a.P] = f == 13 ? __uint_as_float(clamp_bits) : 0.f;
+      for (int q = 0; q < RS / 4; ++q)
+        rec[q] = q == 3 ? make_float4(0.f, __uint_as_float(clamp_bits), 0.f, 0.f) : make_float4(0.f, 0.f, 0.f, 0.f);
       continue;
     }
     // (two colours: the first call's own screen-space gradient; the chain below takes both calls')
@@ -378,10 +383,12 @@ __global__ __launch_bounds__(256) void k_view_grad(GaussBackwardArgs a, ViewGrad
     dm.x += viewm[2] * r.ddep;
     dm.y += viewm[6] * r.ddep;
     dm.z += viewm[10] * r.ddep;
-    const float f[GSR_GRAD_FIELDS2] = {dm.x,  dm.y,  dm.z,  dcv[0], dcv[1], dcv[2], dcv[3], dcv[4], dcv[5],
-                                       r.dcr, r.dcg, r.dcbl, r.dop, __uint_as_float(clamp_bits), r.dr2, r.dg2, r.db2};
+    // record fields: dmean3D (3), dcov3D (6), raw dcolor (3), dopacity, SH clamp bits, [second colour (3)]
+    const float f[GSR_REC_STRIDE2] = {dm.x,   dm.y,  dm.z,  dcv[0], dcv[1], dcv[2], dcv[3],
+                                      dcv[4], dcv[5], r.dcr, r.dcg,  r.dcbl, r.dop,  __uint_as_float(clamp_bits),
+                                      r.dr2,  r.dg2, r.db2, 0.f,   0.f,    0.f};
 #pragma unroll
-    for (int k = 0; k < NF; ++k) rec[(size_t)k * a.P] = f[k];
+    for (int q = 0; q < RS / 4; ++q) rec[q] = make_float4(f[4 * q], f[4 * q + 1], f[4 * q + 2], f[4 * q + 3]);
   }
 }
 
@@ -433,26 +440,29 @@ __global__ __launch_bounds__(256) void k_gauss_accum(GaussBackwardArgs a, AccumA
       }
     }
     const float* sh_row = has_sh ? s_sh + t * S : nullptr;
-    // the views' records (written for every (view, Gaussian), zeros when culled) stream through three
-    // register buffers: while one view's SH backward runs, the next two views' loads are in flight
-    // (the accumulators hold this kernel to 2 waves per SIMD, so the loads in flight come from depth)
-    // buffer loads: one per-lane byte offset for every field and view, the view's base and the field
-    // offset in scalars (no per-load address registers to recycle while loads are in flight)
-    const int lane_off = idx * 4;
-    const int field_bytes = a.P * 4;
-    const int nf = b.dcolors2 ? GSR_GRAD_FIELDS2 : GSR_GRAD_FIELDS;  // record stride (fields) per view
-    auto load = [&](float* f, int& rad, int vl) {
-      const auto rr = __builtin_amdgcn_make_buffer_rsrc((void*)(b.radii + (size_t)(b.v0 + vl) * a.P), 0,
-                                                        field_bytes, 0x00020000);
-      rad = (int)__builtin_amdgcn_raw_buffer_load_b32(rr, lane_off, 0, 0);
-      const auto rv = __builtin_amdgcn_make_buffer_rsrc((void*)(b.vrec + (size_t)vl * nf * a.P), 0,
-                                                        GSR_GRAD_FIELDS * field_bytes, 0x00020000);
-#pragma unroll
-      for (int k = 0; k < GSR_GRAD_FIELDS; ++k)
-        f[k] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rv, lane_off, k * field_bytes, 0));
+    // The group's reached views of this Gaussian (reach bits, k_render_bwd): only their records exist.
+    // They stream through three register buffers in view order: while one view's SH backward runs, the
+    // next two views' records (16-byte loads of the whole slot) are in flight (the accumulators hold this
+    // kernel to 2 waves per SIMD, so the loads in flight come from depth).
+    const int RS = b.dcolors2 ? GSR_REC_STRIDE2 : GSR_REC_STRIDE;
+    float d2[3] = {0.f, 0.f, 0.f};  // two colours: the second colour's sums
+    if (b.dcolors2 && acc)
+      for (int k = 0; k < 3; ++k) d2[k] = b.dcolors2[3 * idx + k];
+    unsigned long long pending = b.reach[idx];
+    auto next_view = [&]() -> int {
+      if (pending == 0ull) return -1;
+      const int v = __builtin_ctzll(pending);
+      pending &= pending - 1ull;
+      return v;
     };
-    auto process = [&](const float* f, int rad, int vl) {
-      if (rad <= 0) return;
+    auto load = [&](float4 (&f)[4], int vl) {
+      const float4* src = reinterpret_cast<const float4*>(b.vrec + ((size_t)vl * a.P + idx) * RS);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) f[q] = src[q];
+    };
+    auto process = [&](const float4 (&f4)[4], int vl) {
+      const float f[16] = {f4[0].x, f4[0].y, f4[0].z, f4[0].w, f4[1].x, f4[1].y, f4[1].z, f4[1].w,
+                           f4[2].x, f4[2].y, f4[2].z, f4[2].w, f4[3].x, f4[3].y, f4[3].z, f4[3].w};
       dmean.x += f[0];
       dmean.y += f[1];
       dmean.z += f[2];
@@ -462,6 +472,11 @@ __global__ __launch_bounds__(256) void k_gauss_accum(GaussBackwardArgs a, AccumA
       dcg += f[10];
       dcb += f[11];
       dop += f[12];
+      if (b.dcolors2) {
+        d2[0] += f[14];
+        d2[1] += f[15];
+        d2[2] += b.vrec[((size_t)vl * a.P + idx) * RS + 16];
+      }
       // (a view whose colour gradient is zero adds nothing to dL/dSH nor, through the view direction,
       // to dL/dmean: skipped)
       if (has_sh && ((f[9] != 0.f) | (f[10] != 0.f) | (f[11] != 0.f))) {
@@ -482,27 +497,26 @@ __global__ __launch_bounds__(256) void k_gauss_accum(GaussBackwardArgs a, AccumA
         sh_backward(a.deg, a.M, shv, dsh, dRGB, mean, cpos, dmean);
       }
     };
-    float fa[GSR_GRAD_FIELDS], fb[GSR_GRAD_FIELDS], fc[GSR_GRAD_FIELDS];
-    int ra = 0, rb = 0, rc = 0;
-    // the parameter loads above complete here (vmcnt(0)), so the loop's waits count record loads only
-    __builtin_amdgcn_s_waitcnt(0x0F70);
-    if (b.V > 0) load(fa, ra, 0);
-    if (b.V > 1) load(fb, rb, 1);
-    if (b.V > 2) load(fc, rc, 2);
-    int vl = 0;
-    // (the refills are unconditional, clamped to the last view, so every path has the same loads in
-    // flight and each process waits for its own buffer only)
-    const int vlast = b.V - 1;
-    for (; vl + 2 < b.V; vl += 3) {
-      process(fa, ra, vl);
-      load(fa, ra, min(vl + 3, vlast));
-      process(fb, rb, vl + 1);
-      load(fb, rb, min(vl + 4, vlast));
-      process(fc, rc, vl + 2);
-      load(fc, rc, min(vl + 5, vlast));
+    float4 fa[4], fb[4], fc[4];
+    int va_ = next_view(), vb_ = next_view(), vc_ = next_view();
+    if (va_ >= 0) load(fa, va_);
+    if (vb_ >= 0) load(fb, vb_);
+    if (vc_ >= 0) load(fc, vc_);
+    // (buffers refill in turn, so the views are summed in ascending order, as one pass over the group)
+    for (;;) {
+      if (va_ < 0) break;
+      process(fa, va_);
+      va_ = next_view();
+      if (va_ >= 0) load(fa, va_);
+      if (vb_ < 0) break;
+      process(fb, vb_);
+      vb_ = next_view();
+      if (vb_ >= 0) load(fb, vb_);
+      if (vc_ < 0) break;
+      process(fc, vc_);
+      vc_ = next_view();
+      if (vc_ >= 0) load(fc, vc_);
     }
-    if (vl < b.V) process(fa, ra, vl);
-    if (vl + 1 < b.V) process(fb, rb, vl + 1);
     // (the sums already include the earlier groups: plain stores)
     a.dL_dmeans3D[3 * idx] = dmean.x;
     a.dL_dmeans3D[3 * idx + 1] = dmean.y;
@@ -513,17 +527,8 @@ __global__ __launch_bounds__(256) void k_gauss_accum(GaussBackwardArgs a, AccumA
       a.dL_dcolors[3 * idx + 1] = dcg;
       a.dL_dcolors[3 * idx + 2] = dcb;
     }
-    if (b.dcolors2) {
-      // two colours: the second colour's sums (zero records for culled views add nothing)
-      float d2[3] = {0.f, 0.f, 0.f};
-      if (acc)
-        for (int k = 0; k < 3; ++k) d2[k] = b.dcolors2[3 * idx + k];
-      for (int w = 0; w < b.V; ++w) {
-        const float* r2 = b.vrec + ((size_t)w * GSR_GRAD_FIELDS2 + GSR_GRAD_FIELDS) * a.P + idx;
-        for (int k = 0; k < 3; ++k) d2[k] += r2[(size_t)k * a.P];
-      }
+    if (b.dcolors2)
       for (int k = 0; k < 3; ++k) b.dcolors2[3 * idx + k] = d2[k];
-    }
     if (b.dcov_carry)
       for (int k = 0; k < 6; ++k) b.dcov_carry[6 * idx + k] = dcov[k];
     if (a.dL_dcov3D && a.dL_dcov3D != b.dcov_carry)

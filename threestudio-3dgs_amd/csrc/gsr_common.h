@@ -288,21 +288,28 @@ struct ImageState {
 #define GSR_GRAD_FIELDS 14
 #define GSR_GRAD_FIELDS2 17
 // [views of the group][fields][P] floats.
+// One (view, Gaussian) record of k_view_grad: GSR_GRAD_FIELDS floats (two colours: GSR_GRAD_FIELDS2) in a
+// 16-byte aligned slot, written and read whole (four / five 16-byte accesses).
+#define GSR_REC_STRIDE 16
+#define GSR_REC_STRIDE2 20
 struct BackwardState {
-  float4* grow;  // [3 (two colours: 4) * instances of the group]
-  float* vrec;   // [views][GSR_GRAD_FIELDS (two colours: GSR_GRAD_FIELDS2)][P]
+  unsigned long long* reach;  // [P]: bit v set = view v of the group gave the Gaussian a gradient row
+  float4* grow;               // [3 (two colours: 4) * instances of the group]
+  float* vrec;  // [views][P][GSR_REC_STRIDE (two colours: GSR_REC_STRIDE2)]; only the reached pairs' are written
+  static size_t reach_bytes(int P) { return align_up(sizeof(unsigned long long) * (size_t)(P > 0 ? P : 1), 256); }
   static size_t rows_bytes(long long K, bool two = false) {
     return align_up(sizeof(float4) * (two ? 4 : 3) * (size_t)(K > 0 ? K : 1), 256);
   }
   static size_t bytes_for(long long K, int views, int P, bool two = false) {
-    return rows_bytes(K, two) + align_up(sizeof(float) * (two ? GSR_GRAD_FIELDS2 : GSR_GRAD_FIELDS) * (size_t)views *
-                                             (size_t)(P > 0 ? P : 1),
-                                         256);
+    return reach_bytes(P) + rows_bytes(K, two) +
+           align_up(sizeof(float) * (two ? GSR_REC_STRIDE2 : GSR_REC_STRIDE) * (size_t)views * (size_t)(P > 0 ? P : 1),
+                    256);
   }
-  static BackwardState carve(void* base, long long K, bool two = false) {
+  static BackwardState carve(void* base, long long K, int P, bool two = false) {
     BackwardState s;
-    s.grow = (float4*)base;
-    s.vrec = (float*)((char*)base + rows_bytes(K, two));
+    s.reach = (unsigned long long*)base;
+    s.grow = (float4*)((char*)base + reach_bytes(P));
+    s.vrec = (float*)((char*)s.grow + rows_bytes(K, two));
     return s;
   }
 };

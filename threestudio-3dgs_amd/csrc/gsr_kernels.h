@@ -88,18 +88,17 @@ struct ViewGradArgs {
   int V, v0, W, H, gx, tiles, cut_in_lds, pad_;
   GeomState g;
   ImageState img;
-  const int* radii;        // the set's (V, P)
+  const unsigned long long* reach;  // [P] reach bits of this group's views (k_render_bwd)
   const float4* grow;      // gradient rows of this group of views
   float* dmeans2D;         // the set's (V, P, 3)
-  float* vrec;             // [V][GSR_GRAD_FIELDS][P] records of this group
+  float* vrec;             // [V][P][GSR_REC_STRIDE(2)] records of this group (reached pairs only)
   uint32_t row_start[GSR_SET_MAX];
   ViewCam cam[GSR_SET_MAX];
 };
 // B: per Gaussian, sums the group's records, SH backward per view, scale / rotation once.
 struct AccumArgs {
   int V, v0, accumulate, pad_;
-  const GaussRec* rec;      // the set's (V, P) records (SH clamp flags in d.w)
-  const int* radii;         // the set's (V, P)
+  const unsigned long long* reach;  // [P] reach bits of this group's views: the records to read
   const float* vrec;
   // running dL/dcov3D over the groups / sets already summed (P x 6; the dL_dcov3D output itself when the
   // caller wants it): with accumulate, every sum continues from the stored value in view order, so a

@@ -692,7 +692,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(TWO ? 4 : 5
                                                     const float* __restrict__ dL_dcolor,
                                                     const float* __restrict__ dL_ddepth,
                                                     const float* __restrict__ dL_dalpha,
-                                                    float4* __restrict__ grow) {
+                                                    float4* __restrict__ grow,
+                                                    unsigned long long* __restrict__ reach) {
   __shared__ BwdLDS<TWO> s;
   constexpr int NG = TWO ? NGV2 : NGV;                           // raw sums per (candidate, quadrant)
   constexpr int QS = TWO ? GSR_QSUM_STRIDE2 : GSR_QSUM_STRIDE;  // per candidate
@@ -807,6 +808,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(TWO ? 4 : 5
   float4 npc2 = zero4;  // two colours: piece 2's thread also moves the second colour
   uint32_t ngo = 0u;
   uint32_t gi_next = 0u;
+  // this view's reach bit (staged candidates have rows): word v >> 5 of the Gaussian's 64 bits
+  unsigned int* const reach32 = reinterpret_cast<unsigned int*>(reach) + (v >> 5);
+  const unsigned int vbit = 1u << (v & 31);
   if (maxc > 0) {
     const uint32_t g0 = fetch_index(maxc);
     if (maxc - 1 - cs >= 0) {
@@ -817,7 +821,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(TWO ? 4 : 5
         else  // the second rasterizer call's colours replace the first's
           npc = make_float4(rs.col2[3 * g0], rs.col2[3 * g0 + 1], rs.col2[3 * g0 + 2], 0.f);
       }
-      if (piece == 3) ngo = goff[g0];
+      if (piece == 3) {
+        ngo = goff[g0];
+        atomicOr(reach32 + 2 * g0, vbit);  // the Gaussian gets a row in this view (k_view_grad reads it)
+      }
     }
     if (maxc > 64) gi_next = fetch_index(maxc - 64);
   }
@@ -984,7 +991,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(TWO ? 4 : 5
             else
               npc = c2;
           }
-          if (piece == 3) ngo = goff[gi_next];
+          if (piece == 3) {
+            ngo = goff[gi_next];
+            atomicOr(reach32 + 2 * gi_next, vbit);
+          }
         }
         if (hi > 128) gi_next = fetch_index(hi - 128);
       }
@@ -1197,12 +1207,12 @@ void launch_render_backward(const RenderSet& rs, const GeomState& g, const uint3
     hipLaunchKernelGGL(k_render_bwd<true>, grid, dim3(256), 0, stream, rs, (const uint2*)img.ranges,
                        (const uint32_t*)img.quad_maxc, sorted_gauss, (const GaussRec*)g.rec,
                        (const uint32_t*)g.goff, (const float*)img.final_T, (const uint32_t*)img.n_contrib,
-                       dL_dcolor, dL_ddepth, dL_dalpha, bw.grow);
+                       dL_dcolor, dL_ddepth, dL_dalpha, bw.grow, bw.reach);
   else
     hipLaunchKernelGGL(k_render_bwd<false>, grid, dim3(256), 0, stream, rs, (const uint2*)img.ranges,
                        (const uint32_t*)img.quad_maxc, sorted_gauss, (const GaussRec*)g.rec,
                        (const uint32_t*)g.goff, (const float*)img.final_T, (const uint32_t*)img.n_contrib,
-                       dL_dcolor, dL_ddepth, dL_dalpha, bw.grow);
+                       dL_dcolor, dL_ddepth, dL_dalpha, bw.grow, bw.reach);
 }
 
 }  // namespace gsr
