@@ -1,13 +1,14 @@
 // gsr_backward.hip — per-Gaussian backward of a view set.
 //
 // Two launches per group of views:
-//   A. k_view_grad, one thread per (view, Gaussian): gather-sum of the Gaussian's per-instance
-//      gradient rows written by k_render_bwd (fixed order -> bitwise reproducible), with the tile
-//      cut-offs of the view staged in LDS so the ~92 % of instances no pixel reached cost one LDS
-//      read each; then BACKWARD::computeCov2DCUDA (conic -> 2D cov -> 3D cov and camera-space mean)
-//      and the projection / view-depth part of BACKWARD::preprocessCUDA [EXT].  Writes the view's
-//      means2D gradient and a 13-float record (dmean3D, dcov3D, raw dcolor, dopacity).
-//   B. k_gauss_accum, one thread per Gaussian: streams its records over the group's views, runs the
+//   A. k_view_grad, per (view, Gaussian) of the Gaussians the view's blend reached (reach bits set by
+//      k_render_bwd; the others only get their zero means2D gradient): gather-sum of the Gaussian's
+//      per-instance gradient rows written by k_render_bwd (fixed order -> bitwise reproducible), with the
+//      tile cut-offs of the view staged in LDS so the instances no pixel reached cost one LDS read each;
+//      then BACKWARD::computeCov2DCUDA (conic -> 2D cov -> 3D cov and camera-space mean) and the
+//      projection / view-depth part of BACKWARD::preprocessCUDA [EXT].  Writes the view's means2D
+//      gradient and a 64-byte record slot (dmean3D, dcov3D, raw dcolor, dopacity, SH clamp bits).
+//   B. k_gauss_accum, one thread per Gaussian: streams its reached views' records, runs the
 //      SH -> RGB backward (incl. the view-direction term) per view with dL/dSH accumulated in
 //      registers, then 3D cov -> scale and (unnormalised) quaternion once (linear in dL/dcov3D).
 // Splitting at the view boundary keeps A light (≈70 VGPRs, thousands of waves in flight to hide the
@@ -17,6 +18,7 @@
 // w.r.t. scale_modifier * scale.
 #include "gsr_kernels.h"
 #include "gsr_math.h"
+#include "gsr_wave.h"
 
 namespace gsr {
 
@@ -309,41 +311,57 @@ __global__ __launch_bounds__(256) void k_view_grad(GaussBackwardArgs a, ViewGrad
   constexpr int RS = TWO ? GSR_REC_STRIDE2 : GSR_REC_STRIDE;
   float4* recv = reinterpret_cast<float4*>(va.vrec + (size_t)vl * RS * a.P);
   const unsigned long long vbit = 1ull << vl;
-  // Only the Gaussians this view's blend gave a gradient row (reach bit, set by k_render_bwd; ~15 % of a
+  // Only the Gaussians this view's blend gave a gradient row (reach bit, set by k_render_bwd; ~20 % of a
   // view at 1M) are loaded and get a record; the others write their zero means2D gradient only
-  // (k_gauss_accum reads the reached records only).  The next item's reach bit and record are loaded
-  // while the current one is processed.
-  const int idx_base = a.g0 + (blockIdx.x / va.V) * (256 * GSR_VG_ITEMS) + t;
-  bool nreach = false;
-  GaussRec nrec;
-  uint32_t ngo = 0u;
-  if (idx_base < a.g1) {
-    nreach = (va.reach[idx_base] & vbit) != 0ull;
-    if (nreach) {
-      const size_t o0 = (size_t)vg * a.P + idx_base;
-      nrec = va.g.rec[o0], ngo = va.g.goff[o0];
-    }
-  }
-#pragma unroll 1
+  // (k_gauss_accum reads the reached records only).  Pass 1: each wave reads the reach bits of its 1024
+  // items (16 per lane, 256 apart), zeroes the unreached ones' means2D gradient and lists the reached ones
+  // in LDS; pass 2: the wave's lanes take the listed items in turn, so a wave walks ~4 dense rounds of
+  // gathers and chain rules instead of 16 sparse ones.  The next listed item's record is loaded while the
+  // current one is processed.
+  __shared__ uint16_t s_list[4][64 * GSR_VG_ITEMS];
+  const int wave = t >> 6, lane = t & 63;
+  uint16_t* list = s_list[wave];
+  const int slice = a.g0 + (blockIdx.x / va.V) * (256 * GSR_VG_ITEMS);
+  int cnt = 0;  // wave-uniform
+#pragma unroll
   for (int it = 0; it < GSR_VG_ITEMS; ++it) {
-    const int idx = idx_base + it * 256;
-    if (idx >= a.g1) break;
-    const size_t o = (size_t)vg * a.P + idx;
-    const bool has_rows = nreach;
-    const GaussRec gr = nrec;
-    const uint32_t go = ngo;
-    if (it + 1 < GSR_VG_ITEMS && idx + 256 < a.g1) {
-      nreach = (va.reach[idx + 256] & vbit) != 0ull;
-      if (nreach) nrec = va.g.rec[o + 256], ngo = va.g.goff[o + 256];
-    }
-    float* m2 = va.dmeans2D + 3 * o;
-    float4* rec = recv + (size_t)idx * (RS / 4);
-    if (!has_rows) {
+    const int local = it * 256 + t;
+    const int idx = slice + local;
+    const bool valid = idx < a.g1;
+    const bool rch = valid && (va.reach[idx] & vbit) != 0ull;
+    if (valid && !rch) {
+      float* m2 = va.dmeans2D + 3 * ((size_t)vg * a.P + idx);
       m2[0] = 0.f;
       m2[1] = 0.f;
       m2[2] = 0.f;
-      continue;
     }
+    const unsigned long long bal = __ballot(rch);
+    if (rch) list[cnt + mask_rank(bal)] = (uint16_t)local;
+    cnt += __popcll(bal);
+  }
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the wave's own list, read back by its lanes
+  GaussRec nrec;
+  uint32_t ngo = 0u;
+  int nidx = 0;
+  if (lane < cnt) {
+    nidx = slice + list[lane];
+    const size_t o0 = (size_t)vg * a.P + nidx;
+    nrec = va.g.rec[o0], ngo = va.g.goff[o0];
+  }
+#pragma unroll 1
+  for (int i = lane; i - lane < cnt; i += 64) {
+    if (i >= cnt) break;
+    const int idx = nidx;
+    const size_t o = (size_t)vg * a.P + idx;
+    const GaussRec gr = nrec;
+    const uint32_t go = ngo;
+    if (i + 64 < cnt) {
+      nidx = slice + list[i + 64];
+      const size_t on = (size_t)vg * a.P + nidx;
+      nrec = va.g.rec[on], ngo = va.g.goff[on];
+    }
+    float* m2 = va.dmeans2D + 3 * o;
+    float4* rec = recv + (size_t)idx * (RS / 4);
     const uint32_t clamp_bits = gr.d.w;
     const RowSums r = gather_rows<TWO>((uint32_t)idx, gr, go, va.gx, cut, grow);
     // rows that sum to zero (no pixel of the staged tiles kept the Gaussian): a zero record without the
