@@ -652,7 +652,7 @@ static int set_backward(int V, int P, int degree, int M, const int* K, int width
     va.gx = gx;
     va.tiles = gx * gy;
     va.cut_in_lds = 0;
-    va.pad_ = 0;
+    va.items = 0;
     va.g = g;
     va.img = img;
     va.reach = bw.reach;

@@ -321,13 +321,14 @@ __global__ __launch_bounds__(256) void k_view_grad(GaussBackwardArgs a, ViewGrad
   __shared__ uint16_t s_list[4][64 * GSR_VG_ITEMS];
   const int wave = t >> 6, lane = t & 63;
   uint16_t* list = s_list[wave];
-  const int slice = a.g0 + (blockIdx.x / va.V) * (256 * GSR_VG_ITEMS);
+  const int items = va.items;  // per thread (<= GSR_VG_ITEMS; fewer for launches of few views)
+  const int slice = a.g0 + (blockIdx.x / va.V) * (256 * items);
   int cnt = 0;  // wave-uniform
 #pragma unroll
   for (int it = 0; it < GSR_VG_ITEMS; ++it) {
     const int local = it * 256 + t;
     const int idx = slice + local;
-    const bool valid = idx < a.g1;
+    const bool valid = it < items && idx < a.g1;  // (it < items: uniform)
     const bool rch = valid && (va.reach[idx] & vbit) != 0ull;
     if (valid && !rch) {
       float* m2 = va.dmeans2D + 3 * ((size_t)vg * a.P + idx);
@@ -425,16 +426,58 @@ __global__ __launch_bounds__(256) void k_gauss_accum(GaussBackwardArgs a, AccumA
   const bool has_sh = a.shs != nullptr && F > 0;
   const bool acc = b.accumulate != 0;
   const float invF = has_sh ? 1.0f / (float)F : 0.0f;
+  // Only the Gaussians some view of the group reached (reach bits) have records; the others keep their sums
+  // (accumulate: nothing read or written) or get zero outputs.  The block's reached SH rows are staged in
+  // LDS (a list of the reached rows, each row read by consecutive threads), its dL/dSH rows stored from LDS
+  // with coalesced writes (all rows, zeros included; with accumulate only the reached rows).
+  __shared__ uint8_t s_rl[256];
+  __shared__ int s_wcnt[4];
+  const unsigned long long reach_word = idx < a.g1 ? b.reach[idx] : 0ull;
+  const bool reached = reach_word != 0ull;
+  int nr = 0;  // reached rows of the block
   if (has_sh) {
-    const float* src = a.shs + (size_t)block0 * F;
-    const int cnt = nblk * F;
+    const unsigned long long bal = __ballot(reached);
+    const int w = t >> 6;
+    if ((t & 63) == 0) s_wcnt[w] = (int)__popcll(bal);
+    __syncthreads();
+    int base = 0;
+    for (int k = 0; k < 4; ++k) {
+      base += k < w ? s_wcnt[k] : 0;
+      nr += s_wcnt[k];
+    }
+    if (reached) s_rl[base + mask_rank(bal)] = (uint8_t)t;
+    __syncthreads();
+    const int cnt = nr * F;
     for (int e = t; e < cnt; e += 256) {
-      const int te = (int)(((float)e + 0.5f) * invF);
-      s_sh[te * S + (e - te * F)] = src[e];
+      const int r = (int)(((float)e + 0.5f) * invF);
+      const int tl = s_rl[r];
+      const int k = e - r * F;
+      s_sh[tl * S + k] = a.shs[(size_t)(block0 + tl) * F + k];
     }
     __syncthreads();
   }
-  if (idx < a.g1) {
+  if (idx < a.g1 && !reached) {
+    if (!acc) {
+      for (int k = 0; k < 3; ++k) a.dL_dmeans3D[3 * idx + k] = 0.f;
+      a.dL_dopacity[idx] = 0.f;
+      if (a.dL_dcolors)
+        for (int k = 0; k < 3; ++k) a.dL_dcolors[3 * idx + k] = 0.f;
+      if (b.dcolors2)
+        for (int k = 0; k < 3; ++k) b.dcolors2[3 * idx + k] = 0.f;
+      if (b.dcov_carry)
+        for (int k = 0; k < 6; ++k) b.dcov_carry[6 * idx + k] = 0.f;
+      if (a.dL_dcov3D && a.dL_dcov3D != b.dcov_carry)
+        for (int k = 0; k < 6; ++k) a.dL_dcov3D[6 * idx + k] = 0.f;
+      if (!a.cov3D_precomp && a.dL_dscales) {
+        for (int k = 0; k < 3; ++k) a.dL_dscales[3 * idx + k] = 0.f;
+        for (int k = 0; k < 4; ++k) a.dL_drotations[4 * idx + k] = 0.f;
+      }
+      if (has_sh) {
+        float* row = s_sh + t * S;
+        for (int k = 0; k < F; ++k) row[k] = 0.f;
+      }
+    }
+  } else if (idx < a.g1) {
     const float3 mean = make_float3(a.means3D[3 * idx], a.means3D[3 * idx + 1], a.means3D[3 * idx + 2]);
     float3 dmean = make_float3(0.f, 0.f, 0.f);
     float dcov[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
@@ -466,7 +509,7 @@ __global__ __launch_bounds__(256) void k_gauss_accum(GaussBackwardArgs a, AccumA
     float d2[3] = {0.f, 0.f, 0.f};  // two colours: the second colour's sums
     if (b.dcolors2 && acc)
       for (int k = 0; k < 3; ++k) d2[k] = b.dcolors2[3 * idx + k];
-    unsigned long long pending = b.reach[idx];
+    unsigned long long pending = reach_word;
     auto next_view = [&]() -> int {
       if (pending == 0ull) return -1;
       const int v = __builtin_ctzll(pending);
@@ -574,12 +617,21 @@ __global__ __launch_bounds__(256) void k_gauss_accum(GaussBackwardArgs a, AccumA
   }
   if (has_sh) {
     __syncthreads();
-    float* dst = a.dL_dsh + (size_t)block0 * F;
-    const int cnt = nblk * F;
-    for (int e = t; e < cnt; e += 256) {
-      const int te = (int)(((float)e + 0.5f) * invF);
-      const float x = s_sh[te * S + (e - te * F)];
-      dst[e] = x;
+    if (!acc) {
+      float* dst = a.dL_dsh + (size_t)block0 * F;
+      const int cnt = nblk * F;
+      for (int e = t; e < cnt; e += 256) {
+        const int te = (int)(((float)e + 0.5f) * invF);
+        dst[e] = s_sh[te * S + (e - te * F)];
+      }
+    } else {
+      const int cnt = nr * F;
+      for (int e = t; e < cnt; e += 256) {
+        const int r = (int)(((float)e + 0.5f) * invF);
+        const int tl = s_rl[r];
+        const int k = e - r * F;
+        a.dL_dsh[(size_t)(block0 + tl) * F + k] = s_sh[tl * S + k];
+      }
     }
   }
 }
@@ -592,12 +644,14 @@ void launch_gauss_backward(const GaussBackwardArgs& a, ViewGradArgs va, const Ac
   if (n <= 0 || va.V <= 0) return;
   const size_t cut_bytes = sizeof(uint2) * (size_t)va.tiles;
   va.cut_in_lds = cut_bytes <= GSR_CUT_LDS_MAX ? 1 : 0;
+  // items per thread: GSR_VG_ITEMS, halved (down to 2) while the launch would have fewer than 1024 blocks
+  va.items = GSR_VG_ITEMS;
+  while (va.items > 2 && (long long)va.V * div_up(n, 256 * va.items) < 1024) va.items >>= 1;
+  const dim3 vg_grid(va.V * div_up(n, 256 * va.items));
   if (b.dcolors2)
-    hipLaunchKernelGGL(k_view_grad<true>, dim3(va.V * div_up(n, 256 * GSR_VG_ITEMS)), dim3(256),
-                       va.cut_in_lds ? cut_bytes : 0, stream, a, va);
+    hipLaunchKernelGGL(k_view_grad<true>, vg_grid, dim3(256), va.cut_in_lds ? cut_bytes : 0, stream, a, va);
   else
-    hipLaunchKernelGGL(k_view_grad<false>, dim3(va.V * div_up(n, 256 * GSR_VG_ITEMS)), dim3(256),
-                       va.cut_in_lds ? cut_bytes : 0, stream, a, va);
+    hipLaunchKernelGGL(k_view_grad<false>, vg_grid, dim3(256), va.cut_in_lds ? cut_bytes : 0, stream, a, va);
   const size_t lds = (a.shs && a.M > 0) ? (size_t)256 * sh_lds_stride(a.M) * sizeof(float) : 0;
   hipLaunchKernelGGL(k_gauss_accum, dim3(div_up(n, 256)), dim3(256), lds, stream, a, b);
 }

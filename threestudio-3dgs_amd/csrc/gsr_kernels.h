@@ -85,7 +85,7 @@ struct GaussBackwardArgs {  // shared Gaussian parameters and the gradients of t
 };
 // A: per (view, Gaussian) gather + screen-space chain rule for views v0 .. v0+V-1 of a set.
 struct ViewGradArgs {
-  int V, v0, W, H, gx, tiles, cut_in_lds, pad_;
+  int V, v0, W, H, gx, tiles, cut_in_lds, items;  // items: Gaussians per thread (launch_gauss_backward)
   GeomState g;
   ImageState img;
   const unsigned long long* reach;  // [P] reach bits of this group's views (k_render_bwd)

@@ -294,8 +294,10 @@ def rasterize_gaussians_backward(bg, means3D, radii, colors, scales, rotations, 
     dL_dopacity = torch.zeros((P, 1), **fopt) if P == 0 else torch.empty((P, 1), **fopt)
     dL_dcov3D = torch.zeros((P, 6), **fopt) if P == 0 else torch.empty((P, 6), **fopt)
     dL_dsh = torch.zeros((P, M, 3), **fopt) if (P == 0 or M == 0) else torch.empty((P, M, 3), **fopt)
-    dL_dscales = torch.zeros((P, 3), **fopt)
-    dL_drotations = torch.zeros((P, 4), **fopt)
+    # (written whole by the kernels unless cov3D_precomp replaces scales / rotations)
+    pre = cov3D_precomp is not None and cov3D_precomp.numel() > 0
+    dL_dscales = torch.zeros((P, 3), **fopt) if (P == 0 or pre) else torch.empty((P, 3), **fopt)
+    dL_drotations = torch.zeros((P, 4), **fopt) if (P == 0 or pre) else torch.empty((P, 4), **fopt)
     if P == 0:
         return dL_dmeans2D, dL_dcolors, dL_dopacity, dL_dmeans3D, dL_dcov3D, dL_dsh, dL_dscales, dL_drotations
 
