@@ -78,6 +78,11 @@ def parse():
                          "per-Gaussian backward forms them (view_shard.ChunkedGradReduce, overlapped on a side "
                          "stream) instead of one flat all-reduce after it")
     ap.add_argument("--grad-chunks", type=int, default=4, help="Gaussian ranges of the overlapped reduction")
+    ap.add_argument("--gather", choices=["overlap", "sync"], default="overlap",
+                    help="N > 1: the image all-gather runs asynchronously beside the backward (overlap: the step's "
+                         "loss decomposes over views — fixed per-view upstream gradients, as MVDream's per-group "
+                         "guidance with group-aligned shards — so a view's gradient needs only its own rank's "
+                         "image; the gathered batch is awaited before the step ends) or before it (sync)")
     ap.add_argument("--per-view-views", type=int, default=16,
                     help="views of the drop-in per-view path (one GaussianRasterizer call per view, the "
                          "reference's loop) timed after the headline, reported beside it (0 = skip)")
@@ -514,7 +519,8 @@ def main():
 
     import gsr_synthetic as gs
     from diff_gaussian_rasterization import _C
-    from diff_gaussian_rasterization.view_shard import ChunkedGradReduce, all_gather_views, allreduce_grads, shard_range
+    from diff_gaussian_rasterization.view_shard import (ChunkedGradReduce, all_gather_views, all_gather_views_async,
+                                                        allreduce_grads, shard_range)
 
     global GRAD_REDUCE
     overlap = world > 1 and args.overlap_reduce == "on" and args.path == "batched" and args.views >= world \
@@ -557,19 +563,27 @@ def main():
         shade = shading_inputs(mine, device)
         up_n = torch.randn((len(mine), 3, H, W), generator=gen, device=device)
 
+    pending = []
+
+    def gather(img):
+        # forward exchange: every rank receives the whole batch of rendered images (the composited RGB the
+        # batch renderer returns; depth / alpha terms are per view)
+        if args.gather == "overlap":
+            pending.append(all_gather_views_async(img, args.views))
+        else:
+            all_gather_views(img, args.views)
+
     def step():
         if args.workload == "sugar":
             outs = render_views_sugar(rep, settings, shade)
             if world > 1:
-                all_gather_views(outs[0], args.views)
+                gather(outs[0])
             torch.autograd.backward(outs, (up_c, up_d, up_a, up_n, up_n))
         elif args.path == "batched":
             outs = render_views(rep, settings, bg_img, shade)
             c, d, a = outs[:3]
             if world > 1:
-                # forward exchange: every rank receives the whole batch of rendered images (the
-                # composited RGB a batch-level loss consumes; depth / alpha terms are per view)
-                all_gather_views(c, args.views)
+                gather(c)
             # the loss's gradient w.r.t. the rendered images is injected as fixed upstream gradients
             if shade is None:
                 torch.autograd.backward((c, d, a), (up_c, up_d, up_a))
@@ -580,13 +594,15 @@ def main():
                                 None if shade is None else tuple(t[i] for t in shade))
                     for i, cam in enumerate(mine)]
             if world > 1:
-                all_gather_views(torch.stack([o[0] for o in outs]), args.views)
+                gather(torch.stack([o[0] for o in outs]))
             ts = [t for o in outs for t in o[:3]]
             gs_ = [t for g in upstream for t in g]
             if shade is not None:
                 ts += [o[4] for o in outs]
                 gs_ += list(up_n)
             torch.autograd.backward(ts, gs_)
+        while pending:  # the overlapped gather completes within the step
+            pending.pop().wait()
         if GRAD_REDUCE is None:
             allreduce_grads(rep.params)  # one flat RCCL all-reduce of the Gaussian parameter gradients
         # (else the rasterizer's backward summed them over ranks range by range, overlapped with it)
@@ -656,7 +672,8 @@ def main():
                         "gradient all-reduce",
             "n_gaussians": args.gaussians, "resolution": [H, W], "sh_degree": args.sh_degree,
             "global_views_per_step": args.views, "views_per_rank": per,
-            "parallelism": (f"views sharded over {world} rank(s) ({comm} all-gather of the images, " + (
+            "parallelism": (f"views sharded over {world} rank(s) ({comm} all-gather of the images" + (
+                " overlapped with the backward, " if args.gather == "overlap" else " before the backward, ") + (
                 f"all-reduce of the Gaussian gradients in {args.grad_chunks} ranges overlapped with the "
                 "per-Gaussian backward)" if GRAD_REDUCE is not None else "in-place all-reduce of the Gaussian "
                 "gradients)") if world > 1 else "1 rank, no collectives"),

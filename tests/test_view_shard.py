@@ -374,3 +374,33 @@ def test_chunked_reduce_equals_flat(tmp_path):
         z = np.load(tmp_path / f"chunk{rank}.npz")
         for i in range(4):
             np.testing.assert_array_equal(z[f"a{i}"], z[f"b{i}"])
+
+
+def _async_gather_worker(rank, world, port, tmp, batch):
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
+    try:
+        from diff_gaussian_rasterization.view_shard import all_gather_views, all_gather_views_async
+
+        lo, hi = shard_range(batch, world, rank)
+        local = (torch.arange(lo, hi, dtype=torch.float32)[:, None, None] * 10.0
+                 + torch.arange(6, dtype=torch.float32).reshape(1, 2, 3)).requires_grad_(True)
+        pending = all_gather_views_async(local, batch)
+        sync = all_gather_views(local, batch)
+        out = pending.wait()
+        np.save(os.path.join(tmp, f"async{rank}.npy"), out.numpy())
+        np.save(os.path.join(tmp, f"sync{rank}.npy"), sync.detach().numpy())
+        assert not out.requires_grad
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,batch", [(2, 8), (3, 7)])
+def test_async_gather_equals_sync(world, batch, tmp_path):
+    """all_gather_views_async (the bench's gather overlapped with the backward) returns the same batch as the
+    synchronous all_gather_views, for even and uneven shards."""
+    mp.spawn(_async_gather_worker, args=(world, _free_port(), str(tmp_path), batch), nprocs=world, join=True)
+    want = (np.arange(batch, dtype=np.float32)[:, None, None] * 10.0
+            + np.arange(6, dtype=np.float32).reshape(1, 2, 3))
+    for r in range(world):
+        np.testing.assert_array_equal(np.load(tmp_path / f"async{r}.npy"), want)
+        np.testing.assert_array_equal(np.load(tmp_path / f"sync{r}.npy"), want)

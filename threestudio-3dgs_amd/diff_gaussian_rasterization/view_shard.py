@@ -89,6 +89,56 @@ def all_gather_views(local: torch.Tensor, batch_size: int, group=None) -> torch.
     return _GatherViews.apply(local, batch_size, group)
 
 
+class PendingGather:
+    """An all-gather of view slices in flight (all_gather_views_async): wait() returns the (batch_size, ...)
+    tensor, a constant (no autograd history), after making the current stream wait for the collective."""
+
+    def __init__(self, work, finish):
+        self._work, self._finish, self._out = work, finish, None
+
+    def wait(self) -> torch.Tensor:
+        if self._out is None:
+            if self._work is not None:
+                self._work.wait()
+            self._out = self._finish()
+        return self._out
+
+
+def all_gather_views_async(local: torch.Tensor, batch_size: int, group=None) -> PendingGather:
+    """all_gather_views launched asynchronously (RCCL runs it on its own stream once `local` is ready, beside
+    whatever the caller enqueues next).  For a loss that decomposes over views (or over groups of views
+    rendered on one rank, e.g. MVDream's 4-view guidance groups with group-aligned shards), each view's
+    gradient needs only its own rank's image, so the gather of the full batch (the batch renderer's output
+    contract) can overlap the backward; the gathered batch carries no gradient.  Same values as
+    all_gather_views."""
+    world, rank = _world()
+    if world == 1:
+        out = local.detach()
+        return PendingGather(None, lambda: out)
+    counts = [shard_range(batch_size, world, r) for r in range(world)]
+    n_max = max(b - a for a, b in counts)
+    even = all(b - a == n_max for a, b in counts)
+    src = local.detach().contiguous()
+    if dist.get_backend(group) == "nccl" and even:
+        out = local.new_empty((batch_size,) + tuple(local.shape[1:]))
+        work = dist.all_gather_into_tensor(out, src, group=group, async_op=True)
+        return PendingGather(work, lambda: out)
+    pad = local.new_zeros((n_max,) + tuple(local.shape[1:]))
+    pad[: local.shape[0]] = src
+    if dist.get_backend(group) == "nccl":
+        buf = local.new_empty((world * n_max,) + tuple(local.shape[1:]))
+        work = dist.all_gather_into_tensor(buf, pad, group=group, async_op=True)
+        parts = None
+
+        def finish():
+            ps = list(buf.split(n_max))
+            return torch.cat([ps[r][: b - a] for r, (a, b) in enumerate(counts)], 0)
+        return PendingGather(work, finish)
+    parts = [torch.empty_like(pad) for _ in range(world)]
+    work = dist.all_gather(parts, pad, group=group, async_op=True)
+    return PendingGather(work, lambda: torch.cat([parts[r][: b - a] for r, (a, b) in enumerate(counts)], 0))
+
+
 def _contiguous_span(grads):
     """The tensors as one 1-D view when they tile a gap-free range of a single storage (in any order,
     same dtype and device, each contiguous, no overlaps), else None."""
