@@ -229,7 +229,7 @@ def render_views_sugar(rep: Replica, settings, shade):
     the face normals as colors_precomp and a fresh zero means2D (no viewspace gradient, :179-189); then
     normalize, flip x/y, normal map and the alpha > 0.99 gradient masks in torch (:190-197)."""
     from diff_gaussian_rasterization.batched import rasterize_views
-    from diff_gaussian_rasterization.shading import depth_normal_views
+    from diff_gaussian_rasterization.shading import depth_normal_views, sugar_normal_map
 
     P = rep.means3D.shape[0]
     dev = rep.means3D.device
@@ -251,11 +251,7 @@ def render_views_sugar(rep: Replica, settings, shade):
                                                              grad_reduce=GRAD_REDUCE)
     rays_o, rays_d, _ = shade
     _, nmap_dist = depth_normal_views(depth, alpha, rays_o, rays_d)
-    normal = torch.nn.functional.normalize(normal, dim=1)
-    normal = torch.cat([-normal[:, :2], normal[:, 2:]], 1)
-    nmap = normal * 0.5 * alpha + 0.5
-    mask = (alpha > 0.99).expand_as(nmap)
-    nmap = torch.where(mask, nmap, nmap.detach())
+    nmap = sugar_normal_map(normal, alpha)  # normalize, flip x / y, alpha-weighted map, alpha > 0.99 mask (fused)
     depth = torch.where(alpha > 0.99, depth, depth.detach())
     return color.clamp(0, 1), depth, alpha, nmap, nmap_dist
 

@@ -312,6 +312,18 @@ int gsr_composite_backward(int V, int height, int width, const float* dL_dout, c
                            float* dL_dbg, void* stream);
 
 /*
+ * SuGaR normal map (replaces the torch lines of renderer/diff_sugar_rasterizer_normal.py:192-197 after the
+ * second rasterizer call): normal (V, 3, H, W) = the blended face normals, alpha (V, 1, H, W);
+ *   out = (-u_x, -u_y, u_z) * 0.5 * alpha + 0.5 with u = normal / max(|normal|, 1e-12) (torch's order).
+ * Backward: the gradient flows only where alpha > 0.99 (the rest is detached in the reference);
+ * dL_dnormal (V, 3, H, W) and dL_dalpha (V, 1, H, W) are written whole (zeros where masked).
+ */
+int gsr_normal_map_forward(int V, int height, int width, const float* normal, const float* alpha, float* out,
+                           void* stream);
+int gsr_normal_map_backward(int V, int height, int width, const float* dL_dout, const float* normal,
+                            const float* alpha, float* dL_dnormal, float* dL_dalpha, void* stream);
+
+/*
  * Fused shading / depth-normal epilogue of the MVDream shading renderer and the SuGaR normal renderer
  * (replaces the torch ops of renderer/diff_gaussian_rasterizer_shading.py:169-208 with Depth2Normal
  * :22-51 and material/gaussian_material.py:41-104; renderer/diff_sugar_rasterizer_normal.py:170-197).

@@ -102,6 +102,18 @@ def torch_depth_normal_views(depth, alpha, rays_o, rays_d):
     return torch.stack([o[0] for o in outs]), torch.stack([o[1] for o in outs])
 
 
+def torch_sugar_normal_map(normal, alpha):
+    """renderer/diff_sugar_rasterizer_normal.py:192-197 per view (the torch lines the fused pass replaces)."""
+    outs = []
+    for v in range(normal.shape[0]):
+        n = torch.nn.functional.normalize(normal[v], dim=0)
+        n = torch.cat([-n[:2], n[2:]], 0)
+        nmap = n * 0.5 * alpha[v] + 0.5
+        mask = (alpha[v] > 0.99).repeat(3, 1, 1)
+        outs.append(torch.where(mask, nmap, nmap.detach()))
+    return torch.stack(outs)
+
+
 class FakeGeometry:
     def __init__(self, scene, device, dtype=torch.float32, pred_normal=False):
         leaf = lambda x: torch.tensor(x, device=device, dtype=dtype, requires_grad=True)  # noqa: E731

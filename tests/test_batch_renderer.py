@@ -26,7 +26,8 @@ def _scene():
 
 
 _SWAPS = (("_rasterize_views", rf.torch_rasterize_views), ("_shade_views", rf.torch_shade_views),
-          ("_depth_normal_maps", rf.torch_depth_normal_maps), ("_depth_normal_views", rf.torch_depth_normal_views))
+          ("_depth_normal_maps", rf.torch_depth_normal_maps), ("_depth_normal_views", rf.torch_depth_normal_views),
+          ("_sugar_normal_map", rf.torch_sugar_normal_map))
 
 
 def _cpu(monkeypatch=None):

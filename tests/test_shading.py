@@ -255,3 +255,55 @@ def test_shade_saturated_masks_match_torch():
         a, b = t[k].grad.double(), r[k].grad.double()
         err = ((a - b).abs() / b.abs().clamp(min=1.0)).max()
         assert float(err) <= 1e-4, f"grad {k}: {float(err)}"
+
+
+def _normal_map_ref(normal, alpha):
+    """renderer/diff_sugar_rasterizer_normal.py:192-197 for one view, in torch (the reference's lines)."""
+    n = torch.nn.functional.normalize(normal, dim=0)
+    n = torch.cat([-n[:2], n[2:]], 0)
+    nmap = n * 0.5 * alpha + 0.5
+    mask = (alpha > 0.99).repeat(3, 1, 1)
+    return torch.where(mask, nmap, nmap.detach())
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("V,H,W", [(1, 16, 16), (3, 27, 50)])
+def test_sugar_normal_map_matches_torch(V, H, W):
+    """The fused SuGaR normal map (normalize, axis flip, alpha-weighted map, alpha > 0.99 gradient mask) against
+    the reference's torch lines in fp64 / fp32; a third of the pixels below the 0.99 mask and a few zero
+    normals (the 1e-12 clamp)."""
+    from diff_gaussian_rasterization.shading import sugar_normal_map
+
+    g = torch.Generator().manual_seed(11 + W)
+    normal = torch.randn((V, 3, H, W), generator=g, dtype=torch.float64)
+    # (masks clear of 0.99, so fp32 and fp64 take the same side; the zero normals sit where alpha <= 0.99,
+    # their clamped forward exercised, their gradient masked)
+    alpha = torch.where(torch.rand((V, 1, H, W), generator=g) < 0.33, torch.rand((V, 1, H, W), generator=g) * 0.98,
+                        0.995 + 0.005 * torch.rand((V, 1, H, W), generator=g)).double()
+    normal[:, :, 0, :3] = 0.0
+    alpha[:, :, 0, :3] = 0.5
+    up = torch.randn((V, 3, H, W), generator=g, dtype=torch.float64)
+    n_gpu = normal.float().cuda().requires_grad_(True)
+    a_gpu = alpha.float().cuda().requires_grad_(True)
+    out = sugar_normal_map(n_gpu, a_gpu)
+    out.backward(up.float().cuda())
+    for v in range(V):
+        res = {}
+        for dt in (torch.float64, torch.float32):
+            n = normal[v].to(dt).clone().requires_grad_(True)
+            a = alpha[v].to(dt).clone().requires_grad_(True)
+            o = _normal_map_ref(n, a)
+            o.backward(up[v].to(dt))
+            res[dt] = (o, n.grad, a.grad)
+        (o64, n64, a64), (o32, n32, a32) = res[torch.float64], res[torch.float32]
+        _check("nmap", out[v], o64, o32, 1e-6)
+        _check("dnormal", n_gpu.grad[v], n64, n32, 1e-5)
+        _check("dalpha", a_gpu.grad[v], a64, a32, 1e-5)
+
+
+def test_sugar_normal_map_has_no_cpu_path():
+    from diff_gaussian_rasterization import _C
+    from diff_gaussian_rasterization.shading import sugar_normal_map
+
+    with pytest.raises(_C.GSRError):
+        sugar_normal_map(torch.ones((1, 3, 4, 4)), torch.ones((1, 1, 4, 4)))

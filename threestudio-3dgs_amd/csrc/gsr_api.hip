@@ -291,6 +291,25 @@ int gsr_composite_backward(int V, int height, int width, const float* dL_dout, c
   return last_launch();
 }
 
+int gsr_normal_map_forward(int V, int height, int width, const float* normal, const float* alpha, float* out,
+                           void* stream) {
+  if (V < 0 || height < 0 || width < 0) return fail(GSR_EINVAL, "%s", "bad sizes");
+  if (V == 0 || height == 0 || width == 0) return last_launch();
+  if (normal == nullptr || alpha == nullptr || out == nullptr) return fail(GSR_EINVAL, "%s", "null pointer argument");
+  launch_normal_map_fwd(V, (size_t)height * width, normal, alpha, out, (hipStream_t)stream);
+  return last_launch();
+}
+
+int gsr_normal_map_backward(int V, int height, int width, const float* dL_dout, const float* normal,
+                            const float* alpha, float* dL_dnormal, float* dL_dalpha, void* stream) {
+  if (V < 0 || height < 0 || width < 0) return fail(GSR_EINVAL, "%s", "bad sizes");
+  if (V == 0 || height == 0 || width == 0) return last_launch();
+  if (dL_dout == nullptr || normal == nullptr || alpha == nullptr || dL_dnormal == nullptr || dL_dalpha == nullptr)
+    return fail(GSR_EINVAL, "%s", "null pointer argument");
+  launch_normal_map_bwd(V, (size_t)height * width, dL_dout, normal, alpha, dL_dnormal, dL_dalpha, (hipStream_t)stream);
+  return last_launch();
+}
+
 static int shade_args(int V, int H, int W, int flags, const int* modes, const float* color, const float* depth,
                       const float* alpha, const float* rays_o, const float* rays_d, const float* bg, int bg_layout,
                       const float* light, const float* pred_normal, const float* ambient, const float* diffuse,

@@ -116,6 +116,10 @@ void launch_composite_fwd(int V, size_t HW, const float* color, const float* alp
 void launch_composite_bwd(int V, size_t HW, const float* dout, const float* color, const float* alpha,
                           const float* bg, int layout, float* dcolor, float* dalpha, float* dbg,
                           hipStream_t stream);
+// SuGaR normal map (normalize, flip, alpha-weighted map, alpha > 0.99 gradient mask) — gsr_epilogue.hip.
+void launch_normal_map_fwd(int V, size_t HW, const float* normal, const float* alpha, float* out, hipStream_t stream);
+void launch_normal_map_bwd(int V, size_t HW, const float* dout, const float* normal, const float* alpha,
+                           float* dnormal, float* dalpha, hipStream_t stream);
 // Shading / depth-normal epilogue — gsr_shading.hip (include/gsr.h gsr_shade_*).
 struct ShadeArgs {
   // a launch covers views v0 .. v0+V-1 (V <= GSR_SET_MAX); the view planes below are the whole call's

@@ -54,6 +54,8 @@ SIGNATURES = {
     "gsr_mark_visible": (_i, [_i, _vp, _vp, _vp, _vp, _vp]),
     "gsr_composite_forward": (_i, [_i, _i, _i, _vp, _vp, _vp, _i, _vp, _vp]),
     "gsr_composite_backward": (_i, [_i, _i, _i, _vp, _vp, _vp, _vp, _i, _vp, _vp, _vp, _vp]),
+    "gsr_normal_map_forward": (_i, [_i, _i, _i, _vp, _vp, _vp, _vp]),
+    "gsr_normal_map_backward": (_i, [_i, _i, _i, _vp, _vp, _vp, _vp, _vp, _vp]),
     "gsr_shade_forward": (_i, [_i, _i, _i, _i, _i] + [_vp] * 6 + [_i] + [_vp] * 8 + [_vp]),
     "gsr_shade_backward": (_i, [_i, _i, _i, _i, _i] + [_vp] * 6 + [_i] + [_vp] * 12 + [_vp]),
     "gsr_shade_views_forward": (_i, [_i, _i, _i, _i, ctypes.POINTER(_i)] + [_vp] * 6 + [_i] + [_vp] * 2

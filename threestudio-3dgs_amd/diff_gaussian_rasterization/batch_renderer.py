@@ -109,6 +109,12 @@ def _depth_normal_views(*args, **kwargs):
     return depth_normal_views(*args, **kwargs)
 
 
+def _sugar_normal_map(*args, **kwargs):
+    from .shading import sugar_normal_map
+
+    return sugar_normal_map(*args, **kwargs)
+
+
 def _depth_normal_maps(*args, **kwargs):
     from .shading import depth_normal_maps
 
@@ -293,11 +299,10 @@ def render_views_local(renderer, batch: dict, mode: str, lo: int, hi: int, draws
             if batch.get("compute_normal_from_dist", True):
                 _, nmap_dist = _depth_normal_views(depth, alpha, batch["rays_o"][lo:hi], batch["rays_d"][lo:hi])
                 out["comp_normal_from_dist"] = nmap_dist
-            normal = torch.nn.functional.normalize(normal, dim=1)
-            normal = torch.cat([-normal[:, :2], normal[:, 2:]], 1)  # p3d -> threestudio axes (:193)
-            nmap = normal * 0.5 * alpha + 0.5
+            # normalize, p3d -> threestudio axes, alpha-weighted map, alpha > 0.99 gradient mask (:192-197)
+            nmap = _sugar_normal_map(normal, alpha)
             mask = alpha > 0.99
-            out.update(comp_rgb=color.clamp(0, 1), comp_normal=torch.where(mask.expand_as(nmap), nmap, nmap.detach()),
+            out.update(comp_rgb=color.clamp(0, 1), comp_normal=nmap,
                        comp_depth=torch.where(mask, depth, depth.detach()), comp_mask=alpha)
         else:
             raise ValueError(f"unknown mode {mode!r}")

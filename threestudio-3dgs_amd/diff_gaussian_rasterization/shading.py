@@ -183,3 +183,43 @@ def depth_normal_maps(depth, alpha, rays_o, rays_d):
     rays_o, rays_d = _views(rays_o, 3).expand(V, H, W, 3), _views(rays_d, 3).expand(V, H, W, 3)
     _, nmap, depth_out = _Shade.apply(None, depth, alpha, rays_o, rays_d, None, None, None, 0, (), 0, (), ())
     return (nmap[0], depth_out[0]) if single else (nmap, depth_out)
+
+
+class _NormalMap(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, normal, alpha):
+        lib = _C.load_library()
+        dev = normal.device
+        _C._require_gpu(dev)
+        V, _, H, W = normal.shape
+        n = _C._f32(normal, "normal", dev)
+        a = _C._f32(alpha, "alpha", dev)
+        out = torch.empty((V, 3, H, W), dtype=torch.float32, device=dev)
+        _C._check(lib.gsr_normal_map_forward(V, H, W, _C._ptr(n), _C._ptr(a), _C._ptr(out), _C._stream(dev)))
+        ctx.save_for_backward(n, a)
+        return out
+
+    @staticmethod
+    def backward(ctx, g_out):
+        lib = _C.load_library()
+        n, a = ctx.saved_tensors
+        V, _, H, W = n.shape
+        dev = n.device
+        g = g_out.float().contiguous()
+        dn = torch.empty_like(n)
+        da = torch.empty_like(a)
+        _C._check(lib.gsr_normal_map_backward(V, H, W, _C._ptr(g), _C._ptr(n), _C._ptr(a), _C._ptr(dn), _C._ptr(da),
+                                              _C._stream(dev)))
+        return dn, da
+
+
+def sugar_normal_map(normal, alpha):
+    """The SuGaR normal renderer's normal map from its second rasterizer call (face normals blended):
+    ``F.normalize(normal)``, x / y negated (p3d -> threestudio axes), ``normal * 0.5 * alpha + 0.5``, with the
+    gradient kept only where ``alpha > 0.99`` (renderer/diff_sugar_rasterizer_normal.py:192-197) — one HIP pass
+    each way.  normal (3, H, W) or (V, 3, H, W), alpha (1, H, W) or (V, 1, H, W)."""
+    single = normal.dim() == 3
+    if single:
+        normal, alpha = normal.unsqueeze(0), alpha.unsqueeze(0)
+    out = _NormalMap.apply(normal, alpha)
+    return out[0] if single else out
