@@ -179,10 +179,10 @@ def settings_for(rep: Replica, cam, bg_zero):
 
 def placeholders(rep: Replica, V: int):
     """The views' screen-space placeholders (renderer/diff_gaussian_rasterizer.py:73-81 creates one zero
-    (P, 3) tensor per view): V leaves that are views of one zeroed (V, P, 3) buffer — one fill kernel for
-    the batch instead of V."""
-    buf = torch.zeros((V, rep.means3D.shape[0], 3), device=rep.means3D.device)
-    return [buf[v].requires_grad_(True) for v in range(V)]
+    (P, 3) tensor per view): V leaves, each one zero broadcast to (P, 3) — their values are never read, so no
+    (V, P, 3) fill; .grad is a dense (P, 3) tensor as for the reference's zeros."""
+    zero = torch.zeros((1, 1), device=rep.means3D.device)
+    return [zero.expand(rep.means3D.shape[0], 3).requires_grad_(True) for _ in range(V)]
 
 
 COMPOSITE = os.environ.get("GSR_BENCH_COMPOSITE", "fused")  # "separate": gsr_composite_* as its own pass

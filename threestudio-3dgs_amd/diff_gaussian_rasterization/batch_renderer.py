@@ -201,9 +201,10 @@ def render_view_reference(renderer, batch: dict, batch_idx: int) -> dict:
 
 def _placeholders(P, n, dev, dtype):
     """One screen-space placeholder per view (renderer/diff_gaussian_rasterizer.py:67-77): leaves whose
-    .grad is the view's viewspace gradient, carved from one zeroed buffer (one fill for the batch)."""
-    buf = torch.zeros((n, P, 3), device=dev, dtype=dtype)
-    return [buf[v].requires_grad_(True) for v in range(n)]
+    .grad is the view's viewspace gradient.  Their values are zeros and never read, so each is one zero
+    broadcast to (P, 3) (no (n, P, 3) fill; .grad is a dense (P, 3) tensor as for the reference's zeros)."""
+    zero = torch.zeros((1, 1), device=dev, dtype=dtype)
+    return [zero.expand(P, 3).requires_grad_(True) for _ in range(n)]
 
 
 def render_views_local(renderer, batch: dict, mode: str, lo: int, hi: int, draws: dict | None = None) -> dict:
