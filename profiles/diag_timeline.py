@@ -102,9 +102,11 @@ def main():
             rep.zero_grad()
         torch.cuda.synchronize()
         res = {}
-        for which, name in ((0, "k_render_fwd"), (1, "k_render_bwd")):
-            buf = np.zeros((nb, 4), np.uint32)
-            assert lib.gsr_diag_timeline(which, buf.ctypes.data, nb) == 0
+        # (one view: the quadrant-wave forward has 16 blocks per super-tile, the backward 4; only the
+        # launched blocks are read, later slots may hold an earlier, larger launch's stamps)
+        for which, name, n in ((0, "k_render_fwd", nb), (1, "k_render_bwd", nb // 4)):
+            buf = np.zeros((n, 4), np.uint32)
+            assert lib.gsr_diag_timeline(which, buf.ctypes.data, n) == 0
             res[name] = summarise(buf, name)
         out.append({"view": vi, **res})
     os.makedirs(os.path.join(ROOT, "gpurun_out"), exist_ok=True)
