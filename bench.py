@@ -69,7 +69,7 @@ def parse():
     ap.add_argument("--path", choices=["batched", "per-view"], default="batched",
                     help="batched: rasterize_views (one autograd node per rank's views); per-view: one "
                          "GaussianRasterizer call per view, exactly as the reference renderer loop does")
-    ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "r03b_traffic.json"),
+    ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "r03c_traffic.json"),
                     help="PMC summary (profiles/summarize.py) supplying roofline.traffic and the VALU counts")
     ap.add_argument("--pairs", default=os.path.join(ROOT, "profiles", "r03_pairs.json"),
                     help="device-counted blend pairs (profiles/diag_pairs.py) for the VALU roofline")
