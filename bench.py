@@ -386,13 +386,18 @@ def time_per_view_path(rep, cams, bg_zero, bg_img, upstream, n_views):
     (renderer/gaussian_batch_renderer.py:21-76) with the background composite in torch — timed on
     n_views views of the same workload (views/s; 1 GPU)."""
     n = min(n_views, len(cams))
+    # one background tensor per view, as the reference's background network returns a fresh (H, W, 3) image
+    # per view (renderer/diff_gaussian_rasterizer_background.py:116); slices of one batch leaf would make
+    # autograd zero-fill the whole batch's gradient once per view
+    bgs = [bg_img[i].detach().clone().requires_grad_(True) for i in range(n)]
 
     def run():
-        outs = [render_view(rep, cams[i], bg_zero, bg_img[i]) for i in range(n)]
+        outs = [render_view(rep, cams[i], bg_zero, bgs[i]) for i in range(n)]
         ts = [t for o in outs for t in o[:3]]
         torch.autograd.backward(ts, [g for u in upstream[:n] for g in u])
         rep.zero_grad()
-        bg_img.grad = None
+        for b in bgs:
+            b.grad = None
 
     run()
     torch.cuda.synchronize()
@@ -547,6 +552,9 @@ def main():
     # the background network's output per view, (H, W, 3) as the reference's background MLP returns it
     # (renderer/diff_gaussian_rasterizer_background.py:116); a trainable leaf so its gradient is formed
     bg_img = torch.rand((len(mine), H, W, 3), generator=gen, device=device).requires_grad_(True)
+    # the per-view path's backgrounds: one leaf per view (the background network's per-view output)
+    bg_views = [bg_img[i].detach().clone().requires_grad_(True) for i in range(len(mine))] \
+        if args.path == "per-view" else []
     log(f"[bench] rank {rank}/{world}: setup {time.perf_counter() - t_setup:.1f}s, {len(mine)} views/rank")
 
     settings = [settings_for(rep, cam, bg_zero) for cam in mine]
@@ -588,7 +596,7 @@ def main():
             else:
                 torch.autograd.backward((c, d, a, outs[4]), (up_c, up_d, up_a, up_n))
         else:
-            outs = [render_view(rep, cam, bg_zero, bg_img[i],
+            outs = [render_view(rep, cam, bg_zero, bg_views[i],
                                 None if shade is None else tuple(t[i] for t in shade))
                     for i, cam in enumerate(mine)]
             if world > 1:
@@ -606,6 +614,8 @@ def main():
         # (else the rasterizer's backward summed them over ranks range by range, overlapped with it)
         rep.zero_grad()
         bg_img.grad = None
+        for b in bg_views:
+            b.grad = None
 
     for _ in range(args.warmup):
         step()
