@@ -83,6 +83,12 @@ def main():
     keys = b[0:4 * int(ranges[:, 1].max())].view(np.uint32)  # packed tile << gbits | Gaussian, result in key[0]
     gbits = vbits
     L = (ranges[:, 1] - ranges[:, 0]).astype(np.int64)
+    qm = im[io[1]:io[1] + 16 * T].view(np.uint32).reshape(T, 4)
+    maxc = qm.max(1).astype(np.int64)
+    pct = lambda x, q: int(np.percentile(x, q))  # noqa: E731
+    maxc_stats = {"p50": pct(maxc, 50), "p90": pct(maxc, 90), "p99": pct(maxc, 99), "max": int(maxc.max()),
+                  "sum": int(maxc.sum()), "tiles_over": {str(c): int((maxc > c).sum()) for c in (128, 256, 512, 1024)},
+                  "sum_over_cap": {str(c): int(np.maximum(maxc - c, 0).sum()) for c in (128, 256, 512)}}
     # per tile: the list position where its last pixel terminated (or the list end when some pixel never did)
     need = np.zeros(T, np.int64)
     for t in range(T):
@@ -90,7 +96,7 @@ def main():
         fT = final_T[16 * ty:16 * ty + 16, 16 * tx:16 * tx + 16]
         nc = n_contrib[16 * ty:16 * ty + 16, 16 * tx:16 * tx + 16]
         need[t] = L[t] if (fT >= 1e-2).any() else int(nc.max()) + 1
-    out = {"view": vi, "visible": nvis, "listed": int(L.sum()), "tiles": T,
+    out = {"view": vi, "visible": nvis, "listed": int(L.sum()), "tiles": T, "blended_prefix_maxc": maxc_stats,
            "tiles_never_saturated": int(sum(1 for t in range(T) if need[t] >= L[t] and L[t] > 0)),
            "needed_prefix_instances": int(np.minimum(need, L).sum()), "splits": []}
     for X in (0.05, 0.1, 0.15, 0.2, 0.3, 0.5):

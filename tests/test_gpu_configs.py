@@ -264,18 +264,95 @@ def test_backward_view_groups_bitwise(monkeypatch):
         assert np.array_equal(one["g_means2D"][v], split["g_means2D"][v])
 
 
-def test_view_sets_bitwise(monkeypatch):
+@pytest.mark.parametrize("split", ["off", "on"])
+def test_view_sets_bitwise(split, monkeypatch):
     """20 views as one set vs four sets of 5 (later sets continue the sums: include/gsr.h accumulate with
-    the running dL/dcov3D): identical images and bitwise identical gradients."""
+    the running dL/dcov3D): identical images and bitwise identical gradients.  The split backward of sets of
+    <= 8 views (gsr_render.hip split_on) replays other fp32 sums than the whole-prefix walk of a 20-view set:
+    "off" compares 20 views against 4 x 5 with it disabled, "on" 8 views against 4 x 2 with it on in both."""
     scene = gs.make_scene(12_000, sh_degree=2, seed=31)
-    cams = [make_camera(128, 112, elevation=(i % 3) * 12.0, azimuth=18.0 * i) for i in range(20)]
-    ups = [gs.upstream_grads(112, 128, seed=120 + v) for v in range(20)]
+    nv = 20 if split == "off" else 8
+    if split == "off":
+        monkeypatch.setenv("GSR_BWD_SPLIT", "0")
+    cams = [make_camera(128, 112, elevation=(i % 3) * 12.0, azimuth=18.0 * i) for i in range(nv)]
+    ups = [gs.upstream_grads(112, 128, seed=120 + v) for v in range(nv)]
     one = _batched_grads(scene, cams, ups)
-    sets = _batched_grads(scene, cams, ups, monkeypatch, set_max=5)
+    sets = _batched_grads(scene, cams, ups, monkeypatch, set_max=5 if split == "off" else 2)
     for k in ("color", "depth", "alpha", "radii"):
         assert np.array_equal(one[k], sets[k]), k
     for k in ("g_means3D", "g_opacity", "g_sh", "g_scales", "g_rotations"):
         assert np.array_equal(one[k], sets[k]), k
+
+
+def _deep_scene():
+    """Many faint Gaussians in a small image: tiles blend well past GSR_SPLIT_NCK x GSR_SPLIT_CH candidates."""
+    scene = gs.make_scene(80_000, sh_degree=1, seed=71, scale_mult=2.0, opacity_range=(0.005, 0.03))
+    return scene, make_camera(80, 64, azimuth=25.0)
+
+
+def _quad_maxc(scene, cam):
+    """Per tile, the deepest blended list position of its quadrants (the image state's quad_maxc)."""
+    import torch
+
+    from diff_gaussian_rasterization import _C
+
+    dev = "cuda"
+    t = {k: torch.tensor(scene[k], device=dev) for k in ("means3D", "opacities", "scales", "rotations", "shs")}
+    with torch.no_grad():
+        out = _C.rasterize_gaussians(torch.zeros(3, device=dev), t["means3D"], None, t["opacities"], t["scales"],
+                                     t["rotations"], 1.0, None, torch.tensor(cam["view"], device=dev),
+                                     torch.tensor(cam["proj"], device=dev), cam["tanx"], cam["tany"], cam["H"],
+                                     cam["W"], t["shs"], int(scene["sh_degree"]), torch.tensor(cam["campos"], device=dev),
+                                     False, False)
+    image = out[7].cpu().numpy()
+    tiles = ((cam["W"] + 15) // 16) * ((cam["H"] + 15) // 16)
+    off = (8 * tiles + 255) // 256 * 256  # csrc/gsr_common.h ImageState: ranges, then quad_maxc
+    return image[off:off + 16 * tiles].view(np.uint32).reshape(tiles, 4).max(1)
+
+
+@pytest.mark.parametrize("size", ["listed", "overflow"])
+def test_split_backward_matches_whole_walk(size, monkeypatch):
+    """The split backward (sets of <= 8 views: GSR_SPLIT_NCK + 1 workgroups per tile, each replaying
+    GSR_SPLIT_CH candidates from the forward's per-pixel checkpoint) against the whole-prefix walk
+    (GSR_BWD_SPLIT=0): the same candidates and rows, other fp32 sums (the accumulated colour behind a chunk is
+    suffix sums of the later chunks' own blends over T_chunk instead of the back-to-front recursion) — every
+    gradient within the parity bar 1e-4 max(1, |g|) (lists here reach 20k candidates: both fp32 orders drift
+    ~1e-5 from each other); and the scene does exercise every chunk.  "overflow": more later chunks than the
+    GSR_SPLIT_EXTRA listed items, the tiles' own workgroups walk the rest (ImageState::split_cap)."""
+    from gsr_testutil import gpu_render
+
+    scene, cam = _deep_scene()
+    if size == "overflow":
+        cam = make_camera(448, 384, azimuth=25.0)
+    maxc = _quad_maxc(scene, cam)
+    later = int(np.minimum(15, np.maximum(maxc.astype(np.int64) - 1, 0) // 256).sum())
+    print(f"later chunks {later}")
+    assert (later > 1024) == (size == "overflow"), later
+    print(f"split scene: tile maxc p50 {int(np.median(maxc))} max {int(maxc.max())} tiles > 256: {(maxc > 256).sum()}")
+    assert (maxc > 256).sum() > 5 and maxc.max() > 1536, f"chunks not exercised: max {maxc.max()}"
+    g = gs.upstream_grads(cam["H"], cam["W"], seed=17)
+    split = gpu_render(scene, cam, [0.3, 0.2, 0.1], grads=g)
+    monkeypatch.setenv("GSR_BWD_SPLIT", "0")
+    whole = gpu_render(scene, cam, [0.3, 0.2, 0.1], grads=g)
+    for k in ("color", "depth", "alpha", "radii"):
+        assert np.array_equal(split[k], whole[k]), k
+    for k in ("g_means3D", "g_means2D", "g_opacity", "g_sh", "g_scales", "g_rotations"):
+        ref = whole[k].astype(np.float64)
+        err = float((np.abs(split[k] - ref) / np.maximum(1.0, np.abs(ref))).max())
+        assert err <= 1e-4, f"{k}: {err}"
+
+
+def test_split_backward_parity():
+    """The split backward against the fp64 oracle with every parity test's bars (deep tiles: all chunks)."""
+    from gsr_testutil import gpu_render
+
+    scene, cam = _deep_scene()
+    bg = [0.3, 0.2, 0.1]
+    g = gs.upstream_grads(cam["H"], cam["W"], seed=17)
+    gpu = gpu_render(scene, cam, bg, grads=g)
+    ref = run_oracle(scene, cam, bg, grads=g)
+    check_forward(gpu, ref, "split deep", K_gpu=gpu["K"])
+    check_grads(gpu, ref, ["means3D", "means2D", "opacity", "sh", "scales", "rotations"], "split deep")
 
 
 # ------------------------------------------------------------------------------------------------
@@ -429,6 +506,9 @@ def test_second_colors_match_separate_call(bwd, monkeypatch):
     import torch
 
     monkeypatch.setenv("GSR_TWO_COLOR_BWD", bwd)
+    # the two-colour backward never splits (its checkpoints hold the first colour only): compare it with
+    # whole-prefix walks of the separate calls
+    monkeypatch.setenv("GSR_BWD_SPLIT", "0")
 
     from diff_gaussian_rasterization.batched import rasterize_views
 

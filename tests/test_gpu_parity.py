@@ -204,9 +204,15 @@ def _settings(cam, bg, deg, dev="cuda", mod=1.0):
 
 
 @pytest.mark.parametrize("nviews", [1, 5, 19, 67])
-def test_batched_views_match_per_view(nviews):
-    """rasterize_views (view sets: one launch per stage for up to 64 views; 67 = two sets) == per-view calls."""
+def test_batched_views_match_per_view(nviews, monkeypatch):
+    """rasterize_views (view sets: one launch per stage for up to 64 views; 67 = two sets) == per-view calls.
+    Per-view calls and sets of <= 8 views split the backward (gsr_render.hip split_on), larger sets walk whole
+    prefixes: the 19- and 67-view cases compare with the split disabled (tests/test_gpu_configs.py
+    test_split_backward_* hold the split to the whole walk and the oracle)."""
     import torch
+
+    if nviews > 8:
+        monkeypatch.setenv("GSR_BWD_SPLIT", "0")
 
     from diff_gaussian_rasterization import GaussianRasterizer
     from diff_gaussian_rasterization.batched import rasterize_views
@@ -280,6 +286,7 @@ def test_forward_kernels_bitwise(kind, switch, monkeypatch):
     def run(kernel):
         if switch == "fwd_kernel":
             monkeypatch.setenv("GSR_FWD_KERNEL", kernel)
+            monkeypatch.setenv("GSR_BWD_SPLIT", "0")  # the tile-wave forward writes no split checkpoints
         elif kernel == "tile":
             monkeypatch.delenv("GSR_TILE_ORDER", raising=False)
         else:

@@ -61,7 +61,14 @@ struct RenderSet {
   const float* dpix2;
   // dispatch order (ImageState::order of the set, indexed by v0 + v): null = views in turn, raster order
   const uint32_t* order;
+  // split backward (gsr_render.hip split_on): the forward writes its checkpoints here, the backward walks the
+  // tiles in chunks from them; null = off
+  float* ckpt;
+  uint32_t* split_items;  // with ckpt: the later chunks' backward items (ImageState::split_items)
+  uint32_t* split_cap;    // with ckpt: ImageState::split_cap
 };
+// backward tile splitting on for a launch of V views (GSR_BWD_SPLIT=0 turns it off)
+bool split_on(int V);
 // Each view's super-tiles by listed instances, heaviest first (after binning) — gsr_render.hip
 void launch_tile_order(int V, int gx, int gy, const uint2* ranges, uint32_t* order, hipStream_t stream);
 // GSR_TILE_ORDER=raster: the blends dispatch views in turn in raster order (A/B); the order is still written

@@ -146,7 +146,8 @@ __device__ __forceinline__ bool quadrant_hit(const float4 r0, const float4 r1, f
 // Gaussians whose alpha >= 1/255 ellipse can reach its quadrant, and blends them with a
 // branch-free predicated body.  No workgroup barriers couple quadrants that terminate at
 // different depths, and 4x more independent waves balance the load across the 256 CUs.
-template <bool C2>
+// CK: also the split backward's per-chunk states (rs.ckpt, gsr_common.h ckpt_offset).
+template <bool C2, bool CK>
 __global__ __launch_bounds__(64) void k_render_fwd(RenderSet rs,
                                                    const uint2* __restrict__ ranges,
                                                    const uint32_t* __restrict__ sorted_gauss,
@@ -208,8 +209,21 @@ __global__ __launch_bounds__(64) void k_render_fwd(RenderSet rs,
     if (C2) n3 = make_float4(col2[3 * g0], col2[3 * g0 + 1], col2[3 * g0 + 2], 0.f);
   }
   if (64 + lane < n) gi_next = sorted_gauss[range.x + 64 + lane] & gmask;
+  // split backward: T at each chunk boundary the walk reaches, and each chunk's own colour / depth sums
+  float* const ckpt = CK ? rs.ckpt + ckpt_offset((size_t)(rs.v0 + v), (size_t)rs.gx * rs.gy, tile, 0) : nullptr;
+  const int cpix = 64 * q + lane;
+  if (CK && blockIdx.x == 0 && lane == 0) rs.split_items[0] = 0u;  // k_ckpt_suffix lists the split items
+  float Pr = 0.f, Pg = 0.f, Pb = 0.f, Pd = 0.f;
+  int chunk = 0;
   for (int base = 0; base < n; base += 64) {
     if (__all(done)) break;
+    if (CK && base > 0 && base % GSR_SPLIT_CH == 0 && base <= GSR_SPLIT_NCK * GSR_SPLIT_CH) {
+      // chunk `chunk` ends: its sums into its slot, T into the next one's
+      reinterpret_cast<float4*>(ckpt + (size_t)chunk * GSR_CKPT_FIELDS * 256 + 256)[cpix] = make_float4(Pr, Pg, Pb, Pd);
+      ++chunk;
+      ckpt[(size_t)chunk * GSR_CKPT_FIELDS * 256 + cpix] = T;
+      Pr = Pg = Pb = Pd = 0.f;
+    }
     const int i = base + lane;
     const float4 r0 = n0, r1 = n1, r2 = n2, r3 = n3;
     if (base + 64 + lane < n) {
@@ -255,6 +269,12 @@ __global__ __launch_bounds__(64) void k_render_fwd(RenderSet rs,
       Cg = fmaf(c.y, aT, Cg);
       Cb = fmaf(c.z, aT, Cb);
       D = fmaf(b.z, aT, D);
+      if (CK) {
+        Pr = fmaf(c.x, aT, Pr);
+        Pg = fmaf(c.y, aT, Pg);
+        Pb = fmaf(c.z, aT, Pb);
+        Pd = fmaf(b.z, aT, Pd);
+      }
       if (C2) {
         Er = fmaf(e.x, aT, Er);
         Eg = fmaf(e.y, aT, Eg);
@@ -302,6 +322,10 @@ __global__ __launch_bounds__(64) void k_render_fwd(RenderSet rs,
       cp[HW] = fminf(fmaxf((Cg + T * bg[1]) + am * bgi[1], 0.0f), 1.0f);
       cp[2 * HW] = fminf(fmaxf((Cb + T * bg[2]) + am * bgi[2], 0.0f), 1.0f);
     }
+  }
+  if (CK && chunk > 0) {
+    // the chunk the walk ended in (the backward reads chunks up to the quadrant's deepest blend only)
+    reinterpret_cast<float4*>(ckpt + (size_t)chunk * GSR_CKPT_FIELDS * 256 + 256)[cpix] = make_float4(Pr, Pg, Pb, Pd);
   }
   uint32_t mc = last_contributor;
 #pragma unroll
@@ -635,6 +659,51 @@ bool tile_order_on() {
   return !(e != nullptr && strcmp(e, "raster") == 0);
 }
 
+// The split backward's chunk sums -> suffix sums (slot k: the colour / depth blended from candidate k CH to
+// the quadrant's last blend), in place; one workgroup per tile, a wave per quadrant, slots 1 .. the one
+// holding the quadrant's deepest blend (only those were written).  All loads are issued before the sums.
+__global__ __launch_bounds__(256) void k_ckpt_suffix(RenderSet rs, const uint32_t* __restrict__ quad_maxc) {
+  const int tiles = rs.gx * rs.gy;
+  const int v = blockIdx.x / tiles, tile = blockIdx.x % tiles;
+  const int t = threadIdx.x, q = t >> 6;
+  const size_t vg = (size_t)(rs.v0 + v);
+  const int qmaxc = (int)quad_maxc[(vg * tiles + tile) * 4 + q];
+  const int cl = qmaxc > 0 ? min(GSR_SPLIT_NCK, (qmaxc - 1) / GSR_SPLIT_CH) : 0;
+  if (t == 0) {
+    // the tile's chunks after the first (its block_map workgroup replays chunk 0) as backward items
+    const uint4 qm = reinterpret_cast<const uint4*>(quad_maxc)[vg * tiles + tile];
+    const int maxc = (int)max(max(qm.x, qm.y), max(qm.z, qm.w));
+    const int nc = maxc > 0 ? min(GSR_SPLIT_NCK, (maxc - 1) / GSR_SPLIT_CH) : 0;
+    // the deepest chunks first: when the list is full, the tile's own workgroup walks the remaining
+    // (shallowest) ones, [0, cap), in one contiguous stretch
+    uint32_t cap = 0xffffffffu;
+    if (nc > 0) {
+      const uint32_t at = atomicAdd(rs.split_items, (uint32_t)nc);
+      const int m = (int)min((uint32_t)nc, at < GSR_SPLIT_EXTRA ? GSR_SPLIT_EXTRA - at : 0u);
+      for (int j = 0; j < m; ++j)
+        rs.split_items[1 + at + j] = ((uint32_t)vg << 26) | ((uint32_t)(nc - j) << 22) | (uint32_t)tile;
+      if (m > 0) cap = (uint32_t)(nc - m + 1) * GSR_SPLIT_CH;
+    }
+    rs.split_cap[vg * tiles + tile] = cap;
+  }
+  if (cl < 2) return;  // (wave-uniform) one chunk behind the first boundary at most: already its sum
+  float4* const part = reinterpret_cast<float4*>(rs.ckpt + ckpt_offset(vg, (size_t)tiles, tile, 0) + 256) + t;
+  constexpr size_t SL = GSR_CKPT_FIELDS * 256 / 4;  // float4 per slot
+  float4 p[GSR_SPLIT_NCK + 1];
+#pragma unroll
+  for (int j = 1; j <= GSR_SPLIT_NCK; ++j) p[j] = part[(size_t)min(j, cl) * SL];
+  float4 acc = p[GSR_SPLIT_NCK];
+#pragma unroll
+  for (int j = GSR_SPLIT_NCK - 1; j >= 1; --j) {
+    if (j < cl) {
+      acc = make_float4(p[j].x + acc.x, p[j].y + acc.y, p[j].z + acc.z, p[j].w + acc.w);
+      part[(size_t)j * SL] = acc;
+    } else if (j == cl) {
+      acc = p[j];
+    }
+  }
+}
+
 // Which forward: the tile-wave kernel gathers each candidate once but walks a quadrant's candidates one
 // branch at a time and the whole tile list to the tile's deepest termination; it wins when Gaussians span
 // several tiles (C3: 6.7 rectangle tiles per Gaussian, render_fwd -3 %), the quadrant-wave kernel when
@@ -666,46 +735,40 @@ void launch_render_forward(const RenderSet& rs, const GeomState& g, const uint32
       hipLaunchKernelGGL(k_render_fwd_tile<false>, grid, dim3(64), 0, stream, rs, (const uint2*)img.ranges,
                          sorted_gauss, (const GaussRec*)g.rec, out_color, out_depth, out_alpha, img.final_T,
                          img.n_contrib, img.quad_maxc);
-  } else if (rs.col2 != nullptr) {
-    hipLaunchKernelGGL(k_render_fwd<true>, dim3(block_grid(rs, 16)), dim3(64), 0, stream, rs,
-                       (const uint2*)img.ranges, sorted_gauss, (const GaussRec*)g.rec, out_color, out_depth,
-                       out_alpha, img.final_T, img.n_contrib, img.quad_maxc);
   } else {
-    hipLaunchKernelGGL(k_render_fwd<false>, dim3(block_grid(rs, 16)), dim3(64), 0, stream, rs,
-                       (const uint2*)img.ranges, sorted_gauss, (const GaussRec*)g.rec, out_color, out_depth,
-                       out_alpha, img.final_T, img.n_contrib, img.quad_maxc);
+    auto kern = rs.col2 != nullptr ? (rs.ckpt != nullptr ? k_render_fwd<true, true> : k_render_fwd<true, false>)
+                                   : (rs.ckpt != nullptr ? k_render_fwd<false, true> : k_render_fwd<false, false>);
+    hipLaunchKernelGGL(kern, dim3(block_grid(rs, 16)), dim3(64), 0, stream, rs, (const uint2*)img.ranges,
+                       sorted_gauss, (const GaussRec*)g.rec, out_color, out_depth, out_alpha, img.final_T,
+                       img.n_contrib, img.quad_maxc);
+    if (rs.ckpt != nullptr)
+      hipLaunchKernelGGL(k_ckpt_suffix, dim3(rs.V * nt), dim3(256), 0, stream, rs, (const uint32_t*)img.quad_maxc);
   }
   hipLaunchKernelGGL(k_tile_info, dim3(rs.V * div_up(nt, 256)), dim3(256), 0, stream, rs,
                      (const uint2*)img.ranges, (const uint32_t*)img.quad_maxc, sorted_gauss,
                      (const GaussRec*)g.rec, img.tile_info, img.cut);
 }
 
+// One workgroup's backward of one tile: the whole blended prefix, or with `split` (split_on) chunk `chunk`,
+// candidates [chunk CH, (chunk + 1) CH) (chunk GSR_SPLIT_NCK: to the end of the prefix).
 template <bool TWO>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(TWO ? 4 : 5, 8))) void k_render_bwd(RenderSet rs,
-                                                    const uint2* __restrict__ ranges,
-                                                    const uint32_t* __restrict__ quad_maxc,
-                                                    const uint32_t* __restrict__ sorted_gauss,
-                                                    const GaussRec* __restrict__ rec,
-                                                    const uint32_t* __restrict__ goff,
-                                                    const float* __restrict__ final_Ts,
-                                                    const uint32_t* __restrict__ n_contrib,
-                                                    const float* __restrict__ dL_dcolor,
-                                                    const float* __restrict__ dL_ddepth,
-                                                    const float* __restrict__ dL_dalpha,
-                                                    float4* __restrict__ grow,
-                                                    unsigned long long* __restrict__ reach) {
-  __shared__ BwdLDS<TWO> s;
+__device__ __forceinline__ void bwd_tile(BwdLDS<TWO>& s, const RenderSet& rs, int v, int tile, int chunk, bool split,
+                                         const uint2* __restrict__ ranges, const uint32_t* __restrict__ quad_maxc,
+                                         const uint32_t* __restrict__ sorted_gauss, const GaussRec* __restrict__ rec,
+                                         const uint32_t* __restrict__ goff, const float* __restrict__ final_Ts,
+                                         const uint32_t* __restrict__ n_contrib, const float* __restrict__ dL_dcolor,
+                                         const float* __restrict__ dL_ddepth, const float* __restrict__ dL_dalpha,
+                                         float4* __restrict__ grow, unsigned long long* __restrict__ reach) {
   constexpr int NG = TWO ? NGV2 : NGV;                           // raw sums per (candidate, quadrant)
   constexpr int QS = TWO ? GSR_QSUM_STRIDE2 : GSR_QSUM_STRIDE;  // per candidate
   constexpr int GS = TWO ? 4 : 8;                                // candidates per 16x16 product
   constexpr int NPL = TWO ? 7 : 4;                               // dL/dpixel planes in the B operand
   constexpr int RW = TWO ? 4 : 3;                                // float4 per gradient row
-  int v, tile, q_unused;
-  if (!block_map<4>(blockIdx.x, rs, v, tile, q_unused)) return;
   GSR_TL_BEGIN
   const int W = rs.W, H = rs.H, grid_x = rs.gx;
+  const size_t vgs = (size_t)(rs.v0 + v);
   {
-    const size_t vg = (size_t)(rs.v0 + v), tiles = (size_t)rs.gx * rs.gy, HWs = (size_t)W * H;
+    const size_t vg = vgs, tiles = (size_t)rs.gx * rs.gy, HWs = (size_t)W * H;
     ranges += vg * tiles;
     quad_maxc += vg * 4 * tiles;
     sorted_gauss += rs.inst_start[v];
@@ -734,6 +797,17 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(TWO ? 4 : 5
   const uint4 qm = reinterpret_cast<const uint4*>(quad_maxc)[tile];
   const int qmaxc = (int)(q == 0 ? qm.x : q == 1 ? qm.y : q == 2 ? qm.z : qm.w);
   const int maxc = (int)max(max(qm.x, qm.y), max(qm.z, qm.w));
+  // the candidates [lo, hi) of the tile list this workgroup replays
+  int lo = 0, hi = maxc;
+  if (split) {
+    lo = chunk * GSR_SPLIT_CH;
+    if (chunk == 0)
+      hi = (int)min((uint32_t)maxc, rs.split_cap[vgs * rs.gx * rs.gy + tile]);
+    else
+      hi = chunk == GSR_SPLIT_NCK ? maxc : min(maxc, lo + GSR_SPLIT_CH);
+  }
+  lo = __builtin_amdgcn_readfirstlane(lo);  // (workgroup-uniform: scalars)
+  hi = __builtin_amdgcn_readfirstlane(hi);
   const size_t pid = (size_t)py * W + px;
   const size_t HW = (size_t)H * W;
 
@@ -762,7 +836,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(TWO ? 4 : 5
         const float gch = (pre >= 0.0f && pre <= 1.0f) ? dpix[ch] : 0.0f;
         dpix[ch] = gch;
         da -= gch * b;
-        if (rs.dcbg != nullptr) rs.dcbg[((size_t)v * HW + pid) * 3 + ch] = gch * am;
+        if (rs.dcbg != nullptr && chunk == 0) rs.dcbg[((size_t)v * HW + pid) * 3 + ch] = gch * am;
       }
       dpix_a = da + dpix_a;
     }
@@ -792,6 +866,20 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(TWO ? 4 : 5
   // normal-from-depth loss) and lose its significant bits.
   float S = 0.f, Sd = 0.f;
   const float nbg = -T_final * bg_dot;
+  if (split && hi < maxc && qmaxc > hi) {
+    // A chunk that ends before the quadrant's deepest blend starts from the forward's state at candidate
+    // hi: T there, and the colour / alpha / depth blended behind it over T (the reference's accum_rec
+    // there): the later chunks' own sums (slots up to the one holding the quadrant's last blend)
+    const size_t tiles = (size_t)rs.gx * rs.gy;
+    const float* ck = rs.ckpt + ckpt_offset(vgs, tiles, tile, hi / GSR_SPLIT_CH);
+    const float Th = ck[t];
+    const float4 b4 = reinterpret_cast<const float4*>(ck + 256)[t];  // k_ckpt_suffix: all later blends
+    const float br = b4.x, bgc = b4.y, bb = b4.z, bd = b4.w;
+    const float inv = 1.0f / Th;
+    T = Th;
+    S = (br * dpix[0] + bgc * dpix[1] + bb * dpix[2]) * inv + (1.0f - T_final * inv) * dpix_a;
+    Sd = bd * inv;
+  }
   const float ddelx_dx = 0.5f * W, ddely_dy = 0.5f * H;
   const float4 zero4 = make_float4(0.f, 0.f, 0.f, 0.f);
 
@@ -811,9 +899,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(TWO ? 4 : 5
   // this view's reach bit (staged candidates have rows): word v >> 5 of the Gaussian's 64 bits
   unsigned int* const reach32 = reinterpret_cast<unsigned int*>(reach) + (v >> 5);
   const unsigned int vbit = 1u << (v & 31);
-  if (maxc > 0) {
-    const uint32_t g0 = fetch_index(maxc);
-    if (maxc - 1 - cs >= 0) {
+  if (hi > lo) {
+    const uint32_t g0 = fetch_index(hi);
+    if (hi - 1 - cs >= lo) {
       npc = reinterpret_cast<const float4*>(rec + g0)[piece];
       if (piece == 2 && rs.col2 != nullptr) {
         if (TWO)
@@ -826,7 +914,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(TWO ? 4 : 5
         atomicOr(reach32 + 2 * g0, vbit);  // the Gaussian gets a row in this view (k_view_grad reads it)
       }
     }
-    if (maxc > 64) gi_next = fetch_index(maxc - 64);
+    if (hi - 64 > lo) gi_next = fetch_index(hi - 64);
   }
 
   // branch-free replay step; non-contributing lanes run it with alpha = 0 (state unchanged) and
@@ -962,10 +1050,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(TWO ? 4 : 5
 
   uint32_t* mylist = s.list[q];
   float* myq = s.qsum + q * NG;
-  for (int hi = maxc; hi > 0; hi -= 64) {
+  for (int h = hi; h > lo; h -= 64) {
     {
-      const int rel_c = hi - 1 - cs;
-      if (rel_c >= 0) {
+      const int rel_c = h - 1 - cs;
+      if (rel_c >= lo) {
         // the conic pre-multiplied for gauss_power2 (.w of s1: list position)
         if (piece == 0) {
           s.s0[cs] = make_float4(npc.x, npc.y, GSR_CONIC_K_AC * npc.z, GSR_CONIC_K_B * npc.w);
@@ -980,8 +1068,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(TWO ? 4 : 5
           s.slot[cs] = ngo + (uint32_t)((tyi - ymin) * (xmax - xmin) + (txi - xmin));
         }
       }
-      if (hi > 64) {
-        if (hi - 65 - cs >= 0) {
+      if (h - 64 > lo) {
+        if (h - 65 - cs >= lo) {
           npc = reinterpret_cast<const float4*>(rec + gi_next)[piece];
           if (piece == 2 && rs.col2 != nullptr) {
             const float4 c2 =
@@ -996,17 +1084,17 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(TWO ? 4 : 5
             atomicOr(reach32 + 2 * gi_next, vbit);
           }
         }
-        if (hi > 128) gi_next = fetch_index(hi - 128);
+        if (h - 128 > lo) gi_next = fetch_index(h - 128);
       }
     }
     __syncthreads();
     // this wave's quadrant: cull the staged batch, list the kept candidates, zero the others' sums
-    const int rel_l = hi - 1 - lane;
+    const int rel_l = h - 1 - lane;
     bool keep = false;
 #ifdef GSR_EXP_NOCULL
-    if (rel_l >= 0 && rel_l < qmaxc) keep = s.s0[lane].x > -1e30f;
+    if (rel_l >= lo && rel_l < qmaxc) keep = s.s0[lane].x > -1e30f;
 #else
-    if (rel_l >= 0 && rel_l < qmaxc) {
+    if (rel_l >= lo && rel_l < qmaxc) {
       // the staged conic back to (a, b, c) for the (padded, conservative) cull
       const float4 c0 = s.s0[lane], c1 = s.s1[lane];
       keep = quadrant_hit(make_float4(c0.x, c0.y, c0.z * (1.0f / GSR_CONIC_K_AC), c0.w * (1.0f / GSR_CONIC_K_B)),
@@ -1101,14 +1189,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(TWO ? 4 : 5
       tl_work += c0 + c1 + c2 + c3;                                  // kept (candidate, quadrant) pairs
       tl_max += 4 * max(max(c0, c1), max(c2, c3));                  // lockstep cost in pair slots
       tl_q[0] += c0, tl_q[1] += c1, tl_q[2] += c2, tl_q[3] += c3;
-      tl_staged += min(hi, 64);
+      tl_staged += min(h - lo, 64);
       tl_any += __popcll(s.kmask[0] | s.kmask[1] | s.kmask[2] | s.kmask[3]);
     }
 #endif
 #ifdef GSR_EXP_NOFLUSH
     if (hi < 0)
 #else
-    if (hi - 1 - cs >= 0)
+    if (h - 1 - cs >= lo)
 #endif
     {
       // four threads per candidate (t = 4 c + quadrant): per quadrant, turn the sums over pixel
@@ -1197,22 +1285,66 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(TWO ? 4 : 5
   (void)tl_any;
 }
 
+// The backward blend: a workgroup per tile (block_map: heaviest first, XCD-aware), after `extra` workgroups
+// that replay the split tiles' later chunks (split_on: the items k_ckpt_suffix listed, view << 26 | chunk << 22
+// | tile, count in items[0], at most GSR_SPLIT_EXTRA; a heavy tile's chunks run side by side instead of one
+// after the other, its own workgroup walks the chunks not listed, from ImageState::split_cap down).
+template <bool TWO>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(TWO ? 4 : 5, 8))) void k_render_bwd(
+    RenderSet rs, const uint2* __restrict__ ranges, const uint32_t* __restrict__ quad_maxc,
+    const uint32_t* __restrict__ sorted_gauss, const GaussRec* __restrict__ rec, const uint32_t* __restrict__ goff,
+    const float* __restrict__ final_Ts, const uint32_t* __restrict__ n_contrib, const float* __restrict__ dL_dcolor,
+    const float* __restrict__ dL_ddepth, const float* __restrict__ dL_dalpha, float4* __restrict__ grow,
+    unsigned long long* __restrict__ reach, int extra, const uint32_t* __restrict__ items) {
+  __shared__ BwdLDS<TWO> s;
+  int v, tile, chunk = 0;
+  if (!TWO && (int)blockIdx.x < extra) {
+    if (blockIdx.x >= items[0]) return;
+    const uint32_t it = items[1 + blockIdx.x];
+    v = (int)(it >> 26) - rs.v0;
+    if (v < 0 || v >= rs.V) return;  // another view group's tile
+    tile = (int)(it & 0x3fffffu);
+    chunk = (int)((it >> 22) & 15u);
+  } else {
+    int q_unused;
+    if (!block_map<4>((int)blockIdx.x - extra, rs, v, tile, q_unused)) return;
+  }
+  bwd_tile<TWO>(s, rs, v, tile, chunk, rs.ckpt != nullptr && !TWO, ranges, quad_maxc, sorted_gauss, rec, goff, final_Ts,
+                n_contrib, dL_dcolor, dL_ddepth, dL_dalpha, grow, reach);
+}
+
 void launch_render_backward(const RenderSet& rs, const GeomState& g, const uint32_t* sorted_gauss,
                             const ImageState& img, const float* dL_dcolor, const float* dL_ddepth,
                             const float* dL_dalpha, const BackwardState& bw, hipStream_t stream) {
   const int nt = rs.gx * rs.gy;
   if (nt <= 0 || rs.V <= 0) return;
-  const dim3 grid(block_grid(rs, 4));
+  // split tiles' later chunks: a workgroup per listed item (C3 per view: ~800 items)
+  const bool split = rs.ckpt != nullptr && rs.dpix2 == nullptr && rs.col2 == nullptr;
+  const int extra = split ? GSR_SPLIT_EXTRA : 0;  // (the count k_ckpt_suffix lists at most)
+  const dim3 grid(block_grid(rs, 4) + extra);
+  const uint32_t* items = split ? img.split_items : nullptr;
   if (rs.dpix2 != nullptr)
     hipLaunchKernelGGL(k_render_bwd<true>, grid, dim3(256), 0, stream, rs, (const uint2*)img.ranges,
                        (const uint32_t*)img.quad_maxc, sorted_gauss, (const GaussRec*)g.rec,
                        (const uint32_t*)g.goff, (const float*)img.final_T, (const uint32_t*)img.n_contrib,
-                       dL_dcolor, dL_ddepth, dL_dalpha, bw.grow, bw.reach);
+                       dL_dcolor, dL_ddepth, dL_dalpha, bw.grow, bw.reach, 0, nullptr);
   else
     hipLaunchKernelGGL(k_render_bwd<false>, grid, dim3(256), 0, stream, rs, (const uint2*)img.ranges,
                        (const uint32_t*)img.quad_maxc, sorted_gauss, (const GaussRec*)g.rec,
                        (const uint32_t*)g.goff, (const float*)img.final_T, (const uint32_t*)img.n_contrib,
-                       dL_dcolor, dL_ddepth, dL_dalpha, bw.grow, bw.reach);
+                       dL_dcolor, dL_ddepth, dL_dalpha, bw.grow, bw.reach, extra, items);
+}
+
+// Split backward for small launches (<= GSR_SPLIT_VIEWS views): a launch of few views lasts as long as its
+// deepest tile's backward (one workgroup walks the whole blended prefix), so the forward checkpoints each
+// pixel's state every GSR_SPLIT_CH candidates and the backward replays the chunks in parallel.
+// GSR_BWD_SPLIT=0 turns it off (A/B); the tile-wave forward writes no checkpoints.
+bool split_on(int V) {
+  if (V < 1 || V > GSR_SPLIT_VIEWS) return false;
+  const char* e = getenv("GSR_BWD_SPLIT");
+  if (e != nullptr && strcmp(e, "0") == 0) return false;
+  const char* f = getenv("GSR_FWD_KERNEL");
+  return !(f != nullptr && strcmp(f, "tile") == 0);
 }
 
 }  // namespace gsr
