@@ -334,8 +334,10 @@ def test_split_backward_matches_whole_walk(size, monkeypatch):
     split = gpu_render(scene, cam, [0.3, 0.2, 0.1], grads=g)
     monkeypatch.setenv("GSR_BWD_SPLIT", "0")
     whole = gpu_render(scene, cam, [0.3, 0.2, 0.1], grads=g)
-    for k in ("color", "depth", "alpha", "radii"):
+    for k in ("alpha", "radii"):
         assert np.array_equal(split[k], whole[k]), k
+    for k in ("color", "depth"):  # the split forward sums each chunk's blends, then the chunks
+        assert np.abs(split[k] - whole[k]).max() <= 1e-5 * max(1.0, float(np.abs(whole[k]).max())), k
     for k in ("g_means3D", "g_means2D", "g_opacity", "g_sh", "g_scales", "g_rotations"):
         ref = whole[k].astype(np.float64)
         err = float((np.abs(split[k] - ref) / np.maximum(1.0, np.abs(ref))).max())

@@ -528,9 +528,10 @@ static int set_render(int V, int P, const int* K, int width, int height, const f
     rs.out_col2 = out_color2;
     rs.dpix2 = nullptr;
     rs.order = tile_order_on() ? img.order : nullptr;
-    rs.ckpt = split_on(V) ? img.ckpt : nullptr;
+    rs.ckpt = split_on(V, P, width, height, total) ? img.ckpt : nullptr;
     rs.split_items = img.split_items;
     rs.split_cap = img.split_cap;
+    rs.split_extra = split_extra(V, (size_t)gx * gy);
     rs.V = V;
     rs.v0 = 0;
     rs.P = P;
@@ -659,9 +660,10 @@ static int set_backward(int V, int P, int degree, int M, const int* K, int width
     rs.dpix2 = two ? dL_dcolor2 + (size_t)g0 * 3 * HW : nullptr;
     rs.order = tile_order_on() ? img.order : nullptr;
     // the forward checkpointed the first colour of the whole set (its V)
-    rs.ckpt = split_on(V) && !two && colors_override == nullptr ? img.ckpt : nullptr;
+    rs.ckpt = split_on(V, P, width, height, total) && !two && colors_override == nullptr ? img.ckpt : nullptr;
     rs.split_items = img.split_items;
     rs.split_cap = img.split_cap;
+    rs.split_extra = split_extra(V, (size_t)gx * gy);
     rs.V = g1 - g0;
     rs.v0 = g0;
     rs.P = P;

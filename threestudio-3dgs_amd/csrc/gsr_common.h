@@ -241,14 +241,22 @@ struct BinningState {
   }
 };
 
-// Backward tile splitting for small launches (<= GSR_SPLIT_VIEWS views: the per-view drop-in path, small
-// sets), whose duration is their longest tile's: a tile's blended prefix is walked in chunks of
-// GSR_SPLIT_CH candidates by separate workgroups, each starting from the forward's per-pixel state at its
-// chunk's end; at most GSR_SPLIT_NCK boundaries per tile (the last chunk takes the rest of the list).
-#define GSR_SPLIT_VIEWS 8
+// Backward tile splitting for launches of few tiles (V x tiles <= GSR_SPLIT_MAX_TILES: the per-view drop-in
+// path, small images, small sets), whose duration is their longest tile's: a tile's blended prefix is walked
+// in chunks of GSR_SPLIT_CH candidates by separate workgroups, each starting from the forward's per-pixel
+// state at its chunk's end; at most GSR_SPLIT_NCK boundaries per tile (the last chunk takes the rest).
+#define GSR_SPLIT_MAX_TILES 4096  // one 1024^2 view (measured: 4-view and 64-view x 256^2 sets gain nothing)
 #define GSR_SPLIT_CH 256
 #define GSR_SPLIT_NCK 15
-#define GSR_SPLIT_EXTRA 1024  // backward workgroups that walk the listed later chunks
+__host__ __device__ inline bool split_fits(int V, size_t tiles) {
+  return V >= 1 && tiles > 0 && (size_t)V * tiles <= GSR_SPLIT_MAX_TILES;
+}
+// backward workgroups for the listed later chunks (the list's capacity): a quarter of the set's tiles,
+// 1024 .. 4096 (C3 per view lists ~800)
+__host__ __device__ inline int split_extra(int V, size_t tiles) {
+  const size_t e = (size_t)V * tiles / 4;
+  return e < 1024 ? 1024 : e > 4096 ? 4096 : (int)e;
+}
 #define GSR_CKPT_FIELDS 5  // a plane of T, a plane of float4 (r, g, b, depth)
 // Slot k of a tile (quadrant q's lane l = pixel 64 q + l): T at boundary k GSR_SPLIT_CH (slot 0: unused),
 // then per pixel the colour / depth blended from candidate k CH on: the forward writes each chunk's own sums
@@ -269,7 +277,7 @@ struct ImageState {
   uint32_t* n_contrib; // [V][H*W]
   uint32_t* order;     // [V][super-tiles] each view's 2x2-tile super-tiles, most listed instances first
                        // (written after binning; the blends' dispatch order, gsr_render.hip block_map)
-  float* ckpt;         // sets of <= GSR_SPLIT_VIEWS views: [V][tiles][GSR_SPLIT_NCK + 1][5][256] forward
+  float* ckpt;         // split_fits sets: [V][tiles][GSR_SPLIT_NCK + 1][5][256] forward
                        // chunk states for the split backward (ckpt_offset)
   uint32_t* split_items; // split sets: [0] count, then the tiles' later chunks (gsr_render.hip k_ckpt_suffix)
   uint32_t* split_cap;   // split sets: [V][tiles] the end of the stretch the tile's own workgroup walks
@@ -287,9 +295,9 @@ struct ImageState {
     s.n_contrib = c.take<uint32_t>(nv * (pix > 0 ? pix : 1));
     const size_t st = (size_t)((div_up(W, GSR_TILE_X) + 1) >> 1) * ((div_up(H, GSR_TILE_Y) + 1) >> 1);
     s.order = c.take<uint32_t>(nv * (st > 0 ? st : 1));
-    const bool split = V >= 1 && V <= GSR_SPLIT_VIEWS && tiles > 0;
+    const bool split = split_fits(V, tiles);
     s.ckpt = c.take<float>(split ? ckpt_offset(nv, tiles, 0, 0) : 1);
-    s.split_items = c.take<uint32_t>(split ? 1 + GSR_SPLIT_EXTRA : 1);
+    s.split_items = c.take<uint32_t>(split ? 1 + (size_t)split_extra(V, tiles) : 1);
     s.split_cap = c.take<uint32_t>(split ? nv * tiles : 1);
     if (bytes) *bytes = align_up(c.off, 256);
     return s;

@@ -66,9 +66,11 @@ struct RenderSet {
   float* ckpt;
   uint32_t* split_items;  // with ckpt: the later chunks' backward items (ImageState::split_items)
   uint32_t* split_cap;    // with ckpt: ImageState::split_cap
+  int split_extra;        // with ckpt: split_extra(the set's V, tiles)
 };
-// backward tile splitting on for a launch of V views (GSR_BWD_SPLIT=0 turns it off)
-bool split_on(int V);
+// backward tile splitting on for a set of V views (split_fits) whose forward takes the quadrant-wave kernel
+// (GSR_BWD_SPLIT=0 turns it off); instances = the set's K total
+bool split_on(int V, int P, int width, int height, long long instances);
 // Each view's super-tiles by listed instances, heaviest first (after binning) — gsr_render.hip
 void launch_tile_order(int V, int gx, int gy, const uint2* ranges, uint32_t* order, hipStream_t stream);
 // GSR_TILE_ORDER=raster: the blends dispatch views in turn in raster order (A/B); the order is still written

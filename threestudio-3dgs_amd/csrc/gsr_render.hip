@@ -218,8 +218,12 @@ __global__ __launch_bounds__(64) void k_render_fwd(RenderSet rs,
   for (int base = 0; base < n; base += 64) {
     if (__all(done)) break;
     if (CK && base > 0 && base % GSR_SPLIT_CH == 0 && base <= GSR_SPLIT_NCK * GSR_SPLIT_CH) {
-      // chunk `chunk` ends: its sums into its slot, T into the next one's
+      // chunk `chunk` ends: its sums into its slot and the running totals, T into the next one's slot
       reinterpret_cast<float4*>(ckpt + (size_t)chunk * GSR_CKPT_FIELDS * 256 + 256)[cpix] = make_float4(Pr, Pg, Pb, Pd);
+      Cr += Pr;
+      Cg += Pg;
+      Cb += Pb;
+      D += Pd;
       ++chunk;
       ckpt[(size_t)chunk * GSR_CKPT_FIELDS * 256 + cpix] = T;
       Pr = Pg = Pb = Pd = 0.f;
@@ -265,15 +269,17 @@ __global__ __launch_bounds__(64) void k_render_fwd(RenderSet rs,
       // non-blending lanes run the same arithmetic with alpha = 0 (no change), no selects of state
       const float a_eff = blend ? alpha : 0.0f;
       const float aT = a_eff * T;
-      Cr = fmaf(c.x, aT, Cr);
-      Cg = fmaf(c.y, aT, Cg);
-      Cb = fmaf(c.z, aT, Cb);
-      D = fmaf(b.z, aT, D);
       if (CK) {
+        // the chunk's own sums (added to the totals at its end: the chunked sum, no second accumulation)
         Pr = fmaf(c.x, aT, Pr);
         Pg = fmaf(c.y, aT, Pg);
         Pb = fmaf(c.z, aT, Pb);
         Pd = fmaf(b.z, aT, Pd);
+      } else {
+        Cr = fmaf(c.x, aT, Cr);
+        Cg = fmaf(c.y, aT, Cg);
+        Cb = fmaf(c.z, aT, Cb);
+        D = fmaf(b.z, aT, D);
       }
       if (C2) {
         Er = fmaf(e.x, aT, Er);
@@ -289,6 +295,12 @@ __global__ __launch_bounds__(64) void k_render_fwd(RenderSet rs,
       e = en;
     }
     __syncthreads();
+  }
+  if (CK) {
+    Cr += Pr;
+    Cg += Pg;
+    Cb += Pb;
+    D += Pd;
   }
   if (inside) {
     const size_t pid = (size_t)py * W + px;
@@ -679,7 +691,8 @@ __global__ __launch_bounds__(256) void k_ckpt_suffix(RenderSet rs, const uint32_
     uint32_t cap = 0xffffffffu;
     if (nc > 0) {
       const uint32_t at = atomicAdd(rs.split_items, (uint32_t)nc);
-      const int m = (int)min((uint32_t)nc, at < GSR_SPLIT_EXTRA ? GSR_SPLIT_EXTRA - at : 0u);
+      const uint32_t E = (uint32_t)rs.split_extra;
+      const int m = (int)min((uint32_t)nc, at < E ? E - at : 0u);
       for (int j = 0; j < m; ++j)
         rs.split_items[1 + at + j] = ((uint32_t)vg << 26) | ((uint32_t)(nc - j) << 22) | (uint32_t)tile;
       if (m > 0) cap = (uint32_t)(nc - m + 1) * GSR_SPLIT_CH;
@@ -1287,7 +1300,7 @@ __device__ __forceinline__ void bwd_tile(BwdLDS<TWO>& s, const RenderSet& rs, in
 
 // The backward blend: a workgroup per tile (block_map: heaviest first, XCD-aware), after `extra` workgroups
 // that replay the split tiles' later chunks (split_on: the items k_ckpt_suffix listed, view << 26 | chunk << 22
-// | tile, count in items[0], at most GSR_SPLIT_EXTRA; a heavy tile's chunks run side by side instead of one
+// | tile, count in items[0], at most rs.split_extra; a heavy tile's chunks run side by side instead of one
 // after the other, its own workgroup walks the chunks not listed, from ImageState::split_cap down).
 template <bool TWO>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(TWO ? 4 : 5, 8))) void k_render_bwd(
@@ -1320,7 +1333,7 @@ void launch_render_backward(const RenderSet& rs, const GeomState& g, const uint3
   if (nt <= 0 || rs.V <= 0) return;
   // split tiles' later chunks: a workgroup per listed item (C3 per view: ~800 items)
   const bool split = rs.ckpt != nullptr && rs.dpix2 == nullptr && rs.col2 == nullptr;
-  const int extra = split ? GSR_SPLIT_EXTRA : 0;  // (the count k_ckpt_suffix lists at most)
+  const int extra = split ? rs.split_extra : 0;  // (the count k_ckpt_suffix lists at most)
   const dim3 grid(block_grid(rs, 4) + extra);
   const uint32_t* items = split ? img.split_items : nullptr;
   if (rs.dpix2 != nullptr)
@@ -1335,16 +1348,16 @@ void launch_render_backward(const RenderSet& rs, const GeomState& g, const uint3
                        dL_dcolor, dL_ddepth, dL_dalpha, bw.grow, bw.reach, extra, items);
 }
 
-// Split backward for small launches (<= GSR_SPLIT_VIEWS views): a launch of few views lasts as long as its
-// deepest tile's backward (one workgroup walks the whole blended prefix), so the forward checkpoints each
-// pixel's state every GSR_SPLIT_CH candidates and the backward replays the chunks in parallel.
-// GSR_BWD_SPLIT=0 turns it off (A/B); the tile-wave forward writes no checkpoints.
-bool split_on(int V) {
-  if (V < 1 || V > GSR_SPLIT_VIEWS) return false;
+// Split backward for launches of few tiles (split_fits): such a launch lasts as long as its deepest tile's
+// backward (one workgroup walks the whole blended prefix), so the forward keeps each pixel's state every
+// GSR_SPLIT_CH candidates and the backward replays the chunks in parallel.  Only the quadrant-wave forward
+// writes the states.  GSR_BWD_SPLIT=0 turns it off (A/B).
+bool split_on(int V, int P, int width, int height, long long instances) {
+  const size_t tiles = (size_t)div_up(width, GSR_TILE_X) * div_up(height, GSR_TILE_Y);
+  if (!split_fits(V, tiles)) return false;
   const char* e = getenv("GSR_BWD_SPLIT");
   if (e != nullptr && strcmp(e, "0") == 0) return false;
-  const char* f = getenv("GSR_FWD_KERNEL");
-  return !(f != nullptr && strcmp(f, "tile") == 0);
+  return !fwd_tile_kernel(instances, (long long)V * P, V);
 }
 
 }  // namespace gsr
