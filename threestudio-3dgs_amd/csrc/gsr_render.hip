@@ -408,20 +408,40 @@ __global__ __launch_bounds__(256) void k_tile_info(RenderSet rs, const uint2* __
 // colour, no depth / alpha terms), u_1 = G dL/dalpha_1 and u = u_1 + u_2; 16 sums per candidate:
 //   0-5 the u moments, 6-9 sum w dL/d(r,g,b,depth), 10-12 sum u_1 (1, x, y), 13-15 sum w dL/d(r2,g2,b2)
 // from 4 candidates per product (A rows 0-3 u, 4-7 u_1, 8-11 w; B columns 6-12 the 7 pixel planes).
+//
+// Hit-list variant (HITS; the default for the two-colour backward, where SuGaR's ~13-pixel Gaussians
+// leave most of a product's 64 pixels empty): the replay appends each (pixel, candidate) pair that
+// blended, (u, u_1, w, pixel), to its wave's list (ballot-compacted, candidate after candidate); after
+// the batch one thread per kept (candidate, quadrant) pair of the whole workgroup walks that pair's
+// hits and forms the same sums (moments about the quadrant centre, exact products x^2, x y, y^2 of the
+// half-integer offsets), so a batch's sums cost one pass over its hits on one wave instead of 16
+// matrix-core products per 4 candidates on every wave.  A wave whose list fills sums its finished
+// candidates itself first.  Fixed order per pair: bitwise repeatable.
 #define NGV2 16
 #define GSR_QSUM_STRIDE 41   // floats per candidate: 4 quadrants x 10 raw sums, +1 pad
 #define GSR_QSUM_STRIDE2 65  // two colours: 4 x 16, +1
-template <bool TWO>
+// Hit-list sums (HITS): per wave a buffer of the (pixel, candidate) pairs that blended, HCAP entries
+// (sized so the workgroup keeps 5 / 4 workgroups per CU like the matrix-core variant)
+#define GSR_HCAP1 208
+#define GSR_HCAP2 160
+template <bool TWO, bool HITS>
 struct BwdLDS {
   float4 s0[65], s1[65], s2[65];
   float4 s3[TWO ? 65 : 1];  // two colours: the second colour
   uint32_t slot[64];
+  // per wave: kept candidates of the batch (matrix-core sums: batch index; hit lists: index | first hit
+  // << 8 | hits << 16)
   uint32_t list[4][64];
   float qsum[64 * (TWO ? GSR_QSUM_STRIDE2 : GSR_QSUM_STRIDE)];
   // per wave: the group's A operand, u = G dL/dalpha (slots 0-7) and w = alpha T (slots 8-15) of
   // its 8 candidates, stored so that MFMA lane l's 16 values are 4 chunks of 16 B (swizzled:
   // conflict-free 16-B reads, 2-way 4-B writes)
-  float uw[4][64 * 16];
+  float uw[4][HITS ? 4 : 64 * 16];
+  // hit lists: per wave (u, u_1, w, pixel) of each blended (pixel, candidate), candidate after candidate
+  float4 hits[4][HITS ? (TWO ? GSR_HCAP2 : GSR_HCAP1) : 1];
+  // hit lists: per pixel of each quadrant dL/d(r, g, b, depth) (two colours: + dL/d(r2, g2, b2), 0)
+  float4 planes[4][HITS ? (TWO ? 128 : 64) : 1];
+  uint32_t pend[4];  // hit lists: per wave, kept candidates already summed | kept count << 8
   unsigned long long kmask[4];  // per quadrant: kept candidates of the batch
 #ifdef GSR_TIMELINE
   int tl_cnt[4];
@@ -764,8 +784,8 @@ void launch_render_forward(const RenderSet& rs, const GeomState& g, const uint32
 
 // One workgroup's backward of one tile: the whole blended prefix, or with `split` (split_on) chunk `chunk`,
 // candidates [chunk CH, (chunk + 1) CH) (chunk GSR_SPLIT_NCK: to the end of the prefix).
-template <bool TWO>
-__device__ __forceinline__ void bwd_tile(BwdLDS<TWO>& s, const RenderSet& rs, int v, int tile, int chunk, bool split,
+template <bool TWO, bool HITS>
+__device__ __forceinline__ void bwd_tile(BwdLDS<TWO, HITS>& s, const RenderSet& rs, int v, int tile, int chunk, bool split,
                                          const uint2* __restrict__ ranges, const uint32_t* __restrict__ quad_maxc,
                                          const uint32_t* __restrict__ sorted_gauss, const GaussRec* __restrict__ rec,
                                          const uint32_t* __restrict__ goff, const float* __restrict__ final_Ts,
@@ -777,6 +797,7 @@ __device__ __forceinline__ void bwd_tile(BwdLDS<TWO>& s, const RenderSet& rs, in
   constexpr int GS = TWO ? 4 : 8;                                // candidates per 16x16 product
   constexpr int NPL = TWO ? 7 : 4;                               // dL/dpixel planes in the B operand
   constexpr int RW = TWO ? 4 : 3;                                // float4 per gradient row
+  constexpr int HCAP = TWO ? GSR_HCAP2 : GSR_HCAP1;              // hit-list entries per wave
   GSR_TL_BEGIN
   const int W = rs.W, H = rs.H, grid_x = rs.gx;
   const size_t vgs = (size_t)(rs.v0 + v);
@@ -934,6 +955,7 @@ __device__ __forceinline__ void bwd_tile(BwdLDS<TWO>& s, const RenderSet& rs, in
   // contribute zeros.  Returns per pixel u = G dL/dalpha (the mean2D / conic / opacity
   // gradients are linear in u's moments over the pixel offsets) and w = alpha T (the colour / depth
   // weights); the sums over the quadrant's 64 pixels are formed by the matrix cores (below).
+  bool rhit = false;  // the last replay step blended this lane's pixel (hit lists)
   auto replay = [&](const float4& ga, const float4& gb, const float4& gc, float& u, float& w) {
     const uint32_t rel = __float_as_uint(gb.w);
     const float dx = ga.x - pxf, dy = ga.y - pyf;
@@ -941,6 +963,7 @@ __device__ __forceinline__ void bwd_tile(BwdLDS<TWO>& s, const RenderSet& rs, in
     const float G = __builtin_amdgcn_exp2f(power2);
     const float alpha = fminf(GSR_ALPHA_MAX, gb.y * G);
     const bool hit = rel < last_contributor && power2 <= 0.0f && alpha >= GSR_ALPHA_MIN;
+    rhit = hit;
     const float a_eff = hit ? alpha : 0.0f;
     const float g_eff = hit ? G : 0.0f;
     const float oma = 1.f - a_eff;
@@ -962,6 +985,7 @@ __device__ __forceinline__ void bwd_tile(BwdLDS<TWO>& s, const RenderSet& rs, in
     const float G = __builtin_amdgcn_exp2f(power2);
     const float alpha = fminf(GSR_ALPHA_MAX, gb.y * G);
     const bool hit = rel < last_contributor && power2 <= 0.0f && alpha >= GSR_ALPHA_MIN;
+    rhit = hit;
     const float a_eff = hit ? alpha : 0.0f;
     const float g_eff = hit ? G : 0.0f;
     const float oma = 1.f - a_eff;
@@ -1005,7 +1029,11 @@ __device__ __forceinline__ void bwd_tile(BwdLDS<TWO>& s, const RenderSet& rs, in
   // (other lanes' pixels) goes through LDS once, in the qsum area (first written after the first
   // staging barrier, by which time every wave has read its bv).
   float bv[16];
-  {
+  if constexpr (HITS) {
+    // hit lists: this quadrant's dL/dpixel planes, read per hit by whichever thread sums the pair
+    s.planes[q][TWO ? 2 * lane : lane] = make_float4(dpix[0], dpix[1], dpix[2], dpix_d);
+    if (TWO) s.planes[q][2 * lane + 1] = make_float4(dpix2[0], dpix2[1], dpix2[2], 0.f);
+  } else {
     float* sdp = s.qsum + q * (NPL * 68 + 16);
     sdp[0 * 68 + lane] = dpix[0];
     sdp[1 * 68 + lane] = dpix[1];
@@ -1055,7 +1083,7 @@ __device__ __forceinline__ void bwd_tile(BwdLDS<TWO>& s, const RenderSet& rs, in
   } else {
     useful = (lane < 32) ? (ncol < 6) : dcol;
   }
-  if (TWO) {
+  if (TWO && !HITS) {
     // A rows 12-15 are never written: zero them once (their products are not read either)
 #pragma unroll
     for (int r = 12; r < 16; ++r) s.uw[q][16 * r + wa[3]] = 0.f;
@@ -1063,6 +1091,48 @@ __device__ __forceinline__ void bwd_tile(BwdLDS<TWO>& s, const RenderSet& rs, in
 
   uint32_t* mylist = s.list[q];
   float* myq = s.qsum + q * NG;
+
+  // hit lists: the sums of one kept (candidate, quadrant qq) pair from its hits, list entry e =
+  // batch index | first hit << 8 | hits << 16, into the pair's qsum slots (same fields as the
+  // matrix-core product: x, y = pixel offsets from the quadrant centre)
+  auto sum_pair = [&](int qq, uint32_t e) {
+    const int j = (int)(e & 63u), st = (int)((e >> 8) & 255u), n = (int)(e >> 16);
+    const float4* hb = s.hits[qq];
+    const float4* pl = s.planes[qq];
+    float c[NG];
+#pragma unroll
+    for (int f = 0; f < NG; ++f) c[f] = 0.f;
+    for (int k = st; k < st + n; ++k) {
+      const float4 hv = hb[k];
+      const uint32_t p = __float_as_uint(hv.w);
+      const float x = (float)(p & 7u) - 3.5f, y = (float)(p >> 3) - 3.5f;
+      const float u = hv.x, w = hv.z;
+      c[0] += u;
+      c[1] = fmaf(u, x, c[1]);
+      c[2] = fmaf(u, y, c[2]);
+      c[3] = fmaf(u, x * x, c[3]);  // (x^2, x y, y^2 of half-integers are exact)
+      c[4] = fmaf(u, x * y, c[4]);
+      c[5] = fmaf(u, y * y, c[5]);
+      const float4 d = pl[TWO ? 2 * p : p];
+      c[6] = fmaf(w, d.x, c[6]);
+      c[7] = fmaf(w, d.y, c[7]);
+      c[8] = fmaf(w, d.z, c[8]);
+      c[9] = fmaf(w, d.w, c[9]);
+      if constexpr (TWO) {
+        const float u1 = hv.y;
+        const float4 d2 = pl[2 * p + 1];
+        c[10 % NG] += u1;
+        c[11 % NG] = fmaf(u1, x, c[11 % NG]);
+        c[12 % NG] = fmaf(u1, y, c[12 % NG]);
+        c[13 % NG] = fmaf(w, d2.x, c[13 % NG]);
+        c[14 % NG] = fmaf(w, d2.y, c[14 % NG]);
+        c[15 % NG] = fmaf(w, d2.z, c[15 % NG]);
+      }
+    }
+    float* dst = s.qsum + j * QS + NG * qq;
+#pragma unroll
+    for (int f = 0; f < NG; ++f) dst[f] = c[f];
+  };
   for (int h = hi; h > lo; h -= 64) {
     {
       const int rel_c = h - 1 - cs;
@@ -1120,12 +1190,52 @@ __device__ __forceinline__ void bwd_tile(BwdLDS<TWO>& s, const RenderSet& rs, in
 #ifdef GSR_TIMELINE
     if (lane == 0) s.tl_cnt[q] = cnt;
 #endif
-    if (keep) mylist[mask_rank(bal)] = (uint32_t)lane;
+    if (!HITS && keep) mylist[mask_rank(bal)] = (uint32_t)lane;
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // this wave's list is read back by its own lanes
     // kept candidates in groups of 8: replay -> (u, w) rows in LDS -> matrix-core sums.
     // The kept set is the uniform ballot mask: walk it with scalar bit scans, prefetching the next
     // candidate's staged record while the current one is replayed.
     unsigned long long rest = bal;
+    if constexpr (HITS) {
+      // replay -> the blended lanes' (u, u_1, w, pixel) appended to the wave's hit list; the sums wait
+      // for the batch's end (below) unless the list fills first
+      int fill = 0, done = 0;  // (wave-uniform) entries in use; kept candidates already summed
+      if (cnt > 0) {
+        int j = (int)__builtin_ctzll(rest);
+        float4 ca = s.s0[j], cb = s.s1[j], cc = s.s2[j];
+        float4 cd2 = TWO ? s.s3[j] : zero4;
+        for (int c = 0; c < cnt; ++c) {
+          rest &= rest - 1ull;
+          const int jn = (c + 1 < cnt) ? (int)__builtin_ctzll(rest) : j;
+          const float4 na = s.s0[jn], nb = s.s1[jn], nc = s.s2[jn];
+          const float4 nd = TWO ? s.s3[jn] : zero4;
+          float u, u1 = 0.f, w;
+          if (TWO)
+            replay2(ca, cb, cc, cd2, u, u1, w);
+          else
+            replay(ca, cb, cc, u, w);
+          const unsigned long long hm = __ballot(rhit);
+          const int n = __popcll(hm);
+          if (fill + n > HCAP) {
+            // list full: this wave sums its finished candidates now (one lane each), then starts over
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            if (lane < c - done) sum_pair(q, mylist[done + lane]);
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // (in-order LDS: read before rewritten)
+            fill = 0;
+            done = c;
+          }
+          if (rhit) s.hits[q][fill + (int)mask_rank(hm)] = make_float4(u, u1, w, __uint_as_float((uint32_t)lane));
+          if (lane == 0) mylist[c] = (uint32_t)j | ((uint32_t)fill << 8) | ((uint32_t)n << 16);
+          fill += n;
+          ca = na;
+          cb = nb;
+          cc = nc;
+          cd2 = nd;
+          j = jn;
+        }
+      }
+      if (lane == 0) s.pend[q] = (uint32_t)done | ((uint32_t)cnt << 8);
+    } else
 #ifdef GSR_EXP_NOGROUP
     if (cnt < 0)
 #endif
@@ -1196,6 +1306,23 @@ __device__ __forceinline__ void bwd_tile(BwdLDS<TWO>& s, const RenderSet& rs, in
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // rows are rewritten by the next group
     }
     __syncthreads();
+    if constexpr (HITS) {
+      // the batch's remaining kept (candidate, quadrant) pairs of all four waves, one per thread in
+      // quadrant order (a C5 batch has ~40: one wave sums them, the others' SIMDs serve other workgroups)
+      int qq = -1, idx = 0, base = 0;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const uint32_t pk = s.pend[k];
+        const int d0 = (int)(pk & 255u), np = (int)(pk >> 8) - d0;
+        if (qq < 0 && t < base + np) {
+          qq = k;
+          idx = d0 + t - base;
+        }
+        base += np;
+      }
+      if (qq >= 0) sum_pair(qq, s.list[qq][idx]);
+      __syncthreads();
+    }
 #ifdef GSR_TIMELINE
     if (t == 0) {
       const int c0 = s.tl_cnt[0], c1 = s.tl_cnt[1], c2 = s.tl_cnt[2], c3 = s.tl_cnt[3];
@@ -1302,14 +1429,14 @@ __device__ __forceinline__ void bwd_tile(BwdLDS<TWO>& s, const RenderSet& rs, in
 // that replay the split tiles' later chunks (split_on: the items k_ckpt_suffix listed, view << 26 | chunk << 22
 // | tile, count in items[0], at most rs.split_extra; a heavy tile's chunks run side by side instead of one
 // after the other, its own workgroup walks the chunks not listed, from ImageState::split_cap down).
-template <bool TWO>
+template <bool TWO, bool HITS>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(TWO ? 4 : 5, 8))) void k_render_bwd(
     RenderSet rs, const uint2* __restrict__ ranges, const uint32_t* __restrict__ quad_maxc,
     const uint32_t* __restrict__ sorted_gauss, const GaussRec* __restrict__ rec, const uint32_t* __restrict__ goff,
     const float* __restrict__ final_Ts, const uint32_t* __restrict__ n_contrib, const float* __restrict__ dL_dcolor,
     const float* __restrict__ dL_ddepth, const float* __restrict__ dL_dalpha, float4* __restrict__ grow,
     unsigned long long* __restrict__ reach, int extra, const uint32_t* __restrict__ items) {
-  __shared__ BwdLDS<TWO> s;
+  __shared__ BwdLDS<TWO, HITS> s;
   int v, tile, chunk = 0;
   if (!TWO && (int)blockIdx.x < extra) {
     if (blockIdx.x >= items[0]) return;
@@ -1322,8 +1449,18 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(TWO ? 4 : 5
     int q_unused;
     if (!block_map<4>((int)blockIdx.x - extra, rs, v, tile, q_unused)) return;
   }
-  bwd_tile<TWO>(s, rs, v, tile, chunk, rs.ckpt != nullptr && !TWO, ranges, quad_maxc, sorted_gauss, rec, goff, final_Ts,
+  bwd_tile<TWO, HITS>(s, rs, v, tile, chunk, rs.ckpt != nullptr && !TWO, ranges, quad_maxc, sorted_gauss, rec, goff, final_Ts,
                 n_contrib, dL_dcolor, dL_ddepth, dL_dalpha, grow, reach);
+}
+
+// Sums of the backward blend: hit lists (HITS) or matrix-core products.  Hit lists win where the
+// Gaussians are small (the two-colour SuGaR backward, C5); the matrix cores where they are large (C3).
+// GSR_BWD_SUMS=hits / mfma forces one (A/B).
+static bool bwd_hit_lists(bool two) {
+  const char* e = getenv("GSR_BWD_SUMS");
+  if (e != nullptr && strcmp(e, "hits") == 0) return true;
+  if (e != nullptr && strcmp(e, "mfma") == 0) return false;
+  return two;
 }
 
 void launch_render_backward(const RenderSet& rs, const GeomState& g, const uint32_t* sorted_gauss,
@@ -1336,16 +1473,13 @@ void launch_render_backward(const RenderSet& rs, const GeomState& g, const uint3
   const int extra = split ? rs.split_extra : 0;  // (the count k_ckpt_suffix lists at most)
   const dim3 grid(block_grid(rs, 4) + extra);
   const uint32_t* items = split ? img.split_items : nullptr;
-  if (rs.dpix2 != nullptr)
-    hipLaunchKernelGGL(k_render_bwd<true>, grid, dim3(256), 0, stream, rs, (const uint2*)img.ranges,
-                       (const uint32_t*)img.quad_maxc, sorted_gauss, (const GaussRec*)g.rec,
-                       (const uint32_t*)g.goff, (const float*)img.final_T, (const uint32_t*)img.n_contrib,
-                       dL_dcolor, dL_ddepth, dL_dalpha, bw.grow, bw.reach, 0, nullptr);
-  else
-    hipLaunchKernelGGL(k_render_bwd<false>, grid, dim3(256), 0, stream, rs, (const uint2*)img.ranges,
-                       (const uint32_t*)img.quad_maxc, sorted_gauss, (const GaussRec*)g.rec,
-                       (const uint32_t*)g.goff, (const float*)img.final_T, (const uint32_t*)img.n_contrib,
-                       dL_dcolor, dL_ddepth, dL_dalpha, bw.grow, bw.reach, extra, items);
+  const bool hits = bwd_hit_lists(rs.dpix2 != nullptr);
+  auto kern = rs.dpix2 != nullptr ? (hits ? k_render_bwd<true, true> : k_render_bwd<true, false>)
+                                  : (hits ? k_render_bwd<false, true> : k_render_bwd<false, false>);
+  hipLaunchKernelGGL(kern, grid, dim3(256), 0, stream, rs, (const uint2*)img.ranges, (const uint32_t*)img.quad_maxc,
+                     sorted_gauss, (const GaussRec*)g.rec, (const uint32_t*)g.goff, (const float*)img.final_T,
+                     (const uint32_t*)img.n_contrib, dL_dcolor, dL_ddepth, dL_dalpha, bw.grow, bw.reach,
+                     rs.dpix2 != nullptr ? 0 : extra, rs.dpix2 != nullptr ? nullptr : items);
 }
 
 // Split backward for launches of few tiles (split_fits): such a launch lasts as long as its deepest tile's
