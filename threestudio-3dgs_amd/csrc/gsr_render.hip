@@ -1210,10 +1210,16 @@ __device__ __forceinline__ void bwd_tile(BwdLDS<TWO, HITS>& s, const RenderSet& 
           const float4 na = s.s0[jn], nb = s.s1[jn], nc = s.s2[jn];
           const float4 nd = TWO ? s.s3[jn] : zero4;
           float u, u1 = 0.f, w;
+#ifdef GSR_EXP_NOREPLAY
+          u = ca.x * pxf;
+          w = cb.x * pyf;
+          rhit = ((lane + j) & 7) == 0;
+#else
           if (TWO)
             replay2(ca, cb, cc, cd2, u, u1, w);
           else
             replay(ca, cb, cc, u, w);
+#endif
           const unsigned long long hm = __ballot(rhit);
           const int n = __popcll(hm);
           if (fill + n > HCAP) {
@@ -1320,6 +1326,9 @@ __device__ __forceinline__ void bwd_tile(BwdLDS<TWO, HITS>& s, const RenderSet& 
         }
         base += np;
       }
+#ifdef GSR_EXP_NOPHASE2
+      qq = -1;
+#endif
       if (qq >= 0) sum_pair(qq, s.list[qq][idx]);
       __syncthreads();
     }
