@@ -945,7 +945,9 @@ __device__ __forceinline__ void bwd_tile(BwdLDS<TWO, HITS>& s, const RenderSet& 
       }
       if (piece == 3) {
         ngo = goff[g0];
+#ifndef GSR_EXP_NOREACH
         atomicOr(reach32 + 2 * g0, vbit);  // the Gaussian gets a row in this view (k_view_grad reads it)
+#endif
       }
     }
     if (hi - 64 > lo) gi_next = fetch_index(hi - 64);
@@ -1164,7 +1166,9 @@ __device__ __forceinline__ void bwd_tile(BwdLDS<TWO, HITS>& s, const RenderSet& 
           }
           if (piece == 3) {
             ngo = goff[gi_next];
+#ifndef GSR_EXP_NOREACH
             atomicOr(reach32 + 2 * gi_next, vbit);
+#endif
           }
         }
         if (h - 128 > lo) gi_next = fetch_index(h - 128);
@@ -1200,7 +1204,11 @@ __device__ __forceinline__ void bwd_tile(BwdLDS<TWO, HITS>& s, const RenderSet& 
       // replay -> the blended lanes' (u, u_1, w, pixel) appended to the wave's hit list; the sums wait
       // for the batch's end (below) unless the list fills first
       int fill = 0, done = 0;  // (wave-uniform) entries in use; kept candidates already summed
+#ifdef GSR_EXP_NOGROUP
+      if (cnt < 0) {
+#else
       if (cnt > 0) {
+#endif
         int j = (int)__builtin_ctzll(rest);
         float4 ca = s.s0[j], cb = s.s1[j], cc = s.s2[j];
         float4 cd2 = TWO ? s.s3[j] : zero4;
