@@ -1097,11 +1097,10 @@ __device__ __forceinline__ void bwd_tile(BwdLDS<TWO, HITS>& s, const RenderSet& 
   // hit lists: the sums of one kept (candidate, quadrant qq) pair from its hits, list entry e =
   // batch index | first hit << 8 | hits << 16, into the pair's qsum slots (same fields as the
   // matrix-core product: x, y = pixel offsets from the quadrant centre)
-  auto sum_pair = [&](int qq, uint32_t e) {
-    const int j = (int)(e & 63u), st = (int)((e >> 8) & 255u), n = (int)(e >> 16);
+  auto pair_sums = [&](int qq, uint32_t e, float (&c)[NG]) {
+    const int st = (int)((e >> 8) & 255u), n = (int)(e >> 16);
     const float4* hb = s.hits[qq];
     const float4* pl = s.planes[qq];
-    float c[NG];
 #pragma unroll
     for (int f = 0; f < NG; ++f) c[f] = 0.f;
     for (int k = st; k < st + n; ++k) {
@@ -1131,7 +1130,12 @@ __device__ __forceinline__ void bwd_tile(BwdLDS<TWO, HITS>& s, const RenderSet& 
         c[15 % NG] = fmaf(w, d2.z, c[15 % NG]);
       }
     }
-    float* dst = s.qsum + j * QS + NG * qq;
+  };
+  // (a list that filled: its finished pairs' sums wait in qsum for the flush)
+  auto sum_pair = [&](int qq, uint32_t e) {
+    float c[NG];
+    pair_sums(qq, e, c);
+    float* dst = s.qsum + (int)(e & 63u) * QS + NG * qq;
 #pragma unroll
     for (int f = 0; f < NG; ++f) dst[f] = c[f];
   };
@@ -1320,26 +1324,7 @@ __device__ __forceinline__ void bwd_tile(BwdLDS<TWO, HITS>& s, const RenderSet& 
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // rows are rewritten by the next group
     }
     __syncthreads();
-    if constexpr (HITS) {
-      // the batch's remaining kept (candidate, quadrant) pairs of all four waves, one per thread in
-      // quadrant order (a C5 batch has ~40: one wave sums them, the others' SIMDs serve other workgroups)
-      int qq = -1, idx = 0, base = 0;
-#pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        const uint32_t pk = s.pend[k];
-        const int d0 = (int)(pk & 255u), np = (int)(pk >> 8) - d0;
-        if (qq < 0 && t < base + np) {
-          qq = k;
-          idx = d0 + t - base;
-        }
-        base += np;
-      }
-#ifdef GSR_EXP_NOPHASE2
-      qq = -1;
-#endif
-      if (qq >= 0) sum_pair(qq, s.list[qq][idx]);
-      __syncthreads();
-    }
+    // (hit lists: the pairs the lists still hold are summed by their flush threads below)
 #ifdef GSR_TIMELINE
     if (t == 0) {
       const int c0 = s.tl_cnt[0], c1 = s.tl_cnt[1], c2 = s.tl_cnt[2], c3 = s.tl_cnt[3];
@@ -1370,7 +1355,21 @@ __device__ __forceinline__ void bwd_tile(BwdLDS<TWO, HITS>& s, const RenderSet& 
 #pragma unroll
       for (int i = 0; i < NM; ++i) m[i] = 0.f;
       if ((s.kmask[qq] >> cs) & 1ull) {
-        const float* C = s.qsum + cs * QS + NG * qq;
+        float Cv[NG];
+        if constexpr (HITS) {
+          // this (candidate, quadrant) pair's sums: from its hits, or from qsum when its wave's list filled
+          // before the batch's end (its rank among the quadrant's kept candidates is below pend's count)
+          const int rank = __popcll(s.kmask[qq] & ((1ull << cs) - 1ull));
+          if (rank >= (int)(s.pend[qq] & 255u)) {
+#pragma unroll
+            for (int f = 0; f < NG; ++f) Cv[f] = 0.f;
+            pair_sums(qq, s.list[qq][rank], Cv);
+          } else {
+#pragma unroll
+            for (int f = 0; f < NG; ++f) Cv[f] = s.qsum[cs * QS + NG * qq + f];
+          }
+        }
+        const float* C = HITS ? Cv : s.qsum + cs * QS + NG * qq;
         const float mx = ga.x - ((float)(txi * GSR_TILE_X + (qq & 1) * 8) + 3.5f);
         const float my = ga.y - ((float)(tyi * GSR_TILE_Y + (qq >> 1) * 8) + 3.5f);
         m[0] = C[0];
