@@ -73,6 +73,8 @@ def parse():
                     help="PMC summary (profiles/summarize.py) supplying roofline.traffic and the VALU counts")
     ap.add_argument("--pairs", default=os.path.join(ROOT, "profiles", "r03_pairs.json"),
                     help="device-counted blend pairs (profiles/diag_pairs.py) for the VALU roofline")
+    ap.add_argument("--traffic-sugar", default=os.path.join(ROOT, "profiles", "r03d_sugar_traffic.json"),
+                    help="PMC summary of the C5 line (--workload sugar, profiles/summarize.py r03d_sugar)")
     ap.add_argument("--overlap-reduce", choices=["on", "off"], default="on",
                     help="N > 1: sum the Gaussian gradients over ranks inside the backward, range by range as the "
                          "per-Gaussian backward forms them (view_shard.ChunkedGradReduce, overlapped on a side "
@@ -432,13 +434,23 @@ def roofline_fields(args, phases, Ks, Ls, H, W):
     # fewer views: the per-launch counts scale with the views (per-view work is the same)
     profiled = (args.workload == "c3" and args.epilogue == "background" and args.res == 1024
                 and args.gaussians == 1_000_000 and args.sh_degree == 3 and args.path == "batched")
+    # the C5 line's counters (profiles/summarize.py r03d_sugar: the same command with --workload sugar)
+    sugar = (args.workload == "sugar" and args.res == 800 and args.sh_degree == 3 and args.path == "batched"
+             and not SUGAR_SEPARATE)
+    traffic_path = args.traffic_sugar if sugar else args.traffic
     pairs = read_json(args.pairs) if profiled else None
     out = {}
     n_fw = max(1, len(Ks))
     rows = {}
     # the forward of this workload: the tile-wave kernel when Gaussians span >= 3 tiles (gsr_render.hip)
     fwd_names = ["k_render_fwd_tile<false>", "k_render_fwd<false>", "k_render_fwd"]
-    bwd_names = ["k_render_bwd<false>", "k_render_bwd"]
+    bwd_names = ["k_render_bwd<false, false>", "k_render_bwd<false>", "k_render_bwd"]
+    if sugar:  # both SuGaR calls in one two-colour blend (quadrant waves) and one hit-list backward
+        fwd_names = ["k_render_fwd<true, false>", "k_render_fwd<true>"]
+        bwd_names = ["k_render_bwd<true, true>", "k_render_bwd<true, false>", "k_render_bwd<true>"]
+        profiled_here = True
+    else:
+        profiled_here = profiled
     for phase, kernel in (("render_fwd", fwd_names), ("render_bwd", bwd_names)):
         ms, n = phases[phase]
         n = max(1, n)
@@ -450,8 +462,8 @@ def roofline_fields(args, phases, Ks, Ls, H, W):
         gbs = alg / sec / 1e9 if sec > 0 else 0.0
         views_per_launch = n_fw / n
         scale = views_per_launch / PROFILE_VIEWS_PER_LAUNCH
-        traffic = read_traffic(args.traffic, kernel) if profiled else None
-        valu = read_traffic(args.traffic, kernel, "valu_insts_per_launch") if profiled else None
+        traffic = read_traffic(traffic_path, kernel) if profiled_here else None
+        valu = read_traffic(traffic_path, kernel, "valu_insts_per_launch") if profiled_here else None
         traffic = round(traffic * scale) if traffic is not None else None
         valu = round(valu * scale) if valu is not None else None
         r = {"kernel": "k_render_bwd" if phase == "render_bwd" else "k_render_fwd (tile / quadrant waves)",
@@ -478,19 +490,22 @@ def roofline_fields(args, phases, Ks, Ls, H, W):
                 v["lockstep_slots_per_kept_pair"] = round(pairs["bwd_lockstep_slots_per_kept_pair"], 3)
         if v:
             v["peak_insts_per_s"] = VALU_PEAK_INSTS
-            v["source"] = ("SQ_INSTS_VALU: " + os.path.relpath(args.traffic, ROOT) +
+            v["source"] = ("SQ_INSTS_VALU: " + os.path.relpath(traffic_path, ROOT) +
                            ("; pairs: " + os.path.relpath(args.pairs, ROOT) if pairs else ""))
             r["valu"] = v
         r["limiter"] = "VALU issue / LDS latency per (pixel, Gaussian) pair, not HBM (see counter_frac, valu)"
+        if sugar and phase == "render_bwd":
+            r["limiter"] = ("waits: waves parked on the batch barriers behind the busiest quadrant and on the "
+                            "staging gathers (2/3 of wave cycles, profiles/r03/sq_c5/), not HBM")
         rows[phase] = r
     dominant = max(phases.items(), key=lambda kv: kv[1][0])[0]
     blend = "render_bwd" if phases["render_bwd"][0] >= phases["render_fwd"][0] else "render_fwd"
     out["roofline"] = rows[blend]
     out["roofline_fwd_blend"] = rows["render_fwd"]
     out["dominant_kernel"] = dominant
-    if not profiled:
+    if not profiled and not sugar:
         out["counters_note"] = ("no counter fields: profiles/ holds PMC counters of the default workload "
-                                "(C3 background path, 1M, 1024^2) only")
+                                "(C3 background path, 1M, 1024^2) and of the C5 line only")
     out["roofline_note"] = ("frac = SURVEY.md §8d algorithmic bytes / HIP-event duration (backward without the "
                             "reference's 80 B/instance atomic RMW, never performed here); counter_frac = PMC HBM "
                             "bytes / duration; valu_frac = SQ_INSTS_VALU / (duration x VALU issue peak). Both "
