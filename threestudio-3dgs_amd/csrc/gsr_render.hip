@@ -205,7 +205,9 @@ __global__ __launch_bounds__(64) void k_render_fwd(RenderSet rs,
     const uint32_t g0 = sorted_gauss[range.x + lane] & gmask;
     n0 = rec[g0].a;
     n1 = rec[g0].b;
+#ifndef GSR_EXP_FWD_NOC
     n2 = rec[g0].c;
+#endif
     if (C2) n3 = make_float4(col2[3 * g0], col2[3 * g0 + 1], col2[3 * g0 + 2], 0.f);
   }
   if (64 + lane < n) gi_next = sorted_gauss[range.x + 64 + lane] & gmask;
@@ -233,7 +235,9 @@ __global__ __launch_bounds__(64) void k_render_fwd(RenderSet rs,
     if (base + 64 + lane < n) {
       n0 = rec[gi_next].a;
       n1 = rec[gi_next].b;
+#ifndef GSR_EXP_FWD_NOC
       n2 = rec[gi_next].c;
+#endif
       if (C2) n3 = make_float4(col2[3 * gi_next], col2[3 * gi_next + 1], col2[3 * gi_next + 2], 0.f);
     }
     if (base + 128 + lane < n) gi_next = sorted_gauss[range.x + base + 128 + lane] & gmask;
