@@ -16,9 +16,11 @@ SH3, background path: bg = 0, then composite with a (H, W, 3) background image +
 (4 elevations x 16 azimuths), views sharded across ranks (strong scaling: the 64-view batch is fixed).
 
 Single GPU:  python bench.py [--steps K --warmup W]
-N GPUs:      python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 \
+N GPUs:      python bench.py --gpus N ...   (starts N ranks itself through torch.distributed.run), or
+             python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 \
                  --master-port P bench.py --gpus N --steps K --warmup W
-Rank 0 prints one JSON line.
+--gpus must equal the launched world size.  Rank 0 prints one JSON line; at N = 1 it carries the C5 (SuGaR
+normal renderer) and 8-view-set lines as sub-objects (--extra-lines).
 """
 from __future__ import annotations
 
@@ -80,11 +82,16 @@ def parse():
                          "per-Gaussian backward forms them (view_shard.ChunkedGradReduce, overlapped on a side "
                          "stream) instead of one flat all-reduce after it")
     ap.add_argument("--grad-chunks", type=int, default=4, help="Gaussian ranges of the overlapped reduction")
-    ap.add_argument("--gather", choices=["overlap", "sync"], default="overlap",
-                    help="N > 1: the image all-gather runs asynchronously beside the backward (overlap: the step's "
-                         "loss decomposes over views — fixed per-view upstream gradients, as MVDream's per-group "
-                         "guidance with group-aligned shards — so a view's gradient needs only its own rank's "
-                         "image; the gathered batch is awaited before the step ends) or before it (sync)")
+    ap.add_argument("--gather", choices=["overlap", "sync"], default="sync",
+                    help="N > 1: the image all-gather completes before the backward (sync, the headline: the "
+                         "reference's guidance consumes the gathered comp_rgb before loss.backward(), "
+                         "system/gaussian_splatting.py:65-67,129), or runs asynchronously beside it (overlap: valid "
+                         "when the loss decomposes over views or rank-aligned view groups; with sync the overlapped "
+                         "variant is timed after the headline and reported as gather_overlap)")
+    ap.add_argument("--extra-lines", default="c5,views8",
+                    help="N = 1, default workload: secondary workloads timed after the headline and reported as "
+                         "sub-objects (c5: BASELINE configs[4], the SuGaR normal renderer; views8: a rank's 8-view "
+                         "share of the batch at N = 8); 'none' to skip")
     ap.add_argument("--per-view-views", type=int, default=16,
                     help="views of the drop-in per-view path (one GaussianRasterizer call per view, the "
                          "reference's loop) timed after the headline, reported beside it (0 = skip)")
@@ -259,21 +266,23 @@ def render_views_sugar(rep: Replica, settings, shade):
 
 
 PROFILE_VIEWS_PER_LAUNCH = 64  # profiles/run_profiles.sh: bench.py defaults, one 64-view set per launch
+# the blend kernels the committed counters must name (forward, backward), as rocprofv3 demangles them: C3's
+# 64-view launch takes the tile-wave forward and the matrix-core backward; C5 the two-colour quadrant-wave
+# forward and the hit-list backward (gsr_render.hip fwd_tile_kernel / bwd_hit_lists)
+KERNELS = {"c3": ("k_render_fwd_tile<false>", "k_render_bwd<false, false>"),
+           "sugar": ("k_render_fwd<true, false>", "k_render_bwd<true, true>")}
 
 
 def read_traffic(path, kernel, field="per_launch_bytes"):
-    """Per-launch value of `kernel` (a name or a list of names, first found wins) from a committed PMC
-    summary (profiles/summarize.py): HBM bytes (FETCH_SIZE x2 gfx950 correction + WRITE_SIZE, separate
-    --pmc passes) or SQ_INSTS_VALU; None if absent."""
+    """Per-launch value of `kernel` (its exact demangled name, KERNELS) from a committed PMC summary
+    (profiles/summarize.py): HBM bytes (FETCH_SIZE x2 gfx950 correction + WRITE_SIZE, separate --pmc passes)
+    or SQ_INSTS_VALU; None if the file holds no counters of that kernel."""
     try:
         with open(path) as f:
             t = json.load(f)[field]
     except (OSError, KeyError, ValueError, TypeError):
         return None
-    for k in ([kernel] if isinstance(kernel, str) else kernel):
-        if k in t:
-            return float(t[k])
-    return None
+    return float(t[kernel]) if kernel in t else None
 
 
 def read_json(path):
@@ -442,16 +451,10 @@ def roofline_fields(args, phases, Ks, Ls, H, W):
     out = {}
     n_fw = max(1, len(Ks))
     rows = {}
-    # the forward of this workload: the tile-wave kernel when Gaussians span >= 3 tiles (gsr_render.hip)
-    fwd_names = ["k_render_fwd_tile<false>", "k_render_fwd<false>", "k_render_fwd"]
-    bwd_names = ["k_render_bwd<false, false>", "k_render_bwd<false>", "k_render_bwd"]
-    if sugar:  # both SuGaR calls in one two-colour blend (quadrant waves) and one hit-list backward
-        fwd_names = ["k_render_fwd<true, false>", "k_render_fwd<true>"]
-        bwd_names = ["k_render_bwd<true, true>", "k_render_bwd<true, false>", "k_render_bwd<true>"]
-        profiled_here = True
-    else:
-        profiled_here = profiled
-    for phase, kernel in (("render_fwd", fwd_names), ("render_bwd", bwd_names)):
+    names = KERNELS["sugar" if sugar else "c3"]
+    profiled_here = profiled or sugar
+    stale = []
+    for phase, kernel in (("render_fwd", names[0]), ("render_bwd", names[1])):
         ms, n = phases[phase]
         n = max(1, n)
         if phase == "render_fwd":
@@ -462,12 +465,16 @@ def roofline_fields(args, phases, Ks, Ls, H, W):
         gbs = alg / sec / 1e9 if sec > 0 else 0.0
         views_per_launch = n_fw / n
         scale = views_per_launch / PROFILE_VIEWS_PER_LAUNCH
-        traffic = read_traffic(traffic_path, kernel) if profiled_here else None
-        valu = read_traffic(traffic_path, kernel, "valu_insts_per_launch") if profiled_here else None
+        # the forward kernel depends on the views per launch (gsr_render.hip fwd_tile_kernel: the tile-wave
+        # kernel from 48 views): its counters apply to the profiled 64-view launch only
+        use = profiled_here and (phase == "render_bwd" or views_per_launch == PROFILE_VIEWS_PER_LAUNCH)
+        traffic = read_traffic(traffic_path, kernel) if use else None
+        valu = read_traffic(traffic_path, kernel, "valu_insts_per_launch") if use else None
+        if use and traffic is None:
+            stale.append(kernel)
         traffic = round(traffic * scale) if traffic is not None else None
         valu = round(valu * scale) if valu is not None else None
-        r = {"kernel": "k_render_bwd" if phase == "render_bwd" else "k_render_fwd (tile / quadrant waves)",
-             "bound": "hbm",
+        r = {"kernel": kernel, "bound": "hbm",
              "achieved": round(gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
              "frac": round(gbs / HBM_PEAK_GBS, 4), "traffic": traffic, "avg_launch_us": round(1e6 * sec, 2),
              "algorithmic_bytes": round(alg), "views_per_launch": round(views_per_launch, 2)}
@@ -475,6 +482,8 @@ def roofline_fields(args, phases, Ks, Ls, H, W):
             r["counter_frac"] = round(traffic / sec / (HBM_PEAK_GBS * 1e9), 4)
         if phase == "render_bwd":
             r["reference_rmw_bytes"] = round(80.0 * sum(Ls) / n)
+        if traffic is not None:
+            r["counters"] = {"file": os.path.relpath(traffic_path, ROOT), "kernel": kernel}
         v = {}
         if valu is not None and sec > 0:
             v["insts_per_launch"] = valu
@@ -506,6 +515,9 @@ def roofline_fields(args, phases, Ks, Ls, H, W):
     if not profiled and not sugar:
         out["counters_note"] = ("no counter fields: profiles/ holds PMC counters of the default workload "
                                 "(C3 background path, 1M, 1024^2) and of the C5 line only")
+    elif stale:
+        out["counters_note"] = (f"no counter fields for {', '.join(stale)}: {os.path.relpath(traffic_path, ROOT)} "
+                                "holds no counters of that kernel (profiled on another build)")
     out["roofline_note"] = ("frac = SURVEY.md §8d algorithmic bytes / HIP-event duration (backward without the "
                             "reference's 80 B/instance atomic RMW, never performed here); counter_frac = PMC HBM "
                             "bytes / duration; valu_frac = SQ_INSTS_VALU / (duration x VALU issue peak). Both "
@@ -513,28 +525,42 @@ def roofline_fields(args, phases, Ks, Ls, H, W):
     return out
 
 
-def main():
-    args = parse()
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
-        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        # GSR_BENCH_BACKEND=gloo / GSR_BENCH_SHARE_GPU=1: rehearse the multi-rank path on a one-GPU box
-        if os.environ.get("GSR_BENCH_SHARE_GPU") == "1":
-            local = 0
-        torch.cuda.set_device(local)
-        backend = os.environ.get("GSR_BENCH_BACKEND", "nccl")
-        comm = "RCCL" if backend == "nccl" else backend
-        if backend == "nccl":
-            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-        else:
-            dist.init_process_group(backend)
-    elif os.environ.get("GSR_BENCH_SHARE_GPU") == "1":
-        local = 0
-    device = torch.device("cuda", local)
-    torch.cuda.set_device(device)
+def _free_port():
+    import socket
 
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def launch_command(args_list, n):
+    """The torchrun command that runs this script as n ranks (one process per GPU), as the driver does."""
+    return [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+            "--master-addr", "127.0.0.1", f"--master-port={_free_port()}", os.path.abspath(__file__)] + list(args_list)
+
+
+def launch_ranks(args_list, n):
+    """`python bench.py --gpus N` without a launcher: start the N ranks as child processes (nothing here has
+    touched the GPU yet) and return their exit status."""
+    import subprocess
+
+    log(f"[bench] --gpus {n} without WORLD_SIZE: launching {n} ranks (torch.distributed.run)")
+    return subprocess.call(launch_command(args_list, n))
+
+
+def check_world(gpus, world):
+    """--gpus must name the world the ranks run in (a mismatch would report another configuration)."""
+    if gpus != world:
+        raise SystemExit(f"bench.py: --gpus {gpus} but WORLD_SIZE={world}: launch one rank per GPU "
+                         f"(python bench.py --gpus {gpus}, or torch.distributed.run --nproc-per-node {gpus})")
+
+
+def run_workload(args, world, rank, device, comm, headline=True):
+    """Build the workload of `args`, run W warm-up and K timed steps (barrier + synchronize on both sides, max
+    over ranks) and return (result dict on rank 0 else None, scene).  headline: also the per-view-path and
+    distCUDA2 lines and, for N > 1, the overlapped-gather variant of the same step."""
     import gsr_synthetic as gs
     from diff_gaussian_rasterization import _C
     from diff_gaussian_rasterization.view_shard import (ChunkedGradReduce, all_gather_views, all_gather_views_async,
@@ -570,7 +596,8 @@ def main():
     # the per-view path's backgrounds: one leaf per view (the background network's per-view output)
     bg_views = [bg_img[i].detach().clone().requires_grad_(True) for i in range(len(mine))] \
         if args.path == "per-view" else []
-    log(f"[bench] rank {rank}/{world}: setup {time.perf_counter() - t_setup:.1f}s, {len(mine)} views/rank")
+    log(f"[bench] rank {rank}/{world}: {args.workload} setup {time.perf_counter() - t_setup:.1f}s, "
+        f"{len(mine)} views/rank")
 
     settings = [settings_for(rep, cam, bg_zero) for cam in mine]
     up_c = torch.stack([u[0] for u in upstream]) if upstream else None
@@ -585,14 +612,18 @@ def main():
         up_n = torch.randn((len(mine), 3, H, W), generator=gen, device=device)
 
     pending = []
+    gather_mode = [args.gather]
 
     def gather(img):
         # forward exchange: every rank receives the whole batch of rendered images (the composited RGB the
-        # batch renderer returns; depth / alpha terms are per view)
-        if args.gather == "overlap":
+        # batch renderer returns; depth / alpha terms are per view).  sync: the gathered batch exists before the
+        # backward starts, as in the reference's step, where the guidance consumes comp_rgb before
+        # loss.backward() (system/gaussian_splatting.py:65-67,129)
+        if gather_mode[0] == "overlap":
             pending.append(all_gather_views_async(img, args.views))
         else:
-            all_gather_views(img, args.views)
+            full = all_gather_views(img, args.views)
+            return full
 
     def step():
         if args.workload == "sugar":
@@ -632,6 +663,23 @@ def main():
         for b in bg_views:
             b.grad = None
 
+    def timed(steps):
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            step()
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        el = time.perf_counter() - t0
+        if world > 1:
+            t = torch.tensor([el], device=device, dtype=torch.float64)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            el = float(t.item())
+        return el
+
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize()
@@ -641,37 +689,34 @@ def main():
     if not args.no_profile:
         _C.profile_read(reset=True)
         _C.profile_enable(True)
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        step()
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    elapsed = time.perf_counter() - t0
+    elapsed = timed(args.steps)
     phases = None
     if not args.no_profile:
         _C.profile_enable(False)
         phases = _C.profile_read(reset=True)
-    if world > 1:
-        t = torch.tensor([elapsed], device=device, dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+    Ks = [k for k, _, _ in _C.RECENT_FORWARDS]
+    # instances the kernels actually walk: the tile lists after the exact ellipse-vs-tile culling
+    Ls = list(_C.RECENT_LISTED) if args.path == "batched" else list(Ks)
+    host_trace = _C.host_trace_read() if _C.HOST_TRACE else None
+
+    variant = None
+    if headline and world > 1 and args.gather == "sync":
+        # the same step with the image all-gather overlapped with the backward (valid when the loss decomposes
+        # over views or rank-aligned view groups; reported beside the headline, never as it)
+        gather_mode[0] = "overlap"
+        step()
+        el = timed(args.steps)
+        gather_mode[0] = args.gather
+        variant = {"value": round(args.views * args.steps / el, 3), "ms_per_step": round(1000.0 * el / args.steps, 3),
+                   "gather": "asynchronous, awaited at step end (beside the backward)"}
 
     total_views = args.views * args.steps
     value = total_views / elapsed
-    Ks = [k for k, _, _ in _C.RECENT_FORWARDS]
     K_mean = float(np.mean(Ks)) if Ks else 0.0
-    # instances the kernels actually walk: the tile lists after the exact ellipse-vs-tile culling
-    Ls = list(_C.RECENT_LISTED) if args.path == "batched" else list(Ks)
     L_mean = float(np.mean(Ls)) if Ls else 0.0
 
     if rank != 0:
-        if world > 1:
-            dist.destroy_process_group()
-        return
+        return None, scene
 
     res = {
         "metric": METRIC,
@@ -691,8 +736,8 @@ def main():
                         "normal renderer (2 passes + normal-from-depth) over a 64-view orbit batch, fwd+bwd" if args.workload == "sugar" else
                         ("C3 per view (1M Gaussians, 1024x1024, SH3, background path)" if args.epilogue ==
                          "background" else "1M Gaussians, 1024x1024, SH3, MVDream shading path (depth-normal, "
-                         "point-light material, composite)") + " over the C4 64-view orbit batch, fwd+bwd (fixed random upstream image gradients) + image all-gather + "
-                        "gradient all-reduce",
+                         "point-light material, composite)") + f" over the C4 {args.views}-view orbit batch, fwd+bwd "
+                        "(fixed random upstream image gradients) + image all-gather + gradient all-reduce",
             "n_gaussians": args.gaussians, "resolution": [H, W], "sh_degree": args.sh_degree,
             "global_views_per_step": args.views, "views_per_rank": per,
             "parallelism": (f"views sharded over {world} rank(s) ({comm} all-gather of the images" + (
@@ -706,14 +751,18 @@ def main():
             "epilogue": "sugar_normal (normal-from-depth, 2 passes)" if args.workload == "sugar" else args.epilogue,
         },
     }
+    if world > 1:
+        res["config"]["gather"] = args.gather
+    if variant is not None:
+        res["gather_overlap"] = variant
     if args.workload == "sugar":
         # how the two rasterizer calls run: one forward blending both colour sets + one backward pass for
         # both (gsr_set_backward_two_colors), or A/B variants
         res["config"]["two_calls"] = ("separate renders" if SUGAR_SEPARATE else "shared forward, " + (
             "separate backward passes" if os.environ.get("GSR_TWO_COLOR_BWD") == "separate"
             else "one two-colour backward pass"))
-    if _C.HOST_TRACE:  # GSR_HOST_TRACE=1: host (Python + ctypes) time per step of the rasterizer's phases
-        res["host_ms_per_step"] = {k: round(1000.0 * v / args.steps, 3) for k, v in _C.host_trace_read().items()}
+    if host_trace is not None:  # GSR_HOST_TRACE=1: host (Python + ctypes) time per step of the rasterizer's phases
+        res["host_ms_per_step"] = {k: round(1000.0 * v / args.steps, 3) for k, v in host_trace.items()}
     if phases is not None:
         nv = max(1, args.steps * per)
         kern = {k: {"ms_per_view": round(ms / nv, 4), "launches": n} for k, (ms, n) in phases.items()}
@@ -723,17 +772,81 @@ def main():
         res["gap_ms_per_step"] = round(1000.0 * elapsed / args.steps - sum(ms for ms, _ in phases.values()) /
                                        args.steps, 3)
         res.update(roofline_fields(args, phases, Ks, Ls, H, W))
-    if not args.no_knn:
+    if headline and not args.no_knn:
         res["init_knn"] = time_knn(rep.means3D.detach())
-    if world == 1 and args.per_view_views > 0 and args.workload == "c3" and args.epilogue == "background" \
-            and args.path == "batched":
+    if headline and world == 1 and args.per_view_views > 0 and args.workload == "c3" \
+            and args.epilogue == "background" and args.path == "batched":
         res["per_view_path"] = time_per_view_path(rep, mine, bg_zero, bg_img, upstream, args.per_view_views)
-    if world == 1 and not args.no_cpu_baseline:
+    return res, scene
+
+
+def compact(res, keep_roofline=True):
+    """A secondary workload's line as a sub-object of the headline: its rate, config and kernel times (and its
+    dominant blend's roofline)."""
+    out = {k: res[k] for k in ("value", "unit", "ms_per_step", "steps", "warmup") if k in res}
+    out["config"] = res["config"]
+    for k in ("kernels", "gap_ms_per_step"):
+        if k in res:
+            out[k] = res[k]
+    if keep_roofline:
+        for k in ("roofline", "roofline_fwd_blend", "dominant_kernel"):
+            if k in res:
+                out[k] = res[k]
+    return out
+
+
+def main():
+    args = parse()
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(launch_ranks(sys.argv[1:], args.gpus))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    check_world(args.gpus, world)
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    comm = "none"
+    if world > 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        # GSR_BENCH_BACKEND=gloo / GSR_BENCH_SHARE_GPU=1: rehearse the multi-rank path on a one-GPU box
+        if os.environ.get("GSR_BENCH_SHARE_GPU") == "1":
+            local = 0
+        torch.cuda.set_device(local)
+        backend = os.environ.get("GSR_BENCH_BACKEND", "nccl")
+        comm = "RCCL" if backend == "nccl" else backend
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(backend)
+    elif os.environ.get("GSR_BENCH_SHARE_GPU") == "1":
+        local = 0
+    device = torch.device("cuda", local)
+    torch.cuda.set_device(device)
+
+    res, scene = run_workload(args, world, rank, device, comm, headline=True)
+    default_c3 = (args.workload == "c3" and args.epilogue == "background" and args.path == "batched"
+                  and args.res == 1024 and args.gaussians == 1_000_000 and args.views == 64)
+    extra = [] if args.extra_lines == "none" else args.extra_lines.split(",")
+    if world == 1 and default_c3 and extra:
+        c3_scene = scene
+        for name in extra:
+            sub = argparse.Namespace(**vars(args))
+            sub.steps, sub.warmup = max(3, min(args.steps, 10)), max(1, min(args.warmup, 2))
+            if name == "c5":  # BASELINE configs[4]: the SuGaR normal renderer (2M Gaussians, 800^2, two calls)
+                sub.workload, sub.res = "sugar", 800
+            elif name == "views8":  # a rank's share of the 64-view batch at N = 8
+                sub.views = 8
+            else:
+                raise SystemExit(f"unknown --extra-lines entry {name!r}")
+            r, _ = run_workload(sub, world, rank, device, comm, headline=False)
+            torch.cuda.empty_cache()
+            res[name] = compact(r)
+        scene = c3_scene
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cb = cpu_baseline(scene, args.res, args.cpu_views)
         rnd = lambda v: round(v, 5) if isinstance(v, float) else v  # noqa: E731
         res["cpu_baseline"] = {k: ({kk: rnd(vv) for kk, vv in v.items()} if isinstance(v, dict) else rnd(v))
                                for k, v in cb.items()}
-    print(json.dumps(res), flush=True)
+    if rank == 0:
+        print(json.dumps(res), flush=True)
     if world > 1:
         dist.destroy_process_group()
 

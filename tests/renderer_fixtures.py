@@ -53,8 +53,19 @@ RASTERIZE = gpu_rasterize
 
 
 def torch_rasterize_views(settings_list, means3D, means2D_list, opacities, shs=None, colors_precomp=None,
-                          scales=None, rotations=None, cov3D_precomp=None, background=None, colors2=None):
-    """batched.rasterize_views restated as a loop over torch_rasterize (for the CPU tests)."""
+                          scales=None, rotations=None, cov3D_precomp=None, background=None, colors2=None,
+                          grad_reduce=None):
+    """batched.rasterize_views restated as a loop over torch_rasterize (for the CPU tests).  grad_reduce: the
+    call's per-Gaussian gradients are summed over ranks in its backward, as the HIP call does (here through
+    view_shard.reduce_on_backward on its inputs, in the HIP call's gradient order)."""
+    if grad_reduce is not None and grad_reduce.active():
+        from diff_gaussian_rasterization.view_shard import reduce_on_backward
+
+        names = ("means3D", "shs", "colors_precomp", "opacities", "scales", "rotations", "colors2")
+        vals = dict(zip(names, (means3D, shs, colors_precomp, opacities, scales, rotations, colors2)))
+        keep = [k for k in names if vals[k] is not None and vals[k].requires_grad]
+        vals.update(zip(keep, reduce_on_backward(grad_reduce, [vals[k] for k in keep])))
+        means3D, shs, colors_precomp, opacities, scales, rotations, colors2 = (vals[k] for k in names)
     outs = [torch_rasterize(s, means3D, m2, opacities, shs=shs, colors_precomp=colors_precomp, scales=scales,
                             rotations=rotations, cov3D_precomp=cov3D_precomp)
             for s, m2 in zip(settings_list, means2D_list)]

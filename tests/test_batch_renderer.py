@@ -153,6 +153,51 @@ def _worker(rank, world, port, tmp, B, kind):
         dist.destroy_process_group()
 
 
+def _reduce_worker(rank, world, port, tmp, B, mode, pred_normal):
+    from diff_gaussian_rasterization.view_shard import ChunkedGradReduce
+
+    dist.init_process_group("gloo", init_method="file://" + os.path.join(tmp, f"rendezvous_{port}"), rank=rank,
+                            world_size=world)
+    try:
+        _cpu()
+        batch = rf.make_batch(B, H, W, "cpu", torch.float64)
+        r = rf.FakeRenderer(mode, _mode_scene(mode), "cpu", torch.float64, pred_normal=pred_normal)
+        r.grad_reduce = ChunkedGradReduce(n_chunks=3)
+        out, _ = _run(r, batch)  # gradients already summed over ranks inside the backward (no allreduce_grads)
+        lo, hi = shard_range(B, world, rank)
+        assert len(out["radii"]) == hi - lo
+        np.savez(os.path.join(tmp, f"red{rank}.npz"), comp_rgb=out["comp_rgb"].detach().numpy(),
+                 **{"g" + k: v.grad.numpy() for k, v in r.geometry.params.items() if v.grad is not None})
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,B,mode,pred_normal", [
+    (2, 1, "background", False),   # rank 1 renders no view
+    (3, 2, "background", False),   # rank 2 renders no view
+    (2, 3, "shading", True),       # main + predicted-normal call: one reduction after both
+    (2, 1, "normal", True),        # ... and a view-less rank joining it
+    (2, 1, "sugar_normal", False),  # two colour sets (colors2 gradient in the reduction)
+])
+def test_grad_reduce_with_viewless_ranks(world, B, mode, pred_normal, tmp_path, monkeypatch):
+    """renderer.grad_reduce (the per-Gaussian gradients summed over ranks inside the rasterizer's backward) with
+    a batch smaller than the world: ranks without views join the ranged collectives with zero gradients
+    (batch_renderer._join_reduce), so no rank blocks and every replica ends with the single-process gradient;
+    with the predicted-normal pass one reduction covers both calls."""
+    _cpu(monkeypatch)
+    batch = rf.make_batch(B, H, W, "cpu", torch.float64)
+    r = rf.FakeRenderer(mode, _mode_scene(mode), "cpu", torch.float64, pred_normal=pred_normal)
+    out, grads = _run(r, batch)
+    mp.spawn(_reduce_worker, args=(world, _free_port(), str(tmp_path), B, mode, pred_normal), nprocs=world,
+             join=True)
+    for rank in range(world):
+        z = np.load(tmp_path / f"red{rank}.npz")
+        np.testing.assert_array_equal(z["comp_rgb"], out["comp_rgb"].detach().numpy())
+        assert set(k[1:] for k in z.files if k.startswith("g")) == set(grads), f"rank {rank}"
+        for k, v in grads.items():
+            np.testing.assert_allclose(z["g" + k], v.numpy(), rtol=1e-10, atol=1e-12, err_msg=f"rank {rank} {k}")
+
+
 @pytest.mark.parametrize("world,B", [(2, 5), (3, 2)])
 @pytest.mark.parametrize("kind", ["fused", "callback", "fused_shading_train"])
 def test_sharded_equals_single_process(world, B, kind, tmp_path, monkeypatch):

@@ -27,7 +27,7 @@ def test_counters_scale_with_views_per_launch():
     full = bench.roofline_fields(a, PHASES, [6.6e6] * 64, [4.95e6] * 64, 1024, 1024)
     half = bench.roofline_fields(a, PHASES, [6.6e6] * 32, [4.95e6] * 32, 1024, 1024)
     t64, t32 = full["roofline"]["traffic"], half["roofline"]["traffic"]
-    assert full["roofline"]["kernel"] == "k_render_bwd" and t64 is not None and t64 > 0
+    assert full["roofline"]["kernel"] == bench.KERNELS["c3"][1] and t64 is not None and t64 > 0
     assert abs(t32 - t64 / 2) <= 1
     v64, v32 = full["roofline"]["valu"]["insts_per_launch"], half["roofline"]["valu"]["insts_per_launch"]
     assert abs(v32 - v64 / 2) <= 1
@@ -39,7 +39,7 @@ def test_roofline_is_the_slower_blend_not_the_dominant_phase():
     a = _args()
     ph = dict(PHASES, binning=(50.0, 1))
     r = bench.roofline_fields(a, ph, [6.6e6] * 64, [4.95e6] * 64, 1024, 1024)
-    assert r["dominant_kernel"] == "binning" and r["roofline"]["kernel"] == "k_render_bwd"
+    assert r["dominant_kernel"] == "binning" and r["roofline"]["kernel"] == bench.KERNELS["c3"][1]
 
 
 def test_no_counters_for_unprofiled_workloads():
@@ -57,3 +57,57 @@ def test_c5_line_reads_its_own_counters():
     assert r["roofline"]["traffic"] is not None and r["roofline"]["traffic"] > 0
     assert r["roofline_fwd_blend"]["traffic"] is not None
     assert "counters_note" not in r and "barriers" in r["roofline"]["limiter"]
+
+
+def test_committed_counters_name_the_timed_kernels():
+    """The default traffic files hold counters of exactly the kernels the bench times (bench.KERNELS), so a
+    kernel renamed or replaced in the build cannot borrow another kernel's counters."""
+    a = _args()
+    for path, kind in ((a.traffic, "c3"), (a.traffic_sugar, "sugar")):
+        for kernel in bench.KERNELS[kind]:
+            assert bench.read_traffic(path, kernel) is not None, (path, kernel)
+            assert bench.read_traffic(path, kernel, "valu_insts_per_launch") is not None, (path, kernel)
+
+
+def test_fwd_counters_only_for_the_profiled_launch():
+    """At 32 views per launch (a rank's share at N = 2) the forward is the quadrant-wave kernel, not the profiled
+    tile-wave one: no forward counters; the backward's scale with the views."""
+    r = bench.roofline_fields(_args(), PHASES, [6.6e6] * 32, [4.95e6] * 32, 1024, 1024)
+    assert r["roofline_fwd_blend"]["traffic"] is None and r["roofline"]["traffic"] is not None
+
+
+def test_stale_counter_file_gives_no_fields(tmp_path):
+    import json
+
+    f = tmp_path / "old.json"
+    f.write_text(json.dumps({"per_launch_bytes": {"k_render_bwd<false>": 1e9, "k_render_fwd_tile<false>": 1e9},
+                             "valu_insts_per_launch": {"k_render_bwd<false>": 1e9}}))
+    r = bench.roofline_fields(_args("--traffic", str(f)), PHASES, [6.6e6] * 64, [4.95e6] * 64, 1024, 1024)
+    assert r["roofline"]["traffic"] is None and bench.KERNELS["c3"][1] in r["counters_note"]
+
+
+def test_launcher_command_and_world_check():
+    cmd = bench.launch_command(["--gpus", "4", "--steps", "3"], 4)
+    assert cmd[1:4] == ["-m", "torch.distributed.run", "--nnodes=1"] and "--nproc-per-node=4" in cmd
+    assert cmd[cmd.index("--master-addr") + 1] == "127.0.0.1" and cmd[-3:] == ["--gpus", "4", "--steps", "3"][-3:]
+    assert cmd[-5].endswith("bench.py")
+    bench.check_world(2, 2)
+    import pytest
+
+    with pytest.raises(SystemExit):
+        bench.check_world(8, 1)
+
+
+def test_launcher_starts_ranks_without_world_size(monkeypatch):
+    """`bench.py --gpus 2` without a launcher environment hands over to N ranks before touching the GPU."""
+    import subprocess
+
+    calls = []
+    monkeypatch.delenv("WORLD_SIZE", raising=False)
+    monkeypatch.setattr(subprocess, "call", lambda cmd: calls.append(cmd) or 0)
+    monkeypatch.setattr(sys, "argv", ["bench.py", "--gpus", "2", "--steps", "1"])
+    import pytest
+
+    with pytest.raises(SystemExit) as e:
+        bench.main()
+    assert e.value.code == 0 and len(calls) == 1 and "--nproc-per-node=2" in calls[0]

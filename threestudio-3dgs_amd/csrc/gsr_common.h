@@ -3,6 +3,16 @@
 #pragma once
 
 #include <hip/hip_runtime.h>
+
+// Timing experiments (GSR_EXP_*: parts of the blends compiled out) compute wrong results by design.  They build
+// only as a diagnostic library (`make exp EXP=<name>` -> build_exp_<name>/libgsr_hip_exp.so, which defines
+// GSR_DIAG_BUILD), never as the product libgsr_hip.so.
+#if !defined(GSR_DIAG_BUILD) &&                                                                          \
+    (defined(GSR_EXP_COALROWS) || defined(GSR_EXP_FWD_NOC) || defined(GSR_EXP_LDSPAD) ||                  \
+     defined(GSR_EXP_NOCULL) || defined(GSR_EXP_NOFLUSH) || defined(GSR_EXP_NOGROUP) ||                   \
+     defined(GSR_EXP_NOMFMA) || defined(GSR_EXP_NOREACH) || defined(GSR_EXP_NOREPLAY))
+#error "GSR_EXP_* experiment switches build only through `make exp` (a diagnostic library, not libgsr_hip.so)"
+#endif
 #include <stddef.h>
 #include <stdint.h>
 

@@ -50,6 +50,7 @@ import numpy as np
 import torch
 
 from .cameras import get_cam_info_gaussian
+from . import view_shard
 from .view_shard import _world, all_gather_views, shard_range
 
 MODES = ("plain", "background", "advanced", "shading", "normal", "sugar_normal")
@@ -207,6 +208,41 @@ def _placeholders(P, n, dev, dtype):
     return [zero.expand(P, 3).requires_grad_(True) for _ in range(n)]
 
 
+def _has_pred_normal(pc, mode: str) -> bool:
+    return mode in ("shading", "normal") and bool(getattr(pc.cfg, "pred_normal", False))
+
+
+def _active_reduce(renderer):
+    reduce = getattr(renderer, "grad_reduce", None)
+    return reduce if reduce is not None and reduce.active() else None
+
+
+def _reduce_tensors(pc, mode, override, means3D, shs, common, normals):
+    """(name, tensor) pairs whose gradients the renderer's reduction sums over ranks, in the order the
+    reducing call lists them: the rasterizer's inputs (means3D, shs, colors_precomp, opacities, scales,
+    rotations, colors2; batched._RasterizeViews.backward) for one call, plus the normals of the
+    predicted-normal call when that reduction runs once after both calls.  Only tensors requiring grad."""
+    pairs = [("means3D", means3D), ("shs", shs), ("override", override), ("opacities", common["opacities"]),
+             ("scales", common["scales"]), ("rotations", common["rotations"])]
+    if mode == "sugar_normal":
+        pairs.append(("colors2", pc.get_gs_normals))
+    if normals is not None:
+        pairs.append(("normals", normals))
+    return [(k, t) for k, t in pairs if t is not None and t.requires_grad]
+
+
+def _join_reduce(renderer, batch: dict, mode: str, shapes):
+    """A rank without views: empty outputs of `shapes` joining the reduction the other ranks' rasterizer
+    backward issues (view_shard.join_grad_reduce), with the tensors that call differentiates."""
+    pc = renderer.geometry
+    override = batch.get("override_color")
+    common = dict(opacities=pc.get_opacity, scales=pc.get_scaling, rotations=pc.get_rotation)
+    normals = pc.get_normal if _has_pred_normal(pc, mode) else None
+    pairs = _reduce_tensors(pc, mode, override, pc.get_xyz, pc.get_features if override is None else None, common,
+                            normals)
+    return view_shard.join_grad_reduce(_active_reduce(renderer), [t for _, t in pairs], shapes)
+
+
 def render_views_local(renderer, batch: dict, mode: str, lo: int, hi: int, draws: dict | None = None) -> dict:
     """Render views [lo, hi) of the batch with the fused path of `mode`.  Returns per-view stacked images
     (n, C, H, W) under the batch dict's keys, plus the per-view lists.  `draws`: batch_draws of the whole
@@ -230,20 +266,27 @@ def render_views_local(renderer, batch: dict, mode: str, lo: int, hi: int, draws
     draws = {k: v[lo:hi] for k, v in draws.items()}
     m2 = _placeholders(P, n, dev, means3D.dtype)
     common = dict(opacities=pc.get_opacity, scales=pc.get_scaling, rotations=pc.get_rotation)
-    reduce = getattr(renderer, "grad_reduce", None)
-    if reduce is not None:  # the main call's per-Gaussian gradients summed over ranks inside its backward
-        if mode in ("shading", "normal") and getattr(pc.cfg, "pred_normal", False):
-            raise ValueError("grad_reduce covers one rasterizer call: not with the predicted-normal pass")
+    normals = pc.get_normal if _has_pred_normal(pc, mode) else None
+    reduce = _active_reduce(renderer)
+    common_main = common
+    if reduce is not None and normals is None:
+        # the main call's per-Gaussian gradients summed over ranks inside its backward, range by range
         common_main = dict(common, grad_reduce=reduce)
-    else:
-        common_main = common
+    elif reduce is not None:
+        # two rasterizer calls on the same parameters: one reduction of the gradients both accumulate, after
+        # both backward passes (view-less ranks join it with the same tensors, render_batch)
+        names, tensors = zip(*_reduce_tensors(pc, mode, override, means3D, shs, common, normals))
+        red = dict(zip(names, view_shard.reduce_on_backward(reduce, list(tensors))))
+        means3D, shs, override = red.get("means3D", means3D), red.get("shs", shs), red.get("override", override)
+        normals = red.get("normals", normals)
+        common = common_main = {k: red.get(k, v) for k, v in common.items()}
 
     def pred_normal_pass(settings):
         # the predicted-normal call (renderer/diff_gaussian_rasterizer_shading.py:177-187,
         # renderer/diff_gaussian_rasterizer_normal.py:175-185): same settings, SH = the geometry's normals
         # (degree 0 through M = 1), a fresh zero means2D per view
         zeros = [torch.zeros_like(m) for m in m2]
-        pred, _, _, _ = _rasterize_views(settings, means3D, zeros, shs=pc.get_normal.unsqueeze(1),
+        pred, _, _, _ = _rasterize_views(settings, means3D, zeros, shs=normals.unsqueeze(1),
                                          colors_precomp=None, **common)
         return pred
 
@@ -339,8 +382,13 @@ def render_batch(renderer, batch: dict, mode: str, group=None, shard: bool = Tru
     if world > 1:
         outputs["view_range"] = (lo, hi)
     channels = dict(_OUT_KEYS)
+    joined = {}
+    if hi <= lo and world > 1 and _active_reduce(renderer) is not None:
+        # the other ranks sum their gradients inside the rasterizer's backward: this rank's empty slices come
+        # from a node whose backward joins those collectives with zeros (no deadlock, same replica gradients)
+        joined = dict(zip(keys, _join_reduce(renderer, batch, mode, [(0, channels[k], H, W) for k in keys])))
     for key in keys:
-        img = local.get(key)
+        img = local.get(key, joined.get(key))
         if img is None:  # a rank without views: an empty slice of the agreed shape (a leaf, so that the
             # rank's loss still has a graph and its backward runs; its parameter gradients stay None and
             # view_shard.allreduce_grads contributes zeros for them)
@@ -394,9 +442,10 @@ class GaussianBatchRenderer:
     batch_render_mode = None
     shard_views = True
     shard_group = None
-    # view_shard.ChunkedGradReduce: the fused path's main rasterizer call sums its per-Gaussian gradients over
-    # ranks inside the backward (overlapped); needs a view on every rank (batch >= world).  The predicted-
-    # normal pass and any parameter-direct loss terms are not covered: reduce those with allreduce_grads.
+    # view_shard.ChunkedGradReduce: the fused path's rasterizer call sums its per-Gaussian gradients over ranks
+    # inside the backward (overlapped with it); with the predicted-normal pass, one reduction after both calls.
+    # Ranks without views (batch < world) join the same collectives with zero gradients.  Parameter-direct
+    # loss terms are not covered: reduce those with allreduce_grads.
     grad_reduce = None
 
     def batch_forward(self, batch):

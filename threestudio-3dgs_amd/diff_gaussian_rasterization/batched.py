@@ -205,7 +205,10 @@ class _RasterizeViews(torch.autograd.Function):
             if fused2:
                 g2 = g_color2.float().contiguous()
             reducer = ctx.grad_reduce if ctx.grad_reduce is not None and ctx.grad_reduce.active() else None
-            events = reducer.chunk_events(dev) if reducer is not None else None
+            # per-range events only when the last set's call is the last writer of the per-Gaussian sums: with
+            # the second colour's backward run separately after it (GSR_TWO_COLOR_BWD=separate), that call
+            # adds into the same gradients, so the reduction waits for the whole stream instead
+            events = reducer.chunk_events(dev) if reducer is not None and (fused2 or not second) else None
             for si, vs in enumerate(ctx.sets):
                 if events is not None and si == len(ctx.sets) - 1:
                     # the last set's call forms the final per-Gaussian sums: in ranges, an event after each
@@ -270,7 +273,7 @@ class _RasterizeViews(torch.autograd.Function):
         if ctx.grad_reduce is not None and P > 0:
             # the per-Gaussian gradients' sums over ranks, range by range as the backward finishes them
             shared = [grads[k] for k in (2, 3, 4, 5, 6, 7, 8, 10)]
-            ctx.grad_reduce.launch(shared, P, events if P > 0 and ctx.grad_reduce.active() else None)
+            ctx.grad_reduce.launch(shared, P, events if P > 0 else None)
         _C.host_mark("bwd_host", t0)
         return tuple(grads)
 

@@ -320,6 +320,63 @@ class ChunkedGradReduce:
         self.launched += 1
 
 
+class _ReduceOnBackward(torch.autograd.Function):
+    """Identity on (P, ...) tensors whose backward sums their accumulated gradients over ranks
+    (ChunkedGradReduce.launch, without events: the ranges wait for the whole launch stream)."""
+
+    @staticmethod
+    def forward(ctx, grad_reduce, P, *tensors):
+        ctx.grad_reduce, ctx.P = grad_reduce, P
+        ctx.like = [(t.shape, t.dtype, t.device) for t in tensors]
+        return tuple(t.view_as(t) for t in tensors)
+
+    @staticmethod
+    def backward(ctx, *grads):
+        grads = [torch.zeros(s, dtype=d, device=v) if g is None else g.contiguous()
+                 for g, (s, d, v) in zip(grads, ctx.like)]
+        ctx.grad_reduce.launch(grads, ctx.P, None)
+        return (None, None) + tuple(grads)
+
+
+def reduce_on_backward(grad_reduce, tensors):
+    """The tensors (rows = Gaussians, all requiring grad) through an identity whose backward all-reduces the
+    gradients every use of them accumulated — one reduction for several rasterizer calls on the same
+    parameters (the shading / normal renderers' main and predicted-normal calls,
+    renderer/diff_gaussian_rasterizer_shading.py:119-128,177-187), issued after both calls' backward."""
+    if not tensors:
+        return []
+    return list(_ReduceOnBackward.apply(grad_reduce, int(tensors[0].shape[0]), *tensors))
+
+
+class _JoinReduce(torch.autograd.Function):
+    """A rank that renders no view (batch < world) in place of the rasterizer call whose backward issues the
+    per-Gaussian gradient reduction: empty image slices in the forward; in the backward zero gradients for
+    the same tensors, passed through the same ranged collectives, so the other ranks' reductions complete
+    and this replica receives their sum."""
+
+    @staticmethod
+    def forward(ctx, grad_reduce, P, shapes, *tensors):
+        ctx.grad_reduce, ctx.P = grad_reduce, P
+        ctx.like = [(t.shape, t.dtype, t.device) for t in tensors]
+        t0 = tensors[0]
+        return tuple(t0.new_empty(s) for s in shapes)
+
+    @staticmethod
+    def backward(ctx, *_grads):
+        grads = [torch.zeros(s, dtype=d, device=v) for s, d, v in ctx.like]
+        ctx.grad_reduce.launch(grads, ctx.P, None)
+        return (None, None, None) + tuple(grads)
+
+
+def join_grad_reduce(grad_reduce, tensors, shapes):
+    """Empty outputs of the given shapes whose backward joins `grad_reduce`'s collectives with zero gradients
+    of `tensors` (the tensors the other ranks' reducing call differentiates, in that call's order)."""
+    tensors = [t for t in tensors if t is not None and t.requires_grad]
+    if not tensors:
+        raise ValueError("join_grad_reduce: no tensor requires grad")
+    return list(_JoinReduce.apply(grad_reduce, int(tensors[0].shape[0]), [tuple(s) for s in shapes], *tensors))
+
+
 def reduce_densify_stats(radii, viewspace_points, visibility_filter, num_points: int, group=None, device=None):
     """Per-Gaussian densification statistics over the whole batch (all ranks).
 
