@@ -262,8 +262,8 @@ def test_batched_views_match_per_view(nviews, monkeypatch):
 @pytest.mark.parametrize("switch", ["fwd_kernel", "dispatch_order"])
 @pytest.mark.parametrize("kind", ["ball_composite", "sugar_two_colors"])
 def test_forward_kernels_bitwise(kind, switch, monkeypatch):
-    """fwd_kernel: the one-wave-per-tile forward and the quadrant-wave forward (GSR_FWD_KERNEL) blend
-    exactly the same candidates per pixel in the same order; dispatch_order: the blends' work-ordered
+    """fwd_kernel: the one-wave-per-tile forward, the quadrant-wave forward and the quadrant waves sharing
+    one staged batch per tile (GSR_FWD_KERNEL) blend exactly the same candidates per pixel in the same order; dispatch_order: the blends' work-ordered
     dispatch and raster order (GSR_TILE_ORDER=raster) only change which workgroup starts first.  Every
     output — colour, depth, alpha, the composite, the second colour set, radii — and every gradient (the
     backward reads the forward's per-pixel state) must be bitwise equal."""
@@ -315,3 +315,6 @@ def test_forward_kernels_bitwise(kind, switch, monkeypatch):
     tile, quad = run("tile"), run("quadrant")
     for i, (x, y) in enumerate(zip(tile, quad)):
         assert torch.equal(x, y), f"output {i} differs: {float((x.double() - y.double()).abs().max())}"
+    if switch == "fwd_kernel":  # the quadrant waves sharing each staged batch per tile (k_render_fwd_shared)
+        for i, (x, y) in enumerate(zip(run("shared"), quad)):
+            assert torch.equal(x, y), f"shared: output {i} differs: {float((x.double() - y.double()).abs().max())}"

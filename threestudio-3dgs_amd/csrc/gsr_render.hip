@@ -648,6 +648,185 @@ __global__ __launch_bounds__(64) void k_render_fwd_tile(RenderSet rs, const uint
 #endif
 }
 
+// Forward, one 256-thread workgroup per 16x16 tile sharing each batch of 64 candidates: wave q blends 8x8
+// quadrant q exactly as the quadrant-wave kernel does (same candidates per pixel, same order, same operations:
+// bitwise identical outputs), but the batch's records are gathered once per tile — each wave loads one 16-B
+// piece of every candidate (wave 0 rec.a, 1 rec.b, 2 rec.c, 3 the second colour), so a record line is read
+// once instead of once per quadrant wave (the quadrant-wave kernel's C5 forward moved 5.6x its algorithmic
+// bytes, profiles/r03d_sugar_traffic.json).  The batches are double-buffered in LDS (one barrier per batch);
+// each wave culls the staged batch for its quadrant (quadrant_hit on the raw conic) and walks its kept
+// candidates by scalar bit scans of the ballot mask (no compaction).  A wave whose pixels are all done keeps
+// staging for the others; the workgroup stops when all four are done (flags written before the barrier).
+template <bool C2>
+__global__ __launch_bounds__(256) void k_render_fwd_shared(RenderSet rs, const uint2* __restrict__ ranges,
+                                                          const uint32_t* __restrict__ sorted_gauss,
+                                                          const GaussRec* __restrict__ rec,
+                                                          float* __restrict__ out_color, float* __restrict__ out_depth,
+                                                          float* __restrict__ out_alpha, float* __restrict__ final_T,
+                                                          uint32_t* __restrict__ n_contrib,
+                                                          uint32_t* __restrict__ quad_maxc) {
+  // [buffer][candidate]: raw conic pieces for the cull, pre-multiplied ones for the blend (slot 64: the
+  // look-ahead read past a wave's last kept candidate, never used)
+  __shared__ float4 sR0[2][64], sR1[2][64], sA[2][65], sB[2][65], sC[2][65];
+  __shared__ float4 sE[2][C2 ? 65 : 1];
+  __shared__ uint32_t sdone[2][4];
+  int v, tile, q_unused;
+  if (!block_map<4>(blockIdx.x, rs, v, tile, q_unused)) return;
+  GSR_TL_BEGIN
+  const int q = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+  const int lane = threadIdx.x & 63;
+  const int W = rs.W, H = rs.H, grid_x = rs.gx;
+  const size_t HWs = (size_t)W * H;
+  {
+    const size_t vg = (size_t)(rs.v0 + v), tiles = (size_t)rs.gx * rs.gy;
+    ranges += vg * tiles;
+    quad_maxc += vg * 4 * tiles;
+    sorted_gauss += rs.inst_start[v];
+    rec += vg * rs.P;
+    out_color += vg * 3 * HWs;
+    out_depth += vg * HWs;
+    out_alpha += vg * HWs;
+    final_T += vg * HWs;
+    n_contrib += vg * HWs;
+  }
+  const float* bg = rs.bg[v];
+  const int qx0 = (tile % grid_x) * GSR_TILE_X + (q & 1) * 8;
+  const int qy0 = (tile / grid_x) * GSR_TILE_Y + (q >> 1) * 8;
+  const int px = qx0 + (lane & 7), py = qy0 + (lane >> 3);
+  const bool inside = px < W && py < H;
+  const float pxf = (float)px, pyf = (float)py;
+  const uint2 range = ranges[tile];
+  const int n = (int)(range.y - range.x);
+  const uint32_t gmask = rs.gmask;
+  const float4 zero4 = make_float4(0.f, 0.f, 0.f, 0.f);
+  const float* col2 = rs.col2;
+  const float4* recp = reinterpret_cast<const float4*>(rec);
+
+  bool done = !inside;
+  float T = 1.0f, Cr = 0.f, Cg = 0.f, Cb = 0.f, D = 0.f;
+  float Er = 0.f, Eg = 0.f, Eb = 0.f;
+  uint32_t last_contributor = 0;
+#ifdef GSR_TIMELINE
+  unsigned long long pc_eval = 0, pc_slot = 0;
+#endif
+  // this wave's piece of a candidate's record
+  const bool loader = C2 || q < 3;
+  auto piece = [&](uint32_t g) -> float4 {
+    if (q < 3) return recp[4 * (size_t)g + q];
+    return make_float4(col2[3 * (size_t)g], col2[3 * (size_t)g + 1], col2[3 * (size_t)g + 2], 0.f);
+  };
+  float4 np = zero4;
+  uint32_t gi_next = 0u;
+  if (loader && lane < n) np = piece(sorted_gauss[range.x + lane] & gmask);
+  if (loader && 64 + lane < n) gi_next = sorted_gauss[range.x + 64 + lane] & gmask;
+  int buf = 0;
+  for (int base = 0; base < n; base += 64, buf ^= 1) {
+    const int i = base + lane;
+    // stage this batch (the conic pre-multiplied for gauss_power2 as the other kernels do; .w of sB: 1 + list
+    // position)
+    if (q == 0) {
+      sR0[buf][lane] = np;
+      sA[buf][lane] = make_float4(np.x, np.y, GSR_CONIC_K_AC * np.z, GSR_CONIC_K_B * np.w);
+    } else if (q == 1) {
+      sR1[buf][lane] = np;
+      sB[buf][lane] = make_float4(GSR_CONIC_K_AC * np.x, np.y, np.z, __uint_as_float((uint32_t)(i + 1)));
+    } else if (q == 2) {
+      sC[buf][lane] = np;
+    } else if (C2) {
+      sE[buf][lane] = np;
+    }
+    const bool wave_done = __all(done);
+    if (lane == 0) sdone[buf][q] = wave_done ? 1u : 0u;
+    // the next batch's pieces (one batch ahead) and indices (two ahead)
+    if (loader && base + 64 + lane < n) np = piece(gi_next);
+    if (loader && base + 128 + lane < n) gi_next = sorted_gauss[range.x + base + 128 + lane] & gmask;
+    __syncthreads();
+    if (sdone[buf][0] & sdone[buf][1] & sdone[buf][2] & sdone[buf][3]) break;
+    if (wave_done) continue;
+    bool keep = false;
+    if (i < n) keep = quadrant_hit(sR0[buf][lane], sR1[buf][lane], (float)qx0, (float)qy0);
+    unsigned long long m = __ballot(keep);
+    if (m == 0ull) continue;
+    int k = (int)__builtin_ctzll(m);
+    float4 a = sA[buf][k], b = sB[buf][k], c = sC[buf][k], e = C2 ? sE[buf][k] : zero4;
+    for (int j = 1;; ++j) {
+      m &= m - 1ull;
+      const int kn = m != 0ull ? (int)__builtin_ctzll(m) : 64;
+      const float4 an = sA[buf][kn], bn = sB[buf][kn], cn = sC[buf][kn];
+      const float4 en = C2 ? sE[buf][kn] : zero4;
+      const float dx = a.x - pxf, dy = a.y - pyf;
+      const float power2 = gauss_power2(a.z, a.w, b.x, dx, dy);  // log2(e) * power
+      const float alpha = fminf(GSR_ALPHA_MAX, b.y * __builtin_amdgcn_exp2f(power2));
+#ifdef GSR_TIMELINE
+      pc_eval += done ? 0ull : 1ull;
+      pc_slot += 1ull;
+#endif
+      const bool ok = !done && power2 <= 0.0f && alpha >= GSR_ALPHA_MIN;
+      const float test_T = T * (1.0f - alpha);
+      const bool term = ok && test_T < GSR_T_EPS;
+      const bool blend = ok && !term;
+      const float a_eff = blend ? alpha : 0.0f;
+      const float aT = a_eff * T;
+      Cr = fmaf(c.x, aT, Cr);
+      Cg = fmaf(c.y, aT, Cg);
+      Cb = fmaf(c.z, aT, Cb);
+      D = fmaf(b.z, aT, D);
+      if (C2) {
+        Er = fmaf(e.x, aT, Er);
+        Eg = fmaf(e.y, aT, Eg);
+        Eb = fmaf(e.z, aT, Eb);
+      }
+      T = blend ? test_T : T;
+      last_contributor = blend ? __float_as_uint(b.w) : last_contributor;
+      done = done || term;
+      if (m == 0ull) break;
+      if ((j & 7) == 0 && __all(done)) break;
+      a = an;
+      b = bn;
+      c = cn;
+      e = en;
+    }
+  }
+  if (inside) {
+    const size_t pid = (size_t)py * W + px;
+    final_T[pid] = T;
+    n_contrib[pid] = last_contributor;
+    {
+#pragma clang fp contract(off)
+      out_color[pid] = Cr + T * bg[0];
+      out_color[HWs + pid] = Cg + T * bg[1];
+      out_color[2 * HWs + pid] = Cb + T * bg[2];
+    }
+    out_depth[pid] = D;
+    out_alpha[pid] = 1.0f - T;
+    if (C2) {
+#pragma clang fp contract(off)
+      float* o2 = rs.out_col2 + (size_t)(rs.v0 + v) * 3 * HWs + pid;
+      o2[0] = Er + T * bg[0];
+      o2[HWs] = Eg + T * bg[1];
+      o2[2 * HWs] = Eb + T * bg[2];
+    }
+    if (rs.cbg != nullptr) {
+#pragma clang fp contract(off)
+      const float am = 1.0f - (1.0f - T);
+      const float* bgi = rs.cbg + ((size_t)v * HWs + pid) * 3;
+      float* cp = rs.comp + (size_t)v * 3 * HWs + pid;
+      cp[0] = fminf(fmaxf((Cr + T * bg[0]) + am * bgi[0], 0.0f), 1.0f);
+      cp[HWs] = fminf(fmaxf((Cg + T * bg[1]) + am * bgi[1], 0.0f), 1.0f);
+      cp[2 * HWs] = fminf(fmaxf((Cb + T * bg[2]) + am * bgi[2], 0.0f), 1.0f);
+    }
+  }
+  uint32_t mc = last_contributor;
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) mc = max(mc, (uint32_t)__shfl_xor((int)mc, o, 64));
+  if (lane == 0) quad_maxc[4 * tile + q] = mc;
+#ifdef GSR_TIMELINE
+  atomicAdd(&g_pairs[0], pc_eval);
+  atomicAdd(&g_pairs[1], pc_slot);
+#endif
+  GSR_TL_END(0, mc)
+}
+
 // One block per view: bucket its super-tiles by the bit length of their listed instances (sum over the
 // 2x2 tiles), heaviest bucket first (LDS counts, exclusive scan, LDS-atomic placement: the order inside a
 // bucket may vary between runs — it only changes which workgroup starts first, never a result).
@@ -752,9 +931,17 @@ __global__ __launch_bounds__(256) void k_ckpt_suffix(RenderSet rs, const uint32_
 // forces one (A/B and tests).
 static bool fwd_tile_kernel(long long instances, long long gaussians, int views) {
   const char* e = getenv("GSR_FWD_KERNEL");
-  if (e != nullptr && strcmp(e, "quadrant") == 0) return false;
+  if (e != nullptr && (strcmp(e, "quadrant") == 0 || strcmp(e, "shared") == 0)) return false;
   if (e != nullptr && strcmp(e, "tile") == 0) return true;
   return views >= 48 && gaussians > 0 && instances >= 3 * gaussians;
+}
+// Otherwise the quadrant waves: sharing each staged batch per tile (k_render_fwd_shared, one gather per
+// candidate and tile) unless the launch writes the split backward's checkpoints (only the free-running
+// quadrant-wave kernel keeps them) or GSR_FWD_KERNEL=quadrant.
+static bool fwd_shared_kernel(bool ckpt) {
+  if (ckpt) return false;
+  const char* e = getenv("GSR_FWD_KERNEL");
+  return !(e != nullptr && strcmp(e, "quadrant") == 0);
 }
 
 void launch_render_forward(const RenderSet& rs, const GeomState& g, const uint32_t* sorted_gauss,
@@ -772,6 +959,11 @@ void launch_render_forward(const RenderSet& rs, const GeomState& g, const uint32
       hipLaunchKernelGGL(k_render_fwd_tile<false>, grid, dim3(64), 0, stream, rs, (const uint2*)img.ranges,
                          sorted_gauss, (const GaussRec*)g.rec, out_color, out_depth, out_alpha, img.final_T,
                          img.n_contrib, img.quad_maxc);
+  } else if (fwd_shared_kernel(rs.ckpt != nullptr)) {
+    auto kern = rs.col2 != nullptr ? k_render_fwd_shared<true> : k_render_fwd_shared<false>;
+    hipLaunchKernelGGL(kern, dim3(block_grid(rs, 4)), dim3(256), 0, stream, rs, (const uint2*)img.ranges,
+                       sorted_gauss, (const GaussRec*)g.rec, out_color, out_depth, out_alpha, img.final_T,
+                       img.n_contrib, img.quad_maxc);
   } else {
     auto kern = rs.col2 != nullptr ? (rs.ckpt != nullptr ? k_render_fwd<true, true> : k_render_fwd<true, false>)
                                    : (rs.ckpt != nullptr ? k_render_fwd<false, true> : k_render_fwd<false, false>);
