@@ -259,12 +259,13 @@ def test_batched_views_match_per_view(nviews, monkeypatch):
         assert err <= 1e-5 * scale, f"{k}: {err} vs scale {scale}"
 
 
-@pytest.mark.parametrize("switch", ["fwd_kernel", "dispatch_order"])
+@pytest.mark.parametrize("switch", ["fwd_kernel", "dispatch_order", "bwd_kernel"])
 @pytest.mark.parametrize("kind", ["ball_composite", "sugar_two_colors"])
 def test_forward_kernels_bitwise(kind, switch, monkeypatch):
     """fwd_kernel: the one-wave-per-tile forward, the quadrant-wave forward and the quadrant waves sharing
     one staged batch per tile (GSR_FWD_KERNEL) blend exactly the same candidates per pixel in the same order; dispatch_order: the blends' work-ordered
-    dispatch and raster order (GSR_TILE_ORDER=raster) only change which workgroup starts first.  Every
+    dispatch and raster order (GSR_TILE_ORDER=raster) only change which workgroup starts first; bwd_kernel: the
+    hit-list backward as one wave per tile or as four lockstep quadrant waves (GSR_BWD_KERNEL).  Every
     output — colour, depth, alpha, the composite, the second colour set, radii — and every gradient (the
     backward reads the forward's per-pixel state) must be bitwise equal."""
     import torch
@@ -287,6 +288,12 @@ def test_forward_kernels_bitwise(kind, switch, monkeypatch):
         if switch == "fwd_kernel":
             monkeypatch.setenv("GSR_FWD_KERNEL", kernel)
             monkeypatch.setenv("GSR_BWD_SPLIT", "0")  # the tile-wave forward writes no split checkpoints
+        elif switch == "bwd_kernel":
+            # hit-list sums: one wave per tile walking the quadrants in turn (k_render_bwd_tw) vs the workgroup of
+            # lockstep quadrant waves (k_render_bwd<·, true>)
+            monkeypatch.setenv("GSR_BWD_SUMS", "hits")
+            monkeypatch.setenv("GSR_BWD_SPLIT", "0")
+            monkeypatch.setenv("GSR_BWD_KERNEL", "tile" if kernel == "tile" else "quadrant")
         elif kernel == "tile":
             monkeypatch.delenv("GSR_TILE_ORDER", raising=False)
         else:

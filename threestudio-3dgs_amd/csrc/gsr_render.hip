@@ -1665,6 +1665,347 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(TWO ? 4 : 5
                 n_contrib, dL_dcolor, dL_ddepth, dL_dalpha, grow, reach);
 }
 
+// Backward, one 64-thread wave per 16x16 tile (each lane holds the same pixel of the four 8x8 quadrants) —
+// the small-Gaussian regime (C5: SuGaR's surface Gaussians blend at ~13 pixels, a candidate usually in one
+// quadrant).  The workgroup-per-tile kernel above walks the quadrants in lockstep batches (three barriers per
+// batch, each batch as long as its busiest quadrant: 2.25 slots per kept pair at C5, waves parked on barriers
+// two thirds of their cycles, profiles/r03/sq_c5/); here one wave replays a batch's kept candidates quadrant
+// after quadrant, so a batch costs the sum of its kept (candidate, quadrant) pairs and nothing waits on
+// another wave.  Per batch: each lane stages one candidate's whole record (one 64-B line) and tests it
+// against the four quadrants (the same conservative cull); per quadrant the kept candidates are replayed
+// back to front (the same replay as k_render_bwd: per pixel the same candidates, order and operations) and
+// the lanes that blended append (u, u_1, w, pixel) to the wave's hit list; lane c then forms candidate c's
+// sums from its hits (the same pair_sums order), turns them into moments about the mean and adds the
+// quadrants as ((q0 + q1) + (q2 + q3)) — the order of the other kernel's quad DPP adds — and writes one row
+// per staged candidate.  A full hit list is summed early (each pair's sums are formed once, whenever).
+// Outputs match the hit-list k_render_bwd<TWO, true> (up to the sign of zero sums).
+#define GSR_HCAP_TW 256
+template <bool TWO>
+__global__ __launch_bounds__(64) void k_render_bwd_tw(
+    RenderSet rs, const uint2* __restrict__ ranges, const uint32_t* __restrict__ quad_maxc,
+    const uint32_t* __restrict__ sorted_gauss, const GaussRec* __restrict__ rec, const uint32_t* __restrict__ goff,
+    const float* __restrict__ final_Ts, const uint32_t* __restrict__ n_contrib, const float* __restrict__ dL_dcolor,
+    const float* __restrict__ dL_ddepth, const float* __restrict__ dL_dalpha, float4* __restrict__ grow,
+    unsigned long long* __restrict__ reach) {
+  constexpr int NG = TWO ? NGV2 : NGV;  // raw sums per (candidate, quadrant)
+  constexpr int NM = TWO ? 15 : NGV;    // moments per candidate
+  constexpr int RW = TWO ? 4 : 3;       // float4 per gradient row
+  __shared__ float4 s0[65], s1[65], s2[65];
+  __shared__ float4 s3[TWO ? 65 : 1];
+  __shared__ uint32_t slot[64];
+  __shared__ uint32_t list[64];             // the current quadrant: first hit | hits << 16 per kept candidate
+  __shared__ float4 hits[GSR_HCAP_TW];      // (u, u_1, w, pixel) of the current quadrant's blended pairs
+  __shared__ float4 planes[TWO ? 128 : 64];  // the current quadrant's dL/dpixel per pixel
+  int v, tile, q_unused;
+  if (!block_map<4>(blockIdx.x, rs, v, tile, q_unused)) return;
+  GSR_TL_BEGIN
+  const int W = rs.W, H = rs.H, grid_x = rs.gx;
+  const size_t vgs = (size_t)(rs.v0 + v);
+  const size_t HW = (size_t)H * W;
+  {
+    const size_t tiles = (size_t)rs.gx * rs.gy;
+    ranges += vgs * tiles;
+    quad_maxc += vgs * 4 * tiles;
+    sorted_gauss += rs.inst_start[v];
+    rec += vgs * rs.P;
+    goff += vgs * rs.P;
+    final_Ts += vgs * HW;
+    n_contrib += vgs * HW;
+    dL_dcolor += (size_t)v * 3 * HW;
+    if (dL_ddepth) dL_ddepth += (size_t)v * HW;
+    if (dL_dalpha) dL_dalpha += (size_t)v * HW;
+    grow += (size_t)RW * rs.row_start[v];
+  }
+  const float* bg = rs.bg[v];
+  const int lane = threadIdx.x;
+  const int txi = tile % grid_x, tyi = tile / grid_x;
+  const uint2 range = ranges[tile];
+  const uint4 qm = reinterpret_cast<const uint4*>(quad_maxc)[tile];
+  const int qmaxc[4] = {(int)qm.x, (int)qm.y, (int)qm.z, (int)qm.w};
+  const int hi = __builtin_amdgcn_readfirstlane((int)max(max(qm.x, qm.y), max(qm.z, qm.w)));
+  const int lo = 0;
+
+  // per pixel (one per quadrant) the replay state and the pixel's upstream gradients
+  float T[4], S[4], Sd[4], S2[4], dp0[4], dp1[4], dp2[4], dpd[4], dpa[4], e0[4], e1[4], e2[4], nbg[4], nbg2[4];
+  uint32_t last[4];
+  const float lxf = (float)(txi * GSR_TILE_X + (lane & 7)), lyf = (float)(tyi * GSR_TILE_Y + (lane >> 3));
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const int px = txi * GSR_TILE_X + (q & 1) * 8 + (lane & 7), py = tyi * GSR_TILE_Y + (q >> 1) * 8 + (lane >> 3);
+    const bool inside = px < W && py < H;
+    const size_t pid = (size_t)py * W + px;
+    const float T_final = inside ? final_Ts[pid] : 0.0f;
+    T[q] = T_final;
+    last[q] = inside ? n_contrib[pid] : 0u;
+    float d[3] = {0.f, 0.f, 0.f};
+    float dd = 0.f, da = 0.f;
+    if (inside) {
+      d[0] = dL_dcolor[pid];
+      d[1] = dL_dcolor[HW + pid];
+      d[2] = dL_dcolor[2 * HW + pid];
+      if (dL_ddepth) dd = dL_ddepth[pid];
+      if (dL_dalpha) da = dL_dalpha[pid];
+      if (rs.cbg != nullptr) {
+#pragma clang fp contract(off)
+        const float am = 1.0f - (1.0f - T_final);
+        const float* bgi = rs.cbg + ((size_t)v * HW + pid) * 3;
+        const float* col = rs.ccolor + (size_t)v * 3 * HW + pid;
+        float dsum = 0.0f;
+#pragma unroll
+        for (int ch = 0; ch < 3; ++ch) {
+          const float b = bgi[ch];
+          const float pre = col[(size_t)ch * HW] + am * b;
+          const float gch = (pre >= 0.0f && pre <= 1.0f) ? d[ch] : 0.0f;
+          d[ch] = gch;
+          dsum -= gch * b;
+          if (rs.dcbg != nullptr) rs.dcbg[((size_t)v * HW + pid) * 3 + ch] = gch * am;
+        }
+        da = dsum + da;
+      }
+    }
+    dp0[q] = d[0], dp1[q] = d[1], dp2[q] = d[2], dpd[q] = dd, dpa[q] = da;
+    nbg[q] = -T_final * (bg[0] * d[0] + bg[1] * d[1] + bg[2] * d[2]);
+    e0[q] = e1[q] = e2[q] = 0.f;
+    if (TWO && inside) {
+      const float* d2 = rs.dpix2 + (size_t)v * 3 * HW;
+      e0[q] = d2[pid];
+      e1[q] = d2[HW + pid];
+      e2[q] = d2[2 * HW + pid];
+    }
+    nbg2[q] = TWO ? -T_final * (bg[0] * e0[q] + bg[1] * e1[q] + bg[2] * e2[q]) : 0.f;
+    S[q] = Sd[q] = S2[q] = 0.f;
+  }
+  const float ddelx_dx = 0.5f * W, ddely_dy = 0.5f * H;
+  const float4 zero4 = make_float4(0.f, 0.f, 0.f, 0.f);
+
+  // lane c stages candidate c (list position h - 1 - c) of each batch: its whole record, one batch ahead;
+  // indices two batches ahead
+  const uint32_t gmask = rs.gmask;
+  unsigned int* const reach32 = reinterpret_cast<unsigned int*>(reach) + (v >> 5);
+  const unsigned int vbit = 1u << (v & 31);
+  float4 na = zero4, nb = zero4, nc = zero4, nd = zero4, n2 = zero4;
+  uint32_t ngo = 0u, gi_next = 0u;
+  auto load = [&](uint32_t g) {
+    const float4* r = reinterpret_cast<const float4*>(rec + g);
+    na = r[0];
+    nb = r[1];
+    nc = r[2];
+    nd = r[3];
+    if (rs.col2 != nullptr) {
+      const float4 c2 = make_float4(rs.col2[3 * g], rs.col2[3 * g + 1], rs.col2[3 * g + 2], 0.f);
+      if (TWO)
+        n2 = c2;
+      else  // the second rasterizer call's colours replace the first's
+        nc = c2;
+    }
+    ngo = goff[g];
+#ifndef GSR_EXP_NOREACH
+    atomicOr(reach32 + 2 * g, vbit);  // the Gaussian gets a row in this view (k_view_grad reads it)
+#endif
+  };
+  if (hi > lo) {
+    if (hi - 1 - lane >= lo) load(sorted_gauss[range.x + hi - 1 - lane] & gmask);
+    if (hi - 65 - lane >= lo) gi_next = sorted_gauss[range.x + hi - 65 - lane] & gmask;
+  }
+
+  // hit-list sums of one (candidate, quadrant) pair -> moments about the candidate's mean (the flush of
+  // k_render_bwd), added to the candidate's running total as the quad DPP order does
+  float acca[NM], accb[NM];
+  auto pair_moments = [&](const int qq, const uint32_t e, float (&m)[NM]) {
+    const int st = (int)(e & 0xffffu), n = (int)(e >> 16);
+    float C[NG];
+#pragma unroll
+    for (int f = 0; f < NG; ++f) C[f] = 0.f;
+    for (int k = st; k < st + n; ++k) {
+      const float4 hv = hits[k];
+      const uint32_t p = __float_as_uint(hv.w);
+      const float x = (float)(p & 7u) - 3.5f, y = (float)(p >> 3) - 3.5f;
+      const float u = hv.x, w = hv.z;
+      C[0] += u;
+      C[1] = fmaf(u, x, C[1]);
+      C[2] = fmaf(u, y, C[2]);
+      C[3] = fmaf(u, x * x, C[3]);
+      C[4] = fmaf(u, x * y, C[4]);
+      C[5] = fmaf(u, y * y, C[5]);
+      const float4 d = planes[TWO ? 2 * p : p];
+      C[6] = fmaf(w, d.x, C[6]);
+      C[7] = fmaf(w, d.y, C[7]);
+      C[8] = fmaf(w, d.z, C[8]);
+      C[9] = fmaf(w, d.w, C[9]);
+      if constexpr (TWO) {
+        const float u1 = hv.y;
+        const float4 d2 = planes[2 * p + 1];
+        C[10 % NG] += u1;
+        C[11 % NG] = fmaf(u1, x, C[11 % NG]);
+        C[12 % NG] = fmaf(u1, y, C[12 % NG]);
+        C[13 % NG] = fmaf(w, d2.x, C[13 % NG]);
+        C[14 % NG] = fmaf(w, d2.y, C[14 % NG]);
+        C[15 % NG] = fmaf(w, d2.z, C[15 % NG]);
+      }
+    }
+    const float4 ga = s0[lane];
+    const float mx = ga.x - ((float)(txi * GSR_TILE_X + (qq & 1) * 8) + 3.5f);
+    const float my = ga.y - ((float)(tyi * GSR_TILE_Y + (qq >> 1) * 8) + 3.5f);
+    m[0] = C[0];
+    m[1] = mx * C[0] - C[1];
+    m[2] = my * C[0] - C[2];
+    m[3] = mx * (mx * C[0] - 2.f * C[1]) + C[3];
+    m[4] = mx * (my * C[0] - C[2]) - my * C[1] + C[4];
+    m[5] = my * (my * C[0] - 2.f * C[2]) + C[5];
+    m[6] = C[6];
+    m[7] = C[7];
+    m[8] = C[8];
+    m[9] = C[9];
+    if (TWO) {
+      m[10 % NM] = mx * C[10 % NG] - C[11 % NG];
+      m[11 % NM] = my * C[10 % NG] - C[12 % NG];
+      m[12 % NM] = C[13 % NG];
+      m[13 % NM] = C[14 % NG];
+      m[14 % NM] = C[15 % NG];
+    }
+  };
+  // the pending pairs of quadrant qq (lanes whose bit is set) into the running totals
+  auto flush = [&](const int qq, const unsigned long long pend) {
+    if (!((pend >> lane) & 1ull)) return;
+    float m[NM];
+    pair_moments(qq, list[lane], m);
+#pragma unroll
+    for (int i = 0; i < NM; ++i) {
+      if (qq == 0) acca[i] = m[i];
+      else if (qq == 1) acca[i] = acca[i] + m[i];
+      else if (qq == 2) accb[i] = m[i];
+      else accb[i] = accb[i] + m[i];
+    }
+  };
+
+  for (int h = hi; h > lo; h -= 64) {
+    const int rel_c = h - 1 - lane;
+    const bool staged = rel_c >= lo;
+    // this lane's candidate: pre-multiplied conic for gauss_power2 (.w of s1: list position), row slot
+    const float4 ca = make_float4(na.x, na.y, GSR_CONIC_K_AC * na.z, GSR_CONIC_K_B * na.w);
+    const float4 cb = make_float4(GSR_CONIC_K_AC * nb.x, nb.y, nb.z, __uint_as_float((uint32_t)rel_c));
+    uint32_t keep4 = 0u;
+    if (staged) {
+      s0[lane] = ca;
+      s1[lane] = cb;
+      s2[lane] = nc;
+      if (TWO) s3[lane] = n2;
+      const uint32_t dx_ = __float_as_uint(nd.x), dy_ = __float_as_uint(nd.y);
+      const int xmin = dx_ & 0xffff, ymin = dx_ >> 16, xmax = dy_ & 0xffff;
+      slot[lane] = ngo + (uint32_t)((tyi - ymin) * (xmax - xmin) + (txi - xmin));
+      // the staged conic back to (a, b, c) for the (padded, conservative) cull, as k_render_bwd does
+      const float4 r0 = make_float4(ca.x, ca.y, ca.z * (1.0f / GSR_CONIC_K_AC), ca.w * (1.0f / GSR_CONIC_K_B));
+      const float4 r1 = make_float4(cb.x * (1.0f / GSR_CONIC_K_AC), cb.y, cb.z, cb.w);
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+        if (rel_c < qmaxc[q] &&
+            quadrant_hit(r0, r1, (float)(txi * GSR_TILE_X + (q & 1) * 8), (float)(tyi * GSR_TILE_Y + (q >> 1) * 8)))
+          keep4 |= 1u << q;
+    }
+    // the next batch's records and the one after's indices
+    if (h - 64 > lo) {
+      if (h - 65 - lane >= lo) load(gi_next);
+      if (h - 129 - lane >= lo) gi_next = sorted_gauss[range.x + h - 129 - lane] & gmask;
+    }
+#pragma unroll
+    for (int i = 0; i < NM; ++i) acca[i] = accb[i] = 0.f;
+    __syncthreads();  // (one wave: orders the staging writes before other lanes' reads)
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const unsigned long long kq = __ballot((keep4 >> q) & 1u);
+      if (kq == 0ull) continue;
+      // this quadrant's dL/dpixel planes for the sums
+      planes[TWO ? 2 * lane : lane] = make_float4(dp0[q], dp1[q], dp2[q], dpd[q]);
+      if (TWO) planes[2 * lane + 1] = make_float4(e0[q], e1[q], e2[q], 0.f);
+      const float pxf = lxf + (float)((q & 1) * 8), pyf = lyf + (float)((q >> 1) * 8);
+      int fill = 0;
+      unsigned long long pend = 0ull, rest = kq;
+      int j = (int)__builtin_ctzll(rest);
+      float4 ga = s0[j], gb = s1[j], gc = s2[j];
+      float4 gd = TWO ? s3[j] : zero4;
+      while (true) {
+        rest &= rest - 1ull;
+        const int jn = rest != 0ull ? (int)__builtin_ctzll(rest) : j;
+        const float4 xa = s0[jn], xb = s1[jn], xc = s2[jn];
+        const float4 xd = TWO ? s3[jn] : zero4;
+        // the replay step of k_render_bwd (replay / replay2) on this quadrant's pixel
+        const uint32_t rel = __float_as_uint(gb.w);
+        const float dx = ga.x - pxf, dy = ga.y - pyf;
+        const float power2 = gauss_power2(ga.z, ga.w, gb.x, dx, dy);
+        const float G = __builtin_amdgcn_exp2f(power2);
+        const float alpha = fminf(GSR_ALPHA_MAX, gb.y * G);
+        const bool hit = rel < last[q] && power2 <= 0.0f && alpha >= GSR_ALPHA_MIN;
+        const float a_eff = hit ? alpha : 0.0f;
+        const float g_eff = hit ? G : 0.0f;
+        const float oma = 1.f - a_eff;
+        const float inv_1ma = fast_rcp(oma);
+        T[q] = T[q] * inv_1ma;
+        const float cd = fmaf(gc.x, dp0[q], fmaf(gc.y, dp1[q], fmaf(gc.z, dp2[q], dpa[q])));
+        float u, u1 = 0.f;
+        if (TWO) {
+          const float cd2 = fmaf(gd.x, e0[q], fmaf(gd.y, e1[q], gd.z * e2[q]));
+          u1 = g_eff * fmaf(T[q], fmaf(gb.z - Sd[q], dpd[q], cd - S[q]), inv_1ma * nbg[q]);
+          u = fmaf(g_eff, fmaf(T[q], cd2 - S2[q], inv_1ma * nbg2[q]), u1);
+          S2[q] = fmaf(a_eff, cd2, oma * S2[q]);
+        } else {
+          u = g_eff * fmaf(T[q], fmaf(gb.z - Sd[q], dpd[q], cd - S[q]), inv_1ma * nbg[q]);
+        }
+        const float w = a_eff * T[q];
+        S[q] = fmaf(a_eff, cd, oma * S[q]);
+        Sd[q] = fmaf(a_eff, gb.z, oma * Sd[q]);
+        const unsigned long long hm = __ballot(hit);
+        const int n = __popcll(hm);
+        if (fill + n > GSR_HCAP_TW) {
+          // list full: the finished pairs' sums now, then start over
+          __syncthreads();
+          flush(q, pend);
+          __syncthreads();
+          fill = 0;
+          pend = 0ull;
+        }
+        if (hit) hits[fill + (int)mask_rank(hm)] = make_float4(u, u1, w, __uint_as_float((uint32_t)lane));
+        if (lane == 0) list[j] = (uint32_t)fill | ((uint32_t)n << 16);
+        fill += n;
+        pend |= 1ull << j;
+        if (rest == 0ull) break;
+        ga = xa;
+        gb = xb;
+        gc = xc;
+        gd = xd;
+        j = jn;
+      }
+      __syncthreads();
+      flush(q, pend);
+      __syncthreads();  // (hits, list and planes are rewritten by the next quadrant)
+    }
+    if (staged) {
+      // ((q0 + q1) + (q2 + q3)) per moment, then the reference's terms (k_render_bwd's flush)
+      float m[NM];
+#pragma unroll
+      for (int i = 0; i < NM; ++i) m[i] = acca[i] + accb[i];
+      const float4 ga = s0[lane];
+      const float4 gb = s1[lane];
+      const float o = gb.y;
+      float4* row = grow + RW * (size_t)slot[lane];
+      const float k = o * (1.0f / 1.4426950408889634f);
+      {
+        const float dmx = k * ddelx_dx * (2.0f * ga.z * m[1] + ga.w * m[2]);
+        const float dmy = k * ddely_dy * (2.0f * gb.x * m[2] + ga.w * m[1]);
+        row[0] = make_float4(dmx, dmy, -0.5f * o * m[3], -0.5f * o * m[4]);
+      }
+      row[1] = make_float4(-0.5f * o * m[5], m[0], m[6], m[7]);
+      row[2] = TWO ? make_float4(m[8], m[9], m[12 % NM], m[13 % NM]) : make_float4(m[8], m[9], 0.f, 0.f);
+      if (TWO) {
+        const float dmx1 = k * ddelx_dx * (2.0f * ga.z * m[10 % NM] + ga.w * m[11 % NM]);
+        const float dmy1 = k * ddely_dy * (2.0f * gb.x * m[11 % NM] + ga.w * m[10 % NM]);
+        row[3] = make_float4(m[14 % NM], dmx1, dmy1, 0.f);
+      }
+    }
+    __syncthreads();  // (the staged batch is rewritten next)
+  }
+  GSR_TL_END(1, hi)
+}
+
 // Sums of the backward blend: hit lists (HITS) or matrix-core products.  Hit lists win where the
 // Gaussians are small (the two-colour SuGaR backward, C5); the matrix cores where they are large (C3).
 // GSR_BWD_SUMS=hits / mfma forces one (A/B).
@@ -1673,6 +2014,13 @@ static bool bwd_hit_lists(bool two) {
   if (e != nullptr && strcmp(e, "hits") == 0) return true;
   if (e != nullptr && strcmp(e, "mfma") == 0) return false;
   return two;
+}
+
+// Hit-list sums: one wave per tile walking the quadrants one after the other (k_render_bwd_tw) unless
+// GSR_BWD_KERNEL=quadrant (the workgroup of lockstep quadrant waves, k_render_bwd<·, true>).
+static bool bwd_tile_wave() {
+  const char* e = getenv("GSR_BWD_KERNEL");
+  return !(e != nullptr && strcmp(e, "quadrant") == 0);
 }
 
 void launch_render_backward(const RenderSet& rs, const GeomState& g, const uint32_t* sorted_gauss,
@@ -1686,6 +2034,14 @@ void launch_render_backward(const RenderSet& rs, const GeomState& g, const uint3
   const dim3 grid(block_grid(rs, 4) + extra);
   const uint32_t* items = split ? img.split_items : nullptr;
   const bool hits = bwd_hit_lists(rs.dpix2 != nullptr);
+  if (hits && extra == 0 && bwd_tile_wave()) {
+    auto kt = rs.dpix2 != nullptr ? k_render_bwd_tw<true> : k_render_bwd_tw<false>;
+    hipLaunchKernelGGL(kt, dim3(block_grid(rs, 4)), dim3(64), 0, stream, rs, (const uint2*)img.ranges,
+                       (const uint32_t*)img.quad_maxc, sorted_gauss, (const GaussRec*)g.rec, (const uint32_t*)g.goff,
+                       (const float*)img.final_T, (const uint32_t*)img.n_contrib, dL_dcolor, dL_ddepth, dL_dalpha,
+                       bw.grow, bw.reach);
+    return;
+  }
   auto kern = rs.dpix2 != nullptr ? (hits ? k_render_bwd<true, true> : k_render_bwd<true, false>)
                                   : (hits ? k_render_bwd<false, true> : k_render_bwd<false, false>);
   hipLaunchKernelGGL(kern, grid, dim3(256), 0, stream, rs, (const uint2*)img.ranges, (const uint32_t*)img.quad_maxc,
