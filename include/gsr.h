@@ -59,8 +59,9 @@ const char* gsr_version(void);
  *      path dL_dcov3D is required (the running dL/dcov3D carry), otherwise GSR_EINVAL.
  *   3  gsr_shade_views_forward / gsr_shade_views_backward (per-view light colours and shading modes);
  *      gsr_set_backward_chunks / gsr_grad_chunk_range (per-Gaussian sums in ranges, events for overlap).
+ *   4  gsr_set_image_bytes_ex (image buffers sized for the forward's split decision, which the buffer records).
  */
-#define GSR_ABI_VERSION 3
+#define GSR_ABI_VERSION 4
 int gsr_abi_version(void);
 /* Message of the last failing call on this thread ("" if none). */
 const char* gsr_last_error(void);
@@ -142,6 +143,11 @@ int gsr_backward(int P, int degree, int M, int K, int width, int height, const f
 size_t gsr_set_geom_bytes(int V, int P);
 size_t gsr_set_binning_bytes(int V, int P, const int* num_rendered, int width, int height);
 size_t gsr_set_image_bytes(int V, int width, int height);
+/* The image bytes of exactly this forward (gsr_set_image_bytes is the upper bound): the split backward's
+ * checkpoints only when the forward writes them (a launch of <= 4096 tiles on the quadrant waves, one colour
+ * set: 335 MB for one 1024^2 view, held until the backward).  two_colors != 0: gsr_set_render_two_colors.
+ * The forward records its decision in the buffer; the backward follows it whatever the environment says then. */
+size_t gsr_set_image_bytes_ex(int V, int P, const int* num_rendered, int width, int height, int two_colors);
 /* Scratch holding the gradient rows and per-(view, Gaussian) records of all V views; gsr_set_backward
  * also accepts less (>= what the largest single view needs) and then walks the views in groups that fit. */
 size_t gsr_set_backward_bytes(int V, int P, const int* num_rendered);

@@ -80,3 +80,23 @@ def test_oracle_library_builds_and_exports():
     for name in ("oracle_forward_f32", "oracle_forward_f64", "oracle_backward_f32", "oracle_backward_f64",
                  "oracle_eval_sh_f64", "oracle_cov3d_f64"):
         assert hasattr(lib, name)
+
+
+def test_image_bytes_follow_the_split_decision(monkeypatch):
+    """gsr_set_image_bytes_ex sizes the image buffer for the forward's split decision: with the split backward's
+    checkpoints (335 MB for one 1024^2 view) only when the forward writes them (one colour set, quadrant waves,
+    GSR_BWD_SPLIT not 0); gsr_set_image_bytes stays the upper bound."""
+    import ctypes
+
+    lib = _C.load_library()
+    K = (ctypes.c_int * 1)(5000)
+    full = lib.gsr_set_image_bytes(1, 1024, 1024)
+    monkeypatch.delenv("GSR_BWD_SPLIT", raising=False)
+    monkeypatch.delenv("GSR_FWD_KERNEL", raising=False)
+    split = lib.gsr_set_image_bytes_ex(1, 1000, K, 1024, 1024, 0)
+    two = lib.gsr_set_image_bytes_ex(1, 1000, K, 1024, 1024, 1)
+    assert split == full and two < full and full - two >= 4096 * 16 * 5 * 256 * 4 - 256
+    monkeypatch.setenv("GSR_BWD_SPLIT", "0")
+    assert lib.gsr_set_image_bytes_ex(1, 1000, K, 1024, 1024, 0) == two
+    K64 = (ctypes.c_int * 64)(*([5000] * 64))
+    assert lib.gsr_set_image_bytes_ex(64, 1000, K64, 1024, 1024, 0) == lib.gsr_set_image_bytes(64, 1024, 1024)

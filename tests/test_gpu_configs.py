@@ -311,7 +311,8 @@ def _quad_maxc(scene, cam):
                                      False, False)
     image = out[7].cpu().numpy()
     tiles = ((cam["W"] + 15) // 16) * ((cam["H"] + 15) // 16)
-    off = (8 * tiles + 255) // 256 * 256  # csrc/gsr_common.h ImageState: ranges, then quad_maxc
+    # csrc/gsr_common.h ImageState: split_mode (one 256-byte unit), ranges, then quad_maxc
+    off = 256 + (8 * tiles + 255) // 256 * 256
     return image[off:off + 16 * tiles].view(np.uint32).reshape(tiles, 4).max(1)
 
 
@@ -339,10 +340,10 @@ def test_split_backward_matches_whole_walk(size, monkeypatch):
     split = gpu_render(scene, cam, [0.3, 0.2, 0.1], grads=g)
     monkeypatch.setenv("GSR_BWD_SPLIT", "0")
     whole = gpu_render(scene, cam, [0.3, 0.2, 0.1], grads=g)
-    for k in ("alpha", "radii"):
+    # the forward that writes the checkpoints keeps its running totals in list order: its outputs are bitwise
+    # those of the launch without checkpoints (a view's bits do not depend on the launch size)
+    for k in ("alpha", "radii", "color", "depth"):
         assert np.array_equal(split[k], whole[k]), k
-    for k in ("color", "depth"):  # the split forward sums each chunk's blends, then the chunks
-        assert np.abs(split[k] - whole[k]).max() <= 1e-5 * max(1.0, float(np.abs(whole[k]).max())), k
     for k in ("g_means3D", "g_means2D", "g_opacity", "g_sh", "g_scales", "g_rotations"):
         ref = whole[k].astype(np.float64)
         err = float((np.abs(split[k] - ref) / np.maximum(1.0, np.abs(ref))).max())

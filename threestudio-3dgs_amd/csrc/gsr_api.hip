@@ -193,6 +193,14 @@ size_t gsr_set_image_bytes(int V, int width, int height) {
   ImageState::carve(nullptr, V, width, height, &b);
   return b;
 }
+size_t gsr_set_image_bytes_ex(int V, int P, const int* K, int width, int height, int two_colors) {
+  SegInfo seg;
+  long long total = 0;
+  if (V < 1 || V > GSR_SET_MAX || K == nullptr || inst_segments(V, K, seg, &total) != GSR_OK) return 0;
+  size_t b = 0;
+  ImageState::carve(nullptr, V, width, height, &b, split_forward(V, P, width, height, total, two_colors != 0));
+  return b;
+}
 // the running dL/dcov3D (P x 6) kept at the end of the work buffer across view groups
 static size_t carry_bytes(int P) { return align_up(sizeof(float) * 6 * (size_t)(P > 0 ? P : 1), 256); }
 
@@ -502,10 +510,13 @@ static int set_render(int V, int P, const int* K, int width, int height, const f
   GeomState g = GeomState::carve(geom, V, P, nullptr);
   const TilePack tp = tile_pack(P, width, height);
   BinningState b = BinningState::carve(binning, V, total, inst.blk[V], !tp.packed, nullptr);
-  ImageState img = ImageState::carve(image, V, width, height, nullptr);
+  // the split decision of this forward, recorded in the image state for its backward
+  const bool split = split_forward(V, P, width, height, total, colors2 != nullptr);
+  ImageState img = ImageState::carve(image, V, width, height, nullptr, split);
   const int gx = div_up(width, GSR_TILE_X), gy = div_up(height, GSR_TILE_Y);
   const int tres = tile_sort_result(width, height);
   inst.ndev = g.counters + 2 * V;  // kept instances per view (<= K, the list capacity)
+  GSR_HIP_CHECK(hipMemsetAsync(img.split_mode, split ? 1 : 0, sizeof(uint32_t), s));
   {
     PhaseScope ps(GSR_PHASE_BINNING, s);
     GSR_HIP_CHECK(hipMemsetAsync(img.ranges, 0, sizeof(uint2) * (size_t)V * gx * gy, s));
@@ -528,7 +539,8 @@ static int set_render(int V, int P, const int* K, int width, int height, const f
     rs.out_col2 = out_color2;
     rs.dpix2 = nullptr;
     rs.order = tile_order_on() ? img.order : nullptr;
-    rs.ckpt = split_on(V, P, width, height, total) ? img.ckpt : nullptr;
+    rs.ckpt = split ? img.ckpt : nullptr;
+    rs.split_mode = img.split_mode;
     rs.split_items = img.split_items;
     rs.split_cap = img.split_cap;
     rs.split_extra = split_extra(V, (size_t)gx * gy);
@@ -625,7 +637,8 @@ static int set_backward(int V, int P, int degree, int M, const int* K, int width
   GeomState g = GeomState::carve((void*)geom, V, P, nullptr);
   const TilePack tp = tile_pack(P, width, height);
   BinningState b = BinningState::carve((void*)binning, V, total, inst.blk[V], !tp.packed, nullptr);
-  ImageState img = ImageState::carve((void*)image, V, width, height, nullptr);
+  // (the checkpoints, carved last, exist when the forward split: split_mode says so on the device)
+  ImageState img = ImageState::carve((void*)image, V, width, height, nullptr, true);
   const int gx = div_up(width, GSR_TILE_X), gy = div_up(height, GSR_TILE_Y);
   const size_t HW = (size_t)width * height;
   const int tres = tile_sort_result(width, height);
@@ -659,8 +672,10 @@ static int set_backward(int V, int P, int degree, int M, const int* K, int width
     rs.out_col2 = nullptr;
     rs.dpix2 = two ? dL_dcolor2 + (size_t)g0 * 3 * HW : nullptr;
     rs.order = tile_order_on() ? img.order : nullptr;
-    // the forward checkpointed the first colour of the whole set (its V)
-    rs.ckpt = split_on(V, P, width, height, total) && !two && colors_override == nullptr ? img.ckpt : nullptr;
+    // a one-colour backward of the first colour may replay split chunks: whether the forward wrote them is its
+    // recorded decision (split_mode, read by the kernels), not this call's environment
+    rs.ckpt = split_fits(V, (size_t)gx * gy) && !two && colors_override == nullptr ? img.ckpt : nullptr;
+    rs.split_mode = img.split_mode;
     rs.split_items = img.split_items;
     rs.split_cap = img.split_cap;
     rs.split_extra = split_extra(V, (size_t)gx * gy);

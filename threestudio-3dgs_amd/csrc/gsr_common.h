@@ -287,16 +287,21 @@ struct ImageState {
   uint32_t* n_contrib; // [V][H*W]
   uint32_t* order;     // [V][super-tiles] each view's 2x2-tile super-tiles, most listed instances first
                        // (written after binning; the blends' dispatch order, gsr_render.hip block_map)
-  float* ckpt;         // split_fits sets: [V][tiles][GSR_SPLIT_NCK + 1][5][256] forward
-                       // chunk states for the split backward (ckpt_offset)
+  uint32_t* split_mode;  // [0] != 0: the forward wrote the split backward's checkpoints (set_render writes it; the
+                         // backward blend reads it on the device: the forward's decision, whatever the environment
+                         // says by the time the backward runs)
   uint32_t* split_items; // split sets: [0] count, then the tiles' later chunks (gsr_render.hip k_ckpt_suffix)
   uint32_t* split_cap;   // split sets: [V][tiles] the end of the stretch the tile's own workgroup walks
-  static ImageState carve(void* base, int V, int W, int H, size_t* bytes) {
+  float* ckpt;           // carved last, only for a forward that splits (with_ckpt):
+                         // [V][tiles][GSR_SPLIT_NCK + 1][5][256] chunk states for the split backward (ckpt_offset):
+                         // 335 MB for one 1024^2 view, held until its backward
+  static ImageState carve(void* base, int V, int W, int H, size_t* bytes, bool with_ckpt = true) {
     Carver c(base);
     ImageState s;
     const size_t nv = (size_t)(V > 0 ? V : 1);
     const size_t tiles = (size_t)div_up(W, GSR_TILE_X) * div_up(H, GSR_TILE_Y);
     const size_t pix = (size_t)W * H;
+    s.split_mode = c.take<uint32_t>(1);
     s.ranges = c.take<uint2>(nv * (tiles > 0 ? tiles : 1));
     s.quad_maxc = c.take<uint32_t>(nv * 4 * (tiles > 0 ? tiles : 1));
     s.tile_info = c.take<uint4>(nv * (tiles > 0 ? tiles : 1));
@@ -306,9 +311,9 @@ struct ImageState {
     const size_t st = (size_t)((div_up(W, GSR_TILE_X) + 1) >> 1) * ((div_up(H, GSR_TILE_Y) + 1) >> 1);
     s.order = c.take<uint32_t>(nv * (st > 0 ? st : 1));
     const bool split = split_fits(V, tiles);
-    s.ckpt = c.take<float>(split ? ckpt_offset(nv, tiles, 0, 0) : 1);
     s.split_items = c.take<uint32_t>(split ? 1 + (size_t)split_extra(V, tiles) : 1);
     s.split_cap = c.take<uint32_t>(split ? nv * tiles : 1);
+    s.ckpt = c.take<float>(split && with_ckpt ? ckpt_offset(nv, tiles, 0, 0) : 1);
     if (bytes) *bytes = align_up(c.off, 256);
     return s;
   }

@@ -64,6 +64,7 @@ struct RenderSet {
   // split backward (gsr_render.hip split_on): the forward writes its checkpoints here, the backward walks the
   // tiles in chunks from them; null = off
   float* ckpt;
+  const uint32_t* split_mode;  // backward: ImageState::split_mode (did the forward write the checkpoints?)
   uint32_t* split_items;  // with ckpt: the later chunks' backward items (ImageState::split_items)
   uint32_t* split_cap;    // with ckpt: ImageState::split_cap
   int split_extra;        // with ckpt: split_extra(the set's V, tiles)
@@ -71,6 +72,11 @@ struct RenderSet {
 // backward tile splitting on for a set of V views (split_fits) whose forward takes the quadrant-wave kernel
 // (GSR_BWD_SPLIT=0 turns it off); instances = the set's K total
 bool split_on(int V, int P, int width, int height, long long instances);
+// the forward of this set writes split checkpoints: split_on for one colour set (the two-colour backward never
+// splits); the image buffer holds checkpoints only then (gsr_set_image_bytes_ex)
+inline bool split_forward(int V, int P, int width, int height, long long instances, bool two_colors) {
+  return !two_colors && split_on(V, P, width, height, instances);
+}
 // Each view's super-tiles by listed instances, heaviest first (after binning) — gsr_render.hip
 void launch_tile_order(int V, int gx, int gy, const uint2* ranges, uint32_t* order, hipStream_t stream);
 // GSR_TILE_ORDER=raster: the blends dispatch views in turn in raster order (A/B); the order is still written

@@ -220,12 +220,8 @@ __global__ __launch_bounds__(64) void k_render_fwd(RenderSet rs,
   for (int base = 0; base < n; base += 64) {
     if (__all(done)) break;
     if (CK && base > 0 && base % GSR_SPLIT_CH == 0 && base <= GSR_SPLIT_NCK * GSR_SPLIT_CH) {
-      // chunk `chunk` ends: its sums into its slot and the running totals, T into the next one's slot
+      // chunk `chunk` ends: its sums into its slot, T into the next one's slot
       reinterpret_cast<float4*>(ckpt + (size_t)chunk * GSR_CKPT_FIELDS * 256 + 256)[cpix] = make_float4(Pr, Pg, Pb, Pd);
-      Cr += Pr;
-      Cg += Pg;
-      Cb += Pb;
-      D += Pd;
       ++chunk;
       ckpt[(size_t)chunk * GSR_CKPT_FIELDS * 256 + cpix] = T;
       Pr = Pg = Pb = Pd = 0.f;
@@ -273,17 +269,17 @@ __global__ __launch_bounds__(64) void k_render_fwd(RenderSet rs,
       // non-blending lanes run the same arithmetic with alpha = 0 (no change), no selects of state
       const float a_eff = blend ? alpha : 0.0f;
       const float aT = a_eff * T;
+      // the running totals in list order whatever the launch (the outputs' bits do not depend on whether the
+      // launch writes checkpoints), and beside them the chunk's own sums for the split backward
+      Cr = fmaf(c.x, aT, Cr);
+      Cg = fmaf(c.y, aT, Cg);
+      Cb = fmaf(c.z, aT, Cb);
+      D = fmaf(b.z, aT, D);
       if (CK) {
-        // the chunk's own sums (added to the totals at its end: the chunked sum, no second accumulation)
         Pr = fmaf(c.x, aT, Pr);
         Pg = fmaf(c.y, aT, Pg);
         Pb = fmaf(c.z, aT, Pb);
         Pd = fmaf(b.z, aT, Pd);
-      } else {
-        Cr = fmaf(c.x, aT, Cr);
-        Cg = fmaf(c.y, aT, Cg);
-        Cb = fmaf(c.z, aT, Cb);
-        D = fmaf(b.z, aT, D);
       }
       if (C2) {
         Er = fmaf(e.x, aT, Er);
@@ -299,12 +295,6 @@ __global__ __launch_bounds__(64) void k_render_fwd(RenderSet rs,
       e = en;
     }
     __syncthreads();
-  }
-  if (CK) {
-    Cr += Pr;
-    Cg += Pg;
-    Cb += Pb;
-    D += Pd;
   }
   if (inside) {
     const size_t pid = (size_t)py * W + px;
@@ -1650,8 +1640,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(TWO ? 4 : 5
     unsigned long long* __restrict__ reach, int extra, const uint32_t* __restrict__ items) {
   __shared__ BwdLDS<TWO, HITS> s;
   int v, tile, chunk = 0;
+  // the forward's split decision (ImageState::split_mode): checkpoints and items exist only then
+  const bool split = !TWO && rs.ckpt != nullptr && *rs.split_mode != 0u;
   if (!TWO && (int)blockIdx.x < extra) {
-    if (blockIdx.x >= items[0]) return;
+    if (!split || blockIdx.x >= items[0]) return;
     const uint32_t it = items[1 + blockIdx.x];
     v = (int)(it >> 26) - rs.v0;
     if (v < 0 || v >= rs.V) return;  // another view group's tile
@@ -1661,7 +1653,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(TWO ? 4 : 5
     int q_unused;
     if (!block_map<4>((int)blockIdx.x - extra, rs, v, tile, q_unused)) return;
   }
-  bwd_tile<TWO, HITS>(s, rs, v, tile, chunk, rs.ckpt != nullptr && !TWO, ranges, quad_maxc, sorted_gauss, rec, goff, final_Ts,
+  bwd_tile<TWO, HITS>(s, rs, v, tile, chunk, split, ranges, quad_maxc, sorted_gauss, rec, goff, final_Ts,
                 n_contrib, dL_dcolor, dL_ddepth, dL_dalpha, grow, reach);
 }
 

@@ -67,6 +67,7 @@ SIGNATURES = {
     "gsr_set_geom_bytes": (_sz, [_i, _i]),
     "gsr_set_binning_bytes": (_sz, [_i, _i, ctypes.POINTER(_i), _i, _i]),
     "gsr_set_image_bytes": (_sz, [_i, _i, _i]),
+    "gsr_set_image_bytes_ex": (_sz, [_i, _i, ctypes.POINTER(_i), _i, _i, _i]),
     "gsr_set_backward_bytes": (_sz, [_i, _i, ctypes.POINTER(_i)]),
     "gsr_set_preprocess": (
         _i,
@@ -147,7 +148,7 @@ def host_trace_read(reset: bool = True) -> dict:
     return out
 
 
-ABI_VERSION = 3  # include/gsr.h GSR_ABI_VERSION this binding is written against
+ABI_VERSION = 4  # include/gsr.h GSR_ABI_VERSION this binding is written against
 
 
 def load_library(path: str | None = None):
@@ -272,7 +273,8 @@ def rasterize_gaussians(bg, means3D, colors, opacity, scales, rotations, scale_m
         global LAST_GEOM
         LAST_GEOM = geom
     binning = torch.empty(int(lib.gsr_binning_bytes(num_rendered, W, H)), **u8)
-    image = torch.empty(int(lib.gsr_image_bytes(W, H)), **u8)
+    # sized for this forward's split decision (no split checkpoints unless the forward writes them)
+    image = torch.empty(int(lib.gsr_set_image_bytes_ex(1, P, (ctypes.c_int * 1)(num_rendered), W, H, 0)), **u8)
     _check(lib.gsr_forward_render(P, num_rendered, W, H, _ptr(bg), _ptr(geom), _ptr(binning), _ptr(image),
                                   _ptr(out_color), _ptr(out_depth), _ptr(out_alpha), stream))
     return num_rendered, out_color, out_depth, out_alpha, radii, geom, binning, image

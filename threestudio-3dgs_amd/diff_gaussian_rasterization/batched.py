@@ -123,7 +123,8 @@ class _RasterizeViews(torch.autograd.Function):
             _C.RECENT_FORWARDS.extend((k, H, W) for k in vs.K)
             Karr = vs.Karr = _arr(ctypes.c_int, vs.K)
             vs.binning = torch.empty(int(lib.gsr_set_binning_bytes(vs.V, P, Karr, W, H)), dtype=torch.uint8, device=dev)
-            vs.image = torch.empty(int(lib.gsr_set_image_bytes(vs.V, W, H)), dtype=torch.uint8, device=dev)
+            vs.image = torch.empty(int(lib.gsr_set_image_bytes_ex(vs.V, P, Karr, W, H, int(c2 is not None))),
+                                   dtype=torch.uint8, device=dev)
             sl = slice(vs.lo, vs.hi)
             if c2 is not None:
                 _C._check(lib.gsr_set_render_two_colors(
