@@ -8,7 +8,7 @@ import numpy as np
 import torch
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-for p in (os.path.join(ROOT, "threestudio-3dgs_amd"), os.path.join(ROOT, "tests")):
+for p in (os.path.join(ROOT, "threestudio-3dgs_amd"), os.path.join(ROOT, "tests"), os.path.join(ROOT, "oracle")):
     sys.path.insert(0, p)
 
 from gsr_testutil import gs, make_camera  # noqa: E402
