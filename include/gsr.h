@@ -59,7 +59,8 @@ const char* gsr_version(void);
  *      path dL_dcov3D is required (the running dL/dcov3D carry), otherwise GSR_EINVAL.
  *   3  gsr_shade_views_forward / gsr_shade_views_backward (per-view light colours and shading modes);
  *      gsr_set_backward_chunks / gsr_grad_chunk_range (per-Gaussian sums in ranges, events for overlap).
- *   4  gsr_set_image_bytes_ex (image buffers sized for the forward's split decision, which the buffer records).
+ *   4  gsr_set_image_bytes_ex (image buffers sized for the forward's split decision, which the buffer records);
+ *      gsr_profile_kernel (the blend kernels the phases ran).
  */
 #define GSR_ABI_VERSION 4
 int gsr_abi_version(void);
@@ -297,6 +298,10 @@ int gsr_set_backward_composite(int V, int P, int degree, int M, const int* num_r
 #define GSR_NUM_PHASES 6
 int gsr_profile_enable(int enable);
 int gsr_profile_read(double* ms, long long* launches, int reset);
+/* The blend kernel the last GSR_PHASE_RENDER_FWD / GSR_PHASE_RENDER_BWD launch of this process used, as
+ * rocprofv3 names it (e.g. "k_render_bwd<false, false>"); "" for other phases or before any launch.  Lets a
+ * caller attribute committed PMC counters to the kernel actually timed. */
+const char* gsr_profile_kernel(int phase);
 
 /*
  * Fused background composite of the background renderer (replaces the torch epilogue of

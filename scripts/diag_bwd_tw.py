@@ -19,7 +19,7 @@ def main():
     from test_gpu_configs import _settings
 
     two = len(sys.argv) < 2 or sys.argv[1] == "two"
-    os.environ["GSR_BWD_SUMS"] = "hits"
+    os.environ["GSR_BWD_SUMS"] = "hits" if two or (len(sys.argv) > 2 and sys.argv[2] == "hits") else "mfma"
     os.environ["GSR_BWD_SPLIT"] = "0"
     dev = "cuda"
     scene = gs.make_sugar_scene(5, sh_degree=0, seed=3)

@@ -262,10 +262,10 @@ def test_batched_views_match_per_view(nviews, monkeypatch):
 @pytest.mark.parametrize("switch", ["fwd_kernel", "dispatch_order", "bwd_kernel"])
 @pytest.mark.parametrize("kind", ["ball_composite", "sugar_two_colors"])
 def test_forward_kernels_bitwise(kind, switch, monkeypatch):
-    """fwd_kernel: the one-wave-per-tile forward, the quadrant-wave forward and the quadrant waves sharing
-    one staged batch per tile (GSR_FWD_KERNEL) blend exactly the same candidates per pixel in the same order; dispatch_order: the blends' work-ordered
+    """fwd_kernel: the one-wave-per-tile forward and the quadrant-wave forward (GSR_FWD_KERNEL) blend exactly
+    the same candidates per pixel in the same order; dispatch_order: the blends' work-ordered
     dispatch and raster order (GSR_TILE_ORDER=raster) only change which workgroup starts first; bwd_kernel: the
-    hit-list backward as one wave per tile or as four lockstep quadrant waves (GSR_BWD_KERNEL).  Every
+    backward blend as one wave per tile or as four lockstep quadrant waves (GSR_BWD_KERNEL).  Every
     output — colour, depth, alpha, the composite, the second colour set, radii — and every gradient (the
     backward reads the forward's per-pixel state) must be bitwise equal."""
     import torch
@@ -289,9 +289,9 @@ def test_forward_kernels_bitwise(kind, switch, monkeypatch):
             monkeypatch.setenv("GSR_FWD_KERNEL", kernel)
             monkeypatch.setenv("GSR_BWD_SPLIT", "0")  # the tile-wave forward writes no split checkpoints
         elif switch == "bwd_kernel":
-            # hit-list sums: one wave per tile walking the quadrants in turn (k_render_bwd_tw) vs the workgroup of
-            # lockstep quadrant waves (k_render_bwd<·, true>)
-            monkeypatch.setenv("GSR_BWD_SUMS", "hits")
+            # one wave per tile walking the quadrants in turn (k_render_bwd_tw / _twm) vs the workgroup of lockstep
+            # quadrant waves (k_render_bwd): hit-list sums for the two colours, matrix-core sums for one
+            monkeypatch.setenv("GSR_BWD_SUMS", "hits" if kind == "sugar_two_colors" else "mfma")
             monkeypatch.setenv("GSR_BWD_SPLIT", "0")
             monkeypatch.setenv("GSR_BWD_KERNEL", "tile" if kernel == "tile" else "quadrant")
         elif kernel == "tile":
@@ -322,6 +322,3 @@ def test_forward_kernels_bitwise(kind, switch, monkeypatch):
     tile, quad = run("tile"), run("quadrant")
     for i, (x, y) in enumerate(zip(tile, quad)):
         assert torch.equal(x, y), f"output {i} differs: {float((x.double() - y.double()).abs().max())}"
-    if switch == "fwd_kernel":  # the quadrant waves sharing each staged batch per tile (k_render_fwd_shared)
-        for i, (x, y) in enumerate(zip(run("shared"), quad)):
-            assert torch.equal(x, y), f"shared: output {i} differs: {float((x.double() - y.double()).abs().max())}"

@@ -937,6 +937,10 @@ int gsr_profile_read(double* ms, long long* launches, int reset) {
   return GSR_OK;
 }
 
+const char* gsr_profile_kernel(int phase) {
+  return phase == GSR_PHASE_RENDER_FWD ? blend_kernel_name(0) : phase == GSR_PHASE_RENDER_BWD ? blend_kernel_name(1) : "";
+}
+
 int gsr_mark_visible(int P, const float* means3D, const float* viewmatrix, const float* projmatrix,
                      uint8_t* present, void* stream) {
   if (P < 0) return fail(GSR_EINVAL, "%s", "P must be >= 0");

@@ -72,6 +72,8 @@ struct RenderSet {
 // backward tile splitting on for a set of V views (split_fits) whose forward takes the quadrant-wave kernel
 // (GSR_BWD_SPLIT=0 turns it off); instances = the set's K total
 bool split_on(int V, int P, int width, int height, long long instances);
+// the blend kernel the last forward (0) / backward (1) blend launch used, as rocprofv3 names it
+const char* blend_kernel_name(int which);
 // the forward of this set writes split checkpoints: split_on for one colour set (the two-colour backward never
 // splits); the image buffer holds checkpoints only then (gsr_set_image_bytes_ex)
 inline bool split_forward(int V, int P, int width, int height, long long instances, bool two_colors) {

@@ -117,6 +117,12 @@ __device__ __forceinline__ float vsel(unsigned long long m, float if_set, float 
   return r;
 }
 
+// bg . dL/dpixel with an explicit operation order (the backward kernels' background terms: every kernel
+// variant forms the same bits, independent of how the compiler would contract the expression)
+__device__ __forceinline__ float bg_dot3(const float* bg, float d0, float d1, float d2) {
+  return fmaf(bg[2], d2, fmaf(bg[1], d1, bg[0] * d0));
+}
+
 __device__ __forceinline__ float quad_form(float a, float b, float c, float u, float v) {
   return fmaf(a * u, u, fmaf(2.0f * b * u, v, c * v * v));
 }
@@ -638,185 +644,6 @@ __global__ __launch_bounds__(64) void k_render_fwd_tile(RenderSet rs, const uint
 #endif
 }
 
-// Forward, one 256-thread workgroup per 16x16 tile sharing each batch of 64 candidates: wave q blends 8x8
-// quadrant q exactly as the quadrant-wave kernel does (same candidates per pixel, same order, same operations:
-// bitwise identical outputs), but the batch's records are gathered once per tile — each wave loads one 16-B
-// piece of every candidate (wave 0 rec.a, 1 rec.b, 2 rec.c, 3 the second colour), so a record line is read
-// once instead of once per quadrant wave (the quadrant-wave kernel's C5 forward moved 5.6x its algorithmic
-// bytes, profiles/r03d_sugar_traffic.json).  The batches are double-buffered in LDS (one barrier per batch);
-// each wave culls the staged batch for its quadrant (quadrant_hit on the raw conic) and walks its kept
-// candidates by scalar bit scans of the ballot mask (no compaction).  A wave whose pixels are all done keeps
-// staging for the others; the workgroup stops when all four are done (flags written before the barrier).
-template <bool C2>
-__global__ __launch_bounds__(256) void k_render_fwd_shared(RenderSet rs, const uint2* __restrict__ ranges,
-                                                          const uint32_t* __restrict__ sorted_gauss,
-                                                          const GaussRec* __restrict__ rec,
-                                                          float* __restrict__ out_color, float* __restrict__ out_depth,
-                                                          float* __restrict__ out_alpha, float* __restrict__ final_T,
-                                                          uint32_t* __restrict__ n_contrib,
-                                                          uint32_t* __restrict__ quad_maxc) {
-  // [buffer][candidate]: raw conic pieces for the cull, pre-multiplied ones for the blend (slot 64: the
-  // look-ahead read past a wave's last kept candidate, never used)
-  __shared__ float4 sR0[2][64], sR1[2][64], sA[2][65], sB[2][65], sC[2][65];
-  __shared__ float4 sE[2][C2 ? 65 : 1];
-  __shared__ uint32_t sdone[2][4];
-  int v, tile, q_unused;
-  if (!block_map<4>(blockIdx.x, rs, v, tile, q_unused)) return;
-  GSR_TL_BEGIN
-  const int q = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
-  const int lane = threadIdx.x & 63;
-  const int W = rs.W, H = rs.H, grid_x = rs.gx;
-  const size_t HWs = (size_t)W * H;
-  {
-    const size_t vg = (size_t)(rs.v0 + v), tiles = (size_t)rs.gx * rs.gy;
-    ranges += vg * tiles;
-    quad_maxc += vg * 4 * tiles;
-    sorted_gauss += rs.inst_start[v];
-    rec += vg * rs.P;
-    out_color += vg * 3 * HWs;
-    out_depth += vg * HWs;
-    out_alpha += vg * HWs;
-    final_T += vg * HWs;
-    n_contrib += vg * HWs;
-  }
-  const float* bg = rs.bg[v];
-  const int qx0 = (tile % grid_x) * GSR_TILE_X + (q & 1) * 8;
-  const int qy0 = (tile / grid_x) * GSR_TILE_Y + (q >> 1) * 8;
-  const int px = qx0 + (lane & 7), py = qy0 + (lane >> 3);
-  const bool inside = px < W && py < H;
-  const float pxf = (float)px, pyf = (float)py;
-  const uint2 range = ranges[tile];
-  const int n = (int)(range.y - range.x);
-  const uint32_t gmask = rs.gmask;
-  const float4 zero4 = make_float4(0.f, 0.f, 0.f, 0.f);
-  const float* col2 = rs.col2;
-  const float4* recp = reinterpret_cast<const float4*>(rec);
-
-  bool done = !inside;
-  float T = 1.0f, Cr = 0.f, Cg = 0.f, Cb = 0.f, D = 0.f;
-  float Er = 0.f, Eg = 0.f, Eb = 0.f;
-  uint32_t last_contributor = 0;
-#ifdef GSR_TIMELINE
-  unsigned long long pc_eval = 0, pc_slot = 0;
-#endif
-  // this wave's piece of a candidate's record
-  const bool loader = C2 || q < 3;
-  auto piece = [&](uint32_t g) -> float4 {
-    if (q < 3) return recp[4 * (size_t)g + q];
-    return make_float4(col2[3 * (size_t)g], col2[3 * (size_t)g + 1], col2[3 * (size_t)g + 2], 0.f);
-  };
-  float4 np = zero4;
-  uint32_t gi_next = 0u;
-  if (loader && lane < n) np = piece(sorted_gauss[range.x + lane] & gmask);
-  if (loader && 64 + lane < n) gi_next = sorted_gauss[range.x + 64 + lane] & gmask;
-  int buf = 0;
-  for (int base = 0; base < n; base += 64, buf ^= 1) {
-    const int i = base + lane;
-    // stage this batch (the conic pre-multiplied for gauss_power2 as the other kernels do; .w of sB: 1 + list
-    // position)
-    if (q == 0) {
-      sR0[buf][lane] = np;
-      sA[buf][lane] = make_float4(np.x, np.y, GSR_CONIC_K_AC * np.z, GSR_CONIC_K_B * np.w);
-    } else if (q == 1) {
-      sR1[buf][lane] = np;
-      sB[buf][lane] = make_float4(GSR_CONIC_K_AC * np.x, np.y, np.z, __uint_as_float((uint32_t)(i + 1)));
-    } else if (q == 2) {
-      sC[buf][lane] = np;
-    } else if (C2) {
-      sE[buf][lane] = np;
-    }
-    const bool wave_done = __all(done);
-    if (lane == 0) sdone[buf][q] = wave_done ? 1u : 0u;
-    // the next batch's pieces (one batch ahead) and indices (two ahead)
-    if (loader && base + 64 + lane < n) np = piece(gi_next);
-    if (loader && base + 128 + lane < n) gi_next = sorted_gauss[range.x + base + 128 + lane] & gmask;
-    __syncthreads();
-    if (sdone[buf][0] & sdone[buf][1] & sdone[buf][2] & sdone[buf][3]) break;
-    if (wave_done) continue;
-    bool keep = false;
-    if (i < n) keep = quadrant_hit(sR0[buf][lane], sR1[buf][lane], (float)qx0, (float)qy0);
-    unsigned long long m = __ballot(keep);
-    if (m == 0ull) continue;
-    int k = (int)__builtin_ctzll(m);
-    float4 a = sA[buf][k], b = sB[buf][k], c = sC[buf][k], e = C2 ? sE[buf][k] : zero4;
-    for (int j = 1;; ++j) {
-      m &= m - 1ull;
-      const int kn = m != 0ull ? (int)__builtin_ctzll(m) : 64;
-      const float4 an = sA[buf][kn], bn = sB[buf][kn], cn = sC[buf][kn];
-      const float4 en = C2 ? sE[buf][kn] : zero4;
-      const float dx = a.x - pxf, dy = a.y - pyf;
-      const float power2 = gauss_power2(a.z, a.w, b.x, dx, dy);  // log2(e) * power
-      const float alpha = fminf(GSR_ALPHA_MAX, b.y * __builtin_amdgcn_exp2f(power2));
-#ifdef GSR_TIMELINE
-      pc_eval += done ? 0ull : 1ull;
-      pc_slot += 1ull;
-#endif
-      const bool ok = !done && power2 <= 0.0f && alpha >= GSR_ALPHA_MIN;
-      const float test_T = T * (1.0f - alpha);
-      const bool term = ok && test_T < GSR_T_EPS;
-      const bool blend = ok && !term;
-      const float a_eff = blend ? alpha : 0.0f;
-      const float aT = a_eff * T;
-      Cr = fmaf(c.x, aT, Cr);
-      Cg = fmaf(c.y, aT, Cg);
-      Cb = fmaf(c.z, aT, Cb);
-      D = fmaf(b.z, aT, D);
-      if (C2) {
-        Er = fmaf(e.x, aT, Er);
-        Eg = fmaf(e.y, aT, Eg);
-        Eb = fmaf(e.z, aT, Eb);
-      }
-      T = blend ? test_T : T;
-      last_contributor = blend ? __float_as_uint(b.w) : last_contributor;
-      done = done || term;
-      if (m == 0ull) break;
-      if ((j & 7) == 0 && __all(done)) break;
-      a = an;
-      b = bn;
-      c = cn;
-      e = en;
-    }
-  }
-  if (inside) {
-    const size_t pid = (size_t)py * W + px;
-    final_T[pid] = T;
-    n_contrib[pid] = last_contributor;
-    {
-#pragma clang fp contract(off)
-      out_color[pid] = Cr + T * bg[0];
-      out_color[HWs + pid] = Cg + T * bg[1];
-      out_color[2 * HWs + pid] = Cb + T * bg[2];
-    }
-    out_depth[pid] = D;
-    out_alpha[pid] = 1.0f - T;
-    if (C2) {
-#pragma clang fp contract(off)
-      float* o2 = rs.out_col2 + (size_t)(rs.v0 + v) * 3 * HWs + pid;
-      o2[0] = Er + T * bg[0];
-      o2[HWs] = Eg + T * bg[1];
-      o2[2 * HWs] = Eb + T * bg[2];
-    }
-    if (rs.cbg != nullptr) {
-#pragma clang fp contract(off)
-      const float am = 1.0f - (1.0f - T);
-      const float* bgi = rs.cbg + ((size_t)v * HWs + pid) * 3;
-      float* cp = rs.comp + (size_t)v * 3 * HWs + pid;
-      cp[0] = fminf(fmaxf((Cr + T * bg[0]) + am * bgi[0], 0.0f), 1.0f);
-      cp[HWs] = fminf(fmaxf((Cg + T * bg[1]) + am * bgi[1], 0.0f), 1.0f);
-      cp[2 * HWs] = fminf(fmaxf((Cb + T * bg[2]) + am * bgi[2], 0.0f), 1.0f);
-    }
-  }
-  uint32_t mc = last_contributor;
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) mc = max(mc, (uint32_t)__shfl_xor((int)mc, o, 64));
-  if (lane == 0) quad_maxc[4 * tile + q] = mc;
-#ifdef GSR_TIMELINE
-  atomicAdd(&g_pairs[0], pc_eval);
-  atomicAdd(&g_pairs[1], pc_slot);
-#endif
-  GSR_TL_END(0, mc)
-}
-
 // One block per view: bucket its super-tiles by the bit length of their listed instances (sum over the
 // 2x2 tiles), heaviest bucket first (LDS counts, exclusive scan, LDS-atomic placement: the order inside a
 // bucket may vary between runs — it only changes which workgroup starts first, never a result).
@@ -921,18 +748,18 @@ __global__ __launch_bounds__(256) void k_ckpt_suffix(RenderSet rs, const uint32_
 // forces one (A/B and tests).
 static bool fwd_tile_kernel(long long instances, long long gaussians, int views) {
   const char* e = getenv("GSR_FWD_KERNEL");
-  if (e != nullptr && (strcmp(e, "quadrant") == 0 || strcmp(e, "shared") == 0)) return false;
+  if (e != nullptr && strcmp(e, "quadrant") == 0) return false;
   if (e != nullptr && strcmp(e, "tile") == 0) return true;
   return views >= 48 && gaussians > 0 && instances >= 3 * gaussians;
 }
-// Otherwise the quadrant waves: sharing each staged batch per tile (k_render_fwd_shared, one gather per
-// candidate and tile) unless the launch writes the split backward's checkpoints (only the free-running
-// quadrant-wave kernel keeps them) or GSR_FWD_KERNEL=quadrant.
-static bool fwd_shared_kernel(bool ckpt) {
-  if (ckpt) return false;
-  const char* e = getenv("GSR_FWD_KERNEL");
-  return !(e != nullptr && strcmp(e, "quadrant") == 0);
-}
+// (Measured and removed, round 4: the quadrant waves of a tile sharing one staged copy of each batch in LDS —
+// one record gather per candidate and tile instead of per quadrant wave — with a workgroup barrier per batch:
+// C5 render_fwd 0.146 -> 0.277 ms/view, 8-view C3 sets 0.052 -> 0.070; the quadrant waves' independence is
+// worth more than the 5.6x redundant record traffic; profiles/r04/fwd_shared_ab.txt.)
+
+// the blend kernels a launch used (gsr_profile_kernel; rocprofv3's names of them)
+static const char* g_blend_kernel[2] = {"", ""};
+const char* blend_kernel_name(int which) { return which >= 0 && which < 2 ? g_blend_kernel[which] : ""; }
 
 void launch_render_forward(const RenderSet& rs, const GeomState& g, const uint32_t* sorted_gauss,
                            const ImageState& img, float* out_color, float* out_depth, float* out_alpha,
@@ -941,6 +768,7 @@ void launch_render_forward(const RenderSet& rs, const GeomState& g, const uint32
   if (nt <= 0 || rs.V <= 0) return;
   if (fwd_tile_kernel(instances, (long long)rs.V * rs.P, rs.V)) {
     const dim3 grid(block_grid(rs, 4));
+    g_blend_kernel[0] = rs.col2 != nullptr ? "k_render_fwd_tile<true>" : "k_render_fwd_tile<false>";
     if (rs.col2 != nullptr)
       hipLaunchKernelGGL(k_render_fwd_tile<true>, grid, dim3(64), 0, stream, rs, (const uint2*)img.ranges,
                          sorted_gauss, (const GaussRec*)g.rec, out_color, out_depth, out_alpha, img.final_T,
@@ -949,14 +777,11 @@ void launch_render_forward(const RenderSet& rs, const GeomState& g, const uint32
       hipLaunchKernelGGL(k_render_fwd_tile<false>, grid, dim3(64), 0, stream, rs, (const uint2*)img.ranges,
                          sorted_gauss, (const GaussRec*)g.rec, out_color, out_depth, out_alpha, img.final_T,
                          img.n_contrib, img.quad_maxc);
-  } else if (fwd_shared_kernel(rs.ckpt != nullptr)) {
-    auto kern = rs.col2 != nullptr ? k_render_fwd_shared<true> : k_render_fwd_shared<false>;
-    hipLaunchKernelGGL(kern, dim3(block_grid(rs, 4)), dim3(256), 0, stream, rs, (const uint2*)img.ranges,
-                       sorted_gauss, (const GaussRec*)g.rec, out_color, out_depth, out_alpha, img.final_T,
-                       img.n_contrib, img.quad_maxc);
   } else {
     auto kern = rs.col2 != nullptr ? (rs.ckpt != nullptr ? k_render_fwd<true, true> : k_render_fwd<true, false>)
                                    : (rs.ckpt != nullptr ? k_render_fwd<false, true> : k_render_fwd<false, false>);
+    g_blend_kernel[0] = rs.col2 != nullptr ? (rs.ckpt != nullptr ? "k_render_fwd<true, true>" : "k_render_fwd<true, false>")
+                                           : (rs.ckpt != nullptr ? "k_render_fwd<false, true>" : "k_render_fwd<false, false>");
     hipLaunchKernelGGL(kern, dim3(block_grid(rs, 16)), dim3(64), 0, stream, rs, (const uint2*)img.ranges,
                        sorted_gauss, (const GaussRec*)g.rec, out_color, out_depth, out_alpha, img.final_T,
                        img.n_contrib, img.quad_maxc);
@@ -1061,7 +886,7 @@ __device__ __forceinline__ void bwd_tile(BwdLDS<TWO, HITS>& s, const RenderSet& 
       dpix_a = da + dpix_a;
     }
   }
-  const float bg_dot = bg[0] * dpix[0] + bg[1] * dpix[1] + bg[2] * dpix[2];
+  const float bg_dot = bg_dot3(bg, dpix[0], dpix[1], dpix[2]);
   // two colours: the second call's dL/dpixel (same background, no depth / alpha outputs)
   float dpix2[3] = {0.f, 0.f, 0.f};
   if (TWO && inside) {
@@ -1070,7 +895,7 @@ __device__ __forceinline__ void bwd_tile(BwdLDS<TWO, HITS>& s, const RenderSet& 
     dpix2[1] = d2[HW + pid];
     dpix2[2] = d2[2 * HW + pid];
   }
-  const float nbg2 = TWO ? -T_final * (bg[0] * dpix2[0] + bg[1] * dpix2[1] + bg[2] * dpix2[2]) : 0.f;
+  const float nbg2 = TWO ? -T_final * bg_dot3(bg, dpix2[0], dpix2[1], dpix2[2]) : 0.f;
   float S2 = 0.f;
 
   // The reference keeps per channel the colour accumulated behind the current Gaussian
@@ -1756,7 +1581,7 @@ __global__ __launch_bounds__(64) void k_render_bwd_tw(
       }
     }
     dp0[q] = d[0], dp1[q] = d[1], dp2[q] = d[2], dpd[q] = dd, dpa[q] = da;
-    nbg[q] = -T_final * (bg[0] * d[0] + bg[1] * d[1] + bg[2] * d[2]);
+    nbg[q] = -T_final * bg_dot3(bg, d[0], d[1], d[2]);
     e0[q] = e1[q] = e2[q] = 0.f;
     if (TWO && inside) {
       const float* d2 = rs.dpix2 + (size_t)v * 3 * HW;
@@ -1764,7 +1589,7 @@ __global__ __launch_bounds__(64) void k_render_bwd_tw(
       e1[q] = d2[HW + pid];
       e2[q] = d2[2 * HW + pid];
     }
-    nbg2[q] = TWO ? -T_final * (bg[0] * e0[q] + bg[1] * e1[q] + bg[2] * e2[q]) : 0.f;
+    nbg2[q] = TWO ? -T_final * bg_dot3(bg, e0[q], e1[q], e2[q]) : 0.f;
     S[q] = Sd[q] = S2[q] = 0.f;
   }
   const float ddelx_dx = 0.5f * W, ddely_dy = 0.5f * H;
@@ -1998,6 +1823,310 @@ __global__ __launch_bounds__(64) void k_render_bwd_tw(
   GSR_TL_END(1, hi)
 }
 
+// Backward, one 64-thread wave per 16x16 tile with the matrix-core sums (the one-colour default, C3): the
+// quadrants walked in turn as in k_render_bwd_tw, each quadrant's kept candidates replayed in groups of 8 and
+// summed over the quadrant's 64 pixels by the same 16 v_mfma_f32_16x16x4_f32 products as k_render_bwd (same A
+// and B operands, same accumulator split), so every per-(candidate, quadrant) sum is bitwise the same; the
+// sums are turned into moments and added over the quadrants in the other kernel's order.  The workgroup
+// kernel spends its time in the quadrant lockstep (1.47 slots per kept pair at C3) and three barriers per
+// batch; here a batch costs its kept pairs.
+template <bool UNUSED>
+__global__ __launch_bounds__(64) void k_render_bwd_twm(
+    RenderSet rs, const uint2* __restrict__ ranges, const uint32_t* __restrict__ quad_maxc,
+    const uint32_t* __restrict__ sorted_gauss, const GaussRec* __restrict__ rec, const uint32_t* __restrict__ goff,
+    const float* __restrict__ final_Ts, const uint32_t* __restrict__ n_contrib, const float* __restrict__ dL_dcolor,
+    const float* __restrict__ dL_ddepth, const float* __restrict__ dL_dalpha, float4* __restrict__ grow,
+    unsigned long long* __restrict__ reach) {
+  constexpr int NM = NGV;
+  constexpr int GST = 11;  // floats per candidate of gsum (10 sums + pad)
+  __shared__ float4 s0[65], s1[65], s2[65];
+  __shared__ uint32_t slot[64];
+  __shared__ uint32_t klist[64];          // the current quadrant's kept candidates in order
+  __shared__ float uw[64 * 16];           // one group's A operand (k_render_bwd's swizzled layout)
+  __shared__ float dpl[4][4 * 68 + 16];   // per quadrant dL/d(r, g, b, depth) per pixel (+16 zeros): B's D part
+  __shared__ float gsum[64 * GST];        // the current quadrant's sums per candidate
+  int v, tile, q_unused;
+  if (!block_map<4>(blockIdx.x, rs, v, tile, q_unused)) return;
+  GSR_TL_BEGIN
+  const int W = rs.W, H = rs.H, grid_x = rs.gx;
+  const size_t vgs = (size_t)(rs.v0 + v);
+  const size_t HW = (size_t)H * W;
+  {
+    const size_t tiles = (size_t)rs.gx * rs.gy;
+    ranges += vgs * tiles;
+    quad_maxc += vgs * 4 * tiles;
+    sorted_gauss += rs.inst_start[v];
+    rec += vgs * rs.P;
+    goff += vgs * rs.P;
+    final_Ts += vgs * HW;
+    n_contrib += vgs * HW;
+    dL_dcolor += (size_t)v * 3 * HW;
+    if (dL_ddepth) dL_ddepth += (size_t)v * HW;
+    if (dL_dalpha) dL_dalpha += (size_t)v * HW;
+    grow += (size_t)3 * rs.row_start[v];
+  }
+  const float* bg = rs.bg[v];
+  const int lane = threadIdx.x;
+  const int txi = tile % grid_x, tyi = tile / grid_x;
+  const uint2 range = ranges[tile];
+  const uint4 qm = reinterpret_cast<const uint4*>(quad_maxc)[tile];
+  const int qmaxc[4] = {(int)qm.x, (int)qm.y, (int)qm.z, (int)qm.w};
+  const int hi = __builtin_amdgcn_readfirstlane((int)max(max(qm.x, qm.y), max(qm.z, qm.w)));
+  const int lo = 0;
+
+  float T[4], S[4], Sd[4], dp0[4], dp1[4], dp2[4], dpd[4], dpa[4], nbg[4];
+  uint32_t last[4];
+  const float lxf = (float)(txi * GSR_TILE_X + (lane & 7)), lyf = (float)(tyi * GSR_TILE_Y + (lane >> 3));
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const int px = txi * GSR_TILE_X + (q & 1) * 8 + (lane & 7), py = tyi * GSR_TILE_Y + (q >> 1) * 8 + (lane >> 3);
+    const bool inside = px < W && py < H;
+    const size_t pid = (size_t)py * W + px;
+    const float T_final = inside ? final_Ts[pid] : 0.0f;
+    T[q] = T_final;
+    last[q] = inside ? n_contrib[pid] : 0u;
+    float d[3] = {0.f, 0.f, 0.f};
+    float dd = 0.f, da = 0.f;
+    if (inside) {
+      d[0] = dL_dcolor[pid];
+      d[1] = dL_dcolor[HW + pid];
+      d[2] = dL_dcolor[2 * HW + pid];
+      if (dL_ddepth) dd = dL_ddepth[pid];
+      if (dL_dalpha) da = dL_dalpha[pid];
+      if (rs.cbg != nullptr) {
+#pragma clang fp contract(off)
+        const float am = 1.0f - (1.0f - T_final);
+        const float* bgi = rs.cbg + ((size_t)v * HW + pid) * 3;
+        const float* col = rs.ccolor + (size_t)v * 3 * HW + pid;
+        float dsum = 0.0f;
+#pragma unroll
+        for (int ch = 0; ch < 3; ++ch) {
+          const float b = bgi[ch];
+          const float pre = col[(size_t)ch * HW] + am * b;
+          const float gch = (pre >= 0.0f && pre <= 1.0f) ? d[ch] : 0.0f;
+          d[ch] = gch;
+          dsum -= gch * b;
+          if (rs.dcbg != nullptr) rs.dcbg[((size_t)v * HW + pid) * 3 + ch] = gch * am;
+        }
+        da = dsum + da;
+      }
+    }
+    dp0[q] = d[0], dp1[q] = d[1], dp2[q] = d[2], dpd[q] = dd, dpa[q] = da;
+    nbg[q] = -T_final * bg_dot3(bg, d[0], d[1], d[2]);
+    S[q] = Sd[q] = 0.f;
+    float* sdp = dpl[q];
+    sdp[0 * 68 + lane] = d[0];
+    sdp[1 * 68 + lane] = d[1];
+    sdp[2 * 68 + lane] = d[2];
+    sdp[3 * 68 + lane] = dd;
+    if (lane < 16) sdp[4 * 68 + lane] = 0.f;
+  }
+  const float ddelx_dx = 0.5f * W, ddely_dy = 0.5f * H;
+  const float4 zero4 = make_float4(0.f, 0.f, 0.f, 0.f);
+
+  // the matrix-core operand maps of k_render_bwd (one colour)
+  const int ncol = lane & 15;
+  const bool dcol = ncol >= 6 && ncol < 10;
+  float fa[2], fbb[2], fc;
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    const float y = (float)(2 * (lane >> 4) + h) - 3.5f;
+    fa[h] = ncol == 0 ? 1.f : ncol == 2 ? y : ncol == 5 ? y * y : 0.f;
+    fbb[h] = ncol == 1 ? 1.f : ncol == 4 ? y : 0.f;
+  }
+  fc = ncol == 3 ? 1.f : 0.f;
+  int wa[4];
+#pragma unroll
+  for (int sgrp = 0; sgrp < 4; ++sgrp) wa[sgrp] = 256 * (lane >> 4) + 4 * (((lane >> 2) & 3) ^ sgrp) + (lane & 3);
+  const float4* asrc = reinterpret_cast<const float4*>(uw + 16 * lane);
+  const int aswz = (lane >> 2) & 3;
+  const int mb = 4 * ((lane >> 4) & 1);
+  const bool useful = (lane < 32) ? (ncol < 6) : dcol;
+
+  const uint32_t gmask = rs.gmask;
+  unsigned int* const reach32 = reinterpret_cast<unsigned int*>(reach) + (v >> 5);
+  const unsigned int vbit = 1u << (v & 31);
+  float4 na = zero4, nb = zero4, nc = zero4, nd = zero4;
+  uint32_t ngo = 0u, gi_next = 0u;
+  auto load = [&](uint32_t g) {
+    const float4* r = reinterpret_cast<const float4*>(rec + g);
+    na = r[0];
+    nb = r[1];
+    nc = r[2];
+    nd = r[3];
+    if (rs.col2 != nullptr)  // the second rasterizer call's colours replace the first's
+      nc = make_float4(rs.col2[3 * g], rs.col2[3 * g + 1], rs.col2[3 * g + 2], 0.f);
+    ngo = goff[g];
+    atomicOr(reach32 + 2 * g, vbit);  // the Gaussian gets a row in this view (k_view_grad reads it)
+  };
+  if (hi > lo) {
+    if (hi - 1 - lane >= lo) load(sorted_gauss[range.x + hi - 1 - lane] & gmask);
+    if (hi - 65 - lane >= lo) gi_next = sorted_gauss[range.x + hi - 65 - lane] & gmask;
+  }
+  float acca[NM], accb[NM];
+
+  for (int h = hi; h > lo; h -= 64) {
+    const int rel_c = h - 1 - lane;
+    const bool staged = rel_c >= lo;
+    const float4 ca = make_float4(na.x, na.y, GSR_CONIC_K_AC * na.z, GSR_CONIC_K_B * na.w);
+    const float4 cb = make_float4(GSR_CONIC_K_AC * nb.x, nb.y, nb.z, __uint_as_float((uint32_t)rel_c));
+    uint32_t keep4 = 0u;
+    if (staged) {
+      s0[lane] = ca;
+      s1[lane] = cb;
+      s2[lane] = nc;
+      const uint32_t dx_ = __float_as_uint(nd.x), dy_ = __float_as_uint(nd.y);
+      const int xmin = dx_ & 0xffff, ymin = dx_ >> 16, xmax = dy_ & 0xffff;
+      slot[lane] = ngo + (uint32_t)((tyi - ymin) * (xmax - xmin) + (txi - xmin));
+      const float4 r0 = make_float4(ca.x, ca.y, ca.z * (1.0f / GSR_CONIC_K_AC), ca.w * (1.0f / GSR_CONIC_K_B));
+      const float4 r1 = make_float4(cb.x * (1.0f / GSR_CONIC_K_AC), cb.y, cb.z, cb.w);
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+        if (rel_c < qmaxc[q] &&
+            quadrant_hit(r0, r1, (float)(txi * GSR_TILE_X + (q & 1) * 8), (float)(tyi * GSR_TILE_Y + (q >> 1) * 8)))
+          keep4 |= 1u << q;
+    }
+    if (h - 64 > lo) {
+      if (h - 65 - lane >= lo) load(gi_next);
+      if (h - 129 - lane >= lo) gi_next = sorted_gauss[range.x + h - 129 - lane] & gmask;
+    }
+#pragma unroll
+    for (int i = 0; i < NM; ++i) acca[i] = accb[i] = 0.f;
+    __syncthreads();
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const bool kept = (keep4 >> q) & 1u;
+      const unsigned long long kq = __ballot(kept);
+      if (kq == 0ull) continue;
+      const int cnt = __popcll(kq);
+      if (kept) klist[mask_rank(kq)] = (uint32_t)lane;
+      // this quadrant's B operand: bv[i] = D + F for k-step i (k_render_bwd)
+      float bv[16];
+      {
+        const float4* dsrc =
+            reinterpret_cast<const float4*>(dpl[q] + (dcol ? (ncol - 6) * 68 + 16 * (lane >> 4) : 4 * 68));
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          const float4 d4 = dsrc[k];
+          const float dk[4] = {d4.x, d4.y, d4.z, d4.w};
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const int i = 4 * k + e;
+            const float x = (float)(i & 7) - 3.5f;
+            bv[i] = dk[e] + (fa[i >> 3] + x * (fbb[i >> 3] + x * fc));
+          }
+        }
+      }
+      const float pxf = lxf + (float)((q & 1) * 8), pyf = lyf + (float)((q >> 1) * 8);
+      unsigned long long rest = kq;
+      __syncthreads();  // (klist)
+      for (int g0 = 0; g0 < cnt; g0 += 8) {
+        const int gn = min(8, cnt - g0);
+        int j = (int)__builtin_ctzll(rest);
+        float4 ga = s0[j], gb = s1[j], gc = s2[j];
+#pragma unroll
+        for (int c = 0; c < 8; ++c) {
+          if (c < gn) {
+            rest &= rest - 1ull;
+            const int jn = (c + 1 < gn) ? (int)__builtin_ctzll(rest) : j;
+            const float4 xa = s0[jn], xb = s1[jn], xc = s2[jn];
+            const uint32_t rel = __float_as_uint(gb.w);
+            const float dx = ga.x - pxf, dy = ga.y - pyf;
+            const float power2 = gauss_power2(ga.z, ga.w, gb.x, dx, dy);
+            const float G = __builtin_amdgcn_exp2f(power2);
+            const float alpha = fminf(GSR_ALPHA_MAX, gb.y * G);
+            const bool hit = rel < last[q] && power2 <= 0.0f && alpha >= GSR_ALPHA_MIN;
+            const float a_eff = hit ? alpha : 0.0f;
+            const float g_eff = hit ? G : 0.0f;
+            const float oma = 1.f - a_eff;
+            const float inv_1ma = fast_rcp(oma);
+            T[q] = T[q] * inv_1ma;
+            const float cd = fmaf(gc.x, dp0[q], fmaf(gc.y, dp1[q], fmaf(gc.z, dp2[q], dpa[q])));
+            const float dL_da = fmaf(T[q], fmaf(gb.z - Sd[q], dpd[q], cd - S[q]), inv_1ma * nbg[q]);
+            const float u = g_eff * dL_da;
+            const float w = a_eff * T[q];
+            S[q] = fmaf(a_eff, cd, oma * S[q]);
+            Sd[q] = fmaf(a_eff, gb.z, oma * Sd[q]);
+            uw[16 * c + wa[c >> 2]] = u;
+            uw[16 * (c + 8) + wa[2 + (c >> 2)]] = w;
+            ga = xa;
+            gb = xb;
+            gc = xc;
+            j = jn;
+          }
+        }
+        __syncthreads();  // (the wave reads its own lanes' rows)
+        float av[16];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          const float4 a4 = asrc[k ^ aswz];
+          av[4 * k] = a4.x, av[4 * k + 1] = a4.y, av[4 * k + 2] = a4.z, av[4 * k + 3] = a4.w;
+        }
+        const uint4 jl = *reinterpret_cast<const uint4*>(klist + g0 + mb);
+        typedef float f4 __attribute__((ext_vector_type(4)));
+        f4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+          if (i & 1)
+            acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(av[i], bv[i], acc1, 0, 0, 0);
+          else
+            acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(av[i], bv[i], acc0, 0, 0, 0);
+        }
+        if (useful) {
+          const uint32_t jr[4] = {jl.x, jl.y, jl.z, jl.w};
+#pragma unroll
+          for (int r = 0; r < 4; ++r)
+            if (mb + r < gn) gsum[jr[r] * (uint32_t)GST + (uint32_t)ncol] = acc0[r] + acc1[r];
+        }
+        __syncthreads();  // (uw is rewritten by the next group; gsum read below)
+      }
+      if (kept) {
+        // this pair's sums -> moments about the candidate's mean (k_render_bwd's flush), quadrant order
+        const float* C = gsum + lane * GST;
+        const float4 ga = s0[lane];
+        const float mx = ga.x - ((float)(txi * GSR_TILE_X + (q & 1) * 8) + 3.5f);
+        const float my = ga.y - ((float)(tyi * GSR_TILE_Y + (q >> 1) * 8) + 3.5f);
+        float m[NM];
+        m[0] = C[0];
+        m[1] = mx * C[0] - C[1];
+        m[2] = my * C[0] - C[2];
+        m[3] = mx * (mx * C[0] - 2.f * C[1]) + C[3];
+        m[4] = mx * (my * C[0] - C[2]) - my * C[1] + C[4];
+        m[5] = my * (my * C[0] - 2.f * C[2]) + C[5];
+        m[6] = C[6];
+        m[7] = C[7];
+        m[8] = C[8];
+        m[9] = C[9];
+#pragma unroll
+        for (int i = 0; i < NM; ++i) {
+          if (q == 0) acca[i] = m[i];
+          else if (q == 1) acca[i] = acca[i] + m[i];
+          else if (q == 2) accb[i] = m[i];
+          else accb[i] = accb[i] + m[i];
+        }
+      }
+      __syncthreads();  // (klist, gsum are rewritten by the next quadrant)
+    }
+    if (staged) {
+      float m[NM];
+#pragma unroll
+      for (int i = 0; i < NM; ++i) m[i] = acca[i] + accb[i];
+      const float4 ga = s0[lane];
+      const float4 gb = s1[lane];
+      const float o = gb.y;
+      float4* row = grow + 3 * (size_t)slot[lane];
+      const float k = o * (1.0f / 1.4426950408889634f);
+      const float dmx = k * ddelx_dx * (2.0f * ga.z * m[1] + ga.w * m[2]);
+      const float dmy = k * ddely_dy * (2.0f * gb.x * m[2] + ga.w * m[1]);
+      row[0] = make_float4(dmx, dmy, -0.5f * o * m[3], -0.5f * o * m[4]);
+      row[1] = make_float4(-0.5f * o * m[5], m[0], m[6], m[7]);
+      row[2] = make_float4(m[8], m[9], 0.f, 0.f);
+    }
+    __syncthreads();
+  }
+  GSR_TL_END(1, hi)
+}
+
 // Sums of the backward blend: hit lists (HITS) or matrix-core products.  Hit lists win where the
 // Gaussians are small (the two-colour SuGaR backward, C5); the matrix cores where they are large (C3).
 // GSR_BWD_SUMS=hits / mfma forces one (A/B).
@@ -2028,14 +2157,25 @@ void launch_render_backward(const RenderSet& rs, const GeomState& g, const uint3
   const bool hits = bwd_hit_lists(rs.dpix2 != nullptr);
   if (hits && extra == 0 && bwd_tile_wave()) {
     auto kt = rs.dpix2 != nullptr ? k_render_bwd_tw<true> : k_render_bwd_tw<false>;
+    g_blend_kernel[1] = rs.dpix2 != nullptr ? "k_render_bwd_tw<true>" : "k_render_bwd_tw<false>";
     hipLaunchKernelGGL(kt, dim3(block_grid(rs, 4)), dim3(64), 0, stream, rs, (const uint2*)img.ranges,
                        (const uint32_t*)img.quad_maxc, sorted_gauss, (const GaussRec*)g.rec, (const uint32_t*)g.goff,
                        (const float*)img.final_T, (const uint32_t*)img.n_contrib, dL_dcolor, dL_ddepth, dL_dalpha,
                        bw.grow, bw.reach);
     return;
   }
+  if (!hits && rs.dpix2 == nullptr && extra == 0 && bwd_tile_wave()) {
+    g_blend_kernel[1] = "k_render_bwd_twm<false>";
+    hipLaunchKernelGGL(k_render_bwd_twm<false>, dim3(block_grid(rs, 4)), dim3(64), 0, stream, rs,
+                       (const uint2*)img.ranges, (const uint32_t*)img.quad_maxc, sorted_gauss, (const GaussRec*)g.rec,
+                       (const uint32_t*)g.goff, (const float*)img.final_T, (const uint32_t*)img.n_contrib, dL_dcolor,
+                       dL_ddepth, dL_dalpha, bw.grow, bw.reach);
+    return;
+  }
   auto kern = rs.dpix2 != nullptr ? (hits ? k_render_bwd<true, true> : k_render_bwd<true, false>)
                                   : (hits ? k_render_bwd<false, true> : k_render_bwd<false, false>);
+  g_blend_kernel[1] = rs.dpix2 != nullptr ? (hits ? "k_render_bwd<true, true>" : "k_render_bwd<true, false>")
+                                          : (hits ? "k_render_bwd<false, true>" : "k_render_bwd<false, false>");
   hipLaunchKernelGGL(kern, grid, dim3(256), 0, stream, rs, (const uint2*)img.ranges, (const uint32_t*)img.quad_maxc,
                      sorted_gauss, (const GaussRec*)g.rec, (const uint32_t*)g.goff, (const float*)img.final_T,
                      (const uint32_t*)img.n_contrib, dL_dcolor, dL_ddepth, dL_dalpha, bw.grow, bw.reach,

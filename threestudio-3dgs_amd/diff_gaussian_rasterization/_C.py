@@ -68,6 +68,7 @@ SIGNATURES = {
     "gsr_set_binning_bytes": (_sz, [_i, _i, ctypes.POINTER(_i), _i, _i]),
     "gsr_set_image_bytes": (_sz, [_i, _i, _i]),
     "gsr_set_image_bytes_ex": (_sz, [_i, _i, ctypes.POINTER(_i), _i, _i, _i]),
+    "gsr_profile_kernel": (ctypes.c_char_p, [_i]),
     "gsr_set_backward_bytes": (_sz, [_i, _i, ctypes.POINTER(_i)]),
     "gsr_set_preprocess": (
         _i,
@@ -367,3 +368,10 @@ def profile_read(reset: bool = True) -> dict:
     cnt = (ctypes.c_longlong * n)()
     _check(load_library().gsr_profile_read(ms, cnt, 1 if reset else 0))
     return {PHASES[i]: (float(ms[i]), int(cnt[i])) for i in range(n)}
+
+
+def profile_kernels() -> dict:
+    """The blend kernels the last forward / backward blend launches used (include/gsr.h gsr_profile_kernel), as
+    rocprofv3 names them: {"render_fwd": ..., "render_bwd": ...}."""
+    lib = load_library()
+    return {PHASES[i]: lib.gsr_profile_kernel(i).decode() for i in (3, 4)}
