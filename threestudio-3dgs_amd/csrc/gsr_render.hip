@@ -2030,7 +2030,9 @@ __global__ __launch_bounds__(64) void k_render_bwd_tw(
 // kernel spends its time in the quadrant lockstep (1.47 slots per kept pair at C3) and three barriers per
 // batch; here a batch costs its kept pairs.
 template <bool UNUSED>
-__global__ __launch_bounds__(64) void k_render_bwd_twm(
+// 3 waves per SIMD: 168 VGPRs, no spills (the compiler's own choice counts the matrix-core accumulators as AGPRs
+// and stops at 2)
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3, 8))) void k_render_bwd_twm(
     RenderSet rs, const uint2* __restrict__ ranges, const uint32_t* __restrict__ quad_maxc,
     const uint32_t* __restrict__ sorted_gauss, const GaussRec* __restrict__ rec, const uint32_t* __restrict__ goff,
     const float* __restrict__ final_Ts, const uint32_t* __restrict__ n_contrib, const float* __restrict__ dL_dcolor,
