@@ -75,8 +75,8 @@ def parse():
                     help="PMC summary (profiles/summarize.py) supplying roofline.traffic and the VALU counts")
     ap.add_argument("--pairs", default=os.path.join(ROOT, "profiles", "r03_pairs.json"),
                     help="device-counted blend pairs (profiles/diag_pairs.py) for the VALU roofline")
-    ap.add_argument("--traffic-sugar", default=os.path.join(ROOT, "profiles", "r03d_sugar_traffic.json"),
-                    help="PMC summary of the C5 line (--workload sugar, profiles/summarize.py r03d_sugar)")
+    ap.add_argument("--traffic-sugar", default=os.path.join(ROOT, "profiles", "r04c_sugar_traffic.json"),
+                    help="PMC summary of the C5 line (--workload sugar, profiles/summarize.py r04c_sugar)")
     ap.add_argument("--overlap-reduce", choices=["on", "off"], default="on",
                     help="N > 1: sum the Gaussian gradients over ranks inside the backward, range by range as the "
                          "per-Gaussian backward forms them (view_shard.ChunkedGradReduce, overlapped on a side "
@@ -267,10 +267,10 @@ def render_views_sugar(rep: Replica, settings, shade):
 
 PROFILE_VIEWS_PER_LAUNCH = 64  # profiles/run_profiles.sh: bench.py defaults, one 64-view set per launch
 # the blend kernels of the default workloads (forward, backward), as rocprofv3 demangles them: C3's 64-view
-# launch takes the tile-wave forward and the one-wave-per-tile matrix-core backward; C5 the two-colour
+# launch takes the tile-wave forward and the lockstep matrix-core backward; C5 the two-colour
 # quadrant-wave forward and the one-wave-per-tile hit-list backward (gsr_render.hip).  A run uses the names the
 # library reports it launched (gsr_profile_kernel); the committed counters must name these (test_bench_fields)
-KERNELS = {"c3": ("k_render_fwd_tile<false>", "k_render_bwd_twm<false>"),
+KERNELS = {"c3": ("k_render_fwd_tile<false>", "k_render_bwd<false, false>"),
            "sugar": ("k_render_fwd<true, false>", "k_render_bwd_tw<true>")}
 
 

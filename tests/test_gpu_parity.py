@@ -262,8 +262,8 @@ def test_batched_views_match_per_view(nviews, monkeypatch):
 @pytest.mark.parametrize("switch", ["fwd_kernel", "dispatch_order", "bwd_kernel"])
 @pytest.mark.parametrize("kind", ["ball_composite", "sugar_two_colors"])
 def test_forward_kernels_bitwise(kind, switch, monkeypatch):
-    """fwd_kernel: the one-wave-per-tile forwards (candidate-major and quadrant-major) and the quadrant-wave
-    forward (GSR_FWD_KERNEL) blend exactly the same candidates per pixel in the same order; dispatch_order: the blends' work-ordered
+    """fwd_kernel: the one-wave-per-tile forward and the quadrant-wave forward (GSR_FWD_KERNEL) blend exactly
+    the same candidates per pixel in the same order; dispatch_order: the blends' work-ordered
     dispatch and raster order (GSR_TILE_ORDER=raster) only change which workgroup starts first; bwd_kernel: the
     backward blend as one wave per tile or as four lockstep quadrant waves (GSR_BWD_KERNEL).  Every
     output — colour, depth, alpha, the composite, the second colour set, radii — and every gradient (the
@@ -322,6 +322,3 @@ def test_forward_kernels_bitwise(kind, switch, monkeypatch):
     tile, quad = run("tile"), run("quadrant")
     for i, (x, y) in enumerate(zip(tile, quad)):
         assert torch.equal(x, y), f"output {i} differs: {float((x.double() - y.double()).abs().max())}"
-    if switch == "fwd_kernel":  # the tile wave walking the quadrants in turn (k_render_fwd_tq)
-        for i, (x, y) in enumerate(zip(run("tq"), quad)):
-            assert torch.equal(x, y), f"tq: output {i} differs: {float((x.double() - y.double()).abs().max())}"

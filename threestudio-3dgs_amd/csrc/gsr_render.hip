@@ -644,193 +644,6 @@ __global__ __launch_bounds__(64) void k_render_fwd_tile(RenderSet rs, const uint
 #endif
 }
 
-// Forward, one 64-thread wave per 16x16 tile walking the quadrants in turn (4 pixels per lane, the same pixel of
-// each 8x8 quadrant): per batch each lane gathers one candidate's record once (the quadrant-wave kernel gathers it
-// in each of four waves) and tests it against the quadrants still blending; then per quadrant the wave walks that
-// quadrant's kept candidates by scalar bit scans of their ballot mask and blends its pixel — per pixel exactly the
-// quadrant-wave kernel's candidates, order and operations (bitwise identical outputs).  Unlike k_render_fwd_tile
-// (candidate-major: every staged candidate visited with four quadrant branches) a batch costs its kept
-// (candidate, quadrant) pairs; the wave stops when all four quadrants are done.
-template <bool C2>
-__global__ __launch_bounds__(64) void k_render_fwd_tq(RenderSet rs, const uint2* __restrict__ ranges,
-                                                      const uint32_t* __restrict__ sorted_gauss,
-                                                      const GaussRec* __restrict__ rec, float* __restrict__ out_color,
-                                                      float* __restrict__ out_depth, float* __restrict__ out_alpha,
-                                                      float* __restrict__ final_T, uint32_t* __restrict__ n_contrib,
-                                                      uint32_t* __restrict__ quad_maxc) {
-  __shared__ float4 s0[65], s1[65], s2[65];
-  __shared__ float4 s3[C2 ? 65 : 1];
-  int v, tile, q_unused;
-  if (!block_map<4>(blockIdx.x, rs, v, tile, q_unused)) return;
-  GSR_TL_BEGIN
-  const int W = rs.W, H = rs.H, grid_x = rs.gx;
-  const size_t HWs = (size_t)W * H;
-  {
-    const size_t vg = (size_t)(rs.v0 + v), tiles = (size_t)rs.gx * rs.gy;
-    ranges += vg * tiles;
-    quad_maxc += vg * 4 * tiles;
-    sorted_gauss += rs.inst_start[v];
-    rec += vg * rs.P;
-    out_color += vg * 3 * HWs;
-    out_depth += vg * HWs;
-    out_alpha += vg * HWs;
-    final_T += vg * HWs;
-    n_contrib += vg * HWs;
-  }
-  const float* bg = rs.bg[v];
-  const int lane = threadIdx.x;
-  const int tx0 = (tile % grid_x) * GSR_TILE_X, ty0 = (tile / grid_x) * GSR_TILE_Y;
-  float T[4], Cr[4], Cg[4], Cb[4], D[4], Er[4], Eg[4], Eb[4];
-  uint32_t last[4];
-  bool done[4], inside[4];
-  uint32_t qactive = 0u;  // quadrants with a pixel still blending (uniform)
-#pragma unroll
-  for (int q = 0; q < 4; ++q) {
-    const int px = tx0 + (q & 1) * 8 + (lane & 7), py = ty0 + (q >> 1) * 8 + (lane >> 3);
-    inside[q] = px < W && py < H;
-    done[q] = !inside[q];
-    T[q] = 1.0f;
-    Cr[q] = Cg[q] = Cb[q] = D[q] = 0.f;
-    Er[q] = Eg[q] = Eb[q] = 0.f;
-    last[q] = 0u;
-    qactive |= __all(done[q]) ? 0u : (1u << q);
-  }
-  const float lxf = (float)(tx0 + (lane & 7)), lyf = (float)(ty0 + (lane >> 3));
-  const uint2 range = ranges[tile];
-  const int n = (int)(range.y - range.x);
-  const uint32_t gmask = rs.gmask;
-  const float4 zero4 = make_float4(0.f, 0.f, 0.f, 0.f);
-  const float* col2 = rs.col2;
-  float4 n0 = zero4, n1 = zero4, n2 = zero4, n3 = zero4;
-  uint32_t gi_next = 0u;
-  if (lane < n) {
-    const uint32_t g0 = sorted_gauss[range.x + lane] & gmask;
-    n0 = rec[g0].a;
-    n1 = rec[g0].b;
-    n2 = rec[g0].c;
-    if (C2) n3 = make_float4(col2[3 * g0], col2[3 * g0 + 1], col2[3 * g0 + 2], 0.f);
-  }
-  if (64 + lane < n) gi_next = sorted_gauss[range.x + 64 + lane] & gmask;
-#ifdef GSR_TIMELINE
-  unsigned long long pc_eval = 0, pc_slot = 0;
-#endif
-  for (int base = 0; base < n && qactive != 0u; base += 64) {
-    const int i = base + lane;
-    const float4 r0 = n0, r1 = n1, r2 = n2, r3 = n3;
-    if (base + 64 + lane < n) {
-      n0 = rec[gi_next].a;
-      n1 = rec[gi_next].b;
-      n2 = rec[gi_next].c;
-      if (C2) n3 = make_float4(col2[3 * gi_next], col2[3 * gi_next + 1], col2[3 * gi_next + 2], 0.f);
-    }
-    if (base + 128 + lane < n) gi_next = sorted_gauss[range.x + base + 128 + lane] & gmask;
-    uint32_t m = 0u;
-    if (i < n) {
-#pragma unroll
-      for (int q = 0; q < 4; ++q)
-        if ((qactive >> q) & 1u)
-          m |= quadrant_hit(r0, r1, (float)(tx0 + (q & 1) * 8), (float)(ty0 + (q >> 1) * 8)) ? (1u << q) : 0u;
-    }
-    // the conic pre-multiplied for gauss_power2 (.w of s1: 1 + list position)
-    s0[lane] = make_float4(r0.x, r0.y, GSR_CONIC_K_AC * r0.z, GSR_CONIC_K_B * r0.w);
-    s1[lane] = make_float4(GSR_CONIC_K_AC * r1.x, r1.y, r1.z, __uint_as_float((uint32_t)(i + 1)));
-    s2[lane] = r2;
-    if (C2) s3[lane] = r3;
-    __syncthreads();  // (one wave: the staging writes before the other lanes' reads)
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      if (!((qactive >> q) & 1u)) continue;
-      unsigned long long kq = __ballot((m >> q) & 1u);
-      if (kq == 0ull) continue;
-      const float pxf = lxf + (float)((q & 1) * 8), pyf = lyf + (float)((q >> 1) * 8);
-      int k = (int)__builtin_ctzll(kq);
-      float4 a = s0[k], b = s1[k], c = s2[k], e = C2 ? s3[k] : zero4;
-      for (int j = 1;; ++j) {
-        kq &= kq - 1ull;
-        const int kn = kq != 0ull ? (int)__builtin_ctzll(kq) : 64;
-        const float4 an = s0[kn], bn = s1[kn], cn = s2[kn];
-        const float4 en = C2 ? s3[kn] : zero4;
-        const float dx = a.x - pxf, dy = a.y - pyf;
-        const float power2 = gauss_power2(a.z, a.w, b.x, dx, dy);  // log2(e) * power
-        const float alpha = fminf(GSR_ALPHA_MAX, b.y * __builtin_amdgcn_exp2f(power2));
-#ifdef GSR_TIMELINE
-        pc_eval += done[q] ? 0ull : 1ull;
-        pc_slot += 1ull;
-#endif
-        const bool ok = !done[q] && power2 <= 0.0f && alpha >= GSR_ALPHA_MIN;
-        const float test_T = T[q] * (1.0f - alpha);
-        const bool term = ok && test_T < GSR_T_EPS;
-        const bool blend = ok && !term;
-        const float a_eff = blend ? alpha : 0.0f;
-        const float aT = a_eff * T[q];
-        Cr[q] = fmaf(c.x, aT, Cr[q]);
-        Cg[q] = fmaf(c.y, aT, Cg[q]);
-        Cb[q] = fmaf(c.z, aT, Cb[q]);
-        D[q] = fmaf(b.z, aT, D[q]);
-        if (C2) {
-          Er[q] = fmaf(e.x, aT, Er[q]);
-          Eg[q] = fmaf(e.y, aT, Eg[q]);
-          Eb[q] = fmaf(e.z, aT, Eb[q]);
-        }
-        T[q] = blend ? test_T : T[q];
-        last[q] = blend ? __float_as_uint(b.w) : last[q];
-        done[q] = done[q] || term;
-        if (kq == 0ull) break;
-        if ((j & 7) == 0 && __all(done[q])) break;
-        a = an;
-        b = bn;
-        c = cn;
-        e = en;
-      }
-      if (__all(done[q])) qactive &= ~(1u << q);
-    }
-    __syncthreads();  // (the staged batch is rewritten next)
-  }
-#pragma unroll
-  for (int q = 0; q < 4; ++q) {
-    const int px = tx0 + (q & 1) * 8 + (lane & 7), py = ty0 + (q >> 1) * 8 + (lane >> 3);
-    if (inside[q]) {
-      const size_t pid = (size_t)py * W + px;
-      const float Tq = T[q];
-      final_T[pid] = Tq;
-      n_contrib[pid] = last[q];
-      {
-#pragma clang fp contract(off)
-        out_color[pid] = Cr[q] + Tq * bg[0];
-        out_color[HWs + pid] = Cg[q] + Tq * bg[1];
-        out_color[2 * HWs + pid] = Cb[q] + Tq * bg[2];
-      }
-      out_depth[pid] = D[q];
-      out_alpha[pid] = 1.0f - Tq;
-      if (C2) {
-#pragma clang fp contract(off)
-        float* o2 = rs.out_col2 + (size_t)(rs.v0 + v) * 3 * HWs + pid;
-        o2[0] = Er[q] + Tq * bg[0];
-        o2[HWs] = Eg[q] + Tq * bg[1];
-        o2[2 * HWs] = Eb[q] + Tq * bg[2];
-      }
-      if (rs.cbg != nullptr) {
-#pragma clang fp contract(off)
-        const float am = 1.0f - (1.0f - Tq);
-        const float* bgi = rs.cbg + ((size_t)v * HWs + pid) * 3;
-        float* cp = rs.comp + (size_t)v * 3 * HWs + pid;
-        cp[0] = fminf(fmaxf((Cr[q] + Tq * bg[0]) + am * bgi[0], 0.0f), 1.0f);
-        cp[HWs] = fminf(fmaxf((Cg[q] + Tq * bg[1]) + am * bgi[1], 0.0f), 1.0f);
-        cp[2 * HWs] = fminf(fmaxf((Cb[q] + Tq * bg[2]) + am * bgi[2], 0.0f), 1.0f);
-      }
-    }
-    uint32_t mc = last[q];
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) mc = max(mc, (uint32_t)__shfl_xor((int)mc, o, 64));
-    if (lane == 0) quad_maxc[4 * tile + q] = mc;
-  }
-#ifdef GSR_TIMELINE
-  atomicAdd(&g_pairs[0], pc_eval);
-  atomicAdd(&g_pairs[1], pc_slot);
-#endif
-  GSR_TL_END(0, 0)
-}
-
 // One block per view: bucket its super-tiles by the bit length of their listed instances (sum over the
 // 2x2 tiles), heaviest bucket first (LDS counts, exclusive scan, LDS-atomic placement: the order inside a
 // bucket may vary between runs — it only changes which workgroup starts first, never a result).
@@ -936,18 +749,14 @@ __global__ __launch_bounds__(256) void k_ckpt_suffix(RenderSet rs, const uint32_
 static bool fwd_tile_kernel(long long instances, long long gaussians, int views) {
   const char* e = getenv("GSR_FWD_KERNEL");
   if (e != nullptr && strcmp(e, "quadrant") == 0) return false;
-  if (e != nullptr && (strcmp(e, "tile") == 0 || strcmp(e, "tq") == 0)) return true;
+  if (e != nullptr && strcmp(e, "tile") == 0) return true;
   return views >= 48 && gaussians > 0 && instances >= 3 * gaussians;
 }
-// tile waves walking the quadrants in turn (k_render_fwd_tq) instead of candidate-major (k_render_fwd_tile)
-static bool fwd_tq_kernel() {
-  const char* e = getenv("GSR_FWD_KERNEL");
-  return e != nullptr && strcmp(e, "tq") == 0;
-}
-// (Measured and removed, round 4: the quadrant waves of a tile sharing one staged copy of each batch in LDS —
-// one record gather per candidate and tile instead of per quadrant wave — with a workgroup barrier per batch:
-// C5 render_fwd 0.146 -> 0.277 ms/view, 8-view C3 sets 0.052 -> 0.070; the quadrant waves' independence is
-// worth more than the 5.6x redundant record traffic; profiles/r04/fwd_shared_ab.txt.)
+// (Measured and removed, round 4 — the forward's free-running quadrant waves beat every variant that gathers a
+// record once per tile, their 5.6x redundant C5 record traffic included, profiles/r04/fwd_shared_ab.txt,
+// profiles/r04/tile_wave_ab.txt: the quadrant waves of a tile sharing one staged copy of each batch in LDS with a
+// barrier per batch, C5 render_fwd 0.146 -> 0.277 ms/view, 8-view C3 sets 0.052 -> 0.070; one wave per tile
+// walking the quadrants in turn, C5 0.142 -> 0.237, C3 0.045 -> 0.066.)
 
 // the blend kernels a launch used (gsr_profile_kernel; rocprofv3's names of them)
 static const char* g_blend_kernel[2] = {"", ""};
@@ -960,12 +769,6 @@ void launch_render_forward(const RenderSet& rs, const GeomState& g, const uint32
   if (nt <= 0 || rs.V <= 0) return;
   if (fwd_tile_kernel(instances, (long long)rs.V * rs.P, rs.V)) {
     const dim3 grid(block_grid(rs, 4));
-    if (fwd_tq_kernel()) {
-      g_blend_kernel[0] = rs.col2 != nullptr ? "k_render_fwd_tq<true>" : "k_render_fwd_tq<false>";
-      hipLaunchKernelGGL(rs.col2 != nullptr ? k_render_fwd_tq<true> : k_render_fwd_tq<false>, grid, dim3(64), 0,
-                         stream, rs, (const uint2*)img.ranges, sorted_gauss, (const GaussRec*)g.rec, out_color,
-                         out_depth, out_alpha, img.final_T, img.n_contrib, img.quad_maxc);
-    } else {
     g_blend_kernel[0] = rs.col2 != nullptr ? "k_render_fwd_tile<true>" : "k_render_fwd_tile<false>";
     if (rs.col2 != nullptr)
       hipLaunchKernelGGL(k_render_fwd_tile<true>, grid, dim3(64), 0, stream, rs, (const uint2*)img.ranges,
@@ -975,7 +778,6 @@ void launch_render_forward(const RenderSet& rs, const GeomState& g, const uint32
       hipLaunchKernelGGL(k_render_fwd_tile<false>, grid, dim3(64), 0, stream, rs, (const uint2*)img.ranges,
                          sorted_gauss, (const GaussRec*)g.rec, out_color, out_depth, out_alpha, img.final_T,
                          img.n_contrib, img.quad_maxc);
-    }
   } else {
     auto kern = rs.col2 != nullptr ? (rs.ckpt != nullptr ? k_render_fwd<true, true> : k_render_fwd<true, false>)
                                    : (rs.ckpt != nullptr ? k_render_fwd<false, true> : k_render_fwd<false, false>);
@@ -2338,11 +2140,16 @@ static bool bwd_hit_lists(bool two) {
   return two;
 }
 
-// Hit-list sums: one wave per tile walking the quadrants one after the other (k_render_bwd_tw) unless
-// GSR_BWD_KERNEL=quadrant (the workgroup of lockstep quadrant waves, k_render_bwd<·, true>).
-static bool bwd_tile_wave() {
+// One wave per tile walking the quadrants in turn, or the workgroup of lockstep quadrant waves (k_render_bwd).
+// Hit-list sums (C5): the tile wave (k_render_bwd_tw; C5 render_bwd 0.397 -> 0.329 ms/view) unless
+// GSR_BWD_KERNEL=quadrant.  Matrix-core sums (C3): the lockstep workgroup (the tile wave k_render_bwd_twm, with
+// GSR_BWD_KERNEL=tile, measured 0.098 -> 0.102 ms/view at C3, 0.104 -> 0.119 for 8-view sets:
+// profiles/r04/tile_wave_ab.txt).
+static bool bwd_tile_wave(bool hits) {
   const char* e = getenv("GSR_BWD_KERNEL");
-  return !(e != nullptr && strcmp(e, "quadrant") == 0);
+  if (e != nullptr && strcmp(e, "quadrant") == 0) return false;
+  if (e != nullptr && strcmp(e, "tile") == 0) return true;
+  return hits;
 }
 
 void launch_render_backward(const RenderSet& rs, const GeomState& g, const uint32_t* sorted_gauss,
@@ -2356,7 +2163,7 @@ void launch_render_backward(const RenderSet& rs, const GeomState& g, const uint3
   const dim3 grid(block_grid(rs, 4) + extra);
   const uint32_t* items = split ? img.split_items : nullptr;
   const bool hits = bwd_hit_lists(rs.dpix2 != nullptr);
-  if (hits && extra == 0 && bwd_tile_wave()) {
+  if (hits && extra == 0 && bwd_tile_wave(true)) {
     auto kt = rs.dpix2 != nullptr ? k_render_bwd_tw<true> : k_render_bwd_tw<false>;
     g_blend_kernel[1] = rs.dpix2 != nullptr ? "k_render_bwd_tw<true>" : "k_render_bwd_tw<false>";
     hipLaunchKernelGGL(kt, dim3(block_grid(rs, 4)), dim3(64), 0, stream, rs, (const uint2*)img.ranges,
@@ -2365,7 +2172,7 @@ void launch_render_backward(const RenderSet& rs, const GeomState& g, const uint3
                        bw.grow, bw.reach);
     return;
   }
-  if (!hits && rs.dpix2 == nullptr && extra == 0 && bwd_tile_wave()) {
+  if (!hits && rs.dpix2 == nullptr && extra == 0 && bwd_tile_wave(false)) {
     g_blend_kernel[1] = "k_render_bwd_twm<false>";
     hipLaunchKernelGGL(k_render_bwd_twm<false>, dim3(block_grid(rs, 4)), dim3(64), 0, stream, rs,
                        (const uint2*)img.ranges, (const uint32_t*)img.quad_maxc, sorted_gauss, (const GaussRec*)g.rec,
