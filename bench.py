@@ -271,7 +271,7 @@ PROFILE_VIEWS_PER_LAUNCH = 64  # profiles/run_profiles.sh: bench.py defaults, on
 # quadrant-wave forward and the one-wave-per-tile hit-list backward (gsr_render.hip).  A run uses the names the
 # library reports it launched (gsr_profile_kernel); the committed counters must name these (test_bench_fields)
 KERNELS = {"c3": ("k_render_fwd_tile<false>", "k_render_bwd<false, false>"),
-           "sugar": ("k_render_fwd<true, false>", "k_render_bwd_tw<true>")}
+           "sugar": ("k_render_fwd<true, false>", "k_render_bwd_tw<true, 2>")}
 
 
 def read_traffic(path, kernel, field="per_launch_bytes"):

@@ -293,7 +293,9 @@ def test_forward_kernels_bitwise(kind, switch, monkeypatch):
             # quadrant waves (k_render_bwd): hit-list sums for the two colours, matrix-core sums for one
             monkeypatch.setenv("GSR_BWD_SUMS", "hits" if kind == "sugar_two_colors" else "mfma")
             monkeypatch.setenv("GSR_BWD_SPLIT", "0")
-            monkeypatch.setenv("GSR_BWD_KERNEL", "tile" if kernel == "tile" else "quadrant")
+            monkeypatch.setenv("GSR_BWD_KERNEL", "tile" if kernel.startswith("tile") else "quadrant")
+            # (hit lists: one or two waves per tile, GSR_BWD_TW_WAVES)
+            monkeypatch.setenv("GSR_BWD_TW_WAVES", "1" if kernel == "tile1" else "2")
         elif kernel == "tile":
             monkeypatch.delenv("GSR_TILE_ORDER", raising=False)
         else:
@@ -322,3 +324,6 @@ def test_forward_kernels_bitwise(kind, switch, monkeypatch):
     tile, quad = run("tile"), run("quadrant")
     for i, (x, y) in enumerate(zip(tile, quad)):
         assert torch.equal(x, y), f"output {i} differs: {float((x.double() - y.double()).abs().max())}"
+    if switch == "bwd_kernel" and kind == "sugar_two_colors":
+        for i, (x, y) in enumerate(zip(run("tile1"), quad)):
+            assert torch.equal(x, y), f"one wave: output {i} differs: {float((x.double() - y.double()).abs().max())}"

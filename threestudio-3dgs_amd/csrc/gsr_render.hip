@@ -1483,23 +1483,25 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(TWO ? 4 : 5
                 n_contrib, dL_dcolor, dL_ddepth, dL_dalpha, grow, reach);
 }
 
-// Backward, one 64-thread wave per 16x16 tile (each lane holds the same pixel of the four 8x8 quadrants) —
-// the small-Gaussian regime (C5: SuGaR's surface Gaussians blend at ~13 pixels, a candidate usually in one
-// quadrant).  The workgroup-per-tile kernel above walks the quadrants in lockstep batches (three barriers per
-// batch, each batch as long as its busiest quadrant: 2.25 slots per kept pair at C5, waves parked on barriers
-// two thirds of their cycles, profiles/r03/sq_c5/); here one wave replays a batch's kept candidates quadrant
-// after quadrant, so a batch costs the sum of its kept (candidate, quadrant) pairs and nothing waits on
-// another wave.  Per batch: each lane stages one candidate's whole record (one 64-B line) and tests it
-// against the four quadrants (the same conservative cull); per quadrant the kept candidates are replayed
-// back to front (the same replay as k_render_bwd: per pixel the same candidates, order and operations) and
-// the lanes that blended append (u, u_1, w, pixel) to the wave's hit list; lane c then forms candidate c's
-// sums from its hits (the same pair_sums order), turns them into moments about the mean and adds the
-// quadrants as ((q0 + q1) + (q2 + q3)) — the order of the other kernel's quad DPP adds — and writes one row
-// per staged candidate.  A full hit list is summed early (each pair's sums are formed once, whenever).
-// Outputs match the hit-list k_render_bwd<TWO, true> (up to the sign of zero sums).
+// Backward with hit-list sums, NW waves per 16x16 tile, each walking its 4 / NW quadrants in turn (each lane
+// holds the same pixel of each of its quadrants) — the small-Gaussian regime (C5: SuGaR's surface Gaussians
+// blend at ~13 pixels, a candidate usually in one quadrant).  The workgroup-per-tile kernel above walks the
+// four quadrants in lockstep batches (three barriers per batch, each batch as long as its busiest quadrant:
+// 2.25 slots per kept pair at C5, waves parked on barriers two thirds of their cycles, profiles/r03/sq_c5/);
+// here a wave replays a batch's kept candidates quadrant after quadrant, so a batch costs the sum of its
+// quadrants' kept (candidate, quadrant) pairs.  NW = 1: one wave, nothing waits on another; NW = 2: two waves
+// (quadrants 0-1 and 2-3, half the per-lane pixel state: more waves per SIMD), two barriers per batch.
+// Per batch: lane c stages candidate c's record (wave 0 the conic / position / rect pieces and the cull
+// against the four quadrants, the last wave the colour pieces) and per quadrant the kept candidates are
+// replayed back to front (the same replay as k_render_bwd: per pixel the same candidates, order and
+// operations); the lanes that blended append (u, u_1, w, pixel) to their wave's hit list; lane c then forms
+// candidate c's sums from its hits (the same pair_sums order), turns them into moments about the mean and
+// adds the quadrants as ((q0 + q1) + (q2 + q3)) — the order of the other kernel's quad DPP adds — and wave 0
+// writes one row per staged candidate.  A full hit list is summed early (each pair's sums are formed once,
+// whenever).  Outputs match the hit-list k_render_bwd<TWO, true> bitwise.
 #define GSR_HCAP_TW 256
-template <bool TWO>
-__global__ __launch_bounds__(64) void k_render_bwd_tw(
+template <bool TWO, int NW>
+__global__ __launch_bounds__(64 * NW) void k_render_bwd_tw(
     RenderSet rs, const uint2* __restrict__ ranges, const uint32_t* __restrict__ quad_maxc,
     const uint32_t* __restrict__ sorted_gauss, const GaussRec* __restrict__ rec, const uint32_t* __restrict__ goff,
     const float* __restrict__ final_Ts, const uint32_t* __restrict__ n_contrib, const float* __restrict__ dL_dcolor,
@@ -1508,12 +1510,16 @@ __global__ __launch_bounds__(64) void k_render_bwd_tw(
   constexpr int NG = TWO ? NGV2 : NGV;  // raw sums per (candidate, quadrant)
   constexpr int NM = TWO ? 15 : NGV;    // moments per candidate
   constexpr int RW = TWO ? 4 : 3;       // float4 per gradient row
+  constexpr int NQ = 4 / NW;            // quadrants per wave
+  static_assert(NW == 1 || NW == 2, "one or two waves per tile");
   __shared__ float4 s0[65], s1[65], s2[65];
   __shared__ float4 s3[TWO ? 65 : 1];
   __shared__ uint32_t slot[64];
-  __shared__ uint32_t list[64];             // the current quadrant: first hit | hits << 16 per kept candidate
-  __shared__ float4 hits[GSR_HCAP_TW];      // (u, u_1, w, pixel) of the current quadrant's blended pairs
-  __shared__ float4 planes[TWO ? 128 : 64];  // the current quadrant's dL/dpixel per pixel
+  __shared__ uint32_t skeep[NW > 1 ? 64 : 1];          // the cull's 4-bit quadrant masks (NW = 2)
+  __shared__ float sacc[NW > 1 ? NM * 64 : 1];          // wave 1's (q2 + q3) moments (NW = 2)
+  __shared__ uint32_t slist[NW][64];                    // the current quadrant: first hit | hits << 16
+  __shared__ float4 shits[NW][GSR_HCAP_TW];             // (u, u_1, w, pixel) of the current quadrant's blends
+  __shared__ float4 splanes[NW][TWO ? 128 : 64];        // the current quadrant's dL/dpixel per pixel
   int v, tile, q_unused;
   if (!block_map<4>(blockIdx.x, rs, v, tile, q_unused)) return;
   GSR_TL_BEGIN
@@ -1535,7 +1541,12 @@ __global__ __launch_bounds__(64) void k_render_bwd_tw(
     grow += (size_t)RW * rs.row_start[v];
   }
   const float* bg = rs.bg[v];
-  const int lane = threadIdx.x;
+  const int lane = threadIdx.x & 63;
+  const int wv = NW > 1 ? __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6)) : 0;
+  const int qb = NQ * wv;  // this wave's first quadrant
+  uint32_t* list = slist[wv];
+  float4* hits = shits[wv];
+  float4* planes = splanes[wv];
   const int txi = tile % grid_x, tyi = tile / grid_x;
   const uint2 range = ranges[tile];
   const uint4 qm = reinterpret_cast<const uint4*>(quad_maxc)[tile];
@@ -1543,18 +1554,20 @@ __global__ __launch_bounds__(64) void k_render_bwd_tw(
   const int hi = __builtin_amdgcn_readfirstlane((int)max(max(qm.x, qm.y), max(qm.z, qm.w)));
   const int lo = 0;
 
-  // per pixel (one per quadrant) the replay state and the pixel's upstream gradients
-  float T[4], S[4], Sd[4], S2[4], dp0[4], dp1[4], dp2[4], dpd[4], dpa[4], e0[4], e1[4], e2[4], nbg[4], nbg2[4];
-  uint32_t last[4];
+  // per pixel (one per quadrant of this wave) the replay state and the pixel's upstream gradients
+  float T[NQ], S[NQ], Sd[NQ], S2[NQ], dp0[NQ], dp1[NQ], dp2[NQ], dpd[NQ], dpa[NQ], e0[NQ], e1[NQ], e2[NQ], nbg[NQ],
+      nbg2[NQ];
+  uint32_t last[NQ];
   const float lxf = (float)(txi * GSR_TILE_X + (lane & 7)), lyf = (float)(tyi * GSR_TILE_Y + (lane >> 3));
 #pragma unroll
-  for (int q = 0; q < 4; ++q) {
+  for (int j = 0; j < NQ; ++j) {
+    const int q = qb + j;
     const int px = txi * GSR_TILE_X + (q & 1) * 8 + (lane & 7), py = tyi * GSR_TILE_Y + (q >> 1) * 8 + (lane >> 3);
     const bool inside = px < W && py < H;
     const size_t pid = (size_t)py * W + px;
     const float T_final = inside ? final_Ts[pid] : 0.0f;
-    T[q] = T_final;
-    last[q] = inside ? n_contrib[pid] : 0u;
+    T[j] = T_final;
+    last[j] = inside ? n_contrib[pid] : 0u;
     float d[3] = {0.f, 0.f, 0.f};
     float dd = 0.f, da = 0.f;
     if (inside) {
@@ -1581,23 +1594,24 @@ __global__ __launch_bounds__(64) void k_render_bwd_tw(
         da = dsum + da;
       }
     }
-    dp0[q] = d[0], dp1[q] = d[1], dp2[q] = d[2], dpd[q] = dd, dpa[q] = da;
-    nbg[q] = -T_final * bg_dot3(bg, d[0], d[1], d[2]);
-    e0[q] = e1[q] = e2[q] = 0.f;
+    dp0[j] = d[0], dp1[j] = d[1], dp2[j] = d[2], dpd[j] = dd, dpa[j] = da;
+    nbg[j] = -T_final * bg_dot3(bg, d[0], d[1], d[2]);
+    e0[j] = e1[j] = e2[j] = 0.f;
     if (TWO && inside) {
       const float* d2 = rs.dpix2 + (size_t)v * 3 * HW;
-      e0[q] = d2[pid];
-      e1[q] = d2[HW + pid];
-      e2[q] = d2[2 * HW + pid];
+      e0[j] = d2[pid];
+      e1[j] = d2[HW + pid];
+      e2[j] = d2[2 * HW + pid];
     }
-    nbg2[q] = TWO ? -T_final * bg_dot3(bg, e0[q], e1[q], e2[q]) : 0.f;
-    S[q] = Sd[q] = S2[q] = 0.f;
+    nbg2[j] = TWO ? -T_final * bg_dot3(bg, e0[j], e1[j], e2[j]) : 0.f;
+    S[j] = Sd[j] = S2[j] = 0.f;
   }
   const float ddelx_dx = 0.5f * W, ddely_dy = 0.5f * H;
   const float4 zero4 = make_float4(0.f, 0.f, 0.f, 0.f);
 
-  // lane c stages candidate c (list position h - 1 - c) of each batch: its whole record, one batch ahead;
-  // indices two batches ahead
+  // lane c stages candidate c (list position h - 1 - c) of each batch, one batch ahead; indices two batches
+  // ahead.  Wave 0: rec.a, rec.b (the cull), rec.d + the row slot; the last wave: rec.c and the second colour.
+  const bool stage_geo = wv == 0, stage_col = wv == NW - 1;
   const uint32_t gmask = rs.gmask;
   unsigned int* const reach32 = reinterpret_cast<unsigned int*>(reach) + (v >> 5);
   const unsigned int vbit = 1u << (v & 31);
@@ -1605,21 +1619,25 @@ __global__ __launch_bounds__(64) void k_render_bwd_tw(
   uint32_t ngo = 0u, gi_next = 0u;
   auto load = [&](uint32_t g) {
     const float4* r = reinterpret_cast<const float4*>(rec + g);
-    na = r[0];
-    nb = r[1];
-    nc = r[2];
-    nd = r[3];
-    if (rs.col2 != nullptr) {
-      const float4 c2 = make_float4(rs.col2[3 * g], rs.col2[3 * g + 1], rs.col2[3 * g + 2], 0.f);
-      if (TWO)
-        n2 = c2;
-      else  // the second rasterizer call's colours replace the first's
-        nc = c2;
-    }
-    ngo = goff[g];
+    if (stage_geo) {
+      na = r[0];
+      nb = r[1];
+      nd = r[3];
+      ngo = goff[g];
 #ifndef GSR_EXP_NOREACH
-    atomicOr(reach32 + 2 * g, vbit);  // the Gaussian gets a row in this view (k_view_grad reads it)
+      atomicOr(reach32 + 2 * g, vbit);  // the Gaussian gets a row in this view (k_view_grad reads it)
 #endif
+    }
+    if (stage_col) {
+      nc = r[2];
+      if (rs.col2 != nullptr) {
+        const float4 c2 = make_float4(rs.col2[3 * g], rs.col2[3 * g + 1], rs.col2[3 * g + 2], 0.f);
+        if (TWO)
+          n2 = c2;
+        else  // the second rasterizer call's colours replace the first's
+          nc = c2;
+      }
+    }
   };
   if (hi > lo) {
     if (hi - 1 - lane >= lo) load(sorted_gauss[range.x + hi - 1 - lane] & gmask);
@@ -1627,8 +1645,8 @@ __global__ __launch_bounds__(64) void k_render_bwd_tw(
   }
 
   // hit-list sums of one (candidate, quadrant) pair -> moments about the candidate's mean (the flush of
-  // k_render_bwd), added to the candidate's running total as the quad DPP order does
-  float acca[NM], accb[NM];
+  // k_render_bwd); acc = q0 + q1 (NW = 2: this wave's pair, q0 + q1 or q2 + q3), accb = q2 + q3 (NW = 1)
+  float acc[NM], accb[NW == 1 ? NM : 1];
   auto pair_moments = [&](const int qq, const uint32_t e, float (&m)[NM]) {
     const int st = (int)(e & 0xffffu), n = (int)(e >> 16);
     float C[NG];
@@ -1682,32 +1700,30 @@ __global__ __launch_bounds__(64) void k_render_bwd_tw(
       m[14 % NM] = C[15 % NG];
     }
   };
-  // the pending pairs of quadrant qq (lanes whose bit is set) into the running totals
-  auto flush = [&](const int qq, const unsigned long long pend) {
+  // the pending pairs of this wave's quadrant j (lanes whose bit is set) into the running total
+  auto flush = [&](const int j, const unsigned long long pend) {
     if (!((pend >> lane) & 1ull)) return;
     float m[NM];
-    pair_moments(qq, list[lane], m);
+    pair_moments(qb + j, list[lane], m);
 #pragma unroll
     for (int i = 0; i < NM; ++i) {
-      if (qq == 0) acca[i] = m[i];
-      else if (qq == 1) acca[i] = acca[i] + m[i];
-      else if (qq == 2) accb[i] = m[i];
-      else accb[i] = accb[i] + m[i];
+      if (j == 0) acc[i] = m[i];
+      else if (j == 1) acc[i] = acc[i] + m[i];
+      else if (j == 2) accb[i % (NW == 1 ? NM : 1)] = m[i];
+      else accb[i % (NW == 1 ? NM : 1)] = accb[i % (NW == 1 ? NM : 1)] + m[i];
     }
   };
 
   for (int h = hi; h > lo; h -= 64) {
     const int rel_c = h - 1 - lane;
     const bool staged = rel_c >= lo;
-    // this lane's candidate: pre-multiplied conic for gauss_power2 (.w of s1: list position), row slot
-    const float4 ca = make_float4(na.x, na.y, GSR_CONIC_K_AC * na.z, GSR_CONIC_K_B * na.w);
-    const float4 cb = make_float4(GSR_CONIC_K_AC * nb.x, nb.y, nb.z, __uint_as_float((uint32_t)rel_c));
     uint32_t keep4 = 0u;
-    if (staged) {
+    if (staged && stage_geo) {
+      // pre-multiplied conic for gauss_power2 (.w of s1: list position), row slot
+      const float4 ca = make_float4(na.x, na.y, GSR_CONIC_K_AC * na.z, GSR_CONIC_K_B * na.w);
+      const float4 cb = make_float4(GSR_CONIC_K_AC * nb.x, nb.y, nb.z, __uint_as_float((uint32_t)rel_c));
       s0[lane] = ca;
       s1[lane] = cb;
-      s2[lane] = nc;
-      if (TWO) s3[lane] = n2;
       const uint32_t dx_ = __float_as_uint(nd.x), dy_ = __float_as_uint(nd.y);
       const int xmin = dx_ & 0xffff, ymin = dx_ >> 16, xmax = dy_ & 0xffff;
       slot[lane] = ngo + (uint32_t)((tyi - ymin) * (xmax - xmin) + (txi - xmin));
@@ -1719,6 +1735,11 @@ __global__ __launch_bounds__(64) void k_render_bwd_tw(
         if (rel_c < qmaxc[q] &&
             quadrant_hit(r0, r1, (float)(txi * GSR_TILE_X + (q & 1) * 8), (float)(tyi * GSR_TILE_Y + (q >> 1) * 8)))
           keep4 |= 1u << q;
+      if (NW > 1) skeep[lane] = keep4;
+    }
+    if (staged && stage_col) {
+      s2[lane] = nc;
+      if (TWO) s3[lane] = n2;
     }
     // the next batch's records and the one after's indices
     if (h - 64 > lo) {
@@ -1726,24 +1747,29 @@ __global__ __launch_bounds__(64) void k_render_bwd_tw(
       if (h - 129 - lane >= lo) gi_next = sorted_gauss[range.x + h - 129 - lane] & gmask;
     }
 #pragma unroll
-    for (int i = 0; i < NM; ++i) acca[i] = accb[i] = 0.f;
-    __syncthreads();  // (one wave: orders the staging writes before other lanes' reads)
+    for (int i = 0; i < NM; ++i) acc[i] = 0.f;
+    if (NW == 1)
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
+      for (int i = 0; i < NM; ++i) accb[i % (NW == 1 ? NM : 1)] = 0.f;
+    __syncthreads();  // (the staging of every wave before any wave's reads)
+    if (NW > 1) keep4 = staged ? skeep[lane] : 0u;
+#pragma unroll
+    for (int j = 0; j < NQ; ++j) {
+      const int q = qb + j;
       const unsigned long long kq = __ballot((keep4 >> q) & 1u);
       if (kq == 0ull) continue;
       // this quadrant's dL/dpixel planes for the sums
-      planes[TWO ? 2 * lane : lane] = make_float4(dp0[q], dp1[q], dp2[q], dpd[q]);
-      if (TWO) planes[2 * lane + 1] = make_float4(e0[q], e1[q], e2[q], 0.f);
+      planes[TWO ? 2 * lane : lane] = make_float4(dp0[j], dp1[j], dp2[j], dpd[j]);
+      if (TWO) planes[2 * lane + 1] = make_float4(e0[j], e1[j], e2[j], 0.f);
       const float pxf = lxf + (float)((q & 1) * 8), pyf = lyf + (float)((q >> 1) * 8);
       int fill = 0;
       unsigned long long pend = 0ull, rest = kq;
-      int j = (int)__builtin_ctzll(rest);
-      float4 ga = s0[j], gb = s1[j], gc = s2[j];
-      float4 gd = TWO ? s3[j] : zero4;
+      int jc = (int)__builtin_ctzll(rest);
+      float4 ga = s0[jc], gb = s1[jc], gc = s2[jc];
+      float4 gd = TWO ? s3[jc] : zero4;
       while (true) {
         rest &= rest - 1ull;
-        const int jn = rest != 0ull ? (int)__builtin_ctzll(rest) : j;
+        const int jn = rest != 0ull ? (int)__builtin_ctzll(rest) : jc;
         const float4 xa = s0[jn], xb = s1[jn], xc = s2[jn];
         const float4 xd = TWO ? s3[jn] : zero4;
         // the replay step of k_render_bwd (replay / replay2) on this quadrant's pixel
@@ -1752,55 +1778,66 @@ __global__ __launch_bounds__(64) void k_render_bwd_tw(
         const float power2 = gauss_power2(ga.z, ga.w, gb.x, dx, dy);
         const float G = __builtin_amdgcn_exp2f(power2);
         const float alpha = fminf(GSR_ALPHA_MAX, gb.y * G);
-        const bool hit = rel < last[q] && power2 <= 0.0f && alpha >= GSR_ALPHA_MIN;
+        const bool hit = rel < last[j] && power2 <= 0.0f && alpha >= GSR_ALPHA_MIN;
         const float a_eff = hit ? alpha : 0.0f;
         const float g_eff = hit ? G : 0.0f;
         const float oma = 1.f - a_eff;
         const float inv_1ma = fast_rcp(oma);
-        T[q] = T[q] * inv_1ma;
-        const float cd = fmaf(gc.x, dp0[q], fmaf(gc.y, dp1[q], fmaf(gc.z, dp2[q], dpa[q])));
+        T[j] = T[j] * inv_1ma;
+        const float cd = fmaf(gc.x, dp0[j], fmaf(gc.y, dp1[j], fmaf(gc.z, dp2[j], dpa[j])));
         float u, u1 = 0.f;
         if (TWO) {
-          const float cd2 = fmaf(gd.x, e0[q], fmaf(gd.y, e1[q], gd.z * e2[q]));
-          u1 = g_eff * fmaf(T[q], fmaf(gb.z - Sd[q], dpd[q], cd - S[q]), inv_1ma * nbg[q]);
-          u = fmaf(g_eff, fmaf(T[q], cd2 - S2[q], inv_1ma * nbg2[q]), u1);
-          S2[q] = fmaf(a_eff, cd2, oma * S2[q]);
+          const float cd2 = fmaf(gd.x, e0[j], fmaf(gd.y, e1[j], gd.z * e2[j]));
+          u1 = g_eff * fmaf(T[j], fmaf(gb.z - Sd[j], dpd[j], cd - S[j]), inv_1ma * nbg[j]);
+          u = fmaf(g_eff, fmaf(T[j], cd2 - S2[j], inv_1ma * nbg2[j]), u1);
+          S2[j] = fmaf(a_eff, cd2, oma * S2[j]);
         } else {
-          u = g_eff * fmaf(T[q], fmaf(gb.z - Sd[q], dpd[q], cd - S[q]), inv_1ma * nbg[q]);
+          u = g_eff * fmaf(T[j], fmaf(gb.z - Sd[j], dpd[j], cd - S[j]), inv_1ma * nbg[j]);
         }
-        const float w = a_eff * T[q];
-        S[q] = fmaf(a_eff, cd, oma * S[q]);
-        Sd[q] = fmaf(a_eff, gb.z, oma * Sd[q]);
+        const float w = a_eff * T[j];
+        S[j] = fmaf(a_eff, cd, oma * S[j]);
+        Sd[j] = fmaf(a_eff, gb.z, oma * Sd[j]);
         const unsigned long long hm = __ballot(hit);
         const int n = __popcll(hm);
         if (fill + n > GSR_HCAP_TW) {
-          // list full: the finished pairs' sums now, then start over
-          __syncthreads();
-          flush(q, pend);
-          __syncthreads();
+          // list full: the finished pairs' sums now, then start over (this wave's own LDS: in-order)
+          asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+          flush(j, pend);
+          asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
           fill = 0;
           pend = 0ull;
         }
         if (hit) hits[fill + (int)mask_rank(hm)] = make_float4(u, u1, w, __uint_as_float((uint32_t)lane));
-        if (lane == 0) list[j] = (uint32_t)fill | ((uint32_t)n << 16);
+        if (lane == 0) list[jc] = (uint32_t)fill | ((uint32_t)n << 16);
         fill += n;
-        pend |= 1ull << j;
+        pend |= 1ull << jc;
         if (rest == 0ull) break;
         ga = xa;
         gb = xb;
         gc = xc;
         gd = xd;
-        j = jn;
+        jc = jn;
       }
-      __syncthreads();
-      flush(q, pend);
-      __syncthreads();  // (hits, list and planes are rewritten by the next quadrant)
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      flush(j, pend);
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // (hits, list and planes are rewritten next)
     }
-    if (staged) {
+    if (NW > 1) {
+      if (wv == 1)
+#pragma unroll
+        for (int i = 0; i < NM; ++i) sacc[i * 64 + lane] = acc[i];
+      __syncthreads();  // (wave 1's moments to wave 0; both waves' reads of the staged batch are done)
+    }
+    if (staged && wv == 0) {
       // ((q0 + q1) + (q2 + q3)) per moment, then the reference's terms (k_render_bwd's flush)
       float m[NM];
+      if (NW > 1) {
 #pragma unroll
-      for (int i = 0; i < NM; ++i) m[i] = acca[i] + accb[i];
+        for (int i = 0; i < NM; ++i) m[i] = acc[i] + sacc[i * 64 + lane];
+      } else {
+#pragma unroll
+        for (int i = 0; i < NM; ++i) m[i] = acc[i] + accb[i % (NW == 1 ? NM : 1)];
+      }
       const float4 ga = s0[lane];
       const float4 gb = s1[lane];
       const float o = gb.y;
@@ -1819,7 +1856,7 @@ __global__ __launch_bounds__(64) void k_render_bwd_tw(
         row[3] = make_float4(m[14 % NM], dmx1, dmy1, 0.f);
       }
     }
-    __syncthreads();  // (the staged batch is rewritten next)
+    if (NW == 1) __syncthreads();  // (the staged batch is rewritten next)
   }
   GSR_TL_END(1, hi)
 }
@@ -2145,6 +2182,11 @@ static bool bwd_hit_lists(bool two) {
 // GSR_BWD_KERNEL=quadrant.  Matrix-core sums (C3): the lockstep workgroup (the tile wave k_render_bwd_twm, with
 // GSR_BWD_KERNEL=tile, measured 0.098 -> 0.102 ms/view at C3, 0.104 -> 0.119 for 8-view sets:
 // profiles/r04/tile_wave_ab.txt).
+// waves per tile of the hit-list tile kernel (GSR_BWD_TW_WAVES=1|2)
+static int bwd_tw_waves() {
+  const char* e = getenv("GSR_BWD_TW_WAVES");
+  return e != nullptr && strcmp(e, "1") == 0 ? 1 : 2;
+}
 static bool bwd_tile_wave(bool hits) {
   const char* e = getenv("GSR_BWD_KERNEL");
   if (e != nullptr && strcmp(e, "quadrant") == 0) return false;
@@ -2164,9 +2206,12 @@ void launch_render_backward(const RenderSet& rs, const GeomState& g, const uint3
   const uint32_t* items = split ? img.split_items : nullptr;
   const bool hits = bwd_hit_lists(rs.dpix2 != nullptr);
   if (hits && extra == 0 && bwd_tile_wave(true)) {
-    auto kt = rs.dpix2 != nullptr ? k_render_bwd_tw<true> : k_render_bwd_tw<false>;
-    g_blend_kernel[1] = rs.dpix2 != nullptr ? "k_render_bwd_tw<true>" : "k_render_bwd_tw<false>";
-    hipLaunchKernelGGL(kt, dim3(block_grid(rs, 4)), dim3(64), 0, stream, rs, (const uint2*)img.ranges,
+    const bool two = bwd_tw_waves() == 2;
+    auto kt = rs.dpix2 != nullptr ? (two ? k_render_bwd_tw<true, 2> : k_render_bwd_tw<true, 1>)
+                                  : (two ? k_render_bwd_tw<false, 2> : k_render_bwd_tw<false, 1>);
+    g_blend_kernel[1] = rs.dpix2 != nullptr ? (two ? "k_render_bwd_tw<true, 2>" : "k_render_bwd_tw<true, 1>")
+                                            : (two ? "k_render_bwd_tw<false, 2>" : "k_render_bwd_tw<false, 1>");
+    hipLaunchKernelGGL(kt, dim3(block_grid(rs, 4)), dim3(two ? 128 : 64), 0, stream, rs, (const uint2*)img.ranges,
                        (const uint32_t*)img.quad_maxc, sorted_gauss, (const GaussRec*)g.rec, (const uint32_t*)g.goff,
                        (const float*)img.final_T, (const uint32_t*)img.n_contrib, dL_dcolor, dL_ddepth, dL_dalpha,
                        bw.grow, bw.reach);
