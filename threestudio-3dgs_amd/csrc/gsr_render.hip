@@ -214,7 +214,11 @@ __global__ __launch_bounds__(64) void k_render_fwd(RenderSet rs,
 #ifndef GSR_EXP_FWD_NOC
     n2 = rec[g0].c;
 #endif
+#ifdef GSR_EXP_NOCOL2
+    if (C2) n3 = make_float4(__uint_as_float(g0), 0.f, 0.f, 0.f);  // timing only: no col2 gather
+#else
     if (C2) n3 = make_float4(col2[3 * g0], col2[3 * g0 + 1], col2[3 * g0 + 2], 0.f);
+#endif
   }
   if (64 + lane < n) gi_next = sorted_gauss[range.x + 64 + lane] & gmask;
   // split backward: T at each chunk boundary the walk reaches, and each chunk's own colour / depth sums
@@ -240,7 +244,11 @@ __global__ __launch_bounds__(64) void k_render_fwd(RenderSet rs,
 #ifndef GSR_EXP_FWD_NOC
       n2 = rec[gi_next].c;
 #endif
+#ifdef GSR_EXP_NOCOL2
+      if (C2) n3 = make_float4(__uint_as_float(gi_next), 0.f, 0.f, 0.f);  // timing only: no col2 gather
+#else
       if (C2) n3 = make_float4(col2[3 * gi_next], col2[3 * gi_next + 1], col2[3 * gi_next + 2], 0.f);
+#endif
     }
     if (base + 128 + lane < n) gi_next = sorted_gauss[range.x + base + 128 + lane] & gmask;
     bool keep = false;
