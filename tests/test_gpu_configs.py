@@ -269,6 +269,26 @@ def test_backward_view_groups_bitwise(monkeypatch):
         assert np.array_equal(one["g_means2D"][v], split["g_means2D"][v])
 
 
+@pytest.mark.parametrize("groups", ["one", "six"])
+def test_gauss_fused_bitwise(groups, monkeypatch):
+    """Without SH (precomputed colours: the SuGaR renderers) the per-Gaussian backward runs fused (k_gauss_fused:
+    one thread per Gaussian walks the views, no per-(view, Gaussian) records) — bitwise the gradients of the
+    split kernels (GSR_GAUSS_FUSED=0: k_view_grad + k_gauss_accum), in one view group and continued over six."""
+    scene = gs.make_scene(20_000, sh_degree=0, seed=33)
+    scene = dict(scene, colors_precomp=(scene["shs"][:, 0, :] * np.float32(gs.C0) + np.float32(0.5)).astype(np.float32))
+    scene.pop("shs")
+    cams = [make_camera(192, 160, elevation=5.0 * i, azimuth=60.0 * i) for i in range(6)]
+    ups = [gs.upstream_grads(160, 192, seed=90 + v) for v in range(6)]
+    budget = 1 if groups == "six" else None
+    fused = _batched_grads(scene, cams, ups, monkeypatch, budget=budget)
+    monkeypatch.setenv("GSR_GAUSS_FUSED", "0")
+    split = _batched_grads(scene, cams, ups, monkeypatch, budget=budget)
+    for k in ("g_means3D", "g_opacity", "g_colors", "g_scales", "g_rotations"):
+        assert np.array_equal(fused[k], split[k]), k
+    for v in range(6):
+        assert np.array_equal(fused["g_means2D"][v], split["g_means2D"][v]), v
+
+
 @pytest.mark.parametrize("split", ["off", "on"])
 def test_view_sets_bitwise(split, monkeypatch):
     """20 views as one set vs four sets of 5 (later sets continue the sums: include/gsr.h accumulate with

@@ -16,6 +16,9 @@
 // Gradient conventions of the reference are kept: the 0.99 alpha clamp is ignored in
 // dL/dG, the frustum clamp zeroes dL/dt_x,y only, denom2inv carries +1e-7, the scale gradient is
 // w.r.t. scale_modifier * scale.
+#include <cstdlib>
+#include <cstring>
+
 #include "gsr_kernels.h"
 #include "gsr_math.h"
 #include "gsr_wave.h"
@@ -636,12 +639,170 @@ __global__ __launch_bounds__(256) void k_gauss_accum(GaussBackwardArgs a, AccumA
   }
 }
 
+// ---- A+B fused, without SH (colours precomputed: the SuGaR normal renderer, C5) -------------------------
+// One thread per Gaussian walks the group's views in order: for each view its blend reached (reach bit) the
+// k_view_grad work (rows gathered up to the tile cut-offs, conic -> 2D cov -> 3D cov / mean, projection and
+// depth terms, the view's means2D gradient) and, instead of writing a 64/80-byte record for k_gauss_accum
+// to read back, the sums in registers in the same view order; the unreached views get their zero means2D
+// gradient.  With no SH there is no per-view SH backward to keep apart from the gather (the reason for the
+// split), and the records were ~200 MB/view of HBM writes + reads at C5.  The same operations in the same
+// order as k_view_grad + k_gauss_accum: bitwise the same gradients (up to the sign of zero sums).  Lanes of a
+// wave walk the same view at a time: the camera comes through scalar loads; a view's record / row slot of
+// consecutive Gaussians are consecutive (coalesced); the next reached view's are loaded one view ahead.
+template <bool TWO>
+__global__ __launch_bounds__(256) void k_gauss_fused(GaussBackwardArgs a, ViewGradArgs va, AccumArgs b) {
+  const int idx = a.g0 + blockIdx.x * 256 + threadIdx.x;
+  const bool valid = idx < a.g1;
+  const int ix = valid ? idx : a.g0;  // (threads past the range follow the loop uniformly, write nothing)
+  const bool acc = b.accumulate != 0;
+  const unsigned long long reach_word = valid ? va.reach[ix] : 0ull;
+  float3 dmean = make_float3(0.f, 0.f, 0.f);
+  float dcov[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  float dop = 0.f, dcr = 0.f, dcg = 0.f, dcb = 0.f;
+  float d2[3] = {0.f, 0.f, 0.f};
+  if (valid && acc) {
+    // continue the earlier groups' sums in place (same summation order as one group)
+    dmean = make_float3(a.dL_dmeans3D[3 * idx], a.dL_dmeans3D[3 * idx + 1], a.dL_dmeans3D[3 * idx + 2]);
+    dop = a.dL_dopacity[idx];
+    if (a.dL_dcolors) dcr = a.dL_dcolors[3 * idx], dcg = a.dL_dcolors[3 * idx + 1], dcb = a.dL_dcolors[3 * idx + 2];
+    if (b.dcov_carry)
+#pragma unroll
+      for (int k = 0; k < 6; ++k) dcov[k] = b.dcov_carry[6 * idx + k];
+    if (TWO)
+      for (int k = 0; k < 3; ++k) d2[k] = b.dcolors2[3 * idx + k];
+  }
+  const float3 mean = make_float3(a.means3D[3 * ix], a.means3D[3 * ix + 1], a.means3D[3 * ix + 2]);
+  float cov3D[6];
+  if (reach_word != 0ull) {
+    if (a.cov3D_precomp) {
+#pragma unroll
+      for (int k = 0; k < 6; ++k) cov3D[k] = a.cov3D_precomp[6 * ix + k];
+    } else {
+      const float3 scale = make_float3(a.scales[3 * ix], a.scales[3 * ix + 1], a.scales[3 * ix + 2]);
+      const float4 rot = make_float4(a.rotations[4 * ix], a.rotations[4 * ix + 1], a.rotations[4 * ix + 2],
+                                     a.rotations[4 * ix + 3]);
+      cov3d_from_scale_rot(scale, a.scale_modifier, rot, cov3D);
+    }
+  }
+  // the next reached view's record and row slot (one view ahead)
+  GaussRec nrec;
+  uint32_t ngo = 0u;
+  auto fetch = [&](int vl) {
+    const size_t o = (size_t)(va.v0 + vl) * a.P + ix;
+    nrec = va.g.rec[o];
+    ngo = va.g.goff[o];
+  };
+  const int vfirst = reach_word != 0ull ? (int)__builtin_ctzll(reach_word) : va.V;
+  if (vfirst < va.V) fetch(vfirst);
+#pragma unroll 1
+  for (int vl = 0; vl < va.V; ++vl) {
+    const int vg = va.v0 + vl;
+    float* m2 = va.dmeans2D + 3 * ((size_t)vg * a.P + ix);
+    if (!((reach_word >> vl) & 1ull)) {
+      if (valid) m2[0] = 0.f, m2[1] = 0.f, m2[2] = 0.f;
+      continue;
+    }
+    const GaussRec gr = nrec;
+    const uint32_t go = ngo;
+    const unsigned long long later = reach_word & ~((2ull << vl) - 1ull);
+    if (later != 0ull) fetch((int)__builtin_ctzll(later));
+    const ViewCam& cam = va.cam[vl];
+    typedef __attribute__((address_space(4))) const float* cfptr;
+    float viewm[16], projm[16];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) viewm[i] = ((cfptr)cam.view)[i], projm[i] = ((cfptr)cam.proj)[i];
+    ViewGeom vgm;
+    vgm.view = viewm;
+    vgm.proj = projm;
+    vgm.tanx = cam.tanx;
+    vgm.tany = cam.tany;
+    vgm.fy = va.H / (2.0f * cam.tany);
+    vgm.fx = va.W / (2.0f * cam.tanx);
+    const float4* grow = va.grow + (size_t)(TWO ? 4 : 3) * va.row_start[vl];
+    const uint2* cut = va.img.cut + (size_t)vg * va.tiles;
+    const RowSums r = gather_rows<TWO>((uint32_t)ix, gr, go, va.gx, cut, grow);
+    bool reached = (r.dmx != 0.f) | (r.dmy != 0.f) | (r.dca != 0.f) | (r.dcb != 0.f) | (r.dcc != 0.f) |
+                   (r.dop != 0.f) | (r.dcr != 0.f) | (r.dcg != 0.f) | (r.dcbl != 0.f) | (r.ddep != 0.f);
+    if (TWO) reached = reached | (r.dr2 != 0.f) | (r.dg2 != 0.f) | (r.db2 != 0.f);
+    if (!reached) {
+      if (valid) m2[0] = 0.f, m2[1] = 0.f, m2[2] = 0.f;
+      continue;
+    }
+    if (valid) {
+      m2[0] = TWO ? r.dmx1 : r.dmx;
+      m2[1] = TWO ? r.dmy1 : r.dmy;
+      m2[2] = 0.f;
+    }
+    float dcv[6];
+    float3 dm;
+    cov2d_backward(mean, cov3D, vgm, r.dca, r.dcb, r.dcc, dcv, dm);
+    proj_backward(mean, projm, r.dmx, r.dmy, dm);
+    dm.x += viewm[2] * r.ddep;
+    dm.y += viewm[6] * r.ddep;
+    dm.z += viewm[10] * r.ddep;
+    // the record's fields summed as k_gauss_accum sums them (view order)
+    dmean.x += dm.x;
+    dmean.y += dm.y;
+    dmean.z += dm.z;
+#pragma unroll
+    for (int k = 0; k < 6; ++k) dcov[k] += dcv[k];
+    dcr += r.dcr;
+    dcg += r.dcg;
+    dcb += r.dcbl;
+    dop += r.dop;
+    if (TWO) {
+      d2[0] += r.dr2;
+      d2[1] += r.dg2;
+      d2[2] += r.db2;
+    }
+  }
+  if (!valid) return;
+  a.dL_dmeans3D[3 * idx] = dmean.x;
+  a.dL_dmeans3D[3 * idx + 1] = dmean.y;
+  a.dL_dmeans3D[3 * idx + 2] = dmean.z;
+  a.dL_dopacity[idx] = dop;
+  if (a.dL_dcolors) {
+    a.dL_dcolors[3 * idx] = dcr;
+    a.dL_dcolors[3 * idx + 1] = dcg;
+    a.dL_dcolors[3 * idx + 2] = dcb;
+  }
+  if (TWO)
+    for (int k = 0; k < 3; ++k) b.dcolors2[3 * idx + k] = d2[k];
+  if (b.dcov_carry)
+    for (int k = 0; k < 6; ++k) b.dcov_carry[6 * idx + k] = dcov[k];
+  if (a.dL_dcov3D && a.dL_dcov3D != b.dcov_carry)
+    for (int k = 0; k < 6; ++k) a.dL_dcov3D[6 * idx + k] = dcov[k];
+  if (!a.cov3D_precomp && a.dL_dscales) {
+    const float3 scale = make_float3(a.scales[3 * idx], a.scales[3 * idx + 1], a.scales[3 * idx + 2]);
+    const float4 rot = make_float4(a.rotations[4 * idx], a.rotations[4 * idx + 1], a.rotations[4 * idx + 2],
+                                   a.rotations[4 * idx + 3]);
+    float ds[3], dq[4];
+    scale_rot_backward(scale, rot, a.scale_modifier, dcov, ds, dq);
+    for (int k = 0; k < 3; ++k) a.dL_dscales[3 * idx + k] = ds[k];
+    for (int k = 0; k < 4; ++k) a.dL_drotations[4 * idx + k] = dq[k];
+  }
+}
+
+// the fused per-Gaussian backward for launches without SH (GSR_GAUSS_FUSED=0: the split kernels, A/B)
+static bool gauss_fused_on(const GaussBackwardArgs& a) {
+  if (a.shs != nullptr && a.M > 0) return false;
+  const char* e = getenv("GSR_GAUSS_FUSED");
+  return !(e != nullptr && strcmp(e, "0") == 0);
+}
+
 // LDS budget for the staged tile cut-offs of k_view_grad (larger images read them from L2).
 #define GSR_CUT_LDS_MAX (48 * 1024)
 
 void launch_gauss_backward(const GaussBackwardArgs& a, ViewGradArgs va, const AccumArgs& b, hipStream_t stream) {
   const int n = a.g1 - a.g0;
   if (n <= 0 || va.V <= 0) return;
+  if (gauss_fused_on(a)) {
+    if (b.dcolors2)
+      hipLaunchKernelGGL(k_gauss_fused<true>, dim3(div_up(n, 256)), dim3(256), 0, stream, a, va, b);
+    else
+      hipLaunchKernelGGL(k_gauss_fused<false>, dim3(div_up(n, 256)), dim3(256), 0, stream, a, va, b);
+    return;
+  }
   const size_t cut_bytes = sizeof(uint2) * (size_t)va.tiles;
   va.cut_in_lds = cut_bytes <= GSR_CUT_LDS_MAX ? 1 : 0;
   // items per thread: GSR_VG_ITEMS, halved (down to 2) while the launch would have fewer than 1024 blocks
