@@ -8,7 +8,7 @@ rc=$?; [ $rc -le 1 ] || exit $rc
 timeout -k 10 300 python -u bench.py --no-cpu-baseline --no-knn > gpurun_out/${T}_bench.json 2> gpurun_out/${T}_bench.log || exit 1
 GSR_BWD_TW_WAVES=1 timeout -k 10 300 python -u bench.py --no-cpu-baseline --no-knn --per-view-views 0 --extra-lines c5 > gpurun_out/${T}_bench_tw1.json 2> gpurun_out/${T}_bench_tw1.log || exit 1
 timeout -k 10 300 python -u bench.py --no-cpu-baseline --no-knn --per-view-views 0 --extra-lines c5 > gpurun_out/${T}_bench2.json 2> gpurun_out/${T}_bench2.log || exit 1
-GSR_GAUSS_FUSED=0 timeout -k 10 300 python -u bench.py --no-cpu-baseline --no-knn --per-view-views 0 --extra-lines c5 > gpurun_out/${T}_bench_split.json 2> gpurun_out/${T}_bench_split.log || exit 1
+GSR_GAUSS_FUSED=0 timeout -k 10 300 python -u bench.py --no-cpu-baseline --no-knn --extra-lines c5 > gpurun_out/${T}_bench_split.json 2> gpurun_out/${T}_bench_split.log || exit 1
 # timing only: the C5 forward without the second colour's gathers (GSR_EXP_NOCOL2 diagnostic library)
 for lib in product exp; do
   if [ $lib = exp ]; then export GSR_HIP_LIB=$PWD/threestudio-3dgs_amd/csrc/build_exp_NOCOL2/libgsr_hip_exp.so; fi
