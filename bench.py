@@ -507,8 +507,8 @@ def roofline_fields(args, phases, Ks, Ls, H, W, launched=None):
             r["valu"] = v
         r["limiter"] = "VALU issue / LDS latency per (pixel, Gaussian) pair, not HBM (see counter_frac, valu)"
         if sugar and phase == "render_bwd":
-            r["limiter"] = ("waits: waves parked on the batch barriers behind the busiest quadrant and on the "
-                            "staging gathers (2/3 of wave cycles, profiles/r03/sq_c5/), not HBM")
+            r["limiter"] = ("latency of the per-candidate replay chain and its LDS round trips (the quadrants of a "
+                            "tile walked in turn by one or two waves, 3 waves per SIMD), not HBM; VALU ~30 % busy")
         rows[phase] = r
     dominant = max(phases.items(), key=lambda kv: kv[1][0])[0]
     blend = "render_bwd" if phases["render_bwd"][0] >= phases["render_fwd"][0] else "render_fwd"

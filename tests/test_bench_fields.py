@@ -50,13 +50,13 @@ def test_no_counters_for_unprofiled_workloads():
 
 
 def test_c5_line_reads_its_own_counters():
-    """The C5 line (--workload sugar at its 800^2) takes the two-colour kernels' counters from
-    profiles/r03d_sugar_traffic.json (hit-list backward, quadrant-wave two-colour forward)."""
+    """The C5 line (--workload sugar at its 800^2) takes the two-colour kernels' counters from its own traffic file
+    (the tile-wave hit-list backward, the quadrant-wave two-colour forward)."""
     a = _args("--workload", "sugar", "--res", "800")
     r = bench.roofline_fields(a, PHASES, [2.7e6] * 64, [2.69e6] * 64, 800, 800)
     assert r["roofline"]["traffic"] is not None and r["roofline"]["traffic"] > 0
     assert r["roofline_fwd_blend"]["traffic"] is not None
-    assert "counters_note" not in r and "barriers" in r["roofline"]["limiter"]
+    assert "counters_note" not in r and "not HBM" in r["roofline"]["limiter"]
 
 
 def test_committed_counters_name_the_timed_kernels():
