@@ -317,17 +317,22 @@ __global__ __launch_bounds__(64) void k_emit(int P, int nbe, int grid_x, GeomSta
 // rounds' keys are loaded first, neighbours come from the adjacent lanes (shuffles) and, at round
 // edges, from the neighbouring round (readlane).
 #define GSR_RANGE_ROUNDS 16
+// A block covers GSR_RANGE_TILE instances: each wave GSR_RANGE_CHUNKS consecutive chunks of 64 x
+// GSR_RANGE_ROUNDS (fewer, longer-lived workgroups: the launch was bound by workgroup dispatch, 2.6 TB/s).
+#define GSR_RANGE_CHUNKS (GSR_RANGE_TILE / (4 * 64 * GSR_RANGE_ROUNDS))
 __global__ __launch_bounds__(256) void k_tile_ranges(SegInfo inst, int n_tiles, int gbits,
                                                      const uint32_t* __restrict__ keys,
                                                      uint2* __restrict__ ranges) {
   uint32_t lb;
   const int v = seg_of_block(inst, blockIdx.x, lb);
   const int lane = threadIdx.x & 63;
-  const uint32_t base = (lb * 4 + (threadIdx.x >> 6)) * (64u * GSR_RANGE_ROUNDS);
   const uint32_t K = seg_live(inst, v);
-  if (base >= K) return;  // wave-uniform
   const uint32_t* kv = keys + inst.start[v];
   uint2* rv = ranges + (size_t)v * n_tiles;
+#pragma unroll 1
+  for (int ch = 0; ch < GSR_RANGE_CHUNKS; ++ch) {
+  const uint32_t base = ((lb * 4 + (threadIdx.x >> 6)) * GSR_RANGE_CHUNKS + ch) * (64u * GSR_RANGE_ROUNDS);
+  if (base >= K) return;  // wave-uniform
   uint32_t t[GSR_RANGE_ROUNDS];
 #pragma unroll
   for (int r = 0; r < GSR_RANGE_ROUNDS; ++r) {
@@ -351,6 +356,7 @@ __global__ __launch_bounds__(256) void k_tile_ranges(SegInfo inst, int n_tiles, 
       if (prev != t[r]) rv[t[r]].x = p;
       if (next != t[r]) rv[t[r]].y = p + 1;
     }
+  }
   }
 }
 

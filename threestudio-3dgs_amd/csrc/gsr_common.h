@@ -35,7 +35,7 @@
 #define GSR_GOFF_TILE 4096  // Gaussians per block of the gradient-row offset scan (256 threads x 16)
 #define GSR_DUP_TILE 64  // depth-sorted Gaussians per emission group (one wave)
 // Tile ranges: 4 waves x 16 rounds x 64 instances per block.
-#define GSR_RANGE_TILE 4096
+#define GSR_RANGE_TILE 16384
 
 // Rasterizer constants of the reference algorithm ([EXT] graphdeco
 // cuda_rasterizer/forward.cu + auxiliary.h).
