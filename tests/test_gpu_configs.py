@@ -269,26 +269,24 @@ def test_backward_view_groups_bitwise(monkeypatch):
         assert np.array_equal(one["g_means2D"][v], split["g_means2D"][v])
 
 
-@pytest.mark.parametrize("case", ["colors-one-group", "colors-six-groups", "sh3-one-view", "sh3-six-groups"])
+@pytest.mark.parametrize("case", ["colors-one-group", "colors-six-groups", "colors-one-view"])
 def test_gauss_fused_bitwise(case, monkeypatch):
     """The per-Gaussian backward fused into one kernel (k_gauss_fused: one thread per Gaussian walks the views,
-    no per-(view, Gaussian) records) — without SH (precomputed colours: the SuGaR renderers), and with SH for
-    one view per launch (the per-view drop-in path; six groups of one view continue the sums) — gives bitwise
-    the gradients of the split kernels (GSR_GAUSS_FUSED=0: k_view_grad + k_gauss_accum)."""
-    scene = gs.make_scene(20_000, sh_degree=0 if case.startswith("colors") else 3, seed=33)
-    if case.startswith("colors"):
-        scene = dict(scene, colors_precomp=(scene["shs"][:, 0, :] * np.float32(gs.C0) +
-                                            np.float32(0.5)).astype(np.float32))
-        scene.pop("shs")
-    nv = 1 if case == "sh3-one-view" else 6
+    no per-(view, Gaussian) records; launches without SH — precomputed colours, the SuGaR renderers — as one
+    group, as six groups of one view that continue the sums, and as one view) gives bitwise the gradients of
+    the split kernels (GSR_GAUSS_FUSED=0: k_view_grad + k_gauss_accum)."""
+    scene = gs.make_scene(20_000, sh_degree=0, seed=33)
+    scene = dict(scene, colors_precomp=(scene["shs"][:, 0, :] * np.float32(gs.C0) +
+                                        np.float32(0.5)).astype(np.float32))
+    scene.pop("shs")
+    nv = 1 if case == "colors-one-view" else 6
     cams = [make_camera(192, 160, elevation=5.0 * i, azimuth=60.0 * i) for i in range(nv)]
     ups = [gs.upstream_grads(160, 192, seed=90 + v) for v in range(nv)]
     budget = 1 if case.endswith("six-groups") else None
     fused = _batched_grads(scene, cams, ups, monkeypatch, budget=budget)
     monkeypatch.setenv("GSR_GAUSS_FUSED", "0")
     split = _batched_grads(scene, cams, ups, monkeypatch, budget=budget)
-    keys = ["g_means3D", "g_opacity", "g_scales", "g_rotations"] + (["g_colors"] if case.startswith("colors")
-                                                                    else ["g_sh"])
+    keys = ["g_means3D", "g_opacity", "g_scales", "g_rotations", "g_colors"]
     for k in keys:
         assert np.array_equal(fused[k], split[k]), k
     for v in range(nv):

@@ -259,13 +259,16 @@ def test_batched_views_match_per_view(nviews, monkeypatch):
         assert err <= 1e-5 * scale, f"{k}: {err} vs scale {scale}"
 
 
-@pytest.mark.parametrize("switch", ["fwd_kernel", "dispatch_order", "bwd_kernel"])
+@pytest.mark.parametrize("switch", ["fwd_kernel", "dispatch_order", "bwd_kernel", "tile_keys"])
 @pytest.mark.parametrize("kind", ["ball_composite", "sugar_two_colors"])
 def test_forward_kernels_bitwise(kind, switch, monkeypatch):
     """fwd_kernel: the one-wave-per-tile forward and the quadrant-wave forward (GSR_FWD_KERNEL) blend exactly
     the same candidates per pixel in the same order; dispatch_order: the blends' work-ordered
     dispatch and raster order (GSR_TILE_ORDER=raster) only change which workgroup starts first; bwd_kernel: the
-    backward blend as one wave per tile or as four lockstep quadrant waves (GSR_BWD_KERNEL).  Every
+    backward blend as one wave per tile or as four lockstep quadrant waves (GSR_BWD_KERNEL); tile_keys: packed
+    (tile, Gaussian) keys vs keys + values with the quadrant masks k_emit writes (the quadrant-wave forward
+    then gathers only its quadrant's candidates) and without them (GSR_TILE_KEYS; large sets take the
+    unpacked layout by themselves).  Every
     output — colour, depth, alpha, the composite, the second colour set, radii — and every gradient (the
     backward reads the forward's per-pixel state) must be bitwise equal."""
     import torch
@@ -295,7 +298,12 @@ def test_forward_kernels_bitwise(kind, switch, monkeypatch):
             monkeypatch.setenv("GSR_BWD_SPLIT", "0")
             monkeypatch.setenv("GSR_BWD_KERNEL", "tile" if kernel.startswith("tile") else "quadrant")
             # (hit lists: one or two waves per tile, GSR_BWD_TW_WAVES)
-            monkeypatch.setenv("GSR_BWD_TW_WAVES", "1" if kernel == "tile1" else "2")
+            monkeypatch.setenv("GSR_BWD_TW_WAVES", "2" if kernel == "tile2" else "1")
+        elif switch == "tile_keys":
+            if kernel == "tile":
+                monkeypatch.delenv("GSR_TILE_KEYS", raising=False)
+            else:
+                monkeypatch.setenv("GSR_TILE_KEYS", "plain" if kernel == "plain" else "unpacked")
         elif kernel == "tile":
             monkeypatch.delenv("GSR_TILE_ORDER", raising=False)
         else:
@@ -324,6 +332,9 @@ def test_forward_kernels_bitwise(kind, switch, monkeypatch):
     tile, quad = run("tile"), run("quadrant")
     for i, (x, y) in enumerate(zip(tile, quad)):
         assert torch.equal(x, y), f"output {i} differs: {float((x.double() - y.double()).abs().max())}"
+    if switch == "tile_keys":
+        for i, (x, y) in enumerate(zip(run("plain"), quad)):
+            assert torch.equal(x, y), f"plain keys: output {i} differs: {float((x.double() - y.double()).abs().max())}"
     if switch == "bwd_kernel" and kind == "sugar_two_colors":
-        for i, (x, y) in enumerate(zip(run("tile1"), quad)):
-            assert torch.equal(x, y), f"one wave: output {i} differs: {float((x.double() - y.double()).abs().max())}"
+        for i, (x, y) in enumerate(zip(run("tile2"), quad)):
+            assert torch.equal(x, y), f"two waves: output {i} differs: {float((x.double() - y.double()).abs().max())}"

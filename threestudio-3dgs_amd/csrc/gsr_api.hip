@@ -521,10 +521,10 @@ static int set_render(int V, int P, const int* K, int width, int height, const f
     PhaseScope ps(GSR_PHASE_BINNING, s);
     GSR_HIP_CHECK(hipMemsetAsync(img.ranges, 0, sizeof(uint2) * (size_t)V * gx * gy, s));
     if (total > 0) {
-      launch_emit(V, P, width, g, inst, tp.gbits, b.key[0], b.val[0], s);
+      launch_emit(V, P, width, g, inst, tp, b.key[0], b.val[0], s);
       const int res = seg_sort(b.key, b.val, false, inst, tp.gbits, tp.tile_bits, b.sort_counts, b.sort_totals, s);
       if (res != tres) return fail(GSR_EHIP, "%s", "internal: tile sort buffer");
-      launch_tile_ranges(inst, gx * gy, tp.gbits, b.key[res], img.ranges, s);
+      launch_tile_ranges(inst, gx * gy, tp, b.key[res], img.ranges, s);
     }
     launch_tile_order(V, gx, gy, img.ranges, img.order, s);  // always written: the backward may use it
   }
@@ -544,6 +544,7 @@ static int set_render(int V, int P, const int* K, int width, int height, const f
     rs.split_items = img.split_items;
     rs.split_cap = img.split_cap;
     rs.split_extra = split_extra(V, (size_t)gx * gy);
+    rs.qkeys = tp.qmask ? b.key[tres] : nullptr;
     rs.V = V;
     rs.v0 = 0;
     rs.P = P;
@@ -679,6 +680,7 @@ static int set_backward(int V, int P, int degree, int M, const int* K, int width
     rs.split_items = img.split_items;
     rs.split_cap = img.split_cap;
     rs.split_extra = split_extra(V, (size_t)gx * gy);
+    rs.qkeys = tp.qmask ? b.key[tres] : nullptr;
     rs.V = g1 - g0;
     rs.v0 = g0;
     rs.P = P;

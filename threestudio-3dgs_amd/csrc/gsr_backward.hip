@@ -649,10 +649,9 @@ __global__ __launch_bounds__(256) void k_gauss_accum(GaussBackwardArgs a, AccumA
 // order as k_view_grad + k_gauss_accum: bitwise the same gradients (up to the sign of zero sums).  Lanes of a
 // wave walk the same view at a time: the camera comes through scalar loads; a view's record / row slot of
 // consecutive Gaussians are consecutive (coalesced); the next reached view's are loaded one view ahead.
-// SH (one view per launch only: the per-view drop-in path, or a set's last single view): the view's SH
-// backward follows its chain rule directly (no accumulators across views; the SH row read from HBM), as
-// k_gauss_accum does for that view.
-template <bool TWO, bool SH>
+// With SH coefficients the two-kernel path runs: a fused SH variant (one thread per Gaussian reading and writing
+// its 48 coefficients) measured 0.2 ms/view slower on the per-view path (profiles/r04/fused_ab.txt).
+template <bool TWO>
 __global__ __launch_bounds__(256) void k_gauss_fused(GaussBackwardArgs a, ViewGradArgs va, AccumArgs b) {
   const int idx = a.g0 + blockIdx.x * 256 + threadIdx.x;
   const bool valid = idx < a.g1;
@@ -663,16 +662,6 @@ __global__ __launch_bounds__(256) void k_gauss_fused(GaussBackwardArgs a, ViewGr
   float dcov[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
   float dop = 0.f, dcr = 0.f, dcg = 0.f, dcb = 0.f;
   float d2[3] = {0.f, 0.f, 0.f};
-  const int F = SH ? 3 * a.M : 0;
-  float dsh[SH ? 48 : 1];
-#pragma unroll
-  for (int k = 0; k < (SH ? 48 : 1); ++k) dsh[k] = 0.f;
-  if (SH && valid && acc) {
-    const float* prev = a.dL_dsh + (size_t)idx * F;
-#pragma unroll
-    for (int k = 0; k < 48; ++k)
-      if (k < F) dsh[k % (SH ? 48 : 1)] = prev[k];
-  }
   if (valid && acc) {
     // continue the earlier groups' sums in place (same summation order as one group)
     dmean = make_float3(a.dL_dmeans3D[3 * idx], a.dL_dmeans3D[3 * idx + 1], a.dL_dmeans3D[3 * idx + 2]);
@@ -768,28 +757,8 @@ __global__ __launch_bounds__(256) void k_gauss_fused(GaussBackwardArgs a, ViewGr
       d2[1] += r.dg2;
       d2[2] += r.db2;
     }
-    if (SH && ((r.dcr != 0.f) | (r.dcg != 0.f) | (r.dcbl != 0.f))) {
-      // k_gauss_accum's SH backward of this view (colour gradient masked by the forward's clamp flags)
-      const uint32_t cl = gr.d.w;
-      const float3 dRGB = make_float3((cl & 1u) ? 0.f : r.dcr, (cl & 2u) ? 0.f : r.dcg, (cl & 4u) ? 0.f : r.dcbl);
-      float shv[48];
-      const float4* row4 = reinterpret_cast<const float4*>(a.shs + (size_t)ix * F);
-#pragma unroll
-      for (int c = 0; c < 12; ++c) {
-        const float4 q = 4 * c < F ? row4[c] : make_float4(0.f, 0.f, 0.f, 0.f);
-        shv[4 * c] = q.x, shv[4 * c + 1] = q.y, shv[4 * c + 2] = q.z, shv[4 * c + 3] = q.w;
-      }
-      const float cpos[3] = {((cfptr)b.campos[vl])[0], ((cfptr)b.campos[vl])[1], ((cfptr)b.campos[vl])[2]};
-      sh_backward(a.deg, a.M, shv, *reinterpret_cast<float(*)[48]>(dsh), dRGB, mean, cpos, dmean);
-    }
   }
   if (!valid) return;
-  if (SH) {
-    float* dst = a.dL_dsh + (size_t)idx * F;
-#pragma unroll
-    for (int k = 0; k < 48; ++k)
-      if (k < F) dst[k] = dsh[k % (SH ? 48 : 1)];
-  }
   a.dL_dmeans3D[3 * idx] = dmean.x;
   a.dL_dmeans3D[3 * idx + 1] = dmean.y;
   a.dL_dmeans3D[3 * idx + 2] = dmean.z;
@@ -816,10 +785,9 @@ __global__ __launch_bounds__(256) void k_gauss_fused(GaussBackwardArgs a, ViewGr
   }
 }
 
-// the fused per-Gaussian backward for launches without SH, or with SH and one view (GSR_GAUSS_FUSED=0: the
-// split kernels, A/B)
-static bool gauss_fused_on(const GaussBackwardArgs& a, int V) {
-  if (a.shs != nullptr && a.M > 0 && (V != 1 || 3 * a.M > 48)) return false;
+// the fused per-Gaussian backward for launches without SH (GSR_GAUSS_FUSED=0: the split kernels, A/B)
+static bool gauss_fused_on(const GaussBackwardArgs& a) {
+  if (a.shs != nullptr && a.M > 0) return false;
   const char* e = getenv("GSR_GAUSS_FUSED");
   return !(e != nullptr && strcmp(e, "0") == 0);
 }
@@ -830,10 +798,8 @@ static bool gauss_fused_on(const GaussBackwardArgs& a, int V) {
 void launch_gauss_backward(const GaussBackwardArgs& a, ViewGradArgs va, const AccumArgs& b, hipStream_t stream) {
   const int n = a.g1 - a.g0;
   if (n <= 0 || va.V <= 0) return;
-  if (gauss_fused_on(a, va.V)) {
-    const bool sh = a.shs != nullptr && a.M > 0;
-    auto kern = b.dcolors2 ? (sh ? k_gauss_fused<true, true> : k_gauss_fused<true, false>)
-                           : (sh ? k_gauss_fused<false, true> : k_gauss_fused<false, false>);
+  if (gauss_fused_on(a)) {
+    auto kern = b.dcolors2 ? k_gauss_fused<true> : k_gauss_fused<false>;
     hipLaunchKernelGGL(kern, dim3(div_up(n, 256)), dim3(256), 0, stream, a, va, b);
     return;
   }

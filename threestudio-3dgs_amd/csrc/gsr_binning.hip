@@ -204,11 +204,17 @@ struct EmitLDS {
   uint32_t rk[64];              // per row of the chunk: its first kept position (chunk-relative)
   uint32_t rtile[64];           // per row of the chunk: tile id of its first kept tile
   uint32_t rgi[64];             // per row of the chunk: the Gaussian
+  uint32_t rx0[64];             // per row of the chunk (QM): its first kept tile column
+  uint2 rq[64];                 // per row of the chunk (QM): span_quads of its upper and lower 8-pixel band
   uint32_t kown[64];            // kept position -> 1 + owning row (marks)
 };
 
 #define GSR_EMIT_GROUPS 2  // consecutive 64-Gaussian groups per wave (the next group's gathers prefetched)
 
+// QM (unpacked keys): each key also carries the instance's quadrant mask (GSR_QMASK_SHIFT): per row the
+// quadrant-column ranges of its two 8-pixel bands (span_quads, the span_row bound at half the tile size), per
+// instance four integer compares.
+template <bool QM>
 __global__ __launch_bounds__(64) void k_emit(int P, int nbe, int grid_x, GeomState g, SegInfo inst, int gbits,
                                              uint32_t* __restrict__ keys, uint32_t* __restrict__ vals) {
   const uint32_t* __restrict__ order = g.sorted_dval();
@@ -281,6 +287,11 @@ __global__ __launch_bounds__(64) void k_emit(int P, int nbe, int grid_x, GeomSta
         kc = (uint32_t)(t1 - t0);
         tile0 = (uint32_t)row * (uint32_t)grid_x + (uint32_t)t0;
         rg = s.gi[ow];
+        if (QM) {
+          const float v1 = s.sp[ow].py - (float)(row * GSR_TILE_Y);
+          s.rx0[lane] = (uint32_t)t0;
+          s.rq[lane] = make_uint2(span_quads(s.sp[ow], v1), span_quads(s.sp[ow], v1 - 8.0f));
+        }
       }
       const uint32_t kincl = wave_incl_sum_dpp(kc);
       const uint32_t kstart = kincl - kc;
@@ -301,7 +312,12 @@ __global__ __launch_bounds__(64) void k_emit(int P, int nbe, int grid_x, GeomSta
           const uint32_t rr = kw1 - 1u;
           const uint32_t tile = s.rtile[rr] + (j - s.rk[rr]);
           const uint32_t gv = s.rgi[rr];
-          kout[kbase + j] = vout ? tile : ((tile << gbits) | gv);
+          uint32_t qm = 0u;
+          if (QM) {
+            const uint2 rq = s.rq[rr];
+            qm = quads_of_tile(rq.x, rq.y, (int)(s.rx0[rr] + (j - s.rk[rr])));
+          }
+          kout[kbase + j] = vout ? (QM ? tile | qm << GSR_QMASK_SHIFT : tile) : ((tile << gbits) | gv);
           if (vout) vout[kbase + j] = gv;
         }
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // kown[] is rewritten by the next chunk
@@ -320,7 +336,7 @@ __global__ __launch_bounds__(64) void k_emit(int P, int nbe, int grid_x, GeomSta
 // A block covers GSR_RANGE_TILE instances: each wave GSR_RANGE_CHUNKS consecutive chunks of 64 x
 // GSR_RANGE_ROUNDS (fewer, longer-lived workgroups: the launch was bound by workgroup dispatch, 2.6 TB/s).
 #define GSR_RANGE_CHUNKS (GSR_RANGE_TILE / (4 * 64 * GSR_RANGE_ROUNDS))
-__global__ __launch_bounds__(256) void k_tile_ranges(SegInfo inst, int n_tiles, int gbits,
+__global__ __launch_bounds__(256) void k_tile_ranges(SegInfo inst, int n_tiles, int gbits, uint32_t tmask,
                                                      const uint32_t* __restrict__ keys,
                                                      uint2* __restrict__ ranges) {
   uint32_t lb;
@@ -337,11 +353,11 @@ __global__ __launch_bounds__(256) void k_tile_ranges(SegInfo inst, int n_tiles, 
 #pragma unroll
   for (int r = 0; r < GSR_RANGE_ROUNDS; ++r) {
     const uint32_t i = base + 64u * r + lane;
-    t[r] = i < K ? kv[i] >> gbits : 0xFFFFFFFFu;
+    t[r] = i < K ? (kv[i] >> gbits) & tmask : 0xFFFFFFFFu;
   }
-  const uint32_t before = base > 0 ? kv[base - 1] >> gbits : 0xFFFFFFFFu;
+  const uint32_t before = base > 0 ? (kv[base - 1] >> gbits) & tmask : 0xFFFFFFFFu;
   const uint32_t e = base + 64u * GSR_RANGE_ROUNDS;
-  const uint32_t after = e < K ? kv[e] >> gbits : 0xFFFFFFFFu;
+  const uint32_t after = e < K ? (kv[e] >> gbits) & tmask : 0xFFFFFFFFu;
 #pragma unroll
   for (int r = 0; r < GSR_RANGE_ROUNDS; ++r) {
     const uint32_t p = base + 64u * r + lane;
@@ -372,18 +388,25 @@ void launch_binning_counts(int V, int P, const GeomState& g, hipStream_t stream)
   hipLaunchKernelGGL(k_inst_scan, dim3(V), dim3(1024), 0, stream, P > 0 ? nbe : 0, g);
 }
 
-void launch_emit(int V, int P, int W, const GeomState& g, const SegInfo& inst, int gbits, uint32_t* keys,
+void launch_emit(int V, int P, int W, const GeomState& g, const SegInfo& inst, const TilePack& tp, uint32_t* keys,
                  uint32_t* vals, hipStream_t stream) {
   if (V <= 0 || P <= 0) return;
   const int nbe = GeomState::dup_blocks(P);
-  hipLaunchKernelGGL(k_emit, dim3(V * div_up(nbe, GSR_EMIT_GROUPS)), dim3(64), 0, stream, P, nbe,
-                     div_up(W, GSR_TILE_X), g, inst, gbits, keys, vals);
+  const dim3 grid(V * div_up(nbe, GSR_EMIT_GROUPS));
+  if (tp.qmask)
+    hipLaunchKernelGGL(k_emit<true>, grid, dim3(64), 0, stream, P, nbe, div_up(W, GSR_TILE_X), g, inst, tp.gbits,
+                       keys, vals);
+  else
+    hipLaunchKernelGGL(k_emit<false>, grid, dim3(64), 0, stream, P, nbe, div_up(W, GSR_TILE_X), g, inst, tp.gbits,
+                       keys, vals);
 }
 
-void launch_tile_ranges(SegInfo inst, int n_tiles, int gbits, const uint32_t* keys, uint2* ranges, hipStream_t stream) {
+void launch_tile_ranges(SegInfo inst, int n_tiles, const TilePack& tp, const uint32_t* keys, uint2* ranges,
+                        hipStream_t stream) {
   seg_fill_blocks(inst, GSR_RANGE_TILE);
   if (inst.blk[inst.V] == 0) return;
-  hipLaunchKernelGGL(k_tile_ranges, dim3(inst.blk[inst.V]), dim3(256), 0, stream, inst, n_tiles, gbits, keys, ranges);
+  hipLaunchKernelGGL(k_tile_ranges, dim3(inst.blk[inst.V]), dim3(256), 0, stream, inst, n_tiles, tp.gbits, tp.tmask,
+                     keys, ranges);
 }
 
 // markVisible / checkFrustum of the reference (API completeness).

@@ -15,6 +15,8 @@
 #error "GSR_EXP_* experiment switches build only through `make exp` (a diagnostic library, not libgsr_hip.so)"
 #endif
 #include <stddef.h>
+#include <stdlib.h>
+#include <string.h>
 #include <stdint.h>
 
 #define GSR_TILE_X 16
@@ -76,19 +78,31 @@ static inline int tile_key_bits(int W, int H) {
 // Instance key layout.  When the Gaussian index and the tile id fit one 32-bit word together
 // (1M Gaussians at 1024^2: 20 + 12 bits) the tile sort moves packed keys (tile << gbits | Gaussian)
 // and no values: half the bytes of every binning pass.  Otherwise keys = tile, values = Gaussian.
+// Unpacked keys carry beside the tile id, in bits [GSR_QMASK_SHIFT, +4), the instance's 8x8 quadrant mask
+// (quadrant_hit of each quadrant, k_emit): the tile sort and k_tile_ranges look at the tile bits only, and the
+// quadrant-wave forward gathers the records of its own quadrant's candidates only.
+#define GSR_QMASK_SHIFT 28
 struct TilePack {
   bool packed;
+  bool qmask;  // keys hold the quadrant masks (unpacked)
   int gbits, tile_bits;
   uint32_t gmask;  // sorted entry -> Gaussian
+  uint32_t tmask;  // key >> gbits -> tile id
 };
 static inline TilePack tile_pack(int P, int W, int H) {
+  // GSR_TILE_KEYS (parity tests): "unpacked" = keys + values at any size (keys with quadrant masks), "plain" =
+  // the same without masks; unset = packed whenever both fit one word
+  const char* e = getenv("GSR_TILE_KEYS");
+  const bool force = e != nullptr && (strcmp(e, "unpacked") == 0 || strcmp(e, "plain") == 0);
   TilePack t;
   t.tile_bits = tile_key_bits(W, H);
   int gb = 1;
   while (gb < 32 && (1ll << gb) < (long long)P) ++gb;
-  t.packed = gb + t.tile_bits <= 32;
+  t.packed = gb + t.tile_bits <= 32 && !force;
   t.gbits = t.packed ? gb : 0;
   t.gmask = t.packed ? (uint32_t)((1ull << gb) - 1ull) : 0xFFFFFFFFu;
+  t.qmask = !t.packed && t.tile_bits <= GSR_QMASK_SHIFT && !(e != nullptr && strcmp(e, "plain") == 0);
+  t.tmask = t.tile_bits >= 32 ? 0xFFFFFFFFu : (uint32_t)((1ull << t.tile_bits) - 1ull);
   return t;
 }
 
@@ -472,6 +486,40 @@ __device__ __forceinline__ void span_row(const SpanPrep& p, int ty, int xmin, in
   const int a0 = (int)ceilf(lo), a1 = (int)floorf(hi) + 1;
   tx0 = max(xmin, min(a0, xmax));
   tx1 = max(tx0, min(a1, xmax));
+}
+// The same bound on an 8-pixel band (pixel rows y with mean_y - y in [v1 - 7, v1]) at 8-pixel column
+// granularity: the 8x8 quadrant columns c (pixels 8c .. 8c + 7) of the band that can hold a pixel with
+// alpha >= 1/255, as c0 | c1 << 16 for [c0, c1) clamped to [0, 0x7fff] (k_emit's quadrant masks: two bands per
+// tile row).  Same derivation and margins as span_row, so never tighter than a quadrant some pixel blends.
+__device__ __forceinline__ uint32_t span_quads(const SpanPrep& p, float v1) {
+#pragma clang fp contract(off)
+  if (p.mode != 2) return p.mode == 1 ? 0x7fffu << 16 : 0u;
+  const float v0 = v1 - 7.0f;
+  float umax = -3.0e38f, umin = 3.0e38f;
+  if (-p.ve >= v0 && -p.ve <= v1) umax = p.ue;
+  if (p.ve >= v0 && p.ve <= v1) umin = -p.ue;
+  const float e0 = p.thra - p.D * (v0 * v0), e1 = p.thra - p.D * (v1 * v1);
+  if (e0 >= 0.0f) {
+    const float r = __builtin_amdgcn_sqrtf(e0), m = -p.b * v0;
+    umax = fmaxf(umax, (m + r) * p.ia);
+    umin = fminf(umin, (m - r) * p.ia);
+  }
+  if (e1 >= 0.0f) {
+    const float r = __builtin_amdgcn_sqrtf(e1), m = -p.b * v1;
+    umax = fmaxf(umax, (m + r) * p.ia);
+    umin = fminf(umin, (m - r) * p.ia);
+  }
+  if (!(umax >= umin)) return 0u;
+  const float lo = fminf(fmaxf((p.px - 7.0f - umax - 0.05f) * 0.125f, -1.0f), 32767.0f);
+  const float hi = fminf(fmaxf((p.px - umin + 0.05f) * 0.125f, -1.0f), 32767.0f);
+  const int c0 = max(0, (int)ceilf(lo)), c1 = max(c0, min((int)floorf(hi) + 1, 0x7fff));
+  return (uint32_t)c0 | (uint32_t)c1 << 16;
+}
+// quadrant mask of tile column tx from its row's two band ranges (span_quads of the upper / lower band)
+__device__ __forceinline__ uint32_t quads_of_tile(uint32_t up, uint32_t dn, int tx) {
+  const uint32_t c = 2u * (uint32_t)tx;
+  auto in = [](uint32_t r, uint32_t x) { return x >= (r & 0xffffu) && x < (r >> 16); };
+  return (in(up, c) ? 1u : 0u) | (in(up, c + 1u) ? 2u : 0u) | (in(dn, c) ? 4u : 0u) | (in(dn, c + 1u) ? 8u : 0u);
 }
 
 }  // namespace gsr

@@ -29,15 +29,46 @@ void launch_preprocess(const PreprocessArgs& a, const SetCams& cams, const GeomS
 void launch_binning_counts(int V, int P, const GeomState& g, hipStream_t stream);
 // vals == nullptr: packed keys (tile << gbits | Gaussian)
 // dkeys = the depth sort's key buffer (sorted depth keys; culled = ~0)
-void launch_emit(int V, int P, int W, const GeomState& g, const SegInfo& inst, int gbits, uint32_t* keys,
+void launch_emit(int V, int P, int W, const GeomState& g, const SegInfo& inst, const TilePack& tp, uint32_t* keys,
                  uint32_t* vals, hipStream_t stream);
-void launch_tile_ranges(SegInfo inst, int n_tiles, int gbits, const uint32_t* keys, uint2* ranges, hipStream_t stream);
+void launch_tile_ranges(SegInfo inst, int n_tiles, const TilePack& tp, const uint32_t* keys, uint2* ranges,
+                        hipStream_t stream);
 void launch_mark_visible(int P, const float* means3D, const float* view, const float* proj,
                          uint8_t* present, hipStream_t stream);
 
 // Tile blend — gsr_render.hip.  A launch covers views v0 .. v0+V-1 of a set (geom / image arrays
 // indexed by v0 + v); sorted_gauss = the tile sort's value buffer; inst_start[v] = the view's
 // first instance in it; row_start[v] = the view's first gradient row slot in the backward scratch.
+// Can some pixel centre of the 8x8 quadrant with origin (qx, qy) reach alpha >= 1/255 for this
+// Gaussian?  alpha = o exp(-q/2), q = a dx^2 + 2 b dx dy + c dy^2 (dx = mean - pixel), so the pair
+// can blend only if q <= 2 ln(255 o).  The test takes the exact minimum of q over the continuous
+// rectangle spanned by the quadrant's pixel centres (<= the minimum over the pixels themselves) and
+// compares it with a padded threshold, so it never drops a pair the reference would blend; for
+// rotated, elongated footprints it is much tighter than the ellipse's bounding box.
+__device__ __forceinline__ float quad_form(float a, float b, float c, float u, float v) {
+  return fmaf(a * u, u, fmaf(2.0f * b * u, v, c * v * v));
+}
+__device__ __forceinline__ bool quadrant_hit(const float4 r0, const float4 r1, float qx, float qy) {
+  const float o = r1.y;
+  if (!(o >= GSR_ALPHA_MIN * 0.9999f)) return false;
+  const float a = r0.z, b = r0.w, c = r1.x;
+  if (!(a > 0.0f && c > 0.0f && a * c - b * b > 0.0f)) return true;
+  const float tau = fmaxf(0.0f, __logf(255.0f * o));
+  const float thr = 2.0f * (tau * 1.002f + 2e-3f);
+  // dx ranges over [u0, u1], dy over [v0, v1]
+  const float u1 = r0.x - qx, u0 = u1 - 7.0f;
+  const float v1 = r0.y - qy, v0 = v1 - 7.0f;
+  if (u0 <= 0.0f && u1 >= 0.0f && v0 <= 0.0f && v1 >= 0.0f) return true;
+  const float ia = 1.0f / a, ic = 1.0f / c;
+  // edges u = u0, u1: best v = clamp(-b u / c); edges v = v0, v1: best u = clamp(-b v / a)
+  const float q0 = quad_form(a, b, c, u0, fminf(fmaxf(-b * u0 * ic, v0), v1));
+  const float q1 = quad_form(a, b, c, u1, fminf(fmaxf(-b * u1 * ic, v0), v1));
+  const float q2 = quad_form(a, b, c, fminf(fmaxf(-b * v0 * ia, u0), u1), v0);
+  const float q3 = quad_form(a, b, c, fminf(fmaxf(-b * v1 * ia, u0), u1), v1);
+  const float qmin = fminf(fminf(q0, q1), fminf(q2, q3));
+  return qmin * 0.998f <= thr;
+}
+
 struct RenderSet {
   int V, v0, P, W, H, gx, gy;
   uint32_t gmask;  // sorted entry -> Gaussian (TilePack)
@@ -68,6 +99,9 @@ struct RenderSet {
   uint32_t* split_items;  // with ckpt: the later chunks' backward items (ImageState::split_items)
   uint32_t* split_cap;    // with ckpt: ImageState::split_cap
   int split_extra;        // with ckpt: split_extra(the set's V, tiles)
+  // the sorted keys when they carry the quadrant masks (TilePack::qmask; indexed like the sorted Gaussians),
+  // else null
+  const uint32_t* qkeys;
 };
 // backward tile splitting on for a set of V views (split_fits) whose forward takes the quadrant-wave kernel
 // (GSR_BWD_SPLIT=0 turns it off); instances = the set's K total

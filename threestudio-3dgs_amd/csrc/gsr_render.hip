@@ -103,12 +103,6 @@ __device__ __forceinline__ void tile_pixel(int t, int& lx, int& ly) {
   ly = ((w >> 1) << 3) | (l >> 3);
 }
 
-// Can some pixel centre of the 8x8 quadrant with origin (qx, qy) reach alpha >= 1/255 for this
-// Gaussian?  alpha = o exp(-q/2), q = a dx^2 + 2 b dx dy + c dy^2 (dx = mean - pixel), so the pair
-// can blend only if q <= 2 ln(255 o).  The test takes the exact minimum of q over the continuous
-// rectangle spanned by the quadrant's pixel centres (<= the minimum over the pixels themselves) and
-// compares it with a padded threshold, so it never drops a pair the reference would blend; for
-// rotated, elongated footprints it is much tighter than the ellipse's bounding box.
 // per-lane select by a wave mask: one v_cndmask_b32 (keeps the replay's state updates branch-free;
 // left to itself the compiler turns a run of selects on one condition into an exec-masked branch)
 __device__ __forceinline__ float vsel(unsigned long long m, float if_set, float if_clear) {
@@ -121,30 +115,6 @@ __device__ __forceinline__ float vsel(unsigned long long m, float if_set, float 
 // variant forms the same bits, independent of how the compiler would contract the expression)
 __device__ __forceinline__ float bg_dot3(const float* bg, float d0, float d1, float d2) {
   return fmaf(bg[2], d2, fmaf(bg[1], d1, bg[0] * d0));
-}
-
-__device__ __forceinline__ float quad_form(float a, float b, float c, float u, float v) {
-  return fmaf(a * u, u, fmaf(2.0f * b * u, v, c * v * v));
-}
-__device__ __forceinline__ bool quadrant_hit(const float4 r0, const float4 r1, float qx, float qy) {
-  const float o = r1.y;
-  if (!(o >= GSR_ALPHA_MIN * 0.9999f)) return false;
-  const float a = r0.z, b = r0.w, c = r1.x;
-  if (!(a > 0.0f && c > 0.0f && a * c - b * b > 0.0f)) return true;
-  const float tau = fmaxf(0.0f, __logf(255.0f * o));
-  const float thr = 2.0f * (tau * 1.002f + 2e-3f);
-  // dx ranges over [u0, u1], dy over [v0, v1]
-  const float u1 = r0.x - qx, u0 = u1 - 7.0f;
-  const float v1 = r0.y - qy, v0 = v1 - 7.0f;
-  if (u0 <= 0.0f && u1 >= 0.0f && v0 <= 0.0f && v1 >= 0.0f) return true;
-  const float ia = 1.0f / a, ic = 1.0f / c;
-  // edges u = u0, u1: best v = clamp(-b u / c); edges v = v0, v1: best u = clamp(-b v / a)
-  const float q0 = quad_form(a, b, c, u0, fminf(fmaxf(-b * u0 * ic, v0), v1));
-  const float q1 = quad_form(a, b, c, u1, fminf(fmaxf(-b * u1 * ic, v0), v1));
-  const float q2 = quad_form(a, b, c, fminf(fmaxf(-b * v0 * ia, u0), u1), v0);
-  const float q3 = quad_form(a, b, c, fminf(fmaxf(-b * v1 * ia, u0), u1), v1);
-  const float qmin = fminf(fminf(q0, q1), fminf(q2, q3));
-  return qmin * 0.998f <= thr;
 }
 
 // Forward: one wave (64 threads) per 8x8 quadrant of a 16x16 tile.  The wave streams the tile's
@@ -207,7 +177,13 @@ __global__ __launch_bounds__(64) void k_render_fwd(RenderSet rs,
   float4 n0 = zero4, n1 = zero4, n2 = zero4, n3 = zero4;
   uint32_t gi_next = 0u;
   const float* col2 = rs.col2;
-  if (lane < n) {
+  // quadrant masks in the keys (TilePack::qmask): the keep decision comes with the index, and only this
+  // quadrant's candidates are gathered (k_emit ran the same quadrant_hit)
+  const uint32_t* qkeys = rs.qkeys ? rs.qkeys + rs.inst_start[v] + range.x : nullptr;
+  const int qsh = GSR_QMASK_SHIFT + q;
+  bool kn = false, kn_next = false;  // the keep bits of the batch in n0..n3 / of gi_next
+  if (lane < n) kn = qkeys == nullptr || ((qkeys[lane] >> qsh) & 1u);
+  if (kn) {
     const uint32_t g0 = sorted_gauss[range.x + lane] & gmask;
     n0 = rec[g0].a;
     n1 = rec[g0].b;
@@ -220,7 +196,10 @@ __global__ __launch_bounds__(64) void k_render_fwd(RenderSet rs,
     if (C2) n3 = make_float4(col2[3 * g0], col2[3 * g0 + 1], col2[3 * g0 + 2], 0.f);
 #endif
   }
-  if (64 + lane < n) gi_next = sorted_gauss[range.x + 64 + lane] & gmask;
+  if (64 + lane < n) {
+    gi_next = sorted_gauss[range.x + 64 + lane] & gmask;
+    kn_next = qkeys == nullptr || ((qkeys[64 + lane] >> qsh) & 1u);
+  }
   // split backward: T at each chunk boundary the walk reaches, and each chunk's own colour / depth sums
   float* const ckpt = CK ? rs.ckpt + ckpt_offset((size_t)(rs.v0 + v), (size_t)rs.gx * rs.gy, tile, 0) : nullptr;
   const int cpix = 64 * q + lane;
@@ -238,7 +217,9 @@ __global__ __launch_bounds__(64) void k_render_fwd(RenderSet rs,
     }
     const int i = base + lane;
     const float4 r0 = n0, r1 = n1, r2 = n2, r3 = n3;
-    if (base + 64 + lane < n) {
+    const bool kc = kn;
+    kn = base + 64 + lane < n && kn_next;
+    if (kn) {
       n0 = rec[gi_next].a;
       n1 = rec[gi_next].b;
 #ifndef GSR_EXP_FWD_NOC
@@ -250,9 +231,12 @@ __global__ __launch_bounds__(64) void k_render_fwd(RenderSet rs,
       if (C2) n3 = make_float4(col2[3 * gi_next], col2[3 * gi_next + 1], col2[3 * gi_next + 2], 0.f);
 #endif
     }
-    if (base + 128 + lane < n) gi_next = sorted_gauss[range.x + base + 128 + lane] & gmask;
+    if (base + 128 + lane < n) {
+      gi_next = sorted_gauss[range.x + base + 128 + lane] & gmask;
+      kn_next = qkeys == nullptr || ((qkeys[base + 128 + lane] >> qsh) & 1u);
+    }
     bool keep = false;
-    if (i < n) keep = quadrant_hit(r0, r1, (float)qx0, (float)qy0);
+    if (i < n) keep = qkeys ? kc : quadrant_hit(r0, r1, (float)qx0, (float)qy0);
     const unsigned long long bal = __ballot(keep);
     const int cnt = __popcll(bal);
     if (keep) {
@@ -2190,10 +2174,12 @@ static bool bwd_hit_lists(bool two) {
 // GSR_BWD_KERNEL=quadrant.  Matrix-core sums (C3): the lockstep workgroup (the tile wave k_render_bwd_twm, with
 // GSR_BWD_KERNEL=tile, measured 0.098 -> 0.102 ms/view at C3, 0.104 -> 0.119 for 8-view sets:
 // profiles/r04/tile_wave_ab.txt).
-// waves per tile of the hit-list tile kernel (GSR_BWD_TW_WAVES=1|2)
+// waves per tile of the hit-list tile kernel (GSR_BWD_TW_WAVES=1|2): one (C5 render_bwd 0.3275 ms/view against
+// 0.3489 for two waves splitting the quadrants, whose per-batch barriers cost more than the overlap gains,
+// profiles/r04/tw_waves_ab.txt)
 static int bwd_tw_waves() {
   const char* e = getenv("GSR_BWD_TW_WAVES");
-  return e != nullptr && strcmp(e, "1") == 0 ? 1 : 2;
+  return e != nullptr && strcmp(e, "2") == 0 ? 2 : 1;
 }
 static bool bwd_tile_wave(bool hits) {
   const char* e = getenv("GSR_BWD_KERNEL");
