@@ -20,6 +20,10 @@
 #include "gsr_kernels.h"
 #include "gsr_wave.h"
 
+#ifndef GSR_BWD_OVERLAP
+#define GSR_BWD_OVERLAP 1  // replay steps of a full group scheduled together (k_render_bwd; 2 spills 4 VGPRs)
+#endif
+
 namespace gsr {
 
 // blockIdx -> (tile, quadrant).  Blocks b and b+8 share an XCD under round-robin dispatch (speed
@@ -1263,6 +1267,26 @@ __device__ __forceinline__ void bwd_tile(BwdLDS<TWO, HITS>& s, const RenderSet& 
 #endif
     for (int g0 = 0; g0 < cnt; g0 += GS) {
       const int gn = min(GS, cnt - g0);
+      if (!TWO && gn == GS) {
+        // a full group: the 8 replay steps without per-step branches, one basic block, so the independent
+        // per-candidate terms (staged-record reads, alpha, exp2, 1 / (1 - alpha)) of later candidates can be
+        // scheduled under earlier candidates' dependent updates (same operations, same order per pixel)
+        int jj[GS];
+#pragma unroll
+        for (int c = 0; c < GS; ++c) {
+          jj[c] = (int)__builtin_ctzll(rest);
+          rest &= rest - 1ull;
+        }
+#pragma unroll
+        for (int c = 0; c < GS; ++c) {
+          const float4 ca = s.s0[jj[c]], cb = s.s1[jj[c]], cc = s.s2[jj[c]];
+          float u, w;
+          replay(ca, cb, cc, u, w);
+          uw[16 * c + wa[c >> 2]] = u;
+          uw[16 * (c + 8) + wa[2 + (c >> 2)]] = w;
+          if ((c & (GSR_BWD_OVERLAP - 1)) == GSR_BWD_OVERLAP - 1) __builtin_amdgcn_sched_barrier(0);  // (VGPR budget)
+        }
+      } else {
       int j = (int)__builtin_ctzll(rest);
       float4 ca = s.s0[j], cb = s.s1[j], cc = s.s2[j];
       float4 cd2 = TWO ? s.s3[j] : zero4;
@@ -1296,6 +1320,7 @@ __device__ __forceinline__ void bwd_tile(BwdLDS<TWO, HITS>& s, const RenderSet& 
           cd2 = nd;
           j = jn;
         }
+      }
       }
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the wave reads its own lanes' rows
 #ifdef GSR_EXP_NOMFMA
@@ -1756,39 +1781,54 @@ __global__ __launch_bounds__(64 * NW) void k_render_bwd_tw(
       const float pxf = lxf + (float)((q & 1) * 8), pyf = lyf + (float)((q >> 1) * 8);
       int fill = 0;
       unsigned long long pend = 0ull, rest = kq;
-      int jc = (int)__builtin_ctzll(rest);
-      float4 ga = s0[jc], gb = s1[jc], gc = s2[jc];
-      float4 gd = TWO ? s3[jc] : zero4;
-      while (true) {
-        rest &= rest - 1ull;
-        const int jn = rest != 0ull ? (int)__builtin_ctzll(rest) : jc;
-        const float4 xa = s0[jn], xb = s1[jn], xc = s2[jn];
-        const float4 xd = TWO ? s3[jn] : zero4;
-        // the replay step of k_render_bwd (replay / replay2) on this quadrant's pixel
+      // the replay step of k_render_bwd (replay / replay2) on this quadrant's pixel, software-pipelined: the
+      // per-candidate terms that do not depend on the running state (alpha, G, 1 / (1 - alpha), the colour
+      // dots) of candidate k + 1 are formed while candidate k updates T, S, Sd, S2 — the same operations on the
+      // same values as the plain loop, so the same bits
+      struct Pre {
+        bool hit;
+        float a_eff, g_eff, oma, inv, cd, cd2, z;
+      };
+      auto pre = [&](const float4 ga, const float4 gb, const float4 gc, const float4 gd) {
+        Pre p;
         const uint32_t rel = __float_as_uint(gb.w);
         const float dx = ga.x - pxf, dy = ga.y - pyf;
         const float power2 = gauss_power2(ga.z, ga.w, gb.x, dx, dy);
         const float G = __builtin_amdgcn_exp2f(power2);
         const float alpha = fminf(GSR_ALPHA_MAX, gb.y * G);
-        const bool hit = rel < last[j] && power2 <= 0.0f && alpha >= GSR_ALPHA_MIN;
-        const float a_eff = hit ? alpha : 0.0f;
-        const float g_eff = hit ? G : 0.0f;
-        const float oma = 1.f - a_eff;
-        const float inv_1ma = fast_rcp(oma);
+        p.hit = rel < last[j] && power2 <= 0.0f && alpha >= GSR_ALPHA_MIN;
+        p.a_eff = p.hit ? alpha : 0.0f;
+        p.g_eff = p.hit ? G : 0.0f;
+        p.oma = 1.f - p.a_eff;
+        p.inv = fast_rcp(p.oma);
+        p.cd = fmaf(gc.x, dp0[j], fmaf(gc.y, dp1[j], fmaf(gc.z, dp2[j], dpa[j])));
+        p.cd2 = TWO ? fmaf(gd.x, e0[j], fmaf(gd.y, e1[j], gd.z * e2[j])) : 0.f;
+        p.z = gb.z;
+        return p;
+      };
+      int jc = (int)__builtin_ctzll(rest);
+      Pre pc = pre(s0[jc], s1[jc], s2[jc], TWO ? s3[jc] : zero4);
+      while (true) {
+        rest &= rest - 1ull;
+        const int jn = rest != 0ull ? (int)__builtin_ctzll(rest) : jc;
+        const float4 xa = s0[jn], xb = s1[jn], xc = s2[jn];
+        const float4 xd = TWO ? s3[jn] : zero4;
+        const bool hit = pc.hit;
+        const float a_eff = pc.a_eff, g_eff = pc.g_eff, oma = pc.oma, inv_1ma = pc.inv, cd = pc.cd;
         T[j] = T[j] * inv_1ma;
-        const float cd = fmaf(gc.x, dp0[j], fmaf(gc.y, dp1[j], fmaf(gc.z, dp2[j], dpa[j])));
         float u, u1 = 0.f;
         if (TWO) {
-          const float cd2 = fmaf(gd.x, e0[j], fmaf(gd.y, e1[j], gd.z * e2[j]));
-          u1 = g_eff * fmaf(T[j], fmaf(gb.z - Sd[j], dpd[j], cd - S[j]), inv_1ma * nbg[j]);
+          const float cd2 = pc.cd2;
+          u1 = g_eff * fmaf(T[j], fmaf(pc.z - Sd[j], dpd[j], cd - S[j]), inv_1ma * nbg[j]);
           u = fmaf(g_eff, fmaf(T[j], cd2 - S2[j], inv_1ma * nbg2[j]), u1);
           S2[j] = fmaf(a_eff, cd2, oma * S2[j]);
         } else {
-          u = g_eff * fmaf(T[j], fmaf(gb.z - Sd[j], dpd[j], cd - S[j]), inv_1ma * nbg[j]);
+          u = g_eff * fmaf(T[j], fmaf(pc.z - Sd[j], dpd[j], cd - S[j]), inv_1ma * nbg[j]);
         }
         const float w = a_eff * T[j];
         S[j] = fmaf(a_eff, cd, oma * S[j]);
-        Sd[j] = fmaf(a_eff, gb.z, oma * Sd[j]);
+        Sd[j] = fmaf(a_eff, pc.z, oma * Sd[j]);
+        const Pre pn = pre(xa, xb, xc, xd);  // (candidate k + 1: independent of the updates above)
         const unsigned long long hm = __ballot(hit);
         const int n = __popcll(hm);
         if (fill + n > GSR_HCAP_TW) {
@@ -1804,10 +1844,7 @@ __global__ __launch_bounds__(64 * NW) void k_render_bwd_tw(
         fill += n;
         pend |= 1ull << jc;
         if (rest == 0ull) break;
-        ga = xa;
-        gb = xb;
-        gc = xc;
-        gd = xd;
+        pc = pn;
         jc = jn;
       }
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
