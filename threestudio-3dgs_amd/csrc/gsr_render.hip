@@ -468,7 +468,6 @@ __global__ __launch_bounds__(64) void k_render_fwd_tile(RenderSet rs, const uint
                                                         uint32_t* __restrict__ quad_maxc) {
   __shared__ float4 s0[64], s1[64], s2[64];
   __shared__ float4 s3[C2 ? 64 : 1];
-  __shared__ uint32_t smask[64];
   int v, tile, q_unused;
   if (!block_map<4>(blockIdx.x, rs, v, tile, q_unused)) return;
   const int W = rs.W, H = rs.H, grid_x = rs.gx;
@@ -550,18 +549,45 @@ __global__ __launch_bounds__(64) void k_render_fwd_tile(RenderSet rs, const uint
     s1[lane] = make_float4(GSR_CONIC_K_AC * r1.x, r1.y, r1.z, __uint_as_float((uint32_t)(i + 1)));
     s2[lane] = r2;
     if (C2) s3[lane] = r3;
-    smask[lane] = m;
+    // per quadrant the batch's candidates whose mask has it (uniform, in scalar registers): the walk visits
+    // the set bits of their union in order, reading each quadrant's bit with scalar ops and the next
+    // candidate's staged record while the current one blends (no per-candidate LDS read of its mask)
+    unsigned long long qb[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) qb[q] = __ballot((m >> q) & 1u);
     __syncthreads();
-    const int cnt = min(64, n - base);
-    for (int k = 0; k < cnt; ++k) {
-      if ((k & 7) == 0) {
+    auto live = [&]() {
+      unsigned long long u = 0ull;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) u |= (qactive >> q) & 1u ? qb[q] : 0ull;
+      return u;
+    };
+    unsigned long long rest = live();
+    int k = rest != 0ull ? (int)__builtin_ctzll(rest) : 0;
+    float4 a = s0[k], b = s1[k], c = s2[k];
+    float4 e = C2 ? s3[k] : zero4;
+    for (int walked = 0; rest != 0ull; ++walked) {
+      if (walked > 0 && (walked & 7) == 0) {
+        // (finished quadrants leave the walk: they would blend nothing)
         qactive = active_mask();
         if (qactive == 0u) break;
+        rest &= live();
+        if (rest == 0ull) break;
+        const int kk = (int)__builtin_ctzll(rest);
+        if (kk != k) {
+          k = kk;
+          a = s0[k], b = s1[k], c = s2[k];
+          e = C2 ? s3[k] : zero4;
+        }
       }
-      const uint32_t mk = __builtin_amdgcn_readfirstlane(smask[k]) & qactive;
-      if (mk == 0u) continue;
-      const float4 a = s0[k], b = s1[k], c = s2[k];
-      const float4 e = C2 ? s3[k] : zero4;
+      rest &= rest - 1ull;
+      const int kn = rest != 0ull ? (int)__builtin_ctzll(rest) : k;
+      const float4 an = s0[kn], bn = s1[kn], cn = s2[kn];
+      const float4 en = C2 ? s3[kn] : zero4;
+      uint32_t mk = 0u;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) mk |= (uint32_t)((qb[q] >> k) & 1ull) << q;
+      mk &= qactive;
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
         if (mk & (1u << q)) {
@@ -592,6 +618,11 @@ __global__ __launch_bounds__(64) void k_render_fwd_tile(RenderSet rs, const uint
           done[q] = done[q] || term;
         }
       }
+      a = an;
+      b = bn;
+      c = cn;
+      e = en;
+      k = kn;
     }
     __syncthreads();
     qactive = active_mask();
