@@ -342,6 +342,70 @@ def test_c4_batch_single_vs_two_ranks(B, S, tmp_path):
         assert bool(z["same"]), f"rank {rank}: replicas differ after densification"
         assert int(z["P"]) == int(single["P"]) > C4_P
     _c4_oracle_views(single, B, S, check)
+    if B <= 8:
+        _c4_oracle_sums(single, B, S)
+
+
+def _c4_oracle_sums(single, B, S):
+    """The batch's summed parameter gradients (the ones the optimizer steps on, all B views) against the fp64 /
+    fp32 oracle summed over the same views: the oracle's per-view gradients w.r.t. the activated parameters
+    (means3D, SH, opacity, scales, rotations) summed over views in fp64 (and in fp32 for the allowance), then
+    taken through the model's activations in fp64 — sigmoid (opacity), exp (scaling), normalize (rotation) —
+    against the GPU's gradients of the raw parameters (tests/densify_reference.py getters).  Gaussians blended at
+    a pixel whose composited value the GPU flipped on its own in any view are excused (flip_excuse)."""
+    import oracle
+    from gsr_testutil import check_grads, flip_excuse, oracle_cam
+    from test_gpu_configs import _composite, _composite_upstream
+
+    scene = gs.make_scene(C4_P, sh_degree=3, seed=0)
+    w2c, proj, campos, bg_img = single["w2c"], single["proj"], single["campos"], single["bg_img"]
+    w = _c4_upstream(B, S).numpy()
+    tan = math.tan(float(np.float32(math.radians(60.0))) * 0.5)
+    keys = ("means3D", "sh", "opacity", "scales", "rotations")
+    sums = {prec: {k: 0.0 for k in keys} for prec in ("f32", "f64")}
+    refs = []
+    px = lambda a: np.asarray(a).reshape(3, -1).T  # noqa: E731
+    zero_bg = np.zeros(3, np.float32)
+    for v in range(B):  # (≈ 12 s per 1M-Gaussian 1024^2 view on 16 host threads: two forwards, aux, two backwards)
+        cam = dict(view=w2c[v].astype(np.float32), proj=proj[v].astype(np.float32),
+                   campos=campos[v].astype(np.float32), tanx=tan, tany=tan, W=S, H=S)
+        oc = oracle_cam(cam)
+        g_r = w[v].transpose(2, 0, 1).astype(np.float32)
+        renders = {}
+        for prec, dt in (("f32", np.float32), ("f64", np.float64)):
+            f = oracle.forward(scene, oc, zero_bg, prec)
+            render, pre = _composite(f["color"].astype(dt), f["alpha"].astype(dt), bg_img[v].astype(dt))
+            renders[prec] = render
+            gcol, ga = _composite_upstream(g_r, np.zeros((1, S, S), np.float32), pre, bg_img[v])
+            b = oracle.backward(scene, oc, zero_bg, gcol.astype(np.float32), np.zeros((1, S, S), np.float32),
+                                ga.astype(np.float32), prec=prec)
+            for k in keys:
+                sums[prec][k] = sums[prec][k] + b[k].astype(np.float64)
+        gpu_img = single["comp_rgb"][v].transpose(2, 0, 1)
+        e_g = np.abs(px(gpu_img) - px(renders["f64"])).max(1)
+        e_3 = np.abs(px(renders["f32"]) - px(renders["f64"])).max(1)
+        refs.append(dict(aux64=oracle.gauss_aux(scene, oc, "f64"), W=S,
+                         gpu_only_px=np.nonzero((e_g > 1e-5) & ~(e_3 > 1e-5))[0]))
+
+    # through the activations of DensifyModel (raw parameters as the model holds them, in fp64)
+    raw_op = np.log(np.clip(scene["opacities"].astype(np.float64), 1e-4, 1 - 1e-4)) - np.log1p(
+        -np.clip(scene["opacities"].astype(np.float64), 1e-4, 1 - 1e-4))
+    raw_op = np.float32(raw_op).astype(np.float64)  # (inverse_sigmoid of the float32 tensor)
+    sig = 1.0 / (1.0 + np.exp(-raw_op))
+    scl = np.exp(np.log(scene["scales"].astype(np.float32)).astype(np.float64))
+    rot = scene["rotations"].astype(np.float64)
+    nrm = np.maximum(np.linalg.norm(rot, axis=1, keepdims=True), 1e-12)
+    q = rot / nrm
+
+    def raw(s):
+        g_rot = (s["rotations"] - q * (q * s["rotations"]).sum(1, keepdims=True)) / nrm
+        return {"g_xyz": s["means3D"], "g_f_dc": s["sh"][:, :1], "g_f_rest": s["sh"][:, 1:],
+                "g_opacity": s["opacity"] * (sig * (1.0 - sig)), "g_scaling": s["scales"] * scl, "g_rotation": g_rot}
+
+    r = {"b32": {k[2:]: v for k, v in raw(sums["f32"]).items()}, "b64": {k[2:]: v for k, v in raw(sums["f64"]).items()}}
+    names = ("xyz", "f_dc", "f_rest", "opacity", "scaling", "rotation")  # DensifyModel.parameters() order
+    gpu = {"g_" + n: single[f"g{i}"].reshape(r["b64"][n].shape) for i, n in enumerate(names)}
+    check_grads(gpu, r, names, f"C4 {S}^2 summed over {B} views", excuse=flip_excuse(refs))
 
 
 def _c4_oracle_views(single, B, S, views):
