@@ -1812,54 +1812,39 @@ __global__ __launch_bounds__(64 * NW) void k_render_bwd_tw(
       const float pxf = lxf + (float)((q & 1) * 8), pyf = lyf + (float)((q >> 1) * 8);
       int fill = 0;
       unsigned long long pend = 0ull, rest = kq;
-      // the replay step of k_render_bwd (replay / replay2) on this quadrant's pixel, software-pipelined: the
-      // per-candidate terms that do not depend on the running state (alpha, G, 1 / (1 - alpha), the colour
-      // dots) of candidate k + 1 are formed while candidate k updates T, S, Sd, S2 — the same operations on the
-      // same values as the plain loop, so the same bits
-      struct Pre {
-        bool hit;
-        float a_eff, g_eff, oma, inv, cd, cd2, z;
-      };
-      auto pre = [&](const float4 ga, const float4 gb, const float4 gc, const float4 gd) {
-        Pre p;
-        const uint32_t rel = __float_as_uint(gb.w);
-        const float dx = ga.x - pxf, dy = ga.y - pyf;
-        const float power2 = gauss_power2(ga.z, ga.w, gb.x, dx, dy);
-        const float G = __builtin_amdgcn_exp2f(power2);
-        const float alpha = fminf(GSR_ALPHA_MAX, gb.y * G);
-        p.hit = rel < last[j] && power2 <= 0.0f && alpha >= GSR_ALPHA_MIN;
-        p.a_eff = p.hit ? alpha : 0.0f;
-        p.g_eff = p.hit ? G : 0.0f;
-        p.oma = 1.f - p.a_eff;
-        p.inv = fast_rcp(p.oma);
-        p.cd = fmaf(gc.x, dp0[j], fmaf(gc.y, dp1[j], fmaf(gc.z, dp2[j], dpa[j])));
-        p.cd2 = TWO ? fmaf(gd.x, e0[j], fmaf(gd.y, e1[j], gd.z * e2[j])) : 0.f;
-        p.z = gb.z;
-        return p;
-      };
       int jc = (int)__builtin_ctzll(rest);
-      Pre pc = pre(s0[jc], s1[jc], s2[jc], TWO ? s3[jc] : zero4);
+      float4 ga = s0[jc], gb = s1[jc], gc = s2[jc];
+      float4 gd = TWO ? s3[jc] : zero4;
       while (true) {
         rest &= rest - 1ull;
         const int jn = rest != 0ull ? (int)__builtin_ctzll(rest) : jc;
         const float4 xa = s0[jn], xb = s1[jn], xc = s2[jn];
         const float4 xd = TWO ? s3[jn] : zero4;
-        const bool hit = pc.hit;
-        const float a_eff = pc.a_eff, g_eff = pc.g_eff, oma = pc.oma, inv_1ma = pc.inv, cd = pc.cd;
+        // the replay step of k_render_bwd (replay / replay2) on this quadrant's pixel
+        const uint32_t rel = __float_as_uint(gb.w);
+        const float dx = ga.x - pxf, dy = ga.y - pyf;
+        const float power2 = gauss_power2(ga.z, ga.w, gb.x, dx, dy);
+        const float G = __builtin_amdgcn_exp2f(power2);
+        const float alpha = fminf(GSR_ALPHA_MAX, gb.y * G);
+        const bool hit = rel < last[j] && power2 <= 0.0f && alpha >= GSR_ALPHA_MIN;
+        const float a_eff = hit ? alpha : 0.0f;
+        const float g_eff = hit ? G : 0.0f;
+        const float oma = 1.f - a_eff;
+        const float inv_1ma = fast_rcp(oma);
         T[j] = T[j] * inv_1ma;
+        const float cd = fmaf(gc.x, dp0[j], fmaf(gc.y, dp1[j], fmaf(gc.z, dp2[j], dpa[j])));
         float u, u1 = 0.f;
         if (TWO) {
-          const float cd2 = pc.cd2;
-          u1 = g_eff * fmaf(T[j], fmaf(pc.z - Sd[j], dpd[j], cd - S[j]), inv_1ma * nbg[j]);
+          const float cd2 = fmaf(gd.x, e0[j], fmaf(gd.y, e1[j], gd.z * e2[j]));
+          u1 = g_eff * fmaf(T[j], fmaf(gb.z - Sd[j], dpd[j], cd - S[j]), inv_1ma * nbg[j]);
           u = fmaf(g_eff, fmaf(T[j], cd2 - S2[j], inv_1ma * nbg2[j]), u1);
           S2[j] = fmaf(a_eff, cd2, oma * S2[j]);
         } else {
-          u = g_eff * fmaf(T[j], fmaf(pc.z - Sd[j], dpd[j], cd - S[j]), inv_1ma * nbg[j]);
+          u = g_eff * fmaf(T[j], fmaf(gb.z - Sd[j], dpd[j], cd - S[j]), inv_1ma * nbg[j]);
         }
         const float w = a_eff * T[j];
         S[j] = fmaf(a_eff, cd, oma * S[j]);
-        Sd[j] = fmaf(a_eff, pc.z, oma * Sd[j]);
-        const Pre pn = pre(xa, xb, xc, xd);  // (candidate k + 1: independent of the updates above)
+        Sd[j] = fmaf(a_eff, gb.z, oma * Sd[j]);
         const unsigned long long hm = __ballot(hit);
         const int n = __popcll(hm);
         if (fill + n > GSR_HCAP_TW) {
@@ -1875,7 +1860,10 @@ __global__ __launch_bounds__(64 * NW) void k_render_bwd_tw(
         fill += n;
         pend |= 1ull << jc;
         if (rest == 0ull) break;
-        pc = pn;
+        ga = xa;
+        gb = xb;
+        gc = xc;
+        gd = xd;
         jc = jn;
       }
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
