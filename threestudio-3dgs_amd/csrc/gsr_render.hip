@@ -20,6 +20,12 @@
 #include "gsr_kernels.h"
 #include "gsr_wave.h"
 
+#ifndef GSR_FWD_PREFETCH
+// the quadrant-wave forward reads the next candidate's staged record before blending the current one (left to
+// itself the compiler sinks those reads to their use; the two-colour variant then runs at 7 waves per SIMD
+// instead of 8)
+#define GSR_FWD_PREFETCH 1
+#endif
 #ifndef GSR_BWD_OVERLAP
 #define GSR_BWD_OVERLAP 1  // replay steps of a full group scheduled together (k_render_bwd; 2 spills 4 VGPRs)
 #endif
@@ -257,6 +263,9 @@ __global__ __launch_bounds__(64) void k_render_fwd(RenderSet rs,
       if ((k & 7) == 0 && __all(done)) break;
       const float4 an = s0[k + 1], bn = s1[k + 1], cn = s2[k + 1];
       const float4 en = C2 ? s3[k + 1] : zero4;
+#if GSR_FWD_PREFETCH
+      asm volatile("" ::: "memory");  // (the next candidate's reads stay ahead of this step: a prefetch)
+#endif
       const float dx = a.x - pxf, dy = a.y - pyf;
       const float power2 = gauss_power2(a.z, a.w, b.x, dx, dy);  // log2(e) * power
       const float alpha = fminf(GSR_ALPHA_MAX, b.y * __builtin_amdgcn_exp2f(power2));
@@ -584,6 +593,9 @@ __global__ __launch_bounds__(64) void k_render_fwd_tile(RenderSet rs, const uint
       const int kn = rest != 0ull ? (int)__builtin_ctzll(rest) : k;
       const float4 an = s0[kn], bn = s1[kn], cn = s2[kn];
       const float4 en = C2 ? s3[kn] : zero4;
+#if GSR_FWD_PREFETCH
+      asm volatile("" ::: "memory");  // (read ahead of this step's blends, as in k_render_fwd)
+#endif
       uint32_t mk = 0u;
 #pragma unroll
       for (int q = 0; q < 4; ++q) mk |= (uint32_t)((qb[q] >> k) & 1ull) << q;
@@ -1812,14 +1824,18 @@ __global__ __launch_bounds__(64 * NW) void k_render_bwd_tw(
       const float pxf = lxf + (float)((q & 1) * 8), pyf = lyf + (float)((q >> 1) * 8);
       int fill = 0;
       unsigned long long pend = 0ull, rest = kq;
+      // candidate records in two register sets used in turn (the loop body twice, roles swapped: no register
+      // copies between steps); each step reads the next candidate's into the other set
       int jc = (int)__builtin_ctzll(rest);
-      float4 ga = s0[jc], gb = s1[jc], gc = s2[jc];
-      float4 gd = TWO ? s3[jc] : zero4;
-      while (true) {
+      float4 pa = s0[jc], pb = s1[jc], pc = s2[jc];
+      float4 pd = TWO ? s3[jc] : zero4;
+      float4 ya, yb, yc, yd;
+      auto step = [&](const float4& ga, const float4& gb, const float4& gc, const float4& gd, float4& xa, float4& xb,
+                      float4& xc, float4& xd) -> bool {
         rest &= rest - 1ull;
         const int jn = rest != 0ull ? (int)__builtin_ctzll(rest) : jc;
-        const float4 xa = s0[jn], xb = s1[jn], xc = s2[jn];
-        const float4 xd = TWO ? s3[jn] : zero4;
+        xa = s0[jn], xb = s1[jn], xc = s2[jn];
+        xd = TWO ? s3[jn] : zero4;
         // the replay step of k_render_bwd (replay / replay2) on this quadrant's pixel
         const uint32_t rel = __float_as_uint(gb.w);
         const float dx = ga.x - pxf, dy = ga.y - pyf;
@@ -1859,12 +1875,11 @@ __global__ __launch_bounds__(64 * NW) void k_render_bwd_tw(
         if (lane == 0) list[jc] = (uint32_t)fill | ((uint32_t)n << 16);
         fill += n;
         pend |= 1ull << jc;
-        if (rest == 0ull) break;
-        ga = xa;
-        gb = xb;
-        gc = xc;
-        gd = xd;
+        if (rest == 0ull) return false;
         jc = jn;
+        return true;
+      };
+      while (step(pa, pb, pc, pd, ya, yb, yc, yd) && step(ya, yb, yc, yd, pa, pb, pc, pd)) {
       }
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       flush(j, pend);
