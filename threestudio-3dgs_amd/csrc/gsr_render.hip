@@ -1320,14 +1320,21 @@ __device__ __forceinline__ void bwd_tile(BwdLDS<TWO, HITS>& s, const RenderSet& 
           jj[c] = (int)__builtin_ctzll(rest);
           rest &= rest - 1ull;
         }
+        float4 ca = s.s0[jj[0]], cb = s.s1[jj[0]], cc = s.s2[jj[0]];
 #pragma unroll
         for (int c = 0; c < GS; ++c) {
-          const float4 ca = s.s0[jj[c]], cb = s.s1[jj[c]], cc = s.s2[jj[c]];
+          // the next candidate's staged record read ahead of this step (kept ahead by the compiler barrier)
+          const int cn = c + 1 < GS ? c + 1 : c;
+          const float4 na = s.s0[jj[cn]], nb = s.s1[jj[cn]], nc = s.s2[jj[cn]];
+          asm volatile("" ::: "memory");
           float u, w;
           replay(ca, cb, cc, u, w);
           uw[16 * c + wa[c >> 2]] = u;
           uw[16 * (c + 8) + wa[2 + (c >> 2)]] = w;
           if ((c & (GSR_BWD_OVERLAP - 1)) == GSR_BWD_OVERLAP - 1) __builtin_amdgcn_sched_barrier(0);  // (VGPR budget)
+          ca = na;
+          cb = nb;
+          cc = nc;
         }
       } else {
       int j = (int)__builtin_ctzll(rest);
