@@ -121,6 +121,15 @@ __device__ __forceinline__ float vsel(unsigned long long m, float if_set, float 
   return r;
 }
 
+// a wave-uniform float kept in a scalar register
+__device__ __forceinline__ float sgpr_f(float x) {
+  float r;
+  // (the builtin is folded away for a uniform x; the nops cover the VALU-write -> readlane hazard inline asm hides
+  // from the compiler; once per kernel)
+  asm volatile("s_nop 4\n\tv_readfirstlane_b32 %0, %1" : "=s"(r) : "v"(x));
+  return r;
+}
+
 // bg . dL/dpixel with an explicit operation order (the backward kernels' background terms: every kernel
 // variant forms the same bits, independent of how the compiler would contract the expression)
 __device__ __forceinline__ float bg_dot3(const float* bg, float d0, float d1, float d2) {
@@ -498,12 +507,15 @@ __global__ __launch_bounds__(64) void k_render_fwd_tile(RenderSet rs, const uint
   const int tx0 = (tile % grid_x) * GSR_TILE_X, ty0 = (tile / grid_x) * GSR_TILE_Y;
   float pxf[4], pyf[4], T[4], Cr[4], Cg[4], Cb[4], D[4], Er[4], Eg[4], Eb[4];
   uint32_t last[4];
-  bool done[4], inside[4];
+  bool inside[4];
+  // per quadrant the lanes whose pixel is done (outside the image, or terminated): uniform 64-bit masks, so the
+  // step's conditions combine in scalar registers and the selects read them directly
+  unsigned long long dm[4];
 #pragma unroll
   for (int q = 0; q < 4; ++q) {
     const int px = tx0 + (q & 1) * 8 + (lane & 7), py = ty0 + (q >> 1) * 8 + (lane >> 3);
     inside[q] = px < W && py < H;
-    done[q] = !inside[q];
+    dm[q] = __ballot(!inside[q]);
     pxf[q] = (float)px;
     pyf[q] = (float)py;
     T[q] = 1.0f;
@@ -511,6 +523,9 @@ __global__ __launch_bounds__(64) void k_render_fwd_tile(RenderSet rs, const uint
     Er[q] = Eg[q] = Eb[q] = 0.f;
     last[q] = 0u;
   }
+  // the quadrant origins of the cull (wave-uniform: held in scalar registers, not reloaded from spill slots)
+  const float qox[2] = {sgpr_f((float)tx0), sgpr_f((float)(tx0 + 8))};
+  const float qoy[2] = {sgpr_f((float)ty0), sgpr_f((float)(ty0 + 8))};
   const uint2 range = ranges[tile];
   const int n = (int)(range.y - range.x);
   const uint32_t gmask = rs.gmask;
@@ -530,7 +545,7 @@ __global__ __launch_bounds__(64) void k_render_fwd_tile(RenderSet rs, const uint
   auto active_mask = [&]() -> uint32_t {
     uint32_t m = 0u;
 #pragma unroll
-    for (int q = 0; q < 4; ++q) m |= __all(done[q]) ? 0u : (1u << q);
+    for (int q = 0; q < 4; ++q) m |= dm[q] == ~0ull ? 0u : (1u << q);
     return m;
   };
   uint32_t qactive = active_mask();
@@ -551,7 +566,7 @@ __global__ __launch_bounds__(64) void k_render_fwd_tile(RenderSet rs, const uint
     if (i < n) {
 #pragma unroll
       for (int q = 0; q < 4; ++q)
-        m |= quadrant_hit(r0, r1, (float)(tx0 + (q & 1) * 8), (float)(ty0 + (q >> 1) * 8)) ? (1u << q) : 0u;
+        m |= quadrant_hit(r0, r1, qox[q & 1], qoy[q >> 1]) ? (1u << q) : 0u;
     }
     // the conic pre-multiplied for gauss_power2 (.w of s1: 1 + list position)
     s0[lane] = make_float4(r0.x, r0.y, GSR_CONIC_K_AC * r0.z, GSR_CONIC_K_B * r0.w);
@@ -563,25 +578,25 @@ __global__ __launch_bounds__(64) void k_render_fwd_tile(RenderSet rs, const uint
     // candidate's staged record while the current one blends (no per-candidate LDS read of its mask)
     unsigned long long qb[4];
 #pragma unroll
-    for (int q = 0; q < 4; ++q) qb[q] = __ballot((m >> q) & 1u);
+    for (int q = 0; q < 4; ++q) qb[q] = (qactive >> q) & 1u ? __ballot((m >> q) & 1u) : 0ull;
     __syncthreads();
-    auto live = [&]() {
-      unsigned long long u = 0ull;
-#pragma unroll
-      for (int q = 0; q < 4; ++q) u |= (qactive >> q) & 1u ? qb[q] : 0ull;
-      return u;
-    };
+    auto live = [&]() { return (qb[0] | qb[1]) | (qb[2] | qb[3]); };
     unsigned long long rest = live();
     int k = rest != 0ull ? (int)__builtin_ctzll(rest) : 0;
-    float4 a = s0[k], b = s1[k], c = s2[k];
-    float4 e = C2 ? s3[k] : zero4;
-    for (int walked = 0; rest != 0ull; ++walked) {
+    int walked = 0;
+    // one step: candidate k from the register set `cur`, the next candidate's staged record into `nxt` (the step
+    // runs twice per loop iteration with the sets swapped: no register copies); false when the walk ends
+    auto step = [&](float4& a, float4& b, float4& c, float4& e, float4& an, float4& bn, float4& cn,
+                    float4& en) -> bool {
       if (walked > 0 && (walked & 7) == 0) {
         // (finished quadrants leave the walk: they would blend nothing)
         qactive = active_mask();
-        if (qactive == 0u) break;
+        if (qactive == 0u) return false;
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+          if (!((qactive >> q) & 1u)) qb[q] = 0ull;
         rest &= live();
-        if (rest == 0ull) break;
+        if (rest == 0ull) return false;
         const int kk = (int)__builtin_ctzll(rest);
         if (kk != k) {
           k = kk;
@@ -589,32 +604,29 @@ __global__ __launch_bounds__(64) void k_render_fwd_tile(RenderSet rs, const uint
           e = C2 ? s3[k] : zero4;
         }
       }
+      ++walked;
       rest &= rest - 1ull;
       const int kn = rest != 0ull ? (int)__builtin_ctzll(rest) : k;
-      const float4 an = s0[kn], bn = s1[kn], cn = s2[kn];
-      const float4 en = C2 ? s3[kn] : zero4;
+      an = s0[kn], bn = s1[kn], cn = s2[kn];
+      en = C2 ? s3[kn] : zero4;
 #if GSR_FWD_PREFETCH
       asm volatile("" ::: "memory");  // (read ahead of this step's blends, as in k_render_fwd)
 #endif
-      uint32_t mk = 0u;
-#pragma unroll
-      for (int q = 0; q < 4; ++q) mk |= (uint32_t)((qb[q] >> k) & 1ull) << q;
-      mk &= qactive;
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
-        if (mk & (1u << q)) {
+        if ((qb[q] >> k) & 1ull) {
 #ifdef GSR_TIMELINE
-          pc_eval += done[q] ? 0ull : 1ull;
+          pc_eval += (dm[q] >> lane) & 1ull ? 0ull : 1ull;
           pc_slot += 1ull;
 #endif
           const float dx = a.x - pxf[q], dy = a.y - pyf[q];
           const float power2 = gauss_power2(a.z, a.w, b.x, dx, dy);  // log2(e) * power
           const float alpha = fminf(GSR_ALPHA_MAX, b.y * __builtin_amdgcn_exp2f(power2));
-          const bool ok = !done[q] && power2 <= 0.0f && alpha >= GSR_ALPHA_MIN;
+          const unsigned long long okm = (__ballot(power2 <= 0.0f) & __ballot(alpha >= GSR_ALPHA_MIN)) & ~dm[q];
           const float test_T = T[q] * (1.0f - alpha);
-          const bool term = ok && test_T < GSR_T_EPS;
-          const bool blend = ok && !term;
-          const float a_eff = blend ? alpha : 0.0f;
+          const unsigned long long termm = okm & __ballot(test_T < GSR_T_EPS);
+          const unsigned long long blendm = okm & ~termm;
+          const float a_eff = vsel(blendm, alpha, 0.0f);
           const float aT = a_eff * T[q];
           Cr[q] = fmaf(c.x, aT, Cr[q]);
           Cg[q] = fmaf(c.y, aT, Cg[q]);
@@ -625,16 +637,20 @@ __global__ __launch_bounds__(64) void k_render_fwd_tile(RenderSet rs, const uint
             Eg[q] = fmaf(e.y, aT, Eg[q]);
             Eb[q] = fmaf(e.z, aT, Eb[q]);
           }
-          T[q] = blend ? test_T : T[q];
-          last[q] = blend ? __float_as_uint(b.w) : last[q];
-          done[q] = done[q] || term;
+          T[q] = vsel(blendm, test_T, T[q]);
+          last[q] = __float_as_uint(vsel(blendm, b.w, __uint_as_float(last[q])));
+          dm[q] |= termm;
         }
       }
-      a = an;
-      b = bn;
-      c = cn;
-      e = en;
       k = kn;
+      return rest != 0ull;
+    };
+    if (rest != 0ull) {
+      float4 pa = s0[k], pb = s1[k], pc = s2[k];
+      float4 pd = C2 ? s3[k] : zero4;
+      float4 ya, yb, yc, yd;
+      while (step(pa, pb, pc, pd, ya, yb, yc, yd) && step(ya, yb, yc, yd, pa, pb, pc, pd)) {
+      }
     }
     __syncthreads();
     qactive = active_mask();
