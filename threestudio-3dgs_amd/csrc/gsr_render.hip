@@ -26,6 +26,9 @@
 // instead of 8)
 #define GSR_FWD_PREFETCH 1
 #endif
+#ifndef GSR_FWD_WPE
+#define GSR_FWD_WPE 1  // k_render_fwd minimum waves per SIMD (7 / 8 spill the two-colour variant)
+#endif
 #ifndef GSR_BWD_OVERLAP
 #define GSR_BWD_OVERLAP 1  // replay steps of a full group scheduled together (k_render_bwd; 2 spills 4 VGPRs)
 #endif
@@ -143,7 +146,7 @@ __device__ __forceinline__ float bg_dot3(const float* bg, float d0, float d1, fl
 // different depths, and 4x more independent waves balance the load across the 256 CUs.
 // CK: also the split backward's per-chunk states (rs.ckpt, gsr_common.h ckpt_offset).
 template <bool C2, bool CK>
-__global__ __launch_bounds__(64) void k_render_fwd(RenderSet rs,
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(GSR_FWD_WPE, 8))) void k_render_fwd(RenderSet rs,
                                                    const uint2* __restrict__ ranges,
                                                    const uint32_t* __restrict__ sorted_gauss,
                                                    const GaussRec* __restrict__ rec,
@@ -183,7 +186,7 @@ __global__ __launch_bounds__(64) void k_render_fwd(RenderSet rs,
   const uint2 range = ranges[tile];
   const int n = (int)(range.y - range.x);
 
-  bool done = !inside;
+  unsigned long long dmk = __ballot(!inside);  // lanes whose pixel is done (outside, or terminated)
   float T = 1.0f, Cr = 0.f, Cg = 0.f, Cb = 0.f, D = 0.f;
   float Er = 0.f, Eg = 0.f, Eb = 0.f;  // second colour (C2)
   uint32_t last_contributor = 0;
@@ -226,7 +229,7 @@ __global__ __launch_bounds__(64) void k_render_fwd(RenderSet rs,
   float Pr = 0.f, Pg = 0.f, Pb = 0.f, Pd = 0.f;
   int chunk = 0;
   for (int base = 0; base < n; base += 64) {
-    if (__all(done)) break;
+    if (dmk == ~0ull) break;
     if (CK && base > 0 && base % GSR_SPLIT_CH == 0 && base <= GSR_SPLIT_NCK * GSR_SPLIT_CH) {
       // chunk `chunk` ends: its sums into its slot, T into the next one's slot
       reinterpret_cast<float4*>(ckpt + (size_t)chunk * GSR_CKPT_FIELDS * 256 + 256)[cpix] = make_float4(Pr, Pg, Pb, Pd);
@@ -267,11 +270,14 @@ __global__ __launch_bounds__(64) void k_render_fwd(RenderSet rs,
       if (C2) s3[pos] = r3;
     }
     __syncthreads();
-    float4 a = s0[0], b = s1[0], c = s2[0], e = C2 ? s3[0] : zero4;
-    for (int k = 0; k < cnt; ++k) {
-      if ((k & 7) == 0 && __all(done)) break;
-      const float4 an = s0[k + 1], bn = s1[k + 1], cn = s2[k + 1];
-      const float4 en = C2 ? s3[k + 1] : zero4;
+    // one blend step: candidate k from the register set `cur`, the next staged record into `nxt` (the loop runs
+    // the step twice with the sets swapped: no register copies); done / ok / term / blend as uniform lane masks
+    int k = 0;
+    auto step = [&](const float4& a, const float4& b, const float4& c, const float4& e, float4& an, float4& bn,
+                    float4& cn, float4& en) -> bool {
+      if (k >= cnt || ((k & 7) == 0 && dmk == ~0ull)) return false;
+      an = s0[k + 1], bn = s1[k + 1], cn = s2[k + 1];
+      en = C2 ? s3[k + 1] : zero4;
 #if GSR_FWD_PREFETCH
       asm volatile("" ::: "memory");  // (the next candidate's reads stay ahead of this step: a prefetch)
 #endif
@@ -279,15 +285,15 @@ __global__ __launch_bounds__(64) void k_render_fwd(RenderSet rs,
       const float power2 = gauss_power2(a.z, a.w, b.x, dx, dy);  // log2(e) * power
       const float alpha = fminf(GSR_ALPHA_MAX, b.y * __builtin_amdgcn_exp2f(power2));
 #ifdef GSR_TIMELINE
-      pc_eval += done ? 0ull : 1ull;
+      pc_eval += (dmk >> lane) & 1ull ? 0ull : 1ull;
       pc_slot += 1ull;
 #endif
-      const bool ok = !done && power2 <= 0.0f && alpha >= GSR_ALPHA_MIN;
+      const unsigned long long okm = (__ballot(power2 <= 0.0f) & __ballot(alpha >= GSR_ALPHA_MIN)) & ~dmk;
       const float test_T = T * (1.0f - alpha);
-      const bool term = ok && test_T < GSR_T_EPS;
-      const bool blend = ok && !term;
+      const unsigned long long termm = okm & __ballot(test_T < GSR_T_EPS);
+      const unsigned long long blendm = okm & ~termm;
       // non-blending lanes run the same arithmetic with alpha = 0 (no change), no selects of state
-      const float a_eff = blend ? alpha : 0.0f;
+      const float a_eff = vsel(blendm, alpha, 0.0f);
       const float aT = a_eff * T;
       // the running totals in list order whatever the launch (the outputs' bits do not depend on whether the
       // launch writes checkpoints), and beside them the chunk's own sums for the split backward
@@ -306,13 +312,17 @@ __global__ __launch_bounds__(64) void k_render_fwd(RenderSet rs,
         Eg = fmaf(e.y, aT, Eg);
         Eb = fmaf(e.z, aT, Eb);
       }
-      T = blend ? test_T : T;  // = T (1 - a_eff)
-      last_contributor = blend ? __float_as_uint(b.w) : last_contributor;
-      done = done || term;
-      a = an;
-      b = bn;
-      c = cn;
-      e = en;
+      T = vsel(blendm, test_T, T);  // = T (1 - a_eff)
+      last_contributor = __float_as_uint(vsel(blendm, b.w, __uint_as_float(last_contributor)));
+      dmk |= termm;
+      ++k;
+      return true;
+    };
+    {
+      float4 pa = s0[0], pb = s1[0], pc = s2[0], pd = C2 ? s3[0] : zero4;
+      float4 ya, yb, yc, yd;
+      while (step(pa, pb, pc, pd, ya, yb, yc, yd) && step(ya, yb, yc, yd, pa, pb, pc, pd)) {
+      }
     }
     __syncthreads();
   }
