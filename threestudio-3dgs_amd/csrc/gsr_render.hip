@@ -1875,9 +1875,11 @@ __global__ __launch_bounds__(64 * NW) void k_render_bwd_tw(
         const float power2 = gauss_power2(ga.z, ga.w, gb.x, dx, dy);
         const float G = __builtin_amdgcn_exp2f(power2);
         const float alpha = fminf(GSR_ALPHA_MAX, gb.y * G);
-        const bool hit = rel < last[j] && power2 <= 0.0f && alpha >= GSR_ALPHA_MIN;
-        const float a_eff = hit ? alpha : 0.0f;
-        const float g_eff = hit ? G : 0.0f;
+        // (the step's blend condition as a uniform lane mask: the selects read it directly)
+        const unsigned long long hm = (__ballot(rel < last[j]) & __ballot(power2 <= 0.0f)) & __ballot(alpha >= GSR_ALPHA_MIN);
+        const bool hit = (hm >> lane) & 1ull;
+        const float a_eff = vsel(hm, alpha, 0.0f);
+        const float g_eff = vsel(hm, G, 0.0f);
         const float oma = 1.f - a_eff;
         const float inv_1ma = fast_rcp(oma);
         T[j] = T[j] * inv_1ma;
@@ -1894,7 +1896,6 @@ __global__ __launch_bounds__(64 * NW) void k_render_bwd_tw(
         const float w = a_eff * T[j];
         S[j] = fmaf(a_eff, cd, oma * S[j]);
         Sd[j] = fmaf(a_eff, gb.z, oma * Sd[j]);
-        const unsigned long long hm = __ballot(hit);
         const int n = __popcll(hm);
         if (fill + n > GSR_HCAP_TW) {
           // list full: the finished pairs' sums now, then start over (this wave's own LDS: in-order)
