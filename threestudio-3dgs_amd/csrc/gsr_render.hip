@@ -1732,9 +1732,19 @@ __global__ __launch_bounds__(64 * NW) void k_render_bwd_tw(
       }
     }
   };
+  // the forward's quadrant masks when the keys carry them (TilePack::qmask): the cull is read, not recomputed
+  // (both bounds are conservative: a pair either keeps has no blend beyond the other's, so the sums agree)
+  const uint32_t* qkeys = rs.qkeys ? rs.qkeys + rs.inst_start[v] + range.x : nullptr;
+  uint32_t nqm = 0u, qm_next = 0u;  // the masks of the staged-next candidate / of gi_next
   if (hi > lo) {
-    if (hi - 1 - lane >= lo) load(sorted_gauss[range.x + hi - 1 - lane] & gmask);
-    if (hi - 65 - lane >= lo) gi_next = sorted_gauss[range.x + hi - 65 - lane] & gmask;
+    if (hi - 1 - lane >= lo) {
+      load(sorted_gauss[range.x + hi - 1 - lane] & gmask);
+      if (qkeys) nqm = qkeys[hi - 1 - lane] >> GSR_QMASK_SHIFT;
+    }
+    if (hi - 65 - lane >= lo) {
+      gi_next = sorted_gauss[range.x + hi - 65 - lane] & gmask;
+      if (qkeys) qm_next = qkeys[hi - 65 - lane] >> GSR_QMASK_SHIFT;
+    }
   }
 
   // hit-list sums of one (candidate, quadrant) pair -> moments about the candidate's mean (the flush of
@@ -1820,14 +1830,19 @@ __global__ __launch_bounds__(64 * NW) void k_render_bwd_tw(
       const uint32_t dx_ = __float_as_uint(nd.x), dy_ = __float_as_uint(nd.y);
       const int xmin = dx_ & 0xffff, ymin = dx_ >> 16, xmax = dy_ & 0xffff;
       slot[lane] = ngo + (uint32_t)((tyi - ymin) * (xmax - xmin) + (txi - xmin));
-      // the staged conic back to (a, b, c) for the (padded, conservative) cull, as k_render_bwd does
-      const float4 r0 = make_float4(ca.x, ca.y, ca.z * (1.0f / GSR_CONIC_K_AC), ca.w * (1.0f / GSR_CONIC_K_B));
-      const float4 r1 = make_float4(cb.x * (1.0f / GSR_CONIC_K_AC), cb.y, cb.z, cb.w);
+      if (qkeys) {
 #pragma unroll
-      for (int q = 0; q < 4; ++q)
-        if (rel_c < qmaxc[q] &&
-            quadrant_hit(r0, r1, (float)(txi * GSR_TILE_X + (q & 1) * 8), (float)(tyi * GSR_TILE_Y + (q >> 1) * 8)))
-          keep4 |= 1u << q;
+        for (int q = 0; q < 4; ++q) keep4 |= rel_c < qmaxc[q] ? nqm & (1u << q) : 0u;
+      } else {
+        // the staged conic back to (a, b, c) for the (padded, conservative) cull, as k_render_bwd does
+        const float4 r0 = make_float4(ca.x, ca.y, ca.z * (1.0f / GSR_CONIC_K_AC), ca.w * (1.0f / GSR_CONIC_K_B));
+        const float4 r1 = make_float4(cb.x * (1.0f / GSR_CONIC_K_AC), cb.y, cb.z, cb.w);
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+          if (rel_c < qmaxc[q] &&
+              quadrant_hit(r0, r1, (float)(txi * GSR_TILE_X + (q & 1) * 8), (float)(tyi * GSR_TILE_Y + (q >> 1) * 8)))
+            keep4 |= 1u << q;
+      }
       if (NW > 1) skeep[lane] = keep4;
     }
     if (staged && stage_col) {
@@ -1836,8 +1851,14 @@ __global__ __launch_bounds__(64 * NW) void k_render_bwd_tw(
     }
     // the next batch's records and the one after's indices
     if (h - 64 > lo) {
-      if (h - 65 - lane >= lo) load(gi_next);
-      if (h - 129 - lane >= lo) gi_next = sorted_gauss[range.x + h - 129 - lane] & gmask;
+      if (h - 65 - lane >= lo) {
+        load(gi_next);
+        nqm = qm_next;
+      }
+      if (h - 129 - lane >= lo) {
+        gi_next = sorted_gauss[range.x + h - 129 - lane] & gmask;
+        if (qkeys) qm_next = qkeys[h - 129 - lane] >> GSR_QMASK_SHIFT;
+      }
     }
 #pragma unroll
     for (int i = 0; i < NM; ++i) acc[i] = 0.f;
