@@ -187,6 +187,77 @@ class _ForceChunks:
         self.ranges_seen = len(events)
 
 
+class _SnapshotReduce:
+    """A grad_reduce stand-in that reads the gradients on a side stream the way ChunkedGradReduce's all-reduces
+    do: after the library's per-range events when it is given them, else after the whole main stream."""
+
+    def __init__(self, n):
+        from diff_gaussian_rasterization.view_shard import ChunkedGradReduce
+
+        self._r = ChunkedGradReduce(n_chunks=n)
+        self.snap = None
+        self.used_events = None
+
+    def active(self):
+        return True
+
+    def chunk_events(self, device):
+        return self._r.chunk_events(device)
+
+    def launch(self, grads, P, events=None):
+        side = torch.cuda.Stream()
+        if events:
+            for e in events:
+                side.wait_event(e)
+        else:
+            side.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(side):
+            self.snap = [g.clone() for g in grads if g is not None]
+        self.grads = [g for g in grads if g is not None]
+        self.used_events = bool(events)
+
+
+@pytest.mark.parametrize("bwd", ["fused", "separate"])
+def test_chunked_reduce_reads_finished_gradients(bwd, monkeypatch):
+    """with the SuGaR normal renderer's second rasterizer call backpropagated separately
+    (GSR_TWO_COLOR_BWD=separate) its kernels still add into the shared gradients after the first call's
+    ranges are formed, so the reduction must wait for the whole stream (no per-range events); with the fused
+    two-colour backward the per-range events cover every writer.  The gradients a side-stream reader sees equal
+    the final ones either way."""
+    from diff_gaussian_rasterization import GaussianRasterizationSettings
+    from diff_gaussian_rasterization.batched import rasterize_views
+    from diff_gaussian_rasterization.cameras import get_cam_info_gaussian
+
+    monkeypatch.setenv("GSR_TWO_COLOR_BWD", bwd)
+    scene = gs.make_sugar_scene(4, sh_degree=0, seed=5)
+    P = scene["means3D"].shape[0]
+    batch = rf.make_batch(3, H, W, "cuda", seed=11)
+    fovy = batch["fovy"]
+    w2c, proj, campos = get_cam_info_gaussian(batch["c2w"], fovy, fovy, znear=0.1, zfar=100)
+    tan = math.tan(float(fovy[0]) * 0.5)
+    settings = [GaussianRasterizationSettings(image_height=H, image_width=W, tanfovx=tan, tanfovy=tan,
+                                              bg=torch.zeros(3, device="cuda"), scale_modifier=1.0,
+                                              viewmatrix=w2c[v], projmatrix=proj[v], sh_degree=0, campos=campos[v],
+                                              prefiltered=False, debug=False) for v in range(3)]
+    t = {k: torch.tensor(scene[k], device="cuda", requires_grad=True)
+         for k in ("means3D", "opacities", "scales", "rotations", "normals")}
+    cols = torch.tensor(scene["shs"][:, 0, :] * np.float32(gs.C0) + np.float32(0.5), device="cuda",
+                        requires_grad=True)
+    m2 = [torch.zeros((P, 3), device="cuda", requires_grad=True) for _ in range(3)]
+    snap = _SnapshotReduce(4)
+    outs = rasterize_views(settings, t["means3D"], m2, t["opacities"], colors_precomp=cols, scales=t["scales"],
+                           rotations=t["rotations"], colors2=t["normals"], grad_reduce=snap)
+    up = [torch.randn_like(o, generator=torch.Generator("cuda").manual_seed(20 + i)) if o.is_floating_point()
+          else None for i, o in enumerate(outs)]
+    torch.autograd.backward([o for o, u in zip(outs, up) if u is not None], [u for u in up if u is not None])
+    torch.cuda.synchronize()
+    assert snap.snap is not None
+    # the separate second-colour backward writes after the first call's ranges: no per-range events then
+    assert snap.used_events == (bwd == "fused")
+    for i, (a, b) in enumerate(zip(snap.snap, snap.grads)):  # what the reader saw vs the finished buffers
+        assert torch.equal(a, b), f"gradient buffer {i} read before its last writer finished"
+
+
 @pytest.mark.parametrize("n_chunks,P", [(4, 20_000), (3, 4096 * 5 + 17), (16, 9000)])
 def test_chunked_gauss_backward_bitwise(n_chunks, P):
     """gsr_set_backward_chunks: the per-Gaussian backward in Gaussian ranges (with events) gives bitwise the
