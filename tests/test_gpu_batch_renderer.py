@@ -433,11 +433,11 @@ def _c4_oracle_sums(single, B, S):
     w = _c4_upstream(B, S).numpy()
     tan = math.tan(float(np.float32(math.radians(60.0))) * 0.5)
     keys = ("means3D", "sh", "opacity", "scales", "rotations")
-    sums = {prec: {k: 0.0 for k in keys} for prec in ("f32", "f64")}
+    sums = {prec: {k: 0.0 for k in keys} for prec in ("f32", "f64", "f32r")}
     refs = []
     px = lambda a: np.asarray(a).reshape(3, -1).T  # noqa: E731
     zero_bg = np.zeros(3, np.float32)
-    for v in range(B):  # (≈ 12 s per 1M-Gaussian 1024^2 view on 16 host threads: two forwards, aux, two backwards)
+    for v in range(B):  # (≈ 15 s per 1M-Gaussian 1024^2 view on 16 host threads: two forwards, aux, three backwards)
         cam = dict(view=w2c[v].astype(np.float32), proj=proj[v].astype(np.float32),
                    campos=campos[v].astype(np.float32), tanx=tan, tany=tan, W=S, H=S)
         oc = oracle_cam(cam)
@@ -448,10 +448,13 @@ def _c4_oracle_sums(single, B, S):
             render, pre = _composite(f["color"].astype(dt), f["alpha"].astype(dt), bg_img[v].astype(dt))
             renders[prec] = render
             gcol, ga = _composite_upstream(g_r, np.zeros((1, S, S), np.float32), pre, bg_img[v])
-            b = oracle.backward(scene, oc, zero_bg, gcol.astype(np.float32), np.zeros((1, S, S), np.float32),
-                                ga.astype(np.float32), prec=prec)
-            for k in keys:
-                sums[prec][k] = sums[prec][k] + b[k].astype(np.float64)
+            args = (scene, oc, zero_bg, gcol.astype(np.float32), np.zeros((1, S, S), np.float32), ga.astype(np.float32))
+            runs = [(prec, oracle.backward(*args, prec=prec))]
+            if prec == "f32":  # the null model: the fp32 reference with its per-Gaussian sums in another order
+                runs.append(("f32r", oracle.backward(*args, prec="f32c", order=1)))
+            for tag, b in runs:
+                for k in keys:
+                    sums[tag][k] = sums[tag][k] + b[k].astype(np.float64)
         gpu_img = single["comp_rgb"][v].transpose(2, 0, 1)
         e_g = np.abs(px(gpu_img) - px(renders["f64"])).max(1)
         e_3 = np.abs(px(renders["f32"]) - px(renders["f64"])).max(1)
@@ -473,7 +476,8 @@ def _c4_oracle_sums(single, B, S):
         return {"g_xyz": s["means3D"], "g_f_dc": s["sh"][:, :1], "g_f_rest": s["sh"][:, 1:],
                 "g_opacity": s["opacity"] * (sig * (1.0 - sig)), "g_scaling": s["scales"] * scl, "g_rotation": g_rot}
 
-    r = {"b32": {k[2:]: v for k, v in raw(sums["f32"]).items()}, "b64": {k[2:]: v for k, v in raw(sums["f64"]).items()}}
+    r = {"b32": {k[2:]: v for k, v in raw(sums["f32"]).items()}, "b64": {k[2:]: v for k, v in raw(sums["f64"]).items()},
+         "b32r": {k[2:]: v for k, v in raw(sums["f32r"]).items()}}
     names = ("xyz", "f_dc", "f_rest", "opacity", "scaling", "rotation")  # DensifyModel.parameters() order
     gpu = {"g_" + n: single[f"g{i}"].reshape(r["b64"][n].shape) for i, n in enumerate(names)}
     check_grads(gpu, r, names, f"C4 {S}^2 summed over {B} views", excuse=flip_excuse(refs))
