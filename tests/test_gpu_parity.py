@@ -299,8 +299,6 @@ def test_forward_kernels_bitwise(kind, switch, monkeypatch):
             monkeypatch.setenv("GSR_BWD_KERNEL", "tile" if kernel.startswith("tile") else "quadrant")
             # (hit lists: one or two waves per tile, GSR_BWD_TW_WAVES)
             monkeypatch.setenv("GSR_BWD_TW_WAVES", "2" if kernel.startswith("tile2") else "1")
-            # (the two-phase quadrant walk: per-lane blends after a ballot pass, GSR_BWD_TW_PHASED)
-            monkeypatch.setenv("GSR_BWD_TW_PHASED", "1" if kernel.endswith("phased") else "0")
         elif switch == "tile_keys":
             if kernel == "tile":
                 monkeypatch.delenv("GSR_TILE_KEYS", raising=False)
@@ -338,6 +336,6 @@ def test_forward_kernels_bitwise(kind, switch, monkeypatch):
         for i, (x, y) in enumerate(zip(run("plain"), quad)):
             assert torch.equal(x, y), f"plain keys: output {i} differs: {float((x.double() - y.double()).abs().max())}"
     if switch == "bwd_kernel" and kind == "sugar_two_colors":
-        for variant in ("tile2", "tile_phased", "tile2_phased"):
+        for variant in ("tile2",):
             for i, (x, y) in enumerate(zip(run(variant), quad)):
                 assert torch.equal(x, y), f"{variant}: output {i} differs: {float((x.double() - y.double()).abs().max())}"

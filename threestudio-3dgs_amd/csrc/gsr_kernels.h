@@ -99,7 +99,6 @@ struct RenderSet {
   uint32_t* split_items;  // with ckpt: the later chunks' backward items (ImageState::split_items)
   uint32_t* split_cap;    // with ckpt: ImageState::split_cap
   int split_extra;        // with ckpt: split_extra(the set's V, tiles)
-  int tw_phased;          // k_render_bwd_tw: two-phase quadrant walk (gsr_render.hip bwd_tw_phased)
   // the sorted keys when they carry the quadrant masks (TilePack::qmask; indexed like the sorted Gaussians),
   // else null
   const uint32_t* qkeys;

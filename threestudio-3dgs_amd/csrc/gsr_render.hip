@@ -1613,8 +1613,6 @@ __global__ __launch_bounds__(64 * NW) void k_render_bwd_tw(
   __shared__ uint32_t slist[NW][64];                    // the current quadrant: first hit | hits << 16
   __shared__ float4 shits[NW][GSR_HCAP_TW];             // (u, u_1, w, pixel) of the current quadrant's blends
   __shared__ float4 splanes[NW][TWO ? 128 : 64];        // the current quadrant's dL/dpixel per pixel
-  __shared__ uint2 skb[NW][64];                         // two-phase walk: the k-th kept candidate's blend ballot
-  __shared__ uint32_t skj[NW][64];                      // two-phase walk: its staged index | first hit << 8
   int v, tile, q_unused;
   if (!block_map<4>(blockIdx.x, rs, v, tile, q_unused)) return;
   GSR_TL_BEGIN
@@ -1642,8 +1640,6 @@ __global__ __launch_bounds__(64 * NW) void k_render_bwd_tw(
   uint32_t* list = slist[wv];
   float4* hits = shits[wv];
   float4* planes = splanes[wv];
-  uint2* kball = skb[wv];
-  uint32_t* kent = skj[wv];
   const int txi = tile % grid_x, tyi = tile / grid_x;
   const uint2 range = ranges[tile];
   const uint4 qm = reinterpret_cast<const uint4*>(quad_maxc)[tile];
@@ -1882,153 +1878,63 @@ __global__ __launch_bounds__(64 * NW) void k_render_bwd_tw(
       const float pxf = lxf + (float)((q & 1) * 8), pyf = lyf + (float)((q >> 1) * 8);
       int fill = 0;
       unsigned long long pend = 0ull, rest = kq;
-      if (rs.tw_phased) {
-        // Two phases per chunk of kept candidates (a chunk ends where the next candidate's hits would overflow
-        // the list: the same flush points as the one-phase walk).  Phase 1, per kept candidate: alpha and the
-        // blend ballot only (no state), its list entry, and in each lane a bit for every candidate that blends
-        // the lane's pixel.  Phase 2, per lane: its own blends in candidate order — the state update and the
-        // hit of the one-phase step, whose non-blending steps leave T, S, Sd, S2 unchanged (alpha = 0), so
-        // skipping them changes no bit; the hit goes to the candidate's segment at the lane's ballot rank (the
-        // one-phase order).  A chunk costs its kept candidates' cheap evaluations plus the largest per-lane
-        // blend count, instead of a full step per kept candidate.
-        while (rest != 0ull) {
-          uint32_t m0 = 0u, m1 = 0u;
-          int kc = 0;
-          while (rest != 0ull) {
-            const int jc = (int)__builtin_ctzll(rest);
-            const float4 ga = s0[jc], gb = s1[jc];
-            const uint32_t rel = __float_as_uint(gb.w);
-            const float dx = ga.x - pxf, dy = ga.y - pyf;
-            const float power2 = gauss_power2(ga.z, ga.w, gb.x, dx, dy);
-            const float G = __builtin_amdgcn_exp2f(power2);
-            const float alpha = fminf(GSR_ALPHA_MAX, gb.y * G);
-            const unsigned long long hm =
-                (__ballot(rel < last[j]) & __ballot(power2 <= 0.0f)) & __ballot(alpha >= GSR_ALPHA_MIN);
-            const int n = __popcll(hm);
-            if (fill + n > GSR_HCAP_TW) break;  // (uniform) the next chunk starts here
-            if (lane == 0) {
-              kball[kc] = make_uint2((uint32_t)hm, (uint32_t)(hm >> 32));
-              kent[kc] = (uint32_t)jc | ((uint32_t)fill << 8);
-              list[jc] = (uint32_t)fill | ((uint32_t)n << 16);
-            }
-            const uint32_t bit = (uint32_t)((hm >> lane) & 1ull);
-            if (kc < 32)
-              m0 |= bit << kc;
-            else
-              m1 |= bit << (kc - 32);
-            fill += n;
-            pend |= 1ull << jc;
-            ++kc;
-            rest &= rest - 1ull;
-          }
-          asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // (the entries, read back by other lanes)
-          while ((m0 | m1) != 0u) {
-            int k;
-            if (m0 != 0u) {
-              k = (int)__builtin_ctz(m0);
-              m0 &= m0 - 1u;
-            } else {
-              k = 32 + (int)__builtin_ctz(m1);
-              m1 &= m1 - 1u;
-            }
-            const uint32_t e = kent[k];
-            const uint2 hb = kball[k];
-            const int jc = (int)(e & 0xffu);
-            const float4 ga = s0[jc], gb = s1[jc], gc = s2[jc];
-            const float4 gd = TWO ? s3[jc] : zero4;
-            // the one-phase step on a blending lane (a_eff = alpha, g_eff = G)
-            const float dx = ga.x - pxf, dy = ga.y - pyf;
-            const float power2 = gauss_power2(ga.z, ga.w, gb.x, dx, dy);
-            const float G = __builtin_amdgcn_exp2f(power2);
-            const float alpha = fminf(GSR_ALPHA_MAX, gb.y * G);
-            const float a_eff = alpha, g_eff = G;
-            const float oma = 1.f - a_eff;
-            const float inv_1ma = fast_rcp(oma);
-            T[j] = T[j] * inv_1ma;
-            const float cd = fmaf(gc.x, dp0[j], fmaf(gc.y, dp1[j], fmaf(gc.z, dp2[j], dpa[j])));
-            float u, u1 = 0.f;
-            if (TWO) {
-              const float cd2 = fmaf(gd.x, e0[j], fmaf(gd.y, e1[j], gd.z * e2[j]));
-              u1 = g_eff * fmaf(T[j], fmaf(gb.z - Sd[j], dpd[j], cd - S[j]), inv_1ma * nbg[j]);
-              u = fmaf(g_eff, fmaf(T[j], cd2 - S2[j], inv_1ma * nbg2[j]), u1);
-              S2[j] = fmaf(a_eff, cd2, oma * S2[j]);
-            } else {
-              u = g_eff * fmaf(T[j], fmaf(gb.z - Sd[j], dpd[j], cd - S[j]), inv_1ma * nbg[j]);
-            }
-            const float w = a_eff * T[j];
-            S[j] = fmaf(a_eff, cd, oma * S[j]);
-            Sd[j] = fmaf(a_eff, gb.z, oma * Sd[j]);
-            const uint32_t rank = __builtin_amdgcn_mbcnt_hi(hb.y, __builtin_amdgcn_mbcnt_lo(hb.x, 0u));
-            hits[(int)(e >> 8) + (int)rank] = make_float4(u, u1, w, __uint_as_float((uint32_t)lane));
-          }
-          if (rest != 0ull) {
-            // list full: the finished pairs' sums now, then start over (this wave's own LDS: in-order)
-            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-            flush(j, pend);
-            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-            fill = 0;
-            pend = 0ull;
-          }
+      // candidate records in two register sets used in turn (the loop body twice, roles swapped: no register
+      // copies between steps); each step reads the next candidate's into the other set
+      int jc = (int)__builtin_ctzll(rest);
+      float4 pa = s0[jc], pb = s1[jc], pc = s2[jc];
+      float4 pd = TWO ? s3[jc] : zero4;
+      float4 ya, yb, yc, yd;
+      auto step = [&](const float4& ga, const float4& gb, const float4& gc, const float4& gd, float4& xa, float4& xb,
+                      float4& xc, float4& xd) -> bool {
+        rest &= rest - 1ull;
+        const int jn = rest != 0ull ? (int)__builtin_ctzll(rest) : jc;
+        xa = s0[jn], xb = s1[jn], xc = s2[jn];
+        xd = TWO ? s3[jn] : zero4;
+        // the replay step of k_render_bwd (replay / replay2) on this quadrant's pixel
+        const uint32_t rel = __float_as_uint(gb.w);
+        const float dx = ga.x - pxf, dy = ga.y - pyf;
+        const float power2 = gauss_power2(ga.z, ga.w, gb.x, dx, dy);
+        const float G = __builtin_amdgcn_exp2f(power2);
+        const float alpha = fminf(GSR_ALPHA_MAX, gb.y * G);
+        // (the step's blend condition as a uniform lane mask: the selects read it directly)
+        const unsigned long long hm = (__ballot(rel < last[j]) & __ballot(power2 <= 0.0f)) & __ballot(alpha >= GSR_ALPHA_MIN);
+        const bool hit = (hm >> lane) & 1ull;
+        const float a_eff = vsel(hm, alpha, 0.0f);
+        const float g_eff = vsel(hm, G, 0.0f);
+        const float oma = 1.f - a_eff;
+        const float inv_1ma = fast_rcp(oma);
+        T[j] = T[j] * inv_1ma;
+        const float cd = fmaf(gc.x, dp0[j], fmaf(gc.y, dp1[j], fmaf(gc.z, dp2[j], dpa[j])));
+        float u, u1 = 0.f;
+        if (TWO) {
+          const float cd2 = fmaf(gd.x, e0[j], fmaf(gd.y, e1[j], gd.z * e2[j]));
+          u1 = g_eff * fmaf(T[j], fmaf(gb.z - Sd[j], dpd[j], cd - S[j]), inv_1ma * nbg[j]);
+          u = fmaf(g_eff, fmaf(T[j], cd2 - S2[j], inv_1ma * nbg2[j]), u1);
+          S2[j] = fmaf(a_eff, cd2, oma * S2[j]);
+        } else {
+          u = g_eff * fmaf(T[j], fmaf(gb.z - Sd[j], dpd[j], cd - S[j]), inv_1ma * nbg[j]);
         }
-      } else {
-        // candidate records in two register sets used in turn (the loop body twice, roles swapped: no register
-        // copies between steps); each step reads the next candidate's into the other set
-        int jc = (int)__builtin_ctzll(rest);
-        float4 pa = s0[jc], pb = s1[jc], pc = s2[jc];
-        float4 pd = TWO ? s3[jc] : zero4;
-        float4 ya, yb, yc, yd;
-        auto step = [&](const float4& ga, const float4& gb, const float4& gc, const float4& gd, float4& xa, float4& xb,
-                        float4& xc, float4& xd) -> bool {
-          rest &= rest - 1ull;
-          const int jn = rest != 0ull ? (int)__builtin_ctzll(rest) : jc;
-          xa = s0[jn], xb = s1[jn], xc = s2[jn];
-          xd = TWO ? s3[jn] : zero4;
-          // the replay step of k_render_bwd (replay / replay2) on this quadrant's pixel
-          const uint32_t rel = __float_as_uint(gb.w);
-          const float dx = ga.x - pxf, dy = ga.y - pyf;
-          const float power2 = gauss_power2(ga.z, ga.w, gb.x, dx, dy);
-          const float G = __builtin_amdgcn_exp2f(power2);
-          const float alpha = fminf(GSR_ALPHA_MAX, gb.y * G);
-          // (the step's blend condition as a uniform lane mask: the selects read it directly)
-          const unsigned long long hm = (__ballot(rel < last[j]) & __ballot(power2 <= 0.0f)) & __ballot(alpha >= GSR_ALPHA_MIN);
-          const bool hit = (hm >> lane) & 1ull;
-          const float a_eff = vsel(hm, alpha, 0.0f);
-          const float g_eff = vsel(hm, G, 0.0f);
-          const float oma = 1.f - a_eff;
-          const float inv_1ma = fast_rcp(oma);
-          T[j] = T[j] * inv_1ma;
-          const float cd = fmaf(gc.x, dp0[j], fmaf(gc.y, dp1[j], fmaf(gc.z, dp2[j], dpa[j])));
-          float u, u1 = 0.f;
-          if (TWO) {
-            const float cd2 = fmaf(gd.x, e0[j], fmaf(gd.y, e1[j], gd.z * e2[j]));
-            u1 = g_eff * fmaf(T[j], fmaf(gb.z - Sd[j], dpd[j], cd - S[j]), inv_1ma * nbg[j]);
-            u = fmaf(g_eff, fmaf(T[j], cd2 - S2[j], inv_1ma * nbg2[j]), u1);
-            S2[j] = fmaf(a_eff, cd2, oma * S2[j]);
-          } else {
-            u = g_eff * fmaf(T[j], fmaf(gb.z - Sd[j], dpd[j], cd - S[j]), inv_1ma * nbg[j]);
-          }
-          const float w = a_eff * T[j];
-          S[j] = fmaf(a_eff, cd, oma * S[j]);
-          Sd[j] = fmaf(a_eff, gb.z, oma * Sd[j]);
-          const int n = __popcll(hm);
-          if (fill + n > GSR_HCAP_TW) {
-            // list full: the finished pairs' sums now, then start over (this wave's own LDS: in-order)
-            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-            flush(j, pend);
-            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-            fill = 0;
-            pend = 0ull;
-          }
-          if (hit) hits[fill + (int)mask_rank(hm)] = make_float4(u, u1, w, __uint_as_float((uint32_t)lane));
-          if (lane == 0) list[jc] = (uint32_t)fill | ((uint32_t)n << 16);
-          fill += n;
-          pend |= 1ull << jc;
-          if (rest == 0ull) return false;
-          jc = jn;
-          return true;
-        };
-        while (step(pa, pb, pc, pd, ya, yb, yc, yd) && step(ya, yb, yc, yd, pa, pb, pc, pd)) {
+        const float w = a_eff * T[j];
+        S[j] = fmaf(a_eff, cd, oma * S[j]);
+        Sd[j] = fmaf(a_eff, gb.z, oma * Sd[j]);
+        const int n = __popcll(hm);
+        if (fill + n > GSR_HCAP_TW) {
+          // list full: the finished pairs' sums now, then start over (this wave's own LDS: in-order)
+          asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+          flush(j, pend);
+          asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+          fill = 0;
+          pend = 0ull;
         }
+        if (hit) hits[fill + (int)mask_rank(hm)] = make_float4(u, u1, w, __uint_as_float((uint32_t)lane));
+        if (lane == 0) list[jc] = (uint32_t)fill | ((uint32_t)n << 16);
+        fill += n;
+        pend |= 1ull << jc;
+        if (rest == 0ull) return false;
+        jc = jn;
+        return true;
+      };
+      while (step(pa, pb, pc, pd, ya, yb, yc, yd) && step(ya, yb, yc, yd, pa, pb, pc, pd)) {
       }
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       flush(j, pend);
@@ -2401,11 +2307,6 @@ static int bwd_tw_waves() {
   const char* e = getenv("GSR_BWD_TW_WAVES");
   return e != nullptr && strcmp(e, "2") == 0 ? 2 : 1;
 }
-// the tile-wave hit-list backward's two-phase quadrant walk (GSR_BWD_TW_PHASED=1|0)
-static int bwd_tw_phased() {
-  const char* e = getenv("GSR_BWD_TW_PHASED");
-  return e != nullptr && strcmp(e, "1") == 0 ? 1 : 0;
-}
 static bool bwd_tile_wave(bool hits) {
   const char* e = getenv("GSR_BWD_KERNEL");
   if (e != nullptr && strcmp(e, "quadrant") == 0) return false;
@@ -2430,9 +2331,7 @@ void launch_render_backward(const RenderSet& rs, const GeomState& g, const uint3
                                   : (two ? k_render_bwd_tw<false, 2> : k_render_bwd_tw<false, 1>);
     g_blend_kernel[1] = rs.dpix2 != nullptr ? (two ? "k_render_bwd_tw<true, 2>" : "k_render_bwd_tw<true, 1>")
                                             : (two ? "k_render_bwd_tw<false, 2>" : "k_render_bwd_tw<false, 1>");
-    RenderSet rt = rs;
-    rt.tw_phased = bwd_tw_phased();
-    hipLaunchKernelGGL(kt, dim3(block_grid(rs, 4)), dim3(two ? 128 : 64), 0, stream, rt, (const uint2*)img.ranges,
+    hipLaunchKernelGGL(kt, dim3(block_grid(rs, 4)), dim3(two ? 128 : 64), 0, stream, rs, (const uint2*)img.ranges,
                        (const uint32_t*)img.quad_maxc, sorted_gauss, (const GaussRec*)g.rec, (const uint32_t*)g.goff,
                        (const float*)img.final_T, (const uint32_t*)img.n_contrib, dL_dcolor, dL_ddepth, dL_dalpha,
                        bw.grow, bw.reach);
