@@ -304,7 +304,8 @@ struct ImageState {
                        // (written after binning; the blends' dispatch order, gsr_render.hip block_map)
   uint32_t* split_mode;  // [0] != 0: the forward wrote the split backward's checkpoints (set_render writes it; the
                          // backward blend reads it on the device: the forward's decision, whatever the environment
-                         // says by the time the backward runs)
+                         // says by the time the backward runs); [1] != 0: the tile-wave forward wrote each
+                         // listed instance's quadrant mask (RenderSet::qbytes)
   uint32_t* split_items; // split sets: [0] count, then the tiles' later chunks (gsr_render.hip k_ckpt_suffix)
   uint32_t* split_cap;   // split sets: [V][tiles] the end of the stretch the tile's own workgroup walks
   float* ckpt;           // carved last, only for a forward that splits (with_ckpt):
@@ -316,7 +317,7 @@ struct ImageState {
     const size_t nv = (size_t)(V > 0 ? V : 1);
     const size_t tiles = (size_t)div_up(W, GSR_TILE_X) * div_up(H, GSR_TILE_Y);
     const size_t pix = (size_t)W * H;
-    s.split_mode = c.take<uint32_t>(1);
+    s.split_mode = c.take<uint32_t>(2);
     s.ranges = c.take<uint2>(nv * (tiles > 0 ? tiles : 1));
     s.quad_maxc = c.take<uint32_t>(nv * 4 * (tiles > 0 ? tiles : 1));
     s.tile_info = c.take<uint4>(nv * (tiles > 0 ? tiles : 1));

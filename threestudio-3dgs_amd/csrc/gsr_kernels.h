@@ -102,10 +102,16 @@ struct RenderSet {
   // the sorted keys when they carry the quadrant masks (TilePack::qmask; indexed like the sorted Gaussians),
   // else null
   const uint32_t* qkeys;
+  // per listed instance (indexed like the sorted Gaussians) its 4-bit quadrant mask, in the binning buffer's free
+  // ping-pong key array: the tile-wave forward writes it, the lockstep backward reads it instead of recomputing
+  // its cull when split_mode[1] says the forward wrote it
+  uint8_t* qbytes;
 };
 // backward tile splitting on for a set of V views (split_fits) whose forward takes the quadrant-wave kernel
 // (GSR_BWD_SPLIT=0 turns it off); instances = the set's K total
 bool split_on(int V, int P, int width, int height, long long instances);
+// the forward of a set takes the one-wave-per-tile kernel (k_render_fwd_tile)
+bool fwd_tile_chosen(long long instances, long long gaussians, int views);
 // the blend kernel the last forward (0) / backward (1) blend launch used, as rocprofv3 names it
 const char* blend_kernel_name(int which);
 // the forward of this set writes split checkpoints: split_on for one colour set (the two-colour backward never

@@ -537,6 +537,7 @@ __global__ __launch_bounds__(64) void k_render_fwd_tile(RenderSet rs, const uint
   const float qox[2] = {sgpr_f((float)tx0), sgpr_f((float)(tx0 + 8))};
   const float qoy[2] = {sgpr_f((float)ty0), sgpr_f((float)(ty0 + 8))};
   const uint2 range = ranges[tile];
+  uint8_t* const qbytes = rs.qbytes ? rs.qbytes + rs.inst_start[v] + range.x : nullptr;
   const int n = (int)(range.y - range.x);
   const uint32_t gmask = rs.gmask;
   const float4 zero4 = make_float4(0.f, 0.f, 0.f, 0.f);
@@ -583,6 +584,8 @@ __global__ __launch_bounds__(64) void k_render_fwd_tile(RenderSet rs, const uint
     s1[lane] = make_float4(GSR_CONIC_K_AC * r1.x, r1.y, r1.z, __uint_as_float((uint32_t)(i + 1)));
     s2[lane] = r2;
     if (C2) s3[lane] = r3;
+    if (qbytes != nullptr && i < n) qbytes[i] = (uint8_t)m;  // (the backward's cull; batches past the last
+                                                             // blend are never read by it)
     // per quadrant the batch's candidates whose mask has it (uniform, in scalar registers): the walk visits
     // the set bits of their union in order, reading each quadrant's bit with scalar ops and the next
     // candidate's staged record while the current one blends (no per-candidate LDS read of its mask)
@@ -817,6 +820,9 @@ static bool fwd_tile_kernel(long long instances, long long gaussians, int views)
   if (e != nullptr && strcmp(e, "tile") == 0) return true;
   return views >= 48 && gaussians > 0 && instances >= 3 * gaussians;
 }
+bool fwd_tile_chosen(long long instances, long long gaussians, int views) {
+  return fwd_tile_kernel(instances, gaussians, views);
+}
 // (Measured and removed, round 4 — the forward's free-running quadrant waves beat every variant that gathers a
 // record once per tile, their 5.6x redundant C5 record traffic included, profiles/r04/fwd_shared_ab.txt,
 // profiles/r04/tile_wave_ab.txt: the quadrant waves of a tile sharing one staged copy of each batch in LDS with a
@@ -1010,6 +1016,14 @@ __device__ __forceinline__ void bwd_tile(BwdLDS<TWO, HITS>& s, const RenderSet& 
   // this view's reach bit (staged candidates have rows): word v >> 5 of the Gaussian's 64 bits
   unsigned int* const reach32 = reinterpret_cast<unsigned int*>(reach) + (v >> 5);
   const unsigned int vbit = 1u << (v & 31);
+  // the tile-wave forward's per-instance quadrant masks (ImageState::split_mode[1]): the cull is read, one
+  // batch ahead, instead of recomputed (both bounds are conservative: a pair either keeps has no blend beyond
+  // the other's, so the sums agree)
+  const uint8_t* const qbm =
+      rs.qbytes != nullptr && rs.split_mode != nullptr && rs.split_mode[1] != 0u ? rs.qbytes + rs.inst_start[v] + range.x
+                                                                                 : nullptr;
+  uint32_t nqb = 0u;
+  if (qbm != nullptr && hi - 1 - lane >= lo) nqb = qbm[hi - 1 - lane];
   if (hi > lo) {
     const uint32_t g0 = fetch_index(hi);
     if (hi - 1 - cs >= lo) {
@@ -1255,6 +1269,8 @@ __device__ __forceinline__ void bwd_tile(BwdLDS<TWO, HITS>& s, const RenderSet& 
         if (h - 128 > lo) gi_next = fetch_index(h - 128);
       }
     }
+    const uint32_t qcur = nqb;
+    if (qbm != nullptr && h - 65 - lane >= lo) nqb = qbm[h - 65 - lane];
     __syncthreads();
     // this wave's quadrant: cull the staged batch, list the kept candidates, zero the others' sums
     const int rel_l = h - 1 - lane;
@@ -1262,7 +1278,9 @@ __device__ __forceinline__ void bwd_tile(BwdLDS<TWO, HITS>& s, const RenderSet& 
 #ifdef GSR_EXP_NOCULL
     if (rel_l >= lo && rel_l < qmaxc) keep = s.s0[lane].x > -1e30f;
 #else
-    if (rel_l >= lo && rel_l < qmaxc) {
+    if (qbm != nullptr) {
+      keep = rel_l >= lo && rel_l < qmaxc && ((qcur >> q) & 1u);
+    } else if (rel_l >= lo && rel_l < qmaxc) {
       // the staged conic back to (a, b, c) for the (padded, conservative) cull
       const float4 c0 = s.s0[lane], c1 = s.s1[lane];
       keep = quadrant_hit(make_float4(c0.x, c0.y, c0.z * (1.0f / GSR_CONIC_K_AC), c0.w * (1.0f / GSR_CONIC_K_B)),
