@@ -333,10 +333,13 @@ __global__ __launch_bounds__(64) void k_emit(int P, int nbe, int grid_x, GeomSta
 // rounds' keys are loaded first, neighbours come from the adjacent lanes (shuffles) and, at round
 // edges, from the neighbouring round (readlane).
 #define GSR_RANGE_ROUNDS 16
-// A block covers GSR_RANGE_TILE instances: each wave GSR_RANGE_CHUNKS consecutive chunks of 64 x
-// GSR_RANGE_ROUNDS (fewer, longer-lived workgroups: the launch was bound by workgroup dispatch, 2.6 TB/s).
-#define GSR_RANGE_CHUNKS (GSR_RANGE_TILE / (4 * 64 * GSR_RANGE_ROUNDS))
-__global__ __launch_bounds__(256) void k_tile_ranges(SegInfo inst, int n_tiles, int gbits, uint32_t tmask,
+// A block covers `chunks` x 4096 instances: each wave `chunks` consecutive chunks of 64 x GSR_RANGE_ROUNDS.
+// Large sets take GSR_RANGE_TILE per block (fewer, longer-lived workgroups: the 64-view launch was bound by
+// workgroup dispatch, 2.6 TB/s); a set with few instances (one view: ~5M) one chunk per wave, so its few
+// blocks do not walk their chunks one after the other (launch_tile_ranges).
+#define GSR_RANGE_CHUNK_ITEMS (4 * 64 * GSR_RANGE_ROUNDS)
+#define GSR_RANGE_CHUNKS (GSR_RANGE_TILE / GSR_RANGE_CHUNK_ITEMS)
+__global__ __launch_bounds__(256) void k_tile_ranges(SegInfo inst, int n_tiles, int gbits, uint32_t tmask, int chunks,
                                                      const uint32_t* __restrict__ keys,
                                                      uint2* __restrict__ ranges) {
   uint32_t lb;
@@ -346,8 +349,8 @@ __global__ __launch_bounds__(256) void k_tile_ranges(SegInfo inst, int n_tiles, 
   const uint32_t* kv = keys + inst.start[v];
   uint2* rv = ranges + (size_t)v * n_tiles;
 #pragma unroll 1
-  for (int ch = 0; ch < GSR_RANGE_CHUNKS; ++ch) {
-  const uint32_t base = ((lb * 4 + (threadIdx.x >> 6)) * GSR_RANGE_CHUNKS + ch) * (64u * GSR_RANGE_ROUNDS);
+  for (int ch = 0; ch < chunks; ++ch) {
+  const uint32_t base = ((lb * 4 + (threadIdx.x >> 6)) * (uint32_t)chunks + ch) * (64u * GSR_RANGE_ROUNDS);
   if (base >= K) return;  // wave-uniform
   uint32_t t[GSR_RANGE_ROUNDS];
 #pragma unroll
@@ -403,10 +406,14 @@ void launch_emit(int V, int P, int W, const GeomState& g, const SegInfo& inst, c
 
 void launch_tile_ranges(SegInfo inst, int n_tiles, const TilePack& tp, const uint32_t* keys, uint2* ranges,
                         hipStream_t stream) {
-  seg_fill_blocks(inst, GSR_RANGE_TILE);
+  // one chunk per wave while that gives at most 8192 blocks (a few views), else GSR_RANGE_CHUNKS
+  long long total = 0;
+  for (int v = 0; v < inst.V; ++v) total += inst.n[v];
+  const int chunks = total <= 8192ll * GSR_RANGE_CHUNK_ITEMS ? 1 : GSR_RANGE_CHUNKS;
+  seg_fill_blocks(inst, chunks * GSR_RANGE_CHUNK_ITEMS);
   if (inst.blk[inst.V] == 0) return;
   hipLaunchKernelGGL(k_tile_ranges, dim3(inst.blk[inst.V]), dim3(256), 0, stream, inst, n_tiles, tp.gbits, tp.tmask,
-                     keys, ranges);
+                     chunks, keys, ranges);
 }
 
 // markVisible / checkFrustum of the reference (API completeness).
