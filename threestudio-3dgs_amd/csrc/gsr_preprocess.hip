@@ -48,13 +48,17 @@ __global__ __launch_bounds__(256) void k_preprocess(PreprocessArgs a, SetCams ca
     // coalesced 16-byte loads of the block's contiguous SH slice (256 * 3M floats, 16-B aligned)
     const int n = min(GSR_PRE_GAUSS, a.P - idx0) * nsh;
     const float4* src = reinterpret_cast<const float4*>(a.shs + (size_t)idx0 * nsh);
+    // (row = e / nsh through a float reciprocal: exact for e < 2^14, and a few instructions instead of an
+    // integer division per element — it matters for one-view launches, where the staging is not amortised)
+    const float inv_nsh = 1.0f / (float)nsh;
     for (int e4 = t; e4 * 4 < n; e4 += 256) {
       const float4 q = src[e4];
       const float qv[4] = {q.x, q.y, q.z, q.w};
 #pragma unroll
       for (int k = 0; k < 4; ++k) {
         const int e = 4 * e4 + k;
-        if (e < n) s_sh[(e / nsh) * sstride + e % nsh] = qv[k];
+        const int r = (int)(((float)e + 0.5f) * inv_nsh);
+        if (e < n) s_sh[r * sstride + (e - r * nsh)] = qv[k];
       }
     }
     __syncthreads();
