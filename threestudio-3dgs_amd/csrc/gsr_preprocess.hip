@@ -31,22 +31,19 @@ void launch_preprocess_kernel(const PreprocessArgs& a, const SetCams& cams, cons
 __attribute__((amdgpu_waves_per_eu(6, 8)))
 __global__ __launch_bounds__(256) void k_preprocess(PreprocessArgs a, SetCams cams, GeomState g) {
   extern __shared__ float s_sh[];  // [128][3M + 1] this block's SH coefficients (odd stride)
-  // one-view launches (the per-view drop-in path): 256 Gaussians per block, one thread each, SH rows read from
-  // HBM (the view halves would leave half the threads idle, and the staging would buy nothing for one view)
-  const bool one = a.V == 1;
   const int nvc = (a.V + GSR_PRE_VIEWS - 1) / GSR_PRE_VIEWS;
-  const int vc = one ? 0 : blockIdx.x % nvc;
-  const int idx0 = one ? blockIdx.x * 256 : (blockIdx.x / nvc) * GSR_PRE_GAUSS;
+  const int vc = blockIdx.x % nvc;
+  const int idx0 = (blockIdx.x / nvc) * GSR_PRE_GAUSS;
   const int t = threadIdx.x;
-  const int gl = one ? t : t % GSR_PRE_GAUSS;
-  const int half = one ? 0 : __builtin_amdgcn_readfirstlane(t / GSR_PRE_GAUSS);  // wave-uniform: scalar camera loads
+  const int gl = t % GSR_PRE_GAUSS;
+  const int half = __builtin_amdgcn_readfirstlane(t / GSR_PRE_GAUSS);  // wave-uniform: scalar camera loads
   const int idx = idx0 + gl;
   const int vb = vc * GSR_PRE_VIEWS, ve = min(a.V, vb + GSR_PRE_VIEWS);
   const int vh = (ve - vb + 1) / 2;
-  const int v0 = one ? 0 : vb + half * vh, v1 = one ? 1 : (half == 0 ? min(ve, vb + vh) : ve);
+  const int v0 = vb + half * vh, v1 = half == 0 ? min(ve, vb + vh) : ve;
   const int nsh = a.colors_precomp == nullptr ? 3 * a.M : 0;
   const int sstride = nsh + 1;
-  const bool staged = !one && nsh > 0 && GSR_PRE_GAUSS * sstride <= GSR_PRE_LDS_FLOATS;
+  const bool staged = nsh > 0 && GSR_PRE_GAUSS * sstride <= GSR_PRE_LDS_FLOATS;
   if (staged) {
     // coalesced 16-byte loads of the block's contiguous SH slice (256 * 3M floats, 16-B aligned)
     const int n = min(GSR_PRE_GAUSS, a.P - idx0) * nsh;
@@ -219,9 +216,9 @@ void launch_preprocess(const PreprocessArgs& a, const SetCams& cams, const GeomS
 void launch_preprocess_kernel(const PreprocessArgs& a, const SetCams& cams, const GeomState& g, hipStream_t stream) {
   const int nvc = (a.V + GSR_PRE_VIEWS - 1) / GSR_PRE_VIEWS;
   const size_t want = a.colors_precomp == nullptr ? (size_t)GSR_PRE_GAUSS * (3 * a.M + 1) : 0;
-  const size_t lds = a.V == 1 ? 0 : (want <= GSR_PRE_LDS_FLOATS ? sizeof(float) * want : 0);
-  const int blocks = a.V == 1 ? (a.P + 255) / 256 : nvc * ((a.P + GSR_PRE_GAUSS - 1) / GSR_PRE_GAUSS);
-  hipLaunchKernelGGL(k_preprocess, dim3(blocks), dim3(256), lds, stream, a, cams, g);
+  const size_t lds = want <= GSR_PRE_LDS_FLOATS ? sizeof(float) * want : 0;
+  hipLaunchKernelGGL(k_preprocess, dim3(nvc * ((a.P + GSR_PRE_GAUSS - 1) / GSR_PRE_GAUSS)), dim3(256), lds, stream, a,
+                     cams, g);
 }
 
 }  // namespace gsr
