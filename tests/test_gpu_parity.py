@@ -259,7 +259,7 @@ def test_batched_views_match_per_view(nviews, monkeypatch):
         assert err <= 1e-5 * scale, f"{k}: {err} vs scale {scale}"
 
 
-@pytest.mark.parametrize("switch", ["fwd_kernel", "dispatch_order", "bwd_kernel", "tile_keys"])
+@pytest.mark.parametrize("switch", ["fwd_kernel", "dispatch_order", "bwd_kernel", "tile_keys", "tile_sort_bits"])
 @pytest.mark.parametrize("kind", ["ball_composite", "sugar_two_colors"])
 def test_forward_kernels_bitwise(kind, switch, monkeypatch):
     """fwd_kernel: the one-wave-per-tile forward and the quadrant-wave forward (GSR_FWD_KERNEL) blend exactly
@@ -299,6 +299,12 @@ def test_forward_kernels_bitwise(kind, switch, monkeypatch):
             monkeypatch.setenv("GSR_BWD_KERNEL", "tile" if kernel.startswith("tile") else "quadrant")
             # (hit lists: one or two waves per tile, GSR_BWD_TW_WAVES)
             monkeypatch.setenv("GSR_BWD_TW_WAVES", "2" if kernel.startswith("tile2") else "1")
+        elif switch == "tile_sort_bits":
+            # the stable tile sort in 3 passes of 4 bits instead of 2 of 6: the same lists
+            if kernel == "tile":
+                monkeypatch.delenv("GSR_TILE_SORT_BITS", raising=False)
+            else:
+                monkeypatch.setenv("GSR_TILE_SORT_BITS", "4")
         elif switch == "tile_keys":
             if kernel == "tile":
                 monkeypatch.delenv("GSR_TILE_KEYS", raising=False)

@@ -96,7 +96,7 @@ static int effective_degree(int degree, int M) {
 }
 
 // ping-pong buffers holding the sorts' results (one pass per <= 8 key bits)
-static int tile_sort_result(int W, int H) { return digit_plan(tile_key_bits(W, H)).passes & 1; }
+static int tile_sort_result(int W, int H) { return digit_plan(tile_key_bits(W, H), tile_sort_bits()).passes & 1; }
 static int depth_sort_result() { return digit_plan(32).passes & 1; }
 
 static GaussBackwardArgs shared_args(int P, int degree, int M, const float* means3D, const float* scales,
@@ -526,7 +526,8 @@ static int set_render(int V, int P, const int* K, int width, int height, const f
     GSR_HIP_CHECK(hipMemsetAsync(img.ranges, 0, sizeof(uint2) * (size_t)V * gx * gy, s));
     if (total > 0) {
       launch_emit(V, P, width, g, inst, tp, b.key[0], b.val[0], s);
-      const int res = seg_sort(b.key, b.val, false, inst, tp.gbits, tp.tile_bits, b.sort_counts, b.sort_totals, s);
+      const int res = seg_sort(b.key, b.val, false, inst, tp.gbits, tp.tile_bits, b.sort_counts, b.sort_totals, s,
+                               tile_sort_bits());
       if (res != tres) return fail(GSR_EHIP, "%s", "internal: tile sort buffer");
       launch_tile_ranges(inst, gx * gy, tp, b.key[res], img.ranges, s);
     }

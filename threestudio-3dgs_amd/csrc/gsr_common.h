@@ -114,14 +114,21 @@ struct DigitPlan {
     return key_bits - lo < bits ? key_bits - lo : bits;
   }
 };
-static inline DigitPlan digit_plan(int key_bits) {
+static inline DigitPlan digit_plan(int key_bits, int max_bits = GSR_RADIX_BITS) {
   if (key_bits < 1) key_bits = 1;
+  if (max_bits < 1 || max_bits > GSR_RADIX_BITS) max_bits = GSR_RADIX_BITS;
   DigitPlan d;
-  d.passes = (key_bits + GSR_RADIX_BITS - 1) / GSR_RADIX_BITS;
+  d.passes = (key_bits + max_bits - 1) / max_bits;
   d.bits = (key_bits + d.passes - 1) / d.passes;
   return d;
 }
-
+// widest digit of the tile sort (GSR_TILE_SORT_BITS, A/B; default GSR_RADIX_BITS: a 12-bit tile id in 2 passes of 6,
+// 8 bits or fewer in one pass)
+static inline int tile_sort_bits() {
+  const char* e = getenv("GSR_TILE_SORT_BITS");
+  const int b = e != nullptr ? atoi(e) : GSR_RADIX_BITS;
+  return b >= 2 && b <= GSR_RADIX_BITS ? b : GSR_RADIX_BITS;
+}
 // Segments of a view set (kernel argument): segment v = items [start[v], start[v] + n[v]) of a
 // flat array, cut into blocks of `tile` items; blocks of segment v are [blk[v], blk[v+1]).
 // Item counts of a set stay below 2^32 (checked on the host).

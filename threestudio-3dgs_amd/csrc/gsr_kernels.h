@@ -13,7 +13,7 @@ namespace gsr {
 // vals == nullptr or vals[0] == nullptr (and not identity): keys only.  counts needs
 // RADIX x (total 4096-item blocks) words, totals RADIX x V.
 int seg_sort(uint32_t* keys[2], uint32_t* vals[2], bool vals_identity, SegInfo seg, int bit_lo, int key_bits,
-             uint32_t* counts, uint32_t* totals, hipStream_t stream);
+             uint32_t* counts, uint32_t* totals, hipStream_t stream, int max_bits = GSR_RADIX_BITS);
 
 // Forward preprocess (cull, project, EWA, SH) of every (view, Gaussian) — gsr_preprocess.hip
 struct PreprocessArgs {

@@ -208,9 +208,9 @@ static void launch_pass(bool kv, const uint32_t* kin, const uint32_t* vin, uint3
 }
 
 int seg_sort(uint32_t* keys[2], uint32_t* vals[2], bool vals_identity, SegInfo seg, int bit_lo, int key_bits,
-             uint32_t* counts, uint32_t* totals, hipStream_t stream) {
+             uint32_t* counts, uint32_t* totals, hipStream_t stream, int max_bits) {
   const bool kv = vals != nullptr && (vals[0] != nullptr || vals_identity);
-  const DigitPlan plan = digit_plan(key_bits);
+  const DigitPlan plan = digit_plan(key_bits, max_bits);
   seg_fill_blocks(seg, GSR_SORT_TILE);
   const uint32_t nb = seg.blk[seg.V];
   int src = 0;
@@ -226,6 +226,8 @@ int seg_sort(uint32_t* keys[2], uint32_t* vals[2], bool vals_identity, SegInfo s
         launch_pass<8>(kv, keys[src], vin, keys[dst], vout, seg, nb, shift, bits, last, counts, totals, stream);
       else if (bits == 6)
         launch_pass<6>(kv, keys[src], vin, keys[dst], vout, seg, nb, shift, bits, last, counts, totals, stream);
+      else if (bits == 4)
+        launch_pass<4>(kv, keys[src], vin, keys[dst], vout, seg, nb, shift, bits, last, counts, totals, stream);
       else
         launch_pass<0>(kv, keys[src], vin, keys[dst], vout, seg, nb, shift, bits, last, counts, totals, stream);
     }
