@@ -18,7 +18,9 @@ HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 # stated at the kernel's attribute: the one-colour tile-wave forward at 6 waves per SIMD spills outside
 # the candidate loop (gsr_render.hip, profiles/r02_fwd_occupancy_ab.txt); the two-colour per-Gaussian
 # backward at 4 waves per SIMD spills outside the row loop (gsr_backward.hip, C5 only)
-ALLOWED_VGPR_SPILL = {"17k_render_fwd_tileILb0E": 3, "11k_view_gradILb1E": 4}
+# The lockstep backward at 5 waves per SIMD spills one VGPR, stored before and reloaded after its batch loop
+# (the forward masks' prefetch register; measured faster, profiles/r04/blend_loops_ab.txt session r04k).
+ALLOWED_VGPR_SPILL = {"17k_render_fwd_tileILb0E": 3, "11k_view_gradILb1E": 4, "12k_render_bwdILb0ELb0E": 1}
 
 
 def kernel_resources(src, tmp_path):
