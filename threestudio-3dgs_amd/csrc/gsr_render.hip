@@ -124,6 +124,8 @@ __device__ __forceinline__ float vsel(unsigned long long m, float if_set, float 
   return r;
 }
 
+typedef float f2 __attribute__((ext_vector_type(2)));  // packed fp32 pairs (v_pk_*_f32)
+
 // a wave-uniform float kept in a scalar register
 __device__ __forceinline__ float sgpr_f(float x) {
   float r;
@@ -183,12 +185,17 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(GSR_FWD_WPE,
   const int px = qx0 + (lane & 7), py = qy0 + (lane >> 3);
   const bool inside = px < W && py < H;
   const float pxf = (float)px, pyf = (float)py;
+  const f2 pxy = {pxf, pyf};
   const uint2 range = ranges[tile];
   const int n = (int)(range.y - range.x);
 
   unsigned long long dmk = __ballot(!inside);  // lanes whose pixel is done (outside, or terminated)
-  float T = 1.0f, Cr = 0.f, Cg = 0.f, Cb = 0.f, D = 0.f;
-  float Er = 0.f, Eg = 0.f, Eb = 0.f;  // second colour (C2)
+  // running totals, packed in pairs (v_pk_fma_f32: two exact fmas per instruction): (r, g), (b, depth), second
+  // colour (r, g) and b
+  float T = 1.0f;
+  f2 CrCg = {0.f, 0.f}, CbD = {0.f, 0.f};
+  f2 ErEg = {0.f, 0.f};  // second colour (C2)
+  float Eb = 0.f;
   uint32_t last_contributor = 0;
 #ifdef GSR_TIMELINE
   unsigned long long pc_eval = 0, pc_slot = 0;
@@ -226,16 +233,18 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(GSR_FWD_WPE,
   float* const ckpt = CK ? rs.ckpt + ckpt_offset((size_t)(rs.v0 + v), (size_t)rs.gx * rs.gy, tile, 0) : nullptr;
   const int cpix = 64 * q + lane;
   if (CK && blockIdx.x == 0 && lane == 0) rs.split_items[0] = 0u;  // k_ckpt_suffix lists the split items
-  float Pr = 0.f, Pg = 0.f, Pb = 0.f, Pd = 0.f;
+  f2 PrPg = {0.f, 0.f}, PbPd = {0.f, 0.f};
   int chunk = 0;
   for (int base = 0; base < n; base += 64) {
     if (dmk == ~0ull) break;
     if (CK && base > 0 && base % GSR_SPLIT_CH == 0 && base <= GSR_SPLIT_NCK * GSR_SPLIT_CH) {
       // chunk `chunk` ends: its sums into its slot, T into the next one's slot
-      reinterpret_cast<float4*>(ckpt + (size_t)chunk * GSR_CKPT_FIELDS * 256 + 256)[cpix] = make_float4(Pr, Pg, Pb, Pd);
+      reinterpret_cast<float4*>(ckpt + (size_t)chunk * GSR_CKPT_FIELDS * 256 + 256)[cpix] =
+          make_float4(PrPg.x, PrPg.y, PbPd.x, PbPd.y);
       ++chunk;
       ckpt[(size_t)chunk * GSR_CKPT_FIELDS * 256 + cpix] = T;
-      Pr = Pg = Pb = Pd = 0.f;
+      PrPg = f2{0.f, 0.f};
+      PbPd = f2{0.f, 0.f};
     }
     const int i = base + lane;
     const float4 r0 = n0, r1 = n1, r2 = n2, r3 = n3;
@@ -262,11 +271,12 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(GSR_FWD_WPE,
     const unsigned long long bal = __ballot(keep);
     const int cnt = __popcll(bal);
     if (keep) {
-      // the conic pre-multiplied for gauss_power2 (.w of s1: 1 + list position)
+      // the conic pre-multiplied for gauss_power2, staged as s0 = (x, y, B, C), s1 = (A, opacity, depth, 1 + list
+      // position), s2 = (r, g, b, depth): the pairs the step packs are adjacent
       const uint32_t pos = mask_rank(bal);
-      s0[pos] = make_float4(r0.x, r0.y, GSR_CONIC_K_AC * r0.z, GSR_CONIC_K_B * r0.w);
-      s1[pos] = make_float4(GSR_CONIC_K_AC * r1.x, r1.y, r1.z, __uint_as_float((uint32_t)(i + 1)));
-      s2[pos] = r2;
+      s0[pos] = make_float4(r0.x, r0.y, GSR_CONIC_K_B * r0.w, GSR_CONIC_K_AC * r1.x);
+      s1[pos] = make_float4(GSR_CONIC_K_AC * r0.z, r1.y, r1.z, __uint_as_float((uint32_t)(i + 1)));
+      s2[pos] = make_float4(r2.x, r2.y, r2.z, r1.z);
       if (C2) s3[pos] = r3;
     }
     __syncthreads();
@@ -281,8 +291,10 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(GSR_FWD_WPE,
 #if GSR_FWD_PREFETCH
       asm volatile("" ::: "memory");  // (the next candidate's reads stay ahead of this step: a prefetch)
 #endif
-      const float dx = a.x - pxf, dy = a.y - pyf;
-      const float power2 = gauss_power2(a.z, a.w, b.x, dx, dy);  // log2(e) * power
+      // gauss_power2(A, B, C, dx, dy) = fma(dx, fma(A, dx, B dy), (C dy) dy), with (B dy, C dy) as one product
+      const f2 dd = f2{a.x, a.y} - pxy;
+      const f2 bc = f2{a.z, a.w} * f2{dd.y, dd.y};
+      const float power2 = fmaf(dd.x, fmaf(b.x, dd.x, bc.x), bc.y * dd.y);  // log2(e) * power
       const float alpha = fminf(GSR_ALPHA_MAX, b.y * __builtin_amdgcn_exp2f(power2));
 #ifdef GSR_TIMELINE
       pc_eval += (dmk >> lane) & 1ull ? 0ull : 1ull;
@@ -297,19 +309,15 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(GSR_FWD_WPE,
       const float aT = a_eff * T;
       // the running totals in list order whatever the launch (the outputs' bits do not depend on whether the
       // launch writes checkpoints), and beside them the chunk's own sums for the split backward
-      Cr = fmaf(c.x, aT, Cr);
-      Cg = fmaf(c.y, aT, Cg);
-      Cb = fmaf(c.z, aT, Cb);
-      D = fmaf(b.z, aT, D);
+      const f2 aT2 = {aT, aT};
+      CrCg = __builtin_elementwise_fma(f2{c.x, c.y}, aT2, CrCg);
+      CbD = __builtin_elementwise_fma(f2{c.z, c.w}, aT2, CbD);
       if (CK) {
-        Pr = fmaf(c.x, aT, Pr);
-        Pg = fmaf(c.y, aT, Pg);
-        Pb = fmaf(c.z, aT, Pb);
-        Pd = fmaf(b.z, aT, Pd);
+        PrPg = __builtin_elementwise_fma(f2{c.x, c.y}, aT2, PrPg);
+        PbPd = __builtin_elementwise_fma(f2{c.z, c.w}, aT2, PbPd);
       }
       if (C2) {
-        Er = fmaf(e.x, aT, Er);
-        Eg = fmaf(e.y, aT, Eg);
+        ErEg = __builtin_elementwise_fma(f2{e.x, e.y}, aT2, ErEg);
         Eb = fmaf(e.z, aT, Eb);
       }
       T = vsel(blendm, test_T, T);  // = T (1 - a_eff)
@@ -331,6 +339,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(GSR_FWD_WPE,
     const size_t HW = (size_t)H * W;
     final_T[pid] = T;
     n_contrib[pid] = last_contributor;
+    const float Cr = CrCg.x, Cg = CrCg.y, Cb = CbD.x, D = CbD.y;
     {
       // C + T bg as a rounded product then a rounded sum (the oracle's order, and the same value the fused
       // composite below starts from), never contracted: every instantiation stores the same bits
@@ -344,8 +353,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(GSR_FWD_WPE,
     if (C2) {
 #pragma clang fp contract(off)
       float* o2 = rs.out_col2 + (size_t)(rs.v0 + v) * 3 * HW + pid;
-      o2[0] = Er + T * bg[0];
-      o2[HW] = Eg + T * bg[1];
+      o2[0] = ErEg.x + T * bg[0];
+      o2[HW] = ErEg.y + T * bg[1];
       o2[2 * HW] = Eb + T * bg[2];
     }
     if (rs.cbg != nullptr) {
@@ -361,7 +370,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(GSR_FWD_WPE,
   }
   if (CK && chunk > 0) {
     // the chunk the walk ended in (the backward reads chunks up to the quadrant's deepest blend only)
-    reinterpret_cast<float4*>(ckpt + (size_t)chunk * GSR_CKPT_FIELDS * 256 + 256)[cpix] = make_float4(Pr, Pg, Pb, Pd);
+    reinterpret_cast<float4*>(ckpt + (size_t)chunk * GSR_CKPT_FIELDS * 256 + 256)[cpix] =
+        make_float4(PrPg.x, PrPg.y, PbPd.x, PbPd.y);
   }
   uint32_t mc = last_contributor;
 #pragma unroll
@@ -515,7 +525,10 @@ __global__ __launch_bounds__(64) void k_render_fwd_tile(RenderSet rs, const uint
   const float* bg = rs.bg[v];
   const int lane = threadIdx.x;
   const int tx0 = (tile % grid_x) * GSR_TILE_X, ty0 = (tile / grid_x) * GSR_TILE_Y;
-  float pxf[4], pyf[4], T[4], Cr[4], Cg[4], Cb[4], D[4], Er[4], Eg[4], Eb[4];
+  // per quadrant: the pixel, T, and the running totals packed in pairs (v_pk_fma_f32): (r, g), (b, depth),
+  // second colour (r, g) and b
+  float T[4], Eb[4];
+  f2 pxy[4], CrCg[4], CbD[4], ErEg[4];
   uint32_t last[4];
   bool inside[4];
   // per quadrant the lanes whose pixel is done (outside the image, or terminated): uniform 64-bit masks, so the
@@ -526,11 +539,10 @@ __global__ __launch_bounds__(64) void k_render_fwd_tile(RenderSet rs, const uint
     const int px = tx0 + (q & 1) * 8 + (lane & 7), py = ty0 + (q >> 1) * 8 + (lane >> 3);
     inside[q] = px < W && py < H;
     dm[q] = __ballot(!inside[q]);
-    pxf[q] = (float)px;
-    pyf[q] = (float)py;
+    pxy[q] = f2{(float)px, (float)py};
     T[q] = 1.0f;
-    Cr[q] = Cg[q] = Cb[q] = D[q] = 0.f;
-    Er[q] = Eg[q] = Eb[q] = 0.f;
+    CrCg[q] = CbD[q] = ErEg[q] = f2{0.f, 0.f};
+    Eb[q] = 0.f;
     last[q] = 0u;
   }
   // the quadrant origins of the cull (wave-uniform: held in scalar registers, not reloaded from spill slots)
@@ -579,10 +591,11 @@ __global__ __launch_bounds__(64) void k_render_fwd_tile(RenderSet rs, const uint
       for (int q = 0; q < 4; ++q)
         m |= quadrant_hit(r0, r1, qox[q & 1], qoy[q >> 1]) ? (1u << q) : 0u;
     }
-    // the conic pre-multiplied for gauss_power2 (.w of s1: 1 + list position)
-    s0[lane] = make_float4(r0.x, r0.y, GSR_CONIC_K_AC * r0.z, GSR_CONIC_K_B * r0.w);
-    s1[lane] = make_float4(GSR_CONIC_K_AC * r1.x, r1.y, r1.z, __uint_as_float((uint32_t)(i + 1)));
-    s2[lane] = r2;
+    // the conic pre-multiplied for gauss_power2, staged as s0 = (x, y, B, C), s1 = (A, opacity, depth, 1 + list
+    // position), s2 = (r, g, b, depth): the pairs the step packs are adjacent (as k_render_fwd)
+    s0[lane] = make_float4(r0.x, r0.y, GSR_CONIC_K_B * r0.w, GSR_CONIC_K_AC * r1.x);
+    s1[lane] = make_float4(GSR_CONIC_K_AC * r0.z, r1.y, r1.z, __uint_as_float((uint32_t)(i + 1)));
+    s2[lane] = make_float4(r2.x, r2.y, r2.z, r1.z);
     if (C2) s3[lane] = r3;
     if (qbytes != nullptr && i < n) qbytes[i] = (uint8_t)m;  // (the backward's cull; batches past the last
                                                              // blend are never read by it)
@@ -632,8 +645,8 @@ __global__ __launch_bounds__(64) void k_render_fwd_tile(RenderSet rs, const uint
           pc_eval += (dm[q] >> lane) & 1ull ? 0ull : 1ull;
           pc_slot += 1ull;
 #endif
-          const float dx = a.x - pxf[q], dy = a.y - pyf[q];
-          const float power2 = gauss_power2(a.z, a.w, b.x, dx, dy);  // log2(e) * power
+          const float dx = a.x - pxy[q].x, dy = a.y - pxy[q].y;
+          const float power2 = fmaf(dx, fmaf(b.x, dx, a.z * dy), (a.w * dy) * dy);  // log2(e) * power
           const float alpha = fminf(GSR_ALPHA_MAX, b.y * __builtin_amdgcn_exp2f(power2));
           const unsigned long long okm = (__ballot(power2 <= 0.0f) & __ballot(alpha >= GSR_ALPHA_MIN)) & ~dm[q];
           const float test_T = T[q] * (1.0f - alpha);
@@ -641,13 +654,11 @@ __global__ __launch_bounds__(64) void k_render_fwd_tile(RenderSet rs, const uint
           const unsigned long long blendm = okm & ~termm;
           const float a_eff = vsel(blendm, alpha, 0.0f);
           const float aT = a_eff * T[q];
-          Cr[q] = fmaf(c.x, aT, Cr[q]);
-          Cg[q] = fmaf(c.y, aT, Cg[q]);
-          Cb[q] = fmaf(c.z, aT, Cb[q]);
-          D[q] = fmaf(b.z, aT, D[q]);
+          const f2 aT2 = {aT, aT};
+          CrCg[q] = __builtin_elementwise_fma(f2{c.x, c.y}, aT2, CrCg[q]);
+          CbD[q] = __builtin_elementwise_fma(f2{c.z, c.w}, aT2, CbD[q]);
           if (C2) {
-            Er[q] = fmaf(e.x, aT, Er[q]);
-            Eg[q] = fmaf(e.y, aT, Eg[q]);
+            ErEg[q] = __builtin_elementwise_fma(f2{e.x, e.y}, aT2, ErEg[q]);
             Eb[q] = fmaf(e.z, aT, Eb[q]);
           }
           T[q] = vsel(blendm, test_T, T[q]);
@@ -678,17 +689,17 @@ __global__ __launch_bounds__(64) void k_render_fwd_tile(RenderSet rs, const uint
       n_contrib[pid] = last[q];
       {
 #pragma clang fp contract(off)
-        out_color[pid] = Cr[q] + Tq * bg[0];
-        out_color[HWs + pid] = Cg[q] + Tq * bg[1];
-        out_color[2 * HWs + pid] = Cb[q] + Tq * bg[2];
+        out_color[pid] = CrCg[q].x + Tq * bg[0];
+        out_color[HWs + pid] = CrCg[q].y + Tq * bg[1];
+        out_color[2 * HWs + pid] = CbD[q].x + Tq * bg[2];
       }
-      out_depth[pid] = D[q];
+      out_depth[pid] = CbD[q].y;
       out_alpha[pid] = 1.0f - Tq;
       if (C2) {
 #pragma clang fp contract(off)
         float* o2 = rs.out_col2 + (size_t)(rs.v0 + v) * 3 * HWs + pid;
-        o2[0] = Er[q] + Tq * bg[0];
-        o2[HWs] = Eg[q] + Tq * bg[1];
+        o2[0] = ErEg[q].x + Tq * bg[0];
+        o2[HWs] = ErEg[q].y + Tq * bg[1];
         o2[2 * HWs] = Eb[q] + Tq * bg[2];
       }
       if (rs.cbg != nullptr) {
@@ -696,9 +707,9 @@ __global__ __launch_bounds__(64) void k_render_fwd_tile(RenderSet rs, const uint
         const float am = 1.0f - (1.0f - Tq);
         const float* bgi = rs.cbg + ((size_t)v * HWs + pid) * 3;
         float* cp = rs.comp + (size_t)v * 3 * HWs + pid;
-        cp[0] = fminf(fmaxf((Cr[q] + Tq * bg[0]) + am * bgi[0], 0.0f), 1.0f);
-        cp[HWs] = fminf(fmaxf((Cg[q] + Tq * bg[1]) + am * bgi[1], 0.0f), 1.0f);
-        cp[2 * HWs] = fminf(fmaxf((Cb[q] + Tq * bg[2]) + am * bgi[2], 0.0f), 1.0f);
+        cp[0] = fminf(fmaxf((CrCg[q].x + Tq * bg[0]) + am * bgi[0], 0.0f), 1.0f);
+        cp[HWs] = fminf(fmaxf((CrCg[q].y + Tq * bg[1]) + am * bgi[1], 0.0f), 1.0f);
+        cp[2 * HWs] = fminf(fmaxf((CbD[q].x + Tq * bg[2]) + am * bgi[2], 0.0f), 1.0f);
       }
     }
     uint32_t mc = last[q];
