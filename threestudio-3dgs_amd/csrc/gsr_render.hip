@@ -1635,7 +1635,7 @@ __global__ __launch_bounds__(64 * NW) void k_render_bwd_tw(
   constexpr int NQ = 4 / NW;            // quadrants per wave
   static_assert(NW == 1 || NW == 2, "one or two waves per tile");
   __shared__ float4 s0[65], s1[65], s2[65];
-  __shared__ float4 s3[TWO ? 65 : 1];
+  __shared__ float4 s3[65];  // (b, b2) of the interleaved colours
   __shared__ uint32_t slot[64];
   __shared__ uint32_t skeep[NW > 1 ? 64 : 1];          // the cull's 4-bit quadrant masks (NW = 2)
   __shared__ float sacc[NW > 1 ? NM * 64 : 1];          // wave 1's (q2 + q3) moments (NW = 2)
@@ -1676,9 +1676,12 @@ __global__ __launch_bounds__(64 * NW) void k_render_bwd_tw(
   const int hi = __builtin_amdgcn_readfirstlane((int)max(max(qm.x, qm.y), max(qm.z, qm.w)));
   const int lo = 0;
 
-  // per pixel (one per quadrant of this wave) the replay state and the pixel's upstream gradients
-  float T[NQ], S[NQ], Sd[NQ], S2[NQ], dp0[NQ], dp1[NQ], dp2[NQ], dpd[NQ], dpa[NQ], e0[NQ], e1[NQ], e2[NQ], nbg[NQ],
-      nbg2[NQ];
+  // per pixel (one per quadrant of this wave) the replay state and the pixel's upstream gradients, the two colours'
+  // terms packed in pairs for v_pk_*_f32 (two exact operations per instruction): de_k = (dL/dpix_k, dL/dpix2_k),
+  // dpa0 = (dL/dalpha term, -0: the second colour's chain starts with a product, fma(x, y, -0) = x y exactly),
+  // nbgs = the two background terms, SS2 = (S, S2)
+  float T[NQ], Sd[NQ], dpd[NQ];
+  f2 de0[NQ], de1[NQ], de2[NQ], dpa0[NQ], nbgs[NQ], SS2[NQ];
   uint32_t last[NQ];
   const float lxf = (float)(txi * GSR_TILE_X + (lane & 7)), lyf = (float)(tyi * GSR_TILE_Y + (lane >> 3));
 #pragma unroll
@@ -1716,17 +1719,21 @@ __global__ __launch_bounds__(64 * NW) void k_render_bwd_tw(
         da = dsum + da;
       }
     }
-    dp0[j] = d[0], dp1[j] = d[1], dp2[j] = d[2], dpd[j] = dd, dpa[j] = da;
-    nbg[j] = -T_final * bg_dot3(bg, d[0], d[1], d[2]);
-    e0[j] = e1[j] = e2[j] = 0.f;
+    float e[3] = {0.f, 0.f, 0.f};
     if (TWO && inside) {
       const float* d2 = rs.dpix2 + (size_t)v * 3 * HW;
-      e0[j] = d2[pid];
-      e1[j] = d2[HW + pid];
-      e2[j] = d2[2 * HW + pid];
+      e[0] = d2[pid];
+      e[1] = d2[HW + pid];
+      e[2] = d2[2 * HW + pid];
     }
-    nbg2[j] = TWO ? -T_final * bg_dot3(bg, e0[j], e1[j], e2[j]) : 0.f;
-    S[j] = Sd[j] = S2[j] = 0.f;
+    de0[j] = f2{d[0], e[0]};
+    de1[j] = f2{d[1], e[1]};
+    de2[j] = f2{d[2], e[2]};
+    dpd[j] = dd;
+    dpa0[j] = f2{da, -0.0f};
+    nbgs[j] = f2{-T_final * bg_dot3(bg, d[0], d[1], d[2]), TWO ? -T_final * bg_dot3(bg, e[0], e[1], e[2]) : 0.f};
+    SS2[j] = f2{0.f, 0.f};
+    Sd[j] = 0.f;
   }
   const float ddelx_dx = 0.5f * W, ddely_dy = 0.5f * H;
   const float4 zero4 = make_float4(0.f, 0.f, 0.f, 0.f);
@@ -1851,11 +1858,10 @@ __global__ __launch_bounds__(64 * NW) void k_render_bwd_tw(
     const bool staged = rel_c >= lo;
     uint32_t keep4 = 0u;
     if (staged && stage_geo) {
-      // pre-multiplied conic for gauss_power2 (.w of s1: list position), row slot
-      const float4 ca = make_float4(na.x, na.y, GSR_CONIC_K_AC * na.z, GSR_CONIC_K_B * na.w);
-      const float4 cb = make_float4(GSR_CONIC_K_AC * nb.x, nb.y, nb.z, __uint_as_float((uint32_t)rel_c));
-      s0[lane] = ca;
-      s1[lane] = cb;
+      // the pre-multiplied conic as s0 = (x, y, B, C), s1 = (A, opacity, depth, list position): the products the
+      // step packs are adjacent; row slot
+      s0[lane] = make_float4(na.x, na.y, GSR_CONIC_K_B * na.w, GSR_CONIC_K_AC * nb.x);
+      s1[lane] = make_float4(GSR_CONIC_K_AC * na.z, nb.y, nb.z, __uint_as_float((uint32_t)rel_c));
       const uint32_t dx_ = __float_as_uint(nd.x), dy_ = __float_as_uint(nd.y);
       const int xmin = dx_ & 0xffff, ymin = dx_ >> 16, xmax = dy_ & 0xffff;
       slot[lane] = ngo + (uint32_t)((tyi - ymin) * (xmax - xmin) + (txi - xmin));
@@ -1863,20 +1869,19 @@ __global__ __launch_bounds__(64 * NW) void k_render_bwd_tw(
 #pragma unroll
         for (int q = 0; q < 4; ++q) keep4 |= rel_c < qmaxc[q] ? nqm & (1u << q) : 0u;
       } else {
-        // the staged conic back to (a, b, c) for the (padded, conservative) cull, as k_render_bwd does
-        const float4 r0 = make_float4(ca.x, ca.y, ca.z * (1.0f / GSR_CONIC_K_AC), ca.w * (1.0f / GSR_CONIC_K_B));
-        const float4 r1 = make_float4(cb.x * (1.0f / GSR_CONIC_K_AC), cb.y, cb.z, cb.w);
+        // the (padded, conservative) cull on the record's conic
 #pragma unroll
         for (int q = 0; q < 4; ++q)
           if (rel_c < qmaxc[q] &&
-              quadrant_hit(r0, r1, (float)(txi * GSR_TILE_X + (q & 1) * 8), (float)(tyi * GSR_TILE_Y + (q >> 1) * 8)))
+              quadrant_hit(na, nb, (float)(txi * GSR_TILE_X + (q & 1) * 8), (float)(tyi * GSR_TILE_Y + (q >> 1) * 8)))
             keep4 |= 1u << q;
       }
       if (NW > 1) skeep[lane] = keep4;
     }
     if (staged && stage_col) {
-      s2[lane] = nc;
-      if (TWO) s3[lane] = n2;
+      // colours interleaved with the second colours (zeros for one colour): (r, r2, g, g2), (b, b2)
+      s2[lane] = make_float4(nc.x, n2.x, nc.y, n2.y);
+      s3[lane] = make_float4(nc.z, n2.z, 0.f, 0.f);
     }
     // the next batch's records and the one after's indices
     if (h - 64 > lo) {
@@ -1902,27 +1907,28 @@ __global__ __launch_bounds__(64 * NW) void k_render_bwd_tw(
       const unsigned long long kq = __ballot((keep4 >> q) & 1u);
       if (kq == 0ull) continue;
       // this quadrant's dL/dpixel planes for the sums
-      planes[TWO ? 2 * lane : lane] = make_float4(dp0[j], dp1[j], dp2[j], dpd[j]);
-      if (TWO) planes[2 * lane + 1] = make_float4(e0[j], e1[j], e2[j], 0.f);
-      const float pxf = lxf + (float)((q & 1) * 8), pyf = lyf + (float)((q >> 1) * 8);
+      planes[TWO ? 2 * lane : lane] = make_float4(de0[j].x, de1[j].x, de2[j].x, dpd[j]);
+      if (TWO) planes[2 * lane + 1] = make_float4(de0[j].y, de1[j].y, de2[j].y, 0.f);
+      const f2 pxy = {lxf + (float)((q & 1) * 8), lyf + (float)((q >> 1) * 8)};
       int fill = 0;
       unsigned long long pend = 0ull, rest = kq;
       // candidate records in two register sets used in turn (the loop body twice, roles swapped: no register
       // copies between steps); each step reads the next candidate's into the other set
       int jc = (int)__builtin_ctzll(rest);
       float4 pa = s0[jc], pb = s1[jc], pc = s2[jc];
-      float4 pd = TWO ? s3[jc] : zero4;
+      float4 pd = s3[jc];
       float4 ya, yb, yc, yd;
       auto step = [&](const float4& ga, const float4& gb, const float4& gc, const float4& gd, float4& xa, float4& xb,
                       float4& xc, float4& xd) -> bool {
         rest &= rest - 1ull;
         const int jn = rest != 0ull ? (int)__builtin_ctzll(rest) : jc;
         xa = s0[jn], xb = s1[jn], xc = s2[jn];
-        xd = TWO ? s3[jn] : zero4;
-        // the replay step of k_render_bwd (replay / replay2) on this quadrant's pixel
+        xd = s3[jn];
+        // the replay step of k_render_bwd (replay / replay2) on this quadrant's pixel, in packed pairs
         const uint32_t rel = __float_as_uint(gb.w);
-        const float dx = ga.x - pxf, dy = ga.y - pyf;
-        const float power2 = gauss_power2(ga.z, ga.w, gb.x, dx, dy);
+        const f2 dd = f2{ga.x, ga.y} - pxy;
+        const f2 bc = f2{ga.z, ga.w} * f2{dd.y, dd.y};
+        const float power2 = fmaf(dd.x, fmaf(gb.x, dd.x, bc.x), bc.y * dd.y);  // gauss_power2(A, B, C, dx, dy)
         const float G = __builtin_amdgcn_exp2f(power2);
         const float alpha = fminf(GSR_ALPHA_MAX, gb.y * G);
         // (the step's blend condition as a uniform lane mask: the selects read it directly)
@@ -1933,18 +1939,21 @@ __global__ __launch_bounds__(64 * NW) void k_render_bwd_tw(
         const float oma = 1.f - a_eff;
         const float inv_1ma = fast_rcp(oma);
         T[j] = T[j] * inv_1ma;
-        const float cd = fmaf(gc.x, dp0[j], fmaf(gc.y, dp1[j], fmaf(gc.z, dp2[j], dpa[j])));
+        // (cd, cd2): cd = fma(r, d0, fma(g, d1, fma(b, d2, dpa))), cd2 = fma(r2, e0, fma(g2, e1, b2 e2))
+        f2 cdp = __builtin_elementwise_fma(f2{gd.x, gd.y}, de2[j], dpa0[j]);
+        cdp = __builtin_elementwise_fma(f2{gc.z, gc.w}, de1[j], cdp);
+        cdp = __builtin_elementwise_fma(f2{gc.x, gc.y}, de0[j], cdp);
+        const f2 dif = cdp - SS2[j];                            // (cd - S, cd2 - S2)
+        const f2 ibg = f2{inv_1ma, inv_1ma} * nbgs[j];          // (inv nbg, inv nbg2)
         float u, u1 = 0.f;
         if (TWO) {
-          const float cd2 = fmaf(gd.x, e0[j], fmaf(gd.y, e1[j], gd.z * e2[j]));
-          u1 = g_eff * fmaf(T[j], fmaf(gb.z - Sd[j], dpd[j], cd - S[j]), inv_1ma * nbg[j]);
-          u = fmaf(g_eff, fmaf(T[j], cd2 - S2[j], inv_1ma * nbg2[j]), u1);
-          S2[j] = fmaf(a_eff, cd2, oma * S2[j]);
+          u1 = g_eff * fmaf(T[j], fmaf(gb.z - Sd[j], dpd[j], dif.x), ibg.x);
+          u = fmaf(g_eff, fmaf(T[j], dif.y, ibg.y), u1);
         } else {
-          u = g_eff * fmaf(T[j], fmaf(gb.z - Sd[j], dpd[j], cd - S[j]), inv_1ma * nbg[j]);
+          u = g_eff * fmaf(T[j], fmaf(gb.z - Sd[j], dpd[j], dif.x), ibg.x);
         }
         const float w = a_eff * T[j];
-        S[j] = fmaf(a_eff, cd, oma * S[j]);
+        SS2[j] = __builtin_elementwise_fma(f2{a_eff, a_eff}, cdp, f2{oma, oma} * SS2[j]);  // (S, S2)
         Sd[j] = fmaf(a_eff, gb.z, oma * Sd[j]);
         const int n = __popcll(hm);
         if (fill + n > GSR_HCAP_TW) {
@@ -1991,15 +2000,16 @@ __global__ __launch_bounds__(64 * NW) void k_render_bwd_tw(
       float4* row = grow + RW * (size_t)slot[lane];
       const float k = o * (1.0f / 1.4426950408889634f);
       {
-        const float dmx = k * ddelx_dx * (2.0f * ga.z * m[1] + ga.w * m[2]);
-        const float dmy = k * ddely_dy * (2.0f * gb.x * m[2] + ga.w * m[1]);
+        // (A = gb.x, B = ga.z, C = ga.w in this kernel's staging)
+        const float dmx = k * ddelx_dx * (2.0f * gb.x * m[1] + ga.z * m[2]);
+        const float dmy = k * ddely_dy * (2.0f * ga.w * m[2] + ga.z * m[1]);
         row[0] = make_float4(dmx, dmy, -0.5f * o * m[3], -0.5f * o * m[4]);
       }
       row[1] = make_float4(-0.5f * o * m[5], m[0], m[6], m[7]);
       row[2] = TWO ? make_float4(m[8], m[9], m[12 % NM], m[13 % NM]) : make_float4(m[8], m[9], 0.f, 0.f);
       if (TWO) {
-        const float dmx1 = k * ddelx_dx * (2.0f * ga.z * m[10 % NM] + ga.w * m[11 % NM]);
-        const float dmy1 = k * ddely_dy * (2.0f * gb.x * m[11 % NM] + ga.w * m[10 % NM]);
+        const float dmx1 = k * ddelx_dx * (2.0f * gb.x * m[10 % NM] + ga.z * m[11 % NM]);
+        const float dmy1 = k * ddely_dy * (2.0f * ga.w * m[11 % NM] + ga.z * m[10 % NM]);
         row[3] = make_float4(m[14 % NM], dmx1, dmy1, 0.f);
       }
     }
