@@ -126,6 +126,13 @@ __device__ __forceinline__ float vsel(unsigned long long m, float if_set, float 
 
 typedef float f2 __attribute__((ext_vector_type(2)));  // packed fp32 pairs (v_pk_*_f32)
 
+// one screen-mean gradient component, k dd (2 a m_a + b m_b), in an explicit operation order: the backward
+// kernels stage the conic in different slots, and left to itself the compiler contracts the sum differently
+// per kernel, which breaks the variants' bitwise agreement
+__device__ __forceinline__ float mean_grad(float k, float dd, float a, float b, float m_a, float m_b) {
+  return k * dd * fmaf(2.0f * a, m_a, b * m_b);
+}
+
 // a wave-uniform float kept in a scalar register
 __device__ __forceinline__ float sgpr_f(float x) {
   float r;
@@ -1538,16 +1545,16 @@ __device__ __forceinline__ void bwd_tile(BwdLDS<TWO, HITS>& s, const RenderSet& 
       // -o (W/2) (a m1 + b m2) etc. with the staged A = -log2e a / 2, B = -log2e b, C = -log2e c / 2
       const float k = o * (1.0f / 1.4426950408889634f);
       if (qq == 0) {
-        const float dmx = k * ddelx_dx * (2.0f * ga.z * m[1] + ga.w * m[2]);
-        const float dmy = k * ddely_dy * (2.0f * gb.x * m[2] + ga.w * m[1]);
+        const float dmx = mean_grad(k, ddelx_dx, ga.z, ga.w, m[1], m[2]);
+        const float dmy = mean_grad(k, ddely_dy, gb.x, ga.w, m[2], m[1]);
         row[0] = make_float4(dmx, dmy, -0.5f * o * m[3], -0.5f * o * m[4]);
       } else if (qq == 1) {
         row[1] = make_float4(-0.5f * o * m[5], m[0], m[6], m[7]);
       } else if (qq == 2) {
         row[2] = TWO ? make_float4(m[8], m[9], m[12 % NM], m[13 % NM]) : make_float4(m[8], m[9], 0.f, 0.f);
       } else if (TWO) {
-        const float dmx1 = k * ddelx_dx * (2.0f * ga.z * m[10 % NM] + ga.w * m[11 % NM]);
-        const float dmy1 = k * ddely_dy * (2.0f * gb.x * m[11 % NM] + ga.w * m[10 % NM]);
+        const float dmx1 = mean_grad(k, ddelx_dx, ga.z, ga.w, m[10 % NM], m[11 % NM]);
+        const float dmy1 = mean_grad(k, ddely_dy, gb.x, ga.w, m[11 % NM], m[10 % NM]);
         row[3] = make_float4(m[14 % NM], dmx1, dmy1, 0.f);
       }
     }
@@ -2001,15 +2008,15 @@ __global__ __launch_bounds__(64 * NW) void k_render_bwd_tw(
       const float k = o * (1.0f / 1.4426950408889634f);
       {
         // (A = gb.x, B = ga.z, C = ga.w in this kernel's staging)
-        const float dmx = k * ddelx_dx * (2.0f * gb.x * m[1] + ga.z * m[2]);
-        const float dmy = k * ddely_dy * (2.0f * ga.w * m[2] + ga.z * m[1]);
+        const float dmx = mean_grad(k, ddelx_dx, gb.x, ga.z, m[1], m[2]);
+        const float dmy = mean_grad(k, ddely_dy, ga.w, ga.z, m[2], m[1]);
         row[0] = make_float4(dmx, dmy, -0.5f * o * m[3], -0.5f * o * m[4]);
       }
       row[1] = make_float4(-0.5f * o * m[5], m[0], m[6], m[7]);
       row[2] = TWO ? make_float4(m[8], m[9], m[12 % NM], m[13 % NM]) : make_float4(m[8], m[9], 0.f, 0.f);
       if (TWO) {
-        const float dmx1 = k * ddelx_dx * (2.0f * gb.x * m[10 % NM] + ga.z * m[11 % NM]);
-        const float dmy1 = k * ddely_dy * (2.0f * ga.w * m[11 % NM] + ga.z * m[10 % NM]);
+        const float dmx1 = mean_grad(k, ddelx_dx, gb.x, ga.z, m[10 % NM], m[11 % NM]);
+        const float dmy1 = mean_grad(k, ddely_dy, ga.w, ga.z, m[11 % NM], m[10 % NM]);
         row[3] = make_float4(m[14 % NM], dmx1, dmy1, 0.f);
       }
     }
@@ -2313,8 +2320,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3, 8))) void
       const float o = gb.y;
       float4* row = grow + 3 * (size_t)slot[lane];
       const float k = o * (1.0f / 1.4426950408889634f);
-      const float dmx = k * ddelx_dx * (2.0f * ga.z * m[1] + ga.w * m[2]);
-      const float dmy = k * ddely_dy * (2.0f * gb.x * m[2] + ga.w * m[1]);
+      const float dmx = mean_grad(k, ddelx_dx, ga.z, ga.w, m[1], m[2]);
+      const float dmy = mean_grad(k, ddely_dy, gb.x, ga.w, m[2], m[1]);
       row[0] = make_float4(dmx, dmy, -0.5f * o * m[3], -0.5f * o * m[4]);
       row[1] = make_float4(-0.5f * o * m[5], m[0], m[6], m[7]);
       row[2] = make_float4(m[8], m[9], 0.f, 0.f);
