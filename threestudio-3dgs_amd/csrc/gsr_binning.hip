@@ -37,22 +37,31 @@ __global__ __launch_bounds__(256) void k_inst_count(int P, int nbe, GeomState g)
   if (lane == 0) g.kept_counts[(size_t)v * nbe + lb] = ktot;
 }
 
-// One 1024-thread workgroup per view: exclusive scan of its kept counts in place, in one pass per 16K
-// blocks (16 consecutive entries per thread); kept instances -> counters[2V + v].
-#define GSR_ISCAN_PER 16
+// One 1024-thread workgroup per view: exclusive scan of its kept counts in place, GSR_ISCAN_PER x 1024 entries
+// per round, staged through LDS so that the loads and stores are coalesced and each thread scans
+// GSR_ISCAN_PER consecutive entries (one pad word per 8: conflict-free runs); kept instances -> counters[2V + v].
+// (One view's 15.6K entries in two rounds: this scan is a single workgroup's latency on the one-view path.)
+#define GSR_ISCAN_PER 8
 __global__ __launch_bounds__(1024) void k_inst_scan(int nbe, GeomState g) {
+  constexpr int CH = 1024 * GSR_ISCAN_PER;
+  __shared__ uint32_t s_x[CH + CH / 8];
   __shared__ uint32_t s_w[16];
   const int v = blockIdx.x, t = threadIdx.x, w = t >> 6, lane = t & 63;
   uint32_t* kept = g.kept_counts + (size_t)v * nbe;
+  auto pad = [](int i) { return i + (i >> 3); };
   uint32_t carry = 0u;
-  for (int c0 = 0; c0 < nbe; c0 += 1024 * GSR_ISCAN_PER) {
-    const int i0 = c0 + t * GSR_ISCAN_PER;
+  for (int c0 = 0; c0 < nbe; c0 += CH) {
+#pragma unroll
+    for (int k = 0; k < GSR_ISCAN_PER; ++k) {
+      const int i = k * 1024 + t;
+      s_x[pad(i)] = c0 + i < nbe ? kept[c0 + i] : 0u;
+    }
+    __syncthreads();
     uint32_t x[GSR_ISCAN_PER], run = 0u;
 #pragma unroll
     for (int k = 0; k < GSR_ISCAN_PER; ++k) {
-      const int i = i0 + k;
       x[k] = run;
-      run += i < nbe ? kept[i] : 0u;
+      run += s_x[pad(t * GSR_ISCAN_PER + k)];
     }
     uint32_t inc = run;
 #pragma unroll
@@ -69,12 +78,17 @@ __global__ __launch_bounds__(1024) void k_inst_scan(int nbe, GeomState g) {
       before += i < w ? sw : 0u;
       tot += sw;
     }
-    __syncthreads();
     const uint32_t off = carry + before + (inc - run);
 #pragma unroll
-    for (int k = 0; k < GSR_ISCAN_PER; ++k)
-      if (i0 + k < nbe) kept[i0 + k] = off + x[k];
+    for (int k = 0; k < GSR_ISCAN_PER; ++k) s_x[pad(t * GSR_ISCAN_PER + k)] = off + x[k];
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < GSR_ISCAN_PER; ++k) {
+      const int i = k * 1024 + t;
+      if (c0 + i < nbe) kept[c0 + i] = s_x[pad(i)];
+    }
     carry += tot;
+    __syncthreads();  // s_x and s_w are rewritten by the next round
   }
   if (t == 0) g.counters[2 * gridDim.x + v] = carry;
 }
