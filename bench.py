@@ -469,7 +469,7 @@ def roofline_fields(args, phases, Ks, Ls, H, W, launched=None):
         views_per_launch = n_fw / n
         scale = views_per_launch / PROFILE_VIEWS_PER_LAUNCH
         # the forward kernel depends on the views per launch (gsr_render.hip fwd_tile_kernel: the tile-wave
-        # kernel from 48 views): its counters apply to the profiled 64-view launch only
+        # kernel from 16 views, quadrant-wave below): its counters apply to the profiled 64-view launch only
         use = profiled_here and (phase == "render_bwd" or views_per_launch == PROFILE_VIEWS_PER_LAUNCH)
         traffic = read_traffic(traffic_path, kernel) if use else None
         valu = read_traffic(traffic_path, kernel, "valu_insts_per_launch") if use else None

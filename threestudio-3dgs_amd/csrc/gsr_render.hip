@@ -828,15 +828,16 @@ __global__ __launch_bounds__(256) void k_ckpt_suffix(RenderSet rs, const uint32_
 // several tiles (C3: 6.7 rectangle tiles per Gaussian, render_fwd -3 %), the quadrant-wave kernel when
 // they are small (C5 SuGaR, 1.7 tiles per Gaussian: the tile kernel is 1.6x slower).  A launch's duration
 // is also bounded by its slowest wave — a heavy tile's whole list for the tile kernel, only a quadrant's
-// for the other — which many views hide: at C3 the tile kernel needs >= 48 views per launch (ms / view,
-// tile vs quadrant: 1 view 0.298 vs 0.124, 8 views 0.076 vs 0.060, 32 views 0.054 vs 0.052, 64 views 0.050
-// vs 0.052; profiles/r02_fwd_kernel_ab.txt).  Both give identical outputs.  GSR_FWD_KERNEL=tile|quadrant
-// forces one (A/B and tests).
+// for the other — which many views hide.  Round 2 (profiles/r02_fwd_kernel_ab.txt) put the C3 crossover at
+// 48 views; with round 4's tile kernel (scalar-mask walk, packed pairs) and the backward's cull from its
+// masks it is 16 views (C3 views/s, tile vs quadrant: 8 views 2697 vs 2699, 16 views 2991 vs 2968, 32 views
+// 3154 vs 3111; profiles/r04/fwd_small_sets_ab.txt).  Both give identical outputs.  GSR_FWD_KERNEL=
+// tile|quadrant forces one (A/B and tests).
 static bool fwd_tile_kernel(long long instances, long long gaussians, int views) {
   const char* e = getenv("GSR_FWD_KERNEL");
   if (e != nullptr && strcmp(e, "quadrant") == 0) return false;
   if (e != nullptr && strcmp(e, "tile") == 0) return true;
-  return views >= 48 && gaussians > 0 && instances >= 3 * gaussians;
+  return views >= 16 && gaussians > 0 && instances >= 3 * gaussians;
 }
 bool fwd_tile_chosen(long long instances, long long gaussians, int views) {
   return fwd_tile_kernel(instances, gaussians, views);
