@@ -259,7 +259,8 @@ def test_batched_views_match_per_view(nviews, monkeypatch):
         assert err <= 1e-5 * scale, f"{k}: {err} vs scale {scale}"
 
 
-@pytest.mark.parametrize("switch", ["fwd_kernel", "dispatch_order", "bwd_kernel", "tile_keys", "tile_sort_bits"])
+@pytest.mark.parametrize("switch", ["fwd_kernel", "dispatch_order", "bwd_kernel", "tile_keys", "tile_sort_bits",
+                                    "tile_ranges"])
 @pytest.mark.parametrize("kind", ["ball_composite", "sugar_two_colors"])
 def test_forward_kernels_bitwise(kind, switch, monkeypatch):
     """fwd_kernel: the one-wave-per-tile forward and the quadrant-wave forward (GSR_FWD_KERNEL) blend exactly
@@ -268,7 +269,8 @@ def test_forward_kernels_bitwise(kind, switch, monkeypatch):
     backward blend as one wave per tile or as four lockstep quadrant waves (GSR_BWD_KERNEL); tile_keys: packed
     (tile, Gaussian) keys vs keys + values with the quadrant masks k_emit writes (the quadrant-wave forward
     then gathers only its quadrant's candidates) and without them (GSR_TILE_KEYS; large sets take the
-    unpacked layout by themselves).  Every
+    unpacked layout by themselves); tile_ranges: the per-tile list bounds by search (k_tile_bounds, the default)
+    or by streaming the sorted keys (GSR_TILE_RANGES=scan).  Every
     output — colour, depth, alpha, the composite, the second colour set, radii — and every gradient (the
     backward reads the forward's per-pixel state) must be bitwise equal."""
     import torch
@@ -305,6 +307,11 @@ def test_forward_kernels_bitwise(kind, switch, monkeypatch):
                 monkeypatch.delenv("GSR_TILE_SORT_BITS", raising=False)
             else:
                 monkeypatch.setenv("GSR_TILE_SORT_BITS", "4")
+        elif switch == "tile_ranges":
+            if kernel == "tile":
+                monkeypatch.delenv("GSR_TILE_RANGES", raising=False)
+            else:
+                monkeypatch.setenv("GSR_TILE_RANGES", "scan")
         elif switch == "tile_keys":
             if kernel == "tile":
                 monkeypatch.delenv("GSR_TILE_KEYS", raising=False)
