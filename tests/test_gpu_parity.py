@@ -260,7 +260,7 @@ def test_batched_views_match_per_view(nviews, monkeypatch):
 
 
 @pytest.mark.parametrize("switch", ["fwd_kernel", "dispatch_order", "bwd_kernel", "tile_keys", "tile_sort_bits",
-                                    "tile_ranges", "pre_rows"])
+                                    "tile_ranges"])
 @pytest.mark.parametrize("kind", ["ball_composite", "sugar_two_colors"])
 def test_forward_kernels_bitwise(kind, switch, monkeypatch):
     """fwd_kernel: the one-wave-per-tile forward and the quadrant-wave forward (GSR_FWD_KERNEL) blend exactly
@@ -270,8 +270,7 @@ def test_forward_kernels_bitwise(kind, switch, monkeypatch):
     (tile, Gaussian) keys vs keys + values with the quadrant masks k_emit writes (the quadrant-wave forward
     then gathers only its quadrant's candidates) and without them (GSR_TILE_KEYS; large sets take the
     unpacked layout by themselves); tile_ranges: the per-tile list bounds by search (k_tile_bounds, the default)
-    or by streaming the sorted keys (GSR_TILE_RANGES=scan); pre_rows: the preprocess's kept-tile counts by
-    wave-cooperative row walks (the default) or one lane per Gaussian (GSR_PRE_ROWS=lane).  Every
+    or by streaming the sorted keys (GSR_TILE_RANGES=scan).  Every
     output — colour, depth, alpha, the composite, the second colour set, radii — and every gradient (the
     backward reads the forward's per-pixel state) must be bitwise equal."""
     import torch
@@ -308,11 +307,6 @@ def test_forward_kernels_bitwise(kind, switch, monkeypatch):
                 monkeypatch.delenv("GSR_TILE_SORT_BITS", raising=False)
             else:
                 monkeypatch.setenv("GSR_TILE_SORT_BITS", "4")
-        elif switch == "pre_rows":
-            if kernel == "tile":
-                monkeypatch.delenv("GSR_PRE_ROWS", raising=False)
-            else:
-                monkeypatch.setenv("GSR_PRE_ROWS", "lane")
         elif switch == "tile_ranges":
             if kernel == "tile":
                 monkeypatch.delenv("GSR_TILE_RANGES", raising=False)

@@ -11,7 +11,6 @@
 // sorts after every visible depth).
 #include "gsr_kernels.h"
 #include "gsr_math.h"
-#include "gsr_wave.h"
 
 namespace gsr {
 
@@ -28,16 +27,10 @@ void launch_preprocess_kernel(const PreprocessArgs& a, const SetCams& cams, cons
 #define GSR_PRE_GAUSS 128
 #define GSR_PRE_LDS_FLOATS (8 * 1024)  // SH staging up to 32 KB (M <= 21); larger M reads SH from HBM
 
-// Kept tiles (the exact span cull's count, which sizes each view's instance list): ROWS = false, each lane walks
-// its Gaussian's rectangle rows; ROWS = true, the wave walks all its lanes' rows 64 at a time (row -> owning lane
-// by an LDS mark and a max-scan, the owner's span parameters by lane shuffles, counts summed by LDS atomics), so a
-// wave no longer runs as many row steps as its tallest rectangle.  The same counts either way (integers).
 // (6 waves per SIMD: 86 -> 79 VGPRs without spills; the LDS allows 6 blocks — 1 % faster)
-template <bool ROWS>
 __attribute__((amdgpu_waves_per_eu(6, 8)))
 __global__ __launch_bounds__(256) void k_preprocess(PreprocessArgs a, SetCams cams, GeomState g) {
   extern __shared__ float s_sh[];  // [128][3M + 1] this block's SH coefficients (odd stride)
-  __shared__ uint32_t s_own[ROWS ? 4 : 1][64], s_kept[ROWS ? 4 : 1][64];
   const int nvc = (a.V + GSR_PRE_VIEWS - 1) / GSR_PRE_VIEWS;
   const int vc = blockIdx.x % nvc;
   const int idx0 = (blockIdx.x / nvc) * GSR_PRE_GAUSS;
@@ -112,10 +105,6 @@ __global__ __launch_bounds__(256) void k_preprocess(PreprocessArgs a, SetCams ca
     int radius = 0;
     uint2 tiles = make_uint2(0u, 0u);
     uint32_t dkey = 0xFFFFFFFFu;  // culled: sorts after every visible depth
-    SpanPrep sp;
-    sp.mode = 0;
-    int rx0 = 0, rx1 = 0, ry0 = 0;
-    uint32_t h = 0u;  // ROWS: this lane's rectangle rows to walk
     // near-plane cull on the view-space depth (in_frustum of the reference)
     const float3 p_view = xform_point4x3(p_orig, viewmatrix);
     if (p_view.z > GSR_NEAR_CULL) {
@@ -155,63 +144,15 @@ __global__ __launch_bounds__(256) void k_preprocess(PreprocessArgs a, SetCams ca
           if (valid) g.rec[vi] = rec;
           radius = r;
           uint32_t kept = 0;
-          sp = span_prep(rec.a.x, rec.a.y, rec.a.z, rec.a.w, rec.b.x, rec.b.y);
-          if (!ROWS) {
-            for (int ty = ymin; ty < ymax; ++ty) {
-              int t0, t1;
-              span_row(sp, ty, xmin, xmax, t0, t1);
-              kept += (uint32_t)(t1 - t0);
-            }
-          } else {
-            // mode 1: every rectangle tile; mode 2: the rows are walked below by the whole wave
-            kept = sp.mode == 1 ? (uint32_t)area : 0u;
-            h = sp.mode == 2 && valid ? (uint32_t)(ymax - ymin) : 0u;
-            rx0 = xmin, rx1 = xmax, ry0 = ymin;
+          const SpanPrep sp = span_prep(rec.a.x, rec.a.y, rec.a.z, rec.a.w, rec.b.x, rec.b.y);
+          for (int ty = ymin; ty < ymax; ++ty) {
+            int t0, t1;
+            span_row(sp, ty, xmin, xmax, t0, t1);
+            kept += (uint32_t)(t1 - t0);
           }
           tiles = make_uint2((uint32_t)area, kept);
           dkey = __float_as_uint(p_view.z);  // > 0.2: float bits are monotone in depth
         }
-      }
-    }
-    if (ROWS) {
-      const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
-      const uint32_t hincl = wave_incl_sum_dpp(h);
-      const uint32_t roff = hincl - h;
-      const uint32_t R = (uint32_t)__builtin_amdgcn_readlane((int)hincl, 63);  // wave-uniform
-      if (R > 0u) {
-        s_kept[w][lane] = 0u;
-        uint32_t carry = 0u;  // 1 + owner of the previous chunk's last row
-        for (uint32_t r0 = 0; r0 < R; r0 += 64) {
-          s_own[w][lane] = 0u;
-          asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-          if (h && roff >= r0 && roff < r0 + 64) s_own[w][roff - r0] = (uint32_t)lane + 1u;
-          asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-          const uint32_t ow1 = max(carry, wave_incl_max_dpp(s_own[w][lane]));
-          carry = (uint32_t)__builtin_amdgcn_readlane((int)ow1, 63);
-          // the owner's span parameters (every lane takes part in the shuffles)
-          const int ow = (int)ow1 - 1 < 0 ? 0 : (int)ow1 - 1;
-          SpanPrep o;
-          o.px = __shfl(sp.px, ow, 64);
-          o.py = __shfl(sp.py, ow, 64);
-          o.b = __shfl(sp.b, ow, 64);
-          o.D = __shfl(sp.D, ow, 64);
-          o.ia = __shfl(sp.ia, ow, 64);
-          o.thra = __shfl(sp.thra, ow, 64);
-          o.ue = __shfl(sp.ue, ow, 64);
-          o.ve = __shfl(sp.ve, ow, 64);
-          o.mode = 2;
-          const int ox0 = __shfl(rx0, ow, 64), ox1 = __shfl(rx1, ow, 64), oy0 = __shfl(ry0, ow, 64);
-          const uint32_t oroff = (uint32_t)__shfl((int)roff, ow, 64);
-          const uint32_t r = r0 + (uint32_t)lane;
-          if (r < R) {
-            int t0, t1;
-            span_row(o, oy0 + (int)(r - oroff), ox0, ox1, t0, t1);
-            if (t1 > t0) atomicAdd(&s_kept[w][ow], (uint32_t)(t1 - t0));
-          }
-          asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // s_own is rewritten by the next chunk
-        }
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        if (h) tiles.y = s_kept[w][lane];
       }
     }
     if (valid) {
@@ -276,12 +217,8 @@ void launch_preprocess_kernel(const PreprocessArgs& a, const SetCams& cams, cons
   const int nvc = (a.V + GSR_PRE_VIEWS - 1) / GSR_PRE_VIEWS;
   const size_t want = a.colors_precomp == nullptr ? (size_t)GSR_PRE_GAUSS * (3 * a.M + 1) : 0;
   const size_t lds = want <= GSR_PRE_LDS_FLOATS ? sizeof(float) * want : 0;
-  const dim3 grid(nvc * ((a.P + GSR_PRE_GAUSS - 1) / GSR_PRE_GAUSS));
-  const char* e = getenv("GSR_PRE_ROWS");  // wave (default) | lane (A/B and tests)
-  if (e != nullptr && strcmp(e, "lane") == 0)
-    hipLaunchKernelGGL(k_preprocess<false>, grid, dim3(256), lds, stream, a, cams, g);
-  else
-    hipLaunchKernelGGL(k_preprocess<true>, grid, dim3(256), lds, stream, a, cams, g);
+  hipLaunchKernelGGL(k_preprocess, dim3(nvc * ((a.P + GSR_PRE_GAUSS - 1) / GSR_PRE_GAUSS)), dim3(256), lds, stream, a,
+                     cams, g);
 }
 
 }  // namespace gsr
