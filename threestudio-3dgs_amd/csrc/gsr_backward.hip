@@ -418,6 +418,10 @@ __global__ __launch_bounds__(256) void k_view_grad(GaussBackwardArgs a, ViewGrad
 // 256 Gaussians per block.  The block's SH rows (contiguous in HBM) are loaded into LDS with fully
 // coalesced loads; each thread reads its row from LDS for every view, accumulates dL/dSH in registers,
 // writes it back into its LDS row, and the block stores the rows coalesced.
+// 3 waves per SIMD (the LDS staging allows 3 blocks per CU): 233 -> 168 VGPRs with two record buffers instead of
+// three and the SH row read from LDS where used; 7 VGPRs spill outside the view loop.  C3 per-Gaussian backward
+// 0.0323 -> 0.0305 ms/view, 8-view sets 0.0514 -> 0.0477 (profiles/r04/gauss_accum_ab.txt)
+__attribute__((amdgpu_waves_per_eu(3, 8)))
 __global__ __launch_bounds__(256) void k_gauss_accum(GaussBackwardArgs a, AccumArgs b) {
   extern __shared__ __attribute__((aligned(16))) float s_sh[];
   const int t = threadIdx.x;
@@ -505,9 +509,8 @@ __global__ __launch_bounds__(256) void k_gauss_accum(GaussBackwardArgs a, AccumA
     }
     const float* sh_row = has_sh ? s_sh + t * S : nullptr;
     // The group's reached views of this Gaussian (reach bits, k_render_bwd): only their records exist.
-    // They stream through three register buffers in view order: while one view's SH backward runs, the
-    // next two views' records (16-byte loads of the whole slot) are in flight (the accumulators hold this
-    // kernel to 2 waves per SIMD, so the loads in flight come from depth).
+    // They stream through two register buffers in view order: while one view's SH backward runs, the next
+    // view's record (16-byte loads of the whole slot) is in flight.
     const int RS = b.dcolors2 ? GSR_REC_STRIDE2 : GSR_REC_STRIDE;
     float d2[3] = {0.f, 0.f, 0.f};  // two colours: the second colour's sums
     if (b.dcolors2 && acc)
@@ -546,14 +549,8 @@ __global__ __launch_bounds__(256) void k_gauss_accum(GaussBackwardArgs a, AccumA
       if (has_sh && ((f[9] != 0.f) | (f[10] != 0.f) | (f[11] != 0.f))) {
         const uint32_t cl = __float_as_uint(f[13]);
         const float3 dRGB = make_float3((cl & 1u) ? 0.f : f[9], (cl & 2u) ? 0.f : f[10], (cl & 4u) ? 0.f : f[11]);
-        // the SH row as 16-byte LDS reads (stride sh_lds_stride: conflict-free); entries past 3M unused
-        float shv[48];
-        const float4* row4 = reinterpret_cast<const float4*>(sh_row);
-#pragma unroll
-        for (int c = 0; c < 12; ++c) {
-          const float4 q = 4 * c < F ? row4[c] : make_float4(0.f, 0.f, 0.f, 0.f);
-          shv[4 * c] = q.x, shv[4 * c + 1] = q.y, shv[4 * c + 2] = q.z, shv[4 * c + 3] = q.w;
-        }
+        // the SH row read from LDS where sh_backward uses it (not copied to 48 registers first)
+        const float* shv = sh_row;
         // the camera position through scalar loads (uniform view): a vector load here would be the
         // newest in flight and its wait would drain the record prefetch
         typedef __attribute__((address_space(4))) const float* cfptr;
@@ -561,11 +558,10 @@ __global__ __launch_bounds__(256) void k_gauss_accum(GaussBackwardArgs a, AccumA
         sh_backward(a.deg, a.M, shv, dsh, dRGB, mean, cpos, dmean);
       }
     };
-    float4 fa[4], fb[4], fc[4];
-    int va_ = next_view(), vb_ = next_view(), vc_ = next_view();
+    float4 fa[4], fb[4];
+    int va_ = next_view(), vb_ = next_view();
     if (va_ >= 0) load(fa, va_);
     if (vb_ >= 0) load(fb, vb_);
-    if (vc_ >= 0) load(fc, vc_);
     // (buffers refill in turn, so the views are summed in ascending order, as one pass over the group)
     for (;;) {
       if (va_ < 0) break;
@@ -576,10 +572,6 @@ __global__ __launch_bounds__(256) void k_gauss_accum(GaussBackwardArgs a, AccumA
       process(fb, vb_);
       vb_ = next_view();
       if (vb_ >= 0) load(fb, vb_);
-      if (vc_ < 0) break;
-      process(fc, vc_);
-      vc_ = next_view();
-      if (vc_ >= 0) load(fc, vc_);
     }
     // (the sums already include the earlier groups: plain stores)
     a.dL_dmeans3D[3 * idx] = dmean.x;
