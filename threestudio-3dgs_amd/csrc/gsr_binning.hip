@@ -209,6 +209,7 @@ __global__ __launch_bounds__(256) void k_goff_write(int P, int nbg, GeomState g)
 //   kept:  the kept positions of those rows, 64 at a time; lane j's row owner gives its tile directly
 //          (row tile t0 + offset), so every instance is written with a coalesced store, in order,
 //          without per-position span tests, divisions or ballots.
+template <bool QM>
 struct EmitLDS {
   uint32_t gi[GSR_DUP_TILE];
   uint32_t roff[GSR_DUP_TILE];  // per Gaussian: its first row in the group's row list
@@ -218,8 +219,9 @@ struct EmitLDS {
   uint32_t rk[64];              // per row of the chunk: its first kept position (chunk-relative)
   uint32_t rtile[64];           // per row of the chunk: tile id of its first kept tile
   uint32_t rgi[64];             // per row of the chunk: the Gaussian
-  uint32_t rx0[64];             // per row of the chunk (QM): its first kept tile column
-  uint2 rq[64];                 // per row of the chunk (QM): span_quads of its upper and lower 8-pixel band
+  uint32_t rx0[QM ? 64 : 1];    // per row of the chunk (QM): its first kept tile column
+  uint2 rq[QM ? 64 : 1];        // per row of the chunk (QM): span_quads of its upper and lower 8-pixel band
+  // (without QM the struct is 4.6 KB: 8 single-wave workgroups per SIMD instead of 7)
   uint32_t kown[64];            // kept position -> 1 + owning row (marks)
 };
 
@@ -233,7 +235,7 @@ __global__ __launch_bounds__(64) void k_emit(int P, int nbe, int grid_x, GeomSta
                                              uint32_t* __restrict__ keys, uint32_t* __restrict__ vals) {
   const uint32_t* __restrict__ order = g.sorted_dval();
   const uint32_t* __restrict__ dkeys = g.sorted_dkey();
-  __shared__ EmitLDS s;
+  __shared__ EmitLDS<QM> s;
   const int nw = div_up(nbe, GSR_EMIT_GROUPS);
   const int v = blockIdx.x / nw;
   const int lb0 = (blockIdx.x % nw) * GSR_EMIT_GROUPS, lb1 = min(nbe, lb0 + GSR_EMIT_GROUPS);

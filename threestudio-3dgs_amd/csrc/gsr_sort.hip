@@ -104,7 +104,9 @@ struct ScatterLDS {
 };
 
 // KV = false: keys only (packed tile keys); vals_in / vals_out unused.
+// (keys only: 6 waves per SIMD, 83 -> 80 VGPRs — the LDS allows 7 workgroups per CU; with values the LDS allows 4)
 template <bool KV, int BITS>
+__attribute__((amdgpu_waves_per_eu(KV ? 4 : 6, 8)))
 __global__ __launch_bounds__(GSR_SORT_THREADS) void k_seg_scatter(
     const uint32_t* __restrict__ keys_in, const uint32_t* __restrict__ vals_in, uint32_t* __restrict__ keys_out,
     uint32_t* __restrict__ vals_out, SegInfo seg, int shift, int bits_rt, int last, const uint32_t* __restrict__ counts,
