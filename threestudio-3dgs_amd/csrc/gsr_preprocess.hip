@@ -19,10 +19,11 @@ void launch_preprocess_kernel(const PreprocessArgs& a, const SetCams& cams, cons
 // Views handled by one block (the Gaussians' view-independent work and SH staging are shared): the
 // block's 256 threads are 128 Gaussians x 2 halves of the views, so the SH staging (128 x (3M + 1)
 // floats, 24.6 KB at SH3) allows 6 blocks = 6 waves per SIMD instead of 3 with 256 Gaussians.
-// 32 views per block (8 / 16 / 32: 0.032 / 0.030 / 0.029 ms per view at C3): the SH staging and the 3D
-// covariance amortise over more views; 64-view sets still give 2 x 7813 blocks.
+// 64 views per block (8 / 16 / 32 / 64: 0.032 / 0.030 / 0.0285 / 0.0276 ms per view at C3,
+// profiles/r04/pre_views_ab.txt): the SH staging and the 3D covariance amortise over more views; a 64-view set
+// gives 7813 blocks (30 per CU).
 #ifndef GSR_PRE_VIEWS
-#define GSR_PRE_VIEWS 32
+#define GSR_PRE_VIEWS 64
 #endif
 #define GSR_PRE_GAUSS 128
 #define GSR_PRE_LDS_FLOATS (8 * 1024)  // SH staging up to 32 KB (M <= 21); larger M reads SH from HBM
