@@ -225,7 +225,9 @@ struct EmitLDS {
   uint32_t kown[64];            // kept position -> 1 + owning row (marks)
 };
 
+#ifndef GSR_EMIT_GROUPS
 #define GSR_EMIT_GROUPS 2  // consecutive 64-Gaussian groups per wave (the next group's gathers prefetched)
+#endif
 
 // QM (unpacked keys): each key also carries the instance's quadrant mask (GSR_QMASK_SHIFT): per row the
 // quadrant-column ranges of its two 8-pixel bands (span_quads, the span_row bound at half the tile size), per
