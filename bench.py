@@ -762,9 +762,8 @@ def run_workload(args, world, rank, device, comm, headline=True):
     if args.workload == "sugar":
         # how the two rasterizer calls run: one forward blending both colour sets + one backward pass for
         # both (gsr_set_backward_two_colors), or A/B variants
-        res["config"]["two_calls"] = ("separate renders" if SUGAR_SEPARATE else "shared forward, " + (
-            "separate backward passes" if os.environ.get("GSR_TWO_COLOR_BWD") == "separate"
-            else "one two-colour backward pass"))
+        res["config"]["two_calls"] = ("separate renders" if SUGAR_SEPARATE
+                                      else "shared forward, one two-colour backward pass")
     if host_trace is not None:  # GSR_HOST_TRACE=1: host (Python + ctypes) time per step of the rasterizer's phases
         res["host_ms_per_step"] = {k: round(1000.0 * v / args.steps, 3) for k, v in host_trace.items()}
     if phases is not None:

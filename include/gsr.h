@@ -173,6 +173,9 @@ int gsr_set_num_rendered_ex(int V, const void* geom, int P, int* num_rendered, i
  * alpha >= 1/255 ellipse reaches).  Either may be NULL.  Parity tests compare these with the oracle's
  * per-Gaussian preprocess values (the reference's geomBuffer has no public layout). */
 int gsr_set_gauss_state(int V, const void* geom, int P, void* out_rec, void* out_tiles, void* stream);
+/* The binning buffer belongs to this one forward until its last backward: besides the sorted tile lists the
+ * forward may keep per listed instance a quadrant-mask byte in the buffer's second (free) key array, which the
+ * backward's cull reads (csrc/gsr_common.h BinningState); the caller must not reuse the buffer in between. */
 int gsr_set_render(int V, int P, const int* num_rendered, int width, int height, const float* const* bgs,
                    void* geom, void* binning, void* image, float* out_color, float* out_depth,
                    float* out_alpha, void* stream);

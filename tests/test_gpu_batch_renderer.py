@@ -218,9 +218,9 @@ class _SnapshotReduce:
 
 
 @pytest.mark.parametrize("bwd", ["fused", "separate"])
-def test_chunked_reduce_reads_finished_gradients(bwd, monkeypatch):
+def test_chunked_reduce_reads_finished_gradients(bwd):
     """with the SuGaR normal renderer's second rasterizer call backpropagated separately
-    (GSR_TWO_COLOR_BWD=separate) its kernels still add into the shared gradients after the first call's
+    (two_color_backward="separate") its kernels still add into the shared gradients after the first call's
     ranges are formed, so the reduction must wait for the whole stream (no per-range events); with the fused
     two-colour backward the per-range events cover every writer.  The gradients a side-stream reader sees equal
     the final ones either way."""
@@ -228,7 +228,6 @@ def test_chunked_reduce_reads_finished_gradients(bwd, monkeypatch):
     from diff_gaussian_rasterization.batched import rasterize_views
     from diff_gaussian_rasterization.cameras import get_cam_info_gaussian
 
-    monkeypatch.setenv("GSR_TWO_COLOR_BWD", bwd)
     scene = gs.make_sugar_scene(4, sh_degree=0, seed=5)
     P = scene["means3D"].shape[0]
     batch = rf.make_batch(3, H, W, "cuda", seed=11)
@@ -246,7 +245,7 @@ def test_chunked_reduce_reads_finished_gradients(bwd, monkeypatch):
     m2 = [torch.zeros((P, 3), device="cuda", requires_grad=True) for _ in range(3)]
     snap = _SnapshotReduce(4)
     outs = rasterize_views(settings, t["means3D"], m2, t["opacities"], colors_precomp=cols, scales=t["scales"],
-                           rotations=t["rotations"], colors2=t["normals"], grad_reduce=snap)
+                           rotations=t["rotations"], colors2=t["normals"], grad_reduce=snap, two_color_backward=bwd)
     up = [torch.randn_like(o, generator=torch.Generator("cuda").manual_seed(20 + i)) if o.is_floating_point()
           else None for i, o in enumerate(outs)]
     torch.autograd.backward([o for o, u in zip(outs, up) if u is not None], [u for u in up if u is not None])

@@ -259,24 +259,18 @@ def test_batched_views_match_per_view(nviews, monkeypatch):
         assert err <= 1e-5 * scale, f"{k}: {err} vs scale {scale}"
 
 
-@pytest.mark.parametrize("switch", ["fwd_kernel", "dispatch_order", "bwd_kernel", "tile_keys", "tile_sort_bits",
-                                    "tile_ranges"])
-@pytest.mark.parametrize("kind", ["ball_composite", "sugar_two_colors"])
-def test_forward_kernels_bitwise(kind, switch, monkeypatch):
-    """fwd_kernel: the one-wave-per-tile forward and the quadrant-wave forward (GSR_FWD_KERNEL) blend exactly
-    the same candidates per pixel in the same order; dispatch_order: the blends' work-ordered
-    dispatch and raster order (GSR_TILE_ORDER=raster) only change which workgroup starts first; bwd_kernel: the
-    backward blend as one wave per tile or as four lockstep quadrant waves (GSR_BWD_KERNEL); tile_keys: packed
-    (tile, Gaussian) keys vs keys + values with the quadrant masks k_emit writes (the quadrant-wave forward
-    then gathers only its quadrant's candidates) and without them (GSR_TILE_KEYS; large sets take the
-    unpacked layout by themselves); tile_ranges: the per-tile list bounds by search (k_tile_bounds, the default)
-    or by streaming the sorted keys (GSR_TILE_RANGES=scan).  Every
-    output — colour, depth, alpha, the composite, the second colour set, radii — and every gradient (the
-    backward reads the forward's per-pixel state) must be bitwise equal."""
+def bitwise_case(kind, monkeypatch=None, fwd_kernel=None):
+    """One 3-view rasterize_views forward + backward of the bitwise tests (every output, means2D and parameter
+    gradient as numpy arrays).  ball_composite: 40k Gaussians, SH3, ragged 200 x 168 with the fused background
+    composite; sugar_two_colors: a SuGaR scene with the second colour set (both calls in one backward)."""
     import torch
 
     from diff_gaussian_rasterization.batched import rasterize_views
+    from test_gpu_configs import _settings
 
+    if fwd_kernel is not None:
+        monkeypatch.setenv("GSR_FWD_KERNEL", fwd_kernel)
+        monkeypatch.setenv("GSR_BWD_SPLIT", "0")  # the tile-wave forward writes no split checkpoints
     dev = "cuda"
     if kind == "ball_composite":
         scene = gs.make_scene(40_000, sh_degree=3, seed=51)
@@ -288,67 +282,60 @@ def test_forward_kernels_bitwise(kind, switch, monkeypatch):
     cams = [make_camera(W_, H_, elevation=12.0 * i, azimuth=55.0 * i + 5.0) for i in range(3)]
     ups = [torch.tensor(rng.standard_normal((3, 3, H_, W_)).astype(np.float32), device=dev) for _ in range(3)]
     bgimg = torch.tensor(rng.random((3, H_, W_, 3)).astype(np.float32), device=dev)
+    P = scene["means3D"].shape[0]
+    t = {k: torch.tensor(scene[k], device=dev, requires_grad=True)
+         for k in ("means3D", "scales", "rotations", "opacities", "shs")}
+    m2 = [torch.zeros((P, 3), device=dev, requires_grad=True) for _ in cams]
+    st = [_settings(c, [0.1, 0.2, 0.3], int(scene["sh_degree"])) for c in cams]
+    common = dict(opacities=t["opacities"], scales=t["scales"], rotations=t["rotations"])
+    if kind == "ball_composite":
+        outs = rasterize_views(st, t["means3D"], m2, shs=t["shs"], background=bgimg, **common)
+    else:
+        t["normals"] = torch.tensor(scene["normals"], device=dev, requires_grad=True)
+        outs = rasterize_views(st, t["means3D"], m2, shs=t["shs"], colors2=t["normals"], **common)
+    c, r, d, a = outs[:4]
+    loss = (c * ups[0]).sum() + (d * ups[1][:, :1]).sum() + (a * ups[1][:, 1:2]).sum()
+    if len(outs) > 4:
+        loss = loss + (outs[4] * ups[2]).sum()
+    loss.backward()
+    res = [x.detach() for x in outs] + [m.grad for m in m2] + [v.grad for v in t.values()]
+    return [x.cpu().numpy() for x in res]
 
-    def run(kernel):
-        if switch == "fwd_kernel":
-            monkeypatch.setenv("GSR_FWD_KERNEL", kernel)
-            monkeypatch.setenv("GSR_BWD_SPLIT", "0")  # the tile-wave forward writes no split checkpoints
-        elif switch == "bwd_kernel":
-            # one wave per tile walking the quadrants in turn (k_render_bwd_tw / _twm) vs the workgroup of lockstep
-            # quadrant waves (k_render_bwd): hit-list sums for the two colours, matrix-core sums for one
-            monkeypatch.setenv("GSR_BWD_SUMS", "hits" if kind == "sugar_two_colors" else "mfma")
-            monkeypatch.setenv("GSR_BWD_SPLIT", "0")
-            monkeypatch.setenv("GSR_BWD_KERNEL", "tile" if kernel.startswith("tile") else "quadrant")
-            # (hit lists: one or two waves per tile, GSR_BWD_TW_WAVES)
-            monkeypatch.setenv("GSR_BWD_TW_WAVES", "2" if kernel.startswith("tile2") else "1")
-        elif switch == "tile_sort_bits":
-            # the stable tile sort in 3 passes of 4 bits instead of 2 of 6: the same lists
-            if kernel == "tile":
-                monkeypatch.delenv("GSR_TILE_SORT_BITS", raising=False)
-            else:
-                monkeypatch.setenv("GSR_TILE_SORT_BITS", "4")
-        elif switch == "tile_ranges":
-            if kernel == "tile":
-                monkeypatch.delenv("GSR_TILE_RANGES", raising=False)
-            else:
-                monkeypatch.setenv("GSR_TILE_RANGES", "scan")
-        elif switch == "tile_keys":
-            if kernel == "tile":
-                monkeypatch.delenv("GSR_TILE_KEYS", raising=False)
-            else:
-                monkeypatch.setenv("GSR_TILE_KEYS", "plain" if kernel == "plain" else "unpacked")
-        elif kernel == "tile":
-            monkeypatch.delenv("GSR_TILE_ORDER", raising=False)
-        else:
-            monkeypatch.setenv("GSR_TILE_ORDER", "raster")
-        from test_gpu_configs import _settings
 
-        P = scene["means3D"].shape[0]
-        t = {k: torch.tensor(scene[k], device=dev, requires_grad=True)
-             for k in ("means3D", "scales", "rotations", "opacities", "shs")}
-        m2 = [torch.zeros((P, 3), device=dev, requires_grad=True) for _ in cams]
-        st = [_settings(c, [0.1, 0.2, 0.3], int(scene["sh_degree"])) for c in cams]
-        common = dict(opacities=t["opacities"], scales=t["scales"], rotations=t["rotations"])
-        if kind == "ball_composite":
-            outs = rasterize_views(st, t["means3D"], m2, shs=t["shs"], background=bgimg, **common)
-        else:
-            t["normals"] = torch.tensor(scene["normals"], device=dev, requires_grad=True)
-            outs = rasterize_views(st, t["means3D"], m2, shs=t["shs"], colors2=t["normals"], **common)
-        c, r, d, a = outs[:4]
-        loss = (c * ups[0]).sum() + (d * ups[1][:, :1]).sum() + (a * ups[1][:, 1:2]).sum()
-        if len(outs) > 4:
-            loss = loss + (outs[4] * ups[2]).sum()
-        loss.backward()
-        res = [x.detach().clone() for x in outs] + [m.grad.clone() for m in m2]
-        return res + [v.grad.clone() for v in t.values()]
+def _assert_bitwise(xs, ys, what):
+    assert len(xs) == len(ys)
+    for i, (x, y) in enumerate(zip(xs, ys)):
+        assert x.dtype == y.dtype and np.array_equal(x, y), \
+            f"{what}: output {i} differs: {float(np.abs(x.astype(np.float64) - y.astype(np.float64)).max())}"
 
-    tile, quad = run("tile"), run("quadrant")
-    for i, (x, y) in enumerate(zip(tile, quad)):
-        assert torch.equal(x, y), f"output {i} differs: {float((x.double() - y.double()).abs().max())}"
-    if switch == "tile_keys":
-        for i, (x, y) in enumerate(zip(run("plain"), quad)):
-            assert torch.equal(x, y), f"plain keys: output {i} differs: {float((x.double() - y.double()).abs().max())}"
-    if switch == "bwd_kernel" and kind == "sugar_two_colors":
-        for variant in ("tile2",):
-            for i, (x, y) in enumerate(zip(run(variant), quad)):
-                assert torch.equal(x, y), f"{variant}: output {i} differs: {float((x.double() - y.double()).abs().max())}"
+
+@pytest.mark.parametrize("switch", ["fwd_kernel", "tile_keys"])
+@pytest.mark.parametrize("kind", ["ball_composite", "sugar_two_colors"])
+def test_forward_kernels_bitwise(kind, switch, monkeypatch, tmp_path):
+    """fwd_kernel: the one-wave-per-tile forward and the quadrant-wave forward (GSR_FWD_KERNEL) blend exactly
+    the same candidates per pixel in the same order (the backward then culls from the tile-wave forward's
+    quadrant masks or recomputes the cull); tile_keys: packed (tile, Gaussian) keys vs keys + values with the
+    quadrant masks k_emit writes (the quadrant-wave forward then gathers only its quadrant's candidates) and
+    without them (GSR_TILE_KEYS = unpacked | plain; large sets take the unpacked layout by themselves).  The
+    layout override is read once per process (the backward derives the buffer layout from it on the host), so
+    the forced layouts run in child processes.  Every output — colour, depth, alpha, the composite, the second
+    colour set, radii — and every gradient (the backward reads the forward's per-pixel state) must be bitwise
+    equal."""
+    if switch == "fwd_kernel":
+        _assert_bitwise(bitwise_case(kind, monkeypatch, "tile"), bitwise_case(kind, monkeypatch, "quadrant"),
+                        "tile-wave vs quadrant-wave forward")
+        return
+    import os
+    import subprocess
+    import sys
+
+    base = bitwise_case(kind)
+    for layout in ("unpacked", "plain"):
+        out = tmp_path / f"{layout}.npz"
+        code = "import numpy as np, test_gpu_parity as t; np.savez(%r, *t.bitwise_case(%r))" % (str(out), kind)
+        env = dict(os.environ, GSR_TILE_KEYS=layout, PYTHONPATH=os.pathsep.join(p for p in sys.path if p))
+        res = subprocess.run([sys.executable, "-c", code], cwd=os.path.dirname(os.path.abspath(__file__)), env=env,
+                             capture_output=True, text=True, timeout=240)
+        assert res.returncode == 0, res.stderr[-3000:]
+        got = np.load(out)
+        _assert_bitwise([got[f"arr_{i}"] for i in range(len(got.files))], base, f"{layout} keys vs packed")

@@ -22,7 +22,7 @@ HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 # (the forward masks' prefetch register; measured faster, profiles/r04/blend_loops_ab.txt session r04k).
 # The per-Gaussian backward with SH at 3 waves per SIMD spills 7 VGPRs, stored before and reloaded after its view
 # loop (profiles/r04/gauss_accum_ab.txt).
-ALLOWED_VGPR_SPILL = {"17k_render_fwd_tileILb0E": 3, "11k_view_gradILb1E": 4, "12k_render_bwdILb0ELb0E": 1,
+ALLOWED_VGPR_SPILL = {"17k_render_fwd_tileILb0E": 3, "11k_view_gradILb1E": 4, "12k_render_bwdE": 1,
                       "13k_gauss_accum": 7}
 
 

@@ -86,6 +86,20 @@ struct PhaseScope {
 };
 }  // namespace
 
+// The instance key layout's test override (GSR_TILE_KEYS = unpacked | plain), read ONCE per process: the forward
+// and the backward of a set derive the binning buffer's layout (packed keys, quadrant masks, which ping-pong array
+// holds the sorted list) from it on the host, so it must not change between them.
+static int tile_keys_mode() {
+  static const int mode = [] {
+    const char* e = getenv("GSR_TILE_KEYS");
+    if (e != nullptr && strcmp(e, "unpacked") == 0) return 1;
+    if (e != nullptr && strcmp(e, "plain") == 0) return 2;
+    return 0;
+  }();
+  return mode;
+}
+static TilePack set_tile_pack(int P, int W, int H) { return tile_pack(P, W, H, tile_keys_mode()); }
+
 static int effective_degree(int degree, int M) {
   // the reference reads sqrt(M)-1 coefficients at most (pred-normal pass quirk)
   int dm = (int)std::lround(std::sqrt((double)(M > 0 ? M : 1))) - 1;
@@ -96,7 +110,7 @@ static int effective_degree(int degree, int M) {
 }
 
 // ping-pong buffers holding the sorts' results (one pass per <= 8 key bits)
-static int tile_sort_result(int W, int H) { return digit_plan(tile_key_bits(W, H), tile_sort_bits()).passes & 1; }
+static int tile_sort_result(int W, int H) { return digit_plan(tile_key_bits(W, H)).passes & 1; }
 static int depth_sort_result() { return digit_plan(32).passes & 1; }
 
 static GaussBackwardArgs shared_args(int P, int degree, int M, const float* means3D, const float* scales,
@@ -185,7 +199,7 @@ size_t gsr_set_binning_bytes(int V, int P, const int* K, int width, int height) 
   long long total = 0;
   if (V < 1 || V > GSR_SET_MAX || K == nullptr || inst_segments(V, K, seg, &total) != GSR_OK) return 0;
   size_t b = 0;
-  BinningState::carve(nullptr, V, total, seg.blk[V], !tile_pack(P, width, height).packed, &b);
+  BinningState::carve(nullptr, V, total, seg.blk[V], !set_tile_pack(P, width, height).packed, &b);
   return b;
 }
 size_t gsr_set_image_bytes(int V, int width, int height) {
@@ -508,7 +522,7 @@ static int set_render(int V, int P, const int* K, int width, int height, const f
   if (inst_segments(V, K, inst, &total) != GSR_OK) return GSR_EINVAL;
   hipStream_t s = (hipStream_t)stream;
   GeomState g = GeomState::carve(geom, V, P, nullptr);
-  const TilePack tp = tile_pack(P, width, height);
+  const TilePack tp = set_tile_pack(P, width, height);
   BinningState b = BinningState::carve(binning, V, total, inst.blk[V], !tp.packed, nullptr);
   // the split decision of this forward, recorded in the image state for its backward
   const bool split = split_forward(V, P, width, height, total, colors2 != nullptr);
@@ -526,8 +540,7 @@ static int set_render(int V, int P, const int* K, int width, int height, const f
     GSR_HIP_CHECK(hipMemsetAsync(img.ranges, 0, sizeof(uint2) * (size_t)V * gx * gy, s));
     if (total > 0) {
       launch_emit(V, P, width, g, inst, tp, b.key[0], b.val[0], s);
-      const int res = seg_sort(b.key, b.val, false, inst, tp.gbits, tp.tile_bits, b.sort_counts, b.sort_totals, s,
-                               tile_sort_bits());
+      const int res = seg_sort(b.key, b.val, false, inst, tp.gbits, tp.tile_bits, b.sort_counts, b.sort_totals, s);
       if (res != tres) return fail(GSR_EHIP, "%s", "internal: tile sort buffer");
       launch_tile_ranges(inst, gx * gy, tp, b.key[res], img.ranges, s);
     }
@@ -543,7 +556,7 @@ static int set_render(int V, int P, const int* K, int width, int height, const f
     rs.col2 = colors2;
     rs.out_col2 = out_color2;
     rs.dpix2 = nullptr;
-    rs.order = tile_order_on() ? img.order : nullptr;
+    rs.order = img.order;
     rs.ckpt = split ? img.ckpt : nullptr;
     rs.split_mode = img.split_mode;
     rs.split_items = img.split_items;
@@ -642,7 +655,7 @@ static int set_backward(int V, int P, int degree, int M, const int* K, int width
   if (inst_segments(V, K, inst, &total) != GSR_OK) return GSR_EINVAL;
   hipStream_t s = (hipStream_t)stream;
   GeomState g = GeomState::carve((void*)geom, V, P, nullptr);
-  const TilePack tp = tile_pack(P, width, height);
+  const TilePack tp = set_tile_pack(P, width, height);
   BinningState b = BinningState::carve((void*)binning, V, total, inst.blk[V], !tp.packed, nullptr);
   // (the checkpoints, carved last, exist when the forward split: split_mode says so on the device)
   ImageState img = ImageState::carve((void*)image, V, width, height, nullptr, true);
@@ -678,10 +691,12 @@ static int set_backward(int V, int P, int degree, int M, const int* K, int width
     rs.col2 = two ? colors2 : colors_override;
     rs.out_col2 = nullptr;
     rs.dpix2 = two ? dL_dcolor2 + (size_t)g0 * 3 * HW : nullptr;
-    rs.order = tile_order_on() ? img.order : nullptr;
-    // a one-colour backward of the first colour may replay split chunks: whether the forward wrote them is its
-    // recorded decision (split_mode, read by the kernels), not this call's environment
-    rs.ckpt = split_fits(V, (size_t)gx * gy) && !two && colors_override == nullptr ? img.ckpt : nullptr;
+    rs.order = img.order;
+    // a one-colour backward of the first colour replays split chunks when the forward wrote them: the host repeats
+    // the forward's decision (split_forward, so no extra workgroups are launched for a forward that did not split)
+    // and the kernels follow the decision the forward recorded on the device (split_mode), whatever this call's
+    // environment says
+    rs.ckpt = split_forward(V, P, width, height, total, two) && colors_override == nullptr ? img.ckpt : nullptr;
     rs.split_mode = img.split_mode;
     rs.split_items = img.split_items;
     rs.split_cap = img.split_cap;

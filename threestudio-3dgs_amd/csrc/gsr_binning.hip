@@ -346,62 +346,13 @@ __global__ __launch_bounds__(64) void k_emit(int P, int nbe, int grid_x, GeomSta
   }
 }
 
-// After the tile sort: per-tile [start, end) ranges (view-local positions) of each view's list.
-// One wave streams GSR_RANGE_ROUNDS x 64 consecutive instances, lane-interleaved (coalesced): all
-// rounds' keys are loaded first, neighbours come from the adjacent lanes (shuffles) and, at round
-// edges, from the neighbouring round (readlane).
-#define GSR_RANGE_ROUNDS 16
-// A block covers `chunks` x 4096 instances: each wave `chunks` consecutive chunks of 64 x GSR_RANGE_ROUNDS.
-// Large sets take GSR_RANGE_TILE per block (fewer, longer-lived workgroups: the 64-view launch was bound by
-// workgroup dispatch, 2.6 TB/s); a set with few instances (one view: ~5M) one chunk per wave, so its few
-// blocks do not walk their chunks one after the other (launch_tile_ranges).
-#define GSR_RANGE_CHUNK_ITEMS (4 * 64 * GSR_RANGE_ROUNDS)
-#define GSR_RANGE_CHUNKS (GSR_RANGE_TILE / GSR_RANGE_CHUNK_ITEMS)
-__global__ __launch_bounds__(256) void k_tile_ranges(SegInfo inst, int n_tiles, int gbits, uint32_t tmask, int chunks,
-                                                     const uint32_t* __restrict__ keys,
-                                                     uint2* __restrict__ ranges) {
-  uint32_t lb;
-  const int v = seg_of_block(inst, blockIdx.x, lb);
-  const int lane = threadIdx.x & 63;
-  const uint32_t K = seg_live(inst, v);
-  const uint32_t* kv = keys + inst.start[v];
-  uint2* rv = ranges + (size_t)v * n_tiles;
-#pragma unroll 1
-  for (int ch = 0; ch < chunks; ++ch) {
-  const uint32_t base = ((lb * 4 + (threadIdx.x >> 6)) * (uint32_t)chunks + ch) * (64u * GSR_RANGE_ROUNDS);
-  if (base >= K) return;  // wave-uniform
-  uint32_t t[GSR_RANGE_ROUNDS];
-#pragma unroll
-  for (int r = 0; r < GSR_RANGE_ROUNDS; ++r) {
-    const uint32_t i = base + 64u * r + lane;
-    t[r] = i < K ? (kv[i] >> gbits) & tmask : 0xFFFFFFFFu;
-  }
-  const uint32_t before = base > 0 ? (kv[base - 1] >> gbits) & tmask : 0xFFFFFFFFu;
-  const uint32_t e = base + 64u * GSR_RANGE_ROUNDS;
-  const uint32_t after = e < K ? (kv[e] >> gbits) & tmask : 0xFFFFFFFFu;
-#pragma unroll
-  for (int r = 0; r < GSR_RANGE_ROUNDS; ++r) {
-    const uint32_t p = base + 64u * r + lane;
-    if (base + 64u * r >= K) break;  // wave-uniform
-    uint32_t prev = (uint32_t)__shfl_up((int)t[r], 1, 64);
-    uint32_t next = (uint32_t)__shfl_down((int)t[r], 1, 64);
-    if (lane == 0) prev = r == 0 ? before : (uint32_t)__builtin_amdgcn_readlane((int)t[r > 0 ? r - 1 : 0], 63);
-    if (lane == 63)
-      next = r == GSR_RANGE_ROUNDS - 1 ? after
-                                       : (uint32_t)__builtin_amdgcn_readlane((int)t[r + 1 < GSR_RANGE_ROUNDS ? r + 1 : r], 0);
-    if (p < K) {
-      if (prev != t[r]) rv[t[r]].x = p;
-      if (next != t[r]) rv[t[r]].y = p + 1;
-    }
-  }
-  }
-}
-
-// The same ranges by search (the default, launch_tile_ranges): one thread per (view, tile boundary t in
+// After the tile sort: per-tile [start, end) ranges (view-local positions) of each view's list, by search
+// (identifyTileRanges of the reference streams every sorted key instead): one thread per (view, tile boundary t in
 // [0, n_tiles]) finds the first listed instance whose tile is >= t (lower bound over the view's sorted list, a
 // fixed number of halving steps: the trip count is uniform) and writes it as tile t's start and tile t - 1's
 // end.  ~V x tiles x log2(K) dependent loads whose upper levels every thread shares (cache hits), instead of
-// streaming every listed key (C3: 4.95M keys = 20 MB per view).
+// streaming every listed key (C3: 4.95M keys = 20 MB per view; that scan, measured 472 vs 30 us per 64-view
+// launch, profiles/r04/tile_ranges_ab.txt, was removed in round 5).
 __global__ __launch_bounds__(256) void k_tile_bounds(SegInfo inst, int n_tiles, int gbits, uint32_t tmask,
                                                      const uint32_t* __restrict__ keys, uint2* __restrict__ ranges) {
   const int v = blockIdx.y;
@@ -447,21 +398,9 @@ void launch_emit(int V, int P, int W, const GeomState& g, const SegInfo& inst, c
 
 void launch_tile_ranges(SegInfo inst, int n_tiles, const TilePack& tp, const uint32_t* keys, uint2* ranges,
                         hipStream_t stream) {
-  const char* e = getenv("GSR_TILE_RANGES");  // search (default) | scan (A/B and tests)
-  if (e == nullptr || strcmp(e, "scan") != 0) {
-    if (inst.V <= 0 || n_tiles <= 0) return;
-    hipLaunchKernelGGL(k_tile_bounds, dim3(div_up(n_tiles + 1, 256), inst.V), dim3(256), 0, stream, inst, n_tiles,
-                       tp.gbits, tp.tmask, keys, ranges);
-    return;
-  }
-  // one chunk per wave while that gives at most 8192 blocks (a few views), else GSR_RANGE_CHUNKS
-  long long total = 0;
-  for (int v = 0; v < inst.V; ++v) total += inst.n[v];
-  const int chunks = total <= 8192ll * GSR_RANGE_CHUNK_ITEMS ? 1 : GSR_RANGE_CHUNKS;
-  seg_fill_blocks(inst, chunks * GSR_RANGE_CHUNK_ITEMS);
-  if (inst.blk[inst.V] == 0) return;
-  hipLaunchKernelGGL(k_tile_ranges, dim3(inst.blk[inst.V]), dim3(256), 0, stream, inst, n_tiles, tp.gbits, tp.tmask,
-                     chunks, keys, ranges);
+  if (inst.V <= 0 || n_tiles <= 0) return;
+  hipLaunchKernelGGL(k_tile_bounds, dim3(div_up(n_tiles + 1, 256), inst.V), dim3(256), 0, stream, inst, n_tiles,
+                     tp.gbits, tp.tmask, keys, ranges);
 }
 
 // markVisible / checkFrustum of the reference (API completeness).

@@ -36,8 +36,6 @@
 // Instance emission: 256 threads x 4 depth-sorted Gaussians per block.
 #define GSR_GOFF_TILE 4096  // Gaussians per block of the gradient-row offset scan (256 threads x 16)
 #define GSR_DUP_TILE 64  // depth-sorted Gaussians per emission group (one wave)
-// Tile ranges: 4 waves x 16 rounds x 64 instances per block.
-#define GSR_RANGE_TILE 16384
 
 // Rasterizer constants of the reference algorithm ([EXT] graphdeco
 // cuda_rasterizer/forward.cu + auxiliary.h).
@@ -89,11 +87,10 @@ struct TilePack {
   uint32_t gmask;  // sorted entry -> Gaussian
   uint32_t tmask;  // key >> gbits -> tile id
 };
-static inline TilePack tile_pack(int P, int W, int H) {
-  // GSR_TILE_KEYS (parity tests): "unpacked" = keys + values at any size (keys with quadrant masks), "plain" =
-  // the same without masks; unset = packed whenever both fit one word
-  const char* e = getenv("GSR_TILE_KEYS");
-  const bool force = e != nullptr && (strcmp(e, "unpacked") == 0 || strcmp(e, "plain") == 0);
+// force: 0 = packed whenever both fit one word, 1 = keys + values at any size (keys with quadrant masks),
+// 2 = the same without masks (gsr_api.hip tile_keys_mode(): GSR_TILE_KEYS, parity tests, read once per process)
+static inline TilePack tile_pack(int P, int W, int H, int force_mode) {
+  const bool force = force_mode != 0;
   TilePack t;
   t.tile_bits = tile_key_bits(W, H);
   int gb = 1;
@@ -101,7 +98,7 @@ static inline TilePack tile_pack(int P, int W, int H) {
   t.packed = gb + t.tile_bits <= 32 && !force;
   t.gbits = t.packed ? gb : 0;
   t.gmask = t.packed ? (uint32_t)((1ull << gb) - 1ull) : 0xFFFFFFFFu;
-  t.qmask = !t.packed && t.tile_bits <= GSR_QMASK_SHIFT && !(e != nullptr && strcmp(e, "plain") == 0);
+  t.qmask = !t.packed && t.tile_bits <= GSR_QMASK_SHIFT && force_mode != 2;
   t.tmask = t.tile_bits >= 32 ? 0xFFFFFFFFu : (uint32_t)((1ull << t.tile_bits) - 1ull);
   return t;
 }
@@ -121,13 +118,6 @@ static inline DigitPlan digit_plan(int key_bits, int max_bits = GSR_RADIX_BITS) 
   d.passes = (key_bits + max_bits - 1) / max_bits;
   d.bits = (key_bits + d.passes - 1) / d.passes;
   return d;
-}
-// widest digit of the tile sort (GSR_TILE_SORT_BITS, A/B; default GSR_RADIX_BITS: a 12-bit tile id in 2 passes of 6,
-// 8 bits or fewer in one pass)
-static inline int tile_sort_bits() {
-  const char* e = getenv("GSR_TILE_SORT_BITS");
-  const int b = e != nullptr ? atoi(e) : GSR_RADIX_BITS;
-  return b >= 2 && b <= GSR_RADIX_BITS ? b : GSR_RADIX_BITS;
 }
 // Segments of a view set (kernel argument): segment v = items [start[v], start[v] + n[v]) of a
 // flat array, cut into blocks of `tile` items; blocks of segment v are [blk[v], blk[v+1]).
@@ -252,6 +242,11 @@ struct GeomState {
 
 // Per-instance state of a view set ("binning"): the (tile, Gaussian) pairs of view v are
 // [start_v, start_v + K_v) with start_v = K_0 + ... + K_{v-1}.
+// Aliasing contract: after the tile sort, key[r] (r = the sort's result index) holds the sorted list and key[r ^ 1]
+// is free.  The tile-wave forward stores there, one byte per listed instance, the instance's 4-bit quadrant mask
+// (RenderSet::qbytes) and records in ImageState::split_mode[1] that it did; the set's backward reads those bytes
+// for its cull.  Nothing may write key[r ^ 1] between a set's forward and its backward(s) (the binning buffer
+// belongs to that one forward: gsr_set_render ... gsr_set_backward in include/gsr.h).
 struct BinningState {
   uint32_t* key[2];        // tile id ping-pong
   uint32_t* val[2];        // Gaussian index ping-pong; after the sort: sorted position -> Gaussian

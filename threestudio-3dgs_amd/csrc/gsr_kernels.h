@@ -31,6 +31,7 @@ void launch_binning_counts(int V, int P, const GeomState& g, hipStream_t stream)
 // dkeys = the depth sort's key buffer (sorted depth keys; culled = ~0)
 void launch_emit(int V, int P, int W, const GeomState& g, const SegInfo& inst, const TilePack& tp, uint32_t* keys,
                  uint32_t* vals, hipStream_t stream);
+// per-tile [start, end) of each view's sorted list, by search (k_tile_bounds)
 void launch_tile_ranges(SegInfo inst, int n_tiles, const TilePack& tp, const uint32_t* keys, uint2* ranges,
                         hipStream_t stream);
 void launch_mark_visible(int P, const float* means3D, const float* view, const float* proj,
@@ -121,8 +122,6 @@ inline bool split_forward(int V, int P, int width, int height, long long instanc
 }
 // Each view's super-tiles by listed instances, heaviest first (after binning) — gsr_render.hip
 void launch_tile_order(int V, int gx, int gy, const uint2* ranges, uint32_t* order, hipStream_t stream);
-// GSR_TILE_ORDER=raster: the blends dispatch views in turn in raster order (A/B); the order is still written
-bool tile_order_on();
 // instances: the set's rectangle tiles (sum of K) — picks the forward kernel (gsr_render.hip)
 void launch_render_forward(const RenderSet& rs, const GeomState& g, const uint32_t* sorted_gauss,
                            const ImageState& img, float* out_color, float* out_depth, float* out_alpha,

@@ -214,7 +214,10 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(GSR_FWD_WPE,
   uint32_t gi_next = 0u;
   const float* col2 = rs.col2;
   // quadrant masks in the keys (TilePack::qmask): the keep decision comes with the index, and only this
-  // quadrant's candidates are gathered (k_emit ran the same quadrant_hit)
+  // quadrant's candidates are gathered.  k_emit forms the masks with span_quads (a band / column bound on the
+  // alpha >= 1/255 ellipse), not with quadrant_hit: the two tests differ, but each keeps every quadrant that holds
+  // a blending pixel, so the blended candidates per pixel, and the outputs, are the same
+  // (tests/test_quadrant_bounds.py)
   const uint32_t* qkeys = rs.qkeys ? rs.qkeys + rs.inst_start[v] + range.x : nullptr;
   const int qsh = GSR_QMASK_SHIFT + q;
   bool kn = false, kn_next = false;  // the keep bits of the batch in n0..n3 / of gi_next
@@ -443,46 +446,29 @@ __global__ __launch_bounds__(256) void k_tile_info(RenderSet rs, const uint2* __
 // one thread per candidate then adds the four quadrants and writes ONE 48-byte gradient row per
 // instance.
 
-//
-// Two-colour variant (TWO, the SuGaR normal renderer's two rasterizer calls on shared geometry in one
-// pass): the replay forms both calls' dL/dalpha (the second with its own dL/dpixel and accumulated
-// colour, no depth / alpha terms), u_1 = G dL/dalpha_1 and u = u_1 + u_2; 16 sums per candidate:
-//   0-5 the u moments, 6-9 sum w dL/d(r,g,b,depth), 10-12 sum u_1 (1, x, y), 13-15 sum w dL/d(r2,g2,b2)
-// from 4 candidates per product (A rows 0-3 u, 4-7 u_1, 8-11 w; B columns 6-12 the 7 pixel planes).
-//
-// Hit-list variant (HITS; the default for the two-colour backward, where SuGaR's ~13-pixel Gaussians
-// leave most of a product's 64 pixels empty): the replay appends each (pixel, candidate) pair that
-// blended, (u, u_1, w, pixel), to its wave's list (ballot-compacted, candidate after candidate); after
-// the batch one thread per kept (candidate, quadrant) pair of the whole workgroup walks that pair's
-// hits and forms the same sums (moments about the quadrant centre, exact products x^2, x y, y^2 of the
-// half-integer offsets), so a batch's sums cost one pass over its hits on one wave instead of 16
-// matrix-core products per 4 candidates on every wave.  A wave whose list fills sums its finished
-// candidates itself first.  Fixed order per pair: bitwise repeatable.
+// (The SuGaR renderer's two-colour backward, whose Gaussians blend at ~13 pixels, forms its sums from hit
+// lists instead: k_render_bwd_tw below.)
 #define NGV2 16
 #define GSR_QSUM_STRIDE 41   // floats per candidate: 4 quadrants x 10 raw sums, +1 pad
-#define GSR_QSUM_STRIDE2 65  // two colours: 4 x 16, +1
-// Hit-list sums (HITS): per wave a buffer of the (pixel, candidate) pairs that blended, HCAP entries
-// (sized so the workgroup keeps 5 / 4 workgroups per CU like the matrix-core variant)
-#define GSR_HCAP1 208
+// uw: offset of the A operand's 16-pixel group g (256 floats each): groups 0, 2 at 0, 256 and groups 1, 3 at 528, 784,
+// so the groups a 4-B write's lane half holds (0-1 for lanes 0-31, 2-3 for 32-63) lie 16 banks apart (the writes
+// of pixels p and p + 16 do not conflict) and every 16-B read stays conflict-free (offsets of 16 dwords only
+// rotate a read group's banks); 16 floats of padding in all (a pad per group would cost the 5th workgroup per CU:
+// LDS is allocated in 1280-byte granules, 5 x 25 of 128 per CU)
+__device__ __forceinline__ int gsr_uw_pg(int g) { return 256 * (g >> 1) + ((g & 1) ? 528 : 0); }
 #define GSR_HCAP2 160
-template <bool TWO, bool HITS>
+// (LDS is allocated in 1280-byte granules: 5 workgroups of the backward per CU need <= 25 of the 128)
+#define GSR_BWD_LDS_5WG (25 * 1280)
 struct BwdLDS {
   float4 s0[65], s1[65], s2[65];
-  float4 s3[TWO ? 65 : 1];  // two colours: the second colour
   uint32_t slot[64];
-  // per wave: kept candidates of the batch (matrix-core sums: batch index; hit lists: index | first hit
-  // << 8 | hits << 16)
-  uint32_t list[4][64];
-  float qsum[64 * (TWO ? GSR_QSUM_STRIDE2 : GSR_QSUM_STRIDE)];
+  uint32_t list[4][64];  // per wave: the batch indices of its kept candidates
+  float qsum[64 * GSR_QSUM_STRIDE];
   // per wave: the group's A operand, u = G dL/dalpha (slots 0-7) and w = alpha T (slots 8-15) of
   // its 8 candidates, stored so that MFMA lane l's 16 values are 4 chunks of 16 B (swizzled:
-  // conflict-free 16-B reads, 2-way 4-B writes)
-  float uw[4][HITS ? 4 : 64 * 16];
-  // hit lists: per wave (u, u_1, w, pixel) of each blended (pixel, candidate), candidate after candidate
-  float4 hits[4][HITS ? (TWO ? GSR_HCAP2 : GSR_HCAP1) : 1];
-  // hit lists: per pixel of each quadrant dL/d(r, g, b, depth) (two colours: + dL/d(r2, g2, b2), 0)
-  float4 planes[4][HITS ? (TWO ? 128 : 64) : 1];
-  uint32_t pend[4];  // hit lists: per wave, kept candidates already summed | kept count << 8
+  // conflict-free 16-B reads); 16-pixel group g at gsr_uw_pg(g), so a row's 4-B writes from pixels p and
+  // p + 16 land in different banks (conflict-free)
+  float uw[4][3 * 256 + 16 + 256];
   unsigned long long kmask[4];  // per quadrant: kept candidates of the batch
 #ifdef GSR_TIMELINE
   int tl_cnt[4];
@@ -772,10 +758,6 @@ void launch_tile_order(int V, int gx, int gy, const uint2* ranges, uint32_t* ord
   if (V > 0 && gx > 0 && gy > 0) hipLaunchKernelGGL(k_tile_order, dim3(V), dim3(256), 0, stream, gx, gy, ranges, order);
 }
 
-bool tile_order_on() {
-  const char* e = getenv("GSR_TILE_ORDER");
-  return !(e != nullptr && strcmp(e, "raster") == 0);
-}
 
 // The split backward's chunk sums -> suffix sums (slot k: the colour / depth blended from candidate k CH to
 // the quadrant's last blend), in place; one workgroup per tile, a wave per quadrant, slots 1 .. the one
@@ -886,20 +868,18 @@ void launch_render_forward(const RenderSet& rs, const GeomState& g, const uint32
 
 // One workgroup's backward of one tile: the whole blended prefix, or with `split` (split_on) chunk `chunk`,
 // candidates [chunk CH, (chunk + 1) CH) (chunk GSR_SPLIT_NCK: to the end of the prefix).
-template <bool TWO, bool HITS>
-__device__ __forceinline__ void bwd_tile(BwdLDS<TWO, HITS>& s, const RenderSet& rs, int v, int tile, int chunk, bool split,
+__device__ __forceinline__ void bwd_tile(BwdLDS& s, const RenderSet& rs, int v, int tile, int chunk, bool split,
                                          const uint2* __restrict__ ranges, const uint32_t* __restrict__ quad_maxc,
                                          const uint32_t* __restrict__ sorted_gauss, const GaussRec* __restrict__ rec,
                                          const uint32_t* __restrict__ goff, const float* __restrict__ final_Ts,
                                          const uint32_t* __restrict__ n_contrib, const float* __restrict__ dL_dcolor,
                                          const float* __restrict__ dL_ddepth, const float* __restrict__ dL_dalpha,
                                          float4* __restrict__ grow, unsigned long long* __restrict__ reach) {
-  constexpr int NG = TWO ? NGV2 : NGV;                           // raw sums per (candidate, quadrant)
-  constexpr int QS = TWO ? GSR_QSUM_STRIDE2 : GSR_QSUM_STRIDE;  // per candidate
-  constexpr int GS = TWO ? 4 : 8;                                // candidates per 16x16 product
-  constexpr int NPL = TWO ? 7 : 4;                               // dL/dpixel planes in the B operand
-  constexpr int RW = TWO ? 4 : 3;                                // float4 per gradient row
-  constexpr int HCAP = TWO ? GSR_HCAP2 : GSR_HCAP1;              // hit-list entries per wave
+  constexpr int NG = NGV;               // raw sums per (candidate, quadrant)
+  constexpr int QS = GSR_QSUM_STRIDE;    // per candidate
+  constexpr int GS = 8;                  // candidates per 16x16 product
+  constexpr int NPL = 4;                 // dL/dpixel planes in the B operand
+  constexpr int RW = 3;                  // float4 per gradient row
   GSR_TL_BEGIN
   const int W = rs.W, H = rs.H, grid_x = rs.gx;
   const size_t vgs = (size_t)(rs.v0 + v);
@@ -978,16 +958,6 @@ __device__ __forceinline__ void bwd_tile(BwdLDS<TWO, HITS>& s, const RenderSet& 
     }
   }
   const float bg_dot = bg_dot3(bg, dpix[0], dpix[1], dpix[2]);
-  // two colours: the second call's dL/dpixel (same background, no depth / alpha outputs)
-  float dpix2[3] = {0.f, 0.f, 0.f};
-  if (TWO && inside) {
-    const float* d2 = rs.dpix2 + (size_t)v * 3 * HW;
-    dpix2[0] = d2[pid];
-    dpix2[1] = d2[HW + pid];
-    dpix2[2] = d2[2 * HW + pid];
-  }
-  const float nbg2 = TWO ? -T_final * bg_dot3(bg, dpix2[0], dpix2[1], dpix2[2]) : 0.f;
-  float S2 = 0.f;
 
   // The reference keeps per channel the colour accumulated behind the current Gaussian
   // (accum_rec = last_alpha last_c + (1 - last_alpha) accum_rec, deferred by one contributor) and
@@ -1029,7 +999,6 @@ __device__ __forceinline__ void bwd_tile(BwdLDS<TWO, HITS>& s, const RenderSet& 
     return r >= 0 ? (sorted_gauss[range.x + r] & gmask) : 0u;
   };
   float4 npc = zero4;  // the next batch's piece (piece 3 also carries the Gaussian's first row slot)
-  float4 npc2 = zero4;  // two colours: piece 2's thread also moves the second colour
   uint32_t ngo = 0u;
   uint32_t gi_next = 0u;
   // this view's reach bit (staged candidates have rows): word v >> 5 of the Gaussian's 64 bits
@@ -1047,12 +1016,8 @@ __device__ __forceinline__ void bwd_tile(BwdLDS<TWO, HITS>& s, const RenderSet& 
     const uint32_t g0 = fetch_index(hi);
     if (hi - 1 - cs >= lo) {
       npc = reinterpret_cast<const float4*>(rec + g0)[piece];
-      if (piece == 2 && rs.col2 != nullptr) {
-        if (TWO)
-          npc2 = make_float4(rs.col2[3 * g0], rs.col2[3 * g0 + 1], rs.col2[3 * g0 + 2], 0.f);
-        else  // the second rasterizer call's colours replace the first's
-          npc = make_float4(rs.col2[3 * g0], rs.col2[3 * g0 + 1], rs.col2[3 * g0 + 2], 0.f);
-      }
+      if (piece == 2 && rs.col2 != nullptr)  // the second rasterizer call's colours replace the first's
+        npc = make_float4(rs.col2[3 * g0], rs.col2[3 * g0 + 1], rs.col2[3 * g0 + 2], 0.f);
       if (piece == 3) {
         ngo = goff[g0];
 #ifndef GSR_EXP_NOREACH
@@ -1067,7 +1032,6 @@ __device__ __forceinline__ void bwd_tile(BwdLDS<TWO, HITS>& s, const RenderSet& 
   // contribute zeros.  Returns per pixel u = G dL/dalpha (the mean2D / conic / opacity
   // gradients are linear in u's moments over the pixel offsets) and w = alpha T (the colour / depth
   // weights); the sums over the quadrant's 64 pixels are formed by the matrix cores (below).
-  bool rhit = false;  // the last replay step blended this lane's pixel (hit lists)
   auto replay = [&](const float4& ga, const float4& gb, const float4& gc, float& u, float& w) {
     const uint32_t rel = __float_as_uint(gb.w);
     const float dx = ga.x - pxf, dy = ga.y - pyf;
@@ -1075,7 +1039,6 @@ __device__ __forceinline__ void bwd_tile(BwdLDS<TWO, HITS>& s, const RenderSet& 
     const float G = __builtin_amdgcn_exp2f(power2);
     const float alpha = fminf(GSR_ALPHA_MAX, gb.y * G);
     const bool hit = rel < last_contributor && power2 <= 0.0f && alpha >= GSR_ALPHA_MIN;
-    rhit = hit;
     const float a_eff = hit ? alpha : 0.0f;
     const float g_eff = hit ? G : 0.0f;
     const float oma = 1.f - a_eff;
@@ -1087,30 +1050,6 @@ __device__ __forceinline__ void bwd_tile(BwdLDS<TWO, HITS>& s, const RenderSet& 
     w = a_eff * T;
     S = fmaf(a_eff, cd, oma * S);
     Sd = fmaf(a_eff, gb.z, oma * Sd);
-  };
-  // two colours: gd = the second colour; uT = u_1 + u_2, u1 = u_1
-  auto replay2 = [&](const float4& ga, const float4& gb, const float4& gc, const float4& gd, float& uT, float& u1,
-                     float& w) {
-    const uint32_t rel = __float_as_uint(gb.w);
-    const float dx = ga.x - pxf, dy = ga.y - pyf;
-    const float power2 = gauss_power2(ga.z, ga.w, gb.x, dx, dy);
-    const float G = __builtin_amdgcn_exp2f(power2);
-    const float alpha = fminf(GSR_ALPHA_MAX, gb.y * G);
-    const bool hit = rel < last_contributor && power2 <= 0.0f && alpha >= GSR_ALPHA_MIN;
-    rhit = hit;
-    const float a_eff = hit ? alpha : 0.0f;
-    const float g_eff = hit ? G : 0.0f;
-    const float oma = 1.f - a_eff;
-    const float inv_1ma = fast_rcp(oma);
-    T = T * inv_1ma;
-    const float cd = fmaf(gc.x, dpix[0], fmaf(gc.y, dpix[1], fmaf(gc.z, dpix[2], dpix_a)));
-    const float cd2 = fmaf(gd.x, dpix2[0], fmaf(gd.y, dpix2[1], gd.z * dpix2[2]));
-    u1 = g_eff * fmaf(T, fmaf(gb.z - Sd, dpix_d, cd - S), inv_1ma * nbg);
-    uT = fmaf(g_eff, fmaf(T, cd2 - S2, inv_1ma * nbg2), u1);
-    w = a_eff * T;
-    S = fmaf(a_eff, cd, oma * S);
-    Sd = fmaf(a_eff, gb.z, oma * Sd);
-    S2 = fmaf(a_eff, cd2, oma * S2);
   };
 
 
@@ -1141,21 +1080,12 @@ __device__ __forceinline__ void bwd_tile(BwdLDS<TWO, HITS>& s, const RenderSet& 
   // (other lanes' pixels) goes through LDS once, in the qsum area (first written after the first
   // staging barrier, by which time every wave has read its bv).
   float bv[16];
-  if constexpr (HITS) {
-    // hit lists: this quadrant's dL/dpixel planes, read per hit by whichever thread sums the pair
-    s.planes[q][TWO ? 2 * lane : lane] = make_float4(dpix[0], dpix[1], dpix[2], dpix_d);
-    if (TWO) s.planes[q][2 * lane + 1] = make_float4(dpix2[0], dpix2[1], dpix2[2], 0.f);
-  } else {
+  {
     float* sdp = s.qsum + q * (NPL * 68 + 16);
     sdp[0 * 68 + lane] = dpix[0];
     sdp[1 * 68 + lane] = dpix[1];
     sdp[2 * 68 + lane] = dpix[2];
     sdp[3 * 68 + lane] = dpix_d;
-    if (TWO) {
-      sdp[4 * 68 + lane] = dpix2[0];
-      sdp[5 * 68 + lane] = dpix2[1];
-      sdp[6 * 68 + lane] = dpix2[2];
-    }
     if (lane < 16) sdp[NPL * 68 + lane] = 0.f;
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     const float4* dsrc =
@@ -1174,81 +1104,24 @@ __device__ __forceinline__ void bwd_tile(BwdLDS<TWO, HITS>& s, const RenderSet& 
     }
   }
   float* uw = s.uw[q];
-  // writer side: (slot r, pixel p = lane) -> 16 r + 256 (p >> 4) + 4 (((p >> 2) & 3) ^ ((r >> 2) & 3)) + (p & 3)
+  // writer side: (slot r, pixel p = lane) -> 16 r + PG(p >> 4) + 4 (((p >> 2) & 3) ^ ((r >> 2) & 3)) + (p & 3),
+  // PG = gsr_uw_pg
   int wa[4];
 #pragma unroll
-  for (int sgrp = 0; sgrp < 4; ++sgrp) wa[sgrp] = 256 * (lane >> 4) + 4 * (((lane >> 2) & 3) ^ sgrp) + (lane & 3);
-  // reader side: chunk k of lane l at 16 l + 4 (k ^ ((l >> 2) & 3))
-  const float4* asrc = reinterpret_cast<const float4*>(uw + 16 * lane);
+  for (int sgrp = 0; sgrp < 4; ++sgrp)
+    wa[sgrp] = gsr_uw_pg(lane >> 4) + 4 * (((lane >> 2) & 3) ^ sgrp) + (lane & 3);
+  // reader side: chunk k of lane l at 16 (l & 15) + PG(l >> 4) + 4 (k ^ ((l >> 2) & 3))
+  const float4* asrc = reinterpret_cast<const float4*>(uw + 16 * (lane & 15) + gsr_uw_pg(lane >> 4));
   const int aswz = (lane >> 2) & 3;
   // result side: lane l holds rows 4 (l >> 4) + r -> candidate mb + r of the group, u (rows 0-7,
   // columns 0-5 used) or w (rows 8-15, columns 6-9 used)
-  // two colours: rows 4 (l >> 4) + r are candidate r's u (lanes 0-15, columns 0-5), u_1 (16-31,
-  // columns 0-2 -> sums 10-12) or w (32-47, columns 6-12 -> sums 6-9, 13-15); lanes 48-63 unused
-  const int mb = TWO ? 0 : 4 * ((lane >> 4) & 1);
-  bool useful;
-  int field = ncol;
-  if (TWO) {
-    const int rg = lane >> 4;
-    useful = rg == 0 ? ncol < 6 : rg == 1 ? ncol < 3 : rg == 2 ? dcol : false;
-    field = rg == 1 ? 10 + ncol : (rg == 2 && ncol >= 10) ? ncol + 3 : ncol;
-  } else {
-    useful = (lane < 32) ? (ncol < 6) : dcol;
-  }
-  if (TWO && !HITS) {
-    // A rows 12-15 are never written: zero them once (their products are not read either)
-#pragma unroll
-    for (int r = 12; r < 16; ++r) s.uw[q][16 * r + wa[3]] = 0.f;
-  }
+  const int mb = 4 * ((lane >> 4) & 1);
+  const bool useful = (lane < 32) ? (ncol < 6) : dcol;
+  const int field = ncol;
 
   uint32_t* mylist = s.list[q];
   float* myq = s.qsum + q * NG;
 
-  // hit lists: the sums of one kept (candidate, quadrant qq) pair from its hits, list entry e =
-  // batch index | first hit << 8 | hits << 16, into the pair's qsum slots (same fields as the
-  // matrix-core product: x, y = pixel offsets from the quadrant centre)
-  auto pair_sums = [&](int qq, uint32_t e, float (&c)[NG]) {
-    const int st = (int)((e >> 8) & 255u), n = (int)(e >> 16);
-    const float4* hb = s.hits[qq];
-    const float4* pl = s.planes[qq];
-#pragma unroll
-    for (int f = 0; f < NG; ++f) c[f] = 0.f;
-    for (int k = st; k < st + n; ++k) {
-      const float4 hv = hb[k];
-      const uint32_t p = __float_as_uint(hv.w);
-      const float x = (float)(p & 7u) - 3.5f, y = (float)(p >> 3) - 3.5f;
-      const float u = hv.x, w = hv.z;
-      c[0] += u;
-      c[1] = fmaf(u, x, c[1]);
-      c[2] = fmaf(u, y, c[2]);
-      c[3] = fmaf(u, x * x, c[3]);  // (x^2, x y, y^2 of half-integers are exact)
-      c[4] = fmaf(u, x * y, c[4]);
-      c[5] = fmaf(u, y * y, c[5]);
-      const float4 d = pl[TWO ? 2 * p : p];
-      c[6] = fmaf(w, d.x, c[6]);
-      c[7] = fmaf(w, d.y, c[7]);
-      c[8] = fmaf(w, d.z, c[8]);
-      c[9] = fmaf(w, d.w, c[9]);
-      if constexpr (TWO) {
-        const float u1 = hv.y;
-        const float4 d2 = pl[2 * p + 1];
-        c[10 % NG] += u1;
-        c[11 % NG] = fmaf(u1, x, c[11 % NG]);
-        c[12 % NG] = fmaf(u1, y, c[12 % NG]);
-        c[13 % NG] = fmaf(w, d2.x, c[13 % NG]);
-        c[14 % NG] = fmaf(w, d2.y, c[14 % NG]);
-        c[15 % NG] = fmaf(w, d2.z, c[15 % NG]);
-      }
-    }
-  };
-  // (a list that filled: its finished pairs' sums wait in qsum for the flush)
-  auto sum_pair = [&](int qq, uint32_t e) {
-    float c[NG];
-    pair_sums(qq, e, c);
-    float* dst = s.qsum + (int)(e & 63u) * QS + NG * qq;
-#pragma unroll
-    for (int f = 0; f < NG; ++f) dst[f] = c[f];
-  };
   for (int h = hi; h > lo; h -= 64) {
     {
       const int rel_c = h - 1 - cs;
@@ -1260,7 +1133,6 @@ __device__ __forceinline__ void bwd_tile(BwdLDS<TWO, HITS>& s, const RenderSet& 
           s.s1[cs] = make_float4(GSR_CONIC_K_AC * npc.x, npc.y, npc.z, __uint_as_float((uint32_t)rel_c));
         } else if (piece == 2) {
           s.s2[cs] = npc;
-          if (TWO) s.s3[cs] = npc2;
         } else {
           const uint32_t dx_ = __float_as_uint(npc.x), dy_ = __float_as_uint(npc.y);
           const int xmin = dx_ & 0xffff, ymin = dx_ >> 16, xmax = dy_ & 0xffff;
@@ -1270,14 +1142,8 @@ __device__ __forceinline__ void bwd_tile(BwdLDS<TWO, HITS>& s, const RenderSet& 
       if (h - 64 > lo) {
         if (h - 65 - cs >= lo) {
           npc = reinterpret_cast<const float4*>(rec + gi_next)[piece];
-          if (piece == 2 && rs.col2 != nullptr) {
-            const float4 c2 =
-                make_float4(rs.col2[3 * gi_next], rs.col2[3 * gi_next + 1], rs.col2[3 * gi_next + 2], 0.f);
-            if (TWO)
-              npc2 = c2;
-            else
-              npc = c2;
-          }
+          if (piece == 2 && rs.col2 != nullptr)
+            npc = make_float4(rs.col2[3 * gi_next], rs.col2[3 * gi_next + 1], rs.col2[3 * gi_next + 2], 0.f);
           if (piece == 3) {
             ngo = goff[gi_next];
 #ifndef GSR_EXP_NOREACH
@@ -1312,68 +1178,18 @@ __device__ __forceinline__ void bwd_tile(BwdLDS<TWO, HITS>& s, const RenderSet& 
 #ifdef GSR_TIMELINE
     if (lane == 0) s.tl_cnt[q] = cnt;
 #endif
-    if (!HITS && keep) mylist[mask_rank(bal)] = (uint32_t)lane;
+    if (keep) mylist[mask_rank(bal)] = (uint32_t)lane;
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // this wave's list is read back by its own lanes
     // kept candidates in groups of 8: replay -> (u, w) rows in LDS -> matrix-core sums.
     // The kept set is the uniform ballot mask: walk it with scalar bit scans, prefetching the next
     // candidate's staged record while the current one is replayed.
     unsigned long long rest = bal;
-    if constexpr (HITS) {
-      // replay -> the blended lanes' (u, u_1, w, pixel) appended to the wave's hit list; the sums wait
-      // for the batch's end (below) unless the list fills first
-      int fill = 0, done = 0;  // (wave-uniform) entries in use; kept candidates already summed
-#ifdef GSR_EXP_NOGROUP
-      if (cnt < 0) {
-#else
-      if (cnt > 0) {
-#endif
-        int j = (int)__builtin_ctzll(rest);
-        float4 ca = s.s0[j], cb = s.s1[j], cc = s.s2[j];
-        float4 cd2 = TWO ? s.s3[j] : zero4;
-        for (int c = 0; c < cnt; ++c) {
-          rest &= rest - 1ull;
-          const int jn = (c + 1 < cnt) ? (int)__builtin_ctzll(rest) : j;
-          const float4 na = s.s0[jn], nb = s.s1[jn], nc = s.s2[jn];
-          const float4 nd = TWO ? s.s3[jn] : zero4;
-          float u, u1 = 0.f, w;
-#ifdef GSR_EXP_NOREPLAY
-          u = ca.x * pxf;
-          w = cb.x * pyf;
-          rhit = ((lane + j) & 7) == 0;
-#else
-          if (TWO)
-            replay2(ca, cb, cc, cd2, u, u1, w);
-          else
-            replay(ca, cb, cc, u, w);
-#endif
-          const unsigned long long hm = __ballot(rhit);
-          const int n = __popcll(hm);
-          if (fill + n > HCAP) {
-            // list full: this wave sums its finished candidates now (one lane each), then starts over
-            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-            if (lane < c - done) sum_pair(q, mylist[done + lane]);
-            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // (in-order LDS: read before rewritten)
-            fill = 0;
-            done = c;
-          }
-          if (rhit) s.hits[q][fill + (int)mask_rank(hm)] = make_float4(u, u1, w, __uint_as_float((uint32_t)lane));
-          if (lane == 0) mylist[c] = (uint32_t)j | ((uint32_t)fill << 8) | ((uint32_t)n << 16);
-          fill += n;
-          ca = na;
-          cb = nb;
-          cc = nc;
-          cd2 = nd;
-          j = jn;
-        }
-      }
-      if (lane == 0) s.pend[q] = (uint32_t)done | ((uint32_t)cnt << 8);
-    } else
 #ifdef GSR_EXP_NOGROUP
     if (cnt < 0)
 #endif
     for (int g0 = 0; g0 < cnt; g0 += GS) {
       const int gn = min(GS, cnt - g0);
-      if (!TWO && gn == GS) {
+      if (gn == GS) {
         // a full group: the 8 replay steps without per-step branches, one basic block, so the independent
         // per-candidate terms (staged-record reads, alpha, exp2, 1 / (1 - alpha)) of later candidates can be
         // scheduled under earlier candidates' dependent updates (same operations, same order per pixel)
@@ -1402,35 +1218,24 @@ __device__ __forceinline__ void bwd_tile(BwdLDS<TWO, HITS>& s, const RenderSet& 
       } else {
       int j = (int)__builtin_ctzll(rest);
       float4 ca = s.s0[j], cb = s.s1[j], cc = s.s2[j];
-      float4 cd2 = TWO ? s.s3[j] : zero4;
 #pragma unroll
       for (int c = 0; c < GS; ++c) {
         if (c < gn) {
           rest &= rest - 1ull;
           const int jn = (c + 1 < gn) ? (int)__builtin_ctzll(rest) : j;
           const float4 na = s.s0[jn], nb = s.s1[jn], nc = s.s2[jn];
-          const float4 nd = TWO ? s.s3[jn] : zero4;
-          if (TWO) {
-            float uT, u1, w;
-            replay2(ca, cb, cc, cd2, uT, u1, w);
-            uw[16 * c + wa[0]] = uT;
-            uw[16 * (c + 4) + wa[1]] = u1;
-            uw[16 * (c + 8) + wa[2]] = w;
-          } else {
-            float u, w;
+          float u, w;
 #ifdef GSR_EXP_NOREPLAY
-            u = ca.x * pxf;
-            w = cb.x * pyf;
+          u = ca.x * pxf;
+          w = cb.x * pyf;
 #else
-            replay(ca, cb, cc, u, w);
+          replay(ca, cb, cc, u, w);
 #endif
-            uw[16 * c + wa[c >> 2]] = u;
-            uw[16 * (c + 8) + wa[2 + (c >> 2)]] = w;
-          }
+          uw[16 * c + wa[c >> 2]] = u;
+          uw[16 * (c + 8) + wa[2 + (c >> 2)]] = w;
           ca = na;
           cb = nb;
           cc = nc;
-          cd2 = nd;
           j = jn;
         }
       }
@@ -1466,7 +1271,6 @@ __device__ __forceinline__ void bwd_tile(BwdLDS<TWO, HITS>& s, const RenderSet& 
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // rows are rewritten by the next group
     }
     __syncthreads();
-    // (hit lists: the pairs the lists still hold are summed by their flush threads below)
 #ifdef GSR_TIMELINE
     if (t == 0) {
       const int c0 = s.tl_cnt[0], c1 = s.tl_cnt[1], c2 = s.tl_cnt[2], c3 = s.tl_cnt[3];
@@ -1491,27 +1295,12 @@ __device__ __forceinline__ void bwd_tile(BwdLDS<TWO, HITS>& s, const RenderSet& 
       const int qq = piece;
       const float4 ga = s.s0[cs];
       const float4 gb = s.s1[cs];
-      // two colours: m[10], m[11] the u_1 first moments, m[12-14] the second colour sums
-      constexpr int NM = TWO ? 15 : NGV;
+      constexpr int NM = NGV;
       float m[NM];
 #pragma unroll
       for (int i = 0; i < NM; ++i) m[i] = 0.f;
       if ((s.kmask[qq] >> cs) & 1ull) {
-        float Cv[NG];
-        if constexpr (HITS) {
-          // this (candidate, quadrant) pair's sums: from its hits, or from qsum when its wave's list filled
-          // before the batch's end (its rank among the quadrant's kept candidates is below pend's count)
-          const int rank = __popcll(s.kmask[qq] & ((1ull << cs) - 1ull));
-          if (rank >= (int)(s.pend[qq] & 255u)) {
-#pragma unroll
-            for (int f = 0; f < NG; ++f) Cv[f] = 0.f;
-            pair_sums(qq, s.list[qq][rank], Cv);
-          } else {
-#pragma unroll
-            for (int f = 0; f < NG; ++f) Cv[f] = s.qsum[cs * QS + NG * qq + f];
-          }
-        }
-        const float* C = HITS ? Cv : s.qsum + cs * QS + NG * qq;
+        const float* C = s.qsum + cs * QS + NG * qq;
         const float mx = ga.x - ((float)(txi * GSR_TILE_X + (qq & 1) * 8) + 3.5f);
         const float my = ga.y - ((float)(tyi * GSR_TILE_Y + (qq >> 1) * 8) + 3.5f);
         m[0] = C[0];
@@ -1524,13 +1313,6 @@ __device__ __forceinline__ void bwd_tile(BwdLDS<TWO, HITS>& s, const RenderSet& 
         m[7] = C[7];
         m[8] = C[8];
         m[9] = C[9];
-        if (TWO) {
-          m[10 % NM] = mx * C[10] - C[11];
-          m[11 % NM] = my * C[10] - C[12];
-          m[12 % NM] = C[13];
-          m[13 % NM] = C[14];
-          m[14 % NM] = C[15];
-        }
       }
 #pragma unroll
       for (int i = 0; i < NM; ++i) {
@@ -1552,11 +1334,7 @@ __device__ __forceinline__ void bwd_tile(BwdLDS<TWO, HITS>& s, const RenderSet& 
       } else if (qq == 1) {
         row[1] = make_float4(-0.5f * o * m[5], m[0], m[6], m[7]);
       } else if (qq == 2) {
-        row[2] = TWO ? make_float4(m[8], m[9], m[12 % NM], m[13 % NM]) : make_float4(m[8], m[9], 0.f, 0.f);
-      } else if (TWO) {
-        const float dmx1 = mean_grad(k, ddelx_dx, ga.z, ga.w, m[10 % NM], m[11 % NM]);
-        const float dmy1 = mean_grad(k, ddely_dy, gb.x, ga.w, m[11 % NM], m[10 % NM]);
-        row[3] = make_float4(m[14 % NM], dmx1, dmy1, 0.f);
+        row[2] = make_float4(m[8], m[9], 0.f, 0.f);
       }
     }
     __syncthreads();
@@ -1587,18 +1365,18 @@ __device__ __forceinline__ void bwd_tile(BwdLDS<TWO, HITS>& s, const RenderSet& 
 // that replay the split tiles' later chunks (split_on: the items k_ckpt_suffix listed, view << 26 | chunk << 22
 // | tile, count in items[0], at most rs.split_extra; a heavy tile's chunks run side by side instead of one
 // after the other, its own workgroup walks the chunks not listed, from ImageState::split_cap down).
-template <bool TWO, bool HITS>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(TWO ? 4 : 5, 8))) void k_render_bwd(
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5, 8))) void k_render_bwd(
     RenderSet rs, const uint2* __restrict__ ranges, const uint32_t* __restrict__ quad_maxc,
     const uint32_t* __restrict__ sorted_gauss, const GaussRec* __restrict__ rec, const uint32_t* __restrict__ goff,
     const float* __restrict__ final_Ts, const uint32_t* __restrict__ n_contrib, const float* __restrict__ dL_dcolor,
     const float* __restrict__ dL_ddepth, const float* __restrict__ dL_dalpha, float4* __restrict__ grow,
     unsigned long long* __restrict__ reach, int extra, const uint32_t* __restrict__ items) {
-  __shared__ BwdLDS<TWO, HITS> s;
+  __shared__ BwdLDS s;
+  static_assert(sizeof(BwdLDS) <= GSR_BWD_LDS_5WG, "backward blend: 5 workgroups per CU");
   int v, tile, chunk = 0;
   // the forward's split decision (ImageState::split_mode): checkpoints and items exist only then
-  const bool split = !TWO && rs.ckpt != nullptr && *rs.split_mode != 0u;
-  if (!TWO && (int)blockIdx.x < extra) {
+  const bool split = rs.ckpt != nullptr && *rs.split_mode != 0u;
+  if ((int)blockIdx.x < extra) {
     if (!split || blockIdx.x >= items[0]) return;
     const uint32_t it = items[1 + blockIdx.x];
     v = (int)(it >> 26) - rs.v0;
@@ -1609,29 +1387,28 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(TWO ? 4 : 5
     int q_unused;
     if (!block_map<4>((int)blockIdx.x - extra, rs, v, tile, q_unused)) return;
   }
-  bwd_tile<TWO, HITS>(s, rs, v, tile, chunk, split, ranges, quad_maxc, sorted_gauss, rec, goff, final_Ts,
+  bwd_tile(s, rs, v, tile, chunk, split, ranges, quad_maxc, sorted_gauss, rec, goff, final_Ts,
                 n_contrib, dL_dcolor, dL_ddepth, dL_dalpha, grow, reach);
 }
 
-// Backward with hit-list sums, NW waves per 16x16 tile, each walking its 4 / NW quadrants in turn (each lane
-// holds the same pixel of each of its quadrants) — the small-Gaussian regime (C5: SuGaR's surface Gaussians
-// blend at ~13 pixels, a candidate usually in one quadrant).  The workgroup-per-tile kernel above walks the
-// four quadrants in lockstep batches (three barriers per batch, each batch as long as its busiest quadrant:
-// 2.25 slots per kept pair at C5, waves parked on barriers two thirds of their cycles, profiles/r03/sq_c5/);
-// here a wave replays a batch's kept candidates quadrant after quadrant, so a batch costs the sum of its
-// quadrants' kept (candidate, quadrant) pairs.  NW = 1: one wave, nothing waits on another; NW = 2: two waves
-// (quadrants 0-1 and 2-3, half the per-lane pixel state: more waves per SIMD), two barriers per batch.
-// Per batch: lane c stages candidate c's record (wave 0 the conic / position / rect pieces and the cull
-// against the four quadrants, the last wave the colour pieces) and per quadrant the kept candidates are
-// replayed back to front (the same replay as k_render_bwd: per pixel the same candidates, order and
-// operations); the lanes that blended append (u, u_1, w, pixel) to their wave's hit list; lane c then forms
-// candidate c's sums from its hits (the same pair_sums order), turns them into moments about the mean and
-// adds the quadrants as ((q0 + q1) + (q2 + q3)) — the order of the other kernel's quad DPP adds — and wave 0
-// writes one row per staged candidate.  A full hit list is summed early (each pair's sums are formed once,
-// whenever).  Outputs match the hit-list k_render_bwd<TWO, true> bitwise.
+// Backward with hit-list sums, one wave per 16x16 tile walking the four quadrants in turn (each lane holds the
+// same pixel of each quadrant) — the small-Gaussian regime (C5: SuGaR's surface Gaussians blend at ~13 pixels, a
+// candidate usually in one quadrant).  A 64-pixel matrix-core product would carry mostly zeros there, and
+// lockstep quadrant waves would wait for the busiest quadrant of each batch (2.25 slots per kept pair at C5);
+// here a batch costs the sum of its quadrants' kept (candidate, quadrant) pairs and nothing waits on another wave.
+// Per batch: lane c stages candidate c's record and its cull against the four quadrants; per quadrant the kept
+// candidates are replayed back to front (the replay of k_render_bwd: per pixel the same candidates, order and
+// operations); the lanes that blended append (u, u_1, w, pixel) to the wave's hit list; lane c then forms
+// candidate c's sums from its hits (moments about the quadrant centre, exact x^2, x y, y^2 of the half-integer
+// offsets), turns them into moments about the mean, adds the quadrants as ((q0 + q1) + (q2 + q3)) and writes
+// one row per staged candidate.  A full hit list is summed early (each pair's sums are formed once, whenever).
+// Two colours (TWO, the SuGaR normal renderer's two rasterizer calls on shared geometry): the replay forms both
+// calls' dL/dalpha (the second with its own dL/dpixel and accumulated colour, no depth / alpha terms),
+// u_1 = G dL/dalpha_1 and u = u_1 + u_2; 16 sums per candidate: 0-5 the u moments, 6-9 sum w dL/d(r,g,b,depth),
+// 10-12 sum u_1 (1, x, y), 13-15 sum w dL/d(r2,g2,b2); 64-byte rows.
 #define GSR_HCAP_TW 256
-template <bool TWO, int NW>
-__global__ __launch_bounds__(64 * NW) void k_render_bwd_tw(
+template <bool TWO>
+__global__ __launch_bounds__(64) void k_render_bwd_tw(
     RenderSet rs, const uint2* __restrict__ ranges, const uint32_t* __restrict__ quad_maxc,
     const uint32_t* __restrict__ sorted_gauss, const GaussRec* __restrict__ rec, const uint32_t* __restrict__ goff,
     const float* __restrict__ final_Ts, const uint32_t* __restrict__ n_contrib, const float* __restrict__ dL_dcolor,
@@ -1640,16 +1417,13 @@ __global__ __launch_bounds__(64 * NW) void k_render_bwd_tw(
   constexpr int NG = TWO ? NGV2 : NGV;  // raw sums per (candidate, quadrant)
   constexpr int NM = TWO ? 15 : NGV;    // moments per candidate
   constexpr int RW = TWO ? 4 : 3;       // float4 per gradient row
-  constexpr int NQ = 4 / NW;            // quadrants per wave
-  static_assert(NW == 1 || NW == 2, "one or two waves per tile");
+  constexpr int NQ = 4;                 // quadrants per wave
   __shared__ float4 s0[65], s1[65], s2[65];
   __shared__ float4 s3[65];  // (b, b2) of the interleaved colours
   __shared__ uint32_t slot[64];
-  __shared__ uint32_t skeep[NW > 1 ? 64 : 1];          // the cull's 4-bit quadrant masks (NW = 2)
-  __shared__ float sacc[NW > 1 ? NM * 64 : 1];          // wave 1's (q2 + q3) moments (NW = 2)
-  __shared__ uint32_t slist[NW][64];                    // the current quadrant: first hit | hits << 16
-  __shared__ float4 shits[NW][GSR_HCAP_TW];             // (u, u_1, w, pixel) of the current quadrant's blends
-  __shared__ float4 splanes[NW][TWO ? 128 : 64];        // the current quadrant's dL/dpixel per pixel
+  __shared__ uint32_t list[64];                  // the current quadrant: first hit | hits << 16
+  __shared__ float4 hits[GSR_HCAP_TW];            // (u, u_1, w, pixel) of the current quadrant's blends
+  __shared__ float4 planes[TWO ? 128 : 64];       // the current quadrant's dL/dpixel per pixel
   int v, tile, q_unused;
   if (!block_map<4>(blockIdx.x, rs, v, tile, q_unused)) return;
   GSR_TL_BEGIN
@@ -1672,11 +1446,7 @@ __global__ __launch_bounds__(64 * NW) void k_render_bwd_tw(
   }
   const float* bg = rs.bg[v];
   const int lane = threadIdx.x & 63;
-  const int wv = NW > 1 ? __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6)) : 0;
-  const int qb = NQ * wv;  // this wave's first quadrant
-  uint32_t* list = slist[wv];
-  float4* hits = shits[wv];
-  float4* planes = splanes[wv];
+  constexpr int qb = 0;  // (the wave's first quadrant)
   const int txi = tile % grid_x, tyi = tile / grid_x;
   const uint2 range = ranges[tile];
   const uint4 qm = reinterpret_cast<const uint4*>(quad_maxc)[tile];
@@ -1747,8 +1517,7 @@ __global__ __launch_bounds__(64 * NW) void k_render_bwd_tw(
   const float4 zero4 = make_float4(0.f, 0.f, 0.f, 0.f);
 
   // lane c stages candidate c (list position h - 1 - c) of each batch, one batch ahead; indices two batches
-  // ahead.  Wave 0: rec.a, rec.b (the cull), rec.d + the row slot; the last wave: rec.c and the second colour.
-  const bool stage_geo = wv == 0, stage_col = wv == NW - 1;
+  // ahead: rec.a, rec.b (the cull), rec.d + the row slot, rec.c and the second colour.
   const uint32_t gmask = rs.gmask;
   unsigned int* const reach32 = reinterpret_cast<unsigned int*>(reach) + (v >> 5);
   const unsigned int vbit = 1u << (v & 31);
@@ -1756,7 +1525,7 @@ __global__ __launch_bounds__(64 * NW) void k_render_bwd_tw(
   uint32_t ngo = 0u, gi_next = 0u;
   auto load = [&](uint32_t g) {
     const float4* r = reinterpret_cast<const float4*>(rec + g);
-    if (stage_geo) {
+    {
       na = r[0];
       nb = r[1];
       nd = r[3];
@@ -1765,7 +1534,7 @@ __global__ __launch_bounds__(64 * NW) void k_render_bwd_tw(
       atomicOr(reach32 + 2 * g, vbit);  // the Gaussian gets a row in this view (k_view_grad reads it)
 #endif
     }
-    if (stage_col) {
+    {
       nc = r[2];
       if (rs.col2 != nullptr) {
         const float4 c2 = make_float4(rs.col2[3 * g], rs.col2[3 * g + 1], rs.col2[3 * g + 2], 0.f);
@@ -1792,8 +1561,8 @@ __global__ __launch_bounds__(64 * NW) void k_render_bwd_tw(
   }
 
   // hit-list sums of one (candidate, quadrant) pair -> moments about the candidate's mean (the flush of
-  // k_render_bwd); acc = q0 + q1 (NW = 2: this wave's pair, q0 + q1 or q2 + q3), accb = q2 + q3 (NW = 1)
-  float acc[NM], accb[NW == 1 ? NM : 1];
+  // k_render_bwd); acc = q0 + q1, accb = q2 + q3
+  float acc[NM], accb[NM];
   auto pair_moments = [&](const int qq, const uint32_t e, float (&m)[NM]) {
     const int st = (int)(e & 0xffffu), n = (int)(e >> 16);
     float C[NG];
@@ -1856,8 +1625,8 @@ __global__ __launch_bounds__(64 * NW) void k_render_bwd_tw(
     for (int i = 0; i < NM; ++i) {
       if (j == 0) acc[i] = m[i];
       else if (j == 1) acc[i] = acc[i] + m[i];
-      else if (j == 2) accb[i % (NW == 1 ? NM : 1)] = m[i];
-      else accb[i % (NW == 1 ? NM : 1)] = accb[i % (NW == 1 ? NM : 1)] + m[i];
+      else if (j == 2) accb[i] = m[i];
+      else accb[i] = accb[i] + m[i];
     }
   };
 
@@ -1865,7 +1634,7 @@ __global__ __launch_bounds__(64 * NW) void k_render_bwd_tw(
     const int rel_c = h - 1 - lane;
     const bool staged = rel_c >= lo;
     uint32_t keep4 = 0u;
-    if (staged && stage_geo) {
+    if (staged) {
       // the pre-multiplied conic as s0 = (x, y, B, C), s1 = (A, opacity, depth, list position): the products the
       // step packs are adjacent; row slot
       s0[lane] = make_float4(na.x, na.y, GSR_CONIC_K_B * na.w, GSR_CONIC_K_AC * nb.x);
@@ -1884,9 +1653,8 @@ __global__ __launch_bounds__(64 * NW) void k_render_bwd_tw(
               quadrant_hit(na, nb, (float)(txi * GSR_TILE_X + (q & 1) * 8), (float)(tyi * GSR_TILE_Y + (q >> 1) * 8)))
             keep4 |= 1u << q;
       }
-      if (NW > 1) skeep[lane] = keep4;
     }
-    if (staged && stage_col) {
+    if (staged) {
       // colours interleaved with the second colours (zeros for one colour): (r, r2, g, g2), (b, b2)
       s2[lane] = make_float4(nc.x, n2.x, nc.y, n2.y);
       s3[lane] = make_float4(nc.z, n2.z, 0.f, 0.f);
@@ -1904,11 +1672,9 @@ __global__ __launch_bounds__(64 * NW) void k_render_bwd_tw(
     }
 #pragma unroll
     for (int i = 0; i < NM; ++i) acc[i] = 0.f;
-    if (NW == 1)
 #pragma unroll
-      for (int i = 0; i < NM; ++i) accb[i % (NW == 1 ? NM : 1)] = 0.f;
+    for (int i = 0; i < NM; ++i) accb[i] = 0.f;
     __syncthreads();  // (the staging of every wave before any wave's reads)
-    if (NW > 1) keep4 = staged ? skeep[lane] : 0u;
 #pragma unroll
     for (int j = 0; j < NQ; ++j) {
       const int q = qb + j;
@@ -1986,22 +1752,11 @@ __global__ __launch_bounds__(64 * NW) void k_render_bwd_tw(
       flush(j, pend);
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // (hits, list and planes are rewritten next)
     }
-    if (NW > 1) {
-      if (wv == 1)
-#pragma unroll
-        for (int i = 0; i < NM; ++i) sacc[i * 64 + lane] = acc[i];
-      __syncthreads();  // (wave 1's moments to wave 0; both waves' reads of the staged batch are done)
-    }
-    if (staged && wv == 0) {
+    if (staged) {
       // ((q0 + q1) + (q2 + q3)) per moment, then the reference's terms (k_render_bwd's flush)
       float m[NM];
-      if (NW > 1) {
 #pragma unroll
-        for (int i = 0; i < NM; ++i) m[i] = acc[i] + sacc[i * 64 + lane];
-      } else {
-#pragma unroll
-        for (int i = 0; i < NM; ++i) m[i] = acc[i] + accb[i % (NW == 1 ? NM : 1)];
-      }
+      for (int i = 0; i < NM; ++i) m[i] = acc[i] + accb[i];
       const float4 ga = s0[lane];
       const float4 gb = s1[lane];
       const float o = gb.y;
@@ -2021,385 +1776,40 @@ __global__ __launch_bounds__(64 * NW) void k_render_bwd_tw(
         row[3] = make_float4(m[14 % NM], dmx1, dmy1, 0.f);
       }
     }
-    if (NW == 1) __syncthreads();  // (the staged batch is rewritten next)
+    __syncthreads();  // (the staged batch is rewritten next)
   }
   GSR_TL_END(1, hi)
 }
 
-// Backward, one 64-thread wave per 16x16 tile with the matrix-core sums (the one-colour default, C3): the
-// quadrants walked in turn as in k_render_bwd_tw, each quadrant's kept candidates replayed in groups of 8 and
-// summed over the quadrant's 64 pixels by the same 16 v_mfma_f32_16x16x4_f32 products as k_render_bwd (same A
-// and B operands, same accumulator split), so every per-(candidate, quadrant) sum is bitwise the same; the
-// sums are turned into moments and added over the quadrants in the other kernel's order.  The workgroup
-// kernel spends its time in the quadrant lockstep (1.47 slots per kept pair at C3) and three barriers per
-// batch; here a batch costs its kept pairs.
-template <bool UNUSED>
-// 3 waves per SIMD: 168 VGPRs, no spills (the compiler's own choice counts the matrix-core accumulators as AGPRs
-// and stops at 2)
-__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3, 8))) void k_render_bwd_twm(
-    RenderSet rs, const uint2* __restrict__ ranges, const uint32_t* __restrict__ quad_maxc,
-    const uint32_t* __restrict__ sorted_gauss, const GaussRec* __restrict__ rec, const uint32_t* __restrict__ goff,
-    const float* __restrict__ final_Ts, const uint32_t* __restrict__ n_contrib, const float* __restrict__ dL_dcolor,
-    const float* __restrict__ dL_ddepth, const float* __restrict__ dL_dalpha, float4* __restrict__ grow,
-    unsigned long long* __restrict__ reach) {
-  constexpr int NM = NGV;
-  constexpr int GST = 11;  // floats per candidate of gsum (10 sums + pad)
-  __shared__ float4 s0[65], s1[65], s2[65];
-  __shared__ uint32_t slot[64];
-  __shared__ uint32_t klist[64];          // the current quadrant's kept candidates in order
-  __shared__ float uw[64 * 16];           // one group's A operand (k_render_bwd's swizzled layout)
-  __shared__ float dpl[4][4 * 68 + 16];   // per quadrant dL/d(r, g, b, depth) per pixel (+16 zeros): B's D part
-  __shared__ float gsum[64 * GST];        // the current quadrant's sums per candidate
-  int v, tile, q_unused;
-  if (!block_map<4>(blockIdx.x, rs, v, tile, q_unused)) return;
-  GSR_TL_BEGIN
-  const int W = rs.W, H = rs.H, grid_x = rs.gx;
-  const size_t vgs = (size_t)(rs.v0 + v);
-  const size_t HW = (size_t)H * W;
-  {
-    const size_t tiles = (size_t)rs.gx * rs.gy;
-    ranges += vgs * tiles;
-    quad_maxc += vgs * 4 * tiles;
-    sorted_gauss += rs.inst_start[v];
-    rec += vgs * rs.P;
-    goff += vgs * rs.P;
-    final_Ts += vgs * HW;
-    n_contrib += vgs * HW;
-    dL_dcolor += (size_t)v * 3 * HW;
-    if (dL_ddepth) dL_ddepth += (size_t)v * HW;
-    if (dL_dalpha) dL_dalpha += (size_t)v * HW;
-    grow += (size_t)3 * rs.row_start[v];
-  }
-  const float* bg = rs.bg[v];
-  const int lane = threadIdx.x;
-  const int txi = tile % grid_x, tyi = tile / grid_x;
-  const uint2 range = ranges[tile];
-  const uint4 qm = reinterpret_cast<const uint4*>(quad_maxc)[tile];
-  const int qmaxc[4] = {(int)qm.x, (int)qm.y, (int)qm.z, (int)qm.w};
-  const int hi = __builtin_amdgcn_readfirstlane((int)max(max(qm.x, qm.y), max(qm.z, qm.w)));
-  const int lo = 0;
-
-  float T[4], S[4], Sd[4], dp0[4], dp1[4], dp2[4], dpd[4], dpa[4], nbg[4];
-  uint32_t last[4];
-  const float lxf = (float)(txi * GSR_TILE_X + (lane & 7)), lyf = (float)(tyi * GSR_TILE_Y + (lane >> 3));
-#pragma unroll
-  for (int q = 0; q < 4; ++q) {
-    const int px = txi * GSR_TILE_X + (q & 1) * 8 + (lane & 7), py = tyi * GSR_TILE_Y + (q >> 1) * 8 + (lane >> 3);
-    const bool inside = px < W && py < H;
-    const size_t pid = (size_t)py * W + px;
-    const float T_final = inside ? final_Ts[pid] : 0.0f;
-    T[q] = T_final;
-    last[q] = inside ? n_contrib[pid] : 0u;
-    float d[3] = {0.f, 0.f, 0.f};
-    float dd = 0.f, da = 0.f;
-    if (inside) {
-      d[0] = dL_dcolor[pid];
-      d[1] = dL_dcolor[HW + pid];
-      d[2] = dL_dcolor[2 * HW + pid];
-      if (dL_ddepth) dd = dL_ddepth[pid];
-      if (dL_dalpha) da = dL_dalpha[pid];
-      if (rs.cbg != nullptr) {
-#pragma clang fp contract(off)
-        const float am = 1.0f - (1.0f - T_final);
-        const float* bgi = rs.cbg + ((size_t)v * HW + pid) * 3;
-        const float* col = rs.ccolor + (size_t)v * 3 * HW + pid;
-        float dsum = 0.0f;
-#pragma unroll
-        for (int ch = 0; ch < 3; ++ch) {
-          const float b = bgi[ch];
-          const float pre = col[(size_t)ch * HW] + am * b;
-          const float gch = (pre >= 0.0f && pre <= 1.0f) ? d[ch] : 0.0f;
-          d[ch] = gch;
-          dsum -= gch * b;
-          if (rs.dcbg != nullptr) rs.dcbg[((size_t)v * HW + pid) * 3 + ch] = gch * am;
-        }
-        da = dsum + da;
-      }
-    }
-    dp0[q] = d[0], dp1[q] = d[1], dp2[q] = d[2], dpd[q] = dd, dpa[q] = da;
-    nbg[q] = -T_final * bg_dot3(bg, d[0], d[1], d[2]);
-    S[q] = Sd[q] = 0.f;
-    float* sdp = dpl[q];
-    sdp[0 * 68 + lane] = d[0];
-    sdp[1 * 68 + lane] = d[1];
-    sdp[2 * 68 + lane] = d[2];
-    sdp[3 * 68 + lane] = dd;
-    if (lane < 16) sdp[4 * 68 + lane] = 0.f;
-  }
-  const float ddelx_dx = 0.5f * W, ddely_dy = 0.5f * H;
-  const float4 zero4 = make_float4(0.f, 0.f, 0.f, 0.f);
-
-  // the matrix-core operand maps of k_render_bwd (one colour)
-  const int ncol = lane & 15;
-  const bool dcol = ncol >= 6 && ncol < 10;
-  float fa[2], fbb[2], fc;
-#pragma unroll
-  for (int h = 0; h < 2; ++h) {
-    const float y = (float)(2 * (lane >> 4) + h) - 3.5f;
-    fa[h] = ncol == 0 ? 1.f : ncol == 2 ? y : ncol == 5 ? y * y : 0.f;
-    fbb[h] = ncol == 1 ? 1.f : ncol == 4 ? y : 0.f;
-  }
-  fc = ncol == 3 ? 1.f : 0.f;
-  int wa[4];
-#pragma unroll
-  for (int sgrp = 0; sgrp < 4; ++sgrp) wa[sgrp] = 256 * (lane >> 4) + 4 * (((lane >> 2) & 3) ^ sgrp) + (lane & 3);
-  const float4* asrc = reinterpret_cast<const float4*>(uw + 16 * lane);
-  const int aswz = (lane >> 2) & 3;
-  const int mb = 4 * ((lane >> 4) & 1);
-  const bool useful = (lane < 32) ? (ncol < 6) : dcol;
-
-  const uint32_t gmask = rs.gmask;
-  unsigned int* const reach32 = reinterpret_cast<unsigned int*>(reach) + (v >> 5);
-  const unsigned int vbit = 1u << (v & 31);
-  float4 na = zero4, nb = zero4, nc = zero4, nd = zero4;
-  uint32_t ngo = 0u, gi_next = 0u;
-  auto load = [&](uint32_t g) {
-    const float4* r = reinterpret_cast<const float4*>(rec + g);
-    na = r[0];
-    nb = r[1];
-    nc = r[2];
-    nd = r[3];
-    if (rs.col2 != nullptr)  // the second rasterizer call's colours replace the first's
-      nc = make_float4(rs.col2[3 * g], rs.col2[3 * g + 1], rs.col2[3 * g + 2], 0.f);
-    ngo = goff[g];
-    atomicOr(reach32 + 2 * g, vbit);  // the Gaussian gets a row in this view (k_view_grad reads it)
-  };
-  if (hi > lo) {
-    if (hi - 1 - lane >= lo) load(sorted_gauss[range.x + hi - 1 - lane] & gmask);
-    if (hi - 65 - lane >= lo) gi_next = sorted_gauss[range.x + hi - 65 - lane] & gmask;
-  }
-  float acca[NM], accb[NM];
-
-  for (int h = hi; h > lo; h -= 64) {
-    const int rel_c = h - 1 - lane;
-    const bool staged = rel_c >= lo;
-    const float4 ca = make_float4(na.x, na.y, GSR_CONIC_K_AC * na.z, GSR_CONIC_K_B * na.w);
-    const float4 cb = make_float4(GSR_CONIC_K_AC * nb.x, nb.y, nb.z, __uint_as_float((uint32_t)rel_c));
-    uint32_t keep4 = 0u;
-    if (staged) {
-      s0[lane] = ca;
-      s1[lane] = cb;
-      s2[lane] = nc;
-      const uint32_t dx_ = __float_as_uint(nd.x), dy_ = __float_as_uint(nd.y);
-      const int xmin = dx_ & 0xffff, ymin = dx_ >> 16, xmax = dy_ & 0xffff;
-      slot[lane] = ngo + (uint32_t)((tyi - ymin) * (xmax - xmin) + (txi - xmin));
-      const float4 r0 = make_float4(ca.x, ca.y, ca.z * (1.0f / GSR_CONIC_K_AC), ca.w * (1.0f / GSR_CONIC_K_B));
-      const float4 r1 = make_float4(cb.x * (1.0f / GSR_CONIC_K_AC), cb.y, cb.z, cb.w);
-#pragma unroll
-      for (int q = 0; q < 4; ++q)
-        if (rel_c < qmaxc[q] &&
-            quadrant_hit(r0, r1, (float)(txi * GSR_TILE_X + (q & 1) * 8), (float)(tyi * GSR_TILE_Y + (q >> 1) * 8)))
-          keep4 |= 1u << q;
-    }
-    if (h - 64 > lo) {
-      if (h - 65 - lane >= lo) load(gi_next);
-      if (h - 129 - lane >= lo) gi_next = sorted_gauss[range.x + h - 129 - lane] & gmask;
-    }
-#pragma unroll
-    for (int i = 0; i < NM; ++i) acca[i] = accb[i] = 0.f;
-    __syncthreads();
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const bool kept = (keep4 >> q) & 1u;
-      const unsigned long long kq = __ballot(kept);
-      if (kq == 0ull) continue;
-      const int cnt = __popcll(kq);
-      if (kept) klist[mask_rank(kq)] = (uint32_t)lane;
-      // this quadrant's B operand: bv[i] = D + F for k-step i (k_render_bwd)
-      float bv[16];
-      {
-        const float4* dsrc =
-            reinterpret_cast<const float4*>(dpl[q] + (dcol ? (ncol - 6) * 68 + 16 * (lane >> 4) : 4 * 68));
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-          const float4 d4 = dsrc[k];
-          const float dk[4] = {d4.x, d4.y, d4.z, d4.w};
-#pragma unroll
-          for (int e = 0; e < 4; ++e) {
-            const int i = 4 * k + e;
-            const float x = (float)(i & 7) - 3.5f;
-            bv[i] = dk[e] + (fa[i >> 3] + x * (fbb[i >> 3] + x * fc));
-          }
-        }
-      }
-      const float pxf = lxf + (float)((q & 1) * 8), pyf = lyf + (float)((q >> 1) * 8);
-      unsigned long long rest = kq;
-      __syncthreads();  // (klist)
-      for (int g0 = 0; g0 < cnt; g0 += 8) {
-        const int gn = min(8, cnt - g0);
-        int j = (int)__builtin_ctzll(rest);
-        float4 ga = s0[j], gb = s1[j], gc = s2[j];
-#pragma unroll
-        for (int c = 0; c < 8; ++c) {
-          if (c < gn) {
-            rest &= rest - 1ull;
-            const int jn = (c + 1 < gn) ? (int)__builtin_ctzll(rest) : j;
-            const float4 xa = s0[jn], xb = s1[jn], xc = s2[jn];
-            const uint32_t rel = __float_as_uint(gb.w);
-            const float dx = ga.x - pxf, dy = ga.y - pyf;
-            const float power2 = gauss_power2(ga.z, ga.w, gb.x, dx, dy);
-            const float G = __builtin_amdgcn_exp2f(power2);
-            const float alpha = fminf(GSR_ALPHA_MAX, gb.y * G);
-            const bool hit = rel < last[q] && power2 <= 0.0f && alpha >= GSR_ALPHA_MIN;
-            const float a_eff = hit ? alpha : 0.0f;
-            const float g_eff = hit ? G : 0.0f;
-            const float oma = 1.f - a_eff;
-            const float inv_1ma = fast_rcp(oma);
-            T[q] = T[q] * inv_1ma;
-            const float cd = fmaf(gc.x, dp0[q], fmaf(gc.y, dp1[q], fmaf(gc.z, dp2[q], dpa[q])));
-            const float dL_da = fmaf(T[q], fmaf(gb.z - Sd[q], dpd[q], cd - S[q]), inv_1ma * nbg[q]);
-            const float u = g_eff * dL_da;
-            const float w = a_eff * T[q];
-            S[q] = fmaf(a_eff, cd, oma * S[q]);
-            Sd[q] = fmaf(a_eff, gb.z, oma * Sd[q]);
-            uw[16 * c + wa[c >> 2]] = u;
-            uw[16 * (c + 8) + wa[2 + (c >> 2)]] = w;
-            ga = xa;
-            gb = xb;
-            gc = xc;
-            j = jn;
-          }
-        }
-        __syncthreads();  // (the wave reads its own lanes' rows)
-        float av[16];
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-          const float4 a4 = asrc[k ^ aswz];
-          av[4 * k] = a4.x, av[4 * k + 1] = a4.y, av[4 * k + 2] = a4.z, av[4 * k + 3] = a4.w;
-        }
-        const uint4 jl = *reinterpret_cast<const uint4*>(klist + g0 + mb);
-        typedef float f4 __attribute__((ext_vector_type(4)));
-        f4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-        for (int i = 0; i < 16; ++i) {
-          if (i & 1)
-            acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(av[i], bv[i], acc1, 0, 0, 0);
-          else
-            acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(av[i], bv[i], acc0, 0, 0, 0);
-        }
-        if (useful) {
-          const uint32_t jr[4] = {jl.x, jl.y, jl.z, jl.w};
-#pragma unroll
-          for (int r = 0; r < 4; ++r)
-            if (mb + r < gn) gsum[jr[r] * (uint32_t)GST + (uint32_t)ncol] = acc0[r] + acc1[r];
-        }
-        __syncthreads();  // (uw is rewritten by the next group; gsum read below)
-      }
-      if (kept) {
-        // this pair's sums -> moments about the candidate's mean (k_render_bwd's flush), quadrant order
-        const float* C = gsum + lane * GST;
-        const float4 ga = s0[lane];
-        const float mx = ga.x - ((float)(txi * GSR_TILE_X + (q & 1) * 8) + 3.5f);
-        const float my = ga.y - ((float)(tyi * GSR_TILE_Y + (q >> 1) * 8) + 3.5f);
-        float m[NM];
-        m[0] = C[0];
-        m[1] = mx * C[0] - C[1];
-        m[2] = my * C[0] - C[2];
-        m[3] = mx * (mx * C[0] - 2.f * C[1]) + C[3];
-        m[4] = mx * (my * C[0] - C[2]) - my * C[1] + C[4];
-        m[5] = my * (my * C[0] - 2.f * C[2]) + C[5];
-        m[6] = C[6];
-        m[7] = C[7];
-        m[8] = C[8];
-        m[9] = C[9];
-#pragma unroll
-        for (int i = 0; i < NM; ++i) {
-          if (q == 0) acca[i] = m[i];
-          else if (q == 1) acca[i] = acca[i] + m[i];
-          else if (q == 2) accb[i] = m[i];
-          else accb[i] = accb[i] + m[i];
-        }
-      }
-      __syncthreads();  // (klist, gsum are rewritten by the next quadrant)
-    }
-    if (staged) {
-      float m[NM];
-#pragma unroll
-      for (int i = 0; i < NM; ++i) m[i] = acca[i] + accb[i];
-      const float4 ga = s0[lane];
-      const float4 gb = s1[lane];
-      const float o = gb.y;
-      float4* row = grow + 3 * (size_t)slot[lane];
-      const float k = o * (1.0f / 1.4426950408889634f);
-      const float dmx = mean_grad(k, ddelx_dx, ga.z, ga.w, m[1], m[2]);
-      const float dmy = mean_grad(k, ddely_dy, gb.x, ga.w, m[2], m[1]);
-      row[0] = make_float4(dmx, dmy, -0.5f * o * m[3], -0.5f * o * m[4]);
-      row[1] = make_float4(-0.5f * o * m[5], m[0], m[6], m[7]);
-      row[2] = make_float4(m[8], m[9], 0.f, 0.f);
-    }
-    __syncthreads();
-  }
-  GSR_TL_END(1, hi)
-}
-
-// Sums of the backward blend: hit lists (HITS) or matrix-core products.  Hit lists win where the
-// Gaussians are small (the two-colour SuGaR backward, C5); the matrix cores where they are large (C3).
-// GSR_BWD_SUMS=hits / mfma forces one (A/B).
-static bool bwd_hit_lists(bool two) {
-  const char* e = getenv("GSR_BWD_SUMS");
-  if (e != nullptr && strcmp(e, "hits") == 0) return true;
-  if (e != nullptr && strcmp(e, "mfma") == 0) return false;
-  return two;
-}
-
-// One wave per tile walking the quadrants in turn, or the workgroup of lockstep quadrant waves (k_render_bwd).
-// Hit-list sums (C5): the tile wave (k_render_bwd_tw; C5 render_bwd 0.397 -> 0.329 ms/view) unless
-// GSR_BWD_KERNEL=quadrant.  Matrix-core sums (C3): the lockstep workgroup (the tile wave k_render_bwd_twm, with
-// GSR_BWD_KERNEL=tile, measured 0.098 -> 0.102 ms/view at C3, 0.104 -> 0.119 for 8-view sets:
-// profiles/r04/tile_wave_ab.txt).
-// waves per tile of the hit-list tile kernel (GSR_BWD_TW_WAVES=1|2): one (C5 render_bwd 0.3275 ms/view against
-// 0.3489 for two waves splitting the quadrants, whose per-batch barriers cost more than the overlap gains,
-// profiles/r04/tw_waves_ab.txt)
-static int bwd_tw_waves() {
-  const char* e = getenv("GSR_BWD_TW_WAVES");
-  return e != nullptr && strcmp(e, "2") == 0 ? 2 : 1;
-}
-static bool bwd_tile_wave(bool hits) {
-  const char* e = getenv("GSR_BWD_KERNEL");
-  if (e != nullptr && strcmp(e, "quadrant") == 0) return false;
-  if (e != nullptr && strcmp(e, "tile") == 0) return true;
-  return hits;
-}
-
+// The backward blend kernel of a launch: the two-colour backward (the SuGaR normal renderer's two calls in one
+// replay, C5) walks each tile's quadrants in turn on one wave with hit-list sums (k_render_bwd_tw); every other
+// backward runs the workgroup of four lockstep quadrant waves with the matrix-core sums (k_render_bwd).
+// (Measured and removed, round 4-5 — profiles/r04/tile_wave_ab.txt, tw_waves_ab.txt: the matrix-core tile wave at
+// C3, 0.098 -> 0.102 ms/view, 8-view sets 0.104 -> 0.119; the hit-list tile kernel with two waves per tile, C5
+// 0.3275 -> 0.3489; the lockstep workgroup with hit-list sums, C5 0.397 vs 0.329.)
 void launch_render_backward(const RenderSet& rs, const GeomState& g, const uint32_t* sorted_gauss,
                             const ImageState& img, const float* dL_dcolor, const float* dL_ddepth,
                             const float* dL_dalpha, const BackwardState& bw, hipStream_t stream) {
   const int nt = rs.gx * rs.gy;
   if (nt <= 0 || rs.V <= 0) return;
   // split tiles' later chunks: a workgroup per listed item (C3 per view: ~800 items)
-  const bool split = rs.ckpt != nullptr && rs.dpix2 == nullptr && rs.col2 == nullptr;
+  const bool split = rs.ckpt != nullptr && rs.dpix2 == nullptr && rs.col2 == nullptr;  // (one colour only)
   const int extra = split ? rs.split_extra : 0;  // (the count k_ckpt_suffix lists at most)
   const dim3 grid(block_grid(rs, 4) + extra);
   const uint32_t* items = split ? img.split_items : nullptr;
-  const bool hits = bwd_hit_lists(rs.dpix2 != nullptr);
-  if (hits && extra == 0 && bwd_tile_wave(true)) {
-    const bool two = bwd_tw_waves() == 2;
-    auto kt = rs.dpix2 != nullptr ? (two ? k_render_bwd_tw<true, 2> : k_render_bwd_tw<true, 1>)
-                                  : (two ? k_render_bwd_tw<false, 2> : k_render_bwd_tw<false, 1>);
-    g_blend_kernel[1] = rs.dpix2 != nullptr ? (two ? "k_render_bwd_tw<true, 2>" : "k_render_bwd_tw<true, 1>")
-                                            : (two ? "k_render_bwd_tw<false, 2>" : "k_render_bwd_tw<false, 1>");
-    hipLaunchKernelGGL(kt, dim3(block_grid(rs, 4)), dim3(two ? 128 : 64), 0, stream, rs, (const uint2*)img.ranges,
-                       (const uint32_t*)img.quad_maxc, sorted_gauss, (const GaussRec*)g.rec, (const uint32_t*)g.goff,
-                       (const float*)img.final_T, (const uint32_t*)img.n_contrib, dL_dcolor, dL_ddepth, dL_dalpha,
-                       bw.grow, bw.reach);
-    return;
-  }
-  if (!hits && rs.dpix2 == nullptr && extra == 0 && bwd_tile_wave(false)) {
-    g_blend_kernel[1] = "k_render_bwd_twm<false>";
-    hipLaunchKernelGGL(k_render_bwd_twm<false>, dim3(block_grid(rs, 4)), dim3(64), 0, stream, rs,
+  if (rs.dpix2 != nullptr) {
+    g_blend_kernel[1] = "k_render_bwd_tw<true>";
+    hipLaunchKernelGGL(k_render_bwd_tw<true>, dim3(block_grid(rs, 4)), dim3(64), 0, stream, rs,
                        (const uint2*)img.ranges, (const uint32_t*)img.quad_maxc, sorted_gauss, (const GaussRec*)g.rec,
                        (const uint32_t*)g.goff, (const float*)img.final_T, (const uint32_t*)img.n_contrib, dL_dcolor,
                        dL_ddepth, dL_dalpha, bw.grow, bw.reach);
     return;
   }
-  auto kern = rs.dpix2 != nullptr ? (hits ? k_render_bwd<true, true> : k_render_bwd<true, false>)
-                                  : (hits ? k_render_bwd<false, true> : k_render_bwd<false, false>);
-  g_blend_kernel[1] = rs.dpix2 != nullptr ? (hits ? "k_render_bwd<true, true>" : "k_render_bwd<true, false>")
-                                          : (hits ? "k_render_bwd<false, true>" : "k_render_bwd<false, false>");
-  hipLaunchKernelGGL(kern, grid, dim3(256), 0, stream, rs, (const uint2*)img.ranges, (const uint32_t*)img.quad_maxc,
-                     sorted_gauss, (const GaussRec*)g.rec, (const uint32_t*)g.goff, (const float*)img.final_T,
-                     (const uint32_t*)img.n_contrib, dL_dcolor, dL_ddepth, dL_dalpha, bw.grow, bw.reach,
-                     rs.dpix2 != nullptr ? 0 : extra, rs.dpix2 != nullptr ? nullptr : items);
+  g_blend_kernel[1] = "k_render_bwd";
+  hipLaunchKernelGGL(k_render_bwd, grid, dim3(256), 0, stream, rs, (const uint2*)img.ranges,
+                     (const uint32_t*)img.quad_maxc, sorted_gauss, (const GaussRec*)g.rec, (const uint32_t*)g.goff,
+                     (const float*)img.final_T, (const uint32_t*)img.n_contrib, dL_dcolor, dL_ddepth, dL_dalpha,
+                     bw.grow, bw.reach, extra, items);
 }
 
 // Split backward for launches of few tiles (split_fits): such a launch lasts as long as its deepest tile's

@@ -60,8 +60,8 @@ class _ViewSet:
 
 class _RasterizeViews(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, settings_list, grad_reduce, means3D, sh, colors_precomp, opacities, scales, rotations,
-                cov3D_precomp, composite_bg, colors2, *means2D):
+    def forward(ctx, settings_list, grad_reduce, two_color_bwd, means3D, sh, colors_precomp, opacities, scales,
+                rotations, cov3D_precomp, composite_bg, colors2, *means2D):
         t0 = time.perf_counter()
         lib = _C.load_library()
         V = len(settings_list)
@@ -142,6 +142,7 @@ class _RasterizeViews(torch.autograd.Function):
             t0 = _C.host_mark("fwd_render_launch", t0)
         ctx.settings = settings_list
         ctx.grad_reduce = grad_reduce
+        ctx.two_color_bwd = two_color_bwd
         ctx.sets = sets
         ctx.bg_shape = tuple(composite_bg.shape) if composite_bg is not None else None
         ctx.save_for_backward(m3, shc, col, sc, rot, c3, radii, cbg, color if cbg is not None else None, c2)
@@ -181,7 +182,7 @@ class _RasterizeViews(torch.autograd.Function):
                 off += n
         d_m3, d_sc, d_rot, d_op = carved["m3"], carved["sc"], carved["rot"], carved["op"]
         d_sh, d_c3, d_col = carved["sh"], carved["c3"], carved["col"]
-        d_bg = torch.empty_like(cbg) if cbg is not None and ctx.needs_input_grad[9] else None
+        d_bg = torch.empty_like(cbg) if cbg is not None and ctx.needs_input_grad[10] else None
         # more than one view set in the scale / rotation path: the running dL/dcov3D the later sets
         # continue from (include/gsr.h gsr_set_backward, accumulate)
         d_c2 = torch.zeros((P, 3), **fopt) if second else None
@@ -201,13 +202,13 @@ class _RasterizeViews(torch.autograd.Function):
             stream = _C._stream(dev)
             p = _C._ptr
             # both calls of a two-colour forward in one backward pass (gsr_set_backward_two_colors);
-            # GSR_TWO_COLOR_BWD=separate runs the second call's backward after the first's instead
-            fused2 = second and os.environ.get("GSR_TWO_COLOR_BWD", "fused") != "separate"
+            # two_color_backward="separate" runs the second call's backward after the first's instead
+            fused2 = second and ctx.two_color_bwd != "separate"
             if fused2:
                 g2 = g_color2.float().contiguous()
             reducer = ctx.grad_reduce if ctx.grad_reduce is not None and ctx.grad_reduce.active() else None
             # per-range events only when the last set's call is the last writer of the per-Gaussian sums: with
-            # the second colour's backward run separately after it (GSR_TWO_COLOR_BWD=separate), that call
+            # the second colour's backward run separately after it (two_color_backward="separate"), that call
             # adds into the same gradients, so the reduction waits for the whole stream instead
             events = reducer.chunk_events(dev) if reducer is not None and (fused2 or not second) else None
             for si, vs in enumerate(ctx.sets):
@@ -267,20 +268,21 @@ class _RasterizeViews(torch.autograd.Function):
             d_bg = d_bg.reshape(ctx.bg_shape)
         if getattr(ctx, "needs_c3_scratch", False):
             d_c3 = None
-        grads = [None, None, d_m3, d_sh, d_col, d_op, d_sc, d_rot, d_c3, d_bg, d_c2] + [d_m2[v] for v in range(V)]
+        grads = [None, None, None, d_m3, d_sh, d_col, d_op, d_sc, d_rot, d_c3, d_bg, d_c2] + [d_m2[v] for v in range(V)]
         for k, need in enumerate(ctx.needs_input_grad):
             if not need:
                 grads[k] = None
         if ctx.grad_reduce is not None and P > 0:
             # the per-Gaussian gradients' sums over ranks, range by range as the backward finishes them
-            shared = [grads[k] for k in (2, 3, 4, 5, 6, 7, 8, 10)]
+            shared = [grads[k] for k in (3, 4, 5, 6, 7, 8, 9, 11)]
             ctx.grad_reduce.launch(shared, P, events if P > 0 else None)
         _C.host_mark("bwd_host", t0)
         return tuple(grads)
 
 
 def rasterize_views(settings_list, means3D, means2D_list, opacities, shs=None, colors_precomp=None, scales=None,
-                    rotations=None, cov3D_precomp=None, background=None, colors2=None, grad_reduce=None):
+                    rotations=None, cov3D_precomp=None, background=None, colors2=None, grad_reduce=None,
+                    two_color_backward="fused"):
     """Render V views of one set of Gaussians.  settings_list: V GaussianRasterizationSettings (same image
     size, same sh_degree, scale_modifier and prefiltered flag); means2D_list: V screen-space placeholders
     (P, 3) whose .grad receives each view's viewspace gradient.  Returns (color (V,3,H,W), radii (V,P),
@@ -300,7 +302,11 @@ def rasterize_views(settings_list, means3D, means2D_list, opacities, shs=None, c
 
     grad_reduce (view_shard.ChunkedGradReduce): with torch.distributed initialised, the per-Gaussian
     parameter gradients are summed over ranks inside the backward, range by range as they are formed
-    (overlapping the per-Gaussian backward); the screen-space and background gradients stay per rank."""
+    (overlapping the per-Gaussian backward); the screen-space and background gradients stay per rank.
+
+    two_color_backward: "fused" (default) replays both calls of a colors2 forward in one backward pass;
+    "separate" runs the second call's backward after the first's, as two rasterizer calls would (same
+    gradients up to fp32 summation order; tests compare the two)."""
     if (shs is None) == (colors_precomp is None):
         raise Exception("Please provide excatly one of either SHs or precomputed colors!")
     if ((scales is None or rotations is None) and cov3D_precomp is None) or (
@@ -318,5 +324,7 @@ def rasterize_views(settings_list, means3D, means2D_list, opacities, shs=None, c
         H, W = int(s0.image_height), int(s0.image_width)
         if background.numel() != len(settings_list) * H * W * 3:
             raise ValueError("background must hold (V, H, W, 3) values")
-    return _RasterizeViews.apply(list(settings_list), grad_reduce, means3D, shs, colors_precomp, opacities, scales,
-                                 rotations, cov3D_precomp, background, colors2, *means2D_list)
+    if two_color_backward not in ("fused", "separate"):
+        raise ValueError("two_color_backward is 'fused' or 'separate'")
+    return _RasterizeViews.apply(list(settings_list), grad_reduce, two_color_backward, means3D, shs, colors_precomp,
+                                 opacities, scales, rotations, cov3D_precomp, background, colors2, *means2D_list)
