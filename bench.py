@@ -270,8 +270,8 @@ PROFILE_VIEWS_PER_LAUNCH = 64  # profiles/run_profiles.sh: bench.py defaults, on
 # launch takes the tile-wave forward and the lockstep matrix-core backward; C5 the two-colour
 # quadrant-wave forward and the one-wave-per-tile hit-list backward (gsr_render.hip).  A run uses the names the
 # library reports it launched (gsr_profile_kernel); the committed counters must name these (test_bench_fields)
-KERNELS = {"c3": ("k_render_fwd_tile<false>", "k_render_bwd<false, false>"),
-           "sugar": ("k_render_fwd<true, false>", "k_render_bwd_tw<true, 1>")}
+KERNELS = {"c3": ("k_render_fwd_tile<false>", "k_render_bwd"),
+           "sugar": ("k_render_fwd<true, false>", "k_render_bwd_tw<true>")}
 
 
 def read_traffic(path, kernel, field="per_launch_bytes"):
@@ -292,6 +292,12 @@ def read_json(path):
             return json.load(f)
     except (OSError, ValueError):
         return None
+
+
+def file_build(path):
+    """The build id a committed counter / pair file was captured on (profiles/summarize.py, diag_pairs.py)."""
+    d = read_json(path)
+    return d.get("build_id") if isinstance(d, dict) else None
 
 
 def time_knn(points, reps=10):
@@ -423,7 +429,7 @@ def time_per_view_path(rep, cams, bg_zero, bg_img, upstream, n_views):
             "path": "GaussianRasterizer per view + torch composite (the reference's unchanged renderer loop)"}
 
 
-def roofline_fields(args, phases, Ks, Ls, H, W, launched=None):
+def roofline_fields(args, phases, Ks, Ls, H, W, launched=None, build=None):
     """roofline (the dominant kernel) and roofline_fwd_blend, per launch, from the live HIP-event phase
     timings of this run.
 
@@ -450,6 +456,15 @@ def roofline_fields(args, phases, Ks, Ls, H, W, launched=None):
     traffic_path = args.traffic_sugar if sugar else args.traffic
     pairs = read_json(args.pairs) if profiled else None
     out = {}
+    # counters and pair counts describe the build they were captured on: with `build` (the loaded library's id,
+    # include/gsr.h gsr_version) a file of another build contributes nothing
+    mismatch = []
+    if build is not None:
+        if (profiled or sugar) and file_build(traffic_path) != build:
+            mismatch.append(f"{os.path.relpath(traffic_path, ROOT)} (build {file_build(traffic_path)})")
+        if pairs is not None and pairs.get("build_id") != build:
+            mismatch.append(f"{os.path.relpath(args.pairs, ROOT)} (build {pairs.get('build_id')})")
+            pairs = None
     n_fw = max(1, len(Ks))
     rows = {}
     names = KERNELS["sugar" if sugar else "c3"]
@@ -471,6 +486,7 @@ def roofline_fields(args, phases, Ks, Ls, H, W, launched=None):
         # the forward kernel depends on the views per launch (gsr_render.hip fwd_tile_kernel: the tile-wave
         # kernel from 16 views, quadrant-wave below): its counters apply to the profiled 64-view launch only
         use = profiled_here and (phase == "render_bwd" or views_per_launch == PROFILE_VIEWS_PER_LAUNCH)
+        use = use and not any(m.startswith(os.path.relpath(traffic_path, ROOT)) for m in mismatch)
         traffic = read_traffic(traffic_path, kernel) if use else None
         valu = read_traffic(traffic_path, kernel, "valu_insts_per_launch") if use else None
         if use and traffic is None:
@@ -521,6 +537,11 @@ def roofline_fields(args, phases, Ks, Ls, H, W, launched=None):
     elif stale:
         out["counters_note"] = (f"no counter fields for {', '.join(stale)}: {os.path.relpath(traffic_path, ROOT)} "
                                 "holds no counters of that kernel (profiled on another build)")
+    if mismatch:
+        out["counters_note"] = (out.get("counters_note", "") + "; " if "counters_note" in out else "") + (
+            f"dropped counters captured on another build than the loaded library ({build}): " + ", ".join(mismatch))
+    if build is not None:
+        out["library_build"] = build
     out["roofline_note"] = ("frac = SURVEY.md §8d algorithmic bytes / HIP-event duration (backward without the "
                             "reference's 80 B/instance atomic RMW, never performed here); counter_frac = PMC HBM "
                             "bytes / duration; valu_frac = SQ_INSTS_VALU / (duration x VALU issue peak). Both "
@@ -774,7 +795,7 @@ def run_workload(args, world, rank, device, comm, headline=True):
         # and the GPU idling while the host prepares launches)
         res["gap_ms_per_step"] = round(1000.0 * elapsed / args.steps - sum(ms for ms, _ in phases.values()) /
                                        args.steps, 3)
-        res.update(roofline_fields(args, phases, Ks, Ls, H, W, launched))
+        res.update(roofline_fields(args, phases, Ks, Ls, H, W, launched, build=_C.build_id()))
     if headline and not args.no_knn:
         res["init_knn"] = time_knn(rep.means3D.detach())
     if headline and world == 1 and args.per_view_views > 0 and args.workload == "c3" \

@@ -58,6 +58,7 @@ def main():
                      f"(colours, normals), {V}-view set" if workload == "sugar" else
                      f"bench.py default: 1M Gaussians, {R}x{R}, SH3, {V}-view set, fused background composite"),
         "views": V,
+        "build_id": _C.build_id(lib),  # the sources the counted kernels were built from (bench.py checks it)
         "fwd_pairs_evaluated_per_view": float(buf[0]) / V,
         "fwd_pair_slots_per_view": float(buf[1]) / V,
         "bwd_pairs_replayed_per_view": float(buf[2]) / V,

@@ -5,7 +5,7 @@
 set -e
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
 OUT=gpurun_out/sq_${1:-r01}
-ARGS=${SQ_ARGS:-"--steps 1 --warmup 1 --views 16 --no-cpu-baseline --no-profile"}
+ARGS=${SQ_ARGS:-"--steps 1 --warmup 1 --no-cpu-baseline --no-profile --no-knn --per-view-views 0 --extra-lines none"}
 i=0
 for grp in "SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY" \
            "SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_BRANCH" \

@@ -44,7 +44,18 @@ with open(os.path.join(dst, f"{tag}_pmc.csv"), "w", newline="") as fh:
     wr.writerow(["kernel", "dispatches", "FETCH_SIZE_KB", "WRITE_SIZE_KB", "hbm_bytes_per_launch_corrected"])
     wr.writerows(rows)
 traffic = {r[0].replace("gsr::", ""): r[4] for r in rows if r[0].startswith("gsr::")}  # ours only
-summary = {"source": f"profiles/{tag}_pmc.csv", "per_launch_bytes": traffic}
+def _build_id():
+    """The build id of the library the capture ran (the in-tree product library; bench.py compares it)."""
+    import ctypes
+
+    so = os.path.join(os.path.dirname(dst), "threestudio-3dgs_amd", "diff_gaussian_rasterization", "libgsr_hip.so")
+    lib = ctypes.CDLL(os.environ.get("GSR_HIP_LIB", so))
+    lib.gsr_version.restype = ctypes.c_char_p
+    v = lib.gsr_version().decode()
+    return v.split(" build ", 1)[1] if " build " in v else "unknown"
+
+
+summary = {"source": f"profiles/{tag}_pmc.csv", "build_id": _build_id(), "per_launch_bytes": traffic}
 vpath = os.path.join(src, "valu", "run_counter_collection.csv")
 if os.path.exists(vpath):
     v = agg(vpath, "SQ_INSTS_VALU")

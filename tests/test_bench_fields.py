@@ -111,3 +111,26 @@ def test_launcher_starts_ranks_without_world_size(monkeypatch):
     with pytest.raises(SystemExit) as e:
         bench.main()
     assert e.value.code == 0 and len(calls) == 1 and "--nproc-per-node=2" in calls[0]
+
+
+def test_counters_of_another_build_are_dropped(tmp_path):
+    """counter and pair files record the build id of the library they were captured on
+    (profiles/summarize.py, profiles/diag_pairs.py); bench.py drops them when the loaded library's id differs."""
+    import json
+
+    a0 = _args()
+    t = json.load(open(a0.traffic))
+    p = json.load(open(a0.pairs))
+    for tag, build in (("same", "b0"), ("other", "b1")):
+        tf, pf = tmp_path / f"t_{tag}.json", tmp_path / f"p_{tag}.json"
+        tf.write_text(json.dumps(dict(t, build_id=build)))
+        pf.write_text(json.dumps(dict(p, build_id=build)))
+        r = bench.roofline_fields(_args("--traffic", str(tf), "--pairs", str(pf)), PHASES, [6.6e6] * 64,
+                                  [4.95e6] * 64, 1024, 1024, build="b0")
+        assert r["library_build"] == "b0"
+        if tag == "same":
+            assert r["roofline"]["traffic"] is not None and "pairs_per_launch" in r["roofline"]["valu"]
+            assert "counters_note" not in r
+        else:
+            assert r["roofline"]["traffic"] is None and "valu" not in r["roofline"]
+            assert "another build" in r["counters_note"] and "b1" in r["counters_note"]

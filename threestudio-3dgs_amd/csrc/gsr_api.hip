@@ -183,7 +183,11 @@ static int check_set(int V, int P) {
 
 extern "C" {
 
-const char* gsr_version(void) { return "gsr 0.3.0 gfx950"; }
+#ifndef GSR_BUILD_ID
+#define GSR_BUILD_ID "unknown"
+#endif
+// "gsr <version> gfx950 build <id>": the id hashes the sources the library was built from (csrc/Makefile)
+const char* gsr_version(void) { return "gsr 0.4.0 gfx950 build " GSR_BUILD_ID; }
 int gsr_abi_version(void) { return GSR_ABI_VERSION; }
 const char* gsr_last_error(void) { return g_err; }
 

@@ -11,7 +11,7 @@
     (defined(GSR_EXP_COALROWS) || defined(GSR_EXP_FWD_NOC) || defined(GSR_EXP_LDSPAD) ||                  \
      defined(GSR_EXP_NOCULL) || defined(GSR_EXP_NOFLUSH) || defined(GSR_EXP_NOGROUP) ||                   \
      defined(GSR_EXP_NOMFMA) || defined(GSR_EXP_NOREACH) || defined(GSR_EXP_NOREPLAY) ||                \
-     defined(GSR_EXP_NOCOL2))
+     defined(GSR_EXP_NOCOL2) || defined(GSR_EXP_HOTREC))
 #error "GSR_EXP_* experiment switches build only through `make exp` (a diagnostic library, not libgsr_hip.so)"
 #endif
 #include <stddef.h>

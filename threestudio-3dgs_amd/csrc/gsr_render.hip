@@ -1015,7 +1015,11 @@ __device__ __forceinline__ void bwd_tile(BwdLDS& s, const RenderSet& rs, int v, 
   if (hi > lo) {
     const uint32_t g0 = fetch_index(hi);
     if (hi - 1 - cs >= lo) {
+#ifdef GSR_EXP_HOTREC  // timing only: the staging gathers from 4096 cache-resident records (wrong results)
+      npc = reinterpret_cast<const float4*>(rec + (g0 & 4095u))[piece];
+#else
       npc = reinterpret_cast<const float4*>(rec + g0)[piece];
+#endif
       if (piece == 2 && rs.col2 != nullptr)  // the second rasterizer call's colours replace the first's
         npc = make_float4(rs.col2[3 * g0], rs.col2[3 * g0 + 1], rs.col2[3 * g0 + 2], 0.f);
       if (piece == 3) {
@@ -1141,7 +1145,11 @@ __device__ __forceinline__ void bwd_tile(BwdLDS& s, const RenderSet& rs, int v, 
       }
       if (h - 64 > lo) {
         if (h - 65 - cs >= lo) {
+#ifdef GSR_EXP_HOTREC
+          npc = reinterpret_cast<const float4*>(rec + (gi_next & 4095u))[piece];
+#else
           npc = reinterpret_cast<const float4*>(rec + gi_next)[piece];
+#endif
           if (piece == 2 && rs.col2 != nullptr)
             npc = make_float4(rs.col2[3 * gi_next], rs.col2[3 * gi_next + 1], rs.col2[3 * gi_next + 2], 0.f);
           if (piece == 3) {

@@ -124,6 +124,11 @@ __global__ __launch_bounds__(GSR_SORT_THREADS) void k_seg_scatter(
   const int R = 1 << bits;
 #pragma unroll
   for (int ww = 0; ww < 4; ++ww) s.wcnt[ww][t] = 0u;
+  // the digit's segment total and this block's scanned count do not depend on the keys: loaded with them, so the
+  // block pays one memory latency before its writes instead of two
+  const uint32_t nb = seg.blk[v + 1] - seg.blk[v];
+  const uint32_t dtot = t < R ? totals[(size_t)v * GSR_RADIX + t] : 0u;
+  const uint32_t dcnt = t < R ? counts[(size_t)R * seg.blk[v] + (size_t)t * nb + lb] : 0u;
   const uint32_t b0 = lb * GSR_SORT_TILE + w * (GSR_SORT_TILE / 4);
   uint32_t key[GSR_SORT_ITEMS], val[GSR_SORT_ITEMS], pos[GSR_SORT_ITEMS];
 #pragma unroll
@@ -161,12 +166,10 @@ __global__ __launch_bounds__(GSR_SORT_THREADS) void k_seg_scatter(
   }
   uint32_t tot;
   const uint32_t lstart = block_exclusive_scan<GSR_SORT_THREADS>(bc, &tot, s.wave);
-  const uint32_t dtot = t < R ? totals[(size_t)v * GSR_RADIX + t] : 0u;
   const uint32_t dstart = block_exclusive_scan<GSR_SORT_THREADS>(dtot, &tot, s.wave);
   if (t < R) {
-    const uint32_t nb = seg.blk[v + 1] - seg.blk[v];
     s.local[t] = lstart;
-    s.glob[t] = dstart + counts[(size_t)R * seg.blk[v] + (size_t)t * nb + lb];
+    s.glob[t] = dstart + dcnt;
   }
   __syncthreads();
 #pragma unroll

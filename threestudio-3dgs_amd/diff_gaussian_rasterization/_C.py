@@ -370,6 +370,12 @@ def profile_read(reset: bool = True) -> dict:
     return {PHASES[i]: (float(ms[i]), int(cnt[i])) for i in range(n)}
 
 
+def build_id(lib=None) -> str:
+    """The library's build id (include/gsr.h gsr_version: a hash of the sources it was built from, csrc/Makefile)."""
+    v = (lib or load_library()).gsr_version().decode()
+    return v.split(" build ", 1)[1] if " build " in v else "unknown"
+
+
 def profile_kernels() -> dict:
     """The blend kernels the last forward / backward blend launches used (include/gsr.h gsr_profile_kernel), as
     rocprofv3 names them: {"render_fwd": ..., "render_bwd": ...}."""

@@ -36,6 +36,13 @@ def _world():
     return 1, 0
 
 
+def _collect() -> bool:
+    """The view gather and the gradient reductions issue their collectives whenever a process group exists —
+    also at world size 1, where they are identities (a one-GPU run of the RCCL path: tests/test_gpu_rccl.py);
+    without one they are skipped."""
+    return dist.is_available() and dist.is_initialized()
+
+
 def shard_range(batch_size: int, world: int, rank: int):
     """Contiguous view slice of `rank`; views are split as evenly as possible (first ranks take the remainder)."""
     base, extra = divmod(batch_size, world)
@@ -83,8 +90,7 @@ def all_gather_views(local: torch.Tensor, batch_size: int, group=None) -> torch.
     Autograd: the gathered tensor's gradient reaches the local slice only; the other ranks' slices are
     constants here (their views' gradients are computed on their own ranks).
     """
-    world, _ = _world()
-    if world == 1:
+    if not _collect():
         return local
     return _GatherViews.apply(local, batch_size, group)
 
@@ -112,7 +118,7 @@ def all_gather_views_async(local: torch.Tensor, batch_size: int, group=None) -> 
     contract) can overlap the backward; the gathered batch carries no gradient.  Same values as
     all_gather_views."""
     world, rank = _world()
-    if world == 1:
+    if not _collect():
         out = local.detach()
         return PendingGather(None, lambda: out)
     counts = [shard_range(batch_size, world, r) for r in range(world)]
@@ -193,7 +199,7 @@ def allreduce_grads(params, group=None, average: bool = False):
     reduced in place, without a copy.  Loss terms computed on every rank from the parameters directly go
     through replicated_loss first."""
     world, _ = _world()
-    if world == 1 or not params:
+    if not _collect() or not params:
         return
     flags = _has_grad_flags(params, group)  # collective on every rank (which ranks lack a grad is rank-local)
     params = [p for p, f in zip(params, flags) if f]
@@ -268,7 +274,7 @@ class ChunkedGradReduce:
         self.launched = 0
 
     def active(self) -> bool:
-        return _world()[0] > 1
+        return _collect()
 
     def chunk_events(self, device):
         """Events the backward records after each range (created now: torch creates them on first record)."""
