@@ -55,7 +55,7 @@ def composite_upstream(g_render, g_alpha, pre, bg_hwc):
     return gcol, ga
 
 
-GRAD_KEYS = ("means3D", "sh", "opacity", "scales", "rotations", "colors")
+GRAD_KEYS = ("means3D", "sh", "opacity", "scales", "rotations", "colors", "cov3D")
 
 
 def _view_task(task):
@@ -126,6 +126,52 @@ def _pool(workers):
 
 def workers_for(n_tasks, cap=16):
     return max(1, min(n_tasks, cap, os.cpu_count() or 1))
+
+
+def scale_rot_chain(dcov, scales, rots, mod=1.0, dt=np.float32):
+    """The scale / rotation chain rule of oracle/gsr_oracle.c (oracle_backward, computeCov3D's backward) applied
+    once to dL/dcov3D already summed over views and calls, in precision `dt` — the association the GPU's
+    per-Gaussian backward uses (it sums dL/dcov3D over the set's views before the chain rule; the oracle applies
+    it per view).  A null model for the summed scale / rotation gradients."""
+    c = np.asarray(dcov, dt)
+    q = np.asarray(rots, dt)
+    r, x, y, z = q[:, 0], q[:, 1], q[:, 2], q[:, 3]
+    one, two = dt(1), dt(2)
+    R = np.empty((q.shape[0], 3, 3), dt)
+    R[:, 0, 0] = one - two * (y * y + z * z)
+    R[:, 0, 1] = two * (x * y - r * z)
+    R[:, 0, 2] = two * (x * z + r * y)
+    R[:, 1, 0] = two * (x * y + r * z)
+    R[:, 1, 1] = one - two * (x * x + z * z)
+    R[:, 1, 2] = two * (y * z - r * x)
+    R[:, 2, 0] = two * (x * z - r * y)
+    R[:, 2, 1] = two * (y * z + r * x)
+    R[:, 2, 2] = one - two * (x * x + y * y)
+    s = dt(mod) * np.asarray(scales, dt)
+    h = dt(0.5)
+    G = np.stack([np.stack([c[:, 0], h * c[:, 1], h * c[:, 2]], 1),
+                  np.stack([h * c[:, 1], c[:, 3], h * c[:, 4]], 1),
+                  np.stack([h * c[:, 2], h * c[:, 4], c[:, 5]], 1)], 1)
+    dE = np.empty_like(R)
+    for a in range(3):
+        for k in range(3):
+            dE[:, a, k] = two * (G[:, a, 0] * s[:, k] * R[:, 0, k] + G[:, a, 1] * s[:, k] * R[:, 1, k]
+                                 + G[:, a, 2] * s[:, k] * R[:, 2, k])
+    dsc = np.stack([dE[:, 0, k] * R[:, 0, k] + dE[:, 1, k] * R[:, 1, k] + dE[:, 2, k] * R[:, 2, k]
+                    for k in range(3)], 1)
+    dR = dE * s[:, None, :]
+    d = lambda a, k: dR[:, a, k]  # noqa: E731
+    f4 = dt(4)
+    drot = np.stack([
+        -two * z * d(0, 1) + two * y * d(0, 2) + two * z * d(1, 0) - two * x * d(1, 2) - two * y * d(2, 0)
+        + two * x * d(2, 1),
+        two * y * d(0, 1) + two * z * d(0, 2) + two * y * d(1, 0) - f4 * x * d(1, 1) - two * r * d(1, 2)
+        + two * z * d(2, 0) + two * r * d(2, 1) - f4 * x * d(2, 2),
+        -f4 * y * d(0, 0) + two * x * d(0, 1) + two * r * d(0, 2) + two * x * d(1, 0) + two * z * d(1, 2)
+        - two * r * d(2, 0) + two * z * d(2, 1) - f4 * y * d(2, 2),
+        -f4 * z * d(0, 0) - two * r * d(0, 1) + two * x * d(0, 2) + two * r * d(1, 0) - f4 * z * d(1, 1)
+        + two * y * d(1, 2) + two * x * d(2, 0) + two * y * d(2, 1)], 1)
+    return dsc, drot
 
 
 def views_and_sums(tasks, keep_views=True, workers=None):

@@ -131,6 +131,11 @@ def test_c5_kernel_selection_vs_oracle():
     refs = {tag: {k: tot1[p][k] + tot2[p][k] for k in keys} for tag, p in tags}
     for tag, p in tags:
         refs[tag]["colors"], refs[tag]["normals"] = tot1[p]["colors"], tot2[p]["colors"]
+    # the scale / rotation gradients' null model is the GPU's association: the fp32 oracle's dL/dcov3D summed over
+    # both calls and the 16 views, then one fp32 chain rule (the per-view chain rules of the oracle cancel
+    # differently on SuGaR's flat Gaussians, whose third scale is ~0)
+    refs["b32r"]["scales"], refs["b32r"]["rotations"] = oracle_pool.scale_rot_chain(
+        tot1["f32"]["cov3D"] + tot2["f32"]["cov3D"], s1["scales"], s1["rotations"])
     g = {"g_" + k: t[n].grad.cpu().numpy() for k, n in (("means3D", "means3D"), ("opacity", "opacities"),
                                                         ("scales", "scales"), ("rotations", "rotations"),
                                                         ("colors", "colors_precomp"), ("normals", "normals"))}

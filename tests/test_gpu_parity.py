@@ -259,7 +259,7 @@ def test_batched_views_match_per_view(nviews, monkeypatch):
         assert err <= 1e-5 * scale, f"{k}: {err} vs scale {scale}"
 
 
-def bitwise_case(kind, monkeypatch=None, fwd_kernel=None):
+def bitwise_case(kind, monkeypatch=None, fwd_kernel=None, between=None):
     """One 3-view rasterize_views forward + backward of the bitwise tests (every output, means2D and parameter
     gradient as numpy arrays).  ball_composite: 40k Gaussians, SH3, ragged 200 x 168 with the fused background
     composite; sugar_two_colors: a SuGaR scene with the second colour set (both calls in one backward)."""
@@ -297,6 +297,8 @@ def bitwise_case(kind, monkeypatch=None, fwd_kernel=None):
     loss = (c * ups[0]).sum() + (d * ups[1][:, :1]).sum() + (a * ups[1][:, 1:2]).sum()
     if len(outs) > 4:
         loss = loss + (outs[4] * ups[2]).sum()
+    if between is not None:  # (after the forward, before the backward)
+        between()
     loss.backward()
     res = [x.detach() for x in outs] + [m.grad for m in m2] + [v.grad for v in t.values()]
     return [x.cpu().numpy() for x in res]
@@ -309,7 +311,7 @@ def _assert_bitwise(xs, ys, what):
             f"{what}: output {i} differs: {float(np.abs(x.astype(np.float64) - y.astype(np.float64)).max())}"
 
 
-@pytest.mark.parametrize("switch", ["fwd_kernel", "tile_keys"])
+@pytest.mark.parametrize("switch", ["fwd_kernel", "tile_keys", "mid_pass"])
 @pytest.mark.parametrize("kind", ["ball_composite", "sugar_two_colors"])
 def test_forward_kernels_bitwise(kind, switch, monkeypatch, tmp_path):
     """fwd_kernel: the one-wave-per-tile forward and the quadrant-wave forward (GSR_FWD_KERNEL) blend exactly
@@ -320,7 +322,9 @@ def test_forward_kernels_bitwise(kind, switch, monkeypatch, tmp_path):
     layout override is read once per process (the backward derives the buffer layout from it on the host), so
     the forced layouts run in child processes.  Every output — colour, depth, alpha, the composite, the second
     colour set, radii — and every gradient (the backward reads the forward's per-pixel state) must be bitwise
-    equal."""
+    equal.  mid_pass: every switch changed between the forward and the backward (a child process
+    sets GSR_TILE_KEYS, GSR_FWD_KERNEL and GSR_BWD_SPLIT after the forward) changes nothing: the backward
+    follows the forward's recorded decisions and the once-per-process layout latch."""
     if switch == "fwd_kernel":
         _assert_bitwise(bitwise_case(kind, monkeypatch, "tile"), bitwise_case(kind, monkeypatch, "quadrant"),
                         "tile-wave vs quadrant-wave forward")
@@ -330,6 +334,21 @@ def test_forward_kernels_bitwise(kind, switch, monkeypatch, tmp_path):
     import sys
 
     base = bitwise_case(kind)
+    if switch == "mid_pass":
+        out = tmp_path / "mid.npz"
+        code = ("import os, numpy as np, test_gpu_parity as t\n"
+                "def flip():\n"
+                "    os.environ.update(GSR_TILE_KEYS='plain', GSR_FWD_KERNEL='quadrant', GSR_BWD_SPLIT='1')\n"
+                "np.savez(%r, *t.bitwise_case(%r, between=flip))\n" % (str(out), kind))
+        env = dict(os.environ, PYTHONPATH=os.pathsep.join(p for p in sys.path if p))
+        for k in ("GSR_TILE_KEYS", "GSR_FWD_KERNEL", "GSR_BWD_SPLIT"):
+            env.pop(k, None)
+        res = subprocess.run([sys.executable, "-c", code], cwd=os.path.dirname(os.path.abspath(__file__)), env=env,
+                             capture_output=True, text=True, timeout=240)
+        assert res.returncode == 0, res.stderr[-3000:]
+        got = np.load(out)
+        _assert_bitwise([got[f"arr_{i}"] for i in range(len(got.files))], base, "switches changed mid-pass")
+        return
     for layout in ("unpacked", "plain"):
         out = tmp_path / f"{layout}.npz"
         code = "import numpy as np, test_gpu_parity as t; np.savez(%r, *t.bitwise_case(%r))" % (str(out), kind)

@@ -8,10 +8,9 @@
 //      then BACKWARD::computeCov2DCUDA (conic -> 2D cov -> 3D cov and camera-space mean) and the
 //      projection / view-depth part of BACKWARD::preprocessCUDA [EXT].  Writes the view's means2D
 //      gradient and a 64-byte record slot (dmean3D, dcov3D, raw dcolor, dopacity, SH clamp bits).
-//   B. k_gauss_accum, four lanes per Gaussian: streams its reached views' records, runs the
+//   B. k_gauss_accum, one thread per Gaussian: streams its reached views' records, runs the
 //      SH -> RGB backward (incl. the view-direction term) per view with dL/dSH accumulated in
-//      registers (one SH channel per lane), then 3D cov -> scale and (unnormalised) quaternion once
-//      (linear in dL/dcov3D).
+//      registers, then 3D cov -> scale and (unnormalised) quaternion once (linear in dL/dcov3D).
 // Splitting at the view boundary keeps A light (≈70 VGPRs, thousands of waves in flight to hide the
 // gather latency) and leaves only B to carry the 48 SH accumulators.
 // Gradient conventions of the reference are kept: the 0.99 alpha clamp is ignored in
@@ -158,6 +157,80 @@ __device__ __forceinline__ void proj_backward(const float3 mean, const float* pr
   dmean.z += (proj[8] * m_w - proj[11] * mul1) * dmx + (proj[9] * m_w - proj[11] * mul2) * dmy;
 }
 
+// computeColorFromSH backward for one view: accumulates basis x dL/dRGB into dsh (registers, 3 x 16,
+// summed over views) and adds the view-direction term to dmean.  sh = the Gaussian's (M, 3) row (LDS).
+__device__ __forceinline__ void sh_backward(int deg, int M, const float* sh, float (&dsh)[48], float3 dRGB,
+                                            const float3 mean, const float* campos, float3& dmean) {
+  const float3 dir_orig = make_float3(mean.x - campos[0], mean.y - campos[1], mean.z - campos[2]);
+  const float len = sqrtf(dir_orig.x * dir_orig.x + dir_orig.y * dir_orig.y + dir_orig.z * dir_orig.z);
+  const float x = dir_orig.x / len, y = dir_orig.y / len, z = dir_orig.z / len;
+  float basis[16];
+  float bdx[16], bdy[16], bdz[16];  // d basis_k / d (x, y, z)
+#pragma unroll
+  for (int k = 0; k < 16; ++k) basis[k] = bdx[k] = bdy[k] = bdz[k] = 0.f;
+  basis[0] = SH_C0;
+  if (deg > 0) {
+    basis[1] = -SH_C1 * y; basis[2] = SH_C1 * z; basis[3] = -SH_C1 * x;
+    bdy[1] = -SH_C1; bdz[2] = SH_C1; bdx[3] = -SH_C1;
+    if (deg > 1) {
+      const float xx = x * x, yy = y * y, zz = z * z, xy = x * y, yz = y * z, xz = x * z;
+      basis[4] = SH_C2[0] * xy; basis[5] = SH_C2[1] * yz;
+      basis[6] = SH_C2[2] * (2.f * zz - xx - yy); basis[7] = SH_C2[3] * xz;
+      basis[8] = SH_C2[4] * (xx - yy);
+      bdx[4] = SH_C2[0] * y; bdy[4] = SH_C2[0] * x;
+      bdy[5] = SH_C2[1] * z; bdz[5] = SH_C2[1] * y;
+      bdx[6] = SH_C2[2] * 2.f * -x; bdy[6] = SH_C2[2] * 2.f * -y; bdz[6] = SH_C2[2] * 2.f * 2.f * z;
+      bdx[7] = SH_C2[3] * z; bdz[7] = SH_C2[3] * x;
+      bdx[8] = SH_C2[4] * 2.f * x; bdy[8] = SH_C2[4] * 2.f * -y;
+      if (deg > 2) {
+        basis[9] = SH_C3[0] * y * (3.f * xx - yy);
+        basis[10] = SH_C3[1] * xy * z;
+        basis[11] = SH_C3[2] * y * (4.f * zz - xx - yy);
+        basis[12] = SH_C3[3] * z * (2.f * zz - 3.f * xx - 3.f * yy);
+        basis[13] = SH_C3[4] * x * (4.f * zz - xx - yy);
+        basis[14] = SH_C3[5] * z * (xx - yy);
+        basis[15] = SH_C3[6] * x * (xx - 3.f * yy);
+        bdx[9] = SH_C3[0] * 3.f * 2.f * xy;          bdy[9] = SH_C3[0] * 3.f * (xx - yy);
+        bdx[10] = SH_C3[1] * yz;                     bdy[10] = SH_C3[1] * xz;          bdz[10] = SH_C3[1] * xy;
+        bdx[11] = SH_C3[2] * -2.f * xy;              bdy[11] = SH_C3[2] * (-3.f * yy + 4.f * zz - xx);
+        bdz[11] = SH_C3[2] * 4.f * 2.f * yz;
+        bdx[12] = SH_C3[3] * -3.f * 2.f * xz;        bdy[12] = SH_C3[3] * -3.f * 2.f * yz;
+        bdz[12] = SH_C3[3] * 3.f * (2.f * zz - xx - yy);
+        bdx[13] = SH_C3[4] * (-3.f * xx + 4.f * zz - yy); bdy[13] = SH_C3[4] * -2.f * xy;
+        bdz[13] = SH_C3[4] * 4.f * 2.f * xz;
+        bdx[14] = SH_C3[5] * 2.f * xz;               bdy[14] = SH_C3[5] * -2.f * yz;   bdz[14] = SH_C3[5] * (xx - yy);
+        bdx[15] = SH_C3[6] * 3.f * (xx - yy);        bdy[15] = SH_C3[6] * -3.f * 2.f * xy;
+      }
+    }
+  }
+  const int ncoef = (deg + 1) * (deg + 1);
+  float3 dRGBdx = make_float3(0.f, 0.f, 0.f), dRGBdy = dRGBdx, dRGBdz = dRGBdx;
+#pragma unroll
+  for (int k = 0; k < 16; ++k) {
+    if (k < ncoef && k < M) {
+      dsh[3 * k] += basis[k] * dRGB.x;
+      dsh[3 * k + 1] += basis[k] * dRGB.y;
+      dsh[3 * k + 2] += basis[k] * dRGB.z;
+      if (k > 0) {
+        const float3 s = make_float3(sh[3 * k], sh[3 * k + 1], sh[3 * k + 2]);
+        dRGBdx.x += bdx[k] * s.x; dRGBdx.y += bdx[k] * s.y; dRGBdx.z += bdx[k] * s.z;
+        dRGBdy.x += bdy[k] * s.x; dRGBdy.y += bdy[k] * s.y; dRGBdy.z += bdy[k] * s.z;
+        dRGBdz.x += bdz[k] * s.x; dRGBdz.y += bdz[k] * s.y; dRGBdz.z += bdz[k] * s.z;
+      }
+    }
+  }
+  const float3 ddir = make_float3(dRGBdx.x * dRGB.x + dRGBdx.y * dRGB.y + dRGBdx.z * dRGB.z,
+                                  dRGBdy.x * dRGB.x + dRGBdy.y * dRGB.y + dRGBdy.z * dRGB.z,
+                                  dRGBdz.x * dRGB.x + dRGBdz.y * dRGB.y + dRGBdz.z * dRGB.z);
+  // d normalize(v) / dv applied to ddir
+  const float3 v = dir_orig;
+  const float sum2 = v.x * v.x + v.y * v.y + v.z * v.z;
+  const float invsum32 = 1.0f / sqrtf(sum2 * sum2 * sum2);
+  dmean.x += ((sum2 - v.x * v.x) * ddir.x - v.y * v.x * ddir.y - v.z * v.x * ddir.z) * invsum32;
+  dmean.y += (-v.x * v.y * ddir.x + (sum2 - v.y * v.y) * ddir.y - v.z * v.y * ddir.z) * invsum32;
+  dmean.z += (-v.x * v.z * ddir.x - v.y * v.z * ddir.y + (sum2 - v.z * v.z) * ddir.z) * invsum32;
+}
+
 // computeCov3D backward: dL/dcov3D -> dL/d(scale_modifier * scale) and dL/d(quaternion as given).
 __device__ __forceinline__ void scale_rot_backward(const float3 scale, const float4 rot, float mod,
                                                    const float dcov[6], float ds[3], float dq[4]) {
@@ -194,6 +267,9 @@ __device__ __forceinline__ void scale_rot_backward(const float3 scale, const flo
 }
 
 
+// LDS row stride (floats) of one Gaussian's 3M SH values: 16-byte multiple plus 16 bytes of padding so
+// per-thread 16-byte LDS accesses at this stride are bank-conflict free.
+static inline __host__ __device__ int sh_lds_stride(int M) { return ((3 * M + 3) & ~3) + 4; }
 
 // ---- A: per (view, Gaussian) ----------------------------------------------------------------
 // Block b -> view b % V, Gaussians [4096 (b / V), +4096) (GSR_VG_ITEMS = 16 per thread, 256 apart; 4, 8,
@@ -338,83 +414,63 @@ __global__ __launch_bounds__(256) void k_view_grad(GaussBackwardArgs a, ViewGrad
   }
 }
 
-// One SH channel of computeColorFromSH's backward at the unit direction (x, y, z): dsh[k] += basis_k dR and
-// (px, py, pz) += d basis_k / d (x, y, z) sh[k] (k >= 1) for k < ncoef, each coefficient's terms formed and consumed
-// in turn (the reference's basis constants and expressions; held as arrays the 64 values would stay live).
-__device__ __forceinline__ void sh_channel_backward(int deg, int ncoef, float x, float y, float z, float dR,
-                                                    const float (&sh)[16], float (&dsh)[16], float& px, float& py,
-                                                    float& pz) {
-#define GSR_SH_TERM(k, B, DX, DY, DZ) \
-  if ((k) < ncoef) {                  \
-    dsh[k] += (B) * dR;               \
-    px += (DX) * sh[k];               \
-    py += (DY) * sh[k];               \
-    pz += (DZ) * sh[k];               \
-  }
-  if (0 < ncoef) dsh[0] += SH_C0 * dR;
-  if (deg > 0) {
-    GSR_SH_TERM(1, -SH_C1 * y, 0.f, -SH_C1, 0.f)
-    GSR_SH_TERM(2, SH_C1 * z, 0.f, 0.f, SH_C1)
-    GSR_SH_TERM(3, -SH_C1 * x, -SH_C1, 0.f, 0.f)
-    if (deg > 1) {
-      const float xx = x * x, yy = y * y, zz = z * z, xy = x * y, yz = y * z, xz = x * z;
-      GSR_SH_TERM(4, SH_C2[0] * xy, SH_C2[0] * y, SH_C2[0] * x, 0.f)
-      GSR_SH_TERM(5, SH_C2[1] * yz, 0.f, SH_C2[1] * z, SH_C2[1] * y)
-      GSR_SH_TERM(6, SH_C2[2] * (2.f * zz - xx - yy), SH_C2[2] * 2.f * -x, SH_C2[2] * 2.f * -y, SH_C2[2] * 2.f * 2.f * z)
-      GSR_SH_TERM(7, SH_C2[3] * xz, SH_C2[3] * z, 0.f, SH_C2[3] * x)
-      GSR_SH_TERM(8, SH_C2[4] * (xx - yy), SH_C2[4] * 2.f * x, SH_C2[4] * 2.f * -y, 0.f)
-      if (deg > 2) {
-        GSR_SH_TERM(9, SH_C3[0] * y * (3.f * xx - yy), SH_C3[0] * 3.f * 2.f * xy, SH_C3[0] * 3.f * (xx - yy), 0.f)
-        GSR_SH_TERM(10, SH_C3[1] * xy * z, SH_C3[1] * yz, SH_C3[1] * xz, SH_C3[1] * xy)
-        GSR_SH_TERM(11, SH_C3[2] * y * (4.f * zz - xx - yy), SH_C3[2] * -2.f * xy, SH_C3[2] * (-3.f * yy + 4.f * zz - xx),
-                    SH_C3[2] * 4.f * 2.f * yz)
-        GSR_SH_TERM(12, SH_C3[3] * z * (2.f * zz - 3.f * xx - 3.f * yy), SH_C3[3] * -3.f * 2.f * xz,
-                    SH_C3[3] * -3.f * 2.f * yz, SH_C3[3] * 3.f * (2.f * zz - xx - yy))
-        GSR_SH_TERM(13, SH_C3[4] * x * (4.f * zz - xx - yy), SH_C3[4] * (-3.f * xx + 4.f * zz - yy), SH_C3[4] * -2.f * xy,
-                    SH_C3[4] * 4.f * 2.f * xz)
-        GSR_SH_TERM(14, SH_C3[5] * z * (xx - yy), SH_C3[5] * 2.f * xz, SH_C3[5] * -2.f * yz, SH_C3[5] * (xx - yy))
-        GSR_SH_TERM(15, SH_C3[6] * x * (xx - 3.f * yy), SH_C3[6] * 3.f * (xx - yy), SH_C3[6] * -3.f * 2.f * xy, 0.f)
-      }
-    }
-  }
-#undef GSR_SH_TERM
-}
-
 // ---- B: per Gaussian, over the group's views ---------------------------------------------------
-// Four lanes (a quad) per Gaussian, 64 Gaussians per block.  Lane j of the quad streams piece j (16 B) of each
-// reached view's record and keeps that piece's sums (j = 0: dL/dmean3D, dcov3D[0]; 1: dcov3D[1..4]; 2: dcov3D[5],
-// dL/dcolour; 3: dL/dopacity, the second colour's sums), and lanes 0-2 own SH channel j: its 16 dL/dSH sums and
-// its 16 coefficients in registers.  Per reached view: the colour gradient and clamp bits broadcast in the quad
-// (DPP), each channel lane's dL/dSH += basis x dL/dRGB_j and its part of the view-direction term, summed over the
-// quad (DPP) into dL/dmean3D.  One thread per Gaussian carrying 48 SH sums and the whole record ran at 3 waves per
-// SIMD with SH rows staged through LDS and ~1.3 TB/s (latency bound, DESIGN.md §8 round-5 candidate 1); here a
-// lane holds ~1/4 of that state, the SH rows and dL/dSH go straight to and from HBM (each quad's three channel
-// lanes cover a row's 48 floats in 16 accesses) and the record pieces of a quad are one coalesced 64-byte read.
-// Every sum adds the same terms in the same (view) order as before except the view-direction term's sum over the
-// three channels (a quad DPP sum).  Reach bits (k_render_bwd): only the reached views have records; a Gaussian no
-// view of the group reached keeps its sums (accumulate) or gets zero outputs.
-__device__ __forceinline__ float quad_sum(float v) {
-  v += dpp_f32<0xB1>(v);     // quad_perm [1,0,3,2]
-  return v + dpp_f32<0x4E>(v);  // quad_perm [2,3,0,1]
-}
+// 256 Gaussians per block.  The block's SH rows (contiguous in HBM) are loaded into LDS with fully
+// coalesced loads; each thread reads its row from LDS for every view, accumulates dL/dSH in registers,
+// writes it back into its LDS row, and the block stores the rows coalesced.
+// 3 waves per SIMD (the LDS staging allows 3 blocks per CU): 233 -> 168 VGPRs with two record buffers instead of
+// three and the SH row read from LDS where used; 7 VGPRs spill outside the view loop.  C3 per-Gaussian backward
+// 0.0323 -> 0.0305 ms/view, 8-view sets 0.0514 -> 0.0477 (profiles/r04/gauss_accum_ab.txt)
+__attribute__((amdgpu_waves_per_eu(3, 8)))
 __global__ __launch_bounds__(256) void k_gauss_accum(GaussBackwardArgs a, AccumArgs b) {
-  const int j = threadIdx.x & 3;  // quad lane: record piece j, SH channel j (j < 3)
-  const int idx = a.g0 + blockIdx.x * 64 + (threadIdx.x >> 2);
-  const bool valid = idx < a.g1;
-  const int ix = valid ? idx : a.g0;
-  const int M = a.M, F = 3 * M;
+  extern __shared__ __attribute__((aligned(16))) float s_sh[];
+  const int t = threadIdx.x;
+  const int block0 = a.g0 + blockIdx.x * 256;
+  const int idx = block0 + t;
+  const int nblk = min(256, a.g1 - block0);
+  const int F = 3 * a.M;
+  const int S = sh_lds_stride(a.M);
   const bool has_sh = a.shs != nullptr && F > 0;
   const bool acc = b.accumulate != 0;
-  const int RS = b.dcolors2 ? GSR_REC_STRIDE2 : GSR_REC_STRIDE;
-  const int ncoef = min(min(M, 16), (a.deg + 1) * (a.deg + 1));  // coefficients the basis reaches
-  const unsigned long long reach_word = valid ? b.reach[ix] : 0ull;
-  const bool chan = has_sh && j < 3;
-  float* const dsh_out = has_sh ? a.dL_dsh + (size_t)ix * F + j : nullptr;
-  if (!valid) return;  // (whole quads: every lane of a quad has the same idx)
-  if (reach_word == 0ull) {
-    if (acc) return;
-    if (j == 0) {
+  const float invF = has_sh ? 1.0f / (float)F : 0.0f;
+  // Only the Gaussians some view of the group reached (reach bits) have records; the others keep their sums
+  // (accumulate: nothing read or written) or get zero outputs.  The block's reached SH rows are staged in
+  // LDS (a list of the reached rows, each row read by consecutive threads), its dL/dSH rows stored from LDS
+  // with coalesced writes (all rows, zeros included; with accumulate only the reached rows).
+  __shared__ uint8_t s_rl[256];
+  __shared__ int s_wcnt[4];
+  const unsigned long long reach_word = idx < a.g1 ? b.reach[idx] : 0ull;
+  const bool reached = reach_word != 0ull;
+  int nr = 0;  // reached rows of the block
+  if (has_sh) {
+    const unsigned long long bal = __ballot(reached);
+    const int w = t >> 6;
+    if ((t & 63) == 0) s_wcnt[w] = (int)__popcll(bal);
+    __syncthreads();
+    int base = 0;
+    for (int k = 0; k < 4; ++k) {
+      base += k < w ? s_wcnt[k] : 0;
+      nr += s_wcnt[k];
+    }
+    if (reached) s_rl[base + mask_rank(bal)] = (uint8_t)t;
+    __syncthreads();
+    const int cnt = nr * F;
+    for (int e = t; e < cnt; e += 256) {
+      const int r = (int)(((float)e + 0.5f) * invF);
+      const int tl = s_rl[r];
+      const int k = e - r * F;
+      s_sh[tl * S + k] = a.shs[(size_t)(block0 + tl) * F + k];
+    }
+    __syncthreads();
+  }
+  if (idx < a.g1 && !reached) {
+    if (!acc) {
       for (int k = 0; k < 3; ++k) a.dL_dmeans3D[3 * idx + k] = 0.f;
+      a.dL_dopacity[idx] = 0.f;
+      if (a.dL_dcolors)
+        for (int k = 0; k < 3; ++k) a.dL_dcolors[3 * idx + k] = 0.f;
+      if (b.dcolors2)
+        for (int k = 0; k < 3; ++k) b.dcolors2[3 * idx + k] = 0.f;
       if (b.dcov_carry)
         for (int k = 0; k < 6; ++k) b.dcov_carry[6 * idx + k] = 0.f;
       if (a.dL_dcov3D && a.dL_dcov3D != b.dcov_carry)
@@ -423,122 +479,119 @@ __global__ __launch_bounds__(256) void k_gauss_accum(GaussBackwardArgs a, AccumA
         for (int k = 0; k < 3; ++k) a.dL_dscales[3 * idx + k] = 0.f;
         for (int k = 0; k < 4; ++k) a.dL_drotations[4 * idx + k] = 0.f;
       }
-    } else if (j == 2) {
-      if (a.dL_dcolors)
-        for (int k = 0; k < 3; ++k) a.dL_dcolors[3 * idx + k] = 0.f;
-    } else if (j == 3) {
-      a.dL_dopacity[idx] = 0.f;
-      if (b.dcolors2)
-        for (int k = 0; k < 3; ++k) b.dcolors2[3 * idx + k] = 0.f;
+      if (has_sh) {
+        float* row = s_sh + t * S;
+        for (int k = 0; k < F; ++k) row[k] = 0.f;
+      }
     }
-    if (chan)
-      for (int k = 0; k < M; ++k) dsh_out[3 * k] = 0.f;
-    return;
-  }
-  // this lane's record-piece sums (continued from the outputs with accumulate: the same order as one group)
-  float s4[4] = {0.f, 0.f, 0.f, 0.f};
-  float s16 = 0.f;  // lane 3, two colours: the second colour's blue sum (record field 16)
-  float dsh[16], shv[16];
+  } else if (idx < a.g1) {
+    const float3 mean = make_float3(a.means3D[3 * idx], a.means3D[3 * idx + 1], a.means3D[3 * idx + 2]);
+    float3 dmean = make_float3(0.f, 0.f, 0.f);
+    float dcov[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    float dop = 0.f, dcr = 0.f, dcg = 0.f, dcb = 0.f;
+    float dsh[48];
 #pragma unroll
-  for (int k = 0; k < 16; ++k) dsh[k] = 0.f, shv[k] = 0.f;
-  if (acc) {
-    if (j == 0) {
-      for (int k = 0; k < 3; ++k) s4[k] = a.dL_dmeans3D[3 * idx + k];
-      if (b.dcov_carry) s4[3] = b.dcov_carry[6 * idx];
-    } else if (j == 1) {
+    for (int k = 0; k < 48; ++k) dsh[k] = 0.f;
+    if (acc) {
+      // continue the earlier groups' sums in place (same summation order as one group)
+      dmean = make_float3(a.dL_dmeans3D[3 * idx], a.dL_dmeans3D[3 * idx + 1], a.dL_dmeans3D[3 * idx + 2]);
+      dop = a.dL_dopacity[idx];
+      if (a.dL_dcolors) dcr = a.dL_dcolors[3 * idx], dcg = a.dL_dcolors[3 * idx + 1], dcb = a.dL_dcolors[3 * idx + 2];
       if (b.dcov_carry)
-        for (int k = 0; k < 4; ++k) s4[k] = b.dcov_carry[6 * idx + 1 + k];
-    } else if (j == 2) {
-      if (b.dcov_carry) s4[0] = b.dcov_carry[6 * idx + 5];
-      if (a.dL_dcolors)
-        for (int k = 0; k < 3; ++k) s4[1 + k] = a.dL_dcolors[3 * idx + k];
-    } else {
-      s4[0] = a.dL_dopacity[idx];
-      if (b.dcolors2) s4[2] = b.dcolors2[3 * idx], s4[3] = b.dcolors2[3 * idx + 1], s16 = b.dcolors2[3 * idx + 2];
-    }
-    if (chan)
 #pragma unroll
-      for (int k = 0; k < 16; ++k)
-        if (k < M) dsh[k] = dsh_out[3 * k];
-  }
-  if (chan)
+        for (int k = 0; k < 6; ++k) dcov[k] = b.dcov_carry[6 * idx + k];
+      if (has_sh) {
+        const float* prev = a.dL_dsh + (size_t)idx * F;
 #pragma unroll
-    for (int k = 1; k < 16; ++k)
-      if (k < ncoef) shv[k] = a.shs[(size_t)ix * F + 3 * k + j];
-  const float3 mean = make_float3(a.means3D[3 * ix], a.means3D[3 * ix + 1], a.means3D[3 * ix + 2]);
-  unsigned long long pending = reach_word;
-  auto next_view = [&]() -> int {
-    if (pending == 0ull) return -1;
-    const int v = __builtin_ctzll(pending);
-    pending &= pending - 1ull;
-    return v;
-  };
-  auto load = [&](float4& f, float& f16, int vl) {
-    const float* base = b.vrec + ((size_t)vl * a.P + ix) * RS;
-    f = reinterpret_cast<const float4*>(base)[j];
-    if (b.dcolors2 && j == 3) f16 = base[16];
-  };
-  auto process = [&](const float4& f, const float f16, int vl) {
-    s4[0] += f.x;
-    if (j != 3) s4[1] += f.y;  // (lane 3: .y holds the clamp bits)
-    s4[2] += f.z;
-    s4[3] += f.w;
-    if (b.dcolors2 && j == 3) s16 += f16;
-    if (!has_sh) return;
-    // the view's colour gradient (piece 2) and clamp bits (piece 3) in every lane of the quad
-    const float cr = dpp_f32<0xAA>(f.y), cg = dpp_f32<0xAA>(f.z), cb = dpp_f32<0xAA>(f.w);
-    const uint32_t cl = __float_as_uint(dpp_f32<0xFF>(f.y));
-    // (a view whose colour gradient is zero adds nothing to dL/dSH nor, through the view direction, to dL/dmean)
-    if (!((cr != 0.f) | (cg != 0.f) | (cb != 0.f))) return;
-    const float dR = j == 0 ? ((cl & 1u) ? 0.f : cr) : j == 1 ? ((cl & 2u) ? 0.f : cg) : j == 2 ? ((cl & 4u) ? 0.f : cb) : 0.f;
-    // the camera position through scalar loads where the view is uniform
-    typedef __attribute__((address_space(4))) const float* cfptr;
-    const float cpos[3] = {((cfptr)b.campos[vl])[0], ((cfptr)b.campos[vl])[1], ((cfptr)b.campos[vl])[2]};
-    const float3 dir = make_float3(mean.x - cpos[0], mean.y - cpos[1], mean.z - cpos[2]);
-    const float len = sqrtf(dir.x * dir.x + dir.y * dir.y + dir.z * dir.z);
-    float px = 0.f, py = 0.f, pz = 0.f;  // this channel's sum over k of d basis_k / d (x, y, z) x sh_k
-    sh_channel_backward(a.deg, ncoef, dir.x / len, dir.y / len, dir.z / len, dR, shv, dsh, px, py, pz);
-    const float3 ddir = make_float3(quad_sum(px * dR), quad_sum(py * dR), quad_sum(pz * dR));
-    if (j == 0) {
-      // d normalize(v) / dv applied to ddir, into dL/dmean3D
-      const float3 v = dir;
-      const float sum2 = v.x * v.x + v.y * v.y + v.z * v.z;
-      const float invsum32 = 1.0f / sqrtf(sum2 * sum2 * sum2);
-      s4[0] += ((sum2 - v.x * v.x) * ddir.x - v.y * v.x * ddir.y - v.z * v.x * ddir.z) * invsum32;
-      s4[1] += (-v.x * v.y * ddir.x + (sum2 - v.y * v.y) * ddir.y - v.z * v.y * ddir.z) * invsum32;
-      s4[2] += (-v.x * v.z * ddir.x - v.y * v.z * ddir.y + (sum2 - v.z * v.z) * ddir.z) * invsum32;
+        for (int k = 0; k < 48; ++k)
+          if (k < F) dsh[k] = prev[k];
+      }
     }
-  };
-  // the reached views stream through two register buffers in ascending order (one view's record in flight while
-  // the other's is processed)
-  float4 fa = make_float4(0.f, 0.f, 0.f, 0.f), fb = fa;
-  float fa16 = 0.f, fb16 = 0.f;
-  int va_ = next_view(), vb_ = next_view();
-  if (va_ >= 0) load(fa, fa16, va_);
-  if (vb_ >= 0) load(fb, fb16, vb_);
-  for (;;) {
-    if (va_ < 0) break;
-    process(fa, fa16, va_);
-    va_ = next_view();
-    if (va_ >= 0) load(fa, fa16, va_);
-    if (vb_ < 0) break;
-    process(fb, fb16, vb_);
-    vb_ = next_view();
-    if (vb_ >= 0) load(fb, fb16, vb_);
-  }
-  // dL/dcov3D to lane 0 (pieces 0-2), then the outputs (the sums include the earlier groups: plain stores)
-  const float c1 = dpp_f32<0x55>(s4[0]), c2 = dpp_f32<0x55>(s4[1]), c3 = dpp_f32<0x55>(s4[2]),
-              c4 = dpp_f32<0x55>(s4[3]), c5 = dpp_f32<0xAA>(s4[0]);
-  if (j == 0) {
-    const float dcov[6] = {s4[3], c1, c2, c3, c4, c5};
-    for (int k = 0; k < 3; ++k) a.dL_dmeans3D[3 * idx + k] = s4[k];
+    const float* sh_row = has_sh ? s_sh + t * S : nullptr;
+    // The group's reached views of this Gaussian (reach bits, k_render_bwd): only their records exist.
+    // They stream through two register buffers in view order: while one view's SH backward runs, the next
+    // view's record (16-byte loads of the whole slot) is in flight.
+    const int RS = b.dcolors2 ? GSR_REC_STRIDE2 : GSR_REC_STRIDE;
+    float d2[3] = {0.f, 0.f, 0.f};  // two colours: the second colour's sums
+    if (b.dcolors2 && acc)
+      for (int k = 0; k < 3; ++k) d2[k] = b.dcolors2[3 * idx + k];
+    unsigned long long pending = reach_word;
+    auto next_view = [&]() -> int {
+      if (pending == 0ull) return -1;
+      const int v = __builtin_ctzll(pending);
+      pending &= pending - 1ull;
+      return v;
+    };
+    auto load = [&](float4 (&f)[4], int vl) {
+      const float4* src = reinterpret_cast<const float4*>(b.vrec + ((size_t)vl * a.P + idx) * RS);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) f[q] = src[q];
+    };
+    auto process = [&](const float4 (&f4)[4], int vl) {
+      const float f[16] = {f4[0].x, f4[0].y, f4[0].z, f4[0].w, f4[1].x, f4[1].y, f4[1].z, f4[1].w,
+                           f4[2].x, f4[2].y, f4[2].z, f4[2].w, f4[3].x, f4[3].y, f4[3].z, f4[3].w};
+      dmean.x += f[0];
+      dmean.y += f[1];
+      dmean.z += f[2];
+#pragma unroll
+      for (int k = 0; k < 6; ++k) dcov[k] += f[3 + k];
+      dcr += f[9];
+      dcg += f[10];
+      dcb += f[11];
+      dop += f[12];
+      if (b.dcolors2) {
+        d2[0] += f[14];
+        d2[1] += f[15];
+        d2[2] += b.vrec[((size_t)vl * a.P + idx) * RS + 16];
+      }
+      // (a view whose colour gradient is zero adds nothing to dL/dSH nor, through the view direction,
+      // to dL/dmean: skipped)
+      if (has_sh && ((f[9] != 0.f) | (f[10] != 0.f) | (f[11] != 0.f))) {
+        const uint32_t cl = __float_as_uint(f[13]);
+        const float3 dRGB = make_float3((cl & 1u) ? 0.f : f[9], (cl & 2u) ? 0.f : f[10], (cl & 4u) ? 0.f : f[11]);
+        // the SH row read from LDS where sh_backward uses it (not copied to 48 registers first)
+        const float* shv = sh_row;
+        // the camera position through scalar loads (uniform view): a vector load here would be the
+        // newest in flight and its wait would drain the record prefetch
+        typedef __attribute__((address_space(4))) const float* cfptr;
+        const float cpos[3] = {((cfptr)b.campos[vl])[0], ((cfptr)b.campos[vl])[1], ((cfptr)b.campos[vl])[2]};
+        sh_backward(a.deg, a.M, shv, dsh, dRGB, mean, cpos, dmean);
+      }
+    };
+    float4 fa[4], fb[4];
+    int va_ = next_view(), vb_ = next_view();
+    if (va_ >= 0) load(fa, va_);
+    if (vb_ >= 0) load(fb, vb_);
+    // (buffers refill in turn, so the views are summed in ascending order, as one pass over the group)
+    for (;;) {
+      if (va_ < 0) break;
+      process(fa, va_);
+      va_ = next_view();
+      if (va_ >= 0) load(fa, va_);
+      if (vb_ < 0) break;
+      process(fb, vb_);
+      vb_ = next_view();
+      if (vb_ >= 0) load(fb, vb_);
+    }
+    // (the sums already include the earlier groups: plain stores)
+    a.dL_dmeans3D[3 * idx] = dmean.x;
+    a.dL_dmeans3D[3 * idx + 1] = dmean.y;
+    a.dL_dmeans3D[3 * idx + 2] = dmean.z;
+    a.dL_dopacity[idx] = dop;
+    if (a.dL_dcolors) {
+      a.dL_dcolors[3 * idx] = dcr;
+      a.dL_dcolors[3 * idx + 1] = dcg;
+      a.dL_dcolors[3 * idx + 2] = dcb;
+    }
+    if (b.dcolors2)
+      for (int k = 0; k < 3; ++k) b.dcolors2[3 * idx + k] = d2[k];
     if (b.dcov_carry)
       for (int k = 0; k < 6; ++k) b.dcov_carry[6 * idx + k] = dcov[k];
     if (a.dL_dcov3D && a.dL_dcov3D != b.dcov_carry)
       for (int k = 0; k < 6; ++k) a.dL_dcov3D[6 * idx + k] = dcov[k];
     if (!a.cov3D_precomp && a.dL_dscales) {
-      // from the running dL/dcov3D total (linear, but recomputed rather than summed per group so the result does
-      // not depend on the grouping)
+      // from the running dL/dcov3D total (linear, but recomputed rather than summed per group so the
+      // result does not depend on the grouping)
       const float3 scale = make_float3(a.scales[3 * idx], a.scales[3 * idx + 1], a.scales[3 * idx + 2]);
       const float4 rot = make_float4(a.rotations[4 * idx], a.rotations[4 * idx + 1], a.rotations[4 * idx + 2],
                                      a.rotations[4 * idx + 3]);
@@ -547,19 +600,35 @@ __global__ __launch_bounds__(256) void k_gauss_accum(GaussBackwardArgs a, AccumA
       for (int k = 0; k < 3; ++k) a.dL_dscales[3 * idx + k] = ds[k];
       for (int k = 0; k < 4; ++k) a.dL_drotations[4 * idx + k] = dq[k];
     }
-  } else if (j == 2) {
-    if (a.dL_dcolors)
-      for (int k = 0; k < 3; ++k) a.dL_dcolors[3 * idx + k] = s4[1 + k];
-  } else if (j == 3) {
-    a.dL_dopacity[idx] = s4[0];
-    if (b.dcolors2) b.dcolors2[3 * idx] = s4[2], b.dcolors2[3 * idx + 1] = s4[3], b.dcolors2[3 * idx + 2] = s16;
-  }
-  if (chan)
+    if (has_sh) {
+      // this thread's SH row is no longer read: reuse it for dL/dSH
+      float* row = s_sh + t * S;
+      float4* row4w = reinterpret_cast<float4*>(row);
 #pragma unroll
-    for (int k = 0; k < 16; ++k)
-      if (k < M) dsh_out[3 * k] = dsh[k];
-  if (chan)
-    for (int k = 16; k < M; ++k) dsh_out[3 * k] = 0.f;
+      for (int c = 0; c < 12; ++c)  // 16-byte writes; the padding past 3M is never copied out
+        if (4 * c < F) row4w[c] = make_float4(dsh[4 * c], dsh[4 * c + 1], dsh[4 * c + 2], dsh[4 * c + 3]);
+      for (int k = 48; k < F; ++k) row[k] = 0.f;
+    }
+  }
+  if (has_sh) {
+    __syncthreads();
+    if (!acc) {
+      float* dst = a.dL_dsh + (size_t)block0 * F;
+      const int cnt = nblk * F;
+      for (int e = t; e < cnt; e += 256) {
+        const int te = (int)(((float)e + 0.5f) * invF);
+        dst[e] = s_sh[te * S + (e - te * F)];
+      }
+    } else {
+      const int cnt = nr * F;
+      for (int e = t; e < cnt; e += 256) {
+        const int r = (int)(((float)e + 0.5f) * invF);
+        const int tl = s_rl[r];
+        const int k = e - r * F;
+        a.dL_dsh[(size_t)(block0 + tl) * F + k] = s_sh[tl * S + k];
+      }
+    }
+  }
 }
 
 // ---- A+B fused, without SH (colours precomputed: the SuGaR normal renderer, C5) -------------------------
@@ -736,7 +805,8 @@ void launch_gauss_backward(const GaussBackwardArgs& a, ViewGradArgs va, const Ac
     hipLaunchKernelGGL(k_view_grad<true>, vg_grid, dim3(256), va.cut_in_lds ? cut_bytes : 0, stream, a, va);
   else
     hipLaunchKernelGGL(k_view_grad<false>, vg_grid, dim3(256), va.cut_in_lds ? cut_bytes : 0, stream, a, va);
-  hipLaunchKernelGGL(k_gauss_accum, dim3(div_up(n, 64)), dim3(256), 0, stream, a, b);
+  const size_t lds = (a.shs && a.M > 0) ? (size_t)256 * sh_lds_stride(a.M) * sizeof(float) : 0;
+  hipLaunchKernelGGL(k_gauss_accum, dim3(div_up(n, 256)), dim3(256), lds, stream, a, b);
 }
 
 }  // namespace gsr

@@ -16,6 +16,8 @@
 // walks them in 16 rounds of 64; a lane's rank among equal digits comes from ballot matching,
 // the wave's running count per digit lives in LDS and is touched only by that wave, so the 16
 // rounds need no workgroup barrier.  Order (wave, round, lane) = index order -> stable.
+#include <type_traits>
+
 #include "gsr_kernels.h"
 #include "gsr_wave.h"
 
@@ -40,20 +42,28 @@ __global__ __launch_bounds__(GSR_SORT_THREADS) void k_seg_count(const uint32_t* 
   s_hist[t] = 0u;
   __syncthreads();
   const uint32_t b0 = lb * GSR_SORT_TILE + w * (GSR_SORT_TILE / 4);
-  uint32_t key[GSR_SORT_ITEMS];
+  // (full blocks: no per-item bounds, as k_seg_scatter)
+  auto body = [&](auto full_c) {
+    constexpr bool FULL = decltype(full_c)::value;
+    uint32_t key[GSR_SORT_ITEMS];
 #pragma unroll
-  for (int k = 0; k < GSR_SORT_ITEMS; ++k) {
-    const uint32_t i = b0 + k * 64 + lane;
-    key[k] = i < n ? src[i] : 0u;
-  }
+    for (int k = 0; k < GSR_SORT_ITEMS; ++k) {
+      const uint32_t i = b0 + k * 64 + lane;
+      key[k] = FULL || i < n ? src[i] : 0u;
+    }
 #pragma unroll
-  for (int k = 0; k < GSR_SORT_ITEMS; ++k) {
-    const bool valid = b0 + k * 64 + lane < n;
-    const uint32_t d = (seg_key(kb, key[k]) >> shift) & mask;
-    // one LDS atomic per key: half the time of ballot-matching the digit first (24.4 -> 12.4 us/view
-    // over the 5 passes; the histogram needs no ranks)
-    if (valid) atomicAdd(&s_hist[d], 1u);
-  }
+    for (int k = 0; k < GSR_SORT_ITEMS; ++k) {
+      const bool valid = FULL || b0 + k * 64 + lane < n;
+      const uint32_t d = (seg_key(kb, key[k]) >> shift) & mask;
+      // one LDS atomic per key: half the time of ballot-matching the digit first (24.4 -> 12.4 us/view
+      // over the 5 passes; the histogram needs no ranks)
+      if (valid) atomicAdd(&s_hist[d], 1u);
+    }
+  };
+  if ((lb + 1) * GSR_SORT_TILE <= n)
+    body(std::true_type{});
+  else
+    body(std::false_type{});
   __syncthreads();
   if (t < R) {
     const uint32_t nb = seg.blk[v + 1] - seg.blk[v];
@@ -130,70 +140,80 @@ __global__ __launch_bounds__(GSR_SORT_THREADS) void k_seg_scatter(
   const uint32_t dtot = t < R ? totals[(size_t)v * GSR_RADIX + t] : 0u;
   const uint32_t dcnt = t < R ? counts[(size_t)R * seg.blk[v] + (size_t)t * nb + lb] : 0u;
   const uint32_t b0 = lb * GSR_SORT_TILE + w * (GSR_SORT_TILE / 4);
-  uint32_t key[GSR_SORT_ITEMS], val[GSR_SORT_ITEMS], pos[GSR_SORT_ITEMS];
+  // FULL (every block but a segment's last): no per-item bounds, so each phase's loads, LDS accesses and stores
+  // issue back to back instead of one guarded item at a time
+  auto body = [&](auto full_c) {
+    constexpr bool FULL = decltype(full_c)::value;
+    uint32_t key[GSR_SORT_ITEMS], val[GSR_SORT_ITEMS];
+    uint32_t pos2[GSR_SORT_ITEMS / 2];  // in-wave positions (< 1024), two 16-bit fields per register
 #pragma unroll
-  for (int k = 0; k < GSR_SORT_ITEMS; ++k) {
-    const uint32_t i = b0 + k * 64 + lane;
-    key[k] = i < n ? keys_in[start + i] : 0u;
-    if (KV) val[k] = i < n ? (vals_in ? vals_in[start + i] : i) : 0u;
-  }
-  __syncthreads();
-#pragma unroll
-  for (int k = 0; k < GSR_SORT_ITEMS; ++k) {
-    const bool valid = b0 + k * 64 + lane < n;
-    const uint32_t d = (seg_key(kb, key[k]) >> shift) & mask;
-    const unsigned long long peers = match_digit(d, bits, valid);
-    const uint32_t rank = mask_rank(peers);
-    uint32_t base = 0u;
-    if (valid && rank == 0) {
-      base = s.wcnt[w][d];
-      s.wcnt[w][d] = base + (uint32_t)__popcll(peers);
+    for (int k = 0; k < GSR_SORT_ITEMS; ++k) {
+      const uint32_t i = b0 + k * 64 + lane;
+      key[k] = FULL || i < n ? keys_in[start + i] : 0u;
+      if (KV) val[k] = FULL || i < n ? (vals_in ? vals_in[start + i] : i) : 0u;
     }
-    const int leader = peers ? (int)__builtin_ctzll(peers) : lane;
-    base = (uint32_t)__shfl((int)base, leader, 64);
-    pos[k] = base + rank;
-  }
-  __syncthreads();
-  // per digit: wave offsets, block count, block-local start, segment position of the block's run
-  uint32_t bc = 0u;
-  if (t < R) {
+    __syncthreads();
 #pragma unroll
-    for (int ww = 0; ww < 4; ++ww) {
-      const uint32_t c = s.wcnt[ww][t];
-      s.wcnt[ww][t] = bc;
-      bc += c;
-    }
-  }
-  uint32_t tot;
-  const uint32_t lstart = block_exclusive_scan<GSR_SORT_THREADS>(bc, &tot, s.wave);
-  const uint32_t dstart = block_exclusive_scan<GSR_SORT_THREADS>(dtot, &tot, s.wave);
-  if (t < R) {
-    s.local[t] = lstart;
-    s.glob[t] = dstart + dcnt;
-  }
-  __syncthreads();
-#pragma unroll
-  for (int k = 0; k < GSR_SORT_ITEMS; ++k) {
-    if (b0 + k * 64 + lane < n) {
+    for (int k = 0; k < GSR_SORT_ITEMS; ++k) {
+      const bool valid = FULL || b0 + k * 64 + lane < n;
       const uint32_t d = (seg_key(kb, key[k]) >> shift) & mask;
-      const uint32_t lp = s.local[d] + s.wcnt[w][d] + pos[k];
-      s.keys[lp] = key[k];
-      if (KV) s.vals[lp] = val[k];
+      const unsigned long long peers = match_digit(d, bits, valid);
+      const uint32_t rank = mask_rank(peers);
+      // every lane reads its digit's running count, then the digit's first lane advances it (one wave's LDS
+      // accesses complete in order, so the read sees the count before this round's add: no broadcast needed)
+      const uint32_t base = s.wcnt[w][d];
+      if (valid && rank == 0) s.wcnt[w][d] = base + (uint32_t)__popcll(peers);
+      const uint32_t pk = base + rank;
+      pos2[k >> 1] = (k & 1) ? (pos2[k >> 1] | (pk << 16)) : pk;
     }
-  }
-  __syncthreads();
-  const uint32_t nv = lb * GSR_SORT_TILE < n ? min((uint32_t)GSR_SORT_TILE, n - lb * GSR_SORT_TILE) : 0u;
+    __syncthreads();
+    // per digit: wave offsets, block count, block-local start, segment position of the block's run
+    uint32_t bc = 0u;
+    if (t < R) {
 #pragma unroll
-  for (int k = 0; k < GSR_SORT_ITEMS; ++k) {
-    const uint32_t j = k * GSR_SORT_THREADS + t;
-    if (j < nv) {
-      const uint32_t kk = s.keys[j];
-      const uint32_t d = (seg_key(kb, kk) >> shift) & mask;
-      const uint32_t dst = start + s.glob[d] + (j - s.local[d]);
-      keys_out[dst] = kk;
-      if (KV) vals_out[dst] = s.vals[j];
+      for (int ww = 0; ww < 4; ++ww) {
+        const uint32_t c = s.wcnt[ww][t];
+        s.wcnt[ww][t] = bc;
+        bc += c;
+      }
     }
-  }
+    uint32_t tot;
+    const uint32_t lstart = block_exclusive_scan<GSR_SORT_THREADS>(bc, &tot, s.wave);
+    const uint32_t dstart = block_exclusive_scan<GSR_SORT_THREADS>(dtot, &tot, s.wave);
+    if (t < R) {
+      s.local[t] = lstart;
+      s.glob[t] = dstart + dcnt;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < GSR_SORT_ITEMS; ++k) {
+      if (FULL || b0 + k * 64 + lane < n) {
+        uint32_t d = (seg_key(kb, key[k]) >> shift) & mask;
+        asm volatile("" : "+v"(d));  // (recomputed, not kept from the ranking: 16 registers fewer)
+        const uint32_t lp = s.local[d] + s.wcnt[w][d] + ((pos2[k >> 1] >> (16 * (k & 1))) & 0xFFFFu);
+        s.keys[lp] = key[k];
+        if (KV) s.vals[lp] = val[k];
+      }
+    }
+    __syncthreads();
+    const uint32_t nv = FULL ? (uint32_t)GSR_SORT_TILE
+                             : (lb * GSR_SORT_TILE < n ? min((uint32_t)GSR_SORT_TILE, n - lb * GSR_SORT_TILE) : 0u);
+#pragma unroll
+    for (int k = 0; k < GSR_SORT_ITEMS; ++k) {
+      const uint32_t j = k * GSR_SORT_THREADS + t;
+      if (FULL || j < nv) {
+        const uint32_t kk = s.keys[j];
+        const uint32_t d = (seg_key(kb, kk) >> shift) & mask;
+        const uint32_t dst = start + s.glob[d] + (j - s.local[d]);
+        keys_out[dst] = kk;
+        if (KV) vals_out[dst] = s.vals[j];
+      }
+    }
+  };
+  if ((lb + 1) * GSR_SORT_TILE <= n)
+    body(std::true_type{});
+  else
+    body(std::false_type{});
 }
 
 template <int BITS>

@@ -33,13 +33,17 @@ __device__ __forceinline__ float wave_sum(float x) {
 
 // Lanes of this wave whose `bits`-bit digit equals ours (restricted to lanes with valid=true).
 __device__ __forceinline__ unsigned long long match_digit(uint32_t d, int bits, bool valid) {
-  unsigned long long peers = __ballot(valid);
+  // per bit b: s = 0 / all ones from the lane's bit, x |= ballot ^ s on each 32-bit half (one v_bitop3 each:
+  // table 0xF6 = S0 | (S1 ^ S2)); the peers are the valid lanes with no differing bit
+  uint32_t xlo = 0u, xhi = 0u;
   for (int b = 0; b < bits; ++b) {
-    const bool bit = (d >> b) & 1u;
-    const unsigned long long bal = __ballot(bit);
-    peers &= bit ? bal : ~bal;
+    const uint32_t s = (uint32_t)__builtin_amdgcn_sbfe((int)d, b, 1);
+    const unsigned long long bal = __ballot(s != 0u);
+    xlo = __builtin_amdgcn_bitop3_b32(xlo, (uint32_t)bal, s, 0xF6);
+    xhi = __builtin_amdgcn_bitop3_b32(xhi, (uint32_t)(bal >> 32), s, 0xF6);
   }
-  return peers;
+  const unsigned long long v = __ballot(valid);
+  return (((unsigned long long)~xhi << 32) | ~xlo) & v;
 }
 
 template <int CTRL, int ROW_MASK = 0xf>
