@@ -61,7 +61,8 @@ GRAD_KEYS = ("means3D", "sh", "opacity", "scales", "rotations", "colors", "cov3D
 def _view_task(task):
     """One view: fp32 / fp64 forwards (+ the background composite when bg_img is given, in each precision) and
     the backwards of the upstream gradients `ups` = (dL/dcolour-or-render, dL/ddepth, dL/dalpha) in fp32 and fp64
-    (and fp32 in the other accumulation order, tag "f32r", when `want` holds it).  With `gpu_img` (the GPU's
+    (and fp32 in the other accumulation order, tag "f32r", when `want` holds it; "cov32": the per-view fp32
+    dL/dcov3D stays in the kept view results).  With `gpu_img` (the GPU's
     colour or render of the view): the pixels the GPU flipped on its own and the Gaussians to excuse there.
     Returns dict(f32, f64 forward dicts, aux64, W, H, b = {tag: backward dict}[, gpu_only_px, excuse])."""
     import oracle
@@ -115,7 +116,10 @@ def _chunk(args):
         if ex is not None:
             part["excuse"] = ex if "excuse" not in part else (part["excuse"] | ex)
         if keep_views:
-            r["b"] = {tag: {"means2D": b["means2D"]} for tag, b in r["b"].items()}
+            want = task[6]
+            r["b"] = {tag: dict({"means2D": b["means2D"]},
+                                **({"cov3D": b["cov3D"]} if tag == "f32" and "cov32" in want else {}))
+                      for tag, b in r["b"].items()}
             views.append(r)
     return views, part
 

@@ -113,9 +113,9 @@ def test_c5_kernel_selection_vs_oracle():
     z = np.zeros((1, S, S), np.float32)
     spec_n = ("sugar", 4, 0, 5, "normals")
     views1, tot1 = oracle_pool.views_and_sums(
-        [(spec1, cams[v], bg, ups[v][:3], None, c[v].detach().cpu().numpy(), ("aux32", "f32r")) for v in range(V)])
+        [(spec1, cams[v], bg, ups[v][:3], None, c[v].detach().cpu().numpy(), ("aux32", "f32r", "cov32")) for v in range(V)])
     views2, tot2 = oracle_pool.views_and_sums(
-        [(spec_n, cams[v], bg, (ups[v][3], z, z), None, c2[v].detach().cpu().numpy(), ("f32r",)) for v in range(V)])
+        [(spec_n, cams[v], bg, (ups[v][3], z, z), None, c2[v].detach().cpu().numpy(), ("f32r", "cov32")) for v in range(V)])
     cn, dn, an, rn = (c.detach().cpu().numpy(), d.detach().cpu().numpy(), a.detach().cpu().numpy(), r.cpu().numpy())
     c2n = c2.detach().cpu().numpy()
     for v in range(V):
@@ -131,11 +131,16 @@ def test_c5_kernel_selection_vs_oracle():
     refs = {tag: {k: tot1[p][k] + tot2[p][k] for k in keys} for tag, p in tags}
     for tag, p in tags:
         refs[tag]["colors"], refs[tag]["normals"] = tot1[p]["colors"], tot2[p]["colors"]
-    # the scale / rotation gradients' null model is the GPU's association: the fp32 oracle's dL/dcov3D summed over
-    # both calls and the 16 views, then one fp32 chain rule (the per-view chain rules of the oracle cancel
-    # differently on SuGaR's flat Gaussians, whose third scale is ~0)
-    refs["b32r"]["scales"], refs["b32r"]["rotations"] = oracle_pool.scale_rot_chain(
-        tot1["f32"]["cov3D"] + tot2["f32"]["cov3D"], s1["scales"], s1["rotations"])
+    # the scale / rotation gradients' null model is the GPU's association: per view the two calls' fp32 dL/dcov3D
+    # added, summed over the 16 views in view order in fp32, then one fp32 chain rule (the oracle applies the chain
+    # rule per view and call, and its sums over views are float64; on SuGaR's flat Gaussians, whose third scale is
+    # ~0, the cancellation makes the association visible)
+    acc = np.zeros_like(views1[0]["b"]["f32"]["cov3D"], dtype=np.float32)
+    for v in range(V):
+        acc = (acc + (views1[v]["b"]["f32"]["cov3D"].astype(np.float32)
+                      + views2[v]["b"]["f32"]["cov3D"].astype(np.float32))).astype(np.float32)
+    refs["b32r"]["scales"], refs["b32r"]["rotations"] = oracle_pool.scale_rot_chain(acc, s1["scales"],
+                                                                                     s1["rotations"])
     g = {"g_" + k: t[n].grad.cpu().numpy() for k, n in (("means3D", "means3D"), ("opacity", "opacities"),
                                                         ("scales", "scales"), ("rotations", "rotations"),
                                                         ("colors", "colors_precomp"), ("normals", "normals"))}

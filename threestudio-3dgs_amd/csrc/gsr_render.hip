@@ -1407,8 +1407,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5, 8))) voi
 // Per batch: lane c stages candidate c's record and its cull against the four quadrants; per quadrant the kept
 // candidates are replayed back to front (the replay of k_render_bwd: per pixel the same candidates, order and
 // operations); the lanes that blended append (u, u_1, w, pixel) to the wave's hit list; lane c then forms
-// candidate c's sums from its hits (moments about the quadrant centre, exact x^2, x y, y^2 of the half-integer
-// offsets), turns them into moments about the mean, adds the quadrants as ((q0 + q1) + (q2 + q3)) and writes
+// candidate c's sums from its hits (moments about the candidate's mean, d = mean - pixel per hit as the reference
+// forms it), adds the quadrants as ((q0 + q1) + (q2 + q3)) and writes
 // one row per staged candidate.  A full hit list is summed early (each pair's sums are formed once, whenever).
 // Two colours (TWO, the SuGaR normal renderer's two rasterizer calls on shared geometry): the replay forms both
 // calls' dL/dalpha (the second with its own dL/dpixel and accumulated colour, no depth / alpha terms),
@@ -1571,22 +1571,27 @@ __global__ __launch_bounds__(64) void k_render_bwd_tw(
   // hit-list sums of one (candidate, quadrant) pair -> moments about the candidate's mean (the flush of
   // k_render_bwd); acc = q0 + q1, accb = q2 + q3
   float acc[NM], accb[NM];
+  // The u moments are taken directly about the mean, per hit d = mean - pixel as the reference forms it: SuGaR's
+  // Gaussians blend a few pixels, often away from the quadrant's centre, where moments about the centre turned into
+  // moments about the mean cancel to a few bits (the scale gradients of flat Gaussians amplify that).
   auto pair_moments = [&](const int qq, const uint32_t e, float (&m)[NM]) {
     const int st = (int)(e & 0xffffu), n = (int)(e >> 16);
+    const float4 ga = s0[lane];
+    const float qx0 = (float)(txi * GSR_TILE_X + (qq & 1) * 8), qy0 = (float)(tyi * GSR_TILE_Y + (qq >> 1) * 8);
     float C[NG];
 #pragma unroll
     for (int f = 0; f < NG; ++f) C[f] = 0.f;
     for (int k = st; k < st + n; ++k) {
       const float4 hv = hits[k];
       const uint32_t p = __float_as_uint(hv.w);
-      const float x = (float)(p & 7u) - 3.5f, y = (float)(p >> 3) - 3.5f;
+      const float dx = ga.x - (qx0 + (float)(p & 7u)), dy = ga.y - (qy0 + (float)(p >> 3));
       const float u = hv.x, w = hv.z;
       C[0] += u;
-      C[1] = fmaf(u, x, C[1]);
-      C[2] = fmaf(u, y, C[2]);
-      C[3] = fmaf(u, x * x, C[3]);
-      C[4] = fmaf(u, x * y, C[4]);
-      C[5] = fmaf(u, y * y, C[5]);
+      C[1] = fmaf(u, dx, C[1]);
+      C[2] = fmaf(u, dy, C[2]);
+      C[3] = fmaf(u, dx * dx, C[3]);
+      C[4] = fmaf(u, dx * dy, C[4]);
+      C[5] = fmaf(u, dy * dy, C[5]);
       const float4 d = planes[TWO ? 2 * p : p];
       C[6] = fmaf(w, d.x, C[6]);
       C[7] = fmaf(w, d.y, C[7]);
@@ -1596,29 +1601,18 @@ __global__ __launch_bounds__(64) void k_render_bwd_tw(
         const float u1 = hv.y;
         const float4 d2 = planes[2 * p + 1];
         C[10 % NG] += u1;
-        C[11 % NG] = fmaf(u1, x, C[11 % NG]);
-        C[12 % NG] = fmaf(u1, y, C[12 % NG]);
+        C[11 % NG] = fmaf(u1, dx, C[11 % NG]);
+        C[12 % NG] = fmaf(u1, dy, C[12 % NG]);
         C[13 % NG] = fmaf(w, d2.x, C[13 % NG]);
         C[14 % NG] = fmaf(w, d2.y, C[14 % NG]);
         C[15 % NG] = fmaf(w, d2.z, C[15 % NG]);
       }
     }
-    const float4 ga = s0[lane];
-    const float mx = ga.x - ((float)(txi * GSR_TILE_X + (qq & 1) * 8) + 3.5f);
-    const float my = ga.y - ((float)(tyi * GSR_TILE_Y + (qq >> 1) * 8) + 3.5f);
-    m[0] = C[0];
-    m[1] = mx * C[0] - C[1];
-    m[2] = my * C[0] - C[2];
-    m[3] = mx * (mx * C[0] - 2.f * C[1]) + C[3];
-    m[4] = mx * (my * C[0] - C[2]) - my * C[1] + C[4];
-    m[5] = my * (my * C[0] - 2.f * C[2]) + C[5];
-    m[6] = C[6];
-    m[7] = C[7];
-    m[8] = C[8];
-    m[9] = C[9];
+#pragma unroll
+    for (int f = 0; f < 10; ++f) m[f] = C[f];
     if (TWO) {
-      m[10 % NM] = mx * C[10 % NG] - C[11 % NG];
-      m[11 % NM] = my * C[10 % NG] - C[12 % NG];
+      m[10 % NM] = C[11 % NG];
+      m[11 % NM] = C[12 % NG];
       m[12 % NM] = C[13 % NG];
       m[13 % NM] = C[14 % NG];
       m[14 % NM] = C[15 % NG];
