@@ -71,12 +71,12 @@ def parse():
     ap.add_argument("--path", choices=["batched", "per-view"], default="batched",
                     help="batched: rasterize_views (one autograd node per rank's views); per-view: one "
                          "GaussianRasterizer call per view, exactly as the reference renderer loop does")
-    ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "r04u_traffic.json"),
+    ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "r05l_traffic.json"),
                     help="PMC summary (profiles/summarize.py) supplying roofline.traffic and the VALU counts")
-    ap.add_argument("--pairs", default=os.path.join(ROOT, "profiles", "r03_pairs.json"),
+    ap.add_argument("--pairs", default=os.path.join(ROOT, "profiles", "r05l_pairs.json"),
                     help="device-counted blend pairs (profiles/diag_pairs.py) for the VALU roofline")
-    ap.add_argument("--traffic-sugar", default=os.path.join(ROOT, "profiles", "r04u_sugar_traffic.json"),
-                    help="PMC summary of the C5 line (--workload sugar, profiles/summarize.py r04c_sugar)")
+    ap.add_argument("--traffic-sugar", default=os.path.join(ROOT, "profiles", "r05l_sugar_traffic.json"),
+                    help="PMC summary of the C5 line (--workload sugar, profiles/summarize.py r05l_sugar)")
     ap.add_argument("--overlap-reduce", choices=["on", "off"], default="on",
                     help="N > 1: sum the Gaussian gradients over ranks inside the backward, range by range as the "
                          "per-Gaussian backward forms them (view_shard.ChunkedGradReduce, overlapped on a side "
@@ -523,8 +523,8 @@ def roofline_fields(args, phases, Ks, Ls, H, W, launched=None, build=None):
             r["valu"] = v
         r["limiter"] = "VALU issue / LDS latency per (pixel, Gaussian) pair, not HBM (see counter_frac, valu)"
         if sugar and phase == "render_bwd":
-            r["limiter"] = ("latency of the per-candidate replay chain and its LDS round trips (the quadrants of a "
-                            "tile walked in turn by one or two waves, 3 waves per SIMD), not HBM; VALU ~30 % busy")
+            r["limiter"] = ("latency of the per-candidate replay chain and its LDS round trips (the four quadrants of "
+                            "a tile walked in turn by one wave, 2 waves per SIMD at 225 VGPRs), not HBM")
         rows[phase] = r
     dominant = max(phases.items(), key=lambda kv: kv[1][0])[0]
     blend = "render_bwd" if phases["render_bwd"][0] >= phases["render_fwd"][0] else "render_fwd"
