@@ -1345,7 +1345,10 @@ __device__ __forceinline__ void bwd_tile(BwdLDS& s, const RenderSet& rs, int v, 
         row[2] = make_float4(m[8], m[9], 0.f, 0.f);
       }
     }
-    __syncthreads();
+    // No barrier before the next batch's staging: candidate cs's staged record and slot are read here by threads
+    // 4 cs .. 4 cs + 3 and rewritten there by the same four threads (t >> 2 = cs), lanes of one wave whose LDS
+    // accesses complete in program order; the next batch's replay, which rewrites the sums read here, waits at the
+    // staging barrier.
   }
 #ifdef GSR_TIMELINE
   // bwd record: z = sum over batches of 4 x the busiest quadrant's kept count (not HW_ID)
