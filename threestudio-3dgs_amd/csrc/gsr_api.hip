@@ -535,10 +535,11 @@ static int set_render(int V, int P, const int* K, int width, int height, const f
   const int tres = tile_sort_result(width, height);
   inst.ndev = g.counters + 2 * V;  // kept instances per view (<= K, the list capacity)
   GSR_HIP_CHECK(hipMemsetAsync(img.split_mode, split ? 1 : 0, sizeof(uint32_t), s));
-  // the tile-wave forward records each listed instance's quadrant mask for the backward's cull (in the free
-  // ping-pong key array of the binning buffer); [1] says whether this forward does
+  // the forward records its cull of each listed instance for the backward (in the free ping-pong key array of the
+  // binning buffer, 4 bytes per instance); [1] says in which layout: 1 = the tile-wave forward's 4-bit mask per
+  // byte, 2 = one byte per (instance, quadrant) from the quadrant-wave forward's waves
   const bool tile_masks = fwd_tile_chosen(total, (long long)V * P, V);
-  GSR_HIP_CHECK(hipMemsetAsync(img.split_mode + 1, tile_masks ? 1 : 0, sizeof(uint32_t), s));
+  GSR_HIP_CHECK(hipMemsetAsync(img.split_mode + 1, total > 0 ? (tile_masks ? 1 : 2) : 0, sizeof(uint32_t), s));
   {
     PhaseScope ps(GSR_PHASE_BINNING, s);
     GSR_HIP_CHECK(hipMemsetAsync(img.ranges, 0, sizeof(uint2) * (size_t)V * gx * gy, s));
@@ -567,7 +568,7 @@ static int set_render(int V, int P, const int* K, int width, int height, const f
     rs.split_cap = img.split_cap;
     rs.split_extra = split_extra(V, (size_t)gx * gy);
     rs.qkeys = tp.qmask ? b.key[tres] : nullptr;
-    rs.qbytes = tile_masks ? reinterpret_cast<uint8_t*>(b.key[tres ^ 1]) : nullptr;
+    rs.qbytes = total > 0 ? reinterpret_cast<uint8_t*>(b.key[tres ^ 1]) : nullptr;
     rs.V = V;
     rs.v0 = 0;
     rs.P = P;

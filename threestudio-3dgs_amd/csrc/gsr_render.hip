@@ -278,6 +278,9 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(GSR_FWD_WPE,
     }
     bool keep = false;
     if (i < n) keep = qkeys ? kc : quadrant_hit(r0, r1, (float)qx0, (float)qy0);
+    // the backward's cull (RenderSet::qbytes, layout 2: byte 4 i + q of the set's listed instance i; batches past
+    // the quadrant's termination are never walked, and the backward reads only below its deepest blend)
+    if (rs.qbytes != nullptr && i < n) rs.qbytes[4 * ((size_t)rs.inst_start[v] + range.x + i) + q] = keep ? 1u : 0u;
     const unsigned long long bal = __ballot(keep);
     const int cnt = __popcll(bal);
     if (keep) {
@@ -1004,14 +1007,18 @@ __device__ __forceinline__ void bwd_tile(BwdLDS& s, const RenderSet& rs, int v, 
   // this view's reach bit (staged candidates have rows): word v >> 5 of the Gaussian's 64 bits
   unsigned int* const reach32 = reinterpret_cast<unsigned int*>(reach) + (v >> 5);
   const unsigned int vbit = 1u << (v & 31);
-  // the tile-wave forward's per-instance quadrant masks (ImageState::split_mode[1]): the cull is read, one
+  // the forward's per-instance quadrant cull (ImageState::split_mode[1]): the cull is read, one
   // batch ahead, instead of recomputed (both bounds are conservative: a pair either keeps has no blend beyond
   // the other's, so the sums agree)
-  const uint8_t* const qbm =
-      rs.qbytes != nullptr && rs.split_mode != nullptr && rs.split_mode[1] != 0u ? rs.qbytes + rs.inst_start[v] + range.x
-                                                                                 : nullptr;
+  // (layout 1, the tile-wave forward: byte i = the 4-bit mask of instance i; layout 2, the quadrant-wave forward:
+  // byte 4 i + q = quadrant q keeps instance i)
+  // (split_mode[1] is set by a byte memset: its low byte is the layout)
+  const uint32_t qlayout = rs.qbytes != nullptr && rs.split_mode != nullptr ? (rs.split_mode[1] & 0xffu) : 0u;
+  const size_t qpos0 = (size_t)rs.inst_start[v] + range.x;
+  const uint8_t* const qbm = qlayout == 0u ? nullptr : qlayout == 1u ? rs.qbytes + qpos0 : rs.qbytes + 4 * qpos0 + q;
+  const uint32_t qstride = qlayout == 2u ? 4u : 1u, qsh = qlayout == 2u ? 0u : (uint32_t)q;
   uint32_t nqb = 0u;
-  if (qbm != nullptr && hi - 1 - lane >= lo) nqb = qbm[hi - 1 - lane];
+  if (qbm != nullptr && hi - 1 - lane >= lo) nqb = qbm[qstride * (uint32_t)(hi - 1 - lane)];
   if (hi > lo) {
     const uint32_t g0 = fetch_index(hi);
     if (hi - 1 - cs >= lo) {
@@ -1163,7 +1170,7 @@ __device__ __forceinline__ void bwd_tile(BwdLDS& s, const RenderSet& rs, int v, 
       }
     }
     const uint32_t qcur = nqb;
-    if (qbm != nullptr && h - 65 - lane >= lo) nqb = qbm[h - 65 - lane];
+    if (qbm != nullptr && h - 65 - lane >= lo) nqb = qbm[qstride * (uint32_t)(h - 65 - lane)];
     __syncthreads();
     // this wave's quadrant: cull the staged batch, list the kept candidates, zero the others' sums
     const int rel_l = h - 1 - lane;
@@ -1172,7 +1179,7 @@ __device__ __forceinline__ void bwd_tile(BwdLDS& s, const RenderSet& rs, int v, 
     if (rel_l >= lo && rel_l < qmaxc) keep = s.s0[lane].x > -1e30f;
 #else
     if (qbm != nullptr) {
-      keep = rel_l >= lo && rel_l < qmaxc && ((qcur >> q) & 1u);
+      keep = rel_l >= lo && rel_l < qmaxc && ((qcur >> qsh) & 1u);
     } else if (rel_l >= lo && rel_l < qmaxc) {
       // the staged conic back to (a, b, c) for the (padded, conservative) cull
       const float4 c0 = s.s0[lane], c1 = s.s1[lane];
