@@ -34,7 +34,7 @@ __global__ __launch_bounds__(GSR_SORT_THREADS) void k_seg_count(const uint32_t* 
   __shared__ uint32_t s_hist[GSR_RADIX];
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
   uint32_t lb;
-  const int v = seg_of_block(seg, blockIdx.x, lb);
+  const int v = seg_of_block(seg, xcd_block(blockIdx.x, gridDim.x), lb);  // (logical block: XCD-contiguous)
   const uint32_t n = seg_live(seg, v);
   const uint32_t* src = keys + seg.start[v];
   const uint32_t mask = (1u << bits) - 1u;
@@ -114,9 +114,10 @@ struct ScatterLDS {
 };
 
 // KV = false: keys only (packed tile keys); vals_in / vals_out unused.
-// (keys only: 6 waves per SIMD, 83 -> 80 VGPRs — the LDS allows 7 workgroups per CU; with values the LDS allows 4)
+// (keys only: 5 waves per SIMD, 88 VGPRs without spills — the LDS allows 7 workgroups per CU, but at 6 waves the
+// 80-VGPR budget spills in the full-block path; with values the LDS allows 4; profiles/r05/ab_r05s5.txt)
 template <bool KV, int BITS>
-__attribute__((amdgpu_waves_per_eu(KV ? 4 : 6, 8)))
+__attribute__((amdgpu_waves_per_eu(KV ? 4 : 5, 8)))
 __global__ __launch_bounds__(GSR_SORT_THREADS) void k_seg_scatter(
     const uint32_t* __restrict__ keys_in, const uint32_t* __restrict__ vals_in, uint32_t* __restrict__ keys_out,
     uint32_t* __restrict__ vals_out, SegInfo seg, int shift, int bits_rt, int last, const uint32_t* __restrict__ counts,
@@ -127,7 +128,7 @@ __global__ __launch_bounds__(GSR_SORT_THREADS) void k_seg_scatter(
   __shared__ ScatterLDS<KV> s;
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
   uint32_t lb;
-  const int v = seg_of_block(seg, blockIdx.x, lb);
+  const int v = seg_of_block(seg, xcd_block(blockIdx.x, gridDim.x), lb);  // (logical block: XCD-contiguous)
   const uint32_t n = seg_live(seg, v);
   const uint32_t start = seg.start[v];
   const uint32_t mask = (1u << bits) - 1u;
