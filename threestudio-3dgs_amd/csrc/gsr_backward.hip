@@ -39,7 +39,7 @@ template <bool TWO>
 __device__ __forceinline__ RowSums gather_rows(uint32_t idx, const GaussRec& gr, uint32_t i0, int grid_x,
                                                const uint2* cut, const float4* grow) {
   RowSums r = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-  constexpr int RW = 4;  // 64-B rows (one colour: the fourth float4 unused and never read)
+  constexpr int RW = TWO ? 4 : 3;
   const uint4 gd = gr.d;
   const float4 ga = gr.a, gb = gr.b;
   const uint32_t dkey = __float_as_uint(gb.z);

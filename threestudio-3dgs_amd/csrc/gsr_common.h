@@ -369,12 +369,11 @@ struct ImageState {
 #define GSR_REC_STRIDE2 20
 struct BackwardState {
   unsigned long long* reach;  // [P]: bit v set = view v of the group gave the Gaussian a gradient row
-  float4* grow;               // [4 * instances of the group]: 64-B rows (one colour uses 3 float4 of each)
+  float4* grow;               // [3 (two colours: 4) * instances of the group]
   float* vrec;  // [views][P][GSR_REC_STRIDE (two colours: GSR_REC_STRIDE2)]; only the reached pairs' are written
   static size_t reach_bytes(int P) { return align_up(sizeof(unsigned long long) * (size_t)(P > 0 ? P : 1), 256); }
   static size_t rows_bytes(long long K, bool two = false) {
-    (void)two;  // (both layouts: 64-B rows, so each row gather is one aligned segment)
-    return align_up(sizeof(float4) * 4 * (size_t)(K > 0 ? K : 1), 256);
+    return align_up(sizeof(float4) * (two ? 4 : 3) * (size_t)(K > 0 ? K : 1), 256);
   }
   static size_t bytes_for(long long K, int views, int P, bool two = false) {
     return reach_bytes(P) + rows_bytes(K, two) +

@@ -882,7 +882,7 @@ __device__ __forceinline__ void bwd_tile(BwdLDS& s, const RenderSet& rs, int v, 
   constexpr int QS = GSR_QSUM_STRIDE;    // per candidate
   constexpr int GS = 8;                  // candidates per 16x16 product
   constexpr int NPL = 4;                 // dL/dpixel planes in the B operand
-  constexpr int RW = 4;                  // float4 per gradient row: 64-B aligned (the fourth unused, §3.2 item 26)
+  constexpr int RW = 3;                  // float4 per gradient row
   GSR_TL_BEGIN
   const int W = rs.W, H = rs.H, grid_x = rs.gx;
   const size_t vgs = (size_t)(rs.v0 + v);
@@ -1434,7 +1434,7 @@ __global__ __launch_bounds__(64) void k_render_bwd_tw(
     unsigned long long* __restrict__ reach) {
   constexpr int NG = TWO ? NGV2 : NGV;  // raw sums per (candidate, quadrant)
   constexpr int NM = TWO ? 15 : NGV;    // moments per candidate
-  constexpr int RW = 4;                  // float4 per gradient row (64-B aligned)
+  constexpr int RW = TWO ? 4 : 3;       // float4 per gradient row
   constexpr int NQ = 4;                 // quadrants per wave
   __shared__ float4 s0[65], s1[65], s2[65];
   __shared__ float4 s3[65];  // (b, b2) of the interleaved colours
