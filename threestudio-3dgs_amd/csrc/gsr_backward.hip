@@ -281,15 +281,17 @@ static inline __host__ __device__ int sh_lds_stride(int M) { return ((3 * M + 3)
 #endif
 // (4 waves per SIMD for both variants: the two-colour one would otherwise take 136 VGPRs and 3 waves;
 // capped it spills 4 VGPRs outside the row loop and its per-Gaussian backward is 4 % faster on C5)
-template <bool TWO>
+// CUT_LDS (= va.cut_in_lds) at compile time: the cut-off reads are ds_read from the staged copy, not flat loads
+// through a pointer that may be either (a flat load of LDS waits on both counters at the memory path's latency).
+template <bool TWO, bool CUT_LDS>
 __attribute__((amdgpu_waves_per_eu(4, 8)))
 __global__ __launch_bounds__(256) void k_view_grad(GaussBackwardArgs a, ViewGradArgs va) {
   extern __shared__ uint2 s_cut[];
   const int t = threadIdx.x;
   const int vl = blockIdx.x % va.V;
   const int vg = va.v0 + vl;
-  const uint2* cut = va.cut_in_lds ? reinterpret_cast<const uint2*>(s_cut) : va.img.cut + (size_t)vg * va.tiles;
-  if (va.cut_in_lds) {
+  const uint2* cut = CUT_LDS ? reinterpret_cast<const uint2*>(s_cut) : va.img.cut + (size_t)vg * va.tiles;
+  if (CUT_LDS) {
     const uint4* src = reinterpret_cast<const uint4*>(va.img.cut + (size_t)vg * va.tiles);
     uint4* dst = reinterpret_cast<uint4*>(s_cut);
     for (int k = t; k < va.tiles / 2; k += 256) dst[k] = src[k];
@@ -801,10 +803,9 @@ void launch_gauss_backward(const GaussBackwardArgs& a, ViewGradArgs va, const Ac
   va.items = GSR_VG_ITEMS;
   while (va.items > 2 && (long long)va.V * div_up(n, 256 * va.items) < 1024) va.items >>= 1;
   const dim3 vg_grid(va.V * div_up(n, 256 * va.items));
-  if (b.dcolors2)
-    hipLaunchKernelGGL(k_view_grad<true>, vg_grid, dim3(256), va.cut_in_lds ? cut_bytes : 0, stream, a, va);
-  else
-    hipLaunchKernelGGL(k_view_grad<false>, vg_grid, dim3(256), va.cut_in_lds ? cut_bytes : 0, stream, a, va);
+  auto vg_kern = b.dcolors2 ? (va.cut_in_lds ? k_view_grad<true, true> : k_view_grad<true, false>)
+                            : (va.cut_in_lds ? k_view_grad<false, true> : k_view_grad<false, false>);
+  hipLaunchKernelGGL(vg_kern, vg_grid, dim3(256), va.cut_in_lds ? cut_bytes : 0, stream, a, va);
   const size_t lds = (a.shs && a.M > 0) ? (size_t)256 * sh_lds_stride(a.M) * sizeof(float) : 0;
   hipLaunchKernelGGL(k_gauss_accum, dim3(div_up(n, 256)), dim3(256), lds, stream, a, b);
 }

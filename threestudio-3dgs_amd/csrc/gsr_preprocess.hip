@@ -29,6 +29,9 @@ void launch_preprocess_kernel(const PreprocessArgs& a, const SetCams& cams, cons
 #define GSR_PRE_LDS_FLOATS (8 * 1024)  // SH staging up to 32 KB (M <= 21); larger M reads SH from HBM
 
 // (6 waves per SIMD: 86 -> 79 VGPRs without spills; the LDS allows 6 blocks — 1 % faster)
+// SH_LDS: the SH coefficients are staged (known at compile time, so the SH evaluation reads them with ds_read,
+// not flat loads through a pointer that may point either way)
+template <bool SH_LDS>
 __attribute__((amdgpu_waves_per_eu(6, 8)))
 __global__ __launch_bounds__(256) void k_preprocess(PreprocessArgs a, SetCams cams, GeomState g) {
   extern __shared__ float s_sh[];  // [128][3M + 1] this block's SH coefficients (odd stride)
@@ -44,7 +47,7 @@ __global__ __launch_bounds__(256) void k_preprocess(PreprocessArgs a, SetCams ca
   const int v0 = vb + half * vh, v1 = half == 0 ? min(ve, vb + vh) : ve;
   const int nsh = a.colors_precomp == nullptr ? 3 * a.M : 0;
   const int sstride = nsh + 1;
-  const bool staged = nsh > 0 && GSR_PRE_GAUSS * sstride <= GSR_PRE_LDS_FLOATS;
+  const bool staged = SH_LDS;  // (host: nsh > 0 && GSR_PRE_GAUSS * sstride <= GSR_PRE_LDS_FLOATS)
   if (staged) {
     // coalesced 16-byte loads of the block's contiguous SH slice (256 * 3M floats, 16-B aligned)
     const int n = min(GSR_PRE_GAUSS, a.P - idx0) * nsh;
@@ -217,9 +220,10 @@ void launch_preprocess(const PreprocessArgs& a, const SetCams& cams, const GeomS
 void launch_preprocess_kernel(const PreprocessArgs& a, const SetCams& cams, const GeomState& g, hipStream_t stream) {
   const int nvc = (a.V + GSR_PRE_VIEWS - 1) / GSR_PRE_VIEWS;
   const size_t want = a.colors_precomp == nullptr ? (size_t)GSR_PRE_GAUSS * (3 * a.M + 1) : 0;
-  const size_t lds = want <= GSR_PRE_LDS_FLOATS ? sizeof(float) * want : 0;
-  hipLaunchKernelGGL(k_preprocess, dim3(nvc * ((a.P + GSR_PRE_GAUSS - 1) / GSR_PRE_GAUSS)), dim3(256), lds, stream, a,
-                     cams, g);
+  const bool sh_lds = a.colors_precomp == nullptr && a.M > 0 && want <= GSR_PRE_LDS_FLOATS;
+  const size_t lds = sh_lds ? sizeof(float) * want : 0;
+  hipLaunchKernelGGL(sh_lds ? k_preprocess<true> : k_preprocess<false>,
+                     dim3(nvc * ((a.P + GSR_PRE_GAUSS - 1) / GSR_PRE_GAUSS)), dim3(256), lds, stream, a, cams, g);
 }
 
 }  // namespace gsr

@@ -229,13 +229,16 @@ def rasterize_gaussians(bg, means3D, colors, opacity, scales, rotations, scale_m
     P = int(means3D.size(0))
     H, W = int(image_height), int(image_width)
     fopt = dict(dtype=torch.float32, device=device)
-    out_color = torch.zeros((3, H, W), **fopt)
-    out_depth = torch.zeros((1, H, W), **fopt)
-    out_alpha = torch.zeros((1, H, W), **fopt)
-    radii = torch.zeros((P,), dtype=torch.int32, device=device)
     u8 = dict(dtype=torch.uint8, device=device)
     if P == 0:
-        return 0, out_color, out_depth, out_alpha, radii, torch.empty(0, **u8), torch.empty(0, **u8), torch.empty(0, **u8)
+        return (0, torch.zeros((3, H, W), **fopt), torch.zeros((1, H, W), **fopt), torch.zeros((1, H, W), **fopt),
+                torch.zeros((0,), dtype=torch.int32, device=device), torch.empty(0, **u8), torch.empty(0, **u8),
+                torch.empty(0, **u8))
+    # (no zero fill: the preprocess writes every radius and the blend every pixel, as on the batched path)
+    out_color = torch.empty((3, H, W), **fopt)
+    out_depth = torch.empty((1, H, W), **fopt)
+    out_alpha = torch.empty((1, H, W), **fopt)
+    radii = torch.empty((P,), dtype=torch.int32, device=device)
 
     means3D = _f32(means3D, "means3D", device)
     colors = _f32(colors, "colors_precomp", device)
