@@ -14,27 +14,40 @@
 
 namespace gsr {
 
-// Kept tiles of each 64-Gaussian group of every view's depth order (one wave per group, 4 groups per
-// block): kept_counts[v][group].  The counts ride in the depth-sorted values (streamed); a count that
-// did not fit its field is read from tiles.y.
+// Kept tiles of each 64-Gaussian group of every view's depth order (GSR_INST_GROUPS consecutive groups per
+// wave, 4 waves per block: a block per 4 groups made the launch a quarter-million 1-KB blocks):
+// kept_counts[v][group].  The counts ride in the depth-sorted values (streamed); a count that did not fit its
+// field is read from tiles.y.
+#ifndef GSR_INST_GROUPS
+#define GSR_INST_GROUPS 8
+#endif
 __global__ __launch_bounds__(256) void k_inst_count(int P, int nbe, GeomState g) {
   const uint32_t* __restrict__ order = g.sorted_dval();
-  const int nb4 = (nbe + 3) / 4;
-  const int v = blockIdx.x / nb4;
-  const int lb = (blockIdx.x - v * nb4) * 4 + (threadIdx.x >> 6);
-  if (lb >= nbe) return;
+  constexpr int GPB = 4 * GSR_INST_GROUPS;  // groups per block
+  const int nbb = (nbe + GPB - 1) / GPB;
+  const int v = blockIdx.x / nbb;
+  const int lb0 = (blockIdx.x - v * nbb) * GPB + (threadIdx.x >> 6) * GSR_INST_GROUPS;
   const int lane = threadIdx.x & 63;
   const size_t vo = (size_t)v * P;
-  const int r = lb * GSR_DUP_TILE + lane;
-  uint32_t kept = 0u;
-  if (r < P) {
-    const uint32_t val = order[vo + r];
-    const uint32_t ks = g.vsent();
-    kept = g.vbits <= 26 ? val >> g.vbits : ks;
-    if (kept == ks) kept = g.tiles[vo + (val & g.vmask())].y;
+  const uint32_t ks = g.vsent();
+  uint32_t val[GSR_INST_GROUPS];
+#pragma unroll
+  for (int k = 0; k < GSR_INST_GROUPS; ++k) {  // (all loads first)
+    const int r = (lb0 + k) * GSR_DUP_TILE + lane;
+    val[k] = lb0 + k < nbe && r < P ? order[vo + r] : 0u;
   }
-  const uint32_t ktot = __builtin_amdgcn_readlane((int)wave_incl_sum_dpp(kept), 63);
-  if (lane == 0) g.kept_counts[(size_t)v * nbe + lb] = ktot;
+  uint32_t mine = 0u;  // lane k keeps group lb0 + k's total
+#pragma unroll
+  for (int k = 0; k < GSR_INST_GROUPS; ++k) {
+    uint32_t kept = 0u;
+    if (lb0 + k < nbe && (lb0 + k) * GSR_DUP_TILE + lane < P) {
+      kept = g.vbits <= 26 ? val[k] >> g.vbits : ks;
+      if (kept == ks) kept = g.tiles[vo + (val[k] & g.vmask())].y;
+    }
+    const uint32_t ktot = __builtin_amdgcn_readlane((int)wave_incl_sum_dpp(kept), 63);
+    if (lane == k) mine = ktot;
+  }
+  if (lane < GSR_INST_GROUPS && lb0 + lane < nbe) g.kept_counts[(size_t)v * nbe + lb0 + lane] = mine;
 }
 
 // One 1024-thread workgroup per view: exclusive scan of its kept counts in place, GSR_ISCAN_PER x 1024 entries
@@ -379,7 +392,8 @@ void launch_binning_counts(int V, int P, const GeomState& g, hipStream_t stream)
   hipLaunchKernelGGL(k_goff_scan, dim3(V), dim3(1024), 0, stream, P > 0 ? nbg : 0, g);  // K_v, visible
   if (P > 0) hipLaunchKernelGGL(k_goff_write, dim3(V * nbg), dim3(256), 0, stream, P, nbg, g);
   if (P > 0)
-    hipLaunchKernelGGL(k_inst_count, dim3(V * ((nbe + 3) / 4)), dim3(256), 0, stream, P, nbe, g);
+    hipLaunchKernelGGL(k_inst_count, dim3(V * ((nbe + 4 * GSR_INST_GROUPS - 1) / (4 * GSR_INST_GROUPS))), dim3(256),
+                       0, stream, P, nbe, g);
   hipLaunchKernelGGL(k_inst_scan, dim3(V), dim3(1024), 0, stream, P > 0 ? nbe : 0, g);
 }
 
