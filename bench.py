@@ -71,12 +71,12 @@ def parse():
     ap.add_argument("--path", choices=["batched", "per-view"], default="batched",
                     help="batched: rasterize_views (one autograd node per rank's views); per-view: one "
                          "GaussianRasterizer call per view, exactly as the reference renderer loop does")
-    ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "r05xb_traffic.json"),
+    ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "r05zz_traffic.json"),
                     help="PMC summary (profiles/summarize.py) supplying roofline.traffic and the VALU counts")
-    ap.add_argument("--pairs", default=os.path.join(ROOT, "profiles", "r05xb_pairs.json"),
+    ap.add_argument("--pairs", default=os.path.join(ROOT, "profiles", "r05zz_pairs.json"),
                     help="device-counted blend pairs (profiles/diag_pairs.py) for the VALU roofline")
-    ap.add_argument("--traffic-sugar", default=os.path.join(ROOT, "profiles", "r05xb_sugar_traffic.json"),
-                    help="PMC summary of the C5 line (--workload sugar, profiles/summarize.py r05xb_sugar)")
+    ap.add_argument("--traffic-sugar", default=os.path.join(ROOT, "profiles", "r05zz_sugar_traffic.json"),
+                    help="PMC summary of the C5 line (--workload sugar, profiles/summarize.py r05zz_sugar)")
     ap.add_argument("--overlap-reduce", choices=["on", "off"], default="on",
                     help="N > 1: sum the Gaussian gradients over ranks inside the backward, range by range as the "
                          "per-Gaussian backward forms them (view_shard.ChunkedGradReduce, overlapped on a side "
