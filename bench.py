@@ -164,12 +164,13 @@ def render_view(rep: Replica, cam, bg_zero, bg_img, shade=None):
         scales=rep.scales, rotations=rep.rotations, cov3D_precomp=None)
     H, W = cam["H"], cam["W"]
     if shade is not None:
-        # the shading renderer's torch epilogue (renderer/diff_gaussian_rasterizer_shading.py:169-208)
-        import torch_reference as tr
+        # the shading renderer's epilogue (renderer/diff_gaussian_rasterizer_shading.py:169-208) for this one view,
+        # through the product's fused shading kernels (shading.shade_views)
+        from diff_gaussian_rasterization.shading import shade_views
 
         rays_o, rays_d, light = shade
-        ka, kd = (torch.tensor(k, device=color.device) for k in (SHADE_KA, SHADE_KD))
-        render, normal, depth_m = tr.shading_epilogue(color, depth, alpha, rays_o, rays_d, bg_img, light, ka, kd)
+        render, normal, depth_m = shade_views(color, depth, alpha, rays_o, rays_d, bg_img, light, SHADE_KA,
+                                              SHADE_KD, "diffuse")
         return render, depth_m, alpha, radii, normal
     # background path composite + clamp, the reference's torch lines
     # (renderer/diff_gaussian_rasterizer_background.py:129-132, 139)
@@ -462,7 +463,8 @@ def roofline_fields(args, phases, Ks, Ls, H, W, launched=None, build=None):
     if build is not None:
         if (profiled or sugar) and file_build(traffic_path) != build:
             mismatch.append(f"{os.path.relpath(traffic_path, ROOT)} (build {file_build(traffic_path)})")
-        if pairs is not None and pairs.get("build_id") != build:
+        # (pair counts come from the diagnostic build of the same sources: its id carries a "-diag" suffix)
+        if pairs is not None and pairs.get("build_id") not in (build, build + "-diag"):
             mismatch.append(f"{os.path.relpath(args.pairs, ROOT)} (build {pairs.get('build_id')})")
             pairs = None
     n_fw = max(1, len(Ks))
@@ -581,6 +583,36 @@ def check_world(gpus, world):
                          f"(python bench.py --gpus {gpus}, or torch.distributed.run --nproc-per-node {gpus})")
 
 
+def config_fields(args, world, per, comm, K_mean, L_mean, chunked_reduce):
+    """The bench line's `config`: the workload (naming only the collectives that run: none at N = 1), the
+    parallelism, and the collective backend / world size as torch.distributed reports them (comm_backend None
+    without a process group), so a multi-rank run shows that RCCL saw N ranks."""
+    cfg = {
+        "workload": ("C5: ~2M surface-aligned SuGaR Gaussians (icosphere, 6 per face), 800x800, SH3, SuGaR "
+                     "normal renderer (2 passes + normal-from-depth) over a 64-view orbit batch, fwd+bwd"
+                     if args.workload == "sugar" else
+                     ("C3 per view (1M Gaussians, 1024x1024, SH3, background path)" if args.epilogue ==
+                      "background" else "1M Gaussians, 1024x1024, SH3, MVDream shading path (depth-normal, "
+                      "point-light material, composite)") + f" over the C4 {args.views}-view orbit batch, fwd+bwd "
+                     "(fixed random upstream image gradients)")
+                    + (" + image all-gather + gradient all-reduce" if world > 1 else ""),
+        "n_gaussians": args.gaussians, "resolution": [args.res, args.res], "sh_degree": args.sh_degree,
+        "global_views_per_step": args.views, "views_per_rank": per,
+        "parallelism": (f"views sharded over {world} rank(s) ({comm} all-gather of the images" + (
+            " overlapped with the backward, " if args.gather == "overlap" else " before the backward, ") + (
+            f"all-reduce of the Gaussian gradients in {args.grad_chunks} ranges overlapped with the "
+            "per-Gaussian backward)" if chunked_reduce else "in-place all-reduce of the Gaussian "
+            "gradients)") if world > 1 else "1 rank, no collectives"),
+        "mean_instances_K": round(K_mean),
+        "mean_listed_instances": round(L_mean),
+        "path": args.path,
+        "epilogue": "sugar_normal (normal-from-depth, 2 passes)" if args.workload == "sugar" else args.epilogue,
+    }
+    cfg["comm_backend"] = dist.get_backend() if dist.is_initialized() else None
+    cfg["comm_world_size"] = dist.get_world_size() if dist.is_initialized() else 1
+    return cfg
+
+
 def run_workload(args, world, rank, device, comm, headline=True):
     """Build the workload of `args`, run W warm-up and K timed steps (barrier + synchronize on both sides, max
     over ranks) and return (result dict on rank 0 else None, scene).  headline: also the per-view-path and
@@ -631,7 +663,6 @@ def run_workload(args, world, rank, device, comm, headline=True):
     shade = None
     up_n = None
     if args.epilogue == "shading" or args.workload == "sugar":
-        sys.path.insert(0, os.path.join(ROOT, "tests"))  # per-view path: the reference's torch epilogue
         shade = shading_inputs(mine, device)
         up_n = torch.randn((len(mine), 3, H, W), generator=gen, device=device)
 
@@ -756,25 +787,7 @@ def run_workload(args, world, rank, device, comm, headline=True):
         "vs_baseline": None,
         "dtype": "fp32",
         "data": "synthetic (seeded scene per SURVEY.md §8d; no datasets offline)",
-        "config": {
-            "workload": "C5: ~2M surface-aligned SuGaR Gaussians (icosphere, 6 per face), 800x800, SH3, SuGaR "
-                        "normal renderer (2 passes + normal-from-depth) over a 64-view orbit batch, fwd+bwd" if args.workload == "sugar" else
-                        ("C3 per view (1M Gaussians, 1024x1024, SH3, background path)" if args.epilogue ==
-                         "background" else "1M Gaussians, 1024x1024, SH3, MVDream shading path (depth-normal, "
-                         "point-light material, composite)") + f" over the C4 {args.views}-view orbit batch, fwd+bwd "
-                        "(fixed random upstream image gradients) + image all-gather + gradient all-reduce",
-            "n_gaussians": args.gaussians, "resolution": [H, W], "sh_degree": args.sh_degree,
-            "global_views_per_step": args.views, "views_per_rank": per,
-            "parallelism": (f"views sharded over {world} rank(s) ({comm} all-gather of the images" + (
-                " overlapped with the backward, " if args.gather == "overlap" else " before the backward, ") + (
-                f"all-reduce of the Gaussian gradients in {args.grad_chunks} ranges overlapped with the "
-                "per-Gaussian backward)" if GRAD_REDUCE is not None else "in-place all-reduce of the Gaussian "
-                "gradients)") if world > 1 else "1 rank, no collectives"),
-            "mean_instances_K": round(K_mean),
-            "mean_listed_instances": round(L_mean),
-            "path": args.path,
-            "epilogue": "sugar_normal (normal-from-depth, 2 passes)" if args.workload == "sugar" else args.epilogue,
-        },
+        "config": config_fields(args, world, per, comm, K_mean, L_mean, GRAD_REDUCE is not None),
     }
     if world > 1:
         res["config"]["gather"] = args.gather

@@ -402,6 +402,18 @@ size_t gsr_knn_workspace_bytes(int P);
 int gsr_knn_mean_dist(int P, const float* points, float* mean_dist, void* workspace, size_t workspace_bytes,
                       void* stream);
 
+/*
+ * The view-segmented stable LSD radix sort that every sort of this library runs (the depth sort, the tile sort and
+ * distCUDA2's Morton sort: csrc/gsr_sort.hip; it replaces the reference extension's cub::DeviceRadixSort::SortPairs
+ * calls of one view at a time).  Exposed for tests: V (1..64) segments of n[v] (key, value) pairs laid
+ * out back to back in keys / vals (device), each sorted in place by the key's low key_bits (1..32) bits, stably
+ * (equal keys keep their order), in passes of at most max_bits (1..8) bits.  vals may be NULL (keys only).
+ * work: gsr_sort_work_bytes(V, n) bytes of device memory.
+ */
+size_t gsr_sort_work_bytes(int V, const int* n);
+int gsr_sort_pairs(int V, const int* n, uint32_t* keys, uint32_t* vals, int key_bits, int max_bits, void* work,
+                   size_t work_bytes, void* stream);
+
 /* Replaces markVisible/checkFrustum (API completeness; unused by the reference).  present (P,) u8. */
 int gsr_mark_visible(int P, const float* means3D, const float* viewmatrix, const float* projmatrix,
                      uint8_t* present, void* stream);

@@ -134,3 +134,51 @@ def test_counters_of_another_build_are_dropped(tmp_path):
         else:
             assert r["roofline"]["traffic"] is None and "valu" not in r["roofline"]
             assert "another build" in r["counters_note"] and "b1" in r["counters_note"]
+
+
+def test_config_names_only_the_collectives_that_run(monkeypatch):
+    """VERDICT r05 item 7: at N = 1 the workload names no all-gather / all-reduce and the parallelism says so;
+    comm_backend / comm_world_size are what torch.distributed reports (None / 1 without a process group, the
+    group's backend and size with one — a world-1 gloo group here, RCCL's 'nccl' on the GPU node)."""
+    import torch.distributed as dist
+
+    a = _args()
+    c1 = bench.config_fields(a, 1, 64, "none", 6.6e6, 4.95e6, False)
+    assert "all-gather" not in c1["workload"] and "all-reduce" not in c1["workload"]
+    assert c1["parallelism"] == "1 rank, no collectives"
+    assert c1["comm_backend"] is None and c1["comm_world_size"] == 1
+    c8 = bench.config_fields(a, 8, 8, "RCCL", 6.6e6, 4.95e6, True)
+    assert "all-gather" in c8["workload"] and "RCCL all-gather" in c8["parallelism"]
+    monkeypatch.setenv("MASTER_ADDR", "127.0.0.1")
+    monkeypatch.setenv("MASTER_PORT", str(bench._free_port()))
+    dist.init_process_group("gloo", rank=0, world_size=1)
+    try:
+        cg = bench.config_fields(a, 1, 64, "gloo", 6.6e6, 4.95e6, False)
+        assert cg["comm_backend"] == "gloo" and cg["comm_world_size"] == 1
+    finally:
+        dist.destroy_process_group()
+
+
+def test_product_timing_imports_no_test_code():
+    """the per-view shading leg runs the product's shading kernels (shading.shade_views), not
+    the tests' torch restatement; only the CPU baseline imports the oracle (test infrastructure, as the checker)."""
+    src = open(os.path.join(ROOT, "bench.py")).read()
+    assert "torch_reference" not in src and '"tests"' not in src
+    assert src.count("import oracle") == 1
+
+
+def test_pairs_of_the_diag_build_of_the_same_sources_are_used(tmp_path):
+    """the diagnostic library's id is the product's id + "-diag" (csrc/Makefile); its pair counts are
+    accepted for the product of the same sources, another build's are not."""
+    import json
+
+    a0 = _args()
+    t = json.load(open(a0.traffic))
+    p = json.load(open(a0.pairs))
+    tf, pf = tmp_path / "t.json", tmp_path / "p.json"
+    tf.write_text(json.dumps(dict(t, build_id="b0")))
+    for pid, ok in (("b0-diag", True), ("b1-diag", False)):
+        pf.write_text(json.dumps(dict(p, build_id=pid)))
+        r = bench.roofline_fields(_args("--traffic", str(tf), "--pairs", str(pf)), PHASES, [6.6e6] * 64,
+                                  [4.95e6] * 64, 1024, 1024, build="b0")
+        assert ("pairs_per_launch" in r["roofline"]["valu"]) == ok, pid

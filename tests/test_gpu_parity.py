@@ -322,9 +322,11 @@ def test_forward_kernels_bitwise(kind, switch, monkeypatch, tmp_path):
     layout override is read once per process (the backward derives the buffer layout from it on the host), so
     the forced layouts run in child processes.  Every output — colour, depth, alpha, the composite, the second
     colour set, radii — and every gradient (the backward reads the forward's per-pixel state) must be bitwise
-    equal.  mid_pass: every switch changed between the forward and the backward (a child process
-    sets GSR_TILE_KEYS, GSR_FWD_KERNEL and GSR_BWD_SPLIT after the forward) changes nothing: the backward
-    follows the forward's recorded decisions and the once-per-process layout latch."""
+    equal.  mid_pass: every switch changed between the forward and the backward to a value
+    that differs from what the forward ran with (a child process sets GSR_TILE_KEYS=plain, GSR_FWD_KERNEL=tile
+    and GSR_BWD_SPLIT=0 after a default forward: 3 views of 143 tiles take the quadrant-wave forward and split
+    their backward) changes nothing: the backward follows the forward's recorded decisions on the device and
+    the once-per-process layout latch."""
     if switch == "fwd_kernel":
         _assert_bitwise(bitwise_case(kind, monkeypatch, "tile"), bitwise_case(kind, monkeypatch, "quadrant"),
                         "tile-wave vs quadrant-wave forward")
@@ -338,7 +340,7 @@ def test_forward_kernels_bitwise(kind, switch, monkeypatch, tmp_path):
         out = tmp_path / "mid.npz"
         code = ("import os, numpy as np, test_gpu_parity as t\n"
                 "def flip():\n"
-                "    os.environ.update(GSR_TILE_KEYS='plain', GSR_FWD_KERNEL='quadrant', GSR_BWD_SPLIT='1')\n"
+                "    os.environ.update(GSR_TILE_KEYS='plain', GSR_FWD_KERNEL='tile', GSR_BWD_SPLIT='0')\n"
                 "np.savez(%r, *t.bitwise_case(%r, between=flip))\n" % (str(out), kind))
         env = dict(os.environ, PYTHONPATH=os.pathsep.join(p for p in sys.path if p))
         for k in ("GSR_TILE_KEYS", "GSR_FWD_KERNEL", "GSR_BWD_SPLIT"):

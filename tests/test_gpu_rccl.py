@@ -4,7 +4,8 @@
 background renderer through the batch renderer twice — with the gradient all-reduce inside the rasterizer's
 backward (view_shard.ChunkedGradReduce: per-range events, a side stream, grouped RCCL all-reduces) and with
 view_shard.allreduce_grads afterwards (one in-place flat RCCL all-reduce) — plus the synchronous and the
-asynchronous image all-gather (all_gather_into_tensor).  At world size 1 every collective is an identity, so
+asynchronous image all-gather (all_gather_into_tensor), with view_shard.COLLECTIVES_AT_WORLD_ONE set (by default a
+world-1 group skips the collectives).  At world size 1 every collective is an identity, so
 images, gradients and the gathered batches must be bitwise those of the same step without a process group.
 Multi-rank RCCL (xGMI) stays for the driver's 8-GPU run; the multi-rank logic is covered by the gloo tests.
 
@@ -33,6 +34,7 @@ dist.init_process_group("nccl", device_id=torch.device("cuda", 0))  # before any
 assert dist.get_backend() == "nccl" and dist.get_world_size() == 1
 import test_gpu_batch_renderer as t
 from diff_gaussian_rasterization import view_shard
+view_shard.COLLECTIVES_AT_WORLD_ONE = True  # run the RCCL path although the world has one rank
 
 out = sys.argv[1]
 torch.manual_seed(100)

@@ -404,3 +404,26 @@ def test_async_gather_equals_sync(world, batch, tmp_path):
     for r in range(world):
         np.testing.assert_array_equal(np.load(tmp_path / f"async{r}.npy"), want)
         np.testing.assert_array_equal(np.load(tmp_path / f"sync{r}.npy"), want)
+
+
+def test_world_one_group_skips_collectives_unless_opted_in(tmp_path):
+    """a world-size-1 process group (a single-GPU run under a launcher) issues no collectives by
+    default — the gather returns the local slice itself and the chunked reduction is inactive; with
+    view_shard.COLLECTIVES_AT_WORLD_ONE (the one-GPU RCCL test) the same calls run the collectives, as identities."""
+    from diff_gaussian_rasterization import view_shard
+
+    dist.init_process_group("gloo", init_method="file://" + os.path.join(str(tmp_path), "rdv_w1"), rank=0,
+                            world_size=1)
+    try:
+        x = torch.randn(3, 2, 4, requires_grad=True)
+        assert view_shard.all_gather_views(x, 3) is x
+        assert not view_shard.ChunkedGradReduce(n_chunks=2).active()
+        view_shard.COLLECTIVES_AT_WORLD_ONE = True
+        try:
+            g = view_shard.all_gather_views(x, 3)
+            assert g is not x and torch.equal(g, x.detach()) and g.grad_fn is not None
+            assert view_shard.ChunkedGradReduce(n_chunks=2).active()
+        finally:
+            view_shard.COLLECTIVES_AT_WORLD_ONE = False
+    finally:
+        dist.destroy_process_group()

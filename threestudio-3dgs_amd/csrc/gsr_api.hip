@@ -476,6 +476,56 @@ int gsr_knn_mean_dist(int P, const float* points, float* mean_dist, void* worksp
   return last_launch();
 }
 
+// ---- the view-segmented radix sort (tests: every sort of the library runs seg_sort) -----------------
+struct SortWork {
+  uint32_t *keys2, *vals2, *counts, *totals;
+  static SortWork carve(void* base, int V, long long total, uint32_t blocks, size_t* bytes) {
+    Carver c(base);
+    SortWork w;
+    w.keys2 = c.take<uint32_t>((size_t)(total > 0 ? total : 1));
+    w.vals2 = c.take<uint32_t>((size_t)(total > 0 ? total : 1));
+    w.counts = c.take<uint32_t>((size_t)GSR_RADIX * (blocks > 0 ? blocks : 1));
+    w.totals = c.take<uint32_t>((size_t)GSR_RADIX * (size_t)V);
+    if (bytes) *bytes = align_up(c.off, 256);
+    return w;
+  }
+};
+
+size_t gsr_sort_work_bytes(int V, const int* n) {
+  SegInfo seg;
+  long long total = 0;
+  if (V < 1 || V > GSR_SET_MAX || n == nullptr || inst_segments(V, n, seg, &total) != GSR_OK) return 0;
+  size_t b = 0;
+  SortWork::carve(nullptr, V, total, seg.blk[V], &b);
+  return b;
+}
+
+int gsr_sort_pairs(int V, const int* n, uint32_t* keys, uint32_t* vals, int key_bits, int max_bits, void* work,
+                   size_t work_bytes, void* stream) {
+  if (V < 1 || V > GSR_SET_MAX) return fail(GSR_EINVAL, "%s", "1..64 segments");
+  if (n == nullptr || keys == nullptr || work == nullptr) return fail(GSR_EINVAL, "%s", "null pointer argument");
+  if (key_bits < 1 || key_bits > 32 || max_bits < 1 || max_bits > GSR_RADIX_BITS)
+    return fail(GSR_EINVAL, "%s", "key_bits must be 1..32 and max_bits 1..8");
+  SegInfo seg;
+  long long total = 0;
+  if (inst_segments(V, n, seg, &total) != GSR_OK) return GSR_EINVAL;
+  size_t need = 0;
+  SortWork w = SortWork::carve(work, V, total, seg.blk[V], &need);
+  if (work_bytes < need) return fail(GSR_EINVAL, "%s", "sort work buffer too small");
+  if (total == 0) return last_launch();
+  hipStream_t s = (hipStream_t)stream;
+  uint32_t* kk[2] = {keys, w.keys2};
+  uint32_t* vv[2] = {vals, vals != nullptr ? w.vals2 : nullptr};
+  const int r = seg_sort(kk, vals != nullptr ? vv : nullptr, false, seg, 0, key_bits, w.counts, w.totals, s,
+                         max_bits);
+  if (r == 1) {  // (an odd number of passes: the result is in the work buffer)
+    GSR_HIP_CHECK(hipMemcpyAsync(keys, w.keys2, sizeof(uint32_t) * (size_t)total, hipMemcpyDeviceToDevice, s));
+    if (vals != nullptr)
+      GSR_HIP_CHECK(hipMemcpyAsync(vals, w.vals2, sizeof(uint32_t) * (size_t)total, hipMemcpyDeviceToDevice, s));
+  }
+  return last_launch();
+}
+
 int gsr_set_num_rendered_ex(int V, const void* geom, int P, int* num_rendered, int* num_visible, int* num_listed,
                             void* stream) {
   if (check_set(V, P) != GSR_OK) return GSR_EINVAL;
@@ -697,11 +747,11 @@ static int set_backward(int V, int P, int degree, int M, const int* K, int width
     rs.out_col2 = nullptr;
     rs.dpix2 = two ? dL_dcolor2 + (size_t)g0 * 3 * HW : nullptr;
     rs.order = img.order;
-    // a one-colour backward of the first colour replays split chunks when the forward wrote them: the host repeats
-    // the forward's decision (split_forward, so no extra workgroups are launched for a forward that did not split)
-    // and the kernels follow the decision the forward recorded on the device (split_mode), whatever this call's
-    // environment says
-    rs.ckpt = split_forward(V, P, width, height, total, two) && colors_override == nullptr ? img.ckpt : nullptr;
+    // a one-colour backward of the first colour replays split chunks when the forward wrote them.  The host passes
+    // the checkpoints whenever the set's size allows a split (split_fits, no environment read here: ADVICE r05) and
+    // the kernels follow the decision the forward recorded on the device (split_mode): the extra workgroups of a
+    // forward that did not split return at once, and the checkpoints are read only after one that did
+    rs.ckpt = !two && colors_override == nullptr && split_fits(V, (size_t)gx * gy) ? img.ckpt : nullptr;
     rs.split_mode = img.split_mode;
     rs.split_items = img.split_items;
     rs.split_cap = img.split_cap;

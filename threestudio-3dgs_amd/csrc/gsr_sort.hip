@@ -160,9 +160,12 @@ __global__ __launch_bounds__(GSR_SORT_THREADS) void k_seg_scatter(
       const uint32_t d = (seg_key(kb, key[k]) >> shift) & mask;
       const unsigned long long peers = match_digit(d, bits, valid);
       const uint32_t rank = mask_rank(peers);
-      // every lane reads its digit's running count, then the digit's first lane advances it (one wave's LDS
-      // accesses complete in order, so the read sees the count before this round's add: no broadcast needed)
+      // every lane reads its digit's running count, then the digit's first lane advances it.  The order across lanes
+      // is explicit: the compiler barrier keeps the wave's ds_read before its ds_write in the program,
+      // and the write's data is the read's result, so the wave issues the write only after the read has returned —
+      // every lane's read sees the count before this round's add (no broadcast of the leader's value needed)
       const uint32_t base = s.wcnt[w][d];
+      asm volatile("" ::: "memory");
       if (valid && rank == 0) s.wcnt[w][d] = base + (uint32_t)__popcll(peers);
       const uint32_t pk = base + rank;
       pos2[k >> 1] = (k & 1) ? (pos2[k >> 1] | (pk << 16)) : pk;

@@ -62,6 +62,8 @@ SIGNATURES = {
                                 + [ctypes.POINTER(_f)] * 2 + [_vp] * 4 + [_vp]),
     "gsr_shade_views_backward": (_i, [_i, _i, _i, _i, ctypes.POINTER(_i)] + [_vp] * 6 + [_i] + [_vp] * 2
                                  + [ctypes.POINTER(_f)] * 2 + [_vp] * 8 + [_vp]),
+    "gsr_sort_work_bytes": (_sz, [_i, ctypes.POINTER(_i)]),
+    "gsr_sort_pairs": (_i, [_i, ctypes.POINTER(_i), _vp, _vp, _i, _i, _vp, _sz, _vp]),
     "gsr_knn_workspace_bytes": (_sz, [_i]),
     "gsr_knn_mean_dist": (_i, [_i, _vp, _vp, _vp, _sz, _vp]),
     "gsr_set_geom_bytes": (_sz, [_i, _i]),

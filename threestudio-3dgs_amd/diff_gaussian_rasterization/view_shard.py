@@ -36,11 +36,18 @@ def _world():
     return 1, 0
 
 
+# Opt-in: issue the collectives also in a world-size-1 process group, where they are identities — the
+# one-GPU run of the RCCL path (tests/test_gpu_rccl.py sets it).  Off by default, so a single-GPU run under a
+# launcher that opens a process group pays for no per-range events, side-stream reductions or gather copies.
+COLLECTIVES_AT_WORLD_ONE = False
+
+
 def _collect() -> bool:
-    """The view gather and the gradient reductions issue their collectives whenever a process group exists —
-    also at world size 1, where they are identities (a one-GPU run of the RCCL path: tests/test_gpu_rccl.py);
-    without one they are skipped."""
-    return dist.is_available() and dist.is_initialized()
+    """The view gather and the gradient reductions issue their collectives when a process group of more than one
+    rank exists (or of one rank with COLLECTIVES_AT_WORLD_ONE); otherwise they are skipped."""
+    if not (dist.is_available() and dist.is_initialized()):
+        return False
+    return dist.get_world_size() > 1 or COLLECTIVES_AT_WORLD_ONE
 
 
 def shard_range(batch_size: int, world: int, rank: int):
