@@ -41,9 +41,11 @@ import torch.distributed as dist  # noqa: E402
 
 METRIC = "rendered views/sec fwd+bwd @1M Gaussians, 1024², SH=3; 1/2/4/8 GPU"
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md chip table)
-# VALU issue peak: 256 CUs x 4 SIMDs x 2.4 GHz, one wave64 instruction per SIMD every 2 cycles
-# (MI355X_MICROARCH.md: "issues each VALU instruction over 2 cycles") = 157.3 TFLOP/s fp32 as FMAs
-VALU_PEAK_INSTS = 256 * 4 * 2.4e9 / 2
+# VALU issue peak: 256 CUs x 4 SIMDs x 2.4 GHz, one wave64 fp32 instruction per SIMD every 4 cycles (MI355X_MICROARCH.md,
+# measured issue cost of one wave's stream on one SIMD: v_fma_f32 / v_add_f32 4 cycles, v_exp_f32 / v_rcp_f32 8; the
+# 157.3 TFLOP/s fp32 peak counts packed v_pk_fma_f32, two lanes' worth per instruction).  Until round 5 this was
+# taken as 2 cycles, which halved every valu_frac.
+VALU_PEAK_INSTS = 256 * 4 * 2.4e9 / 4
 FP32_PEAK_TFLOPS = 157.3
 SH_C0 = 0.28209479177387814
 
@@ -442,8 +444,8 @@ def roofline_fields(args, phases, Ks, Ls, H, W, launched=None, build=None):
                                        instance with plain stores and never performs it — reported as
                                        reference_rmw_bytes, not counted)
     counter_frac = PMC HBM bytes per launch (profiles/<tag>_traffic.json) / duration / 8 TB/s;
-    valu = SQ_INSTS_VALU per launch (profiles/<tag>_traffic.json) against the VALU issue peak (one wave64
-    instruction per SIMD per 2 cycles, 157.3 TF fp32 as FMAs) and the device-counted pairs
+    valu = SQ_INSTS_VALU per launch (profiles/<tag>_traffic.json) against the VALU issue peak (one wave64 fp32
+    instruction per SIMD per 4 cycles, MI355X_MICROARCH.md) and the device-counted pairs
     (profiles/<tag>_pairs.json, diagnostic build): the blends are issue / latency bound, not HBM bound."""
     tiles = math.ceil(W / 16) * math.ceil(H / 16)
     # the committed counters (profiles/run_profiles.sh) are of bench.py's default workload at N = 1: one

@@ -15,14 +15,13 @@ CSRC = os.path.join(ROOT, "threestudio-3dgs_amd", "csrc")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 
 # mangled-name fragment -> VGPRs allowed to spill, each an occupancy choice measured on the GPU and
-# stated at the kernel's attribute: the one-colour tile-wave forward at 6 waves per SIMD spills outside
-# the candidate loop (gsr_render.hip, profiles/r02_fwd_occupancy_ab.txt); the two-colour per-Gaussian
-# backward at 4 waves per SIMD spills outside the row loop (gsr_backward.hip, C5 only)
-# The lockstep backward at 5 waves per SIMD spills one VGPR, stored before and reloaded after its batch loop
-# (the forward masks' prefetch register; measured faster, profiles/r04/blend_loops_ab.txt session r04k).
-# The per-Gaussian backward with SH at 3 waves per SIMD spills 7 VGPRs, stored before and reloaded after its view
-# loop (profiles/r04/gauss_accum_ab.txt).
-ALLOWED_VGPR_SPILL = {"17k_render_fwd_tileILb0E": 3, "11k_view_gradILb1E": 4, "12k_render_bwdE": 1,
+# stated at the kernel's attribute: the two-colour per-Gaussian backward at 4 waves per SIMD spills outside the
+# row loop (gsr_backward.hip, C5 only); the per-Gaussian backward with SH at 3 waves per SIMD spills 7 VGPRs,
+# stored before and reloaded after its view loop (profiles/r04/gauss_accum_ab.txt).  The one-colour tile-wave
+# forward (6 waves per SIMD) and the lockstep backward (5 waves per SIMD) spill nothing since round 6 (their
+# loop-invariant per-lane addresses and uniform constants are formed where used or kept in scalar registers): a
+# spill reload inside their loops would also wait for every memory operation in flight.
+ALLOWED_VGPR_SPILL = {"17k_render_fwd_tileILb0E": 0, "11k_view_gradILb1E": 4, "12k_render_bwdE": 0,
                       "13k_gauss_accum": 7}
 
 

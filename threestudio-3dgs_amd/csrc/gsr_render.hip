@@ -278,9 +278,6 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(GSR_FWD_WPE,
     }
     bool keep = false;
     if (i < n) keep = qkeys ? kc : quadrant_hit(r0, r1, (float)qx0, (float)qy0);
-    // the backward's cull (RenderSet::qbytes, layout 2: byte 4 i + q of the set's listed instance i; batches past
-    // the quadrant's termination are never walked, and the backward reads only below its deepest blend)
-    if (rs.qbytes != nullptr && i < n) rs.qbytes[4 * ((size_t)rs.inst_start[v] + range.x + i) + q] = keep ? 1u : 0u;
     const unsigned long long bal = __ballot(keep);
     const int cnt = __popcll(bal);
     if (keep) {
@@ -296,6 +293,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(GSR_FWD_WPE,
     // one blend step: candidate k from the register set `cur`, the next staged record into `nxt` (the loop runs
     // the step twice with the sets swapped: no register copies); done / ok / term / blend as uniform lane masks
     int k = 0;
+    unsigned long long hbm = 0ull;  // staged candidates (by position) that blended at least one pixel (uniform)
     auto step = [&](const float4& a, const float4& b, const float4& c, const float4& e, float4& an, float4& bn,
                     float4& cn, float4& en) -> bool {
       if (k >= cnt || ((k & 7) == 0 && dmk == ~0ull)) return false;
@@ -336,6 +334,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(GSR_FWD_WPE,
       T = vsel(blendm, test_T, T);  // = T (1 - a_eff)
       last_contributor = __float_as_uint(vsel(blendm, b.w, __uint_as_float(last_contributor)));
       dmk |= termm;
+      hbm |= blendm != 0ull ? 1ull << k : 0ull;
       ++k;
       return true;
     };
@@ -345,6 +344,12 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(GSR_FWD_WPE,
       while (step(pa, pb, pc, pd, ya, yb, yc, yd) && step(ya, yb, yc, yd, pa, pb, pc, pd)) {
       }
     }
+    // the backward's exact cull (RenderSet::qbytes, layout 2: byte 4 i + q of the set's listed instance i): whether
+    // candidate i blended any pixel of this quadrant (a pair the forward blended nowhere has no backward hit: same
+    // alpha, power and position tests).  Batches past the quadrant's termination are never walked, and the backward
+    // reads only below its deepest blend.
+    if (rs.qbytes != nullptr && i < n)
+      rs.qbytes[4 * ((size_t)rs.inst_start[v] + range.x + i) + q] = keep && ((hbm >> mask_rank(bal)) & 1ull) ? 1u : 0u;
     __syncthreads();
   }
   if (inside) {
@@ -458,6 +463,10 @@ __global__ __launch_bounds__(256) void k_tile_info(RenderSet rs, const uint2* __
 // of pixels p and p + 16 do not conflict) and every 16-B read stays conflict-free (offsets of 16 dwords only
 // rotate a read group's banks); 16 floats of padding in all (a pad per group would cost the 5th workgroup per CU:
 // LDS is allocated in 1280-byte granules, 5 x 25 of 128 per CU)
+// One wave's LDS accesses are performed in program order (the DS unit takes a wave's instructions in issue order),
+// so a wave reading what its own lanes just wrote needs no s_waitcnt — only that the compiler keep the accesses in
+// program order (a memory clobber): the wave keeps issuing while the writes drain.
+#define GSR_WAVE_LDS_ORDER() asm volatile("" ::: "memory")
 __device__ __forceinline__ int gsr_uw_pg(int g) { return 256 * (g >> 1) + ((g & 1) ? 528 : 0); }
 #define GSR_HCAP2 160
 // (LDS is allocated in 1280-byte granules: 5 workgroups of the backward per CU need <= 25 of the 128)
@@ -465,6 +474,7 @@ __device__ __forceinline__ int gsr_uw_pg(int g) { return 256 * (g >> 1) + ((g & 
 struct BwdLDS {
   float4 s0[65], s1[65], s2[65];
   uint32_t slot[64];
+  uint32_t gidx[64];     // the staged candidates' Gaussians (their reach bits are set after the cull)
   uint32_t list[4][64];  // per wave: the batch indices of its kept candidates
   float qsum[64 * GSR_QSUM_STRIDE];
   // per wave: the group's A operand, u = G dL/dalpha (slots 0-7) and w = alpha T (slots 8-15) of
@@ -593,85 +603,78 @@ __global__ __launch_bounds__(64) void k_render_fwd_tile(RenderSet rs, const uint
     s1[lane] = make_float4(GSR_CONIC_K_AC * r0.z, r1.y, r1.z, __uint_as_float((uint32_t)(i + 1)));
     s2[lane] = make_float4(r2.x, r2.y, r2.z, r1.z);
     if (C2) s3[lane] = r3;
-    if (qbytes != nullptr && i < n) qbytes[i] = (uint8_t)m;  // (the backward's cull; batches past the last
-                                                             // blend are never read by it)
-    // per quadrant the batch's candidates whose mask has it (uniform, in scalar registers): the walk visits
-    // the set bits of their union in order, reading each quadrant's bit with scalar ops and the next
-    // candidate's staged record while the current one blends (no per-candidate LDS read of its mask)
+    // per quadrant the batch's candidates whose mask has it (uniform, in scalar registers)
     unsigned long long qb[4];
 #pragma unroll
     for (int q = 0; q < 4; ++q) qb[q] = (qactive >> q) & 1u ? __ballot((m >> q) & 1u) : 0ull;
     __syncthreads();
-    auto live = [&]() { return (qb[0] | qb[1]) | (qb[2] | qb[3]); };
-    unsigned long long rest = live();
-    int k = rest != 0ull ? (int)__builtin_ctzll(rest) : 0;
-    int walked = 0;
-    // one step: candidate k from the register set `cur`, the next candidate's staged record into `nxt` (the step
-    // runs twice per loop iteration with the sets swapped: no register copies); false when the walk ends
-    auto step = [&](float4& a, float4& b, float4& c, float4& e, float4& an, float4& bn, float4& cn,
-                    float4& en) -> bool {
-      if (walked > 0 && (walked & 7) == 0) {
-        // (finished quadrants leave the walk: they would blend nothing)
-        qactive = active_mask();
-        if (qactive == 0u) return false;
+    // The quadrants in turn, each walking its own candidates in list order: a pixel lies in one quadrant, so it
+    // sees exactly the candidates, order and operations of the quadrant-wave kernel (bitwise), and a step is one
+    // (candidate, quadrant) pair with no per-candidate quadrant tests (the union walk branched on four mask bits
+    // per candidate: as many scalar as vector instructions, r05 SQ counters).  The next candidate's staged record
+    // is read while the current one blends; a finished quadrant stops its walk (its lanes would blend nothing).
+    // per quadrant the batch's candidates that blended at least one of its pixels (uniform): the backward's exact
+    // cull (a (candidate, quadrant) pair the forward blended nowhere has no backward hit either: same alpha, power
+    // and list-position tests, and a pixel's hits are exactly its blends before its last contributor)
+    unsigned long long hb[4] = {0ull, 0ull, 0ull, 0ull};
 #pragma unroll
-        for (int q = 0; q < 4; ++q)
-          if (!((qactive >> q) & 1u)) qb[q] = 0ull;
-        rest &= live();
-        if (rest == 0ull) return false;
-        const int kk = (int)__builtin_ctzll(rest);
-        if (kk != k) {
-          k = kk;
-          a = s0[k], b = s1[k], c = s2[k];
-          e = C2 ? s3[k] : zero4;
-        }
-      }
-      ++walked;
-      rest &= rest - 1ull;
-      const int kn = rest != 0ull ? (int)__builtin_ctzll(rest) : k;
-      an = s0[kn], bn = s1[kn], cn = s2[kn];
-      en = C2 ? s3[kn] : zero4;
-#if GSR_FWD_PREFETCH
-      asm volatile("" ::: "memory");  // (read ahead of this step's blends, as in k_render_fwd)
-#endif
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        if ((qb[q] >> k) & 1ull) {
+    for (int q = 0; q < 4; ++q) {
+      unsigned long long rest = qb[q];
+      if (rest == 0ull) continue;
+      int k = (int)__builtin_ctzll(rest);
+      // one step: candidate k from the register set `cur`, the next candidate's staged record into `nxt` (the step
+      // runs twice per loop iteration with the sets swapped: no register copies); false when the walk ends.  The
+      // bookkeeping is scalar and as short as it goes: k's bit cleared by one xor with the bit the exact mask also
+      // records, the next index by one find-first over rest with bit 63 forced (63 when rest is empty: a valid
+      // staged slot, read but never blended)
+      auto step = [&](float4& a, float4& b, float4& c, float4& e, float4& an, float4& bn, float4& cn,
+                      float4& en) -> bool {
+        const unsigned long long kbit = 1ull << k;
+        rest ^= kbit;
+        const int kn = (int)__builtin_ctzll(rest | (1ull << 63));
+        an = s0[kn], bn = s1[kn], cn = s2[kn];
+        en = C2 ? s3[kn] : zero4;
+        // (the next record's reads issued before any of this step's arithmetic: a whole step to arrive)
+        __builtin_amdgcn_sched_barrier(0);
 #ifdef GSR_TIMELINE
-          pc_eval += (dm[q] >> lane) & 1ull ? 0ull : 1ull;
-          pc_slot += 1ull;
+        pc_eval += (dm[q] >> lane) & 1ull ? 0ull : 1ull;
+        pc_slot += 1ull;
 #endif
-          const float dx = a.x - pxy[q].x, dy = a.y - pxy[q].y;
-          const float power2 = fmaf(dx, fmaf(b.x, dx, a.z * dy), (a.w * dy) * dy);  // log2(e) * power
-          const float alpha = fminf(GSR_ALPHA_MAX, b.y * __builtin_amdgcn_exp2f(power2));
-          const unsigned long long okm = (__ballot(power2 <= 0.0f) & __ballot(alpha >= GSR_ALPHA_MIN)) & ~dm[q];
-          const float test_T = T[q] * (1.0f - alpha);
-          const unsigned long long termm = okm & __ballot(test_T < GSR_T_EPS);
-          const unsigned long long blendm = okm & ~termm;
-          const float a_eff = vsel(blendm, alpha, 0.0f);
-          const float aT = a_eff * T[q];
-          const f2 aT2 = {aT, aT};
-          CrCg[q] = __builtin_elementwise_fma(f2{c.x, c.y}, aT2, CrCg[q]);
-          CbD[q] = __builtin_elementwise_fma(f2{c.z, c.w}, aT2, CbD[q]);
-          if (C2) {
-            ErEg[q] = __builtin_elementwise_fma(f2{e.x, e.y}, aT2, ErEg[q]);
-            Eb[q] = fmaf(e.z, aT, Eb[q]);
-          }
-          T[q] = vsel(blendm, test_T, T[q]);
-          last[q] = __float_as_uint(vsel(blendm, b.w, __uint_as_float(last[q])));
-          dm[q] |= termm;
+        const float dx = a.x - pxy[q].x, dy = a.y - pxy[q].y;
+        const float power2 = fmaf(dx, fmaf(b.x, dx, a.z * dy), (a.w * dy) * dy);  // log2(e) * power
+        const float alpha = fminf(GSR_ALPHA_MAX, b.y * __builtin_amdgcn_exp2f(power2));
+        const unsigned long long okm = (__ballot(power2 <= 0.0f) & __ballot(alpha >= GSR_ALPHA_MIN)) & ~dm[q];
+        const float test_T = T[q] * (1.0f - alpha);
+        const unsigned long long termm = okm & __ballot(test_T < GSR_T_EPS);
+        const unsigned long long blendm = okm & ~termm;
+        const float a_eff = vsel(blendm, alpha, 0.0f);
+        const float aT = a_eff * T[q];
+        const f2 aT2 = {aT, aT};
+        CrCg[q] = __builtin_elementwise_fma(f2{c.x, c.y}, aT2, CrCg[q]);
+        CbD[q] = __builtin_elementwise_fma(f2{c.z, c.w}, aT2, CbD[q]);
+        if (C2) {
+          ErEg[q] = __builtin_elementwise_fma(f2{e.x, e.y}, aT2, ErEg[q]);
+          Eb[q] = fmaf(e.z, aT, Eb[q]);
         }
-      }
-      k = kn;
-      return rest != 0ull;
-    };
-    if (rest != 0ull) {
+        T[q] = vsel(blendm, test_T, T[q]);
+        last[q] = __float_as_uint(vsel(blendm, b.w, __uint_as_float(last[q])));
+        dm[q] |= termm;
+        hb[q] |= blendm != 0ull ? kbit : 0ull;
+        k = kn;
+        return rest != 0ull;
+      };
       float4 pa = s0[k], pb = s1[k], pc = s2[k];
       float4 pd = C2 ? s3[k] : zero4;
       float4 ya, yb, yc, yd;
-      while (step(pa, pb, pc, pd, ya, yb, yc, yd) && step(ya, yb, yc, yd, pa, pb, pc, pd)) {
+      // (a finished quadrant stops its walk, tested every second step: its lanes would blend nothing)
+      while (dm[q] != ~0ull && step(pa, pb, pc, pd, ya, yb, yc, yd) && step(ya, yb, yc, yd, pa, pb, pc, pd)) {
       }
     }
+    // the backward's cull of this batch: candidate i's 4-bit mask of quadrants it blended in (batches past the last
+    // blend are never read by it)
+    if (qbytes != nullptr && i < n)
+      qbytes[i] = (uint8_t)(((hb[0] >> lane) & 1ull) | (((hb[1] >> lane) & 1ull) << 1) |
+                            (((hb[2] >> lane) & 1ull) << 2) | (((hb[3] >> lane) & 1ull) << 3));
     __syncthreads();
     qactive = active_mask();
   }
@@ -975,6 +978,7 @@ __device__ __forceinline__ void bwd_tile(BwdLDS& s, const RenderSet& rs, int v, 
   // normal-from-depth loss) and lose its significant bits.
   float S = 0.f, Sd = 0.f;
   const float nbg = -T_final * bg_dot;
+  const f2 pxy = {pxf, pyf};
   if (split && hi < maxc && qmaxc > hi) {
     // A chunk that ends before the quadrant's deepest blend starts from the forward's state at candidate
     // hi: T there, and the colour / alpha / depth blended behind it over T (the reference's accum_rec
@@ -989,7 +993,8 @@ __device__ __forceinline__ void bwd_tile(BwdLDS& s, const RenderSet& rs, int v, 
     S = (br * dpix[0] + bgc * dpix[1] + bb * dpix[2]) * inv + (1.0f - T_final * inv) * dpix_a;
     Sd = bd * inv;
   }
-  const float ddelx_dx = 0.5f * W, ddely_dy = 0.5f * H;
+  // (uniform: kept in scalar registers, not in vector registers the loop would spill)
+  const float ddelx_dx = sgpr_f(0.5f * W), ddely_dy = sgpr_f(0.5f * H);
   const float4 zero4 = make_float4(0.f, 0.f, 0.f, 0.f);
 
   // All 256 threads stage the batches: thread t moves 16-byte piece (t & 3) of candidate t >> 2's
@@ -997,14 +1002,20 @@ __device__ __forceinline__ void bwd_tile(BwdLDS& s, const RenderSet& rs, int v, 
   // ahead, record pieces one ahead.
   const uint32_t gmask = rs.gmask;
   const int cs = t >> 2, piece = t & 3;
-  auto fetch_index = [&](int h) -> uint32_t {
+  // the list entry (packed keys: the Gaussian index in the low bits) — masked where it is used, not where it is
+  // loaded: a use right after the load made the wave wait for every memory operation in flight (the batch's
+  // record gathers included) before the staging barrier
+  auto fetch_raw = [&](int h) -> uint32_t {
     const int r = h - 1 - cs;
-    return r >= 0 ? (sorted_gauss[range.x + r] & gmask) : 0u;
+    return r >= 0 ? sorted_gauss[range.x + r] : 0u;
   };
-  float4 npc = zero4;  // the next batch's piece (piece 3 also carries the Gaussian's first row slot)
-  uint32_t ngo = 0u;
+  auto fetch_index = [&](int h) -> uint32_t { return fetch_raw(h) & gmask; };
+  float4 npc = zero4;  // the next batch's piece
+  uint32_t ngo = 0u;   // piece 3: the Gaussian's first row slot; piece 2: the Gaussian (staged for the reach bit)
   uint32_t gi_next = 0u;
-  // this view's reach bit (staged candidates have rows): word v >> 5 of the Gaussian's 64 bits
+  // this view's reach bit: word v >> 5 of the Gaussian's 64 bits, set for every candidate some quadrant of the tile
+  // keeps (k_view_grad walks the rows of exactly the reached (view, Gaussian) pairs; the rows of a staged candidate
+  // no quadrant kept are zeros, and a Gaussian no tile kept has only such rows)
   unsigned int* const reach32 = reinterpret_cast<unsigned int*>(reach) + (v >> 5);
   const unsigned int vbit = 1u << (v & 31);
   // the forward's per-instance quadrant cull (ImageState::split_mode[1]): the cull is read, one
@@ -1029,38 +1040,44 @@ __device__ __forceinline__ void bwd_tile(BwdLDS& s, const RenderSet& rs, int v, 
 #endif
       if (piece == 2 && rs.col2 != nullptr)  // the second rasterizer call's colours replace the first's
         npc = make_float4(rs.col2[3 * g0], rs.col2[3 * g0 + 1], rs.col2[3 * g0 + 2], 0.f);
-      if (piece == 3) {
-        ngo = goff[g0];
-#ifndef GSR_EXP_NOREACH
-        atomicOr(reach32 + 2 * g0, vbit);  // the Gaussian gets a row in this view (k_view_grad reads it)
-#endif
-      }
+      if (piece == 2) ngo = g0;
+      if (piece == 3) ngo = goff[g0];
     }
-    if (hi - 64 > lo) gi_next = fetch_index(hi - 64);
+    if (hi - 64 > lo) gi_next = fetch_raw(hi - 64);
   }
 
   // branch-free replay step; non-contributing lanes run it with alpha = 0 (state unchanged) and
   // contribute zeros.  Returns per pixel u = G dL/dalpha (the mean2D / conic / opacity
   // gradients are linear in u's moments over the pixel offsets) and w = alpha T (the colour / depth
   // weights); the sums over the quadrant's 64 pixels are formed by the matrix cores (below).
+  // The replay's running state as packed fp32 pairs (v_pk_mul_f32 / v_pk_fma_f32 issue two lanes' worth at the
+  // cost of one): SS = (S, Sd) and TT = (dL/dalpha of the step, T).  Staged record ga = (x, y, B, C), gb = (A,
+  // opacity, depth, list position), gc = (r, g, b, ·): the pairs (x, y) and (B, C) are adjacent (the forwards'
+  // layout), so the offsets and the exponent's two products are one instruction each.  Every lane's operations
+  // are the scalar ones, in the same order: the same bits.
+  f2 SS = {S, Sd};
+  f2 TT = {0.f, T};
   auto replay = [&](const float4& ga, const float4& gb, const float4& gc, float& u, float& w) {
     const uint32_t rel = __float_as_uint(gb.w);
-    const float dx = ga.x - pxf, dy = ga.y - pyf;
-    const float power2 = gauss_power2(ga.z, ga.w, gb.x, dx, dy);  // log2(e) * power
+    const f2 dd = f2{ga.x, ga.y} - pxy;
+    const f2 bcp = f2{ga.z, ga.w} * f2{dd.y, dd.y};
+    const float power2 = fmaf(dd.x, fmaf(gb.x, dd.x, bcp.x), bcp.y * dd.y);  // gauss_power2: log2(e) * power
     const float G = __builtin_amdgcn_exp2f(power2);
     const float alpha = fminf(GSR_ALPHA_MAX, gb.y * G);
     const bool hit = rel < last_contributor && power2 <= 0.0f && alpha >= GSR_ALPHA_MIN;
-    const float a_eff = hit ? alpha : 0.0f;
-    const float g_eff = hit ? G : 0.0f;
+    const f2 ga2 = {hit ? G : 0.0f, hit ? alpha : 0.0f};  // (G, alpha) of a contributor, zeros otherwise
+    const float a_eff = ga2.y;
     const float oma = 1.f - a_eff;
     const float inv_1ma = fast_rcp(oma);  // 1 for non-contributors
-    T = T * inv_1ma;
+    TT.y = TT.y * inv_1ma;                // T
     const float cd = fmaf(gc.x, dpix[0], fmaf(gc.y, dpix[1], fmaf(gc.z, dpix[2], dpix_a)));
-    const float dL_dalpha = fmaf(T, fmaf(gb.z - Sd, dpix_d, cd - S), inv_1ma * nbg);
-    u = g_eff * dL_dalpha;
-    w = a_eff * T;
-    S = fmaf(a_eff, cd, oma * S);
-    Sd = fmaf(a_eff, gb.z, oma * Sd);
+    TT.x = fmaf(TT.y, fmaf(gb.z - SS.y, dpix_d, cd - SS.x), inv_1ma * nbg);  // dL/dalpha
+    const f2 uw2 = ga2 * TT;  // u = G dL/dalpha, w = alpha T
+    u = uw2.x;
+    w = uw2.y;
+    const f2 om = f2{oma, oma} * SS;
+    SS.x = fmaf(a_eff, cd, om.x);
+    SS.y = fmaf(a_eff, gb.z, om.y);
   };
 
 
@@ -1130,184 +1147,31 @@ __device__ __forceinline__ void bwd_tile(BwdLDS& s, const RenderSet& rs, int v, 
   const bool useful = (lane < 32) ? (ncol < 6) : dcol;
   const int field = ncol;
 
-  uint32_t* mylist = s.list[q];
+  uint32_t* mylist = s.list[q];  // per kept candidate: its offset (batch index x QS) in qsum
   float* myq = s.qsum + q * NG;
 
-  for (int h = hi; h > lo; h -= 64) {
-    {
-      const int rel_c = h - 1 - cs;
-      if (rel_c >= lo) {
-        // the conic pre-multiplied for gauss_power2 (.w of s1: list position)
-        if (piece == 0) {
-          s.s0[cs] = make_float4(npc.x, npc.y, GSR_CONIC_K_AC * npc.z, GSR_CONIC_K_B * npc.w);
-        } else if (piece == 1) {
-          s.s1[cs] = make_float4(GSR_CONIC_K_AC * npc.x, npc.y, npc.z, __uint_as_float((uint32_t)rel_c));
-        } else if (piece == 2) {
-          s.s2[cs] = npc;
-        } else {
-          const uint32_t dx_ = __float_as_uint(npc.x), dy_ = __float_as_uint(npc.y);
-          const int xmin = dx_ & 0xffff, ymin = dx_ >> 16, xmax = dy_ & 0xffff;
-          s.slot[cs] = ngo + (uint32_t)((tyi - ymin) * (xmax - xmin) + (txi - xmin));
-        }
-      }
-      if (h - 64 > lo) {
-        if (h - 65 - cs >= lo) {
-#ifdef GSR_EXP_HOTREC
-          npc = reinterpret_cast<const float4*>(rec + (gi_next & 4095u))[piece];
-#else
-          npc = reinterpret_cast<const float4*>(rec + gi_next)[piece];
-#endif
-          if (piece == 2 && rs.col2 != nullptr)
-            npc = make_float4(rs.col2[3 * gi_next], rs.col2[3 * gi_next + 1], rs.col2[3 * gi_next + 2], 0.f);
-          if (piece == 3) {
-            ngo = goff[gi_next];
-#ifndef GSR_EXP_NOREACH
-            atomicOr(reach32 + 2 * gi_next, vbit);
-#endif
-          }
-        }
-        if (h - 128 > lo) gi_next = fetch_index(h - 128);
-      }
-    }
-    const uint32_t qcur = nqb;
-    if (qbm != nullptr && h - 65 - lane >= lo) nqb = qbm[qstride * (uint32_t)(h - 65 - lane)];
-    __syncthreads();
-    // this wave's quadrant: cull the staged batch, list the kept candidates, zero the others' sums
-    const int rel_l = h - 1 - lane;
-    bool keep = false;
-#ifdef GSR_EXP_NOCULL
-    if (rel_l >= lo && rel_l < qmaxc) keep = s.s0[lane].x > -1e30f;
-#else
-    if (qbm != nullptr) {
-      keep = rel_l >= lo && rel_l < qmaxc && ((qcur >> qsh) & 1u);
-    } else if (rel_l >= lo && rel_l < qmaxc) {
-      // the staged conic back to (a, b, c) for the (padded, conservative) cull
-      const float4 c0 = s.s0[lane], c1 = s.s1[lane];
-      keep = quadrant_hit(make_float4(c0.x, c0.y, c0.z * (1.0f / GSR_CONIC_K_AC), c0.w * (1.0f / GSR_CONIC_K_B)),
-                          make_float4(c1.x * (1.0f / GSR_CONIC_K_AC), c1.y, c1.z, c1.w), (float)qx0, (float)qy0);
-    }
-#endif
-    const unsigned long long bal = __ballot(keep);
-    const int cnt = __popcll(bal);
-    if (lane == 0) s.kmask[q] = bal;  // the flush reads this quadrant's sums of kept candidates only
-#ifdef GSR_TIMELINE
-    if (lane == 0) s.tl_cnt[q] = cnt;
-#endif
-    if (keep) mylist[mask_rank(bal)] = (uint32_t)lane;
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // this wave's list is read back by its own lanes
-    // kept candidates in groups of 8: replay -> (u, w) rows in LDS -> matrix-core sums.
-    // The kept set is the uniform ballot mask: walk it with scalar bit scans, prefetching the next
-    // candidate's staged record while the current one is replayed.
-    unsigned long long rest = bal;
-#ifdef GSR_EXP_NOGROUP
-    if (cnt < 0)
-#endif
-    for (int g0 = 0; g0 < cnt; g0 += GS) {
-      const int gn = min(GS, cnt - g0);
-      if (gn == GS) {
-        // a full group: the 8 replay steps without per-step branches, one basic block, so the independent
-        // per-candidate terms (staged-record reads, alpha, exp2, 1 / (1 - alpha)) of later candidates can be
-        // scheduled under earlier candidates' dependent updates (same operations, same order per pixel)
-        int jj[GS];
-#pragma unroll
-        for (int c = 0; c < GS; ++c) {
-          jj[c] = (int)__builtin_ctzll(rest);
-          rest &= rest - 1ull;
-        }
-        float4 ca = s.s0[jj[0]], cb = s.s1[jj[0]], cc = s.s2[jj[0]];
-#pragma unroll
-        for (int c = 0; c < GS; ++c) {
-          // the next candidate's staged record read ahead of this step (kept ahead by the compiler barrier)
-          const int cn = c + 1 < GS ? c + 1 : c;
-          const float4 na = s.s0[jj[cn]], nb = s.s1[jj[cn]], nc = s.s2[jj[cn]];
-          asm volatile("" ::: "memory");
-          float u, w;
-          replay(ca, cb, cc, u, w);
-          uw[16 * c + wa[c >> 2]] = u;
-          uw[16 * (c + 8) + wa[2 + (c >> 2)]] = w;
-          if ((c & (GSR_BWD_OVERLAP - 1)) == GSR_BWD_OVERLAP - 1) __builtin_amdgcn_sched_barrier(0);  // (VGPR budget)
-          ca = na;
-          cb = nb;
-          cc = nc;
-        }
-      } else {
-      int j = (int)__builtin_ctzll(rest);
-      float4 ca = s.s0[j], cb = s.s1[j], cc = s.s2[j];
-#pragma unroll
-      for (int c = 0; c < GS; ++c) {
-        if (c < gn) {
-          rest &= rest - 1ull;
-          const int jn = (c + 1 < gn) ? (int)__builtin_ctzll(rest) : j;
-          const float4 na = s.s0[jn], nb = s.s1[jn], nc = s.s2[jn];
-          float u, w;
-#ifdef GSR_EXP_NOREPLAY
-          u = ca.x * pxf;
-          w = cb.x * pyf;
-#else
-          replay(ca, cb, cc, u, w);
-#endif
-          uw[16 * c + wa[c >> 2]] = u;
-          uw[16 * (c + 8) + wa[2 + (c >> 2)]] = w;
-          ca = na;
-          cb = nb;
-          cc = nc;
-          j = jn;
-        }
-      }
-      }
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the wave reads its own lanes' rows
-#ifdef GSR_EXP_NOMFMA
-      continue;
-#endif
-      float av[16];
-#pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        const float4 a4 = asrc[k ^ aswz];
-        av[4 * k] = a4.x, av[4 * k + 1] = a4.y, av[4 * k + 2] = a4.z, av[4 * k + 3] = a4.w;
-      }
-      // the candidates of this lane's 4 result rows (m = mb + r)
-      const uint4 jl = *reinterpret_cast<const uint4*>(mylist + g0 + mb);
-      typedef float f4 __attribute__((ext_vector_type(4)));
-      f4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-      for (int i = 0; i < 16; ++i) {
-        if (i & 1)
-          acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(av[i], bv[i], acc1, 0, 0, 0);
-        else
-          acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(av[i], bv[i], acc0, 0, 0, 0);
-      }
-      // lane l: column ncol, rows 4 (l >> 4) + r; u rows 0-7 (columns 0-5), w rows 8-15 (6-9)
-      if (useful) {
-        const uint32_t jr[4] = {jl.x, jl.y, jl.z, jl.w};
-#pragma unroll
-        for (int r = 0; r < 4; ++r)
-          if (mb + r < gn) myq[jr[r] * (uint32_t)QS + (uint32_t)field] = acc0[r] + acc1[r];
-      }
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // rows are rewritten by the next group
-    }
-    __syncthreads();
-#ifdef GSR_TIMELINE
-    if (t == 0) {
-      const int c0 = s.tl_cnt[0], c1 = s.tl_cnt[1], c2 = s.tl_cnt[2], c3 = s.tl_cnt[3];
-      tl_work += c0 + c1 + c2 + c3;                                  // kept (candidate, quadrant) pairs
-      tl_max += 4 * max(max(c0, c1), max(c2, c3));                  // lockstep cost in pair slots
-      tl_q[0] += c0, tl_q[1] += c1, tl_q[2] += c2, tl_q[3] += c3;
-      tl_staged += min(h - lo, 64);
-      tl_any += __popcll(s.kmask[0] | s.kmask[1] | s.kmask[2] | s.kmask[3]);
-    }
-#endif
+  // The flush of a batch hb (its candidates [hb - 64, hb)): four threads per candidate (t = 4 c + quadrant): per
+  // quadrant, turn the sums over pixel coordinates relative to the quadrant centre into the moments of u over
+  // dx = mean - pixel (dx = mx' - x with mx' = mean - quadrant centre); add the 4 quadrants (quad DPP); form the
+  // reference's terms
+  //   dmean2D = -o (W/2, H/2) (a m1 + b m2, c m2 + b m1), dconic = -o/2 (m3, m4, m5), dopacity = m0
+  // as one 16-byte piece of the 48-byte row per thread (piece 3: none).  It runs at the start of the NEXT batch's
+  // iteration, before that batch's staging (the same four threads of one wave read candidate cs's entries here and
+  // rewrite them there: in order), and its stores are issued right after the staging has waited for the gathers
+  // (one in-order vmcnt counts loads and stores: stores issued just after that wait are a whole batch old at the
+  // next one, so no wave ever waits for a store it has just issued).
+  float4 rowv = zero4;
+  float4* rowp = nullptr;
+  auto flush = [&](int hb) {
+    rowp = nullptr;
 #ifdef GSR_EXP_NOFLUSH
     if (hi < 0)
 #else
-    if (h - 1 - cs >= lo)
+    if (hb - 1 - cs >= lo)
 #endif
     {
-      // four threads per candidate (t = 4 c + quadrant): per quadrant, turn the sums over pixel
-      // coordinates relative to the quadrant centre into the moments of u over dx = mean - pixel
-      // (dx = mx' - x with mx' = mean - quadrant centre); add the 4 quadrants (quad DPP); form the reference's terms
-      //   dmean2D = -o (W/2, H/2) (a m1 + b m2, c m2 + b m1), dconic = -o/2 (m3, m4, m5), dopacity = m0
-      // and write the 48-byte row, one 16-byte piece per thread.
-      const int qq = piece;
+      int qq = piece;
+      asm volatile("" : "+v"(qq));  // (the quadrant centres formed here, not held in vector registers across the loop)
       const float4 ga = s.s0[cs];
       const float4 gb = s.s1[cs];
       constexpr int NM = NGV;
@@ -1343,19 +1207,230 @@ __device__ __forceinline__ void bwd_tile(BwdLDS& s, const RenderSet& rs, int v, 
       // -o (W/2) (a m1 + b m2) etc. with the staged A = -log2e a / 2, B = -log2e b, C = -log2e c / 2
       const float k = o * (1.0f / 1.4426950408889634f);
       if (qq == 0) {
-        const float dmx = mean_grad(k, ddelx_dx, ga.z, ga.w, m[1], m[2]);
-        const float dmy = mean_grad(k, ddely_dy, gb.x, ga.w, m[2], m[1]);
-        row[0] = make_float4(dmx, dmy, -0.5f * o * m[3], -0.5f * o * m[4]);
+        const float dmx = mean_grad(k, ddelx_dx, gb.x, ga.z, m[1], m[2]);  // (A, B): staged s1.x, s0.z
+        const float dmy = mean_grad(k, ddely_dy, ga.w, ga.z, m[2], m[1]);  // (C, B): staged s0.w, s0.z
+        rowv = make_float4(dmx, dmy, -0.5f * o * m[3], -0.5f * o * m[4]);
+        rowp = row;
       } else if (qq == 1) {
-        row[1] = make_float4(-0.5f * o * m[5], m[0], m[6], m[7]);
+        rowv = make_float4(-0.5f * o * m[5], m[0], m[6], m[7]);
+        rowp = row + 1;
       } else if (qq == 2) {
-        row[2] = make_float4(m[8], m[9], 0.f, 0.f);
+        rowv = make_float4(m[8], m[9], 0.f, 0.f);
+        rowp = row + 2;
       }
     }
-    // No barrier before the next batch's staging: candidate cs's staged record and slot are read here by threads
-    // 4 cs .. 4 cs + 3 and rewritten there by the same four threads (t >> 2 = cs), lanes of one wave whose LDS
-    // accesses complete in program order; the next batch's replay, which rewrites the sums read here, waits at the
-    // staging barrier.
+  };
+
+  // One wait point per batch.  The vector memory counter is one in-order count of loads and stores, and a wait for
+  // an operation also waits for every older one; the compiler counts conservatively across the branches of this
+  // loop, so a use of a loaded value after new loads or stores were issued waited for those too (the next batch's
+  // gathers, the rows just stored).  Here each batch starts with one explicit wait for everything in flight —
+  // issued during the previous batch, so done by now — then consumes every loaded value (staging, the cull bits,
+  // the list entries) before it issues anything new: the previous batch's row stores, the next batch's gathers,
+  // the list entries after them and (after the cull) the next cull bits.
+  for (int h = hi; h > lo; h -= 64) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (h != hi) flush(h + 64);  // the previous batch's rows (LDS reads before this batch's staging rewrites them)
+    uint32_t qcur;
+    asm volatile("v_mov_b32 %0, %1" : "=v"(qcur) : "v"(nqb));  // (a real copy: consumed before new loads)
+    const uint32_t gnx = gi_next & gmask;
+    // (the quad's conic a from piece 0 and c from piece 1, for the other's staged half)
+    const float conic_a = __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, npc.z), 0x00, 0xf, 0xf, false));
+    const float conic_c = __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, npc.x), 0x55, 0xf, 0xf, false));
+    {
+      const int rel_c = h - 1 - cs;
+      // (the candidate's LDS addresses formed here each batch, not held in vector registers across the loop)
+      int cst = cs;
+      asm volatile("" : "+v"(cst));
+      if (rel_c >= lo) {
+        // the conic pre-multiplied for gauss_power2, s0 = (x, y, B, C), s1 = (A, opacity, depth, list position):
+        // conic a and c come from the quad's other pieces (piece 0 holds (x, y, a, b), piece 1 (c, o, depth, ·))
+        if (piece == 0) {
+          s.s0[cst] = make_float4(npc.x, npc.y, GSR_CONIC_K_B * npc.w, GSR_CONIC_K_AC * conic_c);
+        } else if (piece == 1) {
+          s.s1[cst] = make_float4(GSR_CONIC_K_AC * conic_a, npc.y, npc.z, __uint_as_float((uint32_t)rel_c));
+        } else if (piece == 2) {
+          s.s2[cst] = npc;
+          s.gidx[cst] = ngo;  // (the Gaussian, for its reach bit)
+        } else {
+          const uint32_t dx_ = __float_as_uint(npc.x), dy_ = __float_as_uint(npc.y);
+          const int xmin = dx_ & 0xffff, ymin = dx_ >> 16, xmax = dy_ & 0xffff;
+          s.slot[cst] = ngo + (uint32_t)((tyi - ymin) * (xmax - xmin) + (txi - xmin));
+        }
+      }
+      if (rowp != nullptr) *rowp = rowv;  // (the previous batch's row piece)
+      if (h - 64 > lo) {
+        // the next batch's Gaussians (their list entries were loaded a batch ago), then the entries of the batch
+        // after it (into the same register)
+        if (h - 65 - cs >= lo) {
+          // (32-bit byte offsets from the view's scalar base: one VGPR per address, nothing hoisted out of the loop)
+#ifdef GSR_EXP_HOTREC
+          npc = *reinterpret_cast<const float4*>(reinterpret_cast<const char*>(rec) + (((gnx & 4095u) * 4u + piece) << 4));
+#else
+          npc = *reinterpret_cast<const float4*>(reinterpret_cast<const char*>(rec) + ((gnx * 4u + (uint32_t)piece) << 4));
+#endif
+          if (piece == 2 && rs.col2 != nullptr)
+            npc = make_float4(rs.col2[3 * gnx], rs.col2[3 * gnx + 1], rs.col2[3 * gnx + 2], 0.f);
+          if (piece == 2) ngo = gnx;  // (before the load below: a select after it would wait for the load)
+          if (piece == 3) ngo = goff[gnx];
+        }
+        if (h - 128 > lo) gi_next = fetch_raw(h - 128);
+      }
+    }
+    __syncthreads();
+    // this wave's quadrant: cull the staged batch, list the kept candidates, zero the others' sums
+    const int rel_l = h - 1 - lane;
+    bool keep = false;
+#ifdef GSR_EXP_NOCULL
+    if (rel_l >= lo && rel_l < qmaxc) keep = s.s0[lane].x > -1e30f;
+#else
+    if (qbm != nullptr) {
+      keep = rel_l >= lo && rel_l < qmaxc && ((qcur >> qsh) & 1u);
+    } else if (rel_l >= lo && rel_l < qmaxc) {
+      // the staged conic back to (a, b, c) for the (padded, conservative) cull
+      const float4 c0 = s.s0[lane], c1 = s.s1[lane];
+      keep = quadrant_hit(make_float4(c0.x, c0.y, c1.x * (1.0f / GSR_CONIC_K_AC), c0.z * (1.0f / GSR_CONIC_K_B)),
+                          make_float4(c0.w * (1.0f / GSR_CONIC_K_AC), c1.y, c1.z, c1.w), (float)qx0, (float)qy0);
+    }
+#endif
+    // the next batch's cull, read after this one's into the same register (a copy at the loop latch waited for
+    // every memory operation in flight, the flush's row stores included)
+    if (qbm != nullptr && h - 65 - lane >= lo) nqb = qbm[qstride * (uint32_t)(h - 65 - lane)];
+    const unsigned long long bal = __ballot(keep);
+    const int cnt = __popcll(bal);
+    if (lane == 0) s.kmask[q] = bal;  // the flush reads this quadrant's sums of kept candidates only
+#ifndef GSR_EXP_NOREACH
+    // the reach bits of the kept candidates: with the tile-wave forward's 4-bit masks (layout 1) wave 0 sets one
+    // per candidate any quadrant kept (a set mask bit is a blend, which lies below that quadrant's deepest blend);
+    // otherwise each wave for its own kept candidates (the same bit, set up to four times)
+    if (qlayout == 1u ? (q == 0 && rel_l >= lo && (qcur & 0xfu) != 0u) : keep) {
+      uint32_t vb;
+      asm volatile("v_mov_b32 %0, %1" : "=v"(vb) : "s"(vbit));  // (moved into a vector register here, not held)
+      atomicOr(reach32 + 2 * s.gidx[lane], vb);
+    }
+#endif
+#ifdef GSR_TIMELINE
+    if (lane == 0) s.tl_cnt[q] = cnt;
+#endif
+    if (keep) mylist[mask_rank(bal)] = (uint32_t)lane * (uint32_t)QS;  // (the candidate's row in qsum)
+    GSR_WAVE_LDS_ORDER();  // this wave's list is read back by its own lanes
+    // kept candidates in groups of 8: replay -> (u, w) rows in LDS -> matrix-core sums.
+    // The kept set is the uniform ballot mask: walk it with scalar bit scans, prefetching the next
+    // candidate's staged record while the current one is replayed.
+    unsigned long long rest = bal;
+#ifdef GSR_EXP_NOGROUP
+    if (cnt < 0)
+#endif
+    for (int g0 = 0; g0 < cnt; g0 += GS) {
+      const int gn = min(GS, cnt - g0);
+      if (gn == GS) {
+        // a full group: the 8 replay steps without per-step branches, one basic block, so the independent
+        // per-candidate terms (staged-record reads, alpha, exp2, 1 / (1 - alpha)) of later candidates can be
+        // scheduled under earlier candidates' dependent updates (same operations, same order per pixel)
+        int jj[GS];
+#pragma unroll
+        for (int c = 0; c < GS; ++c) {
+          jj[c] = (int)__builtin_ctzll(rest);
+          rest &= rest - 1ull;
+        }
+        float4 ca = s.s0[jj[0]], cb = s.s1[jj[0]], cc = s.s2[jj[0]];
+#pragma unroll
+        for (int c = 0; c < GS; ++c) {
+          // the next candidate's staged record read ahead of this step (kept ahead by the compiler barrier; none
+          // after the last: a read nobody uses still holds registers the matrix-core operands then wait for)
+          float4 na, nb, nc;
+          if (c + 1 < GS) {
+            na = s.s0[jj[c + 1]], nb = s.s1[jj[c + 1]], nc = s.s2[jj[c + 1]];
+            asm volatile("" ::: "memory");
+          }
+          float u, w;
+          replay(ca, cb, cc, u, w);
+          uw[16 * c + wa[c >> 2]] = u;
+          uw[16 * (c + 8) + wa[2 + (c >> 2)]] = w;
+          if ((c & (GSR_BWD_OVERLAP - 1)) == GSR_BWD_OVERLAP - 1) __builtin_amdgcn_sched_barrier(0);  // (VGPR budget)
+          if (c + 1 < GS) {
+            ca = na;
+            cb = nb;
+            cc = nc;
+          }
+        }
+      } else {
+      int j = (int)__builtin_ctzll(rest);
+      float4 ca = s.s0[j], cb = s.s1[j], cc = s.s2[j];
+#pragma unroll
+      for (int c = 0; c < GS; ++c) {
+        if (c < gn) {
+          rest &= rest - 1ull;
+          const int jn = (c + 1 < gn) ? (int)__builtin_ctzll(rest) : j;
+          const float4 na = s.s0[jn], nb = s.s1[jn], nc = s.s2[jn];
+          float u, w;
+#ifdef GSR_EXP_NOREPLAY
+          u = ca.x * pxf;
+          w = cb.x * pyf;
+#else
+          replay(ca, cb, cc, u, w);
+#endif
+          uw[16 * c + wa[c >> 2]] = u;
+          uw[16 * (c + 8) + wa[2 + (c >> 2)]] = w;
+          ca = na;
+          cb = nb;
+          cc = nc;
+          j = jn;
+        }
+      }
+      }
+      GSR_WAVE_LDS_ORDER();  // the wave reads its own lanes' rows
+#ifdef GSR_EXP_NOMFMA
+      continue;
+#endif
+      float av[16];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const float4 a4 = asrc[k ^ aswz];
+        av[4 * k] = a4.x, av[4 * k + 1] = a4.y, av[4 * k + 2] = a4.z, av[4 * k + 3] = a4.w;
+      }
+      // the candidates of this lane's 4 result rows (m = mb + r)
+      const uint4 jl = *reinterpret_cast<const uint4*>(mylist + g0 + mb);
+      typedef float f4 __attribute__((ext_vector_type(4)));
+      f4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        if (i & 1)
+          acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(av[i], bv[i], acc1, 0, 0, 0);
+        else
+          acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(av[i], bv[i], acc0, 0, 0, 0);
+      }
+      // lane l: column ncol, rows 4 (l >> 4) + r; u rows 0-7 (columns 0-5), w rows 8-15 (6-9)
+      if (useful) {
+        const uint32_t jr[4] = {jl.x, jl.y, jl.z, jl.w};
+        if (gn == GS) {
+#pragma unroll
+          for (int r = 0; r < 4; ++r) myq[jr[r] + (uint32_t)field] = acc0[r] + acc1[r];
+        } else {
+          // rows past the group's end go to candidate 0's padding word (qsum[QS - 1], never read): no branches
+#pragma unroll
+          for (int r = 0; r < 4; ++r)
+            myq[mb + r < gn ? jr[r] + (uint32_t)field : (uint32_t)(QS - 1 - NG * q)] = acc0[r] + acc1[r];
+        }
+      }
+      GSR_WAVE_LDS_ORDER();  // rows are rewritten by the next group
+    }
+    __syncthreads();
+#ifdef GSR_TIMELINE
+    if (t == 0) {
+      const int c0 = s.tl_cnt[0], c1 = s.tl_cnt[1], c2 = s.tl_cnt[2], c3 = s.tl_cnt[3];
+      tl_work += c0 + c1 + c2 + c3;                                  // kept (candidate, quadrant) pairs
+      tl_max += 4 * max(max(c0, c1), max(c2, c3));                  // lockstep cost in pair slots
+      tl_q[0] += c0, tl_q[1] += c1, tl_q[2] += c2, tl_q[3] += c3;
+      tl_staged += min(h - lo, 64);
+      tl_any += __popcll(s.kmask[0] | s.kmask[1] | s.kmask[2] | s.kmask[3]);
+    }
+#endif
+  }
+  if (hi > lo) {
+    // the last batch's rows
+    flush(lo + ((hi - lo - 1) & 63) + 1);
+    if (rowp != nullptr) *rowp = rowv;
   }
 #ifdef GSR_TIMELINE
   // bwd record: z = sum over batches of 4 x the busiest quadrant's kept count (not HW_ID)
@@ -1405,6 +1480,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5, 8))) voi
     int q_unused;
     if (!block_map<4>((int)blockIdx.x - extra, rs, v, tile, q_unused)) return;
   }
+  // (workgroup-uniform, loaded from memory: readfirstlane keeps them and the per-tile pointers derived from them in
+  // scalar registers)
+  v = __builtin_amdgcn_readfirstlane(v);
+  tile = __builtin_amdgcn_readfirstlane(tile);
+  chunk = __builtin_amdgcn_readfirstlane(chunk);
   bwd_tile(s, rs, v, tile, chunk, split, ranges, quad_maxc, sorted_gauss, rec, goff, final_Ts,
                 n_contrib, dL_dcolor, dL_ddepth, dL_dalpha, grow, reach);
 }
@@ -1540,7 +1620,7 @@ __global__ __launch_bounds__(64) void k_render_bwd_tw(
   unsigned int* const reach32 = reinterpret_cast<unsigned int*>(reach) + (v >> 5);
   const unsigned int vbit = 1u << (v & 31);
   float4 na = zero4, nb = zero4, nc = zero4, nd = zero4, n2 = zero4;
-  uint32_t ngo = 0u, gi_next = 0u;
+  uint32_t ngo = 0u, gi_next = 0u, ng = 0u;
   auto load = [&](uint32_t g) {
     const float4* r = reinterpret_cast<const float4*>(rec + g);
     {
@@ -1548,9 +1628,7 @@ __global__ __launch_bounds__(64) void k_render_bwd_tw(
       nb = r[1];
       nd = r[3];
       ngo = goff[g];
-#ifndef GSR_EXP_NOREACH
-      atomicOr(reach32 + 2 * g, vbit);  // the Gaussian gets a row in this view (k_view_grad reads it)
-#endif
+      ng = g;  // (its reach bit is set at the staging, once the cull is known)
     }
     {
       nc = r[2];
@@ -1563,18 +1641,32 @@ __global__ __launch_bounds__(64) void k_render_bwd_tw(
       }
     }
   };
-  // the forward's quadrant masks when the keys carry them (TilePack::qmask): the cull is read, not recomputed
-  // (both bounds are conservative: a pair either keeps has no blend beyond the other's, so the sums agree)
-  const uint32_t* qkeys = rs.qkeys ? rs.qkeys + rs.inst_start[v] + range.x : nullptr;
+  // The cull is read, not recomputed: the forward's exact masks when it recorded them (ImageState::split_mode[1];
+  // layout 1, the tile-wave forward: byte i = the 4-bit mask of the quadrants instance i blended in; layout 2, the
+  // quadrant-wave forward: byte 4 i + q = quadrant q blended instance i — a pair the forward blended nowhere has no
+  // backward hit), else the quadrant masks the keys carry (TilePack::qmask, conservative).
+  const uint32_t qlayout = rs.qbytes != nullptr && rs.split_mode != nullptr ? (rs.split_mode[1] & 0xffu) : 0u;
+  const uint8_t* const qbm = qlayout != 0u ? rs.qbytes + (qlayout == 2u ? 4 : 1) * ((size_t)rs.inst_start[v] + range.x)
+                                           : nullptr;
+  const uint32_t* qkeys = qbm == nullptr && rs.qkeys ? rs.qkeys + rs.inst_start[v] + range.x : nullptr;
+  auto cull_mask = [&](int pos) -> uint32_t {
+    if (qlayout == 2u) {
+      const uint32_t b = reinterpret_cast<const uint32_t*>(qbm)[pos];  // bytes q0..q3, each 0 or 1
+      return (b & 1u) | ((b >> 7) & 2u) | ((b >> 14) & 4u) | ((b >> 21) & 8u);
+    }
+    if (qlayout == 1u) return qbm[pos];
+    return qkeys[pos] >> GSR_QMASK_SHIFT;
+  };
+  const bool masks = qbm != nullptr || qkeys != nullptr;
   uint32_t nqm = 0u, qm_next = 0u;  // the masks of the staged-next candidate / of gi_next
   if (hi > lo) {
     if (hi - 1 - lane >= lo) {
       load(sorted_gauss[range.x + hi - 1 - lane] & gmask);
-      if (qkeys) nqm = qkeys[hi - 1 - lane] >> GSR_QMASK_SHIFT;
+      if (masks) nqm = cull_mask(hi - 1 - lane);
     }
     if (hi - 65 - lane >= lo) {
       gi_next = sorted_gauss[range.x + hi - 65 - lane] & gmask;
-      if (qkeys) qm_next = qkeys[hi - 65 - lane] >> GSR_QMASK_SHIFT;
+      if (masks) qm_next = cull_mask(hi - 65 - lane);
     }
   }
 
@@ -1654,7 +1746,7 @@ __global__ __launch_bounds__(64) void k_render_bwd_tw(
       const uint32_t dx_ = __float_as_uint(nd.x), dy_ = __float_as_uint(nd.y);
       const int xmin = dx_ & 0xffff, ymin = dx_ >> 16, xmax = dy_ & 0xffff;
       slot[lane] = ngo + (uint32_t)((tyi - ymin) * (xmax - xmin) + (txi - xmin));
-      if (qkeys) {
+      if (masks) {
 #pragma unroll
         for (int q = 0; q < 4; ++q) keep4 |= rel_c < qmaxc[q] ? nqm & (1u << q) : 0u;
       } else {
@@ -1671,6 +1763,11 @@ __global__ __launch_bounds__(64) void k_render_bwd_tw(
       s2[lane] = make_float4(nc.x, n2.x, nc.y, n2.y);
       s3[lane] = make_float4(nc.z, n2.z, 0.f, 0.f);
     }
+#ifndef GSR_EXP_NOREACH
+    // the reach bit of a candidate some quadrant keeps (k_view_grad / k_gauss_fused walk exactly the reached pairs;
+    // a staged candidate no quadrant keeps gets a zero row)
+    if (staged && keep4 != 0u) atomicOr(reach32 + 2 * ng, vbit);
+#endif
     // the next batch's records and the one after's indices
     if (h - 64 > lo) {
       if (h - 65 - lane >= lo) {
@@ -1679,7 +1776,7 @@ __global__ __launch_bounds__(64) void k_render_bwd_tw(
       }
       if (h - 129 - lane >= lo) {
         gi_next = sorted_gauss[range.x + h - 129 - lane] & gmask;
-        if (qkeys) qm_next = qkeys[h - 129 - lane] >> GSR_QMASK_SHIFT;
+        if (masks) qm_next = cull_mask(h - 129 - lane);
       }
     }
 #pragma unroll
