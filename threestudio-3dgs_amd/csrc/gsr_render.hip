@@ -294,9 +294,9 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(GSR_FWD_WPE,
     // the step twice with the sets swapped: no register copies); done / ok / term / blend as uniform lane masks
     int k = 0;
     unsigned long long hbm = 0ull;  // staged candidates (by position) that blended at least one pixel (uniform)
+    // (true while candidates remain; the wave's termination is tested every second step, in the loop below)
     auto step = [&](const float4& a, const float4& b, const float4& c, const float4& e, float4& an, float4& bn,
                     float4& cn, float4& en) -> bool {
-      if (k >= cnt || ((k & 7) == 0 && dmk == ~0ull)) return false;
       an = s0[k + 1], bn = s1[k + 1], cn = s2[k + 1];
       en = C2 ? s3[k + 1] : zero4;
 #if GSR_FWD_PREFETCH
@@ -336,12 +336,12 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(GSR_FWD_WPE,
       dmk |= termm;
       hbm |= blendm != 0ull ? 1ull << k : 0ull;
       ++k;
-      return true;
+      return k < cnt;
     };
-    {
+    if (cnt > 0) {
       float4 pa = s0[0], pb = s1[0], pc = s2[0], pd = C2 ? s3[0] : zero4;
       float4 ya, yb, yc, yd;
-      while (step(pa, pb, pc, pd, ya, yb, yc, yd) && step(ya, yb, yc, yd, pa, pb, pc, pd)) {
+      while (dmk != ~0ull && step(pa, pb, pc, pd, ya, yb, yc, yd) && step(ya, yb, yc, yd, pa, pb, pc, pd)) {
       }
     }
     // the backward's exact cull (RenderSet::qbytes, layout 2: byte 4 i + q of the set's listed instance i): whether
@@ -1284,14 +1284,10 @@ __device__ __forceinline__ void bwd_tile(BwdLDS& s, const RenderSet& rs, int v, 
 #ifdef GSR_EXP_NOCULL
     if (rel_l >= lo && rel_l < qmaxc) keep = s.s0[lane].x > -1e30f;
 #else
-    if (qbm != nullptr) {
-      keep = rel_l >= lo && rel_l < qmaxc && ((qcur >> qsh) & 1u);
-    } else if (rel_l >= lo && rel_l < qmaxc) {
-      // the staged conic back to (a, b, c) for the (padded, conservative) cull
-      const float4 c0 = s.s0[lane], c1 = s.s1[lane];
-      keep = quadrant_hit(make_float4(c0.x, c0.y, c1.x * (1.0f / GSR_CONIC_K_AC), c0.z * (1.0f / GSR_CONIC_K_B)),
-                          make_float4(c0.w * (1.0f / GSR_CONIC_K_AC), c1.y, c1.z, c1.w), (float)qx0, (float)qy0);
-    }
+    // (every forward records its masks — layout 1 or 2 — whenever a list is non-empty; without them, which no
+    // forward of this library leaves, every candidate before the quadrant's deepest blend is replayed: the replay's
+    // own alpha tests keep that exact)
+    keep = rel_l >= lo && rel_l < qmaxc && (qbm == nullptr || ((qcur >> qsh) & 1u));
 #endif
     // the next batch's cull, read after this one's into the same register (a copy at the loop latch waited for
     // every memory operation in flight, the flush's row stores included)
@@ -1355,14 +1351,24 @@ __device__ __forceinline__ void bwd_tile(BwdLDS& s, const RenderSet& rs, int v, 
           }
         }
       } else {
-      int j = (int)__builtin_ctzll(rest);
-      float4 ca = s.s0[j], cb = s.s1[j], cc = s.s2[j];
+      // the group's last, partial batch of gn < 8 candidates: the same steps, guarded (uniform branches), and no
+      // read ahead after the last one (a dead read's registers made the matrix-core operand reads wait for it)
+      int jj[GS];
+#pragma unroll
+      for (int c = 0; c < GS; ++c) {
+        jj[c] = (int)__builtin_ctzll(rest | (1ull << 63));
+        rest &= rest - 1ull;
+      }
+      float4 ca = s.s0[jj[0]], cb = s.s1[jj[0]], cc = s.s2[jj[0]];
 #pragma unroll
       for (int c = 0; c < GS; ++c) {
         if (c < gn) {
-          rest &= rest - 1ull;
-          const int jn = (c + 1 < gn) ? (int)__builtin_ctzll(rest) : j;
-          const float4 na = s.s0[jn], nb = s.s1[jn], nc = s.s2[jn];
+          const bool more = c + 1 < gn;
+          float4 na, nb, nc;
+          if (more) {
+            na = s.s0[jj[c + 1]], nb = s.s1[jj[c + 1]], nc = s.s2[jj[c + 1]];
+            asm volatile("" ::: "memory");
+          }
           float u, w;
 #ifdef GSR_EXP_NOREPLAY
           u = ca.x * pxf;
@@ -1372,10 +1378,11 @@ __device__ __forceinline__ void bwd_tile(BwdLDS& s, const RenderSet& rs, int v, 
 #endif
           uw[16 * c + wa[c >> 2]] = u;
           uw[16 * (c + 8) + wa[2 + (c >> 2)]] = w;
-          ca = na;
-          cb = nb;
-          cc = nc;
-          j = jn;
+          if (more) {
+            ca = na;
+            cb = nb;
+            cc = nc;
+          }
         }
       }
       }
