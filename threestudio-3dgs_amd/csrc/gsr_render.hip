@@ -142,6 +142,13 @@ __device__ __forceinline__ float sgpr_f(float x) {
   return r;
 }
 
+// a copy the compiler cannot fold away: it ends the source register's live range at this point
+__device__ __forceinline__ float vcopy(float x) {
+  float r;
+  asm volatile("v_mov_b32 %0, %1" : "=v"(r) : "v"(x));
+  return r;
+}
+
 // bg . dL/dpixel with an explicit operation order (the backward kernels' background terms: every kernel
 // variant forms the same bits, independent of how the compiler would contract the expression)
 __device__ __forceinline__ float bg_dot3(const float* bg, float d0, float d1, float d2) {
@@ -1656,24 +1663,27 @@ __global__ __launch_bounds__(64) void k_render_bwd_tw(
   const uint8_t* const qbm = qlayout != 0u ? rs.qbytes + (qlayout == 2u ? 4 : 1) * ((size_t)rs.inst_start[v] + range.x)
                                            : nullptr;
   const uint32_t* qkeys = qbm == nullptr && rs.qkeys ? rs.qkeys + rs.inst_start[v] + range.x : nullptr;
-  auto cull_mask = [&](int pos) -> uint32_t {
-    if (qlayout == 2u) {
-      const uint32_t b = reinterpret_cast<const uint32_t*>(qbm)[pos];  // bytes q0..q3, each 0 or 1
-      return (b & 1u) | ((b >> 7) & 2u) | ((b >> 14) & 4u) | ((b >> 21) & 8u);
-    }
+  // (loaded raw, decoded where used: a use right after the load would wait for every memory operation in flight)
+  auto cull_raw = [&](int pos) -> uint32_t {
+    if (qlayout == 2u) return reinterpret_cast<const uint32_t*>(qbm)[pos];  // bytes q0..q3, each 0 or 1
     if (qlayout == 1u) return qbm[pos];
-    return qkeys[pos] >> GSR_QMASK_SHIFT;
+    return qkeys[pos];
+  };
+  auto cull_decode = [&](uint32_t b) -> uint32_t {
+    if (qlayout == 2u) return (b & 1u) | ((b >> 7) & 2u) | ((b >> 14) & 4u) | ((b >> 21) & 8u);
+    if (qlayout == 1u) return b;
+    return b >> GSR_QMASK_SHIFT;
   };
   const bool masks = qbm != nullptr || qkeys != nullptr;
-  uint32_t nqm = 0u, qm_next = 0u;  // the masks of the staged-next candidate / of gi_next
+  uint32_t nqm = 0u, qm_next = 0u;  // the mask of the staged-next candidate / the raw mask word of gi_next
   if (hi > lo) {
     if (hi - 1 - lane >= lo) {
       load(sorted_gauss[range.x + hi - 1 - lane] & gmask);
-      if (masks) nqm = cull_mask(hi - 1 - lane);
+      if (masks) nqm = cull_decode(cull_raw(hi - 1 - lane));
     }
-    if (hi - 65 - lane >= lo) {
-      gi_next = sorted_gauss[range.x + hi - 65 - lane] & gmask;
-      if (masks) qm_next = cull_mask(hi - 65 - lane);
+    if (hi - 64 > lo) {
+      gi_next = sorted_gauss[range.x + max(hi - 65 - lane, lo)];  // (raw: masked where used)
+      if (masks) qm_next = cull_raw(max(hi - 65 - lane, lo));
     }
   }
 
@@ -1741,18 +1751,64 @@ __global__ __launch_bounds__(64) void k_render_bwd_tw(
     }
   };
 
+  // The previous batch's row: ((q0 + q1) + (q2 + q3)) per moment, then the reference's terms (k_render_bwd's flush),
+  // written at the start of the next batch (before its staging rewrites the staged record and slot).
+  // (computed from the staged record and slot before the next staging rewrites them; stored after that staging)
+  float4 rv[RW];
+  uint32_t rslot = 0u;
+  auto make_row = [&]() {
+    float m[NM];
+#pragma unroll
+    for (int i = 0; i < NM; ++i) m[i] = acc[i] + accb[i];
+    const float4 ga = s0[lane];
+    const float4 gb = s1[lane];
+    const float o = gb.y;
+    rslot = slot[lane];
+    const float k = o * (1.0f / 1.4426950408889634f);
+    {
+      // (A = gb.x, B = ga.z, C = ga.w in this kernel's staging)
+      const float dmx = mean_grad(k, ddelx_dx, gb.x, ga.z, m[1], m[2]);
+      const float dmy = mean_grad(k, ddely_dy, ga.w, ga.z, m[2], m[1]);
+      rv[0] = make_float4(dmx, dmy, -0.5f * o * m[3], -0.5f * o * m[4]);
+    }
+    rv[1] = make_float4(-0.5f * o * m[5], m[0], m[6], m[7]);
+    rv[2] = TWO ? make_float4(m[8], m[9], m[12 % NM], m[13 % NM]) : make_float4(m[8], m[9], 0.f, 0.f);
+    if (TWO) {
+      const float dmx1 = mean_grad(k, ddelx_dx, gb.x, ga.z, m[10 % NM], m[11 % NM]);
+      const float dmy1 = mean_grad(k, ddely_dy, ga.w, ga.z, m[11 % NM], m[10 % NM]);
+      rv[RW - 1] = make_float4(m[14 % NM], dmx1, dmy1, 0.f);
+    }
+  };
+  auto store_row = [&]() {
+    float4* row = grow + RW * (size_t)rslot;
+#pragma unroll
+    for (int i = 0; i < RW; ++i) row[i] = rv[i];
+  };
+  // One wait point per batch (as k_render_bwd): everything in flight was issued during the previous batch; every
+  // loaded value is consumed before anything new is issued (a memory operation issued ahead of a use of an earlier
+  // load, in a branch some lanes skip, turns the compiler's wait for that load into a wait for everything).
   for (int h = hi; h > lo; h -= 64) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const bool row_pending = h != hi && h + 63 - lane >= lo;  // (the previous batch staged this lane)
+    if (row_pending) make_row();
+    // the loaded record, copied out of the load registers here (the staging packs it into LDS tuples; packing the
+    // load registers themselves had the compiler copy them at the loop end, right after the loads, waiting on them)
+    const float4 ca = make_float4(vcopy(na.x), vcopy(na.y), vcopy(na.z), vcopy(na.w));
+    const float4 cb = make_float4(vcopy(nb.x), vcopy(nb.y), vcopy(nb.z), 0.f);
+    const float4 cc = make_float4(vcopy(nc.x), vcopy(nc.y), vcopy(nc.z), 0.f);
+    const float4 c2 = TWO ? make_float4(vcopy(n2.x), vcopy(n2.y), vcopy(n2.z), 0.f) : zero4;
+    const uint32_t cdx = __float_as_uint(vcopy(nd.x)), cdy = __float_as_uint(vcopy(nd.y));
+    const uint32_t cgo = __float_as_uint(vcopy(__uint_as_float(ngo)));
     const int rel_c = h - 1 - lane;
     const bool staged = rel_c >= lo;
     uint32_t keep4 = 0u;
     if (staged) {
       // the pre-multiplied conic as s0 = (x, y, B, C), s1 = (A, opacity, depth, list position): the products the
       // step packs are adjacent; row slot
-      s0[lane] = make_float4(na.x, na.y, GSR_CONIC_K_B * na.w, GSR_CONIC_K_AC * nb.x);
-      s1[lane] = make_float4(GSR_CONIC_K_AC * na.z, nb.y, nb.z, __uint_as_float((uint32_t)rel_c));
-      const uint32_t dx_ = __float_as_uint(nd.x), dy_ = __float_as_uint(nd.y);
-      const int xmin = dx_ & 0xffff, ymin = dx_ >> 16, xmax = dy_ & 0xffff;
-      slot[lane] = ngo + (uint32_t)((tyi - ymin) * (xmax - xmin) + (txi - xmin));
+      s0[lane] = make_float4(ca.x, ca.y, GSR_CONIC_K_B * ca.w, GSR_CONIC_K_AC * cb.x);
+      s1[lane] = make_float4(GSR_CONIC_K_AC * ca.z, cb.y, cb.z, __uint_as_float((uint32_t)rel_c));
+      const int xmin = cdx & 0xffff, ymin = cdx >> 16, xmax = cdy & 0xffff;
+      slot[lane] = cgo + (uint32_t)((tyi - ymin) * (xmax - xmin) + (txi - xmin));
       if (masks) {
 #pragma unroll
         for (int q = 0; q < 4; ++q) keep4 |= rel_c < qmaxc[q] ? nqm & (1u << q) : 0u;
@@ -1761,30 +1817,32 @@ __global__ __launch_bounds__(64) void k_render_bwd_tw(
 #pragma unroll
         for (int q = 0; q < 4; ++q)
           if (rel_c < qmaxc[q] &&
-              quadrant_hit(na, nb, (float)(txi * GSR_TILE_X + (q & 1) * 8), (float)(tyi * GSR_TILE_Y + (q >> 1) * 8)))
+              quadrant_hit(ca, cb, (float)(txi * GSR_TILE_X + (q & 1) * 8), (float)(tyi * GSR_TILE_Y + (q >> 1) * 8)))
             keep4 |= 1u << q;
       }
     }
     if (staged) {
       // colours interleaved with the second colours (zeros for one colour): (r, r2, g, g2), (b, b2)
-      s2[lane] = make_float4(nc.x, n2.x, nc.y, n2.y);
-      s3[lane] = make_float4(nc.z, n2.z, 0.f, 0.f);
+      s2[lane] = make_float4(cc.x, c2.x, cc.y, c2.y);
+      s3[lane] = make_float4(cc.z, c2.z, 0.f, 0.f);
     }
+    // (the next batch's record index and cull, from values loaded a batch ago: formed here, not where used)
+    uint32_t g_next = gi_next & gmask;
+    nqm = cull_decode(qm_next);
+    asm volatile("" : "+v"(g_next), "+v"(nqm)::"memory");
 #ifndef GSR_EXP_NOREACH
     // the reach bit of a candidate some quadrant keeps (k_view_grad / k_gauss_fused walk exactly the reached pairs;
     // a staged candidate no quadrant keeps gets a zero row)
     if (staged && keep4 != 0u) atomicOr(reach32 + 2 * ng, vbit);
 #endif
-    // the next batch's records and the one after's indices
+    if (row_pending) store_row();
+    // the next batch's records and the one after's indices: every lane loads (positions clamped into the list, an
+    // unstaged lane's record is never read) so the loaded values replace the registers without merges
     if (h - 64 > lo) {
-      if (h - 65 - lane >= lo) {
-        load(gi_next);
-        nqm = qm_next;
-      }
-      if (h - 129 - lane >= lo) {
-        gi_next = sorted_gauss[range.x + h - 129 - lane] & gmask;
-        if (masks) qm_next = cull_mask(h - 129 - lane);
-      }
+      load(g_next);
+      const int pn = max(h - 129 - lane, lo);
+      gi_next = sorted_gauss[range.x + pn];
+      if (masks) qm_next = cull_raw(pn);
     }
 #pragma unroll
     for (int i = 0; i < NM; ++i) acc[i] = 0.f;
@@ -1868,31 +1926,12 @@ __global__ __launch_bounds__(64) void k_render_bwd_tw(
       flush(j, pend);
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // (hits, list and planes are rewritten next)
     }
-    if (staged) {
-      // ((q0 + q1) + (q2 + q3)) per moment, then the reference's terms (k_render_bwd's flush)
-      float m[NM];
-#pragma unroll
-      for (int i = 0; i < NM; ++i) m[i] = acc[i] + accb[i];
-      const float4 ga = s0[lane];
-      const float4 gb = s1[lane];
-      const float o = gb.y;
-      float4* row = grow + RW * (size_t)slot[lane];
-      const float k = o * (1.0f / 1.4426950408889634f);
-      {
-        // (A = gb.x, B = ga.z, C = ga.w in this kernel's staging)
-        const float dmx = mean_grad(k, ddelx_dx, gb.x, ga.z, m[1], m[2]);
-        const float dmy = mean_grad(k, ddely_dy, ga.w, ga.z, m[2], m[1]);
-        row[0] = make_float4(dmx, dmy, -0.5f * o * m[3], -0.5f * o * m[4]);
-      }
-      row[1] = make_float4(-0.5f * o * m[5], m[0], m[6], m[7]);
-      row[2] = TWO ? make_float4(m[8], m[9], m[12 % NM], m[13 % NM]) : make_float4(m[8], m[9], 0.f, 0.f);
-      if (TWO) {
-        const float dmx1 = mean_grad(k, ddelx_dx, gb.x, ga.z, m[10 % NM], m[11 % NM]);
-        const float dmy1 = mean_grad(k, ddely_dy, ga.w, ga.z, m[11 % NM], m[10 % NM]);
-        row[3] = make_float4(m[14 % NM], dmx1, dmy1, 0.f);
-      }
-    }
     __syncthreads();  // (the staged batch is rewritten next)
+  }
+  // (the last batch's rows)
+  if (hi > lo && lo + ((hi - lo - 1) & 63) - lane >= lo) {
+    make_row();
+    store_row();
   }
   GSR_TL_END(1, hi)
 }
