@@ -227,7 +227,10 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(GSR_FWD_WPE,
   // (tests/test_quadrant_bounds.py)
   const uint32_t* qkeys = rs.qkeys ? rs.qkeys + rs.inst_start[v] + range.x : nullptr;
   const int qsh = GSR_QMASK_SHIFT + q;
-  bool kn = false, kn_next = false;  // the keep bits of the batch in n0..n3 / of gi_next
+  // (gi_next and its key word stay raw until the next batch: masked or tested right after their load, the wave
+  // would wait there for every load in flight, the records just issued included)
+  bool kn = false;           // the keep bit of the batch in n0..n3
+  uint32_t kw_next = ~0u;    // gi_next's key word (qkeys; all ones without)
   if (lane < n) kn = qkeys == nullptr || ((qkeys[lane] >> qsh) & 1u);
   if (kn) {
     const uint32_t g0 = sorted_gauss[range.x + lane] & gmask;
@@ -243,8 +246,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(GSR_FWD_WPE,
 #endif
   }
   if (64 + lane < n) {
-    gi_next = sorted_gauss[range.x + 64 + lane] & gmask;
-    kn_next = qkeys == nullptr || ((qkeys[64 + lane] >> qsh) & 1u);
+    gi_next = sorted_gauss[range.x + 64 + lane];
+    if (qkeys != nullptr) kw_next = qkeys[64 + lane];
   }
   // split backward: T at each chunk boundary the walk reaches, and each chunk's own colour / depth sums
   float* const ckpt = CK ? rs.ckpt + ckpt_offset((size_t)(rs.v0 + v), (size_t)rs.gx * rs.gy, tile, 0) : nullptr;
@@ -252,6 +255,10 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(GSR_FWD_WPE,
   if (CK && blockIdx.x == 0 && lane == 0) rs.split_items[0] = 0u;  // k_ckpt_suffix lists the split items
   f2 PrPg = {0.f, 0.f}, PbPd = {0.f, 0.f};
   int chunk = 0;
+  // the previous batch's cull byte, stored once the next batch's loads are issued (a store at the batch end would
+  // hold up the next batch's wait for its records)
+  uint8_t* qbp = nullptr;
+  uint8_t qbv = 0u;
   for (int base = 0; base < n; base += 64) {
     if (dmk == ~0ull) break;
     if (CK && base > 0 && base % GSR_SPLIT_CH == 0 && base <= GSR_SPLIT_NCK * GSR_SPLIT_CH) {
@@ -266,23 +273,25 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(GSR_FWD_WPE,
     const int i = base + lane;
     const float4 r0 = n0, r1 = n1, r2 = n2, r3 = n3;
     const bool kc = kn;
-    kn = base + 64 + lane < n && kn_next;
+    kn = base + 64 + lane < n && ((kw_next >> qsh) & 1u);
+    const uint32_t gn = gi_next & gmask;
     if (kn) {
-      n0 = rec[gi_next].a;
-      n1 = rec[gi_next].b;
+      n0 = rec[gn].a;
+      n1 = rec[gn].b;
 #ifndef GSR_EXP_FWD_NOC
-      n2 = rec[gi_next].c;
+      n2 = rec[gn].c;
 #endif
 #ifdef GSR_EXP_NOCOL2
-      if (C2) n3 = make_float4(__uint_as_float(gi_next), 0.f, 0.f, 0.f);  // timing only: no col2 gather
+      if (C2) n3 = make_float4(__uint_as_float(gn), 0.f, 0.f, 0.f);  // timing only: no col2 gather
 #else
-      if (C2) n3 = make_float4(col2[3 * gi_next], col2[3 * gi_next + 1], col2[3 * gi_next + 2], 0.f);
+      if (C2) n3 = make_float4(col2[3 * gn], col2[3 * gn + 1], col2[3 * gn + 2], 0.f);
 #endif
     }
     if (base + 128 + lane < n) {
-      gi_next = sorted_gauss[range.x + base + 128 + lane] & gmask;
-      kn_next = qkeys == nullptr || ((qkeys[base + 128 + lane] >> qsh) & 1u);
+      gi_next = sorted_gauss[range.x + base + 128 + lane];
+      if (qkeys != nullptr) kw_next = qkeys[base + 128 + lane];
     }
+    if (qbp != nullptr) *qbp = qbv;
     bool keep = false;
     if (i < n) keep = qkeys ? kc : quadrant_hit(r0, r1, (float)qx0, (float)qy0);
     const unsigned long long bal = __ballot(keep);
@@ -355,10 +364,15 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(GSR_FWD_WPE,
     // candidate i blended any pixel of this quadrant (a pair the forward blended nowhere has no backward hit: same
     // alpha, power and position tests).  Batches past the quadrant's termination are never walked, and the backward
     // reads only below its deepest blend.
-    if (rs.qbytes != nullptr && i < n)
-      rs.qbytes[4 * ((size_t)rs.inst_start[v] + range.x + i) + q] = keep && ((hbm >> mask_rank(bal)) & 1ull) ? 1u : 0u;
+    if (rs.qbytes != nullptr && i < n) {
+      qbp = rs.qbytes + 4 * ((size_t)rs.inst_start[v] + range.x + i) + q;
+      qbv = keep && ((hbm >> mask_rank(bal)) & 1ull) ? 1u : 0u;
+    } else {
+      qbp = nullptr;
+    }
     __syncthreads();
   }
+  if (qbp != nullptr) *qbp = qbv;
   if (inside) {
     const size_t pid = (size_t)py * W + px;
     const size_t HW = (size_t)H * W;
@@ -576,7 +590,9 @@ __global__ __launch_bounds__(64) void k_render_fwd_tile(RenderSet rs, const uint
     n2 = rec[g0].c;
     if (C2) n3 = make_float4(col2[3 * g0], col2[3 * g0 + 1], col2[3 * g0 + 2], 0.f);
   }
-  if (64 + lane < n) gi_next = sorted_gauss[range.x + 64 + lane] & gmask;
+  // (gi_next stays raw until the next batch: masked right after its load, the wave would wait there for every
+  // load in flight, the records just issued included)
+  if (64 + lane < n) gi_next = sorted_gauss[range.x + 64 + lane];
   // quadrants with a pixel still blending (uniform)
   auto active_mask = [&]() -> uint32_t {
     uint32_t m = 0u;
@@ -588,16 +604,22 @@ __global__ __launch_bounds__(64) void k_render_fwd_tile(RenderSet rs, const uint
 #ifdef GSR_TIMELINE
   unsigned long long pc_eval = 0, pc_slot = 0;
 #endif
+  // the previous batch's cull byte, stored once the next batch's loads are issued (a store at the batch end would
+  // hold up the next batch's wait for its records)
+  uint8_t qbv = 0u;
+  int qbi = -1;
   for (int base = 0; base < n && qactive != 0u; base += 64) {
     const int i = base + lane;
     const float4 r0 = n0, r1 = n1, r2 = n2, r3 = n3;
     if (base + 64 + lane < n) {
-      n0 = rec[gi_next].a;
-      n1 = rec[gi_next].b;
-      n2 = rec[gi_next].c;
-      if (C2) n3 = make_float4(col2[3 * gi_next], col2[3 * gi_next + 1], col2[3 * gi_next + 2], 0.f);
+      const uint32_t gn = gi_next & gmask;
+      n0 = rec[gn].a;
+      n1 = rec[gn].b;
+      n2 = rec[gn].c;
+      if (C2) n3 = make_float4(col2[3 * gn], col2[3 * gn + 1], col2[3 * gn + 2], 0.f);
     }
-    if (base + 128 + lane < n) gi_next = sorted_gauss[range.x + base + 128 + lane] & gmask;
+    if (base + 128 + lane < n) gi_next = sorted_gauss[range.x + base + 128 + lane];
+    if (qbi >= 0) qbytes[qbi] = qbv;
     uint32_t m = 0u;
     if (i < n) {
 #pragma unroll
@@ -679,12 +701,13 @@ __global__ __launch_bounds__(64) void k_render_fwd_tile(RenderSet rs, const uint
     }
     // the backward's cull of this batch: candidate i's 4-bit mask of quadrants it blended in (batches past the last
     // blend are never read by it)
-    if (qbytes != nullptr && i < n)
-      qbytes[i] = (uint8_t)(((hb[0] >> lane) & 1ull) | (((hb[1] >> lane) & 1ull) << 1) |
-                            (((hb[2] >> lane) & 1ull) << 2) | (((hb[3] >> lane) & 1ull) << 3));
+    qbi = qbytes != nullptr && i < n ? i : -1;
+    qbv = (uint8_t)(((hb[0] >> lane) & 1ull) | (((hb[1] >> lane) & 1ull) << 1) | (((hb[2] >> lane) & 1ull) << 2) |
+                    (((hb[3] >> lane) & 1ull) << 3));
     __syncthreads();
     qactive = active_mask();
   }
+  if (qbi >= 0) qbytes[qbi] = qbv;
 #pragma unroll
   for (int q = 0; q < 4; ++q) {
     const int px = tx0 + (q & 1) * 8 + (lane & 7), py = ty0 + (q >> 1) * 8 + (lane >> 3);
