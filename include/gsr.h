@@ -413,6 +413,11 @@ int gsr_knn_mean_dist(int P, const float* points, float* mean_dist, void* worksp
 size_t gsr_sort_work_bytes(int V, const int* n);
 int gsr_sort_pairs(int V, const int* n, uint32_t* keys, uint32_t* vals, int key_bits, int max_bits, void* work,
                    size_t work_bytes, void* stream);
+/* How the sort's scatter ranks equal digits within a wave, decided once per process: 1 = LDS atomic adds (the device
+ * was found, by a probe kernel at the first call, to service one instruction's lanes that hit the same counter in lane
+ * order, which keeps the sort stable), 0 = ballot matching (the probe failed, or GSR_SORT_RANK=ballot).  Both give
+ * the same bits.  Runs the probe if it has not run yet (a device synchronisation). */
+int gsr_sort_rank_mode(void);
 
 /* Replaces markVisible/checkFrustum (API completeness; unused by the reference).  present (P,) u8. */
 int gsr_mark_visible(int P, const float* means3D, const float* viewmatrix, const float* projmatrix,

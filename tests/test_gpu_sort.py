@@ -76,3 +76,42 @@ def test_sort_pairs_all_equal_and_descending():
     ek, ev = _expect(keys, vals, sizes, 32)
     np.testing.assert_array_equal(gk, ek)
     np.testing.assert_array_equal(gv, ev)
+
+
+def test_rank_mode_probe_selects_lds_atomics():
+    """The scatter ranks equal digits with LDS atomic adds only after the once-per-process probe found the device
+    servicing same-counter lanes in lane order (gsr_sort.hip k_lds_rank_probe); on MI355X it does, so the fast
+    path is the one the other tests here check against numpy's stable sort."""
+    from diff_gaussian_rasterization import _C
+
+    assert _C.load_library().gsr_sort_rank_mode() == 1
+
+
+def test_ballot_ranks_give_the_same_bits(tmp_path):
+    """GSR_SORT_RANK=ballot (read once per process: a child process) sorts to the same bits as the default."""
+    import os
+    import subprocess
+    import sys
+
+    rng = np.random.default_rng(7)
+    sizes = [4096 * 2 + 5, 777, 12288]
+    keys = rng.integers(0, 64, size=sum(sizes), dtype=np.uint64).astype(np.uint32)
+    vals = np.arange(sum(sizes), dtype=np.uint32)
+    np.save(tmp_path / "k.npy", keys)
+    np.save(tmp_path / "v.npy", vals)
+    code = (
+        "import sys, numpy as np; sys.path[:0] = [%r, %r]; import test_gpu_sort as t; from diff_gaussian_rasterization "
+        "import _C; k = np.load(%r); v = np.load(%r); gk, gv = t._sort(k, v, %r, 32, 6); "
+        "np.save(%r, gk); np.save(%r, gv); print(_C.load_library().gsr_sort_rank_mode())"
+        % (os.path.dirname(os.path.abspath(__file__)),
+           os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "threestudio-3dgs_amd"),
+           str(tmp_path / "k.npy"), str(tmp_path / "v.npy"), sizes,
+           str(tmp_path / "bk.npy"), str(tmp_path / "bv.npy")))
+    env = dict(os.environ, GSR_SORT_RANK="ballot")
+    out = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=240,
+                         cwd=os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    assert out.returncode == 0, out.stderr[-2000:]
+    assert out.stdout.strip().splitlines()[-1] == "0"  # the child ranked by ballot matching
+    gk, gv = _sort(keys, vals, sizes, 32, 6)
+    np.testing.assert_array_equal(gk, np.load(tmp_path / "bk.npy"))
+    np.testing.assert_array_equal(gv, np.load(tmp_path / "bv.npy"))

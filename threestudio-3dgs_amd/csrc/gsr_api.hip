@@ -526,6 +526,8 @@ int gsr_sort_pairs(int V, const int* n, uint32_t* keys, uint32_t* vals, int key_
   return last_launch();
 }
 
+int gsr_sort_rank_mode(void) { return sort_rank_mode(); }
+
 int gsr_set_num_rendered_ex(int V, const void* geom, int P, int* num_rendered, int* num_visible, int* num_listed,
                             void* stream) {
   if (check_set(V, P) != GSR_OK) return GSR_EINVAL;

@@ -14,6 +14,9 @@ namespace gsr {
 // RADIX x (total 4096-item blocks) words, totals RADIX x V.
 int seg_sort(uint32_t* keys[2], uint32_t* vals[2], bool vals_identity, SegInfo seg, int bit_lo, int key_bits,
              uint32_t* counts, uint32_t* totals, hipStream_t stream, int max_bits = GSR_RADIX_BITS);
+// The scatter's in-wave ranking: 1 = LDS-atomic ranks (the device was probed to service same-counter lanes in lane
+// order), 0 = ballot matching.  Decided once per process (gsr_sort.hip).
+int sort_rank_mode();
 
 // Forward preprocess (cull, project, EWA, SH) of every (view, Gaussian) — gsr_preprocess.hip
 struct PreprocessArgs {

@@ -16,6 +16,8 @@
 // walks them in 16 rounds of 64; a lane's rank among equal digits comes from ballot matching,
 // the wave's running count per digit lives in LDS and is touched only by that wave, so the 16
 // rounds need no workgroup barrier.  Order (wave, round, lane) = index order -> stable.
+#include <cstdlib>
+#include <cstring>
 #include <type_traits>
 
 #include "gsr_kernels.h"
@@ -107,16 +109,15 @@ template <bool KV>
 struct ScatterLDS {
   uint32_t keys[GSR_SORT_TILE];
   uint32_t vals[KV ? GSR_SORT_TILE : 1];
-  uint32_t wcnt[4][GSR_RADIX];  // per-wave running count per digit -> per-wave offset within the digit
-  uint32_t local[GSR_RADIX];    // block-local start of each digit
-  uint32_t glob[GSR_RADIX];     // segment position of this block's first item of each digit
+  uint32_t wcnt[4][GSR_RADIX];  // per-wave running count per digit -> the wave's block-local start of the digit
+  uint32_t glob[GSR_RADIX];     // segment position of this block's first item of each digit, less its local start
   uint32_t wave[8];
 };
 
 // KV = false: keys only (packed tile keys); vals_in / vals_out unused.
 // (keys only: 5 waves per SIMD, 88 VGPRs without spills — the LDS allows 7 workgroups per CU, but at 6 waves the
 // 80-VGPR budget spills in the full-block path; with values the LDS allows 4; profiles/r05/ab_r05s5.txt)
-template <bool KV, int BITS>
+template <bool KV, int BITS, bool ATOMIC>
 __attribute__((amdgpu_waves_per_eu(KV ? 4 : 5, 8)))
 __global__ __launch_bounds__(GSR_SORT_THREADS) void k_seg_scatter(
     const uint32_t* __restrict__ keys_in, const uint32_t* __restrict__ vals_in, uint32_t* __restrict__ keys_out,
@@ -158,6 +159,10 @@ __global__ __launch_bounds__(GSR_SORT_THREADS) void k_seg_scatter(
     for (int k = 0; k < GSR_SORT_ITEMS; ++k) {
       const bool valid = FULL || b0 + k * 64 + lane < n;
       const uint32_t d = (seg_key(kb, key[k]) >> shift) & mask;
+    if (ATOMIC) {
+      const uint32_t pk = valid ? atomicAdd(&s.wcnt[w][d], 1u) : 0u;
+      pos2[k >> 1] = (k & 1) ? (pos2[k >> 1] | (pk << 16)) : pk;
+    } else {
       const unsigned long long peers = match_digit(d, bits, valid);
       const uint32_t rank = mask_rank(peers);
       // every lane reads its digit's running count, then the digit's first lane advances it.  The order across lanes
@@ -170,23 +175,29 @@ __global__ __launch_bounds__(GSR_SORT_THREADS) void k_seg_scatter(
       const uint32_t pk = base + rank;
       pos2[k >> 1] = (k & 1) ? (pos2[k >> 1] | (pk << 16)) : pk;
     }
+    }
     __syncthreads();
-    // per digit: wave offsets, block count, block-local start, segment position of the block's run
-    uint32_t bc = 0u;
+    // per digit: each wave's block-local start (the digit's block-local start + the earlier waves' counts) and the
+    // segment position of the block's run less its block-local start (one LDS read per item in each phase below)
+    uint32_t wc[4], bc = 0u;
     if (t < R) {
 #pragma unroll
       for (int ww = 0; ww < 4; ++ww) {
-        const uint32_t c = s.wcnt[ww][t];
-        s.wcnt[ww][t] = bc;
-        bc += c;
+        wc[ww] = s.wcnt[ww][t];
+        bc += wc[ww];
       }
     }
     uint32_t tot;
     const uint32_t lstart = block_exclusive_scan<GSR_SORT_THREADS>(bc, &tot, s.wave);
     const uint32_t dstart = block_exclusive_scan<GSR_SORT_THREADS>(dtot, &tot, s.wave);
     if (t < R) {
-      s.local[t] = lstart;
-      s.glob[t] = dstart + dcnt;
+      uint32_t run = lstart;
+#pragma unroll
+      for (int ww = 0; ww < 4; ++ww) {
+        s.wcnt[ww][t] = run;
+        run += wc[ww];
+      }
+      s.glob[t] = dstart + dcnt - lstart;
     }
     __syncthreads();
 #pragma unroll
@@ -194,7 +205,7 @@ __global__ __launch_bounds__(GSR_SORT_THREADS) void k_seg_scatter(
       if (FULL || b0 + k * 64 + lane < n) {
         uint32_t d = (seg_key(kb, key[k]) >> shift) & mask;
         asm volatile("" : "+v"(d));  // (recomputed, not kept from the ranking: 16 registers fewer)
-        const uint32_t lp = s.local[d] + s.wcnt[w][d] + ((pos2[k >> 1] >> (16 * (k & 1))) & 0xFFFFu);
+        const uint32_t lp = s.wcnt[w][d] + ((pos2[k >> 1] >> (16 * (k & 1))) & 0xFFFFu);
         s.keys[lp] = key[k];
         if (KV) s.vals[lp] = val[k];
       }
@@ -208,7 +219,7 @@ __global__ __launch_bounds__(GSR_SORT_THREADS) void k_seg_scatter(
       if (FULL || j < nv) {
         const uint32_t kk = s.keys[j];
         const uint32_t d = (seg_key(kb, kk) >> shift) & mask;
-        const uint32_t dst = start + s.glob[d] + (j - s.local[d]);
+        const uint32_t dst = start + s.glob[d] + j;
         keys_out[dst] = kk;
         if (KV) vals_out[dst] = s.vals[j];
       }
@@ -220,20 +231,83 @@ __global__ __launch_bounds__(GSR_SORT_THREADS) void k_seg_scatter(
     body(std::false_type{});
 }
 
+// In-wave ranks from LDS atomics (k_seg_scatter<.., ATOMIC = true>) are stable only if the LDS services one
+// instruction's lanes that hit the same counter in lane order — what gfx950 does (the GPU sort and parity tests
+// compare against stable sorts), but nothing the ISA promises.  So it is checked once per process on the device
+// (k_lds_rank_probe: 32 rounds of digit patterns — one counter for all lanes, runs, pairs, hashed — every lane's
+// returned count against its ballot-matched rank); if any lane disagrees, or GSR_SORT_RANK=ballot is set, every
+// pass ranks by ballot matching.
+#ifndef GSR_SORT_ATOMIC_MASK
+#define GSR_SORT_ATOMIC_MASK 3  // bits 0 / 1: keys-only first / later passes, bits 2 / 3: key-value first / later
+#endif
+
+__global__ __launch_bounds__(256) void k_lds_rank_probe(uint32_t* __restrict__ bad) {
+  __shared__ uint32_t cnt[4][64];
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  cnt[w][lane] = 0u;
+  __syncthreads();
+  uint32_t err = 0u;
+  for (int r = 0; r < 32; ++r) {
+    const uint32_t h = ((uint32_t)lane * 0x9E3779B1u) ^ ((uint32_t)r * 0x85EBCA6Bu);
+    uint32_t d;
+    switch (r & 3) {
+      case 0: d = (uint32_t)r & 63u; break;                       // every lane one counter
+      case 1: d = ((uint32_t)lane >> (r & 7)) & 63u; break;       // runs of 2^k lanes
+      case 2: d = ((uint32_t)lane & ((r >> 2) & 7u)) & 63u; break;  // interleaved peers
+      default: d = (h >> 26) & 63u; break;                        // hashed
+    }
+    const uint32_t got = atomicAdd(&cnt[w][d], 1u);
+    const unsigned long long peers = match_digit(d, 6, true);
+    const uint32_t first = (uint32_t)__shfl((int)got, (int)__builtin_ctzll(peers), 64);
+    err |= (got - first) != mask_rank(peers) ? 1u : 0u;
+  }
+  if (err) atomicOr(bad, 1u);
+}
+
+// 1: LDS-atomic ranks in use, 0: ballot matching (probe failed, or GSR_SORT_RANK=ballot); decided once per process
+int sort_rank_mode() {
+  static const int mode = [] {
+    const char* e = getenv("GSR_SORT_RANK");
+    if (e != nullptr && strcmp(e, "ballot") == 0) return 0;
+    uint32_t* d = nullptr;
+    uint32_t h = 1u;
+    if (hipMalloc(&d, sizeof(uint32_t)) != hipSuccess) return 0;
+    bool ok = hipMemset(d, 0, sizeof(uint32_t)) == hipSuccess;
+    if (ok) {
+      hipLaunchKernelGGL(k_lds_rank_probe, dim3(1), dim3(256), 0, 0, d);
+      ok = hipGetLastError() == hipSuccess && hipMemcpy(&h, d, sizeof(uint32_t), hipMemcpyDeviceToHost) == hipSuccess;
+    }
+    (void)hipFree(d);
+    return ok && h == 0u ? 1 : 0;
+  }();
+  return mode;
+}
 template <int BITS>
-static void launch_pass(bool kv, const uint32_t* kin, const uint32_t* vin, uint32_t* kout, uint32_t* vout,
+static void launch_pass(bool kv, int pass, const uint32_t* kin, const uint32_t* vin, uint32_t* kout, uint32_t* vout,
                         const SegInfo& seg, uint32_t nb, int shift, int bits, int last, uint32_t* counts,
                         uint32_t* totals, hipStream_t stream) {
   hipLaunchKernelGGL(k_seg_count<0>, dim3(nb), dim3(GSR_SORT_THREADS), 0, stream, kin, seg, shift, bits, last,
                      counts);
   hipLaunchKernelGGL(k_seg_scan, dim3(seg.V << bits), dim3(256), 0, stream, seg, 1 << bits, last, counts, totals);
-  if (kv)
-    hipLaunchKernelGGL((k_seg_scatter<true, BITS>), dim3(nb), dim3(GSR_SORT_THREADS), 0, stream, kin, vin, kout,
-                       vout, seg, shift, bits, last, (const uint32_t*)counts, (const uint32_t*)totals);
-  else
-    hipLaunchKernelGGL((k_seg_scatter<false, BITS>), dim3(nb), dim3(GSR_SORT_THREADS), 0, stream, kin,
-                       (const uint32_t*)nullptr, kout, (uint32_t*)nullptr, seg, shift, bits, last,
-                       (const uint32_t*)counts, (const uint32_t*)totals);
+  const int sel = (pass == 0 ? 1 : 2) << (kv ? 2 : 0);
+  const bool atomic = (GSR_SORT_ATOMIC_MASK & sel) != 0 && sort_rank_mode() == 1;
+  const uint32_t* cc = counts;
+  const uint32_t* tt = totals;
+  if (kv) {
+    if (atomic)
+      hipLaunchKernelGGL((k_seg_scatter<true, BITS, true>), dim3(nb), dim3(GSR_SORT_THREADS), 0, stream, kin, vin, kout,
+                         vout, seg, shift, bits, last, cc, tt);
+    else
+      hipLaunchKernelGGL((k_seg_scatter<true, BITS, false>), dim3(nb), dim3(GSR_SORT_THREADS), 0, stream, kin, vin,
+                         kout, vout, seg, shift, bits, last, cc, tt);
+  } else {
+    if (atomic)
+      hipLaunchKernelGGL((k_seg_scatter<false, BITS, true>), dim3(nb), dim3(GSR_SORT_THREADS), 0, stream, kin,
+                         (const uint32_t*)nullptr, kout, (uint32_t*)nullptr, seg, shift, bits, last, cc, tt);
+    else
+      hipLaunchKernelGGL((k_seg_scatter<false, BITS, false>), dim3(nb), dim3(GSR_SORT_THREADS), 0, stream, kin,
+                         (const uint32_t*)nullptr, kout, (uint32_t*)nullptr, seg, shift, bits, last, cc, tt);
+  }
 }
 
 int seg_sort(uint32_t* keys[2], uint32_t* vals[2], bool vals_identity, SegInfo seg, int bit_lo, int key_bits,
@@ -252,13 +326,13 @@ int seg_sort(uint32_t* keys[2], uint32_t* vals[2], bool vals_identity, SegInfo s
       const uint32_t* vin = (p == 0 && vals_identity) ? nullptr : (kv ? vals[src] : nullptr);
       uint32_t* vout = kv ? vals[dst] : nullptr;
       if (bits == 8)
-        launch_pass<8>(kv, keys[src], vin, keys[dst], vout, seg, nb, shift, bits, last, counts, totals, stream);
+        launch_pass<8>(kv, p, keys[src], vin, keys[dst], vout, seg, nb, shift, bits, last, counts, totals, stream);
       else if (bits == 6)
-        launch_pass<6>(kv, keys[src], vin, keys[dst], vout, seg, nb, shift, bits, last, counts, totals, stream);
+        launch_pass<6>(kv, p, keys[src], vin, keys[dst], vout, seg, nb, shift, bits, last, counts, totals, stream);
       else if (bits == 4)
-        launch_pass<4>(kv, keys[src], vin, keys[dst], vout, seg, nb, shift, bits, last, counts, totals, stream);
+        launch_pass<4>(kv, p, keys[src], vin, keys[dst], vout, seg, nb, shift, bits, last, counts, totals, stream);
       else
-        launch_pass<0>(kv, keys[src], vin, keys[dst], vout, seg, nb, shift, bits, last, counts, totals, stream);
+        launch_pass<0>(kv, p, keys[src], vin, keys[dst], vout, seg, nb, shift, bits, last, counts, totals, stream);
     }
     src = dst;
   }

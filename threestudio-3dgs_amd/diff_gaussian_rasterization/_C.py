@@ -64,6 +64,7 @@ SIGNATURES = {
                                  + [ctypes.POINTER(_f)] * 2 + [_vp] * 8 + [_vp]),
     "gsr_sort_work_bytes": (_sz, [_i, ctypes.POINTER(_i)]),
     "gsr_sort_pairs": (_i, [_i, ctypes.POINTER(_i), _vp, _vp, _i, _i, _vp, _sz, _vp]),
+    "gsr_sort_rank_mode": (_i, []),
     "gsr_knn_workspace_bytes": (_sz, [_i]),
     "gsr_knn_mean_dist": (_i, [_i, _vp, _vp, _vp, _sz, _vp]),
     "gsr_set_geom_bytes": (_sz, [_i, _i]),
