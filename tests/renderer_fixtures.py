@@ -11,6 +11,8 @@ light material's fields, material/gaussian_material.py:17-41), ``background_tens
     shading       renderer/diff_gaussian_rasterizer_shading.py:79-231 (Depth2Normal + material: the
                   tests/torch_reference.shading_epilogue restatement)
     sugar_normal  renderer/diff_sugar_rasterizer_normal.py:80-223
+    sugar_shading renderer/diff_sugar_rasterizer_shading.py:80-224 (the point-light material restated:
+                  point_light_material below)
 
 The per-view rasterizer call goes through ``RASTERIZE`` (GaussianRasterizer on the GPU); the CPU tests
 swap it for the torch formulation (tests/torch_reference.render) together with the batch renderer's
@@ -147,6 +149,23 @@ class FakeGeometry:
     get_normal = property(lambda self: self.params["normals"])
 
 
+def point_light_material(positions, shading_normal, light_positions, albedo, ka, kd, shading):
+    """material/gaussian_material.py:41-104 (GaussianDiffuseWithPointLightMaterial.forward) with the light colours
+    and shading mode the material would draw (batch_renderer.material_params, same draws in the same order)."""
+    F = torch.nn.functional
+    ka = torch.tensor(ka, dtype=albedo.dtype, device=albedo.device)
+    kd = torch.tensor(kd, dtype=albedo.dtype, device=albedo.device)
+    light_directions = F.normalize(light_positions - positions, dim=-1)
+    diffuse_light = torch.sum(shading_normal * light_directions, -1, keepdim=True).clamp(min=0.0) * kd
+    textureless_color = diffuse_light + ka
+    color = albedo.clamp(0.0, 1.0) * textureless_color
+    if shading == "albedo":
+        return albedo + textureless_color * 0
+    if shading == "textureless":
+        return albedo * 0 + textureless_color
+    return color
+
+
 def _background_net(dirs):
     """Per-ray background colours (stands in for the background MLP: (n, H, W, 3) -> (n, H, W, 3))."""
     return torch.sigmoid(2.0 * dirs)
@@ -171,7 +190,7 @@ class FakeRenderer(GaussianBatchRenderer):
     # the reference's per-view DiffGaussian.forward of each mode
     def forward(self, cam, bg_color, scaling_modifier=1.0, override_color=None, **kwargs):
         pc = self.geometry
-        if self.mode in ("background", "shading"):
+        if self.mode in ("background", "shading", "sugar_shading"):
             bg_color = bg_color * 0
         else:  # renderer/diff_gaussian_rasterizer.py:59-64
             invert = (np.random.rand() > self.cfg.invert_bg_prob) if self.training else True
@@ -227,6 +246,27 @@ class FakeRenderer(GaussianBatchRenderer):
             nmap = torch.where(mask.expand_as(nmap), nmap, nmap.detach())
             depth = torch.where(mask, depth, depth.detach())
             pkg.update(render=img.clamp(0, 1), normal=nmap, normal_from_dist=nmap_dist, mask=alpha, depth=depth)
+        elif self.mode == "sugar_shading":
+            # renderer/diff_sugar_rasterizer_shading.py:170-213
+            rays_d, rays_o = kwargs["rays_d"][b], kwargs["rays_o"][b]
+            if kwargs.get("override_bg_color") is not None:
+                comp_rgb_bg = kwargs["override_bg_color"].expand(1, H, W, -1)
+            else:
+                comp_rgb_bg = self.background(dirs=rays_d.unsqueeze(0))
+            xyz_map = rays_o + depth.permute(1, 2, 0) * rays_d
+            kw2 = dict(kw, means2D=torch.zeros_like(sp), shs=None, colors_precomp=pc.get_gs_normals)
+            normal_map, _, _, _ = RASTERIZE(settings, **kw2)
+            normal_map = torch.nn.functional.normalize(normal_map, dim=0)
+            light = kwargs["light_positions"][b, None, None, :].expand(H, W, -1)
+            ka, kd, smode = material_params(self.material, self.training)
+            rgb_fg = point_light_material(xyz_map, normal_map.permute(1, 2, 0), light,
+                                          (img / (alpha + 1e-6)).permute(1, 2, 0), ka, kd, smode).permute(2, 0, 1)
+            img = rgb_fg * alpha + (1 - alpha) * comp_rgb_bg.reshape(H, W, 3).permute(2, 0, 1)
+            normal_map = normal_map * 0.5 * alpha + 0.5
+            mask = alpha > 0.99
+            normal_map = torch.where(mask.repeat(3, 1, 1), normal_map, normal_map.detach())
+            depth = torch.where(mask, depth, depth.detach())
+            pkg.update(render=img.clamp(0, 1), normal=normal_map, mask=alpha, depth=depth, comp_rgb_bg=comp_rgb_bg)
         return pkg
 
 

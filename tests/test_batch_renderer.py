@@ -49,7 +49,7 @@ def _run(renderer, batch):
 
 
 def _mode_scene(mode):
-    if mode == "sugar_normal":
+    if mode in ("sugar_normal", "sugar_shading"):
         sc = gs.make_sugar_scene(1, sh_degree=0, seed=2)
         sc["shs"] = sc["shs"][:, :1]
         return sc
@@ -58,10 +58,10 @@ def _mode_scene(mode):
 
 @pytest.mark.parametrize("mode,training,pred_normal", [
     ("plain", False, False), ("background", False, False), ("advanced", False, False), ("shading", False, False),
-    ("normal", False, False), ("sugar_normal", False, False),
+    ("normal", False, False), ("sugar_normal", False, False), ("sugar_shading", False, False),
     # training: the per-view random draws (background inversion; soft-shading ambient ratio and shading mode)
     ("plain", True, False), ("advanced", True, False), ("normal", True, False), ("shading", True, False),
-    ("sugar_normal", True, False),
+    ("sugar_normal", True, False), ("sugar_shading", True, False),
     # the predicted-normal second pass (renderer/diff_gaussian_rasterizer_shading.py:177-197, _normal.py:175-185)
     ("shading", True, True), ("normal", False, True),
 ])
@@ -106,6 +106,8 @@ def test_mode_detection():
     assert br.batch_mode(Plain()) == "advanced"
     Plain.__module__ = "threestudio_3dgs.renderer.diff_gaussian_rasterizer_normal"
     assert br.batch_mode(Plain()) == "normal"
+    Plain.__module__ = "threestudio_3dgs.renderer.diff_sugar_rasterizer_shading"
+    assert br.batch_mode(Plain()) == "sugar_shading"
     Plain.__module__ = "threestudio_3dgs.renderer.diff_sugar_rasterizer_temporal"
     assert br.batch_mode(Plain()) is None  # keeps the per-view loop
     p = Plain()
@@ -178,6 +180,7 @@ def _reduce_worker(rank, world, port, tmp, B, mode, pred_normal):
     (2, 3, "shading", True),       # main + predicted-normal call: one reduction after both
     (2, 1, "normal", True),        # ... and a view-less rank joining it
     (2, 1, "sugar_normal", False),  # two colour sets (colors2 gradient in the reduction)
+    (2, 3, "sugar_shading", False),  # ... with the material on the blended normals, views split 2 / 1
 ])
 def test_grad_reduce_with_viewless_ranks(world, B, mode, pred_normal, tmp_path, monkeypatch):
     """renderer.grad_reduce (the per-Gaussian gradients summed over ranks inside the rasterizer's backward) with

@@ -29,7 +29,7 @@ H, W = 96, 128
 
 
 def _scene(mode):
-    if mode == "sugar_normal":
+    if mode in ("sugar_normal", "sugar_shading"):
         s = gs.make_sugar_scene(4, sh_degree=0, seed=2)
         s["shs"] = s["shs"][:, :1]
         return s
@@ -45,9 +45,10 @@ def _close(a, b, tol, what):
 
 @pytest.mark.parametrize("mode,training,pred_normal", [
     ("plain", False, False), ("background", False, False), ("advanced", False, False), ("shading", False, False),
-    ("normal", False, False), ("sugar_normal", False, False),
+    ("normal", False, False), ("sugar_normal", False, False), ("sugar_shading", False, False),
     # training: per-view background inversion / soft-shading ambient ratio and shading mode, drawn as the loop does
     ("plain", True, False), ("advanced", True, False), ("shading", True, False), ("normal", True, False),
+    ("sugar_shading", True, False),
     # the predicted-normal second pass, both paths
     ("shading", True, True), ("normal", False, True),
 ])

@@ -22,10 +22,13 @@ renderer's epilogue fused on the GPU:
                                                                          Depth2Normal map + masked depth
     "sugar_normal"  renderer/diff_sugar_rasterizer_normal.py:80-223      two passes (colours, face normals)
                                                                          + normal-from-distance (gsr_shade_*)
+    "sugar_shading" renderer/diff_sugar_rasterizer_shading.py:80-224     two passes (colours, face normals) +
+                                                                         point-light material on the blended
+                                                                         normals + composite (batched torch)
 
 The mode comes from the renderer's ``batch_render_mode`` attribute or, when unset, from the module the
-renderer class is defined in (the reference's file names above).  Any other renderer (st, temporal, sugar
-shading) keeps the reference's per-view loop, still on the HIP rasterizer.
+renderer class is defined in (the reference's file names above).  Any other renderer (st, temporal) keeps the
+reference's per-view loop, still on the HIP rasterizer.
 
 With ``torch.distributed`` initialised, every rank renders its contiguous slice of the batch
 (view_shard.shard_range) and the image outputs are all-gathered (RCCL over xGMI); the per-view lists
@@ -53,7 +56,7 @@ from .cameras import get_cam_info_gaussian
 from . import view_shard
 from .view_shard import _world, all_gather_views, shard_range
 
-MODES = ("plain", "background", "advanced", "shading", "normal", "sugar_normal")
+MODES = ("plain", "background", "advanced", "shading", "normal", "sugar_normal", "sugar_shading")
 _MODULE_MODES = {
     "diff_gaussian_rasterizer": "plain",
     "diff_gaussian_rasterizer_background": "background",
@@ -61,9 +64,13 @@ _MODULE_MODES = {
     "diff_gaussian_rasterizer_shading": "shading",
     "diff_gaussian_rasterizer_normal": "normal",
     "diff_sugar_rasterizer_normal": "sugar_normal",
+    "diff_sugar_rasterizer_shading": "sugar_shading",
 }
 # modes whose renderer draws a background inversion per view / calls the material per view
 _INVERT_BG = ("plain", "advanced", "normal", "sugar_normal")
+_MATERIAL = ("shading", "sugar_shading")
+# modes whose second rasterizer call blends the face normals (the second colour set of one call)
+_TWO_COLOR = ("sugar_normal", "sugar_shading")
 # batch dict image keys of the reference (renderer/gaussian_batch_renderer.py:78-121) -> channels
 _OUT_KEYS = (("comp_rgb", 3), ("comp_normal", 3), ("comp_normal_from_dist", 3), ("comp_pred_normal", 3),
              ("comp_depth", 1), ("comp_mask", 1))
@@ -108,6 +115,12 @@ def _depth_normal_views(*args, **kwargs):
     from .shading import depth_normal_views
 
     return depth_normal_views(*args, **kwargs)
+
+
+def _sugar_shade_views(*args, **kwargs):
+    from .shading import sugar_shade_views
+
+    return sugar_shade_views(*args, **kwargs)
 
 
 def _sugar_normal_map(*args, **kwargs):
@@ -170,11 +183,11 @@ def _inverted_bgs(renderer, n):
 def batch_draws(renderer, mode: str, bs: int) -> dict:
     """The random draws the reference's per-view loop makes for a batch of `bs` views, in view order:
     "bgs" (per-view background colour) for the modes that invert it, "lights" (per-view (ka, kd, shading))
-    for the shading mode.  Every rank makes all of them and keeps its slice."""
+    for the modes that call the material.  Every rank makes all of them and keeps its slice."""
     out = {}
     if mode in _INVERT_BG:
         out["bgs"] = _inverted_bgs(renderer, bs)
-    if mode == "shading":
+    if mode in _MATERIAL:
         out["lights"] = [material_params(renderer.material, renderer.training) for _ in range(bs)]
     return out
 
@@ -224,7 +237,7 @@ def _reduce_tensors(pc, mode, override, means3D, shs, common, normals):
     predicted-normal call when that reduction runs once after both calls.  Only tensors requiring grad."""
     pairs = [("means3D", means3D), ("shs", shs), ("override", override), ("opacities", common["opacities"]),
              ("scales", common["scales"]), ("rotations", common["rotations"])]
-    if mode == "sugar_normal":
+    if mode in _TWO_COLOR:
         pairs.append(("colors2", pc.get_gs_normals))
     if normals is not None:
         pairs.append(("normals", normals))
@@ -348,6 +361,24 @@ def render_views_local(renderer, batch: dict, mode: str, lo: int, hi: int, draws
             mask = alpha > 0.99
             out.update(comp_rgb=color.clamp(0, 1), comp_normal=nmap,
                        comp_depth=torch.where(mask, depth, depth.detach()), comp_mask=alpha)
+        elif mode == "sugar_shading":
+            zero = [renderer.background_tensor * 0] * n
+            settings = _settings(pc, cams, zero, H, W, scaling_modifier)
+            # the renderer's two calls (:158-167 colours or SH, :183-192 face normals with a zero means2D) from one
+            # geometry, sort and blend
+            color, radii, depth, alpha, normal = _rasterize_views(settings, means3D, m2, shs=shs,
+                                                                  colors_precomp=override,
+                                                                  colors2=pc.get_gs_normals, **common_main)
+            rays_o, rays_d = batch["rays_o"][lo:hi], batch["rays_d"][lo:hi]
+            if batch.get("override_bg_color") is not None:
+                bg_img = batch["override_bg_color"].reshape(1, 1, 1, 3).expand(n, H, W, 3)
+            else:
+                bg_img = renderer.background(dirs=rays_d).reshape(n, H, W, 3)
+            lights = draws["lights"]
+            render, nmap, depth_m = _sugar_shade_views(color, depth, alpha, normal, rays_o, rays_d, bg_img,
+                                                       batch["light_positions"][lo:hi], [x[0] for x in lights],
+                                                       [x[1] for x in lights], [x[2] for x in lights])
+            out.update(comp_rgb=render, comp_normal=nmap, comp_depth=depth_m, comp_mask=alpha, comp_rgb_bg=bg_img)
         else:
             raise ValueError(f"unknown mode {mode!r}")
     out["viewspace_points"] = m2
@@ -360,7 +391,8 @@ def _mode_keys(renderer, mode):
     keys = {"plain": ["comp_rgb"], "background": ["comp_rgb"], "advanced": ["comp_rgb", "comp_depth", "comp_mask"],
             "shading": ["comp_rgb", "comp_normal", "comp_depth", "comp_mask"],
             "normal": ["comp_rgb", "comp_normal", "comp_depth", "comp_mask"],
-            "sugar_normal": ["comp_rgb", "comp_normal", "comp_depth", "comp_mask"]}[mode]
+            "sugar_normal": ["comp_rgb", "comp_normal", "comp_depth", "comp_mask"],
+            "sugar_shading": ["comp_rgb", "comp_normal", "comp_depth", "comp_mask"]}[mode]
     if mode in ("shading", "normal") and getattr(renderer.geometry.cfg, "pred_normal", False):
         keys.append("comp_pred_normal")
     return keys
@@ -395,7 +427,7 @@ def render_batch(renderer, batch: dict, mode: str, group=None, shard: bool = Tru
             img = torch.empty((0, channels[key], H, W), device=dev, dtype=dtype, requires_grad=True)
         full = all_gather_views(img, bs, group) if world > 1 else img
         outputs[key] = full.permute(0, 2, 3, 1)
-    if mode == "shading":
+    if mode in _MATERIAL:
         bgl = local.get("comp_rgb_bg")
         if bgl is None:
             bgl = torch.empty((0, H, W, 3), device=dev, dtype=dtype)

@@ -223,3 +223,44 @@ def sugar_normal_map(normal, alpha):
         normal, alpha = normal.unsqueeze(0), alpha.unsqueeze(0)
     out = _NormalMap.apply(normal, alpha)
     return out[0] if single else out
+
+
+def sugar_shade_views(color, depth, alpha, normal, rays_o, rays_d, bg, light_positions, ambient, diffuse, shading):
+    """The SuGaR shading renderer's epilogue over a view set (renderer/diff_sugar_rasterizer_shading.py:170-213):
+    positions X = rays_o + depth rays_d; shading normal = F.normalize of the second call's blended face normals
+    (differentiated: the material's gradient reaches the normals, unlike the MVDream renderer's detached
+    predicted normal, so this is not the HIP shading pass); the point-light material of
+    material/gaussian_material.py:41-104 with the view's drawn (ka, kd, shading); the composite
+    ``fg alpha + (1 - alpha) bg``; the normal map ``n 0.5 alpha + 0.5`` and depth, detached where alpha <= 0.99.
+    Batched torch ops over the views (one call per set instead of the reference's ~30 per view).
+    color / normal (V, 3, H, W), depth / alpha (V, 1, H, W), rays (V, H, W, 3), bg (V, H, W, 3), light (V, 3);
+    ambient / diffuse: V triples, shading: V of "diffuse" | "albedo" | "textureless".
+    Returns render clamped to [0, 1] (V, 3, H, W), normal map (V, 3, H, W), depth (V, 1, H, W)."""
+    import torch.nn.functional as F
+
+    V = depth.shape[0]
+    dt, dev = depth.dtype, depth.device
+    xyz = rays_o + depth.permute(0, 2, 3, 1) * rays_d
+    nrm = F.normalize(normal, dim=1)
+    s = nrm.permute(0, 2, 3, 1)
+    albedo = (color / (alpha + 1e-6)).permute(0, 2, 3, 1)
+    lp = light_positions.reshape(V, 1, 1, 3)
+    ka = torch.tensor(ambient, dtype=dt, device=dev).reshape(V, 1, 1, 3)
+    kd = torch.tensor(diffuse, dtype=dt, device=dev).reshape(V, 1, 1, 3)
+    light_dir = F.normalize(lp - xyz, dim=-1)
+    diffuse_light = torch.sum(s * light_dir, -1, keepdim=True).clamp(min=0.0) * kd
+    textureless = diffuse_light + ka
+    shaded = albedo.clamp(0.0, 1.0) * textureless
+    # per view, the material's return for its shading mode ("+ x * 0" as the material writes it)
+    outs = {"albedo": albedo + textureless * 0, "textureless": albedo * 0 + textureless, "diffuse": shaded}
+    for m in set(shading):
+        if m not in outs:
+            raise ValueError(f"Unknown shading type {m}")
+    sel = [torch.tensor([m == k for m in shading], device=dev).reshape(V, 1, 1, 1) for k in ("albedo", "textureless")]
+    fg = torch.where(sel[0], outs["albedo"], torch.where(sel[1], outs["textureless"], outs["diffuse"]))
+    render = fg.permute(0, 3, 1, 2) * alpha + (1 - alpha) * bg.permute(0, 3, 1, 2)
+    nmap = nrm * 0.5 * alpha + 0.5
+    mask = alpha > 0.99
+    nmap = torch.where(mask.expand_as(nmap), nmap, nmap.detach())
+    depth_m = torch.where(mask, depth, depth.detach())
+    return render.clamp(0, 1), nmap, depth_m
