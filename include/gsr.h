@@ -61,8 +61,10 @@ const char* gsr_version(void);
  *      gsr_set_backward_chunks / gsr_grad_chunk_range (per-Gaussian sums in ranges, events for overlap).
  *   4  gsr_set_image_bytes_ex (image buffers sized for the forward's split decision, which the buffer records);
  *      gsr_profile_kernel (the blend kernels the phases ran).
+ *   5  gsr_sort_work_bytes / gsr_sort_pairs / gsr_sort_rank_mode (the library's sort, for tests);
+ *      gsr_set_preprocess_ex (the two-colour render's second colours written into the records).
  */
-#define GSR_ABI_VERSION 4
+#define GSR_ABI_VERSION 5
 int gsr_abi_version(void);
 /* Message of the last failing call on this thread ("" if none). */
 const char* gsr_last_error(void);
@@ -158,6 +160,18 @@ int gsr_set_preprocess(int V, int P, int degree, int M, const float* means3D, co
                        const float* const* viewmatrices, const float* const* projmatrices,
                        const float* const* campos, const float* tanfovx, const float* tanfovy,
                        int width, int height, int prefiltered, int* radii, void* geom, void* stream);
+/* As gsr_set_preprocess, for a set that gsr_set_render_two_colors will blend with colors2 (P, 3) as the second
+ * colour set (the SuGaR renderers' second rasterizer call): the preprocess writes each Gaussian's second colour
+ * into the per-(view, Gaussian) record it writes anyway (no extra traffic), so the two-colour blends read it with
+ * the record instead of gathering it from colors2 apart.  A two-colour call given another colors2 array reads
+ * that array (the set remembers which pointer it embedded).  colors2 NULL = gsr_set_preprocess. */
+int gsr_set_preprocess_ex(int V, int P, int degree, int M, const float* means3D, const float* scales,
+                          float scale_modifier, const float* rotations, const float* opacities, const float* shs,
+                          const float* colors_precomp, const float* cov3D_precomp,
+                          const float* const* viewmatrices, const float* const* projmatrices,
+                          const float* const* campos, const float* tanfovx, const float* tanfovy,
+                          int width, int height, int prefiltered, int* radii, void* geom, const float* colors2,
+                          void* stream);
 /* One D2H read of every view's K (and visible count, may be NULL); synchronises `stream`.
  * K = the reference's num_rendered (tiles of every visible Gaussian's 3-sigma rectangle): the
  * capacity the binning and backward scratch are sized by. */

@@ -612,7 +612,9 @@ def test_second_colors_match_separate_call(bwd, monkeypatch):
 def test_two_color_backward_groups_and_sets_bitwise(monkeypatch):
     """The one-pass two-colour backward (gsr_set_backward_two_colors) walked in view groups that fit a small
     work buffer, and over several view sets (accumulate: dL/dcolors2 and the running dL/dcov3D continue in
-    view order): bitwise the gradients of one group / one set."""
+    view order): bitwise the gradients of one group / one set.  And the second colours read from the records the
+    preprocess embedded them in (gsr_set_preprocess_ex, the default) against gathered from colors2 apart: the same
+    images and gradients, bit for bit."""
     import torch
 
     from diff_gaussian_rasterization import batched
@@ -634,20 +636,26 @@ def test_two_color_backward_groups_and_sets_bitwise(monkeypatch):
                                                  scales=t["scales"], rotations=t["rotations"], colors2=t["normals"])
         ((c * ups[0]).sum() + (d * ups[1][:, :1]).sum() + (a * ups[1][:, 1:2]).sum() + (c2 * ups[2]).sum()).backward()
         torch.cuda.synchronize()
-        return [m.grad.clone() for m in m2], {k: v.grad.clone() for k, v in t.items()}
+        return [m.grad.clone() for m in m2], {k: v.grad.clone() for k, v in t.items()}, (c, d, a, c2)
 
-    m2_one, g_one = run()
+    m2_one, g_one, o_one = run()
     with monkeypatch.context() as mp:
         mp.setattr(batched, "WORK_BUDGET", 1)  # one view per group
-        m2_grp, g_grp = run()
+        m2_grp, g_grp, _ = run()
     with monkeypatch.context() as mp:
         mp.setattr(batched, "SET_MAX", 2)  # three sets of two views
-        m2_set, g_set = run()
-    for other, what in ((g_grp, "groups"), (g_set, "sets")):
+        m2_set, g_set, _ = run()
+    with monkeypatch.context() as mp:
+        mp.setattr(batched, "EMBED_COLORS2", False)  # the blends gather colors2 apart
+        m2_gat, g_gat, o_gat = run()
+    for x, y in zip(o_one, o_gat):
+        assert torch.equal(x, y), "embedded vs gathered second colours: images"
+    for other, what in ((g_grp, "groups"), (g_set, "sets"), (g_gat, "gathered colors2")):
         for k in g_one:
             assert torch.equal(g_one[k], other[k]), f"{what}: grad {k}"
     for v in range(6):
         assert torch.equal(m2_one[v], m2_grp[v]) and torch.equal(m2_one[v], m2_set[v]), f"means2D {v}"
+        assert torch.equal(m2_one[v], m2_gat[v]), f"means2D {v} (gathered colors2)"
 
 
 def test_two_color_backward_with_fused_composite():

@@ -234,6 +234,17 @@ int gsr_set_preprocess(int V, int P, int degree, int M, const float* means3D, co
                        const float* const* projmatrices, const float* const* campos, const float* tanfovx,
                        const float* tanfovy, int width, int height, int prefiltered, int* radii, void* geom,
                        void* stream) {
+  return gsr_set_preprocess_ex(V, P, degree, M, means3D, scales, scale_modifier, rotations, opacities, shs,
+                               colors_precomp, cov3D_precomp, viewmatrices, projmatrices, campos, tanfovx, tanfovy,
+                               width, height, prefiltered, radii, geom, nullptr, stream);
+}
+
+int gsr_set_preprocess_ex(int V, int P, int degree, int M, const float* means3D, const float* scales,
+                          float scale_modifier, const float* rotations, const float* opacities, const float* shs,
+                          const float* colors_precomp, const float* cov3D_precomp, const float* const* viewmatrices,
+                          const float* const* projmatrices, const float* const* campos, const float* tanfovx,
+                          const float* tanfovy, int width, int height, int prefiltered, int* radii, void* geom,
+                          const float* colors2, void* stream) {
   (void)prefiltered;
   if (check_set(V, P) != GSR_OK) return GSR_EINVAL;
   if (width <= 0 || height <= 0) return fail(GSR_EINVAL, "%s", "image size must be positive");
@@ -271,6 +282,7 @@ int gsr_set_preprocess(int V, int P, int degree, int M, const float* means3D, co
   a.W = width;
   a.H = height;
   a.radii = radii;
+  a.col2 = colors2;
   {
     PhaseScope ps(GSR_PHASE_PREPROCESS, s);
     launch_preprocess(a, cams, g, s);
@@ -611,6 +623,7 @@ static int set_render(int V, int P, const int* K, int width, int height, const f
     rs.ccolor = nullptr;
     rs.dcbg = nullptr;
     rs.col2 = colors2;
+    rs.col2_rec = g.drange + 130;
     rs.out_col2 = out_color2;
     rs.dpix2 = nullptr;
     rs.order = img.order;
@@ -746,6 +759,7 @@ static int set_backward(int V, int P, int degree, int M, const int* K, int width
     rs.ccolor = color ? color + (size_t)g0 * 3 * HW : nullptr;
     rs.dcbg = dL_dbg ? dL_dbg + (size_t)g0 * HW * 3 : nullptr;
     rs.col2 = two ? colors2 : colors_override;
+    rs.col2_rec = g.drange + 130;
     rs.out_col2 = nullptr;
     rs.dpix2 = two ? dL_dcolor2 + (size_t)g0 * 3 * HW : nullptr;
     rs.order = img.order;

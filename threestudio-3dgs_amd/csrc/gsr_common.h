@@ -11,7 +11,7 @@
     (defined(GSR_EXP_COALROWS) || defined(GSR_EXP_FWD_NOC) || defined(GSR_EXP_LDSPAD) ||                  \
      defined(GSR_EXP_NOCULL) || defined(GSR_EXP_NOFLUSH) || defined(GSR_EXP_NOGROUP) ||                   \
      defined(GSR_EXP_NOMFMA) || defined(GSR_EXP_NOREACH) || defined(GSR_EXP_NOREPLAY) ||                \
-     defined(GSR_EXP_NOCOL2) || defined(GSR_EXP_HOTREC))
+     defined(GSR_EXP_NOCOL2) || defined(GSR_EXP_HOTREC) || defined(GSR_EXP_NOEMBED))
 #error "GSR_EXP_* experiment switches build only through `make exp` (a diagnostic library, not libgsr_hip.so)"
 #endif
 #include <stddef.h>
@@ -183,8 +183,10 @@ struct SetCams {
 };
 
 // The per-(view, Gaussian) record every per-instance gather reads: one 64-byte line.
-//   a = (px, py, conic_a, conic_b), b = (conic_c, opacity, view depth, 0), c = (r, g, b, 0),
-//   d = (tile rect xmin | ymin << 16, xmax | ymax << 16, 0, SH clamp flags)
+//   a = (px, py, conic_a, conic_b), b = (conic_c, opacity, view depth, c2.x), c = (r, g, b, c2.y),
+//   d = (tile rect xmin | ymin << 16, xmax | ymax << 16, c2.z, SH clamp flags)
+// c2 = the two-colour render's second colour of the Gaussian when the preprocess was given one (PreprocessArgs::col2,
+// recorded in drange[130..131]), else 0.
 struct __attribute__((aligned(64))) GaussRec {
   float4 a, b, c;
   uint4 d;
@@ -213,7 +215,8 @@ struct GeomState {
   // kept-count field of a depth-sort value: all ones = did not fit (or no room: P > 2^26)
   __host__ __device__ uint32_t vsent() const { return vbits > 26 ? 0u : (1u << (32 - vbits)) - 1u; }
   uint32_t* drange;          // depth key range of the set: [0, 64) min slots, [64, 128) max slots,
-                             // [128] = min visible key, [129] = 1 if 3 depth-sort passes suffice
+                             // [128] = min visible key, [129] = 1 if 3 depth-sort passes suffice,
+                             // [130..131] = the colors2 pointer embedded in the records (0 = none)
   // the depth-sorted (keys, Gaussians) of every view: the 4th pass's output, or the 3rd's when it was skipped
   __device__ const uint32_t* sorted_dval() const { return drange[129] ? dval[1] : dval[0]; }
   __device__ const uint32_t* sorted_dkey() const { return drange[129] ? dkey[1] : dkey[0]; }

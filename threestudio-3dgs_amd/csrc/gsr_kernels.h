@@ -25,6 +25,9 @@ struct PreprocessArgs {
   float scale_modifier;
   int W, H;
   int* radii;  // (V, P)
+  // the second colour set of a two-colour render (colors2, (P, 3)) or null: written into the records' free slots
+  // (GaussRec: b.w, c.w, d.z) so the two-colour blends read it with the record instead of gathering it apart
+  const float* col2;
 };
 void launch_preprocess(const PreprocessArgs& a, const SetCams& cams, const GeomState& g, hipStream_t stream);
 
@@ -100,6 +103,9 @@ struct RenderSet {
   // tiles in chunks from them; null = off
   float* ckpt;
   const uint32_t* split_mode;  // backward: ImageState::split_mode (did the forward write the checkpoints?)
+  // GeomState::drange + 130: the colors2 pointer the set's preprocess embedded in the records (two words; 0 = none).
+  // A two-colour kernel reads the second colours from the records when it equals col2, else from col2 itself
+  const uint32_t* col2_rec;
   uint32_t* split_items;  // with ckpt: the later chunks' backward items (ImageState::split_items)
   uint32_t* split_cap;    // with ckpt: ImageState::split_cap
   int split_extra;        // with ckpt: split_extra(the set's V, tiles)

@@ -90,6 +90,9 @@ __global__ __launch_bounds__(256) void k_preprocess(PreprocessArgs a, SetCams ca
   if (a.colors_precomp != nullptr)
     rgb_pre = make_float3(a.colors_precomp[3 * ix], a.colors_precomp[3 * ix + 1], a.colors_precomp[3 * ix + 2]);
   const float* my_sh = staged ? s_sh + gl * sstride : a.shs + (size_t)ix * nsh;
+  // the two-colour render's second colour, carried in the record's free slots (b.w, c.w, d.z; GaussRec)
+  float3 c2 = make_float3(0.f, 0.f, 0.f);
+  if (a.col2 != nullptr) c2 = make_float3(a.col2[3 * ix], a.col2[3 * ix + 1], a.col2[3 * ix + 2]);
   const int gx = (a.W + GSR_TILE_X - 1) / GSR_TILE_X;
   const int gy = (a.H + GSR_TILE_Y - 1) / GSR_TILE_Y;
 
@@ -141,10 +144,10 @@ __global__ __launch_bounds__(256) void k_preprocess(PreprocessArgs a, SetCams ca
                             &clamp_bits);
           GaussRec rec;
           rec.a = make_float4(pimg.x, pimg.y, conic.x, conic.y);
-          rec.b = make_float4(conic.z, opacity, p_view.z, 0.0f);
-          rec.c = make_float4(rgb.x, rgb.y, rgb.z, 0.0f);
-          rec.d = make_uint4((uint32_t)xmin | ((uint32_t)ymin << 16), (uint32_t)xmax | ((uint32_t)ymax << 16), 0u,
-                             clamp_bits);
+          rec.b = make_float4(conic.z, opacity, p_view.z, c2.x);
+          rec.c = make_float4(rgb.x, rgb.y, rgb.z, c2.y);
+          rec.d = make_uint4((uint32_t)xmin | ((uint32_t)ymin << 16), (uint32_t)xmax | ((uint32_t)ymax << 16),
+                             __float_as_uint(c2.z), clamp_bits);
           if (valid) g.rec[vi] = rec;
           radius = r;
           uint32_t kept = 0;
@@ -189,9 +192,10 @@ __global__ __launch_bounds__(256) void k_preprocess(PreprocessArgs a, SetCams ca
   }
 }
 
-__global__ void k_depth_range_init(uint32_t* drange) {
+__global__ void k_depth_range_init(uint32_t* drange, unsigned long long col2) {
   drange[threadIdx.x] = 0xFFFFFFFFu;
   drange[64 + threadIdx.x] = 0u;
+  if (threadIdx.x < 2) drange[130 + threadIdx.x] = (uint32_t)(col2 >> (32 * threadIdx.x));  // (see GaussRec)
 }
 
 // Fold the 64 slots: [128] = smallest visible key, [129] = 1 when every rebased visible key is below
@@ -212,7 +216,8 @@ __global__ void k_depth_range(uint32_t* drange) {
 }
 
 void launch_preprocess(const PreprocessArgs& a, const SetCams& cams, const GeomState& g, hipStream_t stream) {
-  hipLaunchKernelGGL(k_depth_range_init, dim3(1), dim3(64), 0, stream, g.drange);
+  hipLaunchKernelGGL(k_depth_range_init, dim3(1), dim3(64), 0, stream, g.drange,
+                     (unsigned long long)(uintptr_t)(a.P > 0 ? a.col2 : nullptr));
   if (a.P > 0 && a.V > 0) launch_preprocess_kernel(a, cams, g, stream);
   hipLaunchKernelGGL(k_depth_range, dim3(1), dim3(64), 0, stream, g.drange);
 }

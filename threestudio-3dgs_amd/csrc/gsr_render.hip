@@ -149,6 +149,17 @@ __device__ __forceinline__ float vcopy(float x) {
   return r;
 }
 
+// The set's preprocess embedded exactly this col2 array in the records (GaussRec b.w, c.w, d.z): the two-colour
+// blends then read the second colours with the record (one 4-byte load beside it) instead of gathering col2 apart
+__device__ __forceinline__ bool col2_embedded(const RenderSet& rs) {
+#ifdef GSR_EXP_NOEMBED
+  return false;  // (timing only: the second colours gathered from col2 as before the records carried them)
+#endif
+  if (rs.col2 == nullptr || rs.col2_rec == nullptr) return false;
+  const unsigned long long e = (unsigned long long)rs.col2_rec[0] | ((unsigned long long)rs.col2_rec[1] << 32);
+  return e == (unsigned long long)(uintptr_t)rs.col2;
+}
+
 // bg . dL/dpixel with an explicit operation order (the backward kernels' background terms: every kernel
 // variant forms the same bits, independent of how the compiler would contract the expression)
 __device__ __forceinline__ float bg_dot3(const float* bg, float d0, float d1, float d2) {
@@ -220,6 +231,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(GSR_FWD_WPE,
   float4 n0 = zero4, n1 = zero4, n2 = zero4, n3 = zero4;
   uint32_t gi_next = 0u;
   const float* col2 = rs.col2;
+  const bool emb = C2 && col2_embedded(rs);  // (n3 then read from the record's b.w, c.w, d.z: the same line)
   // quadrant masks in the keys (TilePack::qmask): the keep decision comes with the index, and only this
   // quadrant's candidates are gathered.  k_emit forms the masks with span_quads (a band / column bound on the
   // alpha >= 1/255 ellipse), not with quadrant_hit: the two tests differ, but each keeps every quadrant that holds
@@ -242,7 +254,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(GSR_FWD_WPE,
 #ifdef GSR_EXP_NOCOL2
     if (C2) n3 = make_float4(__uint_as_float(g0), 0.f, 0.f, 0.f);  // timing only: no col2 gather
 #else
-    if (C2) n3 = make_float4(col2[3 * g0], col2[3 * g0 + 1], col2[3 * g0 + 2], 0.f);
+    if (C2 && emb) n3 = make_float4(rec[g0].b.w, rec[g0].c.w, __uint_as_float(rec[g0].d.z), 0.f);
+    else if (C2) n3 = make_float4(col2[3 * g0], col2[3 * g0 + 1], col2[3 * g0 + 2], 0.f);
 #endif
   }
   if (64 + lane < n) {
@@ -284,7 +297,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(GSR_FWD_WPE,
 #ifdef GSR_EXP_NOCOL2
       if (C2) n3 = make_float4(__uint_as_float(gn), 0.f, 0.f, 0.f);  // timing only: no col2 gather
 #else
-      if (C2) n3 = make_float4(col2[3 * gn], col2[3 * gn + 1], col2[3 * gn + 2], 0.f);
+      if (C2 && emb) n3 = make_float4(rec[gn].b.w, rec[gn].c.w, __uint_as_float(rec[gn].d.z), 0.f);
+      else if (C2) n3 = make_float4(col2[3 * gn], col2[3 * gn + 1], col2[3 * gn + 2], 0.f);
 #endif
     }
     if (base + 128 + lane < n) {
@@ -581,6 +595,7 @@ __global__ __launch_bounds__(64) void k_render_fwd_tile(RenderSet rs, const uint
   const uint32_t gmask = rs.gmask;
   const float4 zero4 = make_float4(0.f, 0.f, 0.f, 0.f);
   const float* col2 = rs.col2;
+  const bool emb = C2 && col2_embedded(rs);  // (n3 then read from the record's b.w, c.w, d.z: the same line)
   float4 n0 = zero4, n1 = zero4, n2 = zero4, n3 = zero4;
   uint32_t gi_next = 0u;
   if (lane < n) {
@@ -588,7 +603,8 @@ __global__ __launch_bounds__(64) void k_render_fwd_tile(RenderSet rs, const uint
     n0 = rec[g0].a;
     n1 = rec[g0].b;
     n2 = rec[g0].c;
-    if (C2) n3 = make_float4(col2[3 * g0], col2[3 * g0 + 1], col2[3 * g0 + 2], 0.f);
+    if (C2 && emb) n3 = make_float4(rec[g0].b.w, rec[g0].c.w, __uint_as_float(rec[g0].d.z), 0.f);
+    else if (C2) n3 = make_float4(col2[3 * g0], col2[3 * g0 + 1], col2[3 * g0 + 2], 0.f);
   }
   // (gi_next stays raw until the next batch: masked right after its load, the wave would wait there for every
   // load in flight, the records just issued included)
@@ -616,7 +632,8 @@ __global__ __launch_bounds__(64) void k_render_fwd_tile(RenderSet rs, const uint
       n0 = rec[gn].a;
       n1 = rec[gn].b;
       n2 = rec[gn].c;
-      if (C2) n3 = make_float4(col2[3 * gn], col2[3 * gn + 1], col2[3 * gn + 2], 0.f);
+      if (C2 && emb) n3 = make_float4(rec[gn].b.w, rec[gn].c.w, __uint_as_float(rec[gn].d.z), 0.f);
+      else if (C2) n3 = make_float4(col2[3 * gn], col2[3 * gn + 1], col2[3 * gn + 2], 0.f);
     }
     if (base + 128 + lane < n) gi_next = sorted_gauss[range.x + base + 128 + lane];
     if (qbi >= 0) qbytes[qbi] = qbv;
@@ -1658,6 +1675,7 @@ __global__ __launch_bounds__(64) void k_render_bwd_tw(
   const unsigned int vbit = 1u << (v & 31);
   float4 na = zero4, nb = zero4, nc = zero4, nd = zero4, n2 = zero4;
   uint32_t ngo = 0u, gi_next = 0u, ng = 0u;
+  const bool emb = col2_embedded(rs);  // the second colours in the records (b.w, c.w, d.z): no gather of col2
   auto load = [&](uint32_t g) {
     const float4* r = reinterpret_cast<const float4*>(rec + g);
     {
@@ -1669,7 +1687,7 @@ __global__ __launch_bounds__(64) void k_render_bwd_tw(
     }
     {
       nc = r[2];
-      if (rs.col2 != nullptr) {
+      if (rs.col2 != nullptr && !(TWO && emb)) {  // (embedded: the record's b.w, c.w, d.z, read at the staging)
         const float4 c2 = make_float4(rs.col2[3 * g], rs.col2[3 * g + 1], rs.col2[3 * g + 2], 0.f);
         if (TWO)
           n2 = c2;
@@ -1819,7 +1837,9 @@ __global__ __launch_bounds__(64) void k_render_bwd_tw(
     const float4 ca = make_float4(vcopy(na.x), vcopy(na.y), vcopy(na.z), vcopy(na.w));
     const float4 cb = make_float4(vcopy(nb.x), vcopy(nb.y), vcopy(nb.z), 0.f);
     const float4 cc = make_float4(vcopy(nc.x), vcopy(nc.y), vcopy(nc.z), 0.f);
-    const float4 c2 = TWO ? make_float4(vcopy(n2.x), vcopy(n2.y), vcopy(n2.z), 0.f) : zero4;
+    const float4 c2 = !TWO ? zero4
+                      : emb ? make_float4(vcopy(nb.w), vcopy(nc.w), vcopy(nd.z), 0.f)
+                            : make_float4(vcopy(n2.x), vcopy(n2.y), vcopy(n2.z), 0.f);
     const uint32_t cdx = __float_as_uint(vcopy(nd.x)), cdy = __float_as_uint(vcopy(nd.y));
     const uint32_t cgo = __float_as_uint(vcopy(__uint_as_float(ngo)));
     const int rel_c = h - 1 - lane;

@@ -78,6 +78,11 @@ SIGNATURES = {
         [_i, _i, _i, _i, _vp, _vp, _f, _vp, _vp, _vp, _vp, _vp] + [ctypes.POINTER(_vp)] * 3
         + [ctypes.POINTER(_f)] * 2 + [_i, _i, _i, _vp, _vp, _vp],
     ),
+    "gsr_set_preprocess_ex": (
+        _i,
+        [_i, _i, _i, _i, _vp, _vp, _f, _vp, _vp, _vp, _vp, _vp] + [ctypes.POINTER(_vp)] * 3
+        + [ctypes.POINTER(_f)] * 2 + [_i, _i, _i, _vp, _vp, _vp, _vp],
+    ),
     "gsr_set_num_rendered": (_i, [_i, _vp, _i, ctypes.POINTER(_i), ctypes.POINTER(_i), _vp]),
     "gsr_set_num_rendered_ex": (_i, [_i, _vp, _i, ctypes.POINTER(_i), ctypes.POINTER(_i), ctypes.POINTER(_i), _vp]),
     "gsr_set_gauss_state": (_i, [_i, _vp, _i, _vp, _vp, _vp]),
@@ -152,7 +157,7 @@ def host_trace_read(reset: bool = True) -> dict:
     return out
 
 
-ABI_VERSION = 4  # include/gsr.h GSR_ABI_VERSION this binding is written against
+ABI_VERSION = 5  # include/gsr.h GSR_ABI_VERSION this binding is written against
 
 
 def load_library(path: str | None = None):

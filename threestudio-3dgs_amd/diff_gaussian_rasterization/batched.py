@@ -58,6 +58,12 @@ class _ViewSet:
         return self.arrays
 
 
+# A two-colour forward hands colors2 to the preprocess too (gsr_set_preprocess_ex), which writes each Gaussian's
+# second colour into the record it writes anyway; the blends then read it from the record's line.  False: the
+# blends gather colors2 apart (the same bits; tests/test_gpu_configs.py compares the two).
+EMBED_COLORS2 = True
+
+
 class _RasterizeViews(torch.autograd.Function):
     @staticmethod
     def forward(ctx, settings_list, grad_reduce, two_color_bwd, means3D, sh, colors_precomp, opacities, scales,
@@ -106,10 +112,12 @@ class _RasterizeViews(torch.autograd.Function):
             vs.geom = torch.empty(int(lib.gsr_set_geom_bytes(vs.V, P)), dtype=torch.uint8, device=dev)
             views, projs, campos, tx, ty = vs.cam_arrays()
             t0 = _C.host_mark("fwd_setup", t0)
-            _C._check(lib.gsr_set_preprocess(
+            # (the second colour set, when there is one, rides in the records the preprocess writes: the two-colour
+            # blends then read it with the record instead of gathering it apart)
+            _C._check(lib.gsr_set_preprocess_ex(
                 vs.V, P, int(s0.sh_degree), M, p(m3), p(sc), float(s0.scale_modifier), p(rot), p(op), p(shc), p(col),
                 p(c3), views, projs, campos, tx, ty, W, H, int(bool(s0.prefiltered)), p(radii[lo:hi]), p(vs.geom),
-                stream))
+                p(c2) if c2 is not None and EMBED_COLORS2 else None, stream))
             sets.append(vs)
             t0 = _C.host_mark("fwd_preprocess_launch", t0)
         for vs in sets:
