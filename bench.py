@@ -73,12 +73,12 @@ def parse():
     ap.add_argument("--path", choices=["batched", "per-view"], default="batched",
                     help="batched: rasterize_views (one autograd node per rank's views); per-view: one "
                          "GaussianRasterizer call per view, exactly as the reference renderer loop does")
-    ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "r05zz_traffic.json"),
+    ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "r06y_traffic.json"),
                     help="PMC summary (profiles/summarize.py) supplying roofline.traffic and the VALU counts")
-    ap.add_argument("--pairs", default=os.path.join(ROOT, "profiles", "r05zz_pairs.json"),
+    ap.add_argument("--pairs", default=os.path.join(ROOT, "profiles", "r06y_pairs.json"),
                     help="device-counted blend pairs (profiles/diag_pairs.py) for the VALU roofline")
-    ap.add_argument("--traffic-sugar", default=os.path.join(ROOT, "profiles", "r05zz_sugar_traffic.json"),
-                    help="PMC summary of the C5 line (--workload sugar, profiles/summarize.py r05zz_sugar)")
+    ap.add_argument("--traffic-sugar", default=os.path.join(ROOT, "profiles", "r06y_sugar_traffic.json"),
+                    help="PMC summary of the C5 line (--workload sugar, profiles/summarize.py r06y_sugar)")
     ap.add_argument("--overlap-reduce", choices=["on", "off"], default="on",
                     help="N > 1: sum the Gaussian gradients over ranks inside the backward, range by range as the "
                          "per-Gaussian backward forms them (view_shard.ChunkedGradReduce, overlapped on a side "
@@ -873,6 +873,9 @@ def main():
                 sub.workload, sub.res = "sugar", 800
             elif name == "views8":  # a rank's share of the 64-view batch at N = 8
                 sub.views = 8
+                # as many views timed as the 64-view line's steps (an 8-view step is ≈ 2.5 ms: 5 of them were
+                # dominated by host jitter, 2.5–2.7 ms per step for the same kernel times)
+                sub.steps, sub.warmup = 8 * max(3, min(args.steps, 10)), 5
             else:
                 raise SystemExit(f"unknown --extra-lines entry {name!r}")
             r, _ = run_workload(sub, world, rank, device, comm, headline=False)
