@@ -25,6 +25,13 @@
 
 namespace gsr {
 
+// Histogram copies the count kernel's lanes spread their LDS atomics over (lane mod GSR_COUNT_SUB), rows padded by
+// one word so the copies of a digit sit in different banks: keys whose digits come in runs (a later pass over keys
+// an earlier pass grouped — e.g. SuGaR's tile rows in depth order) had up to 64 lanes of one instruction adding to
+// one counter, serialised (C5's second tile-sort count pass: 537 against 137 us per launch for the first).
+#ifndef GSR_COUNT_SUB
+#define GSR_COUNT_SUB 4
+#endif
 // BITS: the digit width at compile time (6 and 8: the ballot-matching loop unrolls), 0 = runtime `bits`.
 template <int BITS>
 __global__ __launch_bounds__(GSR_SORT_THREADS) void k_seg_count(const uint32_t* __restrict__ keys, SegInfo seg,
@@ -33,7 +40,7 @@ __global__ __launch_bounds__(GSR_SORT_THREADS) void k_seg_count(const uint32_t* 
   const int bits = BITS ? BITS : bits_rt;
   if (seg_skip_last(seg, last)) return;
   const uint32_t kb = seg_key_base(seg);
-  __shared__ uint32_t s_hist[GSR_RADIX];
+  __shared__ uint32_t s_hist[GSR_COUNT_SUB * (GSR_RADIX + 1)];
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
   uint32_t lb;
   const int v = seg_of_block(seg, xcd_block(blockIdx.x, gridDim.x), lb);  // (logical block: XCD-contiguous)
@@ -41,8 +48,9 @@ __global__ __launch_bounds__(GSR_SORT_THREADS) void k_seg_count(const uint32_t* 
   const uint32_t* src = keys + seg.start[v];
   const uint32_t mask = (1u << bits) - 1u;
   const int R = 1 << bits;
-  s_hist[t] = 0u;
+  for (int i = t; i < GSR_COUNT_SUB * (GSR_RADIX + 1); i += GSR_SORT_THREADS) s_hist[i] = 0u;
   __syncthreads();
+  uint32_t* const hist = s_hist + (lane & (GSR_COUNT_SUB - 1)) * (GSR_RADIX + 1);
   const uint32_t b0 = lb * GSR_SORT_TILE + w * (GSR_SORT_TILE / 4);
   // (full blocks: no per-item bounds, as k_seg_scatter)
   auto body = [&](auto full_c) {
@@ -59,7 +67,7 @@ __global__ __launch_bounds__(GSR_SORT_THREADS) void k_seg_count(const uint32_t* 
       const uint32_t d = (seg_key(kb, key[k]) >> shift) & mask;
       // one LDS atomic per key: half the time of ballot-matching the digit first (24.4 -> 12.4 us/view
       // over the 5 passes; the histogram needs no ranks)
-      if (valid) atomicAdd(&s_hist[d], 1u);
+      if (valid) atomicAdd(&hist[d], 1u);
     }
   };
   if ((lb + 1) * GSR_SORT_TILE <= n)
@@ -69,7 +77,10 @@ __global__ __launch_bounds__(GSR_SORT_THREADS) void k_seg_count(const uint32_t* 
   __syncthreads();
   if (t < R) {
     const uint32_t nb = seg.blk[v + 1] - seg.blk[v];
-    counts[(size_t)R * seg.blk[v] + (size_t)t * nb + lb] = s_hist[t];
+    uint32_t c = 0u;
+#pragma unroll
+    for (int sb = 0; sb < GSR_COUNT_SUB; ++sb) c += s_hist[sb * (GSR_RADIX + 1) + t];
+    counts[(size_t)R * seg.blk[v] + (size_t)t * nb + lb] = c;
   }
 }
 
