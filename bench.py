@@ -79,6 +79,9 @@ def parse():
                     help="device-counted blend pairs (profiles/diag_pairs.py) for the VALU roofline")
     ap.add_argument("--traffic-sugar", default=os.path.join(ROOT, "profiles", "r06y_sugar_traffic.json"),
                     help="PMC summary of the C5 line (--workload sugar, profiles/summarize.py r06y_sugar)")
+    ap.add_argument("--fused-clamp", choices=["on", "off"], default="on",
+                    help="C5: the renderer's render.clamp(0, 1) formed in the blends (rasterize_views clamp=True) "
+                         "or by torch on the colour output (off: the A/B baseline)")
     ap.add_argument("--overlap-reduce", choices=["on", "off"], default="on",
                     help="N > 1: sum the Gaussian gradients over ranks inside the backward, range by range as the "
                          "per-Gaussian backward forms them (view_shard.ChunkedGradReduce, overlapped on a side "
@@ -203,6 +206,7 @@ SHADE_KA, SHADE_KD = (0.1, 0.1, 0.1), (0.9, 0.9, 0.9)  # the material's default 
 
 
 GRAD_REDUCE = None  # view_shard.ChunkedGradReduce when the reduction is overlapped with the backward (N > 1)
+FUSED_CLAMP = True  # C5: the renderer's clamp formed in the blends (--fused-clamp)
 
 
 def render_views(rep: Replica, settings, bg_img, shade=None):
@@ -251,21 +255,24 @@ def render_views_sugar(rep: Replica, settings, shade):
     colors = rep.shs[:, 0, :] * SH_C0 + 0.5
     if SUGAR_SEPARATE:  # the two rasterizer calls as two view-set renders (A/B of the shared-geometry path)
         color, radii, depth, alpha = rasterize_views(settings, rep.means3D, m2, rep.opacities, colors_precomp=colors,
-                                                     scales=rep.scales, rotations=rep.rotations)
+                                                     scales=rep.scales, rotations=rep.rotations, clamp=True)
         zeros = [torch.zeros((P, 3), device=dev) for _ in settings]
         normal, _, _, _ = rasterize_views(settings, rep.means3D, zeros, rep.opacities, colors_precomp=rep.normals,
                                           scales=rep.scales, rotations=rep.rotations)
     else:
         # pass 2 (face normals, zero means2D) shares pass 1's geometry, sorts and blend (colors2)
+        # (the renderer's render.clamp(0, 1), :212, formed in the blends: clamp=True)
         color, radii, depth, alpha, normal = rasterize_views(settings, rep.means3D, m2, rep.opacities,
                                                              colors_precomp=colors, scales=rep.scales,
                                                              rotations=rep.rotations, colors2=rep.normals,
-                                                             grad_reduce=GRAD_REDUCE)
+                                                             grad_reduce=GRAD_REDUCE, clamp=FUSED_CLAMP)
+        if not FUSED_CLAMP:
+            color = color.clamp(0, 1)
     rays_o, rays_d, _ = shade
     _, nmap_dist = depth_normal_views(depth, alpha, rays_o, rays_d)
     nmap = sugar_normal_map(normal, alpha)  # normalize, flip x / y, alpha-weighted map, alpha > 0.99 mask (fused)
     depth = torch.where(alpha > 0.99, depth, depth.detach())
-    return color.clamp(0, 1), depth, alpha, nmap, nmap_dist
+    return color, depth, alpha, nmap, nmap_dist
 
 
 PROFILE_VIEWS_PER_LAUNCH = 64  # profiles/run_profiles.sh: bench.py defaults, one 64-view set per launch
@@ -624,7 +631,8 @@ def run_workload(args, world, rank, device, comm, headline=True):
     from diff_gaussian_rasterization.view_shard import (ChunkedGradReduce, all_gather_views, all_gather_views_async,
                                                         allreduce_grads, shard_range)
 
-    global GRAD_REDUCE
+    global GRAD_REDUCE, FUSED_CLAMP
+    FUSED_CLAMP = args.fused_clamp == "on"
     overlap = world > 1 and args.overlap_reduce == "on" and args.path == "batched" and args.views >= world \
         and not SUGAR_SEPARATE
     GRAD_REDUCE = ChunkedGradReduce(n_chunks=args.grad_chunks) if overlap else None

@@ -231,7 +231,8 @@ int gsr_grad_chunk_range(int P, int n_chunks, int chunk, int* g0, int* g1);
  * call's preprocess, sorts and binning are the first's; its blend weights too, so the forward blends both
  * colour sets in one pass:
  *   gsr_set_render_two_colors  as gsr_set_render (bg_images / out_render: the fused composite, both NULL
- *                              for none) plus out_color2 (V, 3, H, W) = the blend of colors2 (P, 3) with
+ *                              for none; out_render alone: the clamp alone, as gsr_set_render_composite)
+ *                              plus out_color2 (V, 3, H, W) = the blend of colors2 (P, 3) with
  *                              the same weights and background: the second call's colour output (its
  *                              radii / depth / alpha equal the first call's).
  *   gsr_set_backward_colors    the second call's backward on the shared forward state: colours = colors2,
@@ -243,7 +244,8 @@ int gsr_grad_chunk_range(int P, int n_chunks, int chunk, int* g0, int* g1);
  *   gsr_set_backward_two_colors  both calls' backward in one pass (replaces gsr_set_backward[_composite]
  *                              followed by gsr_set_backward_colors): the blend is replayed once, forming
  *                              both calls' dL/dalpha; arguments as gsr_set_backward_composite (bg_images
- *                              and color both NULL: no composite) plus colors2, dL_dcolor2 = dL/d(out_color2)
+ *                              and color both NULL: no composite; color alone: the clamp alone) plus colors2,
+ *                              dL_dcolor2 = dL/d(out_color2)
  *                              and dL_dcolors2 (P, 3) = the gradient of colors2.  dL_dmeans2D receives the
  *                              first call's screen-space gradient only (the second call's means2D is the
  *                              reference's fresh zero tensor); the parameter gradients hold both calls'
@@ -284,6 +286,9 @@ int gsr_set_backward_two_colors(int V, int P, int degree, int M, const int* num_
  * colour / depth / alpha outputs are written as by gsr_set_render.  The backward takes dL/drender in
  * place of dL/dcolor, the forward's colour output, and forms dL/dbg (NULL: not formed) in the blend's
  * per-pixel prologue (clamp mask, dL/dalpha += -sum_c g_c bg_c, dL/dbg = g (1 - alpha)).
+ * bg_images NULL: the clamp alone — out_render = clamp(color, 0, 1), the renderers' `rendered_image.clamp(0, 1)`
+ * (renderer/diff_gaussian_rasterizer.py:141, renderer/diff_sugar_rasterizer_normal.py:212) bit-identical to the
+ * torch expression; the backward masks dL/drender by the forward's colour (dL_dbg must be NULL).
  */
 int gsr_set_render_composite(int V, int P, const int* num_rendered, int width, int height, const float* const* bgs,
                              void* geom, void* binning, void* image, float* out_color, float* out_depth,

@@ -56,7 +56,7 @@ RASTERIZE = gpu_rasterize
 
 def torch_rasterize_views(settings_list, means3D, means2D_list, opacities, shs=None, colors_precomp=None,
                           scales=None, rotations=None, cov3D_precomp=None, background=None, colors2=None,
-                          grad_reduce=None):
+                          grad_reduce=None, clamp=False):
     """batched.rasterize_views restated as a loop over torch_rasterize (for the CPU tests).  grad_reduce: the
     call's per-Gaussian gradients are summed over ranks in its backward, as the HIP call does (here through
     view_shard.reduce_on_backward on its inputs, in the HIP call's gradient order)."""
@@ -74,6 +74,8 @@ def torch_rasterize_views(settings_list, means3D, means2D_list, opacities, shs=N
     color, radii, depth, alpha = (torch.stack([o[i] for o in outs]) for i in range(4))
     if background is not None:
         color = (color + (1 - alpha) * background.permute(0, 3, 1, 2)).clamp(0, 1)
+    elif clamp:
+        color = color.clamp(0, 1)
     if colors2 is None:
         return color, radii, depth, alpha
     second = [torch_rasterize(s, means3D, torch.zeros_like(m2), opacities, colors_precomp=colors2, scales=scales,

@@ -109,3 +109,59 @@ def test_fused_composite_matches_unfused(V, H, W):
         assert torch.equal(g0[k], g1[k]), k
     for a, c in zip(m0, m1):
         assert torch.equal(a, c)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("V,H,W,two", [(3, 64, 48, False), (2, 40, 37, True)])
+def test_fused_clamp_matches_torch_clamp(V, H, W, two):
+    """rasterize_views(..., clamp=True) == rasterize_views(...)[0].clamp(0, 1) — the renderers' clamp of the
+    colour output (renderer/diff_gaussian_rasterizer.py:141, renderer/diff_sugar_rasterizer_normal.py:212) formed
+    in the blends: forward bit-identical, every gradient identical (the mask applied in the backward's per-pixel
+    prologue), one colour set and two (the SuGaR normal renderer's calls)."""
+    import gsr_synthetic as gs
+    from gsr_testutil import make_camera
+    from diff_gaussian_rasterization import GaussianRasterizationSettings
+    from diff_gaussian_rasterization.batched import rasterize_views
+
+    P = 3000
+    scene = gs.make_scene(P, sh_degree=3, seed=V + 10)
+    dev = "cuda"
+    settings = []
+    for v in range(V):
+        cam = make_camera(W, H, azimuth=40.0 * v)
+        # backgrounds outside [0, 1]: the clamp bites on empty and thin pixels
+        settings.append(GaussianRasterizationSettings(
+            image_height=H, image_width=W, tanfovx=cam["tanx"], tanfovy=cam["tany"],
+            bg=torch.tensor([1.3, -0.2, 0.5], device=dev), scale_modifier=1.0,
+            viewmatrix=torch.tensor(cam["view"], device=dev), projmatrix=torch.tensor(cam["proj"], device=dev),
+            sh_degree=3, campos=torch.tensor(cam["campos"], device=dev), prefiltered=False, debug=False))
+    g = torch.Generator(device=dev).manual_seed(9)
+    ups = [torch.randn((V, 3, H, W), generator=g, device=dev), torch.randn((V, 1, H, W), generator=g, device=dev),
+           torch.randn((V, 1, H, W), generator=g, device=dev), torch.randn((V, 3, H, W), generator=g, device=dev)]
+    n = torch.randn((P, 3), generator=g, device=dev)
+    normals = n / n.norm(dim=1, keepdim=True)
+    res = []
+    for fused in (False, True):
+        t = {k: torch.tensor(scene[k], device=dev, requires_grad=True)
+             for k in ("means3D", "scales", "rotations", "opacities", "shs")}
+        t["normals"] = normals.clone().requires_grad_(True)
+        m2 = [torch.zeros((P, 3), device=dev, requires_grad=True) for _ in range(V)]
+        kw = dict(shs=t["shs"], scales=t["scales"], rotations=t["rotations"])
+        if two:
+            kw["colors2"] = t["normals"]
+        outs = rasterize_views(settings, t["means3D"], m2, t["opacities"], clamp=fused, **kw)
+        out = outs[0] if fused else outs[0].clamp(0, 1)
+        ts = [out, outs[2], outs[3]] + ([outs[4]] if two else [])
+        torch.autograd.backward(ts, ups[:len(ts)])
+        res.append(([x.detach() for x in ts], {k: v.grad for k, v in t.items()}, [m.grad for m in m2]))
+    (o0, g0, m0), (o1, g1, m1) = res
+    assert float((o0[0] == 0).float().mean() + (o0[0] == 1).float().mean()) > 0.01  # the clamp did bite
+    for a, c in zip(o0, o1):
+        assert torch.equal(a, c)
+    for k in g0:
+        if g0[k] is None:
+            assert g1[k] is None, k
+            continue
+        assert torch.equal(g0[k], g1[k]), k
+    for a, c in zip(m0, m1):
+        assert torch.equal(a, c)

@@ -663,7 +663,8 @@ int gsr_set_render(int V, int P, const int* K, int width, int height, const floa
 int gsr_set_render_composite(int V, int P, const int* K, int width, int height, const float* const* bgs, void* geom,
                              void* binning, void* image, float* out_color, float* out_depth, float* out_alpha,
                              const float* bg_images, float* out_render, void* stream) {
-  if (bg_images == nullptr || out_render == nullptr) return fail(GSR_EINVAL, "%s", "null composite argument");
+  // (bg_images NULL: the clamp alone, out_render = clamp(color, 0, 1))
+  if (out_render == nullptr) return fail(GSR_EINVAL, "%s", "null composite argument");
   return set_render(V, P, K, width, height, bgs, geom, binning, image, out_color, out_depth, out_alpha, bg_images,
                     out_render, stream);
 }
@@ -673,7 +674,8 @@ int gsr_set_render_two_colors(int V, int P, const int* K, int width, int height,
                               float* out_alpha, const float* bg_images, float* out_render, const float* colors2,
                               float* out_color2, void* stream) {
   if (colors2 == nullptr || out_color2 == nullptr) return fail(GSR_EINVAL, "%s", "null second colour argument");
-  if ((bg_images == nullptr) != (out_render == nullptr)) return fail(GSR_EINVAL, "%s", "composite needs both images");
+  // (out_render without bg_images: the clamp alone)
+  if (bg_images != nullptr && out_render == nullptr) return fail(GSR_EINVAL, "%s", "composite needs out_render");
   return set_render(V, P, K, width, height, bgs, geom, binning, image, out_color, out_depth, out_alpha, bg_images,
                     out_render, stream, colors2, out_color2);
 }
@@ -893,7 +895,9 @@ int gsr_set_backward_composite(int V, int P, int degree, int M, const int* K, in
                                float* dL_dbg, float* dL_dmeans2D, float* dL_dcolors, float* dL_dopacity,
                                float* dL_dmeans3D, float* dL_dcov3D, float* dL_dsh, float* dL_dscales,
                                float* dL_drotations, int accumulate, void* work, size_t work_bytes, void* stream) {
-  if (bg_images == nullptr || color == nullptr) return fail(GSR_EINVAL, "%s", "null composite argument");
+  // (bg_images NULL: the clamp alone; no dL_dbg then)
+  if (color == nullptr) return fail(GSR_EINVAL, "%s", "null composite argument");
+  if (bg_images == nullptr && dL_dbg != nullptr) return fail(GSR_EINVAL, "%s", "dL_dbg needs bg_images");
   return set_backward(V, P, degree, M, K, width, height, bgs, means3D, scales, scale_modifier, rotations, shs,
                       cov3D_precomp, viewmatrices, projmatrices, campos, tanfovx, tanfovy, radii, geom, binning, image,
                       dL_drender, dL_ddepth, dL_dalpha, dL_dmeans2D, dL_dcolors, dL_dopacity, dL_dmeans3D, dL_dcov3D,
@@ -952,7 +956,9 @@ int gsr_set_backward_two_colors(int V, int P, int degree, int M, const int* K, i
                                 int accumulate, void* work, size_t work_bytes, void* stream) {
   if (colors2 == nullptr || dL_dcolor2 == nullptr || dL_dcolors2 == nullptr)
     return fail(GSR_EINVAL, "%s", "null second colour argument");
-  if ((bg_images == nullptr) != (color == nullptr)) return fail(GSR_EINVAL, "%s", "composite needs both images");
+  // (color without bg_images: the clamp alone; neither: no composite)
+  if (bg_images != nullptr && color == nullptr) return fail(GSR_EINVAL, "%s", "composite needs the forward's color");
+  if (bg_images == nullptr && dL_dbg != nullptr) return fail(GSR_EINVAL, "%s", "dL_dbg needs bg_images");
   return set_backward(V, P, degree, M, K, width, height, bgs, means3D, scales, scale_modifier, rotations, shs,
                       cov3D_precomp, viewmatrices, projmatrices, campos, tanfovx, tanfovy, radii, geom, binning, image,
                       dL_dcolor, dL_ddepth, dL_dalpha, dL_dmeans2D, dL_dcolors, dL_dopacity, dL_dmeans3D, dL_dcov3D,

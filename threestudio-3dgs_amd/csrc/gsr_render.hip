@@ -410,15 +410,22 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(GSR_FWD_WPE,
       o2[HW] = ErEg.y + T * bg[1];
       o2[2 * HW] = Eb + T * bg[2];
     }
-    if (rs.cbg != nullptr) {
-      // fused composite, the same operations as the torch epilogue on the stored outputs (bit-identical)
+    if (rs.comp != nullptr) {
+      // fused composite (without background images: the renderer's clamp alone), the same operations as the torch
+      // epilogue on the stored outputs (bit-identical)
 #pragma clang fp contract(off)
-      const float am = 1.0f - (1.0f - T);
-      const float* bgi = rs.cbg + ((size_t)v * HW + pid) * 3;
+      float p0 = Cr + T * bg[0], p1 = Cg + T * bg[1], p2 = Cb + T * bg[2];
+      if (rs.cbg != nullptr) {
+        const float am = 1.0f - (1.0f - T);
+        const float* bgi = rs.cbg + ((size_t)v * HW + pid) * 3;
+        p0 = p0 + am * bgi[0];
+        p1 = p1 + am * bgi[1];
+        p2 = p2 + am * bgi[2];
+      }
       float* cp = rs.comp + (size_t)v * 3 * HW + pid;
-      cp[0] = fminf(fmaxf((Cr + T * bg[0]) + am * bgi[0], 0.0f), 1.0f);
-      cp[HW] = fminf(fmaxf((Cg + T * bg[1]) + am * bgi[1], 0.0f), 1.0f);
-      cp[2 * HW] = fminf(fmaxf((Cb + T * bg[2]) + am * bgi[2], 0.0f), 1.0f);
+      cp[0] = fminf(fmaxf(p0, 0.0f), 1.0f);
+      cp[HW] = fminf(fmaxf(p1, 0.0f), 1.0f);
+      cp[2 * HW] = fminf(fmaxf(p2, 0.0f), 1.0f);
     }
   }
   if (CK && chunk > 0) {
@@ -748,14 +755,20 @@ __global__ __launch_bounds__(64) void k_render_fwd_tile(RenderSet rs, const uint
         o2[HWs] = ErEg[q].y + Tq * bg[1];
         o2[2 * HWs] = Eb[q] + Tq * bg[2];
       }
-      if (rs.cbg != nullptr) {
+      if (rs.comp != nullptr) {
 #pragma clang fp contract(off)
-        const float am = 1.0f - (1.0f - Tq);
-        const float* bgi = rs.cbg + ((size_t)v * HWs + pid) * 3;
+        float p0 = CrCg[q].x + Tq * bg[0], p1 = CrCg[q].y + Tq * bg[1], p2 = CbD[q].x + Tq * bg[2];
+        if (rs.cbg != nullptr) {
+          const float am = 1.0f - (1.0f - Tq);
+          const float* bgi = rs.cbg + ((size_t)v * HWs + pid) * 3;
+          p0 = p0 + am * bgi[0];
+          p1 = p1 + am * bgi[1];
+          p2 = p2 + am * bgi[2];
+        }
         float* cp = rs.comp + (size_t)v * 3 * HWs + pid;
-        cp[0] = fminf(fmaxf((CrCg[q].x + Tq * bg[0]) + am * bgi[0], 0.0f), 1.0f);
-        cp[HWs] = fminf(fmaxf((CrCg[q].y + Tq * bg[1]) + am * bgi[1], 0.0f), 1.0f);
-        cp[2 * HWs] = fminf(fmaxf((CbD[q].x + Tq * bg[2]) + am * bgi[2], 0.0f), 1.0f);
+        cp[0] = fminf(fmaxf(p0, 0.0f), 1.0f);
+        cp[HWs] = fminf(fmaxf(p1, 0.0f), 1.0f);
+        cp[2 * HWs] = fminf(fmaxf(p2, 0.0f), 1.0f);
       }
     }
     uint32_t mc = last[q];
@@ -1008,6 +1021,14 @@ __device__ __forceinline__ void bwd_tile(BwdLDS& s, const RenderSet& rs, int v, 
         if (rs.dcbg != nullptr && chunk == 0) rs.dcbg[((size_t)v * HW + pid) * 3 + ch] = gch * am;
       }
       dpix_a = da + dpix_a;
+    } else if (rs.ccolor != nullptr) {
+      // the clamp alone: dL/dclamped masked by the forward's colour
+      const float* col = rs.ccolor + (size_t)v * 3 * HW + pid;
+#pragma unroll
+      for (int ch = 0; ch < 3; ++ch) {
+        const float pre = col[(size_t)ch * HW];
+        dpix[ch] = (pre >= 0.0f && pre <= 1.0f) ? dpix[ch] : 0.0f;
+      }
     }
   }
   const float bg_dot = bg_dot3(bg, dpix[0], dpix[1], dpix[2]);
@@ -1647,6 +1668,14 @@ __global__ __launch_bounds__(64) void k_render_bwd_tw(
           if (rs.dcbg != nullptr) rs.dcbg[((size_t)v * HW + pid) * 3 + ch] = gch * am;
         }
         da = dsum + da;
+      } else if (rs.ccolor != nullptr) {
+        // the clamp alone: dL/dclamped masked by the forward's colour
+        const float* col = rs.ccolor + (size_t)v * 3 * HW + pid;
+#pragma unroll
+        for (int ch = 0; ch < 3; ++ch) {
+          const float pre = col[(size_t)ch * HW];
+          d[ch] = (pre >= 0.0f && pre <= 1.0f) ? d[ch] : 0.0f;
+        }
       }
     }
     float e[3] = {0.f, 0.f, 0.f};

@@ -306,19 +306,20 @@ def render_views_local(renderer, batch: dict, mode: str, lo: int, hi: int, draws
     with torch.autocast(device_type=dev.type, enabled=False):
         if mode in ("plain", "advanced"):
             settings = _settings(pc, cams, draws["bgs"], H, W, scaling_modifier)
+            # (the renderer's clamp(0, 1) formed in the blends)
             color, radii, depth, alpha = _rasterize_views(settings, means3D, m2, shs=shs, colors_precomp=override,
-                                                          **common_main)
-            out["comp_rgb"] = color.clamp(0, 1)
+                                                          clamp=True, **common_main)
+            out["comp_rgb"] = color
             if mode == "advanced":
                 out.update(comp_depth=depth, comp_mask=alpha)
         elif mode == "normal":
             settings = _settings(pc, cams, draws["bgs"], H, W, scaling_modifier)
             color, radii, depth, alpha = _rasterize_views(settings, means3D, m2, shs=shs, colors_precomp=override,
-                                                          **common_main)
+                                                          clamp=True, **common_main)
             nmap, depth_m = _depth_normal_maps(depth, alpha, batch["rays_o"][lo:hi], batch["rays_d"][lo:hi])
             if getattr(pc.cfg, "pred_normal", False):
                 out["comp_pred_normal"] = pred_normal_pass(settings)
-            out.update(comp_rgb=color.clamp(0, 1), comp_normal=nmap, comp_depth=depth_m, comp_mask=alpha)
+            out.update(comp_rgb=color, comp_normal=nmap, comp_depth=depth_m, comp_mask=alpha)
         elif mode == "background":
             zero = [renderer.background_tensor * 0] * n
             settings = _settings(pc, cams, zero, H, W, scaling_modifier)
@@ -352,14 +353,15 @@ def render_views_local(renderer, batch: dict, mode: str, lo: int, hi: int, draws
             # means2D) from one geometry, sort and blend: the normals are the second colour set
             color, radii, depth, alpha, normal = _rasterize_views(settings, means3D, m2, shs=shs,
                                                                   colors_precomp=override,
-                                                                  colors2=pc.get_gs_normals, **common_main)
+                                                                  colors2=pc.get_gs_normals, clamp=True,
+                                                                  **common_main)
             if batch.get("compute_normal_from_dist", True):
                 _, nmap_dist = _depth_normal_views(depth, alpha, batch["rays_o"][lo:hi], batch["rays_d"][lo:hi])
                 out["comp_normal_from_dist"] = nmap_dist
             # normalize, p3d -> threestudio axes, alpha-weighted map, alpha > 0.99 gradient mask (:192-197)
             nmap = _sugar_normal_map(normal, alpha)
             mask = alpha > 0.99
-            out.update(comp_rgb=color.clamp(0, 1), comp_normal=nmap,
+            out.update(comp_rgb=color, comp_normal=nmap,
                        comp_depth=torch.where(mask, depth, depth.detach()), comp_mask=alpha)
         elif mode == "sugar_shading":
             zero = [renderer.background_tensor * 0] * n

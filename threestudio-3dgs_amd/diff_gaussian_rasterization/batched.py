@@ -66,7 +66,7 @@ EMBED_COLORS2 = True
 
 class _RasterizeViews(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, settings_list, grad_reduce, two_color_bwd, means3D, sh, colors_precomp, opacities, scales,
+    def forward(ctx, settings_list, grad_reduce, two_color_bwd, clamp, means3D, sh, colors_precomp, opacities, scales,
                 rotations, cov3D_precomp, composite_bg, colors2, *means2D):
         t0 = time.perf_counter()
         lib = _C.load_library()
@@ -90,8 +90,12 @@ class _RasterizeViews(torch.autograd.Function):
         fopt = dict(dtype=torch.float32, device=dev)
         color = torch.empty((V, 3, H, W), **fopt)
         cbg = None
+        # the renderer's clamp(0, 1) fused into the blends without a background image (clamp_only) or with it
+        clamp_only = bool(clamp) and composite_bg is None
         if composite_bg is not None:
             cbg = _C._f32(composite_bg, "background", dev).reshape(V, H, W, 3)
+        fused_out = cbg is not None or clamp_only
+        if fused_out:
             render = torch.empty((V, 3, H, W), **fopt)
         depth = torch.empty((V, 1, H, W), **fopt)
         alpha = torch.empty((V, 1, H, W), **fopt)
@@ -138,26 +142,27 @@ class _RasterizeViews(torch.autograd.Function):
                 _C._check(lib.gsr_set_render_two_colors(
                     vs.V, P, Karr, W, H, vs.bgs, p(vs.geom), p(vs.binning), p(vs.image),
                     p(color[sl]), p(depth[sl]), p(alpha[sl]), p(cbg[sl]) if cbg is not None else None,
-                    p(render[sl]) if cbg is not None else None, p(c2), p(color2[sl]), stream))
-            elif cbg is None:
+                    p(render[sl]) if fused_out else None, p(c2), p(color2[sl]), stream))
+            elif not fused_out:
                 _C._check(lib.gsr_set_render(vs.V, P, Karr, W, H, vs.bgs, p(vs.geom),
                                              p(vs.binning), p(vs.image), p(color[sl]), p(depth[sl]), p(alpha[sl]),
                                              stream))
             else:
                 _C._check(lib.gsr_set_render_composite(
                     vs.V, P, Karr, W, H, vs.bgs, p(vs.geom), p(vs.binning), p(vs.image),
-                    p(color[sl]), p(depth[sl]), p(alpha[sl]), p(cbg[sl]), p(render[sl]), stream))
+                    p(color[sl]), p(depth[sl]), p(alpha[sl]), p(cbg[sl]) if cbg is not None else None,
+                    p(render[sl]), stream))
             t0 = _C.host_mark("fwd_render_launch", t0)
         ctx.settings = settings_list
         ctx.grad_reduce = grad_reduce
         ctx.two_color_bwd = two_color_bwd
         ctx.sets = sets
         ctx.bg_shape = tuple(composite_bg.shape) if composite_bg is not None else None
-        ctx.save_for_backward(m3, shc, col, sc, rot, c3, radii, cbg, color if cbg is not None else None, c2)
+        ctx.save_for_backward(m3, shc, col, sc, rot, c3, radii, cbg, color if fused_out else None, c2)
         ctx.mark_non_differentiable(radii)
         if c2 is not None:
-            return (color if cbg is None else render), radii, depth, alpha, color2
-        return (color if cbg is None else render), radii, depth, alpha
+            return (render if fused_out else color), radii, depth, alpha, color2
+        return (render if fused_out else color), radii, depth, alpha
 
     @staticmethod
     def backward(ctx, g_color, _g_radii, g_depth, g_alpha, g_color2=None):
@@ -190,7 +195,7 @@ class _RasterizeViews(torch.autograd.Function):
                 off += n
         d_m3, d_sc, d_rot, d_op = carved["m3"], carved["sc"], carved["rot"], carved["op"]
         d_sh, d_c3, d_col = carved["sh"], carved["c3"], carved["col"]
-        d_bg = torch.empty_like(cbg) if cbg is not None and ctx.needs_input_grad[10] else None
+        d_bg = torch.empty_like(cbg) if cbg is not None and ctx.needs_input_grad[11] else None
         # more than one view set in the scale / rotation path: the running dL/dcov3D the later sets
         # continue from (include/gsr.h gsr_set_backward, accumulate)
         d_c2 = torch.zeros((P, 3), **fopt) if second else None
@@ -243,12 +248,12 @@ class _RasterizeViews(torch.autograd.Function):
                         vs.V, P, int(s0.sh_degree), M, Karr, W, H, vs.bgs, p(m3), p(sc),
                         float(s0.scale_modifier), p(rot), p(shc), p(c3), views, projs, campos, tx, ty, p(radii[sl]),
                         p(vs.geom), p(vs.binning), p(vs.image), p(cbg[sl]) if cbg is not None else None,
-                        p(color[sl]) if cbg is not None else None, p(gc[sl]), gdp, gap,
+                        p(color[sl]) if color is not None else None, p(gc[sl]), gdp, gap,
                         p(d_bg[sl]) if d_bg is not None else None, p(c2), p(g2[sl]), p(d_m2[sl]), p(d_col), p(d_c2),
                         p(d_op), p(d_m3), p(d_c3), p(d_sh), p(d_sc), p(d_rot), 1 if si > 0 else 0, p(work),
                         work.numel(), stream))
                     continue
-                if cbg is None:
+                if color is None:
                     _C._check(lib.gsr_set_backward(
                         vs.V, P, int(s0.sh_degree), M, Karr, W, H, vs.bgs, p(m3), p(sc),
                         float(s0.scale_modifier), p(rot), p(shc), p(c3), views, projs, campos, tx, ty, p(radii[sl]),
@@ -259,7 +264,8 @@ class _RasterizeViews(torch.autograd.Function):
                     _C._check(lib.gsr_set_backward_composite(
                         vs.V, P, int(s0.sh_degree), M, Karr, W, H, vs.bgs, p(m3), p(sc),
                         float(s0.scale_modifier), p(rot), p(shc), p(c3), views, projs, campos, tx, ty, p(radii[sl]),
-                        p(vs.geom), p(vs.binning), p(vs.image), p(cbg[sl]), p(color[sl]), p(gc[sl]), gdp, gap,
+                        p(vs.geom), p(vs.binning), p(vs.image), p(cbg[sl]) if cbg is not None else None,
+                        p(color[sl]), p(gc[sl]), gdp, gap,
                         p(d_bg[sl]) if d_bg is not None else None, p(d_m2[sl]), p(d_col), p(d_op), p(d_m3), p(d_c3),
                         p(d_sh), p(d_sc), p(d_rot), 1 if si > 0 else 0, p(work), work.numel(), stream))
                 if second:
@@ -276,13 +282,14 @@ class _RasterizeViews(torch.autograd.Function):
             d_bg = d_bg.reshape(ctx.bg_shape)
         if getattr(ctx, "needs_c3_scratch", False):
             d_c3 = None
-        grads = [None, None, None, d_m3, d_sh, d_col, d_op, d_sc, d_rot, d_c3, d_bg, d_c2] + [d_m2[v] for v in range(V)]
+        grads = [None, None, None, None, d_m3, d_sh, d_col, d_op, d_sc, d_rot, d_c3, d_bg, d_c2] + \
+            [d_m2[v] for v in range(V)]
         for k, need in enumerate(ctx.needs_input_grad):
             if not need:
                 grads[k] = None
         if ctx.grad_reduce is not None and P > 0:
             # the per-Gaussian gradients' sums over ranks, range by range as the backward finishes them
-            shared = [grads[k] for k in (3, 4, 5, 6, 7, 8, 9, 11)]
+            shared = [grads[k] for k in (4, 5, 6, 7, 8, 9, 10, 12)]
             ctx.grad_reduce.launch(shared, P, events if P > 0 else None)
         _C.host_mark("bwd_host", t0)
         return tuple(grads)
@@ -290,7 +297,7 @@ class _RasterizeViews(torch.autograd.Function):
 
 def rasterize_views(settings_list, means3D, means2D_list, opacities, shs=None, colors_precomp=None, scales=None,
                     rotations=None, cov3D_precomp=None, background=None, colors2=None, grad_reduce=None,
-                    two_color_backward="fused"):
+                    two_color_backward="fused", clamp=False):
     """Render V views of one set of Gaussians.  settings_list: V GaussianRasterizationSettings (same image
     size, same sh_degree, scale_modifier and prefiltered flag); means2D_list: V screen-space placeholders
     (P, 3) whose .grad receives each view's viewspace gradient.  Returns (color (V,3,H,W), radii (V,P),
@@ -300,6 +307,11 @@ def rasterize_views(settings_list, means3D, means2D_list, opacities, shs=None, c
     images (V, H, W, 3) (renderer/diff_gaussian_rasterizer_background.py:116,129-132,139); the first
     output is then render = clamp(color + (1 - alpha) * background, 0, 1) (bit-identical to the torch
     expression, same gradients incl. the background's) instead of color.
+
+    clamp=True without a background: the first output is the renderers' ``rendered_image.clamp(0, 1)``
+    (e.g. renderer/diff_sugar_rasterizer_normal.py:212, renderer/diff_gaussian_rasterizer.py:141) formed in the
+    blend kernels, its gradient mask in the backward's per-pixel prologue: the same bits as clamping the colour
+    output in torch, without its four elementwise passes over the images.
 
     colors2 (P, 3): a second rasterizer call that differs only in its colours — the SuGaR normal renderer's
     ``rasterizer(..., means2D=zeros_like(means2D), shs=None, colors_precomp=pc.get_gs_normals, ...)``
@@ -334,5 +346,6 @@ def rasterize_views(settings_list, means3D, means2D_list, opacities, shs=None, c
             raise ValueError("background must hold (V, H, W, 3) values")
     if two_color_backward not in ("fused", "separate"):
         raise ValueError("two_color_backward is 'fused' or 'separate'")
-    return _RasterizeViews.apply(list(settings_list), grad_reduce, two_color_backward, means3D, shs, colors_precomp,
-                                 opacities, scales, rotations, cov3D_precomp, background, colors2, *means2D_list)
+    return _RasterizeViews.apply(list(settings_list), grad_reduce, two_color_backward, bool(clamp), means3D, shs,
+                                 colors_precomp, opacities, scales, rotations, cov3D_precomp, background, colors2,
+                                 *means2D_list)
