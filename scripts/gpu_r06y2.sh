@@ -1,6 +1,20 @@
 #!/bin/bash
-# Round-6 final build 9ea4e4f, part 2: rocprofv3 kernel trace + FETCH / WRITE / VALU passes of the C3 and C5
-# workloads, device-counted pairs (diagnostic build of the same sources), SQ counters of the C3 blends.
+# Round-6 session y2: P0 (GSR_FWD_PAIR=0: HEAD's tile forward, one candidate per step, the next one's staged record
+# read a step ahead) vs P1 (GSR_FWD_PAIR=1: candidates in pairs, the two power -> exp -> alpha chains issued together,
+# then blended in list order; 71 VGPRs, 7 waves per SIMD), headline alternated; then the forward bitwise / parity /
+# headline tests on P1.
 set -o pipefail
 mkdir -p gpurun_out
-T=r06y STEPS="prof profsugar pairs sq" bash scripts/gpu_session.sh
+BASE="--no-cpu-baseline --no-knn --per-view-views 0 --extra-lines none"
+for round in 1 2 3; do
+  for spec in P0=build_ab/libgsr_hip_P0.so P1=build_ab/libgsr_hip_P1.so; do
+    name=${spec%%=*}; lib=${spec#*=}
+    GSR_HIP_LIB=$PWD/$lib timeout -k 10 300 python -u bench.py $BASE --steps 10 --warmup 3 > gpurun_out/r06y2_v64_${name}_${round}.json \
+      2> gpurun_out/r06y2_v64_${name}_${round}.log || exit 1
+    python scripts/bench_summary.py gpurun_out/r06y2_v64_${name}_${round}.json
+  done
+done
+GSR_HIP_LIB=$PWD/build_ab/libgsr_hip_P1.so timeout -k 10 900 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_headline.py tests/test_gpu_configs.py \
+  -m gpu -x -v --timeout 300 --timeout-method thread > gpurun_out/r06y2_gpu_tests.log 2>&1 || { tail -30 gpurun_out/r06y2_gpu_tests.log; exit 1; }
+tail -2 gpurun_out/r06y2_gpu_tests.log
+echo "r06y2 done"
