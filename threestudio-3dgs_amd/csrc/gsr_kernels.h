@@ -99,6 +99,8 @@ struct RenderSet {
   const float* dpix2;
   // dispatch order (ImageState::order of the set, indexed by v0 + v): null = views in turn, raster order
   const uint32_t* order;
+  // with an order: views whose super-tiles are dealt heaviest-first together (block_map; order_chunk)
+  int ochunk;
   // split backward (gsr_render.hip split_on): the forward writes its checkpoints here, the backward walks the
   // tiles in chunks from them; null = off
   float* ckpt;
@@ -122,6 +124,8 @@ struct RenderSet {
 bool split_on(int V, int P, int width, int height, long long instances);
 // the forward of a set takes the one-wave-per-tile kernel (k_render_fwd_tile)
 bool fwd_tile_chosen(long long instances, long long gaussians, int views);
+// the dispatch-order chunk of a blend launch over V views (forward or backward) — gsr_render.hip
+int order_chunk(int V, bool forward);
 // the blend kernel the last forward (0) / backward (1) blend launch used, as rocprofv3 names it
 const char* blend_kernel_name(int which);
 // the forward of this set writes split checkpoints: split_on for one colour set (the two-colour backward never

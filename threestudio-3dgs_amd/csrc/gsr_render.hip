@@ -70,9 +70,26 @@ __device__ unsigned long long g_pairs[8];
 // short ones fill the tail; chunks bound how many views' records compete in L2 at once (chunk 1 / 4 / 8 /
 // 16 / all 64: C3 backward 0.0976 / 0.0955 / 0.0955 / 0.098 / 0.100 ms/view, 8-view launches best fully
 // interleaved; profiles/r02_tile_order_ab.txt).  Without: the views in turn, super-tiles in raster order.
+// The chunk is rs.ochunk (order_chunk): 8 views, and for sets of GSR_ORDER_BIG_SET views or more 2 in the
+// forwards and 4 in the backwards — re-measured on the round-6 kernels (profiles/r06/ab_r06z3.txt, ab_r06z5.txt):
+// 64-view C3 forward 0.0436 -> 0.0388 ms/view at chunk 2 (fewer views' records compete in the caches), C5
+// backward 0.227 -> 0.221 at 4; 8-view sets stay fully interleaved (their forward 0.045 -> 0.048 at chunk 2).
 #ifndef GSR_ORDER_CHUNK
 #define GSR_ORDER_CHUNK 8
 #endif
+#ifndef GSR_ORDER_BIG_SET
+#define GSR_ORDER_BIG_SET 32
+#endif
+#ifndef GSR_ORDER_CHUNK_FWD_BIG
+#define GSR_ORDER_CHUNK_FWD_BIG 2
+#endif
+#ifndef GSR_ORDER_CHUNK_BWD_BIG
+#define GSR_ORDER_CHUNK_BWD_BIG 4
+#endif
+int order_chunk(int V, bool forward) {
+  if (V >= GSR_ORDER_BIG_SET) return forward ? GSR_ORDER_CHUNK_FWD_BIG : GSR_ORDER_CHUNK_BWD_BIG;
+  return GSR_ORDER_CHUNK;
+}
 template <int PER>
 __device__ __forceinline__ bool block_map(int b, const RenderSet& rs, int& v, int& tile, int& q) {
   const int sgx = (rs.gx + 1) >> 1, sgy = (rs.gy + 1) >> 1, S = sgx * sgy;
@@ -84,9 +101,10 @@ __device__ __forceinline__ bool block_map(int b, const RenderSet& rs, int& v, in
     if (m >= rs.V * S) return false;
     // chunks of GSR_ORDER_CHUNK views, interleaved inside a chunk (all its views' heaviest super-tiles
     // first), the chunks in turn
-    const int c = m / (GSR_ORDER_CHUNK * S), local = m - c * GSR_ORDER_CHUNK * S;
-    const int vc = min(GSR_ORDER_CHUNK, rs.V - c * GSR_ORDER_CHUNK);
-    v = c * GSR_ORDER_CHUNK + local % vc;
+    const int ch = rs.ochunk;
+    const int c = m / (ch * S), local = m - c * ch * S;
+    const int vc = min(ch, rs.V - c * ch);
+    v = c * ch + local % vc;
     s = (int)rs.order[(size_t)(rs.v0 + v) * S + local / vc];
   } else {
     const int G = PER * 8 * ((S + 7) >> 3);
