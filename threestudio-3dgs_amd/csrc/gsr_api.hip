@@ -627,7 +627,7 @@ static int set_render(int V, int P, const int* K, int width, int height, const f
     rs.out_col2 = out_color2;
     rs.dpix2 = nullptr;
     rs.order = img.order;
-    rs.ochunk = order_chunk(V, true);
+    rs.ochunk = order_chunk(V, gx, gy, true);
     rs.ckpt = split ? img.ckpt : nullptr;
     rs.split_mode = img.split_mode;
     rs.split_items = img.split_items;
@@ -778,7 +778,7 @@ static int set_backward(int V, int P, int degree, int M, const int* K, int width
     rs.qkeys = tp.qmask ? b.key[tres] : nullptr;
     rs.qbytes = reinterpret_cast<uint8_t*>(b.key[tres ^ 1]);  // (valid when img.split_mode[1] says so)
     rs.V = g1 - g0;
-    rs.ochunk = order_chunk(rs.V, false);
+    rs.ochunk = order_chunk(rs.V, gx, gy, false);
     rs.v0 = g0;
     rs.P = P;
     rs.W = width;

@@ -124,8 +124,8 @@ struct RenderSet {
 bool split_on(int V, int P, int width, int height, long long instances);
 // the forward of a set takes the one-wave-per-tile kernel (k_render_fwd_tile)
 bool fwd_tile_chosen(long long instances, long long gaussians, int views);
-// the dispatch-order chunk of a blend launch over V views (forward or backward) — gsr_render.hip
-int order_chunk(int V, bool forward);
+// the dispatch-order chunk of a blend launch over V views of gx x gy tiles (forward or backward) — gsr_render.hip
+int order_chunk(int V, int gx, int gy, bool forward);
 // the blend kernel the last forward (0) / backward (1) blend launch used, as rocprofv3 names it
 const char* blend_kernel_name(int which);
 // the forward of this set writes split checkpoints: split_on for one colour set (the two-colour backward never

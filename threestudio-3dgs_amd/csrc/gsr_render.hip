@@ -70,15 +70,20 @@ __device__ unsigned long long g_pairs[8];
 // short ones fill the tail; chunks bound how many views' records compete in L2 at once (chunk 1 / 4 / 8 /
 // 16 / all 64: C3 backward 0.0976 / 0.0955 / 0.0955 / 0.098 / 0.100 ms/view, 8-view launches best fully
 // interleaved; profiles/r02_tile_order_ab.txt).  Without: the views in turn, super-tiles in raster order.
-// The chunk is rs.ochunk (order_chunk): 8 views, and for sets of GSR_ORDER_BIG_SET views or more 2 in the
-// forwards and 4 in the backwards — re-measured on the round-6 kernels (profiles/r06/ab_r06z3.txt, ab_r06z5.txt):
-// 64-view C3 forward 0.0436 -> 0.0388 ms/view at chunk 2 (fewer views' records compete in the caches), C5
-// backward 0.227 -> 0.221 at 4; 8-view sets stay fully interleaved (their forward 0.045 -> 0.048 at chunk 2).
+// The chunk is rs.ochunk (order_chunk): 8 views, and for sets of GSR_ORDER_BIG_SET views or more of views with
+// GSR_ORDER_BIG_VIEW super-tiles or more 2 in the forwards and 4 in the backwards — re-measured on the round-6
+// kernels (profiles/r06/ab_r06z3.txt, ab_r06z5.txt): 64-view C3 forward 0.0436 -> 0.0388 ms/view at chunk 2 (fewer
+// views' records compete in the caches), C5 backward 0.227 -> 0.221 at 4; 8-view sets stay fully interleaved (their
+// forward 0.045 -> 0.048 at chunk 2), and so do small views (64 views at 256^2: 64 super-tiles a view, forward
+// 0.019 -> 0.023 at chunk 2 — two views' heaviest tiles cannot fill the chip, the later chunks' start late).
 #ifndef GSR_ORDER_CHUNK
 #define GSR_ORDER_CHUNK 8
 #endif
 #ifndef GSR_ORDER_BIG_SET
 #define GSR_ORDER_BIG_SET 32
+#endif
+#ifndef GSR_ORDER_BIG_VIEW
+#define GSR_ORDER_BIG_VIEW 512  // super-tiles per view (1024^2: 1024, C5's 800^2: 625, 256^2: 64)
 #endif
 #ifndef GSR_ORDER_CHUNK_FWD_BIG
 #define GSR_ORDER_CHUNK_FWD_BIG 2
@@ -86,8 +91,9 @@ __device__ unsigned long long g_pairs[8];
 #ifndef GSR_ORDER_CHUNK_BWD_BIG
 #define GSR_ORDER_CHUNK_BWD_BIG 4
 #endif
-int order_chunk(int V, bool forward) {
-  if (V >= GSR_ORDER_BIG_SET) return forward ? GSR_ORDER_CHUNK_FWD_BIG : GSR_ORDER_CHUNK_BWD_BIG;
+int order_chunk(int V, int gx, int gy, bool forward) {
+  const int S = ((gx + 1) >> 1) * ((gy + 1) >> 1);  // super-tiles per view (block_map)
+  if (V >= GSR_ORDER_BIG_SET && S >= GSR_ORDER_BIG_VIEW) return forward ? GSR_ORDER_CHUNK_FWD_BIG : GSR_ORDER_CHUNK_BWD_BIG;
   return GSR_ORDER_CHUNK;
 }
 template <int PER>
