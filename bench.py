@@ -73,12 +73,12 @@ def parse():
     ap.add_argument("--path", choices=["batched", "per-view"], default="batched",
                     help="batched: rasterize_views (one autograd node per rank's views); per-view: one "
                          "GaussianRasterizer call per view, exactly as the reference renderer loop does")
-    ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "r06v_traffic.json"),
+    ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "r06h_traffic.json"),
                     help="PMC summary (profiles/summarize.py) supplying roofline.traffic and the VALU counts")
-    ap.add_argument("--pairs", default=os.path.join(ROOT, "profiles", "r06v_pairs.json"),
+    ap.add_argument("--pairs", default=os.path.join(ROOT, "profiles", "r06h_pairs.json"),
                     help="device-counted blend pairs (profiles/diag_pairs.py) for the VALU roofline")
-    ap.add_argument("--traffic-sugar", default=os.path.join(ROOT, "profiles", "r06v_sugar_traffic.json"),
-                    help="PMC summary of the C5 line (--workload sugar, profiles/summarize.py r06v_sugar)")
+    ap.add_argument("--traffic-sugar", default=os.path.join(ROOT, "profiles", "r06h_sugar_traffic.json"),
+                    help="PMC summary of the C5 line (--workload sugar, profiles/summarize.py r06h_sugar)")
     ap.add_argument("--fused-clamp", choices=["on", "off"], default="on",
                     help="C5: the renderer's render.clamp(0, 1) formed in the blends (rasterize_views clamp=True) "
                          "or by torch on the colour output (off: the A/B baseline)")
